@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Headline benchmark: FeatureNet-3D training throughput (samples/s).
+
+Metric / config from BASELINE.json: "samples/sec (64^3 voxel, 24-class) train
+at 1/2/4/8 MI355X".  One training step = forward + backward + Adam update of
+the full FeatureNet-3D (4 Conv3d+BN+ReLU, fused MaxPool3d, FC128, FC24) on a
+per-GPU batch of synthetic 64^3 binary voxel grids with random labels and
+random-init weights, bf16 compute / fp32 master weights.  Data parallel over
+N GPUs = one process per GPU, RCCL all-reduce of gradient buckets overlapped
+with backward (weak scaling: the per-GPU batch is fixed).
+
+    python bench.py                       # 1 GPU, defaults
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
+
+``--impl torch`` runs the stock PyTorch-ROCm eager baseline (MIOpen + DDP) on
+the same data for the first-party comparison recorded in BASELINE.md.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# measured first-party baseline (stock PyTorch-ROCm eager, 1x MI355X, same config);
+# see BASELINE.md.  None until measured.
+TORCH_BASELINE_SAMPLES_PER_S_PER_GPU = None
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=128, help="per-GPU batch")
+    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--classes", type=int, default=24)
+    ap.add_argument("--impl", choices=["native", "torch"], default="native")
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches resident on device")
+    ap.add_argument("--tiny", action="store_true", help="16^3 2-class plumbing config (not the headline)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = args.device == "cuda"
+    if use_cuda:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if world > 1:
+        from featurenet_amd.parallel.ddp import init_from_env
+
+        init_from_env("nccl" if use_cuda else "gloo")
+
+    torch.manual_seed(1234 + rank)
+    if args.tiny:
+        args.size, args.classes = 16, 2
+    B, S, NC = args.batch, args.size, args.classes
+    # synthetic 64^3 occupancy grids (~30% filled) + random labels, device resident
+    xs = [(torch.rand(B, S, S, S, 1, device=dev) < 0.3).to(torch.bfloat16) for _ in range(args.pool)]
+    ys = [torch.randint(0, NC, (B,), device=dev) for _ in range(args.pool)]
+
+    if args.impl == "native":
+        from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+        from featurenet_amd.ops import FlatAdam, softmax_xent
+        from featurenet_amd.parallel.ddp import GradBucketer
+        from featurenet_amd.train.flat import FlatParams
+
+        torch.manual_seed(1234)  # identical init on every rank (also broadcast below)
+        cfg = FeatureNet3DConfig.tiny() if args.tiny else FeatureNet3DConfig(input_size=S, num_classes=NC)
+        model = FeatureNet3D(cfg).to(dev)
+        flat = FlatParams(model)
+        opt = FlatAdam(flat.data, flat.grad, lr=1e-3)
+        bucketer = GradBucketer(flat, bucket_mb=args.bucket_mb)
+        bucketer.broadcast_from(0)
+
+        def step(i):
+            flat.zero_grad()
+            logits = model(xs[i % args.pool])
+            loss = softmax_xent(logits, ys[i % args.pool])
+            loss.backward()
+            scale = bucketer.finish()
+            opt.step(grad_scale=scale)
+            return loss
+        model_name = "FeatureNet-3D"
+        flops = model.train_flops_per_sample()
+    else:
+        from bench.torch_baseline import TorchFeatureNet3D
+
+        torch.manual_seed(1234)
+        model = TorchFeatureNet3D(input_size=S, num_classes=NC).to(dev)
+        if use_cuda:
+            model = model.to(memory_format=torch.channels_last_3d)
+        dmodel = model
+        if world > 1:
+            dmodel = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local] if use_cuda else None)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        xs = [x.permute(0, 4, 1, 2, 3) for x in xs]  # NCDHW view of the channels-last data
+        if use_cuda:
+            xs = [x.contiguous(memory_format=torch.channels_last_3d) for x in xs]
+        lossf = torch.nn.CrossEntropyLoss()
+
+        def step(i):
+            opt.zero_grad(set_to_none=True)
+            with torch.autocast(device_type="cuda" if use_cuda else "cpu", dtype=torch.bfloat16):
+                logits = dmodel(xs[i % args.pool])
+            loss = lossf(logits.float(), ys[i % args.pool])
+            loss.backward()
+            opt.step()
+            return loss
+        model_name = "FeatureNet-3D (stock PyTorch eager baseline)"
+        flops = None
+
+    def sync():
+        if use_cuda:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for i in range(args.warmup):
+        step(i)
+    sync()
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev if use_cuda else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / max(args.steps, 1) * 1e3
+    value = args.steps * B * world / elapsed
+    base = TORCH_BASELINE_SAMPLES_PER_S_PER_GPU
+    vs = (value / (base * world)) if base else None
+    if rank == 0:
+        out = {
+            "metric": "samples/sec (64^3 voxel, 24-class) train",
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if vs is None else round(vs, 3),
+            "dtype": "bf16",
+            "data": "synthetic (random 64^3 binary voxels, random labels, random-init weights)",
+            "config": {
+                "model": model_name,
+                "global_batch": B * world,
+                "per_gpu_batch": B,
+                "seq_len": None,
+                "input": f"{S}^3x1 voxels",
+                "classes": NC,
+                "parallelism": f"dp{world}",
+                "impl": args.impl,
+                "optimizer": "adam",
+            },
+            "final_loss": None if loss is None else round(float(loss.detach()), 4),
+        }
+        if flops:
+            out["model_tflops_per_s"] = round(flops * value / 1e12, 2)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+// pybind11 surface of the featurenet_amd HIP kernel library (module `_C`).
+//
+// Every entry point takes raw device addresses (Python ints from
+// tensor.data_ptr()) and the HIP stream handle of the caller's current torch
+// stream, so the Python op layer owns allocation and the kernels can be
+// captured into hipGraphs.  Errors raise RuntimeError with the HIP message.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+extern "C" {
+int fn_igemm_fwd(const void*, const void*, const float*, void*, float*, const int*, const int*, long long, int, int,
+                 int, int, int, hipStream_t);
+int fn_igemm_fwd_mblocks(long long);
+int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
+                   hipStream_t);
+int fn_slab_reduce(const float*, float*, long long, int, int, hipStream_t);
+int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
+                int, int, int, int, hipStream_t);
+int fn_bn_finalize(const float*, int, int, double, const float*, const float*, float*, float*, float, float, float*,
+                   float*, float*, float*, int, hipStream_t);
+int fn_bn_apply(const void*, const float*, const float*, void*, long long, int, int, hipStream_t);
+int fn_bn_bwd_apply(const void*, const void*, const float*, const float*, const float*, const float*, const float*,
+                    const float*, void*, long long, int, float, int, hipStream_t);
+int fn_pool_fwd(const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
+int fn_pool_bwd(const void*, const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
+int fn_softmax_xent(const float*, const long long*, float*, float*, int*, int, int, float, float, hipStream_t);
+int fn_adam_flat(float*, const float*, float*, float*, void*, long long, float, float, float, float, float, float,
+                 float, float, int, hipStream_t);
+int fn_sgd_flat(float*, const float*, float*, void*, long long, float, float, float, int, float, hipStream_t);
+int fn_bias_act(const void*, const float*, void*, long long, int, int, hipStream_t);
+int fn_act_bwd(const void*, const void*, void*, long long, int, hipStream_t);
+int fn_dropout(const void*, void*, long long, float, unsigned, unsigned, hipStream_t);
+int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
+}
+
+template <typename T>
+static T P(uintptr_t a) {
+  return reinterpret_cast<T>(a);
+}
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void chk(int rc, const char* what) {
+  if (rc == 0) return;
+  if (rc < 0) throw std::runtime_error(std::string(what) + ": unsupported configuration (code " + std::to_string(rc) + ")");
+  throw std::runtime_error(std::string(what) + ": " + hipGetErrorString((hipError_t)rc));
+}
+
+static void need(const std::vector<int>& v, size_t n, const char* what) {
+  if (v.size() != n) throw std::runtime_error(std::string(what) + ": bad geometry length");
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "featurenet_amd gfx950 HIP kernels";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("igemm_fwd", [](uintptr_t src, uintptr_t wt, uintptr_t bias, uintptr_t out, uintptr_t stats, uintptr_t tab,
+                        std::vector<int> geom, long long M, int N, int K, int ldw, int vec, int act, uintptr_t st) {
+    need(geom, 13, "igemm_fwd");
+    chk(fn_igemm_fwd(P<const void*>(src), P<const void*>(wt), P<const float*>(bias), P<void*>(out), P<float*>(stats),
+                     P<const int*>(tab), geom.data(), M, N, K, ldw, vec, act, S(st)),
+        "igemm_fwd");
+  });
+  m.def("igemm_fwd_mblocks", &fn_igemm_fwd_mblocks);
+  m.def("igemm_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t part, uintptr_t tab, std::vector<int> geom,
+                          long long M, int Cout, int K, int splits, int vec, uintptr_t st) {
+    need(geom, 13, "igemm_wgrad");
+    chk(fn_igemm_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(part), P<const int*>(tab), geom.data(), M,
+                       Cout, K, splits, vec, S(st)),
+        "igemm_wgrad");
+  });
+  m.def("slab_reduce", [](uintptr_t part, uintptr_t out, long long n, int S_, int acc, uintptr_t st) {
+    chk(fn_slab_reduce(P<const float*>(part), P<float*>(out), n, S_, acc, S(st)), "slab_reduce");
+  });
+  m.def("colstats", [](uintptr_t x, uintptr_t dz, uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd,
+                       uintptr_t part, long long M, int C, int act, int mode, int nb, uintptr_t st) {
+    chk(fn_colstats(P<const void*>(x), P<const void*>(dz), P<const float*>(scale), P<const float*>(shift),
+                    P<const float*>(mean), P<const float*>(invstd), P<float*>(part), M, C, act, mode, nb, S(st)),
+        "colstats");
+  });
+  m.def("bn_finalize", [](uintptr_t part, int nb, int C, double count, uintptr_t gamma, uintptr_t beta,
+                          uintptr_t rmean, uintptr_t rvar, float momentum, float eps, uintptr_t o0, uintptr_t o1,
+                          uintptr_t o2, uintptr_t o3, int mode, uintptr_t st) {
+    chk(fn_bn_finalize(P<const float*>(part), nb, C, count, P<const float*>(gamma), P<const float*>(beta),
+                       P<float*>(rmean), P<float*>(rvar), momentum, eps, P<float*>(o0), P<float*>(o1), P<float*>(o2),
+                       P<float*>(o3), mode, S(st)),
+        "bn_finalize");
+  });
+  m.def("bn_apply", [](uintptr_t y, uintptr_t scale, uintptr_t shift, uintptr_t z, long long total, int C, int act,
+                       uintptr_t st) {
+    chk(fn_bn_apply(P<const void*>(y), P<const float*>(scale), P<const float*>(shift), P<void*>(z), total, C, act,
+                    S(st)),
+        "bn_apply");
+  });
+  m.def("bn_bwd_apply", [](uintptr_t dz, uintptr_t y, uintptr_t scale, uintptr_t shift, uintptr_t mean,
+                           uintptr_t invstd, uintptr_t dbeta, uintptr_t dgamma, uintptr_t dy, long long total, int C,
+                           float inv_count, int act, uintptr_t st) {
+    chk(fn_bn_bwd_apply(P<const void*>(dz), P<const void*>(y), P<const float*>(scale), P<const float*>(shift),
+                        P<const float*>(mean), P<const float*>(invstd), P<const float*>(dbeta),
+                        P<const float*>(dgamma), P<void*>(dy), total, C, inv_count, act, S(st)),
+        "bn_bwd_apply");
+  });
+  m.def("pool_fwd", [](uintptr_t x, uintptr_t out, uintptr_t scale, uintptr_t shift, std::vector<int> geom,
+                       int is_max, int count_pad, int act, uintptr_t st) {
+    need(geom, 17, "pool_fwd");
+    chk(fn_pool_fwd(P<const void*>(x), P<void*>(out), P<const float*>(scale), P<const float*>(shift), geom.data(),
+                    is_max, count_pad, act, S(st)),
+        "pool_fwd");
+  });
+  m.def("pool_bwd", [](uintptr_t dout, uintptr_t x, uintptr_t dx, uintptr_t scale, uintptr_t shift,
+                       std::vector<int> geom, int is_max, int count_pad, int act, uintptr_t st) {
+    need(geom, 17, "pool_bwd");
+    chk(fn_pool_bwd(P<const void*>(dout), P<const void*>(x), P<void*>(dx), P<const float*>(scale),
+                    P<const float*>(shift), geom.data(), is_max, count_pad, act, S(st)),
+        "pool_bwd");
+  });
+  m.def("softmax_xent", [](uintptr_t logits, uintptr_t labels, uintptr_t loss, uintptr_t dlogits, uintptr_t correct,
+                           int B, int NC, float gscale, float smoothing, uintptr_t st) {
+    chk(fn_softmax_xent(P<const float*>(logits), P<const long long*>(labels), P<float*>(loss), P<float*>(dlogits),
+                        P<int*>(correct), B, NC, gscale, smoothing, S(st)),
+        "softmax_xent");
+  });
+  m.def("adam_flat", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t pb, long long n, float lr,
+                        float b1, float b2, float eps, float wd, float bc1, float bc2, float gscale, int keras_eps,
+                        uintptr_t st) {
+    chk(fn_adam_flat(P<float*>(p), P<const float*>(g), P<float*>(mm), P<float*>(v), P<void*>(pb), n, lr, b1, b2, eps,
+                     wd, bc1, bc2, gscale, keras_eps, S(st)),
+        "adam_flat");
+  });
+  m.def("sgd_flat", [](uintptr_t p, uintptr_t g, uintptr_t buf, uintptr_t pb, long long n, float lr, float momentum,
+                       float wd, int nesterov, float gscale, uintptr_t st) {
+    chk(fn_sgd_flat(P<float*>(p), P<const float*>(g), P<float*>(buf), P<void*>(pb), n, lr, momentum, wd, nesterov,
+                    gscale, S(st)),
+        "sgd_flat");
+  });
+  m.def("bias_act", [](uintptr_t x, uintptr_t bias, uintptr_t y, long long total, int C, int act, uintptr_t st) {
+    chk(fn_bias_act(P<const void*>(x), P<const float*>(bias), P<void*>(y), total, C, act, S(st)), "bias_act");
+  });
+  m.def("act_bwd", [](uintptr_t dy, uintptr_t y, uintptr_t dx, long long total, int act, uintptr_t st) {
+    chk(fn_act_bwd(P<const void*>(dy), P<const void*>(y), P<void*>(dx), total, act, S(st)), "act_bwd");
+  });
+  m.def("dropout", [](uintptr_t x, uintptr_t y, long long total, float p, unsigned seed, unsigned offset,
+                      uintptr_t st) {
+    chk(fn_dropout(P<const void*>(x), P<void*>(y), total, p, seed, offset, S(st)), "dropout");
+  });
+  m.def("cast_f32_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t st) {
+    chk(fn_cast_f32_bf16(P<const float*>(x), P<void*>(y), n, S(st)), "cast_f32_bf16");
+  });
+}

@@ -1,0 +1,471 @@
+// BatchNorm(+activation) and pooling kernels, channels-last, bf16 I/O, fp32 math.
+//
+// Forward training path of a BN layer that follows an implicit-GEMM conv:
+//   conv epilogue -> per-block (sum, sumsq) slabs  (conv_igemm.hip, STATS=true)
+//   bn_finalize   -> mean / invstd / scale / shift + running-stat update
+//   bn_apply      -> z = act(y*scale + shift)          (or fused into pooling)
+// Backward:
+//   bn_bwd_reduce -> per-block (sum g, sum g*xhat) slabs, g = dz * act'(z)
+//   bn_finalize   -> dbeta / dgamma
+//   bn_bwd_apply  -> dy = gamma*invstd*(g - dbeta/M - xhat*dgamma/M)
+// MaxPool/AvgPool take an optional BN+act prologue so the normalised
+// activation of the layer feeding a pool is never written to HBM
+// (FeatureNet-3D conv4 -> BN -> ReLU -> MaxPool3d is one read of y4).
+#include "common.h"
+
+// ---------------------------------------------------------------------------
+// Column statistics: per-block partial sums over rows of a [M][C] tensor.
+//   MODE 0: (sum x, sum x^2)                       -- forward stats
+//   MODE 1: (sum g, sum g*xhat), g = dz*act'(z)     -- BN backward
+// VW = channels per thread (8 -> 16-B vector loads, 1 -> scalar fallback).
+// ---------------------------------------------------------------------------
+template <int VW, int MODE>
+__global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dz,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                       float* __restrict__ part, long long M, int C, int act,
+                                                       long long rows_per_block) {
+  __shared__ float red[256][2 * VW + 1];
+  const int tid = threadIdx.x;
+  const int cpr = C / VW;           // chunks per row
+  const int rpp = 256 / cpr;        // rows per pass
+  const bool active = tid < rpp * cpr;
+  const int ch = active ? tid % cpr : 0;
+  const int r0 = active ? tid / cpr : 0;
+  const long long mbeg = (long long)blockIdx.x * rows_per_block;
+  long long mend = mbeg + rows_per_block;
+  if (mend > M) mend = M;
+  float s0[VW], s1[VW], sc[VW], sh[VW], mu[VW], is[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    s0[j] = 0.f; s1[j] = 0.f;
+    if (MODE == 1 && active) {
+      const int c = ch * VW + j;
+      sc[j] = scale[c]; sh[j] = shift[c]; mu[j] = mean[c]; is[j] = invstd[c];
+    }
+  }
+  if (active) {
+    for (long long m = mbeg + r0; m < mend; m += rpp) {
+      const long long off = m * C + (long long)ch * VW;
+      if constexpr (VW == 8) {
+        Pack8 px;
+        px.u = *(const uint4*)(x + off);
+        if constexpr (MODE == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { const float v = bf2f(px.e[j]); s0[j] += v; s1[j] += v * v; }
+        } else {
+          Pack8 pd;
+          pd.u = *(const uint4*)(dz + off);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float y = bf2f(px.e[j]);
+            const float z = act_fwd(y * sc[j] + sh[j], act);
+            const float g = bf2f(pd.e[j]) * act_bwd_from_out(z, act);
+            s0[j] += g;
+            s1[j] += g * (y - mu[j]) * is[j];
+          }
+        }
+      } else {
+        const float y = bf2f(x[off]);
+        if constexpr (MODE == 0) { s0[0] += y; s1[0] += y * y; }
+        else {
+          const float z = act_fwd(y * sc[0] + sh[0], act);
+          const float g = bf2f(dz[off]) * act_bwd_from_out(z, act);
+          s0[0] += g;
+          s1[0] += g * (y - mu[0]) * is[0];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < VW; ++j) { red[tid][j] = active ? s0[j] : 0.f; red[tid][VW + j] = active ? s1[j] : 0.f; }
+  __syncthreads();
+  // one thread per channel sums the rpp partials that share its chunk
+  for (int c = tid; c < C; c += 256) {
+    const int chk = c / VW, j = c % VW;
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < rpp; ++i) { a += red[i * cpr + chk][j]; b += red[i * cpr + chk][VW + j]; }
+    part[(long long)blockIdx.x * 2 * C + c] = a;
+    part[(long long)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Reduce [nb][2][C] slabs per channel in fp64 and finalise.
+//   MODE 0 (forward): mean, invstd, scale=gamma*invstd, shift=beta-mean*scale,
+//                     running stats update (unbiased var, Keras/torch style).
+//   MODE 1 (backward): out0 = dbeta = sum g, out1 = dgamma = sum g*xhat.
+// One 256-thread block per channel.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ part, int nb, int C, double count,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                          float momentum, float eps, float* __restrict__ out0,
+                                                          float* __restrict__ out1, float* __restrict__ out2,
+                                                          float* __restrict__ out3) {
+  __shared__ double sa[256], sb[256];
+  const int c = blockIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    a += (double)part[(long long)i * 2 * C + c];
+    b += (double)part[(long long)i * 2 * C + C + c];
+  }
+  sa[threadIdx.x] = a; sb[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) { sa[threadIdx.x] += sa[threadIdx.x + s]; sb[threadIdx.x] += sb[threadIdx.x + s]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (MODE == 0) {
+      const double mean = sa[0] / count;
+      double var = sb[0] / count - mean * mean;
+      if (var < 0.0) var = 0.0;
+      const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+      const float g = gamma ? gamma[c] : 1.f;
+      const float bt = beta ? beta[c] : 0.f;
+      out0[c] = (float)mean;
+      out1[c] = invstd;
+      out2[c] = g * invstd;
+      out3[c] = bt - (float)mean * g * invstd;
+      if (run_mean) {
+        const double unb = count > 1.0 ? var * count / (count - 1.0) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
+      }
+    } else {
+      out0[c] = (float)sa[0];
+      out1[c] = (float)sb[0];
+    }
+  }
+}
+
+// z = act(y*scale + shift)
+template <int VW>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, bf16* __restrict__ z,
+                                                       long long total, int C, int act) {
+  const long long nvec = total / VW;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    const int c0 = (int)((i * VW) % C);
+    if constexpr (VW == 8) {
+      Pack8 p;
+      p.u = *(const uint4*)(y + i * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p.e[j] = f2bf(act_fwd(bf2f(p.e[j]) * scale[c0 + j] + shift[c0 + j], act));
+      *(uint4*)(z + i * 8) = p.u;
+    } else {
+      z[i] = f2bf(act_fwd(bf2f(y[i]) * scale[c0] + shift[c0], act));
+    }
+  }
+}
+
+// dy = gamma*invstd*(g - dbeta/M - xhat*dgamma/M), g = dz*act'(z)
+template <int VW>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ y,
+                                                           const float* __restrict__ scale, const float* __restrict__ shift,
+                                                           const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                           const float* __restrict__ dbeta, const float* __restrict__ dgamma,
+                                                           bf16* __restrict__ dy, long long total, int C, float inv_count,
+                                                           int act) {
+  const long long nvec = total / VW;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
+    const int c0 = (int)((i * VW) % C);
+    Pack8 py, pd, po;
+    if constexpr (VW == 8) {
+      py.u = *(const uint4*)(y + i * 8);
+      pd.u = *(const uint4*)(dz + i * 8);
+    } else {
+      py.e[0] = y[i];
+      pd.e[0] = dz[i];
+    }
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const int c = c0 + j;
+      const float yv = bf2f(py.e[j]);
+      const float zv = act_fwd(yv * scale[c] + shift[c], act);
+      const float g = bf2f(pd.e[j]) * act_bwd_from_out(zv, act);
+      const float xh = (yv - mean[c]) * invstd[c];
+      // scale = gamma*invstd
+      po.e[j] = f2bf(scale[c] * (g - dbeta[c] * inv_count - xh * dgamma[c] * inv_count));
+    }
+    if constexpr (VW == 8) *(uint4*)(dy + i * 8) = po.u;
+    else dy[i] = po.e[0];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pooling (max / avg), 1-D/2-D/3-D channels-last with optional BN+act prologue.
+// geom: N, D, H, W, C, OD, OH, OW, KD, KH, KW, SD, SH, SW, PD, PH, PW
+// ---------------------------------------------------------------------------
+struct PoolGeom {
+  int N, D, H, W, C, OD, OH, OW, KD, KH, KW, sd, sh, sw, pd, ph, pw;
+};
+
+__device__ __forceinline__ float load_pre(const bf16* x, long long idx, int c, const float* scale, const float* shift,
+                                          int act) {
+  float v = bf2f(x[idx]);
+  if (scale) v = act_fwd(v * scale[c] + shift[c], act);
+  return v;
+}
+
+template <int VW>
+__global__ __launch_bounds__(256) void pool_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       PoolGeom g, int is_max, int count_pad, int act) {
+  const int cpr = g.C / VW;
+  const long long total = (long long)g.N * g.OD * g.OH * g.OW * cpr;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int ch = (int)(i % cpr);
+    long long t = i / cpr;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH); t /= g.OH;
+    const int od = (int)(t % g.OD);
+    const long long n = t / g.OD;
+    float accv[VW];
+#pragma unroll
+    for (int j = 0; j < VW; ++j) accv[j] = is_max ? -INFINITY : 0.f;
+    int cnt = 0;
+    for (int kd = 0; kd < g.KD; ++kd) {
+      const int id = od * g.sd - g.pd + kd;
+      if ((unsigned)id >= (unsigned)g.D) continue;
+      for (int kh = 0; kh < g.KH; ++kh) {
+        const int ih = oh * g.sh - g.ph + kh;
+        if ((unsigned)ih >= (unsigned)g.H) continue;
+        for (int kw = 0; kw < g.KW; ++kw) {
+          const int iw = ow * g.sw - g.pw + kw;
+          if ((unsigned)iw >= (unsigned)g.W) continue;
+          ++cnt;
+          const long long base = (((n * g.D + id) * g.H + ih) * (long long)g.W + iw) * g.C + ch * VW;
+          if constexpr (VW == 8) {
+            Pack8 p;
+            p.u = *(const uint4*)(x + base);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float v = bf2f(p.e[j]);
+              if (scale) v = act_fwd(v * scale[ch * 8 + j] + shift[ch * 8 + j], act);
+              accv[j] = is_max ? fmaxf(accv[j], v) : accv[j] + v;
+            }
+          } else {
+            const float v = load_pre(x, base, ch, scale, shift, act);
+            accv[0] = is_max ? fmaxf(accv[0], v) : accv[0] + v;
+          }
+        }
+      }
+    }
+    const float div = count_pad ? (float)(g.KD * g.KH * g.KW) : (float)(cnt > 0 ? cnt : 1);
+    const long long ob = i * VW;
+    if constexpr (VW == 8) {
+      Pack8 p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p.e[j] = f2bf(is_max ? accv[j] : accv[j] / div);
+      *(uint4*)(out + ob) = p.u;
+    } else {
+      out[ob] = f2bf(is_max ? accv[0] : accv[0] / div);
+    }
+  }
+}
+
+// Gather-form backward: every input element collects from the windows that
+// contain it (deterministic, no atomics, works for overlapping windows).
+// For max pooling the window's arg-max is recomputed (first max wins, matching
+// the forward's fmaxf scan order).
+template <int VW>
+__global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ x,
+                                                       bf16* __restrict__ dx, const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, PoolGeom g, int is_max,
+                                                       int count_pad, int act) {
+  const int cpr = g.C / VW;
+  const long long total = (long long)g.N * g.D * g.H * g.W * cpr;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int ch = (int)(i % cpr);
+    long long t = i / cpr;
+    const int iw = (int)(t % g.W); t /= g.W;
+    const int ih = (int)(t % g.H); t /= g.H;
+    const int id = (int)(t % g.D);
+    const long long n = t / g.D;
+    float gacc[VW];
+    float self[VW];
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      gacc[j] = 0.f;
+      const int c = ch * VW + j;
+      self[j] = is_max ? load_pre(x, i * VW + j, c, scale, shift, act) : 0.f;
+    }
+    // output windows covering (id, ih, iw): o*s - p <= i <= o*s - p + k - 1
+    const int od0 = max(0, (id + g.pd - g.KD + g.sd) / g.sd), od1 = min(g.OD - 1, (id + g.pd) / g.sd);
+    const int oh0 = max(0, (ih + g.ph - g.KH + g.sh) / g.sh), oh1 = min(g.OH - 1, (ih + g.ph) / g.sh);
+    const int ow0 = max(0, (iw + g.pw - g.KW + g.sw) / g.sw), ow1 = min(g.OW - 1, (iw + g.pw) / g.sw);
+    for (int od = od0; od <= od1; ++od)
+      for (int oh = oh0; oh <= oh1; ++oh)
+        for (int ow = ow0; ow <= ow1; ++ow) {
+          // guard the floor-division edge cases of negative numerators
+          if (id < od * g.sd - g.pd || id >= od * g.sd - g.pd + g.KD) continue;
+          if (ih < oh * g.sh - g.ph || ih >= oh * g.sh - g.ph + g.KH) continue;
+          if (iw < ow * g.sw - g.pw || iw >= ow * g.sw - g.pw + g.KW) continue;
+          const long long obase = (((n * g.OD + od) * g.OH + oh) * (long long)g.OW + ow) * g.C + ch * VW;
+          if (!is_max) {
+            int cnt = g.KD * g.KH * g.KW;
+            if (!count_pad) {
+              cnt = 0;
+              for (int kd = 0; kd < g.KD; ++kd) {
+                const int a = od * g.sd - g.pd + kd;
+                if ((unsigned)a >= (unsigned)g.D) continue;
+                for (int kh = 0; kh < g.KH; ++kh) {
+                  const int b = oh * g.sh - g.ph + kh;
+                  if ((unsigned)b >= (unsigned)g.H) continue;
+                  for (int kw = 0; kw < g.KW; ++kw) {
+                    const int cc = ow * g.sw - g.pw + kw;
+                    if ((unsigned)cc < (unsigned)g.W) ++cnt;
+                  }
+                }
+              }
+            }
+            const float inv = 1.f / (float)(cnt > 0 ? cnt : 1);
+#pragma unroll
+            for (int j = 0; j < VW; ++j) gacc[j] += bf2f(dout[obase + j]) * inv;
+          } else {
+            // find first arg-max position of this window for each channel
+            bool won[VW];
+            float best[VW];
+#pragma unroll
+            for (int j = 0; j < VW; ++j) { best[j] = -INFINITY; won[j] = false; }
+            bool done = false;
+            for (int kd = 0; kd < g.KD && !done; ++kd) {
+              const int a = od * g.sd - g.pd + kd;
+              if ((unsigned)a >= (unsigned)g.D) continue;
+              for (int kh = 0; kh < g.KH; ++kh) {
+                const int b = oh * g.sh - g.ph + kh;
+                if ((unsigned)b >= (unsigned)g.H) continue;
+                for (int kw = 0; kw < g.KW; ++kw) {
+                  const int cc = ow * g.sw - g.pw + kw;
+                  if ((unsigned)cc >= (unsigned)g.W) continue;
+                  const long long base = (((n * g.D + a) * g.H + b) * (long long)g.W + cc) * g.C + ch * VW;
+                  const bool me = (a == id && b == ih && cc == iw);
+#pragma unroll
+                  for (int j = 0; j < VW; ++j) {
+                    const float v = me ? self[j] : load_pre(x, base + j, ch * VW + j, scale, shift, act);
+                    if (v > best[j]) { best[j] = v; won[j] = me; }
+                  }
+                }
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < VW; ++j)
+              if (won[j]) gacc[j] += bf2f(dout[obase + j]);
+          }
+        }
+    if constexpr (VW == 8) {
+      Pack8 p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p.e[j] = f2bf(gacc[j]);
+      *(uint4*)(dx + i * 8) = p.u;
+    } else {
+      dx[i] = f2bf(gacc[0]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+static unsigned ew_blocks(long long work) {
+  long long b = (work + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 8192) b = 8192;
+  return (unsigned)b;
+}
+
+extern "C" int fn_colstats(const void* x, const void* dz, const float* scale, const float* shift, const float* mean,
+                           const float* invstd, float* part, long long M, int C, int act, int mode, int nb,
+                           hipStream_t st) {
+  const bool vec = (C % 8) == 0 && C / 8 <= 256;
+  if (!vec && C > 256) return -2;
+  const long long rpb = (M + nb - 1) / nb;
+  const bf16* xx = (const bf16*)x;
+  const bf16* dd = (const bf16*)dz;
+#define CS_CASE(VW, MD) \
+  hipLaunchKernelGGL((colstats_kernel<VW, MD>), dim3(nb), dim3(256), 0, st, xx, dd, scale, shift, mean, invstd, part, M, C, act, rpb)
+  if (vec) { if (mode == 0) CS_CASE(8, 0); else CS_CASE(8, 1); }
+  else { if (mode == 0) CS_CASE(1, 0); else CS_CASE(1, 1); }
+#undef CS_CASE
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_bn_finalize(const float* part, int nb, int C, double count, const float* gamma, const float* beta,
+                              float* run_mean, float* run_var, float momentum, float eps, float* o0, float* o1,
+                              float* o2, float* o3, int mode, hipStream_t st) {
+  if (mode == 0)
+    hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3(C), dim3(256), 0, st, part, nb, C, count, gamma, beta, run_mean,
+                       run_var, momentum, eps, o0, o1, o2, o3);
+  else
+    hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(C), dim3(256), 0, st, part, nb, C, count, gamma, beta, run_mean,
+                       run_var, momentum, eps, o0, o1, o2, o3);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_bn_apply(const void* y, const float* scale, const float* shift, void* z, long long total, int C,
+                           int act, hipStream_t st) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(ew_blocks(total / 8)), dim3(256), 0, st, (const bf16*)y, scale, shift,
+                       (bf16*)z, total, C, act);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(ew_blocks(total)), dim3(256), 0, st, (const bf16*)y, scale, shift,
+                       (bf16*)z, total, C, act);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_bn_bwd_apply(const void* dz, const void* y, const float* scale, const float* shift,
+                               const float* mean, const float* invstd, const float* dbeta, const float* dgamma,
+                               void* dy, long long total, int C, float inv_count, int act, hipStream_t st) {
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(ew_blocks(total / 8)), dim3(256), 0, st, (const bf16*)dz,
+                       (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, total, C, inv_count, act);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(ew_blocks(total)), dim3(256), 0, st, (const bf16*)dz,
+                       (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, total, C, inv_count, act);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+static PoolGeom pool_geom(const int* g) {
+  PoolGeom p;
+  p.N = g[0]; p.D = g[1]; p.H = g[2]; p.W = g[3]; p.C = g[4];
+  p.OD = g[5]; p.OH = g[6]; p.OW = g[7];
+  p.KD = g[8]; p.KH = g[9]; p.KW = g[10];
+  p.sd = g[11]; p.sh = g[12]; p.sw = g[13];
+  p.pd = g[14]; p.ph = g[15]; p.pw = g[16];
+  return p;
+}
+
+extern "C" int fn_pool_fwd(const void* x, void* out, const float* scale, const float* shift, const int* geom17,
+                           int is_max, int count_pad, int act, hipStream_t st) {
+  PoolGeom g = pool_geom(geom17);
+  const long long outs = (long long)g.N * g.OD * g.OH * g.OW;
+  if (g.C % 8 == 0)
+    hipLaunchKernelGGL(pool_fwd_kernel<8>, dim3(ew_blocks(outs * (g.C / 8))), dim3(256), 0, st, (const bf16*)x,
+                       (bf16*)out, scale, shift, g, is_max, count_pad, act);
+  else
+    hipLaunchKernelGGL(pool_fwd_kernel<1>, dim3(ew_blocks(outs * g.C)), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
+                       scale, shift, g, is_max, count_pad, act);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_pool_bwd(const void* dout, const void* x, void* dx, const float* scale, const float* shift,
+                           const int* geom17, int is_max, int count_pad, int act, hipStream_t st) {
+  PoolGeom g = pool_geom(geom17);
+  const long long ins = (long long)g.N * g.D * g.H * g.W;
+  if (g.C % 8 == 0)
+    hipLaunchKernelGGL(pool_bwd_kernel<8>, dim3(ew_blocks(ins * (g.C / 8))), dim3(256), 0, st, (const bf16*)dout,
+                       (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, count_pad, act);
+  else
+    hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(ew_blocks(ins * g.C)), dim3(256), 0, st, (const bf16*)dout,
+                       (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, count_pad, act);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,537 @@
+// Implicit-GEMM convolution (1-D/2-D/3-D, channels-last) on CDNA4 MFMA.
+//
+// One kernel family covers the three products a conv layer needs:
+//   fwd  : y[m][co]  = sum_k  A[m][k] * W[co][k]      A = im2col(x)   (gathered)
+//   dgrad: dx[m][ci] = sum_k' A'[m][k'] * WT[ci][k']  A' = "im2col" of dy with
+//          negated tap offsets (stride-1 transposed conv; stride-2 layers are
+//          handled by the caller through zero insertion of dy)
+//   wgrad: dW[co][k] = sum_m dy[m][co] * A[m][k]     (split over m, fp32 slabs)
+//
+// Nothing is materialised: the gather is driven by a per-layer tap table
+// (built once on the host and cached) whose entries hold the element offset of
+// a k-chunk relative to a row's base plus the tap displacement for the
+// bounds test.  For C % 8 == 0 a table entry covers 8 consecutive channels of
+// one tap, so one 16-byte load feeds one 8-element MFMA fragment slice.
+//
+// gfx950 specifics:
+//   * mfma_f32_16x16x32_bf16, 64-lane waves, 256-thread workgroups;
+//   * forward/dgrad: BM=256 rows x BN output channels x BK=64, register-staged
+//     double-buffered LDS with the st_16x32-style XOR swizzle
+//     (chunk ^= row & 7) that makes the 16-lane ds_read_b128 groups
+//     conflict-free on 128-B rows;
+//   * wgrad: the reduction runs over m, which is the slow axis of both
+//     operands in memory, so operands are staged row-major and read with
+//     ds_read_b64_tr_b16 (hardware transpose); rows are padded to 32 mod 256 B
+//     and the MFMA k-order is permuted (same permutation on both operands) so
+//     every transposed read is bank-conflict-free;
+//   * XCD-aware block remap so neighbouring M tiles (which share input halos)
+//     run on the same XCD's L2.
+#include "common.h"
+
+struct GatherGeom {
+  int RD, RH, RW;          // row decode dims: m -> (n, r1, r2, r3)
+  int md, mh, mw;          // base coord = r * mul + add
+  int ad, ah, aw;
+  int SD, SH, SW, SC;      // gathered source tensor dims (channels-last)
+};
+
+// ---------------------------------------------------------------------------
+// Gather helpers
+// ---------------------------------------------------------------------------
+struct RowBase {
+  long long base;   // element offset of (n, bd, bh, bw, 0); may be "outside"
+  int bd, bh, bw;
+  bool valid;
+};
+
+__device__ __forceinline__ RowBase decode_row(long long m, long long M, const GatherGeom& g) {
+  RowBase r;
+  r.valid = m < M;
+  long long mm = r.valid ? m : 0;
+  int c3 = (int)(mm % g.RW); mm /= g.RW;
+  int c2 = (int)(mm % g.RH); mm /= g.RH;
+  int c1 = (int)(mm % g.RD);
+  long long n = mm / g.RD;
+  r.bd = c1 * g.md + g.ad;
+  r.bh = c2 * g.mh + g.ah;
+  r.bw = c3 * g.mw + g.aw;
+  r.base = (((n * g.SD + r.bd) * g.SH + r.bh) * (long long)g.SW + r.bw) * g.SC;
+  return r;
+}
+
+__device__ __forceinline__ bool tap_ok(const RowBase& r, const int4& e, const GatherGeom& g) {
+  return r.valid && (unsigned)(r.bd + e.y) < (unsigned)g.SD &&
+         (unsigned)(r.bh + e.z) < (unsigned)g.SH && (unsigned)(r.bw + e.w) < (unsigned)g.SW;
+}
+
+// load 8 consecutive k of one row (VEC: one 16-B load from one tap)
+template <bool VEC>
+__device__ __forceinline__ uint4 gather8(const bf16* __restrict__ src, const int4* __restrict__ tab,
+                                         const RowBase& r, int k0, int Kdim, const GatherGeom& g) {
+  Pack8 p;
+  if constexpr (VEC) {
+    p.u = make_uint4(0, 0, 0, 0);
+    if (k0 < Kdim) {
+      const int4 e = tab[k0 >> 3];
+      if (tap_ok(r, e, g)) p.u = *(const uint4*)(src + r.base + e.x);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bf16 v = (bf16)0.f;
+      const int k = k0 + j;
+      if (k < Kdim) {
+        const int4 e = tab[k];
+        if (tap_ok(r, e, g)) v = src[r.base + e.x];
+      }
+      p.e[j] = v;
+    }
+  }
+  return p.u;
+}
+
+// ---------------------------------------------------------------------------
+// Forward / dgrad kernel
+// ---------------------------------------------------------------------------
+#define FWD_BM 256
+#define FWD_BK 64
+
+template <int BN, bool VEC, int ACT, bool HAS_BIAS, bool STATS>
+__global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
+    const bf16* __restrict__ src, const bf16* __restrict__ wt, const float* __restrict__ bias,
+    bf16* __restrict__ out, float* __restrict__ stats, const int4* __restrict__ tab, GatherGeom g,
+    long long M, int Ncol, int Kdim, int ldw) {
+  constexpr int A_STAGE = FWD_BM * FWD_BK;      // elements
+  constexpr int B_STAGE = BN * FWD_BK;
+  constexpr int LDO = BN + 8;                   // epilogue staging row (16-B aligned)
+  constexpr int NT = BN / 16;                   // n-tiles per wave
+  constexpr int B_CHUNKS = BN * (FWD_BK / 8);   // 16-B chunks per B stage
+  constexpr int B_PER_T = (B_CHUNKS + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * A_STAGE + 2 * B_STAGE];
+  bf16* As = smem;
+  bf16* Bs = smem + 2 * A_STAGE;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int nmb = gridDim.x;
+  const int mb = xcd_remap(blockIdx.x, nmb);
+  const long long m0 = (long long)mb * FWD_BM;
+  const int n0 = blockIdx.y * BN;
+
+  const RowBase rb = decode_row(m0 + tid, M, g);
+
+  uint4 ra[8];
+  uint4 rbv[B_PER_T];
+
+  auto load_stage = [&](int kt) {
+    const int kbase = kt * FWD_BK;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) ra[c] = gather8<VEC>(src, tab, rb, kbase + c * 8, Kdim, g);
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int idx = tid + i * 256;
+      rbv[i] = make_uint4(0, 0, 0, 0);
+      if (idx < B_CHUNKS) {
+        const int r = idx >> 3, c = idx & 7;
+        const int k = kbase + c * 8;
+        if (n0 + r < Ncol && k < ldw) rbv[i] = *(const uint4*)(wt + (long long)(n0 + r) * ldw + k);
+      }
+    }
+  };
+  auto write_stage = [&](int buf) {
+    bf16* a = As + buf * A_STAGE + tid * FWD_BK;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) *(uint4*)(a + ((c ^ (tid & 7)) << 3)) = ra[c];
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < B_CHUNKS) {
+        const int r = idx >> 3, c = idx & 7;
+        *(uint4*)(Bs + buf * B_STAGE + r * FWD_BK + ((c ^ (r & 7)) << 3)) = rbv[i];
+      }
+    }
+  };
+
+  f32x4 acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (Kdim + FWD_BK - 1) / FWD_BK;
+  load_stage(0);
+  write_stage(0);
+  __syncthreads();
+
+  const int lr = lane & 15;     // row inside a 16-row fragment
+  const int lg = lane >> 4;     // k-group (8 elements each)
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_stage(kt + 1);
+    const bf16* a = As + cur * A_STAGE;
+    const bf16* b = Bs + cur * B_STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = ks * 4 + lg;
+      bf16x8 fa[4], fb[NT];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int row = wave * 64 + mt * 16 + lr;
+        fa[mt] = *(const bf16x8*)(a + row * FWD_BK + ((ch ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int row = nt * 16 + lr;
+        fb[nt] = *(const bf16x8*)(b + row * FWD_BK + ((ch ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+    }
+    if (kt + 1 < nk) write_stage(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: bias + activation, bf16 staging in LDS, BN partial stats ----
+  bf16* Os = smem;  // reuse (all waves passed the final barrier)
+  float csum[NT], csq[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) { csum[nt] = 0.f; csq[nt] = 0.f; }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = nt * 16 + lr;
+    const bool cv = (n0 + col) < Ncol;
+    float bv = 0.f;
+    if constexpr (HAS_BIAS) bv = cv ? bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wave * 64 + mt * 16 + lg * 4 + r;
+        float v = acc[mt][nt][r] + bv;
+        v = act_fwd(v, ACT);
+        const bf16 bvv = f2bf(v);
+        Os[row * LDO + col] = bvv;
+        if constexpr (STATS) {
+          if (cv && (m0 + row) < M) {
+            const float f = bf2f(bvv);
+            csum[nt] += f;
+            csq[nt] += f * f;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (STATS) {
+    __shared__ float red[4][2][BN];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      float s = csum[nt], q = csq[nt];
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      if (lg == 0) { red[wave][0][nt * 16 + lr] = s; red[wave][1][nt * 16 + lr] = q; }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < Ncol) {
+      float s = red[0][0][tid] + red[1][0][tid] + red[2][0][tid] + red[3][0][tid];
+      float q = red[0][1][tid] + red[1][1][tid] + red[2][1][tid] + red[3][1][tid];
+      stats[(long long)mb * 2 * Ncol + n0 + tid] = s;
+      stats[(long long)mb * 2 * Ncol + Ncol + n0 + tid] = q;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 16-B chunks per row
+  const bool vec_out = (Ncol % 8) == 0;
+#pragma unroll
+  for (int i = 0; i < CPR; ++i) {
+    const int idx = tid + i * 256;
+    const int row = idx / CPR, ch = idx % CPR;
+    const long long m = m0 + row;
+    const int col = n0 + ch * 8;
+    if (m < M) {
+      if (vec_out && col + 8 <= Ncol) {
+        *(uint4*)(out + m * Ncol + col) = *(const uint4*)(Os + row * LDO + ch * 8);
+      } else {
+        for (int j = 0; j < 8; ++j)
+          if (col + j < Ncol) out[m * Ncol + col + j] = Os[row * LDO + ch * 8 + j];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight-gradient kernel
+// ---------------------------------------------------------------------------
+#define WG_BR 32     // m-rows per stage (= one MFMA k-step)
+#define WG_BK 256    // k-columns per block
+#define WG_LDX (WG_BK + 16)
+
+template <int BCO>
+struct WgLds {
+  static constexpr int LDY = (BCO == 16) ? 48 : BCO + 16;
+};
+
+// k-order permutation shared by both operands: MFMA k-index (group G, elem j)
+// reads stage row (j<4 ? 4G+j : 16+4G+j-4); see header comment.
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* base, int ld, int col0, int lane) {
+  const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  const bf16* p0 = base + (4 * G + q) * ld + col0 + 4 * p;
+  const bf16* p1 = base + (16 + 4 * G + q) * ld + col0 + 4 * p;
+  s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p0));
+  s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p1));
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  s8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int BCO, bool VEC, bool VECN>
+__global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
+    const bf16* __restrict__ dy, const bf16* __restrict__ src, float* __restrict__ part,
+    const int4* __restrict__ tab, GatherGeom g, long long M, int Cout, int Kdim, long long rows_per_split) {
+  constexpr int LDY = WgLds<BCO>::LDY;
+  constexpr int X_STAGE = WG_BR * WG_LDX;
+  constexpr int Y_STAGE = WG_BR * LDY;
+  constexpr int MT = BCO / 16;
+  constexpr int Y_CHUNKS = WG_BR * (BCO / 8);
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * X_STAGE + 2 * Y_STAGE];
+  bf16* Xs = smem;
+  bf16* Ys = smem + 2 * X_STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kc0 = blockIdx.x * WG_BK;
+  const int co0 = blockIdx.y * BCO;
+  const long long mbeg = (long long)blockIdx.z * rows_per_split;
+  long long mend = mbeg + rows_per_split;
+  if (mend > M) mend = M;
+
+  // X-tile loader: thread -> (row r, 4 consecutive 8-col chunks)
+  const int xr = tid & 31;
+  const int xc = (tid >> 5) * 4;
+  // incremental row decode for row mbeg + xr (advances by WG_BR per stage)
+  long long mcur = mbeg + xr;
+  int c3, c2, c1;
+  long long nn;
+  {
+    long long mm = mcur < M ? mcur : 0;
+    c3 = (int)(mm % g.RW); mm /= g.RW;
+    c2 = (int)(mm % g.RH); mm /= g.RH;
+    c1 = (int)(mm % g.RD); nn = mm / g.RD;
+  }
+  auto make_row = [&]() {
+    RowBase r;
+    r.valid = mcur < mend;
+    r.bd = c1 * g.md + g.ad;
+    r.bh = c2 * g.mh + g.ah;
+    r.bw = c3 * g.mw + g.aw;
+    r.base = (((nn * g.SD + r.bd) * g.SH + r.bh) * (long long)g.SW + r.bw) * g.SC;
+    return r;
+  };
+  auto advance_row = [&]() {
+    mcur += WG_BR;
+    c3 += WG_BR;
+    while (c3 >= g.RW) {
+      c3 -= g.RW;
+      if (++c2 >= g.RH) {
+        c2 = 0;
+        if (++c1 >= g.RD) { c1 = 0; ++nn; }
+      }
+    }
+  };
+
+  uint4 rx[4];
+  uint4 ry;
+  auto load_stage = [&](long long ms) {
+    const RowBase r = make_row();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rx[i] = gather8<VEC>(src, tab, r, kc0 + (xc + i) * 8, Kdim, g);
+    ry = make_uint4(0, 0, 0, 0);
+    if (tid < Y_CHUNKS) {
+      const int row = tid / (BCO / 8), ch = tid % (BCO / 8);
+      const long long m = ms + row;
+      const int co = co0 + ch * 8;
+      if (m < mend) {
+        if constexpr (VECN) {
+          if (co < Cout) ry = *(const uint4*)(dy + m * Cout + co);
+        } else {
+          Pack8 p;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) p.e[j] = (co + j < Cout) ? dy[m * Cout + co + j] : (bf16)0.f;
+          ry = p.u;
+        }
+      }
+    }
+    advance_row();
+  };
+  auto write_stage = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(uint4*)(Xs + buf * X_STAGE + xr * WG_LDX + (xc + i) * 8) = rx[i];
+    if (tid < Y_CHUNKS) {
+      const int row = tid / (BCO / 8), ch = tid % (BCO / 8);
+      *(uint4*)(Ys + buf * Y_STAGE + row * LDY + ch * 8) = ry;
+    }
+  };
+
+  f32x4 acc[MT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const long long nst = (mend - mbeg + WG_BR - 1) / WG_BR;
+  if (nst > 0) {
+    load_stage(mbeg);
+    write_stage(0);
+  }
+  __syncthreads();
+  for (long long s = 0; s < nst; ++s) {
+    const int cur = (int)(s & 1);
+    if (s + 1 < nst) load_stage(mbeg + (s + 1) * WG_BR);
+    const bf16* xs = Xs + cur * X_STAGE;
+    const bf16* ys = Ys + cur * Y_STAGE;
+    bf16x8 fa[MT], fb[4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) fa[mt] = tr_frag(ys, LDY, mt * 16, lane);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) fb[nt] = tr_frag(xs, WG_LDX, wave * 64 + nt * 16, lane);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+    if (s + 1 < nst) write_stage(cur ^ 1);
+    __syncthreads();
+  }
+
+  // D[row=co][col=k]: lane holds rows (lane>>4)*4+r, col lane&15
+  float* dst = part + (long long)blockIdx.z * Cout * Kdim;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int k = kc0 + wave * 64 + nt * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + mt * 16 + (lane >> 4) * 4 + r;
+        if (co < Cout && k < Kdim) dst[(long long)co * Kdim + k] = acc[mt][nt][r];
+      }
+    }
+}
+
+// sum fp32 slabs [S][n] -> out[n] (optionally accumulate into out)
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                          long long n, int S, int accumulate) {
+  const long long stride = (long long)gridDim.x * 256;
+  if ((n & 3) == 0) {
+    const long long n4 = n >> 2;
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += stride) {
+      float4 s = accumulate ? *(const float4*)(out + i * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int z = 0; z < S; ++z) {
+        const float4 v = *(const float4*)(part + (long long)z * n + i * 4);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      *(float4*)(out + i * 4) = s;
+    }
+  } else {
+    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += stride) {
+      float s = accumulate ? out[i] : 0.f;
+      for (int z = 0; z < S; ++z) s += part[(long long)z * n + i];
+      out[i] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers (C ABI, used by bind.cpp)
+// ---------------------------------------------------------------------------
+template <int BN, bool VEC>
+static void launch_fwd_bn(dim3 grid, hipStream_t st, const bf16* src, const bf16* wt, const float* bias, bf16* out,
+                          float* stats, const int4* tab, const GatherGeom& g, long long M, int N, int K, int ldw,
+                          int act) {
+#define FWD_ARGS src, wt, bias, out, stats, tab, g, M, N, K, ldw
+#define FWD_CASE(ACTV, HB, ST) \
+  hipLaunchKernelGGL((igemm_fwd_kernel<BN, VEC, ACTV, HB, ST>), grid, dim3(256), 0, st, FWD_ARGS)
+  const bool hb = bias != nullptr, stt = stats != nullptr;
+  if (act == ACT_NONE) {
+    if (hb) { if (stt) FWD_CASE(ACT_NONE, true, true); else FWD_CASE(ACT_NONE, true, false); }
+    else { if (stt) FWD_CASE(ACT_NONE, false, true); else FWD_CASE(ACT_NONE, false, false); }
+  } else if (act == ACT_RELU) {
+    if (hb) FWD_CASE(ACT_RELU, true, false); else FWD_CASE(ACT_RELU, false, false);
+  } else if (act == ACT_TANH) {
+    if (hb) FWD_CASE(ACT_TANH, true, false); else FWD_CASE(ACT_TANH, false, false);
+  } else {
+    if (hb) FWD_CASE(ACT_SIGMOID, true, false); else FWD_CASE(ACT_SIGMOID, false, false);
+  }
+#undef FWD_CASE
+#undef FWD_ARGS
+}
+
+extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, void* out, float* stats,
+                            const int* tab, const int* geom13, long long M, int Ncol, int Kdim, int ldw, int vec,
+                            int act, hipStream_t st) {
+  GatherGeom g;
+  g.RD = geom13[0]; g.RH = geom13[1]; g.RW = geom13[2];
+  g.md = geom13[3]; g.mh = geom13[4]; g.mw = geom13[5];
+  g.ad = geom13[6]; g.ah = geom13[7]; g.aw = geom13[8];
+  g.SD = geom13[9]; g.SH = geom13[10]; g.SW = geom13[11]; g.SC = geom13[12];
+  if (stats && act != ACT_NONE) return -1;  // stats are taken on the pre-BN output
+  const int BN = Ncol <= 16 ? 16 : (Ncol <= 32 ? 32 : 64);
+  const long long mblocks = (M + FWD_BM - 1) / FWD_BM;
+  dim3 grid((unsigned)mblocks, (Ncol + BN - 1) / BN);
+  const bf16* s = (const bf16*)src;
+  const bf16* w = (const bf16*)wt;
+  bf16* o = (bf16*)out;
+  const int4* t = (const int4*)tab;
+  if (vec) {
+    if (BN == 16) launch_fwd_bn<16, true>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
+    else if (BN == 32) launch_fwd_bn<32, true>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
+    else launch_fwd_bn<64, true>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
+  } else {
+    if (BN == 16) launch_fwd_bn<16, false>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
+    else if (BN == 32) launch_fwd_bn<32, false>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
+    else launch_fwd_bn<64, false>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
+  }
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_igemm_fwd_mblocks(long long M) { return (int)((M + FWD_BM - 1) / FWD_BM); }
+
+extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* part, const int* tab, const int* geom13,
+                              long long M, int Cout, int Kdim, int splits, int vec, hipStream_t st) {
+  GatherGeom g;
+  g.RD = geom13[0]; g.RH = geom13[1]; g.RW = geom13[2];
+  g.md = geom13[3]; g.mh = geom13[4]; g.mw = geom13[5];
+  g.ad = geom13[6]; g.ah = geom13[7]; g.aw = geom13[8];
+  g.SD = geom13[9]; g.SH = geom13[10]; g.SW = geom13[11]; g.SC = geom13[12];
+  const int BCO = Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64);
+  const long long rps = ((M + splits - 1) / splits + WG_BR - 1) / WG_BR * WG_BR;
+  dim3 grid((Kdim + WG_BK - 1) / WG_BK, (Cout + BCO - 1) / BCO, splits);
+  const bool vecn = (Cout % 8) == 0;
+  const bf16* d = (const bf16*)dy;
+  const bf16* s = (const bf16*)src;
+  const int4* t = (const int4*)tab;
+#define WG_CASE(B, V, VN) hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, part, t, g, M, Cout, Kdim, rps)
+  if (vec) {
+    if (vecn) { if (BCO == 16) WG_CASE(16, true, true); else if (BCO == 32) WG_CASE(32, true, true); else WG_CASE(64, true, true); }
+    else { if (BCO == 16) WG_CASE(16, true, false); else if (BCO == 32) WG_CASE(32, true, false); else WG_CASE(64, true, false); }
+  } else {
+    if (vecn) { if (BCO == 16) WG_CASE(16, false, true); else if (BCO == 32) WG_CASE(32, false, true); else WG_CASE(64, false, true); }
+    else { if (BCO == 16) WG_CASE(16, false, false); else if (BCO == 32) WG_CASE(32, false, false); else WG_CASE(64, false, false); }
+  }
+#undef WG_CASE
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_slab_reduce(const float* part, float* out, long long n, int S, int accumulate, hipStream_t st) {
+  long long blocks = (n / 4 + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, out, n, S, accumulate);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

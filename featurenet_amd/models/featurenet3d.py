@@ -1,0 +1,152 @@
+"""FeatureNet-3D: the voxel machining-feature classifier (north-star workload).
+
+Architecture (Zhang, Jaiswal & Rai, "FeatureNet: Machining feature
+recognition based on 3D Convolution Neural Network", CAD 2018 -- recalled, not
+present in the reference repository):
+
+    64^3 x 1 occupancy grid
+    Conv3d 32 @ 7^3, stride 2   -> 29^3   (BN + ReLU)
+    Conv3d 32 @ 5^3             -> 25^3   (BN + ReLU)
+    Conv3d 64 @ 4^3             -> 22^3   (BN + ReLU)
+    Conv3d 64 @ 3^3             -> 20^3   (BN + ReLU + MaxPool3d 2^3 -> 10^3, fused)
+    Dense 128 (ReLU)
+    Dense 24 (softmax, fused into the loss)
+
+All four convolutions run on the implicit-GEMM MFMA kernels; BN statistics
+come out of the conv epilogue; conv4's BN+ReLU is applied inside the
+MaxPool3d kernel.  The same class builds the tiny "16^3, 2-class" CPU
+reference configuration and the per-voxel segmentation variant
+(:class:`FeatureNet3DSeg`).
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass, field
+
+import torch
+from torch import nn
+
+from .layers import Conv, Dense
+
+
+@dataclass
+class FeatureNet3DConfig:
+    input_size: int = 64
+    in_channels: int = 1
+    num_classes: int = 24
+    widths: tuple = (32, 32, 64, 64)
+    kernels: tuple = (7, 5, 4, 3)
+    strides: tuple = (2, 1, 1, 1)
+    pool: int = 2
+    fc: int = 128
+    bn: bool = True
+    init: str = "he"
+
+    def to_dict(self) -> dict:
+        d = asdict(self)
+        return {k: list(v) if isinstance(v, tuple) else v for k, v in d.items()}
+
+    @staticmethod
+    def from_dict(d: dict) -> "FeatureNet3DConfig":
+        d = dict(d)
+        for k in ("widths", "kernels", "strides"):
+            if k in d:
+                d[k] = tuple(d[k])
+        return FeatureNet3DConfig(**d)
+
+    @staticmethod
+    def tiny() -> "FeatureNet3DConfig":
+        """16^3-voxel 2-class tiny 3D-CNN (BASELINE.json config 1, CPU plumbing)."""
+        return FeatureNet3DConfig(input_size=16, num_classes=2, widths=(8, 8, 16, 16), kernels=(3, 3, 3, 3),
+                                  strides=(1, 1, 1, 1), pool=2, fc=32)
+
+
+def _feature_shape(cfg: FeatureNet3DConfig) -> tuple[int, int]:
+    s = cfg.input_size
+    for k, st in zip(cfg.kernels, cfg.strides):
+        s = (s - k) // st + 1
+    s = s // cfg.pool
+    if s <= 0:
+        raise ValueError(f"FeatureNet-3D config collapses the {cfg.input_size}^3 input to nothing")
+    return s, cfg.widths[-1]
+
+
+class FeatureNet3D(nn.Module):
+    def __init__(self, cfg: FeatureNet3DConfig | None = None):
+        super().__init__()
+        self.cfg = cfg = cfg or FeatureNet3DConfig()
+        convs = []
+        cin = cfg.in_channels
+        n = len(cfg.widths)
+        for i, (w, k, s) in enumerate(zip(cfg.widths, cfg.kernels, cfg.strides)):
+            last = i == n - 1
+            convs.append(Conv(cin, w, (k, k, k), (s, s, s), "valid", bn=cfg.bn, act="relu",
+                              pool=(cfg.pool,) * 3 if last and cfg.pool > 1 else None, init=cfg.init))
+            cin = w
+        self.convs = nn.ModuleList(convs)
+        sp, c = _feature_shape(cfg)
+        self.flat_features = sp ** 3 * c
+        self.fc1 = Dense(self.flat_features, cfg.fc, act="relu", init=cfg.init)
+        self.fc2 = Dense(cfg.fc, cfg.num_classes, act=None)
+
+    def features(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dim() == 4:  # [N, D, H, W] occupancy -> add channel axis
+            x = x.unsqueeze(-1)
+        for c in self.convs:
+            x = c(x)
+        return x
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        """x: [N, S, S, S, 1] (or [N, S, S, S]) -> fp32 logits [N, num_classes]."""
+        f = self.features(x)
+        f = f.reshape(f.shape[0], -1)
+        h = self.fc1(f)
+        return self.fc2(h, out_fp32=True)
+
+    def train_flops_per_sample(self) -> int:
+        """Analytic FLOPs of one training sample (fwd + dgrad + wgrad)."""
+        cfg = self.cfg
+        shape = (1, cfg.input_size, cfg.input_size, cfg.input_size, cfg.in_channels)
+        fwd = 0
+        bwd = 0
+        for i, c in enumerate(self.convs):
+            cs, ps = c.specs(shape)
+            f = cs.flops()
+            fwd += f
+            bwd += f * (2 if i > 0 else 1)  # conv1 needs no dgrad (input has no grad)
+            shape = ps.out_shape5 if ps is not None else cs.out_shape5
+        fc = 2 * (self.flat_features * cfg.fc + cfg.fc * cfg.num_classes)
+        return fwd + bwd + 3 * fc
+
+
+class FeatureNet3DSeg(nn.Module):
+    """Per-voxel multi-feature segmentation head (BASELINE.json config 4).
+
+    Encoder = FeatureNet-3D convs with ``same`` padding (spatial size kept
+    except for the stride-2 stem), decoder = nearest 2x upsample + 3^3 conv
+    back to the input grid, 1x1x1 classifier producing per-voxel logits
+    ``[N, S, S, S, num_classes]``.
+    """
+
+    def __init__(self, input_size: int = 64, in_channels: int = 1, num_classes: int = 25, widths=(32, 32, 64, 64)):
+        super().__init__()
+        self.input_size, self.num_classes = input_size, num_classes
+        w0, w1, w2, w3 = widths
+        self.enc = nn.ModuleList([
+            Conv(in_channels, w0, (7, 7, 7), (2, 2, 2), "same", bn=True, act="relu", init="he"),
+            Conv(w0, w1, (5, 5, 5), 1, "same", bn=True, act="relu", init="he"),
+            Conv(w1, w2, (4, 4, 4), 1, "same", bn=True, act="relu", init="he"),
+            Conv(w2, w3, (3, 3, 3), 1, "same", bn=True, act="relu", init="he"),
+        ])
+        self.dec = Conv(w3, w1, (3, 3, 3), 1, "same", bn=True, act="relu", init="he")
+        self.head = Conv(w1, num_classes, (1, 1, 1), 1, "valid", bn=False, act=None, bias=True)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dim() == 4:
+            x = x.unsqueeze(-1)
+        for c in self.enc:
+            x = c(x)
+        # nearest x2 upsample on the channels-last grid
+        n, d, h, w, c = x.shape
+        x = x.reshape(n, d, 1, h, 1, w, 1, c).expand(n, d, 2, h, 2, w, 2, c).reshape(n, 2 * d, 2 * h, 2 * w, c)
+        x = self.dec(x.contiguous())
+        return self.head(x)  # [N, S, S, S, classes]

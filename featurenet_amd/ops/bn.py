@@ -1,0 +1,163 @@
+"""BatchNorm(+activation) and BN+act+pool ops.
+
+Reference parity: Keras ``BatchNormalization`` (``model/operation.py:139-150``,
+axis forced to 1 there -- see :mod:`featurenet_amd.ir.compile` for the compat
+flag) and the north-star BatchNorm3d+ReLU(+MaxPool3d) block of FeatureNet-3D.
+
+GPU path: statistics come either from the producing conv's epilogue slab
+(no extra pass over ``y``) or from ``colstats``; ``bn_finalize`` reduces the
+slab in fp64; ``bn_apply`` (or ``pool_fwd`` with the BN prologue) writes the
+normalised activation.  Backward is two passes over ``y``: ``colstats``
+(mode 1) for (sum g, sum g*xhat) and ``bn_bwd_apply``.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from . import reference as ref
+from .spec import PoolSpec, act_code
+
+
+def _stats_slab(y2: torch.Tensor) -> torch.Tensor:
+    M, C = y2.shape
+    nb = int(max(1, min(2048, M // 256)))
+    part = torch.empty(nb, 2, C, dtype=torch.float32, device=y2.device)
+    _native.kernels().colstats(y2.data_ptr(), 0, 0, 0, 0, 0, part.data_ptr(), M, C, 0, 0, nb, _native.stream(y2))
+    return part
+
+
+def _finalize_fwd(slab, count, gamma, beta, rmean, rvar, momentum, eps, update_running=True):
+    C = slab.shape[-1]
+    out = torch.empty(4, C, dtype=torch.float32, device=slab.device)
+    _native.kernels().bn_finalize(
+        slab.data_ptr(), slab.shape[0], C, float(count), _native.ptr(gamma), _native.ptr(beta),
+        _native.ptr(rmean) if update_running else 0, _native.ptr(rvar) if update_running else 0,
+        float(momentum), float(eps), out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), out[3].data_ptr(), 0,
+        _native.stream(slab))
+    return out  # mean, invstd, scale, shift
+
+
+def _eval_params(gamma, beta, rmean, rvar, eps, C, device):
+    g = gamma.detach().float() if gamma is not None else torch.ones(C, device=device)
+    b = beta.detach().float() if beta is not None else torch.zeros(C, device=device)
+    invstd = torch.rsqrt(rvar.float() + eps)
+    scale = g * invstd
+    shift = b - rmean.float() * scale
+    return torch.stack([rmean.float(), invstd, scale, shift])
+
+
+def _bwd_param_grads(dz2, y2, prm, act):
+    """(dbeta, dgamma) = (sum g, sum g*xhat)."""
+    M, C = y2.shape
+    K = _native.kernels()
+    nb = int(max(1, min(2048, M // 256)))
+    part = torch.empty(nb, 2, C, dtype=torch.float32, device=y2.device)
+    st = _native.stream(y2)
+    K.colstats(y2.data_ptr(), dz2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), prm[0].data_ptr(),
+               prm[1].data_ptr(), part.data_ptr(), M, C, act, 1, nb, st)
+    out = torch.empty(2, C, dtype=torch.float32, device=y2.device)
+    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, out[0].data_ptr(), out[1].data_ptr(), 0, 0,
+                  1, st)
+    return out[0], out[1]
+
+
+def _bwd_input(dz2, y2, prm, dbeta, dgamma, act, training):
+    M, C = y2.shape
+    dy = torch.empty_like(y2)
+    if training:
+        db, dg, inv = dbeta, dgamma, 1.0 / M
+    else:
+        db = dg = torch.zeros_like(dbeta)
+        inv = 0.0
+    _native.kernels().bn_bwd_apply(dz2.data_ptr(), y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(),
+                                   prm[0].data_ptr(), prm[1].data_ptr(), db.data_ptr(), dg.data_ptr(), dy.data_ptr(),
+                                   y2.numel(), C, inv, act, _native.stream(y2))
+    return dy
+
+
+class BatchNormActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, gamma, beta, slab, rmean, rvar, training, momentum, eps, act):
+        C = y.shape[-1]
+        y2 = y.reshape(-1, C)
+        if training:
+            if slab is None:
+                slab = _stats_slab(y2)
+            prm = _finalize_fwd(slab, y2.shape[0], gamma, beta, rmean, rvar, momentum, eps)
+        else:
+            prm = _eval_params(gamma, beta, rmean, rvar, eps, C, y.device)
+        z = torch.empty_like(y)
+        _native.kernels().bn_apply(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), z.data_ptr(), y2.numel(), C,
+                                   act, _native.stream(y))
+        ctx.save_for_backward(y, prm)
+        ctx.act, ctx.training = act, training
+        ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        y, prm = ctx.saved_tensors
+        C = y.shape[-1]
+        y2 = y.reshape(-1, C)
+        dz2 = dz.contiguous().to(torch.bfloat16).reshape(-1, C)
+        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act)
+        dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
+        return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
+                dbeta if ctx.has_beta else None, None, None, None, None, None, None, None)
+
+
+class BatchNormActPoolFn(torch.autograd.Function):
+    """p = pool(act(bn(y))) without materialising act(bn(y))."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, slab, rmean, rvar, training, momentum, eps, act, pspec, is_max, count_pad):
+        C = y.shape[-1]
+        y2 = y.reshape(-1, C)
+        if training:
+            if slab is None:
+                slab = _stats_slab(y2)
+            prm = _finalize_fwd(slab, y2.shape[0], gamma, beta, rmean, rvar, momentum, eps)
+        else:
+            prm = _eval_params(gamma, beta, rmean, rvar, eps, C, y.device)
+        p = torch.empty(pspec.out_shape5, dtype=torch.bfloat16, device=y.device)
+        _native.kernels().pool_fwd(y.data_ptr(), p.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), pspec.geom17(),
+                                   int(is_max), int(count_pad), act, _native.stream(y))
+        ctx.save_for_backward(y, prm)
+        ctx.act, ctx.training, ctx.pspec, ctx.is_max, ctx.count_pad = act, training, pspec, is_max, count_pad
+        ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
+        return p
+
+    @staticmethod
+    def backward(ctx, dp):
+        y, prm = ctx.saved_tensors
+        C = y.shape[-1]
+        dz = torch.empty_like(y)
+        dp = dp.contiguous().to(torch.bfloat16)
+        _native.kernels().pool_bwd(dp.data_ptr(), y.data_ptr(), dz.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(),
+                                   ctx.pspec.geom17(), int(ctx.is_max), int(ctx.count_pad), ctx.act,
+                                   _native.stream(y))
+        y2, dz2 = y.reshape(-1, C), dz.reshape(-1, C)
+        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act)
+        dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
+        return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
+                dbeta if ctx.has_beta else None) + (None,) * 10
+
+
+def batchnorm_act(y5, gamma, beta, running_mean, running_var, training: bool, momentum: float = 0.1,
+                  eps: float = 1e-5, act=None, stats_slab=None):
+    if _native.use_native(y5):
+        return BatchNormActFn.apply(y5.to(torch.bfloat16).contiguous(), gamma, beta, stats_slab, running_mean,
+                                    running_var, training, momentum, eps, act_code(act))
+    return ref.batchnorm_act(y5, gamma, beta, running_mean, running_var, training, momentum, eps, act)
+
+
+def batchnorm_act_pool(y5, gamma, beta, running_mean, running_var, training: bool, pspec: PoolSpec,
+                       kind: str = "max", momentum: float = 0.1, eps: float = 1e-5, act=None, stats_slab=None,
+                       count_pad: bool = False):
+    if _native.use_native(y5):
+        return BatchNormActPoolFn.apply(y5.to(torch.bfloat16).contiguous(), gamma, beta, stats_slab, running_mean,
+                                        running_var, training, momentum, eps, act_code(act), pspec, kind == "max",
+                                        count_pad)
+    z = ref.batchnorm_act(y5, gamma, beta, running_mean, running_var, training, momentum, eps, act)
+    return ref.pool(z, pspec, kind, count_pad)

@@ -1,0 +1,223 @@
+"""Convolution op: native implicit-GEMM HIP kernels on GPU, reference on CPU.
+
+Reference parity: this op is what the reference builds with Keras
+``Conv1D/Conv2D`` (``model/input.py:294-306``) and the 1x1 channel projection
+inside ``Combination`` (``model/operation.py:179-186``); the north-star
+Conv3d layers of FeatureNet-3D use the same code path.
+
+GPU path (all in ``csrc/kernels/conv_igemm.hip``):
+  forward -> ``igemm_fwd``   (optional fused bias+activation, or BN statistics)
+  dgrad   -> ``igemm_fwd``   in transposed-conv mode (negated tap table)
+  wgrad   -> ``igemm_wgrad`` (split-m fp32 slabs) + ``slab_reduce``
+"""
+from __future__ import annotations
+
+import math
+import threading
+
+import numpy as np
+import torch
+
+from .. import _native
+from . import reference as ref
+from .spec import ConvSpec, act_code
+
+_TAB_LOCK = threading.Lock()
+_TAB_CACHE: dict = {}
+
+
+# ---------------------------------------------------------------------------
+# tap tables
+# ---------------------------------------------------------------------------
+def _fwd_table(spec: ConvSpec, vec: bool) -> np.ndarray:
+    C = spec.C
+    kd, kh, kw, ci = np.meshgrid(np.arange(spec.KD), np.arange(spec.KH), np.arange(spec.KW), np.arange(C),
+                                 indexing="ij")
+    kd, kh, kw, ci = (a.reshape(-1) for a in (kd, kh, kw, ci))
+    zd, zh, zw = kd * spec.dd, kh * spec.dh, kw * spec.dw
+    off = ((zd * spec.H + zh) * spec.W + zw) * C + ci
+    tab = np.stack([off, zd, zh, zw], axis=1).astype(np.int64)
+    if vec:
+        tab = tab[::8]
+    return tab
+
+
+def _dgrad_table(spec: ConvSpec, vec: bool) -> np.ndarray:
+    """k' = tap*K + co over dy (dims OD', OH', OW' = zero-inserted dy)."""
+    K = spec.K
+    ODu, OHu, OWu = _dgrad_src_dims(spec)
+    kd, kh, kw, co = np.meshgrid(np.arange(spec.KD), np.arange(spec.KH), np.arange(spec.KW), np.arange(K),
+                                 indexing="ij")
+    kd, kh, kw, co = (a.reshape(-1) for a in (kd, kh, kw, co))
+    zd, zh, zw = -kd * spec.dd, -kh * spec.dh, -kw * spec.dw
+    off = ((zd * OHu + zh) * OWu + zw) * K + co
+    tab = np.stack([off, zd, zh, zw], axis=1).astype(np.int64)
+    if vec:
+        tab = tab[::8]
+    return tab
+
+
+def _dgrad_src_dims(spec: ConvSpec) -> tuple[int, int, int]:
+    return ((spec.OD - 1) * spec.sd + 1, (spec.OH - 1) * spec.sh + 1, (spec.OW - 1) * spec.sw + 1)
+
+
+def _table(spec: ConvSpec, kind: str, vec: bool, device) -> torch.Tensor:
+    key = (spec, kind, vec, str(device))
+    t = _TAB_CACHE.get(key)
+    if t is None:
+        arr = _fwd_table(spec, vec) if kind == "fwd" else _dgrad_table(spec, vec)
+        if np.abs(arr).max(initial=0) >= 2**31:
+            raise ValueError("conv tap offsets overflow int32")
+        t = torch.from_numpy(arr.astype(np.int32)).to(device)
+        with _TAB_LOCK:
+            _TAB_CACHE[key] = t
+    return t
+
+
+def _geom_fwd(spec: ConvSpec) -> list[int]:
+    return [spec.OD, spec.OH, spec.OW, spec.sd, spec.sh, spec.sw, -spec.pd, -spec.ph, -spec.pw,
+            spec.D, spec.H, spec.W, spec.C]
+
+
+def _geom_dgrad(spec: ConvSpec) -> list[int]:
+    ODu, OHu, OWu = _dgrad_src_dims(spec)
+    return [spec.D, spec.H, spec.W, 1, 1, 1, spec.pd, spec.ph, spec.pw, ODu, OHu, OWu, spec.K]
+
+
+def _pack_rows(mat: torch.Tensor) -> tuple[torch.Tensor, int]:
+    """bf16 [R, K] with the row stride padded to a multiple of 8 (zero tail)."""
+    R, K = mat.shape
+    ld = (K + 7) // 8 * 8
+    if ld == K:
+        return mat.to(torch.bfloat16).contiguous(), ld
+    out = torch.zeros(R, ld, dtype=torch.bfloat16, device=mat.device)
+    out[:, :K] = mat
+    return out, ld
+
+
+# ---------------------------------------------------------------------------
+# raw native calls
+# ---------------------------------------------------------------------------
+def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: ConvSpec, act: int,
+                    want_stats: bool):
+    K = _native.kernels()
+    assert x5.is_contiguous() and x5.dtype == torch.bfloat16
+    vec = spec.C % 8 == 0
+    tab = _table(spec, "fwd", vec, x5.device)
+    y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
+    stats = None
+    if want_stats:
+        nmb = K.igemm_fwd_mblocks(spec.M)
+        stats = torch.empty(nmb, 2, spec.K, dtype=torch.float32, device=x5.device)
+    K.igemm_fwd(x5.data_ptr(), wmat.data_ptr(), _native.ptr(bias), y.data_ptr(), _native.ptr(stats),
+                tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K, spec.kdim, ldw, int(vec), act,
+                _native.stream(x5))
+    return y, stats
+
+
+def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    K = _native.kernels()
+    if spec.sd > 1 or spec.sh > 1 or spec.sw > 1:
+        ODu, OHu, OWu = _dgrad_src_dims(spec)
+        up = torch.zeros(spec.N, ODu, OHu, OWu, spec.K, dtype=torch.bfloat16, device=dy5.device)
+        up[:, :: spec.sd, :: spec.sh, :: spec.sw] = dy5
+        dy5 = up
+    dy5 = dy5.contiguous()
+    vec = spec.K % 8 == 0
+    tab = _table(spec, "dgrad", vec, dy5.device)
+    # WT[ci][tap][co] = w[co][tap][ci]
+    wt = w.reshape(spec.K, spec.taps, spec.C).permute(2, 1, 0).reshape(spec.C, spec.taps * spec.K)
+    wt, ldw = _pack_rows(wt)
+    dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
+    M = spec.N * spec.D * spec.H * spec.W
+    K.igemm_fwd(dy5.data_ptr(), wt.data_ptr(), 0, dx.data_ptr(), 0, tab.data_ptr(), _geom_dgrad(spec), M, spec.C,
+                spec.taps * spec.K, ldw, int(vec), 0, _native.stream(dy5))
+    return dx
+
+
+def wgrad_splits(spec: ConvSpec, target_blocks: int = 2048) -> int:
+    col_tiles = math.ceil(spec.kdim / 256)
+    co_tiles = math.ceil(spec.K / 64) if spec.K > 32 else 1
+    s = max(1, math.ceil(target_blocks / (col_tiles * co_tiles)))
+    return int(min(s, max(1, spec.M // 256)))
+
+
+def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    K = _native.kernels()
+    vec = spec.C % 8 == 0
+    tab = _table(spec, "fwd", vec, x5.device)
+    splits = wgrad_splits(spec)
+    part = torch.empty(splits, spec.K, spec.kdim, dtype=torch.float32, device=x5.device)
+    st = _native.stream(x5)
+    K.igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), part.data_ptr(), tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K,
+                  spec.kdim, splits, int(vec), st)
+    dw = torch.empty(spec.K, spec.KD, spec.KH, spec.KW, spec.C, dtype=torch.float32, device=x5.device)
+    K.slab_reduce(part.data_ptr(), dw.data_ptr(), dw.numel(), splits, 0, st)
+    return dw
+
+
+def native_colsum(x2: torch.Tensor) -> torch.Tensor:
+    """Per-column sum of a [M, C] bf16 tensor in fp32 (bias gradients)."""
+    K = _native.kernels()
+    M, C = x2.shape
+    nb = int(max(1, min(1024, M // 64)))
+    part = torch.empty(nb, 2, C, dtype=torch.float32, device=x2.device)
+    st = _native.stream(x2)
+    K.colstats(x2.data_ptr(), 0, 0, 0, 0, 0, part.data_ptr(), M, C, 0, 0, nb, st)
+    out = torch.empty(2, C, dtype=torch.float32, device=x2.device)
+    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, out[0].data_ptr(), out[1].data_ptr(), 0, 0,
+                  1, st)
+    return out[0]
+
+
+def native_act_bwd(dy: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
+    if act == 0:
+        return dy
+    dx = torch.empty_like(dy)
+    _native.kernels().act_bwd(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dy.numel(), act, _native.stream(dy))
+    return dx
+
+
+# ---------------------------------------------------------------------------
+# autograd
+# ---------------------------------------------------------------------------
+class ConvFn(torch.autograd.Function):
+    """y = act(conv(x, w) + b); optional BN statistics slab as a 2nd output."""
+
+    @staticmethod
+    def forward(ctx, x5, w, b, spec: ConvSpec, act: int, want_stats: bool):
+        wmat, ldw = _pack_rows(w.detach().reshape(spec.K, spec.kdim))
+        bias = b.detach().float().contiguous() if b is not None else None
+        y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
+        ctx.spec, ctx.act, ctx.has_b = spec, act, b is not None
+        ctx.x_needs = ctx.needs_input_grad[0]
+        ctx.save_for_backward(x5, w, y if act else None)
+        if stats is not None:
+            ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        x5, w, y = ctx.saved_tensors
+        spec, act = ctx.spec, ctx.act
+        dy = dy.contiguous().to(torch.bfloat16)
+        if act:
+            dy = native_act_bwd(dy, y, act)
+        dx = native_conv_dgrad(dy, w.detach(), spec) if ctx.x_needs else None
+        dw = native_conv_wgrad(dy, x5.contiguous(), spec) if ctx.needs_input_grad[1] else None
+        db = native_colsum(dy.reshape(-1, spec.K)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        return dx, dw, db, None, None, None
+
+
+def conv(x5: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, spec: ConvSpec, act=None,
+         want_stats: bool = False):
+    """Convolution on a 5-D channels-last tensor.
+
+    Returns ``y`` or ``(y, stats)`` when ``want_stats`` (GPU only; stats is the
+    per-block (sum, sumsq) slab consumed by :func:`ops.bn.batchnorm_act`).
+    """
+    if _native.use_native(x5):
+        y, stats = ConvFn.apply(x5.to(torch.bfloat16), w, b, spec, act_code(act), want_stats)
+        return (y, stats) if want_stats else y
+    y = ref.conv(x5, w.to(x5.dtype), None if b is None else b.to(x5.dtype), spec, act)
+    return (y, None) if want_stats else y

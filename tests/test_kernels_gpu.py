@@ -1,0 +1,239 @@
+"""HIP kernel numerics vs the PyTorch fp32 reference of the same op.
+
+Every test feeds identical bf16-rounded inputs to the native kernel and to
+the fp32 reference (``featurenet_amd.ops.reference``) and compares with
+tolerances scaled to bf16 output rounding.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from featurenet_amd import _native  # noqa: E402
+from featurenet_amd.ops import reference as ref  # noqa: E402
+from featurenet_amd.ops.spec import ConvSpec, PoolSpec  # noqa: E402
+
+
+def _native_loaded():
+    assert _native.kernels_available(), "HIP kernel library (_C) must be built and loadable on the GPU box"
+
+
+def close(a, b, rtol=2e-2, atol_frac=1e-2):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    scale = b.abs().max().item() + 1e-6
+    err = (a - b).abs().max().item()
+    assert err <= atol_frac * scale + rtol * 0, f"max abs err {err:.4g} vs scale {scale:.4g}"
+
+
+CONV_CASES = [
+    # (N, D, H, W, C, K, kernel, stride, padding)
+    (2, 29, 29, 29, 32, 32, (5, 5, 5), 1, "valid"),      # FeatureNet conv2
+    (2, 25, 25, 25, 32, 64, (4, 4, 4), 1, "valid"),      # conv3
+    (2, 22, 22, 22, 64, 64, (3, 3, 3), 1, "valid"),      # conv4
+    (2, 64, 64, 64, 1, 32, (7, 7, 7), 2, "valid"),       # conv1 (Cin=1 scalar gather)
+    (4, 1, 32, 32, 3, 6, (1, 5, 5), 1, "same"),           # LeNet-style 2-D, odd channels
+    (4, 1, 16, 16, 16, 24, (1, 3, 3), 2, "same"),         # strided same-padded 2-D
+    (3, 1, 15, 17, 24, 100, (1, 3, 1), 1, "same"),        # asymmetric kernel, Cout > 64
+    (5, 1, 1, 40, 8, 16, (1, 1, 5), 1, "same"),           # 1-D conv
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_bwd(case):
+    _native_loaded()
+    from featurenet_amd.ops.conv import ConvFn
+
+    N, D, H, W, C, K, k, s, pad = case
+    torch.manual_seed(0)
+    dev = "cuda"
+    x = torch.randn(N, D, H, W, C, device=dev).to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, K, k, s, pad)
+    w = (torch.randn(K, spec.KD, spec.KH, spec.KW, C, device=dev) * 0.05).to(torch.bfloat16).float()
+    b = torch.randn(K, device=dev) * 0.1
+    xr = x.float().clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = ref.conv(xr, wr, br, spec)
+    xn = x.clone().requires_grad_(True)
+    wn = w.clone().requires_grad_(True)
+    bn = b.clone().requires_grad_(True)
+    yn, _ = ConvFn.apply(xn, wn, bn, spec, 0, False)
+    assert yn.shape == yr.shape
+    close(yn, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(g)
+    yn.backward(g.to(torch.bfloat16))
+    close(xn.grad, xr.grad)
+    close(wn.grad, wr.grad)
+    close(bn.grad, br.grad)
+
+
+def test_conv_stats_epilogue():
+    _native_loaded()
+    from featurenet_amd.ops.conv import native_conv_fwd, _pack_rows
+
+    torch.manual_seed(1)
+    x = torch.randn(2, 12, 12, 12, 32, device="cuda").to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, 32, (3, 3, 3))
+    w = torch.randn(32, 3, 3, 3, 32, device="cuda") * 0.05
+    wm, ld = _pack_rows(w.reshape(32, -1))
+    y, stats = native_conv_fwd(x, wm, ld, None, spec, 0, True)
+    s = stats.sum(0)
+    yf = y.float().reshape(-1, 32)
+    torch.testing.assert_close(s[0], yf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("C,act", [(32, "relu"), (64, None), (6, "tanh"), (24, "sigmoid")])
+@pytest.mark.parametrize("training", [True, False])
+def test_batchnorm_act(C, act, training):
+    _native_loaded()
+    from featurenet_amd.ops.bn import batchnorm_act
+
+    torch.manual_seed(2)
+    y = (torch.randn(3, 5, 6, 7, C, device="cuda") * 2 + 0.5).to(torch.bfloat16)
+    gamma = (torch.rand(C, device="cuda") + 0.5)
+    beta = torch.randn(C, device="cuda") * 0.1
+    rm, rv = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    rm2, rv2 = rm.clone(), rv.clone()
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    yr = y.float().clone().requires_grad_(True)
+    zr = ref.batchnorm_act(yr, gr, br, rm2, rv2, training, 0.1, 1e-5, act)
+    gn, bn = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    yn = y.clone().requires_grad_(True)
+    zn = batchnorm_act(yn, gn, bn, rm, rv, training, 0.1, 1e-5, act)
+    close(zn, zr)
+    if training:
+        torch.testing.assert_close(rm, rm2, rtol=1e-3, atol=1e-4)
+        torch.testing.assert_close(rv, rv2, rtol=1e-3, atol=1e-4)
+    g = torch.randn_like(zr).to(torch.bfloat16).float()
+    zr.backward(g)
+    zn.backward(g.to(torch.bfloat16))
+    close(yn.grad, yr.grad, atol_frac=2e-2)
+    close(gn.grad, gr.grad)
+    close(bn.grad, br.grad)
+
+
+@pytest.mark.parametrize("shape,kernel,stride,pad,kind", [
+    ((2, 20, 20, 20, 64), (2, 2, 2), None, "valid", "max"),
+    ((3, 1, 9, 9, 16), (1, 3, 3), (1, 2, 2), "same", "max"),
+    ((3, 1, 9, 9, 16), (1, 3, 3), (1, 1, 1), "same", "avg"),
+    ((2, 1, 7, 7, 6), (1, 2, 2), None, "same", "avg"),
+])
+def test_pool(shape, kernel, stride, pad, kind):
+    _native_loaded()
+    from featurenet_amd.ops.pool import pool
+
+    torch.manual_seed(3)
+    x = torch.randn(*shape, device="cuda").to(torch.bfloat16)
+    ps = PoolSpec.make(x.shape, kernel, stride, pad)
+    xr = x.float().clone().requires_grad_(True)
+    yr = ref.pool(xr, ps, kind)
+    xn = x.clone().requires_grad_(True)
+    yn = pool(xn, ps, kind)
+    close(yn, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(g)
+    yn.backward(g.to(torch.bfloat16))
+    close(xn.grad, xr.grad)
+
+
+def test_bn_act_pool_fused():
+    _native_loaded()
+    from featurenet_amd.ops.bn import batchnorm_act_pool
+
+    torch.manual_seed(4)
+    C = 64
+    y = torch.randn(2, 8, 8, 8, C, device="cuda").to(torch.bfloat16)
+    ps = PoolSpec.make(y.shape, (2, 2, 2))
+    g0, b0 = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    gr, br = g0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+    yr = y.float().clone().requires_grad_(True)
+    zr = ref.pool(ref.batchnorm_act(yr, gr, br, rm.clone(), rv.clone(), True, 0.1, 1e-5, "relu"), ps, "max")
+    gn, bn = g0.clone().requires_grad_(True), b0.clone().requires_grad_(True)
+    yn = y.clone().requires_grad_(True)
+    zn = batchnorm_act_pool(yn, gn, bn, rm, rv, True, ps, "max", act="relu")
+    close(zn, zr)
+    g = torch.randn_like(zr).to(torch.bfloat16).float()
+    zr.backward(g)
+    zn.backward(g.to(torch.bfloat16))
+    close(yn.grad, yr.grad, atol_frac=3e-2)
+    close(gn.grad, gr.grad, atol_frac=2e-2)
+    close(bn.grad, br.grad, atol_frac=2e-2)
+
+
+def test_softmax_xent():
+    _native_loaded()
+    from featurenet_amd.ops.loss import softmax_xent
+
+    torch.manual_seed(5)
+    for B, NC in ((7, 24), (64, 100), (3, 2)):
+        logits = torch.randn(B, NC, device="cuda") * 3
+        labels = torch.randint(0, NC, (B,), device="cuda")
+        lr_ = logits.clone().requires_grad_(True)
+        l_ref = torch.nn.functional.cross_entropy(lr_, labels)
+        l_ref.backward()
+        ln_ = logits.clone().requires_grad_(True)
+        l_nat, correct = softmax_xent(ln_, labels, with_correct=True)
+        l_nat.backward()
+        torch.testing.assert_close(l_nat, l_ref, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(ln_.grad, lr_.grad, rtol=1e-4, atol=1e-6)
+        assert int(correct.sum()) == int((logits.argmax(-1) == labels).sum())
+
+
+@pytest.mark.parametrize("keras", [True, False])
+def test_adam_flat(keras):
+    _native_loaded()
+    from featurenet_amd.ops.optim import FlatAdam
+
+    torch.manual_seed(6)
+    n = 10_001
+    p = torch.randn(n, device="cuda")
+    g = torch.randn(n, device="cuda")
+    shadow = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    a = FlatAdam(p.clone(), g, lr=1e-2, keras_eps=keras, shadow=shadow)
+    b = FlatAdam(p.clone().cpu(), g.cpu(), lr=1e-2, keras_eps=keras)
+    for _ in range(3):
+        a.step(0.5)
+        b.step(0.5)
+    torch.testing.assert_close(a.p.cpu(), b.p, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(shadow.float().cpu(), b.p.bfloat16().float(), rtol=1e-2, atol=1e-3)
+
+
+def test_dropout_mask_consistent():
+    _native_loaded()
+    from featurenet_amd.ops.elementwise import dropout
+
+    x = torch.ones(4096, 32, device="cuda", dtype=torch.bfloat16).requires_grad_(True)
+    y = dropout(x, 0.3, True)
+    keep = (y.float() != 0)
+    frac = keep.float().mean().item()
+    assert 0.65 < frac < 0.75
+    y.float().sum().backward()
+    assert torch.equal(x.grad.float() != 0, keep)
+    torch.testing.assert_close(y.float()[keep], torch.full_like(y.float()[keep], 1 / 0.7), rtol=1e-2, atol=1e-2)
+
+
+def test_featurenet3d_matches_reference_step():
+    """One full fwd/bwd of FeatureNet-3D on GPU vs the CPU reference path."""
+    _native_loaded()
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+    from featurenet_amd.ops import softmax_xent
+
+    torch.manual_seed(7)
+    cfg = FeatureNet3DConfig(input_size=32, num_classes=24, kernels=(5, 3, 3, 3), strides=(2, 1, 1, 1))
+    m_gpu = FeatureNet3D(cfg)
+    m_cpu = FeatureNet3D(cfg)
+    m_cpu.load_state_dict(m_gpu.state_dict())
+    m_gpu = m_gpu.cuda()
+    x = (torch.rand(4, 32, 32, 32, 1) < 0.3).float()
+    y = torch.randint(0, 24, (4,))
+    lg = m_gpu(x.cuda().bfloat16())
+    lc = m_cpu(x)
+    close(lg, lc, atol_frac=5e-2)
+    softmax_xent(lg, y.cuda()).backward()
+    softmax_xent(lc, y).backward()
+    for (n1, p1), (n2, p2) in zip(m_gpu.named_parameters(), m_cpu.named_parameters()):
+        close(p1.grad, p2.grad, atol_frac=8e-2)
