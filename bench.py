@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches resident on device")
     ap.add_argument("--tiny", action="store_true", help="16^3 2-class plumbing config (not the headline)")
+    ap.add_argument("--torch-layout", choices=["ndhwc", "ncdhw"], default="ndhwc",
+                    help="memory format of the stock-PyTorch baseline (--impl torch)")
     return ap.parse_args()
 
 
@@ -104,15 +106,15 @@ def main():
 
         torch.manual_seed(1234)
         model = TorchFeatureNet3D(input_size=S, num_classes=NC).to(dev)
-        if use_cuda:
+        cl = use_cuda and args.torch_layout == "ndhwc"
+        if cl:
             model = model.to(memory_format=torch.channels_last_3d)
         dmodel = model
         if world > 1:
             dmodel = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local] if use_cuda else None)
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
         xs = [x.permute(0, 4, 1, 2, 3) for x in xs]  # NCDHW view of the channels-last data
-        if use_cuda:
-            xs = [x.contiguous(memory_format=torch.channels_last_3d) for x in xs]
+        xs = [x.contiguous(memory_format=torch.channels_last_3d) if cl else x.contiguous() for x in xs]
         lossf = torch.nn.CrossEntropyLoss()
 
         def step(i):
@@ -123,7 +125,7 @@ def main():
             loss.backward()
             opt.step()
             return loss
-        model_name = "FeatureNet-3D (stock PyTorch eager baseline)"
+        model_name = f"FeatureNet-3D (stock PyTorch eager baseline, {args.torch_layout})"
         flops = None
 
     def sync():
