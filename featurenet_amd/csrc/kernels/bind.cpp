@@ -62,7 +62,7 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("igemm_fwd", [](uintptr_t src, uintptr_t wt, uintptr_t bias, uintptr_t out, uintptr_t stats, uintptr_t tab,
                         std::vector<int> geom, long long M, int N, int K, int ldw, int vec, int act, uintptr_t st) {
-    need(geom, 13, "igemm_fwd");
+    need(geom, 14, "igemm_fwd");
     chk(fn_igemm_fwd(P<const void*>(src), P<const void*>(wt), P<const float*>(bias), P<void*>(out), P<float*>(stats),
                      P<const int*>(tab), geom.data(), M, N, K, ldw, vec, act, S(st)),
         "igemm_fwd");
@@ -70,7 +70,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("igemm_fwd_mblocks", &fn_igemm_fwd_mblocks);
   m.def("igemm_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t part, uintptr_t tab, std::vector<int> geom,
                           long long M, int Cout, int K, int splits, int vec, uintptr_t st) {
-    need(geom, 13, "igemm_wgrad");
+    need(geom, 14, "igemm_wgrad");
     chk(fn_igemm_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(part), P<const int*>(tab), geom.data(), M,
                        Cout, K, splits, vec, S(st)),
         "igemm_wgrad");

@@ -142,26 +142,45 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
 }
 
 // z = act(y*scale + shift)
+// When the channel-chunk count divides 256 (C = 8..2048 powers of two) every
+// thread keeps ONE channel chunk for the whole grid-stride loop, so the
+// per-channel parameters live in registers and no 64-bit modulo runs per
+// element.
 template <int VW>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16* __restrict__ z,
                                                        long long total, int C, int act) {
   const long long nvec = total / VW;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
-    const int c0 = (int)((i * VW) % C);
-    if constexpr (VW == 8) {
-      Pack8 p;
-      p.u = *(const uint4*)(y + i * 8);
+  const int cpr = C / VW;
+  const long long stride = (long long)gridDim.x * 256;
+  const long long i0 = blockIdx.x * 256LL + threadIdx.x;
+  if ((256 % cpr) == 0) {
+    const int c0 = (int)(threadIdx.x % cpr) * VW;
+    float sc[VW], sh[VW];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) p.e[j] = f2bf(act_fwd(bf2f(p.e[j]) * scale[c0 + j] + shift[c0 + j], act));
-      *(uint4*)(z + i * 8) = p.u;
-    } else {
-      z[i] = f2bf(act_fwd(bf2f(y[i]) * scale[c0] + shift[c0], act));
+    for (int j = 0; j < VW; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+    for (long long i = i0; i < nvec; i += stride) {
+      Pack8 p;
+      if constexpr (VW == 8) p.u = *(const uint4*)(y + i * 8); else p.e[0] = y[i];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) p.e[j] = f2bf(act_fwd(bf2f(p.e[j]) * sc[j] + sh[j], act));
+      if constexpr (VW == 8) *(uint4*)(z + i * 8) = p.u; else z[i] = p.e[0];
     }
+    return;
+  }
+  for (long long i = i0; i < nvec; i += stride) {
+    const int c0 = (int)((i * VW) % C);
+    Pack8 p;
+    if constexpr (VW == 8) p.u = *(const uint4*)(y + i * 8); else p.e[0] = y[i];
+#pragma unroll
+    for (int j = 0; j < VW; ++j) p.e[j] = f2bf(act_fwd(bf2f(p.e[j]) * scale[c0 + j] + shift[c0 + j], act));
+    if constexpr (VW == 8) *(uint4*)(z + i * 8) = p.u; else z[i] = p.e[0];
   }
 }
 
 // dy = gamma*invstd*(g - dbeta/M - xhat*dgamma/M), g = dz*act'(z)
+//    = k1*g + k2*y + k3 per channel with k1 = scale,
+//      k2 = -scale*invstd*dgamma/M, k3 = -scale*(dbeta/M - mean*invstd*dgamma/M)
 template <int VW>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ y,
                                                            const float* __restrict__ scale, const float* __restrict__ shift,
@@ -170,8 +189,25 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
                                                            bf16* __restrict__ dy, long long total, int C, float inv_count,
                                                            int act) {
   const long long nvec = total / VW;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (long long)gridDim.x * 256) {
-    const int c0 = (int)((i * VW) % C);
+  const int cpr = C / VW;
+  const long long stride = (long long)gridDim.x * 256;
+  const long long i0 = blockIdx.x * 256LL + threadIdx.x;
+  const bool fixed = (256 % cpr) == 0;
+  float sc[VW], sh[VW], k2[VW], k3[VW];
+  auto load_params = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      const int c = c0 + j;
+      sc[j] = scale[c];
+      sh[j] = shift[c];
+      const float is = invstd[c];
+      k2[j] = -sc[j] * is * dgamma[c] * inv_count;
+      k3[j] = -sc[j] * (dbeta[c] * inv_count - mean[c] * is * dgamma[c] * inv_count);
+    }
+  };
+  if (fixed) load_params((int)(threadIdx.x % cpr) * VW);
+  for (long long i = i0; i < nvec; i += stride) {
+    if (!fixed) load_params((int)((i * VW) % C));
     Pack8 py, pd, po;
     if constexpr (VW == 8) {
       py.u = *(const uint4*)(y + i * 8);
@@ -182,13 +218,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
     }
 #pragma unroll
     for (int j = 0; j < VW; ++j) {
-      const int c = c0 + j;
       const float yv = bf2f(py.e[j]);
-      const float zv = act_fwd(yv * scale[c] + shift[c], act);
+      const float zv = act_fwd(yv * sc[j] + sh[j], act);
       const float g = bf2f(pd.e[j]) * act_bwd_from_out(zv, act);
-      const float xh = (yv - mean[c]) * invstd[c];
-      // scale = gamma*invstd
-      po.e[j] = f2bf(scale[c] * (g - dbeta[c] * inv_count - xh * dgamma[c] * inv_count));
+      po.e[j] = f2bf(sc[j] * g + k2[j] * yv + k3[j]);
     }
     if constexpr (VW == 8) *(uint4*)(dy + i * 8) = po.u;
     else dy[i] = po.e[0];
@@ -367,6 +400,67 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16* __restrict__ 
   }
 }
 
+// Non-overlapping windows (stride == kernel, no padding, dims divisible):
+// one thread per (output window, 8-channel chunk) reads the window once
+// (16-B vectors), recomputes the BN+act prologue, picks the first arg-max and
+// writes the whole window of dx -- every input element is written exactly
+// once, so no zero-fill pass and no gather recomputation.
+template <int VW>
+__global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ x,
+                                                             bf16* __restrict__ dx, const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, PoolGeom g, int is_max,
+                                                             int act) {
+  const int cpr = g.C / VW;
+  const long long total = (long long)g.N * g.OD * g.OH * g.OW * cpr;
+  const int win = g.KD * g.KH * g.KW;
+  const float inv = 1.f / (float)win;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int ch = (int)(i % cpr);
+    long long t = i / cpr;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH); t /= g.OH;
+    const int od = (int)(t % g.OD);
+    const long long n = t / g.OD;
+    float go[VW], sc[VW], sh[VW], best[VW];
+    int arg[VW];
+    Pack8 pg;
+    if constexpr (VW == 8) pg.u = *(const uint4*)(dout + i * 8); else pg.e[0] = dout[i];
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      go[j] = bf2f(pg.e[j]);
+      best[j] = -INFINITY;
+      arg[j] = 0;
+      sc[j] = scale ? scale[ch * VW + j] : 1.f;
+      sh[j] = scale ? shift[ch * VW + j] : 0.f;
+    }
+    auto base_of = [&](int w) {
+      const int kw = w % g.KW, kh = (w / g.KW) % g.KH, kd = w / (g.KW * g.KH);
+      return ((((n * g.D + od * g.KD + kd) * g.H + oh * g.KH + kh) * (long long)g.W + ow * g.KW + kw) * g.C) +
+             ch * VW;
+    };
+    if (is_max) {
+      for (int w = 0; w < win; ++w) {
+        Pack8 p;
+        const long long b = base_of(w);
+        if constexpr (VW == 8) p.u = *(const uint4*)(x + b); else p.e[0] = x[b];
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          float v = bf2f(p.e[j]);
+          if (scale) v = act_fwd(v * sc[j] + sh[j], act);
+          if (v > best[j]) { best[j] = v; arg[j] = w; }
+        }
+      }
+    }
+    for (int w = 0; w < win; ++w) {
+      Pack8 p;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) p.e[j] = f2bf(is_max ? (arg[j] == w ? go[j] : 0.f) : go[j] * inv);
+      const long long b = base_of(w);
+      if constexpr (VW == 8) *(uint4*)(dx + b) = p.u; else dx[b] = p.e[0];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
@@ -460,6 +554,19 @@ extern "C" int fn_pool_bwd(const void* dout, const void* x, void* dx, const floa
                            const int* geom17, int is_max, int count_pad, int act, hipStream_t st) {
   PoolGeom g = pool_geom(geom17);
   const long long ins = (long long)g.N * g.D * g.H * g.W;
+  const bool tiled = g.sd == g.KD && g.sh == g.KH && g.sw == g.KW && g.pd == 0 && g.ph == 0 && g.pw == 0 &&
+                     g.D == g.OD * g.KD && g.H == g.OH * g.KH && g.W == g.OW * g.KW;
+  if (tiled) {
+    const long long outs = (long long)g.N * g.OD * g.OH * g.OW;
+    if (g.C % 8 == 0)
+      hipLaunchKernelGGL(pool_bwd_tiled_kernel<8>, dim3(ew_blocks(outs * (g.C / 8))), dim3(256), 0, st,
+                         (const bf16*)dout, (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, act);
+    else
+      hipLaunchKernelGGL(pool_bwd_tiled_kernel<1>, dim3(ew_blocks(outs * g.C)), dim3(256), 0, st, (const bf16*)dout,
+                         (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, act);
+    FN_CHECK_LAUNCH();
+    return 0;
+  }
   if (g.C % 8 == 0)
     hipLaunchKernelGGL(pool_bwd_kernel<8>, dim3(ew_blocks(ins * (g.C / 8))), dim3(256), 0, st, (const bf16*)dout,
                        (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, count_pad, act);

@@ -33,7 +33,15 @@ struct GatherGeom {
   int md, mh, mw;          // base coord = r * mul + add
   int ad, ah, aw;
   int SD, SH, SW, SC;      // gathered source tensor dims (channels-last)
+  int kwc;                 // packed-W mode: KW*C valid elements per (kd, kh) row
 };
+
+// gather modes
+#define GM_SCALAR 0   // one table entry per k element (any C)
+#define GM_VEC 1      // C % 8 == 0: one entry per 8 channels of one tap, 16-B load
+#define GM_PACKW 2    // C < 8, W-dilation 1: the (kw, c) run of a (kd, kh) row is
+                      // contiguous in memory -> one (possibly unaligned) 16-B load
+                      // covers 8 consecutive (kw, c) pairs; rows padded to 8
 
 // ---------------------------------------------------------------------------
 // Gather helpers
@@ -64,16 +72,40 @@ __device__ __forceinline__ bool tap_ok(const RowBase& r, const int4& e, const Ga
          (unsigned)(r.bh + e.z) < (unsigned)g.SH && (unsigned)(r.bw + e.w) < (unsigned)g.SW;
 }
 
-// load 8 consecutive k of one row (VEC: one 16-B load from one tap)
-template <bool VEC>
+// load 8 consecutive k of one row
+typedef uint4 uint4_u2 __attribute__((aligned(2)));
+template <int GM>
 __device__ __forceinline__ uint4 gather8(const bf16* __restrict__ src, const int4* __restrict__ tab,
                                          const RowBase& r, int k0, int Kdim, const GatherGeom& g) {
   Pack8 p;
-  if constexpr (VEC) {
+  if constexpr (GM == GM_VEC) {
     p.u = make_uint4(0, 0, 0, 0);
     if (k0 < Kdim) {
       const int4 e = tab[k0 >> 3];
       if (tap_ok(r, e, g)) p.u = *(const uint4*)(src + r.base + e.x);
+    }
+  } else if constexpr (GM == GM_PACKW) {
+    // entry: {row offset + p0, (zd<<16)|zh, (kw_lo<<16)|kw_hi, p0}
+    p.u = make_uint4(0, 0, 0, 0);
+    if (k0 < Kdim && r.valid) {
+      const int4 e = tab[k0 >> 3];
+      const int zd = e.y >> 16, zh = e.y & 0xffff;
+      const int lo = e.z >> 16, hi = e.z & 0xffff;
+      if ((unsigned)(r.bd + zd) < (unsigned)g.SD && (unsigned)(r.bh + zh) < (unsigned)g.SH) {
+        if (r.bw + lo >= 0 && r.bw + hi < g.SW) {
+          p.u = *(const uint4_u2*)(src + r.base + e.x);
+        } else {
+          const long long rowb = r.base + e.x - e.w;   // element offset of (kd, kh, kw=0, c=0)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int pp = e.w + j;
+            const int kw = pp / g.SC;
+            bf16 v = (bf16)0.f;
+            if (pp < g.kwc && (unsigned)(r.bw + kw) < (unsigned)g.SW) v = src[rowb + pp];
+            p.e[j] = v;
+          }
+        }
+      }
     }
   } else {
 #pragma unroll
@@ -96,7 +128,7 @@ __device__ __forceinline__ uint4 gather8(const bf16* __restrict__ src, const int
 #define FWD_BM 256
 #define FWD_BK 64
 
-template <int BN, bool VEC, int ACT, bool HAS_BIAS, bool STATS>
+template <int BN, int GM, int ACT, bool HAS_BIAS, bool STATS>
 __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
     const bf16* __restrict__ src, const bf16* __restrict__ wt, const float* __restrict__ bias,
     bf16* __restrict__ out, float* __restrict__ stats, const int4* __restrict__ tab, GatherGeom g,
@@ -127,7 +159,7 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
   auto load_stage = [&](int kt) {
     const int kbase = kt * FWD_BK;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) ra[c] = gather8<VEC>(src, tab, rb, kbase + c * 8, Kdim, g);
+    for (int c = 0; c < 8; ++c) ra[c] = gather8<GM>(src, tab, rb, kbase + c * 8, Kdim, g);
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int idx = tid + i * 256;
@@ -226,18 +258,19 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
     }
   }
   if constexpr (STATS) {
-    __shared__ float red[4][2][BN];
+    // reuse the (now idle) B staging region: keeps LDS at 2 blocks/CU
+    float* red = reinterpret_cast<float*>(smem + 2 * A_STAGE);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       float s = csum[nt], q = csq[nt];
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-      if (lg == 0) { red[wave][0][nt * 16 + lr] = s; red[wave][1][nt * 16 + lr] = q; }
+      if (lg == 0) { red[(wave * 2 + 0) * BN + nt * 16 + lr] = s; red[(wave * 2 + 1) * BN + nt * 16 + lr] = q; }
     }
     __syncthreads();
     if (tid < BN && n0 + tid < Ncol) {
-      float s = red[0][0][tid] + red[1][0][tid] + red[2][0][tid] + red[3][0][tid];
-      float q = red[0][1][tid] + red[1][1][tid] + red[2][1][tid] + red[3][1][tid];
+      float s = red[0 * BN + tid] + red[2 * BN + tid] + red[4 * BN + tid] + red[6 * BN + tid];
+      float q = red[1 * BN + tid] + red[3 * BN + tid] + red[5 * BN + tid] + red[7 * BN + tid];
       stats[(long long)mb * 2 * Ncol + n0 + tid] = s;
       stats[(long long)mb * 2 * Ncol + Ncol + n0 + tid] = q;
     }
@@ -288,7 +321,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* base, int ld, int col0, in
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int BCO, bool VEC, bool VECN>
+template <int BCO, int GM, bool VECN>
 __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ src, float* __restrict__ part,
     const int4* __restrict__ tab, GatherGeom g, long long M, int Cout, int Kdim, long long rows_per_split) {
@@ -347,7 +380,7 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
   auto load_stage = [&](long long ms) {
     const RowBase r = make_row();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rx[i] = gather8<VEC>(src, tab, r, kc0 + (xc + i) * 8, Kdim, g);
+    for (int i = 0; i < 4; ++i) rx[i] = gather8<GM>(src, tab, r, kc0 + (xc + i) * 8, Kdim, g);
     ry = make_uint4(0, 0, 0, 0);
     if (tid < Y_CHUNKS) {
       const int row = tid / (BCO / 8), ch = tid % (BCO / 8);
@@ -406,8 +439,11 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
     __syncthreads();
   }
 
-  // D[row=co][col=k]: lane holds rows (lane>>4)*4+r, col lane&15
-  float* dst = part + (long long)blockIdx.z * Cout * Kdim;
+  // D[row=co][col=k]: lane holds rows (lane>>4)*4+r, col lane&15.
+  // Split-m partial sums are folded straight into the fp32 dW with no-return
+  // float atomics (one 256-B-class wave instruction per accumulator register;
+  // S x Cout x Kdim x 4 B of atomic traffic, well under the ~1.3 TB/s rate).
+  float* dst = part;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -416,7 +452,7 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + mt * 16 + (lane >> 4) * 4 + r;
-        if (co < Cout && k < Kdim) dst[(long long)co * Kdim + k] = acc[mt][nt][r];
+        if (co < Cout && k < Kdim) atomicAdd(dst + (long long)co * Kdim + k, acc[mt][nt][r]);
       }
     }
 }
@@ -447,7 +483,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // ---------------------------------------------------------------------------
 // Host launchers (C ABI, used by bind.cpp)
 // ---------------------------------------------------------------------------
-template <int BN, bool VEC>
+template <int BN, int VEC>
 static void launch_fwd_bn(dim3 grid, hipStream_t st, const bf16* src, const bf16* wt, const float* bias, bf16* out,
                           float* stats, const int4* tab, const GatherGeom& g, long long M, int N, int K, int ldw,
                           int act) {
@@ -476,7 +512,7 @@ extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, 
   g.RD = geom13[0]; g.RH = geom13[1]; g.RW = geom13[2];
   g.md = geom13[3]; g.mh = geom13[4]; g.mw = geom13[5];
   g.ad = geom13[6]; g.ah = geom13[7]; g.aw = geom13[8];
-  g.SD = geom13[9]; g.SH = geom13[10]; g.SW = geom13[11]; g.SC = geom13[12];
+  g.SD = geom13[9]; g.SH = geom13[10]; g.SW = geom13[11]; g.SC = geom13[12]; g.kwc = geom13[13];
   if (stats && act != ACT_NONE) return -1;  // stats are taken on the pre-BN output
   const int BN = Ncol <= 16 ? 16 : (Ncol <= 32 ? 32 : 64);
   const long long mblocks = (M + FWD_BM - 1) / FWD_BM;
@@ -485,15 +521,16 @@ extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, 
   const bf16* w = (const bf16*)wt;
   bf16* o = (bf16*)out;
   const int4* t = (const int4*)tab;
-  if (vec) {
-    if (BN == 16) launch_fwd_bn<16, true>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
-    else if (BN == 32) launch_fwd_bn<32, true>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
-    else launch_fwd_bn<64, true>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
-  } else {
-    if (BN == 16) launch_fwd_bn<16, false>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
-    else if (BN == 32) launch_fwd_bn<32, false>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
-    else launch_fwd_bn<64, false>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);
-  }
+#define FWD_GM(GMV)                                                                                      \
+  do {                                                                                                   \
+    if (BN == 16) launch_fwd_bn<16, GMV>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);      \
+    else if (BN == 32) launch_fwd_bn<32, GMV>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act); \
+    else launch_fwd_bn<64, GMV>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);              \
+  } while (0)
+  if (vec == GM_VEC) FWD_GM(GM_VEC);
+  else if (vec == GM_PACKW) FWD_GM(GM_PACKW);
+  else FWD_GM(GM_SCALAR);
+#undef FWD_GM
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -506,7 +543,7 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* part, cons
   g.RD = geom13[0]; g.RH = geom13[1]; g.RW = geom13[2];
   g.md = geom13[3]; g.mh = geom13[4]; g.mw = geom13[5];
   g.ad = geom13[6]; g.ah = geom13[7]; g.aw = geom13[8];
-  g.SD = geom13[9]; g.SH = geom13[10]; g.SW = geom13[11]; g.SC = geom13[12];
+  g.SD = geom13[9]; g.SH = geom13[10]; g.SW = geom13[11]; g.SC = geom13[12]; g.kwc = geom13[13];
   const int BCO = Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64);
   const long long rps = ((M + splits - 1) / splits + WG_BR - 1) / WG_BR * WG_BR;
   dim3 grid((Kdim + WG_BK - 1) / WG_BK, (Cout + BCO - 1) / BCO, splits);
@@ -515,13 +552,20 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* part, cons
   const bf16* s = (const bf16*)src;
   const int4* t = (const int4*)tab;
 #define WG_CASE(B, V, VN) hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, part, t, g, M, Cout, Kdim, rps)
-  if (vec) {
-    if (vecn) { if (BCO == 16) WG_CASE(16, true, true); else if (BCO == 32) WG_CASE(32, true, true); else WG_CASE(64, true, true); }
-    else { if (BCO == 16) WG_CASE(16, true, false); else if (BCO == 32) WG_CASE(32, true, false); else WG_CASE(64, true, false); }
-  } else {
-    if (vecn) { if (BCO == 16) WG_CASE(16, false, true); else if (BCO == 32) WG_CASE(32, false, true); else WG_CASE(64, false, true); }
-    else { if (BCO == 16) WG_CASE(16, false, false); else if (BCO == 32) WG_CASE(32, false, false); else WG_CASE(64, false, false); }
-  }
+#define WG_GM(GMV)                                                                   \
+  do {                                                                               \
+    if (vecn) {                                                                      \
+      if (BCO == 16) WG_CASE(16, GMV, true); else if (BCO == 32) WG_CASE(32, GMV, true); \
+      else WG_CASE(64, GMV, true);                                                   \
+    } else {                                                                         \
+      if (BCO == 16) WG_CASE(16, GMV, false); else if (BCO == 32) WG_CASE(32, GMV, false); \
+      else WG_CASE(64, GMV, false);                                                  \
+    }                                                                                \
+  } while (0)
+  if (vec == GM_VEC) WG_GM(GM_VEC);
+  else if (vec == GM_PACKW) WG_GM(GM_PACKW);
+  else WG_GM(GM_SCALAR);
+#undef WG_GM
 #undef WG_CASE
   FN_CHECK_LAUNCH();
   return 0;

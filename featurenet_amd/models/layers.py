@@ -156,3 +156,58 @@ class Pool(nn.Module):
         if len(shape) == 3:
             return out.reshape(n, w, c)
         return out
+
+
+class DepthwiseConv(nn.Module):
+    """Depthwise convolution (Keras ``DepthwiseConv2D``, depth_multiplier ``mult``)."""
+
+    def __init__(self, cin: int, kernel, stride=1, padding="same", act=None, mult: int = 1, bias: bool = True):
+        super().__init__()
+        self.cin, self.mult, self.act = cin, mult, act
+        self.kernel = _triple(kernel)
+        self.stride, self.padding = stride, padding
+        KD, KH, KW = self.kernel
+        self.weight = nn.Parameter(torch.empty(cin * mult, KD, KH, KW, 1))
+        glorot_uniform_(self.weight, KD * KH * KW, KD * KH * KW * mult)
+        self.bias = nn.Parameter(torch.zeros(cin * mult)) if bias else None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        shape = x.shape
+        x5 = x.reshape(to5d_shape(shape))
+        cs = ConvSpec.make(tuple(x5.shape), self.cin * self.mult, self.kernel, self.stride, self.padding)
+        out = ops.depthwise_conv(x5, self.weight, self.bias, cs, self.mult, self.act)
+        n, d, h, w, c = out.shape
+        if len(shape) == 4:
+            return out.reshape(n, h, w, c)
+        if len(shape) == 3:
+            return out.reshape(n, w, c)
+        return out
+
+
+class SeparableConv(nn.Module):
+    """Keras ``SeparableConv1D/2D``: depthwise (no bias) -> pointwise 1x1 (bias) -> activation."""
+
+    def __init__(self, cin: int, cout: int, kernel, stride=1, padding="same", act=None):
+        super().__init__()
+        self.depthwise = DepthwiseConv(cin, kernel, stride, padding, None, 1, bias=False)
+        self.pointwise = Conv(cin, cout, 1, 1, "valid", act=act, bias=True)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.pointwise(self.depthwise(x))
+
+
+class AxisBatchNorm(nn.Module):
+    """BatchNorm over an arbitrary axis (the reference forces ``axis=1``,
+    ``model/operation.py:142``; on NHWC tensors that normalises per image row)."""
+
+    def __init__(self, channels: int, axis: int = -1, act=None, momentum: float = 0.01, eps: float = 1e-3):
+        super().__init__()
+        self.axis = axis
+        self.bn = BatchNorm(channels, act, momentum, eps)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        ax = self.axis if self.axis >= 0 else x.dim() + self.axis
+        if ax == x.dim() - 1:
+            return self.bn(x)
+        xt = x.movedim(ax, -1).contiguous()
+        return self.bn(xt).movedim(-1, ax).contiguous()

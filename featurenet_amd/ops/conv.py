@@ -42,6 +42,51 @@ def _fwd_table(spec: ConvSpec, vec: bool) -> np.ndarray:
     return tab
 
 
+GM_SCALAR, GM_VEC, GM_PACKW = 0, 1, 2
+
+
+def gather_mode(spec: ConvSpec) -> int:
+    """Kernel gather mode for the forward / wgrad im2col of ``x``."""
+    if spec.C % 8 == 0:
+        return GM_VEC
+    if spec.C < 8 and spec.dw == 1:
+        return GM_PACKW
+    return GM_SCALAR
+
+
+def packw_row(spec: ConvSpec) -> int:
+    """Elements per (kd, kh) row of the packed-W K layout (KW*C rounded up to 8)."""
+    return (spec.KW * spec.C + 7) // 8 * 8
+
+
+def _packw_table(spec: ConvSpec) -> np.ndarray:
+    C, R = spec.C, packw_row(spec)
+    rows = []
+    for kd in range(spec.KD):
+        for kh in range(spec.KH):
+            zd, zh = kd * spec.dd, kh * spec.dh
+            base = ((zd * spec.H + zh) * spec.W) * C
+            for p0 in range(0, R, 8):
+                lo = p0 // C
+                hi = (p0 + 7) // C
+                rows.append((base + p0, (zd << 16) | zh, (lo << 16) | hi, p0))
+    return np.asarray(rows, dtype=np.int64)
+
+
+def kdim_gather(spec: ConvSpec) -> int:
+    return spec.KD * spec.KH * packw_row(spec) if gather_mode(spec) == GM_PACKW else spec.kdim
+
+
+def pack_weight_rows(w: torch.Tensor, spec: ConvSpec) -> tuple[torch.Tensor, int]:
+    """Forward B operand [Cout, Kdim'] in the gather layout of ``spec``."""
+    if gather_mode(spec) == GM_PACKW:
+        R = packw_row(spec)
+        out = torch.zeros(spec.K, spec.KD * spec.KH, R, dtype=torch.bfloat16, device=w.device)
+        out[:, :, : spec.KW * spec.C] = w.reshape(spec.K, spec.KD * spec.KH, spec.KW * spec.C)
+        return out.reshape(spec.K, -1), spec.KD * spec.KH * R
+    return _pack_rows(w.reshape(spec.K, spec.kdim))
+
+
 def _dgrad_table(spec: ConvSpec, vec: bool) -> np.ndarray:
     """k' = tap*K + co over dy (dims OD', OH', OW' = zero-inserted dy)."""
     K = spec.K
@@ -65,7 +110,10 @@ def _table(spec: ConvSpec, kind: str, vec: bool, device) -> torch.Tensor:
     key = (spec, kind, vec, str(device))
     t = _TAB_CACHE.get(key)
     if t is None:
-        arr = _fwd_table(spec, vec) if kind == "fwd" else _dgrad_table(spec, vec)
+        if kind == "fwd":
+            arr = _packw_table(spec) if vec == GM_PACKW else _fwd_table(spec, vec == GM_VEC)
+        else:
+            arr = _dgrad_table(spec, vec)
         if np.abs(arr).max(initial=0) >= 2**31:
             raise ValueError("conv tap offsets overflow int32")
         t = torch.from_numpy(arr.astype(np.int32)).to(device)
@@ -76,12 +124,12 @@ def _table(spec: ConvSpec, kind: str, vec: bool, device) -> torch.Tensor:
 
 def _geom_fwd(spec: ConvSpec) -> list[int]:
     return [spec.OD, spec.OH, spec.OW, spec.sd, spec.sh, spec.sw, -spec.pd, -spec.ph, -spec.pw,
-            spec.D, spec.H, spec.W, spec.C]
+            spec.D, spec.H, spec.W, spec.C, spec.KW * spec.C]
 
 
 def _geom_dgrad(spec: ConvSpec) -> list[int]:
     ODu, OHu, OWu = _dgrad_src_dims(spec)
-    return [spec.D, spec.H, spec.W, 1, 1, 1, spec.pd, spec.ph, spec.pw, ODu, OHu, OWu, spec.K]
+    return [spec.D, spec.H, spec.W, 1, 1, 1, spec.pd, spec.ph, spec.pw, ODu, OHu, OWu, spec.K, 0]
 
 
 def _pack_rows(mat: torch.Tensor) -> tuple[torch.Tensor, int]:
@@ -102,15 +150,15 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
                     want_stats: bool):
     K = _native.kernels()
     assert x5.is_contiguous() and x5.dtype == torch.bfloat16
-    vec = spec.C % 8 == 0
-    tab = _table(spec, "fwd", vec, x5.device)
+    gm = gather_mode(spec)
+    tab = _table(spec, "fwd", gm, x5.device)
     y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
     stats = None
     if want_stats:
         nmb = K.igemm_fwd_mblocks(spec.M)
         stats = torch.empty(nmb, 2, spec.K, dtype=torch.float32, device=x5.device)
     K.igemm_fwd(x5.data_ptr(), wmat.data_ptr(), _native.ptr(bias), y.data_ptr(), _native.ptr(stats),
-                tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K, spec.kdim, ldw, int(vec), act,
+                tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K, kdim_gather(spec), ldw, gm, act,
                 _native.stream(x5))
     return y, stats
 
@@ -123,19 +171,19 @@ def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec) -> tor
         up[:, :: spec.sd, :: spec.sh, :: spec.sw] = dy5
         dy5 = up
     dy5 = dy5.contiguous()
-    vec = spec.K % 8 == 0
-    tab = _table(spec, "dgrad", vec, dy5.device)
+    vec = GM_VEC if spec.K % 8 == 0 else GM_SCALAR
+    tab = _table(spec, "dgrad", vec == GM_VEC, dy5.device)
     # WT[ci][tap][co] = w[co][tap][ci]
     wt = w.reshape(spec.K, spec.taps, spec.C).permute(2, 1, 0).reshape(spec.C, spec.taps * spec.K)
     wt, ldw = _pack_rows(wt)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     M = spec.N * spec.D * spec.H * spec.W
     K.igemm_fwd(dy5.data_ptr(), wt.data_ptr(), 0, dx.data_ptr(), 0, tab.data_ptr(), _geom_dgrad(spec), M, spec.C,
-                spec.taps * spec.K, ldw, int(vec), 0, _native.stream(dy5))
+                spec.taps * spec.K, ldw, vec, 0, _native.stream(dy5))
     return dx
 
 
-def wgrad_splits(spec: ConvSpec, target_blocks: int = 2048) -> int:
+def wgrad_splits(spec: ConvSpec, target_blocks: int = 1024) -> int:
     col_tiles = math.ceil(spec.kdim / 256)
     co_tiles = math.ceil(spec.K / 64) if spec.K > 32 else 1
     s = max(1, math.ceil(target_blocks / (col_tiles * co_tiles)))
@@ -144,16 +192,16 @@ def wgrad_splits(spec: ConvSpec, target_blocks: int = 2048) -> int:
 
 def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
     K = _native.kernels()
-    vec = spec.C % 8 == 0
-    tab = _table(spec, "fwd", vec, x5.device)
+    gm = gather_mode(spec)
+    tab = _table(spec, "fwd", gm, x5.device)
     splits = wgrad_splits(spec)
-    part = torch.empty(splits, spec.K, spec.kdim, dtype=torch.float32, device=x5.device)
-    st = _native.stream(x5)
-    K.igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), part.data_ptr(), tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K,
-                  spec.kdim, splits, int(vec), st)
-    dw = torch.empty(spec.K, spec.KD, spec.KH, spec.KW, spec.C, dtype=torch.float32, device=x5.device)
-    K.slab_reduce(part.data_ptr(), dw.data_ptr(), dw.numel(), splits, 0, st)
-    return dw
+    kd = kdim_gather(spec)
+    dw = torch.zeros(spec.K, kd, dtype=torch.float32, device=x5.device)
+    K.igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K,
+                  kd, splits, gm, _native.stream(x5))
+    if gm == GM_PACKW:
+        dw = dw.reshape(spec.K, spec.KD * spec.KH, -1)[:, :, : spec.KW * spec.C].contiguous()
+    return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
 
 
 def native_colsum(x2: torch.Tensor) -> torch.Tensor:
@@ -186,7 +234,7 @@ class ConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x5, w, b, spec: ConvSpec, act: int, want_stats: bool):
-        wmat, ldw = _pack_rows(w.detach().reshape(spec.K, spec.kdim))
+        wmat, ldw = pack_weight_rows(w.detach(), spec)
         bias = b.detach().float().contiguous() if b is not None else None
         y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
         ctx.spec, ctx.act, ctx.has_b = spec, act, b is not None
@@ -221,3 +269,16 @@ def conv(x5: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, spec: ConvSp
         return (y, stats) if want_stats else y
     y = ref.conv(x5, w.to(x5.dtype), None if b is None else b.to(x5.dtype), spec, act)
     return (y, None) if want_stats else y
+
+
+def depthwise_conv(x5: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, spec: ConvSpec, mult: int = 1,
+                   act=None) -> torch.Tensor:
+    """Depthwise conv (reference ``DepthwiseConv2D`` / first half of ``SeparableConv2D``).
+
+    Runs through the reference implementation on both devices for now (grouped
+    conv); the search-space shapes are small 2-D images.
+    """
+    dt = x5.dtype
+    y = ref.depthwise_conv(x5.float() if x5.is_cuda else x5, w.float() if x5.is_cuda else w.to(dt),
+                           None if b is None else (b.float() if x5.is_cuda else b.to(dt)), spec, mult, act)
+    return y.to(dt)
