@@ -20,7 +20,6 @@ int fn_igemm_fwd(const void*, const void*, const float*, void*, float*, const in
 int fn_igemm_fwd_mblocks(long long);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
                    hipStream_t);
-int fn_slab_reduce(const float*, float*, long long, int, int, hipStream_t);
 int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
                 int, int, int, int, hipStream_t);
 int fn_bn_finalize(const float*, int, int, double, const float*, const float*, float*, float*, float, float, float*,
@@ -38,6 +37,7 @@ int fn_bias_act(const void*, const float*, void*, long long, int, int, hipStream
 int fn_act_bwd(const void*, const void*, void*, long long, int, hipStream_t);
 int fn_dropout(const void*, void*, long long, float, unsigned, unsigned, hipStream_t);
 int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
+int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 }
 
 template <typename T>
@@ -74,9 +74,6 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_igemm_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(part), P<const int*>(tab), geom.data(), M,
                        Cout, K, splits, vec, S(st)),
         "igemm_wgrad");
-  });
-  m.def("slab_reduce", [](uintptr_t part, uintptr_t out, long long n, int S_, int acc, uintptr_t st) {
-    chk(fn_slab_reduce(P<const float*>(part), P<float*>(out), n, S_, acc, S(st)), "slab_reduce");
   });
   m.def("colstats", [](uintptr_t x, uintptr_t dz, uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd,
                        uintptr_t part, long long M, int C, int act, int mode, int nb, uintptr_t st) {
@@ -148,6 +145,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout", [](uintptr_t x, uintptr_t y, long long total, float p, unsigned seed, unsigned offset,
                       uintptr_t st) {
     chk(fn_dropout(P<const void*>(x), P<void*>(y), total, p, seed, offset, S(st)), "dropout");
+  });
+  m.def("unpack_bits", [](uintptr_t bits, uintptr_t out, long long nbytes, uintptr_t st) {
+    chk(fn_unpack_bits(P<const void*>(bits), P<void*>(out), nbytes, S(st)), "unpack_bits");
   });
   m.def("cast_f32_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t st) {
     chk(fn_cast_f32_bf16(P<const float*>(x), P<void*>(y), n, S(st)), "cast_f32_bf16");

@@ -5,27 +5,37 @@
 //   dgrad: dx[m][ci] = sum_k' A'[m][k'] * WT[ci][k']  A' = "im2col" of dy with
 //          negated tap offsets (stride-1 transposed conv; stride-2 layers are
 //          handled by the caller through zero insertion of dy)
-//   wgrad: dW[co][k] = sum_m dy[m][co] * A[m][k]     (split over m, fp32 slabs)
+//   wgrad: dW[co][k] = sum_m dy[m][co] * A[m][k]     (split over m, fp32 atomics)
 //
 // Nothing is materialised: the gather is driven by a per-layer tap table
 // (built once on the host and cached) whose entries hold the element offset of
 // a k-chunk relative to a row's base plus the tap displacement for the
 // bounds test.  For C % 8 == 0 a table entry covers 8 consecutive channels of
-// one tap, so one 16-byte load feeds one 8-element MFMA fragment slice.
+// one tap, so one 16-byte load feeds one 8-element MFMA fragment slice; for
+// C < 8 (first layers: FeatureNet-3D's 1-channel voxels, RGB images) the
+// (kw, c) run of a (kd, kh) kernel row is contiguous and one unaligned 16-byte
+// load covers 8 (kw, c) pairs ("packed-W").
 //
 // gfx950 specifics:
 //   * mfma_f32_16x16x32_bf16, 64-lane waves, 256-thread workgroups;
-//   * forward/dgrad: BM=256 rows x BN output channels x BK=64, register-staged
-//     double-buffered LDS with the st_16x32-style XOR swizzle
-//     (chunk ^= row & 7) that makes the 16-lane ds_read_b128 groups
-//     conflict-free on 128-B rows;
-//   * wgrad: the reduction runs over m, which is the slow axis of both
-//     operands in memory, so operands are staged row-major and read with
+//   * forward/dgrad: BM=256 rows x BN output channels x BK=64.  ONE LDS stage
+//     (40 KB at BN=64) so 4 workgroups (16 waves) fit a CU; the next stage's
+//     gathers are issued into registers BEFORE the MFMAs of the current stage
+//     and written after the barrier (issue-early / write-late), and the
+//     uniform tap-table entries of the stage after that are prefetched into
+//     SGPRs, so no load sits behind another load on the critical path.
+//     XOR swizzle (chunk ^= row & 7) makes the 16-lane ds_read_b128 groups
+//     conflict-free on the 128-B rows;
+//   * every gather is branchless (clamped address + select): hipcc otherwise
+//     wraps each conditional load in exec-mask branches with per-load waits;
+//   * wgrad: the reduction runs over m, the slow axis of both operands in
+//     memory, so operands are staged row-major and read with
 //     ds_read_b64_tr_b16 (hardware transpose); rows are padded to 32 mod 256 B
 //     and the MFMA k-order is permuted (same permutation on both operands) so
-//     every transposed read is bank-conflict-free;
-//   * XCD-aware block remap so neighbouring M tiles (which share input halos)
-//     run on the same XCD's L2.
+//     every transposed read is bank-conflict-free.  A thread's k-columns are
+//     fixed for the whole kernel, so its tap-table entries load once;
+//   * XCD-aware block remap so neighbouring tiles (which share input halos /
+//     the same rows of x) run on the same XCD's L2.
 #include "common.h"
 
 struct GatherGeom {
@@ -39,27 +49,17 @@ struct GatherGeom {
 // gather modes
 #define GM_SCALAR 0   // one table entry per k element (any C)
 #define GM_VEC 1      // C % 8 == 0: one entry per 8 channels of one tap, 16-B load
-#define GM_PACKW 2    // C < 8, W-dilation 1: the (kw, c) run of a (kd, kh) row is
-                      // contiguous in memory -> one (possibly unaligned) 16-B load
-                      // covers 8 consecutive (kw, c) pairs; rows padded to 8
+#define GM_PACKW 2    // C < 8, W-dilation 1: (kw, c) run of a (kd, kh) row contiguous
 
-// ---------------------------------------------------------------------------
-// Gather helpers
-// ---------------------------------------------------------------------------
 struct RowBase {
   long long base;   // element offset of (n, bd, bh, bw, 0); may be "outside"
   int bd, bh, bw;
   bool valid;
 };
 
-__device__ __forceinline__ RowBase decode_row(long long m, long long M, const GatherGeom& g) {
+__device__ __forceinline__ RowBase make_row(long long n, int c1, int c2, int c3, bool valid, const GatherGeom& g) {
   RowBase r;
-  r.valid = m < M;
-  long long mm = r.valid ? m : 0;
-  int c3 = (int)(mm % g.RW); mm /= g.RW;
-  int c2 = (int)(mm % g.RH); mm /= g.RH;
-  int c1 = (int)(mm % g.RD);
-  long long n = mm / g.RD;
+  r.valid = valid;
   r.bd = c1 * g.md + g.ad;
   r.bh = c2 * g.mh + g.ah;
   r.bw = c3 * g.mw + g.aw;
@@ -67,59 +67,76 @@ __device__ __forceinline__ RowBase decode_row(long long m, long long M, const Ga
   return r;
 }
 
-__device__ __forceinline__ bool tap_ok(const RowBase& r, const int4& e, const GatherGeom& g) {
-  return r.valid && (unsigned)(r.bd + e.y) < (unsigned)g.SD &&
-         (unsigned)(r.bh + e.z) < (unsigned)g.SH && (unsigned)(r.bw + e.w) < (unsigned)g.SW;
+__device__ __forceinline__ RowBase decode_row(long long m, long long M, const GatherGeom& g) {
+  const bool valid = m < M;
+  long long mm = valid ? m : 0;
+  const int c3 = (int)(mm % g.RW); mm /= g.RW;
+  const int c2 = (int)(mm % g.RH); mm /= g.RH;
+  const int c1 = (int)(mm % g.RD);
+  return make_row(mm / g.RD, c1, c2, c3, valid, g);
 }
 
-// load 8 consecutive k of one row
+__device__ __forceinline__ bool tap_ok(const RowBase& r, const int4& e, const GatherGeom& g) {
+  return r.valid && (unsigned)(r.bd + e.y) < (unsigned)g.SD && (unsigned)(r.bh + e.z) < (unsigned)g.SH &&
+         (unsigned)(r.bw + e.w) < (unsigned)g.SW;
+}
+
 typedef uint4 uint4_u2 __attribute__((aligned(2)));
+
+// 8 consecutive k of one row.  VEC / PACKW take the chunk's (prefetched) table
+// entry `e`; SCALAR reads its 8 per-element entries itself.  Loads are issued
+// unconditionally from a clamped address and masked with a select.
 template <int GM>
-__device__ __forceinline__ uint4 gather8(const bf16* __restrict__ src, const int4* __restrict__ tab,
+__device__ __forceinline__ uint4 gather8(const bf16* __restrict__ src, const int4* __restrict__ tab, const int4& e,
                                          const RowBase& r, int k0, int Kdim, const GatherGeom& g) {
-  Pack8 p;
+  const uint4 zero = make_uint4(0, 0, 0, 0);
   if constexpr (GM == GM_VEC) {
-    p.u = make_uint4(0, 0, 0, 0);
-    if (k0 < Kdim) {
-      const int4 e = tab[k0 >> 3];
-      if (tap_ok(r, e, g)) p.u = *(const uint4*)(src + r.base + e.x);
-    }
+    const bool ok = k0 < Kdim && tap_ok(r, e, g);
+    const uint4 v = *(const uint4*)(src + (ok ? r.base + e.x : 0));
+    return ok ? v : zero;
   } else if constexpr (GM == GM_PACKW) {
     // entry: {row offset + p0, (zd<<16)|zh, (kw_lo<<16)|kw_hi, p0}
-    p.u = make_uint4(0, 0, 0, 0);
-    if (k0 < Kdim && r.valid) {
-      const int4 e = tab[k0 >> 3];
-      const int zd = e.y >> 16, zh = e.y & 0xffff;
-      const int lo = e.z >> 16, hi = e.z & 0xffff;
-      if ((unsigned)(r.bd + zd) < (unsigned)g.SD && (unsigned)(r.bh + zh) < (unsigned)g.SH) {
-        if (r.bw + lo >= 0 && r.bw + hi < g.SW) {
-          p.u = *(const uint4_u2*)(src + r.base + e.x);
-        } else {
-          const long long rowb = r.base + e.x - e.w;   // element offset of (kd, kh, kw=0, c=0)
+    const int zd = e.y >> 16, zh = e.y & 0xffff;
+    const int lo = e.z >> 16, hi = e.z & 0xffff;
+    const bool rowok = k0 < Kdim && r.valid && (unsigned)(r.bd + zd) < (unsigned)g.SD &&
+                       (unsigned)(r.bh + zh) < (unsigned)g.SH;
+    const bool fast = rowok && r.bw + lo >= 0 && r.bw + hi < g.SW;
+    uint4 v = *(const uint4_u2*)(src + (fast ? r.base + e.x : 0));
+    v = fast ? v : zero;
+    if (rowok && !fast) {   // row touches the W border: per-element (rare lanes)
+      Pack8 p;
+      const long long rowb = r.base + e.x - e.w;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int pp = e.w + j;
-            const int kw = pp / g.SC;
-            bf16 v = (bf16)0.f;
-            if (pp < g.kwc && (unsigned)(r.bw + kw) < (unsigned)g.SW) v = src[rowb + pp];
-            p.e[j] = v;
-          }
-        }
+      for (int j = 0; j < 8; ++j) {
+        const int pp = e.w + j;
+        const int kw = pp / g.SC;
+        const bool okj = pp < g.kwc && (unsigned)(r.bw + kw) < (unsigned)g.SW;
+        const bf16 x = src[okj ? rowb + pp : 0];
+        p.e[j] = okj ? x : (bf16)0.f;
       }
+      v = p.u;
     }
+    return v;
   } else {
+    Pack8 p;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      bf16 v = (bf16)0.f;
       const int k = k0 + j;
-      if (k < Kdim) {
-        const int4 e = tab[k];
-        if (tap_ok(r, e, g)) v = src[r.base + e.x];
-      }
-      p.e[j] = v;
+      const int4 ee = tab[k < Kdim ? k : 0];
+      const bool ok = k < Kdim && tap_ok(r, ee, g);
+      const bf16 x = src[ok ? r.base + ee.x : 0];
+      p.e[j] = ok ? x : (bf16)0.f;
     }
+    return p.u;
   }
-  return p.u;
+}
+
+template <int GM>
+__device__ __forceinline__ int4 entry_for(const int4* __restrict__ tab, int k0, int Kdim) {
+  if constexpr (GM == GM_SCALAR) return make_int4(0, 0, 0, 0);
+  const int nchunk = (Kdim + 7) >> 3;
+  const int kc = k0 >> 3;
+  return tab[kc < nchunk ? kc : nchunk - 1];
 }
 
 // ---------------------------------------------------------------------------
@@ -129,7 +146,7 @@ __device__ __forceinline__ uint4 gather8(const bf16* __restrict__ src, const int
 #define FWD_BK 64
 
 template <int BN, int GM, int ACT, bool HAS_BIAS, bool STATS>
-__global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
+__global__ __launch_bounds__(256, (BN >= 64 ? 3 : 4)) void igemm_fwd_kernel(
     const bf16* __restrict__ src, const bf16* __restrict__ wt, const float* __restrict__ bias,
     bf16* __restrict__ out, float* __restrict__ stats, const int4* __restrict__ tab, GatherGeom g,
     long long M, int Ncol, int Kdim, int ldw) {
@@ -139,9 +156,10 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
   constexpr int NT = BN / 16;                   // n-tiles per wave
   constexpr int B_CHUNKS = BN * (FWD_BK / 8);   // 16-B chunks per B stage
   constexpr int B_PER_T = (B_CHUNKS + 255) / 256;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * A_STAGE + 2 * B_STAGE];
+  static_assert(FWD_BM * LDO + 16 * BN <= A_STAGE + B_STAGE, "epilogue staging + stats must fit the stage");
+  __shared__ __attribute__((aligned(16))) bf16 smem[A_STAGE + B_STAGE];
   bf16* As = smem;
-  bf16* Bs = smem + 2 * A_STAGE;
+  bf16* Bs = smem + A_STAGE;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -155,24 +173,28 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
 
   uint4 ra[8];
   uint4 rbv[B_PER_T];
+  int4 te[8];   // uniform tap-table entries of the next stage to gather
 
+  auto fetch_entries = [&](int kt) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) te[c] = entry_for<GM>(tab, kt * FWD_BK + c * 8, Kdim);
+  };
   auto load_stage = [&](int kt) {
     const int kbase = kt * FWD_BK;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) ra[c] = gather8<GM>(src, tab, rb, kbase + c * 8, Kdim, g);
+    for (int c = 0; c < 8; ++c) ra[c] = gather8<GM>(src, tab, te[c], rb, kbase + c * 8, Kdim, g);
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int idx = tid + i * 256;
-      rbv[i] = make_uint4(0, 0, 0, 0);
-      if (idx < B_CHUNKS) {
-        const int r = idx >> 3, c = idx & 7;
-        const int k = kbase + c * 8;
-        if (n0 + r < Ncol && k < ldw) rbv[i] = *(const uint4*)(wt + (long long)(n0 + r) * ldw + k);
-      }
+      const int r = (idx >> 3) < BN ? (idx >> 3) : BN - 1;
+      const int k = kbase + (idx & 7) * 8;
+      const bool ok = idx < B_CHUNKS && n0 + r < Ncol && k < ldw;
+      const uint4 v = *(const uint4*)(wt + (ok ? (long long)(n0 + r) * ldw + k : 0));
+      rbv[i] = ok ? v : make_uint4(0, 0, 0, 0);
     }
   };
-  auto write_stage = [&](int buf) {
-    bf16* a = As + buf * A_STAGE + tid * FWD_BK;
+  auto write_stage = [&]() {
+    bf16* a = As + tid * FWD_BK;
 #pragma unroll
     for (int c = 0; c < 8; ++c) *(uint4*)(a + ((c ^ (tid & 7)) << 3)) = ra[c];
 #pragma unroll
@@ -180,7 +202,7 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
       const int idx = tid + i * 256;
       if (idx < B_CHUNKS) {
         const int r = idx >> 3, c = idx & 7;
-        *(uint4*)(Bs + buf * B_STAGE + r * FWD_BK + ((c ^ (r & 7)) << 3)) = rbv[i];
+        *(uint4*)(Bs + r * FWD_BK + ((c ^ (r & 7)) << 3)) = rbv[i];
       }
     }
   };
@@ -192,17 +214,20 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int nk = (Kdim + FWD_BK - 1) / FWD_BK;
+  fetch_entries(0);
   load_stage(0);
-  write_stage(0);
+  if (nk > 1) fetch_entries(1);
+  write_stage();
   __syncthreads();
 
   const int lr = lane & 15;     // row inside a 16-row fragment
   const int lg = lane >> 4;     // k-group (8 elements each)
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_stage(kt + 1);
-    const bf16* a = As + cur * A_STAGE;
-    const bf16* b = Bs + cur * B_STAGE;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      load_stage(kt + 1);                 // gathers in flight during the MFMAs below
+      if (kt + 2 < nk) fetch_entries(kt + 2);
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = ks * 4 + lg;
@@ -210,12 +235,12 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const int row = wave * 64 + mt * 16 + lr;
-        fa[mt] = *(const bf16x8*)(a + row * FWD_BK + ((ch ^ (row & 7)) << 3));
+        fa[mt] = *(const bf16x8*)(As + row * FWD_BK + ((ch ^ (row & 7)) << 3));
       }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const int row = nt * 16 + lr;
-        fb[nt] = *(const bf16x8*)(b + row * FWD_BK + ((ch ^ (row & 7)) << 3));
+        fb[nt] = *(const bf16x8*)(Bs + row * FWD_BK + ((ch ^ (row & 7)) << 3));
       }
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -223,12 +248,15 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
         for (int nt = 0; nt < NT; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
     }
-    if (kt + 1 < nk) write_stage(cur ^ 1);
-    __syncthreads();
+    __syncthreads();                       // every wave done reading the stage
+    if (more) {
+      write_stage();
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: bias + activation, bf16 staging in LDS, BN partial stats ----
-  bf16* Os = smem;  // reuse (all waves passed the final barrier)
+  bf16* Os = smem;  // reuse the A stage (all waves passed the final barrier)
   float csum[NT], csq[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) { csum[nt] = 0.f; csq[nt] = 0.f; }
@@ -248,18 +276,17 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
         const bf16 bvv = f2bf(v);
         Os[row * LDO + col] = bvv;
         if constexpr (STATS) {
-          if (cv && (m0 + row) < M) {
-            const float f = bf2f(bvv);
-            csum[nt] += f;
-            csq[nt] += f * f;
-          }
+          const bool rv = cv && (m0 + row) < M;
+          const float f = rv ? bf2f(bvv) : 0.f;
+          csum[nt] += f;
+          csq[nt] += f * f;
         }
       }
     }
   }
   if constexpr (STATS) {
-    // reuse the (now idle) B staging region: keeps LDS at 2 blocks/CU
-    float* red = reinterpret_cast<float*>(smem + 2 * A_STAGE);
+    // cross-wave reduction scratch right after the staged output tile
+    float* red = reinterpret_cast<float*>(smem + FWD_BM * LDO);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       float s = csum[nt], q = csq[nt];
@@ -269,8 +296,8 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
     }
     __syncthreads();
     if (tid < BN && n0 + tid < Ncol) {
-      float s = red[0 * BN + tid] + red[2 * BN + tid] + red[4 * BN + tid] + red[6 * BN + tid];
-      float q = red[1 * BN + tid] + red[3 * BN + tid] + red[5 * BN + tid] + red[7 * BN + tid];
+      const float s = red[0 * BN + tid] + red[2 * BN + tid] + red[4 * BN + tid] + red[6 * BN + tid];
+      const float q = red[1 * BN + tid] + red[3 * BN + tid] + red[5 * BN + tid] + red[7 * BN + tid];
       stats[(long long)mb * 2 * Ncol + n0 + tid] = s;
       stats[(long long)mb * 2 * Ncol + Ncol + n0 + tid] = q;
     }
@@ -298,8 +325,8 @@ __global__ __launch_bounds__(256, 2) void igemm_fwd_kernel(
 // ---------------------------------------------------------------------------
 // Weight-gradient kernel
 // ---------------------------------------------------------------------------
-#define WG_BR 32     // m-rows per stage (= one MFMA k-step)
-#define WG_BK 256    // k-columns per block
+#define WG_BR 64     // m-rows per stage (two MFMA k-steps)
+#define WG_BK 256    // k-columns per block (64 per wave)
 #define WG_LDX (WG_BK + 16)
 
 template <int BCO>
@@ -308,7 +335,7 @@ struct WgLds {
 };
 
 // k-order permutation shared by both operands: MFMA k-index (group G, elem j)
-// reads stage row (j<4 ? 4G+j : 16+4G+j-4); see header comment.
+// of k-step s reads stage row 32s + (j<4 ? 4G+j : 16+4G+j-4).
 __device__ __forceinline__ bf16x8 tr_frag(const bf16* base, int ld, int col0, int lane) {
   const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   typedef short s4 __attribute__((ext_vector_type(4)));
@@ -323,27 +350,38 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* base, int ld, int col0, in
 
 template <int BCO, int GM, bool VECN>
 __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
-    const bf16* __restrict__ dy, const bf16* __restrict__ src, float* __restrict__ part,
-    const int4* __restrict__ tab, GatherGeom g, long long M, int Cout, int Kdim, long long rows_per_split) {
+    const bf16* __restrict__ dy, const bf16* __restrict__ src, float* __restrict__ dw,
+    const int4* __restrict__ tab, GatherGeom g, long long M, int Cout, int Kdim, long long rows_per_split,
+    int gx, int gy) {
   constexpr int LDY = WgLds<BCO>::LDY;
   constexpr int X_STAGE = WG_BR * WG_LDX;
   constexpr int Y_STAGE = WG_BR * LDY;
   constexpr int MT = BCO / 16;
   constexpr int Y_CHUNKS = WG_BR * (BCO / 8);
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * X_STAGE + 2 * Y_STAGE];
+  constexpr int Y_PER_T = (Y_CHUNKS + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16 smem[X_STAGE + Y_STAGE];
   bf16* Xs = smem;
-  bf16* Ys = smem + 2 * X_STAGE;
+  bf16* Ys = smem + X_STAGE;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kc0 = blockIdx.x * WG_BK;
-  const int co0 = blockIdx.y * BCO;
-  const long long mbeg = (long long)blockIdx.z * rows_per_split;
+  // XCD-aware remap: consecutive logical blocks (same split, neighbouring
+  // column tiles -> same rows of x and dy) share an XCD.
+  const int nwg = gx * gy * gridDim.z;
+  const int lin = xcd_remap(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z), nwg);
+  const int bx = lin % gx, by = (lin / gx) % gy, bz = lin / (gx * gy);
+  const int kc0 = bx * WG_BK;
+  const int co0 = by * BCO;
+  const long long mbeg = (long long)bz * rows_per_split;
   long long mend = mbeg + rows_per_split;
   if (mend > M) mend = M;
 
-  // X-tile loader: thread -> (row r, 4 consecutive 8-col chunks)
-  const int xr = tid & 31;
-  const int xc = (tid >> 5) * 4;
+  // X-tile loader: thread -> (row xr, 8 consecutive 8-col chunks of its wave)
+  const int xr = tid & 63;
+  const int xc = __builtin_amdgcn_readfirstlane(wave) * 8;
+  int4 te[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) te[i] = entry_for<GM>(tab, kc0 + (xc + i) * 8, Kdim);
+
   // incremental row decode for row mbeg + xr (advances by WG_BR per stage)
   long long mcur = mbeg + xr;
   int c3, c2, c1;
@@ -354,15 +392,6 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
     c2 = (int)(mm % g.RH); mm /= g.RH;
     c1 = (int)(mm % g.RD); nn = mm / g.RD;
   }
-  auto make_row = [&]() {
-    RowBase r;
-    r.valid = mcur < mend;
-    r.bd = c1 * g.md + g.ad;
-    r.bh = c2 * g.mh + g.ah;
-    r.bw = c3 * g.mw + g.aw;
-    r.base = (((nn * g.SD + r.bd) * g.SH + r.bh) * (long long)g.SW + r.bw) * g.SC;
-    return r;
-  };
   auto advance_row = [&]() {
     mcur += WG_BR;
     c3 += WG_BR;
@@ -375,36 +404,46 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
     }
   };
 
-  uint4 rx[4];
-  uint4 ry;
+  uint4 rx[8];
+  uint4 ry[Y_PER_T];
   auto load_stage = [&](long long ms) {
-    const RowBase r = make_row();
+    const RowBase r = make_row(nn, c1, c2, c3, mcur < mend, g);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rx[i] = gather8<GM>(src, tab, r, kc0 + (xc + i) * 8, Kdim, g);
-    ry = make_uint4(0, 0, 0, 0);
-    if (tid < Y_CHUNKS) {
-      const int row = tid / (BCO / 8), ch = tid % (BCO / 8);
+    for (int i = 0; i < 8; ++i) rx[i] = gather8<GM>(src, tab, te[i], r, kc0 + (xc + i) * 8, Kdim, g);
+#pragma unroll
+    for (int i = 0; i < Y_PER_T; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / (BCO / 8), ch = idx % (BCO / 8);
       const long long m = ms + row;
       const int co = co0 + ch * 8;
-      if (m < mend) {
-        if constexpr (VECN) {
-          if (co < Cout) ry = *(const uint4*)(dy + m * Cout + co);
-        } else {
-          Pack8 p;
+      const bool ok = idx < Y_CHUNKS && m < mend;
+      if constexpr (VECN) {
+        const bool okc = ok && co < Cout;
+        const uint4 v = *(const uint4*)(dy + (okc ? m * Cout + co : 0));
+        ry[i] = okc ? v : make_uint4(0, 0, 0, 0);
+      } else {
+        Pack8 p;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) p.e[j] = (co + j < Cout) ? dy[m * Cout + co + j] : (bf16)0.f;
-          ry = p.u;
+        for (int j = 0; j < 8; ++j) {
+          const bool okj = ok && co + j < Cout;
+          const bf16 x = dy[okj ? m * Cout + co + j : 0];
+          p.e[j] = okj ? x : (bf16)0.f;
         }
+        ry[i] = p.u;
       }
     }
     advance_row();
   };
-  auto write_stage = [&](int buf) {
+  auto write_stage = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *(uint4*)(Xs + buf * X_STAGE + xr * WG_LDX + (xc + i) * 8) = rx[i];
-    if (tid < Y_CHUNKS) {
-      const int row = tid / (BCO / 8), ch = tid % (BCO / 8);
-      *(uint4*)(Ys + buf * Y_STAGE + row * LDY + ch * 8) = ry;
+    for (int i = 0; i < 8; ++i) *(uint4*)(Xs + xr * WG_LDX + (xc + i) * 8) = rx[i];
+#pragma unroll
+    for (int i = 0; i < Y_PER_T; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < Y_CHUNKS) {
+        const int row = idx / (BCO / 8), ch = idx % (BCO / 8);
+        *(uint4*)(Ys + row * LDY + ch * 8) = ry[i];
+      }
     }
   };
 
@@ -417,33 +456,36 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
   const long long nst = (mend - mbeg + WG_BR - 1) / WG_BR;
   if (nst > 0) {
     load_stage(mbeg);
-    write_stage(0);
+    write_stage();
   }
   __syncthreads();
   for (long long s = 0; s < nst; ++s) {
-    const int cur = (int)(s & 1);
-    if (s + 1 < nst) load_stage(mbeg + (s + 1) * WG_BR);
-    const bf16* xs = Xs + cur * X_STAGE;
-    const bf16* ys = Ys + cur * Y_STAGE;
-    bf16x8 fa[MT], fb[4];
+    const bool more = s + 1 < nst;
+    if (more) load_stage(mbeg + (s + 1) * WG_BR);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) fa[mt] = tr_frag(ys, LDY, mt * 16, lane);
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[MT], fb[4];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) fb[nt] = tr_frag(xs, WG_LDX, wave * 64 + nt * 16, lane);
+      for (int mt = 0; mt < MT; ++mt) fa[mt] = tr_frag(Ys + ks * 32 * LDY, LDY, mt * 16, lane);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+      for (int nt = 0; nt < 4; ++nt) fb[nt] = tr_frag(Xs + ks * 32 * WG_LDX, WG_LDX, wave * 64 + nt * 16, lane);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
-    if (s + 1 < nst) write_stage(cur ^ 1);
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+    }
     __syncthreads();
+    if (more) {
+      write_stage();
+      __syncthreads();
+    }
   }
 
   // D[row=co][col=k]: lane holds rows (lane>>4)*4+r, col lane&15.
   // Split-m partial sums are folded straight into the fp32 dW with no-return
-  // float atomics (one 256-B-class wave instruction per accumulator register;
-  // S x Cout x Kdim x 4 B of atomic traffic, well under the ~1.3 TB/s rate).
-  float* dst = part;
+  // float atomics (S x Cout x Kdim x 4 B of atomic traffic, well under the
+  // ~1.3 TB/s chip-wide atomic rate for the split counts used).
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -452,44 +494,30 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + mt * 16 + (lane >> 4) * 4 + r;
-        if (co < Cout && k < Kdim) atomicAdd(dst + (long long)co * Kdim + k, acc[mt][nt][r]);
+        if (co < Cout && k < Kdim) atomicAdd(dw + (long long)co * Kdim + k, acc[mt][nt][r]);
       }
     }
-}
-
-// sum fp32 slabs [S][n] -> out[n] (optionally accumulate into out)
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                          long long n, int S, int accumulate) {
-  const long long stride = (long long)gridDim.x * 256;
-  if ((n & 3) == 0) {
-    const long long n4 = n >> 2;
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += stride) {
-      float4 s = accumulate ? *(const float4*)(out + i * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int z = 0; z < S; ++z) {
-        const float4 v = *(const float4*)(part + (long long)z * n + i * 4);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-      *(float4*)(out + i * 4) = s;
-    }
-  } else {
-    for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += stride) {
-      float s = accumulate ? out[i] : 0.f;
-      for (int z = 0; z < S; ++z) s += part[(long long)z * n + i];
-      out[i] = s;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------
 // Host launchers (C ABI, used by bind.cpp)
 // ---------------------------------------------------------------------------
-template <int BN, int VEC>
+static GatherGeom parse_geom(const int* g14) {
+  GatherGeom g;
+  g.RD = g14[0]; g.RH = g14[1]; g.RW = g14[2];
+  g.md = g14[3]; g.mh = g14[4]; g.mw = g14[5];
+  g.ad = g14[6]; g.ah = g14[7]; g.aw = g14[8];
+  g.SD = g14[9]; g.SH = g14[10]; g.SW = g14[11]; g.SC = g14[12]; g.kwc = g14[13];
+  return g;
+}
+
+template <int BN, int GMV>
 static void launch_fwd_bn(dim3 grid, hipStream_t st, const bf16* src, const bf16* wt, const float* bias, bf16* out,
                           float* stats, const int4* tab, const GatherGeom& g, long long M, int N, int K, int ldw,
                           int act) {
 #define FWD_ARGS src, wt, bias, out, stats, tab, g, M, N, K, ldw
 #define FWD_CASE(ACTV, HB, ST) \
-  hipLaunchKernelGGL((igemm_fwd_kernel<BN, VEC, ACTV, HB, ST>), grid, dim3(256), 0, st, FWD_ARGS)
+  hipLaunchKernelGGL((igemm_fwd_kernel<BN, GMV, ACTV, HB, ST>), grid, dim3(256), 0, st, FWD_ARGS)
   const bool hb = bias != nullptr, stt = stats != nullptr;
   if (act == ACT_NONE) {
     if (hb) { if (stt) FWD_CASE(ACT_NONE, true, true); else FWD_CASE(ACT_NONE, true, false); }
@@ -506,14 +534,11 @@ static void launch_fwd_bn(dim3 grid, hipStream_t st, const bf16* src, const bf16
 }
 
 extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, void* out, float* stats,
-                            const int* tab, const int* geom13, long long M, int Ncol, int Kdim, int ldw, int vec,
+                            const int* tab, const int* geom14, long long M, int Ncol, int Kdim, int ldw, int gm,
                             int act, hipStream_t st) {
-  GatherGeom g;
-  g.RD = geom13[0]; g.RH = geom13[1]; g.RW = geom13[2];
-  g.md = geom13[3]; g.mh = geom13[4]; g.mw = geom13[5];
-  g.ad = geom13[6]; g.ah = geom13[7]; g.aw = geom13[8];
-  g.SD = geom13[9]; g.SH = geom13[10]; g.SW = geom13[11]; g.SC = geom13[12]; g.kwc = geom13[13];
+  const GatherGeom g = parse_geom(geom14);
   if (stats && act != ACT_NONE) return -1;  // stats are taken on the pre-BN output
+  if (ldw % 8 != 0) return -3;
   const int BN = Ncol <= 16 ? 16 : (Ncol <= 32 ? 32 : 64);
   const long long mblocks = (M + FWD_BM - 1) / FWD_BM;
   dim3 grid((unsigned)mblocks, (Ncol + BN - 1) / BN);
@@ -527,8 +552,8 @@ extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, 
     else if (BN == 32) launch_fwd_bn<32, GMV>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act); \
     else launch_fwd_bn<64, GMV>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);              \
   } while (0)
-  if (vec == GM_VEC) FWD_GM(GM_VEC);
-  else if (vec == GM_PACKW) FWD_GM(GM_PACKW);
+  if (gm == GM_VEC) FWD_GM(GM_VEC);
+  else if (gm == GM_PACKW) FWD_GM(GM_PACKW);
   else FWD_GM(GM_SCALAR);
 #undef FWD_GM
   FN_CHECK_LAUNCH();
@@ -537,45 +562,34 @@ extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, 
 
 extern "C" int fn_igemm_fwd_mblocks(long long M) { return (int)((M + FWD_BM - 1) / FWD_BM); }
 
-extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* part, const int* tab, const int* geom13,
-                              long long M, int Cout, int Kdim, int splits, int vec, hipStream_t st) {
-  GatherGeom g;
-  g.RD = geom13[0]; g.RH = geom13[1]; g.RW = geom13[2];
-  g.md = geom13[3]; g.mh = geom13[4]; g.mw = geom13[5];
-  g.ad = geom13[6]; g.ah = geom13[7]; g.aw = geom13[8];
-  g.SD = geom13[9]; g.SH = geom13[10]; g.SW = geom13[11]; g.SC = geom13[12]; g.kwc = geom13[13];
+extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const int* tab, const int* geom14,
+                              long long M, int Cout, int Kdim, int splits, int gm, hipStream_t st) {
+  const GatherGeom g = parse_geom(geom14);
   const int BCO = Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64);
   const long long rps = ((M + splits - 1) / splits + WG_BR - 1) / WG_BR * WG_BR;
-  dim3 grid((Kdim + WG_BK - 1) / WG_BK, (Cout + BCO - 1) / BCO, splits);
+  const int gx = (Kdim + WG_BK - 1) / WG_BK, gy = (Cout + BCO - 1) / BCO;
+  dim3 grid(gx, gy, splits);
   const bool vecn = (Cout % 8) == 0;
   const bf16* d = (const bf16*)dy;
   const bf16* s = (const bf16*)src;
   const int4* t = (const int4*)tab;
-#define WG_CASE(B, V, VN) hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, part, t, g, M, Cout, Kdim, rps)
-#define WG_GM(GMV)                                                                   \
-  do {                                                                               \
-    if (vecn) {                                                                      \
+#define WG_CASE(B, V, VN) \
+  hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, dw, t, g, M, Cout, Kdim, rps, gx, gy)
+#define WG_GM(GMV)                                                                        \
+  do {                                                                                    \
+    if (vecn) {                                                                           \
       if (BCO == 16) WG_CASE(16, GMV, true); else if (BCO == 32) WG_CASE(32, GMV, true); \
-      else WG_CASE(64, GMV, true);                                                   \
-    } else {                                                                         \
+      else WG_CASE(64, GMV, true);                                                        \
+    } else {                                                                              \
       if (BCO == 16) WG_CASE(16, GMV, false); else if (BCO == 32) WG_CASE(32, GMV, false); \
-      else WG_CASE(64, GMV, false);                                                  \
-    }                                                                                \
+      else WG_CASE(64, GMV, false);                                                       \
+    }                                                                                     \
   } while (0)
-  if (vec == GM_VEC) WG_GM(GM_VEC);
-  else if (vec == GM_PACKW) WG_GM(GM_PACKW);
+  if (gm == GM_VEC) WG_GM(GM_VEC);
+  else if (gm == GM_PACKW) WG_GM(GM_PACKW);
   else WG_GM(GM_SCALAR);
 #undef WG_GM
 #undef WG_CASE
-  FN_CHECK_LAUNCH();
-  return 0;
-}
-
-extern "C" int fn_slab_reduce(const float* part, float* out, long long n, int S, int accumulate, hipStream_t st) {
-  long long blocks = (n / 4 + 255) / 256;
-  if (blocks < 1) blocks = 1;
-  if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, part, out, n, S, accumulate);
   FN_CHECK_LAUNCH();
   return 0;
 }

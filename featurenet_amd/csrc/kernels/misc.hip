@@ -157,6 +157,20 @@ __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restr
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) y[i] = f2bf(x[i]);
 }
 
+// Bit-packed voxel grids (1 bit/voxel, LSB first) -> bf16 occupancy {0,1}.
+// One thread expands one byte into 8 bf16 (16 B store); the host/PCIe side
+// moves 1/16 of the bf16 bytes (csrc/runtime/voxel.cpp packs them).
+__global__ __launch_bounds__(256) void unpack_bits_kernel(const uint8_t* __restrict__ bits, bf16* __restrict__ out,
+                                                          long long nbytes) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < nbytes; i += (long long)gridDim.x * 256) {
+    const unsigned b = bits[i];
+    Pack8 p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p.e[j] = (b >> j) & 1u ? (bf16)1.f : (bf16)0.f;
+    *(uint4*)(out + i * 8) = p.u;
+  }
+}
+
 // ---------------------------------------------------------------------------
 static unsigned blocks_for(long long work) {
   long long b = (work + 255) / 256;
@@ -210,6 +224,13 @@ extern "C" int fn_dropout(const void* x, void* y, long long total, float p, unsi
                           hipStream_t st) {
   hipLaunchKernelGGL(dropout_kernel, dim3(blocks_for(total)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, total, p,
                      seed, offset);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_unpack_bits(const void* bits, void* out, long long nbytes, hipStream_t st) {
+  hipLaunchKernelGGL(unpack_bits_kernel, dim3(blocks_for(nbytes)), dim3(256), 0, st, (const uint8_t*)bits,
+                     (bf16*)out, nbytes);
   FN_CHECK_LAUNCH();
   return 0;
 }
