@@ -101,22 +101,23 @@ __device__ __forceinline__ uint4 gather8(const bf16* __restrict__ src, const int
     const bool rowok = k0 < Kdim && r.valid && (unsigned)(r.bd + zd) < (unsigned)g.SD &&
                        (unsigned)(r.bh + zh) < (unsigned)g.SH;
     const bool fast = rowok && r.bw + lo >= 0 && r.bw + hi < g.SW;
-    uint4 v = *(const uint4_u2*)(src + (fast ? r.base + e.x : 0));
-    v = fast ? v : zero;
+    const uint4 vv = *(const uint4_u2*)(src + (fast ? r.base + e.x : 0));
+    const unsigned fm = fast ? 0xffffffffu : 0u;
+    unsigned w0 = vv.x & fm, w1 = vv.y & fm, w2 = vv.z & fm, w3 = vv.w & fm;
     if (rowok && !fast) {   // row touches the W border: per-element (rare lanes)
-      Pack8 p;
+      const unsigned short* s16 = reinterpret_cast<const unsigned short*>(src);
       const long long rowb = r.base + e.x - e.w;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int pp = e.w + j;
         const int kw = pp / g.SC;
         const bool okj = pp < g.kwc && (unsigned)(r.bw + kw) < (unsigned)g.SW;
-        const bf16 x = src[okj ? rowb + pp : 0];
-        p.e[j] = okj ? x : (bf16)0.f;
+        const unsigned x = (okj ? (unsigned)s16[okj ? rowb + pp : 0] : 0u) << (16 * (j & 1));
+        if (j < 2) w0 |= x; else if (j < 4) w1 |= x; else if (j < 6) w2 |= x; else w3 |= x;
       }
-      v = p.u;
     }
-    return v;
+    (void)zero;
+    return make_uint4(w0, w1, w2, w3);
   } else {
     Pack8 p;
 #pragma unroll
@@ -146,7 +147,7 @@ __device__ __forceinline__ int4 entry_for(const int4* __restrict__ tab, int k0, 
 #define FWD_BK 64
 
 template <int BN, int GM, int ACT, bool HAS_BIAS, bool STATS>
-__global__ __launch_bounds__(256, (BN >= 64 ? 3 : 4)) void igemm_fwd_kernel(
+__global__ __launch_bounds__(256, (BN >= 64 || GM != GM_VEC ? 3 : 4)) void igemm_fwd_kernel(
     const bf16* __restrict__ src, const bf16* __restrict__ wt, const float* __restrict__ bias,
     bf16* __restrict__ out, float* __restrict__ stats, const int4* __restrict__ tab, GatherGeom g,
     long long M, int Ncol, int Kdim, int ldw) {

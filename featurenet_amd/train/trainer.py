@@ -1,0 +1,200 @@
+"""Trainer: the fit / evaluate / predict loop over native ops.
+
+Reference parity: ``TensorflowGenerator.build/train`` (``tensorflow_generator.py:221-277``:
+compile with Adam(1e-3) + categorical cross-entropy, fit, evaluate test
+accuracy) and ``helpers.train_model`` (``helpers.py:69-175``: optional
+augmentation, callbacks, reload of the best checkpoint, OOM -> dropped
+candidate).
+
+Engine design (MI355X):
+* all trainable parameters live in one fp32 buffer (:class:`FlatParams`),
+  updated by ONE fused Adam/SGD kernel per step;
+* activations are bf16, channels-last, produced by the hand-written kernels;
+* with ``torch.distributed`` initialised (one process per GPU), gradients are
+  reduced in buckets over RCCL while backward is still running
+  (:class:`~featurenet_amd.parallel.ddp.GradBucketer`), each rank trains on its
+  shard of every epoch and metrics are all-reduced;
+* the per-step loss / correct counters stay on the device; the host reads them
+  once per epoch, so the step loop never synchronises.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..ops import FlatAdam, FlatSGD, softmax_xent
+from ..parallel.ddp import GradBucketer
+from .callbacks import Callback
+from .checkpoint import save_checkpoint
+from .data import DeviceLoader
+from .flat import FlatParams
+
+
+class TrainingFailed(RuntimeError):
+    pass
+
+
+@dataclass
+class History:
+    history: dict = field(default_factory=dict)
+    epoch: list = field(default_factory=list)
+
+    def log(self, epoch: int, logs: dict) -> None:
+        self.epoch.append(epoch)
+        for k, v in logs.items():
+            self.history.setdefault(k, []).append(v)
+
+
+class Trainer:
+    def __init__(self, model: torch.nn.Module, optimizer: str = "adam", lr: float = 1e-3, device=None,
+                 keras_eps: bool = True, weight_decay: float = 0.0, momentum: float = 0.9,
+                 label_smoothing: float = 0.0, bucket_mb: float = 32.0, meta: dict | None = None):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        self.model = model.to(self.device)
+        self.flat = FlatParams(self.model)
+        if optimizer == "adam":
+            self.opt = FlatAdam(self.flat.data, self.flat.grad, lr=lr, keras_eps=keras_eps, weight_decay=weight_decay)
+        elif optimizer == "sgd":
+            self.opt = FlatSGD(self.flat.data, self.flat.grad, lr=lr, momentum=momentum, weight_decay=weight_decay)
+        else:
+            raise ValueError(f"unknown optimizer {optimizer!r}")
+        self.optimizer_name = optimizer
+        self.label_smoothing = label_smoothing
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.bucketer = GradBucketer(self.flat, bucket_mb=bucket_mb)
+        self.bucketer.broadcast_from(0)
+        self.stop_training = False
+        self.meta = dict(meta or {})
+        self.history = History()
+
+    # ------------------------------------------------------------------ lr
+    def get_lr(self) -> float:
+        return self.opt.lr
+
+    def set_lr(self, lr: float) -> None:
+        self.opt.lr = float(lr)
+
+    # ------------------------------------------------------------------ steps
+    def _prep(self, xb: torch.Tensor) -> torch.Tensor:
+        if self.device.type == "cuda" and xb.dtype != torch.bfloat16:
+            xb = xb.to(torch.bfloat16)
+        if self.device.type == "cpu" and xb.dtype not in (torch.float32, torch.float64):
+            xb = xb.float()
+        return xb
+
+    def train_step(self, xb: torch.Tensor, yb: torch.Tensor):
+        self.flat.zero_grad()
+        logits = self.model(self._prep(xb))
+        loss, correct = softmax_xent(logits, yb, self.label_smoothing, with_correct=True)
+        loss.backward()
+        scale = self.bucketer.finish()
+        self.opt.step(grad_scale=scale)
+        return loss.detach(), correct
+
+    def _reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            if self.device.type != "cuda" and dist.get_backend() == "nccl":
+                t = t.to("cuda")
+            dist.all_reduce(t)
+        return t
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, x, y, epochs: int = 1, batch_size: int = 128, validation_data=None, callbacks=None,
+            augment: bool = False, packed_size: int | None = None, verbose: int = 1, shuffle: bool = True,
+            seed: int = 0) -> History:
+        callbacks: list[Callback] = list(callbacks or [])
+        loader = DeviceLoader(x, y, batch_size, self.device, shuffle=shuffle, augment=augment,
+                              packed_size=packed_size, rank=self.rank, world=self.world, seed=seed)
+        self.stop_training = False
+        for cb in callbacks:
+            cb.on_train_begin(self)
+        t_start = time.time()
+        try:
+            for epoch in range(epochs):
+                for cb in callbacks:
+                    cb.on_epoch_begin(self, epoch)
+                self.model.train()
+                t0 = time.time()
+                loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+                correct = torch.zeros((), dtype=torch.int64, device=self.device)
+                seen = 0
+                for bi, (xb, yb) in enumerate(loader):
+                    loss, corr = self.train_step(xb, yb)
+                    loss_sum += loss.double() * len(yb)
+                    correct += corr.sum()
+                    seen += len(yb)
+                    if callbacks:
+                        for cb in callbacks:
+                            cb.on_batch_end(self, bi, {})
+                stats = self._reduce(torch.stack([loss_sum, correct.double(),
+                                                  torch.tensor(float(seen), dtype=torch.float64, device=self.device)]))
+                logs = {"loss": float(stats[0] / max(stats[2], 1)), "acc": float(stats[1] / max(stats[2], 1)),
+                        "lr": self.get_lr(), "time": time.time() - t0,
+                        "samples_per_s": float(stats[2]) / max(time.time() - t0, 1e-9)}
+                if validation_data is not None:
+                    vl, va = self.evaluate(*validation_data, batch_size=batch_size, packed_size=packed_size)
+                    logs["val_loss"], logs["val_acc"] = vl, va
+                if not math.isfinite(logs["loss"]):
+                    raise TrainingFailed("non-finite training loss")
+                self.history.log(epoch, logs)
+                if verbose and self.rank == 0:
+                    msg = " ".join(f"{k}={v:.4g}" for k, v in logs.items())
+                    print(f"epoch {epoch + 1}/{epochs} {msg}", flush=True)
+                for cb in callbacks:
+                    cb.on_epoch_end(self, epoch, logs)
+                if self.stop_training:
+                    break
+        except torch.cuda.OutOfMemoryError as e:   # reference: ResourceExhaustedError -> candidate dropped
+            raise TrainingFailed(f"out of device memory: {e}") from e
+        finally:
+            for cb in callbacks:
+                cb.on_train_end(self)
+        self.meta["train_time_s"] = time.time() - t_start
+        return self.history
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def evaluate(self, x, y, batch_size: int = 256, packed_size: int | None = None) -> tuple[float, float]:
+        self.model.eval()
+        loader = DeviceLoader(x, y, batch_size, self.device, shuffle=False, packed_size=packed_size,
+                              rank=self.rank, world=self.world)
+        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        correct = torch.zeros((), dtype=torch.int64, device=self.device)
+        seen = 0
+        for xb, yb in loader:
+            logits = self.model(self._prep(xb))
+            loss, corr = softmax_xent(logits, yb, with_correct=True)
+            loss_sum += loss.double() * len(yb)
+            correct += corr.sum()
+            seen += len(yb)
+        stats = self._reduce(torch.stack([loss_sum, correct.double(),
+                                          torch.tensor(float(seen), dtype=torch.float64, device=self.device)]))
+        self.model.train()
+        n = max(float(stats[2]), 1.0)
+        return float(stats[0]) / n, float(stats[1]) / n
+
+    @torch.no_grad()
+    def predict(self, x, batch_size: int = 256, packed_size: int | None = None) -> np.ndarray:
+        self.model.eval()
+        y_dummy = np.zeros(len(x), dtype=np.int64)
+        loader = DeviceLoader(x, y_dummy, batch_size, self.device, shuffle=False, packed_size=packed_size)
+        out = []
+        for xb, _ in loader:
+            out.append(torch.softmax(self.model(self._prep(xb)).float(), -1).cpu())
+        self.model.train()
+        return torch.cat(out).numpy() if out else np.zeros((0,))
+
+    # ------------------------------------------------------------------ io
+    def save(self, path, include_optimizer: bool = True):
+        meta = dict(self.meta)
+        meta["history"] = self.history.history
+        meta["optimizer_name"] = self.optimizer_name
+        return save_checkpoint(path, self.model, meta, self.opt if include_optimizer else None)
