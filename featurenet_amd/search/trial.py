@@ -1,0 +1,218 @@
+"""Candidate trials and the trial-per-GPU scheduler.
+
+Reference: a candidate is trained by ``TensorflowGenerator`` (build -> train ->
+evaluate -> robustness, ``tensorflow_generator.py:97-136``); invalid
+architectures, >20M-parameter models and OOM are "dropped" candidates
+(``model/keras_model.py:127-156``, ``helpers.py:172-174``).  The reference
+trains candidates strictly one after another in one process (its
+``multiprocessing`` code is commented out: ``full_mnist.py:37-39``).
+
+Here a trial is a pure function ``run_trial(spec, cfg, device) -> spec`` and
+the :class:`TrialScheduler` runs trials concurrently, one worker process per
+GPU (8 concurrent candidates on an 8x MI355X node), with
+
+* a per-trial watchdog: a hung or crashed trial kills only its worker, the
+  trial is marked ``failed`` and the worker is restarted;
+* invalid-candidate semantics: compile errors -> ``status="invalid"``,
+  accuracy 0; OOM / non-finite loss -> ``status="failed"``;
+* fault-injection hooks for tests (``cfg.inject = {spec_name: "build" | "oom" |
+  "hang" | "crash"}``).
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+import queue
+import time
+import traceback
+from dataclasses import asdict, dataclass, field
+
+from ..ir.spec import ModelSpec
+
+
+@dataclass
+class TrialConfig:
+    dataset: str = "cifar"
+    epochs: int = 12
+    batch_size: int = 64
+    lr: float = 1e-3
+    attacks: list = field(default_factory=list)
+    robustness_set_size: int = 500
+    clever_samples: int | None = 20
+    augment: bool = False
+    compat: bool = True
+    fill_defaults: bool = False
+    save_dir: str | None = None
+    save_prefix: str = ""
+    seed: int = 0
+    synthetic_sizes: tuple = (6000, 1000)
+    verbose: int = 0
+    inject: dict = field(default_factory=dict)
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+
+def run_trial(spec: ModelSpec, cfg: TrialConfig, device=None) -> ModelSpec:
+    """Train + evaluate one candidate in this process; never raises."""
+    import torch
+
+    from ..ir.compile import CompileError, compile_model
+    from ..train.callbacks import reference_callbacks
+    from ..train.data import load_dataset
+    from ..train.trainer import Trainer, TrainingFailed
+
+    spec = spec.clone()
+    t0 = time.time()
+    fault = cfg.inject.get(spec.name) if cfg.inject else None
+    try:
+        if fault == "hang":
+            time.sleep(3600)
+        if fault == "crash":
+            os._exit(17)
+        ds = load_dataset(cfg.dataset, synthetic_sizes=tuple(cfg.synthetic_sizes), seed=cfg.seed)
+        torch.manual_seed(cfg.seed)
+        if fault == "build":
+            raise CompileError("injected build failure")
+        model = compile_model(spec, ds.input_shape, ds.num_classes, compat=cfg.compat,
+                              fill_defaults=cfg.fill_defaults)
+        spec.nb_params, spec.nb_layers, spec.nb_flops = model.nb_params, model.nb_layers, model.flops_per_sample
+        if fault == "oom":
+            raise TrainingFailed("out of device memory: injected")
+        trainer = Trainer(model, lr=cfg.lr, device=device, meta={"model_kind": "candidate", "spec": spec.to_dict(),
+                                                                  "input_shape": list(ds.input_shape),
+                                                                  "num_classes": ds.num_classes,
+                                                                  "compat": cfg.compat,
+                                                                  "fill_defaults": cfg.fill_defaults})
+        packed = ds.input_shape[0] if ds.packed else None
+        hist = trainer.fit(ds.x_train, ds.y_train, epochs=cfg.epochs, batch_size=cfg.batch_size,
+                           validation_data=(ds.x_test, ds.y_test), callbacks=reference_callbacks(False),
+                           augment=cfg.augment, packed_size=packed, verbose=cfg.verbose, seed=cfg.seed)
+        loss, acc = trainer.evaluate(ds.x_test, ds.y_test, packed_size=packed)
+        spec.accuracy = float(acc)
+        spec.history = {k: [float(v) for v in vs] for k, vs in hist.history.items()}
+        spec.status = "trained"
+        if cfg.attacks and acc >= 0.5:
+            from ..robust.evaluate import eval_robustness
+
+            r = eval_robustness(model, ds, list(cfg.attacks), set_size=cfg.robustness_set_size,
+                                clever_samples=cfg.clever_samples)
+            spec.robustness_score = float(r.get("score", 0.0))
+            for k in ("clever", "fgsm", "pgd", "cw"):
+                if r.get(k) is not None:
+                    setattr(spec, f"{k}_score", list(r[k]) if isinstance(r[k], tuple) else r[k])
+        if cfg.save_dir:
+            os.makedirs(cfg.save_dir, exist_ok=True)
+            trainer.meta["spec"] = spec.to_dict()
+            trainer.save(os.path.join(cfg.save_dir, f"{cfg.save_prefix}{spec.name}.fnk"))
+    except CompileError as e:
+        spec.status, spec.accuracy, spec.error = "invalid", 0.0, str(e)
+    except TrainingFailed as e:
+        spec.status, spec.accuracy, spec.error = "failed", 0.0, str(e)
+    except Exception as e:  # any other failure drops the candidate, like the reference
+        spec.status, spec.accuracy, spec.error = "failed", 0.0, f"{type(e).__name__}: {e}\n{traceback.format_exc(limit=4)}"
+    spec.metrics = list(spec.metrics) + [{"trial_time_s": time.time() - t0}]
+    return spec
+
+
+# ---------------------------------------------------------------------------
+# process pool
+# ---------------------------------------------------------------------------
+def _worker(dev: str, tasks, results, ready):
+    os.environ.setdefault("OMP_NUM_THREADS", "4")
+    import torch
+
+    device = "cpu"
+    if dev != "cpu":
+        torch.cuda.set_device(int(dev))
+        device = f"cuda:{int(dev)}"
+    ready.put(os.getpid())
+    while True:
+        item = tasks.get()
+        if item is None:
+            return
+        tid, spec_json, cfg = item
+        out = run_trial(ModelSpec.from_json(spec_json), TrialConfig(**cfg), device)
+        results.put((tid, out.to_json()))
+
+
+class TrialScheduler:
+    """Run trials on a set of devices, one worker process per device."""
+
+    def __init__(self, devices=None, timeout_s: float | None = None, mode: str = "auto"):
+        if devices is None:
+            try:
+                import torch
+
+                n = torch.cuda.device_count()
+            except Exception:
+                n = 0
+            devices = [str(i) for i in range(n)] or ["cpu"]
+        self.devices = [str(d) for d in devices]
+        self.timeout_s = timeout_s
+        self.mode = ("inline" if len(self.devices) == 1 and timeout_s is None else "process") if mode == "auto" else mode
+
+    def map(self, specs: list[ModelSpec], cfg: TrialConfig) -> list[ModelSpec]:
+        if not specs:
+            return []
+        if self.mode == "inline":
+            dev = self.devices[0]
+            device = "cpu" if dev == "cpu" else f"cuda:{int(dev)}"
+            return [run_trial(s, cfg, device) for s in specs]
+        return self._map_processes(specs, cfg)
+
+    def _map_processes(self, specs, cfg):
+        ctx = mp.get_context("spawn")
+        results = ctx.Queue()
+        workers: dict[str, dict] = {}
+
+        def start(dev):
+            tq = ctx.Queue()
+            ready = ctx.Queue()
+            p = ctx.Process(target=_worker, args=(dev, tq, results, ready), daemon=True)
+            p.start()
+            workers[dev] = {"proc": p, "tasks": tq, "busy": None, "t0": 0.0}
+
+        for d in self.devices:
+            start(d)
+        pending = list(enumerate(specs))
+        out: dict[int, ModelSpec] = {}
+        cfgd = cfg.to_dict()
+        while len(out) < len(specs):
+            for dev, w in workers.items():
+                if w["busy"] is None and pending:
+                    tid, s = pending.pop(0)
+                    w["busy"], w["t0"] = tid, time.time()
+                    w["tasks"].put((tid, s.to_json(), cfgd))
+            try:
+                tid, js = results.get(timeout=0.5)
+                out[tid] = ModelSpec.from_json(js)
+                for w in workers.values():
+                    if w["busy"] == tid:
+                        w["busy"] = None
+            except queue.Empty:
+                pass
+            # watchdog: hung or dead workers fail their trial and are restarted
+            for dev in list(workers):
+                w = workers[dev]
+                tid = w["busy"]
+                if tid is None:
+                    continue
+                dead = not w["proc"].is_alive()
+                hung = self.timeout_s is not None and time.time() - w["t0"] > self.timeout_s
+                if dead or hung:
+                    if not dead:
+                        w["proc"].kill()
+                    w["proc"].join(timeout=10)
+                    s = specs[tid].clone()
+                    s.status, s.accuracy = "failed", 0.0
+                    s.error = "trial timed out" if hung else f"worker died (exit {w['proc'].exitcode})"
+                    out[tid] = s
+                    start(dev)
+        for w in workers.values():
+            w["tasks"].put(None)
+        for w in workers.values():
+            w["proc"].join(timeout=30)
+            if w["proc"].is_alive():
+                w["proc"].kill()
+        return [out[i] for i in range(len(specs))]
