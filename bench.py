@@ -31,8 +31,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # measured first-party baseline (stock PyTorch-ROCm eager, 1x MI355X, same config);
-# see BASELINE.md.  None until measured.
-TORCH_BASELINE_SAMPLES_PER_S_PER_GPU = None
+# see BASELINE.md and profiles/r1_bench_torch_miopen.log (MIOpen Conv3d/BN/pool,
+# bf16, batch 128, 64^3, 24 classes).  vs_baseline = value / (this * n_gpus).
+TORCH_BASELINE_SAMPLES_PER_S_PER_GPU = 106.8
 
 
 def parse():
@@ -81,7 +82,7 @@ def main():
         from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
         from featurenet_amd.ops import FlatAdam, softmax_xent
         from featurenet_amd.parallel.ddp import GradBucketer
-        from featurenet_amd.train.flat import FlatParams
+        from featurenet_amd.training.flat import FlatParams
 
         torch.manual_seed(1234)  # identical init on every rank (also broadcast below)
         cfg = FeatureNet3DConfig.tiny() if args.tiny else FeatureNet3DConfig(input_size=S, num_classes=NC)
@@ -150,7 +151,8 @@ def main():
     ms = elapsed / max(args.steps, 1) * 1e3
     value = args.steps * B * world / elapsed
     base = TORCH_BASELINE_SAMPLES_PER_S_PER_GPU
-    vs = (value / (base * world)) if base else None
+    same_cfg = args.batch == 128 and args.size == 64 and args.classes == 24 and not args.tiny
+    vs = (value / (base * world)) if base and same_cfg else None
     if rank == 0:
         out = {
             "metric": "samples/sec (64^3 voxel, 24-class) train",

@@ -30,10 +30,10 @@ from .ir.parse import parse_feature_model
 from .ir.spec import ModelSpec
 from .ir.templates import TEMPLATES
 from .models.featurenet3d import FeatureNet3D, FeatureNet3DConfig, FeatureNet3DSeg
-from .train.callbacks import reference_callbacks
-from .train.checkpoint import read_checkpoint, save_checkpoint
-from .train.data import Dataset, load_dataset
-from .train.trainer import Trainer
+from .training.callbacks import reference_callbacks
+from .training.checkpoint import read_checkpoint, save_checkpoint
+from .training.data import Dataset, load_dataset
+from .training.trainer import Trainer
 
 
 @dataclass
@@ -160,7 +160,7 @@ def classify(model, x, batch_size: int = 256, device=None, packed_size: int | No
         model, _ = load(model, device)
     dev = next(model.parameters()).device
     model.eval()
-    from .train.data import unpack_voxels
+    from .training.data import unpack_voxels
 
     xt = torch.as_tensor(np.asarray(x)) if not isinstance(x, torch.Tensor) else x
     probs = []

@@ -79,26 +79,61 @@ class _Builder:
         self.fill_defaults = fill_defaults
         self.mods = nn.ModuleList()
         self.prog: list[tuple] = []
+        self.cost: list[tuple] = []     # per instruction: (params, flops, keras layers)
         self.params = 0
         self.flops = 0
         self.layers = 1  # the Input layer
         self.x = self._emit(("input", None, ()), tuple(input_shape))
 
-    def _emit(self, instr: tuple, shape: tuple) -> Sym:
+    def _emit(self, instr: tuple, shape: tuple, cost: tuple = (0, 0, 0)) -> Sym:
         self.prog.append(instr)
+        self.cost.append(cost)
         return Sym(len(self.prog) - 1, tuple(int(s) for s in shape))
 
     def module(self, mod: nn.Module, x: Sym, shape: tuple, flops: int = 0) -> Sym:
         self.mods.append(mod)
-        self.params += sum(p.numel() for p in mod.parameters()) + sum(b.numel() for b in mod.buffers())
+        n = sum(p.numel() for p in mod.parameters()) + sum(b.numel() for b in mod.buffers())
+        self.params += n
         self.flops += flops
         self.layers += 1
-        return self._emit(("module", len(self.mods) - 1, (x.node,)), shape)
+        return self._emit(("module", len(self.mods) - 1, (x.node,)), shape, (n, flops, 1))
 
     def fn(self, name: str, args, ins: tuple, shape: tuple, layer: bool = True) -> Sym:
         if layer:
             self.layers += 1
-        return self._emit((name, args, tuple(s.node for s in ins)), shape)
+        return self._emit((name, args, tuple(s.node for s in ins)), shape, (0, 0, int(layer)))
+
+    def prune(self, out: int) -> None:
+        """Dead-code elimination: keep only instructions the output depends on.
+
+        A Keras functional ``Model(inputs, outputs)`` only contains layers reachable
+        from its outputs, so cells whose results the block/OutCell wiring drops
+        (``model/block.py``, ``model/cell.py``) neither count towards
+        ``count_params`` nor run; the same holds here.
+        """
+        live = [False] * len(self.prog)
+        live[out] = True
+        live[0] = True
+        for i in range(out, -1, -1):
+            if live[i]:
+                for j in self.prog[i][2]:
+                    live[j] = True
+        remap, prog, cost, mods, mremap = {}, [], [], nn.ModuleList(), {}
+        for i, (kind, arg, ins) in enumerate(self.prog[:out + 1]):
+            if not live[i]:
+                continue
+            if kind in ("module", "head"):
+                if arg not in mremap:
+                    mremap[arg] = len(mods)
+                    mods.append(self.mods[arg])
+                arg = mremap[arg]
+            remap[i] = len(prog)
+            prog.append((kind, arg, tuple(remap[j] for j in ins)))
+            cost.append(self.cost[i])
+        self.prog, self.cost, self.mods = prog, cost, mods
+        self.params = sum(c[0] for c in cost)
+        self.flops = sum(c[1] for c in cost)
+        self.layers = 1 + sum(c[2] for c in cost)
 
     # ----------------------------------------------------------------- layers
     def conv(self, x: Sym, features: int, kernel, stride, padding: str, act, ctype: str) -> Sym:
@@ -332,10 +367,9 @@ class CandidateNet(nn.Module):
             out = b.fn("flatten", None, (out,), (math.prod(out.shape),))
         head = Dense(out.shape[-1], n_classes, act=None)
         b.mods.append(head)
-        b.params += sum(p.numel() for p in head.parameters())
-        b.flops += 2 * out.shape[-1] * n_classes
-        b.layers += 1
-        b.prog.append(("head", len(b.mods) - 1, (out.node,)))
+        b._emit(("head", len(b.mods) - 1, (out.node,)), (n_classes,),
+                (sum(p.numel() for p in head.parameters()), 2 * out.shape[-1] * n_classes, 1))
+        b.prune(len(b.prog) - 1)
         if b.params > max_params:
             raise ModelTooLarge(f"model has {b.params} parameters (> {max_params})")
         self.mods = b.mods

@@ -1,7 +1,7 @@
 """Flat-buffer optimizers (Adam / SGD) backed by one fused HIP kernel each.
 
 All trainable parameters of a model live in ONE fp32 allocation
-(:class:`featurenet_amd.train.flat.FlatParams`), so an optimizer step is a
+(:class:`featurenet_amd.training.flat.FlatParams`), so an optimizer step is a
 single kernel launch over the whole buffer regardless of how many layers the
 NAS candidate has, and the data-parallel all-reduce can work on contiguous
 slices of the matching flat gradient buffer.

@@ -3,7 +3,7 @@
 Replaces the reference's in-graph ``keras.utils.multi_gpu_model``
 (``model/keras_model.py:137-146``), which sliced the batch inside ONE process
 and merged outputs on the CPU.  Here every rank holds a full replica; the
-gradient of the flat buffer (:class:`~featurenet_amd.train.flat.FlatParams`)
+gradient of the flat buffer (:class:`~featurenet_amd.training.flat.FlatParams`)
 is cut into contiguous buckets in backward-production order and each bucket's
 ``all_reduce`` is issued the moment its last gradient has been accumulated
 (``register_post_accumulate_grad_hook``).  ProcessGroupNCCL (= RCCL on ROCm)
@@ -27,7 +27,7 @@ import os
 import torch
 import torch.distributed as dist
 
-from ..train.flat import FlatParams
+from ..training.flat import FlatParams
 
 
 def init_from_env(backend: str | None = None) -> tuple[int, int, int]:

@@ -67,7 +67,7 @@ def eval_robustness(model, dataset, metrics=("clever", "pgd", "cw", "fgsm"), set
             packed_size = dataset.input_shape[0]
     x = torch.as_tensor(np.asarray(xs)).to(device) if not isinstance(xs, torch.Tensor) else xs.to(device)
     if packed_size is not None:
-        from ..train.data import unpack_voxels
+        from ..training.data import unpack_voxels
 
         x = unpack_voxels(x, packed_size)
     x = x.float()[:set_size]

@@ -116,7 +116,7 @@ def run_evolution(base_path: str = "runs", last_pdts_path: str = "", nb_base_pro
     if resume and os.path.isfile(resume):
         population = load_snapshot(resume)
         m = re.search(r"_e(\d+)\.json$", resume)
-        start_epoch = int(m.group(1)) + 1 if m else 0
+        start_epoch = int(m.group(1)) if m else 0     # next generation is start_epoch + 1
         log(f"resuming {len(population)} individuals from {resume} at generation {start_epoch}")
     elif last_pdts_path and os.path.isfile(last_pdts_path):
         initial = specs_from_products(last_pdts_path)

@@ -58,9 +58,9 @@ def run_trial(spec: ModelSpec, cfg: TrialConfig, device=None) -> ModelSpec:
     import torch
 
     from ..ir.compile import CompileError, compile_model
-    from ..train.callbacks import reference_callbacks
-    from ..train.data import load_dataset
-    from ..train.trainer import Trainer, TrainingFailed
+    from ..training.callbacks import reference_callbacks
+    from ..training.data import load_dataset
+    from ..training.trainer import Trainer, TrainingFailed
 
     spec = spec.clone()
     t0 = time.time()
@@ -171,7 +171,9 @@ class TrialScheduler:
             ready = ctx.Queue()
             p = ctx.Process(target=_worker, args=(dev, tq, results, ready), daemon=True)
             p.start()
-            workers[dev] = {"proc": p, "tasks": tq, "busy": None, "t0": 0.0}
+            # keep every queue referenced: a collected queue unlinks its semaphore
+            # before the spawned child has unpickled it
+            workers[dev] = {"proc": p, "tasks": tq, "ready": ready, "busy": None, "t0": 0.0}
 
         for d in self.devices:
             start(d)

@@ -6,7 +6,7 @@ Reference parity (``helpers.py:12-97``, ``sgdr.py:5-85``): ReduceLROnPlateau
 on val_acc (min_delta 0.01, patience 20), ModelCheckpoint keeping the best
 val_loss weights (restored at the end of fit, like the reference's
 reload-and-delete of the temp .h5), TimedStopping and SGDR (cosine annealing
-with warm restarts).  Callbacks talk to a :class:`~featurenet_amd.train.trainer.Trainer`.
+with warm restarts).  Callbacks talk to a :class:`~featurenet_amd.training.trainer.Trainer`.
 """
 from __future__ import annotations
 

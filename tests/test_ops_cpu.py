@@ -1,0 +1,112 @@
+"""CPU oracle semantics: Keras 'same' padding, pooling, BN, loss, flat optimizers.
+
+The HIP kernels are checked against these oracles in ``test_kernels_gpu.py``;
+here the oracles themselves are pinned against naive loop implementations of
+the Keras/TF semantics the reference relies on (asymmetric 'same' padding with
+the extra pad on the high side, pooling windows that ignore padding).
+"""
+import itertools
+
+import numpy as np
+import pytest
+import torch
+
+from featurenet_amd.ops import reference as R
+from featurenet_amd.ops.spec import ConvSpec, PoolSpec, same_pad
+
+
+def _naive_conv(x, w, b, spec):
+    N, D, H, W, C = x.shape
+    K = w.shape[0]
+    out = np.zeros((N, spec.OD, spec.OH, spec.OW, K), np.float64)
+    for n, od, oh, ow in itertools.product(range(N), range(spec.OD), range(spec.OH), range(spec.OW)):
+        acc = np.zeros(K)
+        for kd, kh, kw in itertools.product(range(spec.KD), range(spec.KH), range(spec.KW)):
+            d = od * spec.sd - spec.pd + kd * spec.dd
+            h = oh * spec.sh - spec.ph + kh * spec.dh
+            ww = ow * spec.sw - spec.pw + kw * spec.dw
+            if 0 <= d < D and 0 <= h < H and 0 <= ww < W:
+                acc += w[:, kd, kh, kw, :] @ x[n, d, h, ww, :]
+        out[n, od, oh, ow] = acc + (b if b is not None else 0)
+    return out
+
+
+def test_same_pad_matches_tf():
+    # TF: out = ceil(in/s); total = max((out-1)*s + k - in, 0); lo = total//2
+    assert same_pad(5, 2, 2) == (0, 1)
+    assert same_pad(64, 7, 2) == (2, 3)
+    assert same_pad(7, 3, 1) == (1, 1)
+    assert same_pad(4, 1, 2) == (0, 0)
+
+
+@pytest.mark.parametrize("shape,k,s,pad", [((1, 5, 6, 7, 3), (3, 2, 3), (2, 1, 2), "same"),
+                                           ((2, 6, 6, 6, 2), (3, 3, 3), (1, 1, 1), "valid"),
+                                           ((1, 1, 9, 9, 4), (1, 5, 5), (1, 2, 2), "same")])
+def test_conv_oracle_vs_naive(shape, k, s, pad):
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(shape)
+    spec = ConvSpec.make(shape, 5, k, s, pad)
+    w = rng.standard_normal((5,) + tuple(k) + (shape[-1],))
+    b = rng.standard_normal(5)
+    got = R.conv(torch.tensor(x), torch.tensor(w), torch.tensor(b), spec).numpy()
+    np.testing.assert_allclose(got, _naive_conv(x, w, b, spec), rtol=1e-9, atol=1e-9)
+
+
+def test_maxpool_same_ignores_padding():
+    x = -torch.ones(1, 1, 5, 5, 1, dtype=torch.float64)
+    spec = PoolSpec.make(x.shape, (1, 2, 2), (1, 2, 2), "same")
+    y = R.pool(x, spec, "max")
+    assert y.shape == (1, 1, 3, 3, 1)
+    assert torch.all(y == -1)                         # -inf padding never wins
+    ya = R.pool(torch.ones_like(x), spec, "avg")
+    assert torch.allclose(ya, torch.ones_like(ya))    # Keras avg excludes padding
+
+
+def test_batchnorm_act_oracle():
+    torch.manual_seed(0)
+    y = torch.randn(4, 3, 3, 3, 6, dtype=torch.float64)
+    g, b = torch.rand(6, dtype=torch.float64) + 0.5, torch.randn(6, dtype=torch.float64)
+    rm, rv = torch.zeros(6, dtype=torch.float64), torch.ones(6, dtype=torch.float64)
+    z = R.batchnorm_act(y, g, b, rm, rv, True, 0.01, 1e-3, "relu")
+    flat = y.reshape(-1, 6)
+    mu, var = flat.mean(0), flat.var(0, unbiased=False)
+    ref = torch.relu((flat - mu) / torch.sqrt(var + 1e-3) * g + b).reshape(y.shape)
+    torch.testing.assert_close(z, ref)
+    n = flat.shape[0]
+    torch.testing.assert_close(rm, 0.01 * mu)
+    torch.testing.assert_close(rv, 0.99 + 0.01 * flat.var(0, unbiased=True))
+    assert n == 108
+
+
+def test_softmax_xent_smoothing():
+    logits = torch.tensor([[2.0, 0.0, -1.0]])
+    y = torch.tensor([0])
+    p = torch.softmax(logits, -1)
+    ref = -(0.9 * torch.log(p[0, 0]) + 0.1 / 3 * torch.log(p[0]).sum())
+    torch.testing.assert_close(R.softmax_xent(logits, y, 0.1), ref)
+
+
+def test_flat_adam_matches_keras_formula():
+    from featurenet_amd.ops.optim import FlatAdam
+
+    p = torch.tensor([1.0, -2.0, 3.0])
+    g = torch.tensor([0.1, 0.2, -0.3])
+    opt = FlatAdam(p, g, lr=0.01, keras_eps=True)
+    p0 = p.clone()
+    opt.step()
+    # Keras 2 Adam: lr_t = lr*sqrt(1-b2)/(1-b1); p -= lr_t*m/(sqrt(v)+eps)
+    m, v = 0.1 * g, 0.001 * g * g
+    lr_t = 0.01 * np.sqrt(1 - 0.999) / (1 - 0.9)
+    torch.testing.assert_close(p, p0 - lr_t * m / (torch.sqrt(v) + opt.eps), rtol=1e-5, atol=1e-7)
+
+
+def test_flat_sgd_momentum():
+    from featurenet_amd.ops.optim import FlatSGD
+
+    p = torch.tensor([1.0])
+    g = torch.tensor([0.5])
+    opt = FlatSGD(p, g, lr=0.1, momentum=0.9)
+    opt.step()
+    opt.step()
+    # v1 = -0.05 ; p1 = 0.95 ; v2 = 0.9*-0.05 - 0.05 = -0.095 ; p2 = 0.855
+    torch.testing.assert_close(p, torch.tensor([0.855]))

