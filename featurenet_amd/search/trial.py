@@ -105,6 +105,10 @@ def run_trial(spec: ModelSpec, cfg: TrialConfig, device=None) -> ModelSpec:
             os.makedirs(cfg.save_dir, exist_ok=True)
             trainer.meta["spec"] = spec.to_dict()
             trainer.save(os.path.join(cfg.save_dir, f"{cfg.save_prefix}{spec.name}.fnk"))
+            from ..utils.graph import to_svg
+
+            with open(os.path.join(cfg.save_dir, f"{cfg.save_prefix}{spec.name}.svg"), "w") as f:
+                f.write(to_svg(model))
     except CompileError as e:
         spec.status, spec.accuracy, spec.error = "invalid", 0.0, str(e)
     except TrainingFailed as e:

@@ -1,0 +1,1 @@
+"""NAS task service: SQLite task store, REST API (FastAPI) and worker processes."""

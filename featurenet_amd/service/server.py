@@ -1,0 +1,136 @@
+"""REST task service (reference Flask app, ``ui/back/main.py:145-230``).
+
+Routes (same paths and payloads as the reference, port 9999):
+
+* ``POST   /sample/``                               ``{"data": {dataset, max_sampling_time,
+  nb_initial_config, max_nb_cells, max_nb_blocks, nb_training_iterations, task_name}}``
+  -> creates the task and starts a worker process
+* ``GET    /sample/``                               all tasks (+ ``nb_valid_elements``)
+* ``GET    /sample/{id}[?full=1]``                  one task (+ ``models`` from the
+  ``{N}products.json`` vector list when ``full``)
+* ``GET    /sample/{id}/product/{pId}/graph|model`` the candidate's graph (SVG) or
+  checkpoint (``.fnk``)
+* ``DELETE /sample/``                               drop all tasks
+* ``GET    /``                                      a static dashboard (replaces the React SPA)
+
+Built on FastAPI (installed) instead of Flask (not installed); workers are
+separate processes (``python -m featurenet_amd.service.worker``).
+"""
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+from .store import TaskStore
+
+STATIC = Path(__file__).parent / "static"
+
+
+def _valid_elements(task: dict, count_only: bool = True) -> dict:
+    path = task.get("products")
+    files = sorted(f for f in os.listdir(path) if f.endswith(".fnk")) if path and os.path.isdir(path) else []
+    if count_only:
+        task["nb_valid_elements"] = len(files)
+    else:
+        task["valid_elements"] = files
+    return task
+
+
+def _models(task: dict):
+    path, n = task.get("products"), task.get("nb_initial_config")
+    f = Path(f"{path}/{n}products.json")
+    if not path or not f.is_file():
+        return None
+
+    def fmt(v):
+        s = v[1][1]
+        return {"accuracy": v[0], "name": v[1][0], "nb_blocks": s[0], "nb_layers": s[1], "nb_params": s[2],
+                "nb_flops": s[3], "robustness": v[1][2][0]}
+
+    return [fmt(v) for v in json.loads(f.read_text())]
+
+
+def _file_endswith(folder: str, suffix: str):
+    if not folder or not os.path.isdir(folder):
+        return None
+    for f in sorted(os.listdir(folder)):
+        if f.endswith(suffix):
+            return os.path.join(folder, f)
+    return None
+
+
+def create_app(db_path: str = "samples.db", base_path: str = "products", devices: str | None = None,
+               spawn_workers: bool = True):
+    from fastapi import FastAPI, Request
+    from fastapi.middleware.cors import CORSMiddleware
+    from fastapi.responses import FileResponse, HTMLResponse, JSONResponse
+
+    store = TaskStore(db_path)
+    app = FastAPI(title="featurenet_amd NAS service")
+    app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_methods=["*"], allow_headers=["*"])
+    app.state.store = store
+    app.state.workers = {}
+
+    def start_worker(task_id: str):
+        cmd = [sys.executable, "-m", "featurenet_amd.service.worker", task_id, "--db", db_path, "--base", base_path]
+        if devices:
+            cmd += ["--devices", devices]
+        log = open(Path(base_path) / f"worker_{task_id}.log", "w")
+        app.state.workers[task_id] = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT,
+                                                      cwd=os.getcwd(), start_new_session=True)
+
+    Path(base_path).mkdir(parents=True, exist_ok=True)
+
+    @app.delete("/sample/")
+    def sample_delete_all():
+        return store.delete_all()
+
+    @app.get("/sample/")
+    def sample_all():
+        return [_valid_elements(t) for t in store.all()]
+
+    @app.get("/sample/{task_id}/product/{pid}/{content}")
+    def model_get(task_id: str, pid: str, content: str):
+        task = store.get(task_id)
+        if task is None:
+            return JSONResponse({}, status_code=404)
+        if content == "graph":
+            f, mime = _file_endswith(task.get("products"), f"{pid}.svg"), "image/svg+xml"
+        else:
+            f, mime = _file_endswith(task.get("products"), f"{pid}.fnk"), "application/octet-stream"
+        if f is None:
+            return JSONResponse({})
+        return FileResponse(f, media_type=mime)
+
+    @app.get("/sample/{task_id}")
+    def sample_get(task_id: str, full: str | None = None):
+        task = store.get(task_id)
+        if task is None:
+            return JSONResponse({}, status_code=404)
+        if full:
+            task["models"] = _models(task)
+        return task
+
+    @app.post("/sample/")
+    async def sample_post(request: Request):
+        body = await request.json()
+        data = body.get("data", body) if isinstance(body, dict) else {}
+        task = store.create(data)
+        if spawn_workers:
+            start_worker(task["task_id"])
+        return task
+
+    @app.get("/", response_class=HTMLResponse)
+    def index():
+        return (STATIC / "index.html").read_text()
+
+    return app
+
+
+def serve(host: str = "0.0.0.0", port: int = 9999, db_path: str = "samples.db", base_path: str = "products",
+          devices: str | None = None) -> None:
+    import uvicorn
+
+    uvicorn.run(create_app(db_path, base_path, devices), host=host, port=port)

@@ -1,0 +1,70 @@
+"""REST task service: reference routes, SQLite store, worker pipeline (CPU, tiny)."""
+import os
+
+import pytest
+
+REF = "/root/reference"
+
+
+def test_store_concurrent_field_updates(tmp_path):
+    from featurenet_amd.service.store import TaskStore
+
+    s = TaskStore(tmp_path / "t.db")
+    t = s.create({"task_name": "a b", "dataset": "mnist"})
+    assert t["task_name"] == "a_b" and t["status"] == "init"
+    s.update(t["task_id"], fm="x.xml")
+    s2 = TaskStore(tmp_path / "t.db")          # a second "process" view
+    s2.update(t["task_id"], "fm_complete", pdt="y.pdt")
+    got = s.get(t["task_id"])
+    assert got["fm"] == "x.xml" and got["pdt"] == "y.pdt" and got["status"] == "fm_complete"
+    assert len(s.all()) == 1 and s.delete_all() == 1 and s.all() == []
+
+
+@pytest.mark.skipif(not os.path.isfile(f"{REF}/ui/back/samples.db"), reason="no reference samples.db")
+def test_store_opens_reference_db(tmp_path):
+    import shutil
+
+    from featurenet_amd.service.store import TaskStore
+
+    dst = tmp_path / "samples.db"
+    shutil.copy(f"{REF}/ui/back/samples.db", dst)      # plain SQLite, read as data
+    assert isinstance(TaskStore(dst).all(), list)
+
+
+def test_generated_template_matches_reference():
+    from featurenet_amd.fm.space import SearchSpace
+
+    if not os.path.isfile(f"{REF}/main_1block_nas.xml"):
+        pytest.skip("no reference template")
+    assert SearchSpace().xml() == open(f"{REF}/main_1block_nas.xml").read()
+
+
+def test_rest_routes_and_worker_pipeline(tmp_path):
+    from fastapi.testclient import TestClient
+
+    from featurenet_amd import _native
+    from featurenet_amd.service.server import create_app
+    from featurenet_amd.service.worker import run_task
+
+    if not _native.runtime_available():
+        pytest.skip("native runtime not built")
+    db, base = str(tmp_path / "s.db"), str(tmp_path / "products")
+    app = create_app(db, base, spawn_workers=False)
+    c = TestClient(app)
+    r = c.post("/sample/", json={"data": {"task_name": "t1", "dataset": "mnist", "max_sampling_time": 0.3,
+                                          "nb_initial_config": 3, "max_nb_cells": 1, "max_nb_blocks": 1,
+                                          "nb_training_iterations": 1, "synthetic_sizes": [128, 32]}})
+    tid = r.json()["task_id"]
+    assert c.get("/sample/").json()[0]["task_id"] == tid
+    done = run_task(app.state.store, tid, base, devices=["cpu"])
+    assert done["status"] == "generation_complete", done.get("error")
+    full = c.get(f"/sample/{tid}", params={"full": 1}).json()
+    assert len(full["models"]) == 3
+    assert c.get("/sample/").json()[0]["nb_valid_elements"] >= 1
+    name = full["models"][0]["name"]
+    g = c.get(f"/sample/{tid}/product/{name}/graph")
+    assert g.status_code == 200 and g.text.startswith("<svg")
+    m = c.get(f"/sample/{tid}/product/{name}/model")
+    assert m.status_code == 200 and len(m.content) > 100
+    assert "<html>" in c.get("/").text
+    assert c.delete("/sample/").json() == 1
