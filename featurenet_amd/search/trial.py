@@ -116,6 +116,10 @@ def run_trial(spec: ModelSpec, cfg: TrialConfig, device=None) -> ModelSpec:
     except Exception as e:  # any other failure drops the candidate, like the reference
         spec.status, spec.accuracy, spec.error = "failed", 0.0, f"{type(e).__name__}: {e}\n{traceback.format_exc(limit=4)}"
     spec.metrics = list(spec.metrics) + [{"trial_time_s": time.time() - t0}]
+    from ..utils.events import default_log
+
+    default_log().emit("trial", name=spec.name, status=spec.status, accuracy=spec.accuracy,
+                       params=spec.nb_params, seconds=time.time() - t0, device=str(device))
     return spec
 
 

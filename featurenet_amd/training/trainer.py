@@ -29,6 +29,7 @@ import torch.distributed as dist
 
 from ..ops import FlatAdam, FlatSGD, softmax_xent
 from ..parallel.ddp import GradBucketer
+from ..utils.events import default_log
 from .callbacks import Callback
 from .checkpoint import save_checkpoint
 from .data import DeviceLoader
@@ -145,6 +146,7 @@ class Trainer:
                 if not math.isfinite(logs["loss"]):
                     raise TrainingFailed("non-finite training loss")
                 self.history.log(epoch, logs)
+                default_log().emit("epoch", epoch=epoch, world=self.world, **logs)
                 if verbose and self.rank == 0:
                     msg = " ".join(f"{k}={v:.4g}" for k, v in logs.items())
                     print(f"epoch {epoch + 1}/{epochs} {msg}", flush=True)
