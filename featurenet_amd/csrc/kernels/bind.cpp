@@ -18,6 +18,9 @@ extern "C" {
 int fn_igemm_fwd(const void*, const void*, const float*, void*, float*, const int*, const int*, long long, int, int,
                  int, int, int, hipStream_t);
 int fn_igemm_fwd_mblocks(long long);
+int fn_conv_halo(const void*, const void*, const float*, void*, float*, const int*, int, int, hipStream_t);
+long long fn_conv_halo_lds(const int*, int);
+int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
                    hipStream_t);
 int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
@@ -68,6 +71,23 @@ PYBIND11_MODULE(_C, m) {
         "igemm_fwd");
   });
   m.def("igemm_fwd_mblocks", &fn_igemm_fwd_mblocks);
+  m.def("conv_halo", [](uintptr_t src, uintptr_t wt, uintptr_t bias, uintptr_t out, uintptr_t stats,
+                        std::vector<int> geom, int ncol, int act, uintptr_t st) {
+    need(geom, 16, "conv_halo");
+    chk(fn_conv_halo(P<const void*>(src), P<const void*>(wt), P<const float*>(bias), P<void*>(out), P<float*>(stats),
+                     geom.data(), ncol, act, S(st)),
+        "conv_halo");
+  });
+  m.def("conv_halo_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t dw, std::vector<int> geom, int cout,
+                              int grid_x, uintptr_t st) {
+    need(geom, 16, "conv_halo_wgrad");
+    chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x, S(st)),
+        "conv_halo_wgrad");
+  });
+  m.def("conv_halo_lds", [](std::vector<int> geom, int ncol) {
+    need(geom, 16, "conv_halo_lds");
+    return fn_conv_halo_lds(geom.data(), ncol);
+  });
   m.def("igemm_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t part, uintptr_t tab, std::vector<int> geom,
                           long long M, int Cout, int K, int splits, int vec, uintptr_t st) {
     need(geom, 14, "igemm_wgrad");

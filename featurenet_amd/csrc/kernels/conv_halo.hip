@@ -1,0 +1,514 @@
+// LDS-halo implicit-GEMM convolution for stride-1 3-D convs (CDNA4 MFMA).
+//
+// The gather-based igemm kernel (conv_igemm.hip) re-fetches the im2col row of
+// every output position once per tap: for FeatureNet-3D's 5x5x5 / 4x4x4 /
+// 3x3x3 stride-1 layers that is 27-125 reads of every input voxel, so those
+// layers run L2-bandwidth-bound at 15-25 % of MFMA peak.  This kernel stages
+// a 3-D input tile (the output tile plus its kernel halo) in LDS ONCE per
+// 16-channel slice and builds every MFMA A-fragment straight from it:
+//
+//   output tile  TD x TH x OW   (<= 256 rows; full output rows in W)
+//   LDS halo     (TD+KD-1) x (TH+KH-1) x (OW+KW-1) positions x 16 channels
+//   K loop       pass p over C/16 channel slices, 2 taps per MFMA k-step
+//                (k = [tap][16 ch]), weights streamed through a double-
+//                buffered 64-k LDS stage
+//
+// so global/L2 traffic drops from ~taps x |x| to ~halo/tile x |x| and the
+// kernel becomes MFMA/LDS-bound.  Used for forward (with fused bias/act or BN
+// statistics epilogue) and for dgrad (dx = conv(dy, flip(W)^T), stride 1).
+//
+// A-fragment LDS reads: lane (row lr, k-group lg) reads 16 B at
+// (hbase[row] + tapoff[tap(lg)]) * 32 B + (lg & 1) * 16 B.  Rows are
+// consecutive halo positions, so a ds_read_b128 lane group {lr 0-3,12-15 @ lg,
+// lr 4-11 @ lg^1} touches 16 distinct 16-B slots of a 256-B bank line.
+#include "common.h"
+
+struct HaloGeom {
+  int N, ID, IH, IW, C;    // gathered source (x for fwd, dy for dgrad), channels-last
+  int OD, OH, OW;          // output dims
+  int KD, KH, KW;          // kernel
+  int pd, ph, pw;          // leading pads (stride 1)
+  int TD, TH;              // output tile (rows = TD * TH * OW <= 256)
+};
+
+#define H_BM 256
+#define H_BK 64
+
+template <int BN, int ACT, bool HAS_BIAS, bool STATS>
+__global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wt,
+                                                           const float* __restrict__ bias, bf16* __restrict__ out,
+                                                           float* __restrict__ stats, HaloGeom g, int Ncol) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  constexpr int NT = BN / 16;
+  constexpr int B_STAGE = BN * H_BK;             // elements
+  constexpr int B_CHUNKS = BN * (H_BK / 8);
+  constexpr int B_PER_T = (B_CHUNKS + 255) / 256;
+  constexpr int LDO = BN + 8;
+
+  const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
+  const int HP = HD * HH * HW;                   // halo positions
+  const int T = g.KD * g.KH * g.KW;
+  const int T4 = (T + 3) & ~3;
+  const int spp = T4 >> 2;                       // 64-k stages per channel pass
+  const int npass = g.C >> 4;
+  const int nq = spp * npass;
+  const int ldw = npass * T4 * 16;
+  const int rows = g.TD * g.TH * g.OW;
+
+  bf16* halo = reinterpret_cast<bf16*>(dsm);
+  bf16* Bs = reinterpret_cast<bf16*>(dsm + (size_t)HP * 32);
+  int* taptab = reinterpret_cast<int*>(dsm + (size_t)HP * 32 + 2 * B_STAGE * 2);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
+  const int ntile = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, ntile);
+  const int th_i = tile % thn;
+  const int td_i = (tile / thn) % tdn;
+  const int n = tile / (thn * tdn);
+  const int d0 = td_i * g.TD, h0 = th_i * g.TH;
+  const int n0 = blockIdx.y * BN;
+
+  // tap-offset table (halo position delta of each tap; padding taps -> 0)
+  for (int t = tid; t < T4; t += 256) {
+    int off = 0;
+    if (t < T) {
+      const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
+      off = (kd * HH + kh) * HW + kw;
+    }
+    taptab[t] = off;
+  }
+
+  // this lane's 4 A rows -> halo base positions
+  int hbase[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int r = wave * 64 + mt * 16 + lr;
+    const int rr = r < rows ? r : 0;
+    const int w = rr % g.OW, th = (rr / g.OW) % g.TH, td = rr / (g.OW * g.TH);
+    hbase[mt] = (td * HH + th) * HW + w;
+  }
+
+  auto fill_halo = [&](int p) {
+    const int nchunk = HP * 2;
+    for (int c0 = 0; c0 < nchunk; c0 += 256 * 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j * 256 + tid;
+        const int pos = c >> 1, half = c & 1;
+        const int hw = pos % HW, hh = (pos / HW) % HH, hd = pos / (HW * HH);
+        const int gd = d0 - g.pd + hd, gh = h0 - g.ph + hh, gw = hw - g.pw;
+        const bool ok = c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                        (unsigned)gw < (unsigned)g.IW;
+        const long long off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + p * 16 + half * 8;
+        const uint4 x = *(const uint4*)(src + (ok ? off : 0));
+        v[j] = ok ? x : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j * 256 + tid;
+        if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = v[j];
+      }
+    }
+  };
+
+  uint4 rbv[B_PER_T];
+  auto load_b = [&](int q) {
+    const int kbase = q * H_BK;
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int idx = tid + i * 256;
+      const int r = (idx >> 3) < BN ? (idx >> 3) : BN - 1;
+      const int k = kbase + (idx & 7) * 8;
+      const bool ok = idx < B_CHUNKS && n0 + r < Ncol;
+      const uint4 v = *(const uint4*)(wt + (ok ? (long long)(n0 + r) * ldw + k : 0));
+      rbv[i] = ok ? v : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto write_b = [&](int buf) {
+    bf16* b = Bs + buf * B_STAGE;
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < B_CHUNKS) {
+        const int r = idx >> 3, c = idx & 7;
+        *(uint4*)(b + r * H_BK + ((c ^ (r & 7)) << 3)) = rbv[i];
+      }
+    }
+  };
+
+  f32x4 acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  fill_halo(0);
+  load_b(0);
+  write_b(0);
+  __syncthreads();
+
+  const int mt_live = rows - wave * 64;   // rows of this wave inside the tile (uniform)
+  for (int q = 0; q < nq; ++q) {
+    if (q > 0 && q % spp == 0) {          // next 16-channel slice (all reads of the last one are done)
+      fill_halo(q / spp);
+      __syncthreads();
+    }
+    const bool more = q + 1 < nq;
+    if (more) load_b(q + 1);              // weight loads in flight during the MFMAs
+    const bf16* b = Bs + (q & 1) * B_STAGE;
+    const int tap0 = (q % spp) * 4;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int toff = taptab[tap0 + ks * 2 + (lg >> 1)];
+      bf16x8 fa[4], fb[NT];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        fa[mt] = *(const bf16x8*)(halo + (size_t)(hbase[mt] + toff) * 16 + (lg & 1) * 8);
+      const int ch = ks * 4 + lg;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int row = nt * 16 + lr;
+        fb[nt] = *(const bf16x8*)(b + row * H_BK + ((ch ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        if (mt * 16 < mt_live) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+        }
+      }
+    }
+    if (more) write_b((q + 1) & 1);       // the other buffer: its last readers passed the previous barrier
+    __syncthreads();
+  }
+
+  // ---- epilogue (LDS staging reuses the halo region) ----
+  bf16* Os = reinterpret_cast<bf16*>(dsm);
+  float csum[NT], csq[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) { csum[nt] = 0.f; csq[nt] = 0.f; }
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = nt * 16 + lr;
+    const bool cv = (n0 + col) < Ncol;
+    float bv = 0.f;
+    if constexpr (HAS_BIAS) bv = cv ? bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wave * 64 + mt * 16 + lg * 4 + r;
+        float v = act_fwd(acc[mt][nt][r] + bv, ACT);
+        const bf16 bvv = f2bf(v);
+        Os[row * LDO + col] = bvv;
+        if constexpr (STATS) {
+          bool rv = cv && row < rows;
+          if (rv) {
+            const int td = row / (g.OW * g.TH), th = (row / g.OW) % g.TH;
+            rv = d0 + td < g.OD && h0 + th < g.OH;
+          }
+          const float f = rv ? bf2f(bvv) : 0.f;
+          csum[nt] += f;
+          csq[nt] += f * f;
+        }
+      }
+    }
+  }
+  if constexpr (STATS) {
+    float* red = reinterpret_cast<float*>(dsm + (size_t)H_BM * LDO * 2);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      float s = csum[nt], qq = csq[nt];
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      qq += __shfl_xor(qq, 16, 64); qq += __shfl_xor(qq, 32, 64);
+      if (lg == 0) { red[(wave * 2 + 0) * BN + nt * 16 + lr] = s; red[(wave * 2 + 1) * BN + nt * 16 + lr] = qq; }
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < Ncol) {
+      const float s = red[0 * BN + tid] + red[2 * BN + tid] + red[4 * BN + tid] + red[6 * BN + tid];
+      const float qq = red[1 * BN + tid] + red[3 * BN + tid] + red[5 * BN + tid] + red[7 * BN + tid];
+      stats[(long long)tile * 2 * Ncol + n0 + tid] = s;
+      stats[(long long)tile * 2 * Ncol + Ncol + n0 + tid] = qq;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  const bool vec_out = (Ncol % 8) == 0;
+#pragma unroll
+  for (int i = 0; i < CPR; ++i) {
+    const int idx = tid + i * 256;
+    const int row = idx / CPR, ch = idx % CPR;
+    if (row >= rows) continue;
+    const int w = row % g.OW, th = (row / g.OW) % g.TH, td = row / (g.OW * g.TH);
+    if (d0 + td >= g.OD || h0 + th >= g.OH) continue;
+    const long long m = (((long long)n * g.OD + d0 + td) * g.OH + h0 + th) * g.OW + w;
+    const int col = n0 + ch * 8;
+    if (vec_out && col + 8 <= Ncol) {
+      *(uint4*)(out + m * Ncol + col) = *(const uint4*)(Os + row * LDO + ch * 8);
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (col + j < Ncol) out[m * Ncol + col + j] = Os[row * LDO + ch * 8 + j];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient on the same halo tiles
+// ---------------------------------------------------------------------------
+// dW[co][tap][ci] = sum_rows dy[row][co] * x[pos(row) + tap][ci]
+// One workgroup: a 16-channel input slice (grid.z), a group of 4*TPW taps
+// (grid.y, TPW per wave) and a strided set of output tiles (grid.x,
+// persistent).  Per tile the dy tile [256][Cout] and the x halo slice are
+// staged in LDS once; both MFMA operands are read with ds_read_b64_tr_b16
+// (k = tile rows is the slow axis of both), the x operand at per-lane halo
+// positions row -> pos(row) + tapoff.  fp32 accumulators live across all the
+// workgroup's tiles and are folded into dW with one atomic add per element.
+template <int MT>
+__device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(lo));
+  s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(hi));
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  s8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int MT>
+__global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __restrict__ dy,
+                                                                 const bf16* __restrict__ src,
+                                                                 float* __restrict__ dw, HaloGeom g, int Cout) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  constexpr int TPW = MT == 1 ? 16 : 32 / MT;   // taps per wave (acc <= 128 VGPRs)
+  constexpr int BCO = MT * 16;
+  constexpr int LDY = BCO + 16;            // conflict-free transposed reads (as igemm wgrad)
+  const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
+  const int HP = HD * HH * HW;
+  const int T = g.KD * g.KH * g.KW;
+  const int rows = g.TD * g.TH * g.OW;
+  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
+  const int ntiles = g.N * tdn * thn;
+
+  bf16* Ys = reinterpret_cast<bf16*>(dsm);                                   // [256][LDY]
+  bf16* halo = reinterpret_cast<bf16*>(dsm + (size_t)H_BM * LDY * 2);        // [HP][16]
+  int* rowpos = reinterpret_cast<int*>(dsm + (size_t)H_BM * LDY * 2 + (size_t)HP * 32);  // [256]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int slice = blockIdx.z;
+  const int tap0 = (blockIdx.y * 4 + wave) * TPW;
+
+  for (int r = tid; r < H_BM; r += 256) {
+    int pos = 0;
+    if (r < rows) {
+      const int w = r % g.OW, th = (r / g.OW) % g.TH, td = r / (g.OW * g.TH);
+      pos = (td * HH + th) * HW + w;
+    }
+    rowpos[r] = pos;
+  }
+  int toff[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = tap0 + i < T ? tap0 + i : 0;
+    const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
+    toff[i] = (kd * HH + kh) * HW + kw;
+  }
+  const int ntap = T - tap0 < TPW ? (T - tap0 > 0 ? T - tap0 : 0) : TPW;   // live taps of this wave
+
+  f32x4 acc[TPW][MT];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+    const int d0 = td_i * g.TD, h0 = th_i * g.TH;
+    __syncthreads();   // previous tile's reads are done
+    // dy tile -> Ys (rows outside the output are zero, so they add nothing)
+    constexpr int YC = BCO / 8;
+    for (int idx = tid; idx < H_BM * YC; idx += 256) {
+      const int r = idx / YC, c = idx % YC;
+      bool ok = r < rows;
+      long long m = 0;
+      if (ok) {
+        const int w = r % g.OW, th = (r / g.OW) % g.TH, td = r / (g.OW * g.TH);
+        ok = d0 + td < g.OD && h0 + th < g.OH && c * 8 < Cout;
+        m = (((long long)n * g.OD + d0 + td) * g.OH + h0 + th) * g.OW + w;
+      }
+      const uint4 v = *(const uint4*)(dy + (ok ? m * Cout + c * 8 : 0));
+      *(uint4*)(Ys + r * LDY + c * 8) = ok ? v : make_uint4(0, 0, 0, 0);
+    }
+    // x halo slice -> LDS
+    const int nchunk = HP * 2;
+    for (int c0 = 0; c0 < nchunk; c0 += 256 * 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j * 256 + tid;
+        const int pos = c >> 1, half = c & 1;
+        const int hw = pos % HW, hh = (pos / HW) % HH, hd = pos / (HW * HH);
+        const int gd = d0 - g.pd + hd, gh = h0 - g.ph + hh, gw = hw - g.pw;
+        const bool ok = c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                        (unsigned)gw < (unsigned)g.IW;
+        const long long off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + slice * 16 + half * 8;
+        const uint4 x = *(const uint4*)(src + (ok ? off : 0));
+        v[j] = ok ? x : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j * 256 + tid;
+        if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = v[j];
+      }
+    }
+    __syncthreads();
+    const int kst = (rows + 31) >> 5;
+    for (int ks = 0; ks < kst; ++ks) {
+      bf16x8 fa[MT];
+      const int r_lo = ks * 32 + 4 * G + q, r_hi = r_lo + 16;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        fa[mt] = tr_pair<MT>(Ys + r_lo * LDY + mt * 16 + 4 * p4, Ys + r_hi * LDY + mt * 16 + 4 * p4);
+      const int plo = rowpos[r_lo], phi = rowpos[r_hi];
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        if (i < ntap) {
+          const bf16x8 fb = tr_pair<MT>(halo + (size_t)(plo + toff[i]) * 16 + 4 * p4,
+                                        halo + (size_t)(phi + toff[i]) * 16 + 4 * p4);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb, acc[i][mt], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // D[row=co][col=ci]: lane holds co = mt*16 + (lane>>4)*4 + r, ci = lane & 15
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    if (i < ntap) {
+      const int t = tap0 + i;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = mt * 16 + (lane >> 4) * 4 + r;
+          if (co < Cout)
+            atomicAdd(dw + ((long long)co * T + t) * g.C + slice * 16 + (lane & 15), acc[i][mt][r]);
+        }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+static HaloGeom parse_halo(const int* v) {
+  HaloGeom g;
+  g.N = v[0]; g.ID = v[1]; g.IH = v[2]; g.IW = v[3]; g.C = v[4];
+  g.OD = v[5]; g.OH = v[6]; g.OW = v[7];
+  g.KD = v[8]; g.KH = v[9]; g.KW = v[10];
+  g.pd = v[11]; g.ph = v[12]; g.pw = v[13];
+  g.TD = v[14]; g.TH = v[15];
+  return g;
+}
+
+static size_t halo_lds_bytes(const HaloGeom& g, int BN) {
+  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  const int T4 = (g.KD * g.KH * g.KW + 3) & ~3;
+  const size_t main_ = hp * 32 + 2 * (size_t)BN * H_BK * 2;
+  const size_t epi = (size_t)H_BM * (BN + 8) * 2 + 16 * (size_t)BN * 4;
+  return (main_ > epi ? main_ : epi) + (size_t)T4 * 4 + 16;
+}
+
+template <int BN, int ACT, bool HB, bool ST>
+static int launch_halo(dim3 grid, size_t lds, hipStream_t st, const bf16* s, const bf16* w, const float* b, bf16* o,
+                       float* stats, const HaloGeom& g, int Ncol) {
+  static size_t configured = 0;
+  if (lds > configured) {
+    hipError_t e = hipFuncSetAttribute((const void*)conv_halo_kernel<BN, ACT, HB, ST>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+    configured = lds;
+  }
+  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST>), grid, dim3(256), lds, st, s, w, b, o, stats, g, Ncol);
+  return 0;
+}
+
+// wt: [Ncol][C/16][T4][16] bf16 (tap-padded); returns 0 on success.
+extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, void* out, float* stats,
+                            const int* geom16, int Ncol, int act, hipStream_t st) {
+  const HaloGeom g = parse_halo(geom16);
+  if (g.C % 16 != 0 || g.TD * g.TH * g.OW > H_BM || g.TD < 1 || g.TH < 1) return -2;
+  if (stats && act != ACT_NONE) return -1;
+  const int BN = Ncol <= 32 ? 32 : 64;
+  const size_t lds = halo_lds_bytes(g, BN);
+  if (lds > 160 * 1024) return -4;
+  const int tiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
+  dim3 grid((unsigned)tiles, (Ncol + BN - 1) / BN);
+  const bf16* s = (const bf16*)src;
+  const bf16* w = (const bf16*)wt;
+  bf16* o = (bf16*)out;
+  const bool hb = bias != nullptr;
+  int rc;
+#define HCASE(B, A, H, S) rc = launch_halo<B, A, H, S>(grid, lds, st, s, w, bias, o, stats, g, Ncol)
+#define HBN(B)                                                   \
+  do {                                                           \
+    if (stats) HCASE(B, ACT_NONE, false, true);                  \
+    else if (act == ACT_NONE) { if (hb) HCASE(B, ACT_NONE, true, false); else HCASE(B, ACT_NONE, false, false); } \
+    else if (act == ACT_RELU) HCASE(B, ACT_RELU, true, false);    \
+    else if (act == ACT_TANH) HCASE(B, ACT_TANH, true, false);    \
+    else HCASE(B, ACT_SIGMOID, true, false);                      \
+  } while (0)
+  if (act != ACT_NONE && !hb) return -5;   // activation variants are instantiated with bias only
+  if (BN == 32) HBN(32); else HBN(64);
+#undef HBN
+#undef HCASE
+  if (rc) return rc;
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long long fn_conv_halo_lds(const int* geom16, int Ncol) {
+  const HaloGeom g = parse_halo(geom16);
+  return (long long)halo_lds_bytes(g, Ncol <= 32 ? 32 : 64);
+}
+
+static size_t halo_wgrad_lds(const HaloGeom& g, int MT) {
+  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  return (size_t)H_BM * (MT * 16 + 16) * 2 + hp * 32 + H_BM * 4 + 16;
+}
+
+// dw: fp32 [Cout][T][C], zero-initialised by the caller (atomics accumulate).
+extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, const int* geom16, int Cout,
+                                  int grid_x, hipStream_t st) {
+  const HaloGeom g = parse_halo(geom16);
+  if (g.C % 16 != 0 || g.TD * g.TH * g.OW > H_BM || Cout > 64 || Cout % 8 != 0) return -2;
+  const int MT = (Cout + 15) / 16;
+  const size_t lds = halo_wgrad_lds(g, MT);
+  if (lds > 160 * 1024) return -4;
+  const int T = g.KD * g.KH * g.KW;
+  const int TPW = MT == 1 ? 16 : 32 / MT;
+  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
+  const int gx = grid_x < ntiles ? (grid_x > 0 ? grid_x : 1) : ntiles;
+  dim3 grid((unsigned)gx, (unsigned)((T + 4 * TPW - 1) / (4 * TPW)), (unsigned)(g.C / 16));
+  const bf16* d = (const bf16*)dy;
+  const bf16* s = (const bf16*)src;
+#define WCASE(M)                                                                                           \
+  do {                                                                                                     \
+    static size_t cfg = 0;                                                                                 \
+    if (lds > cfg) {                                                                                       \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_halo_wgrad_kernel<M>,                           \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
+      if (e != hipSuccess) return (int)e;                                                                  \
+      cfg = lds;                                                                                           \
+    }                                                                                                      \
+    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M>), grid, dim3(256), lds, st, d, s, dw, g, Cout);          \
+  } while (0)
+  if (MT == 1) WCASE(1); else if (MT == 2) WCASE(2); else if (MT == 3) WCASE(3); else WCASE(4);
+#undef WCASE
+  FN_CHECK_LAUNCH();
+  return 0;
+}

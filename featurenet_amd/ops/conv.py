@@ -5,14 +5,22 @@ Reference parity: this op is what the reference builds with Keras
 inside ``Combination`` (``model/operation.py:179-186``); the north-star
 Conv3d layers of FeatureNet-3D use the same code path.
 
-GPU path (all in ``csrc/kernels/conv_igemm.hip``):
-  forward -> ``igemm_fwd``   (optional fused bias+activation, or BN statistics)
-  dgrad   -> ``igemm_fwd``   in transposed-conv mode (negated tap table)
-  wgrad   -> ``igemm_wgrad`` (split-m fp32 slabs) + ``slab_reduce``
+GPU path:
+  forward -> ``conv_halo`` (``csrc/kernels/conv_halo.hip``) for stride-1 convs
+             with >= 8 taps and C % 16 == 0 (LDS-staged input halo tiles),
+             else ``igemm_fwd`` (``conv_igemm.hip``, gathered im2col);
+             both fuse bias+activation or emit BN statistics
+  dgrad   -> ``conv_halo`` on dy with the flipped, transposed kernel (stride 1)
+             or ``igemm_fwd`` in transposed-conv mode (negated tap table)
+  wgrad   -> ``conv_halo_wgrad`` (stride 1, Cout <= 64: halo tiles, persistent
+             workgroups, fp32 atomics once per workgroup) or ``igemm_wgrad``
+             (split-m, fp32 atomics)
+``FEATURENET_CONV_HALO=0`` disables the halo path (A/B checks).
 """
 from __future__ import annotations
 
 import math
+import os
 import threading
 
 import numpy as np
@@ -144,10 +152,130 @@ def _pack_rows(mat: torch.Tensor) -> tuple[torch.Tensor, int]:
 
 
 # ---------------------------------------------------------------------------
+# LDS-halo path (stride-1 convs)
+# ---------------------------------------------------------------------------
+HALO_MAX_BYTES = 72 * 1024
+_PLAN_CACHE: dict = {}
+
+
+def halo_plan(OD: int, OH: int, OW: int, KD: int, KH: int, KW: int):
+    """Output tile (TD, TH) x full OW maximising MFMA row utilisation with the
+    16-channel input halo <= HALO_MAX_BYTES; None when no tile fits."""
+    key = (OD, OH, OW, KD, KH, KW)
+    if key in _PLAN_CACHE:
+        return _PLAN_CACHE[key]
+    best, best_score = None, -1.0
+    if OW <= 256:
+        for TD in range(1, OD + 1):
+            for TH in range(1, OH + 1):
+                rows = TD * TH * OW
+                if rows > 256:
+                    break
+                halo = (TD + KD - 1) * (TH + KH - 1) * (OW + KW - 1) * 32
+                if halo > HALO_MAX_BYTES:
+                    continue
+                tiles = math.ceil(OD / TD) * math.ceil(OH / TH)
+                score = OD * OH * OW / (tiles * 256.0) - 1e-9 * halo
+                if score > best_score:
+                    best, best_score = (TD, TH), score
+    _PLAN_CACHE[key] = best
+    return best
+
+
+def _halo_enabled() -> bool:
+    return os.environ.get("FEATURENET_CONV_HALO", "1") != "0"
+
+
+def halo_fwd_plan(spec: ConvSpec):
+    if not _halo_enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
+        return None
+    if spec.C % 16 or spec.K < 16 or spec.taps < 8:
+        return None
+    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW)
+
+
+def halo_dgrad_plan(spec: ConvSpec):
+    if not _halo_enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
+        return None
+    if spec.K % 16 or spec.C < 16 or spec.taps < 8:
+        return None
+    return halo_plan(spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW)
+
+
+def halo_weights(w3: torch.Tensor) -> torch.Tensor:
+    """[Ncol, T, Csrc] -> bf16 [Ncol, Csrc/16 * T4 * 16] in the halo kernel's k order
+    (16-channel slice, tap padded to a multiple of 4, 16 channels)."""
+    n, T, c = w3.shape
+    T4 = (T + 3) // 4 * 4
+    out = torch.zeros(n, c // 16, T4, 16, dtype=torch.bfloat16, device=w3.device)
+    out[:, :, :T] = w3.reshape(n, T, c // 16, 16).permute(0, 2, 1, 3)
+    return out.reshape(n, -1)
+
+
+def halo_wgrad_plan(spec: ConvSpec):
+    if not _halo_enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
+        return None
+    if spec.C % 16 or spec.K % 8 or spec.K > 64 or spec.taps < 8:
+        return None
+    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW)
+
+
+def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> torch.Tensor:
+    """dW via LDS halo tiles; fp32 [K, KD, KH, KW, C]."""
+    TD, TH = plan
+    geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
+            spec.pd, spec.ph, spec.pw, TD, TH]
+    mt = (spec.K + 15) // 16
+    tpw = 16 if mt == 1 else 32 // mt
+    per_tile = math.ceil(spec.taps / (4 * tpw)) * (spec.C // 16)
+    dw = torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
+    _native.kernels().conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), geom, spec.K,
+                                      max(1, target_wgs // per_tile), _native.stream(x5))
+    return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
+
+
+def _halo_call(src5, wmat, bias, out, stats, geom, ncol, act):
+    K = _native.kernels()
+    if act and bias is None:
+        bias = torch.zeros(ncol, dtype=torch.float32, device=src5.device)
+    K.conv_halo(src5.data_ptr(), wmat.data_ptr(), _native.ptr(bias), out.data_ptr(), _native.ptr(stats), geom,
+                ncol, act, _native.stream(src5))
+
+
+def halo_conv_fwd(x5, w, bias, spec: ConvSpec, act: int, want_stats: bool, plan):
+    TD, TH = plan
+    geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
+            spec.pd, spec.ph, spec.pw, TD, TH]
+    wmat = halo_weights(w.reshape(spec.K, spec.taps, spec.C))
+    y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
+    stats = None
+    if want_stats:
+        tiles = spec.N * math.ceil(spec.OD / TD) * math.ceil(spec.OH / TH)
+        stats = torch.empty(tiles, 2, spec.K, dtype=torch.float32, device=x5.device)
+    _halo_call(x5, wmat, bias, y, stats, geom, spec.K, act)
+    return y, stats
+
+
+def halo_conv_dgrad(dy5, w, spec: ConvSpec, plan):
+    """dx = conv(dy, flip(W)^T) with pads K-1-p (stride 1)."""
+    TD, TH = plan
+    geom = [spec.N, spec.OD, spec.OH, spec.OW, spec.K, spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW,
+            spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw, TD, TH]
+    wt = w.reshape(spec.K, spec.taps, spec.C).flip(1).permute(2, 1, 0)      # [C][T][K], taps reversed
+    wmat = halo_weights(wt)
+    dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
+    _halo_call(dy5, wmat, None, dx, None, geom, spec.C, 0)
+    return dx
+
+
+# ---------------------------------------------------------------------------
 # raw native calls
 # ---------------------------------------------------------------------------
 def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: ConvSpec, act: int,
-                    want_stats: bool):
+                    want_stats: bool, w: torch.Tensor | None = None):
+    plan = halo_fwd_plan(spec) if w is not None else None
+    if plan is not None:
+        return halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan)
     K = _native.kernels()
     assert x5.is_contiguous() and x5.dtype == torch.bfloat16
     gm = gather_mode(spec)
@@ -164,6 +292,9 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
 
 
 def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    plan = halo_dgrad_plan(spec)
+    if plan is not None:
+        return halo_conv_dgrad(dy5.contiguous(), w, spec, plan)
     K = _native.kernels()
     if spec.sd > 1 or spec.sh > 1 or spec.sw > 1:
         ODu, OHu, OWu = _dgrad_src_dims(spec)
@@ -191,6 +322,9 @@ def wgrad_splits(spec: ConvSpec, target_blocks: int = 1024) -> int:
 
 
 def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    plan = halo_wgrad_plan(spec)
+    if plan is not None:
+        return halo_conv_wgrad(dy5.contiguous(), x5.contiguous(), spec, plan)
     K = _native.kernels()
     gm = gather_mode(spec)
     tab = _table(spec, "fwd", gm, x5.device)
@@ -234,9 +368,12 @@ class ConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x5, w, b, spec: ConvSpec, act: int, want_stats: bool):
-        wmat, ldw = pack_weight_rows(w.detach(), spec)
         bias = b.detach().float().contiguous() if b is not None else None
-        y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
+        if halo_fwd_plan(spec) is not None:
+            y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats, w=w.detach())
+        else:
+            wmat, ldw = pack_weight_rows(w.detach(), spec)
+            y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
         ctx.spec, ctx.act, ctx.has_b = spec, act, b is not None
         ctx.x_needs = ctx.needs_input_grad[0]
         ctx.save_for_backward(x5, w, y if act else None)

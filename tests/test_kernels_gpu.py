@@ -36,6 +36,9 @@ CONV_CASES = [
     (4, 1, 16, 16, 16, 24, (1, 3, 3), 2, "same"),         # strided same-padded 2-D
     (3, 1, 15, 17, 24, 100, (1, 3, 1), 1, "same"),        # asymmetric kernel, Cout > 64
     (5, 1, 1, 40, 8, 16, (1, 1, 5), 1, "same"),           # 1-D conv
+    (2, 9, 10, 11, 16, 48, (3, 3, 3), 1, "same"),         # halo path: same padding, partial col block
+    (2, 1, 20, 23, 48, 32, (1, 5, 5), 1, "same"),         # halo path: 2-D, 3 channel slices
+    (1, 6, 7, 30, 32, 16, (2, 3, 3), 1, "valid"),         # halo path: even kernel, Cout 16
 ]
 
 
@@ -257,3 +260,48 @@ def test_featurenet3d_matches_reference_step(bn):
             assert c > 0.96 and r < 0.35, f"{n}: rel={r:.3g} cos={c:.4f}"
         else:
             assert c > 0.985 and r < 0.2, f"{n}: rel={r:.3g} cos={c:.4f}"
+
+
+HALO_CASES = [
+    # (N, D, H, W, C, K, kernel, padding, act)
+    (2, 29, 29, 29, 32, 32, (5, 5, 5), "valid", 0),
+    (2, 25, 25, 25, 32, 64, (4, 4, 4), "valid", 0),
+    (2, 22, 22, 22, 64, 64, (3, 3, 3), "valid", 0),
+    (3, 7, 9, 12, 16, 40, (3, 3, 3), "same", 1),
+    (2, 1, 31, 33, 32, 96, (1, 3, 3), "same", 2),
+]
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+def test_conv_halo_fwd_dgrad_stats(case):
+    """LDS-halo kernel (conv_halo.hip): forward (+bias/act), BN-stats epilogue and dgrad."""
+    _native_loaded()
+    from featurenet_amd.ops import conv as C
+
+    N, D, H, W, Ci, K, k, pad, act = case
+    torch.manual_seed(3)
+    x = torch.randn(N, D, H, W, Ci, device="cuda").to(torch.bfloat16)
+    spec = C.ConvSpec.make(x.shape, K, k, 1, pad)
+    assert C.halo_fwd_plan(spec) is not None and C.halo_dgrad_plan(spec) is not None
+    w = (torch.randn(K, spec.KD, spec.KH, spec.KW, Ci, device="cuda") * 0.05).to(torch.bfloat16).float()
+    b = torch.randn(K, device="cuda") * 0.1
+    acts = {0: None, 1: "relu", 2: "tanh"}
+    y, _ = C.halo_conv_fwd(x, w, b, spec, act, False, C.halo_fwd_plan(spec))
+    yr = ref.conv(x.float(), w, b, spec, acts[act])
+    close(y, yr)
+    if act == 0:
+        y2, st = C.halo_conv_fwd(x, w, None, spec, 0, True, C.halo_fwd_plan(spec))
+        yr2 = ref.conv(x.float(), w, None, spec).reshape(-1, K)
+        yb = y2.float().reshape(-1, K)
+        torch.testing.assert_close(st[:, 0].sum(0), yb.sum(0), rtol=2e-3, atol=2e-2)
+        torch.testing.assert_close(st[:, 1].sum(0), (yb * yb).sum(0), rtol=2e-3, atol=2e-2)
+        close(y2.reshape(-1, K), yr2)
+    g = (torch.randn(spec.out_shape5, device="cuda")).to(torch.bfloat16)
+    dx = C.halo_conv_dgrad(g, w, spec, C.halo_dgrad_plan(spec))
+    xr = x.float().clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    ref.conv(xr, wr, None, spec).backward(g.float())
+    close(dx, xr.grad)
+    if C.halo_wgrad_plan(spec) is not None:
+        dw = C.halo_conv_wgrad(g, x, spec, C.halo_wgrad_plan(spec))
+        close(dw, wr.grad)
