@@ -20,6 +20,9 @@ int fn_igemm_fwd(const void*, const void*, const float*, void*, float*, const in
 int fn_igemm_fwd_mblocks(long long);
 int fn_conv_halo(const void*, const void*, const float*, void*, float*, const int*, int, int, hipStream_t);
 long long fn_conv_halo_lds(const int*, int);
+int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, hipStream_t);
+int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
+int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
 int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
                    hipStream_t);
@@ -83,6 +86,20 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 16, "conv_halo_wgrad");
     chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x, S(st)),
         "conv_halo_wgrad");
+  });
+  m.def("dw_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, std::vector<int> geom, int act,
+                     uintptr_t st) {
+    need(geom, 20, "dw_fwd");
+    chk(fn_dw_fwd(P<const void*>(x), P<const float*>(w), P<const float*>(b), P<void*>(y), geom.data(), act, S(st)),
+        "dw_fwd");
+  });
+  m.def("dw_dgrad", [](uintptr_t dy, uintptr_t w, uintptr_t dx, std::vector<int> geom, uintptr_t st) {
+    need(geom, 20, "dw_dgrad");
+    chk(fn_dw_dgrad(P<const void*>(dy), P<const float*>(w), P<void*>(dx), geom.data(), S(st)), "dw_dgrad");
+  });
+  m.def("dw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, std::vector<int> geom, int splits, uintptr_t st) {
+    need(geom, 20, "dw_wgrad");
+    chk(fn_dw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), geom.data(), splits, S(st)), "dw_wgrad");
   });
   m.def("conv_halo_lds", [](std::vector<int> geom, int ncol) {
     need(geom, 16, "conv_halo_lds");

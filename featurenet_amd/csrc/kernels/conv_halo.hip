@@ -34,10 +34,22 @@ struct HaloGeom {
 #define H_BM 256
 #define H_BK 64
 
+// 16-B halo chunks per thread prefetched in registers (the rest of a larger
+// halo is loaded synchronously at the job boundary); BN=64 keeps 64 VGPRs of
+// accumulators, so it prefetches fewer.
+#define H_HC(BN) ((BN) == 32 ? 16 : 7)
+
+// Persistent form: each workgroup owns a contiguous run of output tiles
+// (adjacent tiles share halo rows -> same XCD L2) and walks the sequence of
+// (tile, channel-slice) jobs.  The NEXT job's halo is loaded into registers
+// while the current job computes (written to LDS at the job boundary), and
+// weight stages are prefetched two stages ahead, so neither halo nor weight
+// latency sits on the critical path.
 template <int BN, int ACT, bool HAS_BIAS, bool STATS>
 __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wt,
                                                            const float* __restrict__ bias, bf16* __restrict__ out,
-                                                           float* __restrict__ stats, HaloGeom g, int Ncol) {
+                                                           float* __restrict__ stats, HaloGeom g, int Ncol,
+                                                           int region_bytes) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int NT = BN / 16;
   constexpr int B_STAGE = BN * H_BK;             // elements
@@ -47,6 +59,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
 
   const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
   const int HP = HD * HH * HW;                   // halo positions
+  const int nchunk = HP * 2;
   const int T = g.KD * g.KH * g.KW;
   const int T4 = (T + 3) & ~3;
   const int spp = T4 >> 2;                       // 64-k stages per channel pass
@@ -54,23 +67,24 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
   const int nq = spp * npass;
   const int ldw = npass * T4 * 16;
   const int rows = g.TD * g.TH * g.OW;
+  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
+  const int ntiles = g.N * tdn * thn;
 
-  bf16* halo = reinterpret_cast<bf16*>(dsm);
-  bf16* Bs = reinterpret_cast<bf16*>(dsm + (size_t)HP * 32);
-  int* taptab = reinterpret_cast<int*>(dsm + (size_t)HP * 32 + 2 * B_STAGE * 2);
+  bf16* halo = reinterpret_cast<bf16*>(dsm);                      // also the epilogue staging area
+  bf16* Bs = reinterpret_cast<bf16*>(dsm + region_bytes);
+  int* taptab = reinterpret_cast<int*>(dsm + region_bytes + 2 * B_STAGE * 2);
+  int* posinfo = taptab + T4;                    // packed (hd, hh, hw) of every halo position
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
-  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
-  const int ntile = gridDim.x;
-  const int tile = xcd_remap(blockIdx.x, ntile);
-  const int th_i = tile % thn;
-  const int td_i = (tile / thn) % tdn;
-  const int n = tile / (thn * tdn);
-  const int d0 = td_i * g.TD, h0 = th_i * g.TH;
+  const int worker = xcd_remap(blockIdx.x, gridDim.x);
+  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const int t_begin = worker * per;
+  const int t_end = t_begin + per < ntiles ? t_begin + per : ntiles;
+  if (t_begin >= t_end) return;                  // whole workgroup exits together
+  const int njobs = (t_end - t_begin) * npass;
   const int n0 = blockIdx.y * BN;
 
-  // tap-offset table (halo position delta of each tap; padding taps -> 0)
   for (int t = tid; t < T4; t += 256) {
     int off = 0;
     if (t < T) {
@@ -79,8 +93,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
     }
     taptab[t] = off;
   }
-
-  // this lane's 4 A rows -> halo base positions
+  for (int pos = tid; pos < HP; pos += 256)
+    posinfo[pos] = ((pos / (HW * HH)) << 20) | (((pos / HW) % HH) << 10) | (pos % HW);
   int hbase[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
@@ -89,34 +103,66 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
     const int w = rr % g.OW, th = (rr / g.OW) % g.TH, td = rr / (g.OW * g.TH);
     hbase[mt] = (td * HH + th) * HW + w;
   }
+  __syncthreads();
 
-  auto fill_halo = [&](int p) {
-    const int nchunk = HP * 2;
-    for (int c0 = 0; c0 < nchunk; c0 += 256 * 8) {
-      uint4 v[8];
+  constexpr int HC = H_HC(BN);
+  uint4 hreg[HC];
+  auto halo_src = [&](int job, int c, const bf16*& base, int& off) -> bool {
+    const int tile = t_begin + job / npass, p = job % npass;
+    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+    const int info = posinfo[c < nchunk ? c >> 1 : 0];
+    const int gd = td_i * g.TD - g.pd + (info >> 20), gh = th_i * g.TH - g.ph + ((info >> 10) & 1023);
+    const int gw = (info & 1023) - g.pw;
+    base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * 16;
+    off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c & 1) * 8;
+    return c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+           (unsigned)gw < (unsigned)g.IW;
+  };
+  auto prefetch_halo = [&](int job) {
+    const int tile = t_begin + job / npass, p = job % npass;
+    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+    const int dlo = td_i * g.TD - g.pd, hlo = th_i * g.TH - g.ph;
+    const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * 16;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+    for (int i = 0; i < HC; ++i) {
+      const int c = i * 256 + tid;
+      const int info = posinfo[c < nchunk ? c >> 1 : 0];
+      const int gd = dlo + (info >> 20), gh = hlo + ((info >> 10) & 1023), gw = (info & 1023) - g.pw;
+      const bool ok = c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                      (unsigned)gw < (unsigned)g.IW;
+      const int off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c & 1) * 8;
+      const uint4 x = *(const uint4*)(base + (ok ? off : 0));
+      hreg[i] = ok ? x : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_halo = [&](int job) {
+#pragma unroll
+    for (int i = 0; i < HC; ++i) {
+      const int c = i * 256 + tid;
+      if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = hreg[i];
+    }
+    for (int c0 = HC * 256; c0 < nchunk; c0 += 4 * 256) {   // tail of a large halo: synchronous
+      uint4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16* base;
+        int off;
         const int c = c0 + j * 256 + tid;
-        const int pos = c >> 1, half = c & 1;
-        const int hw = pos % HW, hh = (pos / HW) % HH, hd = pos / (HW * HH);
-        const int gd = d0 - g.pd + hd, gh = h0 - g.ph + hh, gw = hw - g.pw;
-        const bool ok = c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-                        (unsigned)gw < (unsigned)g.IW;
-        const long long off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + p * 16 + half * 8;
-        const uint4 x = *(const uint4*)(src + (ok ? off : 0));
+        const bool ok = halo_src(job, c, base, off);
+        const uint4 x = *(const uint4*)(base + (ok ? off : 0));
         v[j] = ok ? x : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < 4; ++j) {
         const int c = c0 + j * 256 + tid;
         if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = v[j];
       }
     }
   };
 
-  uint4 rbv[B_PER_T];
-  auto load_b = [&](int q) {
-    const int kbase = q * H_BK;
+  uint4 rbA[B_PER_T], rbB[B_PER_T];
+  auto load_b = [&](int q, uint4* dst) {
+    const int kbase = (q % nq) * H_BK;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int idx = tid + i * 256;
@@ -124,17 +170,17 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
       const int k = kbase + (idx & 7) * 8;
       const bool ok = idx < B_CHUNKS && n0 + r < Ncol;
       const uint4 v = *(const uint4*)(wt + (ok ? (long long)(n0 + r) * ldw + k : 0));
-      rbv[i] = ok ? v : make_uint4(0, 0, 0, 0);
+      dst[i] = ok ? v : make_uint4(0, 0, 0, 0);
     }
   };
-  auto write_b = [&](int buf) {
+  auto write_b = [&](int buf, const uint4* srcr) {
     bf16* b = Bs + buf * B_STAGE;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int idx = tid + i * 256;
       if (idx < B_CHUNKS) {
         const int r = idx >> 3, c = idx & 7;
-        *(uint4*)(b + r * H_BK + ((c ^ (r & 7)) << 3)) = rbv[i];
+        *(uint4*)(b + r * H_BK + ((c ^ (r & 7)) << 3)) = srcr[i];
       }
     }
   };
@@ -145,113 +191,116 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  fill_halo(0);
-  load_b(0);
-  write_b(0);
-  __syncthreads();
+  prefetch_halo(0);
+  load_b(0, rbA);
+  write_b(0, rbA);
+  load_b(1, rbA);
+  load_b(2, rbB);
 
-  const int mt_live = rows - wave * 64;   // rows of this wave inside the tile (uniform)
-  for (int q = 0; q < nq; ++q) {
-    if (q > 0 && q % spp == 0) {          // next 16-channel slice (all reads of the last one are done)
-      fill_halo(q / spp);
+  const int mt_live = rows - wave * 64;   // rows of this wave inside a tile (uniform)
+  int s = 0;                              // global stage counter
+  for (int job = 0; job < njobs; ++job) {
+    __syncthreads();                      // previous halo / epilogue staging fully consumed
+    store_halo(job);
+    __syncthreads();
+    if (job + 1 < njobs) prefetch_halo(job + 1);   // lands during this job's MFMAs
+    for (int local = 0; local < spp; ++local, ++s) {
+      const bf16* b = Bs + (s & 1) * B_STAGE;
+      const int tap0 = local * 4;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int toff = taptab[tap0 + ks * 2 + (lg >> 1)];
+        bf16x8 fa[4], fb[NT];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          fa[mt] = *(const bf16x8*)(halo + (size_t)(hbase[mt] + toff) * 16 + (lg & 1) * 8);
+        const int ch = ks * 4 + lg;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const int row = nt * 16 + lr;
+          fb[nt] = *(const bf16x8*)(b + row * H_BK + ((ch ^ (row & 7)) << 3));
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          if (mt * 16 < mt_live) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+          }
+        }
+      }
+      write_b((s + 1) & 1, rbA);          // stage s+1 (its buffer's last readers passed the previous barrier)
+#pragma unroll
+      for (int i = 0; i < B_PER_T; ++i) rbA[i] = rbB[i];
+      load_b(s + 3, rbB);                 // two stages of latency cover
       __syncthreads();
     }
-    const bool more = q + 1 < nq;
-    if (more) load_b(q + 1);              // weight loads in flight during the MFMAs
-    const bf16* b = Bs + (q & 1) * B_STAGE;
-    const int tap0 = (q % spp) * 4;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int toff = taptab[tap0 + ks * 2 + (lg >> 1)];
-      bf16x8 fa[4], fb[NT];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        fa[mt] = *(const bf16x8*)(halo + (size_t)(hbase[mt] + toff) * 16 + (lg & 1) * 8);
-      const int ch = ks * 4 + lg;
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int row = nt * 16 + lr;
-        fb[nt] = *(const bf16x8*)(b + row * H_BK + ((ch ^ (row & 7)) << 3));
-      }
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        if (mt * 16 < mt_live) {
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
-        }
-      }
-    }
-    if (more) write_b((q + 1) & 1);       // the other buffer: its last readers passed the previous barrier
-    __syncthreads();
-  }
+    if (job % npass != npass - 1) continue;
 
-  // ---- epilogue (LDS staging reuses the halo region) ----
-  bf16* Os = reinterpret_cast<bf16*>(dsm);
-  float csum[NT], csq[NT];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) { csum[nt] = 0.f; csq[nt] = 0.f; }
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int col = nt * 16 + lr;
-    const bool cv = (n0 + col) < Ncol;
-    float bv = 0.f;
-    if constexpr (HAS_BIAS) bv = cv ? bias[n0 + col] : 0.f;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wave * 64 + mt * 16 + lg * 4 + r;
-        float v = act_fwd(acc[mt][nt][r] + bv, ACT);
-        const bf16 bvv = f2bf(v);
-        Os[row * LDO + col] = bvv;
-        if constexpr (STATS) {
-          bool rv = cv && row < rows;
-          if (rv) {
-            const int td = row / (g.OW * g.TH), th = (row / g.OW) % g.TH;
-            rv = d0 + td < g.OD && h0 + th < g.OH;
-          }
-          const float f = rv ? bf2f(bvv) : 0.f;
-          csum[nt] += f;
-          csq[nt] += f * f;
-        }
-      }
-    }
-  }
-  if constexpr (STATS) {
-    float* red = reinterpret_cast<float*>(dsm + (size_t)H_BM * LDO * 2);
+    // ---- epilogue of a finished tile (staging in the halo region) ----
+    const int tile = t_begin + job / npass;
+    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+    const int d0 = td_i * g.TD, h0 = th_i * g.TH;
+    bf16* Os = reinterpret_cast<bf16*>(dsm);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      float s = csum[nt], qq = csq[nt];
-      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-      qq += __shfl_xor(qq, 16, 64); qq += __shfl_xor(qq, 32, 64);
-      if (lg == 0) { red[(wave * 2 + 0) * BN + nt * 16 + lr] = s; red[(wave * 2 + 1) * BN + nt * 16 + lr] = qq; }
+      const int col = nt * 16 + lr;
+      float bv = 0.f;
+      if constexpr (HAS_BIAS) bv = (n0 + col) < Ncol ? bias[n0 + col] : 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wave * 64 + mt * 16 + lg * 4 + r;
+          Os[row * LDO + col] = f2bf(act_fwd(acc[mt][nt][r] + bv, ACT));
+        }
+        acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    if constexpr (STATS) {
+      // BN partial sums over the valid rows of the staged (bf16-rounded) tile
+      constexpr int NPART = 256 / BN;
+      float* red = reinterpret_cast<float*>(dsm + (size_t)H_BM * LDO * 2);
+      __syncthreads();
+      const int col = tid % BN, part = tid / BN;
+      float sm = 0.f, qq = 0.f;
+      for (int row = part; row < rows; row += NPART) {
+        const int td = row / (g.OW * g.TH), th = (row / g.OW) % g.TH;
+        if (d0 + td < g.OD && h0 + th < g.OH) {
+          const float f = bf2f(Os[row * LDO + col]);
+          sm += f;
+          qq += f * f;
+        }
+      }
+      red[part * 2 * BN + col] = sm;
+      red[part * 2 * BN + BN + col] = qq;
+      __syncthreads();
+      if (tid < BN && n0 + tid < Ncol) {
+        float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+        for (int q2 = 0; q2 < NPART; ++q2) { a0 += red[q2 * 2 * BN + tid]; a1 += red[q2 * 2 * BN + BN + tid]; }
+        stats[(long long)tile * 2 * Ncol + n0 + tid] = a0;
+        stats[(long long)tile * 2 * Ncol + Ncol + n0 + tid] = a1;
+      }
     }
     __syncthreads();
-    if (tid < BN && n0 + tid < Ncol) {
-      const float s = red[0 * BN + tid] + red[2 * BN + tid] + red[4 * BN + tid] + red[6 * BN + tid];
-      const float qq = red[1 * BN + tid] + red[3 * BN + tid] + red[5 * BN + tid] + red[7 * BN + tid];
-      stats[(long long)tile * 2 * Ncol + n0 + tid] = s;
-      stats[(long long)tile * 2 * Ncol + Ncol + n0 + tid] = qq;
-    }
-  }
-  __syncthreads();
-  constexpr int CPR = BN / 8;
-  const bool vec_out = (Ncol % 8) == 0;
+    constexpr int CPR = BN / 8;
+    const bool vec_out = (Ncol % 8) == 0;
 #pragma unroll
-  for (int i = 0; i < CPR; ++i) {
-    const int idx = tid + i * 256;
-    const int row = idx / CPR, ch = idx % CPR;
-    if (row >= rows) continue;
-    const int w = row % g.OW, th = (row / g.OW) % g.TH, td = row / (g.OW * g.TH);
-    if (d0 + td >= g.OD || h0 + th >= g.OH) continue;
-    const long long m = (((long long)n * g.OD + d0 + td) * g.OH + h0 + th) * g.OW + w;
-    const int col = n0 + ch * 8;
-    if (vec_out && col + 8 <= Ncol) {
-      *(uint4*)(out + m * Ncol + col) = *(const uint4*)(Os + row * LDO + ch * 8);
-    } else {
-      for (int j = 0; j < 8; ++j)
-        if (col + j < Ncol) out[m * Ncol + col + j] = Os[row * LDO + ch * 8 + j];
+    for (int i = 0; i < CPR; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / CPR, ch = idx % CPR;
+      if (row >= rows) continue;
+      const int w = row % g.OW, th = (row / g.OW) % g.TH, td = row / (g.OW * g.TH);
+      if (d0 + td >= g.OD || h0 + th >= g.OH) continue;
+      const long long m = (((long long)n * g.OD + d0 + td) * g.OH + h0 + th) * g.OW + w;
+      const int col = n0 + ch * 8;
+      if (vec_out && col + 8 <= Ncol) {
+        *(uint4*)(out + m * Ncol + col) = *(const uint4*)(Os + row * LDO + ch * 8);
+      } else {
+        for (int j = 0; j < 8; ++j)
+          if (col + j < Ncol) out[m * Ncol + col + j] = Os[row * LDO + ch * 8 + j];
+      }
     }
   }
 }
@@ -415,17 +464,22 @@ static HaloGeom parse_halo(const int* v) {
   return g;
 }
 
-static size_t halo_lds_bytes(const HaloGeom& g, int BN) {
+static size_t halo_region_bytes(const HaloGeom& g, int BN) {
   const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  const size_t epi = (size_t)H_BM * (BN + 8) * 2 + 2 * 256 * 4;
+  const size_t r = hp * 32 > epi ? hp * 32 : epi;
+  return (r + 15) & ~(size_t)15;
+}
+
+static size_t halo_lds_bytes(const HaloGeom& g, int BN) {
   const int T4 = (g.KD * g.KH * g.KW + 3) & ~3;
-  const size_t main_ = hp * 32 + 2 * (size_t)BN * H_BK * 2;
-  const size_t epi = (size_t)H_BM * (BN + 8) * 2 + 16 * (size_t)BN * 4;
-  return (main_ > epi ? main_ : epi) + (size_t)T4 * 4 + 16;
+  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  return halo_region_bytes(g, BN) + 2 * (size_t)BN * H_BK * 2 + (size_t)T4 * 4 + hp * 4 + 16;
 }
 
 template <int BN, int ACT, bool HB, bool ST>
-static int launch_halo(dim3 grid, size_t lds, hipStream_t st, const bf16* s, const bf16* w, const float* b, bf16* o,
-                       float* stats, const HaloGeom& g, int Ncol) {
+static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const bf16* s, const bf16* w,
+                       const float* b, bf16* o, float* stats, const HaloGeom& g, int Ncol) {
   static size_t configured = 0;
   if (lds > configured) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_halo_kernel<BN, ACT, HB, ST>,
@@ -433,9 +487,12 @@ static int launch_halo(dim3 grid, size_t lds, hipStream_t st, const bf16* s, con
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST>), grid, dim3(256), lds, st, s, w, b, o, stats, g, Ncol);
+  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST>), grid, dim3(256), lds, st, s, w, b, o, stats, g, Ncol,
+                     region);
   return 0;
 }
+
+static int g_num_cus = 0;
 
 // wt: [Ncol][C/16][T4][16] bf16 (tap-padded); returns 0 on success.
 extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, void* out, float* stats,
@@ -445,15 +502,26 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   if (stats && act != ACT_NONE) return -1;
   const int BN = Ncol <= 32 ? 32 : 64;
   const size_t lds = halo_lds_bytes(g, BN);
+  const int region = (int)halo_region_bytes(g, BN);
   if (lds > 160 * 1024) return -4;
-  const int tiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
-  dim3 grid((unsigned)tiles, (Ncol + BN - 1) / BN);
+  if (g_num_cus == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
+  const int ncb = (Ncol + BN - 1) / BN;
+  const int per_cu = (int)((160 * 1024) / lds) < 2 ? 1 : 2;
+  int workers = (g_num_cus * per_cu + ncb - 1) / ncb;
+  if (workers > ntiles) workers = ntiles;
+  dim3 grid((unsigned)workers, ncb);
   const bf16* s = (const bf16*)src;
   const bf16* w = (const bf16*)wt;
   bf16* o = (bf16*)out;
   const bool hb = bias != nullptr;
   int rc;
-#define HCASE(B, A, H, S) rc = launch_halo<B, A, H, S>(grid, lds, st, s, w, bias, o, stats, g, Ncol)
+#define HCASE(B, A, H, S) rc = launch_halo<B, A, H, S>(grid, lds, region, st, s, w, bias, o, stats, g, Ncol)
 #define HBN(B)                                                   \
   do {                                                           \
     if (stats) HCASE(B, ACT_NONE, false, true);                  \

@@ -408,13 +408,59 @@ def conv(x5: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, spec: ConvSp
     return (y, None) if want_stats else y
 
 
+def _dw_geom(spec: ConvSpec) -> list[int]:
+    return [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
+            spec.sd, spec.sh, spec.sw, spec.pd, spec.ph, spec.pw, spec.dd, spec.dh, spec.dw]
+
+
+class DepthwiseFn(torch.autograd.Function):
+    """Depthwise conv (multiplier 1) on ``dwconv.hip``: y = act(dwconv(x, w) + b)."""
+
+    @staticmethod
+    def forward(ctx, x5, w, b, spec: ConvSpec, act: int):
+        K = _native.kernels()
+        x5 = x5.contiguous()
+        wf = w.detach().float().reshape(spec.C, spec.taps).contiguous()
+        bias = b.detach().float().contiguous() if b is not None else None
+        y = torch.empty(spec.N, spec.OD, spec.OH, spec.OW, spec.C, dtype=torch.bfloat16, device=x5.device)
+        K.dw_fwd(x5.data_ptr(), wf.data_ptr(), _native.ptr(bias), y.data_ptr(), _dw_geom(spec), act,
+                 _native.stream(x5))
+        ctx.spec, ctx.act, ctx.has_b = spec, act, b is not None
+        ctx.save_for_backward(x5, wf, y if act else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x5, wf, y = ctx.saved_tensors
+        spec, act = ctx.spec, ctx.act
+        K = _native.kernels()
+        st = _native.stream(x5)
+        dy = dy.contiguous().to(torch.bfloat16)
+        if act:
+            dy = native_act_bwd(dy, y, act)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x5)
+            K.dw_dgrad(dy.data_ptr(), wf.data_ptr(), dx.data_ptr(), _dw_geom(spec), st)
+        if ctx.needs_input_grad[1]:
+            dwf = torch.zeros(spec.C, spec.taps, dtype=torch.float32, device=x5.device)
+            splits = int(max(1, min(256, spec.M // 2048)))
+            K.dw_wgrad(dy.data_ptr(), x5.data_ptr(), dwf.data_ptr(), _dw_geom(spec), splits, st)
+            dw = dwf.reshape(spec.C, spec.KD, spec.KH, spec.KW, 1)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = native_colsum(dy.reshape(-1, spec.C))
+        return dx, dw, db, None, None
+
+
 def depthwise_conv(x5: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, spec: ConvSpec, mult: int = 1,
                    act=None) -> torch.Tensor:
-    """Depthwise conv (reference ``DepthwiseConv2D`` / first half of ``SeparableConv2D``).
-
-    Runs through the reference implementation on both devices for now (grouped
-    conv); the search-space shapes are small 2-D images.
+    """Depthwise conv (reference ``DepthwiseConv2D`` / first half of ``SeparableConv2D``,
+    ``model/input.py:296-306``): native ``dwconv.hip`` on GPU for depth multiplier 1
+    (the only multiplier the reference search space produces); the PyTorch
+    reference handles the CPU path and multipliers > 1.
     """
+    if _native.use_native(x5) and mult == 1:
+        return DepthwiseFn.apply(x5.to(torch.bfloat16), w, b, spec, act_code(act))
     dt = x5.dtype
     y = ref.depthwise_conv(x5.float() if x5.is_cuda else x5, w.float() if x5.is_cuda else w.to(dt),
                            None if b is None else (b.float() if x5.is_cuda else b.to(dt)), spec, mult, act)

@@ -267,7 +267,7 @@ HALO_CASES = [
     (2, 29, 29, 29, 32, 32, (5, 5, 5), "valid", 0),
     (2, 25, 25, 25, 32, 64, (4, 4, 4), "valid", 0),
     (2, 22, 22, 22, 64, 64, (3, 3, 3), "valid", 0),
-    (3, 7, 9, 12, 16, 40, (3, 3, 3), "same", 1),
+    (3, 7, 9, 12, 16, 48, (3, 3, 3), "same", 1),
     (2, 1, 31, 33, 32, 96, (1, 3, 3), "same", 2),
 ]
 
@@ -276,7 +276,9 @@ HALO_CASES = [
 def test_conv_halo_fwd_dgrad_stats(case):
     """LDS-halo kernel (conv_halo.hip): forward (+bias/act), BN-stats epilogue and dgrad."""
     _native_loaded()
-    from featurenet_amd.ops import conv as C
+    import importlib
+
+    C = importlib.import_module("featurenet_amd.ops.conv")
 
     N, D, H, W, Ci, K, k, pad, act = case
     torch.manual_seed(3)
@@ -305,3 +307,37 @@ def test_conv_halo_fwd_dgrad_stats(case):
     if C.halo_wgrad_plan(spec) is not None:
         dw = C.halo_conv_wgrad(g, x, spec, C.halo_wgrad_plan(spec))
         close(dw, wr.grad)
+
+
+DW_CASES = [
+    # (N, D, H, W, C, kernel, stride, padding, act)
+    (4, 1, 16, 16, 16, (1, 3, 3), 1, "same", "relu"),
+    (2, 1, 15, 13, 3, (1, 5, 5), 2, "same", None),
+    (2, 6, 7, 8, 8, (3, 3, 3), 1, "valid", "tanh"),
+]
+
+
+@pytest.mark.parametrize("case", DW_CASES)
+def test_depthwise_fwd_bwd(case):
+    """Depthwise kernels (dwconv.hip) vs the grouped-conv fp32 reference."""
+    _native_loaded()
+    from featurenet_amd.ops.conv import DepthwiseFn
+    from featurenet_amd.ops.spec import act_code
+
+    N, D, H, W, C, k, s, pad, act = case
+    torch.manual_seed(5)
+    x = torch.randn(N, D, H, W, C, device="cuda").to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, C, k, s, pad)
+    w = (torch.randn(C, spec.KD, spec.KH, spec.KW, 1, device="cuda") * 0.2).to(torch.bfloat16).float()
+    b = torch.randn(C, device="cuda") * 0.1
+    xr, wr, br = (t.float().clone().requires_grad_(True) for t in (x, w, b))
+    yr = ref.depthwise_conv(xr, wr, br, spec, 1, act)
+    xn, wn, bn = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yn = DepthwiseFn.apply(xn, wn, bn, spec, act_code(act))
+    close(yn, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(g)
+    yn.backward(g.to(torch.bfloat16))
+    close(xn.grad, xr.grad)
+    close(wn.grad, wr.grad)
+    close(bn.grad, br.grad)
