@@ -33,11 +33,13 @@ struct HaloGeom {
 
 #define H_BM 256
 #define H_BK 64
+#define H_BKS 128   // weight-stage depth of the forward halo kernel
 
 // 16-B halo chunks per thread prefetched in registers (the rest of a larger
 // halo is loaded synchronously at the job boundary); BN=64 keeps 64 VGPRs of
 // accumulators, so it prefetches fewer.
-#define H_HC(BN) ((BN) == 32 ? 16 : 7)
+#define H_HC(BN) ((BN) == 32 ? 2 : 0)
+#define H_NTHR 512   // 8 waves: 4 row blocks x 2-way split of every weight stage's k-steps
 
 // Persistent form: each workgroup owns a contiguous run of output tiles
 // (adjacent tiles share halo rows -> same XCD L2) and walks the sequence of
@@ -46,36 +48,42 @@ struct HaloGeom {
 // weight stages are prefetched two stages ahead, so neither halo nor weight
 // latency sits on the critical path.
 template <int BN, int ACT, bool HAS_BIAS, bool STATS>
-__global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wt,
+__global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wt,
                                                            const float* __restrict__ bias, bf16* __restrict__ out,
-                                                           float* __restrict__ stats, HaloGeom g, int Ncol,
-                                                           int region_bytes) {
+                                                           float* __restrict__ stats, const int* __restrict__ toffs,
+                                                           HaloGeom g, int Ncol, int region_bytes) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  constexpr int NT = BN / 16;
-  constexpr int B_STAGE = BN * H_BK;             // elements
-  constexpr int B_CHUNKS = BN * (H_BK / 8);
-  constexpr int B_PER_T = (B_CHUNKS + 255) / 256;
+  // 8 waves = 4 row blocks x 2: BN=32 splits every stage's 4 k-steps between
+  // the two waves of a row block (partials reduced per tile); BN=64 gives each
+  // of them 32 of the 64 columns.  Either way a wave owns 64 rows x 32 cols.
+  constexpr bool KSPLIT = BN == 32;
+  constexpr int NT = 2;
+  constexpr int B_STAGE = BN * H_BKS;            // elements (128 k = 8 taps x 16 channels)
+  constexpr int B_CHUNKS = BN * (H_BKS / 8);
+  constexpr int B_PER_T = (B_CHUNKS + H_NTHR - 1) / H_NTHR;
   constexpr int LDO = BN + 8;
 
   const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
   const int HP = HD * HH * HW;                   // halo positions
   const int nchunk = HP * 2;
   const int T = g.KD * g.KH * g.KW;
-  const int T4 = (T + 3) & ~3;
-  const int spp = T4 >> 2;                       // 64-k stages per channel pass
+  const int T8 = (T + 7) & ~7;
+  const int spp = T8 >> 3;                       // 128-k stages per channel pass
   const int npass = g.C >> 4;
   const int nq = spp * npass;
-  const int ldw = npass * T4 * 16;
+  const int ldw = npass * T8 * 16;
   const int rows = g.TD * g.TH * g.OW;
   const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
   const int ntiles = g.N * tdn * thn;
 
   bf16* halo = reinterpret_cast<bf16*>(dsm);                      // also the epilogue staging area
   bf16* Bs = reinterpret_cast<bf16*>(dsm + region_bytes);
-  int* taptab = reinterpret_cast<int*>(dsm + region_bytes + 2 * B_STAGE * 2);
-  int* posinfo = taptab + T4;                    // packed (hd, hh, hw) of every halo position
+  int* posinfo = reinterpret_cast<int*>(dsm + region_bytes + 2 * B_STAGE * 2);  // packed (hd, hh, hw)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wrow = wave & 3;                                   // 64-row block of the tile
+  const int khalf = __builtin_amdgcn_readfirstlane(wave >> 2);   // k-half (BN=32) or column half (BN=64)
+  const int ccol = KSPLIT ? 0 : khalf * 32;                      // this wave's first column
   const int lr = lane & 15, lg = lane >> 4;
   const int worker = xcd_remap(blockIdx.x, gridDim.x);
   const int per = (ntiles + gridDim.x - 1) / gridDim.x;
@@ -85,20 +93,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
   const int njobs = (t_end - t_begin) * npass;
   const int n0 = blockIdx.y * BN;
 
-  for (int t = tid; t < T4; t += 256) {
-    int off = 0;
-    if (t < T) {
-      const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
-      off = (kd * HH + kh) * HW + kw;
-    }
-    taptab[t] = off;
-  }
-  for (int pos = tid; pos < HP; pos += 256)
+  for (int pos = tid; pos < HP; pos += H_NTHR)
     posinfo[pos] = ((pos / (HW * HH)) << 20) | (((pos / HW) % HH) << 10) | (pos % HW);
   int hbase[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
-    const int r = wave * 64 + mt * 16 + lr;
+    const int r = wrow * 64 + mt * 16 + lr;
     const int rr = r < rows ? r : 0;
     const int w = rr % g.OW, th = (rr / g.OW) % g.TH, td = rr / (g.OW * g.TH);
     hbase[mt] = (td * HH + th) * HW + w;
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
   __syncthreads();
 
   constexpr int HC = H_HC(BN);
-  uint4 hreg[HC];
+  uint4 hreg[HC > 0 ? HC : 1];
   auto halo_src = [&](int job, int c, const bf16*& base, int& off) -> bool {
     const int tile = t_begin + job / npass, p = job % npass;
     const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
     const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * 16;
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
-      const int c = i * 256 + tid;
+      const int c = i * H_NTHR + tid;
       const int info = posinfo[c < nchunk ? c >> 1 : 0];
       const int gd = dlo + (info >> 20), gh = hlo + ((info >> 10) & 1023), gw = (info & 1023) - g.pw;
       const bool ok = c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
@@ -138,36 +138,36 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
   auto store_halo = [&](int job) {
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
-      const int c = i * 256 + tid;
+      const int c = i * H_NTHR + tid;
       if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = hreg[i];
     }
-    for (int c0 = HC * 256; c0 < nchunk; c0 += 4 * 256) {   // tail of a large halo: synchronous
+    for (int c0 = HC * H_NTHR; c0 < nchunk; c0 += 4 * H_NTHR) {   // tail of a large halo: synchronous
       uint4 v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bf16* base;
         int off;
-        const int c = c0 + j * 256 + tid;
+        const int c = c0 + j * H_NTHR + tid;
         const bool ok = halo_src(job, c, base, off);
         const uint4 x = *(const uint4*)(base + (ok ? off : 0));
         v[j] = ok ? x : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = c0 + j * 256 + tid;
+        const int c = c0 + j * H_NTHR + tid;
         if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = v[j];
       }
     }
   };
 
-  uint4 rbA[B_PER_T], rbB[B_PER_T];
+  uint4 rbA[B_PER_T];
   auto load_b = [&](int q, uint4* dst) {
-    const int kbase = (q % nq) * H_BK;
+    const int kbase = (q % nq) * H_BKS;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
-      const int idx = tid + i * 256;
-      const int r = (idx >> 3) < BN ? (idx >> 3) : BN - 1;
-      const int k = kbase + (idx & 7) * 8;
+      const int idx = tid + i * H_NTHR;
+      const int r = (idx >> 4) < BN ? (idx >> 4) : BN - 1;
+      const int k = kbase + (idx & 15) * 8;
       const bool ok = idx < B_CHUNKS && n0 + r < Ncol;
       const uint4 v = *(const uint4*)(wt + (ok ? (long long)(n0 + r) * ldw + k : 0));
       dst[i] = ok ? v : make_uint4(0, 0, 0, 0);
@@ -177,10 +177,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
     bf16* b = Bs + buf * B_STAGE;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
-      const int idx = tid + i * 256;
+      const int idx = tid + i * H_NTHR;
       if (idx < B_CHUNKS) {
-        const int r = idx >> 3, c = idx & 7;
-        *(uint4*)(b + r * H_BK + ((c ^ (r & 7)) << 3)) = srcr[i];
+        const int r = idx >> 4, c = idx & 15;
+        *(uint4*)(b + r * H_BKS + ((c ^ (r & 15)) << 3)) = srcr[i];
       }
     }
   };
@@ -195,9 +195,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
   load_b(0, rbA);
   write_b(0, rbA);
   load_b(1, rbA);
-  load_b(2, rbB);
 
-  const int mt_live = rows - wave * 64;   // rows of this wave inside a tile (uniform)
+  const int mt_live = rows - wrow * 64;   // rows of this wave inside a tile (uniform)
   int s = 0;                              // global stage counter
   for (int job = 0; job < njobs; ++job) {
     __syncthreads();                      // previous halo / epilogue staging fully consumed
@@ -206,10 +205,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
     if (job + 1 < njobs) prefetch_halo(job + 1);   // lands during this job's MFMAs
     for (int local = 0; local < spp; ++local, ++s) {
       const bf16* b = Bs + (s & 1) * B_STAGE;
-      const int tap0 = local * 4;
+      const int* tp = toffs + local * 8 + (KSPLIT ? khalf * 4 : 0);  // uniform -> scalar loads
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int toff = taptab[tap0 + ks * 2 + (lg >> 1)];
+      for (int kk = 0; kk < (KSPLIT ? 2 : 4); ++kk) {
+        const int ks = (KSPLIT ? khalf * 2 : 0) + kk;
+        const int t0 = tp[kk * 2], t1 = tp[kk * 2 + 1];
+        const int toff = (lg & 2) ? t1 : t0;
         bf16x8 fa[4], fb[NT];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
@@ -217,8 +218,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
         const int ch = ks * 4 + lg;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
-          const int row = nt * 16 + lr;
-          fb[nt] = *(const bf16x8*)(b + row * H_BK + ((ch ^ (row & 7)) << 3));
+          const int row = ccol + nt * 16 + lr;
+          fb[nt] = *(const bf16x8*)(b + row * H_BKS + ((ch ^ (row & 15)) << 3));
         }
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
@@ -230,9 +231,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
         }
       }
       write_b((s + 1) & 1, rbA);          // stage s+1 (its buffer's last readers passed the previous barrier)
-#pragma unroll
-      for (int i = 0; i < B_PER_T; ++i) rbA[i] = rbB[i];
-      load_b(s + 3, rbB);                 // two stages of latency cover
+      load_b(s + 2, rbA);                 // a whole stage of MFMAs covers its latency
       __syncthreads();
     }
     if (job % npass != npass - 1) continue;
@@ -241,25 +240,53 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
     const int tile = t_begin + job / npass;
     const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
     const int d0 = td_i * g.TD, h0 = th_i * g.TH;
+    // split-K reduction: the khalf=1 wave of each row block hands its partial
+    // sums to its khalf=0 partner through LDS (lane-major, conflict-free)
+    if constexpr (KSPLIT) {
+      float* part = reinterpret_cast<float*>(dsm);
+      {
+        float* slot = part + (size_t)wrow * (4 * NT * 4 * 64);
+        if (khalf == 1) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) slot[((mt * NT + nt) * 4 + r) * 64 + lane] = acc[mt][nt][r];
+        }
+        __syncthreads();
+        if (khalf == 0) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[mt][nt][r] += slot[((mt * NT + nt) * 4 + r) * 64 + lane];
+        }
+        __syncthreads();
+      }
+    }
     bf16* Os = reinterpret_cast<bf16*>(dsm);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const int col = nt * 16 + lr;
+      const int col = ccol + nt * 16 + lr;
       float bv = 0.f;
       if constexpr (HAS_BIAS) bv = (n0 + col) < Ncol ? bias[n0 + col] : 0.f;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
+        if (!KSPLIT || khalf == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wave * 64 + mt * 16 + lg * 4 + r;
-          Os[row * LDO + col] = f2bf(act_fwd(acc[mt][nt][r] + bv, ACT));
+          for (int r = 0; r < 4; ++r) {
+            const int row = wrow * 64 + mt * 16 + lg * 4 + r;
+            Os[row * LDO + col] = f2bf(act_fwd(acc[mt][nt][r] + bv, ACT));
+          }
         }
         acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
       }
     }
     if constexpr (STATS) {
       // BN partial sums over the valid rows of the staged (bf16-rounded) tile
-      constexpr int NPART = 256 / BN;
+      constexpr int NPART = H_NTHR / BN;
       float* red = reinterpret_cast<float*>(dsm + (size_t)H_BM * LDO * 2);
       __syncthreads();
       const int col = tid % BN, part = tid / BN;
@@ -287,8 +314,8 @@ __global__ __launch_bounds__(256, 2) void conv_halo_kernel(const bf16* __restric
     constexpr int CPR = BN / 8;
     const bool vec_out = (Ncol % 8) == 0;
 #pragma unroll
-    for (int i = 0; i < CPR; ++i) {
-      const int idx = tid + i * 256;
+    for (int i = 0; i < (H_BM * CPR + H_NTHR - 1) / H_NTHR; ++i) {
+      const int idx = tid + i * H_NTHR;
       const int row = idx / CPR, ch = idx % CPR;
       if (row >= rows) continue;
       const int w = row % g.OW, th = (row / g.OW) % g.TH, td = row / (g.OW * g.TH);
@@ -466,20 +493,20 @@ static HaloGeom parse_halo(const int* v) {
 
 static size_t halo_region_bytes(const HaloGeom& g, int BN) {
   const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
-  const size_t epi = (size_t)H_BM * (BN + 8) * 2 + 2 * 256 * 4;
+  size_t epi = (size_t)H_BM * (BN + 8) * 2 + 2 * H_NTHR * 4;
+  if (epi < 32 * 1024) epi = 32 * 1024;          // split-K partial sums (one round)
   const size_t r = hp * 32 > epi ? hp * 32 : epi;
   return (r + 15) & ~(size_t)15;
 }
 
 static size_t halo_lds_bytes(const HaloGeom& g, int BN) {
-  const int T4 = (g.KD * g.KH * g.KW + 3) & ~3;
   const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
-  return halo_region_bytes(g, BN) + 2 * (size_t)BN * H_BK * 2 + (size_t)T4 * 4 + hp * 4 + 16;
+  return halo_region_bytes(g, BN) + 2 * (size_t)BN * H_BKS * 2 + hp * 4 + 16;
 }
 
 template <int BN, int ACT, bool HB, bool ST>
 static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const bf16* s, const bf16* w,
-                       const float* b, bf16* o, float* stats, const HaloGeom& g, int Ncol) {
+                       const float* b, bf16* o, float* stats, const int* toffs, const HaloGeom& g, int Ncol) {
   static size_t configured = 0;
   if (lds > configured) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_halo_kernel<BN, ACT, HB, ST>,
@@ -487,16 +514,17 @@ static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const 
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST>), grid, dim3(256), lds, st, s, w, b, o, stats, g, Ncol,
-                     region);
+  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST>), grid, dim3(H_NTHR), lds, st, s, w, b, o, stats, toffs, g,
+                     Ncol, region);
   return 0;
 }
 
 static int g_num_cus = 0;
 
-// wt: [Ncol][C/16][T4][16] bf16 (tap-padded); returns 0 on success.
+// wt: [Ncol][C/16][T8][16] bf16 (taps padded to a multiple of 8); toffs: int [T8] halo
+// position offsets of the taps (0 for padding taps); returns 0 on success.
 extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, void* out, float* stats,
-                            const int* geom16, int Ncol, int act, hipStream_t st) {
+                            const int* toffs, const int* geom16, int Ncol, int act, hipStream_t st) {
   const HaloGeom g = parse_halo(geom16);
   if (g.C % 16 != 0 || g.TD * g.TH * g.OW > H_BM || g.TD < 1 || g.TH < 1) return -2;
   if (stats && act != ACT_NONE) return -1;
@@ -521,7 +549,7 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   bf16* o = (bf16*)out;
   const bool hb = bias != nullptr;
   int rc;
-#define HCASE(B, A, H, S) rc = launch_halo<B, A, H, S>(grid, lds, region, st, s, w, bias, o, stats, g, Ncol)
+#define HCASE(B, A, H, S) rc = launch_halo<B, A, H, S>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol)
 #define HBN(B)                                                   \
   do {                                                           \
     if (stats) HCASE(B, ACT_NONE, false, true);                  \

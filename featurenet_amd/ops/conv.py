@@ -154,14 +154,24 @@ def _pack_rows(mat: torch.Tensor) -> tuple[torch.Tensor, int]:
 # ---------------------------------------------------------------------------
 # LDS-halo path (stride-1 convs)
 # ---------------------------------------------------------------------------
-HALO_MAX_BYTES = 72 * 1024
+LDS_BUDGET = 80 * 1024      # two workgroups per CU (160 KiB LDS)
 _PLAN_CACHE: dict = {}
 
 
-def halo_plan(OD: int, OH: int, OW: int, KD: int, KH: int, KW: int):
+def _fwd_halo_budget(ncol: int) -> int:
+    bn = 32 if ncol <= 32 else 64
+    return int((LDS_BUDGET - 2 * bn * 128 * 2 - 1024) / 1.125)     # + 4 B/position decode table
+
+
+def _wgrad_halo_budget(cout: int) -> int:
+    mt = (cout + 15) // 16
+    return LDS_BUDGET - 256 * (16 * mt + 16) * 2 - 2048
+
+
+def halo_plan(OD: int, OH: int, OW: int, KD: int, KH: int, KW: int, max_bytes: int = 56 * 1024):
     """Output tile (TD, TH) x full OW maximising MFMA row utilisation with the
-    16-channel input halo <= HALO_MAX_BYTES; None when no tile fits."""
-    key = (OD, OH, OW, KD, KH, KW)
+    16-channel input halo <= max_bytes; None when no tile fits."""
+    key = (OD, OH, OW, KD, KH, KW, max_bytes)
     if key in _PLAN_CACHE:
         return _PLAN_CACHE[key]
     best, best_score = None, -1.0
@@ -172,7 +182,7 @@ def halo_plan(OD: int, OH: int, OW: int, KD: int, KH: int, KW: int):
                 if rows > 256:
                     break
                 halo = (TD + KD - 1) * (TH + KH - 1) * (OW + KW - 1) * 32
-                if halo > HALO_MAX_BYTES:
+                if halo > max_bytes:
                     continue
                 tiles = math.ceil(OD / TD) * math.ceil(OH / TH)
                 score = OD * OH * OW / (tiles * 256.0) - 1e-9 * halo
@@ -191,7 +201,7 @@ def halo_fwd_plan(spec: ConvSpec):
         return None
     if spec.C % 16 or spec.K < 16 or spec.taps < 8:
         return None
-    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW)
+    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, _fwd_halo_budget(spec.K))
 
 
 def halo_dgrad_plan(spec: ConvSpec):
@@ -199,17 +209,37 @@ def halo_dgrad_plan(spec: ConvSpec):
         return None
     if spec.K % 16 or spec.C < 16 or spec.taps < 8:
         return None
-    return halo_plan(spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW)
+    return halo_plan(spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW, _fwd_halo_budget(spec.C))
 
 
 def halo_weights(w3: torch.Tensor) -> torch.Tensor:
-    """[Ncol, T, Csrc] -> bf16 [Ncol, Csrc/16 * T4 * 16] in the halo kernel's k order
-    (16-channel slice, tap padded to a multiple of 4, 16 channels)."""
+    """[Ncol, T, Csrc] -> bf16 [Ncol, Csrc/16 * T8 * 16] in the halo kernel's k order
+    (16-channel slice, tap padded to a multiple of 8, 16 channels)."""
     n, T, c = w3.shape
-    T4 = (T + 3) // 4 * 4
-    out = torch.zeros(n, c // 16, T4, 16, dtype=torch.bfloat16, device=w3.device)
+    T8 = (T + 7) // 8 * 8
+    out = torch.zeros(n, c // 16, T8, 16, dtype=torch.bfloat16, device=w3.device)
     out[:, :, :T] = w3.reshape(n, T, c // 16, 16).permute(0, 2, 1, 3)
     return out.reshape(n, -1)
+
+
+_TOFF_CACHE: dict = {}
+
+
+def halo_tap_offsets(geom: list, device) -> torch.Tensor:
+    """int32 [T8]: halo-position offset of every tap for a (kernel, tile) geometry."""
+    key = (tuple(geom[5:]), str(device))
+    t = _TOFF_CACHE.get(key)
+    if t is None:
+        OW, KD, KH, KW, TD, TH = geom[7], geom[8], geom[9], geom[10], geom[14], geom[15]
+        HH, HW = TH + KH - 1, OW + KW - 1
+        T = KD * KH * KW
+        offs = np.zeros((T + 7) // 8 * 8, dtype=np.int32)
+        kd, kh, kw = np.meshgrid(np.arange(KD), np.arange(KH), np.arange(KW), indexing="ij")
+        offs[:T] = ((kd * HH + kh) * HW + kw).reshape(-1)
+        t = torch.from_numpy(offs).to(device)
+        with _TAB_LOCK:
+            _TOFF_CACHE[key] = t
+    return t
 
 
 def halo_wgrad_plan(spec: ConvSpec):
@@ -217,7 +247,7 @@ def halo_wgrad_plan(spec: ConvSpec):
         return None
     if spec.C % 16 or spec.K % 8 or spec.K > 64 or spec.taps < 8:
         return None
-    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW)
+    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, _wgrad_halo_budget(spec.K))
 
 
 def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> torch.Tensor:
@@ -238,8 +268,9 @@ def _halo_call(src5, wmat, bias, out, stats, geom, ncol, act):
     K = _native.kernels()
     if act and bias is None:
         bias = torch.zeros(ncol, dtype=torch.float32, device=src5.device)
-    K.conv_halo(src5.data_ptr(), wmat.data_ptr(), _native.ptr(bias), out.data_ptr(), _native.ptr(stats), geom,
-                ncol, act, _native.stream(src5))
+    toffs = halo_tap_offsets(geom, src5.device)
+    K.conv_halo(src5.data_ptr(), wmat.data_ptr(), _native.ptr(bias), out.data_ptr(), _native.ptr(stats),
+                toffs.data_ptr(), geom, ncol, act, _native.stream(src5))
 
 
 def halo_conv_fwd(x5, w, bias, spec: ConvSpec, act: int, want_stats: bool, plan):
