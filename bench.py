@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches resident on device")
     ap.add_argument("--tiny", action="store_true", help="16^3 2-class plumbing config (not the headline)")
+    ap.add_argument("--model", choices=["cls", "seg"], default="cls",
+                    help="cls = FeatureNet-3D classifier (headline); seg = per-voxel segmentation head "
+                         "(BASELINE config 4, 25 voxel classes)")
     ap.add_argument("--torch-layout", choices=["ndhwc", "ncdhw"], default="ndhwc",
                     help="memory format of the stock-PyTorch baseline (--impl torch)")
     return ap.parse_args()
@@ -76,7 +79,11 @@ def main():
     B, S, NC = args.batch, args.size, args.classes
     # synthetic 64^3 occupancy grids (~30% filled) + random labels, device resident
     xs = [(torch.rand(B, S, S, S, 1, device=dev) < 0.3).to(torch.bfloat16) for _ in range(args.pool)]
-    ys = [torch.randint(0, NC, (B,), device=dev) for _ in range(args.pool)]
+    if args.model == "seg":
+        NC = 25
+        ys = [torch.randint(0, NC, (B, S, S, S), device=dev) for _ in range(args.pool)]
+    else:
+        ys = [torch.randint(0, NC, (B,), device=dev) for _ in range(args.pool)]
 
     if args.impl == "native":
         from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
@@ -86,7 +93,12 @@ def main():
 
         torch.manual_seed(1234)  # identical init on every rank (also broadcast below)
         cfg = FeatureNet3DConfig.tiny() if args.tiny else FeatureNet3DConfig(input_size=S, num_classes=NC)
-        model = FeatureNet3D(cfg).to(dev)
+        if args.model == "seg":
+            from featurenet_amd.models.featurenet3d import FeatureNet3DSeg
+
+            model = FeatureNet3DSeg(input_size=S, num_classes=NC, widths=cfg.widths).to(dev)
+        else:
+            model = FeatureNet3D(cfg).to(dev)
         flat = FlatParams(model)
         opt = FlatAdam(flat.data, flat.grad, lr=1e-3)
         bucketer = GradBucketer(flat, bucket_mb=args.bucket_mb)
@@ -100,8 +112,8 @@ def main():
             scale = bucketer.finish()
             opt.step(grad_scale=scale)
             return loss
-        model_name = "FeatureNet-3D"
-        flops = model.train_flops_per_sample()
+        model_name = "FeatureNet-3D" if args.model == "cls" else "FeatureNet-3D-Seg (per-voxel head)"
+        flops = model.train_flops_per_sample() if hasattr(model, "train_flops_per_sample") else None
     else:
         from bench.torch_baseline import TorchFeatureNet3D
 
@@ -151,11 +163,12 @@ def main():
     ms = elapsed / max(args.steps, 1) * 1e3
     value = args.steps * B * world / elapsed
     base = TORCH_BASELINE_SAMPLES_PER_S_PER_GPU
-    same_cfg = args.batch == 128 and args.size == 64 and args.classes == 24 and not args.tiny
+    same_cfg = args.batch == 128 and args.size == 64 and args.classes == 24 and not args.tiny and args.model == "cls"
     vs = (value / (base * world)) if base and same_cfg else None
     if rank == 0:
         out = {
-            "metric": "samples/sec (64^3 voxel, 24-class) train",
+            "metric": ("samples/sec (64^3 voxel, 24-class) train" if args.model == "cls"
+                       else "samples/sec (64^3 voxel, per-voxel segmentation) train"),
             "value": round(value, 2),
             "unit": "samples/s",
             "n_gpus": world,

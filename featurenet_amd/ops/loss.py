@@ -37,7 +37,14 @@ class SoftmaxXentFn(torch.autograd.Function):
 
 
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0, with_correct: bool = False):
-    """Mean cross-entropy of ``logits`` [B, NC] against int64 ``labels`` [B]."""
+    """Mean cross-entropy of ``logits`` [B, NC] against int64 ``labels`` [B].
+
+    Dense predictions (per-voxel segmentation, ``logits`` [N, ..., NC] with
+    ``labels`` [N, ...]) are flattened to one row per voxel.
+    """
+    if logits.dim() > 2:
+        logits = logits.reshape(-1, logits.shape[-1])
+        labels = labels.reshape(-1)
     if _native.use_native(logits):
         loss, correct = SoftmaxXentFn.apply(logits, labels.long(), smoothing)
         return (loss, correct) if with_correct else loss

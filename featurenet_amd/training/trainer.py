@@ -129,9 +129,9 @@ class Trainer:
                 seen = 0
                 for bi, (xb, yb) in enumerate(loader):
                     loss, corr = self.train_step(xb, yb)
-                    loss_sum += loss.double() * len(yb)
+                    loss_sum += loss.double() * yb.numel()     # numel: per-voxel labels (segmentation)
                     correct += corr.sum()
-                    seen += len(yb)
+                    seen += yb.numel()
                     if callbacks:
                         for cb in callbacks:
                             cb.on_batch_end(self, bi, {})
@@ -174,9 +174,9 @@ class Trainer:
         for xb, yb in loader:
             logits = self.model(self._prep(xb))
             loss, corr = softmax_xent(logits, yb, with_correct=True)
-            loss_sum += loss.double() * len(yb)
+            loss_sum += loss.double() * yb.numel()
             correct += corr.sum()
-            seen += len(yb)
+            seen += yb.numel()
         stats = self._reduce(torch.stack([loss_sum, correct.double(),
                                           torch.tensor(float(seen), dtype=torch.float64, device=self.device)]))
         self.model.train()

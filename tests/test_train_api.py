@@ -125,3 +125,16 @@ def test_sgdr_cosine():
     assert t.lr == pytest.approx(0.0, abs=1e-12)
     s.on_epoch_end(t, 0, {})
     assert s.batch_since_restart == 0 and s.cycle_length == 2
+
+
+def test_segmentation_head_trains_per_voxel():
+    """BASELINE config 4 (per-voxel segmentation head) on the CPU path: loss/accuracy are per voxel."""
+    rng = np.random.default_rng(0)
+    x = (rng.random((16, 16, 16, 16, 1)) < 0.3).astype(np.float32)
+    y = np.zeros((16, 16, 16, 16), np.int64)
+    y[:, :8] = 1                                   # lower half of every part is "feature"
+    res = fn.train("segmentation", data=(x[:12], y[:12], x[12:], y[12:]), epochs=6, batch_size=4, lr=3e-3,
+                   verbose=0)
+    assert 0.0 <= res.accuracy <= 1.0
+    assert res.accuracy > 0.9
+    assert all(math.isfinite(v) for v in res.history["loss"])
