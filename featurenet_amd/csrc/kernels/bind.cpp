@@ -21,6 +21,9 @@ int fn_igemm_fwd_mblocks(long long);
 int fn_conv_halo(const void*, const void*, const float*, void*, float*, const int*, const int*, int, int,
                  hipStream_t);
 long long fn_conv_halo_lds(const int*, int);
+int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
+                    int, int, hipStream_t);
+int fn_quant_fp8(const void*, void*, long long, float, hipStream_t);
 int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, hipStream_t);
 int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
@@ -87,6 +90,17 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 16, "conv_halo_wgrad");
     chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x, S(st)),
         "conv_halo_wgrad");
+  });
+  m.def("conv_halo_f8", [](uintptr_t src, uintptr_t wt, uintptr_t scale, uintptr_t bias, uintptr_t out,
+                           float inv_out_scale, uintptr_t toffs, std::vector<int> geom, int ncol, int out_f8, int relu,
+                           uintptr_t st) {
+    need(geom, 16, "conv_halo_f8");
+    chk(fn_conv_halo_f8(P<const void*>(src), P<const void*>(wt), P<const float*>(scale), P<const float*>(bias),
+                        P<void*>(out), inv_out_scale, P<const int*>(toffs), geom.data(), ncol, out_f8, relu, S(st)),
+        "conv_halo_f8");
+  });
+  m.def("quant_fp8", [](uintptr_t x, uintptr_t y, long long n, float inv_scale, uintptr_t st) {
+    chk(fn_quant_fp8(P<const void*>(x), P<void*>(y), n, inv_scale, S(st)), "quant_fp8");
   });
   m.def("dw_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, std::vector<int> geom, int act,
                      uintptr_t st) {

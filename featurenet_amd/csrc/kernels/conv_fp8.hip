@@ -1,0 +1,285 @@
+// FP8 (OCP e4m3) LDS-halo convolution for the inference path (CDNA4).
+//
+// Same tiling as the bf16 halo kernel (conv_halo.hip): an output tile of
+// TD x TH x OW rows, its input halo staged in LDS per 16-channel slice, two
+// taps per MFMA k-step, weights streamed through a double-buffered 128-k LDS
+// stage -- but every operand byte is fp8, so the halo, the weight stages and
+// every LDS fragment read are half the size of the bf16 kernel's (the bf16
+// kernel is LDS-bandwidth-bound) and MFMA runs mfma_f32_16x16x32_fp8_fp8.
+// Dequantisation is one multiply in the epilogue:
+//   y = act(acc * scale[co] + bias[co])     scale[co] = s_x * s_w[co]
+// and the result is either re-quantised to fp8 (y * inv_out_scale, saturated
+// to +-448) for the next layer or stored as bf16.
+#include "common.h"
+
+struct F8Geom {
+  int N, ID, IH, IW, C;
+  int OD, OH, OW;
+  int KD, KH, KW;
+  int pd, ph, pw;
+  int TD, TH;
+};
+
+#define F8_BM 256
+#define F8_BK 128   // k (bytes) per weight stage: 8 taps x 16 channels
+
+__device__ __forceinline__ unsigned char f32_to_fp8(float v) {
+  v = fminf(fmaxf(v, -448.f), 448.f);
+  const int p = __builtin_amdgcn_cvt_pk_fp8_f32(v, v, 0, false);
+  return (unsigned char)(p & 0xff);
+}
+
+template <int BN, bool OUT_F8, bool RELU>
+__global__ __launch_bounds__(256, 2) void conv_halo_f8_kernel(const unsigned char* __restrict__ src,
+                                                              const unsigned char* __restrict__ wt,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ bias, void* __restrict__ out,
+                                                              float inv_out_scale, const int* __restrict__ toffs,
+                                                              F8Geom g, int Ncol) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  constexpr int NT = BN / 16;
+  constexpr int B_STAGE = BN * F8_BK;           // bytes
+  constexpr int B_CHUNKS = BN * (F8_BK / 16);
+  constexpr int B_PER_T = (B_CHUNKS + 255) / 256;
+  const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
+  const int HP = HD * HH * HW;
+  const int T = g.KD * g.KH * g.KW;
+  const int T8 = (T + 7) & ~7;
+  const int spp = T8 >> 3;
+  const int npass = g.C >> 4;
+  const int nq = spp * npass;
+  const int ldw = npass * T8 * 16;
+  const int rows = g.TD * g.TH * g.OW;
+  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
+
+  unsigned char* halo = dsm;                                   // [HP][16]
+  unsigned char* Bs = dsm + (((size_t)HP * 16 + 15) & ~(size_t)15);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+  const int d0 = td_i * g.TD, h0 = th_i * g.TH;
+  const int n0 = blockIdx.y * BN;
+
+  int hbase[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int r = wave * 64 + mt * 16 + lr;
+    const int rr = r < rows ? r : 0;
+    const int w = rr % g.OW, th = (rr / g.OW) % g.TH, td = rr / (g.OW * g.TH);
+    hbase[mt] = (td * HH + th) * HW + w;
+  }
+
+  auto fill_halo = [&](int p) {
+    for (int c0 = 0; c0 < HP; c0 += 256 * 4) {
+      uint4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int pos = c0 + j * 256 + tid;
+        const int hw = pos % HW, hh = (pos / HW) % HH, hd = pos / (HW * HH);
+        const int gd = d0 - g.pd + hd, gh = h0 - g.ph + hh, gw = hw - g.pw;
+        const bool ok = pos < HP && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                        (unsigned)gw < (unsigned)g.IW;
+        const long long off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + p * 16;
+        const uint4 x = *(const uint4*)(src + (ok ? off : 0));
+        v[j] = ok ? x : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int pos = c0 + j * 256 + tid;
+        if (pos < HP) *(uint4*)(halo + (size_t)pos * 16) = v[j];
+      }
+    }
+  };
+  uint4 rb[B_PER_T];
+  auto load_b = [&](int q) {
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int idx = tid + i * 256;
+      const int r = (idx >> 3) < BN ? (idx >> 3) : BN - 1;
+      const bool ok = idx < B_CHUNKS && n0 + r < Ncol;
+      const uint4 v = *(const uint4*)(wt + (ok ? (long long)(n0 + r) * ldw + q * F8_BK + (idx & 7) * 16 : 0));
+      rb[i] = ok ? v : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto write_b = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < B_PER_T; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < B_CHUNKS) {
+        const int r = idx >> 3, c = idx & 7;
+        *(uint4*)(Bs + buf * B_STAGE + r * F8_BK + ((c ^ (r & 7)) << 4)) = rb[i];
+      }
+    }
+  };
+
+  f32x4 acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  fill_halo(0);
+  load_b(0);
+  write_b(0);
+  __syncthreads();
+  const int mt_live = rows - wave * 64;
+  for (int q = 0; q < nq; ++q) {
+    if (q > 0 && q % spp == 0) {
+      fill_halo(q / spp);
+      __syncthreads();
+    }
+    const bool more = q + 1 < nq;
+    if (more) load_b(q + 1);
+    const unsigned char* b = Bs + (q & 1) * B_STAGE;
+    const int* tp = toffs + (q % spp) * 8;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int toff = (lg & 2) ? tp[ks * 2 + 1] : tp[ks * 2];
+      long fa[4], fb[NT];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+        fa[mt] = *(const long*)(halo + (size_t)(hbase[mt] + toff) * 16 + (lg & 1) * 8);
+      const int chunk = ks * 2 + (lg >> 1);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const int r = nt * 16 + lr;
+        fb[nt] = *(const long*)(b + r * F8_BK + ((chunk ^ (r & 7)) << 4) + (lg & 1) * 8);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        if (mt * 16 < mt_live) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) {
+      write_b((q + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: dequantise, bias, act, (re)quantise; staged through LDS ----
+  constexpr int ESZ = OUT_F8 ? 1 : 2;
+  constexpr int LDO = BN * ESZ + 16;            // bytes per staged row
+  unsigned char* Os = dsm;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = nt * 16 + lr;
+    const bool cv = n0 + col < Ncol;
+    const float sc = cv ? scale[n0 + col] : 0.f, bv = cv ? bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wave * 64 + mt * 16 + lg * 4 + r;
+        float v = acc[mt][nt][r] * sc + bv;
+        if (RELU) v = fmaxf(v, 0.f);
+        if constexpr (OUT_F8) Os[row * LDO + col] = f32_to_fp8(v * inv_out_scale);
+        else *(bf16*)(Os + row * LDO + col * 2) = f2bf(v);
+      }
+  }
+  __syncthreads();
+  constexpr int CB = BN * ESZ / 16;             // 16-B chunks per row
+  for (int idx = tid; idx < F8_BM * CB; idx += 256) {
+    const int row = idx / CB, ch = idx % CB;
+    if (row >= rows) continue;
+    const int w = row % g.OW, th = (row / g.OW) % g.TH, td = row / (g.OW * g.TH);
+    if (d0 + td >= g.OD || h0 + th >= g.OH) continue;
+    const long long m = (((long long)n * g.OD + d0 + td) * g.OH + h0 + th) * g.OW + w;
+    const int col0 = ch * 16 / ESZ;
+    unsigned char* dst = (unsigned char*)out + (m * Ncol + n0 + col0) * ESZ;
+    if (n0 + col0 + 16 / ESZ <= Ncol && (Ncol * ESZ) % 16 == 0) {
+      *(uint4*)dst = *(const uint4*)(Os + row * LDO + ch * 16);
+    } else {
+      for (int j = 0; j < 16 / ESZ; ++j)
+        if (n0 + col0 + j < Ncol)
+          for (int b2 = 0; b2 < ESZ; ++b2) dst[j * ESZ + b2] = Os[row * LDO + ch * 16 + j * ESZ + b2];
+    }
+  }
+}
+
+static F8Geom parse_f8(const int* v) {
+  F8Geom g;
+  g.N = v[0]; g.ID = v[1]; g.IH = v[2]; g.IW = v[3]; g.C = v[4];
+  g.OD = v[5]; g.OH = v[6]; g.OW = v[7];
+  g.KD = v[8]; g.KH = v[9]; g.KW = v[10];
+  g.pd = v[11]; g.ph = v[12]; g.pw = v[13];
+  g.TD = v[14]; g.TH = v[15];
+  return g;
+}
+
+static size_t f8_lds(const F8Geom& g, int BN, bool out_f8) {
+  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  const size_t main_ = ((hp * 16 + 15) & ~(size_t)15) + 2 * (size_t)BN * F8_BK;
+  const size_t epi = (size_t)F8_BM * (BN * (out_f8 ? 1 : 2) + 16);
+  return (main_ > epi ? main_ : epi) + 16;
+}
+
+// src / wt: fp8 e4m3 bytes; wt [Ncol][C/16][T8][16]; scale/bias fp32 [Ncol]; out fp8 or bf16.
+extern "C" int fn_conv_halo_f8(const void* src, const void* wt, const float* scale, const float* bias, void* out,
+                               float inv_out_scale, const int* toffs, const int* geom16, int Ncol, int out_f8,
+                               int relu, hipStream_t st) {
+  const F8Geom g = parse_f8(geom16);
+  if (g.C % 16 != 0 || g.TD * g.TH * g.OW > F8_BM || Ncol % 16 != 0) return -2;
+  const int BN = Ncol <= 32 ? 32 : 64;
+  const size_t lds = f8_lds(g, BN, out_f8 != 0);
+  if (lds > 160 * 1024) return -4;
+  const int tiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
+  dim3 grid((unsigned)tiles, (Ncol + BN - 1) / BN);
+  const unsigned char* s = (const unsigned char*)src;
+  const unsigned char* w = (const unsigned char*)wt;
+#define F8CASE(B, O, R)                                                                                   \
+  do {                                                                                                    \
+    static size_t cfg = 0;                                                                                \
+    if (lds > cfg) {                                                                                      \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_halo_f8_kernel<B, O, R>,                       \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);           \
+      if (e != hipSuccess) return (int)e;                                                                 \
+      cfg = lds;                                                                                          \
+    }                                                                                                     \
+    hipLaunchKernelGGL((conv_halo_f8_kernel<B, O, R>), grid, dim3(256), lds, st, s, w, scale, bias, out, \
+                       inv_out_scale, toffs, g, Ncol);                                                    \
+  } while (0)
+#define F8BN(B)                                                        \
+  do {                                                                 \
+    if (out_f8) { if (relu) F8CASE(B, true, true); else F8CASE(B, true, false); }   \
+    else { if (relu) F8CASE(B, false, true); else F8CASE(B, false, false); }        \
+  } while (0)
+  if (BN == 32) F8BN(32); else F8BN(64);
+#undef F8BN
+#undef F8CASE
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// x (bf16) -> fp8 e4m3 of x * inv_scale, saturated (activation quantisation between layers).
+__global__ void quant_fp8_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ y, long long n,
+                                 float inv_scale) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  if (i + 8 <= n) {
+    Pack8 p;
+    p.u = *(const uint4*)(x + i);
+    unsigned int lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo |= (unsigned)f32_to_fp8(bf2f(p.e[j]) * inv_scale) << (8 * j);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hi |= (unsigned)f32_to_fp8(bf2f(p.e[4 + j]) * inv_scale) << (8 * j);
+    *(uint2*)(y + i) = make_uint2(lo, hi);
+  } else {
+    for (long long j = i; j < n; ++j) y[j] = f32_to_fp8(bf2f(x[j]) * inv_scale);
+  }
+}
+
+extern "C" int fn_quant_fp8(const void* x, void* y, long long n, float inv_scale, hipStream_t st) {
+  const long long threads = (n + 7) / 8;
+  hipLaunchKernelGGL(quant_fp8_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (const bf16*)x,
+                     (unsigned char*)y, n, inv_scale);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,148 @@
+"""FP8 inference for FeatureNet-3D (BASELINE config 5: 128^3 voxels, batch 1024).
+
+Post-training quantisation, inference only:
+
+* BatchNorm is folded into the conv weights and bias (eval statistics);
+* weights are quantised per output channel to OCP e4m3 (amax / 448);
+* activations between layers are quantised per tensor with scales calibrated
+  from a bf16 forward pass (``amax / 448`` of each layer's post-ReLU output);
+* conv2..conv4 run ``conv_halo_f8`` (``csrc/kernels/conv_fp8.hip``): fp8
+  halo tiles in LDS, ``mfma_f32_16x16x32_fp8_fp8``, dequantise + bias + ReLU
+  (+ requantise to fp8) in the epilogue.  conv1 (1-channel, stride 2) stays on
+  the bf16 implicit-GEMM kernel with the folded BN + ReLU fused, followed by
+  one quantisation pass; conv4 writes bf16 for the max-pool and the two dense
+  layers (hipBLASLt bf16).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native
+from .. import ops
+from ..models.featurenet3d import FeatureNet3D
+from ..ops.conv import halo_plan, halo_tap_offsets
+from ..ops.spec import ConvSpec, PoolSpec
+
+FP8_MAX = 448.0
+
+
+def _fold_bn(conv) -> tuple[torch.Tensor, torch.Tensor]:
+    w = conv.weight.detach().float()
+    if conv.bn:
+        g = conv.gamma.detach().float() / torch.sqrt(conv.running_var.float() + conv.bn_eps)
+        b = conv.beta.detach().float() - conv.running_mean.float() * g
+        return w * g.view(-1, 1, 1, 1, 1), b
+    b = conv.bias.detach().float() if conv.bias is not None else torch.zeros(w.shape[0], device=w.device)
+    return w, b
+
+
+def _to_fp8(t: torch.Tensor) -> torch.Tensor:
+    return t.clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+
+
+class Fp8Conv:
+    """One stride-1 conv layer on the fp8 halo kernel (folded BN, per-channel weight scales)."""
+
+    def __init__(self, conv, in_scale: float, out_scale: float | None, relu: bool = True):
+        w, b = _fold_bn(conv)
+        K, KD, KH, KW, Cin = w.shape
+        sw = w.abs().reshape(K, -1).amax(1).clamp_min(1e-12) / FP8_MAX
+        wq = _to_fp8(w / sw.view(-1, 1, 1, 1, 1))
+        # fp8 weights in the halo kernel's k order ([K][C/16][T8][16] bytes)
+        T = KD * KH * KW
+        T8 = (T + 7) // 8 * 8
+        lay = torch.zeros(K, Cin // 16, T8, 16, dtype=torch.float8_e4m3fn, device=w.device)
+        lay[:, :, :T] = wq.reshape(K, T, Cin // 16, 16).permute(0, 2, 1, 3)
+        self.wq = lay.reshape(K, -1).view(torch.uint8).contiguous()
+        self.scale = (in_scale * sw).float().contiguous()
+        self.bias = b.float().contiguous()
+        self.out_scale, self.relu = out_scale, relu
+        self.K, self.kernel, self.conv = K, (KD, KH, KW), conv
+        self.w_dequant = wq.float() * sw.view(-1, 1, 1, 1, 1)     # for numerics tests
+
+    def __call__(self, xq: torch.Tensor, shape5: tuple) -> tuple[torch.Tensor, tuple]:
+        spec = ConvSpec.make(shape5, self.K, self.kernel, 1, self.conv.padding)
+        # fp8 halo = 16 B/position; halo_plan counts 32 B/position (bf16): <= 64 KiB of fp8 halo
+        plan = halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, 128 * 1024)
+        if plan is None:
+            raise RuntimeError(f"no fp8 halo tile for {spec}")
+        geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
+                spec.pd, spec.ph, spec.pw, plan[0], plan[1]]
+        out_f8 = self.out_scale is not None
+        y = torch.empty(spec.out_shape5, dtype=torch.uint8 if out_f8 else torch.bfloat16, device=xq.device)
+        toffs = halo_tap_offsets(geom, xq.device)
+        _native.kernels().conv_halo_f8(xq.data_ptr(), self.wq.data_ptr(), self.scale.data_ptr(),
+                                       self.bias.data_ptr(), y.data_ptr(),
+                                       1.0 / self.out_scale if out_f8 else 1.0, toffs.data_ptr(), geom, self.K,
+                                       int(out_f8), int(self.relu), _native.stream(xq))
+        return y, spec.out_shape5
+
+
+def quantize_fp8_act(x: torch.Tensor, scale: float) -> torch.Tensor:
+    """bf16 activation -> fp8 bytes of x / scale (native kernel)."""
+    y = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    _native.kernels().quant_fp8(x.data_ptr(), y.data_ptr(), x.numel(), 1.0 / scale, _native.stream(x))
+    return y
+
+
+class Fp8FeatureNet3D:
+    """Inference-only fp8 FeatureNet-3D built from a trained (or random-init) bf16 model."""
+
+    def __init__(self, model: FeatureNet3D, act_scales: list[float]):
+        self.model = model.eval()
+        convs = list(model.convs)
+        c1 = convs[0]
+        w1, b1 = _fold_bn(c1)
+        self.c1_w, self.c1_b = w1, b1
+        self.act_scales = act_scales
+        self.layers = []
+        for i, conv in enumerate(convs[1:], start=1):
+            last = i == len(convs) - 1
+            self.layers.append(Fp8Conv(conv, act_scales[i - 1], None if last else act_scales[i], relu=True))
+        self.pool = convs[-1].pool
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        m = self.model
+        if x.dim() == 4:
+            x = x.unsqueeze(-1)
+        x = x.to(torch.bfloat16).contiguous()
+        c1 = m.convs[0]
+        spec = ConvSpec.make(tuple(x.shape), c1.cout, c1.kernel, c1.stride, c1.padding)
+        y = ops.conv(x, self.c1_w, self.c1_b, spec, "relu")                   # bf16, BN folded, ReLU fused
+        xq = quantize_fp8_act(y, self.act_scales[0])
+        shape = spec.out_shape5
+        for layer in self.layers:
+            xq, shape = layer(xq, shape)
+        feat = xq                                                             # bf16 [N, D, H, W, 64]
+        if self.pool is not None:
+            ps = PoolSpec.make(tuple(feat.shape), self.pool, m.convs[-1].pool_stride, "valid")
+            feat = ops.pool(feat, ps, "max")
+        f = feat.reshape(feat.shape[0], -1)
+        return m.fc2(m.fc1(f), out_fp32=True)
+
+    __call__ = forward
+
+
+@torch.no_grad()
+def calibrate(model: FeatureNet3D, calib_x: torch.Tensor, margin: float = 1.0) -> list[float]:
+    """Per-layer post-ReLU activation scales (amax / 448) from a bf16 eval forward."""
+    model.eval()
+    x = calib_x
+    if x.dim() == 4:
+        x = x.unsqueeze(-1)
+    x = x.to(torch.bfloat16)
+    scales = []
+    for conv in model.convs:
+        x = conv(x)
+        scales.append(max(float(x.float().abs().amax()) * margin, 1e-6) / FP8_MAX)
+    return scales
+
+
+def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor) -> Fp8FeatureNet3D:
+    return Fp8FeatureNet3D(model, calibrate(model, calib_x))
+
+
+_ = math

@@ -362,3 +362,46 @@ def test_segmentation_head_step():
     lg.backward()
     for p in m_gpu.parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all()
+
+
+@pytest.mark.parametrize("out_f8", [False, True])
+def test_conv_halo_fp8(out_f8):
+    """fp8 halo conv (conv_fp8.hip) vs fp32 conv of the same dequantised operands."""
+    _native_loaded()
+    from featurenet_amd.inference.fp8 import Fp8Conv
+    from featurenet_amd.models.layers import Conv
+
+    torch.manual_seed(7)
+    conv = Conv(32, 64, (3, 3, 3), 1, "valid", bias=True).cuda()
+    with torch.no_grad():
+        conv.bias.normal_(0, 0.1)
+    xs = 0.02
+    x = (torch.randn(2, 12, 13, 14, 32, device="cuda") * 2).clamp(-400 * xs, 400 * xs)
+    xq = (x / xs).to(torch.float8_e4m3fn)
+    out_scale = 0.05 if out_f8 else None
+    layer = Fp8Conv(conv, xs, out_scale, relu=True)
+    y, _ = layer(xq.view(torch.uint8), tuple(x.shape))
+    spec = ConvSpec.make(x.shape, 64, (3, 3, 3))
+    yr = torch.relu(ref.conv(xq.float() * xs, layer.w_dequant, layer.bias, spec))
+    if out_f8:
+        yd = y.view(torch.float8_e4m3fn).float() * out_scale
+        err = (yd - yr).abs().max().item()
+        assert err <= 0.07 * yr.abs().max().item() + 2 * out_scale
+    else:
+        close(y, yr)
+
+
+def test_fp8_featurenet3d_matches_bf16():
+    _native_loaded()
+    from featurenet_amd.inference.fp8 import quantize_model
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+
+    torch.manual_seed(0)
+    m = FeatureNet3D(FeatureNet3DConfig(input_size=32, num_classes=24)).cuda().eval()
+    x = (torch.rand(16, 32, 32, 32, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    q = quantize_model(m, x[:8])
+    with torch.no_grad():
+        ref_logits = m(x).float()
+        got = q(x).float()
+    cos = torch.nn.functional.cosine_similarity(got.flatten(), ref_logits.flatten(), dim=0).item()
+    assert cos > 0.97, cos

@@ -78,3 +78,16 @@ def test_igemm_and_misc_calls_match_bindings(fake):
                               torch.zeros(8, 1, 3, 3, 1), None, ds, 0)
     assert y.shape == (2, 1, 9, 9, 8)
     assert {"igemm_fwd", "igemm_wgrad", "colstats", "bn_finalize", "dw_fwd"} <= set(fake.calls)
+
+
+def test_fp8_inference_calls_match_bindings(fake):
+    from featurenet_amd.inference.fp8 import Fp8Conv, quantize_fp8_act
+    from featurenet_amd.models.layers import Conv
+
+    conv = Conv(32, 64, (3, 3, 3), 1, "valid", bias=True)
+    layer = Fp8Conv(conv, 0.02, 0.05)
+    xq = torch.zeros(2, 10, 10, 10, 32, dtype=torch.uint8)
+    y, shape = layer(xq, tuple(xq.shape))
+    assert shape == (2, 8, 8, 8, 64) and y.dtype == torch.uint8
+    quantize_fp8_act(torch.zeros(4, 8, dtype=torch.bfloat16), 0.1)
+    assert {"conv_halo_f8", "quant_fp8"} <= set(fake.calls)
