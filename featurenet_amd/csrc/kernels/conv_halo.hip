@@ -353,6 +353,9 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// halo / dy chunks per thread prefetched into registers for the NEXT tile
+#define WG_HC(MT) ((MT) <= 2 ? 8 : 4)
+
 template <int MT>
 __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __restrict__ dy,
                                                                  const bf16* __restrict__ src,
@@ -361,8 +364,11 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   constexpr int TPW = MT == 1 ? 16 : 32 / MT;   // taps per wave (acc <= 128 VGPRs)
   constexpr int BCO = MT * 16;
   constexpr int LDY = BCO + 16;            // conflict-free transposed reads (as igemm wgrad)
+  constexpr int YC = BCO / 8;              // 16-B chunks per dy row
+  constexpr int HC = WG_HC(MT);
   const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
   const int HP = HD * HH * HW;
+  const int nchunk = HP * 2;
   const int T = g.KD * g.KH * g.KW;
   const int rows = g.TD * g.TH * g.OW;
   const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
@@ -371,20 +377,31 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   bf16* Ys = reinterpret_cast<bf16*>(dsm);                                   // [256][LDY]
   bf16* halo = reinterpret_cast<bf16*>(dsm + (size_t)H_BM * LDY * 2);        // [HP][16]
   int* rowpos = reinterpret_cast<int*>(dsm + (size_t)H_BM * LDY * 2 + (size_t)HP * 32);  // [256]
+  int* rowinfo = rowpos + H_BM;                                               // packed (td, th, w) per row
+  int* posinfo = rowinfo + H_BM;                                              // packed (hd, hh, hw) per position
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
   const int slice = blockIdx.z;
-  const int tap0 = (blockIdx.y * 4 + wave) * TPW;
+  const int tap0 = (blockIdx.y * 4 + wave) * TPW;          // uniform: tap offsets stay in SGPRs
+  // contiguous run of tiles per workgroup (neighbouring tiles share halo rows in L2)
+  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const int t_begin = blockIdx.x * per;
+  const int t_end = t_begin + per < ntiles ? t_begin + per : ntiles;
 
   for (int r = tid; r < H_BM; r += 256) {
-    int pos = 0;
+    int pos = 0, info = -1;
     if (r < rows) {
       const int w = r % g.OW, th = (r / g.OW) % g.TH, td = r / (g.OW * g.TH);
       pos = (td * HH + th) * HW + w;
+      info = (td << 20) | (th << 10) | w;
     }
     rowpos[r] = pos;
+    rowinfo[r] = info;
   }
+  for (int pos = tid; pos < HP; pos += 256)
+    posinfo[pos] = ((pos / (HW * HH)) << 20) | (((pos / HW) % HH) << 10) | (pos % HW);
   int toff[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
@@ -393,6 +410,69 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
     toff[i] = (kd * HH + kh) * HW + kw;
   }
   const int ntap = T - tap0 < TPW ? (T - tap0 > 0 ? T - tap0 : 0) : TPW;   // live taps of this wave
+  __syncthreads();
+
+  uint4 yreg[YC], hreg[HC];
+  auto dy_src = [&](int tile, int idx, long long& m) -> bool {
+    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+    const int r = idx / YC, c = idx % YC;
+    const int info = rowinfo[r];
+    const int td = info >> 20, th = (info >> 10) & 1023, w = info & 1023;
+    m = ((((long long)n * g.OD + td_i * g.TD + td) * g.OH + th_i * g.TH + th) * g.OW + w) * Cout + c * 8;
+    return info >= 0 && td_i * g.TD + td < g.OD && th_i * g.TH + th < g.OH && c * 8 < Cout;
+  };
+  auto halo_src = [&](int tile, int c, long long& off) -> bool {
+    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+    const int info = posinfo[c < nchunk ? c >> 1 : 0];
+    const int gd = td_i * g.TD - g.pd + (info >> 20), gh = th_i * g.TH - g.ph + ((info >> 10) & 1023);
+    const int gw = (info & 1023) - g.pw;
+    off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + slice * 16 + (c & 1) * 8;
+    return c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+           (unsigned)gw < (unsigned)g.IW;
+  };
+  auto prefetch = [&](int tile) {
+#pragma unroll
+    for (int i = 0; i < YC; ++i) {
+      long long m;
+      const bool ok = dy_src(tile, i * 256 + tid, m);
+      const uint4 v = *(const uint4*)(dy + (ok ? m : 0));
+      yreg[i] = ok ? v : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < HC; ++i) {
+      long long off;
+      const bool ok = halo_src(tile, i * 256 + tid, off);
+      const uint4 v = *(const uint4*)(src + (ok ? off : 0));
+      hreg[i] = ok ? v : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int tile) {
+#pragma unroll
+    for (int i = 0; i < YC; ++i) {
+      const int idx = i * 256 + tid;
+      *(uint4*)(Ys + (idx / YC) * LDY + (idx % YC) * 8) = yreg[i];
+    }
+#pragma unroll
+    for (int i = 0; i < HC; ++i) {
+      const int c = i * 256 + tid;
+      if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = hreg[i];
+    }
+    for (int c0 = HC * 256; c0 < nchunk; c0 += 4 * 256) {   // tail of a large halo: synchronous
+      uint4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        long long off;
+        const bool ok = halo_src(tile, c0 + j * 256 + tid, off);
+        const uint4 x = *(const uint4*)(src + (ok ? off : 0));
+        v[j] = ok ? x : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j * 256 + tid;
+        if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = v[j];
+      }
+    }
+  };
 
   f32x4 acc[TPW][MT];
 #pragma unroll
@@ -400,47 +480,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
-    const int d0 = td_i * g.TD, h0 = th_i * g.TH;
-    __syncthreads();   // previous tile's reads are done
-    // dy tile -> Ys (rows outside the output are zero, so they add nothing)
-    constexpr int YC = BCO / 8;
-    for (int idx = tid; idx < H_BM * YC; idx += 256) {
-      const int r = idx / YC, c = idx % YC;
-      bool ok = r < rows;
-      long long m = 0;
-      if (ok) {
-        const int w = r % g.OW, th = (r / g.OW) % g.TH, td = r / (g.OW * g.TH);
-        ok = d0 + td < g.OD && h0 + th < g.OH && c * 8 < Cout;
-        m = (((long long)n * g.OD + d0 + td) * g.OH + h0 + th) * g.OW + w;
-      }
-      const uint4 v = *(const uint4*)(dy + (ok ? m * Cout + c * 8 : 0));
-      *(uint4*)(Ys + r * LDY + c * 8) = ok ? v : make_uint4(0, 0, 0, 0);
-    }
-    // x halo slice -> LDS
-    const int nchunk = HP * 2;
-    for (int c0 = 0; c0 < nchunk; c0 += 256 * 8) {
-      uint4 v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c0 + j * 256 + tid;
-        const int pos = c >> 1, half = c & 1;
-        const int hw = pos % HW, hh = (pos / HW) % HH, hd = pos / (HW * HH);
-        const int gd = d0 - g.pd + hd, gh = h0 - g.ph + hh, gw = hw - g.pw;
-        const bool ok = c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-                        (unsigned)gw < (unsigned)g.IW;
-        const long long off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + slice * 16 + half * 8;
-        const uint4 x = *(const uint4*)(src + (ok ? off : 0));
-        v[j] = ok ? x : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c0 + j * 256 + tid;
-        if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = v[j];
-      }
-    }
+  if (t_begin < t_end) prefetch(t_begin);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+    __syncthreads();                 // previous tile's reads are done
+    store(tile);
     __syncthreads();
+    if (tile + 1 < t_end) prefetch(tile + 1);   // lands during this tile's MFMAs
     const int kst = (rows + 31) >> 5;
     for (int ks = 0; ks < kst; ++ks) {
       bf16x8 fa[MT];
@@ -574,7 +619,7 @@ extern "C" long long fn_conv_halo_lds(const int* geom16, int Ncol) {
 
 static size_t halo_wgrad_lds(const HaloGeom& g, int MT) {
   const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
-  return (size_t)H_BM * (MT * 16 + 16) * 2 + hp * 32 + H_BM * 4 + 16;
+  return (size_t)H_BM * (MT * 16 + 16) * 2 + hp * 32 + 2 * H_BM * 4 + hp * 4 + 16;
 }
 
 // dw: fp32 [Cout][T][C], zero-initialised by the caller (atomics accumulate).

@@ -165,7 +165,7 @@ def _fwd_halo_budget(ncol: int) -> int:
 
 def _wgrad_halo_budget(cout: int) -> int:
     mt = (cout + 15) // 16
-    return LDS_BUDGET - 256 * (16 * mt + 16) * 2 - 2048
+    return int((LDS_BUDGET - 256 * (16 * mt + 16) * 2 - 2048 - 64) / 1.125)    # + 4 B/position table
 
 
 def halo_plan(OD: int, OH: int, OW: int, KD: int, KH: int, KW: int, max_bytes: int = 56 * 1024):
@@ -394,6 +394,65 @@ def native_act_bwd(dy: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 # autograd
 # ---------------------------------------------------------------------------
+# ---------------------------------------------------------------------------
+# space-to-depth: strided convs with few input channels (FeatureNet-3D's
+# 1-channel 7^3 stride-2 stem) become stride-1 convs with s^3*C channels
+# ---------------------------------------------------------------------------
+def s2d_plan(spec: ConvSpec):
+    """(factors, ConvSpec') when a strided, few-channel, unpadded conv maps onto the
+    stride-1 halo kernels after a space-to-depth of the input; else None."""
+    f = (spec.sd, spec.sh, spec.sw)
+    if not _halo_enabled() or f == (1, 1, 1) or (spec.dd, spec.dh, spec.dw) != (1, 1, 1):
+        return None
+    if spec.pd or spec.ph or spec.pw or any(p for p in spec.pads_hi):
+        return None
+    cs = spec.C * f[0] * f[1] * f[2]
+    if cs > 16:
+        return None
+    D2, H2, W2 = (-(-d // s) for d, s in zip((spec.D, spec.H, spec.W), f))
+    k2 = tuple(-(-k // s) for k, s in zip((spec.KD, spec.KH, spec.KW), f))
+    if k2[0] * k2[1] * k2[2] < 8 or D2 < k2[0] or H2 < k2[1] or W2 < k2[2]:
+        return None
+    spec2 = ConvSpec.make((spec.N, D2, H2, W2, 16), spec.K, k2, 1, "valid")
+    if (spec2.OD, spec2.OH, spec2.OW) != (spec.OD, spec.OH, spec.OW) or halo_fwd_plan(spec2) is None:
+        return None
+    return f, spec2
+
+
+def s2d_input(x5: torch.Tensor, f, spec2: ConvSpec) -> torch.Tensor:
+    N, D, H, W, C = x5.shape
+    sd, sh, sw = f
+    D2, H2, W2 = spec2.D, spec2.H, spec2.W
+    xp = torch.zeros(N, D2 * sd, H2 * sh, W2 * sw, C, dtype=torch.bfloat16, device=x5.device)
+    xp[:, :D, :H, :W] = x5
+    x2 = xp.view(N, D2, sd, H2, sh, W2, sw, C).permute(0, 1, 3, 5, 2, 4, 6, 7).reshape(N, D2, H2, W2, -1)
+    out = torch.zeros(N, D2, H2, W2, 16, dtype=torch.bfloat16, device=x5.device)
+    out[..., : x2.shape[-1]] = x2
+    return out
+
+
+def s2d_weight(w: torch.Tensor, f, spec: ConvSpec, spec2: ConvSpec) -> torch.Tensor:
+    K, KD, KH, KW, C = w.shape
+    sd, sh, sw = f
+    kd, kh, kw = spec2.KD, spec2.KH, spec2.KW
+    wp = torch.zeros(K, kd * sd, kh * sh, kw * sw, C, dtype=w.dtype, device=w.device)
+    wp[:, :KD, :KH, :KW] = w
+    w2 = wp.view(K, kd, sd, kh, sh, kw, sw, C).permute(0, 1, 3, 5, 2, 4, 6, 7).reshape(K, kd, kh, kw, -1)
+    out = torch.zeros(K, kd, kh, kw, 16, dtype=w.dtype, device=w.device)
+    out[..., : w2.shape[-1]] = w2
+    return out
+
+
+def s2d_weight_grad(dw2: torch.Tensor, f, spec: ConvSpec) -> torch.Tensor:
+    """Inverse of :func:`s2d_weight` for a gradient (drops padded taps / channels)."""
+    K, kd, kh, kw, _ = dw2.shape
+    sd, sh, sw = f
+    C = spec.C
+    g = dw2[..., : sd * sh * sw * C].reshape(K, kd, kh, kw, sd, sh, sw, C)
+    g = g.permute(0, 1, 4, 2, 5, 3, 6, 7).reshape(K, kd * sd, kh * sh, kw * sw, C)
+    return g[:, : spec.KD, : spec.KH, : spec.KW].contiguous()
+
+
 class ConvFn(torch.autograd.Function):
     """y = act(conv(x, w) + b); optional BN statistics slab as a 2nd output."""
 
@@ -403,6 +462,7 @@ class ConvFn(torch.autograd.Function):
         if halo_fwd_plan(spec) is not None:
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats, w=w.detach())
         else:
+            # (a space-to-depth forward of the 1-channel stem pads K 3x and loses to packed-W igemm)
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
         ctx.spec, ctx.act, ctx.has_b = spec, act, b is not None
@@ -420,7 +480,15 @@ class ConvFn(torch.autograd.Function):
         if act:
             dy = native_act_bwd(dy, y, act)
         dx = native_conv_dgrad(dy, w.detach(), spec) if ctx.x_needs else None
-        dw = native_conv_wgrad(dy, x5.contiguous(), spec) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            s2d = s2d_plan(spec)
+            if s2d is not None:      # strided few-channel stem: wgrad on the halo kernel after space-to-depth
+                f, spec2 = s2d
+                dw2 = native_conv_wgrad(dy, s2d_input(x5.to(torch.bfloat16), f, spec2), spec2)
+                dw = s2d_weight_grad(dw2, f, spec)
+            else:
+                dw = native_conv_wgrad(dy, x5.contiguous(), spec)
         db = native_colsum(dy.reshape(-1, spec.K)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
         return dx, dw, db, None, None, None
 

@@ -405,3 +405,27 @@ def test_fp8_featurenet3d_matches_bf16():
         got = q(x).float()
     cos = torch.nn.functional.cosine_similarity(got.flatten(), ref_logits.flatten(), dim=0).item()
     assert cos > 0.97, cos
+
+
+def test_space_to_depth_stem_matches_reference():
+    """FeatureNet-3D stem (1-ch 7^3 stride 2) through space-to-depth + halo kernels: fwd, stats, wgrad."""
+    _native_loaded()
+    import importlib
+
+    C = importlib.import_module("featurenet_amd.ops.conv")
+    torch.manual_seed(2)
+    x = (torch.rand(2, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, 32, 7, 2)
+    assert C.s2d_plan(spec) is not None
+    w = (torch.randn(32, 7, 7, 7, 1, device="cuda") * 0.05).to(torch.bfloat16).float()
+    wn = w.clone().requires_grad_(True)
+    y, st = C.ConvFn.apply(x, wn, None, spec, 0, True)
+    wr = w.clone().requires_grad_(True)
+    yr = ref.conv(x.float(), wr, None, spec)
+    close(y, yr)
+    yb = y.float().reshape(-1, 32)
+    torch.testing.assert_close(st[:, 0].sum(0), yb.sum(0), rtol=2e-3, atol=5e-2)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    close(wn.grad, wr.grad)
