@@ -40,6 +40,7 @@ int fn_bn_bwd_apply(const void*, const void*, const float*, const float*, const 
 int fn_pool_fwd(const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd(const void*, const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_softmax_xent(const float*, const long long*, float*, float*, int*, int, int, float, float, hipStream_t);
+int fn_adam_flat_dev(float*, const float*, float*, float*, void*, long long, const float*, int*, int, hipStream_t);
 int fn_adam_flat(float*, const float*, float*, float*, void*, long long, float, float, float, float, float, float,
                  float, float, int, hipStream_t);
 int fn_sgd_flat(float*, const float*, float*, void*, long long, float, float, float, int, float, hipStream_t);
@@ -174,6 +175,12 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_softmax_xent(P<const float*>(logits), P<const long long*>(labels), P<float*>(loss), P<float*>(dlogits),
                         P<int*>(correct), B, NC, gscale, smoothing, S(st)),
         "softmax_xent");
+  });
+  m.def("adam_flat_dev", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t pb, long long n,
+                            uintptr_t hp, uintptr_t t, int keras_eps, uintptr_t st) {
+    chk(fn_adam_flat_dev(P<float*>(p), P<const float*>(g), P<float*>(mm), P<float*>(v), P<void*>(pb), n,
+                         P<const float*>(hp), P<int*>(t), keras_eps, S(st)),
+        "adam_flat_dev");
   });
   m.def("adam_flat", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t pb, long long n, float lr,
                         float b1, float b2, float eps, float wd, float bc1, float bc2, float gscale, int keras_eps,

@@ -197,6 +197,45 @@ extern "C" int fn_adam_flat(float* p, const float* g, float* m, float* v, void* 
   return 0;
 }
 
+// Graph-capturable Adam: hyper-parameters and the step counter live in device
+// memory, so a captured training step replays with the current lr / step.
+// hp = {lr, b1, b2, eps, wd, grad_scale}; *t is incremented by the 1-thread
+// kernel that precedes this one in the same stream.
+__global__ void step_inc_kernel(int* t) { *t += 1; }
+
+__global__ __launch_bounds__(256) void adam_flat_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                            float* __restrict__ m, float* __restrict__ v,
+                                                            bf16* __restrict__ pb, long long n,
+                                                            const float* __restrict__ hp, const int* __restrict__ t,
+                                                            int keras_eps) {
+  const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], gscale = hp[5];
+  const float tf = (float)*t;
+  const float bc1 = 1.f - powf(b1, tf), bc2 = 1.f - powf(b2, tf);
+  const float rb2 = rsqrtf(bc2);
+  const float lr_t = lr * sqrtf(bc2) / bc1;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const float gi = g[i] * gscale;
+    float pi = p[i];
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    if (wd != 0.f) pi -= lr * wd * pi;
+    pi -= keras_eps ? lr_t * mi / (sqrtf(vi) + eps) : lr * (mi / bc1) / (sqrtf(vi) * rb2 + eps);
+    p[i] = pi;
+    if (pb) pb[i] = f2bf(pi);
+  }
+}
+
+extern "C" int fn_adam_flat_dev(float* p, const float* g, float* m, float* v, void* pb, long long n, const float* hp,
+                                int* t, int keras_eps, hipStream_t st) {
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, t);
+  hipLaunchKernelGGL(adam_flat_dev_kernel, dim3(blocks_for(n)), dim3(256), 0, st, p, g, m, v, (bf16*)pb, n, hp, t,
+                     keras_eps);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int fn_sgd_flat(float* p, const float* g, float* buf, void* pb, long long n, float lr, float momentum,
                            float wd, int nesterov, float gscale, hipStream_t st) {
   hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks_for(n)), dim3(256), 0, st, p, g, buf, (bf16*)pb, n, lr, momentum,

@@ -30,8 +30,34 @@ class FlatAdam:
         self.keras_eps = keras_eps
         self.shadow = shadow
         self.t = 0
+        self._dev = None     # (hp, t) device state of the graph-capturable form
+
+    # ------------------------------------------------------------ graph mode
+    def enable_device_state(self) -> None:
+        """Keep lr / betas / step on the device so a captured step replays correctly."""
+        if self._dev is None:
+            hp = torch.tensor([self.lr, self.b1, self.b2, self.eps, self.wd, 1.0], dtype=torch.float32,
+                              device=self.p.device)
+            t = torch.tensor([self.t], dtype=torch.int32, device=self.p.device)
+            self._dev = (hp, t)
+
+    def sync_device_state(self, grad_scale: float = 1.0) -> None:
+        """Push host-side hyper-parameter changes (e.g. an lr callback) to the device copy."""
+        if self._dev is not None:
+            self._dev[0].copy_(torch.tensor([self.lr, self.b1, self.b2, self.eps, self.wd, grad_scale]))
+
+    def step_device(self) -> None:
+        """One Adam step entirely driven by device state (safe inside hipGraph capture)."""
+        hp, t = self._dev
+        _native.kernels().adam_flat_dev(self.p.data_ptr(), self.g.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                                        _native.ptr(self.shadow), self.p.numel(), hp.data_ptr(), t.data_ptr(),
+                                        int(self.keras_eps), _native.stream(self.p))
 
     def step(self, grad_scale: float = 1.0) -> None:
+        if self._dev is not None and _native.use_native(self.p):
+            self.t += 1
+            self.step_device()
+            return
         self.t += 1
         bc1 = 1.0 - self.b1 ** self.t
         bc2 = 1.0 - self.b2 ** self.t
@@ -64,6 +90,9 @@ class FlatAdam:
         self.v.copy_(sd["v"])
         self.t = int(sd["t"])
         self.lr = float(sd.get("lr", self.lr))
+        if self._dev is not None:
+            self._dev[1].fill_(self.t)
+            self.sync_device_state()
 
 
 class FlatSGD:

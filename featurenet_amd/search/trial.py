@@ -48,6 +48,7 @@ class TrialConfig:
     synthetic_sizes: tuple = (6000, 1000)
     verbose: int = 0
     inject: dict = field(default_factory=dict)
+    graph: bool = True          # hipGraph-captured training steps on GPU (launch-bound small candidates)
 
     def to_dict(self) -> dict:
         return asdict(self)
@@ -79,7 +80,7 @@ def run_trial(spec: ModelSpec, cfg: TrialConfig, device=None) -> ModelSpec:
         spec.nb_params, spec.nb_layers, spec.nb_flops = model.nb_params, model.nb_layers, model.flops_per_sample
         if fault == "oom":
             raise TrainingFailed("out of device memory: injected")
-        trainer = Trainer(model, lr=cfg.lr, device=device, meta={"model_kind": "candidate", "spec": spec.to_dict(),
+        trainer = Trainer(model, lr=cfg.lr, device=device, graph=cfg.graph, meta={"model_kind": "candidate", "spec": spec.to_dict(),
                                                                   "input_shape": list(ds.input_shape),
                                                                   "num_classes": ds.num_classes,
                                                                   "compat": cfg.compat,

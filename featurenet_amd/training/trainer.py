@@ -36,6 +36,14 @@ from .data import DeviceLoader
 from .flat import FlatParams
 
 
+def _has_dropout(model: torch.nn.Module) -> bool:
+    """Active dropout draws a fresh mask every step (host-side seed), so it cannot replay from a graph."""
+    prog = getattr(model, "prog", None)
+    if prog is not None and any(kind == "dropout" and arg and float(arg) > 0 for kind, arg, _ in prog):
+        return True
+    return any(float(getattr(m, "dropout", 0) or 0) > 0 for m in model.modules())
+
+
 class TrainingFailed(RuntimeError):
     pass
 
@@ -54,7 +62,8 @@ class History:
 class Trainer:
     def __init__(self, model: torch.nn.Module, optimizer: str = "adam", lr: float = 1e-3, device=None,
                  keras_eps: bool = True, weight_decay: float = 0.0, momentum: float = 0.9,
-                 label_smoothing: float = 0.0, bucket_mb: float = 32.0, meta: dict | None = None):
+                 label_smoothing: float = 0.0, bucket_mb: float = 32.0, meta: dict | None = None,
+                 graph: bool = False):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -75,6 +84,14 @@ class Trainer:
         self.stop_training = False
         self.meta = dict(meta or {})
         self.history = History()
+        # hipGraph capture of the whole training step (forward + backward + Adam):
+        # NAS candidates on 28x28 / 32x32 inputs are launch-bound, one replay
+        # replaces ~100 kernel launches.  Single process, Adam, no dropout.
+        self.graph_mode = bool(graph) and self.device.type == "cuda" and self.world == 1 and \
+            optimizer == "adam" and not _has_dropout(self.model)
+        self._graph = None
+        self._gkey = None
+        self._gwarm = 0
 
     # ------------------------------------------------------------------ lr
     def get_lr(self) -> float:
@@ -82,6 +99,8 @@ class Trainer:
 
     def set_lr(self, lr: float) -> None:
         self.opt.lr = float(lr)
+        if self.graph_mode:
+            self.opt.sync_device_state()
 
     # ------------------------------------------------------------------ steps
     def _prep(self, xb: torch.Tensor) -> torch.Tensor:
@@ -91,7 +110,7 @@ class Trainer:
             xb = xb.float()
         return xb
 
-    def train_step(self, xb: torch.Tensor, yb: torch.Tensor):
+    def _eager_step(self, xb: torch.Tensor, yb: torch.Tensor):
         self.flat.zero_grad()
         logits = self.model(self._prep(xb))
         loss, correct = softmax_xent(logits, yb, self.label_smoothing, with_correct=True)
@@ -99,6 +118,37 @@ class Trainer:
         scale = self.bucketer.finish()
         self.opt.step(grad_scale=scale)
         return loss.detach(), correct
+
+    def train_step(self, xb: torch.Tensor, yb: torch.Tensor):
+        if not self.graph_mode:
+            return self._eager_step(xb, yb)
+        key = (tuple(xb.shape), xb.dtype, tuple(yb.shape))
+        if self._graph is not None:
+            if key != self._gkey:                      # e.g. the last partial batch of an epoch
+                return self._eager_step(xb, yb)
+            self._sx.copy_(xb)
+            self._sy.copy_(yb)
+            self._graph.replay()
+            self.opt.t += 1
+            return self._gloss, self._gcorr
+        self.opt.enable_device_state()
+        if self._gwarm < 3:                            # warm caches / kernel tables before capture
+            self._gwarm += 1
+            return self._eager_step(xb, yb)
+        self._sx, self._sy = xb.clone(), yb.clone()
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g):
+            self.flat.zero_grad()
+            logits = self.model(self._prep(self._sx))
+            loss, correct = softmax_xent(logits, self._sy, self.label_smoothing, with_correct=True)
+            loss.backward()
+            self.opt.step_device()
+            self._gloss, self._gcorr = loss.detach(), correct
+        self._graph, self._gkey = g, key
+        self._graph.replay()                           # capture records only; run this batch now
+        self.opt.t += 1
+        return self._gloss, self._gcorr
 
     def _reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
