@@ -103,6 +103,23 @@ def build_runtime(force: bool = False, workers: int | None = None, verbose: bool
     return out
 
 
+def build_runtime_sanitized(out_dir: str | Path | None = None, sanitizers: str = "address,undefined") -> Path:
+    """The host runtime ``_rt`` built with -fsanitize (ASan + UBSan) into its own
+    directory (sanitizers on host code; GPU sanitizers are not used).
+    Load it in a fresh process with ``LD_PRELOAD=$(g++ -print-file-name=libasan.so)``."""
+    src_dir = PKG / "csrc" / "runtime"
+    out_dir = Path(out_dir or (ROOT / "build" / "asan"))
+    out_dir.mkdir(parents=True, exist_ok=True)
+    out = out_dir / f"_rt{EXT}"
+    cxx = os.environ.get("CXX", "g++")
+    flags = ["-O1", "-g", "-std=c++17", "-fPIC", f"-fsanitize={sanitizers}", "-fno-omit-frame-pointer",
+             "-fno-sanitize-recover=undefined"] + _py_includes()
+    srcs = sorted(src_dir.glob("*.cpp"))
+    if not out.exists() or any(_newer(s, out) for s in srcs):
+        _run([cxx, *flags, "-shared", *map(str, srcs), "-o", str(out), "-lpthread"])
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = True) -> None:
     build_runtime(force=force, verbose=verbose)
     build_kernels(force=force, verbose=verbose)
