@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Top-1 accuracy of FeatureNet-3D on the procedural machining-feature set.
+
+The second half of BASELINE.json's metric ("samples/sec ...; top-1 acc"):
+train FeatureNet-3D (64^3, 24 classes, bf16 kernels, Adam 1e-3, batch 128)
+from random init on the procedural voxel dataset of ``csrc/runtime/voxel.cpp``
+(24 machining-feature classes carved into a stock block, random orientation),
+then report held-out top-1 accuracy, the training throughput of the whole run
+(data loading and bit-unpacking included) and a checkpoint round trip
+through ``classify()``.
+
+    python bench/accuracy.py --train-per-class 400 --test-per-class 50 --epochs 6
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench/accuracy.py
+
+The dataset is synthetic (no network for the real FeatureNet CAD set); the
+reference repository publishes no accuracy for this task, so the number is
+first-party ("parity unpinned").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=64)
+    ap.add_argument("--classes", type=int, default=24)
+    ap.add_argument("--train-per-class", type=int, default=400)
+    ap.add_argument("--test-per-class", type=int, default=50)
+    ap.add_argument("--epochs", type=int, default=6)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args()
+
+    import featurenet_amd as fn
+    from featurenet_amd.parallel.ddp import init_from_env
+    from featurenet_amd.training.data import voxel_dataset
+
+    rank, world, local = init_from_env()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    t0 = time.time()
+    ds = voxel_dataset(a.train_per_class * a.classes, a.test_per_class * a.classes, size=a.size,
+                       num_classes=a.classes, seed=a.seed)
+    t_gen = time.time() - t0
+    ckpt = os.path.join(tempfile.mkdtemp(), "fn3d.fnk")
+    t0 = time.time()
+    res = fn.train("featurenet3d", data=ds, epochs=a.epochs, batch_size=a.batch, lr=a.lr, seed=a.seed,
+                   save_path=ckpt if rank == 0 else None, verbose=1 if rank == 0 else 0, callbacks=[])
+    t_train = time.time() - t0
+    hist = res.history
+    out = {
+        "metric": "top-1 accuracy (64^3 voxel, 24-class, procedural machining features)",
+        "value": round(res.accuracy, 4),
+        "unit": "fraction",
+        "n_gpus": world,
+        "epochs": a.epochs,
+        "train_samples": len(ds.y_train),
+        "test_samples": len(ds.y_test),
+        "train_acc_last_epoch": round(hist["acc"][-1], 4),
+        "val_acc_per_epoch": [round(v, 4) for v in hist.get("val_acc", [])],
+        "loss_per_epoch": [round(v, 4) for v in hist["loss"]],
+        "train_samples_per_s_per_epoch": [round(v, 1) for v in hist["samples_per_s"]],
+        "train_wall_s": round(t_train, 2),
+        "datagen_s": round(t_gen, 2),
+        "dtype": "bf16",
+        "data": "synthetic procedural voxels (featurenet_amd._rt.generate_voxels), random-init weights",
+        "config": {"model": "FeatureNet-3D", "global_batch": a.batch * world, "optimizer": "adam",
+                   "lr": a.lr, "parallelism": f"dp{world}"},
+    }
+    if rank == 0:
+        labels, _ = fn.classify(ckpt, ds.x_test, packed_size=a.size)
+        out["classify_roundtrip_acc"] = round(float((labels == np.asarray(ds.y_test)).mean()), 4)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -92,13 +92,13 @@ def _resolve_data(data, batch_size) -> Dataset:
 def train(arch="featurenet3d", data="voxel", epochs: int = 12, batch_size: int = 128, lr: float = 1e-3,
           optimizer: str = "adam", device=None, callbacks=None, augment: bool = False, scheduler: bool = False,
           save_path: str | None = None, compat: bool = True, fill_defaults: bool = False, verbose: int = 1,
-          seed: int = 0, robustness: list | None = None, graph: bool = True) -> TrainResult:
+          seed: int = 0, robustness: list | None = None, graph: bool = True, precise_bn: int = 32) -> TrainResult:
     """Build + train + evaluate one architecture (the reference ``TensorflowGenerator`` pipeline)."""
     torch.manual_seed(seed)
     ds = _resolve_data(data, batch_size)
     model, meta = build_model(arch, ds.input_shape, ds.num_classes, compat=compat, fill_defaults=fill_defaults)
     meta.update({"dataset": ds.name, "synthetic_data": ds.synthetic})
-    trainer = Trainer(model, optimizer=optimizer, lr=lr, device=device, meta=meta, graph=graph)
+    trainer = Trainer(model, optimizer=optimizer, lr=lr, device=device, meta=meta, graph=graph, precise_bn=precise_bn)
     cbs = list(callbacks) if callbacks is not None else reference_callbacks(scheduler)
     packed = ds.input_shape[0] if ds.packed else None
     hist = trainer.fit(ds.x_train, ds.y_train, epochs=epochs, batch_size=batch_size,

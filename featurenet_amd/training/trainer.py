@@ -36,6 +36,17 @@ from .data import DeviceLoader
 from .flat import FlatParams
 
 
+def bn_modules(model: torch.nn.Module) -> list[tuple[torch.nn.Module, str]]:
+    """(module, momentum attribute) of every layer that keeps BN running statistics."""
+    out = []
+    for m in model.modules():
+        if isinstance(getattr(m, "running_mean", None), torch.Tensor):
+            attr = "bn_momentum" if hasattr(m, "bn_momentum") else "momentum" if hasattr(m, "momentum") else None
+            if attr is not None:
+                out.append((m, attr))
+    return out
+
+
 def _has_dropout(model: torch.nn.Module) -> bool:
     """Active dropout draws a fresh mask every step (host-side seed), so it cannot replay from a graph."""
     prog = getattr(model, "prog", None)
@@ -63,7 +74,7 @@ class Trainer:
     def __init__(self, model: torch.nn.Module, optimizer: str = "adam", lr: float = 1e-3, device=None,
                  keras_eps: bool = True, weight_decay: float = 0.0, momentum: float = 0.9,
                  label_smoothing: float = 0.0, bucket_mb: float = 32.0, meta: dict | None = None,
-                 graph: bool = False):
+                 graph: bool = False, precise_bn: int = 32):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -82,6 +93,13 @@ class Trainer:
         self.bucketer = GradBucketer(self.flat, bucket_mb=bucket_mb)
         self.bucketer.broadcast_from(0)
         self.stop_training = False
+        # PreciseBN: before validation / at the end of training, BN running statistics
+        # are re-estimated as the plain average over this many training batches at the
+        # current weights (EMA running stats lag far behind the batch statistics while
+        # Adam moves the weights quickly; the eval-mode accuracy then collapses).
+        # 0 keeps the reference's EMA statistics (Keras BatchNormalization semantics).
+        self.precise_bn = int(precise_bn) if bn_modules(self.model) else 0
+        self._bn_fresh = False
         self.meta = dict(meta or {})
         self.history = History()
         # hipGraph capture of the whole training step (forward + backward + Adam):
@@ -190,6 +208,9 @@ class Trainer:
                 logs = {"loss": float(stats[0] / max(stats[2], 1)), "acc": float(stats[1] / max(stats[2], 1)),
                         "lr": self.get_lr(), "time": time.time() - t0,
                         "samples_per_s": float(stats[2]) / max(time.time() - t0, 1e-9)}
+                self._bn_fresh = False
+                if self.precise_bn and (validation_data is not None or epoch == epochs - 1):
+                    self.recalibrate_bn(x, y, self.precise_bn, batch_size, packed_size, seed + epoch)
                 if validation_data is not None:
                     vl, va = self.evaluate(*validation_data, batch_size=batch_size, packed_size=packed_size)
                     logs["val_loss"], logs["val_acc"] = vl, va
@@ -204,6 +225,8 @@ class Trainer:
                     cb.on_epoch_end(self, epoch, logs)
                 if self.stop_training:
                     break
+            if self.precise_bn and not self._bn_fresh:    # stopped early without validation
+                self.recalibrate_bn(x, y, self.precise_bn, batch_size, packed_size, seed)
         except torch.cuda.OutOfMemoryError as e:   # reference: ResourceExhaustedError -> candidate dropped
             raise TrainingFailed(f"out of device memory: {e}") from e
         finally:
@@ -211,6 +234,42 @@ class Trainer:
                 cb.on_train_end(self)
         self.meta["train_time_s"] = time.time() - t_start
         return self.history
+
+    @torch.no_grad()
+    def recalibrate_bn(self, x, y, batches: int = 32, batch_size: int = 128, packed_size: int | None = None,
+                       seed: int = 0) -> int:
+        """PreciseBN: set every BN layer's running mean / var to the average of the batch
+        statistics over ``batches`` shuffled training batches (train-mode forward, no
+        gradients, momentum 1/(k+1)); replicas average their estimates.  Returns the
+        number of batches used."""
+        mods = bn_modules(self.model)
+        if not mods or batches <= 0:
+            return 0
+        saved = [getattr(m, a) for m, a in mods]
+        was_training = self.model.training
+        self.model.train()
+        loader = DeviceLoader(x, y, batch_size, self.device, shuffle=True, packed_size=packed_size,
+                              rank=self.rank, world=self.world, seed=seed + 7919)
+        k = 0
+        try:
+            for xb, _ in loader:
+                if k >= batches:
+                    break
+                for m, a in mods:
+                    setattr(m, a, 1.0 / (k + 1))
+                self.model(self._prep(xb))
+                k += 1
+        finally:
+            for (m, a), v in zip(mods, saved):
+                setattr(m, a, v)
+            self.model.train(was_training)
+        if self.world > 1 and k:
+            for m, _ in mods:
+                for buf in (m.running_mean, m.running_var):
+                    t = self._reduce(buf.detach().clone())
+                    buf.copy_(t / self.world)
+        self._bn_fresh = True
+        return k
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()

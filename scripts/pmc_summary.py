@@ -1,6 +1,19 @@
-"""Aggregate a rocprofv3 --pmc counter CSV per (kernel, grid): derived utilisation ratios."""
+"""Aggregate a rocprofv3 --pmc counter CSV per (kernel, grid) into utilisation ratios.
+
+Ratios are normalised by the kernel's own duration (End-Start of each dispatch)
+at an assumed shader clock (``--ghz``, profiled runs hold ~2.0-2.1 GHz) over
+all 256 CUs / 1024 SIMDs of an MI355X:
+
+* MFMA util   = SQ_VALU_MFMA_BUSY_CYCLES / (cycles x 1024 SIMDs)
+* LDS util    = SQ_LDS_IDX_ACTIVE / (cycles x 256 CUs)
+* bank confl. = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+* wait / wave = SQ_WAIT_ANY / SQ_WAVE_CYCLES  (waves parked on s_waitcnt / barrier)
+* stall/wave  = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (issue stalls)
+
+usage: python scripts/pmc_summary.py gpurun_out/pmc/pmc_counter_collection.csv [--ghz 2.1]
+"""
+import argparse
 import csv
-import re
 import sys
 from collections import defaultdict
 
@@ -8,25 +21,32 @@ sys.path.insert(0, __file__.rsplit("/", 1)[0])
 from prof_summary import short  # noqa: E402
 
 
-def main(path):
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("--ghz", type=float, default=2.1)
+    ap.add_argument("--top", type=int, default=16)
+    a = ap.parse_args()
     agg = defaultdict(lambda: defaultdict(float))
-    with open(path) as f:
+    durs = defaultdict(dict)
+    with open(a.csv) as f:
         for r in csv.DictReader(f):
-            name = short(r.get("Kernel_Name", ""))
-            grid = r.get("Grid_Size", r.get("Grid_Size_X", ""))
-            key = (name, grid)
+            key = (short(r.get("Kernel_Name", "")), r.get("Grid_Size", ""))
             agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
-            agg[key]["_n"] += 1
-    print("| kernel | grid | MFMA busy / busy | LDS active / busy | LDS bank-conflict / LDS active | wait LDS / wave cyc | wait any / wave cyc |")
-    print("|---|---|---|---|---|---|---|")
-    for (name, grid), c in sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))[:20]:
-        busy = c.get("SQ_BUSY_CYCLES", 0) or 1
+            durs[key][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    print(f"Counters normalised at {a.ghz} GHz over 1024 SIMDs / 256 CUs.\n")
+    print("| kernel | grid (threads) | time ms | MFMA util | LDS util | bank conflict / LDS cyc | wait / wave cyc | issue stall / wave cyc |")
+    print("|---|---|---|---|---|---|---|---|")
+    rows = sorted(agg.items(), key=lambda kv: -sum(durs[kv[0]].values()))[: a.top]
+    for (name, grid), c in rows:
+        ns = sum(durs[(name, grid)].values())
+        cyc = max(ns * a.ghz, 1.0)
         wc = c.get("SQ_WAVE_CYCLES", 0) or 1
-        lds = c.get("SQ_LDS_IDX_ACTIVE", 0) or 1
-        print(f"| `{name}` | {grid} | {c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / busy:.3f} | "
-              f"{c.get('SQ_LDS_IDX_ACTIVE', 0) / busy:.3f} | {c.get('SQ_LDS_BANK_CONFLICT', 0) / lds:.3f} | "
-              f"{c.get('SQ_WAIT_INST_LDS', 0) / wc:.3f} | {c.get('SQ_WAIT_ANY', 0) / wc:.3f} |")
+        lds = c.get("SQ_LDS_IDX_ACTIVE", 0)
+        print(f"| `{name}` | {grid} | {ns / 1e6:.3f} | {c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / (cyc * 1024):.3f} | "
+              f"{lds / (cyc * 256):.3f} | {c.get('SQ_LDS_BANK_CONFLICT', 0) / max(lds, 1):.3f} | "
+              f"{c.get('SQ_WAIT_ANY', 0) / wc:.3f} | {c.get('SQ_WAIT_INST_ANY', 0) / wc:.3f} |")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main()

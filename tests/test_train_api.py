@@ -138,3 +138,47 @@ def test_segmentation_head_trains_per_voxel():
     assert 0.0 <= res.accuracy <= 1.0
     assert res.accuracy > 0.9
     assert all(math.isfinite(v) for v in res.history["loss"])
+
+
+def test_precise_bn_recalibration_is_batch_average():
+    """PreciseBN: running stats become the plain average of the per-batch statistics."""
+    from featurenet_amd.models.layers import BatchNorm, Dense
+    from featurenet_amd.training.trainer import bn_modules
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.bn = BatchNorm(4, momentum=0.1)
+            self.fc = Dense(4, 3)
+
+        def forward(self, x):
+            return self.fc(self.bn(x))
+
+    torch.manual_seed(0)
+    x = (torch.randn(32, 4) * torch.tensor([1.0, 2.0, 3.0, 4.0]) + torch.tensor([5.0, -1.0, 0.0, 2.0])).numpy()
+    y = np.zeros(32, dtype=np.int64)
+    tr = Trainer(Net(), device="cpu", precise_bn=4)
+    assert [type(m).__name__ for m, _ in bn_modules(tr.model)] == ["BatchNorm"]
+    n = tr.recalibrate_bn(x, y, batches=4, batch_size=8)
+    assert n == 4
+    assert tr.model.bn.momentum == 0.1                       # momentum restored
+    xt = torch.from_numpy(x)
+    torch.testing.assert_close(tr.model.bn.running_mean, xt.mean(0), rtol=1e-4, atol=1e-4)
+    # average of unbiased per-batch variances (batches are a permutation of the data)
+    perm_var = tr.model.bn.running_var
+    assert torch.all(perm_var > 0.5 * xt.var(0)) and torch.all(perm_var < 1.5 * xt.var(0))
+
+
+def test_fit_recalibrates_before_validation():
+    torch.manual_seed(0)
+    from featurenet_amd.training.data import voxel_dataset
+
+    ds = voxel_dataset(16, 8, size=32, num_classes=2, seed=3)
+    model = FeatureNet3D(FeatureNet3DConfig(input_size=32, num_classes=2))
+    tr = Trainer(model, device="cpu", precise_bn=2)
+    calls = []
+    orig = tr.recalibrate_bn
+    tr.recalibrate_bn = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    tr.fit(ds.x_train, ds.y_train, epochs=2, batch_size=8, validation_data=(ds.x_test, ds.y_test),
+           packed_size=32, verbose=0)
+    assert len(calls) == 2 and tr._bn_fresh
