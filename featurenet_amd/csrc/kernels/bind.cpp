@@ -28,6 +28,7 @@ int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, h
 int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
 int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, hipStream_t);
+int fn_s2d_pack(const void*, void*, const int*, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
                    hipStream_t);
 int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
@@ -91,6 +92,10 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 16, "conv_halo_wgrad");
     chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x, S(st)),
         "conv_halo_wgrad");
+  });
+  m.def("s2d_pack", [](uintptr_t x, uintptr_t out, std::vector<int> geom, uintptr_t st) {
+    need(geom, 12, "s2d_pack");
+    chk(fn_s2d_pack(P<const void*>(x), P<void*>(out), geom.data(), S(st)), "s2d_pack");
   });
   m.def("conv_halo_f8", [](uintptr_t src, uintptr_t wt, uintptr_t scale, uintptr_t bias, uintptr_t out,
                            float inv_out_scale, uintptr_t toffs, std::vector<int> geom, int ncol, int out_f8, int relu,

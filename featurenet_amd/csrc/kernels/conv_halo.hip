@@ -47,7 +47,7 @@ struct HaloGeom {
 // while the current job computes (written to LDS at the job boundary), and
 // weight stages are prefetched two stages ahead, so neither halo nor weight
 // latency sits on the critical path.
-template <int BN, int ACT, bool HAS_BIAS, bool STATS>
+template <int BN, int ACT, bool HAS_BIAS, bool STATS, int CS>
 __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wt,
                                                            const float* __restrict__ bias, bf16* __restrict__ out,
                                                            float* __restrict__ stats, const int* __restrict__ toffs,
@@ -56,22 +56,26 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   // 8 waves = 4 row blocks x 2: BN=32 splits every stage's 4 k-steps between
   // the two waves of a row block (partials reduced per tile); BN=64 gives each
   // of them 32 of the 64 columns.  Either way a wave owns 64 rows x 32 cols.
+  // CS = channels per halo slice: 16 (k-step = 2 taps x 16 ch) or 8 (k-step =
+  // 4 taps x 8 ch, for 8-channel inputs such as the space-to-depth stem).
   constexpr bool KSPLIT = BN == 32;
   constexpr int NT = 2;
-  constexpr int B_STAGE = BN * H_BKS;            // elements (128 k = 8 taps x 16 channels)
+  constexpr int CPP = CS / 8;                    // 16-B chunks per halo position
+  constexpr int TPS = H_BKS / CS;                // taps per weight stage
+  constexpr int B_STAGE = BN * H_BKS;            // elements (128 k = TPS taps x CS channels)
   constexpr int B_CHUNKS = BN * (H_BKS / 8);
   constexpr int B_PER_T = (B_CHUNKS + H_NTHR - 1) / H_NTHR;
   constexpr int LDO = BN + 8;
 
   const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
   const int HP = HD * HH * HW;                   // halo positions
-  const int nchunk = HP * 2;
+  const int nchunk = HP * CPP;
   const int T = g.KD * g.KH * g.KW;
-  const int T8 = (T + 7) & ~7;
-  const int spp = T8 >> 3;                       // 128-k stages per channel pass
-  const int npass = g.C >> 4;
+  const int Tp = (T + TPS - 1) / TPS * TPS;
+  const int spp = Tp / TPS;                      // 128-k stages per channel pass
+  const int npass = g.C / CS;
   const int nq = spp * npass;
-  const int ldw = npass * T8 * 16;
+  const int ldw = npass * Tp * CS;
   const int rows = g.TD * g.TH * g.OW;
   const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
   const int ntiles = g.N * tdn * thn;
@@ -79,6 +83,8 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   bf16* halo = reinterpret_cast<bf16*>(dsm);                      // also the epilogue staging area
   bf16* Bs = reinterpret_cast<bf16*>(dsm + region_bytes);
   int* posinfo = reinterpret_cast<int*>(dsm + region_bytes + 2 * B_STAGE * 2);  // packed (hd, hh, hw)
+  int* toffs_s = posinfo + HP;                                    // [Tp] tap offsets (LDS: no scalar
+                                                                  // loads inside the k-loop)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wrow = wave & 3;                                   // 64-row block of the tile
@@ -95,6 +101,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 
   for (int pos = tid; pos < HP; pos += H_NTHR)
     posinfo[pos] = ((pos / (HW * HH)) << 20) | (((pos / HW) % HH) << 10) | (pos % HW);
+  for (int t = tid; t < Tp; t += H_NTHR) toffs_s[t] = toffs[t];
   int hbase[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
@@ -110,11 +117,11 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   auto halo_src = [&](int job, int c, const bf16*& base, int& off) -> bool {
     const int tile = t_begin + job / npass, p = job % npass;
     const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
-    const int info = posinfo[c < nchunk ? c >> 1 : 0];
+    const int info = posinfo[c < nchunk ? c / CPP : 0];
     const int gd = td_i * g.TD - g.pd + (info >> 20), gh = th_i * g.TH - g.ph + ((info >> 10) & 1023);
     const int gw = (info & 1023) - g.pw;
-    base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * 16;
-    off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c & 1) * 8;
+    base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * CS;
+    off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c % CPP) * 8;
     return c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
            (unsigned)gw < (unsigned)g.IW;
   };
@@ -122,15 +129,15 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
     const int tile = t_begin + job / npass, p = job % npass;
     const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
     const int dlo = td_i * g.TD - g.pd, hlo = th_i * g.TH - g.ph;
-    const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * 16;
+    const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * CS;
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
       const int c = i * H_NTHR + tid;
-      const int info = posinfo[c < nchunk ? c >> 1 : 0];
+      const int info = posinfo[c < nchunk ? c / CPP : 0];
       const int gd = dlo + (info >> 20), gh = hlo + ((info >> 10) & 1023), gw = (info & 1023) - g.pw;
       const bool ok = c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
                       (unsigned)gw < (unsigned)g.IW;
-      const int off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c & 1) * 8;
+      const int off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c % CPP) * 8;
       const uint4 x = *(const uint4*)(base + (ok ? off : 0));
       hreg[i] = ok ? x : make_uint4(0, 0, 0, 0);
     }
@@ -178,7 +185,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int idx = tid + i * H_NTHR;
-      if (idx < B_CHUNKS) {
+      if (B_CHUNKS % H_NTHR == 0 || idx < B_CHUNKS) {
         const int r = idx >> 4, c = idx & 15;
         *(uint4*)(b + r * H_BKS + ((c ^ (r & 15)) << 3)) = srcr[i];
       }
@@ -196,7 +203,6 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   write_b(0, rbA);
   load_b(1, rbA);
 
-  const int mt_live = rows - wrow * 64;   // rows of this wave inside a tile (uniform)
   int s = 0;                              // global stage counter
   for (int job = 0; job < njobs; ++job) {
     __syncthreads();                      // previous halo / epilogue staging fully consumed
@@ -205,30 +211,30 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
     if (job + 1 < njobs) prefetch_halo(job + 1);   // lands during this job's MFMAs
     for (int local = 0; local < spp; ++local, ++s) {
       const bf16* b = Bs + (s & 1) * B_STAGE;
-      const int* tp = toffs + local * 8 + (KSPLIT ? khalf * 4 : 0);  // uniform -> scalar loads
+      // lane group lg reads tap lg>>1 / channel half lg&1 (CS = 16) or tap lg (CS = 8)
+      const int* tp = toffs_s + local * TPS + (KSPLIT ? khalf * (TPS / 2) : 0) + (CS == 16 ? (lg >> 1) : lg);
 #pragma unroll
       for (int kk = 0; kk < (KSPLIT ? 2 : 4); ++kk) {
         const int ks = (KSPLIT ? khalf * 2 : 0) + kk;
-        const int t0 = tp[kk * 2], t1 = tp[kk * 2 + 1];
-        const int toff = (lg & 2) ? t1 : t0;
+        const int toff = tp[kk * (32 / CS)];
+        const int hsub = CS == 16 ? (lg & 1) * 8 : 0;
         bf16x8 fa[4], fb[NT];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
-          fa[mt] = *(const bf16x8*)(halo + (size_t)(hbase[mt] + toff) * 16 + (lg & 1) * 8);
+          fa[mt] = *(const bf16x8*)(halo + (size_t)(hbase[mt] + toff) * CS + hsub);
         const int ch = ks * 4 + lg;
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           const int row = ccol + nt * 16 + lr;
           fb[nt] = *(const bf16x8*)(b + row * H_BKS + ((ch ^ (row & 15)) << 3));
         }
+        // every row block runs all 4 MFMA row tiles (no branch in the k-loop: rows past
+        // the tile read a valid halo position and are dropped by the epilogue)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          if (mt * 16 < mt_live) {
+        for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
-          }
-        }
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
       }
       write_b((s + 1) & 1, rbA);          // stage s+1 (its buffer's last readers passed the previous barrier)
       load_b(s + 2, rbA);                 // a whole stage of MFMAs covers its latency
@@ -356,27 +362,36 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
 // halo / dy chunks per thread prefetched into registers for the NEXT tile
 #define WG_HC(MT) ((MT) <= 2 ? 8 : 4)
 
-template <int MT>
+// CS = channels per halo slice (grid.z walks C/CS slices).  CS = 16: the MFMA
+// N axis is the slice's 16 input channels, one accumulator per (tap, co
+// block).  CS = 8: the N axis is (tap pair, 8 channels) -- lanes p = 0,1 of a
+// transposed-read quad fetch tap 2j, lanes p = 2,3 tap 2j+1 -- so a wave covers
+// the same taps with half the accumulators.
+template <int MT, int CS>
 __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __restrict__ dy,
                                                                  const bf16* __restrict__ src,
                                                                  float* __restrict__ dw, HaloGeom g, int Cout) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  constexpr int TPW = MT == 1 ? 16 : 32 / MT;   // taps per wave (acc <= 128 VGPRs)
+  // 16x16 accumulator column blocks per (wave, co block); both slice widths give a
+  // wave the same taps (CS = 8 packs two taps per block, so half the blocks)
+  constexpr int NACC = (MT == 1 ? 16 : 32 / MT) / (16 / CS);
+  constexpr int TPW = CS == 16 ? NACC : 2 * NACC;   // taps per wave
+  constexpr int CPP = CS / 8;
   constexpr int BCO = MT * 16;
   constexpr int LDY = BCO + 16;            // conflict-free transposed reads (as igemm wgrad)
   constexpr int YC = BCO / 8;              // 16-B chunks per dy row
   constexpr int HC = WG_HC(MT);
   const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
   const int HP = HD * HH * HW;
-  const int nchunk = HP * 2;
+  const int nchunk = HP * CPP;
   const int T = g.KD * g.KH * g.KW;
   const int rows = g.TD * g.TH * g.OW;
   const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
   const int ntiles = g.N * tdn * thn;
 
   bf16* Ys = reinterpret_cast<bf16*>(dsm);                                   // [256][LDY]
-  bf16* halo = reinterpret_cast<bf16*>(dsm + (size_t)H_BM * LDY * 2);        // [HP][16]
-  int* rowpos = reinterpret_cast<int*>(dsm + (size_t)H_BM * LDY * 2 + (size_t)HP * 32);  // [256]
+  bf16* halo = reinterpret_cast<bf16*>(dsm + (size_t)H_BM * LDY * 2);        // [HP][CS]
+  int* rowpos = reinterpret_cast<int*>(dsm + (size_t)H_BM * LDY * 2 + (size_t)HP * CS * 2);  // [256]
   int* rowinfo = rowpos + H_BM;                                               // packed (td, th, w) per row
   int* posinfo = rowinfo + H_BM;                                              // packed (hd, hh, hw) per position
 
@@ -423,10 +438,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   };
   auto halo_src = [&](int tile, int c, long long& off) -> bool {
     const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
-    const int info = posinfo[c < nchunk ? c >> 1 : 0];
+    const int info = posinfo[c < nchunk ? c / CPP : 0];
     const int gd = td_i * g.TD - g.pd + (info >> 20), gh = th_i * g.TH - g.ph + ((info >> 10) & 1023);
     const int gw = (info & 1023) - g.pw;
-    off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + slice * 16 + (c & 1) * 8;
+    off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + slice * CS + (c % CPP) * 8;
     return c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
            (unsigned)gw < (unsigned)g.IW;
   };
@@ -474,9 +489,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
     }
   };
 
-  f32x4 acc[TPW][MT];
+  f32x4 acc[NACC][MT];
 #pragma unroll
-  for (int i = 0; i < TPW; ++i)
+  for (int i = 0; i < NACC; ++i)
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -486,7 +501,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
     store(tile);
     __syncthreads();
     if (tile + 1 < t_end) prefetch(tile + 1);   // lands during this tile's MFMAs
-    const int kst = (rows + 31) >> 5;
+    const int kst = ntap > 0 ? (rows + 31) >> 5 : 0;   // waves past the last tap only stage
     for (int ks = 0; ks < kst; ++ks) {
       bf16x8 fa[MT];
       const int r_lo = ks * 32 + 4 * G + q, r_hi = r_lo + 16;
@@ -494,30 +509,45 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
       for (int mt = 0; mt < MT; ++mt)
         fa[mt] = tr_pair<MT>(Ys + r_lo * LDY + mt * 16 + 4 * p4, Ys + r_hi * LDY + mt * 16 + 4 * p4);
       const int plo = rowpos[r_lo], phi = rowpos[r_hi];
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        if (i < ntap) {
-          const bf16x8 fb = tr_pair<MT>(halo + (size_t)(plo + toff[i]) * 16 + 4 * p4,
-                                        halo + (size_t)(phi + toff[i]) * 16 + 4 * p4);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb, acc[i][mt], 0, 0, 0);
+      // no per-tap branch: dead taps (past T) read halo position offset 0 and
+      // their accumulators are never stored
+      auto read_b = [&](int i) -> bf16x8 {
+        if constexpr (CS == 16) {
+          return tr_pair<MT>(halo + (size_t)(plo + toff[i]) * 16 + 4 * p4,
+                             halo + (size_t)(phi + toff[i]) * 16 + 4 * p4);
+        } else {
+          const int to = (p4 & 2) ? toff[2 * i + 1] : toff[2 * i];
+          return tr_pair<MT>(halo + (size_t)(plo + to) * 8 + 4 * (p4 & 1),
+                             halo + (size_t)(phi + to) * 8 + 4 * (p4 & 1));
         }
+      };
+      // B fragments double-buffered in registers: tap i+1 is read while tap i's
+      // MFMAs run, so the LDS latency is not exposed once per tap
+      bf16x8 fb_next = read_b(0);
+#pragma unroll
+      for (int i = 0; i < NACC; ++i) {
+        const bf16x8 fb = fb_next;
+        if (i + 1 < NACC) fb_next = read_b(i + 1);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb, acc[i][mt], 0, 0, 0);
       }
     }
   }
-  // D[row=co][col=ci]: lane holds co = mt*16 + (lane>>4)*4 + r, ci = lane & 15
+  // D[row=co][col=n]: lane holds co = mt*16 + (lane>>4)*4 + r, n = lane & 15
+  // (CS=16: n = input channel; CS=8: n = (tap of the pair) * 8 + channel)
 #pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    if (i < ntap) {
-      const int t = tap0 + i;
+  for (int i = 0; i < NACC; ++i) {
+    const int t = CS == 16 ? tap0 + i : tap0 + 2 * i + ((lane & 15) >> 3);
+    const int ci = CS == 16 ? (lane & 15) : (lane & 7);
+    if (t < T && t - tap0 < ntap) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = mt * 16 + (lane >> 4) * 4 + r;
           if (co < Cout)
-            atomicAdd(dw + ((long long)co * T + t) * g.C + slice * 16 + (lane & 15), acc[i][mt][r]);
+            atomicAdd(dw + ((long long)co * T + t) * g.C + slice * CS + ci, acc[i][mt][r]);
         }
     }
   }
@@ -536,46 +566,51 @@ static HaloGeom parse_halo(const int* v) {
   return g;
 }
 
-static size_t halo_region_bytes(const HaloGeom& g, int BN) {
+static int halo_cs(int C) { return C % 16 == 0 ? 16 : (C % 8 == 0 ? 8 : 0); }
+
+static size_t halo_region_bytes(const HaloGeom& g, int BN, int CS) {
   const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
   size_t epi = (size_t)H_BM * (BN + 8) * 2 + 2 * H_NTHR * 4;
   if (epi < 32 * 1024) epi = 32 * 1024;          // split-K partial sums (one round)
-  const size_t r = hp * 32 > epi ? hp * 32 : epi;
+  const size_t r = hp * CS * 2 > epi ? hp * CS * 2 : epi;
   return (r + 15) & ~(size_t)15;
 }
 
-static size_t halo_lds_bytes(const HaloGeom& g, int BN) {
+static size_t halo_lds_bytes(const HaloGeom& g, int BN, int CS) {
   const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
-  return halo_region_bytes(g, BN) + 2 * (size_t)BN * H_BKS * 2 + hp * 4 + 16;
+  const size_t T = (size_t)g.KD * g.KH * g.KW;
+  return halo_region_bytes(g, BN, CS) + 2 * (size_t)BN * H_BKS * 2 + hp * 4 + (T + 15) / 16 * 64 + 16;
 }
 
-template <int BN, int ACT, bool HB, bool ST>
+template <int BN, int ACT, bool HB, bool ST, int CS>
 static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const bf16* s, const bf16* w,
                        const float* b, bf16* o, float* stats, const int* toffs, const HaloGeom& g, int Ncol) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_halo_kernel<BN, ACT, HB, ST>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_halo_kernel<BN, ACT, HB, ST, CS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST>), grid, dim3(H_NTHR), lds, st, s, w, b, o, stats, toffs, g,
-                     Ncol, region);
+  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST, CS>), grid, dim3(H_NTHR), lds, st, s, w, b, o, stats, toffs,
+                     g, Ncol, region);
   return 0;
 }
 
 static int g_num_cus = 0;
 
-// wt: [Ncol][C/16][T8][16] bf16 (taps padded to a multiple of 8); toffs: int [T8] halo
-// position offsets of the taps (0 for padding taps); returns 0 on success.
+// wt: [Ncol][C/CS][Tp][CS] bf16 (taps padded to a multiple of 128/CS), CS = 16 when
+// C % 16 == 0 else 8; toffs: int [>= Tp] halo position offsets of the taps (0 for
+// padding taps); returns 0 on success.
 extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, void* out, float* stats,
                             const int* toffs, const int* geom16, int Ncol, int act, hipStream_t st) {
   const HaloGeom g = parse_halo(geom16);
-  if (g.C % 16 != 0 || g.TD * g.TH * g.OW > H_BM || g.TD < 1 || g.TH < 1) return -2;
+  const int CS = halo_cs(g.C);
+  if (CS == 0 || g.TD * g.TH * g.OW > H_BM || g.TD < 1 || g.TH < 1) return -2;
   if (stats && act != ACT_NONE) return -1;
   const int BN = Ncol <= 32 ? 32 : 64;
-  const size_t lds = halo_lds_bytes(g, BN);
-  const int region = (int)halo_region_bytes(g, BN);
+  const size_t lds = halo_lds_bytes(g, BN, CS);
+  const int region = (int)halo_region_bytes(g, BN, CS);
   if (lds > 160 * 1024) return -4;
   if (g_num_cus == 0) {
     int dev = 0;
@@ -594,17 +629,22 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   bf16* o = (bf16*)out;
   const bool hb = bias != nullptr;
   int rc;
-#define HCASE(B, A, H, S) rc = launch_halo<B, A, H, S>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol)
-#define HBN(B)                                                   \
-  do {                                                           \
-    if (stats) HCASE(B, ACT_NONE, false, true);                  \
-    else if (act == ACT_NONE) { if (hb) HCASE(B, ACT_NONE, true, false); else HCASE(B, ACT_NONE, false, false); } \
-    else if (act == ACT_RELU) HCASE(B, ACT_RELU, true, false);    \
-    else if (act == ACT_TANH) HCASE(B, ACT_TANH, true, false);    \
-    else HCASE(B, ACT_SIGMOID, true, false);                      \
+#define HCASE(B, A, H, S, C) \
+  rc = launch_halo<B, A, H, S, C>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol)
+#define HBN(B, C)                                                   \
+  do {                                                              \
+    if (stats) HCASE(B, ACT_NONE, false, true, C);                  \
+    else if (act == ACT_NONE) { if (hb) HCASE(B, ACT_NONE, true, false, C); else HCASE(B, ACT_NONE, false, false, C); } \
+    else if (act == ACT_RELU) HCASE(B, ACT_RELU, true, false, C);    \
+    else if (act == ACT_TANH) HCASE(B, ACT_TANH, true, false, C);    \
+    else HCASE(B, ACT_SIGMOID, true, false, C);                      \
   } while (0)
   if (act != ACT_NONE && !hb) return -5;   // activation variants are instantiated with bias only
-  if (BN == 32) HBN(32); else HBN(64);
+  if (CS == 16) {
+    if (BN == 32) HBN(32, 16); else HBN(64, 16);
+  } else {
+    if (BN == 32) HBN(32, 8); else HBN(64, 8);
+  }
 #undef HBN
 #undef HCASE
   if (rc) return rc;
@@ -614,42 +654,94 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
 
 extern "C" long long fn_conv_halo_lds(const int* geom16, int Ncol) {
   const HaloGeom g = parse_halo(geom16);
-  return (long long)halo_lds_bytes(g, Ncol <= 32 ? 32 : 64);
+  return (long long)halo_lds_bytes(g, Ncol <= 32 ? 32 : 64, halo_cs(g.C) ? halo_cs(g.C) : 16);
 }
 
-static size_t halo_wgrad_lds(const HaloGeom& g, int MT) {
+static size_t halo_wgrad_lds(const HaloGeom& g, int MT, int CS) {
   const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
-  return (size_t)H_BM * (MT * 16 + 16) * 2 + hp * 32 + 2 * H_BM * 4 + hp * 4 + 16;
+  return (size_t)H_BM * (MT * 16 + 16) * 2 + hp * CS * 2 + 2 * H_BM * 4 + hp * 4 + 16;
 }
 
 // dw: fp32 [Cout][T][C], zero-initialised by the caller (atomics accumulate).
 extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, const int* geom16, int Cout,
                                   int grid_x, hipStream_t st) {
   const HaloGeom g = parse_halo(geom16);
-  if (g.C % 16 != 0 || g.TD * g.TH * g.OW > H_BM || Cout > 64 || Cout % 8 != 0) return -2;
+  const int CS = halo_cs(g.C);
+  if (CS == 0 || g.TD * g.TH * g.OW > H_BM || Cout > 64 || Cout % 8 != 0) return -2;
   const int MT = (Cout + 15) / 16;
-  const size_t lds = halo_wgrad_lds(g, MT);
+  const size_t lds = halo_wgrad_lds(g, MT, CS);
   if (lds > 160 * 1024) return -4;
   const int T = g.KD * g.KH * g.KW;
-  const int TPW = MT == 1 ? 16 : 32 / MT;
+  const int TPW = MT == 1 ? 16 : 32 / MT;       // taps per wave (either slice width)
   const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
   const int gx = grid_x < ntiles ? (grid_x > 0 ? grid_x : 1) : ntiles;
-  dim3 grid((unsigned)gx, (unsigned)((T + 4 * TPW - 1) / (4 * TPW)), (unsigned)(g.C / 16));
+  dim3 grid((unsigned)gx, (unsigned)((T + 4 * TPW - 1) / (4 * TPW)), (unsigned)(g.C / CS));
   const bf16* d = (const bf16*)dy;
   const bf16* s = (const bf16*)src;
-#define WCASE(M)                                                                                           \
+#define WCASE(M, C)                                                                                        \
   do {                                                                                                     \
     static size_t cfg = 0;                                                                                 \
     if (lds > cfg) {                                                                                       \
-      hipError_t e = hipFuncSetAttribute((const void*)conv_halo_wgrad_kernel<M>,                           \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_halo_wgrad_kernel<M, C>,                        \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
       if (e != hipSuccess) return (int)e;                                                                  \
       cfg = lds;                                                                                           \
     }                                                                                                      \
-    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M>), grid, dim3(256), lds, st, d, s, dw, g, Cout);          \
+    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M, C>), grid, dim3(256), lds, st, d, s, dw, g, Cout);       \
   } while (0)
-  if (MT == 1) WCASE(1); else if (MT == 2) WCASE(2); else if (MT == 3) WCASE(3); else WCASE(4);
+  if (CS == 16) {
+    if (MT == 1) WCASE(1, 16); else if (MT == 2) WCASE(2, 16); else if (MT == 3) WCASE(3, 16); else WCASE(4, 16);
+  } else {
+    if (MT == 1) WCASE(1, 8); else if (MT == 2) WCASE(2, 8); else if (MT == 3) WCASE(3, 8); else WCASE(4, 8);
+  }
 #undef WCASE
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// space-to-depth packing for strided few-channel convs (the FeatureNet-3D stem)
+// ---------------------------------------------------------------------------
+// out[n][d2][h2][w2][CO] (CO = 8 or 16 channels, zero padded) with channel
+// ((a * sh + b) * sw + c) * C + ci = x[n][d2*sd + a][h2*sh + b][w2*sw + c][ci]
+// (zero outside x).  One thread per output position, one 16-B store per 8
+// channels; a 1-channel stride-2 stem reads 4 bf16 pairs per position.
+__global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
+                                                        int N, int D, int H, int W, int C, int sd, int sh, int sw,
+                                                        int D2, int H2, int W2, int CO) {
+  const long long npos = (long long)N * D2 * H2 * W2;
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npos) return;
+  const int w2 = (int)(p % W2), h2 = (int)((p / W2) % H2), d2 = (int)((p / ((long long)W2 * H2)) % D2);
+  const long long n = p / ((long long)W2 * H2 * D2);
+  const int creal = sd * sh * sw * C;
+  for (int c0 = 0; c0 < CO; c0 += 8) {
+    Pack8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ch = c0 + j;
+      float f = 0.f;
+      if (ch < creal) {
+        const int ci = ch % C, blk = ch / C;
+        const int c = blk % sw, b = (blk / sw) % sh, a = blk / (sw * sh);
+        const int d = d2 * sd + a, h = h2 * sh + b, w = w2 * sw + c;
+        if (d < D && h < H && w < W) f = bf2f(x[(((n * D + d) * H + h) * W + w) * C + ci]);
+      }
+      v.e[j] = f2bf(f);
+    }
+    *(uint4*)(out + p * CO + c0) = v.u;
+  }
+}
+
+extern "C" int fn_s2d_pack(const void* x, void* out, const int* geom12, hipStream_t st) {
+  const int N = geom12[0], D = geom12[1], H = geom12[2], W = geom12[3], C = geom12[4];
+  const int sd = geom12[5], sh = geom12[6], sw = geom12[7], D2 = geom12[8], H2 = geom12[9], W2 = geom12[10];
+  const int CO = geom12[11];
+  if (CO % 8 != 0 || sd * sh * sw * C > CO) return -2;
+  const long long npos = (long long)N * D2 * H2 * W2;
+  const unsigned blocks = (unsigned)((npos + 255) / 256);
+  hipLaunchKernelGGL(s2d_pack_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)out, N, D, H, W, C, sd,
+                     sh, sw, D2, H2, W2, CO);
   FN_CHECK_LAUNCH();
   return 0;
 }

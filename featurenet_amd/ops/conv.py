@@ -158,19 +158,26 @@ LDS_BUDGET = 80 * 1024      # two workgroups per CU (160 KiB LDS)
 _PLAN_CACHE: dict = {}
 
 
-def _fwd_halo_budget(ncol: int) -> int:
+def halo_cs(C: int) -> int:
+    """Channels per LDS halo slice of the halo kernels: 16, 8 (8-channel inputs) or 0 (unsupported)."""
+    return 16 if C % 16 == 0 else (8 if C % 8 == 0 else 0)
+
+
+def _fwd_halo_budget(ncol: int, cs: int = 16) -> int:
     bn = 32 if ncol <= 32 else 64
-    return int((LDS_BUDGET - 2 * bn * 128 * 2 - 1024) / 1.125)     # + 4 B/position decode table
+    # halo + 4 B/position decode table, expressed in 32-B (16-channel bf16) positions
+    return int((LDS_BUDGET - 2 * bn * 128 * 2 - 1024) * 32 / (cs * 2 + 4))
 
 
-def _wgrad_halo_budget(cout: int) -> int:
+def _wgrad_halo_budget(cout: int, cs: int = 16) -> int:
     mt = (cout + 15) // 16
-    return int((LDS_BUDGET - 256 * (16 * mt + 16) * 2 - 2048 - 64) / 1.125)    # + 4 B/position table
+    return int((LDS_BUDGET - 256 * (16 * mt + 16) * 2 - 2048 - 64) * 32 / (cs * 2 + 4))
 
 
 def halo_plan(OD: int, OH: int, OW: int, KD: int, KH: int, KW: int, max_bytes: int = 56 * 1024):
     """Output tile (TD, TH) x full OW maximising MFMA row utilisation with the
-    16-channel input halo <= max_bytes; None when no tile fits."""
+    halo (counted at 32 B = 16 bf16 channels per position) <= max_bytes; None
+    when no tile fits."""
     key = (OD, OH, OW, KD, KH, KW, max_bytes)
     if key in _PLAN_CACHE:
         return _PLAN_CACHE[key]
@@ -199,9 +206,9 @@ def _halo_enabled() -> bool:
 def halo_fwd_plan(spec: ConvSpec):
     if not _halo_enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
         return None
-    if spec.C % 16 or spec.K < 16 or spec.taps < 8:
+    if not halo_cs(spec.C) or spec.K < 16 or spec.taps < 8:
         return None
-    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, _fwd_halo_budget(spec.K))
+    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, _fwd_halo_budget(spec.K, halo_cs(spec.C)))
 
 
 def halo_dgrad_plan(spec: ConvSpec):
@@ -209,16 +216,18 @@ def halo_dgrad_plan(spec: ConvSpec):
         return None
     if spec.K % 16 or spec.C < 16 or spec.taps < 8:
         return None
-    return halo_plan(spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW, _fwd_halo_budget(spec.C))
+    return halo_plan(spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW, _fwd_halo_budget(spec.C, 16))
 
 
 def halo_weights(w3: torch.Tensor) -> torch.Tensor:
-    """[Ncol, T, Csrc] -> bf16 [Ncol, Csrc/16 * T8 * 16] in the halo kernel's k order
-    (16-channel slice, tap padded to a multiple of 8, 16 channels)."""
+    """[Ncol, T, Csrc] -> bf16 [Ncol, Csrc/CS * Tp * CS] in the halo kernel's k order
+    (CS-channel slice, taps padded to a multiple of 128/CS, CS channels; CS = halo_cs(Csrc))."""
     n, T, c = w3.shape
-    T8 = (T + 7) // 8 * 8
-    out = torch.zeros(n, c // 16, T8, 16, dtype=torch.bfloat16, device=w3.device)
-    out[:, :, :T] = w3.reshape(n, T, c // 16, 16).permute(0, 2, 1, 3)
+    cs = halo_cs(c)
+    tps = 128 // cs
+    Tp = (T + tps - 1) // tps * tps
+    out = torch.zeros(n, c // cs, Tp, cs, dtype=torch.bfloat16, device=w3.device)
+    out[:, :, :T] = w3.reshape(n, T, c // cs, cs).permute(0, 2, 1, 3)
     return out.reshape(n, -1)
 
 
@@ -233,7 +242,7 @@ def halo_tap_offsets(geom: list, device) -> torch.Tensor:
         OW, KD, KH, KW, TD, TH = geom[7], geom[8], geom[9], geom[10], geom[14], geom[15]
         HH, HW = TH + KH - 1, OW + KW - 1
         T = KD * KH * KW
-        offs = np.zeros((T + 7) // 8 * 8, dtype=np.int32)
+        offs = np.zeros((T + 15) // 16 * 16, dtype=np.int32)      # >= Tp for both slice widths
         kd, kh, kw = np.meshgrid(np.arange(KD), np.arange(KH), np.arange(KW), indexing="ij")
         offs[:T] = ((kd * HH + kh) * HW + kw).reshape(-1)
         t = torch.from_numpy(offs).to(device)
@@ -245,9 +254,9 @@ def halo_tap_offsets(geom: list, device) -> torch.Tensor:
 def halo_wgrad_plan(spec: ConvSpec):
     if not _halo_enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
         return None
-    if spec.C % 16 or spec.K % 8 or spec.K > 64 or spec.taps < 8:
+    if not halo_cs(spec.C) or spec.K % 8 or spec.K > 64 or spec.taps < 8:
         return None
-    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, _wgrad_halo_budget(spec.K))
+    return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, _wgrad_halo_budget(spec.K, halo_cs(spec.C)))
 
 
 def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> torch.Tensor:
@@ -256,8 +265,9 @@ def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> tor
     geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
             spec.pd, spec.ph, spec.pw, TD, TH]
     mt = (spec.K + 15) // 16
+    cs = halo_cs(spec.C)
     tpw = 16 if mt == 1 else 32 // mt
-    per_tile = math.ceil(spec.taps / (4 * tpw)) * (spec.C // 16)
+    per_tile = math.ceil(spec.taps / (4 * tpw)) * (spec.C // cs)
     dw = torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
     _native.kernels().conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), geom, spec.K,
                                       max(1, target_wgs // per_tile), _native.stream(x5))
@@ -400,7 +410,12 @@ def native_act_bwd(dy: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 def s2d_plan(spec: ConvSpec):
     """(factors, ConvSpec') when a strided, few-channel, unpadded conv maps onto the
-    stride-1 halo kernels after a space-to-depth of the input; else None."""
+    stride-1 halo kernels after a space-to-depth of the input; else None.
+
+    The packed input has ``s^3*C`` real channels, zero-padded to 8 (one 8-channel
+    halo slice, k-step = 4 taps x 8 channels) or 16; FeatureNet-3D's 1-channel
+    7^3 stride-2 stem becomes a 4^3-tap conv over 8 channels (K = 512 vs the
+    real 343)."""
     f = (spec.sd, spec.sh, spec.sw)
     if not _halo_enabled() or f == (1, 1, 1) or (spec.dd, spec.dh, spec.dw) != (1, 1, 1):
         return None
@@ -409,24 +424,32 @@ def s2d_plan(spec: ConvSpec):
     cs = spec.C * f[0] * f[1] * f[2]
     if cs > 16:
         return None
+    co = 8 if cs <= 8 else 16
     D2, H2, W2 = (-(-d // s) for d, s in zip((spec.D, spec.H, spec.W), f))
     k2 = tuple(-(-k // s) for k, s in zip((spec.KD, spec.KH, spec.KW), f))
     if k2[0] * k2[1] * k2[2] < 8 or D2 < k2[0] or H2 < k2[1] or W2 < k2[2]:
         return None
-    spec2 = ConvSpec.make((spec.N, D2, H2, W2, 16), spec.K, k2, 1, "valid")
+    spec2 = ConvSpec.make((spec.N, D2, H2, W2, co), spec.K, k2, 1, "valid")
     if (spec2.OD, spec2.OH, spec2.OW) != (spec.OD, spec.OH, spec.OW) or halo_fwd_plan(spec2) is None:
         return None
     return f, spec2
 
 
 def s2d_input(x5: torch.Tensor, f, spec2: ConvSpec) -> torch.Tensor:
+    """Space-to-depth packed input [N, D2, H2, W2, C'] (``s2d_pack`` kernel on GPU)."""
     N, D, H, W, C = x5.shape
     sd, sh, sw = f
     D2, H2, W2 = spec2.D, spec2.H, spec2.W
-    xp = torch.zeros(N, D2 * sd, H2 * sh, W2 * sw, C, dtype=torch.bfloat16, device=x5.device)
+    if x5.is_cuda and _native.kernels_available():
+        x5 = x5.to(torch.bfloat16).contiguous()
+        out = torch.empty(N, D2, H2, W2, spec2.C, dtype=torch.bfloat16, device=x5.device)
+        _native.kernels().s2d_pack(x5.data_ptr(), out.data_ptr(), [N, D, H, W, C, sd, sh, sw, D2, H2, W2, spec2.C],
+                                   _native.stream(x5))
+        return out
+    xp = torch.zeros(N, D2 * sd, H2 * sh, W2 * sw, C, dtype=x5.dtype, device=x5.device)
     xp[:, :D, :H, :W] = x5
     x2 = xp.view(N, D2, sd, H2, sh, W2, sw, C).permute(0, 1, 3, 5, 2, 4, 6, 7).reshape(N, D2, H2, W2, -1)
-    out = torch.zeros(N, D2, H2, W2, 16, dtype=torch.bfloat16, device=x5.device)
+    out = torch.zeros(N, D2, H2, W2, spec2.C, dtype=x5.dtype, device=x5.device)
     out[..., : x2.shape[-1]] = x2
     return out
 
@@ -438,7 +461,7 @@ def s2d_weight(w: torch.Tensor, f, spec: ConvSpec, spec2: ConvSpec) -> torch.Ten
     wp = torch.zeros(K, kd * sd, kh * sh, kw * sw, C, dtype=w.dtype, device=w.device)
     wp[:, :KD, :KH, :KW] = w
     w2 = wp.view(K, kd, sd, kh, sh, kw, sw, C).permute(0, 1, 3, 5, 2, 4, 6, 7).reshape(K, kd, kh, kw, -1)
-    out = torch.zeros(K, kd, kh, kw, 16, dtype=w.dtype, device=w.device)
+    out = torch.zeros(K, kd, kh, kw, spec2.C, dtype=w.dtype, device=w.device)
     out[..., : w2.shape[-1]] = w2
     return out
 
@@ -459,15 +482,24 @@ class ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x5, w, b, spec: ConvSpec, act: int, want_stats: bool):
         bias = b.detach().float().contiguous() if b is not None else None
-        if halo_fwd_plan(spec) is not None:
+        s2d = s2d_plan(spec)
+        x_saved = x5
+        if s2d is not None:
+            # strided few-channel stem: space-to-depth -> stride-1 halo conv over 8 channels;
+            # the packed input is what wgrad consumes, so it is saved instead of x
+            f, spec2 = s2d
+            x2 = s2d_input(x5, f, spec2)
+            y, stats = halo_conv_fwd(x2, s2d_weight(w.detach(), f, spec, spec2), bias, spec2, act, want_stats,
+                                     halo_fwd_plan(spec2))
+            x_saved = x2
+        elif halo_fwd_plan(spec) is not None:
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats, w=w.detach())
         else:
-            # (a space-to-depth forward of the 1-channel stem pads K 3x and loses to packed-W igemm)
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
-        ctx.spec, ctx.act, ctx.has_b = spec, act, b is not None
+        ctx.spec, ctx.act, ctx.has_b, ctx.s2d = spec, act, b is not None, s2d
         ctx.x_needs = ctx.needs_input_grad[0]
-        ctx.save_for_backward(x5, w, y if act else None)
+        ctx.save_for_backward(x_saved, w, y if act else None)
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         return y, stats
@@ -482,11 +514,9 @@ class ConvFn(torch.autograd.Function):
         dx = native_conv_dgrad(dy, w.detach(), spec) if ctx.x_needs else None
         dw = None
         if ctx.needs_input_grad[1]:
-            s2d = s2d_plan(spec)
-            if s2d is not None:      # strided few-channel stem: wgrad on the halo kernel after space-to-depth
-                f, spec2 = s2d
-                dw2 = native_conv_wgrad(dy, s2d_input(x5.to(torch.bfloat16), f, spec2), spec2)
-                dw = s2d_weight_grad(dw2, f, spec)
+            if ctx.s2d is not None:      # x5 is the space-to-depth packed input
+                f, spec2 = ctx.s2d
+                dw = s2d_weight_grad(native_conv_wgrad(dy, x5, spec2), f, spec)
             else:
                 dw = native_conv_wgrad(dy, x5.contiguous(), spec)
         db = native_colsum(dy.reshape(-1, spec.K)) if (ctx.has_b and ctx.needs_input_grad[2]) else None

@@ -309,6 +309,55 @@ def test_conv_halo_fwd_dgrad_stats(case):
         close(dw, wr.grad)
 
 
+@pytest.mark.parametrize("case", [
+    (2, 9, 10, 11, 8, 32, (3, 3, 3), "same"),       # 8-channel halo slices (CS = 8), partial taps
+    (2, 12, 12, 12, 8, 64, (4, 4, 4), "valid"),     # s2d-stem shape class, BN = 64
+    (3, 1, 17, 19, 24, 16, (1, 5, 5), "same"),      # C % 16 != 0 -> three 8-channel slices
+])
+def test_conv_halo_cs8(case):
+    """Halo kernels with 8-channel slices: forward + BN stats and wgrad (ConvFn) vs fp32 reference."""
+    _native_loaded()
+    import importlib
+
+    C = importlib.import_module("featurenet_amd.ops.conv")
+    N, D, H, W, Ci, K, k, pad = case
+    torch.manual_seed(11)
+    x = torch.randn(N, D, H, W, Ci, device="cuda").to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, K, k, 1, pad)
+    assert C.halo_cs(Ci) == 8 and C.halo_fwd_plan(spec) is not None and C.halo_wgrad_plan(spec) is not None
+    w = (torch.randn(K, spec.KD, spec.KH, spec.KW, Ci, device="cuda") * 0.05).to(torch.bfloat16).float()
+    wn = w.clone().requires_grad_(True)
+    y, st = C.ConvFn.apply(x, wn, None, spec, 0, True)
+    wr = w.clone().requires_grad_(True)
+    yr = ref.conv(x.float(), wr, None, spec)
+    close(y, yr)
+    yb = y.float().reshape(-1, K)
+    torch.testing.assert_close(st[:, 0].sum(0), yb.sum(0), rtol=2e-3, atol=5e-2)
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    close(wn.grad, wr.grad)
+
+
+def test_s2d_pack_matches_reference_layout():
+    """s2d_pack kernel == the torch view/permute definition of the space-to-depth layout."""
+    _native_loaded()
+    import importlib
+
+    C = importlib.import_module("featurenet_amd.ops.conv")
+    torch.manual_seed(4)
+    for shape, k, s in (((2, 19, 20, 21, 1), 7, 2), ((1, 9, 9, 9, 2), 4, 2)):
+        x = torch.randn(*shape, device="cuda").to(torch.bfloat16)
+        spec = ConvSpec.make(x.shape, 16, k, s)
+        plan = C.s2d_plan(spec)
+        if plan is None:
+            continue
+        f, spec2 = plan
+        got = C.s2d_input(x, f, spec2)
+        want = C.s2d_input(x.cpu(), f, spec2)
+        assert torch.equal(got.cpu(), want)
+
+
 DW_CASES = [
     # (N, D, H, W, C, kernel, stride, padding, act)
     (4, 1, 16, 16, 16, (1, 3, 3), 1, "same", "relu"),
