@@ -54,6 +54,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_f8_kernel(const unsigned cha
 
   unsigned char* halo = dsm;                                   // [HP][16]
   unsigned char* Bs = dsm + (((size_t)HP * 16 + 15) & ~(size_t)15);
+  int* toffs_s = reinterpret_cast<int*>(Bs + 2 * B_STAGE);      // [T8] tap offsets (LDS, not scalar loads)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
@@ -120,11 +121,11 @@ __global__ __launch_bounds__(256, 2) void conv_halo_f8_kernel(const unsigned cha
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  for (int t = tid; t < T8; t += 256) toffs_s[t] = toffs[t];
   fill_halo(0);
   load_b(0);
   write_b(0);
   __syncthreads();
-  const int mt_live = rows - wave * 64;
   for (int q = 0; q < nq; ++q) {
     if (q > 0 && q % spp == 0) {
       fill_halo(q / spp);
@@ -133,10 +134,10 @@ __global__ __launch_bounds__(256, 2) void conv_halo_f8_kernel(const unsigned cha
     const bool more = q + 1 < nq;
     if (more) load_b(q + 1);
     const unsigned char* b = Bs + (q & 1) * B_STAGE;
-    const int* tp = toffs + (q % spp) * 8;
+    const int* tp = toffs_s + (q % spp) * 8 + (lg >> 1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const int toff = (lg & 2) ? tp[ks * 2 + 1] : tp[ks * 2];
+      const int toff = tp[ks * 2];
       long fa[4], fb[NT];
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -147,14 +148,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_f8_kernel(const unsigned cha
         const int r = nt * 16 + lr;
         fb[nt] = *(const long*)(b + r * F8_BK + ((chunk ^ (r & 7)) << 4) + (lg & 1) * 8);
       }
+      // branch-free: rows past the tile compute on a valid halo position and are dropped
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        if (mt * 16 < mt_live) {
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
-        }
-      }
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
     }
     __syncthreads();
     if (more) {
@@ -215,7 +214,8 @@ static F8Geom parse_f8(const int* v) {
 
 static size_t f8_lds(const F8Geom& g, int BN, bool out_f8) {
   const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
-  const size_t main_ = ((hp * 16 + 15) & ~(size_t)15) + 2 * (size_t)BN * F8_BK;
+  const size_t T8 = ((size_t)g.KD * g.KH * g.KW + 7) & ~(size_t)7;
+  const size_t main_ = ((hp * 16 + 15) & ~(size_t)15) + 2 * (size_t)BN * F8_BK + T8 * 4;
   const size_t epi = (size_t)F8_BM * (BN * (out_f8 ? 1 : 2) + 16);
   return (main_ > epi ? main_ : epi) + 16;
 }

@@ -715,6 +715,19 @@ __global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ 
   const int w2 = (int)(p % W2), h2 = (int)((p / W2) % H2), d2 = (int)((p / ((long long)W2 * H2)) % D2);
   const long long n = p / ((long long)W2 * H2 * D2);
   const int creal = sd * sh * sw * C;
+  if (C == 1 && sd == 2 && sh == 2 && sw == 2 && 2 * D2 == D && 2 * H2 == H && 2 * W2 == W) {
+    // the 1-channel stride-2 stem: 4 aligned bf16 pairs (w, w+1) -> one 16-B store
+    const unsigned* xr = reinterpret_cast<const unsigned*>(x);
+    uint4 v;
+    const long long b00 = ((n * D + 2 * d2) * H + 2 * h2) * (long long)W + 2 * w2;
+    v.x = xr[b00 >> 1];
+    v.y = xr[(b00 + W) >> 1];
+    v.z = xr[(b00 + (long long)H * W) >> 1];
+    v.w = xr[(b00 + (long long)H * W + W) >> 1];
+    *(uint4*)(out + p * CO) = v;
+    if (CO == 16) *(uint4*)(out + p * CO + 8) = make_uint4(0, 0, 0, 0);
+    return;
+  }
   for (int c0 = 0; c0 < CO; c0 += 8) {
     Pack8 v;
 #pragma unroll

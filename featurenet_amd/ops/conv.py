@@ -484,14 +484,21 @@ class ConvFn(torch.autograd.Function):
         bias = b.detach().float().contiguous() if b is not None else None
         s2d = s2d_plan(spec)
         x_saved = x5
-        if s2d is not None:
-            # strided few-channel stem: space-to-depth -> stride-1 halo conv over 8 channels;
-            # the packed input is what wgrad consumes, so it is saved instead of x
+        if s2d is not None and s2d[1].kdim <= 1.25 * spec.kdim:
+            # strided few-channel conv: space-to-depth -> stride-1 halo conv; the packed
+            # input is what wgrad consumes, so it is saved instead of x
             f, spec2 = s2d
             x2 = s2d_input(x5, f, spec2)
             y, stats = halo_conv_fwd(x2, s2d_weight(w.detach(), f, spec, spec2), bias, spec2, act, want_stats,
                                      halo_fwd_plan(spec2))
             x_saved = x2
+        elif s2d is not None:
+            # the padded s2d K (FeatureNet-3D stem: 512 vs 343) loses to the packed-W gather
+            # forward; wgrad still runs on the packed input
+            f, spec2 = s2d
+            wmat, ldw = pack_weight_rows(w.detach(), spec)
+            y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
+            x_saved = s2d_input(x5, f, spec2) if ctx.needs_input_grad[1] else x5
         elif halo_fwd_plan(spec) is not None:
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats, w=w.detach())
         else:
@@ -514,7 +521,7 @@ class ConvFn(torch.autograd.Function):
         dx = native_conv_dgrad(dy, w.detach(), spec) if ctx.x_needs else None
         dw = None
         if ctx.needs_input_grad[1]:
-            if ctx.s2d is not None:      # x5 is the space-to-depth packed input
+            if ctx.s2d is not None:      # x5 is the space-to-depth packed input (saved by forward)
                 f, spec2 = ctx.s2d
                 dw = s2d_weight_grad(native_conv_wgrad(dy, x5, spec2), f, spec)
             else:
