@@ -31,6 +31,16 @@ struct HaloGeom {
   int TD, TH;              // output tile (rows = TD * TH * OW <= 256)
 };
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt) but NOT for outstanding global loads, unlike __syncthreads(), whose
+// fence drains vmcnt -- the register prefetches of the next halo / weight stage
+// stay in flight across the barrier (hipcc waits for them, counted, at first use).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 #define H_BM 256
 #define H_BK 64
 #define H_BKS 128   // weight-stage depth of the forward halo kernel
@@ -205,9 +215,9 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 
   int s = 0;                              // global stage counter
   for (int job = 0; job < njobs; ++job) {
-    __syncthreads();                      // previous halo / epilogue staging fully consumed
+    lds_barrier();                      // previous halo / epilogue staging fully consumed
     store_halo(job);
-    __syncthreads();
+    lds_barrier();
     if (job + 1 < njobs) prefetch_halo(job + 1);   // lands during this job's MFMAs
     for (int local = 0; local < spp; ++local, ++s) {
       const bf16* b = Bs + (s & 1) * B_STAGE;
@@ -238,7 +248,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       }
       write_b((s + 1) & 1, rbA);          // stage s+1 (its buffer's last readers passed the previous barrier)
       load_b(s + 2, rbA);                 // a whole stage of MFMAs covers its latency
-      __syncthreads();
+      lds_barrier();
     }
     if (job % npass != npass - 1) continue;
 
@@ -497,9 +507,9 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
 
   if (t_begin < t_end) prefetch(t_begin);
   for (int tile = t_begin; tile < t_end; ++tile) {
-    __syncthreads();                 // previous tile's reads are done
+    lds_barrier();                 // previous tile's reads are done
     store(tile);
-    __syncthreads();
+    lds_barrier();
     if (tile + 1 < t_end) prefetch(tile + 1);   // lands during this tile's MFMAs
     const int kst = ntap > 0 ? (rows + 31) >> 5 : 0;   // waves past the last tap only stage
     for (int ks = 0; ks < kst; ++ks) {
