@@ -300,6 +300,52 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const bf16* __restrict__ 
   }
 }
 
+// Non-overlapping 2x2x2 (or 1x2x2) windows with 8-channel vectors: the common
+// FeatureNet / CNN pooling.  Per-channel BN params live in registers, all window
+// loads are issued before the reduction, 32-bit index math.
+template <int KD>
+__global__ __launch_bounds__(256) void pool2_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
+                                                        const float* __restrict__ scale, const float* __restrict__ shift,
+                                                        PoolGeom g, int is_max, int act, int total) {
+  const int cpr = g.C >> 3;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int ch = i % cpr;
+  int t = i / cpr;
+  const int ow = t % g.OW; t /= g.OW;
+  const int oh = t % g.OH; t /= g.OH;
+  const int od = t % g.OD;
+  const int n = t / g.OD;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale ? scale[ch * 8 + j] : 1.f;
+    sh[j] = scale ? shift[ch * 8 + j] : 0.f;
+  }
+  const long long rowW = (long long)g.W * g.C, plane = (long long)g.H * rowW;
+  const long long b0 = ((long long)(n * g.D + od * KD) * g.H + oh * 2) * rowW + (long long)ow * 2 * g.C + ch * 8;
+  Pack8 p[KD * 4];
+#pragma unroll
+  for (int kd = 0; kd < KD; ++kd)
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 2; ++kw) p[(kd * 2 + kh) * 2 + kw].u = *(const uint4*)(x + b0 + kd * plane + kh * rowW + kw * g.C);
+  Pack8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float acc = is_max ? -INFINITY : 0.f;
+#pragma unroll
+    for (int w = 0; w < KD * 4; ++w) {
+      float v = bf2f(p[w].e[j]);
+      if (scale) v = act_fwd(v * sc[j] + sh[j], act);
+      acc = is_max ? fmaxf(acc, v) : acc + v;
+    }
+    o.e[j] = f2bf(is_max ? acc : acc * (1.f / (KD * 4)));
+  }
+  *(uint4*)(out + (long long)i * 8) = o.u;
+}
+
 // Gather-form backward: every input element collects from the windows that
 // contain it (deterministic, no atomics, works for overlapping windows).
 // For max pooling the window's arg-max is recomputed (first max wins, matching
@@ -540,7 +586,18 @@ extern "C" int fn_pool_fwd(const void* x, void* out, const float* scale, const f
                            int is_max, int count_pad, int act, hipStream_t st) {
   PoolGeom g = pool_geom(geom17);
   const long long outs = (long long)g.N * g.OD * g.OH * g.OW;
-  if (g.C % 8 == 0)
+  const bool win2 = g.KH == 2 && g.KW == 2 && (g.KD == 2 || g.KD == 1) && g.sd == g.KD && g.sh == 2 && g.sw == 2 &&
+                    g.pd == 0 && g.ph == 0 && g.pw == 0 && g.D >= g.OD * g.KD && g.H >= g.OH * 2 &&
+                    g.W >= g.OW * 2 && g.C % 8 == 0 && outs * (g.C / 8) < (1LL << 31);
+  if (win2) {
+    const int total = (int)(outs * (g.C / 8));
+    if (g.KD == 2)
+      hipLaunchKernelGGL(pool2_fwd_kernel<2>, dim3((total + 255) / 256), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
+                         scale, shift, g, is_max, act, total);
+    else
+      hipLaunchKernelGGL(pool2_fwd_kernel<1>, dim3((total + 255) / 256), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
+                         scale, shift, g, is_max, act, total);
+  } else if (g.C % 8 == 0)
     hipLaunchKernelGGL(pool_fwd_kernel<8>, dim3(ew_blocks(outs * (g.C / 8))), dim3(256), 0, st, (const bf16*)x,
                        (bf16*)out, scale, shift, g, is_max, count_pad, act);
   else

@@ -105,9 +105,21 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   const int per = (ntiles + gridDim.x - 1) / gridDim.x;
   const int t_begin = worker * per;
   const int t_end = t_begin + per < ntiles ? t_begin + per : ntiles;
-  if (t_begin >= t_end) return;                  // whole workgroup exits together
-  const int njobs = (t_end - t_begin) * npass;
   const int n0 = blockIdx.y * BN;
+  // BN statistics: one (sum, sumsq) partial per workgroup (not per tile), so the
+  // finalize pass reduces gridDim.x rows instead of thousands
+  float st_sum = 0.f, st_sq = 0.f;
+  auto write_stats = [&]() {
+    if (STATS && tid < BN && n0 + tid < Ncol) {
+      stats[(long long)blockIdx.x * 2 * Ncol + n0 + tid] = st_sum;
+      stats[(long long)blockIdx.x * 2 * Ncol + Ncol + n0 + tid] = st_sq;
+    }
+  };
+  if (t_begin >= t_end) {                        // whole workgroup exits together
+    write_stats();
+    return;
+  }
+  const int njobs = (t_end - t_begin) * npass;
 
   for (int pos = tid; pos < HP; pos += H_NTHR)
     posinfo[pos] = ((pos / (HW * HH)) << 20) | (((pos / HW) % HH) << 10) | (pos % HW);
@@ -318,12 +330,9 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       red[part * 2 * BN + col] = sm;
       red[part * 2 * BN + BN + col] = qq;
       __syncthreads();
-      if (tid < BN && n0 + tid < Ncol) {
-        float a0 = 0.f, a1 = 0.f;
+      if (tid < BN) {
 #pragma unroll
-        for (int q2 = 0; q2 < NPART; ++q2) { a0 += red[q2 * 2 * BN + tid]; a1 += red[q2 * 2 * BN + BN + tid]; }
-        stats[(long long)tile * 2 * Ncol + n0 + tid] = a0;
-        stats[(long long)tile * 2 * Ncol + Ncol + n0 + tid] = a1;
+        for (int q2 = 0; q2 < NPART; ++q2) { st_sum += red[q2 * 2 * BN + tid]; st_sq += red[q2 * 2 * BN + BN + tid]; }
       }
     }
     __syncthreads();
@@ -346,6 +355,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       }
     }
   }
+  write_stats();
 }
 
 // ---------------------------------------------------------------------------
@@ -608,6 +618,7 @@ static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const 
 }
 
 static int g_num_cus = 0;
+extern "C" int fn_conv_halo_workers(const int* geom16, int Ncol);
 
 // wt: [Ncol][C/CS][Tp][CS] bf16 (taps padded to a multiple of 128/CS), CS = 16 when
 // C % 16 == 0 else 8; toffs: int [>= Tp] halo position offsets of the taps (0 for
@@ -622,17 +633,8 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   const size_t lds = halo_lds_bytes(g, BN, CS);
   const int region = (int)halo_region_bytes(g, BN, CS);
   if (lds > 160 * 1024) return -4;
-  if (g_num_cus == 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (g_num_cus <= 0) g_num_cus = 256;
-  }
-  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
   const int ncb = (Ncol + BN - 1) / BN;
-  const int per_cu = (int)((160 * 1024) / lds) < 2 ? 1 : 2;
-  int workers = (g_num_cus * per_cu + ncb - 1) / ncb;
-  if (workers > ntiles) workers = ntiles;
+  const int workers = fn_conv_halo_workers(geom16, Ncol);
   dim3 grid((unsigned)workers, ncb);
   const bf16* s = (const bf16*)src;
   const bf16* w = (const bf16*)wt;
@@ -660,6 +662,26 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   if (rc) return rc;
   FN_CHECK_LAUNCH();
   return 0;
+}
+
+// number of persistent workgroups (= rows of the BN-statistics slab) fn_conv_halo launches
+extern "C" int fn_conv_halo_workers(const int* geom16, int Ncol) {
+  const HaloGeom g = parse_halo(geom16);
+  const int CS = halo_cs(g.C);
+  if (CS == 0) return -2;
+  const int BN = Ncol <= 32 ? 32 : 64;
+  const size_t lds = halo_lds_bytes(g, BN, CS);
+  if (g_num_cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
+      g_num_cus = 256;
+  }
+  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
+  const int ncb = (Ncol + BN - 1) / BN;
+  const int per_cu = (int)((160 * 1024) / lds) < 2 ? 1 : 2;
+  int workers = (g_num_cus * per_cu + ncb - 1) / ncb;
+  return workers > ntiles ? ntiles : workers;
 }
 
 extern "C" long long fn_conv_halo_lds(const int* geom16, int Ncol) {

@@ -290,9 +290,9 @@ def halo_conv_fwd(x5, w, bias, spec: ConvSpec, act: int, want_stats: bool, plan)
     wmat = halo_weights(w.reshape(spec.K, spec.taps, spec.C))
     y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
     stats = None
-    if want_stats:
-        tiles = spec.N * math.ceil(spec.OD / TD) * math.ceil(spec.OH / TH)
-        stats = torch.empty(tiles, 2, spec.K, dtype=torch.float32, device=x5.device)
+    if want_stats:   # one (sum, sumsq) row per persistent workgroup
+        stats = torch.empty(_native.kernels().conv_halo_workers(geom, spec.K), 2, spec.K, dtype=torch.float32,
+                            device=x5.device)
     _halo_call(x5, wmat, bias, y, stats, geom, spec.K, act)
     return y, stats
 
