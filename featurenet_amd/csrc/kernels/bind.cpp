@@ -30,6 +30,7 @@ int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
 int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, hipStream_t);
 int fn_s2d_pack(const void*, void*, const int*, hipStream_t);
+int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
                    hipStream_t);
 int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
@@ -93,6 +94,9 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 16, "conv_halo_wgrad");
     chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x, S(st)),
         "conv_halo_wgrad");
+  });
+  m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {
+    chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K, T, C, mode, stage_k, S(st)), "halo_pack_w");
   });
   m.def("s2d_pack", [](uintptr_t x, uintptr_t out, std::vector<int> geom, uintptr_t st) {
     need(geom, 12, "s2d_pack");

@@ -219,6 +219,23 @@ def halo_dgrad_plan(spec: ConvSpec):
     return halo_plan(spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW, _fwd_halo_budget(spec.C, 16))
 
 
+def halo_pack(w: torch.Tensor, spec: ConvSpec, dgrad: bool) -> torch.Tensor:
+    """Halo-kernel B operand of a conv weight [K, KD, KH, KW, C]: forward layout, or the
+    dgrad layout (taps reversed, K <-> C); one HIP launch on GPU."""
+    if w.is_cuda and _native.kernels_available():
+        wf = w.detach().float().contiguous()
+        ncol, csrc = (spec.C, spec.K) if dgrad else (spec.K, spec.C)
+        cs = halo_cs(csrc)
+        tps = 128 // cs
+        Tp = (spec.taps + tps - 1) // tps * tps
+        out = torch.empty(ncol, csrc * Tp, dtype=torch.bfloat16, device=w.device)
+        _native.kernels().halo_pack_w(wf.data_ptr(), out.data_ptr(), spec.K, spec.taps, spec.C, int(dgrad), 128,
+                                      _native.stream(wf))
+        return out
+    w3 = w.reshape(spec.K, spec.taps, spec.C)
+    return halo_weights(w3.flip(1).permute(2, 1, 0) if dgrad else w3)
+
+
 def halo_weights(w3: torch.Tensor) -> torch.Tensor:
     """[Ncol, T, Csrc] -> bf16 [Ncol, Csrc/CS * Tp * CS] in the halo kernel's k order
     (CS-channel slice, taps padded to a multiple of 128/CS, CS channels; CS = halo_cs(Csrc))."""
@@ -287,7 +304,7 @@ def halo_conv_fwd(x5, w, bias, spec: ConvSpec, act: int, want_stats: bool, plan)
     TD, TH = plan
     geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
             spec.pd, spec.ph, spec.pw, TD, TH]
-    wmat = halo_weights(w.reshape(spec.K, spec.taps, spec.C))
+    wmat = halo_pack(w, spec, dgrad=False)
     y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
     stats = None
     if want_stats:   # one (sum, sumsq) row per persistent workgroup
@@ -302,8 +319,7 @@ def halo_conv_dgrad(dy5, w, spec: ConvSpec, plan):
     TD, TH = plan
     geom = [spec.N, spec.OD, spec.OH, spec.OW, spec.K, spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW,
             spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw, TD, TH]
-    wt = w.reshape(spec.K, spec.taps, spec.C).flip(1).permute(2, 1, 0)      # [C][T][K], taps reversed
-    wmat = halo_weights(wt)
+    wmat = halo_pack(w, spec, dgrad=True)                                    # [C][K/cs][Tp][cs], taps reversed
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     _halo_call(dy5, wmat, None, dx, None, geom, spec.C, 0)
     return dx

@@ -512,3 +512,20 @@ def test_graph_captured_training_matches_eager():
     assert max(abs(a - b) for a, b in zip(le, lg)) < 2e-2 * max(abs(v) for v in le)
     assert res[True][2] == res[False][2] == 62
     print(f"\\nstep time eager {res[False][1] * 1e3:.3f} ms, graph {res[True][1] * 1e3:.3f} ms")
+
+
+@pytest.mark.parametrize("K,C,k", [(32, 32, 5), (64, 32, 4), (16, 24, 3), (32, 8, 4)])
+def test_halo_pack_weights_matches_torch_layout(K, C, k):
+    """halo_pack_w kernel == the torch reference packing (forward and flipped/transposed dgrad layouts)."""
+    _native_loaded()
+    import importlib
+
+    Cm = importlib.import_module("featurenet_amd.ops.conv")
+    torch.manual_seed(9)
+    spec = ConvSpec.make((1, 9, 9, 9, C), K, k)
+    w = torch.randn(K, k, k, k, C, device="cuda")
+    w3 = w.reshape(K, spec.taps, C)
+    torch.testing.assert_close(Cm.halo_pack(w, spec, dgrad=False), Cm.halo_weights(w3), rtol=0, atol=0)
+    if K % 8 == 0:
+        ref_d = Cm.halo_weights(w3.flip(1).permute(2, 1, 0))
+        torch.testing.assert_close(Cm.halo_pack(w, spec, dgrad=True), ref_d, rtol=0, atol=0)
