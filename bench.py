@@ -167,8 +167,8 @@ def main():
     vs = (value / (base * world)) if base and same_cfg else None
     if rank == 0:
         out = {
-            "metric": ("samples/sec (64^3 voxel, 24-class) train" if args.model == "cls"
-                       else "samples/sec (64^3 voxel, per-voxel segmentation) train"),
+            "metric": (f"samples/sec ({S}^3 voxel, {NC}-class) train" if args.model == "cls"
+                       else f"samples/sec ({S}^3 voxel, per-voxel segmentation) train"),
             "value": round(value, 2),
             "unit": "samples/s",
             "n_gpus": world,
