@@ -54,6 +54,8 @@ def parse():
                          "(BASELINE config 4, 25 voxel classes)")
     ap.add_argument("--torch-layout", choices=["ndhwc", "ncdhw"], default="ndhwc",
                     help="memory format of the stock-PyTorch baseline (--impl torch)")
+    ap.add_argument("--torch-amp", choices=["bf16", "off"], default="bf16",
+                    help="stock-PyTorch baseline: bf16 autocast or plain fp32 (whichever MIOpen runs faster)")
     return ap.parse_args()
 
 
@@ -132,13 +134,14 @@ def main():
 
         def step(i):
             opt.zero_grad(set_to_none=True)
-            with torch.autocast(device_type="cuda" if use_cuda else "cpu", dtype=torch.bfloat16):
-                logits = dmodel(xs[i % args.pool])
+            with torch.autocast(device_type="cuda" if use_cuda else "cpu", dtype=torch.bfloat16,
+                                enabled=args.torch_amp == "bf16"):
+                logits = dmodel(xs[i % args.pool].float() if args.torch_amp == "off" else xs[i % args.pool])
             loss = lossf(logits.float(), ys[i % args.pool])
             loss.backward()
             opt.step()
             return loss
-        model_name = f"FeatureNet-3D (stock PyTorch eager baseline, {args.torch_layout})"
+        model_name = f"FeatureNet-3D (stock PyTorch eager baseline, {args.torch_layout}, amp={args.torch_amp})"
         flops = None
 
     def sync():
@@ -178,7 +181,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if vs is None else round(vs, 3),
-            "dtype": "bf16",
+            "dtype": "fp32" if (args.impl == "torch" and args.torch_amp == "off") else "bf16",
             "data": "synthetic (random 64^3 binary voxels, random labels, random-init weights)",
             "config": {
                 "model": model_name,
