@@ -19,12 +19,13 @@
 //   MODE 1: (sum g, sum g*xhat), g = dz*act'(z)     -- BN backward
 // VW = channels per thread (8 -> 16-B vector loads, 1 -> scalar fallback).
 // ---------------------------------------------------------------------------
-template <int VW, int MODE>
+template <int VW, int MODE, int ACT>
 __global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dz,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        const float* __restrict__ mean, const float* __restrict__ invstd,
-                                                       float* __restrict__ part, long long M, int C, int act,
+                                                       float* __restrict__ part, long long M, int C,
                                                        long long rows_per_block) {
+  constexpr int act = ACT;          // compile-time activation: no per-element switch
   __shared__ float red[256][2 * VW + 1];
   const int tid = threadIdx.x;
   const int cpr = C / VW;           // chunks per row
@@ -45,6 +46,7 @@ __global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ 
     }
   }
   if (active) {
+#pragma unroll 4
     for (long long m = mbeg + r0; m < mend; m += rpp) {
       const long long off = m * C + (long long)ch * VW;
       if constexpr (VW == 8) {
@@ -146,10 +148,11 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
 // thread keeps ONE channel chunk for the whole grid-stride loop, so the
 // per-channel parameters live in registers and no 64-bit modulo runs per
 // element.
-template <int VW>
+template <int VW, int ACT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16* __restrict__ z,
-                                                       long long total, int C, int act) {
+                                                       long long total, int C) {
+  constexpr int act = ACT;
   const long long nvec = total / VW;
   const int cpr = C / VW;
   const long long stride = (long long)gridDim.x * 256;
@@ -159,6 +162,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
     float sc[VW], sh[VW];
 #pragma unroll
     for (int j = 0; j < VW; ++j) { sc[j] = scale[c0 + j]; sh[j] = shift[c0 + j]; }
+#pragma unroll 2
     for (long long i = i0; i < nvec; i += stride) {
       Pack8 p;
       if constexpr (VW == 8) p.u = *(const uint4*)(y + i * 8); else p.e[0] = y[i];
@@ -181,13 +185,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
 // dy = gamma*invstd*(g - dbeta/M - xhat*dgamma/M), g = dz*act'(z)
 //    = k1*g + k2*y + k3 per channel with k1 = scale,
 //      k2 = -scale*invstd*dgamma/M, k3 = -scale*(dbeta/M - mean*invstd*dgamma/M)
-template <int VW>
+template <int VW, int ACT>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ y,
                                                            const float* __restrict__ scale, const float* __restrict__ shift,
                                                            const float* __restrict__ mean, const float* __restrict__ invstd,
                                                            const float* __restrict__ dbeta, const float* __restrict__ dgamma,
-                                                           bf16* __restrict__ dy, long long total, int C, float inv_count,
-                                                           int act) {
+                                                           bf16* __restrict__ dy, long long total, int C, float inv_count) {
+  constexpr int act = ACT;
   const long long nvec = total / VW;
   const int cpr = C / VW;
   const long long stride = (long long)gridDim.x * 256;
@@ -206,6 +210,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
     }
   };
   if (fixed) load_params((int)(threadIdx.x % cpr) * VW);
+#pragma unroll 2
   for (long long i = i0; i < nvec; i += stride) {
     if (!fixed) load_params((int)((i * VW) % C));
     Pack8 py, pd, po;
@@ -525,10 +530,18 @@ extern "C" int fn_colstats(const void* x, const void* dz, const float* scale, co
   const long long rpb = (M + nb - 1) / nb;
   const bf16* xx = (const bf16*)x;
   const bf16* dd = (const bf16*)dz;
-#define CS_CASE(VW, MD) \
-  hipLaunchKernelGGL((colstats_kernel<VW, MD>), dim3(nb), dim3(256), 0, st, xx, dd, scale, shift, mean, invstd, part, M, C, act, rpb)
-  if (vec) { if (mode == 0) CS_CASE(8, 0); else CS_CASE(8, 1); }
-  else { if (mode == 0) CS_CASE(1, 0); else CS_CASE(1, 1); }
+#define CS_CASE(VW, MD, A) \
+  hipLaunchKernelGGL((colstats_kernel<VW, MD, A>), dim3(nb), dim3(256), 0, st, xx, dd, scale, shift, mean, invstd, part, M, C, rpb)
+#define CS_ACT(VW)                                                                                  \
+  do {                                                                                              \
+    if (mode == 0) CS_CASE(VW, 0, ACT_NONE);                                                        \
+    else if (act == ACT_RELU) CS_CASE(VW, 1, ACT_RELU);                                             \
+    else if (act == ACT_TANH) CS_CASE(VW, 1, ACT_TANH);                                             \
+    else if (act == ACT_SIGMOID) CS_CASE(VW, 1, ACT_SIGMOID);                                       \
+    else CS_CASE(VW, 1, ACT_NONE);                                                                  \
+  } while (0)
+  if (vec) CS_ACT(8); else CS_ACT(1);
+#undef CS_ACT
 #undef CS_CASE
   FN_CHECK_LAUNCH();
   return 0;
@@ -549,12 +562,19 @@ extern "C" int fn_bn_finalize(const float* part, int nb, int C, double count, co
 
 extern "C" int fn_bn_apply(const void* y, const float* scale, const float* shift, void* z, long long total, int C,
                            int act, hipStream_t st) {
-  if (C % 8 == 0)
-    hipLaunchKernelGGL(bn_apply_kernel<8>, dim3(ew_blocks(total / 8)), dim3(256), 0, st, (const bf16*)y, scale, shift,
-                       (bf16*)z, total, C, act);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<1>, dim3(ew_blocks(total)), dim3(256), 0, st, (const bf16*)y, scale, shift,
-                       (bf16*)z, total, C, act);
+#define BA_CASE(VW, A)                                                                                  \
+  hipLaunchKernelGGL((bn_apply_kernel<VW, A>), dim3(ew_blocks(total / VW)), dim3(256), 0, st, (const bf16*)y, scale, \
+                     shift, (bf16*)z, total, C)
+#define BA_ACT(VW)                                                                                      \
+  do {                                                                                                  \
+    if (act == ACT_RELU) BA_CASE(VW, ACT_RELU);                                                         \
+    else if (act == ACT_TANH) BA_CASE(VW, ACT_TANH);                                                    \
+    else if (act == ACT_SIGMOID) BA_CASE(VW, ACT_SIGMOID);                                              \
+    else BA_CASE(VW, ACT_NONE);                                                                         \
+  } while (0)
+  if (C % 8 == 0) BA_ACT(8); else BA_ACT(1);
+#undef BA_ACT
+#undef BA_CASE
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -562,12 +582,20 @@ extern "C" int fn_bn_apply(const void* y, const float* scale, const float* shift
 extern "C" int fn_bn_bwd_apply(const void* dz, const void* y, const float* scale, const float* shift,
                                const float* mean, const float* invstd, const float* dbeta, const float* dgamma,
                                void* dy, long long total, int C, float inv_count, int act, hipStream_t st) {
-  if (C % 8 == 0)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<8>, dim3(ew_blocks(total / 8)), dim3(256), 0, st, (const bf16*)dz,
-                       (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, total, C, inv_count, act);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, dim3(ew_blocks(total)), dim3(256), 0, st, (const bf16*)dz,
-                       (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, total, C, inv_count, act);
+#define BB_CASE(VW, A)                                                                                  \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<VW, A>), dim3(ew_blocks(total / VW)), dim3(256), 0, st,            \
+                     (const bf16*)dz, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, total, C, \
+                     inv_count)
+#define BB_ACT(VW)                                                                                      \
+  do {                                                                                                  \
+    if (act == ACT_RELU) BB_CASE(VW, ACT_RELU);                                                         \
+    else if (act == ACT_TANH) BB_CASE(VW, ACT_TANH);                                                    \
+    else if (act == ACT_SIGMOID) BB_CASE(VW, ACT_SIGMOID);                                              \
+    else BB_CASE(VW, ACT_NONE);                                                                         \
+  } while (0)
+  if (C % 8 == 0) BB_ACT(8); else BB_ACT(1);
+#undef BB_ACT
+#undef BB_CASE
   FN_CHECK_LAUNCH();
   return 0;
 }

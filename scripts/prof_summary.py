@@ -8,7 +8,10 @@ identical training steps in the trace).
 """
 import argparse
 import csv
+import glob
+import os
 import re
+import sqlite3
 from collections import defaultdict
 
 
@@ -26,6 +29,28 @@ def short(name: str) -> str:
     return n[:80]
 
 
+def rows_of(path: str):
+    """Yield kernel-trace rows as CSV-style dicts from a ``*_kernel_trace.csv`` or a rocprofv3 ``.db``
+    (the default output format; a directory is searched for either)."""
+    if os.path.isdir(path):
+        hits = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True) or \
+            glob.glob(os.path.join(path, "**", "*.db"), recursive=True)
+        if not hits:
+            raise SystemExit(f"no kernel trace under {path}")
+        path = hits[0]
+    if path.endswith(".db"):
+        con = sqlite3.connect(path)
+        q = ("select name, start, end, grid_x, workgroup_x, grid_y, grid_z, vgpr_count, accum_vgpr_count, "
+             "scratch_size, lds_size from kernels")
+        for n, st, en, gx, wx, gy, gz, v, a, sc, lds in con.execute(q):
+            yield {"Kernel_Name": n, "Start_Timestamp": st, "End_Timestamp": en, "Grid_Size_X": gx,
+                   "Workgroup_Size_X": wx, "Grid_Size_Y": gy, "Grid_Size_Z": gz, "VGPR_Count": v,
+                   "Accum_VGPR_Count": a, "Scratch_Size": sc, "LDS_Block_Size": lds}
+        return
+    with open(path) as f:
+        yield from csv.DictReader(f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
@@ -34,8 +59,8 @@ def main():
     a = ap.parse_args()
     agg = defaultdict(lambda: {"ns": 0, "calls": 0, "vgpr": 0, "agpr": 0, "scratch": 0, "lds": 0})
     total = 0
-    with open(a.trace) as f:
-        for r in csv.DictReader(f):
+    if True:
+        for r in rows_of(a.trace):
             ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             grid = (int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"])), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"]))
             k = (short(r["Kernel_Name"]), grid)
