@@ -154,11 +154,13 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
     const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * CS;
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
-      const int c = i * H_NTHR + tid;
-      const int info = posinfo[c < nchunk ? c / CPP : 0];
+      // chunks past the halo are clamped to the last one (a duplicate, identical
+      // LDS write), so every load is consumed by an unconditional store and the
+      // compiler never has to assume a load still in flight at the k-loop top
+      const int c = min(i * H_NTHR + tid, nchunk - 1);
+      const int info = posinfo[c / CPP];
       const int gd = dlo + (info >> 20), gh = hlo + ((info >> 10) & 1023), gw = (info & 1023) - g.pw;
-      const bool ok = c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-                      (unsigned)gw < (unsigned)g.IW;
+      const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH && (unsigned)gw < (unsigned)g.IW;
       const int off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c % CPP) * 8;
       const uint4 x = *(const uint4*)(base + (ok ? off : 0));
       hreg[i] = ok ? x : make_uint4(0, 0, 0, 0);
@@ -167,8 +169,8 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   auto store_halo = [&](int job) {
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
-      const int c = i * H_NTHR + tid;
-      if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = hreg[i];
+      const int c = min(i * H_NTHR + tid, nchunk - 1);
+      *(uint4*)(halo + (size_t)c * 8) = hreg[i];
     }
     for (int c0 = HC * H_NTHR; c0 < nchunk; c0 += 4 * H_NTHR) {   // tail of a large halo: synchronous
       uint4 v[4];
@@ -176,30 +178,43 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       for (int j = 0; j < 4; ++j) {
         const bf16* base;
         int off;
-        const int c = c0 + j * H_NTHR + tid;
+        const int c = min(c0 + j * H_NTHR + tid, nchunk - 1);
         const bool ok = halo_src(job, c, base, off);
         const uint4 x = *(const uint4*)(base + (ok ? off : 0));
         v[j] = ok ? x : make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = c0 + j * H_NTHR + tid;
-        if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = v[j];
+        const int c = min(c0 + j * H_NTHR + tid, nchunk - 1);
+        *(uint4*)(halo + (size_t)c * 8) = v[j];
       }
     }
   };
 
+  // BN=32: stage s+1's weights are loaded at the top of stage s and written after
+  // its MFMAs, so their latency hides behind a whole stage.  BN=64 has no VGPRs
+  // to keep them in flight across the stage (they would spill) and instead loads
+  // stage s+2 at the end of stage s, writing it in the middle of stage s+1.
+  constexpr bool EARLY_B = KSPLIT;
   uint4 rbA[B_PER_T];
   auto load_b = [&](int q, uint4* dst) {
     const int kbase = (q % nq) * H_BKS;
 #pragma unroll
     for (int i = 0; i < B_PER_T; ++i) {
       const int idx = tid + i * H_NTHR;
+      // rows past Ncol re-read the last valid row: a B column only feeds its own
+      // output column, which the epilogue drops, so no zero-fill (and no exec-masked
+      // load whose register init forces a vmcnt(0) at the stage top) is needed
       const int r = (idx >> 4) < BN ? (idx >> 4) : BN - 1;
       const int k = kbase + (idx & 15) * 8;
-      const bool ok = idx < B_CHUNKS && n0 + r < Ncol;
-      const uint4 v = *(const uint4*)(wt + (ok ? (long long)(n0 + r) * ldw + k : 0));
-      dst[i] = ok ? v : make_uint4(0, 0, 0, 0);
+      if constexpr (EARLY_B) {
+        const int row = n0 + r < Ncol ? n0 + r : Ncol - 1;
+        dst[i] = *(const uint4*)(wt + (long long)row * ldw + k);
+      } else {
+        const bool ok = idx < B_CHUNKS && n0 + r < Ncol;
+        const uint4 v = *(const uint4*)(wt + (ok ? (long long)(n0 + r) * ldw + k : 0));
+        dst[i] = ok ? v : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto write_b = [&](int buf, const uint4* srcr) {
@@ -223,7 +238,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   prefetch_halo(0);
   load_b(0, rbA);
   write_b(0, rbA);
-  load_b(1, rbA);
+  if constexpr (!EARLY_B) load_b(1, rbA);
 
   int s = 0;                              // global stage counter
   for (int job = 0; job < njobs; ++job) {
@@ -232,6 +247,10 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
     lds_barrier();
     if (job + 1 < njobs) prefetch_halo(job + 1);   // lands during this job's MFMAs
     for (int local = 0; local < spp; ++local, ++s) {
+      if constexpr (EARLY_B) {
+        load_b(s + 1, rbA);
+        __builtin_amdgcn_sched_barrier(0);  // keep the loads here (the scheduler would sink them to their use)
+      }
       const bf16* b = Bs + (s & 1) * B_STAGE;
       // lane group lg reads tap lg>>1 / channel half lg&1 (CS = 16) or tap lg (CS = 8)
       const int* tp = toffs_s + local * TPS + (KSPLIT ? khalf * (TPS / 2) : 0) + (CS == 16 ? (lg >> 1) : lg);
@@ -259,7 +278,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
       }
       write_b((s + 1) & 1, rbA);          // stage s+1 (its buffer's last readers passed the previous barrier)
-      load_b(s + 2, rbA);                 // a whole stage of MFMAs covers its latency
+      if constexpr (!EARLY_B) load_b(s + 2, rbA);
       lds_barrier();
     }
     if (job % npass != npass - 1) continue;
