@@ -467,6 +467,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   __syncthreads();
 
   uint4 yreg[YC], hreg[HC];
+  // validity of the prefetched chunks as bit masks: the loads themselves are
+  // unconditional (invalid ones read offset 0) and are zeroed only when stored, so
+  // no load is exec-masked over a zero-initialised register -- that pattern makes
+  // hipcc's wait-count pass drain vmcnt at the top of the k-loop, i.e. it turns the
+  // prefetch synchronous
+  unsigned ymask = 0, hmask = 0;
   auto dy_src = [&](int tile, int idx, long long& m) -> bool {
     const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
     const int r = idx / YC, c = idx % YC;
@@ -484,46 +490,52 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
     return c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
            (unsigned)gw < (unsigned)g.IW;
   };
+  auto masked = [](uint4 v, bool ok) -> uint4 {
+    const unsigned m = ok ? ~0u : 0u;
+    return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+  };
   auto prefetch = [&](int tile) {
+    ymask = hmask = 0;
 #pragma unroll
     for (int i = 0; i < YC; ++i) {
       long long m;
       const bool ok = dy_src(tile, i * 256 + tid, m);
-      const uint4 v = *(const uint4*)(dy + (ok ? m : 0));
-      yreg[i] = ok ? v : make_uint4(0, 0, 0, 0);
+      yreg[i] = *(const uint4*)(dy + (ok ? m : 0));
+      ymask |= (unsigned)ok << i;
     }
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
       long long off;
-      const bool ok = halo_src(tile, i * 256 + tid, off);
-      const uint4 v = *(const uint4*)(src + (ok ? off : 0));
-      hreg[i] = ok ? v : make_uint4(0, 0, 0, 0);
+      // chunks past the halo clamp to the last one: a duplicate, identical LDS write
+      const bool ok = halo_src(tile, min(i * 256 + tid, nchunk - 1), off);
+      hreg[i] = *(const uint4*)(src + (ok ? off : 0));
+      hmask |= (unsigned)ok << i;
     }
   };
   auto store = [&](int tile) {
 #pragma unroll
     for (int i = 0; i < YC; ++i) {
       const int idx = i * 256 + tid;
-      *(uint4*)(Ys + (idx / YC) * LDY + (idx % YC) * 8) = yreg[i];
+      *(uint4*)(Ys + (idx / YC) * LDY + (idx % YC) * 8) = masked(yreg[i], (ymask >> i) & 1);
     }
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
-      const int c = i * 256 + tid;
-      if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = hreg[i];
+      const int c = min(i * 256 + tid, nchunk - 1);
+      *(uint4*)(halo + (size_t)c * 8) = masked(hreg[i], (hmask >> i) & 1);
     }
     for (int c0 = HC * 256; c0 < nchunk; c0 += 4 * 256) {   // tail of a large halo: synchronous
       uint4 v[4];
+      bool okv[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         long long off;
-        const bool ok = halo_src(tile, c0 + j * 256 + tid, off);
-        const uint4 x = *(const uint4*)(src + (ok ? off : 0));
-        v[j] = ok ? x : make_uint4(0, 0, 0, 0);
+        okv[j] = halo_src(tile, min(c0 + j * 256 + tid, nchunk - 1), off);
+        v[j] = *(const uint4*)(src + (okv[j] ? off : 0));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int c = c0 + j * 256 + tid;
-        if (c < nchunk) *(uint4*)(halo + (size_t)c * 8) = v[j];
+        const int c = min(c0 + j * 256 + tid, nchunk - 1);
+        *(uint4*)(halo + (size_t)c * 8) = masked(v[j], okv[j]);
       }
     }
   };
