@@ -57,7 +57,10 @@ __device__ __forceinline__ void lds_barrier() {
 // while the current job computes (written to LDS at the job boundary), and
 // weight stages are prefetched two stages ahead, so neither halo nor weight
 // latency sits on the critical path.
-template <int BN, int ACT, bool HAS_BIAS, bool STATS, int CS>
+// RES: every weight stage stays resident in LDS for the whole kernel (short-K convs
+// such as the space-to-depth stem, K = 512): no per-stage weight loads or barriers,
+// the k-loop of a job is pure LDS reads + MFMAs.
+template <int BN, int ACT, bool HAS_BIAS, bool STATS, int CS, bool RES>
 __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wt,
                                                            const float* __restrict__ bias, bf16* __restrict__ out,
                                                            float* __restrict__ stats, const int* __restrict__ toffs,
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 
   bf16* halo = reinterpret_cast<bf16*>(dsm);                      // also the epilogue staging area
   bf16* Bs = reinterpret_cast<bf16*>(dsm + region_bytes);
-  int* posinfo = reinterpret_cast<int*>(dsm + region_bytes + 2 * B_STAGE * 2);  // packed (hd, hh, hw)
+  int* posinfo = reinterpret_cast<int*>(dsm + region_bytes + (RES ? nq : 2) * B_STAGE * 2);  // packed (hd, hh, hw)
   int* toffs_s = posinfo + HP;                                    // [Tp] tap offsets (LDS: no scalar
                                                                   // loads inside the k-loop)
 
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   // its MFMAs, so their latency hides behind a whole stage.  BN=64 has no VGPRs
   // to keep them in flight across the stage (they would spill) and instead loads
   // stage s+2 at the end of stage s, writing it in the middle of stage s+1.
-  constexpr bool EARLY_B = KSPLIT;
+  constexpr bool EARLY_B = KSPLIT || RES;
   uint4 rbA[B_PER_T];
   auto load_b = [&](int q, uint4* dst) {
     const int kbase = (q % nq) * H_BKS;
@@ -236,9 +239,16 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   prefetch_halo(0);
-  load_b(0, rbA);
-  write_b(0, rbA);
-  if constexpr (!EARLY_B) load_b(1, rbA);
+  if constexpr (RES) {
+    for (int q = 0; q < nq; ++q) {        // all stages, once (the job loop's first barrier publishes them)
+      load_b(q, rbA);
+      write_b(q, rbA);
+    }
+  } else {
+    load_b(0, rbA);
+    write_b(0, rbA);
+    if constexpr (!EARLY_B) load_b(1, rbA);
+  }
 
   int s = 0;                              // global stage counter
   for (int job = 0; job < njobs; ++job) {
@@ -247,11 +257,11 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
     lds_barrier();
     if (job + 1 < njobs) prefetch_halo(job + 1);   // lands during this job's MFMAs
     for (int local = 0; local < spp; ++local, ++s) {
-      if constexpr (EARLY_B) {
+      if constexpr (EARLY_B && !RES) {
         load_b(s + 1, rbA);
         __builtin_amdgcn_sched_barrier(0);  // keep the loads here (the scheduler would sink them to their use)
       }
-      const bf16* b = Bs + (s & 1) * B_STAGE;
+      const bf16* b = Bs + (RES ? (job % npass) * spp + local : (s & 1)) * B_STAGE;
       // lane group lg reads tap lg>>1 / channel half lg&1 (CS = 16) or tap lg (CS = 8)
       const int* tp = toffs_s + local * TPS + (KSPLIT ? khalf * (TPS / 2) : 0) + (CS == 16 ? (lg >> 1) : lg);
 #pragma unroll
@@ -277,10 +287,13 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
           for (int nt = 0; nt < NT; ++nt)
             acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
       }
-      write_b((s + 1) & 1, rbA);          // stage s+1 (its buffer's last readers passed the previous barrier)
-      if constexpr (!EARLY_B) load_b(s + 2, rbA);
-      lds_barrier();
+      if constexpr (!RES) {
+        write_b((s + 1) & 1, rbA);        // stage s+1 (its buffer's last readers passed the previous barrier)
+        if constexpr (!EARLY_B) load_b(s + 2, rbA);
+        lds_barrier();
+      }
     }
+    if constexpr (RES) lds_barrier();     // all waves are done with the halo before it is reused
     if (job % npass != npass - 1) continue;
 
     // ---- epilogue of a finished tile (staging in the halo region) ----
@@ -627,23 +640,36 @@ static size_t halo_region_bytes(const HaloGeom& g, int BN, int CS) {
   return (r + 15) & ~(size_t)15;
 }
 
-static size_t halo_lds_bytes(const HaloGeom& g, int BN, int CS) {
-  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
-  const size_t T = (size_t)g.KD * g.KH * g.KW;
-  return halo_region_bytes(g, BN, CS) + 2 * (size_t)BN * H_BKS * 2 + hp * 4 + (T + 15) / 16 * 64 + 16;
+// weight stages of 128 k (TPS taps x CS channels) over all channel slices
+static int halo_nq(const HaloGeom& g, int CS) {
+  const int T = g.KD * g.KH * g.KW, tps = H_BKS / CS;
+  return (g.C / CS) * ((T + tps - 1) / tps);
 }
 
-template <int BN, int ACT, bool HB, bool ST, int CS>
+static size_t halo_lds_bytes(const HaloGeom& g, int BN, int CS, bool res) {
+  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  const size_t T = (size_t)g.KD * g.KH * g.KW;
+  const size_t stages = res ? (size_t)halo_nq(g, CS) : 2;
+  return halo_region_bytes(g, BN, CS) + stages * BN * H_BKS * 2 + hp * 4 + (T + 15) / 16 * 64 + 16;
+}
+
+// weights-resident variant: 8-channel slices, BN = 32, <= 4 stages (32 KB), and
+// still two workgroups per CU
+static bool halo_resident(const HaloGeom& g, int BN, int CS) {
+  return BN == 32 && CS == 8 && halo_nq(g, CS) <= 4 && halo_lds_bytes(g, BN, CS, true) <= 80 * 1024;
+}
+
+template <int BN, int ACT, bool HB, bool ST, int CS, bool RES>
 static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const bf16* s, const bf16* w,
                        const float* b, bf16* o, float* stats, const int* toffs, const HaloGeom& g, int Ncol) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_halo_kernel<BN, ACT, HB, ST, CS>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_halo_kernel<BN, ACT, HB, ST, CS, RES>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST, CS>), grid, dim3(H_NTHR), lds, st, s, w, b, o, stats, toffs,
+  hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST, CS, RES>), grid, dim3(H_NTHR), lds, st, s, w, b, o, stats, toffs,
                      g, Ncol, region);
   return 0;
 }
@@ -661,7 +687,8 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   if (CS == 0 || g.TD * g.TH * g.OW > H_BM || g.TD < 1 || g.TH < 1) return -2;
   if (stats && act != ACT_NONE) return -1;
   const int BN = Ncol <= 32 ? 32 : 64;
-  const size_t lds = halo_lds_bytes(g, BN, CS);
+  const bool res = halo_resident(g, BN, CS);
+  const size_t lds = halo_lds_bytes(g, BN, CS, res);
   const int region = (int)halo_region_bytes(g, BN, CS);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + BN - 1) / BN;
@@ -672,8 +699,10 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   bf16* o = (bf16*)out;
   const bool hb = bias != nullptr;
   int rc;
-#define HCASE(B, A, H, S, C) \
-  rc = launch_halo<B, A, H, S, C>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol)
+#define HCASE(B, A, H, S, C)                                                                     \
+  rc = (B == 32 && C == 8 && res)                                                                \
+           ? launch_halo<B, A, H, S, C, (B == 32 && C == 8)>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol) \
+           : launch_halo<B, A, H, S, C, false>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol)
 #define HBN(B, C)                                                   \
   do {                                                              \
     if (stats) HCASE(B, ACT_NONE, false, true, C);                  \
@@ -701,7 +730,7 @@ extern "C" int fn_conv_halo_workers(const int* geom16, int Ncol) {
   const int CS = halo_cs(g.C);
   if (CS == 0) return -2;
   const int BN = Ncol <= 32 ? 32 : 64;
-  const size_t lds = halo_lds_bytes(g, BN, CS);
+  const size_t lds = halo_lds_bytes(g, BN, CS, halo_resident(g, BN, CS));
   if (g_num_cus == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -717,7 +746,8 @@ extern "C" int fn_conv_halo_workers(const int* geom16, int Ncol) {
 
 extern "C" long long fn_conv_halo_lds(const int* geom16, int Ncol) {
   const HaloGeom g = parse_halo(geom16);
-  return (long long)halo_lds_bytes(g, Ncol <= 32 ? 32 : 64, halo_cs(g.C) ? halo_cs(g.C) : 16);
+  const int BN = Ncol <= 32 ? 32 : 64, CS = halo_cs(g.C) ? halo_cs(g.C) : 16;
+  return (long long)halo_lds_bytes(g, BN, CS, halo_resident(g, BN, CS));
 }
 
 static size_t halo_wgrad_lds(const HaloGeom& g, int MT, int CS) {

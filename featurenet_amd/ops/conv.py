@@ -31,6 +31,9 @@ from . import reference as ref
 from .spec import ConvSpec, act_code
 
 _TAB_LOCK = threading.Lock()
+# the space-to-depth forward pads K (FeatureNet-3D stem: 512 vs 343); it is taken when
+# the padded K is at most this multiple of the real one (else the packed-W gather runs)
+S2D_FWD_RATIO = float(os.environ.get("FN_S2D_FWD_RATIO", "1.25"))
 _TAB_CACHE: dict = {}
 
 
@@ -500,7 +503,7 @@ class ConvFn(torch.autograd.Function):
         bias = b.detach().float().contiguous() if b is not None else None
         s2d = s2d_plan(spec)
         x_saved = x5
-        if s2d is not None and s2d[1].kdim <= 1.25 * spec.kdim:
+        if s2d is not None and s2d[1].kdim <= S2D_FWD_RATIO * spec.kdim:
             # strided few-channel conv: space-to-depth -> stride-1 halo conv; the packed
             # input is what wgrad consumes, so it is saved instead of x
             f, spec2 = s2d

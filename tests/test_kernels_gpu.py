@@ -313,6 +313,7 @@ def test_conv_halo_fwd_dgrad_stats(case):
 @pytest.mark.parametrize("case", [
     (2, 9, 10, 11, 8, 32, (3, 3, 3), "same"),       # 8-channel halo slices (CS = 8), partial taps
     (2, 12, 12, 12, 8, 64, (4, 4, 4), "valid"),     # s2d-stem shape class, BN = 64
+    (2, 12, 12, 12, 8, 32, (4, 4, 4), "valid"),     # s2d stem, BN = 32: weights resident in LDS (4 stages)
     (3, 1, 17, 19, 24, 16, (1, 5, 5), "same"),      # C % 16 != 0 -> three 8-channel slices
 ])
 def test_conv_halo_cs8(case):
