@@ -240,6 +240,16 @@ class DeviceLoader:
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed + rank)
 
+    def derived(self, shuffle: bool = True, seed: int = 0, augment: bool = False) -> "DeviceLoader":
+        """Another loader over the SAME device-resident tensors (no re-upload of the set):
+        own shuffle order / generator, e.g. PreciseBN recalibration batches during fit."""
+        d = object.__new__(DeviceLoader)
+        d.__dict__.update(self.__dict__)
+        d.shuffle, d.augment = shuffle, augment
+        d.gen = torch.Generator(device=self.device)
+        d.gen.manual_seed(seed)
+        return d
+
     def __len__(self) -> int:
         n = len(self.x)
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)

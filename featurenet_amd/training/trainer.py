@@ -182,6 +182,10 @@ class Trainer:
         callbacks: list[Callback] = list(callbacks or [])
         loader = DeviceLoader(x, y, batch_size, self.device, shuffle=shuffle, augment=augment,
                               packed_size=packed_size, rank=self.rank, world=self.world, seed=seed)
+        val_loader = None
+        if validation_data is not None:   # uploaded once, not once per epoch
+            val_loader = DeviceLoader(*validation_data, batch_size, self.device, shuffle=False,
+                                      packed_size=packed_size, rank=self.rank, world=self.world)
         self.stop_training = False
         for cb in callbacks:
             cb.on_train_begin(self)
@@ -210,9 +214,10 @@ class Trainer:
                         "samples_per_s": float(stats[2]) / max(time.time() - t0, 1e-9)}
                 self._bn_fresh = False
                 if self.precise_bn and (validation_data is not None or epoch == epochs - 1):
-                    self.recalibrate_bn(x, y, self.precise_bn, batch_size, packed_size, seed + epoch)
-                if validation_data is not None:
-                    vl, va = self.evaluate(*validation_data, batch_size=batch_size, packed_size=packed_size)
+                    self.recalibrate_bn(x, y, self.precise_bn, batch_size, packed_size, seed + epoch,
+                                        loader=loader.derived(seed=seed + epoch + 7919 * (self.rank + 1)))
+                if val_loader is not None:
+                    vl, va = self.evaluate(None, None, loader=val_loader)
                     logs["val_loss"], logs["val_acc"] = vl, va
                 if not math.isfinite(logs["loss"]):
                     raise TrainingFailed("non-finite training loss")
@@ -226,7 +231,8 @@ class Trainer:
                 if self.stop_training:
                     break
             if self.precise_bn and not self._bn_fresh:    # stopped early without validation
-                self.recalibrate_bn(x, y, self.precise_bn, batch_size, packed_size, seed)
+                self.recalibrate_bn(x, y, self.precise_bn, batch_size, packed_size, seed,
+                                    loader=loader.derived(seed=seed + 7919 * (self.rank + 1)))
         except torch.cuda.OutOfMemoryError as e:   # reference: ResourceExhaustedError -> candidate dropped
             raise TrainingFailed(f"out of device memory: {e}") from e
         finally:
@@ -237,19 +243,21 @@ class Trainer:
 
     @torch.no_grad()
     def recalibrate_bn(self, x, y, batches: int = 32, batch_size: int = 128, packed_size: int | None = None,
-                       seed: int = 0) -> int:
+                       seed: int = 0, loader: DeviceLoader | None = None) -> int:
         """PreciseBN: set every BN layer's running mean / var to the average of the batch
         statistics over ``batches`` shuffled training batches (train-mode forward, no
         gradients, momentum 1/(k+1)); replicas average their estimates.  Returns the
-        number of batches used."""
+        number of batches used.  ``loader`` (e.g. ``DeviceLoader.derived`` of the fit
+        loader) reuses device-resident data instead of uploading ``x``/``y`` again."""
         mods = bn_modules(self.model)
         if not mods or batches <= 0:
             return 0
         saved = [getattr(m, a) for m, a in mods]
         was_training = self.model.training
         self.model.train()
-        loader = DeviceLoader(x, y, batch_size, self.device, shuffle=True, packed_size=packed_size,
-                              rank=self.rank, world=self.world, seed=seed + 7919)
+        if loader is None:
+            loader = DeviceLoader(x, y, batch_size, self.device, shuffle=True, packed_size=packed_size,
+                                  rank=self.rank, world=self.world, seed=seed + 7919)
         k = 0
         try:
             for xb, _ in loader:
@@ -273,10 +281,12 @@ class Trainer:
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()
-    def evaluate(self, x, y, batch_size: int = 256, packed_size: int | None = None) -> tuple[float, float]:
+    def evaluate(self, x, y, batch_size: int = 256, packed_size: int | None = None,
+                 loader: DeviceLoader | None = None) -> tuple[float, float]:
         self.model.eval()
-        loader = DeviceLoader(x, y, batch_size, self.device, shuffle=False, packed_size=packed_size,
-                              rank=self.rank, world=self.world)
+        if loader is None:
+            loader = DeviceLoader(x, y, batch_size, self.device, shuffle=False, packed_size=packed_size,
+                                  rank=self.rank, world=self.world)
         loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         correct = torch.zeros((), dtype=torch.int64, device=self.device)
         seen = 0

@@ -75,3 +75,64 @@ def test_bucketed_allreduce_matches_single_process(tmp_path, bucket_mb):
         acc += flat.grad
     ref = acc * (1.0 / WORLD)
     torch.testing.assert_close(g[0]["grad"], ref, rtol=1e-6, atol=1e-8)
+
+
+_BN_CFG = dict(input_size=16, num_classes=4, widths=(8, 8, 16, 16), kernels=(3, 3, 3, 3), strides=(1, 1, 1, 1),
+               fc=16)
+
+
+def _bn_shards(n=8, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.rand(WORLD * n, 16, 16, 16, 1, generator=g) < 0.3).float()
+    x[n:] *= 2.0                      # the two shards have different statistics
+    return x, torch.randint(0, 4, (WORLD * n,), generator=g)
+
+
+def _precise_bn_worker(rank, tmp):
+    dist.init_process_group("gloo", init_method=f"file://{tmp}/rdzv", rank=rank, world_size=WORLD)
+    try:
+        from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+        from featurenet_amd.training.trainer import Trainer
+
+        torch.manual_seed(rank)
+        tr = Trainer(FeatureNet3D(FeatureNet3DConfig(**_BN_CFG)), lr=1e-3, device="cpu")
+        x, y = _bn_shards()
+        # the trainer shards x by rank itself; one full-shard batch per rank
+        used = tr.recalibrate_bn(x, y, batches=1, batch_size=len(x) // WORLD)
+        assert used == 1
+        torch.save({k: v.clone() for k, v in tr.model.state_dict().items()}, f"{tmp}/bn{rank}.pt")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_precise_bn_averages_running_stats_across_ranks(tmp_path):
+    """PreciseBN under DP: every replica ends with the mean over ranks of its shard's batch statistics."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+    from featurenet_amd.training.trainer import bn_modules
+
+    mp.start_processes(_precise_bn_worker, args=(str(tmp_path),), nprocs=WORLD, start_method="spawn")
+    sd = [torch.load(tmp_path / f"bn{r}.pt", weights_only=True) for r in range(WORLD)]
+    for k in sd[0]:
+        assert torch.equal(sd[0][k], sd[1][k]), k           # replicas agree (weights broadcast, stats reduced)
+    # expected: the same model, momentum 1, one train-mode forward per shard, averaged
+    x, _ = _bn_shards()
+    n = len(x) // WORLD
+    per_rank = []
+    for r in range(WORLD):
+        m = FeatureNet3D(FeatureNet3DConfig(**_BN_CFG))
+        m.load_state_dict(sd[0])
+        mods = bn_modules(m)
+        for mod, attr in mods:
+            setattr(mod, attr, 1.0)
+        m.train()
+        with torch.no_grad():
+            m(x[r * n:(r + 1) * n])
+        per_rank.append([(mod.running_mean.clone(), mod.running_var.clone()) for mod, _ in mods])
+    m = FeatureNet3D(FeatureNet3DConfig(**_BN_CFG))
+    m.load_state_dict(sd[0])
+    for i, (mod, _) in enumerate(bn_modules(m)):
+        exp_mean = (per_rank[0][i][0] + per_rank[1][i][0]) / 2
+        exp_var = (per_rank[0][i][1] + per_rank[1][i][1]) / 2
+        torch.testing.assert_close(mod.running_mean, exp_mean, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(mod.running_var, exp_var, rtol=1e-4, atol=1e-5)
+        assert not torch.allclose(per_rank[0][i][0], per_rank[1][i][0])   # shards really differ
