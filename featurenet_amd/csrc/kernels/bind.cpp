@@ -42,7 +42,10 @@ int fn_bn_bwd_apply(const void*, const void*, const float*, const float*, const 
                     const float*, void*, long long, int, float, int, hipStream_t);
 int fn_pool_fwd(const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd(const void*, const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
-int fn_softmax_xent(const float*, const long long*, float*, float*, int*, int, int, float, float, hipStream_t);
+int fn_softmax_xent_blocks(long long, int);
+int fn_upsample2x(const void*, void*, int, int, int, int, int, int, hipStream_t);
+int fn_softmax_xent_rows(const void*, int, const long long*, float*, void*, int*, long long, int, float, float,
+                         hipStream_t);
 int fn_adam_flat_dev(float*, const float*, float*, float*, void*, long long, const float*, int*, int, hipStream_t);
 int fn_adam_flat(float*, const float*, float*, float*, void*, long long, float, float, float, float, float, float,
                  float, float, int, hipStream_t);
@@ -184,11 +187,16 @@ PYBIND11_MODULE(_C, m) {
                     P<const float*>(shift), geom.data(), is_max, count_pad, act, S(st)),
         "pool_bwd");
   });
-  m.def("softmax_xent", [](uintptr_t logits, uintptr_t labels, uintptr_t loss, uintptr_t dlogits, uintptr_t correct,
-                           int B, int NC, float gscale, float smoothing, uintptr_t st) {
-    chk(fn_softmax_xent(P<const float*>(logits), P<const long long*>(labels), P<float*>(loss), P<float*>(dlogits),
-                        P<int*>(correct), B, NC, gscale, smoothing, S(st)),
-        "softmax_xent");
+  m.def("upsample2x", [](uintptr_t x, uintptr_t y, int N, int D, int H, int W, int C, int backward, uintptr_t st) {
+    chk(fn_upsample2x(P<const void*>(x), P<void*>(y), N, D, H, W, C, backward, S(st)), "upsample2x");
+  });
+  m.def("softmax_xent_blocks", [](long long B, int NC) { return fn_softmax_xent_blocks(B, NC); });
+  m.def("softmax_xent_rows", [](uintptr_t logits, int in_bf16, uintptr_t labels, uintptr_t block_loss,
+                                uintptr_t dlogits, uintptr_t correct, long long B, int NC, float gscale,
+                                float smoothing, uintptr_t st) {
+    chk(fn_softmax_xent_rows(P<const void*>(logits), in_bf16, P<const long long*>(labels), P<float*>(block_loss),
+                             P<void*>(dlogits), P<int*>(correct), B, NC, gscale, smoothing, S(st)),
+        "softmax_xent_rows");
   });
   m.def("adam_flat_dev", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t pb, long long n,
                             uintptr_t hp, uintptr_t t, int keras_eps, uintptr_t st) {

@@ -1,7 +1,8 @@
 // Loss, optimizer and elementwise kernels (gfx950).
 //
-//   softmax_xent   : fused log-softmax + NLL forward and d(logits) in one pass,
-//                    one 64-lane wave per row, plus per-row correctness flags
+//   softmax_xent   : fused log-softmax + NLL forward and d(logits) in one pass
+//                    (8 lanes per row for NC <= 64, bf16 or fp32 in/out),
+//                    per-block loss partials and per-row correctness flags
 //                    (top-1 accuracy without a host sync).
 //   adam_flat      : multi-tensor Adam over ONE flat fp32 parameter buffer
 //                    (all parameters of a model live in a single allocation),
@@ -15,47 +16,155 @@
 #include "common.h"
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits,
-                                                           const long long* __restrict__ labels,
-                                                           float* __restrict__ loss, float* __restrict__ dlogits,
-                                                           int* __restrict__ correct, int B, int NC, float gscale,
-                                                           float smoothing) {
-  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wave >= B) return;
-  const float* row = logits + (long long)wave * NC;
-  float mx = -INFINITY;
-  int amax = 0;
-  for (int c = lane; c < NC; c += 64) {
-    const float v = row[c];
-    if (v > mx) { mx = v; amax = c; }
-  }
-  // wave arg-max (lowest index on ties)
+// Dense-prediction form (per-voxel segmentation: millions of rows, NC ~ 25):
+// LPR lanes per row (8 for NC <= 64, so a wave covers 8 rows and the loads of a
+// wave are one contiguous run), bf16 or fp32 logits read directly, d(logits)
+// written in the logits' dtype with 1/B folded in, per-block partial loss sums
+// (no per-row loss array, no host sync); grid-stride over rows.
+template <typename TIn, int LPR, int EPL>
+__global__ __launch_bounds__(256) void softmax_xent_rows_kernel(const TIn* __restrict__ logits,
+                                                                const long long* __restrict__ labels,
+                                                                float* __restrict__ block_loss, TIn* __restrict__ dlogits,
+                                                                int* __restrict__ correct, long long B, int NC,
+                                                                float gscale, float smoothing) {
+  // EPL > 0: the row (<= LPR*EPL classes) is read ONCE into registers; EPL = 0: any NC,
+  // re-read per pass
+  constexpr int RPB = 256 / LPR;
+  __shared__ float red[256 / 64];
+  const int sub = threadIdx.x % LPR, rloc = threadIdx.x / LPR;
+  const float off = smoothing / (float)NC, on = 1.f - smoothing + off;
+  float acc = 0.f;
+  auto ld = [](const TIn* p) -> float {
+    if constexpr (sizeof(TIn) == 2) return bf2f(*p); else return (float)*p;
+  };
+  for (long long r0 = (long long)blockIdx.x * RPB; r0 < B; r0 += (long long)gridDim.x * RPB) {
+    const long long row = r0 + rloc;
+    const bool live = row < B;
+    const TIn* rp = logits + (live ? row : 0) * NC;
+    float mx = -INFINITY;
+    int am = 0;
+    float v[EPL > 0 ? EPL : 1];
+    if constexpr (EPL > 0) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float om = __shfl_xor(mx, o, 64);
-    const int oa = __shfl_xor(amax, o, 64);
-    if (om > mx || (om == mx && oa < amax)) { mx = om; amax = oa; }
+      for (int e = 0; e < EPL; ++e) {
+        const int c = sub + e * LPR;
+        v[e] = c < NC ? ld(rp + c) : -INFINITY;
+        if (v[e] > mx) { mx = v[e]; am = c; }
+      }
+    } else {
+      for (int c = sub; c < NC; c += LPR) {
+        const float x = ld(rp + c);
+        if (x > mx) { mx = x; am = c; }
+      }
+    }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) {          // group arg-max, lowest index on ties
+      const float om = __shfl_xor(mx, o, 64);
+      const int oa = __shfl_xor(am, o, 64);
+      if (om > mx || (om == mx && oa < am)) { mx = om; am = oa; }
+    }
+    float se = 0.f;
+    if constexpr (EPL > 0) {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) se += sub + e * LPR < NC ? __expf(v[e] - mx) : 0.f;
+    } else {
+      for (int c = sub; c < NC; c += LPR) se += __expf(ld(rp + c) - mx);
+    }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+    const float lse = mx + __logf(se);
+    const long long y = live ? labels[row] : -1;
+    float lrow = 0.f;
+    auto out = [&](int c, float x) {
+      const float lp = x - lse;
+      const float tgt = (c == y) ? on : off;
+      lrow -= tgt * lp;
+      if (live) {
+        const float d = (__expf(lp) - tgt) * gscale;
+        if constexpr (sizeof(TIn) == 2) dlogits[row * NC + c] = f2bf(d); else dlogits[row * NC + c] = d;
+      }
+    };
+    if constexpr (EPL > 0) {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e)
+        if (sub + e * LPR < NC) out(sub + e * LPR, v[e]);
+    } else {
+      for (int c = sub; c < NC; c += LPR) out(c, ld(rp + c));
+    }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) lrow += __shfl_xor(lrow, o, 64);
+    if (live && sub == 0) {
+      acc += lrow;
+      if (correct) correct[row] = (am == y) ? 1 : 0;
+    }
   }
-  float se = 0.f;
-  for (int c = lane; c < NC; c += 64) se += __expf(row[c] - mx);
-  se = wave_sum(se);
-  const float lse = mx + __logf(se);
-  const long long y = labels[wave];
-  const float off = smoothing / (float)NC;
-  const float on = 1.f - smoothing + off;
-  float lrow = 0.f;
-  for (int c = lane; c < NC; c += 64) {
-    const float lp = row[c] - lse;
-    const float tgt = (c == y) ? on : off;
-    lrow -= tgt * lp;
-    if (dlogits) dlogits[(long long)wave * NC + c] = (__expf(lp) - tgt) * gscale;
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) block_loss[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// Tile form for bf16 logits with NC <= NCMAX (the per-voxel segmentation loss):
+// 256 rows per tile move between HBM and LDS as 16-byte vectors (the tile is one
+// contiguous run of 256*NC bf16), then every thread owns one row entirely in
+// registers -- no cross-lane reductions, every global access coalesced.
+template <int NCMAX>
+__global__ __launch_bounds__(256) void softmax_xent_tile_kernel(const bf16* __restrict__ logits,
+                                                                const long long* __restrict__ labels,
+                                                                float* __restrict__ block_loss,
+                                                                bf16* __restrict__ dlogits, int* __restrict__ correct,
+                                                                long long B, int NC, float gscale, float smoothing) {
+  __shared__ __attribute__((aligned(16))) bf16 tile[256 * NCMAX];
+  __shared__ float red[4];
+  const int tid = threadIdx.x;
+  const float off = smoothing / (float)NC, on = 1.f - smoothing + off;
+  float acc = 0.f;
+  for (long long r0 = (long long)blockIdx.x * 256; r0 < B; r0 += (long long)gridDim.x * 256) {
+    const int rows = (int)(B - r0 < 256 ? B - r0 : 256);
+    const int nel = rows * NC;
+    const bf16* src = logits + r0 * NC;           // 16-B aligned: r0 * NC * 2 = 512 * NC * k
+    const int nvec = nel >> 3;
+    __syncthreads();                               // previous tile's stores are done with `tile`
+    for (int i = tid; i < nvec; i += 256) *(uint4*)(tile + i * 8) = *(const uint4*)(src + i * 8);
+    for (int i = (nvec << 3) + tid; i < nel; i += 256) tile[i] = src[i];
+    __syncthreads();
+    if (tid < rows) {
+      const long long row = r0 + tid;
+      float v[NCMAX];
+      float mx = -INFINITY;
+      int am = 0;
+#pragma unroll
+      for (int c = 0; c < NCMAX; ++c) {
+        v[c] = c < NC ? bf2f(tile[tid * NC + c]) : -INFINITY;
+        if (v[c] > mx) { mx = v[c]; am = c; }
+      }
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCMAX; ++c) se += c < NC ? __expf(v[c] - mx) : 0.f;
+      const float lse = mx + __logf(se);
+      const long long y = labels[row];
+      float lrow = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCMAX; ++c) {
+        if (c < NC) {
+          const float lp = v[c] - lse;
+          const float tgt = (c == y) ? on : off;
+          lrow -= tgt * lp;
+          tile[tid * NC + c] = f2bf((__expf(lp) - tgt) * gscale);   // own row only: no race
+        }
+      }
+      acc += lrow;
+      if (correct) correct[row] = (am == y) ? 1 : 0;
+    }
+    __syncthreads();
+    bf16* dst = dlogits + r0 * NC;
+    for (int i = tid; i < nvec; i += 256) *(uint4*)(dst + i * 8) = *(const uint4*)(tile + i * 8);
+    for (int i = (nvec << 3) + tid; i < nel; i += 256) dst[i] = tile[i];
   }
-  lrow = wave_sum(lrow);
-  if (lane == 0) {
-    loss[wave] = lrow;
-    if (correct) correct[wave] = (amax == y) ? 1 : 0;
-  }
+  acc = wave_sum(acc);
+  if ((tid & 63) == 0) red[tid >> 6] = acc;
+  __syncthreads();
+  if (tid == 0) block_loss[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
 // ---------------------------------------------------------------------------
@@ -179,11 +288,112 @@ static unsigned blocks_for(long long work) {
   return (unsigned)b;
 }
 
-extern "C" int fn_softmax_xent(const float* logits, const long long* labels, float* loss, float* dlogits,
-                               int* correct, int B, int NC, float gscale, float smoothing, hipStream_t st) {
-  const unsigned blocks = (unsigned)((B + 3) / 4);
-  hipLaunchKernelGGL(softmax_xent_kernel, dim3(blocks), dim3(256), 0, st, logits, labels, loss, dlogits, correct, B, NC,
-                     gscale, smoothing);
+// ---------------------------------------------------------------------------
+// Nearest-neighbour x2 upsampling of a channels-last [N, D, H, W, C] grid (the
+// segmentation decoder) and its backward (sum over each 2x2x2 block, fp32).
+// One thread per 8-channel source vector: forward = 1 load, 8 stores;
+// backward = 8 loads, 1 store.  C % 8 == 0.
+__global__ __launch_bounds__(256) void upsample2x_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int D,
+                                                         int H, int W, int C, long long total) {
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= total) return;
+  const int cpr = C >> 3;
+  const int cv = (int)(i % cpr);
+  long long t = i / cpr;
+  const int w = (int)(t % W); t /= W;
+  const int h = (int)(t % H); t /= H;
+  const int d = (int)(t % D);
+  const long long n = t / D;
+  const uint4 v = *(const uint4*)(x + i * 8);
+  const long long W2 = 2LL * W, H2 = 2LL * H;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const long long base = (((n * 2 * D + 2 * d + a) * H2 + 2 * h + b) * W2 + 2 * w) * C + cv * 8;
+      *(uint4*)(y + base) = v;
+      *(uint4*)(y + base + C) = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                                                             int D, int H, int W, int C, long long total) {
+  const long long i = blockIdx.x * 256LL + threadIdx.x;
+  if (i >= total) return;
+  const int cpr = C >> 3;
+  const int cv = (int)(i % cpr);
+  long long t = i / cpr;
+  const int w = (int)(t % W); t /= W;
+  const int h = (int)(t % H); t /= H;
+  const int d = (int)(t % D);
+  const long long n = t / D;
+  const long long W2 = 2LL * W, H2 = 2LL * H;
+  Pack8 p[8];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const long long base = (((n * 2 * D + 2 * d + a) * H2 + 2 * h + b) * W2 + 2 * w) * C + cv * 8;
+      p[(a * 2 + b) * 2].u = *(const uint4*)(dy + base);
+      p[(a * 2 + b) * 2 + 1].u = *(const uint4*)(dy + base + C);
+    }
+  Pack8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += bf2f(p[k].e[j]);
+    o.e[j] = f2bf(s);
+  }
+  *(uint4*)(dx + i * 8) = o.u;
+}
+
+extern "C" int fn_upsample2x(const void* x, void* y, int N, int D, int H, int W, int C, int backward,
+                             hipStream_t st) {
+  if (C % 8) return -2;
+  const long long total = (long long)N * D * H * W * (C / 8);
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  if (backward)
+    hipLaunchKernelGGL(upsample2x_bwd_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)y, D, H, W, C,
+                       total);
+  else
+    hipLaunchKernelGGL(upsample2x_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)y, D, H, W, C,
+                       total);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+static int sx_lpr(int NC) { return NC <= 64 ? 8 : 64; }
+
+// number of partial loss sums softmax_xent_rows writes (= its grid); the bf16 tile
+// kernel (NC <= 32) covers 256 rows per block, the lane-group kernel 256/LPR
+extern "C" int fn_softmax_xent_blocks(long long B, int NC) {
+  const long long rpb = NC <= 32 ? 256 : 256 / sx_lpr(NC);
+  const long long need = (B + rpb - 1) / rpb;
+  return (int)(need < 8192 ? (need > 0 ? need : 1) : 8192);
+}
+
+// logits / dlogits bf16 (in_bf16 = 1) or fp32; block_loss: fp32 [fn_softmax_xent_blocks]
+extern "C" int fn_softmax_xent_rows(const void* logits, int in_bf16, const long long* labels, float* block_loss,
+                                    void* dlogits, int* correct, long long B, int NC, float gscale, float smoothing,
+                                    hipStream_t st) {
+  const unsigned blocks = (unsigned)fn_softmax_xent_blocks(B, NC);
+#define SX(T, L, E)                                                                                                \
+  hipLaunchKernelGGL((softmax_xent_rows_kernel<T, L, E>), dim3(blocks), dim3(256), 0, st, (const T*)logits, labels, \
+                     block_loss, (T*)dlogits, correct, B, NC, gscale, smoothing)
+#define SX_T(T)                                         \
+  do {                                                  \
+    if (NC <= 32) SX(T, 8, 4);                          \
+    else if (NC <= 64) SX(T, 8, 8);                     \
+    else SX(T, 64, 0);                                  \
+  } while (0)
+  if (in_bf16 && NC <= 32)
+    hipLaunchKernelGGL(softmax_xent_tile_kernel<32>, dim3(blocks), dim3(256), 0, st, (const bf16*)logits, labels,
+                       block_loss, (bf16*)dlogits, correct, B, NC, gscale, smoothing);
+  else if (in_bf16) SX_T(bf16);
+  else SX_T(float);
+#undef SX_T
+#undef SX
   FN_CHECK_LAUNCH();
   return 0;
 }

@@ -25,6 +25,7 @@ from dataclasses import asdict, dataclass, field
 import torch
 from torch import nn
 
+from ..ops.elementwise import upsample2x
 from .layers import Conv, Dense
 
 
@@ -145,8 +146,5 @@ class FeatureNet3DSeg(nn.Module):
             x = x.unsqueeze(-1)
         for c in self.enc:
             x = c(x)
-        # nearest x2 upsample on the channels-last grid
-        n, d, h, w, c = x.shape
-        x = x.reshape(n, d, 1, h, 1, w, 1, c).expand(n, d, 2, h, 2, w, 2, c).reshape(n, 2 * d, 2 * h, 2 * w, c)
-        x = self.dec(x.contiguous())
+        x = self.dec(upsample2x(x))        # nearest x2 upsample on the channels-last grid
         return self.head(x)  # [N, S, S, S, classes]

@@ -98,3 +98,32 @@ def zero_pad(x5: torch.Tensor, pads) -> torch.Tensor:
     """Zero-pad spatial dims of a 5-D channels-last tensor; pads = (d, h, w) per side."""
     pd, ph, pw = pads
     return torch.nn.functional.pad(x5, (0, 0, pw, pw, ph, ph, pd, pd))
+
+
+class Upsample2xFn(torch.autograd.Function):
+    """Nearest x2 upsampling of a channels-last grid (``upsample2x`` kernels on GPU)."""
+
+    @staticmethod
+    def forward(ctx, x5):
+        N, D, H, W, C = x5.shape
+        xb = x5.to(torch.bfloat16).contiguous()
+        y = torch.empty(N, 2 * D, 2 * H, 2 * W, C, dtype=torch.bfloat16, device=x5.device)
+        _native.kernels().upsample2x(xb.data_ptr(), y.data_ptr(), N, D, H, W, C, 0, _native.stream(xb))
+        ctx.shape = (N, D, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, D, H, W, C = ctx.shape
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.empty(N, D, H, W, C, dtype=torch.bfloat16, device=dy.device)
+        _native.kernels().upsample2x(dy.data_ptr(), dx.data_ptr(), N, D, H, W, C, 1, _native.stream(dy))
+        return dx
+
+
+def upsample2x(x5: torch.Tensor) -> torch.Tensor:
+    """[N, D, H, W, C] -> [N, 2D, 2H, 2W, C], nearest neighbour."""
+    if _native.use_native(x5) and x5.shape[-1] % 8 == 0:
+        return Upsample2xFn.apply(x5)
+    n, d, h, w, c = x5.shape
+    return x5.reshape(n, d, 1, h, 1, w, 1, c).expand(n, d, 2, h, 2, w, 2, c).reshape(n, 2 * d, 2 * h, 2 * w, c)

@@ -16,24 +16,29 @@ from . import reference as ref
 
 class SoftmaxXentFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, labels, smoothing: float):
+    def forward(ctx, logits, labels, smoothing: float, want_correct: bool = True):
         B, NC = logits.shape
-        lg = logits.float().contiguous()
-        loss_rows = torch.empty(B, dtype=torch.float32, device=lg.device)
-        dlog = torch.empty_like(lg)
-        correct = torch.empty(B, dtype=torch.int32, device=lg.device)
-        _native.kernels().softmax_xent(lg.data_ptr(), labels.contiguous().data_ptr(), loss_rows.data_ptr(),
-                                       dlog.data_ptr(), correct.data_ptr(), B, NC, 1.0 / B, float(smoothing),
-                                       _native.stream(lg))
+        lg = logits.contiguous()
+        if lg.dtype not in (torch.bfloat16, torch.float32):
+            lg = lg.float()
+        K = _native.kernels()
+        nblk = K.softmax_xent_blocks(B, NC)
+        part = torch.empty(max(int(nblk), 1), dtype=torch.float32, device=lg.device)
+        dlog = torch.empty_like(lg)                     # 1/B folded in, logits' dtype
+        correct = torch.empty(B, dtype=torch.int32, device=lg.device) if want_correct else None
+        K.softmax_xent_rows(lg.data_ptr(), int(lg.dtype == torch.bfloat16), labels.contiguous().data_ptr(),
+                            part.data_ptr(), dlog.data_ptr(), _native.ptr(correct), B, NC, 1.0 / B,
+                            float(smoothing), _native.stream(lg))
         ctx.save_for_backward(dlog)
         ctx.in_dtype = logits.dtype
-        ctx.mark_non_differentiable(correct)
-        return loss_rows.mean(), correct
+        if correct is not None:
+            ctx.mark_non_differentiable(correct)
+        return part.sum() / B, correct
 
     @staticmethod
     def backward(ctx, dloss, _dc):
         (dlog,) = ctx.saved_tensors
-        return (dlog * dloss).to(ctx.in_dtype), None, None
+        return (dlog * dloss.to(dlog.dtype)).to(ctx.in_dtype), None, None, None
 
 
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0, with_correct: bool = False):
@@ -46,7 +51,7 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 
         logits = logits.reshape(-1, logits.shape[-1])
         labels = labels.reshape(-1)
     if _native.use_native(logits):
-        loss, correct = SoftmaxXentFn.apply(logits, labels.long(), smoothing)
+        loss, correct = SoftmaxXentFn.apply(logits, labels.long(), smoothing, with_correct)
         return (loss, correct) if with_correct else loss
     loss = ref.softmax_xent(logits, labels.long(), smoothing)
     if with_correct:

@@ -187,6 +187,29 @@ def test_softmax_xent():
         assert int(correct.sum()) == int((logits.argmax(-1) == labels).sum())
 
 
+def test_softmax_xent_dense_bf16():
+    """Per-voxel form: bf16 logits [N, D, H, W, NC] read directly, bf16 d(logits), partial-sum loss,
+    label smoothing; vs the fp32 torch reference on the same (bf16-rounded) logits."""
+    _native_loaded()
+    from featurenet_amd.ops.loss import softmax_xent
+
+    torch.manual_seed(6)
+    for shape, NC, sm in (((2, 9, 10, 11), 25, 0.0), ((3, 7, 5, 4), 25, 0.1), ((50000,), 70, 0.0)):
+        logits = (torch.randn(*shape, NC, device="cuda") * 3).to(torch.bfloat16)
+        labels = torch.randint(0, NC, shape, device="cuda")
+        lr_ = logits.float().reshape(-1, NC).clone().requires_grad_(True)
+        l_ref = torch.nn.functional.cross_entropy(lr_, labels.reshape(-1), label_smoothing=sm)
+        l_ref.backward()
+        ln_ = logits.clone().requires_grad_(True)
+        l_nat, correct = softmax_xent(ln_, labels, smoothing=sm, with_correct=True)
+        l_nat.backward()
+        assert ln_.grad.dtype == torch.bfloat16
+        torch.testing.assert_close(l_nat, l_ref, rtol=1e-4, atol=1e-5)
+        g = ln_.grad.float().reshape(-1, NC)
+        assert (g - lr_.grad).abs().max().item() <= 1e-2 * lr_.grad.abs().max().item()
+        assert int(correct.sum()) == int((logits.float().argmax(-1) == labels).sum())
+
+
 @pytest.mark.parametrize("keras", [True, False])
 def test_adam_flat(keras):
     _native_loaded()
@@ -531,3 +554,21 @@ def test_halo_pack_weights_matches_torch_layout(K, C, k):
     if K % 8 == 0:
         ref_d = Cm.halo_weights(w3.flip(1).permute(2, 1, 0))
         torch.testing.assert_close(Cm.halo_pack(w, spec, dgrad=True), ref_d, rtol=0, atol=0)
+
+
+def test_upsample2x_fwd_bwd():
+    """Nearest x2 upsample kernels vs the torch expand/reshape reference (fwd exact, bwd block sums)."""
+    _native_loaded()
+    from featurenet_amd.ops.elementwise import upsample2x
+
+    torch.manual_seed(9)
+    x = torch.randn(2, 3, 4, 5, 16, device="cuda").to(torch.bfloat16)
+    xn = x.clone().requires_grad_(True)
+    y = upsample2x(xn)
+    n, d, h, w, c = x.shape
+    ref_y = x.reshape(n, d, 1, h, 1, w, 1, c).expand(n, d, 2, h, 2, w, 2, c).reshape(n, 2 * d, 2 * h, 2 * w, c)
+    assert torch.equal(y, ref_y)
+    g = torch.randn_like(y.float()).to(torch.bfloat16)
+    y.backward(g)
+    ref_g = g.float().reshape(n, d, 2, h, 2, w, 2, c).sum((2, 4, 6))
+    torch.testing.assert_close(xn.grad.float(), ref_g, rtol=1e-2, atol=2e-2)

@@ -30,7 +30,7 @@ class _FakeK:
         def f(*args):
             assert len(args) == n, f"{name}: called with {len(args)} args, binding takes {n}"
             self.calls.append(name)
-            if name.endswith("_lds") or name.endswith("mblocks") or name.endswith("_workers"):
+            if name.endswith(("_lds", "mblocks", "_workers", "_blocks")):
                 return 1
             return None
         return f
@@ -77,7 +77,12 @@ def test_igemm_and_misc_calls_match_bindings(fake):
     y = C.DepthwiseFn.forward(type("Ctx", (), {"save_for_backward": lambda self, *a: None})(), xs,
                               torch.zeros(8, 1, 3, 3, 1), None, ds, 0)
     assert y.shape == (2, 1, 9, 9, 8)
-    assert {"igemm_fwd", "igemm_wgrad", "colstats", "bn_finalize", "dw_fwd"} <= set(fake.calls)
+    from featurenet_amd.ops.loss import SoftmaxXentFn
+
+    SoftmaxXentFn.forward(type("Ctx", (), {"save_for_backward": lambda self, *a: None,
+                                           "mark_non_differentiable": lambda self, *a: None})(),
+                          torch.zeros(6, 25, dtype=torch.bfloat16), torch.zeros(6, dtype=torch.long), 0.0, True)
+    assert {"igemm_fwd", "igemm_wgrad", "colstats", "bn_finalize", "dw_fwd", "softmax_xent_rows"} <= set(fake.calls)
 
 
 def test_fp8_inference_calls_match_bindings(fake):
