@@ -87,14 +87,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("igemm_fwd_mblocks", &fn_igemm_fwd_mblocks);
   m.def("conv_halo", [](uintptr_t src, uintptr_t wt, uintptr_t bias, uintptr_t out, uintptr_t stats,
                         uintptr_t toffs, std::vector<int> geom, int ncol, int act, uintptr_t st) {
-    need(geom, 16, "conv_halo");
+    need(geom, 17, "conv_halo");
     chk(fn_conv_halo(P<const void*>(src), P<const void*>(wt), P<const float*>(bias), P<void*>(out), P<float*>(stats),
                      P<const int*>(toffs), geom.data(), ncol, act, S(st)),
         "conv_halo");
   });
   m.def("conv_halo_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t dw, std::vector<int> geom, int cout,
                               int grid_x, uintptr_t st) {
-    need(geom, 16, "conv_halo_wgrad");
+    need(geom, 17, "conv_halo_wgrad");
     chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x, S(st)),
         "conv_halo_wgrad");
   });
@@ -131,11 +131,11 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_dw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), geom.data(), splits, S(st)), "dw_wgrad");
   });
   m.def("conv_halo_workers", [](std::vector<int> geom, int ncol) {
-    need(geom, 16, "conv_halo_workers");
+    need(geom, 17, "conv_halo_workers");
     return fn_conv_halo_workers(geom.data(), ncol);
   });
   m.def("conv_halo_lds", [](std::vector<int> geom, int ncol) {
-    need(geom, 16, "conv_halo_lds");
+    need(geom, 17, "conv_halo_lds");
     return fn_conv_halo_lds(geom.data(), ncol);
   });
   m.def("igemm_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t part, uintptr_t tab, std::vector<int> geom,

@@ -7,7 +7,7 @@
 // a 3-D input tile (the output tile plus its kernel halo) in LDS ONCE per
 // 16-channel slice and builds every MFMA A-fragment straight from it:
 //
-//   output tile  TD x TH x OW   (<= 256 rows; full output rows in W)
+//   output tile  TD x TH x TW   (<= 256 rows; TW = OW, or a W split for wide outputs)
 //   LDS halo     (TD+KD-1) x (TH+KH-1) x (OW+KW-1) positions x 16 channels
 //   K loop       pass p over C/16 channel slices, 2 taps per MFMA k-step
 //                (k = [tap][16 ch]), weights streamed through a double-
@@ -28,8 +28,22 @@ struct HaloGeom {
   int OD, OH, OW;          // output dims
   int KD, KH, KW;          // kernel
   int pd, ph, pw;          // leading pads (stride 1)
-  int TD, TH;              // output tile (rows = TD * TH * OW <= 256)
+  int TD, TH;              // output tile (rows = TD * TH * TW <= 256)
+  int TW;                  // tile width in W (OW, or OW split into ceil(OW / TW) column tiles)
 };
+
+// tile index -> (n, td_i, th_i, tw_i); W tiles vary fastest, so consecutive tiles of a
+// workgroup share halo rows
+struct TileIdx { int n, td, th, tw; };
+__device__ __forceinline__ TileIdx tile_idx(int tile, int tdn, int thn, int twn) {
+  TileIdx t;
+  t.tw = twn == 1 ? 0 : tile % twn;               // full-width tiles (the common case): no division
+  const int r = twn == 1 ? tile : tile / twn;
+  t.th = r % thn;
+  t.td = (r / thn) % tdn;
+  t.n = r / (thn * tdn);
+  return t;
+}
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
 // (lgkmcnt) but NOT for outstanding global loads, unlike __syncthreads(), whose
@@ -80,7 +94,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   constexpr int B_PER_T = (B_CHUNKS + H_NTHR - 1) / H_NTHR;
   constexpr int LDO = BN + 8;
 
-  const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
+  const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int HP = HD * HH * HW;                   // halo positions
   const int nchunk = HP * CPP;
   const int T = g.KD * g.KH * g.KW;
@@ -89,9 +103,9 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   const int npass = g.C / CS;
   const int nq = spp * npass;
   const int ldw = npass * Tp * CS;
-  const int rows = g.TD * g.TH * g.OW;
-  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
-  const int ntiles = g.N * tdn * thn;
+  const int rows = g.TD * g.TH * g.TW;
+  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH, twn = (g.OW + g.TW - 1) / g.TW;
+  const int ntiles = g.N * tdn * thn * twn;
 
   bf16* halo = reinterpret_cast<bf16*>(dsm);                      // also the epilogue staging area
   bf16* Bs = reinterpret_cast<bf16*>(dsm + region_bytes);
@@ -132,29 +146,26 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   for (int mt = 0; mt < 4; ++mt) {
     const int r = wrow * 64 + mt * 16 + lr;
     const int rr = r < rows ? r : 0;
-    const int w = rr % g.OW, th = (rr / g.OW) % g.TH, td = rr / (g.OW * g.TH);
+    const int w = rr % g.TW, th = (rr / g.TW) % g.TH, td = rr / (g.TW * g.TH);
     hbase[mt] = (td * HH + th) * HW + w;
   }
   __syncthreads();
 
   constexpr int HC = H_HC(BN);
   uint4 hreg[HC > 0 ? HC : 1];
-  auto halo_src = [&](int job, int c, const bf16*& base, int& off) -> bool {
+  // halo origin of a job (wave-uniform; decoded once per job, not per chunk)
+  auto job_origin = [&](int job, const bf16*& base, int& dlo, int& hlo, int& wlo) {
     const int tile = t_begin + job / npass, p = job % npass;
-    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
-    const int info = posinfo[c < nchunk ? c / CPP : 0];
-    const int gd = td_i * g.TD - g.pd + (info >> 20), gh = th_i * g.TH - g.ph + ((info >> 10) & 1023);
-    const int gw = (info & 1023) - g.pw;
-    base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * CS;
-    off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c % CPP) * 8;
-    return c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-           (unsigned)gw < (unsigned)g.IW;
+    const TileIdx ti = tile_idx(tile, tdn, thn, twn);
+    dlo = ti.td * g.TD - g.pd;
+    hlo = ti.th * g.TH - g.ph;
+    wlo = ti.tw * g.TW - g.pw;
+    base = src + (long long)ti.n * g.ID * g.IH * g.IW * g.C + p * CS;
   };
   auto prefetch_halo = [&](int job) {
-    const int tile = t_begin + job / npass, p = job % npass;
-    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
-    const int dlo = td_i * g.TD - g.pd, hlo = th_i * g.TH - g.ph;
-    const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + p * CS;
+    const bf16* base;
+    int dlo, hlo, wlo;
+    job_origin(job, base, dlo, hlo, wlo);
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
       // chunks past the halo are clamped to the last one (a duplicate, identical
@@ -162,7 +173,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       // compiler never has to assume a load still in flight at the k-loop top
       const int c = min(i * H_NTHR + tid, nchunk - 1);
       const int info = posinfo[c / CPP];
-      const int gd = dlo + (info >> 20), gh = hlo + ((info >> 10) & 1023), gw = (info & 1023) - g.pw;
+      const int gd = dlo + (info >> 20), gh = hlo + ((info >> 10) & 1023), gw = wlo + (info & 1023);
       const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH && (unsigned)gw < (unsigned)g.IW;
       const int off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c % CPP) * 8;
       const uint4 x = *(const uint4*)(base + (ok ? off : 0));
@@ -175,14 +186,19 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       const int c = min(i * H_NTHR + tid, nchunk - 1);
       *(uint4*)(halo + (size_t)c * 8) = hreg[i];
     }
+    if (HC * H_NTHR >= nchunk) return;
+    const bf16* base;
+    int dlo, hlo, wlo;
+    job_origin(job, base, dlo, hlo, wlo);
     for (int c0 = HC * H_NTHR; c0 < nchunk; c0 += 4 * H_NTHR) {   // tail of a large halo: synchronous
       uint4 v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bf16* base;
-        int off;
         const int c = min(c0 + j * H_NTHR + tid, nchunk - 1);
-        const bool ok = halo_src(job, c, base, off);
+        const int info = posinfo[c / CPP];
+        const int gd = dlo + (info >> 20), gh = hlo + ((info >> 10) & 1023), gw = wlo + (info & 1023);
+        const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH && (unsigned)gw < (unsigned)g.IW;
+        const int off = ((gd * g.IH + gh) * g.IW + gw) * g.C + (c % CPP) * 8;
         const uint4 x = *(const uint4*)(base + (ok ? off : 0));
         v[j] = ok ? x : make_uint4(0, 0, 0, 0);
       }
@@ -298,8 +314,10 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 
     // ---- epilogue of a finished tile (staging in the halo region) ----
     const int tile = t_begin + job / npass;
-    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
-    const int d0 = td_i * g.TD, h0 = th_i * g.TH;
+    const TileIdx ti = tile_idx(tile, tdn, thn, twn);
+    const int th_i = ti.th, td_i = ti.td, n = ti.n;
+    const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = ti.tw * g.TW;
+    const bool wfull = w0 + g.TW <= g.OW;          // uniform: the tile's columns are all inside OW
     // split-K reduction: the khalf=1 wave of each row block hands its partial
     // sums to its khalf=0 partner through LDS (lane-major, conflict-free)
     if constexpr (KSPLIT) {
@@ -352,8 +370,8 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       const int col = tid % BN, part = tid / BN;
       float sm = 0.f, qq = 0.f;
       for (int row = part; row < rows; row += NPART) {
-        const int td = row / (g.OW * g.TH), th = (row / g.OW) % g.TH;
-        if (d0 + td < g.OD && h0 + th < g.OH) {
+        const int td = row / (g.TW * g.TH), th = (row / g.TW) % g.TH;
+        if (d0 + td < g.OD && h0 + th < g.OH && (wfull || w0 + row % g.TW < g.OW)) {
           const float f = bf2f(Os[row * LDO + col]);
           sm += f;
           qq += f * f;
@@ -375,9 +393,9 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       const int idx = tid + i * H_NTHR;
       const int row = idx / CPR, ch = idx % CPR;
       if (row >= rows) continue;
-      const int w = row % g.OW, th = (row / g.OW) % g.TH, td = row / (g.OW * g.TH);
-      if (d0 + td >= g.OD || h0 + th >= g.OH) continue;
-      const long long m = (((long long)n * g.OD + d0 + td) * g.OH + h0 + th) * g.OW + w;
+      const int w = row % g.TW, th = (row / g.TW) % g.TH, td = row / (g.TW * g.TH);
+      if (d0 + td >= g.OD || h0 + th >= g.OH || w0 + w >= g.OW) continue;
+      const long long m = (((long long)n * g.OD + d0 + td) * g.OH + h0 + th) * g.OW + w0 + w;
       const int col = n0 + ch * 8;
       if (vec_out && col + 8 <= Ncol) {
         *(uint4*)(out + m * Ncol + col) = *(const uint4*)(Os + row * LDO + ch * 8);
@@ -433,13 +451,13 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   constexpr int LDY = BCO + 16;            // conflict-free transposed reads (as igemm wgrad)
   constexpr int YC = BCO / 8;              // 16-B chunks per dy row
   constexpr int HC = WG_HC(MT);
-  const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.OW + g.KW - 1;
+  const int HD = g.TD + g.KD - 1, HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int HP = HD * HH * HW;
   const int nchunk = HP * CPP;
   const int T = g.KD * g.KH * g.KW;
-  const int rows = g.TD * g.TH * g.OW;
-  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH;
-  const int ntiles = g.N * tdn * thn;
+  const int rows = g.TD * g.TH * g.TW;
+  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH, twn = (g.OW + g.TW - 1) / g.TW;
+  const int ntiles = g.N * tdn * thn * twn;
 
   bf16* Ys = reinterpret_cast<bf16*>(dsm);                                   // [256][LDY]
   bf16* halo = reinterpret_cast<bf16*>(dsm + (size_t)H_BM * LDY * 2);        // [HP][CS]
@@ -460,7 +478,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   for (int r = tid; r < H_BM; r += 256) {
     int pos = 0, info = -1;
     if (r < rows) {
-      const int w = r % g.OW, th = (r / g.OW) % g.TH, td = r / (g.OW * g.TH);
+      const int w = r % g.TW, th = (r / g.TW) % g.TH, td = r / (g.TW * g.TH);
       pos = (td * HH + th) * HW + w;
       info = (td << 20) | (th << 10) | w;
     }
@@ -486,20 +504,32 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   // hipcc's wait-count pass drain vmcnt at the top of the k-loop, i.e. it turns the
   // prefetch synchronous
   unsigned ymask = 0, hmask = 0;
-  auto dy_src = [&](int tile, int idx, long long& m) -> bool {
-    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+  // per-tile origins (wave-uniform; decoded once per tile, not per chunk)
+  struct TileOrg { long long ybase, xbase; int d0, h0, w0, dlo, hlo, wlo; };
+  auto tile_org = [&](int tile) -> TileOrg {
+    const TileIdx ti = tile_idx(tile, tdn, thn, twn);
+    TileOrg o;
+    o.d0 = ti.td * g.TD;
+    o.h0 = ti.th * g.TH;
+    o.w0 = ti.tw * g.TW;
+    o.dlo = o.d0 - g.pd;
+    o.hlo = o.h0 - g.ph;
+    o.wlo = o.w0 - g.pw;
+    o.ybase = (long long)ti.n * g.OD * g.OH * g.OW;
+    o.xbase = (long long)ti.n * g.ID * g.IH * g.IW;
+    return o;
+  };
+  auto dy_src = [&](const TileOrg& o, int idx, long long& m) -> bool {
     const int r = idx / YC, c = idx % YC;
     const int info = rowinfo[r];
-    const int td = info >> 20, th = (info >> 10) & 1023, w = info & 1023;
-    m = ((((long long)n * g.OD + td_i * g.TD + td) * g.OH + th_i * g.TH + th) * g.OW + w) * Cout + c * 8;
-    return info >= 0 && td_i * g.TD + td < g.OD && th_i * g.TH + th < g.OH && c * 8 < Cout;
+    const int td = o.d0 + (info >> 20), th = o.h0 + ((info >> 10) & 1023), w = o.w0 + (info & 1023);
+    m = (o.ybase + ((long long)td * g.OH + th) * g.OW + w) * Cout + c * 8;
+    return info >= 0 && td < g.OD && th < g.OH && w < g.OW && c * 8 < Cout;
   };
-  auto halo_src = [&](int tile, int c, long long& off) -> bool {
-    const int th_i = tile % thn, td_i = (tile / thn) % tdn, n = tile / (thn * tdn);
+  auto halo_src = [&](const TileOrg& o, int c, long long& off) -> bool {
     const int info = posinfo[c < nchunk ? c / CPP : 0];
-    const int gd = td_i * g.TD - g.pd + (info >> 20), gh = th_i * g.TH - g.ph + ((info >> 10) & 1023);
-    const int gw = (info & 1023) - g.pw;
-    off = ((((long long)n * g.ID + gd) * g.IH + gh) * g.IW + gw) * g.C + slice * CS + (c % CPP) * 8;
+    const int gd = o.dlo + (info >> 20), gh = o.hlo + ((info >> 10) & 1023), gw = o.wlo + (info & 1023);
+    off = (o.xbase + ((long long)gd * g.IH + gh) * g.IW + gw) * g.C + slice * CS + (c % CPP) * 8;
     return c < nchunk && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
            (unsigned)gw < (unsigned)g.IW;
   };
@@ -508,11 +538,12 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
     return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
   };
   auto prefetch = [&](int tile) {
+    const TileOrg o = tile_org(tile);
     ymask = hmask = 0;
 #pragma unroll
     for (int i = 0; i < YC; ++i) {
       long long m;
-      const bool ok = dy_src(tile, i * 256 + tid, m);
+      const bool ok = dy_src(o, i * 256 + tid, m);
       yreg[i] = *(const uint4*)(dy + (ok ? m : 0));
       ymask |= (unsigned)ok << i;
     }
@@ -520,7 +551,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
     for (int i = 0; i < HC; ++i) {
       long long off;
       // chunks past the halo clamp to the last one: a duplicate, identical LDS write
-      const bool ok = halo_src(tile, min(i * 256 + tid, nchunk - 1), off);
+      const bool ok = halo_src(o, min(i * 256 + tid, nchunk - 1), off);
       hreg[i] = *(const uint4*)(src + (ok ? off : 0));
       hmask |= (unsigned)ok << i;
     }
@@ -536,13 +567,15 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
       const int c = min(i * 256 + tid, nchunk - 1);
       *(uint4*)(halo + (size_t)c * 8) = masked(hreg[i], (hmask >> i) & 1);
     }
+    if (HC * 256 >= nchunk) return;
+    const TileOrg o = tile_org(tile);
     for (int c0 = HC * 256; c0 < nchunk; c0 += 4 * 256) {   // tail of a large halo: synchronous
       uint4 v[4];
       bool okv[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         long long off;
-        okv[j] = halo_src(tile, min(c0 + j * 256 + tid, nchunk - 1), off);
+        okv[j] = halo_src(o, min(c0 + j * 256 + tid, nchunk - 1), off);
         v[j] = *(const uint4*)(src + (okv[j] ? off : 0));
       }
 #pragma unroll
@@ -626,14 +659,14 @@ static HaloGeom parse_halo(const int* v) {
   g.OD = v[5]; g.OH = v[6]; g.OW = v[7];
   g.KD = v[8]; g.KH = v[9]; g.KW = v[10];
   g.pd = v[11]; g.ph = v[12]; g.pw = v[13];
-  g.TD = v[14]; g.TH = v[15];
+  g.TD = v[14]; g.TH = v[15]; g.TW = v[16];
   return g;
 }
 
 static int halo_cs(int C) { return C % 16 == 0 ? 16 : (C % 8 == 0 ? 8 : 0); }
 
 static size_t halo_region_bytes(const HaloGeom& g, int BN, int CS) {
-  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.TW + g.KW - 1);
   size_t epi = (size_t)H_BM * (BN + 8) * 2 + 2 * H_NTHR * 4;
   if (epi < 32 * 1024) epi = 32 * 1024;          // split-K partial sums (one round)
   const size_t r = hp * CS * 2 > epi ? hp * CS * 2 : epi;
@@ -647,7 +680,7 @@ static int halo_nq(const HaloGeom& g, int CS) {
 }
 
 static size_t halo_lds_bytes(const HaloGeom& g, int BN, int CS, bool res) {
-  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.TW + g.KW - 1);
   const size_t T = (size_t)g.KD * g.KH * g.KW;
   const size_t stages = res ? (size_t)halo_nq(g, CS) : 2;
   return halo_region_bytes(g, BN, CS) + stages * BN * H_BKS * 2 + hp * 4 + (T + 15) / 16 * 64 + 16;
@@ -675,16 +708,16 @@ static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const 
 }
 
 static int g_num_cus = 0;
-extern "C" int fn_conv_halo_workers(const int* geom16, int Ncol);
+extern "C" int fn_conv_halo_workers(const int* geom17, int Ncol);
 
 // wt: [Ncol][C/CS][Tp][CS] bf16 (taps padded to a multiple of 128/CS), CS = 16 when
 // C % 16 == 0 else 8; toffs: int [>= Tp] halo position offsets of the taps (0 for
 // padding taps); returns 0 on success.
 extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, void* out, float* stats,
-                            const int* toffs, const int* geom16, int Ncol, int act, hipStream_t st) {
-  const HaloGeom g = parse_halo(geom16);
+                            const int* toffs, const int* geom17, int Ncol, int act, hipStream_t st) {
+  const HaloGeom g = parse_halo(geom17);
   const int CS = halo_cs(g.C);
-  if (CS == 0 || g.TD * g.TH * g.OW > H_BM || g.TD < 1 || g.TH < 1) return -2;
+  if (CS == 0 || g.TD * g.TH * g.TW > H_BM || g.TW < 1 || g.TW > g.OW || g.TD < 1 || g.TH < 1) return -2;
   if (stats && act != ACT_NONE) return -1;
   const int BN = Ncol <= 32 ? 32 : 64;
   const bool res = halo_resident(g, BN, CS);
@@ -692,7 +725,7 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   const int region = (int)halo_region_bytes(g, BN, CS);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + BN - 1) / BN;
-  const int workers = fn_conv_halo_workers(geom16, Ncol);
+  const int workers = fn_conv_halo_workers(geom17, Ncol);
   dim3 grid((unsigned)workers, ncb);
   const bf16* s = (const bf16*)src;
   const bf16* w = (const bf16*)wt;
@@ -725,8 +758,8 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
 }
 
 // number of persistent workgroups (= rows of the BN-statistics slab) fn_conv_halo launches
-extern "C" int fn_conv_halo_workers(const int* geom16, int Ncol) {
-  const HaloGeom g = parse_halo(geom16);
+extern "C" int fn_conv_halo_workers(const int* geom17, int Ncol) {
+  const HaloGeom g = parse_halo(geom17);
   const int CS = halo_cs(g.C);
   if (CS == 0) return -2;
   const int BN = Ncol <= 32 ? 32 : 64;
@@ -737,36 +770,36 @@ extern "C" int fn_conv_halo_workers(const int* geom16, int Ncol) {
         hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cus <= 0)
       g_num_cus = 256;
   }
-  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
+  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) * ((g.OW + g.TW - 1) / g.TW);
   const int ncb = (Ncol + BN - 1) / BN;
   const int per_cu = (int)((160 * 1024) / lds) < 2 ? 1 : 2;
   int workers = (g_num_cus * per_cu + ncb - 1) / ncb;
   return workers > ntiles ? ntiles : workers;
 }
 
-extern "C" long long fn_conv_halo_lds(const int* geom16, int Ncol) {
-  const HaloGeom g = parse_halo(geom16);
+extern "C" long long fn_conv_halo_lds(const int* geom17, int Ncol) {
+  const HaloGeom g = parse_halo(geom17);
   const int BN = Ncol <= 32 ? 32 : 64, CS = halo_cs(g.C) ? halo_cs(g.C) : 16;
   return (long long)halo_lds_bytes(g, BN, CS, halo_resident(g, BN, CS));
 }
 
 static size_t halo_wgrad_lds(const HaloGeom& g, int MT, int CS) {
-  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.OW + g.KW - 1);
+  const size_t hp = (size_t)(g.TD + g.KD - 1) * (g.TH + g.KH - 1) * (g.TW + g.KW - 1);
   return (size_t)H_BM * (MT * 16 + 16) * 2 + hp * CS * 2 + 2 * H_BM * 4 + hp * 4 + 16;
 }
 
 // dw: fp32 [Cout][T][C], zero-initialised by the caller (atomics accumulate).
-extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, const int* geom16, int Cout,
+extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, const int* geom17, int Cout,
                                   int grid_x, hipStream_t st) {
-  const HaloGeom g = parse_halo(geom16);
+  const HaloGeom g = parse_halo(geom17);
   const int CS = halo_cs(g.C);
-  if (CS == 0 || g.TD * g.TH * g.OW > H_BM || Cout > 64 || Cout % 8 != 0) return -2;
+  if (CS == 0 || g.TD * g.TH * g.TW > H_BM || g.TW < 1 || g.TW > g.OW || Cout > 64 || Cout % 8 != 0) return -2;
   const int MT = (Cout + 15) / 16;
   const size_t lds = halo_wgrad_lds(g, MT, CS);
   if (lds > 160 * 1024) return -4;
   const int T = g.KD * g.KH * g.KW;
   const int TPW = MT == 1 ? 16 : 32 / MT;       // taps per wave (either slice width)
-  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH);
+  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) * ((g.OW + g.TW - 1) / g.TW);
   const int gx = grid_x < ntiles ? (grid_x > 0 ? grid_x : 1) : ntiles;
   dim3 grid((unsigned)gx, (unsigned)((T + 4 * TPW - 1) / (4 * TPW)), (unsigned)(g.C / CS));
   const bf16* d = (const bf16*)dy;

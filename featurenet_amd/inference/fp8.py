@@ -65,7 +65,7 @@ class Fp8Conv:
     def __call__(self, xq: torch.Tensor, shape5: tuple) -> tuple[torch.Tensor, tuple]:
         spec = ConvSpec.make(shape5, self.K, self.kernel, 1, self.conv.padding)
         # fp8 halo = 16 B/position; halo_plan counts 32 B/position (bf16): <= 64 KiB of fp8 halo
-        plan = halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, 128 * 1024)
+        plan = halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, 128 * 1024, wsplit=False)
         if plan is None:
             raise RuntimeError(f"no fp8 halo tile for {spec}")
         geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,

@@ -32,6 +32,8 @@ class Conv(nn.Module):
 
     GPU fusion: conv epilogue emits BN statistics, BN+act is applied inside the
     pooling kernel when a pool follows (the normalised tensor never hits HBM).
+    In eval mode BN is folded into the conv weights/bias and BN+act run in the
+    conv epilogue.
     """
 
     def __init__(self, cin: int, cout: int, kernel, stride=1, padding="valid", dilation=1, bn: bool = False,
@@ -77,7 +79,16 @@ class Conv(nn.Module):
         in_shape = x.shape
         x5 = x.reshape(to5d_shape(in_shape))
         cs, ps = self.specs(tuple(x5.shape))
-        if self.bn:
+        if self.bn and not self.training:
+            # inference: BN folded into the conv (w * gamma/sigma, beta - mean * gamma/sigma), so
+            # BN + act run in the conv epilogue -- no statistics, no separate normalise pass
+            scale = self.gamma * torch.rsqrt(self.running_var + self.bn_eps)
+            w = self.weight * scale.view(-1, 1, 1, 1, 1)
+            b = self.beta - self.running_mean * scale
+            out = ops.conv(x5, w, b, cs, self.act)
+            if ps is not None:
+                out = ops.pool(out, ps, self.pool_kind)
+        elif self.bn:
             y, slab = ops.conv(x5, self.weight, None, cs, None, want_stats=True)
             if ps is not None:
                 out = ops.batchnorm_act_pool(y, self.gamma, self.beta, self.running_mean, self.running_var,

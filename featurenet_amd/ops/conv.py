@@ -177,27 +177,45 @@ def _wgrad_halo_budget(cout: int, cs: int = 16) -> int:
     return int((LDS_BUDGET - 256 * (16 * mt + 16) * 2 - 2048 - 64) * 32 / (cs * 2 + 4))
 
 
-def halo_plan(OD: int, OH: int, OW: int, KD: int, KH: int, KW: int, max_bytes: int = 56 * 1024):
-    """Output tile (TD, TH) x full OW maximising MFMA row utilisation with the
-    halo (counted at 32 B = 16 bf16 channels per position) <= max_bytes; None
-    when no tile fits."""
-    key = (OD, OH, OW, KD, KH, KW, max_bytes)
+def _plan_tw(OD, OH, OW, KD, KH, KW, max_bytes, TW):
+    best, best_score = None, -1.0
+    if TW > 256:
+        return best, best_score
+    for TD in range(1, OD + 1):
+        for TH in range(1, OH + 1):
+            rows = TD * TH * TW
+            if rows > 256:
+                break
+            halo = (TD + KD - 1) * (TH + KH - 1) * (TW + KW - 1) * 32
+            if halo > max_bytes:
+                continue
+            tiles = math.ceil(OD / TD) * math.ceil(OH / TH) * math.ceil(OW / TW)
+            score = OD * OH * OW / (tiles * 256.0) - 1e-9 * halo
+            if score > best_score:
+                best, best_score = (TD, TH, TW), score
+    return best, best_score
+
+
+def halo_plan(OD: int, OH: int, OW: int, KD: int, KH: int, KW: int, max_bytes: int = 56 * 1024,
+              wsplit: bool = True):
+    """Output tile (TD, TH, TW) maximising MFMA row utilisation (rows = TD*TH*TW <= 256)
+    with the halo (counted at 32 B = 16 bf16 channels per position) <= max_bytes; None
+    when no tile fits.  Tiles span the full output width (TW = OW) unless that leaves
+    the 256-row MFMA tile under 75 % used (wide outputs: 128^3 inference, where a
+    5^3 halo of full 57-wide rows only fits a 57-row tile), in which case OW is split
+    into equal column tiles."""
+    key = (OD, OH, OW, KD, KH, KW, max_bytes, wsplit)
     if key in _PLAN_CACHE:
         return _PLAN_CACHE[key]
-    best, best_score = None, -1.0
-    if OW <= 256:
-        for TD in range(1, OD + 1):
-            for TH in range(1, OH + 1):
-                rows = TD * TH * OW
-                if rows > 256:
-                    break
-                halo = (TD + KD - 1) * (TH + KH - 1) * (OW + KW - 1) * 32
-                if halo > max_bytes:
-                    continue
-                tiles = math.ceil(OD / TD) * math.ceil(OH / TH)
-                score = OD * OH * OW / (tiles * 256.0) - 1e-9 * halo
-                if score > best_score:
-                    best, best_score = (TD, TH), score
+    best, best_score = _plan_tw(OD, OH, OW, KD, KH, KW, max_bytes, OW)
+    if wsplit and best_score < 0.75:
+        for k in range(2, 9):
+            TW = -(-OW // k)
+            if TW < 8:
+                break
+            cand, score = _plan_tw(OD, OH, OW, KD, KH, KW, max_bytes, TW)
+            if score > best_score + 0.02:          # a split must pay for its extra halo columns
+                best, best_score = cand, score
     _PLAN_CACHE[key] = best
     return best
 
@@ -260,7 +278,8 @@ def halo_tap_offsets(geom: list, device) -> torch.Tensor:
     t = _TOFF_CACHE.get(key)
     if t is None:
         OW, KD, KH, KW, TD, TH = geom[7], geom[8], geom[9], geom[10], geom[14], geom[15]
-        HH, HW = TH + KH - 1, OW + KW - 1
+        TW = geom[16] if len(geom) > 16 else OW
+        HH, HW = TH + KH - 1, TW + KW - 1
         T = KD * KH * KW
         offs = np.zeros((T + 15) // 16 * 16, dtype=np.int32)      # >= Tp for both slice widths
         kd, kh, kw = np.meshgrid(np.arange(KD), np.arange(KH), np.arange(KW), indexing="ij")
@@ -281,9 +300,9 @@ def halo_wgrad_plan(spec: ConvSpec):
 
 def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> torch.Tensor:
     """dW via LDS halo tiles; fp32 [K, KD, KH, KW, C]."""
-    TD, TH = plan
+    TD, TH, TW = plan
     geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
-            spec.pd, spec.ph, spec.pw, TD, TH]
+            spec.pd, spec.ph, spec.pw, TD, TH, TW]
     mt = (spec.K + 15) // 16
     cs = halo_cs(spec.C)
     tpw = 16 if mt == 1 else 32 // mt
@@ -304,9 +323,9 @@ def _halo_call(src5, wmat, bias, out, stats, geom, ncol, act):
 
 
 def halo_conv_fwd(x5, w, bias, spec: ConvSpec, act: int, want_stats: bool, plan):
-    TD, TH = plan
+    TD, TH, TW = plan
     geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
-            spec.pd, spec.ph, spec.pw, TD, TH]
+            spec.pd, spec.ph, spec.pw, TD, TH, TW]
     wmat = halo_pack(w, spec, dgrad=False)
     y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
     stats = None
@@ -319,9 +338,9 @@ def halo_conv_fwd(x5, w, bias, spec: ConvSpec, act: int, want_stats: bool, plan)
 
 def halo_conv_dgrad(dy5, w, spec: ConvSpec, plan):
     """dx = conv(dy, flip(W)^T) with pads K-1-p (stride 1)."""
-    TD, TH = plan
+    TD, TH, TW = plan
     geom = [spec.N, spec.OD, spec.OH, spec.OW, spec.K, spec.D, spec.H, spec.W, spec.KD, spec.KH, spec.KW,
-            spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw, TD, TH]
+            spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw, TD, TH, TW]
     wmat = halo_pack(w, spec, dgrad=True)                                    # [C][K/cs][Tp][cs], taps reversed
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     _halo_call(dy5, wmat, None, dx, None, geom, spec.C, 0)

@@ -293,6 +293,8 @@ HALO_CASES = [
     (2, 22, 22, 22, 64, 64, (3, 3, 3), "valid", 0),
     (3, 7, 9, 12, 16, 48, (3, 3, 3), "same", 1),
     (2, 1, 31, 33, 32, 96, (1, 3, 3), "same", 2),
+    (1, 6, 6, 61, 32, 32, (5, 5, 5), "valid", 0),     # 57-wide output: W-split tiles (TW < OW)
+    (1, 7, 5, 70, 32, 64, (3, 3, 3), "same", 1),       # W split with padding, BN = 64
 ]
 
 
@@ -309,6 +311,8 @@ def test_conv_halo_fwd_dgrad_stats(case):
     x = torch.randn(N, D, H, W, Ci, device="cuda").to(torch.bfloat16)
     spec = C.ConvSpec.make(x.shape, K, k, 1, pad)
     assert C.halo_fwd_plan(spec) is not None and C.halo_dgrad_plan(spec) is not None
+    if W >= 61:
+        assert C.halo_fwd_plan(spec)[2] < spec.OW, C.halo_fwd_plan(spec)     # the case really splits W
     w = (torch.randn(K, spec.KD, spec.KH, spec.KW, Ci, device="cuda") * 0.05).to(torch.bfloat16).float()
     b = torch.randn(K, device="cuda") * 0.1
     acts = {0: None, 1: "relu", 2: "tanh"}

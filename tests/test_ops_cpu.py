@@ -110,3 +110,25 @@ def test_flat_sgd_momentum():
     opt.step()
     # v1 = -0.05 ; p1 = 0.95 ; v2 = 0.9*-0.05 - 0.05 = -0.095 ; p2 = 0.855
     torch.testing.assert_close(p, torch.tensor([0.855]))
+
+
+def test_eval_bn_folding_matches_unfolded_bn():
+    """Eval-mode Conv folds BN into the conv weights/bias; same result as conv -> BN(running) -> act -> pool."""
+    from featurenet_amd.models.layers import Conv
+    from featurenet_amd.ops import reference as R
+
+    torch.manual_seed(0)
+    m = Conv(4, 8, 3, 1, "same", bn=True, act="relu", pool=2)
+    with torch.no_grad():
+        m.gamma.uniform_(0.5, 1.5)
+        m.beta.uniform_(-0.3, 0.3)
+        m.running_mean.uniform_(-0.5, 0.5)
+        m.running_var.uniform_(0.5, 2.0)
+    m.eval()
+    x = torch.randn(2, 6, 6, 6, 4)
+    got = m(x)
+    cs, ps = m.specs(tuple(x.shape))
+    y = R.conv(x, m.weight, None, cs)
+    z = torch.relu((y - m.running_mean) * torch.rsqrt(m.running_var + m.bn_eps) * m.gamma + m.beta)
+    want = R.pool(z, ps, "max")
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-5)
