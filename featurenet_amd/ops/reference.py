@@ -95,4 +95,5 @@ def pool(x5: torch.Tensor, spec: PoolSpec, kind: str = "max", count_pad: bool = 
 
 
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0) -> torch.Tensor:
-    return F.cross_entropy(logits.float(), labels, label_smoothing=smoothing)
+    lg = logits if logits.dtype == torch.float64 else logits.float()   # >= fp32 (fp64 kept for gradcheck)
+    return F.cross_entropy(lg, labels, label_smoothing=smoothing)

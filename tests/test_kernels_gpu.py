@@ -72,6 +72,67 @@ def test_conv_fwd_bwd(case):
     close(bn.grad, br.grad)
 
 
+def _search_space_shapes(n=18, seed=2024):
+    """Random conv shapes from the reference search space (model/input.py:246-306 and the
+    mutation tables, model/mutation/mutable_input.py): 2-D kernels from the 10 mutation
+    shapes, 3-D cubes, stride 1/2, same/valid padding, channel counts 6..130 that are
+    mostly NOT multiples of 16, occasional dilation (the combination projection)."""
+    import random
+
+    rng = random.Random(seed)
+    k2d = [(1, 1), (3, 1), (1, 3), (3, 3), (5, 1), (1, 5), (5, 5), (7, 1), (1, 7), (7, 7)]
+    out = []
+    for i in range(n):
+        three_d = i % 3 == 0
+        cin = rng.choice([1, 3, 6, 8, 12, 16, 24, 30, 32, 48, 64, 96])
+        cout = rng.choice([6, 12, 16, 25, 32, 40, 64, 100, 130])
+        stride = rng.choice([1, 1, 2])
+        pad = rng.choice(["same", "valid"])
+        dil = 2 if (stride == 1 and rng.random() < 0.15) else 1
+        if three_d:
+            k = rng.choice([1, 3, 4, 5])
+            size = rng.choice([9, 12, 16])
+            shape, kern = (2, size, size + 1, size + 2, cin), (k, k, k)
+        else:
+            kh, kw = rng.choice(k2d)
+            size = rng.choice([14, 28, 32])
+            shape, kern = (3, 1, size, size + 3, cin), (1, kh, kw)
+        out.append((shape, cout, kern, stride, pad, dil))
+    return out
+
+
+@pytest.mark.parametrize("case", _search_space_shapes())
+def test_conv_search_space_shapes(case):
+    """NAS shape generality: fwd / dgrad / wgrad / bias-grad through ConvFn vs the fp32 CPU oracle."""
+    _native_loaded()
+    from featurenet_amd.ops.conv import ConvFn
+
+    shape, K, k, s, pad, dil = case
+    torch.manual_seed(sum(shape) * 7 + K)
+    x = torch.randn(*shape).to(torch.bfloat16)
+    try:
+        spec = ConvSpec.make(x.shape, K, k, s, pad, dil)
+    except ValueError:
+        pytest.skip("kernel larger than the input for this draw")
+    if min(spec.OD, spec.OH, spec.OW) < 1:
+        pytest.skip("empty output")
+    w = (torch.randn(K, spec.KD, spec.KH, spec.KW, shape[-1]) * 0.1).to(torch.bfloat16).float()
+    b = torch.randn(K) * 0.1
+    xr, wr, br = x.float().clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = ref.conv(xr, wr, br, spec)
+    xn = x.cuda().requires_grad_(True)
+    wn, bn = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    yn, _ = ConvFn.apply(xn, wn, bn, spec, 0, False)
+    assert yn.shape == yr.shape
+    close(yn, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(g)
+    yn.backward(g.cuda().to(torch.bfloat16))
+    close(xn.grad, xr.grad)
+    close(wn.grad, wr.grad)
+    close(bn.grad, br.grad)
+
+
 def test_conv_stats_epilogue():
     _native_loaded()
     from featurenet_amd.ops.conv import native_conv_fwd, _pack_rows

@@ -132,3 +132,41 @@ def test_eval_bn_folding_matches_unfolded_bn():
     z = torch.relu((y - m.running_mean) * torch.rsqrt(m.running_var + m.bn_eps) * m.gamma + m.beta)
     want = R.pool(z, ps, "max")
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-5)
+
+
+def test_reference_ops_gradcheck_fp64():
+    """torch.autograd.gradcheck (fp64) of the CPU oracle ops that the HIP kernels are tested against:
+    strided / padded / dilated conv with bias + act, depthwise conv, avg + max pool, training-mode BN,
+    label-smoothed softmax cross-entropy."""
+    from torch.autograd import gradcheck
+
+    from featurenet_amd.ops import reference as R
+    from featurenet_amd.ops.spec import ConvSpec, PoolSpec
+
+    torch.manual_seed(0)
+    d = torch.float64
+    x = torch.randn(2, 1, 7, 8, 3, dtype=d, requires_grad=True)
+    for k, s, pad, dil, act in (((1, 3, 3), 1, "same", 1, "tanh"), ((1, 3, 1), 2, "valid", 1, None),
+                                ((1, 3, 3), 1, "same", 2, "sigmoid")):
+        spec = ConvSpec.make(x.shape, 4, k, s, pad, dil)
+        w = torch.randn(4, spec.KD, spec.KH, spec.KW, 3, dtype=d, requires_grad=True)
+        b = torch.randn(4, dtype=d, requires_grad=True)
+        assert gradcheck(lambda x, w, b: R.conv(x, w, b, spec, act), (x, w, b))
+    x3 = torch.randn(1, 4, 5, 6, 2, dtype=d, requires_grad=True)
+    spec3 = ConvSpec.make(x3.shape, 3, (2, 2, 2), 1, "valid")
+    w3 = torch.randn(3, 2, 2, 2, 2, dtype=d, requires_grad=True)
+    assert gradcheck(lambda x, w: R.conv(x, w, None, spec3, "relu"), (x3, w3))
+    dspec = ConvSpec.make(x.shape, 3, (1, 3, 3), 1, "same")
+    wd = torch.randn(3, 1, 3, 3, 1, dtype=d, requires_grad=True)
+    assert gradcheck(lambda x, w: R.depthwise_conv(x, w, None, dspec), (x, wd))
+    ps = PoolSpec.make(x.shape, (1, 2, 2), (1, 2, 2), "same")
+    assert gradcheck(lambda x: R.pool(x, ps, "avg"), (x,))
+    xm = (torch.arange(2 * 7 * 8 * 3, dtype=d).reshape(2, 1, 7, 8, 3) % 17 / 17.0).requires_grad_(True)   # no ties
+    assert gradcheck(lambda x: R.pool(x, ps, "max"), (xm,))
+    g, be = torch.rand(3, dtype=d, requires_grad=True), torch.randn(3, dtype=d, requires_grad=True)
+    rm, rv = torch.zeros(3, dtype=d), torch.ones(3, dtype=d)
+    assert gradcheck(lambda x, g, be: R.batchnorm_act(x, g, be, rm.clone(), rv.clone(), True, 0.1, 1e-5, "tanh"),
+                     (x, g, be))
+    logits = torch.randn(5, 7, dtype=d, requires_grad=True)
+    y = torch.randint(0, 7, (5,))
+    assert gradcheck(lambda l: R.softmax_xent(l, y, 0.1), (logits,))
