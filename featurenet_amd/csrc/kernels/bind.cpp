@@ -22,6 +22,7 @@ int fn_conv_halo(const void*, const void*, const float*, void*, float*, const in
                  hipStream_t);
 long long fn_conv_halo_lds(const int*, int);
 int fn_conv_halo_workers(const int*, int);
+int fn_conv_halo_wgrad_yblocks(const int*, int);
 int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
                     int, int, hipStream_t);
 int fn_quant_fp8(const void*, void*, long long, float, hipStream_t);
@@ -129,6 +130,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("dw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, std::vector<int> geom, int splits, uintptr_t st) {
     need(geom, 20, "dw_wgrad");
     chk(fn_dw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), geom.data(), splits, S(st)), "dw_wgrad");
+  });
+  m.def("conv_halo_wgrad_yblocks", [](std::vector<int> geom, int cout) {
+    need(geom, 17, "conv_halo_wgrad_yblocks");
+    return fn_conv_halo_wgrad_yblocks(geom.data(), cout);
   });
   m.def("conv_halo_workers", [](std::vector<int> geom, int ncol) {
     need(geom, 17, "conv_halo_workers");

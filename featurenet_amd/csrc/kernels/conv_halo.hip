@@ -437,14 +437,16 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
 // block).  CS = 8: the N axis is (tap pair, 8 channels) -- lanes p = 0,1 of a
 // transposed-read quad fetch tap 2j, lanes p = 2,3 tap 2j+1 -- so a wave covers
 // the same taps with half the accumulators.
-template <int MT, int CS>
+// DIV = 2 halves the taps per wave (and the accumulators) for convs with few taps
+// (3^3 = 27: 4 waves x 16 taps would leave half the waves idle).
+template <int MT, int CS, int DIV>
 __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __restrict__ dy,
                                                                  const bf16* __restrict__ src,
                                                                  float* __restrict__ dw, HaloGeom g, int Cout) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   // 16x16 accumulator column blocks per (wave, co block); both slice widths give a
   // wave the same taps (CS = 8 packs two taps per block, so half the blocks)
-  constexpr int NACC = (MT == 1 ? 16 : 32 / MT) / (16 / CS);
+  constexpr int NACC = (MT == 1 ? 16 : 32 / MT) / (16 / CS) / DIV;
   constexpr int TPW = CS == 16 ? NACC : 2 * NACC;   // taps per wave
   constexpr int CPP = CS / 8;
   constexpr int BCO = MT * 16;
@@ -788,6 +790,22 @@ static size_t halo_wgrad_lds(const HaloGeom& g, int MT, int CS) {
   return (size_t)H_BM * (MT * 16 + 16) * 2 + hp * CS * 2 + 2 * H_BM * 4 + hp * 4 + 16;
 }
 
+// taps-per-wave divisor: 2 when halving the taps per wave fills >= 15 % more of the
+// 4-wave tap slots (few-tap kernels, e.g. 3^3 with Cout <= 32)
+static int halo_wgrad_div(int T, int MT) {
+  const int tpw = MT == 1 ? 16 : 32 / MT;
+  auto used = [&](int t) { const int slots = (T + 4 * t - 1) / (4 * t) * 4 * t; return (double)T / slots; };
+  return (tpw % 2 == 0 && used(tpw / 2) >= 1.15 * used(tpw)) ? 2 : 1;
+}
+
+// grid.y of fn_conv_halo_wgrad (tap groups); the caller sizes grid.x from it
+extern "C" int fn_conv_halo_wgrad_yblocks(const int* geom17, int Cout) {
+  const HaloGeom g = parse_halo(geom17);
+  const int MT = (Cout + 15) / 16, T = g.KD * g.KH * g.KW;
+  const int tpw = (MT == 1 ? 16 : 32 / MT) / halo_wgrad_div(T, MT);
+  return (T + 4 * tpw - 1) / (4 * tpw);
+}
+
 // dw: fp32 [Cout][T][C], zero-initialised by the caller (atomics accumulate).
 extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, const int* geom17, int Cout,
                                   int grid_x, hipStream_t st) {
@@ -798,29 +816,32 @@ extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, co
   const size_t lds = halo_wgrad_lds(g, MT, CS);
   if (lds > 160 * 1024) return -4;
   const int T = g.KD * g.KH * g.KW;
-  const int TPW = MT == 1 ? 16 : 32 / MT;       // taps per wave (either slice width)
+  const int DIV = halo_wgrad_div(T, MT);
+  const int TPW = (MT == 1 ? 16 : 32 / MT) / DIV;   // taps per wave (either slice width)
   const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) * ((g.OW + g.TW - 1) / g.TW);
   const int gx = grid_x < ntiles ? (grid_x > 0 ? grid_x : 1) : ntiles;
   dim3 grid((unsigned)gx, (unsigned)((T + 4 * TPW - 1) / (4 * TPW)), (unsigned)(g.C / CS));
   const bf16* d = (const bf16*)dy;
   const bf16* s = (const bf16*)src;
-#define WCASE(M, C)                                                                                        \
+#define WCASE1(M, C, D)                                                                                    \
   do {                                                                                                     \
     static size_t cfg = 0;                                                                                 \
     if (lds > cfg) {                                                                                       \
-      hipError_t e = hipFuncSetAttribute((const void*)conv_halo_wgrad_kernel<M, C>,                        \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_halo_wgrad_kernel<M, C, D>,                     \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);            \
       if (e != hipSuccess) return (int)e;                                                                  \
       cfg = lds;                                                                                           \
     }                                                                                                      \
-    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M, C>), grid, dim3(256), lds, st, d, s, dw, g, Cout);       \
+    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M, C, D>), grid, dim3(256), lds, st, d, s, dw, g, Cout);    \
   } while (0)
+#define WCASE(M, C) do { if (DIV == 2) WCASE1(M, C, 2); else WCASE1(M, C, 1); } while (0)
   if (CS == 16) {
     if (MT == 1) WCASE(1, 16); else if (MT == 2) WCASE(2, 16); else if (MT == 3) WCASE(3, 16); else WCASE(4, 16);
   } else {
     if (MT == 1) WCASE(1, 8); else if (MT == 2) WCASE(2, 8); else if (MT == 3) WCASE(3, 8); else WCASE(4, 8);
   }
 #undef WCASE
+#undef WCASE1
   FN_CHECK_LAUNCH();
   return 0;
 }

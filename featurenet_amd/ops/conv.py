@@ -303,10 +303,8 @@ def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> tor
     TD, TH, TW = plan
     geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
             spec.pd, spec.ph, spec.pw, TD, TH, TW]
-    mt = (spec.K + 15) // 16
     cs = halo_cs(spec.C)
-    tpw = 16 if mt == 1 else 32 // mt
-    per_tile = math.ceil(spec.taps / (4 * tpw)) * (spec.C // cs)
+    per_tile = int(_native.kernels().conv_halo_wgrad_yblocks(geom, spec.K)) * (spec.C // cs)
     dw = torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
     _native.kernels().conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), geom, spec.K,
                                       max(1, target_wgs // per_tile), _native.stream(x5))

@@ -354,6 +354,7 @@ HALO_CASES = [
     (2, 22, 22, 22, 64, 64, (3, 3, 3), "valid", 0),
     (3, 7, 9, 12, 16, 48, (3, 3, 3), "same", 1),
     (2, 1, 31, 33, 32, 96, (1, 3, 3), "same", 2),
+    (2, 10, 11, 12, 32, 32, (3, 3, 3), "same", 0),    # 27 taps, Cout 32: wgrad with half the taps per wave
     (1, 6, 6, 61, 32, 32, (5, 5, 5), "valid", 0),     # 57-wide output: W-split tiles (TW < OW)
     (1, 7, 5, 70, 32, 64, (3, 3, 3), "same", 1),       # W split with padding, BN = 64
 ]

@@ -30,7 +30,7 @@ class _FakeK:
         def f(*args):
             assert len(args) == n, f"{name}: called with {len(args)} args, binding takes {n}"
             self.calls.append(name)
-            if name.endswith(("_lds", "mblocks", "_workers", "_blocks")):
+            if name.endswith(("_lds", "mblocks", "_workers", "_blocks", "_yblocks")):
                 return 1
             return None
         return f
