@@ -22,6 +22,8 @@ int fn_conv_halo(const void*, const void*, const float*, void*, float*, const in
                  hipStream_t);
 long long fn_conv_halo_lds(const int*, int);
 int fn_conv_halo_workers(const int*, int);
+int fn_pw_fwd(const void*, const void*, const float*, void*, long long, int, int, int, hipStream_t);
+int fn_pw_wgrad(const void*, const void*, float*, long long, int, int, hipStream_t);
 int fn_conv_halo_wgrad_yblocks(const int*, int);
 int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
                     int, int, hipStream_t);
@@ -134,6 +136,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_halo_wgrad_yblocks", [](std::vector<int> geom, int cout) {
     need(geom, 17, "conv_halo_wgrad_yblocks");
     return fn_conv_halo_wgrad_yblocks(geom.data(), cout);
+  });
+  m.def("pw_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, long long M, int K, int N, int act,
+                     uintptr_t st) {
+    chk(fn_pw_fwd(P<const void*>(x), P<const void*>(w), P<const float*>(bias), P<void*>(y), M, K, N, act, S(st)),
+        "pw_fwd");
+  });
+  m.def("pw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, long long M, int K, int N, uintptr_t st) {
+    chk(fn_pw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), M, K, N, S(st)), "pw_wgrad");
   });
   m.def("conv_halo_workers", [](std::vector<int> geom, int ncol) {
     need(geom, 17, "conv_halo_workers");

@@ -1,0 +1,303 @@
+// Pointwise (1x1x1, stride 1) convolutions = skinny GEMMs over every voxel:
+//   forward  Y[M][N] = act(X[M][K] @ W^T + b)      (W: [N][K])
+//   dgrad    dX[M][K] = dY[M][N] @ W               (same kernel, W passed as [K][N])
+//   wgrad    dW[N][K] += dY^T @ X                  (reduction over M)
+// with K, N <= 64 (the segmentation classifier is 32 -> 25, SqueezeNet squeeze /
+// expand and the reference's combination projections are 1x1 as well).
+//
+// These are HBM-bound (two tiny matrices per voxel row), so the design goal is
+// streaming: persistent workgroups walk 256-row tiles; a tile of a channels-last
+// tensor is ONE contiguous run of 256*K bf16, loaded with 16-byte vectors
+// regardless of K (25 is fine) and scattered into a padded LDS layout that the
+// MFMA fragments read with aligned ds_read_b128; the next tile's loads are in
+// flight while the current one computes.  Weights live in registers as MFMA B
+// fragments for the whole kernel.  Output goes back through LDS so the global
+// stores are 16-byte vectors too.
+//
+// Reference parity: Keras Conv2D with kernel (1,1) (model/input.py:294) and the
+// combination projection (model/operation.py:179-186).
+#include "common.h"
+
+#define PW_BM 256
+#define PW_NTHR 256
+
+// number of 16-B chunks of a 256-row tile each thread prefetches (K <= 64:
+// 256*64*2 / 16 / 256 = 8)
+#define PW_CH 8
+
+__device__ __forceinline__ int pw_tiles(long long M) { return (int)((M + PW_BM - 1) / PW_BM); }
+
+// Y = act(X W^T + b).  KP / NP: K, N padded to 32 / 64.  Dynamic LDS: the A tile
+// [256][KP+8] and the output staging [256][NP+8] share one region (bf16).
+template <int KP, int NP, int ACT, bool HAS_BIAS>
+__global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                           const float* __restrict__ bias, bf16* __restrict__ y,
+                                                           long long M, int K, int N) {
+  constexpr int LDA = KP + 8, LDO = NP + 8;
+  constexpr int KS = KP / 32, NT = NP / 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char pw_dsm[];
+  bf16* As = reinterpret_cast<bf16*>(pw_dsm);
+  bf16* Os = As;                                 // aliased: staged only after the MFMAs have read As
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  auto zero_pad = [&]() {                       // K padding of the A tile (the scatter never writes it)
+    for (int i = tid; i < PW_BM * (LDA - K); i += PW_NTHR) As[(i / (LDA - K)) * LDA + K + i % (LDA - K)] = f2bf(0.f);
+  };
+  // weights -> B fragments (k rows beyond K and n cols beyond N are zero)
+  bf16x8 fb[KS][NT];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int n = nt * 16 + lr;
+      Pack8 p;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = ks * 32 + lg * 8 + j;
+        p.e[j] = (n < N && k < K) ? w[(long long)n * K + k] : f2bf(0.f);
+      }
+      fb[ks][nt] = __builtin_bit_cast(bf16x8, p.u);
+    }
+  float bv[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int n = nt * 16 + lr;
+    bv[nt] = (HAS_BIAS && n < N) ? bias[n] : 0.f;
+  }
+
+  const int ntiles = pw_tiles(M);
+  uint4 rb[PW_CH];
+  auto load = [&](int t) {                       // tile t: 256*K contiguous bf16 (16-B aligned: 512*K*t)
+    const long long e0 = (long long)t * PW_BM * K;
+    const long long nel = (M - (long long)t * PW_BM < PW_BM ? M - (long long)t * PW_BM : PW_BM) * K;
+#pragma unroll
+    for (int i = 0; i < PW_CH; ++i) {
+      const int c = i * PW_NTHR + tid;
+      // M % 8 == 0 (host check): every tile is a whole number of 16-B chunks
+      rb[i] = *(const uint4*)(x + e0 + (c * 8 < nel ? c * 8 : 0));
+    }
+  };
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gridDim.x) {
+    const int rows = (int)(M - (long long)t * PW_BM < PW_BM ? M - (long long)t * PW_BM : PW_BM);
+    __syncthreads();                             // previous tile's Os readers are done
+    zero_pad();                                  // Os staging overwrote the padding
+#pragma unroll
+    for (int i = 0; i < PW_CH; ++i) {            // scatter flat chunk -> padded rows
+      const int c = i * PW_NTHR + tid;
+      if (c * 8 < rows * K) {
+        int r = (c * 8) / K, k = c * 8 - r * K;   // one division per chunk, then walk
+        if (K % 8 == 0) {                          // chunk inside one row: one 16-B LDS store
+          *(uint4*)(As + r * LDA + k) = rb[i];
+        } else {
+          Pack8 p;
+          p.u = rb[i];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            As[r * LDA + k] = p.e[j];
+            if (++k == K) { k = 0; ++r; }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);   // next tile in flight during the MFMAs
+    f32x4 acc[4][NT];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8 fa = *(const bf16x8*)(As + (wave * 64 + mt * 16 + lr) * LDA + ks * 32 + lg * 8);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[ks][nt], acc[mt][nt], 0, 0, 0);
+      }
+    __syncthreads();                             // all MFMA reads of As done before Os overwrites it
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          Os[(wave * 64 + mt * 16 + lg * 4 + r) * LDO + nt * 16 + lr] = f2bf(act_fwd(acc[mt][nt][r] + bv[nt], ACT));
+    __syncthreads();
+    // gather padded rows -> flat 256*N run, 16-B stores
+    const long long o0 = (long long)t * PW_BM * N;
+    const int nel = rows * N;
+    for (int c = tid; c * 8 < nel; c += PW_NTHR) {
+      Pack8 p;
+      int r = (c * 8) / N, n = c * 8 - r * N;
+      if (N % 8 == 0) {
+        p.u = *(const uint4*)(Os + r * LDO + n);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          p.e[j] = Os[r * LDO + n];
+          if (++n == N) { n = 0; ++r; }
+        }
+      }
+      *(uint4*)(y + o0 + c * 8) = p.u;           // rows * N is a multiple of 8 (M % 8 == 0)
+    }
+  }
+}
+
+// dW[N][K] += sum_rows dY[row][n] * X[row][k].  Both tiles are scattered into LDS
+// TRANSPOSED ([channel][row]) so the MFMA operands (k = rows) are contiguous
+// 8-row runs; per-workgroup fp32 accumulators, one atomic per element at the end.
+template <int KP, int NP>
+__global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                             float* __restrict__ dw, long long M, int K, int N) {
+  constexpr int LDR = PW_BM + 8;                 // row stride of the transposed tiles
+  constexpr int NTN = NP / 16, NTK = KP / 16;
+  extern __shared__ __attribute__((aligned(16))) unsigned char pw_dsm[];
+  bf16* Yt = reinterpret_cast<bf16*>(pw_dsm);    // [NP][LDR]
+  bf16* Xt = Yt + NP * LDR;                      // [KP][LDR]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  // padded channels (n >= N, k >= K) stay zero
+  for (int i = tid; i < NP * LDR; i += PW_NTHR) Yt[i] = f2bf(0.f);
+  for (int i = tid; i < KP * LDR; i += PW_NTHR) Xt[i] = f2bf(0.f);
+
+  // each wave owns a 64-row quarter of the tile's k dimension (2 k-steps of 32 rows)
+  f32x4 acc[NTN][NTK];
+#pragma unroll
+  for (int a = 0; a < NTN; ++a)
+#pragma unroll
+    for (int b = 0; b < NTK; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int ntiles = pw_tiles(M);
+  uint4 ry[PW_CH], rx[PW_CH];
+  auto load = [&](const bf16* src, int C, int t, uint4* rb) {
+    const long long e0 = (long long)t * PW_BM * C;
+    const long long nel = (M - (long long)t * PW_BM < PW_BM ? M - (long long)t * PW_BM : PW_BM) * C;
+#pragma unroll
+    for (int i = 0; i < PW_CH; ++i) {
+      const int c = i * PW_NTHR + tid;
+      rb[i] = *(const uint4*)(src + e0 + (c * 8 < nel ? c * 8 : 0));
+    }
+  };
+  auto scatter_t = [&](bf16* dst, const uint4* rb, int C, int rows) {
+#pragma unroll
+    for (int i = 0; i < PW_CH; ++i) {
+      const int c = i * PW_NTHR + tid;
+      if (c * 8 < rows * C) {
+        Pack8 p;
+        p.u = rb[i];
+        int r = (c * 8) / C, k = c * 8 - r * C;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dst[k * LDR + r] = p.e[j];
+          if (++k == C) { k = 0; ++r; }
+        }
+      }
+    }
+  };
+  int t = blockIdx.x;
+  if (t < ntiles) { load(dy, N, t, ry); load(x, K, t, rx); }
+  for (; t < ntiles; t += gridDim.x) {
+    const int rows = (int)(M - (long long)t * PW_BM < PW_BM ? M - (long long)t * PW_BM : PW_BM);
+    __syncthreads();
+    scatter_t(Yt, ry, N, rows);
+    scatter_t(Xt, rx, K, rows);
+    if (rows < PW_BM) {                          // ragged last tile: zero the unused rows
+      for (int i = tid; i < NP * (PW_BM - rows); i += PW_NTHR) Yt[(i / (PW_BM - rows)) * LDR + rows + i % (PW_BM - rows)] = f2bf(0.f);
+    }
+    __syncthreads();
+    if (t + gridDim.x < ntiles) { load(dy, N, t + gridDim.x, ry); load(x, K, t + gridDim.x, rx); }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int r0 = wave * 64 + kk * 32 + lg * 8;
+      bf16x8 fa[NTN], fb[NTK];
+#pragma unroll
+      for (int a = 0; a < NTN; ++a) fa[a] = *(const bf16x8*)(Yt + (a * 16 + lr) * LDR + r0);
+#pragma unroll
+      for (int b = 0; b < NTK; ++b) fb[b] = *(const bf16x8*)(Xt + (b * 16 + lr) * LDR + r0);
+#pragma unroll
+      for (int a = 0; a < NTN; ++a)
+#pragma unroll
+        for (int b = 0; b < NTK; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    }
+  }
+  // D[row = n][col = k]: lane holds n = a*16 + lg*4 + r, k = b*16 + lr
+#pragma unroll
+  for (int a = 0; a < NTN; ++a)
+#pragma unroll
+    for (int b = 0; b < NTK; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = a * 16 + lg * 4 + r, k = b * 16 + lr;
+        if (n < N && k < K) atomicAdd(dw + (long long)n * K + k, acc[a][b][r]);
+      }
+}
+
+static int g_pw_cus = 0;
+static int pw_grid(long long M) {
+  if (g_pw_cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_pw_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_pw_cus <= 0)
+      g_pw_cus = 256;
+  }
+  const int tiles = (int)((M + PW_BM - 1) / PW_BM);
+  const int g = g_pw_cus * 2;
+  return tiles < g ? (tiles > 0 ? tiles : 1) : g;
+}
+
+// x: bf16 [M][K], w: bf16 [N][K] (row n = output channel), y: bf16 [M][N]; K, N <= 64
+extern "C" int fn_pw_fwd(const void* x, const void* w, const float* bias, void* y, long long M, int K, int N, int act,
+                         hipStream_t st) {
+  if (K < 1 || K > 64 || N < 1 || N > 64 || M < 8 || M % 8) return -2;
+  const dim3 grid((unsigned)pw_grid(M));
+  const bool hb = bias != nullptr;
+#define PWF(KP, NP, A, HB)                                                                                   \
+  do {                                                                                                         \
+    const size_t lds = (size_t)PW_BM * ((KP > NP ? KP : NP) + 8) * 2;                                        \
+    if (lds > 64 * 1024 &&                                                                                     \
+        hipFuncSetAttribute((const void*)pw_fwd_kernel<KP, NP, A, HB>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            (int)lds) != hipSuccess)                                                           \
+      return -4;                                                                                               \
+    hipLaunchKernelGGL((pw_fwd_kernel<KP, NP, A, HB>), grid, dim3(PW_NTHR), lds, st, (const bf16*)x,          \
+                       (const bf16*)w, bias, (bf16*)y, M, K, N);                                               \
+  } while (0)
+#define PWA(KP, NP)                                                          \
+  do {                                                                       \
+    if (act == ACT_RELU) { if (hb) PWF(KP, NP, ACT_RELU, true); else PWF(KP, NP, ACT_RELU, false); } \
+    else if (act == ACT_NONE) { if (hb) PWF(KP, NP, ACT_NONE, true); else PWF(KP, NP, ACT_NONE, false); } \
+    else if (act == ACT_TANH) PWF(KP, NP, ACT_TANH, true);                  \
+    else PWF(KP, NP, ACT_SIGMOID, true);                                     \
+  } while (0)
+  if ((act == ACT_TANH || act == ACT_SIGMOID) && !hb) return -5;
+  if (K <= 32) { if (N <= 32) PWA(32, 32); else PWA(32, 64); }
+  else { if (N <= 32) PWA(64, 32); else PWA(64, 64); }
+#undef PWA
+#undef PWF
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// dw: fp32 [N][K], accumulated into (zero it for a fresh gradient)
+extern "C" int fn_pw_wgrad(const void* dy, const void* x, float* dw, long long M, int K, int N, hipStream_t st) {
+  if (K < 1 || K > 64 || N < 1 || N > 64 || M < 8 || M % 8) return -2;
+  const dim3 grid((unsigned)pw_grid(M));
+#define PWW(KP, NP)                                                                                          \
+  do {                                                                                                     \
+    const size_t lds = (size_t)(KP + NP) * (PW_BM + 8) * 2;                                                \
+    if (lds > 64 * 1024 &&                                                                                 \
+        hipFuncSetAttribute((const void*)pw_wgrad_kernel<KP, NP>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                            (int)lds) != hipSuccess)                                                       \
+      return -4;                                                                                           \
+    hipLaunchKernelGGL((pw_wgrad_kernel<KP, NP>), grid, dim3(PW_NTHR), lds, st, (const bf16*)dy,          \
+                       (const bf16*)x, dw, M, K, N);                                                       \
+  } while (0)
+  if (K <= 32) { if (N <= 32) PWW(32, 32); else PWW(32, 64); }
+  else { if (N <= 32) PWW(64, 32); else PWW(64, 64); }
+#undef PWW
+  FN_CHECK_LAUNCH();
+  return 0;
+}

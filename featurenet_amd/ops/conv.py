@@ -512,6 +512,35 @@ def s2d_weight_grad(dw2: torch.Tensor, f, spec: ConvSpec) -> torch.Tensor:
     return g[:, : spec.KD, : spec.KH, : spec.KW].contiguous()
 
 
+def pointwise_ok(spec: ConvSpec, want_stats: bool = False) -> bool:
+    """1x1x1 stride-1 unpadded conv that the streaming pointwise kernels take (pointwise.hip)."""
+    return (spec.taps == 1 and (spec.sd, spec.sh, spec.sw) == (1, 1, 1) and not want_stats
+            and (spec.pd, spec.ph, spec.pw) == (0, 0, 0) and spec.K <= 64 and spec.C <= 64
+            and spec.M % 8 == 0 and spec.M >= 8)
+
+
+def pw_fwd(x2: torch.Tensor, w2: torch.Tensor, bias, act: int) -> torch.Tensor:
+    """[M, Kin] x [Nout, Kin]^T (+bias, act) -> bf16 [M, Nout] on the pointwise kernel."""
+    M, Kin = x2.shape
+    N = w2.shape[0]
+    if act and bias is None:
+        bias = torch.zeros(N, dtype=torch.float32, device=x2.device)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
+    wb = w2.detach().to(torch.bfloat16).contiguous()
+    _native.kernels().pw_fwd(x2.data_ptr(), wb.data_ptr(), _native.ptr(bias), y.data_ptr(), M, Kin, N, act,
+                             _native.stream(x2))
+    return y
+
+
+def pw_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    """fp32 dW [Nout, Kin] = dy^T x on the pointwise kernel."""
+    M, N = dy2.shape
+    Kin = x2.shape[1]
+    dw = torch.zeros(N, Kin, dtype=torch.float32, device=x2.device)
+    _native.kernels().pw_wgrad(dy2.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, Kin, N, _native.stream(x2))
+    return dw
+
+
 class ConvFn(torch.autograd.Function):
     """y = act(conv(x, w) + b); optional BN statistics slab as a 2nd output."""
 
@@ -520,7 +549,14 @@ class ConvFn(torch.autograd.Function):
         bias = b.detach().float().contiguous() if b is not None else None
         s2d = s2d_plan(spec)
         x_saved = x5
-        if s2d is not None and s2d[1].kdim <= S2D_FWD_RATIO * spec.kdim:
+        ctx.pw = pointwise_ok(spec, want_stats)
+        if ctx.pw:
+            x5 = x5.contiguous()
+            y = pw_fwd(x5.reshape(-1, spec.C), w.reshape(spec.K, spec.C), bias, act).reshape(spec.out_shape5)
+            stats = None
+            s2d = None
+            x_saved = x5
+        elif s2d is not None and s2d[1].kdim <= S2D_FWD_RATIO * spec.kdim:
             # strided few-channel conv: space-to-depth -> stride-1 halo conv; the packed
             # input is what wgrad consumes, so it is saved instead of x
             f, spec2 = s2d
@@ -554,6 +590,12 @@ class ConvFn(torch.autograd.Function):
         dy = dy.contiguous().to(torch.bfloat16)
         if act:
             dy = native_act_bwd(dy, y, act)
+        if ctx.pw:
+            dy2, x2 = dy.reshape(-1, spec.K), x5.reshape(-1, spec.C)
+            dx = pw_fwd(dy2, w.detach().reshape(spec.K, spec.C).t(), None, 0).reshape(x5.shape) if ctx.x_needs else None
+            dw = pw_wgrad(dy2, x2).reshape(w.shape) if ctx.needs_input_grad[1] else None
+            db = native_colsum(dy2) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+            return dx, dw, db, None, None, None
         dx = native_conv_dgrad(dy, w.detach(), spec) if ctx.x_needs else None
         dw = None
         if ctx.needs_input_grad[1]:

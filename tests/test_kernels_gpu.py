@@ -133,6 +133,42 @@ def test_conv_search_space_shapes(case):
     close(bn.grad, br.grad)
 
 
+@pytest.mark.parametrize("case", [
+    ((2, 8, 8, 8, 32), 25, "none", True),       # segmentation classifier class: 32 -> 25 (+bias)
+    ((4, 1, 14, 14, 24), 48, "relu", True),     # K % 8 == 0, N > 32
+    ((2, 1, 8, 9, 6), 40, "none", False),       # 6 input channels: rows straddle 16-B chunks
+    ((1, 4, 4, 4, 64), 64, "tanh", True),       # 64 x 64
+])
+def test_pointwise_conv(case):
+    """1x1x1 convs on the streaming pointwise kernels (pointwise.hip): fwd + bias + act, dgrad, wgrad."""
+    _native_loaded()
+    from featurenet_amd.ops.conv import ConvFn, pointwise_ok
+    from featurenet_amd.ops.spec import act_code
+
+    shape, K, act, has_b = case
+    torch.manual_seed(K)
+    x = torch.randn(*shape).to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, K, 1, 1)
+    assert pointwise_ok(spec)
+    w = (torch.randn(K, 1, 1, 1, shape[-1]) * 0.2).to(torch.bfloat16).float()
+    b = torch.randn(K) * 0.1 if has_b else None
+    a = None if act == "none" else act
+    xr, wr = x.float().clone().requires_grad_(True), w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True) if has_b else None
+    yr = ref.conv(xr, wr, br, spec, a)
+    xn, wn = x.cuda().requires_grad_(True), w.cuda().requires_grad_(True)
+    bn = b.cuda().requires_grad_(True) if has_b else None
+    yn, _ = ConvFn.apply(xn, wn, bn, spec, act_code(a), False)
+    close(yn, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(g)
+    yn.backward(g.cuda().to(torch.bfloat16))
+    close(xn.grad, xr.grad)
+    close(wn.grad, wr.grad)
+    if has_b:
+        close(bn.grad, br.grad)
+
+
 def test_conv_stats_epilogue():
     _native_loaded()
     from featurenet_amd.ops.conv import native_conv_fwd, _pack_rows
