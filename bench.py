@@ -181,7 +181,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if vs is None else round(vs, 3),
-            "dtype": "fp32" if (args.impl == "torch" and args.torch_amp == "off") else "bf16",
+            "dtype": "fp32" if (not use_cuda or (args.impl == "torch" and args.torch_amp == "off")) else "bf16",
             "data": "synthetic (random 64^3 binary voxels, random labels, random-init weights)",
             "config": {
                 "model": model_name,
