@@ -8,10 +8,11 @@
 // 16-channel slice and builds every MFMA A-fragment straight from it:
 //
 //   output tile  TD x TH x TW   (<= 256 rows; TW = OW, or a W split for wide outputs)
-//   LDS halo     (TD+KD-1) x (TH+KH-1) x (OW+KW-1) positions x 16 channels
-//   K loop       pass p over C/16 channel slices, 2 taps per MFMA k-step
-//                (k = [tap][16 ch]), weights streamed through a double-
-//                buffered 64-k LDS stage
+//   LDS halo     (TD+KD-1) x (TH+KH-1) x (TW+KW-1) positions x CS channels
+//   K loop       pass p over C/CS channel slices (CS = 16, or 8 for 8-channel
+//                inputs), 32/CS taps per MFMA k-step (k = [tap][CS ch]),
+//                weights streamed through a double-buffered 128-k LDS stage
+//                (all stages resident for short-K 8-channel convs)
 //
 // so global/L2 traffic drops from ~taps x |x| to ~halo/tile x |x| and the
 // kernel becomes MFMA/LDS-bound.  Used for forward (with fused bias/act or BN
