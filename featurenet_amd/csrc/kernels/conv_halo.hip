@@ -152,7 +152,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   }
   __syncthreads();
 
-  constexpr int HC = H_HC(BN);
+  constexpr int HC = RES ? 3 : H_HC(BN);   // RES (s2d stem): the whole 8-channel halo prefetched in registers
   uint4 hreg[HC > 0 ? HC : 1];
   // halo origin of a job (wave-uniform; decoded once per job, not per chunk)
   auto job_origin = [&](int job, const bf16*& base, int& dlo, int& hlo, int& wlo) {
@@ -333,7 +333,9 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 #pragma unroll
               for (int r = 0; r < 4; ++r) slot[((mt * NT + nt) * 4 + r) * 64 + lane] = acc[mt][nt][r];
         }
-        __syncthreads();
+        // epilogue hand-offs are LDS-only: lds_barrier, not __syncthreads, whose fence
+        // would drain vmcnt and stall on the next job's halo prefetch
+        lds_barrier();
         if (khalf == 0) {
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
@@ -342,7 +344,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 #pragma unroll
               for (int r = 0; r < 4; ++r) acc[mt][nt][r] += slot[((mt * NT + nt) * 4 + r) * 64 + lane];
         }
-        __syncthreads();
+        lds_barrier();
       }
     }
     bf16* Os = reinterpret_cast<bf16*>(dsm);
@@ -367,7 +369,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       // BN partial sums over the valid rows of the staged (bf16-rounded) tile
       constexpr int NPART = H_NTHR / BN;
       float* red = reinterpret_cast<float*>(dsm + (size_t)H_BM * LDO * 2);
-      __syncthreads();
+      lds_barrier();
       const int col = tid % BN, part = tid / BN;
       float sm = 0.f, qq = 0.f;
       for (int row = part; row < rows; row += NPART) {
@@ -380,13 +382,13 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       }
       red[part * 2 * BN + col] = sm;
       red[part * 2 * BN + BN + col] = qq;
-      __syncthreads();
+      lds_barrier();
       if (tid < BN) {
 #pragma unroll
         for (int q2 = 0; q2 < NPART; ++q2) { st_sum += red[q2 * 2 * BN + tid]; st_sq += red[q2 * 2 * BN + BN + tid]; }
       }
     }
-    __syncthreads();
+    lds_barrier();
     constexpr int CPR = BN / 8;
     const bool vec_out = (Ncol % 8) == 0;
 #pragma unroll
