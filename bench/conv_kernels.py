@@ -26,17 +26,23 @@ LAYERS = {  # name: (input spatial, Cin, Cout, kernel, stride)
 }
 
 
-def timeit(fn, reps: int, warmup: int = 3) -> float:
+def timeit(fn, reps: int, warmup: int = 3, inner: int = 5) -> float:
+    """Median over ``reps`` of the mean time of ``inner`` back-to-back calls (ms).
+
+    Back-to-back calls keep the GPU queue full, so host-side launch work of an op
+    overlaps its predecessor's kernels instead of being timed as idle GPU time
+    (rocprofv3 remains the reference for per-kernel numbers)."""
     for _ in range(warmup):
         fn()
     ts = []
     for _ in range(reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        fn()
+        for _ in range(inner):
+            fn()
         b.record()
         b.synchronize()
-        ts.append(a.elapsed_time(b))
+        ts.append(a.elapsed_time(b) / inner)
     ts.sort()
     return ts[len(ts) // 2]
 
