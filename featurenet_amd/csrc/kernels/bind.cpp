@@ -18,7 +18,7 @@ extern "C" {
 int fn_igemm_fwd(const void*, const void*, const float*, void*, float*, const int*, const int*, long long, int, int,
                  int, int, int, hipStream_t);
 int fn_igemm_fwd_mblocks(long long);
-int fn_conv_halo(const void*, const void*, const float*, void*, float*, const int*, const int*, int, int,
+int fn_conv_halo(const void*, const void*, const float*, void*, float*, const int*, const int*, int, int, int*,
                  hipStream_t);
 long long fn_conv_halo_lds(const int*, int);
 int fn_conv_halo_workers(const int*, int);
@@ -89,10 +89,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("igemm_fwd_mblocks", &fn_igemm_fwd_mblocks);
   m.def("conv_halo", [](uintptr_t src, uintptr_t wt, uintptr_t bias, uintptr_t out, uintptr_t stats,
-                        uintptr_t toffs, std::vector<int> geom, int ncol, int act, uintptr_t st) {
+                        uintptr_t toffs, std::vector<int> geom, int ncol, int act, uintptr_t sched, uintptr_t st) {
     need(geom, 17, "conv_halo");
     chk(fn_conv_halo(P<const void*>(src), P<const void*>(wt), P<const float*>(bias), P<void*>(out), P<float*>(stats),
-                     P<const int*>(toffs), geom.data(), ncol, act, S(st)),
+                     P<const int*>(toffs), geom.data(), ncol, act, P<int*>(sched), S(st)),
         "conv_halo");
   });
   m.def("conv_halo_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t dw, std::vector<int> geom, int cout,

@@ -79,7 +79,8 @@ template <int BN, int ACT, bool HAS_BIAS, bool STATS, int CS, bool RES>
 __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __restrict__ src, const bf16* __restrict__ wt,
                                                            const float* __restrict__ bias, bf16* __restrict__ out,
                                                            float* __restrict__ stats, const int* __restrict__ toffs,
-                                                           HaloGeom g, int Ncol, int region_bytes) {
+                                                           HaloGeom g, int Ncol, int region_bytes,
+                                                           int* __restrict__ sched, int chunk) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   // 8 waves = 4 row blocks x 2: BN=32 splits every stage's 4 k-steps between
   // the two waves of a row block (partials reduced per tile); BN=64 gives each
@@ -119,10 +120,6 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   const int khalf = __builtin_amdgcn_readfirstlane(wave >> 2);   // k-half (BN=32) or column half (BN=64)
   const int ccol = KSPLIT ? 0 : khalf * 32;                      // this wave's first column
   const int lr = lane & 15, lg = lane >> 4;
-  const int worker = xcd_remap(blockIdx.x, gridDim.x);
-  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
-  const int t_begin = worker * per;
-  const int t_end = t_begin + per < ntiles ? t_begin + per : ntiles;
   const int n0 = blockIdx.y * BN;
   // BN statistics: one (sum, sumsq) partial per workgroup (not per tile), so the
   // finalize pass reduces gridDim.x rows instead of thousands
@@ -133,11 +130,45 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       stats[(long long)blockIdx.x * 2 * Ncol + Ncol + n0 + tid] = st_sq;
     }
   };
-  if (t_begin >= t_end) {                        // whole workgroup exits together
+  // Dynamic tile schedule: workgroups take chunks of `chunk` consecutive tiles from
+  // a global counter (sched[1 + blockIdx.y]).  A static partition would make the
+  // whole kernel wait for its last workgroups whenever some CU slots are held by a
+  // concurrent kernel (RCCL all-reduce overlapping backward); with chunks the
+  // resident workgroups simply take more of them.  The last workgroup to finish
+  // (sched[0] counts finished ones) resets the counters for the next launch.
+  // chunk < 0: static partition instead (one contiguous run of -chunk tiles per
+  // workgroup, XCD-aware order) -- kept for A/B measurements
+  const bool dyn = chunk > 0;
+  const int run = dyn ? chunk : -chunk;
+  int nstatic = 0;
+  __shared__ int s_grab;
+  auto grab = [&]() -> int {                     // first tile of a fresh chunk, or -1
+    if (!dyn) {
+      const int t0 = nstatic++ == 0 ? xcd_remap(blockIdx.x, gridDim.x) * run : ntiles;
+      return t0 < ntiles ? t0 : -1;
+    }
+    if (tid == 0) s_grab = atomicAdd(sched + 1 + blockIdx.y, 1) * chunk;
+    lds_barrier();
+    const int t0 = __builtin_amdgcn_readfirstlane(s_grab);
+    lds_barrier();                               // everyone has read s_grab before it can change
+    return t0 < ntiles ? t0 : -1;
+  };
+  auto finish = [&]() {
     write_stats();
+    if (tid == 0) {
+      __threadfence();
+      if (atomicAdd(sched, 1) == (int)(gridDim.x * gridDim.y) - 1) {
+        for (int i = 0; i < (int)gridDim.y; ++i) atomicExch(sched + 1 + i, 0);
+        atomicExch(sched, 0);
+      }
+    }
+  };
+  int tile = grab();
+  if (tile < 0) {                                // whole workgroup exits together
+    finish();
     return;
   }
-  const int njobs = (t_end - t_begin) * npass;
+  int cend = min(tile + run, ntiles);
 
   for (int pos = tid; pos < HP; pos += H_NTHR)
     posinfo[pos] = ((pos / (HW * HH)) << 20) | (((pos / HW) % HH) << 10) | (pos % HW);
@@ -154,19 +185,18 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 
   constexpr int HC = RES ? 3 : H_HC(BN);   // RES (s2d stem): the whole 8-channel halo prefetched in registers
   uint4 hreg[HC > 0 ? HC : 1];
-  // halo origin of a job (wave-uniform; decoded once per job, not per chunk)
-  auto job_origin = [&](int job, const bf16*& base, int& dlo, int& hlo, int& wlo) {
-    const int tile = t_begin + job / npass, p = job % npass;
-    const TileIdx ti = tile_idx(tile, tdn, thn, twn);
+  // halo origin of a job = (tile, channel pass p) (wave-uniform; decoded once per job)
+  auto job_origin = [&](int jt, int p, const bf16*& base, int& dlo, int& hlo, int& wlo) {
+    const TileIdx ti = tile_idx(jt, tdn, thn, twn);
     dlo = ti.td * g.TD - g.pd;
     hlo = ti.th * g.TH - g.ph;
     wlo = ti.tw * g.TW - g.pw;
     base = src + (long long)ti.n * g.ID * g.IH * g.IW * g.C + p * CS;
   };
-  auto prefetch_halo = [&](int job) {
+  auto prefetch_halo = [&](int jt, int p) {
     const bf16* base;
     int dlo, hlo, wlo;
-    job_origin(job, base, dlo, hlo, wlo);
+    job_origin(jt, p, base, dlo, hlo, wlo);
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
       // chunks past the halo are clamped to the last one (a duplicate, identical
@@ -181,7 +211,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       hreg[i] = ok ? x : make_uint4(0, 0, 0, 0);
     }
   };
-  auto store_halo = [&](int job) {
+  auto store_halo = [&](int jt, int p) {
 #pragma unroll
     for (int i = 0; i < HC; ++i) {
       const int c = min(i * H_NTHR + tid, nchunk - 1);
@@ -190,7 +220,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
     if (HC * H_NTHR >= nchunk) return;
     const bf16* base;
     int dlo, hlo, wlo;
-    job_origin(job, base, dlo, hlo, wlo);
+    job_origin(jt, p, base, dlo, hlo, wlo);
     for (int c0 = HC * H_NTHR; c0 < nchunk; c0 += 4 * H_NTHR) {   // tail of a large halo: synchronous
       uint4 v[4];
 #pragma unroll
@@ -255,7 +285,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  prefetch_halo(0);
+  prefetch_halo(tile, 0);
   if constexpr (RES) {
     for (int q = 0; q < nq; ++q) {        // all stages, once (the job loop's first barrier publishes them)
       load_b(q, rbA);
@@ -268,17 +298,28 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   }
 
   int s = 0;                              // global stage counter
-  for (int job = 0; job < njobs; ++job) {
+  int pass = 0;
+  while (true) {
     lds_barrier();                      // previous halo / epilogue staging fully consumed
-    store_halo(job);
+    store_halo(tile, pass);
     lds_barrier();
-    if (job + 1 < njobs) prefetch_halo(job + 1);   // lands during this job's MFMAs
+    // the next job (same tile / next pass, next tile of the chunk, or a new chunk)
+    int ntile = tile, npass_i = pass + 1, ncend = cend;
+    if (npass_i == npass) {
+      npass_i = 0;
+      ntile = tile + 1;
+      if (ntile == cend) {
+        ntile = grab();
+        ncend = ntile < 0 ? -1 : min(ntile + run, ntiles);
+      }
+    }
+    if (ntile >= 0) prefetch_halo(ntile, npass_i);   // lands during this job's MFMAs
     for (int local = 0; local < spp; ++local, ++s) {
       if constexpr (EARLY_B && !RES) {
         load_b(s + 1, rbA);
         __builtin_amdgcn_sched_barrier(0);  // keep the loads here (the scheduler would sink them to their use)
       }
-      const bf16* b = Bs + (RES ? (job % npass) * spp + local : (s & 1)) * B_STAGE;
+      const bf16* b = Bs + (RES ? pass * spp + local : (s & 1)) * B_STAGE;
       // lane group lg reads tap lg>>1 / channel half lg&1 (CS = 16) or tap lg (CS = 8)
       const int* tp = toffs_s + local * TPS + (KSPLIT ? khalf * (TPS / 2) : 0) + (CS == 16 ? (lg >> 1) : lg);
 #pragma unroll
@@ -311,10 +352,12 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
       }
     }
     if constexpr (RES) lds_barrier();     // all waves are done with the halo before it is reused
-    if (job % npass != npass - 1) continue;
+    if (pass != npass - 1) {
+      pass = npass_i;                   // same tile, next channel pass
+      continue;
+    }
 
     // ---- epilogue of a finished tile (staging in the halo region) ----
-    const int tile = t_begin + job / npass;
     const TileIdx ti = tile_idx(tile, tdn, thn, twn);
     const int th_i = ti.th, td_i = ti.td, n = ti.n;
     const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = ti.tw * g.TW;
@@ -407,8 +450,12 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
           if (col + j < Ncol) out[m * Ncol + col + j] = Os[row * LDO + ch * 8 + j];
       }
     }
+    tile = ntile;
+    pass = npass_i;
+    cend = ncend;
+    if (tile < 0) break;
   }
-  write_stats();
+  finish();
 }
 
 // ---------------------------------------------------------------------------
@@ -699,7 +746,8 @@ static bool halo_resident(const HaloGeom& g, int BN, int CS) {
 
 template <int BN, int ACT, bool HB, bool ST, int CS, bool RES>
 static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const bf16* s, const bf16* w,
-                       const float* b, bf16* o, float* stats, const int* toffs, const HaloGeom& g, int Ncol) {
+                       const float* b, bf16* o, float* stats, const int* toffs, const HaloGeom& g, int Ncol,
+                       int* sched, int chunk) {
   static size_t configured = 0;
   if (lds > configured) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_halo_kernel<BN, ACT, HB, ST, CS, RES>,
@@ -708,18 +756,24 @@ static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const 
     configured = lds;
   }
   hipLaunchKernelGGL((conv_halo_kernel<BN, ACT, HB, ST, CS, RES>), grid, dim3(H_NTHR), lds, st, s, w, b, o, stats, toffs,
-                     g, Ncol, region);
+                     g, Ncol, region, sched, chunk);
   return 0;
 }
 
 static int g_num_cus = 0;
+static const bool g_halo_static = [] {
+  const char* e = getenv("FN_HALO_STATIC");
+  return e && e[0] == '1';
+}();
 extern "C" int fn_conv_halo_workers(const int* geom17, int Ncol);
 
 // wt: [Ncol][C/CS][Tp][CS] bf16 (taps padded to a multiple of 128/CS), CS = 16 when
 // C % 16 == 0 else 8; toffs: int [>= Tp] halo position offsets of the taps (0 for
 // padding taps); returns 0 on success.
+// sched: int[1 + column blocks] tile-schedule counters, zero before the first launch
+// (every launch leaves them zero again); at most one launch in flight per buffer.
 extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, void* out, float* stats,
-                            const int* toffs, const int* geom17, int Ncol, int act, hipStream_t st) {
+                            const int* toffs, const int* geom17, int Ncol, int act, int* sched, hipStream_t st) {
   const HaloGeom g = parse_halo(geom17);
   const int CS = halo_cs(g.C);
   if (CS == 0 || g.TD * g.TH * g.TW > H_BM || g.TW < 1 || g.TW > g.OW || g.TD < 1 || g.TH < 1) return -2;
@@ -731,6 +785,12 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + BN - 1) / BN;
   const int workers = fn_conv_halo_workers(geom17, Ncol);
+  if (!sched || ncb > 63) return -6;
+  const int ntiles_all = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) * ((g.OW + g.TW - 1) / g.TW);
+  // ~4 chunks per workgroup: enough slack to absorb late or missing workgroups,
+  // few enough that consecutive tiles (shared halo rows) stay on one workgroup
+  int chunk = ntiles_all / (4 * workers) > 1 ? ntiles_all / (4 * workers) : 1;
+  if (g_halo_static) chunk = -((ntiles_all + workers - 1) / workers);
   dim3 grid((unsigned)workers, ncb);
   const bf16* s = (const bf16*)src;
   const bf16* w = (const bf16*)wt;
@@ -739,8 +799,9 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   int rc;
 #define HCASE(B, A, H, S, C)                                                                     \
   rc = (B == 32 && C == 8 && res)                                                                \
-           ? launch_halo<B, A, H, S, C, (B == 32 && C == 8)>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol) \
-           : launch_halo<B, A, H, S, C, false>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol)
+           ? launch_halo<B, A, H, S, C, (B == 32 && C == 8)>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol, \
+                                                               sched, chunk)                                    \
+           : launch_halo<B, A, H, S, C, false>(grid, lds, region, st, s, w, bias, o, stats, toffs, g, Ncol, sched, chunk)
 #define HBN(B, C)                                                   \
   do {                                                              \
     if (stats) HCASE(B, ACT_NONE, false, true, C);                  \

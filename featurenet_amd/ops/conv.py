@@ -311,13 +311,29 @@ def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> tor
     return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
 
 
+_SCHED: dict = {}
+
+
+def halo_sched(device, stream: int) -> torch.Tensor:
+    """int32[64] tile-schedule counters of the halo kernel (one buffer per device and stream:
+    kernels on one stream run in order, and every launch leaves the counters zero)."""
+    key = (str(device), stream)
+    t = _SCHED.get(key)
+    if t is None:
+        t = torch.zeros(64, dtype=torch.int32, device=device)
+        with _TAB_LOCK:
+            _SCHED[key] = t
+    return t
+
+
 def _halo_call(src5, wmat, bias, out, stats, geom, ncol, act):
     K = _native.kernels()
     if act and bias is None:
         bias = torch.zeros(ncol, dtype=torch.float32, device=src5.device)
     toffs = halo_tap_offsets(geom, src5.device)
+    st = _native.stream(src5)
     K.conv_halo(src5.data_ptr(), wmat.data_ptr(), _native.ptr(bias), out.data_ptr(), _native.ptr(stats),
-                toffs.data_ptr(), geom, ncol, act, _native.stream(src5))
+                toffs.data_ptr(), geom, ncol, act, halo_sched(src5.device, st).data_ptr(), st)
 
 
 def halo_conv_fwd(x5, w, bias, spec: ConvSpec, act: int, want_stats: bool, plan):
