@@ -31,7 +31,7 @@ int fn_quant_fp8(const void*, void*, long long, float, hipStream_t);
 int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, hipStream_t);
 int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
-int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, hipStream_t);
+int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, int*, hipStream_t);
 int fn_s2d_pack(const void*, void*, const int*, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
@@ -96,9 +96,10 @@ PYBIND11_MODULE(_C, m) {
         "conv_halo");
   });
   m.def("conv_halo_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t dw, std::vector<int> geom, int cout,
-                              int grid_x, uintptr_t st) {
+                              int grid_x, uintptr_t sched, uintptr_t st) {
     need(geom, 17, "conv_halo_wgrad");
-    chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x, S(st)),
+    chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x,
+                           P<int*>(sched), S(st)),
         "conv_halo_wgrad");
   });
   m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {

@@ -492,7 +492,8 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
 template <int MT, int CS, int DIV>
 __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __restrict__ dy,
                                                                  const bf16* __restrict__ src,
-                                                                 float* __restrict__ dw, HaloGeom g, int Cout) {
+                                                                 float* __restrict__ dw, HaloGeom g, int Cout,
+                                                                 int* __restrict__ sched, int nstatic_tiles) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   // 16x16 accumulator column blocks per (wave, co block); both slice widths give a
   // wave the same taps (CS = 8 packs two taps per block, so half the blocks)
@@ -522,10 +523,28 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   const int G = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
   const int slice = blockIdx.z;
   const int tap0 = (blockIdx.y * 4 + wave) * TPW;          // uniform: tap offsets stay in SGPRs
-  // contiguous run of tiles per workgroup (neighbouring tiles share halo rows in L2)
-  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
-  const int t_begin = blockIdx.x * per;
-  const int t_end = t_begin + per < ntiles ? t_begin + per : ntiles;
+  // Hybrid schedule.  The first nstatic_tiles tiles are split statically: one
+  // contiguous run per workgroup x, so the grid.y/grid.z workgroups (tap groups,
+  // slices) of a tile walk it in near lockstep and share its dy / halo in L2.  The
+  // remaining tail is taken in single tiles from a per-(y, z) counter, so workgroups
+  // that start late (CU slots held by a concurrent RCCL kernel) do not stretch the
+  // kernel by a whole run.  The last workgroup out resets the counters.
+  const int per = nstatic_tiles / (int)gridDim.x;
+  int* cnt = sched + 1 + blockIdx.z * gridDim.y + blockIdx.y;
+  int ngrab = 0;
+  __shared__ int s_grab;
+  auto grab = [&](int& end) -> int {
+    if (ngrab++ == 0 && per > 0) {
+      end = (int)(blockIdx.x + 1) * per;
+      return (int)blockIdx.x * per;
+    }
+    if (tid == 0) s_grab = per * (int)gridDim.x + atomicAdd(cnt, 1);
+    lds_barrier();
+    const int t0 = __builtin_amdgcn_readfirstlane(s_grab);
+    lds_barrier();
+    end = t0 + 1;
+    return t0 < ntiles ? t0 : -1;
+  };
 
   for (int r = tid; r < H_BM; r += 256) {
     int pos = 0, info = -1;
@@ -644,12 +663,16 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
 #pragma unroll
     for (int j = 0; j < MT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (t_begin < t_end) prefetch(t_begin);
-  for (int tile = t_begin; tile < t_end; ++tile) {
+  int cend = 0;
+  int tile = grab(cend);
+  if (tile >= 0) prefetch(tile);
+  while (tile >= 0) {
     lds_barrier();                 // previous tile's reads are done
     store(tile);
     lds_barrier();
-    if (tile + 1 < t_end) prefetch(tile + 1);   // lands during this tile's MFMAs
+    int ntile = tile + 1, ncend = cend;
+    if (ntile == cend) ntile = grab(ncend);
+    if (ntile >= 0) prefetch(ntile);   // lands during this tile's MFMAs
     const int kst = ntap > 0 ? (rows + 31) >> 5 : 0;   // waves past the last tap only stage
     for (int ks = 0; ks < kst; ++ks) {
       bf16x8 fa[MT];
@@ -681,6 +704,16 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
         for (int mt = 0; mt < MT; ++mt)
           acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb, acc[i][mt], 0, 0, 0);
       }
+    }
+    tile = ntile;
+    cend = ncend;
+  }
+  if (tid == 0) {                  // the last workgroup out resets the tail counters
+    __threadfence();
+    const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
+    if (atomicAdd(sched, 1) == total - 1) {
+      for (int i = 0; i < (int)(gridDim.y * gridDim.z); ++i) atomicExch(sched + 1 + i, 0);
+      atomicExch(sched, 0);
     }
   }
   // D[row=co][col=n]: lane holds co = mt*16 + (lane>>4)*4 + r, n = lane & 15
@@ -871,8 +904,9 @@ extern "C" int fn_conv_halo_wgrad_yblocks(const int* geom17, int Cout) {
 }
 
 // dw: fp32 [Cout][T][C], zero-initialised by the caller (atomics accumulate).
+// sched: int[1 + grid.y * grid.z] zeroed counters (left zero again, see fn_conv_halo)
 extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, const int* geom17, int Cout,
-                                  int grid_x, hipStream_t st) {
+                                  int grid_x, int* sched, hipStream_t st) {
   const HaloGeom g = parse_halo(geom17);
   const int CS = halo_cs(g.C);
   if (CS == 0 || g.TD * g.TH * g.TW > H_BM || g.TW < 1 || g.TW > g.OW || Cout > 64 || Cout % 8 != 0) return -2;
@@ -885,6 +919,9 @@ extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, co
   const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) * ((g.OW + g.TW - 1) / g.TW);
   const int gx = grid_x < ntiles ? (grid_x > 0 ? grid_x : 1) : ntiles;
   dim3 grid((unsigned)gx, (unsigned)((T + 4 * TPW - 1) / (4 * TPW)), (unsigned)(g.C / CS));
+  if (!sched || grid.y * grid.z > 63) return -6;
+  // 7/8 of the tiles in static runs (whole runs per workgroup), the rest as a dynamic tail
+  const int nstatic = g_halo_static ? ntiles : ntiles / gx * 7 / 8 * gx;
   const bf16* d = (const bf16*)dy;
   const bf16* s = (const bf16*)src;
 #define WCASE1(M, C, D)                                                                                    \
@@ -896,7 +933,8 @@ extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, co
       if (e != hipSuccess) return (int)e;                                                                  \
       cfg = lds;                                                                                           \
     }                                                                                                      \
-    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M, C, D>), grid, dim3(256), lds, st, d, s, dw, g, Cout);    \
+    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M, C, D>), grid, dim3(256), lds, st, d, s, dw, g, Cout, sched, \
+                       nstatic);                                                                           \
   } while (0)
 #define WCASE(M, C) do { if (DIV == 2) WCASE1(M, C, 2); else WCASE1(M, C, 1); } while (0)
   if (CS == 16) {

@@ -298,19 +298,6 @@ def halo_wgrad_plan(spec: ConvSpec):
     return halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, _wgrad_halo_budget(spec.K, halo_cs(spec.C)))
 
 
-def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> torch.Tensor:
-    """dW via LDS halo tiles; fp32 [K, KD, KH, KW, C]."""
-    TD, TH, TW = plan
-    geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
-            spec.pd, spec.ph, spec.pw, TD, TH, TW]
-    cs = halo_cs(spec.C)
-    per_tile = int(_native.kernels().conv_halo_wgrad_yblocks(geom, spec.K)) * (spec.C // cs)
-    dw = torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
-    _native.kernels().conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), geom, spec.K,
-                                      max(1, target_wgs // per_tile), _native.stream(x5))
-    return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
-
-
 _SCHED: dict = {}
 
 
@@ -324,6 +311,20 @@ def halo_sched(device, stream: int) -> torch.Tensor:
         with _TAB_LOCK:
             _SCHED[key] = t
     return t
+
+
+def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> torch.Tensor:
+    """dW via LDS halo tiles; fp32 [K, KD, KH, KW, C]."""
+    TD, TH, TW = plan
+    geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
+            spec.pd, spec.ph, spec.pw, TD, TH, TW]
+    cs = halo_cs(spec.C)
+    per_tile = int(_native.kernels().conv_halo_wgrad_yblocks(geom, spec.K)) * (spec.C // cs)
+    dw = torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
+    st = _native.stream(x5)
+    _native.kernels().conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), geom, spec.K,
+                                      max(1, target_wgs // per_tile), halo_sched(x5.device, st).data_ptr(), st)
+    return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
 
 
 def _halo_call(src5, wmat, bias, out, stats, geom, ncol, act):
