@@ -435,6 +435,31 @@ def test_conv_halo_fwd_dgrad_stats(case):
         close(dw, wr.grad)
 
 
+def test_halo_schedule_counters_reset_and_repeatable():
+    """The dynamic tile schedule leaves its counters zero after every launch (the last
+    workgroup out resets them), so back-to-back launches and graph replays start clean;
+    the result does not depend on which workgroup took which tile."""
+    _native_loaded()
+    import importlib
+
+    C = importlib.import_module("featurenet_amd.ops.conv")
+    torch.manual_seed(12)
+    x = torch.randn(2, 20, 21, 22, 32, device="cuda").to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, 64, (3, 3, 3), 1, "same")
+    w = (torch.randn(64, 3, 3, 3, 32, device="cuda") * 0.05).to(torch.bfloat16).float()
+    st = torch.cuda.current_stream().cuda_stream
+    outs, dws = [], []
+    for _ in range(3):
+        y, stats = C.halo_conv_fwd(x, w, None, spec, 0, True, C.halo_fwd_plan(spec))
+        dw = C.halo_conv_wgrad(y.contiguous(), x, spec, C.halo_wgrad_plan(spec))
+        torch.cuda.synchronize()
+        assert int(C.halo_sched(x.device, st).abs().sum()) == 0
+        outs.append(y)
+        dws.append(dw)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    torch.testing.assert_close(dws[0], dws[2], rtol=1e-5, atol=1e-4)   # fp32 atomics: order may differ
+
+
 @pytest.mark.parametrize("case", [
     (2, 9, 10, 11, 8, 32, (3, 3, 3), "same"),       # 8-channel halo slices (CS = 8), partial taps
     (2, 12, 12, 12, 8, 64, (4, 4, 4), "valid"),     # s2d-stem shape class, BN = 64
