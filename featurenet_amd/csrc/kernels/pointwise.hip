@@ -21,9 +21,6 @@
 #define PW_BM 256
 #define PW_NTHR 256
 
-// number of 16-B chunks of a 256-row tile each thread prefetches (K <= 64:
-// 256*64*2 / 16 / 256 = 8)
-#define PW_CH 8
 
 __device__ __forceinline__ int pw_tiles(long long M) { return (int)((M + PW_BM - 1) / PW_BM); }
 
@@ -35,6 +32,7 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
                                                            long long M, int K, int N) {
   constexpr int LDA = KP + 8, LDO = NP + 8;
   constexpr int KS = KP / 32, NT = NP / 16;
+  constexpr int CH = KP / 8;                     // 16-B chunks per thread of a 256 x KP tile
   extern __shared__ __attribute__((aligned(16))) unsigned char pw_dsm[];
   bf16* As = reinterpret_cast<bf16*>(pw_dsm);
   bf16* Os = As;                                 // aliased: staged only after the MFMAs have read As
@@ -67,12 +65,12 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
   }
 
   const int ntiles = pw_tiles(M);
-  uint4 rb[PW_CH];
+  uint4 rb[CH];
   auto load = [&](int t) {                       // tile t: 256*K contiguous bf16 (16-B aligned: 512*K*t)
     const long long e0 = (long long)t * PW_BM * K;
     const long long nel = (M - (long long)t * PW_BM < PW_BM ? M - (long long)t * PW_BM : PW_BM) * K;
 #pragma unroll
-    for (int i = 0; i < PW_CH; ++i) {
+    for (int i = 0; i < CH; ++i) {
       const int c = i * PW_NTHR + tid;
       // M % 8 == 0 (host check): every tile is a whole number of 16-B chunks
       rb[i] = *(const uint4*)(x + e0 + (c * 8 < nel ? c * 8 : 0));
@@ -85,7 +83,7 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
     __syncthreads();                             // previous tile's Os readers are done
     zero_pad();                                  // Os staging overwrote the padding
 #pragma unroll
-    for (int i = 0; i < PW_CH; ++i) {            // scatter flat chunk -> padded rows
+    for (int i = 0; i < CH; ++i) {            // scatter flat chunk -> padded rows
       const int c = i * PW_NTHR + tid;
       if (c * 8 < rows * K) {
         int r = (c * 8) / K, k = c * 8 - r * K;   // one division per chunk, then walk
@@ -172,19 +170,20 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __rest
     for (int b = 0; b < NTK; ++b) acc[a][b] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int ntiles = pw_tiles(M);
-  uint4 ry[PW_CH], rx[PW_CH];
-  auto load = [&](const bf16* src, int C, int t, uint4* rb) {
+  constexpr int CY = NP / 8, CX = KP / 8;        // 16-B chunks per thread of the dy / x tiles
+  uint4 ry[CY], rx[CX];
+  auto load = [&](const bf16* src, int C, int t, uint4* rb, int nch) {
     const long long e0 = (long long)t * PW_BM * C;
     const long long nel = (M - (long long)t * PW_BM < PW_BM ? M - (long long)t * PW_BM : PW_BM) * C;
 #pragma unroll
-    for (int i = 0; i < PW_CH; ++i) {
+    for (int i = 0; i < nch; ++i) {
       const int c = i * PW_NTHR + tid;
       rb[i] = *(const uint4*)(src + e0 + (c * 8 < nel ? c * 8 : 0));
     }
   };
-  auto scatter_t = [&](bf16* dst, const uint4* rb, int C, int rows) {
+  auto scatter_t = [&](bf16* dst, const uint4* rb, int C, int rows, int nch) {
 #pragma unroll
-    for (int i = 0; i < PW_CH; ++i) {
+    for (int i = 0; i < nch; ++i) {
       const int c = i * PW_NTHR + tid;
       if (c * 8 < rows * C) {
         Pack8 p;
@@ -199,17 +198,17 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __rest
     }
   };
   int t = blockIdx.x;
-  if (t < ntiles) { load(dy, N, t, ry); load(x, K, t, rx); }
+  if (t < ntiles) { load(dy, N, t, ry, CY); load(x, K, t, rx, CX); }
   for (; t < ntiles; t += gridDim.x) {
     const int rows = (int)(M - (long long)t * PW_BM < PW_BM ? M - (long long)t * PW_BM : PW_BM);
     __syncthreads();
-    scatter_t(Yt, ry, N, rows);
-    scatter_t(Xt, rx, K, rows);
+    scatter_t(Yt, ry, N, rows, CY);
+    scatter_t(Xt, rx, K, rows, CX);
     if (rows < PW_BM) {                          // ragged last tile: zero the unused rows
       for (int i = tid; i < NP * (PW_BM - rows); i += PW_NTHR) Yt[(i / (PW_BM - rows)) * LDR + rows + i % (PW_BM - rows)] = f2bf(0.f);
     }
     __syncthreads();
-    if (t + gridDim.x < ntiles) { load(dy, N, t + gridDim.x, ry); load(x, K, t + gridDim.x, rx); }
+    if (t + gridDim.x < ntiles) { load(dy, N, t + gridDim.x, ry, CY); load(x, K, t + gridDim.x, rx, CX); }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int r0 = wave * 64 + kk * 32 + lg * 8;
@@ -237,7 +236,7 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __rest
 }
 
 static int g_pw_cus = 0;
-static int pw_grid(long long M) {
+static int pw_grid(long long M, int per_cu) {
   if (g_pw_cus == 0) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -245,7 +244,7 @@ static int pw_grid(long long M) {
       g_pw_cus = 256;
   }
   const int tiles = (int)((M + PW_BM - 1) / PW_BM);
-  const int g = g_pw_cus * 2;
+  const int g = g_pw_cus * per_cu;
   return tiles < g ? (tiles > 0 ? tiles : 1) : g;
 }
 
@@ -253,7 +252,8 @@ static int pw_grid(long long M) {
 extern "C" int fn_pw_fwd(const void* x, const void* w, const float* bias, void* y, long long M, int K, int N, int act,
                          hipStream_t st) {
   if (K < 1 || K > 64 || N < 1 || N > 64 || M < 8 || M % 8) return -2;
-  const dim3 grid((unsigned)pw_grid(M));
+  // ~110-200 VGPRs and <= 37 KB LDS: 4 workgroups per CU for the 32-channel variants
+  const dim3 grid((unsigned)pw_grid(M, (K <= 32 && N <= 32) ? 4 : 2));
   const bool hb = bias != nullptr;
 #define PWF(KP, NP, A, HB)                                                                                   \
   do {                                                                                                         \
@@ -284,7 +284,7 @@ extern "C" int fn_pw_fwd(const void* x, const void* w, const float* bias, void* 
 // dw: fp32 [N][K], accumulated into (zero it for a fresh gradient)
 extern "C" int fn_pw_wgrad(const void* dy, const void* x, float* dw, long long M, int K, int N, hipStream_t st) {
   if (K < 1 || K > 64 || N < 1 || N > 64 || M < 8 || M % 8) return -2;
-  const dim3 grid((unsigned)pw_grid(M));
+  const dim3 grid((unsigned)pw_grid(M, (K <= 32 && N <= 32) ? 3 : 2));
 #define PWW(KP, NP)                                                                                          \
   do {                                                                                                     \
     const size_t lds = (size_t)(KP + NP) * (PW_BM + 8) * 2;                                                \
