@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--impl", choices=["native", "torch"], default="native")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--dist-backend", choices=["auto", "nccl", "gloo"], default="auto",
+                    help="auto = nccl (RCCL) on GPUs, gloo on CPU; gloo on GPUs lets several ranks share one "
+                         "card to exercise the data-parallel path on a 1-GPU box")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches resident on device")
     ap.add_argument("--tiny", action="store_true", help="16^3 2-class plumbing config (not the headline)")
     ap.add_argument("--model", choices=["cls", "seg"], default="cls",
@@ -66,14 +69,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = args.device == "cuda"
     if use_cuda:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        gpu = local % max(1, torch.cuda.device_count())   # ranks share a card only in gloo tests
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
     else:
         dev = torch.device("cpu")
     if world > 1:
         from featurenet_amd.parallel.ddp import init_from_env
 
-        init_from_env("nccl" if use_cuda else "gloo")
+        backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if use_cuda else "gloo")
+        init_from_env(backend)
 
     torch.manual_seed(1234 + rank)
     if args.tiny:
