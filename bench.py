@@ -59,26 +59,83 @@ def parse():
                     help="memory format of the stock-PyTorch baseline (--impl torch)")
     ap.add_argument("--torch-amp", choices=["bf16", "off"], default="bf16",
                     help="stock-PyTorch baseline: bf16 autocast or plain fp32 (whichever MIOpen runs faster)")
+    ap.add_argument("--torch-find", action="store_true",
+                    help="stock-PyTorch baseline: torch.backends.cudnn.benchmark (MIOpen find: times every "
+                         "applicable solver per shape during warmup and keeps the fastest)")
+    ap.add_argument("--force-allreduce", action="store_true",
+                    help="create the process group even at 1 rank and issue the bucketed all-reduces "
+                         "(exercises the RCCL path from the gradient hooks on a 1-GPU box)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _self_launch(n: int) -> int:
+    """--gpus N > 1 without torchrun: run N ranks as CHILD processes (never exec; the
+    parent has not touched the GPU) and return their exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _peak_bf16_tflops(dev) -> float | None:
+    """Dense bf16 MFMA peak of the device: CUs x 4 SIMDs x 1024 flop/clk x max clock."""
+    if dev.type != "cuda":
+        return None
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    mhz = 2400.0
+    try:
+        import subprocess
+
+        out = subprocess.run(["rocminfo"], capture_output=True, text=True, timeout=30).stdout
+        for blk in out.split("Agent ")[1:]:
+            if "gfx950" in blk and "Max Clock Freq. (MHz):" in blk:
+                mhz = float(blk.split("Max Clock Freq. (MHz):")[1].split()[0])
+                break
+    except Exception:  # noqa: BLE001 - rocminfo missing: use the gfx950 spec clock
+        pass
+    return cus * 4 * 1024 * mhz * 1e6 / 1e12
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
     use_cuda = args.device == "cuda"
+    backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if use_cuda else "gloo")
     if use_cuda:
-        gpu = local % max(1, torch.cuda.device_count())   # ranks share a card only in gloo tests
+        ndev = torch.cuda.device_count()
+        if backend == "nccl" and world > ndev:
+            raise SystemExit(f"bench.py: {world} RCCL ranks need {world} GPUs, {ndev} visible "
+                             "(--dist-backend gloo lets ranks share a card)")
+        gpu = local % max(1, ndev)   # ranks share a card only in gloo tests
         torch.cuda.set_device(gpu)
         dev = torch.device("cuda", gpu)
     else:
         dev = torch.device("cpu")
-    if world > 1:
+    if world > 1 or args.force_allreduce:
         from featurenet_amd.parallel.ddp import init_from_env
 
-        backend = args.dist_backend if args.dist_backend != "auto" else ("nccl" if use_cuda else "gloo")
-        init_from_env(backend)
+        if args.force_allreduce and world == 1:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        init_from_env(backend, force=args.force_allreduce)
+    comm_world = dist.get_world_size() if dist.is_initialized() else 1
+    assert comm_world == world, (comm_world, world)
 
     torch.manual_seed(1234 + rank)
     if args.tiny:
@@ -108,7 +165,7 @@ def main():
             model = FeatureNet3D(cfg).to(dev)
         flat = FlatParams(model)
         opt = FlatAdam(flat.data, flat.grad, lr=1e-3)
-        bucketer = GradBucketer(flat, bucket_mb=args.bucket_mb)
+        bucketer = GradBucketer(flat, bucket_mb=args.bucket_mb, force=args.force_allreduce)
         bucketer.broadcast_from(0)
 
         def step(i):
@@ -124,6 +181,9 @@ def main():
     else:
         from bench.torch_baseline import TorchFeatureNet3D
 
+        if args.torch_find:
+            torch.backends.cudnn.benchmark = True
+        bucketer = None
         torch.manual_seed(1234)
         model = TorchFeatureNet3D(input_size=S, num_classes=NC).to(dev)
         cl = use_cuda and args.torch_layout == "ndhwc"
@@ -152,7 +212,7 @@ def main():
     def sync():
         if use_cuda:
             torch.cuda.synchronize()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
 
     for i in range(args.warmup):
@@ -164,10 +224,19 @@ def main():
         loss = step(args.warmup + i)
     sync()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev if use_cuda else "cpu", dtype=torch.float64)
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # communication diagnostics, measured AFTER the timed region: the bucketed
+    # all-reduce of the whole gradient on its own (what the overlap has to hide)
+    allreduce_ms = None
+    n_buckets = None
+    if bucketer is not None:
+        n_buckets = bucketer.n_buckets
+        if bucketer.active:
+            allreduce_ms = bucketer.time_allreduce()
+    peak = _peak_bf16_tflops(dev)
     ms = elapsed / max(args.steps, 1) * 1e3
     value = args.steps * B * world / elapsed
     base = TORCH_BASELINE_SAMPLES_PER_S_PER_GPU
@@ -201,10 +270,21 @@ def main():
             },
             "final_loss": None if loss is None else round(float(loss.detach()), 4),
         }
+        out["dist"] = {
+            "backend": backend if dist.is_initialized() else None,
+            "rccl_world": comm_world if dist.is_initialized() and backend == "nccl" else None,
+            "buckets": n_buckets,
+            "bucket_mb": args.bucket_mb,
+            "allreduce_ms": None if allreduce_ms is None else round(allreduce_ms, 3),
+            "forced_single_rank": bool(args.force_allreduce and world == 1),
+        }
         if flops:
             out["model_tflops_per_s"] = round(flops * value / 1e12, 2)
+            if peak:
+                # whole-job model FLOP/s over the job's aggregate dense bf16 MFMA peak
+                out["pct_bf16_peak"] = round(100.0 * flops * value / 1e12 / (peak * world), 2)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -144,7 +144,8 @@ def cmd_resume(a) -> int:
 def cmd_serve(a) -> int:
     from .service.server import serve
 
-    serve(a.host, a.port, a.db, a.base, a.devices or None)
+    serve(a.host, a.port, a.db, a.base, a.devices or None, max_workers=a.max_workers,
+          cors_origins=[o for o in a.cors.split(",") if o] or None)
     return 0
 
 
@@ -279,11 +280,13 @@ def build_parser() -> argparse.ArgumentParser:
     c.set_defaults(fn=cmd_resume)
 
     s = sub.add_parser("serve", help="REST task service (reference ui/back)")
-    s.add_argument("--host", default="0.0.0.0")
+    s.add_argument("--host", default="127.0.0.1", help="bind address (no authentication: keep it local)")
     s.add_argument("--port", type=int, default=9999)
     s.add_argument("--db", default="samples.db")
     s.add_argument("--base", default="products")
     s.add_argument("--devices", default="")
+    s.add_argument("--max-workers", type=int, default=2, help="concurrently running task workers")
+    s.add_argument("--cors", default="", help="comma list of origins allowed cross-origin (default none)")
     s.set_defaults(fn=cmd_serve)
 
     tr = sub.add_parser("train", help="train one architecture and save a checkpoint")

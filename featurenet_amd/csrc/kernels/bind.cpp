@@ -76,6 +76,50 @@ static void need(const std::vector<int>& v, size_t n, const char* what) {
   if (v.size() != n) throw std::runtime_error(std::string(what) + ": bad geometry length");
 }
 
+// Extent checks: the geometry implies how many elements every kernel operand
+// spans; the caller passes the numel of the tensors it hands over (``ext``),
+// and a geometry/tensor mismatch raises here instead of reading or writing
+// out of bounds on the GPU.  ``ext`` may be empty (no check) for internal
+// callers that size their own scratch.
+static void fits(const std::vector<long long>& ext, size_t i, long long need_elems, const char* what,
+                 const char* operand) {
+  if (ext.empty()) return;
+  if (i >= ext.size()) throw std::runtime_error(std::string(what) + ": missing extent for " + operand);
+  if (need_elems < 0 || ext[i] < need_elems)
+    throw std::runtime_error(std::string(what) + ": " + operand + " has " + std::to_string(ext[i]) +
+                             " elements, geometry needs " + std::to_string(need_elems));
+}
+static long long prod(std::initializer_list<long long> v) {
+  long long r = 1;
+  for (long long x : v) {
+    if (x < 0) return -1;
+    r *= x;
+  }
+  return r;
+}
+// halo geometry: N ID IH IW C | OD OH OW | KD KH KW | pd ph pw | TD TH TW
+static void check_halo(const std::vector<int>& g, const std::vector<long long>& ext, int ncol, bool wgrad,
+                       const char* what) {
+  const long long src = prod({g[0], g[1], g[2], g[3], g[4]});
+  const long long out = prod({g[0], g[5], g[6], g[7], ncol});
+  const int T = g[8] * g[9] * g[10];
+  if (g[4] <= 0 || ncol <= 0 || T <= 0) throw std::runtime_error(std::string(what) + ": empty geometry");
+  if (g[5] > g[1] + 2 * g[11] || g[6] > g[2] + 2 * g[12] || g[7] > g[3] + 2 * g[13])
+    throw std::runtime_error(std::string(what) + ": output larger than the padded input");
+  if (wgrad) {                       // ext = {dy, src, dw}
+    fits(ext, 0, out, what, "dy");
+    fits(ext, 1, src, what, "src");
+    fits(ext, 2, prod({ncol, T, g[4]}), what, "dw");
+  } else {                           // ext = {src, wt, out, toffs}
+    const int cs = g[4] % 16 == 0 ? 16 : 8, tps = 128 / cs;
+    const long long Tp = (T + tps - 1) / tps * tps;
+    fits(ext, 0, src, what, "src");
+    fits(ext, 1, prod({ncol, g[4], Tp}), what, "wt");
+    fits(ext, 2, out, what, "out");
+    fits(ext, 3, Tp, what, "toffs");
+  }
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "featurenet_amd gfx950 HIP kernels";
   m.attr("ARCH") = "gfx950";
@@ -89,19 +133,25 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("igemm_fwd_mblocks", &fn_igemm_fwd_mblocks);
   m.def("conv_halo", [](uintptr_t src, uintptr_t wt, uintptr_t bias, uintptr_t out, uintptr_t stats,
-                        uintptr_t toffs, std::vector<int> geom, int ncol, int act, uintptr_t sched, uintptr_t st) {
+                        uintptr_t toffs, std::vector<int> geom, int ncol, int act, uintptr_t sched, uintptr_t st,
+                        std::vector<long long> ext) {
     need(geom, 17, "conv_halo");
+    check_halo(geom, ext, ncol, false, "conv_halo");
     chk(fn_conv_halo(P<const void*>(src), P<const void*>(wt), P<const float*>(bias), P<void*>(out), P<float*>(stats),
                      P<const int*>(toffs), geom.data(), ncol, act, P<int*>(sched), S(st)),
         "conv_halo");
-  });
+  }, py::arg("src"), py::arg("wt"), py::arg("bias"), py::arg("out"), py::arg("stats"), py::arg("toffs"),
+     py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("sched"), py::arg("st"),
+     py::arg("ext") = std::vector<long long>());
   m.def("conv_halo_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t dw, std::vector<int> geom, int cout,
-                              int grid_x, uintptr_t sched, uintptr_t st) {
+                              int grid_x, uintptr_t sched, uintptr_t st, std::vector<long long> ext) {
     need(geom, 17, "conv_halo_wgrad");
+    check_halo(geom, ext, cout, true, "conv_halo_wgrad");
     chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x,
                            P<int*>(sched), S(st)),
         "conv_halo_wgrad");
-  });
+  }, py::arg("dy"), py::arg("src"), py::arg("dw"), py::arg("geom"), py::arg("cout"), py::arg("grid_x"),
+     py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>());
   m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {
     chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K, T, C, mode, stage_k, S(st)), "halo_pack_w");
   });
@@ -189,20 +239,30 @@ PYBIND11_MODULE(_C, m) {
                         P<const float*>(dgamma), P<void*>(dy), total, C, inv_count, act, S(st)),
         "bn_bwd_apply");
   });
-  m.def("pool_fwd", [](uintptr_t x, uintptr_t out, uintptr_t scale, uintptr_t shift, std::vector<int> geom,
-                       int is_max, int count_pad, int act, uintptr_t st) {
+  // pool geometry: N D H W C | OD OH OW | KD KH KW | sd sh sw | pd ph pw; ext = {x, out}
+  auto check_pool = [](const std::vector<int>& g, const std::vector<long long>& ext, const char* what) {
+    fits(ext, 0, prod({g[0], g[1], g[2], g[3], g[4]}), what, "x");
+    fits(ext, 1, prod({g[0], g[5], g[6], g[7], g[4]}), what, "out");
+  };
+  m.def("pool_fwd", [check_pool](uintptr_t x, uintptr_t out, uintptr_t scale, uintptr_t shift, std::vector<int> geom,
+                       int is_max, int count_pad, int act, uintptr_t st, std::vector<long long> ext) {
     need(geom, 17, "pool_fwd");
+    check_pool(geom, ext, "pool_fwd");
     chk(fn_pool_fwd(P<const void*>(x), P<void*>(out), P<const float*>(scale), P<const float*>(shift), geom.data(),
                     is_max, count_pad, act, S(st)),
         "pool_fwd");
-  });
-  m.def("pool_bwd", [](uintptr_t dout, uintptr_t x, uintptr_t dx, uintptr_t scale, uintptr_t shift,
-                       std::vector<int> geom, int is_max, int count_pad, int act, uintptr_t st) {
+  }, py::arg("x"), py::arg("out"), py::arg("scale"), py::arg("shift"), py::arg("geom"), py::arg("is_max"),
+     py::arg("count_pad"), py::arg("act"), py::arg("st"), py::arg("ext") = std::vector<long long>());
+  m.def("pool_bwd", [check_pool](uintptr_t dout, uintptr_t x, uintptr_t dx, uintptr_t scale, uintptr_t shift,
+                       std::vector<int> geom, int is_max, int count_pad, int act, uintptr_t st,
+                       std::vector<long long> ext) {
     need(geom, 17, "pool_bwd");
+    check_pool(geom, ext, "pool_bwd");   // ext = {x (and dx), dout}
     chk(fn_pool_bwd(P<const void*>(dout), P<const void*>(x), P<void*>(dx), P<const float*>(scale),
                     P<const float*>(shift), geom.data(), is_max, count_pad, act, S(st)),
         "pool_bwd");
-  });
+  }, py::arg("dout"), py::arg("x"), py::arg("dx"), py::arg("scale"), py::arg("shift"), py::arg("geom"),
+     py::arg("is_max"), py::arg("count_pad"), py::arg("act"), py::arg("st"), py::arg("ext") = std::vector<long long>());
   m.def("upsample2x", [](uintptr_t x, uintptr_t y, int N, int D, int H, int W, int C, int backward, uintptr_t st) {
     chk(fn_upsample2x(P<const void*>(x), P<void*>(y), N, D, H, W, C, backward, S(st)), "upsample2x");
   });

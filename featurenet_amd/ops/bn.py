@@ -122,7 +122,7 @@ class BatchNormActPoolFn(torch.autograd.Function):
             prm = _eval_params(gamma, beta, rmean, rvar, eps, C, y.device)
         p = torch.empty(pspec.out_shape5, dtype=torch.bfloat16, device=y.device)
         _native.kernels().pool_fwd(y.data_ptr(), p.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), pspec.geom17(),
-                                   int(is_max), int(count_pad), act, _native.stream(y))
+                                   int(is_max), int(count_pad), act, _native.stream(y), [y.numel(), p.numel()])
         ctx.save_for_backward(y, prm)
         ctx.act, ctx.training, ctx.pspec, ctx.is_max, ctx.count_pad = act, training, pspec, is_max, count_pad
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
@@ -136,7 +136,7 @@ class BatchNormActPoolFn(torch.autograd.Function):
         dp = dp.contiguous().to(torch.bfloat16)
         _native.kernels().pool_bwd(dp.data_ptr(), y.data_ptr(), dz.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(),
                                    ctx.pspec.geom17(), int(ctx.is_max), int(ctx.count_pad), ctx.act,
-                                   _native.stream(y))
+                                   _native.stream(y), [y.numel(), dp.numel()])
         y2, dz2 = y.reshape(-1, C), dz.reshape(-1, C)
         dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None

@@ -323,7 +323,8 @@ def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> tor
     dw = torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
     st = _native.stream(x5)
     _native.kernels().conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), geom, spec.K,
-                                      max(1, target_wgs // per_tile), halo_sched(x5.device, st).data_ptr(), st)
+                                      max(1, target_wgs // per_tile), halo_sched(x5.device, st).data_ptr(), st,
+                                      [dy5.numel(), x5.numel(), dw.numel()])
     return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
 
 
@@ -334,7 +335,8 @@ def _halo_call(src5, wmat, bias, out, stats, geom, ncol, act):
     toffs = halo_tap_offsets(geom, src5.device)
     st = _native.stream(src5)
     K.conv_halo(src5.data_ptr(), wmat.data_ptr(), _native.ptr(bias), out.data_ptr(), _native.ptr(stats),
-                toffs.data_ptr(), geom, ncol, act, halo_sched(src5.device, st).data_ptr(), st)
+                toffs.data_ptr(), geom, ncol, act, halo_sched(src5.device, st).data_ptr(), st,
+                [src5.numel(), wmat.numel(), out.numel(), toffs.numel()])
 
 
 def halo_conv_fwd(x5, w, bias, spec: ConvSpec, act: int, want_stats: bool, plan):

@@ -16,7 +16,7 @@ class PoolFn(torch.autograd.Function):
     def forward(ctx, x5, pspec: PoolSpec, is_max: bool, count_pad: bool):
         out = torch.empty(pspec.out_shape5, dtype=torch.bfloat16, device=x5.device)
         _native.kernels().pool_fwd(x5.data_ptr(), out.data_ptr(), 0, 0, pspec.geom17(), int(is_max), int(count_pad),
-                                   0, _native.stream(x5))
+                                   0, _native.stream(x5), [x5.numel(), out.numel()])
         ctx.save_for_backward(x5)
         ctx.pspec, ctx.is_max, ctx.count_pad = pspec, is_max, count_pad
         return out
@@ -27,7 +27,8 @@ class PoolFn(torch.autograd.Function):
         dx = torch.empty_like(x5)
         dout = dout.contiguous().to(torch.bfloat16)
         _native.kernels().pool_bwd(dout.data_ptr(), x5.data_ptr(), dx.data_ptr(), 0, 0, ctx.pspec.geom17(),
-                                   int(ctx.is_max), int(ctx.count_pad), 0, _native.stream(x5))
+                                   int(ctx.is_max), int(ctx.count_pad), 0, _native.stream(x5),
+                                   [min(x5.numel(), dx.numel()), dout.numel()])
         return dx, None, None, None
 
 

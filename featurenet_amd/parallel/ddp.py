@@ -2,9 +2,10 @@
 
 Replaces the reference's in-graph ``keras.utils.multi_gpu_model``
 (``model/keras_model.py:137-146``), which sliced the batch inside ONE process
-and merged outputs on the CPU.  Here every rank holds a full replica; the
-gradient of the flat buffer (:class:`~featurenet_amd.training.flat.FlatParams`)
-is cut into contiguous buckets in backward-production order and each bucket's
+and merged outputs on the CPU (and silently fell back to one GPU on any
+error, ``:144-146``).  Here every rank holds a full replica; the gradient of
+the flat buffer (:class:`~featurenet_amd.training.flat.FlatParams`) is cut
+into contiguous buckets in backward-production order and each bucket's
 ``all_reduce`` is issued the moment its last gradient has been accumulated
 (``register_post_accumulate_grad_hook``).  ProcessGroupNCCL (= RCCL on ROCm)
 runs collectives on its own HIP stream, ordered after the compute stream at
@@ -15,14 +16,26 @@ optimizer's gradient scale -- no extra pass over the gradients.
 Bucket sizing for MI355X: an 8-GPU node is a fully connected xGMI mesh
 (7 links x ~153 GB/s per GPU); a ring step is bound by one link, so small
 buckets are latency-bound (tens of us per collective) while one huge bucket
-serialises behind the last layer's backward.  Default cap 32 MiB; the
-largest single tensor (e.g. FeatureNet-3D's 64000x128 FC weight, 32.8 MB)
-forms its own bucket and is reduced while the conv stack is still in
-backward.  HBM is never the constraint (288 GB per GPU).
+serialises behind the last layer's backward.  Default cap 32 MiB.  A bucket
+is closed BEFORE a tensor that would push it past the cap, and any tensor of
+at least half the cap gets a bucket of its own: FeatureNet-3D's 64000x128 FC1
+weight gradient (32.8 MB, produced by the very first backward GEMM) is
+therefore reduced alone while the whole conv stack is still in backward,
+and the conv gradients (~1 MB) form the tail bucket.  HBM is never the
+constraint (288 GB per GPU).
+
+Failure handling: the process group is created with an
+explicit timeout (``FN_PG_TIMEOUT`` seconds, default 300) and, on RCCL, with
+the async-error watchdog on, so a dead or hung peer aborts every surviving
+rank with a non-zero exit instead of hanging the job; a collective that
+raises is re-raised as :class:`DistributedFailure` naming the rank and
+bucket.
 """
 from __future__ import annotations
 
 import os
+import time
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -30,66 +43,124 @@ import torch.distributed as dist
 from ..training.flat import FlatParams
 
 
-def init_from_env(backend: str | None = None) -> tuple[int, int, int]:
-    """Initialise torch.distributed from torchrun env vars; returns (rank, world, local_rank)."""
+class DistributedFailure(RuntimeError):
+    """A collective failed or timed out (peer died, network/RCCL error)."""
+
+
+def pg_timeout_s() -> float:
+    return float(os.environ.get("FN_PG_TIMEOUT", "300"))
+
+
+def init_from_env(backend: str | None = None, force: bool = False,
+                  timeout_s: float | None = None) -> tuple[int, int, int]:
+    """Initialise torch.distributed from torchrun env vars; returns (rank, world, local_rank).
+
+    ``force`` creates the process group even at world size 1 (a single-rank
+    RCCL communicator: exercises the bucketed collective path on a 1-GPU box).
+    """
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        timeout = timedelta(seconds=timeout_s if timeout_s is not None else pg_timeout_s())
         if backend == "nccl":
+            # watchdog: a timed-out or failed collective tears the process down
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
             torch.cuda.set_device(local)
-            dist.init_process_group(backend, rank=rank, world_size=world, device_id=torch.device("cuda", local))
+            dist.init_process_group(backend, rank=rank, world_size=world, timeout=timeout,
+                                    device_id=torch.device("cuda", local))
         else:
-            dist.init_process_group(backend, rank=rank, world_size=world)
+            dist.init_process_group(backend, rank=rank, world_size=world, timeout=timeout)
     return rank, world, local
 
 
+def plan_buckets(sizes: list[int], cap: int) -> list[list[int]]:
+    """Group consecutive tensors (element counts ``sizes``) into buckets of at most ``cap`` elements.
+
+    A tensor of at least ``cap // 2`` elements is a bucket of its own; otherwise
+    the open bucket is closed before a tensor that would push it past ``cap``.
+    Returns lists of tensor indices, in order.
+    """
+    out: list[list[int]] = []
+    cur: list[int] = []
+    size = 0
+    for i, n in enumerate(sizes):
+        if n >= cap // 2:
+            if cur:
+                out.append(cur)
+            out.append([i])
+            cur, size = [], 0
+            continue
+        if cur and size + n > cap:
+            out.append(cur)
+            cur, size = [], 0
+        cur.append(i)
+        size += n
+    if cur:
+        out.append(cur)
+    return out
+
+
 class GradBucketer:
-    def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 32.0, overlap: bool = True):
+    def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 32.0, overlap: bool = True,
+                 force: bool = False):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # active: collectives are issued (world > 1, or a forced single-rank communicator)
+        self.active = dist.is_initialized() and (self.world > 1 or force)
         self.overlap = overlap
-        cap = int(bucket_mb * 1024 * 1024 / 4)
+        self.paused = False               # tests: run a backward without issuing collectives
+        self.cap = max(1, int(bucket_mb * 1024 * 1024 / 4))
         self.buckets: list[tuple[int, int]] = []
         self.members: list[list] = []
         self.param_bucket: dict[int, int] = {}
-        start, cur, size = None, [], 0
-        for p, off, n in flat.slices:
-            if start is None:
-                start = off
-            cur.append(p)
-            size = off + n - start
-            if size >= cap:
-                self._close(start, off + n, cur)
-                start, cur = None, []
-        if cur:
-            last_p, last_off, last_n = flat.slices[-1]
-            self._close(start, last_off + last_n, cur)
+        # flat slices are contiguous in flat order: a bucket spans first offset .. last end
+        for idx in plan_buckets([n for _, _, n in flat.slices], self.cap):
+            ps = [flat.slices[i] for i in idx]
+            s = ps[0][1]
+            e = ps[-1][1] + ps[-1][2]
+            if idx[-1] + 1 < len(flat.slices):
+                e = flat.slices[idx[-1] + 1][1]          # include the alignment pad up to the next slice
+            else:
+                e = flat.numel
+            self.buckets.append((s, e))
+            self.members.append([p for p, _, _ in ps])
+            for p, _, _ in ps:
+                self.param_bucket[id(p)] = len(self.buckets) - 1
         self.pending = [len(m) for m in self.members]
         self.launched = [False] * len(self.buckets)
         self.works: list = []
         self.hooks = []
-        if self.world > 1 and overlap:
+        self.n_collectives = 0
+        if self.active and overlap:
             for p, _, _ in flat.slices:
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
-    def _close(self, s: int, e: int, ps: list) -> None:
-        idx = len(self.buckets)
-        self.buckets.append((s, e))
-        self.members.append(list(ps))
-        for p in ps:
-            self.param_bucket[id(p)] = idx
+    @property
+    def n_buckets(self) -> int:
+        return len(self.buckets)
+
+    def bucket_bytes(self) -> list[int]:
+        return [(e - s) * 4 for s, e in self.buckets]
 
     def _launch(self, b: int) -> None:
         s, e = self.buckets[b]
         self.launched[b] = True
-        self.works.append(dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True))
+        try:
+            self.works.append((b, dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True)))
+        except Exception as ex:                      # noqa: BLE001 - re-raised with context
+            raise DistributedFailure(f"rank {self.rank}: all_reduce of bucket {b} failed to launch: {ex}") from ex
+        self.n_collectives += 1
 
     def _on_grad(self, p) -> None:
+        if self.paused:
+            return
         b = self.param_bucket.get(id(p))
         if b is None or self.launched[b]:
             return
@@ -105,22 +176,52 @@ class GradBucketer:
 
     def finish(self) -> float:
         """Complete all reductions; returns the gradient scale (1/world) for the optimizer."""
-        if self.world == 1:
+        if not self.active or self.paused:
             return 1.0
         for i in range(len(self.buckets)):
             if not self.launched[i]:
                 self._launch(i)
-        for w in self.works:
-            w.wait()
+        try:
+            for b, w in self.works:
+                w.wait()
+        except Exception as ex:                      # noqa: BLE001
+            raise DistributedFailure(f"rank {self.rank}: all_reduce of bucket {b} failed: {ex}") from ex
+        finally:
+            self.works.clear()
+            self.pending = [len(m) for m in self.members]
+            self.launched = [False] * len(self.buckets)
+        return 1.0 / self.world
+
+    def reset(self) -> None:
+        """Forget a partially issued step (after a skipped/aborted backward)."""
         self.works.clear()
         self.pending = [len(m) for m in self.members]
         self.launched = [False] * len(self.buckets)
-        return 1.0 / self.world
 
     def broadcast_from(self, src: int = 0) -> None:
         """Make every replica start from rank ``src``'s parameters and buffers."""
-        if self.world == 1:
+        if not self.active or self.world == 1:
             return
         dist.broadcast(self.flat.data, src, group=self.group)
         for b in self.flat.module.buffers():
             dist.broadcast(b, src, group=self.group)
+
+    def time_allreduce(self, iters: int = 5) -> float:
+        """Median wall ms of one all-reduce of the whole flat gradient (bucketed as in training)."""
+        if not self.active:
+            return 0.0
+        cuda = self.flat.grad.is_cuda
+        ts = []
+        for _ in range(iters + 1):
+            if cuda:
+                torch.cuda.synchronize()
+            dist.barrier(group=self.group)
+            t0 = time.perf_counter()
+            works = [dist.all_reduce(self.flat.grad[s:e], group=self.group, async_op=True) for s, e in self.buckets]
+            for w in works:
+                w.wait()
+            if cuda:
+                torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        ts = sorted(ts[1:])
+        return ts[len(ts) // 2]

@@ -174,8 +174,10 @@ def carlini_l2(model, x: torch.Tensor, y: torch.Tensor | None = None, confidence
             f = torch.clamp(real - other + confidence, min=0.0)
             l2 = ((adv - x) ** 2).reshape(B, -1).sum(1)
             loss = (l2 + c * f).sum()
-            opt.zero_grad()
-            loss.backward()
+            # gradient w.r.t. the attack variable only: loss.backward() would also run every
+            # layer's weight-gradient pass into the training gradient buffer (and, under DP,
+            # fire the all-reduce hooks outside a training step)
+            (w.grad,) = torch.autograd.grad(loss, [w])
             opt.step()
             with torch.no_grad():
                 ok = (z.argmax(1) != y) & (f <= 0)

@@ -172,17 +172,22 @@ class TrialScheduler:
 
     def _map_processes(self, specs, cfg):
         ctx = mp.get_context("spawn")
-        results = ctx.Queue()
         workers: dict[str, dict] = {}
+        retired: list[dict] = []
 
         def start(dev):
+            # every worker gets its OWN result queue, replaced with the worker: killing a
+            # process while it writes a shared multiprocessing.Queue can corrupt that queue
             tq = ctx.Queue()
+            rq = ctx.Queue()
             ready = ctx.Queue()
-            p = ctx.Process(target=_worker, args=(dev, tq, results, ready), daemon=True)
+            p = ctx.Process(target=_worker, args=(dev, tq, rq, ready), daemon=True)
             p.start()
             # keep every queue referenced: a collected queue unlinks its semaphore
             # before the spawned child has unpickled it
-            workers[dev] = {"proc": p, "tasks": tq, "ready": ready, "busy": None, "t0": 0.0}
+            if dev in workers:
+                retired.append(workers[dev])
+            workers[dev] = {"proc": p, "tasks": tq, "results": rq, "ready": ready, "busy": None, "t0": 0.0}
 
         for d in self.devices:
             start(d)
@@ -195,14 +200,20 @@ class TrialScheduler:
                     tid, s = pending.pop(0)
                     w["busy"], w["t0"] = tid, time.time()
                     w["tasks"].put((tid, s.to_json(), cfgd))
-            try:
-                tid, js = results.get(timeout=0.5)
-                out[tid] = ModelSpec.from_json(js)
-                for w in workers.values():
-                    if w["busy"] == tid:
-                        w["busy"] = None
-            except queue.Empty:
-                pass
+            got = False
+            for w in list(workers.values()):
+                try:
+                    tid, js = w["results"].get_nowait()
+                except queue.Empty:
+                    continue
+                got = True
+                # only the trial this worker is running counts: a result that arrives after
+                # the watchdog already failed (and restarted) it is dropped
+                if w["busy"] == tid and tid not in out:
+                    out[tid] = ModelSpec.from_json(js)
+                    w["busy"] = None
+            if not got:
+                time.sleep(0.05)
             # watchdog: hung or dead workers fail their trial and are restarted
             for dev in list(workers):
                 w = workers[dev]

@@ -19,6 +19,7 @@ separate processes (``python -m featurenet_amd.service.worker``).
 
 import json
 import os
+import re
 import subprocess
 import sys
 from pathlib import Path
@@ -62,16 +63,24 @@ def _file_endswith(folder: str, suffix: str):
 
 
 def create_app(db_path: str = "samples.db", base_path: str = "products", devices: str | None = None,
-               spawn_workers: bool = True):
+               spawn_workers: bool = True, max_workers: int = 2, cors_origins: list[str] | None = None):
+    """``max_workers`` caps concurrently running worker processes (each trains on the
+    GPUs); ``cors_origins`` enables CORS for those origins only (default: same origin)."""
     from fastapi import FastAPI, Request
-    from fastapi.middleware.cors import CORSMiddleware
     from fastapi.responses import FileResponse, HTMLResponse, JSONResponse
 
     store = TaskStore(db_path)
     app = FastAPI(title="featurenet_amd NAS service")
-    app.add_middleware(CORSMiddleware, allow_origins=["*"], allow_methods=["*"], allow_headers=["*"])
+    if cors_origins:
+        from fastapi.middleware.cors import CORSMiddleware
+
+        app.add_middleware(CORSMiddleware, allow_origins=list(cors_origins), allow_methods=["GET", "POST", "DELETE"],
+                           allow_headers=["Content-Type"])
     app.state.store = store
     app.state.workers = {}
+
+    def running() -> int:
+        return sum(1 for p in app.state.workers.values() if p.poll() is None)
 
     def start_worker(task_id: str):
         cmd = [sys.executable, "-m", "featurenet_amd.service.worker", task_id, "--db", db_path, "--base", base_path]
@@ -81,10 +90,26 @@ def create_app(db_path: str = "samples.db", base_path: str = "products", devices
         app.state.workers[task_id] = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT,
                                                       cwd=os.getcwd(), start_new_session=True)
 
+    def stop_workers() -> int:
+        n = 0
+        for p in app.state.workers.values():
+            if p.poll() is None:
+                p.terminate()                     # the worker's own process only (its session)
+                n += 1
+        for p in app.state.workers.values():
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        app.state.workers.clear()
+        return n
+
+    app.state.stop_workers = stop_workers
     Path(base_path).mkdir(parents=True, exist_ok=True)
 
     @app.delete("/sample/")
     def sample_delete_all():
+        stop_workers()
         return store.delete_all()
 
     @app.get("/sample/")
@@ -96,6 +121,8 @@ def create_app(db_path: str = "samples.db", base_path: str = "products", devices
         task = store.get(task_id)
         if task is None:
             return JSONResponse({}, status_code=404)
+        if not re.fullmatch(r"[A-Za-z0-9_.-]{1,128}", pid) or ".." in pid:
+            return JSONResponse({"error": "bad product id"}, status_code=400)
         if content == "graph":
             f, mime = _file_endswith(task.get("products"), f"{pid}.svg"), "image/svg+xml"
         else:
@@ -117,6 +144,8 @@ def create_app(db_path: str = "samples.db", base_path: str = "products", devices
     async def sample_post(request: Request):
         body = await request.json()
         data = body.get("data", body) if isinstance(body, dict) else {}
+        if spawn_workers and running() >= max_workers:
+            return JSONResponse({"error": f"{max_workers} tasks already running; retry later"}, status_code=429)
         task = store.create(data)
         if spawn_workers:
             start_worker(task["task_id"])
@@ -129,8 +158,10 @@ def create_app(db_path: str = "samples.db", base_path: str = "products", devices
     return app
 
 
-def serve(host: str = "0.0.0.0", port: int = 9999, db_path: str = "samples.db", base_path: str = "products",
-          devices: str | None = None) -> None:
+def serve(host: str = "127.0.0.1", port: int = 9999, db_path: str = "samples.db", base_path: str = "products",
+          devices: str | None = None, max_workers: int = 2, cors_origins: list[str] | None = None) -> None:
+    """Bind to localhost by default: the service has no authentication (as the reference's)."""
     import uvicorn
 
-    uvicorn.run(create_app(db_path, base_path, devices), host=host, port=port)
+    uvicorn.run(create_app(db_path, base_path, devices, max_workers=max_workers, cors_origins=cors_origins),
+                host=host, port=port)

@@ -13,6 +13,7 @@ task concurrently without lost writes.
 from __future__ import annotations
 
 import json
+import re
 import sqlite3
 import time
 import uuid
@@ -27,6 +28,19 @@ SCHEMA = """CREATE TABLE IF NOT EXISTS tasks (
     task_id TEXT,
     PRIMARY KEY (id)
 )"""
+
+
+# fields only the server / worker may set: file locations that routes serve from
+# and the worker writes to, and the task bookkeeping columns
+SERVER_KEYS = frozenset({"products", "pdt", "fm", "fm_template", "error", "status", "task_id", "timestamp",
+                         "valid_elements", "nb_valid_elements", "models"})
+
+
+def safe_name(name) -> str:
+    """A task name usable as ONE path component: [A-Za-z0-9_-], spaces -> '_' (reference
+    ``ui/back/main.py`` replaced spaces only, so '../..' escaped the products directory)."""
+    s = re.sub(r"[^A-Za-z0-9_-]", "", str(name).replace(" ", "_"))
+    return s[:64]
 
 
 class TaskStore:
@@ -61,8 +75,9 @@ class TaskStore:
         return d
 
     def create(self, params: dict, status: str = "init") -> dict:
-        params = dict(params or {})
-        params["task_name"] = str(params.get("task_name", "")).replace(" ", "_")
+        # client data never sets server-owned fields (paths the worker writes or serves from)
+        params = {k: v for k, v in dict(params or {}).items() if k not in SERVER_KEYS}
+        params["task_name"] = safe_name(params.get("task_name", ""))
         task_id = uuid.uuid1().hex[:10]
         ts = int(time.time())
         with self._conn() as c:

@@ -25,10 +25,15 @@ def run_task(store: TaskStore, task_id: str, base_path: str, template: str | Non
     from ..search import pledge_evolution as pe
     from ..search.trial import TrialConfig, TrialScheduler
 
+    from .store import safe_name
+
     task = store.get(task_id)
-    base = os.path.join(base_path, task.get("task_name") or task_id)
+    root = os.path.realpath(base_path)
+    base = os.path.realpath(os.path.join(root, safe_name(task.get("task_name")) or safe_name(task_id)))
+    if os.path.commonpath([root, base]) != root or base == root:
+        return store.update(task_id, "generation_failed", error="task directory escapes the products root")
     nb = (int(task.get("max_nb_blocks", 5)), int(task.get("max_nb_cells", 5)), int(task.get("nb_initial_config", 10)))
-    template = task.get("fm_template") or template
+    # the FM template is a server-side choice (the CLI flag), never a client-supplied path
     if not template:
         template = str(default_template(os.path.join(base, "main_1block_nas.xml")))
     fm = pe.end2end(base, nb, template)

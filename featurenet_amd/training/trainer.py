@@ -28,7 +28,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import FlatAdam, FlatSGD, softmax_xent
-from ..parallel.ddp import GradBucketer
+from ..parallel.ddp import DistributedFailure, GradBucketer
 from ..utils.events import default_log
 from .callbacks import Callback
 from .checkpoint import save_checkpoint
@@ -133,7 +133,11 @@ class Trainer:
         logits = self.model(self._prep(xb))
         loss, correct = softmax_xent(logits, yb, self.label_smoothing, with_correct=True)
         loss.backward()
-        scale = self.bucketer.finish()
+        try:
+            scale = self.bucketer.finish()
+        except DistributedFailure as e:              # fail fast: log and let the process exit non-zero
+            default_log().emit("dp_failure", rank=self.rank, world=self.world, error=str(e))
+            raise
         self.opt.step(grad_scale=scale)
         return loss.detach(), correct
 

@@ -136,3 +136,94 @@ def test_precise_bn_averages_running_stats_across_ranks(tmp_path):
         torch.testing.assert_close(mod.running_mean, exp_mean, rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(mod.running_var, exp_var, rtol=1e-4, atol=1e-5)
         assert not torch.allclose(per_rank[0][i][0], per_rank[1][i][0])   # shards really differ
+
+
+# ---------------------------------------------------------------- bucket planning
+def test_plan_buckets_closes_before_overflow_and_isolates_large_tensors():
+    from featurenet_amd.parallel.ddp import plan_buckets
+
+    # cap 100: 10+30+49 fits (89); 20 would overflow -> new bucket; 60 >= cap/2 -> alone
+    assert plan_buckets([10, 30, 49, 20, 60, 5, 5], 100) == [[0, 1, 2], [3], [4], [5, 6]]
+    assert plan_buckets([200], 100) == [[0]]
+    assert plan_buckets([1] * 5, 4) == [[0, 1, 2, 3], [4]]
+    for sizes in ([3, 7, 1, 90, 45, 2, 60, 1], [1] * 50, [49, 51, 49, 51]):
+        plan = plan_buckets(sizes, 100)
+        assert [i for b in plan for i in b] == list(range(len(sizes)))      # order kept, all covered
+        for b in plan:
+            assert len(b) == 1 or sum(sizes[i] for i in b) <= 100
+
+
+def test_featurenet3d_fc1_gradient_has_its_own_bucket():
+    """at the default 32 MiB cap FC1's 32.8 MB weight gradient must not share a
+    bucket with conv gradients (it is ready first; the convs come much later in backward)."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+    from featurenet_amd.parallel.ddp import GradBucketer
+    from featurenet_amd.training.flat import FlatParams
+
+    m = FeatureNet3D(FeatureNet3DConfig())
+    flat = FlatParams(m)
+    b = GradBucketer(flat, bucket_mb=32.0)
+    names = {id(p): n for n, p in m.named_parameters()}
+    groups = [[names[id(p)] for p in ps] for ps in b.members]
+    fc1 = [g for g in groups if "fc1.weight" in g]
+    assert len(fc1) == 1 and not any(n.startswith("convs.") for n in fc1[0]), groups
+    assert groups.index(fc1[0]) <= 1                              # issued at the start of backward
+    conv_buckets = [g for g in groups if any(n.startswith("convs.") for n in g)]
+    assert conv_buckets and all(not any(n.startswith("fc") for n in g) for g in conv_buckets)
+    # buckets tile the flat buffer contiguously
+    assert b.buckets[0][0] == 0 and b.buckets[-1][1] == flat.numel
+    assert all(b.buckets[i][1] == b.buckets[i + 1][0] for i in range(len(b.buckets) - 1))
+
+
+# ---------------------------------------------------------------- failure detection
+def test_killed_rank_fails_fast(tmp_path):
+    """A rank that dies mid-job makes the survivor exit non-zero (DistributedFailure)
+    well inside the process-group timeout instead of hanging."""
+    import socket
+    import subprocess
+    import sys
+    import time
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    worker = os.path.join(os.path.dirname(__file__), "dp_fault_worker.py")
+    procs = []
+    t0 = time.time()
+    for r in range(WORLD):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(WORLD), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), FN_PG_TIMEOUT="60", FN_KILL_RANK="1", OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, worker], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=150)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise AssertionError("a surviving rank hung after its peer died")
+    elapsed = time.time() - t0
+    assert procs[1].returncode == 17
+    assert procs[0].returncode == 3, outs[0][-2000:]
+    assert "DistributedFailure" in outs[0]
+    assert elapsed < 120
+
+
+def test_process_group_has_explicit_timeout(monkeypatch):
+    from datetime import timedelta
+
+    from featurenet_amd.parallel import ddp
+
+    seen = {}
+
+    def fake_init(backend, **kw):
+        seen.update(kw, backend=backend)
+
+    monkeypatch.setattr(ddp.dist, "is_initialized", lambda: False)
+    monkeypatch.setattr(ddp.dist, "init_process_group", fake_init)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("FN_PG_TIMEOUT", "42")
+    ddp.init_from_env("gloo")
+    assert seen["backend"] == "gloo" and seen["timeout"] == timedelta(seconds=42)

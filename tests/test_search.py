@@ -85,9 +85,40 @@ def test_pledge_evolution_one_generation(tmp_path):
     assert len(ranked) >= 1
     accs = [v[0] for v in ranked]
     assert accs == sorted(accs, reverse=True)
-    # child feature models carry the injected "~Architecture or ~label" constraints
-    xml = (tmp_path / "mnist" / "e0_m0_b0.xml").read_text()
-    assert "~Architecture  or  ~" in xml or r.population
+    assert r.population
+
+
+@need_ref
+def test_pledge_children_exclude_constrained_labels(tmp_path):
+    """generate_children injects ``~Architecture or ~<label>`` per constrained label
+    (reference ``pledge_evolution.py:70-99``): the child FM carries every clause and
+    no sampled child selects a constrained feature."""
+    import random
+
+    from featurenet_amd import _native
+    from featurenet_amd.fm.products import ProductSet
+    from featurenet_amd.fm.sampler import run_pledge
+    from featurenet_amd.search import pledge_evolution as pe
+
+    if not _native.runtime_available():
+        pytest.skip("native runtime not built")
+    fm = pe.end2end(str(tmp_path), (1, 1, 8), f"{REF}/main_1block_nas.xml")
+    base = tmp_path / "base.pdt"
+    run_pledge(fm, 8, base, duration=0.3, seed=1)
+    ps = ProductSet(base)
+    enabled = [set(ps.enabled_labels(p)) for p in ps.products]
+    # non-core leaf labels (absent from some sampled product): excluding them stays satisfiable
+    richest = max(enabled, key=len)
+    labels = sorted(l for l in richest - set.intersection(*enabled) if len(l) > 3)[:2]
+    assert labels, "sampled products are all identical"
+    pdt = pe.generate_children(str(tmp_path / "child"), labels, fm, 6, 1.0, random.Random(0), duration_s=0.3)
+    xml = (tmp_path / "child.xml").read_text()
+    for l in labels:
+        assert f"~Architecture  or  ~{l}" in xml
+    kids = ProductSet(pdt)
+    assert kids.nbProducts >= 1
+    for p in kids.products:
+        assert not set(kids.enabled_labels(p)) & set(labels)
 
 
 @need_ref

@@ -68,3 +68,53 @@ def test_rest_routes_and_worker_pipeline(tmp_path):
     assert m.status_code == 200 and len(m.content) > 100
     assert "<html>" in c.get("/").text
     assert c.delete("/sample/").json() == 1
+
+
+def test_store_rejects_path_escape_and_server_keys(tmp_path):
+    """client task names are one safe path component; server-owned fields are dropped."""
+    from featurenet_amd.service.store import TaskStore, safe_name
+
+    assert safe_name("../../etc x") == "etc_x"
+    s = TaskStore(tmp_path / "t.db")
+    t = s.create({"task_name": "../../evil", "products": "/etc", "fm_template": "/etc/passwd", "pdt": "/x",
+                  "dataset": "mnist"})
+    assert t["task_name"] == "evil"
+    for k in ("products", "fm_template", "pdt"):
+        assert k not in s.get(t["task_id"])
+
+
+def test_worker_cap_and_bad_product_id(tmp_path):
+    from fastapi.testclient import TestClient
+
+    from featurenet_amd.service.server import create_app
+
+    app = create_app(str(tmp_path / "s.db"), str(tmp_path / "p"), spawn_workers=False)
+    c = TestClient(app)
+    tid = c.post("/sample/", json={"data": {"task_name": "t"}}).json()["task_id"]
+    assert c.get(f"/sample/{tid}/product/..%2F..%2Fx/model").status_code in (400, 404)
+    assert c.get(f"/sample/{tid}/product/a..b/model").status_code == 400
+
+    class Running:
+        def poll(self):
+            return None
+
+        def terminate(self):
+            self.t = True
+
+        def wait(self, timeout=None):
+            return 0
+
+    app2 = create_app(str(tmp_path / "s2.db"), str(tmp_path / "p2"), spawn_workers=True, max_workers=1)
+    app2.state.workers["x"] = w = Running()
+    c2 = TestClient(app2)
+    assert c2.post("/sample/", json={"data": {"task_name": "t"}}).status_code == 429
+    c2.delete("/sample/")                                   # DELETE stops running workers
+    assert getattr(w, "t", False) and app2.state.workers == {}
+
+
+def test_server_binds_localhost_by_default():
+    import inspect
+
+    from featurenet_amd.service.server import serve
+
+    assert inspect.signature(serve).parameters["host"].default == "127.0.0.1"
