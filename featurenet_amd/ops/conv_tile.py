@@ -1,0 +1,303 @@
+"""Host side of the big-tile halo conv kernel (``csrc/kernels/conv_tile.hip``).
+
+The kernel runs 4 waves per workgroup, one per SIMD, each owning ``16*MT``
+output rows (512-640-row tiles), with the input halo of a ``CS``-channel
+slice double-buffered in LDS (LDS-DMA) and the weights streamed from L2
+straight into MFMA fragments.  This module
+
+* plans the output tile (``TD x TH x TW``), the channel slice and ``MT`` for
+  a layer from a simple cycle model (MFMA k-steps per job + per-job fixed
+  cost, tail rounding over the 256 CUs), subject to the 160 KiB LDS;
+* builds the row table that permutes the tile's output rows into MFMA
+  fragments whose 16 rows have 16 distinct halo positions mod 16 -- with the
+  chunk-planar halo layout that makes every ``ds_read_b128`` A-fragment read
+  bank-conflict free;
+* packs the conv weight into the fragment-ordered B stream (one HIP launch).
+
+Reference parity: this is the same convolution as ``ops/conv.py`` (Keras
+``Conv2D``/``Conv3D`` semantics, reference ``model/input.py:294``); only the
+MI355X execution strategy differs.
+"""
+from __future__ import annotations
+
+import math
+import os
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native
+
+LDS_MAX = 160 * 1024
+NTHR = 256
+MT_CHOICES = (8, 9, 10)
+_LOCK = threading.Lock()
+_PLANS: dict = {}
+_ROWTAB: dict = {}
+_ZERO: dict = {}
+_SCHED: dict = {}
+
+
+def enabled() -> bool:
+    return os.environ.get("FN_CONV_TILE", "1") != "0"
+
+
+@dataclass(frozen=True)
+class TilePlan:
+    TD: int
+    TH: int
+    TW: int
+    CS: int          # channels per halo slice
+    MT: int          # 16-row MFMA tiles per wave
+    NT: int          # 16-col MFMA tiles per workgroup (2 or 4)
+    HPpad: int
+    nks: int         # k-steps per job
+    nct: int         # 16-col tiles of the packed weights
+    BUF: int         # bytes per LDS buffer
+    mHW: int
+    mHHW: int
+    cost: float      # modelled cycles (per wave, summed over the jobs of one CU)
+
+    @property
+    def rows(self) -> int:
+        return self.TD * self.TH * self.TW
+
+
+def _magic(d: int) -> int:
+    return (2**32 + d - 1) // d
+
+
+def _magic_ok(HH: int, HW: int, npos: int) -> bool:
+    p = np.arange(npos, dtype=np.uint64)
+    m2, m1 = np.uint64(_magic(HH * HW)), np.uint64(_magic(HW))
+    hd = (p * m2) >> np.uint64(32)
+    rem = p - hd * np.uint64(HH * HW)
+    hh = (rem * m1) >> np.uint64(32)
+    return bool(np.all(hd == p // np.uint64(HH * HW)) and np.all(hh == rem // np.uint64(HW)))
+
+
+def _ksteps(T: int, CS: int, PD: int) -> int:
+    k = T * (CS // 32) if CS >= 32 else (T + 1) // 2
+    return -(-k // PD) * PD
+
+
+def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int = 256):
+    """Best TilePlan for an (N, OD, OH, OW) output of a (KD, KH, KW) stride-1 conv over
+    ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply."""
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus)
+    if key in _PLANS:
+        return _PLANS[key]
+    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus)
+    with _LOCK:
+        _PLANS[key] = best
+    return best
+
+
+def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
+    OD, OH, OW = out_dims
+    KD, KH, KW = kdims
+    T = KD * KH * KW
+    if Ncol < 16 or Csrc % 16 or T < 2:
+        return None
+    NT = 2 if Ncol <= 32 else 4
+    ncb = -(-Ncol // (NT * 16))
+    nct = ncb * NT
+    PD = 4 if NT == 2 else 3
+    workers = max(1, n_cus // ncb)
+    cands = []
+    for CS in (32, 16):
+        if Csrc % CS:
+            continue
+        CPP = CS // 8
+        nslice = Csrc // CS
+        nks = _ksteps(T, CS, PD)
+        tw_opts = sorted({OW} | {-(-OW // k) for k in range(2, 5) if -(-OW // k) >= 8})
+        for TW in tw_opts:
+            for TD in range(1, OD + 1):
+                for TH in range(1, OH + 1):
+                    rows = TD * TH * TW
+                    if rows > 64 * MT_CHOICES[-1]:
+                        break
+                    MT = max(MT_CHOICES[0], -(-rows // 64))
+                    if rows < 64 * MT_CHOICES[0] * 0.75:
+                        continue
+                    HH, HW = TH + KH - 1, TW + KW - 1
+                    HP = (TD + KD - 1) * HH * HW
+                    HPpad = -(-HP // 64) * 64
+                    halo = HPpad * CPP * 16
+                    stage = (64 * MT + 1) * (NT * 16 + 8) * 2
+                    BUF = -(-max(halo, stage, NTHR * 64) // 16) * 16
+                    lds = 2 * BUF + 64 + 1024 + 4 * 64 * MT * 4
+                    if lds > LDS_MAX:
+                        continue
+                    tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
+                    jobs = tiles * nslice
+                    mfma = nks * MT * NT * 16                  # cycles of MFMA issue per wave per job
+                    fixed = 1200 + (HPpad * CPP // 64) * 8      # barrier + DMA issue per job
+                    epi = 1500 + rows * NT * 2 // NTHR * 40 / nslice
+                    per_job = mfma + fixed + epi
+                    cost = math.ceil(jobs / workers) * per_job
+                    cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
+                                          float(cost)))
+    # the cheapest few, re-costed with their row tables' residual bank conflicts (a
+    # fragment whose 16 rows repeat a residue mod 16 reads at half rate)
+    best = None
+    for c in sorted(cands, key=lambda c: c.cost)[:12]:
+        HH, HW = c.TH + KH - 1, c.TW + KW - 1
+        if not _magic_ok(HH, HW, c.HPpad):
+            continue
+        tab = row_table(c, kdims)
+        res = tab[:, 0].reshape(-1, 16) % 16
+        dups = sum(16 - len(set(r.tolist())) for r in res)
+        cost = c.cost * (1.0 + 0.5 * dups / res.size)
+        if best is None or cost < best.cost:
+            best = TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct", "BUF",
+                                                        "mHW", "mHHW")), cost)
+    return best
+
+
+def row_table(p: TilePlan, kdims: tuple) -> np.ndarray:
+    """int32 [4*MT*16, 2]: (halo position of the row's tap (0,0,0), natural tile row or -1),
+    fragments of 16 rows with distinct halo positions mod 16 (bank-conflict-free A reads)."""
+    key = (p, tuple(kdims))
+    t = _ROWTAB.get(key)
+    if t is not None:
+        return t
+    KD, KH, KW = kdims
+    HH, HW = p.TH + KH - 1, p.TW + KW - 1
+    td, th, tw = np.meshgrid(np.arange(p.TD), np.arange(p.TH), np.arange(p.TW), indexing="ij")
+    nat = ((td * p.TH + th) * p.TW + tw).reshape(-1)
+    hb = ((td * HH + th) * HW + tw).reshape(-1)
+    nfrag = 4 * p.MT
+    buckets = [list(zip(hb[hb % 16 == r].tolist(), nat[hb % 16 == r].tolist())) for r in range(16)]
+    frags = [[None] * 16 for _ in range(nfrag)]
+    extra = []
+    for r in range(16):
+        for i, item in enumerate(buckets[r]):
+            if i < nfrag:
+                frags[i][r] = item
+            else:
+                extra.append(item)
+    maxhb = int(hb.max())
+    for f in frags:                              # overflow rows fill free slots (a conflict, not an error)
+        for s in range(16):
+            if f[s] is None and extra:
+                f[s] = extra.pop()
+    assert not extra, "row table overflow"
+    for f in frags:                              # dummies: a missing residue, inside the halo
+        for s in range(16):
+            if f[s] is None:
+                used = {x[0] % 16 for x in f if x is not None}
+                cand = [r for r in range(16) if r not in used and r <= maxhb]
+                f[s] = ((cand[0] if cand else 0), -1)
+    tab = np.asarray([x for f in frags for x in f], dtype=np.int32)
+    with _LOCK:
+        _ROWTAB[key] = tab
+    return tab
+
+
+def geometry(p: TilePlan, src_dims: tuple, out_dims: tuple, kdims: tuple, pads: tuple) -> list[int]:
+    N, ID, IH, IW, C = src_dims
+    OD, OH, OW = out_dims
+    KD, KH, KW = kdims
+    m = lambda v: int(np.int32(np.uint32(v)))    # noqa: E731 - unsigned magic as a signed int32
+    return [N, ID, IH, IW, C, OD, OH, OW, KD, KH, KW, pads[0], pads[1], pads[2], p.TD, p.TH, p.TW,
+            p.CS, p.HPpad, p.nks, p.nct, m(p.mHW), m(p.mHHW), p.BUF]
+
+
+def _dev_cached(cache: dict, device, make):
+    key = str(device)
+    t = cache.get(key)
+    if t is None:
+        t = make()
+        with _LOCK:
+            cache[key] = t
+    return t
+
+
+def zero_page(device) -> torch.Tensor:
+    return _dev_cached(_ZERO, device, lambda: torch.zeros(64, dtype=torch.bfloat16, device=device))
+
+
+def sched(device, stream: int) -> torch.Tensor:
+    key = (str(device), stream)
+    t = _SCHED.get(key)
+    if t is None:
+        t = torch.zeros(64, dtype=torch.int32, device=device)
+        with _LOCK:
+            _SCHED[key] = t
+    return t
+
+
+def rowtab_tensor(p: TilePlan, kdims: tuple, device) -> torch.Tensor:
+    key = ("dev", p, tuple(kdims), str(device))
+    t = _ROWTAB.get(key)
+    if t is None:
+        t = torch.from_numpy(row_table(p, kdims)).to(device)
+        with _LOCK:
+            _ROWTAB[key] = t
+    return t
+
+
+def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bool) -> torch.Tensor:
+    """Conv weight [K, taps, C] -> the kernel's fragment-ordered B stream (bf16)."""
+    Csrc = K if dgrad else C
+    nslice = Csrc // p.CS
+    out = torch.empty(nslice * p.nks * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
+    wf = w.detach().float().contiguous()
+    _native.kernels().tile_pack_w(wf.data_ptr(), out.data_ptr(), K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad),
+                                  _native.stream(wf))
+    return out
+
+
+def workers(p: TilePlan, geom: list, ncol: int) -> int:
+    return int(_native.kernels().conv_tile_workers(geom, ncol, p.NT))
+
+
+def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p: TilePlan, geom: list, kdims: tuple,
+        ncol: int, act: int) -> None:
+    st = _native.stream(src5)
+    rt = rowtab_tensor(p, kdims, src5.device)
+    _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), zero_page(src5.device).data_ptr(),
+                                _native.ptr(bias), out.data_ptr(), _native.ptr(stats), geom, ncol, act, p.MT, p.NT,
+                                sched(src5.device, st).data_ptr(), st,
+                                [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2])
+
+
+def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan):
+    """y = act(conv(x, w) + b) (+ BN statistics slab) for a stride-1 conv on the tile kernel."""
+    kd = (spec.KD, spec.KH, spec.KW)
+    geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
+                    (spec.pd, spec.ph, spec.pw))
+    wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=False)
+    y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
+    stats = None
+    if want_stats:
+        stats = torch.zeros(workers(p, geom, spec.K), 2, spec.K, dtype=torch.float32, device=x5.device)
+    run(x5, wpk, bias, y, stats, p, geom, kd, spec.K, act)
+    return y, stats
+
+
+def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan) -> torch.Tensor:
+    """dx = conv(dy, flip(W)^T) with leading pads K-1-p (stride 1) on the tile kernel."""
+    kd = (spec.KD, spec.KH, spec.KW)
+    geom = geometry(p, (spec.N, spec.OD, spec.OH, spec.OW, spec.K), (spec.D, spec.H, spec.W), kd,
+                    (spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw))
+    wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
+    dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
+    run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
+    return dx
+
+
+def fwd_plan(spec):
+    if not enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
+        return None
+    return plan(spec.N, (spec.OD, spec.OH, spec.OW), (spec.KD, spec.KH, spec.KW), spec.C, spec.K)
+
+
+def dgrad_plan(spec):
+    if not enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
+        return None
+    return plan(spec.N, (spec.D, spec.H, spec.W), (spec.KD, spec.KH, spec.KW), spec.K, spec.C)

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Per-layer conv kernel timing for FeatureNet-3D at the headline batch.
+
+For each stride-1 layer (conv2..conv4) times forward (BN-statistics epilogue)
+and dgrad on the big-tile kernel (``conv_tile.hip``) and on the previous halo
+kernel (``conv_halo.hip``), back to back on one stream (events around R
+launches), and prints us/call and model TFLOP/s.
+
+    python scripts/bench_conv_layers.py --batch 128 --reps 10
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from featurenet_amd.ops import conv as cv  # noqa: E402
+from featurenet_amd.ops import conv_tile as ct  # noqa: E402
+from featurenet_amd.ops.spec import ConvSpec  # noqa: E402
+
+LAYERS = [("conv2", 29, 32, 32, 5), ("conv3", 25, 32, 64, 4), ("conv4", 22, 64, 64, 3)]
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    rows = []
+    for name, S, C, K, k in LAYERS:
+        if args.only and name not in args.only.split(","):
+            continue
+        x = torch.randn(args.batch, S, S, S, C, device="cuda").to(torch.bfloat16)
+        spec = ConvSpec.make(x.shape, K, k, 1, "valid")
+        w = torch.randn(K, k, k, k, C, device="cuda") * 0.05
+        dy = torch.randn(spec.out_shape5, device="cuda").to(torch.bfloat16)
+        gf = spec.flops() / 1e9
+        pf, pd = ct.fwd_plan(spec), ct.dgrad_plan(spec)
+        res = {"layer": name, "gflop": round(gf, 1), "tile_fwd_plan": str(pf), "tile_dgrad_plan": str(pd)}
+        hf, hd = cv.halo_fwd_plan(spec), cv.halo_dgrad_plan(spec)
+        res["halo_fwd_us"] = timeit(lambda: cv.halo_conv_fwd(x, w, None, spec, 0, True, hf), args.reps)
+        res["tile_fwd_us"] = timeit(lambda: ct.conv_fwd(x, w, None, spec, 0, True, pf), args.reps)
+        res["halo_dgrad_us"] = timeit(lambda: cv.halo_conv_dgrad(dy, w, spec, hd), args.reps)
+        res["tile_dgrad_us"] = timeit(lambda: ct.conv_dgrad(dy, w, spec, pd), args.reps)
+        for kk in ("halo_fwd", "tile_fwd", "halo_dgrad", "tile_dgrad"):
+            res[kk + "_us"] = round(res[kk + "_us"], 1)
+            res[kk + "_tflops"] = round(gf / res[kk + "_us"] * 1e3, 1)
+        rows.append(res)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
