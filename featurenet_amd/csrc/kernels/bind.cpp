@@ -58,8 +58,8 @@ int fn_act_bwd(const void*, const void*, void*, long long, int, hipStream_t);
 int fn_dropout(const void*, void*, long long, float, unsigned, unsigned, hipStream_t);
 int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
-int fn_conv_tile(const void*, const void*, const void*, const void*, const float*, void*, float*, const int*, int, int,
-                 int, int, int*, hipStream_t);
+int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
+                 const int*, int, int, int, int, int*, hipStream_t);
 int fn_conv_tile_workers(const int*, int, int);
 int fn_tile_pack_w(const float*, void*, int, int, int, int, int, int, int, int, hipStream_t);
 }
@@ -124,16 +124,17 @@ static void check_halo(const std::vector<int>& g, const std::vector<long long>& 
   }
 }
 
-// tile geometry: halo geometry (17) | CS HPpad nks nct mHW mHHW BUF; ext = {src, wpk, out, rowtab rows}
+// tile geometry: halo geometry (17) | CS HPpad nks nct mHW mHHW BUF mTW mTH; ext = {src, wpk, out, rowtab rows}
 static void check_tile(const std::vector<int>& g, const std::vector<long long>& ext, int ncol, int MT,
                        const char* what) {
   if (g[4] <= 0 || ncol <= 0 || g[17] <= 0 || g[4] % g[17]) throw std::runtime_error(std::string(what) + ": bad slice");
   if (g[5] > g[1] + 2 * g[11] + g[8] || g[6] > g[2] + 2 * g[12] + g[9] || g[7] > g[3] + 2 * g[13] + g[10])
     throw std::runtime_error(std::string(what) + ": output larger than the padded input");
   fits(ext, 0, prod({g[0], g[1], g[2], g[3], g[4]}), what, "src");
-  fits(ext, 1, prod({g[4] / g[17], g[19], g[20], 64, 8}), what, "wpk");
+  fits(ext, 1, prod({g[4] / g[17] * g[19] + 4, g[20], 64, 8}), what, "wpk");   // + 4 zero ring k-steps
   fits(ext, 2, prod({g[0], g[5], g[6], g[7], ncol}), what, "out");
   fits(ext, 3, 4LL * MT * 16, what, "rowtab");
+  fits(ext, 4, g[19] + 6LL, what, "ktab");
 }
 
 PYBIND11_MODULE(_C, m) {
@@ -168,20 +169,20 @@ PYBIND11_MODULE(_C, m) {
         "conv_halo_wgrad");
   }, py::arg("dy"), py::arg("src"), py::arg("dw"), py::arg("geom"), py::arg("cout"), py::arg("grid_x"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>());
-  m.def("conv_tile", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t zp, uintptr_t bias, uintptr_t out,
-                        uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT, uintptr_t sched,
-                        uintptr_t st, std::vector<long long> ext) {
-    need(geom, 24, "conv_tile");
+  m.def("conv_tile", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
+                        uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
+                        uintptr_t sched, uintptr_t st, std::vector<long long> ext) {
+    need(geom, 26, "conv_tile");
     check_tile(geom, ext, ncol, MT, "conv_tile");
-    chk(fn_conv_tile(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(zp),
-                     P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol, act, MT, NT,
-                     P<int*>(sched), S(st)),
+    chk(fn_conv_tile(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
+                     P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
+                     act, MT, NT, P<int*>(sched), S(st)),
         "conv_tile");
-  }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
+  }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>());
   m.def("conv_tile_workers", [](std::vector<int> geom, int ncol, int NT) {
-    need(geom, 24, "conv_tile_workers");
+    need(geom, 26, "conv_tile_workers");
     return fn_conv_tile_workers(geom.data(), ncol, NT);
   });
   m.def("tile_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int CS, int nks, int nct, int nslice,

@@ -47,6 +47,7 @@ struct TileGeom {
   int nct;                  // 16-column tiles of the packed weights (ceil(Ncol / 16))
   unsigned mHW, mHHW;       // magic multipliers: p / HW == umulhi(p, mHW) (host-verified)
   int BUF;                  // bytes per LDS buffer (halo or epilogue staging), multiple of 16
+  unsigned mTW, mTH;        // magic multipliers for the epilogue's tile-row decode
 };
 
 __device__ __forceinline__ void tile_lds_barrier() {
@@ -55,12 +56,11 @@ __device__ __forceinline__ void tile_lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-#define CT_NTHR 256
+#define CT_NCW 4                       // compute (MFMA) waves
+#define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
 
-// LDS-DMA of one 16-B chunk per lane into lds_dst + 16 * lane (lds_dst wave-uniform).
-// Inline asm (M0 saved/restored in the same statement), so hipcc does not count it:
-// its waitcnt pass drains vmcnt(0) at every use of an ordinary load while a counted
-// LDS-DMA is in flight.  The kernel waits for these with explicit vmcnt counts.
+// LDS-DMA of one 16-B chunk per lane into lds_dst + 16 * lane (lds_dst wave-uniform);
+// M0 saved/restored in the same statement (it is compiler-reserved)
 __device__ __forceinline__ void ct_glds16(const void* gsrc, unsigned lds_dst) {
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -69,9 +69,19 @@ __device__ __forceinline__ void ct_glds16(const void* gsrc, unsigned lds_dst) {
                : "memory");
 }
 
-// 16-B global load into a B fragment, hidden from hipcc's waitcnt bookkeeping (see
-// ct_glds16): uniform base in SGPRs + per-lane byte offset; completion is waited by
-// ct_wait_b with an explicit count
+// the same with an SGPR base + per-lane 32-bit byte offset (no 64-bit address math)
+__device__ __forceinline__ void ct_glds16_s(const void* sbase, unsigned voff, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_dst)
+               : "memory");
+}
+
+// 16-B global load into a B fragment: SGPR base + per-lane VGPR offset + immediate, no
+// address arithmetic in the k-loop.  Inline asm: hidden from hipcc's waitcnt pass, the
+// ring is waited by ct_wait_b with an exact count (the compute waves issue no other VMEM
+// in the k-loop)
 template <int IMM>
 __device__ __forceinline__ void ct_gload16(bf16x8& dst, const void* sbase, unsigned voff) {
   asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(dst) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
@@ -81,102 +91,109 @@ __device__ __forceinline__ unsigned ct_lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-template <int MT, int NT, int CPP>
+// Persistent workgroup: 4 compute waves (one per SIMD, 16*MT rows x NT*16 columns each)
+// + 1 loader wave.  Per job (tile, channel slice):
+//   barrier A: this job's halo has landed in buffer `cur` (the loader waited for it),
+//              the other buffer is free;
+//   loader:    reads the next job from its grab queue, LDS-DMAs its halo into the other
+//              buffer, pre-grabs the tile after it, waits for all of it (vmcnt(0));
+//   compute:   B-ring prologue, k-loop (MFMA + A reads + B loads only), epilogue on the
+//              job that finishes a tile (all 5 waves: staging, stores, BN statistics).
+template <int MT, int NT, int CPP, int DBG = 0>
 __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
+                                                               const int2* __restrict__ ktab,
                                                                const bf16* __restrict__ zp,
                                                                const float* __restrict__ bias, bf16* __restrict__ out,
                                                                float* __restrict__ stats, TileGeom g, int Ncol,
-                                                               int act, int* __restrict__ sched) {
+                                                               int act, int* __restrict__ sched, int flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int PD = NT == 2 ? 4 : 3;            // B prefetch depth (k-steps in flight)
   constexpr int LDO = NT * 16 + 8;               // epilogue staging row pitch (bf16)
   constexpr int CPR = NT * 2;                    // 16-B chunks per output row
+  constexpr int LCPP = CPP == 2 ? 1 : (CPP == 4 ? 2 : 3);
 
-  const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1, HD = g.TD + g.KD - 1;
-  const int HP = HD * HH * HW;
+  const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
+  const int HP = (g.TD + g.KD - 1) * HH * HW;
   const int PLANE = g.HPpad * 16;                // bytes per 16-B chunk plane
   const int rows = g.TD * g.TH * g.TW;
   const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH, twn = (g.OW + g.TW - 1) / g.TW;
   const int ntiles = g.N * tdn * thn * twn;
   const int nslice = g.C / g.CS;
   const int nks = g.nks;
-  const int T = g.KD * g.KH * g.KW;
-  const int prow = g.HPpad / 64;                 // DMA rows (64 positions) per chunk plane
-  const int NQ = CPP * prow;                     // DMA wave-instructions per job halo
+  const int NQ = CPP * g.HPpad / 64;             // DMA wave-instructions per job halo
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool loader = wave == CT_NCW;
   const int lr = lane & 15, lg = lane >> 4;
   const int ct0 = blockIdx.y * NT;               // first 16-column tile of this workgroup
-  // LDS: [halo / staging buffer 0][buffer 1][grab slot, 64 B][1 KB DMA scratch row][row map]
-  int* s_grab = reinterpret_cast<int*>(dsm + 2 * g.BUF);
-  int* s_orow = reinterpret_cast<int*>(dsm + 2 * g.BUF + 64 + 1024);   // natural tile row of every MFMA row
+  // LDS: [buffer 0][buffer 1][job slots 64 B][row map 4*MT*16 ints][k-step offsets (nks+PD+2)
+  // int2][halo positions HPpad int2: (byte offset from the halo origin, packed hd|hh|hw)]
+  int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);                    // [2][2] (tile, slice) by parity
+  int* s_orow = reinterpret_cast<int*>(dsm + 2 * g.BUF + 64);
+  int2* s_kt = reinterpret_cast<int2*>(dsm + 2 * g.BUF + 64 + 4 * 64 * MT * 4);
+  int2* s_pos = s_kt + (nks + PD + 2);
   for (int i = tid; i < 4 * MT * 16; i += CT_NTHR) s_orow[i] = rowtab[i].y;
+  for (int i = tid; i < nks + PD + 2; i += CT_NTHR) s_kt[i] = ktab[i];
+  for (int p = tid; p < g.HPpad; p += CT_NTHR) {  // positions past HP repeat the last one
+    const int pc = p < HP ? p : HP - 1;
+    const int hd = pc / (HH * HW), hh = (pc / HW) % HH, hw = pc % HW;
+    s_pos[p] = make_int2(((hd * g.IH + hh) * g.IW + hw) * g.C * 2, (hd << 16) | (hh << 8) | hw);
+  }
   float bcol[NT];                                // bias of this lane's epilogue columns
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
-    const int gcol = (blockIdx.y * NT + nt) * 16 + (threadIdx.x & 15);
+    const int gcol = (ct0 + nt) * 16 + lr;
     bcol[nt] = (bias && gcol < Ncol) ? bias[gcol] : 0.f;
   }
-
-  // ---- per-lane constants -------------------------------------------------
-  int lbase[MT];                                 // LDS byte offset of the row's tap-(0,0,0) chunk
-#pragma unroll
+  int lb[MT];                                    // LDS byte offset of the row's tap-(0,0,0) chunk in
+#pragma unroll                                   // the current job's buffer (toggled per job)
   for (int mt = 0; mt < MT; ++mt) {
-    const int2 rt = rowtab[(wave * MT + mt) * 16 + lr];
-    lbase[mt] = rt.x * 16 + (CPP >= 4 ? lg : (lg & 1)) * PLANE;
+    const int2 rt = rowtab[((loader ? 0 : wave) * MT + mt) * 16 + lr];
+    lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (lg & 1)) * PLANE;
   }
 
-  // ---- tile schedule (dynamic, one tile per grab; see conv_halo.hip) ------
-  auto grab = [&]() -> int {
-    if (tid == 0) *s_grab = atomicAdd(sched + 1 + blockIdx.y, 1);
-    tile_lds_barrier();
-    const int t = __builtin_amdgcn_readfirstlane(*s_grab);
-    tile_lds_barrier();
-    return t < ntiles ? t : -1;
-  };
-
-  // ---- halo DMA ---------------------------------------------------------------
-  struct Org { const bf16* base; int dlo, hlo, wlo; };
-  auto job_org = [&](int tile, int slice) -> Org {
+  // ---- loader: job decode and halo DMA --------------------------------------
+  // Halo of job (tile, slice) into the buffer at bufoff.  Interior halos (the common
+  // case for unpadded convs) use SGPR base + the per-position byte offsets of s_pos: no
+  // address math per DMA row; halos crossing the input boundary check every position
+  // and read the zero page outside.
+  auto dma_job = [&](int tile, int slice, int bufoff) {
     int t = tile;
     const int tw = t % twn; t /= twn;
     const int th = t % thn; t /= thn;
     const int td = t % tdn;
     const int n = t / tdn;
-    Org o;
-    o.dlo = td * g.TD - g.pd;
-    o.hlo = th * g.TH - g.ph;
-    o.wlo = tw * g.TW - g.pw;
-    o.base = src + (long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS;
-    return o;
-  };
-  // DMA row q of a job halo (wave-uniform): chunk plane c = q / prow, positions
-  // p0 .. p0+63; lane l moves position p0 + l (zero page outside the input).  Rows
-  // q >= NQ are dummies (zero page -> the scratch row past both buffers) so that every
-  // k-step issues exactly one DMA and the explicit vmcnt counts stay constant.
-  const unsigned lds_base = ct_lds_addr(dsm);
-  auto dma_row = [&](const Org& o, int bufoff, int q) {
-    const bool live = q < NQ;
-    const int qq = live ? q : 0;
-    const int c = qq / prow;
-    const int p0 = (qq - c * prow) * 64;
-    const int p = p0 + lane;
-    const int hd = (int)__umulhi((unsigned)p, g.mHHW);
-    const int rem = p - hd * HH * HW;
-    const int hh = (int)__umulhi((unsigned)rem, g.mHW);
-    const int hw = rem - hh * HW;
-    const int gd = o.dlo + hd, gh = o.hlo + hh, gw = o.wlo + hw;
-    const bool ok = live && p < HP && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-                    (unsigned)gw < (unsigned)g.IW;
-    const bf16* gsrc = ok ? o.base + ((gd * g.IH + gh) * g.IW + gw) * g.C + c * 8 : zp;
-    const unsigned dst = lds_base + (live ? (unsigned)(bufoff + c * PLANE + p0 * 16) : (unsigned)(2 * g.BUF + 64));
-    ct_glds16(gsrc, __builtin_amdgcn_readfirstlane(dst));
+    const int dlo = td * g.TD - g.pd, hlo = th * g.TH - g.ph, wlo = tw * g.TW - g.pw;
+    const bool interior = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID &&
+                          hlo + HH <= g.IH && wlo + HW <= g.IW;
+    const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS;
+    const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
+    if (interior) {
+      const bf16* obase = base + ((long long)dlo * g.IH + hlo) * g.IW * g.C + (long long)wlo * g.C;
+      for (int q = 0; q < NQ; ++q) {             // row q: plane c = q % CPP, positions (q / CPP)*64 ..
+        const int c = q & (CPP - 1);
+        const int r = q >> LCPP;
+        const int po = s_pos[(r << 6) + lane].x;
+        ct_glds16_s(obase, (unsigned)(po + c * 16), dst0 + (unsigned)(c * PLANE + (r << 10)));
+      }
+    } else {
+      for (int q = 0; q < NQ; ++q) {
+        const int c = q & (CPP - 1);
+        const int r = q >> LCPP;
+        const int2 e = s_pos[(r << 6) + lane];
+        const int gd = dlo + (e.y >> 16), gh = hlo + ((e.y >> 8) & 255), gw = wlo + (e.y & 255);
+        const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                        (unsigned)gw < (unsigned)g.IW;
+        const bf16* gsrc = ok ? base + ((gd * g.IH + gh) * g.IW + gw) * g.C + c * 8 : zp;
+        ct_glds16(gsrc, dst0 + (unsigned)(c * PLANE + (r << 10)));
+      }
+    }
   };
 
-  // ---- accumulators and operand registers ---------------------------------
+  // ---- compute: accumulators and operand registers ---------------------------
   f32x4 acc[MT][NT];
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -185,22 +202,19 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   bf16x8 fa[MT];                                 // rotating: fragment mt of k-step k+1 is read right
                                                  // after the NT MFMAs of (mt, k) consumed it
   bf16x8 fb[PD][NT];
-
-  const uint4* wjob = wp;                        // this job's first k-step (uniform)
-  const int wstride = g.nct * 64;                // uint4 per k-step
-  auto load_b = [&](int ks, int slot) {
-    const int k = ks < nks ? ks : nks - 1;       // past the end: a redundant (never used) load
-    const uint4* p = wjob + k * wstride;
-    ct_gload16<0>(fb[slot][0], p, lane * 16);
-    ct_gload16<1024>(fb[slot][1], p, lane * 16);
+  const unsigned wstep = (unsigned)g.nct * 1024u;   // bytes per k-step of the packed weights
+  unsigned voffb[PD];                            // per-lane B offsets of the PD ring slots
+#pragma unroll
+  for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * 16u + (unsigned)u * wstep;
+  auto load_b = [&](const unsigned char* base, int slot) {
+    ct_gload16<0>(fb[slot][0], base, voffb[slot]);
+    ct_gload16<1024>(fb[slot][1], base, voffb[slot]);
     if constexpr (NT == 4) {
-      ct_gload16<2048>(fb[slot][2], p, lane * 16);
-      ct_gload16<3072>(fb[slot][3], p, lane * 16);
+      ct_gload16<2048>(fb[slot][2], base, voffb[slot]);
+      ct_gload16<3072>(fb[slot][3], base, voffb[slot]);
     }
   };
-  // wait until ring slot `slot` has landed: per k-step the kernel issues NT B loads then
-  // one DMA row, so the loads younger than slot's are that DMA + (PD-1) whole k-steps
-  constexpr int VM_B = 1 + (PD - 1) * (NT + 1);
+  constexpr int VM_B = (PD - 1) * NT;            // B loads younger than a ring slot's
   auto wait_b = [&](int slot) {
     if constexpr (NT == 2) {
       asm volatile("s_waitcnt vmcnt(%2)" : "+v"(fb[slot][0]), "+v"(fb[slot][1]) : "n"(VM_B));
@@ -210,133 +224,140 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
                    : "n"(VM_B));
     }
   };
+  // k-step offsets: s_kt[k] = (lanes lg < 2, lanes lg >= 2) byte offsets of k-step k
+  const int khalf = (CPP >= 4 || lg < 2) ? 0 : 4;
+  auto kofs = [&](int k) -> int { return *(const int*)((const unsigned char*)(s_kt + k) + khalf); };
 
-  // scalar tap walker: LDS offset of the k-step for this lane, then advance one k-step
-  constexpr int SUB = CPP >= 4 ? CPP / 4 : 1;    // k-steps per tap (32 channels each)
-  struct Walk { int t, kw, kh, kd, sub; };
-  auto tap_next = [&](Walk& w) {                 // branch-free (selects), so the waitcnt pass
-    ++w.t;                                       // keeps exact counts across k-steps
-    const int kw1 = w.kw + 1;
-    const bool c1 = kw1 == g.KW;
-    w.kw = c1 ? 0 : kw1;
-    const int kh1 = w.kh + (c1 ? 1 : 0);
-    const bool c2 = kh1 == g.KH;
-    w.kh = c2 ? 0 : kh1;
-    w.kd += c2 ? 1 : 0;
-  };
-  auto tap_off = [&](const Walk& w) -> int {    // byte offset of the walker's tap (0 past the last tap)
-    return w.t < T ? ((w.kd * HH + w.kh) * HW + w.kw) * 16 : 0;
-  };
-  auto kofs_next = [&](Walk& w) -> int {
-    int ko;
-    if constexpr (CPP >= 4) {
-      ko = tap_off(w) + w.sub * 4 * PLANE;
-      if constexpr (SUB == 1) {
-        tap_next(w);
-      } else {
-        const int s1 = w.sub + 1;
-        if (s1 == SUB) { w.sub = 0; tap_next(w); } else { w.sub = s1; }
-      }
-    } else {                                     // CS = 16: lanes lg < 2 tap 2ks, lg >= 2 tap 2ks+1
-      const int lo = tap_off(w);
-      tap_next(w);
-      const int hi = tap_off(w);
-      tap_next(w);
-      ko = lg < 2 ? lo : hi;
-    }
-    return ko;
-  };
-  Walk walk;
-  int bufoff = 0;
-  // MFMAs of the current k-step from ring slot `slot`; fragment mt of the next k-step
-  // is read right after its own NT MFMAs.  sched_barrier pins that order: left
-  // alone, hipcc sinks every read to just before its MFMA (exposing the LDS latency)
-  // and every ring refill to the end of the turn (exposing the L2 latency).
-  auto kstep = [&](int slot) {
-    const int ko = kofs_next(walk) + bufoff;
-    wait_b(slot);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[slot][nt], acc[mt][nt], 0, 0, 0);
-      fa[mt] = *(const bf16x8*)(dsm + lbase[mt] + ko);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  int tile = grab();
+  // ---- schedule: first tile (all waves), loader pre-grabs the next one ---------
+  if (tid == 0) {
+    s_job[0] = atomicAdd(sched + 1 + blockIdx.y, 1);
+    s_job[1] = 0;
+  }
+  tile_lds_barrier();
+  int tile = __builtin_amdgcn_readfirstlane(s_job[0]);
+  if (tile >= ntiles) tile = -1;
   int slice = 0;
-  if (tile >= 0) {
-    const Org o = job_org(tile, 0);
-    for (int q = wave; q < NQ; q += 4) dma_row(o, 0, q);
+  int t_next = -1;                               // loader: tile after the current one
+  if (loader) {
+    if (tile >= 0) dma_job(tile, 0, 0);
+    if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
+    t_next = __builtin_amdgcn_readfirstlane(t_next);
+    if (t_next >= ntiles) t_next = -1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  int par = 0, bufoff = 0;
+  // B ring: the first job's k-steps 0..PD-1; every later job's come from the previous
+  // job's last turn, so no job starts on an exposed L2 latency
+  if (!loader && tile >= 0) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024, u);
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      if constexpr (NT == 2) {
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(fb[u][0]), "+v"(fb[u][1]));
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(fb[u][0]), "+v"(fb[u][1]), "+v"(fb[u][2]), "+v"(fb[u][3]));
+      }
+    }
   }
   while (tile >= 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA rows of the job halo
-    tile_lds_barrier();                                 // ... and everyone's; previous buffer free
-    // next job: next slice of this tile, or a new tile
+    tile_lds_barrier();                          // A: job halo landed; other buffer free
+    // next job (every wave computes it; only the loader grabs ahead)
     int ntile = tile, nslc = slice + 1;
     if (nslc == nslice) {
       nslc = 0;
-      ntile = grab();
+      ntile = loader ? t_next : 0;
+      if (loader && lane == 0) s_job[2 * (par ^ 1)] = ntile;   // published for the other waves
     }
-    const Org no = job_org(ntile >= 0 ? ntile : 0, nslc);
-    const int nq = ntile >= 0 ? NQ : 0;          // live DMA rows of the next job's halo
     const int nbuf = bufoff ^ g.BUF;
-    wjob = wp + ((size_t)slice * nks * g.nct + ct0) * 64;
-    int q = nq > 0 ? wave : NQ;                  // next DMA row of this wave (NQ.. = dummies)
-    // ring prologue: each load followed by one DMA row, the pattern of every k-step, so
-    // wait_b's constant count holds from the first k-step on
+    if (loader) {
+      if (!(DBG & 4) && ntile >= 0) dma_job(ntile, nslc, nbuf);
+      if (nslc == 0 && ntile >= 0) {
+        if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
+        t_next = __builtin_amdgcn_readfirstlane(t_next);
+        if (t_next >= ntiles) t_next = -1;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      // ---- k-loop: MFMA + A reads + B loads, nothing else ----
+      const unsigned char* wbase = reinterpret_cast<const unsigned char*>(wp) +
+                                   ((size_t)slice * nks * g.nct + ct0) * 1024 + PD * wstep;
+      // weights of the next job: its slice (slice 0 for a new tile, whatever the tile)
+      const unsigned char* wnext =
+          reinterpret_cast<const unsigned char*>(wp) + ((size_t)nslc * nks * g.nct + ct0) * 1024;
+      if (flags & 1) {                           // debug: per-job ring prologue
 #pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      load_b(u, u);
-      dma_row(no, nbuf, q);
-      q += 4;
-    }
-    walk.t = walk.kw = walk.kh = walk.kd = walk.sub = 0;
-    {
-      const int ko = kofs_next(walk) + bufoff;
+        for (int u = 0; u < PD; ++u) load_b(wbase - PD * wstep, u);
+      }
+      {
+        const int ko = kofs(0);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) fa[mt] = *(const bf16x8*)(dsm + lbase[mt] + ko);
-    }
-    for (int ks = 0; ks < nks; ks += PD) {
+        for (int mt = 0; mt < MT; ++mt) fa[mt] = *(const bf16x8*)(dsm + lb[mt] + ko);
+      }
+      int ko_n = kofs(1);                        // offsets of the next k-step
+      for (int ks = 0; ks < nks; ks += PD) {
+        const unsigned char* wl = (ks + PD >= nks && !(flags & 1)) ? wnext : wbase;   // last turn: next job's steps
+#pragma unroll
+        for (int u = 0; u < PD; ++u) {
+          const int ko = ko_n;
+          ko_n = kofs(ks + u + 2);
+          wait_b(u);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[u][nt], acc[mt][nt], 0, 0, 0);
+            if constexpr (!(DBG & 2)) fa[mt] = *(const bf16x8*)(dsm + lb[mt] + ko);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if constexpr (!(DBG & 1)) load_b(wl, u);   // k-step ks+u+PD, or the next job's step u
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        wbase += PD * wstep;
+      }
+      // the next job's ring loads land before the loop back-edge / the epilogue: hipcc
+      // treats asm-loaded registers as written at issue and may copy them there
 #pragma unroll
       for (int u = 0; u < PD; ++u) {
-        kstep(u);
-        load_b(ks + u + PD, u);
-        dma_row(no, nbuf, q);
-        q += 4;
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (NT == 2) {
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(fb[u][0]), "+v"(fb[u][1]));
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(fb[u][0]), "+v"(fb[u][1]), "+v"(fb[u][2]), "+v"(fb[u][3]));
+        }
       }
     }
-    for (; q < nq; q += 4) dma_row(no, nbuf, q);  // short jobs: the rest of the next halo
 
     if (slice == nslice - 1) {
-      // ---- epilogue: acc -> (bias) -> bf16 staging -> act -> 16-B stores (+BN stats) ----
+      // ---- epilogue (all waves): acc -> (bias) -> bf16 staging -> act -> stores (+BN stats) ----
       int t = tile;
       const int tw_i = t % twn; t /= twn;
       const int th_i = t % thn; t /= thn;
       const int td_i = t % tdn;
       const int n = t / tdn;
       const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
-      tile_lds_barrier();                        // all waves are done reading this job's halo
+      tile_lds_barrier();                        // all compute waves are done reading this job's halo
       bf16* Os = reinterpret_cast<bf16*>(dsm + bufoff);
-      // dummy rows write row 64*MT, a scratch row past the tile
+      if (!loader) {
+        // dummy rows write row 64*MT, a scratch row past the tile
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int4 o4 = *(const int4*)(s_orow + (wave * MT + mt) * 16 + lg * 4);   // rows 4lg .. 4lg+3
-        const int orow[4] = {o4.x, o4.y, o4.z, o4.w};
+        for (int mt = 0; mt < MT; ++mt) {
+          const int4 o4 = *(const int4*)(s_orow + (wave * MT + mt) * 16 + lg * 4);   // rows 4lg .. 4lg+3
+          const int orow[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          const int col = nt * 16 + lr;
+          for (int nt = 0; nt < NT; ++nt) {
+            const int col = nt * 16 + lr;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int orr = orow[r] >= 0 ? orow[r] : 64 * MT;
-            Os[orr * LDO + col] = f2bf(acc[mt][nt][r] + bcol[nt]);
+            for (int r = 0; r < 4; ++r) {
+              const int orr = orow[r] >= 0 ? orow[r] : 64 * MT;
+              Os[orr * LDO + col] = f2bf(acc[mt][nt][r] + bcol[nt]);
+            }
           }
-          acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
         }
       }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
       tile_lds_barrier();
       const long long obase = (long long)n * g.OD * g.OH * g.OW;
       const int ch = tid % CPR;                  // fixed per thread (CT_NTHR % CPR == 0)
@@ -346,7 +367,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
       for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
       for (int idx = tid; idx < rows * CPR; idx += CT_NTHR) {
         const int r = idx / CPR;
-        const int tw = r % g.TW, th = (r / g.TW) % g.TH, td = r / (g.TW * g.TH);
+        const int q = (int)__umulhi((unsigned)r, g.mTW);
+        const int tw = r - q * g.TW;
+        const int td = (int)__umulhi((unsigned)q, g.mTH);
+        const int th = q - td * g.TH;
         if (d0 + td >= g.OD || h0 + th >= g.OH || w0 + tw >= g.OW) continue;
         const long long m = obase + ((long long)(d0 + td) * g.OH + h0 + th) * g.OW + w0 + tw;
         Pack8 v;
@@ -376,16 +400,16 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
         float* red = reinterpret_cast<float*>(dsm + bufoff);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          red[tid * 16 + j] = st_s[j];
-          red[tid * 16 + 8 + j] = st_q[j];
+          red[j * CT_NTHR + tid] = st_s[j];       // [16][threads]: conflict-free
+          red[(8 + j) * CT_NTHR + tid] = st_q[j];
         }
         tile_lds_barrier();
         if (tid < NT * 16) {
           const int c8 = tid / 8, j = tid % 8;   // column tid = c8 * 8 + j
           float s = 0.f, qq = 0.f;
           for (int u = c8; u < CT_NTHR; u += CPR) {
-            s += red[u * 16 + j];
-            qq += red[u * 16 + 8 + j];
+            s += red[j * CT_NTHR + u];
+            qq += red[(8 + j) * CT_NTHR + u];
           }
           const int gcol = ct0 * 16 + tid;
           if (gcol < Ncol) {
@@ -395,11 +419,19 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
         }
       }
     }
+    // advance: the loader published a new tile before this job's barriers
+    if (nslc == 0) {
+      ntile = __builtin_amdgcn_readfirstlane(s_job[2 * (par ^ 1)]);
+    }
     tile = ntile;
     slice = nslc;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) lb[mt] += nbuf - bufoff;
     bufoff = nbuf;
+    par ^= 1;
   }
 
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the last job's unused ring loads
   if (tid == 0) {                                // the last workgroup out resets the counters
     __threadfence();
     if (atomicAdd(sched, 1) == (int)(gridDim.x * gridDim.y) - 1) {
@@ -468,7 +500,7 @@ extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, in
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
-#define CT_GEOM_LEN 24
+#define CT_GEOM_LEN 26
 static TileGeom parse_tile(const int* v) {
   TileGeom g;
   g.N = v[0]; g.ID = v[1]; g.IH = v[2]; g.IW = v[3]; g.C = v[4];
@@ -478,6 +510,7 @@ static TileGeom parse_tile(const int* v) {
   g.TD = v[14]; g.TH = v[15]; g.TW = v[16];
   g.CS = v[17]; g.HPpad = v[18]; g.nks = v[19]; g.nct = v[20];
   g.mHW = (unsigned)v[21]; g.mHHW = (unsigned)v[22]; g.BUF = v[23];
+  g.mTW = (unsigned)v[24]; g.mTH = (unsigned)v[25];
   return g;
 }
 
@@ -497,26 +530,25 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
-template <int MT, int NT, int CPP>
+template <int MT, int NT, int CPP, int DBG = 0>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const bf16* s, const uint4* w, const int2* rt,
-                       const bf16* zp, const float* b, bf16* o, float* stats, const TileGeom& g, int Ncol, int act,
-                       int* sched) {
+                       const int2* kt, const bf16* zp, const float* b, bf16* o, float* stats, const TileGeom& g,
+                       int Ncol, int act, int* sched) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP>), grid, dim3(CT_NTHR), lds, st, s, w, rt, zp, b, o, stats, g,
-                     Ncol, act, sched);
+  static const int flags = [] { const char* e = getenv("FN_TILE_FLAGS"); return e ? atoi(e) : 0; }();
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG>), grid, dim3(CT_NTHR), lds, st, s, w, rt, kt, zp, b, o, stats,
+                     g, Ncol, act, sched, flags);
   return 0;
 }
 
 // instantiations (MT, NT, CPP) -- the Python planner only emits these
-#define CT_INSTANCES(X) \
-  X(8, 2, 2) X(9, 2, 2) X(10, 2, 2) X(8, 2, 4) X(9, 2, 4) X(10, 2, 4) \
-  X(8, 4, 2) X(9, 4, 2) X(10, 4, 2) X(8, 4, 4) X(9, 4, 4) X(10, 4, 4)
+#define CT_INSTANCES(X) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4)
 
 extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 #define CT_SUP(M, N, C) if (MT == M && NT == N && CPP == C) return 1;
@@ -525,25 +557,37 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
   return 0;
 }
 
+static size_t tile_lds_total(const TileGeom& g, int MT, int NT) {
+  const int PD = NT == 2 ? 4 : 3;
+  return 2 * (size_t)g.BUF + 64 + (size_t)4 * 64 * MT * 4 + (size_t)(g.nks + PD + 2) * 8 + (size_t)g.HPpad * 8;
+}
+
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
-// wp: packed weights (fn_tile_pack_w); rowtab: int2[4 * MT * 16] (halo position of the
-// row, natural tile row or -1); zp: >= 16 zero bytes; sched: int[64] zeroed counters
-// (left zero); stats: fp32 [workers][2][Ncol] zero-initialised, or null.
-extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* zp, const float* bias,
-                            void* out, float* stats, const int* geom, int Ncol, int act, int MT, int NT,
-                            int* sched, hipStream_t st) {
+// wp: packed weights (fn_tile_pack_w) with PD zero k-steps past the last slice; rowtab:
+// int2[4 * MT * 16] (halo position of the row, natural tile row or -1); ktab: int2[nks + PD
+// + 2] byte offsets of every k-step's taps (lane halves lg < 2 / lg >= 2; zero past nks);
+// zp: >= 16 zero bytes; sched: int[64] zeroed counters (left zero); stats: fp32
+// [workers][2][Ncol] zero-initialised, or null.
+extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
+                            const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
+                            int NT, int* sched, hipStream_t st) {
   const TileGeom g = parse_tile(geom);
-  if (g.CS != 16 && g.CS % 32 != 0) return -2;
+  if (g.CS != 16 && g.CS != 32 && g.CS != 64) return -2;
   const int CPP = g.CS / 8;
   if (!fn_conv_tile_supported(MT, NT, CPP)) return -2;
   if (g.C % g.CS || g.TD * g.TH * g.TW > 64 * MT || g.TD < 1 || g.TH < 1 || g.TW < 1) return -3;
   const long long HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const long long HP = (g.TD + g.KD - 1) * HH * HW;
   if (g.HPpad < HP || g.HPpad % 64) return -3;
+  if (g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;   // packed 8-bit hd/hh/hw
   const int PD = NT == 2 ? 4 : 3;
   const int T = g.KD * g.KH * g.KW;
   const int need_ks = g.CS >= 32 ? T * (g.CS / 32) : (T + 1) / 2;
   if (g.nks % PD || g.nks < need_ks || g.nct < (Ncol + 15) / 16) return -3;
+  for (long long r = 0; r < 64LL * MT; ++r) {    // epilogue row decode
+    const unsigned long long q = (r * (unsigned long long)g.mTW) >> 32;
+    if (q != (unsigned long long)(r / g.TW) || ((q * g.mTH) >> 32) != q / g.TH) return -3;
+  }
   // the magic divisors must be exact for every position the DMA rows touch
   for (long long p = 0; p < g.HPpad; p += 1) {
     const unsigned long long hd = ((unsigned long long)p * g.mHHW) >> 32;
@@ -553,16 +597,26 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   const size_t halo = (size_t)g.HPpad * CPP * 16;
   const size_t stage = (size_t)(64 * MT + 1) * (NT * 16 + 8) * 2;
   if ((size_t)g.BUF < halo || (size_t)g.BUF < stage || (size_t)g.BUF < (size_t)CT_NTHR * 64 || g.BUF % 16) return -3;
-  const size_t lds = 2 * (size_t)g.BUF + 64 + 1024 + 4 * 64 * MT * 4;
+  const size_t lds = tile_lds_total(g, MT, NT);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
-  if (!sched || !zp || ncb > 63 || ncb * NT > g.nct) return -6;
+  if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
+  static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();
+  if (dbg && MT == 8 && NT == 2 && CPP == 2) {   // experiment variants (timing only, wrong results)
+#define CT_DBG(D) if (dbg == D) rc = launch_tile<8, 2, 2, D>(grid, lds, st, (const bf16*)src, (const uint4*)wp, \
+      (const int2*)rowtab, (const int2*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, sched);
+    CT_DBG(1) CT_DBG(2) CT_DBG(4) CT_DBG(3) CT_DBG(7)
+#undef CT_DBG
+    if (rc) return rc;
+    FN_CHECK_LAUNCH();
+    return 0;
+  }
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
     rc = launch_tile<M, N, C>(grid, lds, st, (const bf16*)src, (const uint4*)wp, (const int2*)rowtab,            \
-                              (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, sched);
+                              (const int2*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, sched);
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;

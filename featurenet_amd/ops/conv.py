@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from . import conv_tile
 from . import reference as ref
 from .spec import ConvSpec, act_code
 
@@ -369,7 +370,12 @@ def halo_conv_dgrad(dy5, w, spec: ConvSpec, plan):
 # ---------------------------------------------------------------------------
 def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: ConvSpec, act: int,
                     want_stats: bool, w: torch.Tensor | None = None):
+    tplan = conv_tile.fwd_plan(spec) if w is not None else None
     plan = halo_fwd_plan(spec) if w is not None else None
+    if tplan is not None and (plan is None or conv_tile.choose(
+            "fwd", spec, lambda: conv_tile.conv_fwd(x5, w, bias, spec, act, want_stats, tplan),
+            lambda: halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan))):
+        return conv_tile.conv_fwd(x5, w, bias, spec, act, want_stats, tplan)
     if plan is not None:
         return halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan)
     K = _native.kernels()
@@ -388,7 +394,13 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
 
 
 def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    tplan = conv_tile.dgrad_plan(spec)
     plan = halo_dgrad_plan(spec)
+    if tplan is not None:
+        dy5 = dy5.contiguous()
+        if plan is None or conv_tile.choose("dgrad", spec, lambda: conv_tile.conv_dgrad(dy5, w, spec, tplan),
+                                            lambda: halo_conv_dgrad(dy5, w, spec, plan)):
+            return conv_tile.conv_dgrad(dy5, w, spec, tplan)
     if plan is not None:
         return halo_conv_dgrad(dy5.contiguous(), w, spec, plan)
     K = _native.kernels()
@@ -590,7 +602,7 @@ class ConvFn(torch.autograd.Function):
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
             x_saved = s2d_input(x5, f, spec2) if ctx.needs_input_grad[1] else x5
-        elif halo_fwd_plan(spec) is not None:
+        elif halo_fwd_plan(spec) is not None or conv_tile.fwd_plan(spec) is not None:
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats, w=w.detach())
         else:
             wmat, ldw = pack_weight_rows(w.detach(), spec)

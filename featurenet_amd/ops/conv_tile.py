@@ -31,8 +31,8 @@ import torch
 from .. import _native
 
 LDS_MAX = 160 * 1024
-NTHR = 256
-MT_CHOICES = (8, 9, 10)
+NTHR = 320          # 4 MFMA waves + 1 loader wave
+MT_CHOICES = (8, 9)
 _LOCK = threading.Lock()
 _PLANS: dict = {}
 _ROWTAB: dict = {}
@@ -101,10 +101,10 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
     T = KD * KH * KW
     if Ncol < 16 or Csrc % 16 or T < 2:
         return None
-    NT = 2 if Ncol <= 32 else 4
+    NT = 2                                       # 32-column blocks (register budget: 5 waves per CU)
     ncb = -(-Ncol // (NT * 16))
     nct = ncb * NT
-    PD = 4 if NT == 2 else 3
+    PD = 4
     workers = max(1, n_cus // ncb)
     cands = []
     for CS in (32, 16):
@@ -129,13 +129,13 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
                     halo = HPpad * CPP * 16
                     stage = (64 * MT + 1) * (NT * 16 + 8) * 2
                     BUF = -(-max(halo, stage, NTHR * 64) // 16) * 16
-                    lds = 2 * BUF + 64 + 1024 + 4 * 64 * MT * 4
+                    lds = 2 * BUF + 64 + 4 * 64 * MT * 4 + (nks + PD + 2) * 8 + HPpad * 8
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
                     jobs = tiles * nslice
                     mfma = nks * MT * NT * 16                  # cycles of MFMA issue per wave per job
-                    fixed = 1200 + (HPpad * CPP // 64) * 8      # barrier + DMA issue per job
+                    fixed = 1500                                # barrier + B-ring prologue per job
                     epi = 1500 + rows * NT * 2 // NTHR * 40 / nslice
                     per_job = mfma + fixed + epi
                     cost = math.ceil(jobs / workers) * per_job
@@ -204,7 +204,7 @@ def geometry(p: TilePlan, src_dims: tuple, out_dims: tuple, kdims: tuple, pads: 
     KD, KH, KW = kdims
     m = lambda v: int(np.int32(np.uint32(v)))    # noqa: E731 - unsigned magic as a signed int32
     return [N, ID, IH, IW, C, OD, OH, OW, KD, KH, KW, pads[0], pads[1], pads[2], p.TD, p.TH, p.TW,
-            p.CS, p.HPpad, p.nks, p.nct, m(p.mHW), m(p.mHHW), p.BUF]
+            p.CS, p.HPpad, p.nks, p.nct, m(p.mHW), m(p.mHHW), p.BUF, m(_magic(p.TW)), m(_magic(p.TH))]
 
 
 def _dev_cached(cache: dict, device, make):
@@ -241,11 +241,50 @@ def rowtab_tensor(p: TilePlan, kdims: tuple, device) -> torch.Tensor:
     return t
 
 
+PD = 4                                           # B-ring depth of the kernel (k-steps in flight)
+
+
+def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
+    """int32 [nks + PD + 2, 2]: LDS byte offsets of every k-step's taps within a halo buffer,
+    for the lane halves lg < 2 / lg >= 2 (equal unless CS = 16: two taps per k-step);
+    (0, 0) past the last tap (zero weights)."""
+    KD, KH, KW = kdims
+    HH, HW = p.TH + KH - 1, p.TW + KW - 1
+    T = KD * KH * KW
+    kd, kh, kw = np.meshgrid(np.arange(KD), np.arange(KH), np.arange(KW), indexing="ij")
+    toff = (((kd * HH + kh) * HW + kw) * 16).reshape(-1)
+    tab = np.zeros((p.nks + PD + 2, 2), dtype=np.int32)
+    plane = p.HPpad * 16
+    for k in range(p.nks):
+        if p.CS >= 32:
+            sub = p.CS // 32
+            t, s = divmod(k, sub)
+            if t < T:
+                tab[k] = toff[t] + s * 4 * plane
+        else:
+            for h in range(2):
+                t = 2 * k + h
+                if t < T:
+                    tab[k, h] = toff[t]
+    return tab
+
+
+def ktab_tensor(p: TilePlan, kdims: tuple, device) -> torch.Tensor:
+    key = ("ktab", p, tuple(kdims), str(device))
+    t = _ROWTAB.get(key)
+    if t is None:
+        t = torch.from_numpy(k_table(p, kdims)).to(device)
+        with _LOCK:
+            _ROWTAB[key] = t
+    return t
+
+
 def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bool) -> torch.Tensor:
-    """Conv weight [K, taps, C] -> the kernel's fragment-ordered B stream (bf16)."""
+    """Conv weight [K, taps, C] -> the kernel's fragment-ordered B stream (bf16), plus PD
+    zero k-steps that the ring's over-the-end loads read."""
     Csrc = K if dgrad else C
     nslice = Csrc // p.CS
-    out = torch.empty(nslice * p.nks * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
+    out = torch.zeros((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
     wf = w.detach().float().contiguous()
     _native.kernels().tile_pack_w(wf.data_ptr(), out.data_ptr(), K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad),
                                   _native.stream(wf))
@@ -260,10 +299,11 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
         ncol: int, act: int) -> None:
     st = _native.stream(src5)
     rt = rowtab_tensor(p, kdims, src5.device)
-    _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), zero_page(src5.device).data_ptr(),
-                                _native.ptr(bias), out.data_ptr(), _native.ptr(stats), geom, ncol, act, p.MT, p.NT,
-                                sched(src5.device, st).data_ptr(), st,
-                                [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2])
+    kt = ktab_tensor(p, kdims, src5.device)
+    _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
+                                zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
+                                _native.ptr(stats), geom, ncol, act, p.MT, p.NT, sched(src5.device, st).data_ptr(),
+                                st, [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 2])
 
 
 def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan):
@@ -301,3 +341,42 @@ def dgrad_plan(spec):
     if not enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
         return None
     return plan(spec.N, (spec.D, spec.H, spec.W), (spec.KD, spec.KH, spec.KW), spec.K, spec.C)
+
+
+# ---------------------------------------------------------------------------
+# kernel selection: the big-tile kernel vs conv_halo, timed once per shape
+# ---------------------------------------------------------------------------
+_CHOICE: dict = {}
+
+
+def _time_ms(fn, reps: int = 3) -> float:
+    fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def choose(kind: str, spec, run_tile, run_other) -> bool:
+    """True when the tile kernel should run ``kind`` ('fwd' / 'dgrad') of ``spec``.
+
+    ``FN_CONV_TILE`` = 1 (default) picks per shape by timing both kernels once (a few
+    launches on the current stream, outside any graph capture; the first call of a
+    shape during capture takes the tile kernel), 2 forces the tile kernel, 0 disables it."""
+    mode = os.environ.get("FN_CONV_TILE", "1")
+    if mode == "0":
+        return False
+    if mode == "2":
+        return True
+    key = (kind, spec)
+    c = _CHOICE.get(key)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return True
+        c = _time_ms(run_tile) <= _time_ms(run_other)
+        with _LOCK:
+            _CHOICE[key] = c
+    return c

@@ -19,7 +19,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from featurenet_amd.ops import conv as cv  # noqa: E402
+import importlib  # noqa: E402
+
+cv = importlib.import_module("featurenet_amd.ops.conv")   # the module (ops.conv is also a function name)
 from featurenet_amd.ops import conv_tile as ct  # noqa: E402
 from featurenet_amd.ops.spec import ConvSpec  # noqa: E402
 
