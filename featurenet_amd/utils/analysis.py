@@ -1,7 +1,10 @@
 """Result analysis: report/evolution plots (SVG) and cross-dataset correlation.
 
 Reference: ``plots/plotter.py`` (accuracy vs time/params, cumulative accuracy
-histogram, learning curves), ``plots/full_evolution_plotter.py`` (per-epoch
+histogram, learning curves, efficiency ``:104-117``, training-time summary
+``:120-124``, standard-vs-FeatureNet learning curves ``:128-169``, overfitting
+grid ``:174-199``, per-feature accuracy attribution / #features vs accuracy
+``:207-297``), ``plots/full_evolution_plotter.py`` (per-epoch
 accuracy x robustness Pareto scatter, robustness histogram with a linear fit)
 and ``correlation.py`` (Kendall tau / Pearson / Spearman between the MNIST and
 CIFAR accuracies of the same products, threshold counts).
@@ -146,6 +149,134 @@ def plot_evolution(session_dir: str | Path, out_dir: str | Path | None = None) -
             k, b = np.polyfit(centers, counts, 1)
             h.line(centers, k * centers + b, f"fit {k:.3g}x+{b:.3g}")
         paths.append(h.save(out / "robustness_hist.svg"))
+    return paths
+
+
+def efficiency(report_path: str | Path, out_path: str | Path, min_accuracy: float = 0.0) -> Path:
+    """Accuracy vs log(parameter count) (reference ``plots/plotter.py:104-117``)."""
+    rows = [r for r in read_report(report_path) if r["accuracy"] >= min_accuracy]
+    return (SvgChart("efficiency", "log(size)", "accuracy")
+            .scatter([math.log(max(r["params"], 1)) for r in rows], [r["accuracy"] for r in rows])
+            .save(out_path))
+
+
+def training_time(report_path: str | Path) -> dict:
+    """Sum / median / mean training time of a report (reference ``plots/plotter.py:120-124``)."""
+    t = np.asarray([r["time"] for r in read_report(report_path)], float)
+    if t.size == 0:
+        return {"n": 0, "sum": 0.0, "median": 0.0, "mean": 0.0}
+    return {"n": int(t.size), "sum": float(t.sum()), "median": float(np.median(t)), "mean": float(t.mean())}
+
+
+def _curves(rows, key):
+    return [np.asarray(r["history"].get(key, []), float) for r in rows if r["history"].get(key)]
+
+
+def _mean_curve(curves, n):
+    cs = [c[:n] for c in curves if len(c) >= 1]
+    if not cs:
+        return np.zeros(0)
+    m = min(n, min(len(c) for c in cs))
+    return np.mean([c[:m] for c in cs], axis=0)
+
+
+def compare_accuracy(report_path: str | Path, out_path: str | Path, group: int = 10, epochs: int = 150,
+                     min_accuracy: float = 0.0) -> Path:
+    """Mean learning curves of two run groups: the first ``group`` report lines (the
+    hand-written "standard implementation") vs the next ``group`` (the FeatureNet-built
+    model); training and test accuracy of each (reference ``plots/plotter.py:128-169``,
+    which compares 10 hand-written LeNet-5 runs with 10 ``lenet5``-template runs)."""
+    rows = [r for r in read_report(report_path) if r["accuracy"] >= min_accuracy]
+    std, ours = rows[:group], rows[group:2 * group]
+    ch = SvgChart("standard vs FeatureNet implementation", "iteration", "accuracy")
+    for name, grp in (("standard", std), ("ours", ours)):
+        for key, lab in (("acc", "training"), ("val_acc", "test")):
+            y = _mean_curve(_curves(grp, key), epochs)
+            if y.size:
+                ch.line(np.arange(y.size), y, f"{name} {lab}")
+    return ch.save(out_path)
+
+
+def overfitting(report_path: str | Path, out_path: str | Path, min_accuracy: float = 0.0, cols: int = 3) -> Path:
+    """One panel per architecture: training vs test accuracy per iteration, titled with the
+    final accuracy and the parameter count (reference ``plots/plotter.py:174-199``)."""
+    rows = [r for r in read_report(report_path) if r["accuracy"] >= min_accuracy]
+    pw, ph = 320, 220
+    nrow = max(1, math.ceil(len(rows) / cols))
+    parts = [f'<svg xmlns="http://www.w3.org/2000/svg" width="{cols * pw}" height="{nrow * ph + 24}" '
+             f'font-family="sans-serif" font-size="10">',
+             f'<text x="{cols * pw / 2}" y="16" text-anchor="middle" font-size="12">'
+             f'<tspan fill="{PALETTE[0]}">training accuracy</tspan>  <tspan fill="{PALETTE[3]}">test accuracy'
+             f'</tspan></text>']
+    for i, r in enumerate(rows):
+        ch = SvgChart(f"architecture {r['index']} {r['accuracy'] * 100:.2f}% {r['params'] / 1e6:.2f}M",
+                      "iteration", "accuracy", w=pw, h=ph)
+        for key in ("acc", "val_acc"):
+            v = r["history"].get(key)
+            if v:
+                ch.scatter(np.arange(len(v)), v)
+        if not ch.series:
+            ch.scatter([0], [r["accuracy"]])
+        body = ch.svg().split("\n", 1)[1].rsplit("</svg>", 1)[0]
+        x, y = (i % cols) * pw, (i // cols) * ph + 24
+        parts.append(f'<g transform="translate({x},{y})">{body}</g>')
+    parts.append("</svg>")
+    p = Path(out_path)
+    p.write_text("\n".join(parts) + "\n")
+    return p
+
+
+def feature_attribution(report_path: str | Path, pdt_path: str | Path, top: int = 10) -> dict:
+    """Per-feature accuracy attribution (reference ``plots/plotter.py:207-297``): for every
+    feature enabled in some product, the average / max / min accuracy of the products that
+    enable it; leaf features (labels with more than 4 ``_``-separated parts) ranked by
+    average accuracy; and the enabled-feature count of every product."""
+    from ..fm.products import ProductSet
+
+    rows = read_report(report_path)
+    acc = {r["index"]: r["accuracy"] for r in rows}
+    ps = ProductSet(pdt_path)
+    per_feat: dict[int, list[float]] = {}
+    counts, accs = [], []
+    for i, prod in enumerate(ps.products):
+        a = acc.get(i, acc.get(i + 1))
+        if a is None:
+            continue
+        ids = ps.selected_ids(prod)
+        counts.append(len(ids))
+        accs.append(a)
+        for f in ids:
+            per_feat.setdefault(f, []).append(a)
+    stats = {ps.features[str(f)]: {"avg": float(np.mean(v)), "max": float(np.max(v)), "min": float(np.min(v)),
+                                   "n": len(v)} for f, v in per_feat.items() if str(f) in ps.features}
+    leaves = {k: v for k, v in stats.items() if len(k.split("_")) > 4}
+    ranked = sorted(leaves.items(), key=lambda kv: kv[1]["avg"])
+    return {"features": stats, "lowest": ranked[:top], "highest": ranked[::-1][:top],
+            "n_features_per_product": counts, "accuracy": accs}
+
+
+def plot_feature_attribution(report_path: str | Path, pdt_path: str | Path, out_dir: str | Path,
+                             top: int = 10) -> list[Path]:
+    """Bars of the lowest / highest average-accuracy leaf features (accuracy squared, as the
+    reference plots it), #enabled features vs accuracy, and max / average accuracy per leaf."""
+    res = feature_attribution(report_path, pdt_path, top)
+    out = Path(out_dir)
+    out.mkdir(parents=True, exist_ok=True)
+    paths = []
+    for name, items in (("lowest", res["lowest"]), ("highest", res["highest"])):
+        ch = SvgChart(f"features with {name} average accuracy", "rank", "accuracy^2")
+        if items:
+            ch.bars(np.arange(len(items) + 1), [v["avg"] ** 2 for _, v in items])
+        paths.append(ch.save(out / f"features_{name}.svg"))
+        (out / f"features_{name}.txt").write_text("".join(f"{k}\t{v['avg']:.4f}\t{v['n']}\n" for k, v in items))
+    paths.append(SvgChart("accuracy vs enabled features", "number of enabled features", "accuracy")
+                 .scatter(res["n_features_per_product"], res["accuracy"]).save(out / "features_count.svg"))
+    leaves = sorted((v for k, v in res["features"].items() if len(k.split("_")) > 4), key=lambda v: v["avg"])
+    ch = SvgChart("accuracy of the configurations of each leaf feature", "leaf feature", "accuracy")
+    if leaves:
+        ch.scatter(np.arange(len(leaves)), [v["max"] for v in leaves], "max")
+        ch.scatter(np.arange(len(leaves)), [v["avg"] for v in leaves], "average")
+    paths.append(ch.save(out / "features_leaves.svg"))
     return paths
 
 

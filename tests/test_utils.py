@@ -67,3 +67,44 @@ def test_graph_export(tmp_path):
     assert len(g["nodes"]) == len(net.prog) and g["params"] == net.nb_params
     assert open(p["dot"]).read().startswith("digraph")
     assert "params:" in summary(net)
+
+
+def _synthetic_report(path, n=20, epochs=12):
+    lines = []
+    for i in range(n):
+        h = "acc#" + "#".join(f"{0.1 + 0.03 * e:.3f}" for e in range(epochs)) + \
+            "|val_acc#" + "#".join(f"{0.1 + 0.02 * e + 0.001 * i:.3f}" for e in range(epochs))
+        lines.append(f"\r\n{i}: {0.3 + 0.01 * i:.3f} False {10 + i} {1000 * (i + 1)} 0 {h}")
+    path.write_text("".join(lines))
+    return path
+
+
+def test_efficiency_overfitting_and_comparison_plots(tmp_path):
+    rep = _synthetic_report(tmp_path / "report.txt")
+    assert analysis.training_time(rep) == {"n": 20, "sum": float(sum(range(10, 30))), "median": 19.5, "mean": 19.5}
+    for fn, name in ((analysis.efficiency, "eff.svg"), (analysis.compare_accuracy, "cmp.svg"),
+                     (analysis.overfitting, "over.svg")):
+        svg = fn(rep, tmp_path / name).read_text()
+        assert svg.startswith("<svg") and svg.rstrip().endswith("</svg>")
+    over = (tmp_path / "over.svg").read_text()
+    assert over.count("<g transform") == 20 and "architecture 19 49.00% 0.02M" in over
+    assert (tmp_path / "cmp.svg").read_text().count("<polyline") == 4      # 2 groups x (train, test)
+
+
+def test_feature_attribution_on_reference_products(tmp_path):
+    import pytest
+    from pathlib import Path
+
+    pdt = Path("/root/reference/datasets/10Products.pdt")
+    if not pdt.exists():
+        pytest.skip("reference product file not available")
+    rep = _synthetic_report(tmp_path / "report.txt", n=10)
+    res = analysis.feature_attribution(rep, pdt)
+    assert len(res["accuracy"]) == 10 and len(res["n_features_per_product"]) == 10
+    assert res["n_features_per_product"][0] == 1448                           # SURVEY 2.3 #30a
+    # a feature enabled in every product averages all ten accuracies
+    full = [v for v in res["features"].values() if v["n"] == 10]
+    assert full and all(abs(v["avg"] - np.mean(res["accuracy"])) < 1e-9 for v in full)
+    assert res["lowest"][0][1]["avg"] <= res["highest"][0][1]["avg"]
+    paths = analysis.plot_feature_attribution(rep, pdt, tmp_path / "feat")
+    assert len(paths) == 4 and all(p.exists() for p in paths)
