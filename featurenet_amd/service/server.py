@@ -67,7 +67,9 @@ def create_app(db_path: str = "samples.db", base_path: str = "products", devices
     """``max_workers`` caps concurrently running worker processes (each trains on the
     GPUs); ``cors_origins`` enables CORS for those origins only (default: same origin)."""
     from fastapi import FastAPI, Request
-    from fastapi.responses import FileResponse, HTMLResponse, JSONResponse
+    from fastapi.responses import FileResponse, HTMLResponse, JSONResponse, Response
+
+    from . import fm_builder
 
     store = TaskStore(db_path)
     app = FastAPI(title="featurenet_amd NAS service")
@@ -150,6 +152,22 @@ def create_app(db_path: str = "samples.db", base_path: str = "products", devices
         if spawn_workers:
             start_worker(task["task_id"])
         return task
+
+    @app.get("/fm/catalogue")
+    def fm_catalogue():
+        """Checkable cell-feature tree of the FM builder (reference ``ui/src/util.js``)."""
+        return fm_builder.catalogue()
+
+    @app.post("/fm/build")
+    async def fm_build(request: Request):
+        """SPLOT XML of the checked cell features (reference ``buildTree``, ``ui/src/pages/fm.js:112-118``)."""
+        body = await request.json()
+        checked = body.get("checked", []) if isinstance(body, dict) else []
+        if not isinstance(checked, list) or not all(isinstance(k, str) for k in checked):
+            return JSONResponse({"error": "checked must be a list of catalogue keys"}, status_code=400)
+        xml = fm_builder.build_fm(checked)
+        return Response(xml, media_type="application/xml",
+                        headers={"Content-Disposition": 'attachment; filename="fm.xml"'})
 
     @app.get("/", response_class=HTMLResponse)
     def index():

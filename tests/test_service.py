@@ -118,3 +118,55 @@ def test_server_binds_localhost_by_default():
     from featurenet_amd.service.server import serve
 
     assert inspect.signature(serve).parameters["host"].default == "127.0.0.1"
+
+
+def _catalogue_keys(node, out):
+    out.append(node)
+    for c in node.get("children", []):
+        _catalogue_keys(c, out)
+    return out
+
+
+def test_fm_builder_routes_produce_a_sampleable_feature_model(tmp_path):
+    """FM builder (reference ui/src/pages/fm.js + util.js buildTree): the checked cell
+    features become a SPLOT model that parses, extends to B x C and samples."""
+    from fastapi.testclient import TestClient
+
+    from featurenet_amd import _native
+    from featurenet_amd.fm import extend, splot
+    from featurenet_amd.service.server import create_app
+
+    app = create_app(str(tmp_path / "s.db"), str(tmp_path / "p"), spawn_workers=False)
+    c = TestClient(app)
+    cat = c.get("/fm/catalogue").json()
+    nodes = _catalogue_keys(cat[0], [])
+    keys = [n["key"] for n in nodes]
+    assert len(keys) == len(set(keys))                                   # unique keys (reference reuses some)
+    assert any(n["title"] == "Convolution" for n in nodes) and any(n["disabled"] for n in nodes)
+    sel = [n["key"] for n in nodes if not n["disabled"] and not any(
+        s in n["key"] for s in ("dense", "pooling", "recurrence", "flatten", "padding/fillsize"))]
+    r = c.post("/fm/build", json={"checked": sel})
+    assert r.status_code == 200 and r.headers["content-disposition"].endswith('fm.xml"')
+    fm = splot.loads(r.text)
+    names = set(fm.names())
+    assert "Block[k]_Element[i]_Cell_Input1_Convolution_kernel_3x3" in names
+    assert not any("Dense" in n for n in names)
+    assert "C7:~Architecture  or  ~Block[k]_Element[i]_Cell_Input1_Zeros" in r.text
+    src = tmp_path / "fm.xml"
+    src.write_text(r.text)
+    extend.generate_featuretree(src, tmp_path / "fm_2_2.xml", 2, 2)
+    big = splot.load(tmp_path / "fm_2_2.xml")
+    assert "Block2_Element2_Cell_Input2_Identity" in set(big.names())
+    if _native.runtime_available():
+        from featurenet_amd.fm.sampler import sample_products
+
+        res = sample_products(big, 4, duration_s=0.5, seed=0)
+        prods = res["products"]
+        assert len(prods) >= 1
+        for prod in prods:
+            chosen = {res["labels"][abs(v) - 1] for v in prod if v > 0}
+            assert big.is_valid(chosen)
+    # unchecking Zeros drops the constraint that names it
+    r2 = c.post("/fm/build", json={"checked": [k for k in sel if "zeros" not in k]})
+    assert "Input1_Zeros" not in r2.text
+    assert c.post("/fm/build", json={"checked": "cell"}).status_code == 400
