@@ -23,8 +23,9 @@
 //     the bank slot of a read is p mod 16, and the host permutes the tile rows
 //     (rowtab) so that the 16 rows of every MFMA fragment have 16 distinct halo
 //     positions mod 16: every ds_read_b128 lane group touches 16 distinct slots;
-//   * per-k-step LDS offsets come from a scalar tap walker, not a table (a
-//     scalar load shares lgkmcnt with the ds_reads and would drain them).
+//   * per-k-step tap offsets come from a small LDS table (a scalar-memory table
+//     would share lgkmcnt with the A reads and drain them; an SALU tap walker
+//     costs issue slots the single wave per SIMD cannot spare).
 //
 // MFMA: v_mfma_f32_16x16x32_bf16.  A = halo rows (lane: row lr, 8 k of group lg),
 // B = weights, k-step = 32 k = one tap x 32 channels (CS >= 32) or two taps x 16
@@ -76,15 +77,6 @@ __device__ __forceinline__ void ct_glds16_s(const void* sbase, unsigned voff, un
                : "=&s"(keep)
                : "v"(voff), "s"(sbase), "s"(lds_dst)
                : "memory");
-}
-
-// 16-B global load into a B fragment: SGPR base + per-lane VGPR offset + immediate, no
-// address arithmetic in the k-loop.  Inline asm: hidden from hipcc's waitcnt pass, the
-// ring is waited by ct_wait_b with an exact count (the compute waves issue no other VMEM
-// in the k-loop)
-template <int IMM>
-__device__ __forceinline__ void ct_gload16(bf16x8& dst, const void* sbase, unsigned voff) {
-  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(dst) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
 }
 
 __device__ __forceinline__ unsigned ct_lds_addr(const void* p) {
@@ -206,23 +198,12 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   unsigned voffb[PD];                            // per-lane B offsets of the PD ring slots
 #pragma unroll
   for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * 16u + (unsigned)u * wstep;
+  // B loads are ordinary loads: hipcc counts them (vmcnt waits before the consuming
+  // MFMAs, correct across its own register copies and spills); the compute waves issue no
+  // hidden VMEM, so its counts are exact
   auto load_b = [&](const unsigned char* base, int slot) {
-    ct_gload16<0>(fb[slot][0], base, voffb[slot]);
-    ct_gload16<1024>(fb[slot][1], base, voffb[slot]);
-    if constexpr (NT == 4) {
-      ct_gload16<2048>(fb[slot][2], base, voffb[slot]);
-      ct_gload16<3072>(fb[slot][3], base, voffb[slot]);
-    }
-  };
-  constexpr int VM_B = (PD - 1) * NT;            // B loads younger than a ring slot's
-  auto wait_b = [&](int slot) {
-    if constexpr (NT == 2) {
-      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(fb[slot][0]), "+v"(fb[slot][1]) : "n"(VM_B));
-    } else {
-      asm volatile("s_waitcnt vmcnt(%4)"
-                   : "+v"(fb[slot][0]), "+v"(fb[slot][1]), "+v"(fb[slot][2]), "+v"(fb[slot][3])
-                   : "n"(VM_B));
-    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const bf16x8*)(base + voffb[slot] + nt * 1024);
   };
   // k-step offsets: s_kt[k] = (lanes lg < 2, lanes lg >= 2) byte offsets of k-step k
   const int khalf = (CPP >= 4 || lg < 2) ? 0 : 4;
@@ -251,14 +232,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   if (!loader && tile >= 0) {
 #pragma unroll
     for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024, u);
-#pragma unroll
-    for (int u = 0; u < PD; ++u) {
-      if constexpr (NT == 2) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(fb[u][0]), "+v"(fb[u][1]));
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(fb[u][0]), "+v"(fb[u][1]), "+v"(fb[u][2]), "+v"(fb[u][3]));
-      }
-    }
   }
   while (tile >= 0) {
     tile_lds_barrier();                          // A: job halo landed; other buffer free
@@ -301,7 +274,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
         for (int u = 0; u < PD; ++u) {
           const int ko = ko_n;
           ko_n = kofs(ks + u + 2);
-          wait_b(u);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -314,16 +286,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
           __builtin_amdgcn_sched_barrier(0);
         }
         wbase += PD * wstep;
-      }
-      // the next job's ring loads land before the loop back-edge / the epilogue: hipcc
-      // treats asm-loaded registers as written at issue and may copy them there
-#pragma unroll
-      for (int u = 0; u < PD; ++u) {
-        if constexpr (NT == 2) {
-          asm volatile("s_waitcnt vmcnt(0)" : "+v"(fb[u][0]), "+v"(fb[u][1]));
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" : "+v"(fb[u][0]), "+v"(fb[u][1]), "+v"(fb[u][2]), "+v"(fb[u][3]));
-        }
       }
     }
 

@@ -107,8 +107,9 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
     PD = 4
     workers = max(1, n_cus // ncb)
     cands = []
+    cs_only = int(os.environ.get("FN_TILE_CS", "0"))
     for CS in (32, 16):
-        if Csrc % CS:
+        if Csrc % CS or (cs_only and CS != cs_only):
             continue
         CPP = CS // 8
         nslice = Csrc // CS
