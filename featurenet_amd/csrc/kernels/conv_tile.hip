@@ -356,22 +356,33 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
         }
       }
       if (stats) {
-        // per-tile column reduction in LDS, folded into this workgroup's slab row (it
-        // owns the row: plain read-modify-write; the caller zeroes the slab)
-        tile_lds_barrier();
-        float* red = reinterpret_cast<float*>(dsm + bufoff);
+        // per-tile column reduction: over the lanes of a wave that share the chunk (xor
+        // shuffles), then over the 5 waves in LDS; folded into this workgroup's slab row
+        // (it owns the row: plain read-modify-write; the caller zeroes the slab)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          red[j * CT_NTHR + tid] = st_s[j];       // [16][threads]: conflict-free
-          red[(8 + j) * CT_NTHR + tid] = st_q[j];
+        for (int off = CPR; off < 64; off <<= 1) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            st_s[j] += __shfl_xor(st_s[j], off);
+            st_q[j] += __shfl_xor(st_q[j], off);
+          }
+        }
+        tile_lds_barrier();                      // staging reads done: the buffer is free
+        float* red = reinterpret_cast<float*>(dsm + bufoff);   // [wave][2][NT*16]
+        if (lane < CPR) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            red[wave * 4 * NT * 16 + lane * 8 + j] = st_s[j];
+            red[wave * 4 * NT * 16 + 2 * NT * 16 + lane * 8 + j] = st_q[j];
+          }
         }
         tile_lds_barrier();
         if (tid < NT * 16) {
-          const int c8 = tid / 8, j = tid % 8;   // column tid = c8 * 8 + j
           float s = 0.f, qq = 0.f;
-          for (int u = c8; u < CT_NTHR; u += CPR) {
-            s += red[j * CT_NTHR + u];
-            qq += red[(8 + j) * CT_NTHR + u];
+#pragma unroll
+          for (int w = 0; w < CT_NCW + 1; ++w) {
+            s += red[w * 4 * NT * 16 + tid];
+            qq += red[w * 4 * NT * 16 + 2 * NT * 16 + tid];
           }
           const int gcol = ct0 * 16 + tid;
           if (gcol < Ncol) {

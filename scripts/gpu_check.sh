@@ -16,7 +16,7 @@ run() {
 }
 fatal() { [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; }
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  run pytest_gpu 900 python -m pytest ${TESTS:-tests} -q -m gpu -p no:cacheprovider; rc=$?
+  run pytest_gpu 900 python -u -m pytest ${TESTS:-tests} -x -v -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider; rc=$?
   if fatal $rc; then exit $rc; fi
 fi
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; if fatal $rc; then exit $rc; fi
