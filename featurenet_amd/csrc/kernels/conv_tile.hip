@@ -36,6 +36,9 @@
 // Dgrad uses the same kernel: dx = conv(dy, flip(W)^T) with leading pads K-1-p.
 #include "common.h"
 
+#include <cstdio>
+#include <vector>
+
 struct TileGeom {
   int N, ID, IH, IW, C;     // gathered source (x for fwd, dy for dgrad), channels-last
   int OD, OH, OW;           // output dims
@@ -59,6 +62,7 @@ __device__ __forceinline__ void tile_lds_barrier() {
 
 #define CT_NCW 4                       // compute (MFMA) waves
 #define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
+#define CT_RED_BYTES ((CT_NCW + 1) * 2 * 32 * 4)   // per-wave BN partial sums of 32 columns (NT = 2)
 
 // LDS-DMA of one 16-B chunk per lane into lds_dst + 16 * lane (lds_dst wave-uniform);
 // M0 saved/restored in the same statement (it is compiler-reserved)
@@ -77,6 +81,15 @@ __device__ __forceinline__ void ct_glds16_s(const void* sbase, unsigned voff, un
                : "=&s"(keep)
                : "v"(voff), "s"(sbase), "s"(lds_dst)
                : "memory");
+}
+
+// packed bf16 pairs (low half = element 0)
+__device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ unsigned bf16x2_pack(float lo, float hi) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t p = {f2bf(lo), f2bf(hi)};
+  return __builtin_bit_cast(unsigned, p);
 }
 
 __device__ __forceinline__ unsigned ct_lds_addr(const void* p) {
@@ -99,12 +112,14 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
                                                                const bf16* __restrict__ zp,
                                                                const float* __restrict__ bias, bf16* __restrict__ out,
                                                                float* __restrict__ stats, TileGeom g, int Ncol,
-                                                               int act, int* __restrict__ sched, int flags) {
+                                                               int act, int* __restrict__ sched,
+                                                               long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int PD = NT == 2 ? 4 : 3;            // B prefetch depth (k-steps in flight)
   constexpr int LDO = NT * 16 + 8;               // epilogue staging row pitch (bf16)
   constexpr int CPR = NT * 2;                    // 16-B chunks per output row
   constexpr int LCPP = CPP == 2 ? 1 : (CPP == 4 ? 2 : 3);
+  static_assert(NT * 16 <= 32, "s_red holds 32 columns per wave");
 
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int HP = (g.TD + g.KD - 1) * HH * HW;
@@ -121,11 +136,12 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   const bool loader = wave == CT_NCW;
   const int lr = lane & 15, lg = lane >> 4;
   const int ct0 = blockIdx.y * NT;               // first 16-column tile of this workgroup
-  // LDS: [buffer 0][buffer 1][job slots 64 B][row map 4*MT*16 ints][k-step offsets (nks+PD+2)
+  // LDS: [buffer 0][buffer 1][job slots 64 B][BN partials][row map 4*MT*16 ints][k-step offsets (nks+PD+2)
   // int2][halo positions HPpad int2: (byte offset from the halo origin, packed hd|hh|hw)]
   int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);                    // [2][2] (tile, slice) by parity
-  int* s_orow = reinterpret_cast<int*>(dsm + 2 * g.BUF + 64);
-  int2* s_kt = reinterpret_cast<int2*>(dsm + 2 * g.BUF + 64 + 4 * 64 * MT * 4);
+  float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);           // [5 waves][2][32] BN partials
+  int* s_orow = reinterpret_cast<int*>(dsm + 2 * g.BUF + 64 + CT_RED_BYTES);
+  int2* s_kt = reinterpret_cast<int2*>(dsm + 2 * g.BUF + 64 + CT_RED_BYTES + 4 * 64 * MT * 4);
   int2* s_pos = s_kt + (nks + PD + 2);
   for (int i = tid; i < 4 * MT * 16; i += CT_NTHR) s_orow[i] = rowtab[i].y;
   for (int i = tid; i < nks + PD + 2; i += CT_NTHR) s_kt[i] = ktab[i];
@@ -153,6 +169,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   // address math per DMA row; halos crossing the input boundary check every position
   // and read the zero page outside.
   auto dma_job = [&](int tile, int slice, int bufoff) {
+    tile = __builtin_amdgcn_readfirstlane(tile);   // (wave-uniform: the SGPR operands need proof)
+    slice = __builtin_amdgcn_readfirstlane(slice);
+    bufoff = __builtin_amdgcn_readfirstlane(bufoff);
     int t = tile;
     const int tw = t % twn; t /= twn;
     const int th = t % thn; t /= thn;
@@ -163,53 +182,128 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
                           hlo + HH <= g.IH && wlo + HW <= g.IW;
     const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS;
     const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
+    // position rows in batches of 8: the s_pos reads of a batch are in flight together
+    // (one LDS latency per batch, not per DMA row)
+    const int NR = g.HPpad >> 6;
     if (interior) {
       const bf16* obase = base + ((long long)dlo * g.IH + hlo) * g.IW * g.C + (long long)wlo * g.C;
-      for (int q = 0; q < NQ; ++q) {             // row q: plane c = q % CPP, positions (q / CPP)*64 ..
-        const int c = q & (CPP - 1);
-        const int r = q >> LCPP;
-        const int po = s_pos[(r << 6) + lane].x;
-        ct_glds16_s(obase, (unsigned)(po + c * 16), dst0 + (unsigned)(c * PLANE + (r << 10)));
+      for (int r0 = 0; r0 < NR; r0 += 8) {
+        int po[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) po[i] = s_pos[((r0 + i < NR ? r0 + i : NR - 1) << 6) + lane].x;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (r0 + i < NR) {
+#pragma unroll
+            for (int c = 0; c < CPP; ++c)
+              ct_glds16_s(obase, (unsigned)(po[i] + c * 16), dst0 + (unsigned)(c * PLANE + ((r0 + i) << 10)));
+          }
+        }
       }
     } else {
-      for (int q = 0; q < NQ; ++q) {
-        const int c = q & (CPP - 1);
-        const int r = q >> LCPP;
-        const int2 e = s_pos[(r << 6) + lane];
-        const int gd = dlo + (e.y >> 16), gh = hlo + ((e.y >> 8) & 255), gw = wlo + (e.y & 255);
-        const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-                        (unsigned)gw < (unsigned)g.IW;
-        const bf16* gsrc = ok ? base + ((gd * g.IH + gh) * g.IW + gw) * g.C + c * 8 : zp;
-        ct_glds16(gsrc, dst0 + (unsigned)(c * PLANE + (r << 10)));
+      for (int r0 = 0; r0 < NR; r0 += 8) {
+        int e[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = s_pos[((r0 + i < NR ? r0 + i : NR - 1) << 6) + lane].y;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (r0 + i < NR) {
+            const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
+            const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                            (unsigned)gw < (unsigned)g.IW;
+            const bf16* gsrc = ok ? base + ((gd * g.IH + gh) * g.IW + gw) * g.C : zp;
+#pragma unroll
+            for (int c = 0; c < CPP; ++c)
+              ct_glds16(ok ? gsrc + c * 8 : zp, dst0 + (unsigned)(c * PLANE + ((r0 + i) << 10)));
+          }
+        }
       }
     }
   };
 
-  // ---- compute: accumulators and operand registers ---------------------------
-  f32x4 acc[MT][NT];
+  // ---- tile end, shared by all 5 waves: stores of the staged tile (activation) and BN
+  // statistics (per-tile partial sums folded into wave 0's running column sums) --------
+  float cst_s = 0.f, cst_q = 0.f;                // BN sums of column tid (tid < 32): this workgroup's tiles
+  auto store_tile = [&](int tile_o, int boff) {
+    int t = tile_o;
+    const int tw_i = t % twn; t /= twn;
+    const int th_i = t % thn; t /= thn;
+    const int td_i = t % tdn;
+    const int n = t / tdn;
+    const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
+    const bf16* Os = reinterpret_cast<const bf16*>(dsm + boff);
+    const long long obase = (long long)n * g.OD * g.OH * g.OW;
+    const int ch = tid % CPR;                    // fixed per thread (CT_NTHR % CPR == 0)
+    const int gc = ct0 * 16 + ch * 8;
+    const bool vec = gc + 8 <= Ncol && (Ncol & 7) == 0;
+    float st_s[8], st_q[8];                      // this tile's BN partial sums of the thread's 8 columns
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+    for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
+#pragma unroll 2
+    for (int idx = tid; idx < rows * CPR; idx += CT_NTHR) {
+      const int r = idx / CPR;
+      const int q = (int)__umulhi((unsigned)r, g.mTW);
+      const int tw = r - q * g.TW;
+      const int td = (int)__umulhi((unsigned)q, g.mTH);
+      const int th = q - td * g.TH;
+      if (d0 + td < g.OD && h0 + th < g.OH && w0 + tw < g.OW) {
+        const long long m = obase + ((long long)(d0 + td) * g.OH + h0 + th) * g.OW + w0 + tw;
+        // 8 bf16 as 4 packed words end to end (a union with per-element writes made hipcc
+        // split the 16-B store into 2-byte ones)
+        const uint4 u = *(const uint4*)(Os + r * LDO + ch * 8);
+        unsigned w4[4] = {u.x, u.y, u.z, u.w};
+        if (act != ACT_NONE) {
 #pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[MT];                                 // rotating: fragment mt of k-step k+1 is read right
-                                                 // after the NT MFMAs of (mt, k) consumed it
-  bf16x8 fb[PD][NT];
-  const unsigned wstep = (unsigned)g.nct * 1024u;   // bytes per k-step of the packed weights
-  unsigned voffb[PD];                            // per-lane B offsets of the PD ring slots
+          for (int k = 0; k < 4; ++k) w4[k] = bf16x2_pack(act_fwd(bf16_lo(w4[k]), act), act_fwd(bf16_hi(w4[k]), act));
+        }
+        if (stats) {
 #pragma unroll
-  for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * 16u + (unsigned)u * wstep;
-  // B loads are ordinary loads: hipcc counts them (vmcnt waits before the consuming
-  // MFMAs, correct across its own register copies and spills); the compute waves issue no
-  // hidden VMEM, so its counts are exact
-  auto load_b = [&](const unsigned char* base, int slot) {
+          for (int k = 0; k < 4; ++k) {
+            const float lo = bf16_lo(w4[k]), hi = bf16_hi(w4[k]);
+            st_s[2 * k] += lo;
+            st_q[2 * k] += lo * lo;
+            st_s[2 * k + 1] += hi;
+            st_q[2 * k + 1] += hi * hi;
+          }
+        }
+        if (vec) {
+          *(uint4*)(out + m * Ncol + gc) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        } else {
+          for (int j = 0; j < 8; ++j)
+            if (gc + j < Ncol) out[m * Ncol + gc + j] = f2bf(j & 1 ? bf16_hi(w4[j >> 1]) : bf16_lo(w4[j >> 1]));
+        }
+      }
+    }
+    if (stats) {
+      // over the lanes of a wave that share the chunk (xor shuffles), then over the 5 waves
+      // in LDS; the next s_red write is a tile later, barriers apart
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const bf16x8*)(base + voffb[slot] + nt * 1024);
+      for (int off = CPR; off < 64; off <<= 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          st_s[j] += __shfl_xor(st_s[j], off);
+          st_q[j] += __shfl_xor(st_q[j], off);
+        }
+      }
+      if (lane < CPR) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s_red[wave * 64 + lane * 8 + j] = st_s[j];
+          s_red[wave * 64 + 32 + lane * 8 + j] = st_q[j];
+        }
+      }
+      tile_lds_barrier();
+      if (tid < NT * 16) {
+#pragma unroll
+        for (int w = 0; w < CT_NCW + 1; ++w) {
+          cst_s += s_red[w * 64 + tid];
+          cst_q += s_red[w * 64 + 32 + tid];
+        }
+      }
+    }
   };
-  // k-step offsets: s_kt[k] = (lanes lg < 2, lanes lg >= 2) byte offsets of k-step k
-  const int khalf = (CPP >= 4 || lg < 2) ? 0 : 4;
-  auto kofs = [&](int k) -> int { return *(const int*)((const unsigned char*)(s_kt + k) + khalf); };
 
-  // ---- schedule: first tile (all waves), loader pre-grabs the next one ---------
+  // ---- schedule: first tile (all waves) ---------------------------------------
   if (tid == 0) {
     s_job[0] = atomicAdd(sched + 1 + blockIdx.y, 1);
     s_job[1] = 0;
@@ -217,33 +311,41 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   tile_lds_barrier();
   int tile = __builtin_amdgcn_readfirstlane(s_job[0]);
   if (tile >= ntiles) tile = -1;
-  int slice = 0;
-  int t_next = -1;                               // loader: tile after the current one
+  // DBG & 16: cycle stamps of wave 0 and the loader (barrier-A wait, job work, tile end)
+  long long st_a = 0, st_k = 0, st_e[4] = {0, 0, 0, 0}, st_0 = 0, st_1 = 0;
+  auto stamp = [&]() -> long long { return (DBG & 16) ? (long long)__builtin_amdgcn_s_memtime() : 0; };
+  auto lap = [&](long long& acc_t) {
+    if constexpr ((DBG & 16) != 0) {
+      const long long t2 = stamp();
+      acc_t += t2 - st_1;
+      st_1 = t2;
+    }
+  };
+  st_0 = stamp();
+
+  // The loader and the compute waves run separate loops over the same job sequence with
+  // the same barriers (A per job; E, S (+R with statistics) per tile), so neither keeps
+  // the other's registers live.
   if (loader) {
+    // ======================= loader wave =======================
+    int t_next;
     if (tile >= 0) dma_job(tile, 0, 0);
     if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
     t_next = __builtin_amdgcn_readfirstlane(t_next);
     if (t_next >= ntiles) t_next = -1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  int par = 0, bufoff = 0;
-  // B ring: the first job's k-steps 0..PD-1; every later job's come from the previous
-  // job's last turn, so no job starts on an exposed L2 latency
-  if (!loader && tile >= 0) {
-#pragma unroll
-    for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024, u);
-  }
-  while (tile >= 0) {
-    tile_lds_barrier();                          // A: job halo landed; other buffer free
-    // next job (every wave computes it; only the loader grabs ahead)
-    int ntile = tile, nslc = slice + 1;
-    if (nslc == nslice) {
-      nslc = 0;
-      ntile = loader ? t_next : 0;
-      if (loader && lane == 0) s_job[2 * (par ^ 1)] = ntile;   // published for the other waves
-    }
-    const int nbuf = bufoff ^ g.BUF;
-    if (loader) {
+    int slice = 0, par = 0, bufoff = 0;
+    while (tile >= 0) {
+      st_1 = stamp();
+      tile_lds_barrier();                        // A: job halo landed; other buffer free
+      lap(st_a);
+      int ntile = tile, nslc = slice + 1;
+      if (nslc == nslice) {
+        nslc = 0;
+        ntile = t_next;
+        if (lane == 0) s_job[2 * (par ^ 1)] = ntile;   // published for the compute waves
+      }
+      const int nbuf = bufoff ^ g.BUF;
       if (!(DBG & 4) && ntile >= 0) dma_job(ntile, nslc, nbuf);
       if (nslc == 0 && ntile >= 0) {
         if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
@@ -251,17 +353,66 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
         if (t_next >= ntiles) t_next = -1;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
+      lap(st_k);
+      if (slice == nslice - 1) {
+        tile_lds_barrier();                      // E
+        lap(st_e[0]);
+        tile_lds_barrier();                      // S: staging written
+        lap(st_e[1]);
+        store_tile(tile, bufoff);
+        lap(st_e[2]);
+      }
+      tile = ntile;
+      slice = nslc;
+      bufoff = nbuf;
+      par ^= 1;
+    }
+  } else {
+    // ======================= compute waves =======================
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    bf16x8 fa[MT];                               // rotating: fragment mt of k-step k+1 is read right
+                                                 // after the NT MFMAs of (mt, k) consumed it
+    bf16x8 fb[PD][NT];
+    const unsigned wstep = (unsigned)g.nct * 1024u;   // bytes per k-step of the packed weights
+    unsigned voffb[PD];                          // per-lane B offsets of the PD ring slots
+#pragma unroll
+    for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * 16u + (unsigned)u * wstep;
+    // B loads are ordinary loads: hipcc counts them (vmcnt waits before the consuming
+    // MFMAs, correct across its own register copies and spills); the compute waves issue
+    // no hidden VMEM, so its counts are exact
+    auto load_b = [&](const unsigned char* base, int slot) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const bf16x8*)(base + voffb[slot] + nt * 1024);
+    };
+    // k-step offsets: s_kt[k] = (lanes lg < 2, lanes lg >= 2) byte offsets of k-step k (the
+    // two halves are equal for CS >= 32; reading them per lane-half anyway keeps the offset a
+    // per-lane value, and hipcc then keeps the A reads interleaved with the MFMAs -- with a
+    // wave-uniform offset it hoisted a turn's reads into a double-buffered block)
+    const int khalf = lg < 2 ? 0 : 4;
+    auto kofs = [&](int k) -> int { return *(const int*)((const unsigned char*)(s_kt + k) + khalf); };
+    // B ring: the first job's k-steps 0..PD-1; every later job's come from the previous
+    // job's last turn, so no job starts on an exposed L2 latency
+    if (tile >= 0) {
+#pragma unroll
+      for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024, u);
+    }
+    int slice = 0, par = 0, bufoff = 0;
+    while (tile >= 0) {
+      st_1 = stamp();
+      tile_lds_barrier();                        // A: job halo landed; other buffer free
+      lap(st_a);
+      const int nslc = slice + 1 == nslice ? 0 : slice + 1;
+      const int nbuf = bufoff ^ g.BUF;
       // ---- k-loop: MFMA + A reads + B loads, nothing else ----
       const unsigned char* wbase = reinterpret_cast<const unsigned char*>(wp) +
                                    ((size_t)slice * nks * g.nct + ct0) * 1024 + PD * wstep;
       // weights of the next job: its slice (slice 0 for a new tile, whatever the tile)
       const unsigned char* wnext =
           reinterpret_cast<const unsigned char*>(wp) + ((size_t)nslc * nks * g.nct + ct0) * 1024;
-      if (flags & 1) {                           // debug: per-job ring prologue
-#pragma unroll
-        for (int u = 0; u < PD; ++u) load_b(wbase - PD * wstep, u);
-      }
       {
         const int ko = kofs(0);
 #pragma unroll
@@ -269,7 +420,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
       }
       int ko_n = kofs(1);                        // offsets of the next k-step
       for (int ks = 0; ks < nks; ks += PD) {
-        const unsigned char* wl = (ks + PD >= nks && !(flags & 1)) ? wnext : wbase;   // last turn: next job's steps
+        const unsigned char* wl = ks + PD >= nks ? wnext : wbase;   // last turn: next job's steps
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
           const int ko = ko_n;
@@ -287,20 +438,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
         }
         wbase += PD * wstep;
       }
-    }
-
-    if (slice == nslice - 1) {
-      // ---- epilogue (all waves): acc -> (bias) -> bf16 staging -> act -> stores (+BN stats) ----
-      int t = tile;
-      const int tw_i = t % twn; t /= twn;
-      const int th_i = t % thn; t /= thn;
-      const int td_i = t % tdn;
-      const int n = t / tdn;
-      const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
-      tile_lds_barrier();                        // all compute waves are done reading this job's halo
-      bf16* Os = reinterpret_cast<bf16*>(dsm + bufoff);
-      if (!loader) {
-        // dummy rows write row 64*MT, a scratch row past the tile
+      lap(st_k);
+      int ntile = tile;
+      if (slice == nslice - 1) {
+        tile_lds_barrier();                      // E: every compute wave is done reading this halo
+        lap(st_e[0]);
+        bf16* Os = reinterpret_cast<bf16*>(dsm + bufoff);
+        // acc (+bias) -> bf16 staging in natural tile rows; dummy rows write row 64*MT
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int4 o4 = *(const int4*)(s_orow + (wave * MT + mt) * 16 + lg * 4);   // rows 4lg .. 4lg+3
@@ -313,98 +457,43 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
               const int orr = orow[r] >= 0 ? orow[r] : 64 * MT;
               Os[orr * LDO + col] = f2bf(acc[mt][nt][r] + bcol[nt]);
             }
+            acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
           }
         }
+        tile_lds_barrier();                      // S
+        lap(st_e[1]);
+        store_tile(tile, bufoff);
+        lap(st_e[2]);
+        // the loader published the next tile before barrier E
+        ntile = __builtin_amdgcn_readfirstlane(s_job[2 * (par ^ 1)]);
       }
+      tile = ntile;
+      slice = nslc;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      tile_lds_barrier();
-      const long long obase = (long long)n * g.OD * g.OH * g.OW;
-      const int ch = tid % CPR;                  // fixed per thread (CT_NTHR % CPR == 0)
-      const int gc = ct0 * 16 + ch * 8;
-      float st_s[8], st_q[8];                    // this tile's BN partial sums of the thread's 8 columns
-#pragma unroll
-      for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
-      for (int idx = tid; idx < rows * CPR; idx += CT_NTHR) {
-        const int r = idx / CPR;
-        const int q = (int)__umulhi((unsigned)r, g.mTW);
-        const int tw = r - q * g.TW;
-        const int td = (int)__umulhi((unsigned)q, g.mTH);
-        const int th = q - td * g.TH;
-        if (d0 + td >= g.OD || h0 + th >= g.OH || w0 + tw >= g.OW) continue;
-        const long long m = obase + ((long long)(d0 + td) * g.OH + h0 + th) * g.OW + w0 + tw;
-        Pack8 v;
-        v.u = *(const uint4*)(Os + r * LDO + ch * 8);
-        if (act != ACT_NONE) {
-          for (int j = 0; j < 8; ++j) v.e[j] = f2bf(act_fwd(bf2f(v.e[j]), act));
-        }
-        if (stats) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float f = bf2f(v.e[j]);
-            st_s[j] += f;
-            st_q[j] += f * f;
-          }
-        }
-        if (gc + 8 <= Ncol && (Ncol & 7) == 0) {
-          *(uint4*)(out + m * Ncol + gc) = v.u;
-        } else {
-          for (int j = 0; j < 8; ++j)
-            if (gc + j < Ncol) out[m * Ncol + gc + j] = v.e[j];
-        }
-      }
-      if (stats) {
-        // per-tile column reduction: over the lanes of a wave that share the chunk (xor
-        // shuffles), then over the 5 waves in LDS; folded into this workgroup's slab row
-        // (it owns the row: plain read-modify-write; the caller zeroes the slab)
-#pragma unroll
-        for (int off = CPR; off < 64; off <<= 1) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            st_s[j] += __shfl_xor(st_s[j], off);
-            st_q[j] += __shfl_xor(st_q[j], off);
-          }
-        }
-        tile_lds_barrier();                      // staging reads done: the buffer is free
-        float* red = reinterpret_cast<float*>(dsm + bufoff);   // [wave][2][NT*16]
-        if (lane < CPR) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            red[wave * 4 * NT * 16 + lane * 8 + j] = st_s[j];
-            red[wave * 4 * NT * 16 + 2 * NT * 16 + lane * 8 + j] = st_q[j];
-          }
-        }
-        tile_lds_barrier();
-        if (tid < NT * 16) {
-          float s = 0.f, qq = 0.f;
-#pragma unroll
-          for (int w = 0; w < CT_NCW + 1; ++w) {
-            s += red[w * 4 * NT * 16 + tid];
-            qq += red[w * 4 * NT * 16 + 2 * NT * 16 + tid];
-          }
-          const int gcol = ct0 * 16 + tid;
-          if (gcol < Ncol) {
-            stats[(long long)blockIdx.x * 2 * Ncol + gcol] += s;
-            stats[(long long)blockIdx.x * 2 * Ncol + Ncol + gcol] += qq;
-          }
-        }
-      }
+      for (int mt = 0; mt < MT; ++mt) lb[mt] += nbuf - bufoff;
+      bufoff = nbuf;
+      par ^= 1;
     }
-    // advance: the loader published a new tile before this job's barriers
-    if (nslc == 0) {
-      ntile = __builtin_amdgcn_readfirstlane(s_job[2 * (par ^ 1)]);
-    }
-    tile = ntile;
-    slice = nslc;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) lb[mt] += nbuf - bufoff;
-    bufoff = nbuf;
-    par ^= 1;
   }
 
+  if (stats && tid < NT * 16 && ct0 * 16 + tid < Ncol) {
+    float* row = stats + (long long)blockIdx.x * 2 * Ncol;
+    row[ct0 * 16 + tid] += cst_s;                // the caller zeroes the slab
+    row[Ncol + ct0 * 16 + tid] += cst_q;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the last job's unused ring loads
+  if constexpr ((DBG & 16) != 0) {
+    if (lane == 0 && (wave == 0 || loader)) {
+      long long* d = stamps + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 16 + (loader ? 8 : 0);
+      d[0] = st_a;
+      d[1] = st_k;
+      d[2] = st_e[0];
+      d[3] = st_e[1];
+      d[4] = st_e[2];
+      d[5] = st_e[3];
+      d[6] = stamp() - st_0;
+    }
+  }
   if (tid == 0) {                                // the last workgroup out resets the counters
     __threadfence();
     if (atomicAdd(sched, 1) == (int)(gridDim.x * gridDim.y) - 1) {
@@ -506,7 +595,7 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
 template <int MT, int NT, int CPP, int DBG = 0>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const bf16* s, const uint4* w, const int2* rt,
                        const int2* kt, const bf16* zp, const float* b, bf16* o, float* stats, const TileGeom& g,
-                       int Ncol, int act, int* sched) {
+                       int Ncol, int act, int* sched, long long* stamps = nullptr) {
   static size_t configured = 0;
   if (lds > configured) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG>,
@@ -514,9 +603,8 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const bf16* s, con
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  static const int flags = [] { const char* e = getenv("FN_TILE_FLAGS"); return e ? atoi(e) : 0; }();
   hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG>), grid, dim3(CT_NTHR), lds, st, s, w, rt, kt, zp, b, o, stats,
-                     g, Ncol, act, sched, flags);
+                     g, Ncol, act, sched, stamps);
   return 0;
 }
 
@@ -532,7 +620,7 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT) {
   const int PD = NT == 2 ? 4 : 3;
-  return 2 * (size_t)g.BUF + 64 + (size_t)4 * 64 * MT * 4 + (size_t)(g.nks + PD + 2) * 8 + (size_t)g.HPpad * 8;
+  return 2 * (size_t)g.BUF + 64 + CT_RED_BYTES + (size_t)4 * 64 * MT * 4 + (size_t)(g.nks + PD + 2) * 8 + (size_t)g.HPpad * 8;
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -577,13 +665,33 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();
-  if (dbg && MT == 8 && NT == 2 && CPP == 2) {   // experiment variants (timing only, wrong results)
-#define CT_DBG(D) if (dbg == D) rc = launch_tile<8, 2, 2, D>(grid, lds, st, (const bf16*)src, (const uint4*)wp, \
-      (const int2*)rowtab, (const int2*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, sched);
-    CT_DBG(1) CT_DBG(2) CT_DBG(4) CT_DBG(3) CT_DBG(7)
+  if (dbg && MT == 8 && NT == 2) {              // experiment variants (timing only; 1-7 give wrong results)
+    static long long* stamps = nullptr;
+    const size_t nst = (size_t)grid.x * grid.y * 16;
+    if ((dbg & 16) && !stamps && hipMalloc(&stamps, 256 * 64 * 16 * sizeof(long long)) != hipSuccess) return -5;
+    if ((dbg & 16) && hipMemsetAsync(stamps, 0, nst * sizeof(long long), st) != hipSuccess) return -5;
+#define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, (const bf16*)src, \
+      (const uint4*)wp, (const int2*)rowtab, (const int2*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, \
+      sched, stamps);
+    CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
+    CT_DBG(4, 23)
 #undef CT_DBG
     if (rc) return rc;
     FN_CHECK_LAUNCH();
+    if (dbg & 16) {                              // mean cycles per workgroup: wave 0 and the loader
+      std::vector<long long> h(nst);
+      if (hipStreamSynchronize(st) != hipSuccess ||
+          hipMemcpy(h.data(), stamps, nst * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return -5;
+      double m[16] = {0};
+      for (size_t i = 0; i < nst; ++i) m[i % 16] += (double)h[i] / (grid.x * grid.y);
+      for (int w = 0; w < 2; ++w)
+        fprintf(stderr,
+                "[conv_tile stamps MT8 CPP%d dbg%d %s] barrierA %.0f job %.0f | tile end: barrierE %.0f stage %.0f "
+                "store+stats %.0f (%.0f) | total %.0f\n",
+                CPP, dbg, w ? "loader" : "wave0 ", m[8 * w], m[8 * w + 1], m[8 * w + 2], m[8 * w + 3], m[8 * w + 4],
+                m[8 * w + 5], m[8 * w + 6]);
+    }
     return 0;
   }
 #define CT_CASE(M, N, C)                                                                                          \

@@ -32,6 +32,7 @@ from .. import _native
 
 LDS_MAX = 160 * 1024
 NTHR = 320          # 4 MFMA waves + 1 loader wave
+RED_BYTES = 5 * 2 * 32 * 4   # per-wave BN partial sums in LDS
 MT_CHOICES = (8, 9)
 _LOCK = threading.Lock()
 _PLANS: dict = {}
@@ -130,7 +131,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
                     halo = HPpad * CPP * 16
                     stage = (64 * MT + 1) * (NT * 16 + 8) * 2
                     BUF = -(-max(halo, stage, NTHR * 64) // 16) * 16
-                    lds = 2 * BUF + 64 + 4 * 64 * MT * 4 + (nks + PD + 2) * 8 + HPpad * 8
+                    lds = 2 * BUF + 64 + RED_BYTES + 4 * 64 * MT * 4 + (nks + PD + 2) * 8 + HPpad * 8
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
