@@ -3,40 +3,44 @@
 // Successor of conv_halo.hip for the wide-channel FeatureNet-3D layers.  Where
 // conv_halo runs 8 waves on <= 256-row tiles with 16-channel halo slices, a
 // double-buffered 128-k weight stage in LDS (one barrier per stage) and a
-// mostly synchronous halo reload per job, this kernel is built around ONE wave
-// per SIMD:
+// mostly synchronous halo reload per job, this kernel is built around ONE MFMA
+// wave per SIMD:
 //
-//   * workgroup = 4 waves, each owning 16*MT output rows (MT = 8..10) x all
-//     NT*16 columns of the workgroup: 512-640-row tiles (cubic-ish output
-//     blocks, 2-4x less halo overhead than conv_halo's plane slabs);
+//   * workgroup = 4 compute waves, each owning 16*MT output positions (MT = 8, 9)
+//     x all NT*16 columns of the workgroup (512-576-position tiles: cubic-ish
+//     output blocks, 2-4x less halo overhead than conv_halo's plane slabs), plus
+//     one loader wave;
 //   * the input halo of a CS-channel slice of a tile ("job") sits in one of two
-//     LDS buffers; the NEXT job's halo streams into the other buffer by LDS-DMA
-//     (global_load_lds_dwordx4, one wave-instruction per k-step, zero page for
-//     padding) while the current job computes -- the only barriers are one per
-//     job (plus the epilogue's);
+//     LDS buffers; the loader LDS-DMAs the NEXT job's halo into the other buffer
+//     (global_load_lds_dwordx4 from SGPR base + per-position offsets, zero page
+//     for padding) while the compute waves run the current one -- one barrier per
+//     job, nothing else;
 //   * weights never touch LDS: pre-packed in MFMA-fragment order
 //     ([slice][k-step][16-col tile][lane][8]) and streamed global -> VGPRs by
-//     every wave (1 KB per fragment, L1/L2 hits), PD k-steps ahead in a register
-//     ring;
-//   * A-fragment reads are bank-conflict free: the halo is stored chunk-planar
+//     every compute wave (1 KB per fragment, L1/L2 hits), PD k-steps ahead in a
+//     register ring that runs on across jobs;
+//   * halo fragment reads are bank-conflict free: the halo is stored chunk-planar
 //     (16-B chunk c of position p at c*PLANE + 16p, PLANE a multiple of 1 KB), so
-//     the bank slot of a read is p mod 16, and the host permutes the tile rows
-//     (rowtab) so that the 16 rows of every MFMA fragment have 16 distinct halo
-//     positions mod 16: every ds_read_b128 lane group touches 16 distinct slots;
+//     the bank slot of a read is p mod 16, and the host permutes the tile
+//     positions (rowtab) so that the 16 of every MFMA fragment have 16 distinct
+//     halo positions mod 16: every ds_read_b128 lane group touches 16 distinct slots;
 //   * per-k-step tap offsets come from a small LDS table (a scalar-memory table
-//     would share lgkmcnt with the A reads and drain them; an SALU tap walker
+//     would share lgkmcnt with the halo reads and drain them; an SALU tap walker
 //     costs issue slots the single wave per SIMD cannot spare).
 //
-// MFMA: v_mfma_f32_16x16x32_bf16.  A = halo rows (lane: row lr, 8 k of group lg),
-// B = weights, k-step = 32 k = one tap x 32 channels (CS >= 32) or two taps x 16
-// channels (CS = 16).  Epilogue: fp32 acc (+bias) -> bf16 staged in LDS in natural
-// tile order -> activation -> 16-B stores; optional BN statistics (per workgroup
-// column sums of the bf16 outputs).
+// MFMA: v_mfma_f32_16x16x32_bf16 with A = weights (16 output channels x 32 k) and
+// B = halo (32 k x 16 positions): the accumulator is C^T, so a lane holds 4
+// consecutive output channels of one position and the epilogue stores them
+// straight from registers (+bias, bf16, activation, 8-B stores; optional BN
+// statistics as per-workgroup column sums of the stored bf16 values) -- no LDS
+// staging and no epilogue barriers.  k-step = 32 k = one tap x 32 channels
+// (CS >= 32) or two taps x 16 channels (CS = 16).
 //
 // Dgrad uses the same kernel: dx = conv(dy, flip(W)^T) with leading pads K-1-p.
 #include "common.h"
 
 #include <cstdio>
+#include <type_traits>
 #include <vector>
 
 struct TileGeom {
@@ -62,7 +66,7 @@ __device__ __forceinline__ void tile_lds_barrier() {
 
 #define CT_NCW 4                       // compute (MFMA) waves
 #define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
-#define CT_RED_BYTES ((CT_NCW + 1) * 2 * 32 * 4)   // per-wave BN partial sums of 32 columns (NT = 2)
+#define CT_RED_BYTES (CT_NCW * 2 * 32 * 4)   // per-compute-wave BN sums of 32 columns (NT = 2)
 
 // LDS-DMA of one 16-B chunk per lane into lds_dst + 16 * lane (lds_dst wave-uniform);
 // M0 saved/restored in the same statement (it is compiler-reserved)
@@ -92,18 +96,20 @@ __device__ __forceinline__ unsigned bf16x2_pack(float lo, float hi) {
   return __builtin_bit_cast(unsigned, p);
 }
 
+// sum over the 16 lanes of a DPP row (every lane of the row gets it): quad swaps, then
+// half-row and row mirrors
+__device__ __forceinline__ float ct_sum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));    // quad [1,0,3,2]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));    // quad [2,3,0,1]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));   // row_half_mirror
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));   // row_mirror
+  return x;
+}
+
 __device__ __forceinline__ unsigned ct_lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-// Persistent workgroup: 4 compute waves (one per SIMD, 16*MT rows x NT*16 columns each)
-// + 1 loader wave.  Per job (tile, channel slice):
-//   barrier A: this job's halo has landed in buffer `cur` (the loader waited for it),
-//              the other buffer is free;
-//   loader:    reads the next job from its grab queue, LDS-DMAs its halo into the other
-//              buffer, pre-grabs the tile after it, waits for all of it (vmcnt(0));
-//   compute:   B-ring prologue, k-loop (MFMA + A reads + B loads only), epilogue on the
-//              job that finishes a tile (all 5 waves: staging, stores, BN statistics).
 template <int MT, int NT, int CPP, int DBG = 0>
 __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __restrict__ src,
                                                                const uint4* __restrict__ wp,
@@ -116,10 +122,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
                                                                long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int PD = NT == 2 ? 4 : 3;            // B prefetch depth (k-steps in flight)
-  constexpr int LDO = NT * 16 + 8;               // epilogue staging row pitch (bf16)
-  constexpr int CPR = NT * 2;                    // 16-B chunks per output row
   constexpr int LCPP = CPP == 2 ? 1 : (CPP == 4 ? 2 : 3);
-  static_assert(NT * 16 <= 32, "s_red holds 32 columns per wave");
+  static_assert(NT == 2, "column order and s_red assume 32-column blocks");
 
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int HP = (g.TD + g.KD - 1) * HH * HW;
@@ -136,31 +140,30 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   const bool loader = wave == CT_NCW;
   const int lr = lane & 15, lg = lane >> 4;
   const int ct0 = blockIdx.y * NT;               // first 16-column tile of this workgroup
-  // LDS: [buffer 0][buffer 1][job slots 64 B][BN partials][row map 4*MT*16 ints][k-step offsets (nks+PD+2)
-  // int2][halo positions HPpad int2: (byte offset from the halo origin, packed hd|hh|hw)]
+  // LDS: [buffer 0][buffer 1][job slots 64 B][BN partials][k-step offsets (nks+PD+2) int2]
+  // [halo positions HPpad int2: (byte offset from the halo origin, packed hd|hh|hw)]
   int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);                    // [2][2] (tile, slice) by parity
-  float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);           // [5 waves][2][32] BN partials
-  int* s_orow = reinterpret_cast<int*>(dsm + 2 * g.BUF + 64 + CT_RED_BYTES);
-  int2* s_kt = reinterpret_cast<int2*>(dsm + 2 * g.BUF + 64 + CT_RED_BYTES + 4 * 64 * MT * 4);
+  float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);           // [4 waves][2][32] BN partials
+  int2* s_kt = reinterpret_cast<int2*>(dsm + 2 * g.BUF + 64 + CT_RED_BYTES);
   int2* s_pos = s_kt + (nks + PD + 2);
-  for (int i = tid; i < 4 * MT * 16; i += CT_NTHR) s_orow[i] = rowtab[i].y;
   for (int i = tid; i < nks + PD + 2; i += CT_NTHR) s_kt[i] = ktab[i];
+  for (int i = tid; i < CT_RED_BYTES / 4; i += CT_NTHR) s_red[i] = 0.f;
   for (int p = tid; p < g.HPpad; p += CT_NTHR) {  // positions past HP repeat the last one
     const int pc = p < HP ? p : HP - 1;
     const int hd = pc / (HH * HW), hh = (pc / HW) % HH, hw = pc % HW;
     s_pos[p] = make_int2(((hd * g.IH + hh) * g.IW + hw) * g.C * 2, (hd << 16) | (hh << 8) | hw);
   }
-  float bcol[NT];                                // bias of this lane's epilogue columns
+  // per compute lane: fragment row (output position) lr of each MFMA tile mt -- its LDS halo
+  // offset lb (toggled between the buffers per job), its output offset relative to the
+  // tile origin (-1: dummy row) and its packed tile coordinates (edge-tile bounds)
+  int lb[MT], roff[MT], rpk[MT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) {
-    const int gcol = (ct0 + nt) * 16 + lr;
-    bcol[nt] = (bias && gcol < Ncol) ? bias[gcol] : 0.f;
-  }
-  int lb[MT];                                    // LDS byte offset of the row's tap-(0,0,0) chunk in
-#pragma unroll                                   // the current job's buffer (toggled per job)
   for (int mt = 0; mt < MT; ++mt) {
     const int2 rt = rowtab[((loader ? 0 : wave) * MT + mt) * 16 + lr];
     lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (lg & 1)) * PLANE;
+    const int tw = rt.y % g.TW, th = (rt.y / g.TW) % g.TH, td = rt.y / (g.TW * g.TH);
+    roff[mt] = rt.y < 0 ? -1 : (td * g.OH + th) * g.OW + tw;
+    rpk[mt] = (td << 16) | (th << 8) | tw;
   }
 
   // ---- loader: job decode and halo DMA --------------------------------------
@@ -221,98 +224,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
     }
   };
 
-  // ---- tile end, shared by all 5 waves: stores of the staged tile (activation) and BN
-  // statistics (per-tile partial sums folded into wave 0's running column sums) --------
-  float cst_s = 0.f, cst_q = 0.f;                // BN sums of column tid (tid < 32): this workgroup's tiles
-  auto store_tile = [&](int tile_o, int boff) {
-    int t = tile_o;
-    const int tw_i = t % twn; t /= twn;
-    const int th_i = t % thn; t /= thn;
-    const int td_i = t % tdn;
-    const int n = t / tdn;
-    const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
-    const bf16* Os = reinterpret_cast<const bf16*>(dsm + boff);
-    const long long obase = (long long)n * g.OD * g.OH * g.OW;
-    const int ch = tid % CPR;                    // fixed per thread (CT_NTHR % CPR == 0)
-    const int gc = ct0 * 16 + ch * 8;
-    const bool vec = gc + 8 <= Ncol && (Ncol & 7) == 0;
-    float st_s[8], st_q[8];                      // this tile's BN partial sums of the thread's 8 columns
-#pragma unroll
-    for (int j = 0; j < 8; ++j) st_s[j] = st_q[j] = 0.f;
-#pragma unroll 2
-    for (int idx = tid; idx < rows * CPR; idx += CT_NTHR) {
-      const int r = idx / CPR;
-      const int q = (int)__umulhi((unsigned)r, g.mTW);
-      const int tw = r - q * g.TW;
-      const int td = (int)__umulhi((unsigned)q, g.mTH);
-      const int th = q - td * g.TH;
-      if (d0 + td < g.OD && h0 + th < g.OH && w0 + tw < g.OW) {
-        const long long m = obase + ((long long)(d0 + td) * g.OH + h0 + th) * g.OW + w0 + tw;
-        // 8 bf16 as 4 packed words end to end (a union with per-element writes made hipcc
-        // split the 16-B store into 2-byte ones)
-        const uint4 u = *(const uint4*)(Os + r * LDO + ch * 8);
-        unsigned w4[4] = {u.x, u.y, u.z, u.w};
-        if (act != ACT_NONE) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) w4[k] = bf16x2_pack(act_fwd(bf16_lo(w4[k]), act), act_fwd(bf16_hi(w4[k]), act));
-        }
-        if (stats) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const float lo = bf16_lo(w4[k]), hi = bf16_hi(w4[k]);
-            st_s[2 * k] += lo;
-            st_q[2 * k] += lo * lo;
-            st_s[2 * k + 1] += hi;
-            st_q[2 * k + 1] += hi * hi;
-          }
-        }
-        if (vec) {
-          *(uint4*)(out + m * Ncol + gc) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-        } else {
-          for (int j = 0; j < 8; ++j)
-            if (gc + j < Ncol) out[m * Ncol + gc + j] = f2bf(j & 1 ? bf16_hi(w4[j >> 1]) : bf16_lo(w4[j >> 1]));
-        }
-      }
-    }
-    if (stats) {
-      // over the lanes of a wave that share the chunk (xor shuffles), then over the 5 waves
-      // in LDS; the next s_red write is a tile later, barriers apart
-#pragma unroll
-      for (int off = CPR; off < 64; off <<= 1) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          st_s[j] += __shfl_xor(st_s[j], off);
-          st_q[j] += __shfl_xor(st_q[j], off);
-        }
-      }
-      if (lane < CPR) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          s_red[wave * 64 + lane * 8 + j] = st_s[j];
-          s_red[wave * 64 + 32 + lane * 8 + j] = st_q[j];
-        }
-      }
-      tile_lds_barrier();
-      if (tid < NT * 16) {
-#pragma unroll
-        for (int w = 0; w < CT_NCW + 1; ++w) {
-          cst_s += s_red[w * 64 + tid];
-          cst_q += s_red[w * 64 + 32 + tid];
-        }
-      }
-    }
-  };
-
-  // ---- schedule: first tile (all waves) ---------------------------------------
-  if (tid == 0) {
-    s_job[0] = atomicAdd(sched + 1 + blockIdx.y, 1);
-    s_job[1] = 0;
-  }
-  tile_lds_barrier();
-  int tile = __builtin_amdgcn_readfirstlane(s_job[0]);
-  if (tile >= ntiles) tile = -1;
   // DBG & 16: cycle stamps of wave 0 and the loader (barrier-A wait, job work, tile end)
-  long long st_a = 0, st_k = 0, st_e[4] = {0, 0, 0, 0}, st_0 = 0, st_1 = 0;
+  long long st_a = 0, st_k = 0, st_e = 0, st_0 = 0, st_1 = 0;
   auto stamp = [&]() -> long long { return (DBG & 16) ? (long long)__builtin_amdgcn_s_memtime() : 0; };
   auto lap = [&](long long& acc_t) {
     if constexpr ((DBG & 16) != 0) {
@@ -323,30 +236,44 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   };
   st_0 = stamp();
 
-  // The loader and the compute waves run separate loops over the same job sequence with
-  // the same barriers (A per job; E, S (+R with statistics) per tile), so neither keeps
-  // the other's registers live.
+  // ---- job protocol ---------------------------------------------------------
+  // s_job[2*par] = (tile, slice) of the job whose halo sits in buffer par (tile -1: done).
+  // The loader publishes job j+1 in slot par^1 right after barrier A(j) and lands its
+  // halo before barrier A(j+1); every wave reads its job after barrier A.  The compute
+  // waves never wait on anything else: the epilogue stores straight from registers.
+  if (tid == 0) {
+    const int t0 = atomicAdd(sched + 1 + blockIdx.y, 1);
+    s_job[0] = t0 < ntiles ? t0 : -1;
+    s_job[1] = 0;
+  }
+  tile_lds_barrier();
+
   if (loader) {
     // ======================= loader wave =======================
-    int t_next;
-    if (tile >= 0) dma_job(tile, 0, 0);
-    if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
-    t_next = __builtin_amdgcn_readfirstlane(t_next);
-    if (t_next >= ntiles) t_next = -1;
+    int tile = __builtin_amdgcn_readfirstlane(s_job[0]), slice = 0, t_next = -1;
+    if (tile >= 0) {
+      dma_job(tile, 0, 0);
+      if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
+      t_next = __builtin_amdgcn_readfirstlane(t_next);
+      if (t_next >= ntiles) t_next = -1;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int slice = 0, par = 0, bufoff = 0;
-    while (tile >= 0) {
+    int par = 0;
+    while (true) {
       st_1 = stamp();
-      tile_lds_barrier();                        // A: job halo landed; other buffer free
+      tile_lds_barrier();                        // A: job halo landed; the other buffer is free
       lap(st_a);
+      if (tile < 0) break;
       int ntile = tile, nslc = slice + 1;
       if (nslc == nslice) {
         nslc = 0;
         ntile = t_next;
-        if (lane == 0) s_job[2 * (par ^ 1)] = ntile;   // published for the compute waves
       }
-      const int nbuf = bufoff ^ g.BUF;
-      if (!(DBG & 4) && ntile >= 0) dma_job(ntile, nslc, nbuf);
+      if (lane == 0) {
+        s_job[2 * (par ^ 1)] = ntile;
+        s_job[2 * (par ^ 1) + 1] = nslc;
+      }
+      if (!(DBG & 4) && ntile >= 0) dma_job(ntile, nslc, (par ^ 1) * g.BUF);
       if (nslc == 0 && ntile >= 0) {
         if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
         t_next = __builtin_amdgcn_readfirstlane(t_next);
@@ -354,21 +281,16 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lap(st_k);
-      if (slice == nslice - 1) {
-        tile_lds_barrier();                      // E
-        lap(st_e[0]);
-        tile_lds_barrier();                      // S: staging written
-        lap(st_e[1]);
-        store_tile(tile, bufoff);
-        lap(st_e[2]);
-      }
       tile = ntile;
       slice = nslc;
-      bufoff = nbuf;
       par ^= 1;
     }
+    tile_lds_barrier();                          // R: the compute waves' BN partials (uniform count)
   } else {
     // ======================= compute waves =======================
+    // MFMA with the weights as A (16 output channels) and the halo as B (16 positions):
+    // acc[mt][nt] = C^T, lane (lr, lg) holds channels (ct0+nt)*16 + 4lg + r of position
+    // lr of tile mt -- 4 consecutive channels of one output row, stored as one 8-B write
     f32x4 acc[MT][NT];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -377,13 +299,19 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
     bf16x8 fa[MT];                               // rotating: fragment mt of k-step k+1 is read right
                                                  // after the NT MFMAs of (mt, k) consumed it
     bf16x8 fb[PD][NT];
+    // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
+    // ct0*16 + 8lg + 4nt + r: a lane ends with 8 consecutive columns of one position
+    const int gc8 = ct0 * 16 + 8 * lg;
+    float bias8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bias8[j] = (bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
     const unsigned wstep = (unsigned)g.nct * 1024u;   // bytes per k-step of the packed weights
     unsigned voffb[PD];                          // per-lane B offsets of the PD ring slots
 #pragma unroll
     for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * 16u + (unsigned)u * wstep;
-    // B loads are ordinary loads: hipcc counts them (vmcnt waits before the consuming
-    // MFMAs, correct across its own register copies and spills); the compute waves issue
-    // no hidden VMEM, so its counts are exact
+    // weight loads are ordinary loads: hipcc counts them (vmcnt waits before the consuming
+    // MFMAs, correct across its own register copies); the compute waves issue no hidden
+    // VMEM, so its counts are exact
     auto load_b = [&](const unsigned char* base, int slot) {
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const bf16x8*)(base + voffb[slot] + nt * 1024);
@@ -394,19 +322,21 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
     // wave-uniform offset it hoisted a turn's reads into a double-buffered block)
     const int khalf = lg < 2 ? 0 : 4;
     auto kofs = [&](int k) -> int { return *(const int*)((const unsigned char*)(s_kt + k) + khalf); };
-    // B ring: the first job's k-steps 0..PD-1; every later job's come from the previous
-    // job's last turn, so no job starts on an exposed L2 latency
-    if (tile >= 0) {
+    // epilogue variant (wave-uniform); columns come in whole 8-column groups (Ncol % 8 == 0)
+    const int emode = (stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0);   // (ACT_NONE / ACT_RELU only)
+    // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
+    // the previous job's last turn, so no job starts on an exposed L2 latency
 #pragma unroll
-      for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024, u);
-    }
-    int slice = 0, par = 0, bufoff = 0;
-    while (tile >= 0) {
+    for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024, u);
+    int par = 0;
+    while (true) {
       st_1 = stamp();
-      tile_lds_barrier();                        // A: job halo landed; other buffer free
+      tile_lds_barrier();                        // A
       lap(st_a);
+      const int tile = __builtin_amdgcn_readfirstlane(s_job[2 * par]);
+      const int slice = __builtin_amdgcn_readfirstlane(s_job[2 * par + 1]);
+      if (tile < 0) break;
       const int nslc = slice + 1 == nslice ? 0 : slice + 1;
-      const int nbuf = bufoff ^ g.BUF;
       // ---- k-loop: MFMA + A reads + B loads, nothing else ----
       const unsigned char* wbase = reinterpret_cast<const unsigned char*>(wp) +
                                    ((size_t)slice * nks * g.nct + ct0) * 1024 + PD * wstep;
@@ -429,7 +359,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
           for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt)
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb[u][nt], acc[mt][nt], 0, 0, 0);
+              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0);
             if constexpr (!(DBG & 2)) fa[mt] = *(const bf16x8*)(dsm + lb[mt] + ko);
             __builtin_amdgcn_sched_barrier(0);
           }
@@ -439,58 +369,97 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
         wbase += PD * wstep;
       }
       lap(st_k);
-      int ntile = tile;
       if (slice == nslice - 1) {
-        tile_lds_barrier();                      // E: every compute wave is done reading this halo
-        lap(st_e[0]);
-        bf16* Os = reinterpret_cast<bf16*>(dsm + bufoff);
-        // acc (+bias) -> bf16 staging in natural tile rows; dummy rows write row 64*MT
+        // ---- epilogue: acc (+bias) -> bf16 -> activation -> 8-B stores (+BN sums) ----
+        int t = tile;
+        const int tw_i = t % twn; t /= twn;
+        const int th_i = t % thn; t /= thn;
+        const int td_i = t % tdn;
+        const int n = t / tdn;
+        const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
+        const int ld = g.OD - d0, lh = g.OH - h0, lw = g.OW - w0;   // in-bounds tile extent
+        const bool edge = ld < g.TD || lh < g.TH || lw < g.TW;
+        bf16* obase = out + (((long long)n * g.OD + d0) * g.OH + h0) * g.OW * Ncol + (long long)w0 * Ncol + gc8;
+        // straight-line variants per (statistics, activation): runtime branches inside the
+        // unrolled per-tile loop made hipcc emit ~1000 basic blocks
+        auto epilogue = [&](auto mode) {
+          constexpr int M = decltype(mode)::value;   // bit 0 stats, bit 1 relu
+          float ts[8], tq[8];                    // this tile's BN partial sums of the lane's 8 columns
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int4 o4 = *(const int4*)(s_orow + (wave * MT + mt) * 16 + lg * 4);   // rows 4lg .. 4lg+3
-          const int orow[4] = {o4.x, o4.y, o4.z, o4.w};
+          for (int j = 0; j < 8; ++j) ts[j] = tq[j] = 0.f;
 #pragma unroll
-          for (int nt = 0; nt < NT; ++nt) {
-            const int col = nt * 16 + lr;
+          for (int mt = 0; mt < MT; ++mt) {
+            bool ok = roff[mt] >= 0 && gc8 < Ncol;
+            if (edge) ok = ok && (rpk[mt] >> 16) < ld && ((rpk[mt] >> 8) & 255) < lh && (rpk[mt] & 255) < lw;
+            float v[8];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int orr = orow[r] >= 0 ? orow[r] : 64 * MT;
-              Os[orr * LDO + col] = f2bf(acc[mt][nt][r] + bcol[nt]);
+            for (int j = 0; j < 8; ++j) {
+              v[j] = bf16_lo(bf16x2_pack(acc[mt][j >> 2][j & 3] + bias8[j], 0.f));   // the stored bf16 value
+              if constexpr ((M & 2) != 0) v[j] = fmaxf(v[j], 0.f);
             }
-            acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-          }
-        }
-        tile_lds_barrier();                      // S
-        lap(st_e[1]);
-        store_tile(tile, bufoff);
-        lap(st_e[2]);
-        // the loader published the next tile before barrier E
-        ntile = __builtin_amdgcn_readfirstlane(s_job[2 * (par ^ 1)]);
-      }
-      tile = ntile;
-      slice = nslc;
+            if constexpr ((M & 1) != 0) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) lb[mt] += nbuf - bufoff;
-      bufoff = nbuf;
+              for (int j = 0; j < 8; ++j) {
+                const float x = ok ? v[j] : 0.f;
+                ts[j] += x;
+                tq[j] += x * x;
+              }
+            }
+            if (ok)
+              *(uint4*)(obase + (long long)roff[mt] * Ncol) = make_uint4(
+                  bf16x2_pack(v[0], v[1]), bf16x2_pack(v[2], v[3]), bf16x2_pack(v[4], v[5]), bf16x2_pack(v[6], v[7]));
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          }
+          if constexpr ((M & 1) != 0) {
+            // over the 16 lanes holding the same columns (DPP), into the wave's LDS sums
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              ts[j] = ct_sum16(ts[j]);
+              tq[j] = ct_sum16(tq[j]);
+            }
+            if (lr == 0) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                atomicAdd(&s_red[wave * 64 + 8 * lg + j], ts[j]);
+                atomicAdd(&s_red[wave * 64 + 32 + 8 * lg + j], tq[j]);
+              }
+            }
+          }
+        };
+        switch (emode) {
+          case 0: epilogue(std::integral_constant<int, 0>{}); break;
+          case 1: epilogue(std::integral_constant<int, 1>{}); break;
+          case 2: epilogue(std::integral_constant<int, 2>{}); break;
+          default: epilogue(std::integral_constant<int, 3>{}); break;
+        }
+        lap(st_e);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) lb[mt] += (1 - 2 * par) * g.BUF;   // the other buffer
       par ^= 1;
+    }
+    tile_lds_barrier();                          // R
+    if (stats && tid < NT * 16 && ct0 * 16 + tid < Ncol) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < CT_NCW; ++w) {
+        s1 += s_red[w * 64 + tid];
+        s2 += s_red[w * 64 + 32 + tid];
+      }
+      float* row = stats + (long long)blockIdx.x * 2 * Ncol;   // this workgroup's slab row
+      row[ct0 * 16 + tid] = s1;
+      row[Ncol + ct0 * 16 + tid] = s2;
     }
   }
 
-  if (stats && tid < NT * 16 && ct0 * 16 + tid < Ncol) {
-    float* row = stats + (long long)blockIdx.x * 2 * Ncol;
-    row[ct0 * 16 + tid] += cst_s;                // the caller zeroes the slab
-    row[Ncol + ct0 * 16 + tid] += cst_q;
-  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // the last job's unused ring loads
   if constexpr ((DBG & 16) != 0) {
     if (lane == 0 && (wave == 0 || loader)) {
       long long* d = stamps + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 16 + (loader ? 8 : 0);
       d[0] = st_a;
       d[1] = st_k;
-      d[2] = st_e[0];
-      d[3] = st_e[1];
-      d[4] = st_e[2];
-      d[5] = st_e[3];
+      d[2] = st_e;
       d[6] = stamp() - st_0;
     }
   }
@@ -526,7 +495,11 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
   const int ks = (int)(r % nks);
   const int slice = (int)(r / nks);
   const int Ncol = dgrad ? C : K;
-  const int col = ct * 16 + (lane & 15);
+  // column order inside each 32-column block: fragment ct&1, row i holds output column
+  // 8*(i/4) + 4*(ct&1) + i%4, so after the kernel's C^T MFMA a lane's two fragments give 8
+  // consecutive output columns (one 16-B store)
+  const int fi = lane & 15;
+  const int col = (ct >> 1) * 32 + 8 * (fi >> 2) + 4 * (ct & 1) + (fi & 3);
   int tap, ch0;
   if (CS >= 32) {
     const int sub = CS / 32;
@@ -620,7 +593,7 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT) {
   const int PD = NT == 2 ? 4 : 3;
-  return 2 * (size_t)g.BUF + 64 + CT_RED_BYTES + (size_t)4 * 64 * MT * 4 + (size_t)(g.nks + PD + 2) * 8 + (size_t)g.HPpad * 8;
+  return 2 * (size_t)g.BUF + 64 + CT_RED_BYTES + (size_t)(g.nks + PD + 2) * 8 + (size_t)g.HPpad * 8;
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -656,12 +629,12 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     if (hd != (unsigned long long)(p / (HH * HW)) || (((rem * g.mHW) >> 32) != rem / HW)) return -3;
   }
   const size_t halo = (size_t)g.HPpad * CPP * 16;
-  const size_t stage = (size_t)(64 * MT + 1) * (NT * 16 + 8) * 2;
-  if ((size_t)g.BUF < halo || (size_t)g.BUF < stage || (size_t)g.BUF < (size_t)CT_NTHR * 64 || g.BUF % 16) return -3;
+  if ((size_t)g.BUF < halo || g.BUF % 1024) return -3;
   const size_t lds = tile_lds_total(g, MT, NT);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
+  if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;   // 16-B column groups; relu or none
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();
@@ -687,10 +660,8 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
       for (size_t i = 0; i < nst; ++i) m[i % 16] += (double)h[i] / (grid.x * grid.y);
       for (int w = 0; w < 2; ++w)
         fprintf(stderr,
-                "[conv_tile stamps MT8 CPP%d dbg%d %s] barrierA %.0f job %.0f | tile end: barrierE %.0f stage %.0f "
-                "store+stats %.0f (%.0f) | total %.0f\n",
-                CPP, dbg, w ? "loader" : "wave0 ", m[8 * w], m[8 * w + 1], m[8 * w + 2], m[8 * w + 3], m[8 * w + 4],
-                m[8 * w + 5], m[8 * w + 6]);
+                "[conv_tile stamps MT8 CPP%d dbg%d %s] barrierA %.0f job %.0f epilogue %.0f | total %.0f\n", CPP, dbg,
+                w ? "loader" : "wave0 ", m[8 * w], m[8 * w + 1], m[8 * w + 2], m[8 * w + 6]);
     }
     return 0;
   }

@@ -370,7 +370,8 @@ def halo_conv_dgrad(dy5, w, spec: ConvSpec, plan):
 # ---------------------------------------------------------------------------
 def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: ConvSpec, act: int,
                     want_stats: bool, w: torch.Tensor | None = None):
-    tplan = conv_tile.fwd_plan(spec) if w is not None else None
+    # the tile kernel's epilogue has the identity and relu only
+    tplan = conv_tile.fwd_plan(spec) if w is not None and act in (0, act_code("relu")) else None
     plan = halo_fwd_plan(spec) if w is not None else None
     if tplan is not None and (plan is None or conv_tile.choose(
             "fwd", spec, lambda: conv_tile.conv_fwd(x5, w, bias, spec, act, want_stats, tplan),
@@ -602,7 +603,7 @@ class ConvFn(torch.autograd.Function):
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
             x_saved = s2d_input(x5, f, spec2) if ctx.needs_input_grad[1] else x5
-        elif halo_fwd_plan(spec) is not None or conv_tile.fwd_plan(spec) is not None:
+        elif halo_fwd_plan(spec) is not None or (conv_tile.fwd_plan(spec) is not None and act in (0, act_code("relu"))):
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats, w=w.detach())
         else:
             wmat, ldw = pack_weight_rows(w.detach(), spec)

@@ -32,7 +32,7 @@ from .. import _native
 
 LDS_MAX = 160 * 1024
 NTHR = 320          # 4 MFMA waves + 1 loader wave
-RED_BYTES = 5 * 2 * 32 * 4   # per-wave BN partial sums in LDS
+RED_BYTES = 4 * 2 * 32 * 4   # per-compute-wave BN sums in LDS
 MT_CHOICES = (8, 9)
 _LOCK = threading.Lock()
 _PLANS: dict = {}
@@ -100,7 +100,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
-    if Ncol < 16 or Csrc % 16 or T < 2:
+    if Ncol < 16 or Ncol % 8 or Csrc % 16 or T < 2:
         return None
     NT = 2                                       # 32-column blocks (register budget: 5 waves per CU)
     ncb = -(-Ncol // (NT * 16))
@@ -128,18 +128,17 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
                     HH, HW = TH + KH - 1, TW + KW - 1
                     HP = (TD + KD - 1) * HH * HW
                     HPpad = -(-HP // 64) * 64
-                    halo = HPpad * CPP * 16
-                    stage = (64 * MT + 1) * (NT * 16 + 8) * 2
-                    BUF = -(-max(halo, stage, NTHR * 64) // 16) * 16
-                    lds = 2 * BUF + 64 + RED_BYTES + 4 * 64 * MT * 4 + (nks + PD + 2) * 8 + HPpad * 8
+                    BUF = HPpad * CPP * 16                     # the halo (a multiple of 2 KiB)
+                    lds = 2 * BUF + 64 + RED_BYTES + (nks + PD + 2) * 8 + HPpad * 8
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
                     jobs = tiles * nslice
                     mfma = nks * MT * NT * 16                  # cycles of MFMA issue per wave per job
-                    fixed = 1500                                # barrier + B-ring prologue per job
-                    epi = 1500 + rows * NT * 2 // NTHR * 40 / nslice
-                    per_job = mfma + fixed + epi
+                    fixed = 800                                 # barrier + first halo reads per job
+                    epi = MT * NT * 40 / nslice                 # register epilogue, once per tile
+                    loader = 1500 + (CPP * HPpad // 64) * 130   # DMA issue + landing of one job's halo
+                    per_job = max(mfma + fixed + epi, loader)
                     cost = math.ceil(jobs / workers) * per_job
                     cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
                                           float(cost)))
@@ -317,7 +316,7 @@ def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats
     y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
     stats = None
     if want_stats:
-        stats = torch.zeros(workers(p, geom, spec.K), 2, spec.K, dtype=torch.float32, device=x5.device)
+        stats = torch.empty(workers(p, geom, spec.K), 2, spec.K, dtype=torch.float32, device=x5.device)
     run(x5, wpk, bias, y, stats, p, geom, kd, spec.K, act)
     return y, stats
 
