@@ -13,7 +13,8 @@ FEATURENET = [((25, 25, 25), (5, 5, 5), 32, 32), ((22, 22, 22), (4, 4, 4), 32, 6
 def test_plans_fit_lds_and_cover_rows(out, k, c, n):
     p = ct.plan(128, out, k, c, n)
     assert p is not None
-    assert 2 * p.BUF + 64 + 1024 + 4 * 64 * p.MT * 4 <= ct.LDS_MAX
+    assert p.BUF >= p.HPpad * (p.CS // 8) * 16
+    assert 2 * p.BUF + 64 + ct.RED_BYTES + (p.nks + ct.PD + 2) * 8 + p.HPpad * 8 <= ct.LDS_MAX
     HP = (p.TD + k[0] - 1) * (p.TH + k[1] - 1) * (p.TW + k[2] - 1)
     assert p.HPpad >= HP and p.HPpad % 64 == 0
     tab = ct.row_table(p, k)
@@ -25,10 +26,20 @@ def test_plans_fit_lds_and_cover_rows(out, k, c, n):
     assert tab[:, 0].max() + toff_max < HP                        # every A read inside the halo
 
 
-@pytest.mark.parametrize("out,k,c,n", [f for f in FEATURENET if f[0] != (25, 25, 25) or f[2] != 64])
-def test_featurenet_fragments_conflict_free(out, k, c, n):
+@pytest.mark.parametrize("out,k,c,n", FEATURENET)
+def test_featurenet_fragments_nearly_conflict_free(out, k, c, n):
+    """The planner may trade a few repeated bank slots for a smaller halo (its cost model
+    charges them); at most 10% of the fragment slots of a FeatureNet layer repeat."""
     p = ct.plan(128, out, k, c, n)
     res = ct.row_table(p, k)[:, 0].reshape(-1, 16) % 16
+    dups = sum(16 - len(set(r.tolist())) for r in res)
+    assert dups <= 0.1 * res.size
+
+
+def test_row_table_conflict_free_when_residues_allow():
+    # 5x5x20 tile of a 3^3 conv: 7x7x22 halo, every residue class has >= 32 rows
+    p = ct.TilePlan(5, 5, 20, 32, 8, 2, 1088, 28, 4, 1088 * 64, ct._magic(22), ct._magic(7 * 22), 0.0)
+    res = ct.row_table(p, (3, 3, 3))[:, 0].reshape(-1, 16) % 16
     assert all(len(set(r.tolist())) == 16 for r in res)
 
 
