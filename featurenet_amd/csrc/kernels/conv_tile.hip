@@ -34,7 +34,7 @@
 // straight from registers (+bias, bf16, activation, 8-B stores; optional BN
 // statistics as per-workgroup column sums of the stored bf16 values) -- no LDS
 // staging and no epilogue barriers.  k-step = 32 k = one tap x 32 channels
-// (CS >= 32) or two taps x 16 channels (CS = 16).
+// (CS >= 32), two taps x 16 channels (CS = 16) or four taps x 8 channels (CS = 8).
 //
 // Dgrad uses the same kernel: dx = conv(dy, flip(W)^T) with leading pads K-1-p.
 #include "common.h"
@@ -114,7 +114,7 @@ template <int MT, int NT, int CPP, int DBG = 0>
 __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
-                                                               const int2* __restrict__ ktab,
+                                                               const int4* __restrict__ ktab,
                                                                const bf16* __restrict__ zp,
                                                                const float* __restrict__ bias, bf16* __restrict__ out,
                                                                float* __restrict__ stats, TileGeom g, int Ncol,
@@ -144,8 +144,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   // [halo positions HPpad int2: (byte offset from the halo origin, packed hd|hh|hw)]
   int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);                    // [2][2] (tile, slice) by parity
   float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);           // [4 waves][2][32] BN partials
-  int2* s_kt = reinterpret_cast<int2*>(dsm + 2 * g.BUF + 64 + CT_RED_BYTES);
-  int2* s_pos = s_kt + (nks + PD + 2);
+  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + CT_RED_BYTES);
+  int2* s_pos = reinterpret_cast<int2*>(s_kt + (nks + PD + 2));
   for (int i = tid; i < nks + PD + 2; i += CT_NTHR) s_kt[i] = ktab[i];
   for (int i = tid; i < CT_RED_BYTES / 4; i += CT_NTHR) s_red[i] = 0.f;
   for (int p = tid; p < g.HPpad; p += CT_NTHR) {  // positions past HP repeat the last one
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int2 rt = rowtab[((loader ? 0 : wave) * MT + mt) * 16 + lr];
-    lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (lg & 1)) * PLANE;
+    lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;   // this lane group's plane
     const int tw = rt.y % g.TW, th = (rt.y / g.TW) % g.TH, td = rt.y / (g.TW * g.TH);
     roff[mt] = rt.y < 0 ? -1 : (td * g.OH + th) * g.OW + tw;
     rpk[mt] = (td << 16) | (th << 8) | tw;
@@ -316,12 +316,12 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const bf16x8*)(base + voffb[slot] + nt * 1024);
     };
-    // k-step offsets: s_kt[k] = (lanes lg < 2, lanes lg >= 2) byte offsets of k-step k (the
-    // two halves are equal for CS >= 32; reading them per lane-half anyway keeps the offset a
-    // per-lane value, and hipcc then keeps the A reads interleaved with the MFMAs -- with a
-    // wave-uniform offset it hoisted a turn's reads into a double-buffered block)
-    const int khalf = lg < 2 ? 0 : 4;
-    auto kofs = [&](int k) -> int { return *(const int*)((const unsigned char*)(s_kt + k) + khalf); };
+    // k-step offsets: s_kt[k][lg] = byte offset of the tap lane group lg reads in k-step k
+    // (all four equal for CS >= 32, pairs for CS = 16, four taps for CS = 8).  Reading
+    // them per lane keeps the offset a per-lane value even where it is uniform: hipcc then
+    // keeps the halo reads interleaved with the MFMAs (with a wave-uniform offset it
+    // hoisted a turn's reads into a double-buffered block)
+    auto kofs = [&](int k) -> int { return *((const int*)(s_kt + k) + lg); };
     // epilogue variant (wave-uniform); columns come in whole 8-column groups (Ncol % 8 == 0)
     const int emode = (stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0);   // (ACT_NONE / ACT_RELU only)
     // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
@@ -479,6 +479,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
 //   Wsrc[col = ct*16 + (lane & 15)][tap][ch], k-step ks of slice:
 //     CS >= 32: tap = ks / (CS/32), ch = slice*CS + (ks % (CS/32))*32 + (lane>>4)*8 + j
 //     CS == 16: tap = 2*ks + (lane>>5), ch = slice*16 + ((lane>>4)&1)*8 + j
+//     CS == 8:  tap = 4*ks + (lane>>4), ch = slice*8 + j
 //   forward: Wsrc[col][tap][ch] = w[col][tap][ch]          (Ncol = K, Csrc = C)
 //   dgrad:   Wsrc[col][tap][ch] = w[ch][T-1-tap][col]      (Ncol = C, Csrc = K)
 // zero for tap >= T or col >= Ncol.
@@ -505,9 +506,12 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
     const int sub = CS / 32;
     tap = ks / sub;
     ch0 = slice * CS + (ks % sub) * 32 + (lane >> 4) * 8;
-  } else {
+  } else if (CS == 16) {
     tap = 2 * ks + (lane >> 5);
     ch0 = slice * 16 + ((lane >> 4) & 1) * 8;
+  } else {                                       // CS = 8: four taps per k-step
+    tap = 4 * ks + (lane >> 4);
+    ch0 = slice * 8;
   }
   Pack8 v;
 #pragma unroll
@@ -524,7 +528,7 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
 
 extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, int CS, int nks, int nct, int nslice,
                               int dgrad, hipStream_t st) {
-  if (CS != 16 && CS % 32 != 0) return -2;
+  if (CS != 8 && CS != 16 && CS % 32 != 0) return -2;
   const long long total = (long long)nslice * nks * nct * 64;
   hipLaunchKernelGGL(tile_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (uint4*)out, K, T,
                      C, CS, nks, nct, nslice, dgrad);
@@ -567,7 +571,7 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
 
 template <int MT, int NT, int CPP, int DBG = 0>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const bf16* s, const uint4* w, const int2* rt,
-                       const int2* kt, const bf16* zp, const float* b, bf16* o, float* stats, const TileGeom& g,
+                       const int4* kt, const bf16* zp, const float* b, bf16* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr) {
   static size_t configured = 0;
   if (lds > configured) {
@@ -582,7 +586,7 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const bf16* s, con
 }
 
 // instantiations (MT, NT, CPP) -- the Python planner only emits these
-#define CT_INSTANCES(X) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4)
+#define CT_INSTANCES(X) X(8, 2, 1) X(9, 2, 1) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4)
 
 extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 #define CT_SUP(M, N, C) if (MT == M && NT == N && CPP == C) return 1;
@@ -593,20 +597,20 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT) {
   const int PD = NT == 2 ? 4 : 3;
-  return 2 * (size_t)g.BUF + 64 + CT_RED_BYTES + (size_t)(g.nks + PD + 2) * 8 + (size_t)g.HPpad * 8;
+  return 2 * (size_t)g.BUF + 64 + CT_RED_BYTES + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8;
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
 // wp: packed weights (fn_tile_pack_w) with PD zero k-steps past the last slice; rowtab:
-// int2[4 * MT * 16] (halo position of the row, natural tile row or -1); ktab: int2[nks + PD
-// + 2] byte offsets of every k-step's taps (lane halves lg < 2 / lg >= 2; zero past nks);
+// int2[4 * MT * 16] (halo position of the row, natural tile row or -1); ktab: int4[nks + PD
+// + 2] byte offsets of the tap each lane group reads per k-step (zero past nks);
 // zp: >= 16 zero bytes; sched: int[64] zeroed counters (left zero); stats: fp32
 // [workers][2][Ncol] zero-initialised, or null.
 extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
                             int NT, int* sched, hipStream_t st) {
   const TileGeom g = parse_tile(geom);
-  if (g.CS != 16 && g.CS != 32 && g.CS != 64) return -2;
+  if (g.CS != 8 && g.CS != 16 && g.CS != 32 && g.CS != 64) return -2;
   const int CPP = g.CS / 8;
   if (!fn_conv_tile_supported(MT, NT, CPP)) return -2;
   if (g.C % g.CS || g.TD * g.TH * g.TW > 64 * MT || g.TD < 1 || g.TH < 1 || g.TW < 1) return -3;
@@ -616,7 +620,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   if (g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;   // packed 8-bit hd/hh/hw
   const int PD = NT == 2 ? 4 : 3;
   const int T = g.KD * g.KH * g.KW;
-  const int need_ks = g.CS >= 32 ? T * (g.CS / 32) : (T + 1) / 2;
+  const int need_ks = g.CS >= 32 ? T * (g.CS / 32) : (g.CS == 16 ? (T + 1) / 2 : (T + 3) / 4);
   if (g.nks % PD || g.nks < need_ks || g.nct < (Ncol + 15) / 16) return -3;
   for (long long r = 0; r < 64LL * MT; ++r) {    // epilogue row decode
     const unsigned long long q = (r * (unsigned long long)g.mTW) >> 32;
@@ -644,7 +648,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     if ((dbg & 16) && !stamps && hipMalloc(&stamps, 256 * 64 * 16 * sizeof(long long)) != hipSuccess) return -5;
     if ((dbg & 16) && hipMemsetAsync(stamps, 0, nst * sizeof(long long), st) != hipSuccess) return -5;
 #define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, (const bf16*)src, \
-      (const uint4*)wp, (const int2*)rowtab, (const int2*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, \
+      (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, \
       sched, stamps);
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
     CT_DBG(4, 23)
@@ -668,7 +672,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
     rc = launch_tile<M, N, C>(grid, lds, st, (const bf16*)src, (const uint4*)wp, (const int2*)rowtab,            \
-                              (const int2*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, sched);
+                              (const int4*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, sched);
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;

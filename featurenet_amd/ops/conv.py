@@ -593,8 +593,8 @@ class ConvFn(torch.autograd.Function):
             # input is what wgrad consumes, so it is saved instead of x
             f, spec2 = s2d
             x2 = s2d_input(x5, f, spec2)
-            y, stats = halo_conv_fwd(x2, s2d_weight(w.detach(), f, spec, spec2), bias, spec2, act, want_stats,
-                                     halo_fwd_plan(spec2))
+            y, stats = native_conv_fwd(x2, None, 0, bias, spec2, act, want_stats,
+                                       w=s2d_weight(w.detach(), f, spec, spec2))
             x_saved = x2
         elif s2d is not None:
             # the padded s2d K (FeatureNet-3D stem: 512 vs 343) loses to the packed-W gather

@@ -80,7 +80,7 @@ def _magic_ok(HH: int, HW: int, npos: int) -> bool:
 
 
 def _ksteps(T: int, CS: int, PD: int) -> int:
-    k = T * (CS // 32) if CS >= 32 else (T + 1) // 2
+    k = T * (CS // 32) if CS >= 32 else -(-T // (32 // CS))   # CS = 16 / 8: 2 / 4 taps per k-step
     return -(-k // PD) * PD
 
 
@@ -100,7 +100,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
-    if Ncol < 16 or Ncol % 8 or Csrc % 16 or T < 2:
+    if Ncol < 16 or Ncol % 8 or Csrc % 8 or T < 2:
         return None
     NT = 2                                       # 32-column blocks (register budget: 5 waves per CU)
     ncb = -(-Ncol // (NT * 16))
@@ -109,8 +109,8 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
     workers = max(1, n_cus // ncb)
     cands = []
     cs_only = int(os.environ.get("FN_TILE_CS", "0"))
-    for CS in (32, 16):
-        if Csrc % CS or (cs_only and CS != cs_only):
+    for CS in (32, 16, 8):
+        if Csrc % CS or (cs_only and CS != cs_only) or (CS == 8 and Csrc % 16 == 0):
             continue
         CPP = CS // 8
         nslice = Csrc // CS
@@ -129,7 +129,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
                     HP = (TD + KD - 1) * HH * HW
                     HPpad = -(-HP // 64) * 64
                     BUF = HPpad * CPP * 16                     # the halo (a multiple of 2 KiB)
-                    lds = 2 * BUF + 64 + RED_BYTES + (nks + PD + 2) * 8 + HPpad * 8
+                    lds = 2 * BUF + 64 + RED_BYTES + (nks + PD + 2) * 16 + HPpad * 8
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
@@ -246,27 +246,28 @@ PD = 4                                           # B-ring depth of the kernel (k
 
 
 def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
-    """int32 [nks + PD + 2, 2]: LDS byte offsets of every k-step's taps within a halo buffer,
-    for the lane halves lg < 2 / lg >= 2 (equal unless CS = 16: two taps per k-step);
-    (0, 0) past the last tap (zero weights)."""
+    """int32 [nks + PD + 2, 4]: LDS byte offset of the tap that lane group lg (lanes 16lg ..
+    16lg+15) reads in each k-step -- one tap for all four groups (CS >= 32: the groups take
+    channel chunks of it), two taps (CS = 16: groups 0,1 / 2,3) or four (CS = 8); 0 past the
+    last tap (zero weights)."""
     KD, KH, KW = kdims
     HH, HW = p.TH + KH - 1, p.TW + KW - 1
     T = KD * KH * KW
     kd, kh, kw = np.meshgrid(np.arange(KD), np.arange(KH), np.arange(KW), indexing="ij")
     toff = (((kd * HH + kh) * HW + kw) * 16).reshape(-1)
-    tab = np.zeros((p.nks + PD + 2, 2), dtype=np.int32)
+    tab = np.zeros((p.nks + PD + 2, 4), dtype=np.int32)
     plane = p.HPpad * 16
     for k in range(p.nks):
-        if p.CS >= 32:
-            sub = p.CS // 32
-            t, s = divmod(k, sub)
+        for lg in range(4):
+            if p.CS >= 32:
+                t, s = divmod(k, p.CS // 32)
+                off = s * 4 * plane
+            elif p.CS == 16:
+                t, off = 2 * k + lg // 2, 0
+            else:
+                t, off = 4 * k + lg, 0
             if t < T:
-                tab[k] = toff[t] + s * 4 * plane
-        else:
-            for h in range(2):
-                t = 2 * k + h
-                if t < T:
-                    tab[k, h] = toff[t]
+                tab[k, lg] = toff[t] + off
     return tab
 
 
@@ -304,7 +305,7 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
     _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                 zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                 _native.ptr(stats), geom, ncol, act, p.MT, p.NT, sched(src5.device, st).data_ptr(),
-                                st, [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 2])
+                                st, [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4])
 
 
 def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan):

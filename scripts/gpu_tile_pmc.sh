@@ -1,10 +1,16 @@
 #!/bin/bash
-# conv_tile: tests, layer bench, then one PMC pass over the layer bench
+# conv_tile PMC passes over the per-layer bench (one rocprofv3 run per counter set)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash scripts/gpu_tile.sh || exit $?
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --kernel-trace --output-format csv -d gpurun_out/pmc_tile -o pmc -- python3 scripts/bench_conv_layers.py --batch 128 --reps 2 > gpurun_out/pmc_tile.log 2>&1
-echo "pmc rc=$?"
+P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
+P2="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU"
+i=0
+for P in "$P1" "$P2"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $P --kernel-trace --output-format csv -d gpurun_out/pmc_tile$i -o pmc -- \
+    python3 scripts/bench_conv_layers.py --batch 128 --reps 2 ${ONLY:+--only $ONLY} > gpurun_out/pmc_tile$i.log 2>&1
+  echo "pmc pass $i rc=$?"
+done
 exit 0

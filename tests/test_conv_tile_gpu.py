@@ -32,6 +32,8 @@ CASES = [
     (3, 11, 12, 13, 16, 48, (3, 3, 3), "same"),      # same padding, 48 columns (partial NT=4 block)
     (2, 9, 10, 11, 32, 96, (3, 3, 3), "same"),       # 2 column blocks
     (4, 1, 40, 37, 32, 32, (1, 5, 5), "same"),       # 2-D conv
+    (6, 32, 32, 32, 8, 32, (4, 4, 4), "valid"),      # FeatureNet-3D stem after space-to-depth (CS = 8)
+    (3, 10, 11, 12, 8, 16, (3, 3, 3), "same"),       # CS = 8, 27 taps (last k-step partial), padding
 ]
 
 
@@ -46,7 +48,7 @@ def test_conv_tile_fwd_dgrad(case):
     w = (torch.randn(K, spec.KD, spec.KH, spec.KW, C, device=dev) * 0.05).to(torch.bfloat16).float()
     b = torch.randn(K, device=dev) * 0.1
     pf, pd = ct.fwd_plan(spec), ct.dgrad_plan(spec)
-    assert pf is not None and pd is not None, (pf, pd)
+    assert pf is not None and (pd is not None or C < 16), (pf, pd)   # dgrad needs >= 16 output columns
 
     # forward with bias + relu
     y, _ = ct.conv_fwd(x, w, b, spec, 1, False, pf)
@@ -65,6 +67,8 @@ def test_conv_tile_fwd_dgrad(case):
     torch.testing.assert_close(s[1], (yb * yb).sum(0), rtol=1e-3, atol=1e-3)
 
     # dgrad: dx = conv_transpose(dy, w)
+    if pd is None:
+        return
     dy = torch.randn(spec.out_shape5, device=dev).to(torch.bfloat16)
     dx = ct.conv_dgrad(dy, w, spec, pd)
     xr = x.float().clone().requires_grad_(True)
