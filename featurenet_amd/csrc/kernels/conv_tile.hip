@@ -486,9 +486,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
 __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restrict__ w, uint4* __restrict__ out, int K,
                                                           int T, int C, int CS, int nks, int nct, int nslice,
                                                           int dgrad) {
-  const long long total = (long long)nslice * nks * nct * 64;
+  const long long total = ((long long)nslice * nks + 4) * nct * 64;   // + the ring's 4 zero k-steps
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
+  if (i >= (long long)nslice * nks * nct * 64) {
+    out[i] = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
   const int lane = (int)(i % 64);
   long long r = i / 64;
   const int ct = (int)(r % nct);
@@ -529,7 +533,7 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
 extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, int CS, int nks, int nct, int nslice,
                               int dgrad, hipStream_t st) {
   if (CS != 8 && CS != 16 && CS % 32 != 0) return -2;
-  const long long total = (long long)nslice * nks * nct * 64;
+  const long long total = ((long long)nslice * nks + 4) * nct * 64;
   hipLaunchKernelGGL(tile_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (uint4*)out, K, T,
                      C, CS, nks, nct, nslice, dgrad);
   FN_CHECK_LAUNCH();

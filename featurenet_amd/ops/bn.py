@@ -15,6 +15,7 @@ from __future__ import annotations
 import torch
 
 from .. import _native
+from ..training.flat import grad_target
 from . import reference as ref
 from .spec import PoolSpec, act_code
 
@@ -47,8 +48,9 @@ def _eval_params(gamma, beta, rmean, rvar, eps, C, device):
     return torch.stack([rmean.float(), invstd, scale, shift])
 
 
-def _bwd_param_grads(dz2, y2, prm, act):
-    """(dbeta, dgamma) = (sum g, sum g*xhat)."""
+def _bwd_param_grads(dz2, y2, prm, act, beta=None, gamma=None):
+    """(dbeta, dgamma) = (sum g, sum g*xhat), written straight into the parameters' flat
+    gradients when :func:`grad_target` offers them."""
     M, C = y2.shape
     K = _native.kernels()
     nb = int(max(1, min(2048, M // 256)))
@@ -56,10 +58,12 @@ def _bwd_param_grads(dz2, y2, prm, act):
     st = _native.stream(y2)
     K.colstats(y2.data_ptr(), dz2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), prm[0].data_ptr(),
                prm[1].data_ptr(), part.data_ptr(), M, C, act, 1, nb, st)
-    out = torch.empty(2, C, dtype=torch.float32, device=y2.device)
-    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, out[0].data_ptr(), out[1].data_ptr(), 0, 0,
-                  1, st)
-    return out[0], out[1]
+    db, dg = grad_target(beta), grad_target(gamma)
+    if db is None or dg is None or db.numel() != C or dg.numel() != C:
+        out = torch.empty(2, C, dtype=torch.float32, device=y2.device)
+        db, dg = out[0], out[1]
+    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, db.data_ptr(), dg.data_ptr(), 0, 0, 1, st)
+    return db, dg
 
 
 def _bwd_input(dz2, y2, prm, dbeta, dgamma, act, training):
@@ -93,6 +97,7 @@ class BatchNormActFn(torch.autograd.Function):
         ctx.save_for_backward(y, prm)
         ctx.act, ctx.training = act, training
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
+        ctx.params = (beta, gamma)                   # leaves: for their direct flat gradients
         return z
 
     @staticmethod
@@ -101,7 +106,7 @@ class BatchNormActFn(torch.autograd.Function):
         C = y.shape[-1]
         y2 = y.reshape(-1, C)
         dz2 = dz.contiguous().to(torch.bfloat16).reshape(-1, C)
-        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act)
+        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
                 dbeta if ctx.has_beta else None, None, None, None, None, None, None, None)
@@ -126,6 +131,7 @@ class BatchNormActPoolFn(torch.autograd.Function):
         ctx.save_for_backward(y, prm)
         ctx.act, ctx.training, ctx.pspec, ctx.is_max, ctx.count_pad = act, training, pspec, is_max, count_pad
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
+        ctx.params = (beta, gamma)
         return p
 
     @staticmethod
@@ -138,7 +144,7 @@ class BatchNormActPoolFn(torch.autograd.Function):
                                    ctx.pspec.geom17(), int(ctx.is_max), int(ctx.count_pad), ctx.act,
                                    _native.stream(y), [y.numel(), dp.numel()])
         y2, dz2 = y.reshape(-1, C), dz.reshape(-1, C)
-        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act)
+        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
                 dbeta if ctx.has_beta else None) + (None,) * 10

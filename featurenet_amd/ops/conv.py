@@ -29,6 +29,7 @@ import torch
 from .. import _native
 from . import conv_tile
 from . import reference as ref
+from ..training.flat import grad_target
 from .spec import ConvSpec, act_code
 
 _TAB_LOCK = threading.Lock()
@@ -314,14 +315,15 @@ def halo_sched(device, stream: int) -> torch.Tensor:
     return t
 
 
-def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512) -> torch.Tensor:
-    """dW via LDS halo tiles; fp32 [K, KD, KH, KW, C]."""
+def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512, out=None) -> torch.Tensor:
+    """dW via LDS halo tiles; fp32 [K, KD, KH, KW, C] (accumulated into ``out`` when given:
+    a zeroed contiguous fp32 tensor of that size, e.g. the parameter's flat gradient)."""
     TD, TH, TW = plan
     geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
             spec.pd, spec.ph, spec.pw, TD, TH, TW]
     cs = halo_cs(spec.C)
     per_tile = int(_native.kernels().conv_halo_wgrad_yblocks(geom, spec.K)) * (spec.C // cs)
-    dw = torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
+    dw = out if out is not None else torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
     st = _native.stream(x5)
     _native.kernels().conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), geom, spec.K,
                                       max(1, target_wgs // per_tile), halo_sched(x5.device, st).data_ptr(), st,
@@ -430,10 +432,12 @@ def wgrad_splits(spec: ConvSpec, target_blocks: int = 1024) -> int:
     return int(min(s, max(1, spec.M // 256)))
 
 
-def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=None) -> torch.Tensor:
+    """fp32 dW [K, KD, KH, KW, C]; ``out`` (zeroed, contiguous, that shape) receives it in place
+    where the kernel allows."""
     plan = halo_wgrad_plan(spec)
     if plan is not None:
-        return halo_conv_wgrad(dy5.contiguous(), x5.contiguous(), spec, plan)
+        return halo_conv_wgrad(dy5.contiguous(), x5.contiguous(), spec, plan, out=out)
     K = _native.kernels()
     gm = gather_mode(spec)
     tab = _table(spec, "fwd", gm, x5.device)
@@ -635,7 +639,8 @@ class ConvFn(torch.autograd.Function):
                 f, spec2 = ctx.s2d
                 dw = s2d_weight_grad(native_conv_wgrad(dy, x5, spec2), f, spec)
             else:
-                dw = native_conv_wgrad(dy, x5.contiguous(), spec)
+                # straight into the parameter's zeroed flat gradient when FlatParams offers it
+                dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w))
         db = native_colsum(dy.reshape(-1, spec.K)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
         return dx, dw, db, None, None, None
 

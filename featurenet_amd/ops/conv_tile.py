@@ -286,7 +286,7 @@ def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bo
     zero k-steps that the ring's over-the-end loads read."""
     Csrc = K if dgrad else C
     nslice = Csrc // p.CS
-    out = torch.zeros((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
+    out = torch.empty((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
     wf = w.detach().float().contiguous()
     _native.kernels().tile_pack_w(wf.data_ptr(), out.data_ptr(), K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad),
                                   _native.stream(wf))
