@@ -33,6 +33,7 @@ int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
 int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, int*, hipStream_t);
 int fn_s2d_pack(const void*, void*, const int*, hipStream_t);
+int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
                    hipStream_t);
@@ -193,6 +194,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {
     chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K, T, C, mode, stage_k, S(st)), "halo_pack_w");
   });
+  m.def("s2d_weight_map", [](uintptr_t src, uintptr_t dst, std::vector<int> geom, int dir, uintptr_t st,
+                             std::vector<long long> ext) {
+    need(geom, 12, "s2d_weight_map");
+    const long long big = prod({geom[0], geom[8], geom[9], geom[10], geom[11]});
+    const long long small = prod({geom[0], geom[1], geom[2], geom[3], geom[4]});
+    fits(ext, 0, dir == 0 ? small : big, "s2d_weight_map", "src");
+    fits(ext, 1, dir == 0 ? big : small, "s2d_weight_map", "dst");
+    chk(fn_s2d_weight_map(P<const float*>(src), P<float*>(dst), geom.data(), dir, S(st)), "s2d_weight_map");
+  }, py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("dir"), py::arg("st"),
+     py::arg("ext") = std::vector<long long>());
   m.def("s2d_pack", [](uintptr_t x, uintptr_t out, std::vector<int> geom, uintptr_t st) {
     need(geom, 12, "s2d_pack");
     chk(fn_s2d_pack(P<const void*>(x), P<void*>(out), geom.data(), S(st)), "s2d_pack");

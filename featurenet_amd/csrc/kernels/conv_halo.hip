@@ -1009,6 +1009,58 @@ extern "C" int fn_s2d_pack(const void* x, void* out, const int* geom12, hipStrea
 }
 
 // ---------------------------------------------------------------------------
+// space-to-depth weight map (one launch instead of pad + permute copies)
+// ---------------------------------------------------------------------------
+// w [K][KD][KH][KW][C] (the strided conv) <-> w2 [K][kd][kh][kw][CO] (the stride-1 conv over
+// the packed input): w2[k][i][j][l][((a*sh + b)*sw + c)*C + ci] = w[k][i*sd+a][j*sh+b][l*sw+c][ci]
+// (zero for taps past KD/KH/KW and channels past sd*sh*sw*C).  dir 0 writes w2 from w
+// (forward), dir 1 writes w from w2 (the gradient back onto the strided conv's weight).
+__global__ __launch_bounds__(256) void s2d_weight_map_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                             int K, int KD, int KH, int KW, int C, int sd, int sh,
+                                                             int sw, int kd, int kh, int kw, int CO, int dir) {
+  const long long total = dir == 0 ? (long long)K * kd * kh * kw * CO : (long long)K * KD * KH * KW * C;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  if (dir == 0) {
+    long long r = i;
+    const int c2 = (int)(r % CO); r /= CO;
+    const int l = (int)(r % kw); r /= kw;
+    const int j = (int)(r % kh); r /= kh;
+    const int ii = (int)(r % kd);
+    const int k = (int)(r / kd);
+    float v = 0.f;
+    if (c2 < sd * sh * sw * C) {
+      const int ci = c2 % C, q = c2 / C;
+      const int c = q % sw, b = (q / sw) % sh, a = q / (sw * sh);
+      const int zd = ii * sd + a, zh = j * sh + b, zw = l * sw + c;
+      if (zd < KD && zh < KH && zw < KW) v = src[((((long long)k * KD + zd) * KH + zh) * KW + zw) * C + ci];
+    }
+    dst[i] = v;
+  } else {
+    long long r = i;
+    const int ci = (int)(r % C); r /= C;
+    const int zw = (int)(r % KW); r /= KW;
+    const int zh = (int)(r % KH); r /= KH;
+    const int zd = (int)(r % KD);
+    const int k = (int)(r / KD);
+    const int c2 = (((zd % sd) * sh + zh % sh) * sw + zw % sw) * C + ci;
+    dst[i] = src[((((long long)k * kd + zd / sd) * kh + zh / sh) * kw + zw / sw) * CO + c2];
+  }
+}
+
+extern "C" int fn_s2d_weight_map(const float* src, float* dst, const int* geom13, int dir, hipStream_t st) {
+  const int K = geom13[0], KD = geom13[1], KH = geom13[2], KW = geom13[3], C = geom13[4];
+  const int sd = geom13[5], sh = geom13[6], sw = geom13[7], kd = geom13[8], kh = geom13[9], kw = geom13[10];
+  const int CO = geom13[11];
+  if (sd * sh * sw * C > CO || kd * sd < KD || kh * sh < KH || kw * sw < KW || (dir != 0 && dir != 1)) return -2;
+  const long long total = dir == 0 ? (long long)K * kd * kh * kw * CO : (long long)K * KD * KH * KW * C;
+  hipLaunchKernelGGL(s2d_weight_map_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, src, dst, K, KD,
+                     KH, KW, C, sd, sh, sw, kd, kh, kw, CO, dir);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // weight packing for the halo kernels (one launch instead of zero-fill + copies)
 // ---------------------------------------------------------------------------
 // w: fp32 (or bf16 when w_bf16) [K][T][C] (the conv weight, taps kd-kh-kw major).

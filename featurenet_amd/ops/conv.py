@@ -526,10 +526,21 @@ def s2d_input(x5: torch.Tensor, f, spec2: ConvSpec) -> torch.Tensor:
     return out
 
 
+def _s2d_wgeom(w_shape, f, spec2: ConvSpec) -> list[int]:
+    K, KD, KH, KW, C = w_shape
+    return [K, KD, KH, KW, C, *f, spec2.KD, spec2.KH, spec2.KW, spec2.C]
+
+
 def s2d_weight(w: torch.Tensor, f, spec: ConvSpec, spec2: ConvSpec) -> torch.Tensor:
     K, KD, KH, KW, C = w.shape
     sd, sh, sw = f
     kd, kh, kw = spec2.KD, spec2.KH, spec2.KW
+    if w.is_cuda and _native.kernels_available():   # one launch (pad + permute + channel pad)
+        wf = w.float().contiguous()
+        out = torch.empty(K, kd, kh, kw, spec2.C, dtype=torch.float32, device=w.device)
+        _native.kernels().s2d_weight_map(wf.data_ptr(), out.data_ptr(), _s2d_wgeom(w.shape, f, spec2), 0,
+                                         _native.stream(wf), [wf.numel(), out.numel()])
+        return out.to(w.dtype)
     wp = torch.zeros(K, kd * sd, kh * sh, kw * sw, C, dtype=w.dtype, device=w.device)
     wp[:, :KD, :KH, :KW] = w
     w2 = wp.view(K, kd, sd, kh, sh, kw, sw, C).permute(0, 1, 3, 5, 2, 4, 6, 7).reshape(K, kd, kh, kw, -1)
@@ -538,11 +549,20 @@ def s2d_weight(w: torch.Tensor, f, spec: ConvSpec, spec2: ConvSpec) -> torch.Ten
     return out
 
 
-def s2d_weight_grad(dw2: torch.Tensor, f, spec: ConvSpec) -> torch.Tensor:
-    """Inverse of :func:`s2d_weight` for a gradient (drops padded taps / channels)."""
+def s2d_weight_grad(dw2: torch.Tensor, f, spec: ConvSpec, out=None) -> torch.Tensor:
+    """Inverse of :func:`s2d_weight` for a gradient (drops padded taps / channels); into
+    ``out`` (fp32, the strided conv's weight shape, e.g. its flat gradient) when given."""
     K, kd, kh, kw, _ = dw2.shape
     sd, sh, sw = f
     C = spec.C
+    if dw2.is_cuda and _native.kernels_available():
+        src = dw2.float().contiguous()
+        if out is None:
+            out = torch.empty(K, spec.KD, spec.KH, spec.KW, C, dtype=torch.float32, device=dw2.device)
+        _native.kernels().s2d_weight_map(src.data_ptr(), out.data_ptr(),
+                                         [K, spec.KD, spec.KH, spec.KW, C, sd, sh, sw, kd, kh, kw, dw2.shape[-1]], 1,
+                                         _native.stream(src), [src.numel(), out.numel()])
+        return out
     g = dw2[..., : sd * sh * sw * C].reshape(K, kd, kh, kw, sd, sh, sw, C)
     g = g.permute(0, 1, 4, 2, 5, 3, 6, 7).reshape(K, kd * sd, kh * sh, kw * sw, C)
     return g[:, : spec.KD, : spec.KH, : spec.KW].contiguous()
@@ -613,6 +633,7 @@ class ConvFn(torch.autograd.Function):
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
         ctx.spec, ctx.act, ctx.has_b, ctx.s2d = spec, act, b is not None, s2d
+        ctx.set_materialize_grads(False)                # no zero-filled gradient for the stats output
         ctx.x_needs = ctx.needs_input_grad[0]
         ctx.save_for_backward(x_saved, w, y if act else None)
         if stats is not None:
@@ -621,6 +642,8 @@ class ConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
+        if dy is None:
+            return None, None, None, None, None, None
         x5, w, y = ctx.saved_tensors
         spec, act = ctx.spec, ctx.act
         dy = dy.contiguous().to(torch.bfloat16)
@@ -637,7 +660,7 @@ class ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             if ctx.s2d is not None:      # x5 is the space-to-depth packed input (saved by forward)
                 f, spec2 = ctx.s2d
-                dw = s2d_weight_grad(native_conv_wgrad(dy, x5, spec2), f, spec)
+                dw = s2d_weight_grad(native_conv_wgrad(dy, x5, spec2), f, spec, out=grad_target(w))
             else:
                 # straight into the parameter's zeroed flat gradient when FlatParams offers it
                 dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w))

@@ -699,3 +699,22 @@ def test_upsample2x_fwd_bwd():
     y.backward(g)
     ref_g = g.float().reshape(n, d, 2, h, 2, w, 2, c).sum((2, 4, 6))
     torch.testing.assert_close(xn.grad.float(), ref_g, rtol=1e-2, atol=2e-2)
+
+
+def test_s2d_weight_map_matches_reference():
+    """Native space-to-depth weight expand / gradient fold == the torch pad+permute reference."""
+    import importlib
+
+    cv = importlib.import_module("featurenet_amd.ops.conv")
+    spec = ConvSpec.make((2, 64, 64, 64, 1), 32, (7, 7, 7), 2, "valid")
+    f, spec2 = cv.s2d_plan(spec)
+    torch.manual_seed(0)
+    w = torch.randn(32, 7, 7, 7, 1)
+    ref_w2 = cv.s2d_weight(w, f, spec, spec2)                 # CPU: torch reference path
+    w2 = cv.s2d_weight(w.cuda(), f, spec, spec2)
+    assert torch.equal(w2.cpu(), ref_w2)
+    g2 = torch.randn_like(ref_w2)
+    ref_g = cv.s2d_weight_grad(g2, f, spec)
+    out = torch.zeros(32, 7, 7, 7, 1, device="cuda")
+    g = cv.s2d_weight_grad(g2.cuda(), f, spec, out=out)
+    assert g.data_ptr() == out.data_ptr() and torch.equal(g.cpu(), ref_g)
