@@ -33,6 +33,10 @@ int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
 int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, int*, hipStream_t);
 int fn_s2d_pack(const void*, void*, const int*, hipStream_t);
+int fn_dense_splits(int, int, int);
+int fn_dense_fwd(const void*, const float*, const float*, void*, float*, int, int, int, int, int, int, hipStream_t);
+int fn_dense_dgrad(const void*, const float*, void*, int, int, int, hipStream_t);
+int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, hipStream_t);
 int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
@@ -194,6 +198,36 @@ PYBIND11_MODULE(_C, m) {
   m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {
     chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K, T, C, mode, stage_k, S(st)), "halo_pack_w");
   });
+  m.def("dense_splits", &fn_dense_splits);
+  m.def("dense_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t part, int M, int N, int K,
+                        int nsplit, int act, int out_fp32, uintptr_t st, std::vector<long long> ext) {
+    fits(ext, 0, (long long)M * K, "dense_fwd", "x");
+    fits(ext, 1, (long long)N * K, "dense_fwd", "w");
+    fits(ext, 2, (long long)M * N, "dense_fwd", "out");
+    fits(ext, 3, (long long)nsplit * M * N, "dense_fwd", "part");
+    chk(fn_dense_fwd(P<const void*>(x), P<const float*>(w), P<const float*>(bias), P<void*>(out), P<float*>(part), M,
+                     N, K, nsplit, act, out_fp32, S(st)),
+        "dense_fwd");
+  }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("part"), py::arg("M"), py::arg("N"),
+     py::arg("K"), py::arg("S"), py::arg("act"), py::arg("out_fp32"), py::arg("st"),
+     py::arg("ext") = std::vector<long long>());
+  m.def("dense_dgrad", [](uintptr_t g, uintptr_t w, uintptr_t dx, int M, int N, int K, uintptr_t st,
+                          std::vector<long long> ext) {
+    fits(ext, 0, (long long)M * N, "dense_dgrad", "g");
+    fits(ext, 1, (long long)N * K, "dense_dgrad", "w");
+    fits(ext, 2, (long long)M * K, "dense_dgrad", "dx");
+    chk(fn_dense_dgrad(P<const void*>(g), P<const float*>(w), P<void*>(dx), M, N, K, S(st)), "dense_dgrad");
+  }, py::arg("g"), py::arg("w"), py::arg("dx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("st"),
+     py::arg("ext") = std::vector<long long>());
+  m.def("dense_wgrad", [](uintptr_t g, uintptr_t x, uintptr_t dw, uintptr_t db, int M, int N, int K, uintptr_t st,
+                          std::vector<long long> ext) {
+    fits(ext, 0, (long long)M * N, "dense_wgrad", "g");
+    fits(ext, 1, (long long)M * K, "dense_wgrad", "x");
+    fits(ext, 2, (long long)N * K, "dense_wgrad", "dw");
+    chk(fn_dense_wgrad(P<const void*>(g), P<const void*>(x), P<float*>(dw), P<float*>(db), M, N, K, S(st)),
+        "dense_wgrad");
+  }, py::arg("g"), py::arg("x"), py::arg("dw"), py::arg("db"), py::arg("M"), py::arg("N"), py::arg("K"),
+     py::arg("st"), py::arg("ext") = std::vector<long long>());
   m.def("s2d_weight_map", [](uintptr_t src, uintptr_t dst, std::vector<int> geom, int dir, uintptr_t st,
                              std::vector<long long> ext) {
     need(geom, 12, "s2d_weight_map");

@@ -1,0 +1,311 @@
+// Dense (fully connected) layer on MFMA: y = act(x W^T + b) and its gradients.
+//
+// Reference parity: Keras Dense (reference model/input.py:174-190) and the classifier head
+// (model/keras_model.py:124).  FeatureNet-3D's FC1 is 128 x 64000 -> 128 (skinny: M*N tiny,
+// K huge); NAS candidates put Dense layers of up to 2048 features after small feature maps.
+//
+//   dense_fwd_part  split-K partial products, x bf16 [M][K] x W fp32 [N][K] (the fp32 master
+//                   weights converted to bf16 on the fly: no per-step weight cast pass), fp32
+//                   partial slabs [S][M][N]; 128x64 output tile per workgroup, 4 waves x
+//                   (32 rows x 64 cols), operands straight from global (16-B loads, no LDS)
+//   dense_fwd_reduce  y = act(sum_s part[s] + b) -> bf16 or fp32 (one pass over M*N)
+//   dense_dgrad     dx [M][K] = g [M][N] W [N][K] -> bf16.  C^T form: A = W^T from an LDS
+//                   tile written transposed ([kk][n], converted to bf16), B = g rows from
+//                   global; a lane ends with 4 consecutive kk of one row (8-B stores)
+//   dense_wgrad     dW [N][K] = g^T x -> fp32 straight into the parameter's (flat) gradient,
+//                   db = column sums of g (workgroup 0).  Both operands from LDS tiles written
+//                   transposed ([kk][m], [n][m]); a lane ends with 4 consecutive kk of one n
+//                   (16-B stores)
+//
+// MFMA v_mfma_f32_16x16x32_bf16: A lane (r = lane&15, g = lane>>4) holds A[r][8g..8g+7],
+// B lane holds B[8g..8g+7][r], C lane holds C[4g..4g+3][r].
+#include "common.h"
+
+#define DN_THREADS 256
+
+__device__ __forceinline__ bf16x8 dn_cvt8(const float4 a, const float4 b) {
+  bf16x8 v;
+  v[0] = f2bf(a.x); v[1] = f2bf(a.y); v[2] = f2bf(a.z); v[3] = f2bf(a.w);
+  v[4] = f2bf(b.x); v[5] = f2bf(b.y); v[6] = f2bf(b.z); v[7] = f2bf(b.w);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// forward: split-K partials
+// ---------------------------------------------------------------------------
+// grid (ceil(N/64), ceil(M/128), S); slice s covers k in [s*kc, min(K, (s+1)*kc)), kc % 32 == 0.
+// Requires K % 8 == 0 (16-B rows).
+__global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* __restrict__ x,
+                                                                    const float* __restrict__ w,
+                                                                    float* __restrict__ part, int M, int N, int K,
+                                                                    int kc) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, gq = lane >> 4;
+  const int row0 = blockIdx.y * 128 + wave * 32, col0 = blockIdx.x * 64;
+  const int kbeg = blockIdx.z * kc, kend = min(K, kbeg + kc);
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // row / column validity is per lane; out-of-range rows read row 0 and are zeroed
+  bool rok[2], cok[4];
+  const bf16* xr[2];
+  const float* wr[4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = row0 + i * 16 + r;
+    rok[i] = m < M;
+    xr[i] = x + (long long)(rok[i] ? m : 0) * K;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = col0 + j * 16 + r;
+    cok[j] = n < N;
+    wr[j] = w + (long long)(cok[j] ? n : 0) * K;
+  }
+  const bf16x8 zero8 = {};
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+    const int k = k0 + 8 * gq;
+    const bool kok = k < kend;                   // kend % 8 == 0 (K % 8 == 0, kc % 32 == 0)
+    bf16x8 fa[2], fb[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16x8 v = *(const bf16x8*)(xr[i] + (kok ? k : 0));
+      fa[i] = (rok[i] && kok) ? v : zero8;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4* p = (const float4*)(wr[j] + (kok ? k : 0));
+      const bf16x8 v = dn_cvt8(p[0], p[1]);
+      fb[j] = (cok[j] && kok) ? v : zero8;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+  }
+  float* ps = part + (long long)blockIdx.z * M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = col0 + j * 16 + r;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = row0 + i * 16 + 4 * gq + q;
+        if (m < M && n < N) ps[(long long)m * N + n] = acc[i][j][q];
+      }
+    }
+}
+
+// y[m][n] = act(sum_s part[s][m][n] + b[n]); bf16 or fp32 output
+__global__ __launch_bounds__(DN_THREADS) void dense_fwd_reduce_kernel(const float* __restrict__ part,
+                                                                      const float* __restrict__ bias, void* out,
+                                                                      int M, int N, int S, int act, int out_fp32) {
+  const long long i = (long long)blockIdx.x * DN_THREADS + threadIdx.x;
+  if (i >= (long long)M * N) return;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[(long long)s * M * N + i];
+  if (bias) v += bias[i % N];
+  v = act_fwd(v, act);
+  if (out_fp32) {
+    ((float*)out)[i] = v;
+  } else {
+    ((bf16*)out)[i] = f2bf(v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dgrad: dx = g W   (C^T = W^T g^T: lane ends with dx[m][4 consecutive kk])
+// ---------------------------------------------------------------------------
+// grid (ceil(K/64), ceil(M/64)); block tile: 64 rows m x 64 columns kk; N % 32 == 0.
+// LDS (dynamic): W tile transposed to [64 kk][N + 8] bf16.
+__global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __restrict__ g,
+                                                                 const float* __restrict__ w,
+                                                                 bf16* __restrict__ dx, int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
+  const int LDN = N + 8;                         // row pitch (bf16): 16-B aligned rows, bank shift
+  bf16* wt = reinterpret_cast<bf16*>(dn_lds);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, gq = lane >> 4;
+  const int kk0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  // stage W[0:N][kk0:kk0+64] -> wt[kk][n] (bf16): thread = (n, 4 consecutive kk)
+  for (int idx = tid; idx < N * 16; idx += DN_THREADS) {
+    const int n = idx >> 4, q = idx & 15;
+    const int kk = kk0 + 4 * q;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (kk + 4 <= K) {
+      v = *(const float4*)(w + (long long)n * K + kk);
+    } else {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < 4; ++e)
+        if (kk + e < K) t[e] = w[(long long)n * K + kk + e];
+      v = make_float4(t[0], t[1], t[2], t[3]);
+    }
+    wt[(4 * q + 0) * LDN + n] = f2bf(v.x);
+    wt[(4 * q + 1) * LDN + n] = f2bf(v.y);
+    wt[(4 * q + 2) * LDN + n] = f2bf(v.z);
+    wt[(4 * q + 3) * LDN + n] = f2bf(v.w);
+  }
+  __syncthreads();
+  // wave: 16 kk rows (A = W^T rows kk) x 64 m columns (B = g^T columns m): 4 tiles
+  const int kkw = wave * 16;
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const bf16x8 zero8 = {};
+  for (int n0 = 0; n0 < N; n0 += 32) {
+    const bf16x8 fa = *(const bf16x8*)(wt + (kkw + r) * LDN + n0 + 8 * gq);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + j * 16 + r;
+      const bf16x8 v = *(const bf16x8*)(g + (long long)(m < M ? m : 0) * N + n0 + 8 * gq);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, m < M ? v : zero8, acc[j], 0, 0, 0);
+    }
+  }
+  // C^T[kk][m]: lane holds m = col r of tile j, kk = kkw + 4gq .. +3
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + j * 16 + r;
+    const int kk = kk0 + kkw + 4 * gq;
+    if (m >= M) continue;
+    bf16* o = dx + (long long)m * K + kk;
+    if (kk + 4 <= K && (K & 3) == 0) {
+      bf16x4 v;
+      v[0] = f2bf(acc[j][0]); v[1] = f2bf(acc[j][1]); v[2] = f2bf(acc[j][2]); v[3] = f2bf(acc[j][3]);
+      *(bf16x4*)o = v;
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (kk + e < K) o[e] = f2bf(acc[j][e]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wgrad: dW = g^T x (fp32, overwrite), db = colsum(g)
+// ---------------------------------------------------------------------------
+// grid (ceil(K/64), ceil(N/64)); block tile: 64 n x 64 kk; reduction over all M (M % 32 == 0).
+// LDS (dynamic): x tile transposed [64 kk][M + 8], g tile transposed [64 n][M + 8].
+__global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __restrict__ g,
+                                                                 const bf16* __restrict__ x,
+                                                                 float* __restrict__ dw, float* __restrict__ db,
+                                                                 int M, int N, int K) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
+  const int LDM = M + 8;
+  bf16* xt = reinterpret_cast<bf16*>(dn_lds);
+  bf16* gt = xt + 64 * LDM;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, gq = lane >> 4;
+  const int kk0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  // x[0:M][kk0:kk0+64] -> xt[kk][m]; g[0:M][n0:n0+64] -> gt[n][m]: thread = (m, 8 columns)
+  for (int idx = tid; idx < M * 8; idx += DN_THREADS) {
+    const int m = idx >> 3, q = idx & 7;
+    const int kk = kk0 + 8 * q, n = n0 + 8 * q;
+    Pack8 vx, vg;
+    if (kk + 8 <= K) {
+      vx.u = *(const uint4*)(x + (long long)m * K + kk);
+    } else {
+      for (int e = 0; e < 8; ++e) vx.e[e] = kk + e < K ? x[(long long)m * K + kk + e] : f2bf(0.f);
+    }
+    if (n + 8 <= N) {
+      vg.u = *(const uint4*)(g + (long long)m * N + n);
+    } else {
+      for (int e = 0; e < 8; ++e) vg.e[e] = n + e < N ? g[(long long)m * N + n + e] : f2bf(0.f);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xt[(8 * q + e) * LDM + m] = vx.e[e];
+      gt[(8 * q + e) * LDM + m] = vg.e[e];
+    }
+  }
+  __syncthreads();
+  // C^T[kk][n] = sum_m x^T[kk][m] g[m][n]: wave = 16 kk rows x 64 n columns
+  const int kkw = wave * 16;
+  f32x4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int mm = 0; mm < M; mm += 32) {
+    const bf16x8 fa = *(const bf16x8*)(xt + (kkw + r) * LDM + mm + 8 * gq);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bf16x8 fb = *(const bf16x8*)(gt + (j * 16 + r) * LDM + mm + 8 * gq);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[j], 0, 0, 0);
+    }
+  }
+  // lane: n = n0 + 16j + r, kk = kk0 + kkw + 4gq .. +3 -> dW[n][kk..kk+3]
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + j * 16 + r;
+    const int kk = kk0 + kkw + 4 * gq;
+    if (n >= N) continue;
+    float* o = dw + (long long)n * K + kk;
+    if (kk + 4 <= K && (K & 3) == 0) {
+      *(float4*)o = make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (kk + e < K) o[e] = acc[j][e];
+    }
+  }
+  // bias gradient: the first column block sums g over M for its 64 n
+  if (db && blockIdx.x == 0 && tid < 64 && n0 + tid < N) {
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += bf2f(gt[tid * LDM + m]);
+    db[n0 + tid] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+extern "C" int fn_dense_splits(int M, int N, int K) {
+  const int tiles = ((N + 63) / 64) * ((M + 127) / 128);
+  int S = (512 + tiles - 1) / tiles;
+  const int maxS = K / 256 > 0 ? K / 256 : 1;   // >= 256 k per slice
+  return S < 1 ? 1 : (S > maxS ? maxS : S);
+}
+
+extern "C" int fn_dense_fwd(const void* x, const float* w, const float* bias, void* out, float* part, int M, int N,
+                            int K, int S, int act, int out_fp32, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 8 || S < 1) return -2;
+  int kc = (K + S - 1) / S;
+  kc = (kc + 31) / 32 * 32;
+  const int Sr = (K + kc - 1) / kc;              // slices actually covering K
+  hipLaunchKernelGGL(dense_fwd_part_kernel, dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0, st,
+                     (const bf16*)x, w, part, M, N, K, kc);
+  FN_CHECK_LAUNCH();
+  const long long tot = (long long)M * N;
+  hipLaunchKernelGGL(dense_fwd_reduce_kernel, dim3((unsigned)((tot + DN_THREADS - 1) / DN_THREADS)),
+                     dim3(DN_THREADS), 0, st, (const float*)part, bias, out, M, N, Sr, act, out_fp32);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+static int dn_lds_attr(const void* fn, size_t lds) {
+  if (lds <= 64 * 1024) return 0;
+  return (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
+extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, int N, int K, hipStream_t st) {
+  if (M <= 0 || K <= 0 || N <= 0 || N % 32 || K % 4) return -2;
+  const size_t lds = (size_t)64 * (N + 8) * 2;
+  if (lds > 160 * 1024) return -4;
+  if (int e = dn_lds_attr((const void*)dense_dgrad_kernel, lds)) return e;
+  hipLaunchKernelGGL(dense_dgrad_kernel, dim3((K + 63) / 64, (M + 63) / 64), dim3(DN_THREADS), lds, st,
+                     (const bf16*)g, w, (bf16*)dx, M, N, K);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db, int M, int N, int K,
+                              hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % 32 || K % 8) return -2;
+  const size_t lds = (size_t)2 * 64 * (M + 8) * 2;
+  if (lds > 160 * 1024) return -4;
+  if (int e = dn_lds_attr((const void*)dense_wgrad_kernel, lds)) return e;
+  hipLaunchKernelGGL(dense_wgrad_kernel, dim3((K + 63) / 64, (N + 63) / 64), dim3(DN_THREADS), lds, st,
+                     (const bf16*)g, (const bf16*)x, dw, db, M, N, K);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

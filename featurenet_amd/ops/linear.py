@@ -3,12 +3,12 @@
 Reference parity: Keras ``Dense`` (``model/input.py:174-190``) and the
 classifier head ``Dense(n_classes, softmax)`` (``model/keras_model.py:124``).
 
-GPU: the matmul itself is a plain library GEMM (hipBLASLt through
-``torch.matmul`` on bf16 operands, fp32 accumulate -- the brief reserves
-hand-written MFMA kernels for the fused hot ops and lets plain GEMMs go to
-the vendor library); bias + activation run in the native ``bias_act`` kernel
-and the activation backward in ``act_bwd``.  The weight gradient is produced
-in fp32 for the fp32 master weights.
+GPU: hand-written MFMA kernels (``csrc/kernels/dense.hip``): split-K forward
+that reads the fp32 master weights directly (no per-step bf16 weight copy) with
+bias + activation in the split reduction, a dgrad and a weight-gradient kernel
+that writes the fp32 ``dW`` (and ``db``) straight into the parameters' flat
+gradients.  Shapes outside the kernels' constraints (K % 8, N % 32 for dgrad,
+M % 32 for wgrad) fall back to hipBLASLt through torch for that product.
 """
 from __future__ import annotations
 
@@ -17,30 +17,18 @@ import os
 import torch
 
 from .. import _native
+from ..training.flat import grad_target
 from . import reference as ref
 from .spec import act_code
 
-_SPLITK = os.environ.get("FN_FC_SPLITK", "1") != "0"
+_NATIVE = os.environ.get("FN_DENSE_NATIVE", "1") != "0"
 
 
-def _skinny_matmul(xb: torch.Tensor, wb: torch.Tensor) -> torch.Tensor:
-    """x [M, K] @ w^T for a small M*N and a huge K (FeatureNet-3D FC1: 128 x 64000 x 128).
-
-    hipBLASLt tiles this with ~56 workgroups on a 256-CU part; a 16-way split of K as a
-    batched GEMM with fp32 partials fills the chip (73 -> ~40 us, ``bench/fc_gemm.py``)."""
-    M, K = xb.shape
-    N = wb.shape[0]
-    s = 16
-    xs = xb.view(M, s, K // s).transpose(0, 1)
-    ws = wb.view(N, s, K // s).permute(1, 2, 0)
-    try:
-        part = torch.bmm(xs, ws, out_dtype=torch.float32)
-    except (TypeError, RuntimeError):
-        part = torch.bmm(xs, ws).float()
-    return part.sum(0).to(torch.bfloat16)
+def _torch_fwd(xb: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return torch.matmul(xb, w.detach().to(torch.bfloat16).t())
 
 
-def _wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+def _wgrad_torch(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     """fp32 dW = dy^T x straight out of the GEMM (no bf16 round trip, no cast pass)."""
     try:
         return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
@@ -51,36 +39,73 @@ def _wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 class LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, act: int, out_fp32: bool):
-        wb = w.detach().to(torch.bfloat16)
-        xb = x.to(torch.bfloat16)
-        if _SPLITK and xb.dim() == 2 and xb.shape[0] * wb.shape[0] <= 256 * 256 and xb.shape[1] >= 16384 \
-                and xb.shape[1] % 16 == 0:
-            y = _skinny_matmul(xb.contiguous(), wb)
+        K = x.shape[-1]
+        N = w.shape[0]
+        x2 = x.reshape(-1, K).to(torch.bfloat16).contiguous()
+        M = x2.shape[0]
+        wf = w.detach()
+        bias = b.detach().float().contiguous() if b is not None else None
+        native = _NATIVE and K % 8 == 0 and wf.dtype == torch.float32 and wf.is_contiguous()
+        if native:
+            Kn = _native.kernels()
+            S = int(Kn.dense_splits(M, N, K))
+            part = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+            y = torch.empty(M, N, dtype=torch.float32 if out_fp32 else torch.bfloat16, device=x.device)
+            Kn.dense_fwd(x2.data_ptr(), wf.data_ptr(), _native.ptr(bias), y.data_ptr(), part.data_ptr(), M, N, K, S,
+                         act, int(out_fp32), _native.stream(x2), [x2.numel(), wf.numel(), y.numel(), part.numel()])
         else:
-            y = torch.matmul(xb, wb.t())
-        if b is not None or act:
-            y2 = torch.empty_like(y)
-            _native.kernels().bias_act(y.data_ptr(), _native.ptr(b.detach().float().contiguous() if b is not None else None),
-                                       y2.data_ptr(), y.numel(), y.shape[-1], act, _native.stream(y))
-            y = y2
-        ctx.save_for_backward(xb, wb, y if act else None)
-        ctx.act, ctx.has_b = act, b is not None
-        return y.float() if out_fp32 else y
+            y = _torch_fwd(x2, wf)
+            if b is not None or act:
+                y2 = torch.empty_like(y)
+                _native.kernels().bias_act(y.data_ptr(), _native.ptr(bias), y2.data_ptr(), y.numel(), N, act,
+                                           _native.stream(y))
+                y = y2
+            if out_fp32:
+                y = y.float()
+        ctx.save_for_backward(x2, w, y if act else None)
+        ctx.act, ctx.has_b, ctx.xshape = act, b is not None, x.shape
+        ctx.bparam = b
+        return y.reshape(*x.shape[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
-        xb, wb, y = ctx.saved_tensors
-        dy = dy.to(torch.bfloat16).contiguous()
+        x2, w, y = ctx.saved_tensors
+        M, K = x2.shape
+        N = w.shape[0]
+        g = dy.reshape(M, N).to(torch.bfloat16).contiguous()
         if ctx.act:
-            g = torch.empty_like(dy)
-            _native.kernels().act_bwd(dy.data_ptr(), y.data_ptr(), g.data_ptr(), dy.numel(), ctx.act,
-                                      _native.stream(dy))
-            dy = g
-        dx = torch.matmul(dy, wb) if ctx.needs_input_grad[0] else None
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        x2 = xb.reshape(-1, xb.shape[-1])
-        dw = _wgrad(dy2, x2) if ctx.needs_input_grad[1] else None
-        db = dy2.float().sum(0) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+            g2 = torch.empty_like(g)
+            _native.kernels().act_bwd(g.data_ptr(), y.reshape(M, N).to(torch.bfloat16).contiguous().data_ptr(),
+                                      g2.data_ptr(), g.numel(), ctx.act, _native.stream(g))
+            g = g2
+        Kn = _native.kernels()
+        st = _native.stream(g)
+        wf = w.detach()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if _NATIVE and N % 32 == 0 and K % 4 == 0 and wf.dtype == torch.float32 and 64 * (N + 8) * 2 <= 160 * 1024:
+                dx = torch.empty(M, K, dtype=torch.bfloat16, device=g.device)
+                Kn.dense_dgrad(g.data_ptr(), wf.data_ptr(), dx.data_ptr(), M, N, K, st,
+                               [g.numel(), wf.numel(), dx.numel()])
+            else:
+                dx = torch.matmul(g, wf.to(torch.bfloat16))
+            dx = dx.reshape(ctx.xshape)
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1]:
+            if _NATIVE and M % 32 == 0 and K % 8 == 0 and 2 * 64 * (M + 8) * 2 <= 160 * 1024:
+                dw = grad_target(w)
+                if dw is None:
+                    dw = torch.empty(N, K, dtype=torch.float32, device=g.device)
+                if want_b:
+                    db = grad_target(ctx.bparam)
+                    if db is None:
+                        db = torch.empty(N, dtype=torch.float32, device=g.device)
+                Kn.dense_wgrad(g.data_ptr(), x2.data_ptr(), dw.data_ptr(), _native.ptr(db), M, N, K, st,
+                               [g.numel(), x2.numel(), dw.numel()])
+            else:
+                dw = _wgrad_torch(g, x2)
+        if want_b and db is None:
+            db = g.float().sum(0)
         return dx, dw, db, None, None
 
 

@@ -718,3 +718,34 @@ def test_s2d_weight_map_matches_reference():
     out = torch.zeros(32, 7, 7, 7, 1, device="cuda")
     g = cv.s2d_weight_grad(g2.cuda(), f, spec, out=out)
     assert g.data_ptr() == out.data_ptr() and torch.equal(g.cpu(), ref_g)
+
+
+@pytest.mark.parametrize("M,K,N,act,bias", [(128, 64000, 128, "relu", True), (128, 128, 24, None, True),
+                                            (64, 2048, 256, "relu", False), (96, 520, 64, None, True),
+                                            (32, 4096, 512, "relu", True)])
+def test_dense_native_matches_fp32(M, K, N, act, bias):
+    """Native Dense (split-K forward, dgrad, fp32 wgrad/db) vs the fp32 PyTorch reference."""
+    from featurenet_amd.ops.linear import LinearFn
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).requires_grad_(True)
+    b = (torch.randn(N, device="cuda") * 0.1).requires_grad_(True) if bias else None
+    xg = x.clone().requires_grad_(True)
+    from featurenet_amd.ops.spec import act_code
+
+    y = LinearFn.apply(xg, w, b, act_code(act), False)
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if bias else None
+    xr = x.float().requires_grad_(True)
+    yr = xr @ wr.t() + (br if bias else 0)
+    if act == "relu":
+        yr = torch.relu(yr)
+    l2 = ((y.float() - yr).norm() / yr.norm()).item()
+    assert l2 < 1e-2, l2
+    dy = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    gx, gw, *gb = torch.autograd.grad(y, [xg, w] + ([b] if bias else []), dy)
+    rx, rw, *rb = torch.autograd.grad(yr, [xr, wr] + ([br] if bias else []), dy.float())
+    for a, r_ in [(gx, rx), (gw, rw)] + ([(gb[0], rb[0])] if bias else []):
+        e = ((a.float() - r_).norm() / (r_.norm() + 1e-12)).item()
+        assert e < 2e-2, e
