@@ -30,10 +30,13 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# measured first-party baseline (stock PyTorch-ROCm eager, 1x MI355X, same config);
-# see BASELINE.md and profiles/r1_bench_torch_miopen.log (MIOpen Conv3d/BN/pool,
-# bf16, batch 128, 64^3, 24 classes).  vs_baseline = value / (this * n_gpus).
-TORCH_BASELINE_SAMPLES_PER_S_PER_GPU = 106.8
+# measured first-party baseline: stock PyTorch-ROCm eager on 1x MI355X, same config (bf16
+# autocast, channels-last, MIOpen find mode via torch.backends.cudnn.benchmark so MIOpen
+# times its solvers and keeps the fastest): `python bench.py --impl torch --torch-find`,
+# profiles/r2_bench_torch_miopen_find.log.  (Round 1 quoted 106.8 samples/s from MIOpen's
+# no-find fallback path -- a pathological baseline, withdrawn.)  The reference itself
+# publishes no number (BASELINE.json "published": {}).  vs_baseline = value / (this * n_gpus).
+TORCH_BASELINE_SAMPLES_PER_S_PER_GPU = 6100.15
 
 
 def parse():
@@ -62,6 +65,10 @@ def parse():
     ap.add_argument("--torch-find", action="store_true",
                     help="stock-PyTorch baseline: torch.backends.cudnn.benchmark (MIOpen find: times every "
                          "applicable solver per shape during warmup and keeps the fastest)")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="native path: replay the whole training step (forward, backward, bucketed "
+                         "all-reduce, Adam) as one captured hipGraph; auto = on for 1 rank and for RCCL "
+                         "ranks (falls back to eager when any rank fails to capture)")
     ap.add_argument("--force-allreduce", action="store_true",
                     help="create the process group even at 1 rank and issue the bucketed all-reduces "
                          "(exercises the RCCL path from the gradient hooks on a 1-GPU box)")
@@ -176,9 +183,14 @@ def main():
             scale = bucketer.finish()
             opt.step(grad_scale=scale)
             return loss
+        graph_on = use_cuda and (args.graph == "on" or (args.graph == "auto" and backend != "gloo"))
+        if graph_on:
+            opt.enable_device_state()
+            opt.sync_device_state(grad_scale=1.0 / world if bucketer.active else 1.0)
         model_name = "FeatureNet-3D" if args.model == "cls" else "FeatureNet-3D-Seg (per-voxel head)"
         flops = model.train_flops_per_sample() if hasattr(model, "train_flops_per_sample") else None
     else:
+        graph_on = False
         from bench.torch_baseline import TorchFeatureNet3D
 
         if args.torch_find:
@@ -218,6 +230,38 @@ def main():
     for i in range(args.warmup):
         step(i)
     sync()
+    graph_used = False
+    if graph_on:
+        # capture one step on static input buffers (the eager warmup above already ran the
+        # per-shape kernel selection); every timed step = copy the batch in + one replay
+        sx, sy = xs[0].clone(), ys[0].clone()
+        g = torch.cuda.CUDAGraph()
+        ok = True
+        try:
+            with torch.cuda.graph(g):
+                flat.zero_grad()
+                gl = softmax_xent(model(sx), sy)
+                gl.backward()
+                bucketer.finish()
+                opt.step_device()
+        except Exception as ex:  # noqa: BLE001 - report and fall back to eager steps
+            print(f"bench.py rank {rank}: step capture failed, eager steps: {ex}", file=sys.stderr)
+            bucketer.reset()
+            ok = False
+        if dist.is_initialized():
+            f = torch.tensor([1.0 if ok else 0.0], device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok = bool(f.item() > 0.5)
+        if ok:
+            graph_used = True
+
+            def step(i):
+                sx.copy_(xs[i % args.pool])
+                sy.copy_(ys[i % args.pool])
+                g.replay()
+                opt.t += 1
+                return gl
+        sync()
     t0 = time.perf_counter()
     loss = None
     for i in range(args.steps):
@@ -266,7 +310,7 @@ def main():
                 "classes": NC,
                 "parallelism": f"dp{world}",
                 "impl": args.impl,
-                "optimizer": "adam",
+                "optimizer": "adam", "graph": graph_used,
             },
             "final_loss": None if loss is None else round(float(loss.detach()), 4),
         }

@@ -65,21 +65,31 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
     wr[j] = w + (long long)(cok[j] ? n : 0) * K;
   }
   const bf16x8 zero8 = {};
-  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+  // one k-step of operands in flight ahead of the MFMAs (raw loads; conversion and masking
+  // happen when the step is consumed)
+  bf16x8 ra[2];
+  float4 rb[4][2];
+  auto load = [&](int k0) {
     const int k = k0 + 8 * gq;
-    const bool kok = k < kend;                   // kend % 8 == 0 (K % 8 == 0, kc % 32 == 0)
-    bf16x8 fa[2], fb[4];
+    const int ks = k < kend ? k : 0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bf16x8 v = *(const bf16x8*)(xr[i] + (kok ? k : 0));
-      fa[i] = (rok[i] && kok) ? v : zero8;
-    }
+    for (int i = 0; i < 2; ++i) ra[i] = *(const bf16x8*)(xr[i] + ks);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float4* p = (const float4*)(wr[j] + (kok ? k : 0));
-      const bf16x8 v = dn_cvt8(p[0], p[1]);
-      fb[j] = (cok[j] && kok) ? v : zero8;
+      const float4* p = (const float4*)(wr[j] + ks);
+      rb[j][0] = p[0];
+      rb[j][1] = p[1];
     }
+  };
+  if (kbeg < kend) load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += 32) {
+    const bool kok = k0 + 8 * gq < kend;        // kend % 8 == 0 (K % 8 == 0, kc % 32 == 0)
+    bf16x8 fa[2], fb[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[i] = (rok[i] && kok) ? ra[i] : zero8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[j] = (cok[j] && kok) ? dn_cvt8(rb[j][0], rb[j][1]) : zero8;
+    if (k0 + 32 < kend) load(k0 + 32);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -100,20 +110,41 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
     }
 }
 
-// y[m][n] = act(sum_s part[s][m][n] + b[n]); bf16 or fp32 output
+// y[m][n] = act(sum_s part[s][m][n] + b[n]); bf16 or fp32 output.  A workgroup takes 64
+// outputs; its 4 waves sum every 4th slice (coalesced 256-B rows, 4 loads in flight per
+// lane) and combine through LDS -- one thread per output with a serial walk over hundreds
+// of slices left FC1's reduction latency-bound (59 us for 16 MB)
 __global__ __launch_bounds__(DN_THREADS) void dense_fwd_reduce_kernel(const float* __restrict__ part,
                                                                       const float* __restrict__ bias, void* out,
                                                                       int M, int N, int S, int act, int out_fp32) {
-  const long long i = (long long)blockIdx.x * DN_THREADS + threadIdx.x;
-  if (i >= (long long)M * N) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long MN = (long long)M * N;
+  const long long i = (long long)blockIdx.x * 64 + lane;
   float v = 0.f;
-  for (int s = 0; s < S; ++s) v += part[(long long)s * M * N + i];
-  if (bias) v += bias[i % N];
-  v = act_fwd(v, act);
-  if (out_fp32) {
-    ((float*)out)[i] = v;
-  } else {
-    ((bf16*)out)[i] = f2bf(v);
+  if (i < MN) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int s = wave;
+    for (; s + 12 < S; s += 16) {
+      a0 += part[(long long)s * MN + i];
+      a1 += part[(long long)(s + 4) * MN + i];
+      a2 += part[(long long)(s + 8) * MN + i];
+      a3 += part[(long long)(s + 12) * MN + i];
+    }
+    for (; s < S; s += 4) a0 += part[(long long)s * MN + i];
+    v = (a0 + a1) + (a2 + a3);
+  }
+  red[wave][lane] = v;
+  __syncthreads();
+  if (wave == 0 && i < MN) {
+    v = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (bias) v += bias[i % N];
+    v = act_fwd(v, act);
+    if (out_fp32) {
+      ((float*)out)[i] = v;
+    } else {
+      ((bf16*)out)[i] = f2bf(v);
+    }
   }
 }
 
@@ -276,8 +307,8 @@ extern "C" int fn_dense_fwd(const void* x, const float* w, const float* bias, vo
                      (const bf16*)x, w, part, M, N, K, kc);
   FN_CHECK_LAUNCH();
   const long long tot = (long long)M * N;
-  hipLaunchKernelGGL(dense_fwd_reduce_kernel, dim3((unsigned)((tot + DN_THREADS - 1) / DN_THREADS)),
-                     dim3(DN_THREADS), 0, st, (const float*)part, bias, out, M, N, Sr, act, out_fp32);
+  hipLaunchKernelGGL(dense_fwd_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(DN_THREADS), 0, st,
+                     (const float*)part, bias, out, M, N, Sr, act, out_fp32);
   FN_CHECK_LAUNCH();
   return 0;
 }
