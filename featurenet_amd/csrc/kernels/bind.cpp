@@ -34,6 +34,10 @@ int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
 int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, int*, hipStream_t);
 int fn_s2d_pack(const void*, void*, const int*, hipStream_t);
 int fn_dense_splits(int, int, int);
+int fn_ew_binary(const void*, const void*, void*, long long, int, hipStream_t);
+int fn_ew_mul_bwd(const void*, const void*, const void*, void*, void*, long long, hipStream_t);
+int fn_concat2(void*, void*, void*, long long, int, int, int, hipStream_t);
+int fn_pad3(void*, void*, const int*, int, hipStream_t);
 int fn_dense_fwd(const void*, const float*, const float*, void*, float*, int, int, int, int, int, int, hipStream_t);
 int fn_dense_dgrad(const void*, const float*, void*, int, int, int, hipStream_t);
 int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, hipStream_t);
@@ -197,6 +201,22 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {
     chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K, T, C, mode, stage_k, S(st)), "halo_pack_w");
+  });
+  m.def("ew_binary", [](uintptr_t a, uintptr_t b, uintptr_t out, long long n, int op, uintptr_t st) {
+    chk(fn_ew_binary(P<const void*>(a), P<const void*>(b), P<void*>(out), n, op, S(st)), "ew_binary");
+  });
+  m.def("ew_mul_bwd", [](uintptr_t g, uintptr_t a, uintptr_t b, uintptr_t da, uintptr_t db, long long n,
+                         uintptr_t st) {
+    chk(fn_ew_mul_bwd(P<const void*>(g), P<const void*>(a), P<const void*>(b), P<void*>(da), P<void*>(db), n, S(st)),
+        "ew_mul_bwd");
+  });
+  m.def("concat2", [](uintptr_t a, uintptr_t b, uintptr_t out, long long outer, int ia, int ib, int dir,
+                      uintptr_t st) {
+    chk(fn_concat2(P<void*>(a), P<void*>(b), P<void*>(out), outer, ia, ib, dir, S(st)), "concat2");
+  });
+  m.def("pad3", [](uintptr_t x, uintptr_t out, std::vector<int> geom, int dir, uintptr_t st) {
+    need(geom, 8, "pad3");
+    chk(fn_pad3(P<void*>(x), P<void*>(out), geom.data(), dir, S(st)), "pad3");
   });
   m.def("dense_splits", &fn_dense_splits);
   m.def("dense_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t part, int M, int N, int K,

@@ -134,6 +134,32 @@ class _Builder:
         self.params = sum(c[0] for c in cost)
         self.flops = sum(c[1] for c in cost)
         self.layers = 1 + sum(c[2] for c in cost)
+        self.fold_pads()
+
+    def fold_pads(self) -> None:
+        """ZeroPadding2D whose only consumer is a convolution: the convolution takes the
+        padding into its own (zero) border instead and the pad becomes an alias of its input
+        -- no padded tensor is materialised.  The instruction stays (Keras counts the
+        ZeroPadding layer in ``nb_layers``)."""
+        from ..models.layers import Conv
+
+        users: dict = {}
+        for j, (kind, arg, ins) in enumerate(self.prog):
+            for i in ins:
+                users.setdefault(i, []).append(j)
+        for i, (kind, arg, ins) in enumerate(self.prog):
+            if kind != "pad" or len(users.get(i, [])) != 1:
+                continue
+            j = users[i][0]
+            jk, ja, jins = self.prog[j]
+            if jk != "module" or jins != (i,) or not isinstance(self.mods[ja], Conv):
+                continue
+            conv = self.mods[ja]
+            if getattr(conv, "extra_pad", (0, 0, 0)) != (0, 0, 0):
+                continue
+            ph, pw = arg
+            conv.extra_pad = (0, ph, pw)
+            self.prog[i] = ("alias", None, ins)
 
     # ----------------------------------------------------------------- layers
     def conv(self, x: Sym, features: int, kernel, stride, padding: str, act, ctype: str) -> Sym:
@@ -406,15 +432,19 @@ class CandidateNet(nn.Module):
                 vals[i] = ops.activation(vals[ins[0]], arg)
             elif kind == "dropout":
                 vals[i] = ops.dropout(vals[ins[0]], arg, self.training)
+            elif kind == "alias":
+                vals[i] = vals[ins[0]]
             elif kind == "pad":
                 ph, pw = arg
-                vals[i] = torch.nn.functional.pad(vals[ins[0]], (0, 0, pw, pw, ph, ph))
+                v = vals[ins[0]]
+                n, h, w, c = v.shape
+                vals[i] = ops.zero_pad(v.reshape(n, 1, h, w, c), (0, ph, pw)).reshape(n, h + 2 * ph, w + 2 * pw, c)
             elif kind == "add":
-                vals[i] = vals[ins[0]] + vals[ins[1]]
+                vals[i] = ops.add(vals[ins[0]], vals[ins[1]])
             elif kind == "mul":
-                vals[i] = vals[ins[0]] * vals[ins[1]]
+                vals[i] = ops.multiply(vals[ins[0]], vals[ins[1]])
             elif kind == "concat":
-                vals[i] = torch.cat([vals[ins[0]], vals[ins[1]]], dim=arg)
+                vals[i] = ops.concat([vals[ins[0]], vals[ins[1]]], arg)
             else:  # pragma: no cover
                 raise RuntimeError(f"bad instruction {kind}")
         return vals[-1]

@@ -67,7 +67,8 @@ class Conv(nn.Module):
     def specs(self, shape5):
         s = self._spec_cache.get(shape5)
         if s is None:
-            cs = ConvSpec.make(shape5, self.cout, self.kernel, self.stride, self.padding, self.dilation)
+            cs = ConvSpec.make(shape5, self.cout, self.kernel, self.stride, self.padding, self.dilation,
+                               extra=getattr(self, "extra_pad", (0, 0, 0)))
             ps = None
             if self.pool is not None:
                 ps = PoolSpec.make(cs.out_shape5, self.pool, self.pool_stride, self.pool_padding)

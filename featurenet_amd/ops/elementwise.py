@@ -5,9 +5,11 @@ Reference parity: ``Activation`` (``model/operation.py:152-165``), ``Dropout``
 ``ZeroPadding2D`` (``:116-137``), ``K.zeros`` (``model/input.py:159-165``).
 
 GPU: activation fwd/bwd and dropout (counter-hash mask regenerated in
-backward, never stored) are native kernels; add/multiply/concat/pad are
-memory-bound one-liners that torch already runs as single vectorised kernels
-on the channels-last layout (concat = write-into-slice).
+backward, never stored) are native kernels, and so are add / multiply (fused
+multiply backward), two-way concat (each input written into its column range)
+and zero padding (border + interior in one pass) -- ``csrc/kernels/combine.hip``.
+A ZeroPadding whose only consumer is a convolution is folded into that
+convolution's padding by the IR compiler instead (no padded tensor at all).
 """
 from __future__ import annotations
 
@@ -82,21 +84,116 @@ def dropout(x: torch.Tensor, p: float, training: bool, generator: random.Random 
     return torch.nn.functional.dropout(x, p, True)
 
 
+def _native_pair(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return _native.use_native(a) and a.shape == b.shape and a.is_cuda and b.is_cuda
+
+
+class BinaryFn(torch.autograd.Function):
+    """out = a + b (op 0) or a * b (op 1), bf16, one pass (``ew_binary``)."""
+
+    @staticmethod
+    def forward(ctx, a, b, op: int):
+        ab, bb = a.to(torch.bfloat16).contiguous(), b.to(torch.bfloat16).contiguous()
+        out = torch.empty_like(ab)
+        _native.kernels().ew_binary(ab.data_ptr(), bb.data_ptr(), out.data_ptr(), ab.numel(), op, _native.stream(ab))
+        ctx.op = op
+        if op == 1:
+            ctx.save_for_backward(ab, bb)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.op == 0:
+            return g, g, None
+        ab, bb = ctx.saved_tensors
+        g = g.to(torch.bfloat16).contiguous()
+        da, db = torch.empty_like(g), torch.empty_like(g)
+        _native.kernels().ew_mul_bwd(g.data_ptr(), ab.data_ptr(), bb.data_ptr(), da.data_ptr(), db.data_ptr(),
+                                     g.numel(), _native.stream(g))
+        return da, db, None
+
+
 def add(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Keras ``Add`` of two branches (native one-pass kernel on GPU)."""
+    if _native_pair(a, b):
+        return BinaryFn.apply(a, b, 0)
     return a + b
 
 
 def multiply(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Keras ``Multiply`` (native forward and one-pass fused backward on GPU)."""
+    if _native_pair(a, b):
+        return BinaryFn.apply(a, b, 1)
     return a * b
 
 
+class Concat2Fn(torch.autograd.Function):
+    """Two tensors joined along ``axis``: each input is written into its column range of the
+    output (``concat2``); the backward splits the gradient with the same kernel."""
+
+    @staticmethod
+    def forward(ctx, a, b, axis: int):
+        ab, bb = a.to(torch.bfloat16).contiguous(), b.to(torch.bfloat16).contiguous()
+        shape = list(ab.shape)
+        shape[axis] += bb.shape[axis]
+        out = torch.empty(shape, dtype=torch.bfloat16, device=ab.device)
+        outer = 1
+        for d in ab.shape[:axis]:
+            outer *= d
+        ia, ib = ab.numel() // outer, bb.numel() // outer
+        _native.kernels().concat2(ab.data_ptr(), bb.data_ptr(), out.data_ptr(), outer, ia, ib, 0, _native.stream(ab))
+        ctx.meta = (ab.shape, bb.shape, outer, ia, ib)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        sa, sb, outer, ia, ib = ctx.meta
+        g = g.to(torch.bfloat16).contiguous()
+        da = torch.empty(sa, dtype=torch.bfloat16, device=g.device)
+        db = torch.empty(sb, dtype=torch.bfloat16, device=g.device)
+        _native.kernels().concat2(da.data_ptr(), db.data_ptr(), g.data_ptr(), outer, ia, ib, 1, _native.stream(g))
+        return da, db, None
+
+
 def concat(tensors, axis: int) -> torch.Tensor:
+    tensors = list(tensors)
+    if len(tensors) == 2 and _native.use_native(tensors[0]) and tensors[0].is_cuda and tensors[1].is_cuda:
+        a, b = tensors
+        ax = axis % a.dim()
+        if a.dim() == b.dim() and all(a.shape[i] == b.shape[i] for i in range(a.dim()) if i != ax):
+            return Concat2Fn.apply(a, b, ax)
     return torch.cat(tensors, dim=axis)
+
+
+class Pad3Fn(torch.autograd.Function):
+    """Zero padding of a channels-last [N, D, H, W, C] grid (``pad3``: border and interior in
+    one pass; the backward crops the interior)."""
+
+    @staticmethod
+    def forward(ctx, x5, pads):
+        xb = x5.to(torch.bfloat16).contiguous()
+        N, D, H, W, C = xb.shape
+        pd, ph, pw = pads
+        out = torch.empty(N, D + 2 * pd, H + 2 * ph, W + 2 * pw, C, dtype=torch.bfloat16, device=xb.device)
+        geom = [N, D, H, W, C, pd, ph, pw]
+        _native.kernels().pad3(xb.data_ptr(), out.data_ptr(), geom, 0, _native.stream(xb))
+        ctx.geom = geom
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        N, D, H, W, C = ctx.geom[:5]
+        g = g.to(torch.bfloat16).contiguous()
+        dx = torch.empty(N, D, H, W, C, dtype=torch.bfloat16, device=g.device)
+        _native.kernels().pad3(dx.data_ptr(), g.data_ptr(), ctx.geom, 1, _native.stream(g))
+        return dx, None
 
 
 def zero_pad(x5: torch.Tensor, pads) -> torch.Tensor:
     """Zero-pad spatial dims of a 5-D channels-last tensor; pads = (d, h, w) per side."""
     pd, ph, pw = pads
+    if _native.use_native(x5) and x5.is_cuda and x5.dim() == 5:
+        return Pad3Fn.apply(x5, (pd, ph, pw))
     return torch.nn.functional.pad(x5, (0, 0, pw, pw, ph, ph, pd, pd))
 
 

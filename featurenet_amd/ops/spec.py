@@ -75,8 +75,15 @@ class ConvSpec:
     OW: int = 0
 
     @staticmethod
-    def make(x_shape5, cout: int, kernel, stride=1, padding="valid", dilation=1) -> "ConvSpec":
+    def make(x_shape5, cout: int, kernel, stride=1, padding="valid", dilation=1, extra=(0, 0, 0)) -> "ConvSpec":
+        """``extra``: zero padding (per side, per dim) folded in from a preceding ZeroPadding
+        layer: the conv behaves as on the input padded by it, then padded by ``padding``."""
         N, D, H, W, C = x_shape5
+        if any(extra):
+            pe = ConvSpec.make((N, D + 2 * extra[0], H + 2 * extra[1], W + 2 * extra[2], C), cout, kernel, stride,
+                               padding, dilation)
+            return ConvSpec(N, D, H, W, C, cout, pe.KD, pe.KH, pe.KW, pe.sd, pe.sh, pe.sw, pe.pd + extra[0],
+                            pe.ph + extra[1], pe.pw + extra[2], pe.dd, pe.dh, pe.dw, pe.OD, pe.OH, pe.OW)
         KD, KH, KW = _triple(kernel)
         sd, sh, sw = _triple(stride)
         dd, dh, dw = _triple(dilation)

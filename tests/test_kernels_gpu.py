@@ -749,3 +749,33 @@ def test_dense_native_matches_fp32(M, K, N, act, bias):
     for a, r_ in [(gx, rx), (gw, rw)] + ([(gb[0], rb[0])] if bias else []):
         e = ((a.float() - r_).norm() / (r_.norm() + 1e-12)).item()
         assert e < 2e-2, e
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 5, 7, 16), (3, 1, 4, 6, 5)])
+def test_combine_kernels_match_torch(shape):
+    """Native add / multiply (+fused backward), two-way concat (+split) and zero padding
+    (+crop) vs torch on bf16 channels-last tensors (vector and scalar paths)."""
+    from featurenet_amd.ops import elementwise as ew
+
+    torch.manual_seed(0)
+    a = torch.randn(shape, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    b = torch.randn(shape, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    g = torch.randn(shape, device="cuda").to(torch.bfloat16)
+    for fn, ref_fn in ((ew.add, torch.add), (ew.multiply, torch.mul)):
+        y = fn(a, b)
+        assert torch.equal(y, ref_fn(a.detach(), b.detach()))
+        ga, gb = torch.autograd.grad(y, [a, b], g)
+        ra, rb = torch.autograd.grad(ref_fn(a, b), [a, b], g)
+        assert torch.equal(ga, ra) and torch.equal(gb, rb)
+    for ax in (1, 4):
+        y = ew.concat([a, b], ax)
+        assert torch.equal(y, torch.cat([a.detach(), b.detach()], ax))
+        gy = torch.randn(y.shape, device="cuda").to(torch.bfloat16)
+        ga, gb = torch.autograd.grad(y, [a, b], gy)
+        assert torch.equal(ga, gy.narrow(ax, 0, shape[ax])) and torch.equal(gb, gy.narrow(ax, shape[ax], shape[ax]))
+    y = ew.zero_pad(a, (1, 2, 0))
+    ref = torch.nn.functional.pad(a.detach(), (0, 0, 0, 0, 2, 2, 1, 1))
+    assert torch.equal(y, ref)
+    gy = torch.randn(y.shape, device="cuda").to(torch.bfloat16)
+    (ga,) = torch.autograd.grad(y, [a], gy)
+    assert torch.equal(ga, gy[:, 1:-1, 2:-2, :, :])

@@ -170,3 +170,22 @@ def test_reference_ops_gradcheck_fp64():
     logits = torch.randn(5, 7, dtype=d, requires_grad=True)
     y = torch.randint(0, 7, (5,))
     assert gradcheck(lambda l: R.softmax_xent(l, y, 0.1), (logits,))
+
+
+def test_conv_spec_extra_padding_equals_padded_input():
+    """A ZeroPadding folded into the next conv (``ConvSpec.make(..., extra=...)``) computes the
+    same as the conv over the explicitly padded input."""
+    import torch
+
+    from featurenet_amd.ops import reference as refops
+    from featurenet_amd.ops.spec import ConvSpec
+
+    torch.manual_seed(0)
+    x = torch.randn(2, 1, 9, 11, 8)
+    w = torch.randn(16, 1, 3, 3, 8)
+    for padding in ("valid", "same"):
+        xp = torch.nn.functional.pad(x, (0, 0, 2, 2, 1, 1))
+        s_pad = ConvSpec.make(tuple(xp.shape), 16, (1, 3, 3), 1, padding)
+        s_fold = ConvSpec.make(tuple(x.shape), 16, (1, 3, 3), 1, padding, extra=(0, 1, 2))
+        assert (s_fold.OD, s_fold.OH, s_fold.OW) == (s_pad.OD, s_pad.OH, s_pad.OW)
+        torch.testing.assert_close(refops.conv(x, w, None, s_fold), refops.conv(xp, w, None, s_pad))
