@@ -418,11 +418,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
               ts[j] = ct_sum16(ts[j]);
               tq[j] = ct_sum16(tq[j]);
             }
-            if (lr == 0) {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                atomicAdd(&s_red[wave * 64 + 8 * lg + j], ts[j]);
-                atomicAdd(&s_red[wave * 64 + 32 + 8 * lg + j], tq[j]);
+            if (lr == 0) {                       // one lane per column of this wave's row: plain
+#pragma unroll                                   // adds, a fixed summation order (deterministic
+              for (int j = 0; j < 8; ++j) {      // statistics, run to run)
+                s_red[wave * 64 + 8 * lg + j] += ts[j];
+                s_red[wave * 64 + 32 + 8 * lg + j] += tq[j];
               }
             }
           }

@@ -67,8 +67,12 @@ def _worker(rank, tmp):
         dist.destroy_process_group()
 
 
-def test_dp_two_ranks_one_gpu_matches_single_process(tmp_path):
+def test_dp_two_ranks_one_gpu_matches_single_process(tmp_path, monkeypatch):
     from featurenet_amd import _native
+
+    # conv kernels by fixed rule, not by per-process timing (two processes sharing the card
+    # time them differently and may pick different, bf16-rounding-different kernels)
+    monkeypatch.setenv("FN_CONV_TILE", "2")
 
     assert _native.kernels_available(), "HIP kernel library (_C) must be built and loadable on the GPU box"
     mp.start_processes(_worker, args=(str(tmp_path),), nprocs=WORLD, start_method="spawn")
