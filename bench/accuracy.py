@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--lr", type=float, default=1e-3)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--fp8", action="store_true",
+                    help="also quantise the trained model to fp8 (inference/fp8.py) and report its held-out top-1")
     a = ap.parse_args()
 
     import featurenet_amd as fn
@@ -82,9 +84,39 @@ def main():
     if rank == 0:
         labels, _ = fn.classify(ckpt, ds.x_test, packed_size=a.size)
         out["classify_roundtrip_acc"] = round(float((labels == np.asarray(ds.y_test)).mean()), 4)
+        if a.fp8:
+            out["fp8"] = fp8_parity(res.model, ds, a.size)
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+@torch.no_grad()
+def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict:
+    """Post-training fp8 quantisation of the trained model (activation scales calibrated on
+    ``calib`` training samples), then held-out top-1 of fp8 vs bf16 and their agreement."""
+    from featurenet_amd.inference.fp8 import quantize_model
+    from featurenet_amd.training.data import unpack_voxels
+
+    dev = next(model.parameters()).device
+    model.eval()
+
+    def batch(xs, i, n):
+        xb = torch.as_tensor(np.asarray(xs[i:i + n])).to(dev)
+        return unpack_voxels(xb, size).to(torch.bfloat16)
+
+    q = quantize_model(model, batch(ds.x_train, 0, calib))
+    y = np.asarray(ds.y_test)
+    pb, pq = [], []
+    for i in range(0, len(y), chunk):
+        xb = batch(ds.x_test, i, chunk)
+        pb.append(model(xb).float().argmax(-1).cpu())
+        pq.append(q(xb).float().argmax(-1).cpu())
+    pb, pq = torch.cat(pb).numpy(), torch.cat(pq).numpy()
+    acc_b, acc_q = float((pb == y).mean()), float((pq == y).mean())
+    return {"top1_bf16": round(acc_b, 4), "top1_fp8": round(acc_q, 4), "drop_pt": round(100 * (acc_b - acc_q), 2),
+            "agreement": round(float((pb == pq).mean()), 4), "calib_samples": calib,
+            "kernel": "conv_halo_f8 (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3)"}
 
 
 if __name__ == "__main__":

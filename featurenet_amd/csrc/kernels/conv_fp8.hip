@@ -5,7 +5,9 @@
 // taps per MFMA k-step, weights streamed through a double-buffered 128-k LDS
 // stage -- but every operand byte is fp8, so the halo, the weight stages and
 // every LDS fragment read are half the size of the bf16 kernel's (the bf16
-// kernel is LDS-bandwidth-bound) and MFMA runs mfma_f32_16x16x32_fp8_fp8.
+// kernel is LDS-bandwidth-bound) and MFMA runs the CDNA4 block-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 (k = 128 per instruction, twice the bf16 MFMA
+// rate; the older mfma_f32_16x16x32_fp8_fp8 runs at the bf16 rate).
 // Dequantisation is one multiply in the epilogue:
 //   y = act(acc * scale[co] + bias[co])     scale[co] = s_x * s_w[co]
 // and the result is either re-quantised to fp8 (y * inv_out_scale, saturated
@@ -21,7 +23,10 @@ struct F8Geom {
 };
 
 #define F8_BM 256
-#define F8_BK 128   // k (bytes) per weight stage: 8 taps x 16 channels
+#define F8_BK 128   // k (bytes) per weight stage: 8 taps x 16 channels = one MFMA k-step
+#define F8_UNIT_SCALE 127   // E8M0 exponent of 1.0
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ unsigned char f32_to_fp8(float v) {
   v = fminf(fmaxf(v, -448.f), 448.f);
@@ -134,27 +139,35 @@ __global__ __launch_bounds__(256, 2) void conv_halo_f8_kernel(const unsigned cha
     const bool more = q + 1 < nq;
     if (more) load_b(q + 1);
     const unsigned char* b = Bs + (q & 1) * B_STAGE;
-    const int* tp = toffs_s + (q % spp) * 8 + (lg >> 1);
+    // one block-scaled MFMA per (mt, nt) covers the whole 128-byte stage: lane group
+    // lg holds k = 32 lg .. 32 lg + 31 = taps 2 lg, 2 lg + 1 of the stage's 8, all 16
+    // channels of each (two 16-B halo reads per row block, two swizzled 16-B chunks of
+    // the weight row)
+    const int* tp = toffs_s + (q % spp) * 8 + 2 * lg;
+    const int to0 = tp[0], to1 = tp[1];
+    i32x8 fa[4], fb[NT];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int toff = tp[ks * 2];
-      long fa[4], fb[NT];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        fa[mt] = *(const long*)(halo + (size_t)(hbase[mt] + toff) * 16 + (lg & 1) * 8);
-      const int chunk = ks * 2 + (lg >> 1);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const int r = nt * 16 + lr;
-        fb[nt] = *(const long*)(b + r * F8_BK + ((chunk ^ (r & 7)) << 4) + (lg & 1) * 8);
-      }
-      // branch-free: rows past the tile compute on a valid halo position and are dropped
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0);
+    for (int mt = 0; mt < 4; ++mt) {
+      const uint4 lo = *(const uint4*)(halo + (size_t)(hbase[mt] + to0) * 16);
+      const uint4 hi = *(const uint4*)(halo + (size_t)(hbase[mt] + to1) * 16);
+      fa[mt] = (i32x8){(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
     }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int r = nt * 16 + lr;
+      const uint4 lo = *(const uint4*)(b + r * F8_BK + (((2 * lg) ^ (r & 7)) << 4));
+      const uint4 hi = *(const uint4*)(b + r * F8_BK + (((2 * lg + 1) ^ (r & 7)) << 4));
+      fb[nt] = (i32x8){(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+    // branch-free: rows past the tile compute on a valid halo position and are dropped.
+    // Formats 0/0 = e4m3 x e4m3; E8M0 block scales 127 = 2^0 (the per-channel
+    // dequantisation stays one multiply in the epilogue)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[mt], fb[nt], acc[mt][nt], 0, 0, 0,
+                                                                         F8_UNIT_SCALE, 0, F8_UNIT_SCALE);
     __syncthreads();
     if (more) {
       write_b((q + 1) & 1);

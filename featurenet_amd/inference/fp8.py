@@ -7,7 +7,7 @@ Post-training quantisation, inference only:
 * activations between layers are quantised per tensor with scales calibrated
   from a bf16 forward pass (``amax / 448`` of each layer's post-ReLU output);
 * conv2..conv4 run ``conv_halo_f8`` (``csrc/kernels/conv_fp8.hip``): fp8
-  halo tiles in LDS, ``mfma_f32_16x16x32_fp8_fp8``, dequantise + bias + ReLU
+  halo tiles in LDS, block-scaled ``mfma_scale_f32_16x16x128_f8f6f4``, dequantise + bias + ReLU
   (+ requantise to fp8) in the epilogue.  conv1 (1-channel, stride 2) stays on
   the bf16 implicit-GEMM kernel with the folded BN + ReLU fused, followed by
   one quantisation pass; conv4 writes bf16 for the max-pool and the two dense
