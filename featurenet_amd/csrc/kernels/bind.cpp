@@ -70,6 +70,9 @@ int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                  const int*, int, int, int, int, int*, hipStream_t);
 int fn_conv_tile_workers(const int*, int, int);
+int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
+                    float, const int*, int, int, int, int, int*, hipStream_t);
+int fn_conv_tile_f8_supported(int, int, int);
 int fn_tile_pack_w(const float*, void*, int, int, int, int, int, int, int, int, hipStream_t);
 }
 
@@ -190,6 +193,25 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>());
+  m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
+                           uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,
+                           int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext) {
+    need(geom, 26, "conv_tile_f8");
+    if (geom[4] <= 0 || ncol <= 0 || geom[17] <= 0 || geom[4] % geom[17])
+      throw std::runtime_error("conv_tile_f8: bad slice");
+    fits(ext, 0, prod({geom[0], geom[1], geom[2], geom[3], geom[4]}), "conv_tile_f8", "src");
+    fits(ext, 1, prod({geom[4] / geom[17] * geom[19] + 4, geom[20], 64, 32}), "conv_tile_f8", "wpk");
+    fits(ext, 2, prod({geom[0], geom[5], geom[6], geom[7], ncol}), "conv_tile_f8", "out");
+    fits(ext, 3, 4LL * MT * 16, "conv_tile_f8", "rowtab");
+    fits(ext, 4, geom[19] + 6LL, "conv_tile_f8", "ktab");
+    chk(fn_conv_tile_f8(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
+                        P<const void*>(zp), P<const float*>(scale), P<const float*>(bias), P<void*>(out), oscale,
+                        geom.data(), ncol, relu, MT, NT, P<int*>(sched), S(st)),
+        "conv_tile_f8");
+  }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("scale"),
+     py::arg("bias"), py::arg("out"), py::arg("oscale"), py::arg("geom"), py::arg("ncol"), py::arg("relu"),
+     py::arg("MT"), py::arg("NT"), py::arg("st"), py::arg("sched"), py::arg("ext") = std::vector<long long>());
+  m.def("conv_tile_f8_supported", &fn_conv_tile_f8_supported);
   m.def("conv_tile_workers", [](std::vector<int> geom, int ncol, int NT) {
     need(geom, 26, "conv_tile_workers");
     return fn_conv_tile_workers(geom.data(), ncol, NT);

@@ -110,20 +110,37 @@ __device__ __forceinline__ unsigned ct_lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-template <int MT, int NT, int CPP, int DBG = 0>
-__global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __restrict__ src,
+typedef int ct_i32x8 __attribute__((ext_vector_type(8)));
+
+// B-ring depth (k-steps in flight): a bf16 k-step is MT*NT 16-cycle MFMAs, an fp8 one
+// MT*NT 32-cycle block-scaled MFMAs, so 2 fp8 steps cover the latency 4 bf16 steps do
+__host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : (NT == 2 ? 4 : 3); }
+
+// F8 = false: bf16 operands, v_mfma_f32_16x16x32_bf16, k-step 32; CPP = 16-B chunks (8
+//   channels) per halo position.
+// F8 = true (inference): OCP e4m3 halo and weights, v_mfma_scale_f32_16x16x128_f8f6f4 (unit
+//   block scales), k-step 128 = each lane group's 32 bytes: tap 4ks+lg x 32 channels (CS =
+//   32, CPP = 2 chunks of 16 channels) or tap 2ks+lg/2 x channels 32(lg&1).. (CS = 64, CPP =
+//   4); the epilogue dequantises (acc * scale[co] + bias[co]), applies ReLU and stores bf16
+//   or re-quantised e4m3 (x oscale).
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false>
+__global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
                                                                const int4* __restrict__ ktab,
-                                                               const bf16* __restrict__ zp,
-                                                               const float* __restrict__ bias, bf16* __restrict__ out,
+                                                               const unsigned char* __restrict__ zp,
+                                                               const float* __restrict__ bias, void* __restrict__ out,
                                                                float* __restrict__ stats, TileGeom g, int Ncol,
                                                                int act, int* __restrict__ sched,
-                                                               long long* __restrict__ stamps) {
+                                                               long long* __restrict__ stamps,
+                                                               const float* __restrict__ scale, float oscale) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  constexpr int PD = NT == 2 ? 4 : 3;            // B prefetch depth (k-steps in flight)
-  constexpr int LCPP = CPP == 2 ? 1 : (CPP == 4 ? 2 : 3);
+  constexpr int PD = ct_pd(NT, F8);
+  constexpr int ESZ = F8 ? 1 : 2;                // bytes per element of the source / weights
+  constexpr int FRAG = F8 ? 32 : 16;             // bytes per lane of one MFMA operand fragment
   static_assert(NT == 2, "column order and s_red assume 32-column blocks");
+  static_assert(!F8 || CPP == 2 || CPP == 4, "fp8: 32- or 64-channel slices");
+  using Frag = std::conditional_t<F8, ct_i32x8, bf16x8>;
 
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int HP = (g.TD + g.KD - 1) * HH * HW;
@@ -151,7 +168,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
   for (int p = tid; p < g.HPpad; p += CT_NTHR) {  // positions past HP repeat the last one
     const int pc = p < HP ? p : HP - 1;
     const int hd = pc / (HH * HW), hh = (pc / HW) % HH, hw = pc % HW;
-    s_pos[p] = make_int2(((hd * g.IH + hh) * g.IW + hw) * g.C * 2, (hd << 16) | (hh << 8) | hw);
+    s_pos[p] = make_int2(((hd * g.IH + hh) * g.IW + hw) * g.C * ESZ, (hd << 16) | (hh << 8) | hw);
   }
   // per compute lane: fragment row (output position) lr of each MFMA tile mt -- its LDS halo
   // offset lb (toggled between the buffers per job), its output offset relative to the
@@ -160,7 +177,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int2 rt = rowtab[((loader ? 0 : wave) * MT + mt) * 16 + lr];
-    lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;   // this lane group's plane
+    // this lane group's (first) plane
+    if constexpr (F8) lb[mt] = rt.x * 16 + (CPP == 4 ? 2 * (lg & 1) : 0) * PLANE;
+    else lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;
     const int tw = rt.y % g.TW, th = (rt.y / g.TW) % g.TH, td = rt.y / (g.TW * g.TH);
     roff[mt] = rt.y < 0 ? -1 : (td * g.OH + th) * g.OW + tw;
     rpk[mt] = (td << 16) | (th << 8) | tw;
@@ -183,13 +202,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
     const int dlo = td * g.TD - g.pd, hlo = th * g.TH - g.ph, wlo = tw * g.TW - g.pw;
     const bool interior = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID &&
                           hlo + HH <= g.IH && wlo + HW <= g.IW;
-    const bf16* base = src + (long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS;
+    const unsigned char* base = src + ((long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS) * ESZ;
     const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
     // position rows in batches of 8: the s_pos reads of a batch are in flight together
     // (one LDS latency per batch, not per DMA row)
     const int NR = g.HPpad >> 6;
     if (interior) {
-      const bf16* obase = base + ((long long)dlo * g.IH + hlo) * g.IW * g.C + (long long)wlo * g.C;
+      const unsigned char* obase = base + (((long long)dlo * g.IH + hlo) * g.IW + wlo) * g.C * ESZ;
       for (int r0 = 0; r0 < NR; r0 += 8) {
         int po[8];
 #pragma unroll
@@ -214,10 +233,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
             const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
             const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
                             (unsigned)gw < (unsigned)g.IW;
-            const bf16* gsrc = ok ? base + ((gd * g.IH + gh) * g.IW + gw) * g.C : zp;
+            const unsigned char* gsrc = ok ? base + (long long)((gd * g.IH + gh) * g.IW + gw) * g.C * ESZ : zp;
 #pragma unroll
             for (int c = 0; c < CPP; ++c)
-              ct_glds16(ok ? gsrc + c * 8 : zp, dst0 + (unsigned)(c * PLANE + ((r0 + i) << 10)));
+              ct_glds16(ok ? gsrc + c * 16 : zp, dst0 + (unsigned)(c * PLANE + ((r0 + i) << 10)));
           }
         }
       }
@@ -296,25 +315,37 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    bf16x8 fa[MT];                               // rotating: fragment mt of k-step k+1 is read right
+    Frag fa[MT];                                 // rotating: fragment mt of k-step k+1 is read right
                                                  // after the NT MFMAs of (mt, k) consumed it
-    bf16x8 fb[PD][NT];
+    Frag fb[PD][NT];
     // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
     // ct0*16 + 8lg + 4nt + r: a lane ends with 8 consecutive columns of one position
     const int gc8 = ct0 * 16 + 8 * lg;
-    float bias8[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) bias8[j] = (bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
-    const unsigned wstep = (unsigned)g.nct * 1024u;   // bytes per k-step of the packed weights
+    float bias8[8];                              // (fp8: re-read per tile in the epilogue, no live
+#pragma unroll                                   // registers across the k-loop)
+    for (int j = 0; j < 8; ++j) bias8[j] = (!F8 && bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
+    constexpr unsigned FTILE = 64u * FRAG;       // bytes of one 16-column fragment of a k-step
+    const unsigned wstep = (unsigned)g.nct * FTILE;   // bytes per k-step of the packed weights
     unsigned voffb[PD];                          // per-lane B offsets of the PD ring slots
 #pragma unroll
-    for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * 16u + (unsigned)u * wstep;
+    for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * FRAG + (unsigned)u * wstep;
     // weight loads are ordinary loads: hipcc counts them (vmcnt waits before the consuming
     // MFMAs, correct across its own register copies); the compute waves issue no hidden
     // VMEM, so its counts are exact
     auto load_b = [&](const unsigned char* base, int slot) {
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const bf16x8*)(base + voffb[slot] + nt * 1024);
+      for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const Frag*)(base + voffb[slot] + nt * FTILE);
+    };
+    // A fragment of row block mt at k-step offset ko: one 16-B read (bf16) or the lane
+    // group's two consecutive chunk planes (fp8)
+    auto read_a = [&](int mt, int ko) -> Frag {
+      if constexpr (F8) {
+        const uint4 lo = *(const uint4*)(dsm + lb[mt] + ko);
+        const uint4 hi = *(const uint4*)(dsm + lb[mt] + ko + PLANE);
+        return (ct_i32x8){(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      } else {
+        return *(const bf16x8*)(dsm + lb[mt] + ko);
+      }
     };
     // k-step offsets: s_kt[k][lg] = byte offset of the tap lane group lg reads in k-step k
     // (all four equal for CS >= 32, pairs for CS = 16, four taps for CS = 8).  Reading
@@ -323,11 +354,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
     // hoisted a turn's reads into a double-buffered block)
     auto kofs = [&](int k) -> int { return *((const int*)(s_kt + k) + lg); };
     // epilogue variant (wave-uniform); columns come in whole 8-column groups (Ncol % 8 == 0)
-    const int emode = (stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0);   // (ACT_NONE / ACT_RELU only)
+    // (fp8: bit 0 relu, bit 1 fp8 output)
+    const int emode = F8 ? ((act == ACT_RELU ? 1 : 0) | (oscale > 0.f ? 2 : 0))
+                         : ((stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0));   // (ACT_NONE / ACT_RELU only)
     // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
     // the previous job's last turn, so no job starts on an exposed L2 latency
 #pragma unroll
-    for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024, u);
+    for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * FTILE, u);
     int par = 0;
     while (true) {
       st_1 = stamp();
@@ -339,14 +372,14 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
       const int nslc = slice + 1 == nslice ? 0 : slice + 1;
       // ---- k-loop: MFMA + A reads + B loads, nothing else ----
       const unsigned char* wbase = reinterpret_cast<const unsigned char*>(wp) +
-                                   ((size_t)slice * nks * g.nct + ct0) * 1024 + PD * wstep;
+                                   ((size_t)slice * nks * g.nct + ct0) * FTILE + PD * wstep;
       // weights of the next job: its slice (slice 0 for a new tile, whatever the tile)
       const unsigned char* wnext =
-          reinterpret_cast<const unsigned char*>(wp) + ((size_t)nslc * nks * g.nct + ct0) * 1024;
+          reinterpret_cast<const unsigned char*>(wp) + ((size_t)nslc * nks * g.nct + ct0) * FTILE;
       {
         const int ko = kofs(0);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) fa[mt] = *(const bf16x8*)(dsm + lb[mt] + ko);
+        for (int mt = 0; mt < MT; ++mt) fa[mt] = read_a(mt, ko);
       }
       int ko_n = kofs(1);                        // offsets of the next k-step
       for (int ks = 0; ks < nks; ks += PD) {
@@ -358,9 +391,14 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-              acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0);
-            if constexpr (!(DBG & 2)) fa[mt] = *(const bf16x8*)(dsm + lb[mt] + ko);
+            for (int nt = 0; nt < NT; ++nt) {
+              if constexpr (F8)   // e4m3 x e4m3 (formats 0, 0), E8M0 scales 127 = 1.0
+                acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[u][nt], fa[mt], acc[mt][nt], 0, 0,
+                                                                                 0, 127, 0, 127);
+              else
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0);
+            }
+            if constexpr (!(DBG & 2)) fa[mt] = read_a(mt, ko);
             __builtin_amdgcn_sched_barrier(0);
           }
           if constexpr (!(DBG & 1)) load_b(wl, u);   // k-step ks+u+PD, or the next job's step u
@@ -379,7 +417,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
         const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
         const int ld = g.OD - d0, lh = g.OH - h0, lw = g.OW - w0;   // in-bounds tile extent
         const bool edge = ld < g.TD || lh < g.TH || lw < g.TW;
-        bf16* obase = out + (((long long)n * g.OD + d0) * g.OH + h0) * g.OW * Ncol + (long long)w0 * Ncol + gc8;
+        const long long obase_e = ((((long long)n * g.OD + d0) * g.OH + h0) * g.OW + w0) * Ncol + gc8;
+        bf16* obase = reinterpret_cast<bf16*>(out) + obase_e;
         // straight-line variants per (statistics, activation): runtime branches inside the
         // unrolled per-tile loop made hipcc emit ~1000 basic blocks
         auto epilogue = [&](auto mode) {
@@ -427,11 +466,64 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
             }
           }
         };
-        switch (emode) {
-          case 0: epilogue(std::integral_constant<int, 0>{}); break;
-          case 1: epilogue(std::integral_constant<int, 1>{}); break;
-          case 2: epilogue(std::integral_constant<int, 2>{}); break;
-          default: epilogue(std::integral_constant<int, 3>{}); break;
+        // fp8 inference epilogue: dequantise + bias (+ReLU) -> bf16 (16-B store) or e4m3 of
+        // y * oscale (8-B store)
+        auto epilogue_f8 = [&](auto mode) {
+          constexpr int M = decltype(mode)::value;   // bit 0 relu, bit 1 fp8 output
+          float sc8[8], bs8[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            sc8[j] = gc8 + j < Ncol ? scale[gc8 + j] : 0.f;
+            bs8[j] = (bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
+          }
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            bool ok = roff[mt] >= 0 && gc8 < Ncol;
+            if (edge) ok = ok && (rpk[mt] >> 16) < ld && ((rpk[mt] >> 8) & 255) < lh && (rpk[mt] & 255) < lw;
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              v[j] = acc[mt][j >> 2][j & 3] * sc8[j] + bs8[j];
+              if constexpr ((M & 1) != 0) v[j] = fmaxf(v[j], 0.f);
+            }
+            if (ok) {
+              if constexpr ((M & 2) != 0) {
+                unsigned wd[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                  float q[4];
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) q[j] = fminf(fmaxf(v[4 * h + j] * oscale, -448.f), 448.f);
+                  int p = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+                  p = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], p, true);
+                  wd[h] = (unsigned)p;
+                }
+                *(uint2*)(reinterpret_cast<unsigned char*>(out) + obase_e + (long long)roff[mt] * Ncol) =
+                    make_uint2(wd[0], wd[1]);
+              } else {
+                *(uint4*)(obase + (long long)roff[mt] * Ncol) =
+                    make_uint4(bf16x2_pack(v[0], v[1]), bf16x2_pack(v[2], v[3]), bf16x2_pack(v[4], v[5]),
+                               bf16x2_pack(v[6], v[7]));
+              }
+            }
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+          }
+        };
+        if constexpr (F8) {
+          switch (emode) {
+            case 0: epilogue_f8(std::integral_constant<int, 0>{}); break;
+            case 1: epilogue_f8(std::integral_constant<int, 1>{}); break;
+            case 2: epilogue_f8(std::integral_constant<int, 2>{}); break;
+            default: epilogue_f8(std::integral_constant<int, 3>{}); break;
+          }
+        } else {
+          switch (emode) {
+            case 0: epilogue(std::integral_constant<int, 0>{}); break;
+            case 1: epilogue(std::integral_constant<int, 1>{}); break;
+            case 2: epilogue(std::integral_constant<int, 2>{}); break;
+            default: epilogue(std::integral_constant<int, 3>{}); break;
+          }
         }
         lap(st_e);
       }
@@ -440,7 +532,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const bf16* __res
       par ^= 1;
     }
     tile_lds_barrier();                          // R
-    if (stats && tid < NT * 16 && ct0 * 16 + tid < Ncol) {
+    if (!F8 && stats && tid < NT * 16 && ct0 * 16 + tid < Ncol) {
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int w = 0; w < CT_NCW; ++w) {
@@ -573,19 +665,21 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
-template <int MT, int NT, int CPP, int DBG = 0>
-static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const bf16* s, const uint4* w, const int2* rt,
-                       const int4* kt, const bf16* zp, const float* b, bf16* o, float* stats, const TileGeom& g,
-                       int Ncol, int act, int* sched, long long* stamps = nullptr) {
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false>
+static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
+                       const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
+                       int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
+                       float oscale = 0.f) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG>), grid, dim3(CT_NTHR), lds, st, s, w, rt, kt, zp, b, o, stats,
-                     g, Ncol, act, sched, stamps);
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8>), grid, dim3(CT_NTHR), lds, st,
+                     (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
+                     stamps, scale, oscale);
   return 0;
 }
 
@@ -599,8 +693,8 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
   return 0;
 }
 
-static size_t tile_lds_total(const TileGeom& g, int MT, int NT) {
-  const int PD = NT == 2 ? 4 : 3;
+static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false) {
+  const int PD = ct_pd(NT, f8);
   return 2 * (size_t)g.BUF + 64 + CT_RED_BYTES + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8;
 }
 
@@ -651,9 +745,8 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     const size_t nst = (size_t)grid.x * grid.y * 16;
     if ((dbg & 16) && !stamps && hipMalloc(&stamps, 256 * 64 * 16 * sizeof(long long)) != hipSuccess) return -5;
     if ((dbg & 16) && hipMemsetAsync(stamps, 0, nst * sizeof(long long), st) != hipSuccess) return -5;
-#define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, (const bf16*)src, \
-      (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, \
-      sched, stamps);
+#define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, src, \
+      (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, stamps);
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
     CT_DBG(4, 23)
 #undef CT_DBG
@@ -675,10 +768,67 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   }
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
-    rc = launch_tile<M, N, C>(grid, lds, st, (const bf16*)src, (const uint4*)wp, (const int2*)rowtab,            \
-                              (const int4*)ktab, (const bf16*)zp, bias, (bf16*)out, stats, g, Ncol, act, sched);
+    rc = launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp,  \
+                              bias, out, stats, g, Ncol, act, sched);
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
+  if (rc) return rc;
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// fp8 (e4m3) inference launcher
+// ---------------------------------------------------------------------------
+// As fn_conv_tile with fp8 bytes for src / wp (packed by the host: [slice][k-step][16-col
+// tile][lane][32 B], the same column order, + 4 zero k-steps) and per-column dequantisation
+// scale[Ncol] (s_x * s_w[co]); oscale > 0 stores e4m3 of y * oscale, 0 stores bf16.
+// (MT = 9 spills at the fp8 fragment sizes: 8 only)
+#define CT_F8_INSTANCES(X) X(8, 2, 2) X(8, 2, 4)
+
+extern "C" int fn_conv_tile_f8_supported(int MT, int NT, int CPP) {
+#define CT_SUP(M, N, C) if (MT == M && NT == N && CPP == C) return 1;
+  CT_F8_INSTANCES(CT_SUP)
+#undef CT_SUP
+  return 0;
+}
+
+extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
+                               const float* scale, const float* bias, void* out, float oscale, const int* geom, int Ncol,
+                               int relu, int MT, int NT, int* sched, hipStream_t st) {
+  const TileGeom g = parse_tile(geom);
+  if (g.CS != 32 && g.CS != 64) return -2;
+  const int CPP = g.CS / 16;
+  if (!fn_conv_tile_f8_supported(MT, NT, CPP) || !scale || !(oscale >= 0.f)) return -2;
+  if (g.C % g.CS || g.TD * g.TH * g.TW > 64 * MT || g.TD < 1 || g.TH < 1 || g.TW < 1) return -3;
+  const long long HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
+  const long long HP = (g.TD + g.KD - 1) * HH * HW;
+  if (g.HPpad < HP || g.HPpad % 64) return -3;
+  if (g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
+  const int PD = ct_pd(NT, true);
+  const int T = g.KD * g.KH * g.KW;
+  const int need_ks = g.CS == 32 ? (T + 3) / 4 : (T + 1) / 2;
+  if (g.nks % PD || g.nks < need_ks || g.nct < (Ncol + 15) / 16) return -3;
+  for (long long p = 0; p < g.HPpad; p += 1) {
+    const unsigned long long hd = ((unsigned long long)p * g.mHHW) >> 32;
+    const unsigned long long rem = p - hd * HH * HW;
+    if (hd != (unsigned long long)(p / (HH * HW)) || (((rem * g.mHW) >> 32) != rem / HW)) return -3;
+  }
+  if ((size_t)g.BUF < (size_t)g.HPpad * CPP * 16 || g.BUF % 1024) return -3;
+  const size_t lds = tile_lds_total(g, MT, NT, true);
+  if (lds > 160 * 1024) return -4;
+  const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
+  if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
+  if (Ncol % 8) return -2;
+  dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
+  int rc = -2;
+#define CT_F8_CASE(M, N, C)                                                                                        \
+  if (MT == M && NT == N && CPP == C)                                                                              \
+    rc = launch_tile<M, N, C, 0, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, \
+                                       zp, bias, out, nullptr, g, Ncol, relu ? ACT_RELU : ACT_NONE, sched, nullptr,   \
+                                       scale, oscale);
+  CT_F8_INSTANCES(CT_F8_CASE)
+#undef CT_F8_CASE
   if (rc) return rc;
   FN_CHECK_LAUNCH();
   return 0;

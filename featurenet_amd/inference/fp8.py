@@ -6,22 +6,27 @@ Post-training quantisation, inference only:
 * weights are quantised per output channel to OCP e4m3 (amax / 448);
 * activations between layers are quantised per tensor with scales calibrated
   from a bf16 forward pass (``amax / 448`` of each layer's post-ReLU output);
-* conv2..conv4 run ``conv_halo_f8`` (``csrc/kernels/conv_fp8.hip``): fp8
+* conv2..conv4 run the fp8 variant of the big-tile kernel (``conv_tile.hip``,
+  ``conv_tile_kernel<8, 2, CPP, 0, true>``: LDS-DMA'd e4m3 halo, weights streamed in
+  MFMA-fragment order, ``v_mfma_scale_f32_16x16x128_f8f6f4``, dequantise + bias + ReLU
+  (+ requantise) from registers), or ``conv_halo_f8`` (``csrc/kernels/conv_fp8.hip``): fp8
   halo tiles in LDS, block-scaled ``mfma_scale_f32_16x16x128_f8f6f4``, dequantise + bias + ReLU
   (+ requantise to fp8) in the epilogue.  conv1 (1-channel, stride 2) stays on
-  the bf16 implicit-GEMM kernel with the folded BN + ReLU fused, followed by
-  one quantisation pass; conv4 writes bf16 for the max-pool and the two dense
-  layers (hipBLASLt bf16).
+  the bf16 path (space-to-depth tile kernel) with the folded BN + ReLU fused,
+  followed by one quantisation pass; conv4 writes bf16 for the max-pool and the
+  two dense layers (native split-K MFMA kernels, bf16).
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from .. import _native
 from .. import ops
 from ..models.featurenet3d import FeatureNet3D
+from ..ops import conv_tile
 from ..ops.conv import halo_plan, halo_tap_offsets
 from ..ops.spec import ConvSpec, PoolSpec
 
@@ -43,7 +48,10 @@ def _to_fp8(t: torch.Tensor) -> torch.Tensor:
 
 
 class Fp8Conv:
-    """One stride-1 conv layer on the fp8 halo kernel (folded BN, per-channel weight scales)."""
+    """One stride-1 conv layer on the fp8 tile kernel (``conv_tile.hip``, F8 variant) or the
+    fp8 halo kernel (``conv_fp8.hip``: fallback for shapes the tile planner rejects, and the
+    A/B reference); folded BN, per-channel weight scales.  ``FN_F8_TILE=0`` forces the halo
+    kernel."""
 
     def __init__(self, conv, in_scale: float, out_scale: float | None, relu: bool = True):
         w, b = _fold_bn(conv)
@@ -56,14 +64,29 @@ class Fp8Conv:
         lay = torch.zeros(K, Cin // 16, T8, 16, dtype=torch.float8_e4m3fn, device=w.device)
         lay[:, :, :T] = wq.reshape(K, T, Cin // 16, 16).permute(0, 2, 1, 3)
         self.wq = lay.reshape(K, -1).view(torch.uint8).contiguous()
+        self.wq_ktc = wq.reshape(K, T, Cin).view(torch.uint8).contiguous()   # [K][T][C] for the tile packing
+        self._tile = {}
         self.scale = (in_scale * sw).float().contiguous()
         self.bias = b.float().contiguous()
         self.out_scale, self.relu = out_scale, relu
         self.K, self.kernel, self.conv = K, (KD, KH, KW), conv
         self.w_dequant = wq.float() * sw.view(-1, 1, 1, 1, 1)     # for numerics tests
 
+    def tile_plan(self, spec):
+        if os.environ.get("FN_F8_TILE", "1") == "0":
+            return None
+        return conv_tile.plan(spec.N, (spec.OD, spec.OH, spec.OW), (spec.KD, spec.KH, spec.KW), spec.C, spec.K,
+                              f8=True)
+
     def __call__(self, xq: torch.Tensor, shape5: tuple) -> tuple[torch.Tensor, tuple]:
         spec = ConvSpec.make(shape5, self.K, self.kernel, 1, self.conv.padding)
+        tp = self.tile_plan(spec)
+        if tp is not None:
+            wpk = self._tile.get(tp)
+            if wpk is None:
+                wpk = self._tile[tp] = conv_tile.pack_weights_f8(self.wq_ktc, tp)
+            y = conv_tile.conv_fwd_f8(xq, wpk, self.scale, self.bias, spec, tp, self.relu, self.out_scale)
+            return y, spec.out_shape5
         # fp8 halo = 16 B/position; halo_plan counts 32 B/position (bf16): <= 64 KiB of fp8 halo
         plan = halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, 128 * 1024, wsplit=False)
         if plan is None:

@@ -60,6 +60,7 @@ class TilePlan:
     mHW: int
     mHHW: int
     cost: float      # modelled cycles (per wave, summed over the jobs of one CU)
+    f8: bool = False  # fp8 (e4m3) inference variant: 16-channel chunks, 128-k steps, ring depth 2
 
     @property
     def rows(self) -> int:
@@ -84,19 +85,20 @@ def _ksteps(T: int, CS: int, PD: int) -> int:
     return -(-k // PD) * PD
 
 
-def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int = 256):
+def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int = 256, f8: bool = False):
     """Best TilePlan for an (N, OD, OH, OW) output of a (KD, KH, KW) stride-1 conv over
-    ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply."""
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus)
+    ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply
+    (``f8``: the e4m3 inference variant, 32- or 64-channel slices)."""
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8)
     if key in _PLANS:
         return _PLANS[key]
-    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus)
+    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8)
     with _LOCK:
         _PLANS[key] = best
     return best
 
 
-def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
+def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
@@ -105,25 +107,26 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
     NT = 2                                       # 32-column blocks (register budget: 5 waves per CU)
     ncb = -(-Ncol // (NT * 16))
     nct = ncb * NT
-    PD = 4
+    PD = PD_F8 if f8 else 4
     workers = max(1, n_cus // ncb)
     cands = []
     cs_only = int(os.environ.get("FN_TILE_CS", "0"))
-    for CS in (32, 16, 8):
+    mt_choices = (8,) if f8 else MT_CHOICES
+    for CS in ((64, 32) if f8 else (32, 16, 8)):
         if Csrc % CS or (cs_only and CS != cs_only) or (CS == 8 and Csrc % 16 == 0):
             continue
-        CPP = CS // 8
+        CPP = CS // 16 if f8 else CS // 8
         nslice = Csrc // CS
-        nks = _ksteps(T, CS, PD)
+        nks = -(-math.ceil(T / (128 // CS)) // PD) * PD if f8 else _ksteps(T, CS, PD)   # f8: 128-k steps
         tw_opts = sorted({OW} | {-(-OW // k) for k in range(2, 5) if -(-OW // k) >= 8})
         for TW in tw_opts:
             for TD in range(1, OD + 1):
                 for TH in range(1, OH + 1):
                     rows = TD * TH * TW
-                    if rows > 64 * MT_CHOICES[-1]:
+                    if rows > 64 * mt_choices[-1]:
                         break
-                    MT = max(MT_CHOICES[0], -(-rows // 64))
-                    if rows < 64 * MT_CHOICES[0] * 0.75:
+                    MT = max(mt_choices[0], -(-rows // 64))
+                    if rows < 64 * mt_choices[0] * 0.75:
                         continue
                     HH, HW = TH + KH - 1, TW + KW - 1
                     HP = (TD + KD - 1) * HH * HW
@@ -134,14 +137,14 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
                     jobs = tiles * nslice
-                    mfma = nks * MT * NT * 16                  # cycles of MFMA issue per wave per job
+                    mfma = nks * MT * NT * (32 if f8 else 16)  # cycles of MFMA issue per wave per job
                     fixed = 800                                 # barrier + first halo reads per job
                     epi = MT * NT * 40 / nslice                 # register epilogue, once per tile
                     loader = 1500 + (CPP * HPpad // 64) * 130   # DMA issue + landing of one job's halo
                     per_job = max(mfma + fixed + epi, loader)
                     cost = math.ceil(jobs / workers) * per_job
                     cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
-                                          float(cost)))
+                                          float(cost), f8))
     # the cheapest few, re-costed with their row tables' residual bank conflicts (a
     # fragment whose 16 rows repeat a residue mod 16 reads at half rate)
     best = None
@@ -155,7 +158,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus):
         cost = c.cost * (1.0 + 0.5 * dups / res.size)
         if best is None or cost < best.cost:
             best = TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct", "BUF",
-                                                        "mHW", "mHHW")), cost)
+                                                        "mHW", "mHHW")), cost, f8)
     return best
 
 
@@ -243,13 +246,14 @@ def rowtab_tensor(p: TilePlan, kdims: tuple, device) -> torch.Tensor:
 
 
 PD = 4                                           # B-ring depth of the kernel (k-steps in flight)
+PD_F8 = 2                                        # (fp8 variant: 2 k-steps of 128)
 
 
 def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
     """int32 [nks + PD + 2, 4]: LDS byte offset of the tap that lane group lg (lanes 16lg ..
     16lg+15) reads in each k-step -- one tap for all four groups (CS >= 32: the groups take
     channel chunks of it), two taps (CS = 16: groups 0,1 / 2,3) or four (CS = 8); 0 past the
-    last tap (zero weights)."""
+    last tap (zero weights).  fp8: four taps (CS = 32) or two (CS = 64, groups 0,1 / 2,3)."""
     KD, KH, KW = kdims
     HH, HW = p.TH + KH - 1, p.TW + KW - 1
     T = KD * KH * KW
@@ -259,7 +263,9 @@ def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
     plane = p.HPpad * 16
     for k in range(p.nks):
         for lg in range(4):
-            if p.CS >= 32:
+            if p.f8:                                 # lane group: 32 bytes of one tap (planes in lb)
+                t, off = (4 * k + lg, 0) if p.CS == 32 else (2 * k + lg // 2, 0)
+            elif p.CS >= 32:
                 t, s = divmod(k, p.CS // 32)
                 off = s * 4 * plane
             elif p.CS == 16:
@@ -382,3 +388,53 @@ def choose(kind: str, spec, run_tile, run_other) -> bool:
         with _LOCK:
             _CHOICE[key] = c
     return c
+
+
+# ---------------------------------------------------------------------------
+# fp8 (e4m3) inference variant
+# ---------------------------------------------------------------------------
+def pack_weights_f8(wq: torch.Tensor, p: TilePlan) -> torch.Tensor:
+    """e4m3 weight bytes [K, taps, C] (uint8) -> the fp8 kernel's fragment stream: uint8
+    [(nslice * nks + 4) * nct * 64 * 32] -- per (slice, k-step, 16-column tile, lane) the 32
+    bytes lane group lg multiplies (tap 4ks+lg x 32 channels for CS = 32, tap 2ks+lg/2 x
+    channels 32(lg&1).. for CS = 64), columns in the bf16 kernel's permuted order, zeros past
+    the last tap / column and 4 zero k-steps for the ring's over-the-end loads."""
+    assert p.f8
+    K, T, C = wq.shape
+    nslice = C // p.CS
+    tps = 128 // p.CS
+    Tp = p.nks * tps
+    wpad = torch.zeros(p.nct * 16, Tp, C, dtype=torch.uint8, device=wq.device)
+    wpad[:K, :T] = wq
+    sl, ks, ct, ln = np.meshgrid(np.arange(nslice), np.arange(p.nks), np.arange(p.nct), np.arange(64), indexing="ij")
+    fi, lg = ln & 15, ln >> 4
+    col = (ct >> 1) * 32 + 8 * (fi >> 2) + 4 * (ct & 1) + (fi & 3)
+    if p.CS == 32:
+        tap, ch0 = 4 * ks + lg, sl * 32
+    else:
+        tap, ch0 = 2 * ks + (lg >> 1), sl * 64 + 32 * (lg & 1)
+    dev = wq.device
+    ci = torch.from_numpy(col.reshape(-1)).to(dev)[:, None]
+    ti = torch.from_numpy(tap.reshape(-1)).to(dev)[:, None]
+    chi = torch.from_numpy(ch0.reshape(-1)).to(dev)[:, None] + torch.arange(32, device=dev)[None, :]
+    body = wpad[ci, ti, chi].reshape(-1)
+    return torch.cat([body, torch.zeros(4 * p.nct * 64 * 32, dtype=torch.uint8, device=dev)]).contiguous()
+
+
+def conv_fwd_f8(xq5: torch.Tensor, wpk: torch.Tensor, scale: torch.Tensor, bias: torch.Tensor, spec, p: TilePlan,
+                relu: bool, out_scale: float | None) -> torch.Tensor:
+    """y = act(conv(x, w) * scale + bias) of e4m3 activations (uint8 [N, D, H, W, C]) on the fp8
+    tile kernel: bf16 output, or e4m3 of y / out_scale when ``out_scale`` is given."""
+    kd = (spec.KD, spec.KH, spec.KW)
+    geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
+                    (spec.pd, spec.ph, spec.pw))
+    y = torch.empty(spec.out_shape5, dtype=torch.uint8 if out_scale else torch.bfloat16, device=xq5.device)
+    st = _native.stream(xq5)
+    rt = rowtab_tensor(p, kd, xq5.device)
+    kt = ktab_tensor(p, kd, xq5.device)
+    _native.kernels().conv_tile_f8(xq5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
+                                   zero_page(xq5.device).data_ptr(), scale.data_ptr(), _native.ptr(bias), y.data_ptr(),
+                                   1.0 / out_scale if out_scale else 0.0, geom, spec.K, int(relu), p.MT, p.NT, st,
+                                   sched(xq5.device, st).data_ptr(),
+                                   [xq5.numel(), wpk.numel(), y.numel(), rt.numel() // 2, kt.numel() // 4])
+    return y

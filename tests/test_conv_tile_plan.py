@@ -46,3 +46,38 @@ def test_row_table_conflict_free_when_residues_allow():
 def test_magic_division_exact():
     for HH, HW in [(9, 29), (14, 25), (7, 22), (13, 28), (15, 33)]:
         assert ct._magic_ok(HH, HW, 4096)
+
+
+@pytest.mark.parametrize("out,k,c,n", [((57, 57, 57), (5, 5, 5), 32, 32), ((54, 54, 54), (4, 4, 4), 32, 64),
+                                       ((52, 52, 52), (3, 3, 3), 64, 64)])
+def test_fp8_plans_and_weight_stream(out, k, c, n):
+    """fp8 tile plans (128^3 inference layers): 32-/64-channel slices, 128-k steps in ring-depth
+    pairs, and the packed e4m3 stream holds w[col][tap][ch] where the kernel's lane map says."""
+    import torch
+    p = ct.plan(128, out, k, c, n, f8=True)
+    assert p is not None and p.f8 and p.CS in (32, 64) and p.MT == 8
+    T = k[0] * k[1] * k[2]
+    tps = 128 // p.CS
+    assert p.nks % ct.PD_F8 == 0 and p.nks * tps >= T
+    assert 2 * p.BUF + 64 + ct.RED_BYTES + (p.nks + ct.PD_F8 + 2) * 16 + p.HPpad * 8 <= ct.LDS_MAX
+    g = torch.Generator().manual_seed(0)
+    wq = torch.randint(1, 255, (n, T, c), generator=g, dtype=torch.uint8)
+    wpk = ct.pack_weights_f8(wq, p)
+    nslice = c // p.CS
+    assert wpk.numel() == (nslice * p.nks + 4) * p.nct * 64 * 32
+    frag = wpk.reshape(-1, p.nct, 64, 32)
+    assert not frag[nslice * p.nks:].any()                       # the ring's zero k-steps
+    for sl, ks, cti, lane in [(0, 0, 0, 0), (nslice - 1, p.nks - 1, p.nct - 1, 63), (0, 1, 1, 37)]:
+        fi, lg = lane & 15, lane >> 4
+        col = (cti >> 1) * 32 + 8 * (fi >> 2) + 4 * (cti & 1) + (fi & 3)
+        tap = 4 * ks + lg if p.CS == 32 else 2 * ks + (lg >> 1)
+        ch0 = sl * p.CS + (0 if p.CS == 32 else 32 * (lg & 1))
+        want = wq[col, tap, ch0:ch0 + 32] if (tap < T and col < n) else torch.zeros(32, dtype=torch.uint8)
+        assert torch.equal(frag[sl * p.nks + ks, cti, lane], want)
+    kt = ct.k_table(p, k)
+    HH, HW = p.TH + k[1] - 1, p.TW + k[2] - 1
+    t = min(5, T - 1)
+    kd, r = divmod(t, k[1] * k[2])
+    kh, kw = divmod(r, k[2])
+    ks, lg = (t // 4, t % 4) if p.CS == 32 else (t // 2, 2 * (t % 2))
+    assert kt[ks, lg] == ((kd * HH + kh) * HW + kw) * 16

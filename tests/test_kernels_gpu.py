@@ -565,24 +565,35 @@ def test_segmentation_head_step():
         assert p.grad is not None and torch.isfinite(p.grad).all()
 
 
-@pytest.mark.parametrize("out_f8", [False, True])
-def test_conv_halo_fp8(out_f8):
-    """fp8 halo conv (conv_fp8.hip) vs fp32 conv of the same dequantised operands."""
+@pytest.mark.parametrize("kernel", ["tile", "halo"])
+@pytest.mark.parametrize("cin,cout,k,dims,out_f8", [
+    (32, 64, 3, (2, 12, 13, 14), False),
+    (32, 64, 3, (2, 12, 13, 14), True),
+    (32, 32, 5, (4, 21, 20, 19), True),       # conv2-like: CS = 32, 4 taps per 128-k step, edge tiles
+    (64, 64, 3, (3, 18, 17, 20), False),      # conv4-like: CS = 64, 2 taps per step
+    (64, 64, 4, (2, 16, 16, 16), True),       # conv3-like tap count (64 -> pads the last step)
+])
+def test_conv_fp8(monkeypatch, kernel, cin, cout, k, dims, out_f8):
+    """fp8 conv -- the F8 tile kernel (conv_tile.hip) or the fp8 halo kernel (conv_fp8.hip) --
+    vs the fp32 conv of the same dequantised operands."""
     _native_loaded()
     from featurenet_amd.inference.fp8 import Fp8Conv
     from featurenet_amd.models.layers import Conv
 
+    monkeypatch.setenv("FN_F8_TILE", "1" if kernel == "tile" else "0")
     torch.manual_seed(7)
-    conv = Conv(32, 64, (3, 3, 3), 1, "valid", bias=True).cuda()
+    conv = Conv(cin, cout, (k, k, k), 1, "valid", bias=True).cuda()
     with torch.no_grad():
         conv.bias.normal_(0, 0.1)
     xs = 0.02
-    x = (torch.randn(2, 12, 13, 14, 32, device="cuda") * 2).clamp(-400 * xs, 400 * xs)
+    x = (torch.randn(*dims, cin, device="cuda") * 2).clamp(-400 * xs, 400 * xs)
     xq = (x / xs).to(torch.float8_e4m3fn)
     out_scale = 0.05 if out_f8 else None
     layer = Fp8Conv(conv, xs, out_scale, relu=True)
+    spec = ConvSpec.make(x.shape, cout, (k, k, k))
+    if kernel == "tile":
+        assert layer.tile_plan(spec) is not None, spec
     y, _ = layer(xq.view(torch.uint8), tuple(x.shape))
-    spec = ConvSpec.make(x.shape, 64, (3, 3, 3))
     yr = torch.relu(ref.conv(xq.float() * xs, layer.w_dequant, layer.bias, spec))
     if out_f8:
         yd = y.view(torch.float8_e4m3fn).float() * out_scale

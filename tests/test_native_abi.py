@@ -98,17 +98,20 @@ def test_igemm_and_misc_calls_match_bindings(fake):
     assert {"igemm_fwd", "igemm_wgrad", "colstats", "bn_finalize", "dw_fwd", "softmax_xent_rows"} <= set(fake.calls)
 
 
-def test_fp8_inference_calls_match_bindings(fake):
+def test_fp8_inference_calls_match_bindings(fake, monkeypatch):
     from featurenet_amd.inference.fp8 import Fp8Conv, quantize_fp8_act
     from featurenet_amd.models.layers import Conv
 
     conv = Conv(32, 64, (3, 3, 3), 1, "valid", bias=True)
     layer = Fp8Conv(conv, 0.02, 0.05)
     xq = torch.zeros(2, 10, 10, 10, 32, dtype=torch.uint8)
-    y, shape = layer(xq, tuple(xq.shape))
+    y, shape = layer(xq, tuple(xq.shape))                      # fp8 tile kernel
+    assert shape == (2, 8, 8, 8, 64) and y.dtype == torch.uint8
+    monkeypatch.setenv("FN_F8_TILE", "0")
+    y, shape = layer(xq, tuple(xq.shape))                      # fp8 halo kernel
     assert shape == (2, 8, 8, 8, 64) and y.dtype == torch.uint8
     quantize_fp8_act(torch.zeros(4, 8, dtype=torch.bfloat16), 0.1)
-    assert {"conv_halo_f8", "quant_fp8"} <= set(fake.calls)
+    assert {"conv_tile_f8", "conv_halo_f8", "quant_fp8"} <= set(fake.calls)
 
 
 def test_halo_extent_check_rejects_undersized_tensors():
