@@ -957,14 +957,14 @@ extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, co
 // channels; a 1-channel stride-2 stem reads 4 bf16 pairs per position.
 __global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
                                                         int N, int D, int H, int W, int C, int sd, int sh, int sw,
-                                                        int D2, int H2, int W2, int CO) {
+                                                        int D2, int H2, int W2, int CO, int pd, int ph, int pw) {
   const long long npos = (long long)N * D2 * H2 * W2;
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= npos) return;
   const int w2 = (int)(p % W2), h2 = (int)((p / W2) % H2), d2 = (int)((p / ((long long)W2 * H2)) % D2);
   const long long n = p / ((long long)W2 * H2 * D2);
   const int creal = sd * sh * sw * C;
-  if (C == 1 && sd == 2 && sh == 2 && sw == 2 && 2 * D2 == D && 2 * H2 == H && 2 * W2 == W) {
+  if (C == 1 && sd == 2 && sh == 2 && sw == 2 && 2 * D2 == D && 2 * H2 == H && 2 * W2 == W && !(pd | ph | pw)) {
     // the 1-channel stride-2 stem: 4 aligned bf16 pairs (w, w+1) -> one 16-B store
     const unsigned* xr = reinterpret_cast<const unsigned*>(x);
     uint4 v;
@@ -986,8 +986,10 @@ __global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ 
       if (ch < creal) {
         const int ci = ch % C, blk = ch / C;
         const int c = blk % sw, b = (blk / sw) % sh, a = blk / (sw * sh);
-        const int d = d2 * sd + a, h = h2 * sh + b, w = w2 * sw + c;
-        if (d < D && h < H && w < W) f = bf2f(x[(((n * D + d) * H + h) * W + w) * C + ci]);
+        // (leading zero pads of a padded strided conv: the packed grid covers the padded input)
+        const int d = d2 * sd + a - pd, h = h2 * sh + b - ph, w = w2 * sw + c - pw;
+        if ((unsigned)d < (unsigned)D && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+          f = bf2f(x[(((n * D + d) * H + h) * W + w) * C + ci]);
       }
       v.e[j] = f2bf(f);
     }
@@ -995,15 +997,19 @@ __global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ 
   }
 }
 
-extern "C" int fn_s2d_pack(const void* x, void* out, const int* geom12, hipStream_t st) {
-  const int N = geom12[0], D = geom12[1], H = geom12[2], W = geom12[3], C = geom12[4];
-  const int sd = geom12[5], sh = geom12[6], sw = geom12[7], D2 = geom12[8], H2 = geom12[9], W2 = geom12[10];
-  const int CO = geom12[11];
-  if (CO % 8 != 0 || sd * sh * sw * C > CO) return -2;
+// geom: N D H W C sd sh sw D2 H2 W2 CO [pd ph pw] (leading pads, default 0)
+extern "C" int fn_s2d_pack(const void* x, void* out, const int* geom, int glen, hipStream_t st) {
+  const int N = geom[0], D = geom[1], H = geom[2], W = geom[3], C = geom[4];
+  const int sd = geom[5], sh = geom[6], sw = geom[7], D2 = geom[8], H2 = geom[9], W2 = geom[10];
+  const int CO = geom[11];
+  const int pd = glen >= 15 ? geom[12] : 0, ph = glen >= 15 ? geom[13] : 0, pw = glen >= 15 ? geom[14] : 0;
+  if (CO % 8 != 0 || sd * sh * sw * C > CO || pd < 0 || ph < 0 || pw < 0 || pd >= sd * D2 || ph >= sh * H2 ||
+      pw >= sw * W2)
+    return -2;
   const long long npos = (long long)N * D2 * H2 * W2;
   const unsigned blocks = (unsigned)((npos + 255) / 256);
   hipLaunchKernelGGL(s2d_pack_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)out, N, D, H, W, C, sd,
-                     sh, sw, D2, H2, W2, CO);
+                     sh, sw, D2, H2, W2, CO, pd, ph, pw);
   FN_CHECK_LAUNCH();
   return 0;
 }

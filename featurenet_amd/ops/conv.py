@@ -481,8 +481,10 @@ def native_act_bwd(dy: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
 # 1-channel 7^3 stride-2 stem) become stride-1 convs with s^3*C channels
 # ---------------------------------------------------------------------------
 def s2d_plan(spec: ConvSpec):
-    """(factors, ConvSpec') when a strided, few-channel, unpadded conv maps onto the
-    stride-1 halo kernels after a space-to-depth of the input; else None.
+    """(factors, ConvSpec') when a strided, few-channel conv maps onto the stride-1 halo
+    kernels after a space-to-depth of the (zero-padded) input; else None.  Padding
+    ("same") is folded into the packing: the packed grid covers the padded input, and
+    the stride-1 conv over it is unpadded.
 
     The packed input has ``s^3*C`` real channels, zero-padded to 8 (one 8-channel
     halo slice, k-step = 4 taps x 8 channels) or 16; FeatureNet-3D's 1-channel
@@ -491,13 +493,12 @@ def s2d_plan(spec: ConvSpec):
     f = (spec.sd, spec.sh, spec.sw)
     if not _halo_enabled() or f == (1, 1, 1) or (spec.dd, spec.dh, spec.dw) != (1, 1, 1):
         return None
-    if spec.pd or spec.ph or spec.pw or any(p for p in spec.pads_hi):
-        return None
     cs = spec.C * f[0] * f[1] * f[2]
     if cs > 16:
         return None
     co = 8 if cs <= 8 else 16
-    D2, H2, W2 = (-(-d // s) for d, s in zip((spec.D, spec.H, spec.W), f))
+    padded = (spec.D + spec.pd + spec.pads_hi[0], spec.H + spec.ph + spec.pads_hi[1], spec.W + spec.pw + spec.pads_hi[2])
+    D2, H2, W2 = (-(-d // s) for d, s in zip(padded, f))
     k2 = tuple(-(-k // s) for k, s in zip((spec.KD, spec.KH, spec.KW), f))
     if k2[0] * k2[1] * k2[2] < 8 or D2 < k2[0] or H2 < k2[1] or W2 < k2[2]:
         return None
@@ -507,19 +508,21 @@ def s2d_plan(spec: ConvSpec):
     return f, spec2
 
 
-def s2d_input(x5: torch.Tensor, f, spec2: ConvSpec) -> torch.Tensor:
-    """Space-to-depth packed input [N, D2, H2, W2, C'] (``s2d_pack`` kernel on GPU)."""
+def s2d_input(x5: torch.Tensor, f, spec2: ConvSpec, pads=(0, 0, 0)) -> torch.Tensor:
+    """Space-to-depth packed input [N, D2, H2, W2, C'] of x zero-padded by ``pads`` in front
+    (``s2d_pack`` kernel on GPU)."""
     N, D, H, W, C = x5.shape
     sd, sh, sw = f
+    pd, ph, pw = pads
     D2, H2, W2 = spec2.D, spec2.H, spec2.W
     if x5.is_cuda and _native.kernels_available():
         x5 = x5.to(torch.bfloat16).contiguous()
         out = torch.empty(N, D2, H2, W2, spec2.C, dtype=torch.bfloat16, device=x5.device)
-        _native.kernels().s2d_pack(x5.data_ptr(), out.data_ptr(), [N, D, H, W, C, sd, sh, sw, D2, H2, W2, spec2.C],
-                                   _native.stream(x5))
+        _native.kernels().s2d_pack(x5.data_ptr(), out.data_ptr(),
+                                   [N, D, H, W, C, sd, sh, sw, D2, H2, W2, spec2.C, pd, ph, pw], _native.stream(x5))
         return out
     xp = torch.zeros(N, D2 * sd, H2 * sh, W2 * sw, C, dtype=x5.dtype, device=x5.device)
-    xp[:, :D, :H, :W] = x5
+    xp[:, pd:pd + D, ph:ph + H, pw:pw + W] = x5[:, :D2 * sd - pd, :H2 * sh - ph, :W2 * sw - pw]
     x2 = xp.view(N, D2, sd, H2, sh, W2, sw, C).permute(0, 1, 3, 5, 2, 4, 6, 7).reshape(N, D2, H2, W2, -1)
     out = torch.zeros(N, D2, H2, W2, spec2.C, dtype=x5.dtype, device=x5.device)
     out[..., : x2.shape[-1]] = x2
@@ -616,7 +619,7 @@ class ConvFn(torch.autograd.Function):
             # strided few-channel conv: space-to-depth -> stride-1 halo conv; the packed
             # input is what wgrad consumes, so it is saved instead of x
             f, spec2 = s2d
-            x2 = s2d_input(x5, f, spec2)
+            x2 = s2d_input(x5, f, spec2, (spec.pd, spec.ph, spec.pw))
             y, stats = native_conv_fwd(x2, None, 0, bias, spec2, act, want_stats,
                                        w=s2d_weight(w.detach(), f, spec, spec2))
             x_saved = x2
@@ -626,7 +629,7 @@ class ConvFn(torch.autograd.Function):
             f, spec2 = s2d
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
-            x_saved = s2d_input(x5, f, spec2) if ctx.needs_input_grad[1] else x5
+            x_saved = s2d_input(x5, f, spec2, (spec.pd, spec.ph, spec.pw)) if ctx.needs_input_grad[1] else x5
         elif halo_fwd_plan(spec) is not None or (conv_tile.fwd_plan(spec) is not None and act in (0, act_code("relu"))):
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats, w=w.detach())
         else:

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Per-layer conv kernel timing for FeatureNet-3D at the headline batch.
 
-For each stride-1 layer (conv2..conv4) times forward (BN-statistics epilogue)
-and dgrad on the big-tile kernel (``conv_tile.hip``) and on the previous halo
-kernel (``conv_halo.hip``), back to back on one stream (events around R
+For each stride-1 layer (conv2..conv4; ``--only seg_dec`` for the segmentation
+decoder conv) times forward (BN-statistics epilogue) and dgrad on the big-tile
+kernel (``conv_tile.hip``) and on the previous halo kernel (``conv_halo.hip``),
+and the halo weight gradient, back to back on one stream (events around R
 launches), and prints us/call and model TFLOP/s.
 
     python scripts/bench_conv_layers.py --batch 128 --reps 10
@@ -25,7 +26,8 @@ cv = importlib.import_module("featurenet_amd.ops.conv")   # the module (ops.conv
 from featurenet_amd.ops import conv_tile as ct  # noqa: E402
 from featurenet_amd.ops.spec import ConvSpec  # noqa: E402
 
-LAYERS = [("stem_s2d", 32, 8, 32, 4), ("conv2", 29, 32, 32, 5), ("conv3", 25, 32, 64, 4), ("conv4", 22, 64, 64, 3)]
+LAYERS = [("stem_s2d", 32, 8, 32, 4, "valid"), ("conv2", 29, 32, 32, 5, "valid"), ("conv3", 25, 32, 64, 4, "valid"),
+          ("conv4", 22, 64, 64, 3, "valid"), ("seg_dec", 64, 64, 32, 3, "same")]
 
 
 def timeit(fn, reps):
@@ -48,21 +50,22 @@ def main():
     args = ap.parse_args()
     torch.manual_seed(0)
     rows = []
-    for name, S, C, K, k in LAYERS:
-        if args.only and name not in args.only.split(","):
+    for name, S, C, K, k, pad in LAYERS:
+        if (args.only and name not in args.only.split(",")) or (not args.only and name == "seg_dec"):
             continue
         x = torch.randn(args.batch, S, S, S, C, device="cuda").to(torch.bfloat16)
-        spec = ConvSpec.make(x.shape, K, k, 1, "valid")
+        spec = ConvSpec.make(x.shape, K, k, 1, pad)
         w = torch.randn(K, k, k, k, C, device="cuda") * 0.05
         dy = torch.randn(spec.out_shape5, device="cuda").to(torch.bfloat16)
         gf = spec.flops() / 1e9
         pf, pd = ct.fwd_plan(spec), ct.dgrad_plan(spec)
         res = {"layer": name, "gflop": round(gf, 1), "tile_fwd_plan": str(pf), "tile_dgrad_plan": str(pd)}
-        hf, hd = cv.halo_fwd_plan(spec), cv.halo_dgrad_plan(spec)
+        hf, hd, hw = cv.halo_fwd_plan(spec), cv.halo_dgrad_plan(spec), cv.halo_wgrad_plan(spec)
         runs = {"halo_fwd": (hf, lambda: cv.halo_conv_fwd(x, w, None, spec, 0, True, hf)),
                 "tile_fwd": (pf, lambda: ct.conv_fwd(x, w, None, spec, 0, True, pf)),
                 "halo_dgrad": (hd, lambda: cv.halo_conv_dgrad(dy, w, spec, hd)),
-                "tile_dgrad": (pd, lambda: ct.conv_dgrad(dy, w, spec, pd))}
+                "tile_dgrad": (pd, lambda: ct.conv_dgrad(dy, w, spec, pd)),
+                "halo_wgrad": (hw, lambda: cv.halo_conv_wgrad(dy, x, spec, hw))}
         for kk, (pl, fn) in runs.items():
             if pl is None:
                 continue

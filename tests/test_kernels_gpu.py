@@ -498,15 +498,17 @@ def test_s2d_pack_matches_reference_layout():
 
     C = importlib.import_module("featurenet_amd.ops.conv")
     torch.manual_seed(4)
-    for shape, k, s in (((2, 19, 20, 21, 1), 7, 2), ((1, 9, 9, 9, 2), 4, 2)):
+    for shape, k, s, pad in (((2, 19, 20, 21, 1), 7, 2, "valid"), ((1, 9, 9, 9, 2), 4, 2, "valid"),
+                             ((2, 20, 18, 22, 1), 7, 2, "same")):
         x = torch.randn(*shape, device="cuda").to(torch.bfloat16)
-        spec = ConvSpec.make(x.shape, 16, k, s)
+        spec = ConvSpec.make(x.shape, 16, k, s, pad)
         plan = C.s2d_plan(spec)
         if plan is None:
             continue
         f, spec2 = plan
-        got = C.s2d_input(x, f, spec2)
-        want = C.s2d_input(x.cpu(), f, spec2)
+        pads = (spec.pd, spec.ph, spec.pw)
+        got = C.s2d_input(x, f, spec2, pads)
+        want = C.s2d_input(x.cpu(), f, spec2, pads)
         assert torch.equal(got.cpu(), want)
 
 
@@ -619,7 +621,8 @@ def test_fp8_featurenet3d_matches_bf16():
     assert cos > 0.97, cos
 
 
-def test_space_to_depth_stem_matches_reference():
+@pytest.mark.parametrize("padding", ["valid", "same"])
+def test_space_to_depth_stem_matches_reference(padding):
     """FeatureNet-3D stem (1-ch 7^3 stride 2) through space-to-depth + halo kernels: fwd, stats, wgrad."""
     _native_loaded()
     import importlib
@@ -627,7 +630,7 @@ def test_space_to_depth_stem_matches_reference():
     C = importlib.import_module("featurenet_amd.ops.conv")
     torch.manual_seed(2)
     x = (torch.rand(2, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
-    spec = ConvSpec.make(x.shape, 32, 7, 2)
+    spec = ConvSpec.make(x.shape, 32, 7, 2, padding)
     assert C.s2d_plan(spec) is not None
     w = (torch.randn(32, 7, 7, 7, 1, device="cuda") * 0.05).to(torch.bfloat16).float()
     wn = w.clone().requires_grad_(True)

@@ -189,3 +189,22 @@ def test_conv_spec_extra_padding_equals_padded_input():
         s_fold = ConvSpec.make(tuple(x.shape), 16, (1, 3, 3), 1, padding, extra=(0, 1, 2))
         assert (s_fold.OD, s_fold.OH, s_fold.OW) == (s_pad.OD, s_pad.OH, s_pad.OW)
         torch.testing.assert_close(refops.conv(x, w, None, s_fold), refops.conv(xp, w, None, s_pad))
+
+
+@pytest.mark.parametrize("shape,k,s,pad", [((2, 12, 11, 13, 1), 7, 2, "same"), ((1, 10, 10, 10, 2), 4, 2, "same"),
+                                           ((2, 13, 12, 11, 1), 7, 2, "valid")])
+def test_s2d_padded_strided_conv_equals_direct(shape, k, s, pad):
+    """Space-to-depth of the zero-padded input + the unpadded stride-1 conv over it == the
+    padded strided conv (the seg model's 'same' 7^3 stride-2 stem takes this path)."""
+    import importlib
+    C = importlib.import_module("featurenet_amd.ops.conv")
+    torch.manual_seed(3)
+    x = torch.randn(*shape)
+    spec = ConvSpec.make(x.shape, 16, k, s, pad)
+    plan = C.s2d_plan(spec)
+    assert plan is not None
+    f, spec2 = plan
+    w = torch.randn(16, k, k, k, shape[-1])
+    x2 = C.s2d_input(x, f, spec2, (spec.pd, spec.ph, spec.pw))
+    y2 = R.conv(x2, C.s2d_weight(w, f, spec, spec2), None, spec2)
+    torch.testing.assert_close(y2, R.conv(x, w, None, spec), rtol=1e-4, atol=1e-4)
