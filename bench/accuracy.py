@@ -116,7 +116,8 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
     acc_b, acc_q = float((pb == y).mean()), float((pq == y).mean())
     return {"top1_bf16": round(acc_b, 4), "top1_fp8": round(acc_q, 4), "drop_pt": round(100 * (acc_b - acc_q), 2),
             "agreement": round(float((pb == pq).mean()), 4), "calib_samples": calib,
-            "kernel": "conv_halo_f8 (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3)"}
+            "kernel": ("conv_halo_f8" if os.environ.get("FN_F8_TILE", "1") == "0" else "conv_tile F8 variant")
+                      + " (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3)"}
 
 
 if __name__ == "__main__":

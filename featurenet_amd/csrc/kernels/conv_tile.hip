@@ -38,6 +38,7 @@
 //
 // Dgrad uses the same kernel: dx = conv(dy, flip(W)^T) with leading pads K-1-p.
 #include "common.h"
+#include "tile_dma.h"
 
 #include <cstdio>
 #include <type_traits>
@@ -58,34 +59,9 @@ struct TileGeom {
   unsigned mTW, mTH;        // magic multipliers for the epilogue's tile-row decode
 };
 
-__device__ __forceinline__ void tile_lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 #define CT_NCW 4                       // compute (MFMA) waves
 #define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
 #define CT_RED_BYTES (CT_NCW * 2 * 32 * 4)   // per-compute-wave BN sums of 32 columns (NT = 2)
-
-// LDS-DMA of one 16-B chunk per lane into lds_dst + 16 * lane (lds_dst wave-uniform);
-// M0 saved/restored in the same statement (it is compiler-reserved)
-__device__ __forceinline__ void ct_glds16(const void* gsrc, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-
-// the same with an SGPR base + per-lane 32-bit byte offset (no 64-bit address math)
-__device__ __forceinline__ void ct_glds16_s(const void* sbase, unsigned voff, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(lds_dst)
-               : "memory");
-}
 
 // packed bf16 pairs (low half = element 0)
 __device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }
@@ -104,10 +80,6 @@ __device__ __forceinline__ float ct_sum16(float x) {
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));   // row_half_mirror
   x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));   // row_mirror
   return x;
-}
-
-__device__ __forceinline__ unsigned ct_lds_addr(const void* p) {
-  return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
 }
 
 typedef int ct_i32x8 __attribute__((ext_vector_type(8)));

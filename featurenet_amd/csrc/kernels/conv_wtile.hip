@@ -1,0 +1,467 @@
+// Weight gradient of a stride-1 3-D convolution on big tiles with a loader wave.
+//
+//   dW[co][tap][ci] = sum over output positions p of dy[p][co] * x[p + tap][ci]
+//
+// The MFMA K axis is the output positions of a tile, so both operands are read from
+// LDS "transposed" (ds_read_b64_tr_b16: each lane names one position row and 4
+// channels; a pair of reads gives the 8 k-values of a 16x16x32 bf16 fragment):
+//   A = dy^T  (16 output channels x 32 positions), MT fragments per k-step
+//   B = x     (32 positions x 16 input channels) at tap offset t, NACC fragments
+// and a wave accumulates MT x NACC 16x16 blocks: all Cout rows x NACC taps of one
+// 16-channel input slice, over every tile its workgroup processes; the blocks are
+// folded into dW with fp32 atomics once, at the end.
+//
+// Structure (as conv_tile.hip): one workgroup per CU = 4 MFMA waves (one per SIMD) + 1
+// loader wave.  A job is one output tile; its x halo (the slice's 16 channels, 32 B per
+// position, position-major) and its dy rows (all Cout channels) are LDS-DMA'd by the
+// loader into one of two buffers while the compute waves run the other -- one barrier
+// per job.  Bank-conflict-free transposed reads:
+//   * x: a 32-lane half reads 8 rows x 4 channel quads at 32*pos + 8*quad -- conflict free
+//     when the 8 rows' halo positions are distinct mod 8; the host orders each aligned
+//     group of 8 k-rows so (rowtab, the same order for dy and x);
+//   * dy: rows of Cout*2 bytes with the 16-B chunks XOR-swizzled per row (the DMA source
+//     chunk of each LDS slot is permuted) so the 8 rows of a half land on 8 distinct bank
+//     groups.
+// Column groups (grid): tap groups (4 waves x NACC taps) x input slices.  Workgroups are
+// XCD-aware: the G column-group workgroups of an XCD share that XCD's contiguous tile
+// range (per-(XCD, group) counters), so a tile's dy and halo are fetched into one L2 and
+// neighbouring tiles' overlapping halos stay there.
+//
+// Reference semantics: the weight gradient of Keras Conv3D (reference model/input.py:294
+// via TF autodiff); the layout / schedule here is MI355X-specific.
+#include "common.h"
+#include "tile_dma.h"
+
+#include <cstdlib>
+
+#define WT_NCW 4
+#define WT_NTHR (64 * (WT_NCW + 1))
+#define WT_GEOM_LEN 24
+
+struct WGeom {
+  int N, ID, IH, IW, C;      // x, channels-last
+  int OD, OH, OW, K;         // dy dims and channels (Cout)
+  int KD, KH, KW;
+  int pd, ph, pw;            // leading pads
+  int TD, TH, TW;            // output tile
+  int HPpad;                 // halo positions, multiple of 32 (whole DMA instructions)
+  int kst;                   // 32-row k-steps per tile
+  int XB;                    // bytes of the x halo of a buffer (HPpad * 32)
+  int BUF;                   // bytes per buffer (XB + kst * 32 * K * 2)
+  int G;                     // column groups (ntg tap groups x C/16 slices)
+  int ntg;                   // tap groups
+};
+
+typedef short wt_s4 __attribute__((ext_vector_type(4)));
+typedef short wt_s8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ bf16x8 wt_tr_pair(const unsigned char* lo, const unsigned char* hi) {
+  const wt_s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) wt_s4*)(lo));
+  const wt_s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) wt_s4*)(hi));
+  const wt_s8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int MT, int NACC>
+__global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __restrict__ x,
+                                                                const bf16* __restrict__ dy,
+                                                                float* __restrict__ dw,   // partials
+                                                                const int2* __restrict__ rowtab,
+                                                                const int* __restrict__ postab,
+                                                                const bf16* __restrict__ zp, WGeom g,
+                                                                int* __restrict__ sched, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  constexpr int CO = MT * 16;
+  constexpr int CPR = CO / 8;                    // 16-B chunks per dy row
+  constexpr int R64 = 256 / (CO * 2);            // dy rows per 64 banks
+  constexpr int NSW = 8 / R64;                   // swizzle classes over 8 rows
+#ifndef WT_PF
+#define WT_PF 4
+#endif
+  constexpr int PF = NACC < WT_PF ? NACC : WT_PF;   // B fragments in flight (register ring)
+  const int ROWS = g.kst * 32;
+  const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
+  const int T = g.KD * g.KH * g.KW;
+  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH, twn = (g.OW + g.TW - 1) / g.TW;
+  const int ntiles = g.N * tdn * thn * twn;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool loader = wave == WT_NCW;
+  // XCD-aware decomposition of the 1-D grid (gridDim.x = 8 * G * workers per group)
+  const int xcd = blockIdx.x & 7, lid = blockIdx.x >> 3;
+  const int grp = lid % g.G;
+  const int tg = grp % g.ntg, slice = grp / g.ntg;
+  const int per = (ntiles + 7) / 8;
+  const int t_lo = xcd * per, t_hi = min(ntiles, t_lo + per);
+  int* cnt = sched + 1 + xcd * g.G + grp;
+
+  // LDS: [buffer 0][buffer 1][s_job 64 B][rows int2 ROWS][positions int HPpad]
+  //      [x offsets int HPpad][dy row offsets int ROWS]
+  int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);
+  int2* s_rows = reinterpret_cast<int2*>(dsm + 2 * g.BUF + 64);
+  int* s_pos = reinterpret_cast<int*>(s_rows + ROWS);
+  int* s_xoff = s_pos + g.HPpad;
+  int* s_yoff = s_xoff + g.HPpad;
+  for (int i = tid; i < ROWS; i += WT_NTHR) {
+    const int2 rt = rowtab[i];
+    s_rows[i] = rt;
+    // byte offset of the row's dy from the tile origin (interior tiles), -1 for a dummy row
+    const int e = rt.y;
+    s_yoff[i] = e < 0 ? -1 : (((e >> 16) * g.OH + ((e >> 8) & 255)) * g.OW + (e & 255)) * CO * 2;
+  }
+  for (int i = tid; i < g.HPpad; i += WT_NTHR) {
+    const int e = postab[i];
+    s_pos[i] = e;
+    // byte offset of the position from the halo origin (interior tiles; 0 past the halo:
+    // those slots are never read)
+    s_xoff[i] = e < 0 ? 0 : (((e >> 16) * g.IH + ((e >> 8) & 255)) * g.IW + (e & 255)) * g.C * 2;
+  }
+  // ---- job protocol ---------------------------------------------------------
+  // s_job[j % 3] = tile of job j (-1: done).  Jobs 0 and 1 are taken before the first
+  // barrier; in iteration j (between barriers A(j) and A(j+1)) the loader takes job j+2's
+  // tile and publishes it and LDS-DMAs job j+1's x halo into the free buffer, and the
+  // compute waves -- after reading jobs j and j+1, before running job j -- DMA a quarter
+  // each of job j+1's dy rows (one wave alone could not keep the LDS fed at this job
+  // size; giving the compute waves part of the x halo as well measured slower).
+  auto grab = [&]() -> int {
+    const int t1 = t_lo + atomicAdd(cnt, 1);
+    return t1 < t_hi ? t1 : -1;
+  };
+  if (tid == 0) {
+    const int t0 = grab();
+    s_job[0] = t0;
+    s_job[1] = t0 >= 0 ? grab() : -1;
+  }
+  tile_lds_barrier();
+
+  auto decode = [&](int tile, int& n, int& d0, int& h0, int& w0) {
+    int t = tile;
+    const int tw = t % twn; t /= twn;
+    const int th = t % thn; t /= thn;
+    const int td = t % tdn;
+    n = t / tdn;
+    d0 = td * g.TD;
+    h0 = th * g.TH;
+    w0 = tw * g.TW;
+  };
+  // dy rows of job `tile` in k order, DMA instructions first, first + step, ... (8 in
+  // flight): slot s = CPR * row + chunk slot, holding source chunk slot ^ swizzle(row)
+  const int ny = (ROWS * CPR) >> 6;
+  auto dma_dy = [&](int tile, int bufoff, int first, int step) {
+    tile = __builtin_amdgcn_readfirstlane(tile);
+    int n, d0, h0, w0;
+    decode(tile, n, d0, h0, w0);
+    const unsigned dst0 = ct_lds_addr(dsm) + (unsigned)bufoff + (unsigned)g.XB;
+    const bf16* ys = dy + (long long)n * g.OD * g.OH * g.OW * CO;
+    const bool y_in = d0 + g.TD <= g.OD && h0 + g.TH <= g.OH && w0 + g.TW <= g.OW;
+    const unsigned char* yo =
+        reinterpret_cast<const unsigned char*>(ys + ((long long)(d0 * g.OH + h0) * g.OW + w0) * CO);
+    for (int j0 = first; j0 < ((dbg & 8) ? 0 : ny); j0 += 8 * step) {   // (dbg 8, timing only: no dy DMA)
+      int o[8], e[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = (64 * min(j0 + i * step, ny - 1) + lane) / CPR;
+        o[i] = s_yoff[r];
+        e[i] = y_in ? 0 : s_rows[r].y;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int j = j0 + i * step;
+        if (j < ny) {
+          const int sl = 64 * j + lane;
+          const int r = sl / CPR;
+          const int c = (sl % CPR) ^ (2 * (((unsigned)r / R64) % NSW));
+          bool ok = o[i] >= 0;
+          if (!y_in) ok = ok && d0 + (e[i] >> 16) < g.OD && h0 + ((e[i] >> 8) & 255) < g.OH && w0 + (e[i] & 255) < g.OW;
+          const void* src = ok ? (const void*)(yo + o[i] + c * 16) : (const void*)zp;
+          ct_glds16(src, dst0 + (unsigned)(j << 10));
+        }
+      }
+    }
+  };
+
+  // x halo of job `tile` (HPpad positions x 2 chunks, one LDS-DMA per 64 slots),
+  // instructions first, first + step, ...  Interior tiles take
+  // precomputed per-slot offsets from an SGPR base (table reads in batches of 8, one LDS
+  // latency per batch); edge tiles check every slot against the input bounds and read
+  // the zero page outside.
+  auto dma_x = [&](int tile, int bufoff, int first, int step) {
+    tile = __builtin_amdgcn_readfirstlane(tile);
+    bufoff = __builtin_amdgcn_readfirstlane(bufoff);
+    int n, d0, h0, w0;
+    decode(tile, n, d0, h0, w0);
+    const int dlo = d0 - g.pd, hlo = h0 - g.ph, wlo = w0 - g.pw;
+    const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
+    const bf16* xs = x + (long long)n * g.ID * g.IH * g.IW * g.C + slice * 16;
+    const int nx = g.HPpad >> 5;               // DMA instructions of the x halo
+    const bool x_in = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID && hlo + HH <= g.IH &&
+                      wlo + HW <= g.IW;
+    if (dbg & 4) {                             // (timing only: no x halo DMA)
+    } else if (x_in) {
+      const bf16* xo = xs + ((long long)(dlo * g.IH + hlo) * g.IW + wlo) * g.C;
+      for (int j0 = first; j0 < nx; j0 += 8 * step) {
+        int o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = s_xoff[((64 * min(j0 + i * step, nx - 1) + lane) >> 1)];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (j0 + i * step < nx)
+            ct_glds16_s(xo, (unsigned)(o[i] + (lane & 1) * 16), dst0 + (unsigned)((j0 + i * step) << 10));
+      }
+    } else {
+      for (int j0 = first; j0 < nx; j0 += 8 * step) {
+        int e[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e[i] = s_pos[((64 * min(j0 + i * step, nx - 1) + lane) >> 1)];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (j0 + i * step < nx) {
+            const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
+            const bool ok = e[i] >= 0 && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                            (unsigned)gw < (unsigned)g.IW;
+            const bf16* src = ok ? xs + ((long long)(gd * g.IH + gh) * g.IW + gw) * g.C + (lane & 1) * 8 : zp;
+            ct_glds16(src, dst0 + (unsigned)((j0 + i * step) << 10));
+          }
+        }
+      }
+    }
+  };
+
+  if (loader) {
+    // ======================= loader wave =======================
+    int cur = __builtin_amdgcn_readfirstlane(s_job[0]);
+    int nxt = __builtin_amdgcn_readfirstlane(s_job[1]);
+    if (cur >= 0) {                              // job 0 entirely by the loader
+      dma_x(cur, 0, 0, 1);
+      dma_dy(cur, 0, 0, 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int par = 0, j = 0;
+    while (true) {
+      tile_lds_barrier();                        // A(j): job j's buffer landed, the other is free
+      if (cur < 0) break;
+      int t2 = -1;
+      if (nxt >= 0) {
+        if (lane == 0) t2 = grab();              // job j+2 (its round trip overlaps the DMAs)
+        if (!(dbg & 1)) dma_x(nxt, (par ^ 1) * g.BUF, 0, 1);   // (dbg 1: timing only, stale data)
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      t2 = __builtin_amdgcn_readfirstlane(t2);
+      if (lane == 0) s_job[(j + 2) % 3] = t2;
+      cur = nxt;
+      nxt = t2;
+      par ^= 1;
+      ++j;
+    }
+    return;
+  }
+
+  // ======================= compute waves =======================
+  const int G4 = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+  const int tap0 = (tg * WT_NCW + wave) * NACC;
+  int toff[NACC];                                // byte offsets of this wave's taps in the halo
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) {
+    const int t = tap0 + i < T ? tap0 + i : 0;   // dead taps read tap 0 (never stored)
+    const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
+    toff[i] = ((kd * HH + kh) * HW + kw) * 32;
+  }
+  const bool live = tap0 < T;
+  f32x4 acc[NACC][MT];
+#pragma unroll
+  for (int i = 0; i < NACC; ++i)
+#pragma unroll
+    for (int j = 0; j < MT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // dy fragment address of k-row r, 16-channel block mt: this lane's 4-channel quad
+  auto dy_addr = [&](int r, int mt) -> int {
+    return r * (CO * 2) + (((2 * mt + (p4 >> 1)) ^ (2 * (((unsigned)r / R64) % NSW))) << 4) + (p4 & 1) * 8;
+  };
+  // One flat loop over (job, k-step): the accumulators are carried by a single loop (with
+  // a job loop around a k-step loop, hipcc copied all of them at every job start).
+  // Every wave runs it (dead taps read tap 0 and are never stored).  B fragments run PF
+  // taps ahead in a register ring, across the k-step boundary; a job starts with a ring
+  // fill after its barrier.
+  int par = 0, ks = 0;
+  const unsigned char* xb = dsm;
+  const unsigned char* yb = dsm;
+  int plo = 0, phi = 0;
+  bf16x8 ring[PF], fa[MT];
+  auto rows_of = [&](int k, int& lo, int& hi) {
+    const int r_lo = k * 32 + 4 * G4 + q;
+    lo = s_rows[r_lo].x + 8 * p4;
+    hi = s_rows[r_lo + 16].x + 8 * p4;
+  };
+  auto read_b = [&](int lo, int hi, int i) -> bf16x8 { return wt_tr_pair(xb + lo + toff[i], xb + hi + toff[i]); };
+  auto read_a = [&](int k, bf16x8* f) {
+    const int r_lo = k * 32 + 4 * G4 + q;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) f[mt] = wt_tr_pair(yb + dy_addr(r_lo, mt), yb + dy_addr(r_lo + 16, mt));
+  };
+  int jc = 0;                                   // job index (s_job ring slot jc % 3)
+  auto start_job = [&]() -> bool {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's dy DMAs of the job about to start
+    tile_lds_barrier();                          // A
+    const int tile = __builtin_amdgcn_readfirstlane(s_job[jc % 3]);
+    if (tile < 0) return false;
+    const int nxt = __builtin_amdgcn_readfirstlane(s_job[(jc + 1) % 3]);
+    if (nxt >= 0 && !(dbg & 1)) dma_dy(nxt, (par ^ 1) * g.BUF, wave, WT_NCW);   // a quarter of job j+1's dy
+    ++jc;
+    xb = dsm + par * g.BUF;
+    yb = xb + g.XB;
+    rows_of(0, plo, phi);
+    read_a(0, fa);
+#pragma unroll
+    for (int p = 0; p < PF; ++p) ring[p] = read_b(plo, phi, p);
+    return true;
+  };
+  if (start_job()) {
+    while (true) {
+      // this k-step's A fragments were read during the previous one (or at the job start);
+      // the next k-step's rows and A fragments are read here, a whole k-step ahead
+      const int ksn = ks + 1 < g.kst ? ks + 1 : ks;   // (a job's last k-step re-reads itself: unused)
+      int plo_n, phi_n;
+      rows_of(ksn, plo_n, phi_n);
+      bf16x8 fa_n[MT];
+#pragma unroll
+      for (int i = 0; i < NACC; ++i) {
+        const bf16x8 fb = ring[i % PF];
+        if (i + PF < NACC) ring[i % PF] = read_b(plo, phi, i + PF);
+        else ring[i % PF] = read_b(plo_n, phi_n, i + PF - NACC);
+        if (i == 0) read_a(ksn, fa_n);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb, acc[i][mt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) fa[mt] = fa_n[mt];
+      plo = plo_n;
+      phi = phi_n;
+      if (++ks == g.kst) {
+        ks = 0;
+        par ^= 1;
+        if (!start_job()) break;
+      }
+    }
+  }
+  // D[row = co][col = ci]: lane holds co = mt*16 + (lane>>4)*4 + r, ci = lane & 15.
+  // Plain stores into this workgroup's partial dW (partial = XCD x worker: the G
+  // column-group workgroups of one (XCD, worker) write disjoint columns of it), summed
+  // in a fixed order by wtile_reduce_kernel: deterministic, no atomics.
+  float* part = dw + (long long)(xcd * ((int)(gridDim.x >> 3) / g.G) + lid / g.G) * g.K * T * g.C;
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) {
+      const int t = tap0 + i;
+      if (t < T) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int co = mt * 16 + G4 * 4 + r;
+            part[((long long)co * T + t) * g.C + slice * 16 + (lane & 15)] = acc[i][mt][r];
+          }
+      }
+    }
+  }
+  if (tid == 0) {                                // the last workgroup out resets the counters
+    __threadfence();
+    if (atomicAdd(sched, 1) == (int)gridDim.x - 1) {
+      for (int i = 0; i < 8 * g.G; ++i) atomicExch(sched + 1 + i, 0);
+      atomicExch(sched, 0);
+    }
+  }
+}
+
+// dw[e] (+)= sum over the partials p = 0 .. W-1 of part[p][e], in that order
+__global__ __launch_bounds__(256) void wtile_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                           long long n, int W, int accumulate) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  if (i + 4 <= n) {
+    float4 a = accumulate ? *(const float4*)(dw + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < W; ++p) {
+      const float4 v = *(const float4*)(part + (long long)p * n + i);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    *(float4*)(dw + i) = a;
+  } else {
+    for (long long j = i; j < n; ++j) {
+      float a = accumulate ? dw[j] : 0.f;
+      for (int p = 0; p < W; ++p) a += part[(long long)p * n + j];
+      dw[j] = a;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launcher
+// ---------------------------------------------------------------------------
+static WGeom parse_wgeom(const int* v) {
+  WGeom g;
+  g.N = v[0]; g.ID = v[1]; g.IH = v[2]; g.IW = v[3]; g.C = v[4];
+  g.OD = v[5]; g.OH = v[6]; g.OW = v[7]; g.K = v[8];
+  g.KD = v[9]; g.KH = v[10]; g.KW = v[11];
+  g.pd = v[12]; g.ph = v[13]; g.pw = v[14];
+  g.TD = v[15]; g.TH = v[16]; g.TW = v[17];
+  g.HPpad = v[18]; g.kst = v[19]; g.XB = v[20]; g.BUF = v[21]; g.G = v[22]; g.ntg = v[23];
+  return g;
+}
+
+static size_t wtile_lds(const WGeom& g) {
+  return 2 * (size_t)g.BUF + 64 + (size_t)g.kst * 32 * 12 + (size_t)g.HPpad * 8;
+}
+
+extern "C" int fn_conv_wtile_supported(int K, int nacc) {
+  return (K == 16 && nacc == 16) || (K == 32 && (nacc == 8 || nacc == 16)) || (K == 64 && nacc == 8);
+}
+
+// dw: fp32 [K][T][C], accumulated into (+=); part: fp32 scratch [8 * workers][K][T][C]; rowtab int2[kst*32] (halo byte offset of
+// the row's tap-0 position, packed tile coords or -1), k order with distinct halo positions
+// mod 8 per aligned group of 8; postab int[HPpad] packed halo coords (-1 past the halo);
+// zp >= 16 zero bytes; sched int[64] zeroed (left zero); workers = workgroups per (XCD,
+// column group).
+extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* part, const void* rowtab,
+                             const void* postab, const void* zp, const int* geom, int nacc, int workers, int* sched,
+                             hipStream_t st) {
+  const WGeom g = parse_wgeom(geom);
+  if (!fn_conv_wtile_supported(g.K, nacc) || g.C % 16 || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
+  const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
+  const long long HP = (long long)(g.TD + g.KD - 1) * HH * HW;
+  const int T = g.KD * g.KH * g.KW;
+  if (g.HPpad < HP || g.HPpad % 32 || g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
+  if ((long long)g.TD * g.TH * g.TW > 32LL * g.kst || g.kst < 1 || g.kst > 32) return -3;
+  if (g.XB != g.HPpad * 32 || g.BUF < g.XB + g.kst * 32 * g.K * 2 || g.BUF % 1024) return -3;
+  if (g.ntg != (T + 4 * nacc - 1) / (4 * nacc) || g.G != g.ntg * (g.C / 16) || 8 * g.G > 63) return -3;
+  if ((g.kst * 32 * (g.K / 8)) % 64) return -3;
+  const size_t lds = wtile_lds(g);
+  if (lds > 160 * 1024) return -4;
+  if (!sched || !zp || !part || workers < 1) return -6;
+  const unsigned grid = 8u * (unsigned)g.G * (unsigned)workers;
+  static const int dbg = [] { const char* e = getenv("FN_WTILE_DBG"); return e ? atoi(e) : 0; }();
+#define WT_CASE(M, A)                                                                                          \
+  if (g.K == M * 16 && nacc == A) {                                                                            \
+    static size_t cfg = 0;                                                                                     \
+    if (lds > cfg) {                                                                                           \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A>,                                 \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
+      if (e != hipSuccess) return (int)e;                                                                      \
+      cfg = lds;                                                                                               \
+    }                                                                                                          \
+    hipLaunchKernelGGL((conv_wtile_kernel<M, A>), dim3(grid), dim3(WT_NTHR), lds, st, (const bf16*)x,          \
+                       (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab, (const bf16*)zp, g, sched, \
+                       dbg);                                                                                   \
+  }
+  WT_CASE(1, 16)
+  WT_CASE(2, 8)
+  WT_CASE(2, 16)
+  WT_CASE(4, 8)
+#undef WT_CASE
+  FN_CHECK_LAUNCH();
+  const long long n = (long long)g.K * T * g.C;
+  hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n / 4 + 256) / 256)), dim3(256), 0, st, part, dw, n,
+                     8 * workers, 1);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,34 @@
+// LDS-DMA and barrier helpers shared by the big-tile conv kernels (conv_tile.hip,
+// conv_wtile.hip).
+#pragma once
+#include "common.h"
+
+__device__ __forceinline__ void tile_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA of one 16-B chunk per lane into lds_dst + 16 * lane (lds_dst wave-uniform);
+// M0 saved/restored in the same statement (it is compiler-reserved)
+__device__ __forceinline__ void ct_glds16(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+// the same with an SGPR base + per-lane 32-bit byte offset (no 64-bit address math)
+__device__ __forceinline__ void ct_glds16_s(const void* sbase, unsigned voff, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_dst)
+               : "memory");
+}
+
+__device__ __forceinline__ unsigned ct_lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+

@@ -28,6 +28,7 @@ import torch
 
 from .. import _native
 from . import conv_tile
+from . import conv_wtile
 from . import reference as ref
 from ..training.flat import grad_target
 from .spec import ConvSpec, act_code
@@ -436,6 +437,13 @@ def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=N
     """fp32 dW [K, KD, KH, KW, C]; ``out`` (zeroed, contiguous, that shape) receives it in place
     where the kernel allows."""
     plan = halo_wgrad_plan(spec)
+    wplan = conv_wtile.plan(spec)
+    if wplan is not None:
+        dy5, x5 = dy5.contiguous(), x5.contiguous()
+        use = plan is None or conv_wtile.choose(
+            spec, lambda: conv_wtile.conv_wgrad(dy5, x5, spec, wplan), lambda: halo_conv_wgrad(dy5, x5, spec, plan))
+        if use:
+            return conv_wtile.conv_wgrad(dy5, x5, spec, wplan, out=out)
     if plan is not None:
         return halo_conv_wgrad(dy5.contiguous(), x5.contiguous(), spec, plan, out=out)
     K = _native.kernels()

@@ -1,0 +1,242 @@
+"""Host side of the big-tile weight-gradient kernel (``csrc/kernels/conv_wtile.hip``).
+
+dW of a stride-1 3-D conv as an MFMA GEMM over output positions (K axis), one
+workgroup per CU (4 MFMA waves + an LDS-DMA loader wave), double-buffered
+tiles, XCD-aware column groups.  This module plans the tile (shape, k-steps,
+LDS), builds the k-row order that keeps the transposed halo reads bank-conflict
+free (every aligned group of 8 k-rows has 8 distinct halo positions mod 8) and
+launches the kernel.
+
+Reference parity: the weight gradient of Keras ``Conv3D`` (reference
+``model/input.py:294``, TF autodiff); ``ops/conv.py`` keeps the conv_halo
+wgrad as the fallback and A/B partner.
+"""
+from __future__ import annotations
+
+import math
+import os
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import _native
+
+LDS_MAX = 160 * 1024
+N_CUS = 256
+_LOCK = threading.Lock()
+_PLANS: dict = {}
+_TABS: dict = {}
+_SCHED: dict = {}
+_ZERO: dict = {}
+
+
+@dataclass(frozen=True)
+class WPlan:
+    TD: int
+    TH: int
+    TW: int
+    HPpad: int
+    kst: int
+    nacc: int
+    ntg: int
+    G: int
+    workers: int
+    BUF: int
+    cost: float
+
+    @property
+    def rows(self) -> int:
+        return self.TD * self.TH * self.TW
+
+
+def mode() -> str:
+    """FN_WTILE: 1 (default) = per-shape timed choice vs conv_halo wgrad, 2 = always, 0 = off."""
+    return os.environ.get("FN_WTILE", "1")
+
+
+def _nacc(K: int, T: int) -> int | None:
+    if K == 16:
+        return 16
+    if K == 64:
+        return 8
+    if K == 32:
+        def used(a):
+            return T / (math.ceil(T / (4 * a)) * 4 * a)
+        return 8 if used(8) >= 1.15 * used(16) else 16
+    return None
+
+
+def plan(spec) -> WPlan | None:
+    if mode() == "0" or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
+        return None
+    key = (spec.N, spec.D, spec.H, spec.W, spec.C, spec.K, spec.KD, spec.KH, spec.KW, spec.OD, spec.OH, spec.OW)
+    if key in _PLANS:
+        return _PLANS[key]
+    p = _plan(spec)
+    with _LOCK:
+        _PLANS[key] = p
+    return p
+
+
+def _plan(spec):
+    K, C = spec.K, spec.C
+    T = spec.KD * spec.KH * spec.KW
+    nacc = _nacc(K, T)
+    if nacc is None or C % 16 or T < 2:
+        return None
+    ntg = -(-T // (4 * nacc))
+    G = ntg * (C // 16)
+    if 8 * G > 63:
+        return None
+    workers = max(1, N_CUS // (8 * G))
+    OD, OH, OW = spec.OD, spec.OH, spec.OW
+    MT = K // 16
+    best = None
+    tw_opts = sorted({OW} | {-(-OW // k) for k in range(2, 6) if -(-OW // k) >= 8})
+    for TW in tw_opts:
+        for TD in range(1, OD + 1):
+            for TH in range(1, OH + 1):
+                rows = TD * TH * TW
+                if rows > 1024:
+                    break
+                kst = -(-rows // 32)
+                if rows < 0.85 * kst * 32 or rows < 96:
+                    continue
+                HH, HW = TH + spec.KH - 1, TW + spec.KW - 1
+                HP = (TD + spec.KD - 1) * HH * HW
+                if max(TD + spec.KD - 1, HH, HW) > 255:
+                    continue
+                HPpad = -(-HP // 32) * 32
+                BUF = -(-(HPpad * 32 + kst * 32 * K * 2) // 1024) * 1024
+                lds = 2 * BUF + 64 + kst * 32 * 12 + HPpad * 8        # + row / position / offset tables
+                if lds > LDS_MAX:
+                    continue
+                tiles = spec.N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
+                jobs = math.ceil(math.ceil(tiles / 8) / workers)
+                mfma = kst * nacc * MT * 16 + 400                 # per compute wave per job
+                loader = 600 + (HPpad * 2 // 64 + kst * K // 16) * 60
+                cost = jobs * max(mfma, loader) * (1.0 + 0.02 * HP / rows)   # halo re-reads (L2 traffic)
+                if best is None or cost < best.cost:
+                    best = WPlan(TD, TH, TW, HPpad, kst, nacc, ntg, G, workers, BUF, float(cost))
+    return best
+
+
+def tables(p: WPlan, kdims: tuple) -> tuple[np.ndarray, np.ndarray]:
+    """(rowtab int32 [kst*32, 2], postab int32 [HPpad]).
+
+    rowtab: per k-row (byte offset 32*hpos of its tap-0 halo position, packed tile coords
+    td<<16 | th<<8 | tw, or -1 for a dummy row), ordered so every aligned group of 8 rows
+    has 8 distinct hpos mod 8; dummies take a missing residue (a real halo position).
+    postab: packed halo coords hd<<16 | hh<<8 | hw per position, -1 past the halo."""
+    key = (p, tuple(kdims))
+    t = _TABS.get(key)
+    if t is not None:
+        return t
+    KD, KH, KW = kdims
+    HH, HW = p.TH + KH - 1, p.TW + KW - 1
+    td, th, tw = np.meshgrid(np.arange(p.TD), np.arange(p.TH), np.arange(p.TW), indexing="ij")
+    hpos = ((td * HH + th) * HW + tw).reshape(-1)
+    pk = ((td << 16) | (th << 8) | tw).reshape(-1)
+    buckets = [list(zip(hpos[hpos % 8 == r].tolist(), pk[hpos % 8 == r].tolist())) for r in range(8)]
+    ngroups = p.kst * 4
+    groups = [[None] * 8 for _ in range(ngroups)]
+    extra = []
+    for r in range(8):
+        for i, item in enumerate(buckets[r]):
+            if i < ngroups:
+                groups[i][r] = item
+            else:
+                extra.append(item)
+    for gr in groups:                             # overflow rows fill free slots (a conflict, not an error)
+        for s in range(8):
+            if gr[s] is None and extra:
+                gr[s] = extra.pop()
+    assert not extra, "row table overflow"
+    for gr in groups:
+        for s in range(8):
+            if gr[s] is None:
+                used = {x[0] % 8 for x in gr if x is not None}
+                cand = [r for r in range(8) if r not in used]
+                gr[s] = ((cand[0] if cand else 0), -1)
+    rows = np.asarray([(h * 32, k) for gr in groups for (h, k) in gr], dtype=np.int32)
+    HP = (p.TD + KD - 1) * HH * HW
+    pos = np.full(p.HPpad, -1, dtype=np.int32)
+    q = np.arange(HP)
+    pos[:HP] = ((q // (HH * HW)) << 16) | (((q // HW) % HH) << 8) | (q % HW)
+    with _LOCK:
+        _TABS[key] = (rows, pos)
+    return rows, pos
+
+
+def _dev(cache: dict, key, make):
+    t = cache.get(key)
+    if t is None:
+        t = make()
+        with _LOCK:
+            cache[key] = t
+    return t
+
+
+_PART: dict = {}
+_RETIRED: list = []
+
+
+def _partials(dev, stream: int, n: int) -> torch.Tensor:
+    """fp32 scratch for the per-(XCD, worker) partial weight gradients (one buffer per device
+    and stream, grown to the largest layer; the kernel overwrites what it reads)."""
+    key = (str(dev), stream)
+    t = _PART.get(key)
+    if t is None or t.numel() < n:
+        t = torch.empty(n, dtype=torch.float32, device=dev)
+        with _LOCK:
+            if key in _PART:                     # a captured hipGraph may still name the old one
+                _RETIRED.append(_PART[key])
+            _PART[key] = t
+    return t
+
+
+def geometry(p: WPlan, spec) -> list[int]:
+    XB = p.HPpad * 32
+    return [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.K, spec.KD, spec.KH, spec.KW,
+            spec.pd, spec.ph, spec.pw, p.TD, p.TH, p.TW, p.HPpad, p.kst, XB, p.BUF, p.G, p.ntg]
+
+
+def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) -> torch.Tensor:
+    """dW fp32 [K, KD, KH, KW, C] on the big-tile wgrad kernel (accumulated into ``out``
+    when given: a zeroed contiguous fp32 tensor of that size, e.g. the flat gradient)."""
+    kd = (spec.KD, spec.KH, spec.KW)
+    dev = x5.device
+    rt_np, pt_np = tables(p, kd)
+    rt = _dev(_TABS, ("rt", p, kd, str(dev)), lambda: torch.from_numpy(rt_np).to(dev))
+    pt = _dev(_TABS, ("pt", p, kd, str(dev)), lambda: torch.from_numpy(pt_np).to(dev))
+    zp = _dev(_ZERO, str(dev), lambda: torch.zeros(64, dtype=torch.bfloat16, device=dev))
+    st = _native.stream(x5)
+    sched = _dev(_SCHED, (str(dev), st), lambda: torch.zeros(64, dtype=torch.int32, device=dev))
+    dw = out if out is not None else torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=dev)
+    part = _partials(dev, st, 8 * p.workers * dw.numel())
+    _native.kernels().conv_wtile(x5.data_ptr(), dy5.data_ptr(), dw.data_ptr(), part.data_ptr(), rt.data_ptr(),
+                                 pt.data_ptr(), zp.data_ptr(), geometry(p, spec), p.nacc, p.workers, sched.data_ptr(),
+                                 st, [x5.numel(), dy5.numel(), dw.numel(), rt.numel() // 2, pt.numel(), part.numel()])
+    return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
+
+
+_CHOICE: dict = {}
+
+
+def choose(spec, run_wtile, run_halo) -> bool:
+    """True when this kernel should run the weight gradient of ``spec``: FN_WTILE=2 always,
+    1 (default) by timing both kernels once per shape (outside graph capture; the first
+    call of a shape during capture takes this kernel)."""
+    if mode() == "2":
+        return True
+    c = _CHOICE.get(spec)
+    if c is None:
+        if torch.cuda.is_current_stream_capturing():
+            return True
+        from .conv_tile import _time_ms
+        c = _time_ms(run_wtile) <= _time_ms(run_halo)
+        with _LOCK:
+            _CHOICE[spec] = c
+    return c

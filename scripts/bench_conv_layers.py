@@ -4,7 +4,7 @@
 For each stride-1 layer (conv2..conv4; ``--only seg_dec`` for the segmentation
 decoder conv) times forward (BN-statistics epilogue) and dgrad on the big-tile
 kernel (``conv_tile.hip``) and on the previous halo kernel (``conv_halo.hip``),
-and the halo weight gradient, back to back on one stream (events around R
+and the weight gradient on conv_halo and on the big-tile wgrad kernel (conv_wtile.hip), back to back on one stream (events around R
 launches), and prints us/call and model TFLOP/s.
 
     python scripts/bench_conv_layers.py --batch 128 --reps 10
@@ -24,6 +24,7 @@ import importlib  # noqa: E402
 
 cv = importlib.import_module("featurenet_amd.ops.conv")   # the module (ops.conv is also a function name)
 from featurenet_amd.ops import conv_tile as ct  # noqa: E402
+from featurenet_amd.ops import conv_wtile as cw  # noqa: E402
 from featurenet_amd.ops.spec import ConvSpec  # noqa: E402
 
 LAYERS = [("stem_s2d", 32, 8, 32, 4, "valid"), ("conv2", 29, 32, 32, 5, "valid"), ("conv3", 25, 32, 64, 4, "valid"),
@@ -61,11 +62,13 @@ def main():
         pf, pd = ct.fwd_plan(spec), ct.dgrad_plan(spec)
         res = {"layer": name, "gflop": round(gf, 1), "tile_fwd_plan": str(pf), "tile_dgrad_plan": str(pd)}
         hf, hd, hw = cv.halo_fwd_plan(spec), cv.halo_dgrad_plan(spec), cv.halo_wgrad_plan(spec)
+        pw = cw.plan(spec)
         runs = {"halo_fwd": (hf, lambda: cv.halo_conv_fwd(x, w, None, spec, 0, True, hf)),
                 "tile_fwd": (pf, lambda: ct.conv_fwd(x, w, None, spec, 0, True, pf)),
                 "halo_dgrad": (hd, lambda: cv.halo_conv_dgrad(dy, w, spec, hd)),
                 "tile_dgrad": (pd, lambda: ct.conv_dgrad(dy, w, spec, pd)),
-                "halo_wgrad": (hw, lambda: cv.halo_conv_wgrad(dy, x, spec, hw))}
+                "halo_wgrad": (hw, lambda: cv.halo_conv_wgrad(dy, x, spec, hw)),
+                "wtile_wgrad": (pw, lambda: cw.conv_wgrad(dy, x, spec, pw))}
         for kk, (pl, fn) in runs.items():
             if pl is None:
                 continue
