@@ -286,7 +286,7 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
   int par = 0, ks = 0;
   const unsigned char* xb = dsm;
   const unsigned char* yb = dsm;
-  int plo = 0, phi = 0;
+  int plo = 0, phi = 0, plo_n = 0, phi_n = 0;   // row offsets of k-steps ks and ks + 1
   bf16x8 ring[PF], fa[MT];
   auto rows_of = [&](int k, int& lo, int& hi) {
     const int r_lo = k * 32 + 4 * G4 + q;
@@ -311,6 +311,7 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
     xb = dsm + par * g.BUF;
     yb = xb + g.XB;
     rows_of(0, plo, phi);
+    rows_of(g.kst > 1 ? 1 : 0, plo_n, phi_n);
     read_a(0, fa);
 #pragma unroll
     for (int p = 0; p < PF; ++p) ring[p] = read_b(plo, phi, p);
@@ -320,24 +321,30 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
     while (true) {
       // this k-step's A fragments were read during the previous one (or at the job start);
       // the next k-step's rows and A fragments are read here, a whole k-step ahead
-      const int ksn = ks + 1 < g.kst ? ks + 1 : ks;   // (a job's last k-step re-reads itself: unused)
-      int plo_n, phi_n;
-      rows_of(ksn, plo_n, phi_n);
+      // row offsets two k-steps ahead (read here, used for the next k-step's ring refill: a
+      // read consumed in the same k-step made hipcc drain every LDS read in flight)
+      const int ksn = ks + 1 < g.kst ? ks + 1 : ks;   // (a job's last k-steps re-read themselves: unused)
+      const int ksnn = ks + 2 < g.kst ? ks + 2 : ksn;
+      int plo_nn, phi_nn;
+      rows_of(ksnn, plo_nn, phi_nn);
       bf16x8 fa_n[MT];
 #pragma unroll
       for (int i = 0; i < NACC; ++i) {
-        const bf16x8 fb = ring[i % PF];
-        if (i + PF < NACC) ring[i % PF] = read_b(plo, phi, i + PF);
-        else ring[i % PF] = read_b(plo_n, phi_n, i + PF - NACC);
-        if (i == 0) read_a(ksn, fa_n);
+        // the MFMAs read the ring slot in place; its refill (tap i + PF) is issued after
+        // them (a copy of the slot would be a VALU write in front of every MFMA)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-          acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], fb, acc[i][mt], 0, 0, 0);
+          acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mt], ring[i % PF], acc[i][mt], 0, 0, 0);
+        if (i == 0) read_a(ksn, fa_n);
+        if (i + PF < NACC) ring[i % PF] = read_b(plo, phi, i + PF);
+        else ring[i % PF] = read_b(plo_n, phi_n, i + PF - NACC);
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) fa[mt] = fa_n[mt];
       plo = plo_n;
       phi = phi_n;
+      plo_n = plo_nn;
+      phi_n = phi_nn;
       if (++ks == g.kst) {
         ks = 0;
         par ^= 1;
