@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--train", type=int, default=6000)
     ap.add_argument("--mode", default="inline", choices=["inline", "process"])
+    ap.add_argument("--dataset", default="mnist", choices=["mnist", "cifar"])
     a = ap.parse_args()
     from featurenet_amd.ir.parse import parse_feature_model
     from featurenet_amd.search.mutation import MutationConfig, Mutator
@@ -32,7 +33,7 @@ def main():
         s.name = f"c{i}"
     sched = TrialScheduler(mode=a.mode)
     for graph in (False, True):
-        cfg = TrialConfig(dataset="mnist", epochs=a.epochs, batch_size=64, synthetic_sizes=(a.train, 1000),
+        cfg = TrialConfig(dataset=a.dataset, epochs=a.epochs, batch_size=64, synthetic_sizes=(a.train, 1000),
                           graph=graph)
         t0 = time.perf_counter()
         out = sched.map(specs, cfg)
