@@ -54,6 +54,9 @@ int fn_bn_bwd_apply(const void*, const void*, const float*, const float*, const 
                     const float*, void*, long long, int, float, int, hipStream_t);
 int fn_pool_fwd(const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd(const void*, const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
+int fn_pool_bwd_stats_blocks(const int*);
+int fn_pool_bwd_stats(const void*, const void*, void*, const float*, const float*, const int*, int, float*,
+                      hipStream_t);
 int fn_softmax_xent_blocks(long long, int);
 int fn_upsample2x(const void*, void*, int, int, int, int, int, int, hipStream_t);
 int fn_softmax_xent_rows(const void*, int, const long long*, float*, void*, int*, long long, int, float, float,
@@ -68,7 +71,7 @@ int fn_dropout(const void*, void*, long long, float, unsigned, unsigned, hipStre
 int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
-                 const int*, int, int, int, int, int*, hipStream_t);
+                 const int*, int, int, int, int, int*, hipStream_t, const void*, const float*);
 int fn_conv_tile_workers(const int*, int, int);
 int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
                     float, const int*, int, int, int, int, int*, hipStream_t);
@@ -186,16 +189,21 @@ PYBIND11_MODULE(_C, m) {
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>());
   m.def("conv_tile", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                         uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
-                        uintptr_t sched, uintptr_t st, std::vector<long long> ext) {
+                        uintptr_t sched, uintptr_t st, std::vector<long long> ext, uintptr_t bny, uintptr_t bnp) {
     need(geom, 26, "conv_tile");
     check_tile(geom, ext, ncol, MT, "conv_tile");
+    if (bny) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
+      fits(ext, 5, prod({geom[0], geom[5], geom[6], geom[7], ncol}), "conv_tile", "bny");
+      fits(ext, 6, 4LL * ncol, "conv_tile", "bnp");
+    }
     chk(fn_conv_tile(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
                      P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
-                     act, MT, NT, P<int*>(sched), S(st)),
+                     act, MT, NT, P<int*>(sched), S(st), P<const void*>(bny), P<const float*>(bnp)),
         "conv_tile");
   }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
-     py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>());
+     py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("bny") = 0,
+     py::arg("bnp") = 0);
   m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
                            uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,
                            int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext) {
@@ -411,6 +419,20 @@ PYBIND11_MODULE(_C, m) {
         "pool_bwd");
   }, py::arg("dout"), py::arg("x"), py::arg("dx"), py::arg("scale"), py::arg("shift"), py::arg("geom"),
      py::arg("is_max"), py::arg("count_pad"), py::arg("act"), py::arg("st"), py::arg("ext") = std::vector<long long>());
+  m.def("pool_bwd_stats_blocks", [](std::vector<int> geom) {
+    need(geom, 17, "pool_bwd_stats_blocks");
+    return fn_pool_bwd_stats_blocks(geom.data());
+  });
+  m.def("pool_bwd_stats", [check_pool](uintptr_t dout, uintptr_t x, uintptr_t dx, uintptr_t scale, uintptr_t shift,
+                             std::vector<int> geom, int act, uintptr_t part, uintptr_t st, std::vector<long long> ext) {
+    need(geom, 17, "pool_bwd_stats");
+    check_pool(geom, ext, "pool_bwd_stats");   // ext = {x (and dx), dout, part}
+    fits(ext, 2, 2LL * fn_pool_bwd_stats_blocks(geom.data()) * geom[4], "pool_bwd_stats", "part");
+    chk(fn_pool_bwd_stats(P<const void*>(dout), P<const void*>(x), P<void*>(dx), P<const float*>(scale),
+                          P<const float*>(shift), geom.data(), act, P<float*>(part), S(st)),
+        "pool_bwd_stats");
+  }, py::arg("dout"), py::arg("x"), py::arg("dx"), py::arg("scale"), py::arg("shift"), py::arg("geom"),
+     py::arg("act"), py::arg("part"), py::arg("st"), py::arg("ext") = std::vector<long long>());
   m.def("upsample2x", [](uintptr_t x, uintptr_t y, int N, int D, int H, int W, int C, int backward, uintptr_t st) {
     chk(fn_upsample2x(P<const void*>(x), P<void*>(y), N, D, H, W, C, backward, S(st)), "upsample2x");
   });

@@ -136,9 +136,15 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
         run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * (float)mean;
         run_var[c] = (1.f - momentum) * run_var[c] + momentum * (float)unb;
       }
-    } else {
+    } else if (MODE == 1) {
       out0[c] = (float)sa[0];
       out1[c] = (float)sb[0];
+    } else {
+      // MODE 2: raw backward moments (sum g, sum g*y) from the conv_tile dgrad epilogue; the
+      // mean / invstd of the forward pass come in run_mean / run_var (read only):
+      // dbeta = sum g, dgamma = sum g*xhat = invstd * (sum g*y - mean * sum g), in fp64
+      out0[c] = (float)sa[0];
+      out1[c] = (float)((double)run_var[c] * (sb[0] - (double)run_mean[c] * sa[0]));
     }
   }
 }
@@ -456,15 +462,23 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16* __restrict__ 
 // (16-B vectors), recomputes the BN+act prologue, picks the first arg-max and
 // writes the whole window of dx -- every input element is written exactly
 // once, so no zero-fill pass and no gather recomputation.
-template <int VW>
+//
+// STATS (max pool after BN+act, VW = 8, 256 % (C/8) == 0 so a thread keeps its channel chunk):
+// also the BN backward's raw moments (sum g, sum g*y), g = dx * act'(z) -- nonzero only at a
+// window's arg-max, where z is the window max and y its pre-BN value -- as per-block rows
+// part[block][2][C] (bn_finalize MODE 2), so no colstats pass over dx and y follows.
+template <int VW, bool STATS = false>
 __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ x,
                                                              bf16* __restrict__ dx, const float* __restrict__ scale,
                                                              const float* __restrict__ shift, PoolGeom g, int is_max,
-                                                             int act) {
+                                                             int act, float* __restrict__ part = nullptr) {
   const int cpr = g.C / VW;
   const long long total = (long long)g.N * g.OD * g.OH * g.OW * cpr;
   const int win = g.KD * g.KH * g.KW;
   const float inv = 1.f / (float)win;
+  float s0[STATS ? VW : 1], s1[STATS ? VW : 1];
+#pragma unroll
+  for (int j = 0; j < (STATS ? VW : 1); ++j) s0[j] = s1[j] = 0.f;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const int ch = (int)(i % cpr);
     long long t = i / cpr;
@@ -472,7 +486,7 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
     const int oh = (int)(t % g.OH); t /= g.OH;
     const int od = (int)(t % g.OD);
     const long long n = t / g.OD;
-    float go[VW], sc[VW], sh[VW], best[VW];
+    float go[VW], sc[VW], sh[VW], best[VW], yarg[VW];
     int arg[VW];
     Pack8 pg;
     if constexpr (VW == 8) pg.u = *(const uint4*)(dout + i * 8); else pg.e[0] = dout[i];
@@ -480,6 +494,7 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
     for (int j = 0; j < VW; ++j) {
       go[j] = bf2f(pg.e[j]);
       best[j] = -INFINITY;
+      yarg[j] = 0.f;
       arg[j] = 0;
       sc[j] = scale ? scale[ch * VW + j] : 1.f;
       sh[j] = scale ? shift[ch * VW + j] : 0.f;
@@ -496,9 +511,18 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
         if constexpr (VW == 8) p.u = *(const uint4*)(x + b); else p.e[0] = x[b];
 #pragma unroll
         for (int j = 0; j < VW; ++j) {
-          float v = bf2f(p.e[j]);
+          const float yv = bf2f(p.e[j]);
+          float v = yv;
           if (scale) v = act_fwd(v * sc[j] + sh[j], act);
-          if (v > best[j]) { best[j] = v; arg[j] = w; }
+          if (v > best[j]) { best[j] = v; arg[j] = w; yarg[j] = yv; }
+        }
+      }
+      if constexpr (STATS) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) {
+          const float gv = go[j] * act_bwd_from_out(best[j], act);   // bf16 dout: exactly the stored dx
+          s0[j] += gv;
+          s1[j] += gv * yarg[j];
         }
       }
     }
@@ -508,6 +532,20 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
       for (int j = 0; j < VW; ++j) p.e[j] = f2bf(is_max ? (arg[j] == w ? go[j] : 0.f) : go[j] * inv);
       const long long b = base_of(w);
       if constexpr (VW == 8) *(uint4*)(dx + b) = p.u; else dx[b] = p.e[0];
+    }
+  }
+  if constexpr (STATS) {
+    __shared__ float red[256][2 * VW + 1];
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < VW; ++j) { red[tid][j] = s0[j]; red[tid][VW + j] = s1[j]; }
+    __syncthreads();
+    for (int c = tid; c < g.C; c += 256) {       // thread t holds chunk t % cpr (256 % cpr == 0)
+      const int chk = c / VW, j = c % VW;
+      float a = 0.f, b = 0.f;
+      for (int t = chk; t < 256; t += cpr) { a += red[t][j]; b += red[t][VW + j]; }
+      part[(long long)blockIdx.x * 2 * g.C + c] = a;
+      part[(long long)blockIdx.x * 2 * g.C + g.C + c] = b;
     }
   }
 }
@@ -553,9 +591,14 @@ extern "C" int fn_bn_finalize(const float* part, int nb, int C, double count, co
   if (mode == 0)
     hipLaunchKernelGGL(bn_finalize_kernel<0>, dim3(C), dim3(256), 0, st, part, nb, C, count, gamma, beta, run_mean,
                        run_var, momentum, eps, o0, o1, o2, o3);
-  else
+  else if (mode == 1)
     hipLaunchKernelGGL(bn_finalize_kernel<1>, dim3(C), dim3(256), 0, st, part, nb, C, count, gamma, beta, run_mean,
                        run_var, momentum, eps, o0, o1, o2, o3);
+  else if (mode == 2 && run_mean && run_var)
+    hipLaunchKernelGGL(bn_finalize_kernel<2>, dim3(C), dim3(256), 0, st, part, nb, C, count, gamma, beta, run_mean,
+                       run_var, momentum, eps, o0, o1, o2, o3);
+  else
+    return -2;
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -631,6 +674,32 @@ extern "C" int fn_pool_fwd(const void* x, void* out, const float* scale, const f
   else
     hipLaunchKernelGGL(pool_fwd_kernel<1>, dim3(ew_blocks(outs * g.C)), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
                        scale, shift, g, is_max, count_pad, act);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+static bool pool_bwd_stats_ok(const PoolGeom& g) {
+  return g.sd == g.KD && g.sh == g.KH && g.sw == g.KW && g.pd == 0 && g.ph == 0 && g.pw == 0 &&
+         g.D == g.OD * g.KD && g.H == g.OH * g.KH && g.W == g.OW * g.KW && g.C % 8 == 0 && 256 % (g.C / 8) == 0;
+}
+
+// blocks of the STATS launch (rows of its part slab); 0 when the geometry has no such path
+extern "C" int fn_pool_bwd_stats_blocks(const int* geom17) {
+  const PoolGeom g = pool_geom(geom17);
+  if (!pool_bwd_stats_ok(g)) return 0;
+  const long long w = ((long long)g.N * g.OD * g.OH * g.OW * (g.C / 8) + 255) / 256;
+  return (int)(w < 1 ? 1 : (w > 2048 ? 2048 : w));
+}
+
+// max-pool backward of a BN+act output plus that BN's raw backward moments (see
+// pool_bwd_tiled_kernel STATS); part: fp32 [fn_pool_bwd_stats_blocks][2][C]
+extern "C" int fn_pool_bwd_stats(const void* dout, const void* x, void* dx, const float* scale, const float* shift,
+                                 const int* geom17, int act, float* part, hipStream_t st) {
+  const PoolGeom g = pool_geom(geom17);
+  const int nb = fn_pool_bwd_stats_blocks(geom17);
+  if (nb <= 0 || !scale || !shift || !part) return -2;
+  hipLaunchKernelGGL((pool_bwd_tiled_kernel<8, true>), dim3(nb), dim3(256), 0, st, (const bf16*)dout, (const bf16*)x,
+                     (bf16*)dx, scale, shift, g, 1, act, part);
   FN_CHECK_LAUNCH();
   return 0;
 }

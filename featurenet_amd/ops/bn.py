@@ -16,6 +16,7 @@ import torch
 
 from .. import _native
 from ..training.flat import grad_target
+from . import bnfuse
 from . import reference as ref
 from .spec import PoolSpec, act_code
 
@@ -48,21 +49,28 @@ def _eval_params(gamma, beta, rmean, rvar, eps, C, device):
     return torch.stack([rmean.float(), invstd, scale, shift])
 
 
-def _bwd_param_grads(dz2, y2, prm, act, beta=None, gamma=None):
+def _bwd_param_grads(dz2, y2, prm, act, beta=None, gamma=None, part=None):
     """(dbeta, dgamma) = (sum g, sum g*xhat), written straight into the parameters' flat
-    gradients when :func:`grad_target` offers them."""
+    gradients when :func:`grad_target` offers them.  ``part``: per-block partial sums
+    [nb, 2, C] already produced by the dgrad epilogue of the conv that consumed this
+    layer's output (:mod:`.bnfuse`); otherwise ``colstats`` computes them."""
     M, C = y2.shape
     K = _native.kernels()
-    nb = int(max(1, min(2048, M // 256)))
-    part = torch.empty(nb, 2, C, dtype=torch.float32, device=y2.device)
     st = _native.stream(y2)
-    K.colstats(y2.data_ptr(), dz2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), prm[0].data_ptr(),
-               prm[1].data_ptr(), part.data_ptr(), M, C, act, 1, nb, st)
+    mode = 2                                     # dgrad-epilogue slabs: raw moments (sum g, sum g*y)
+    if part is None:
+        mode = 1                                 # colstats: (sum g, sum g*xhat)
+        nb = int(max(1, min(2048, M // 256)))
+        part = torch.empty(nb, 2, C, dtype=torch.float32, device=y2.device)
+        K.colstats(y2.data_ptr(), dz2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), prm[0].data_ptr(),
+                   prm[1].data_ptr(), part.data_ptr(), M, C, act, 1, nb, st)
+    nb = part.shape[0]
     db, dg = grad_target(beta), grad_target(gamma)
     if db is None or dg is None or db.numel() != C or dg.numel() != C:
         out = torch.empty(2, C, dtype=torch.float32, device=y2.device)
         db, dg = out[0], out[1]
-    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, db.data_ptr(), dg.data_ptr(), 0, 0, 1, st)
+    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, prm[0].data_ptr() if mode == 2 else 0,
+                  prm[1].data_ptr() if mode == 2 else 0, 0.0, 0.0, db.data_ptr(), dg.data_ptr(), 0, 0, mode, st)
     return db, dg
 
 
@@ -82,7 +90,7 @@ def _bwd_input(dz2, y2, prm, dbeta, dgamma, act, training):
 
 class BatchNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, gamma, beta, slab, rmean, rvar, training, momentum, eps, act):
+    def forward(ctx, y, gamma, beta, slab, rmean, rvar, training, momentum, eps, act, tag=False):
         C = y.shape[-1]
         y2 = y.reshape(-1, C)
         if training:
@@ -94,6 +102,8 @@ class BatchNormActFn(torch.autograd.Function):
         z = torch.empty_like(y)
         _native.kernels().bn_apply(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), z.data_ptr(), y2.numel(), C,
                                    act, _native.stream(y))
+        if tag and act in (0, 1):                # none / relu: the dgrad epilogue's forms
+            bnfuse.tag_output(z, y, prm, act)
         ctx.save_for_backward(y, prm)
         ctx.act, ctx.training = act, training
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
@@ -106,10 +116,11 @@ class BatchNormActFn(torch.autograd.Function):
         C = y.shape[-1]
         y2 = y.reshape(-1, C)
         dz2 = dz.contiguous().to(torch.bfloat16).reshape(-1, C)
-        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params)
+        part = bnfuse.take(dz2, y) if ctx.training else None
+        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
-                dbeta if ctx.has_beta else None, None, None, None, None, None, None, None)
+                dbeta if ctx.has_beta else None, None, None, None, None, None, None, None, None)
 
 
 class BatchNormActPoolFn(torch.autograd.Function):
@@ -140,11 +151,20 @@ class BatchNormActPoolFn(torch.autograd.Function):
         C = y.shape[-1]
         dz = torch.empty_like(y)
         dp = dp.contiguous().to(torch.bfloat16)
-        _native.kernels().pool_bwd(dp.data_ptr(), y.data_ptr(), dz.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(),
-                                   ctx.pspec.geom17(), int(ctx.is_max), int(ctx.count_pad), ctx.act,
-                                   _native.stream(y), [y.numel(), dp.numel()])
+        K = _native.kernels()
+        geom = ctx.pspec.geom17()
+        nb = K.pool_bwd_stats_blocks(geom) if (ctx.is_max and ctx.training and bnfuse.pool_stats_enabled()) else 0
+        part = None
+        if nb > 0:
+            # max-pool backward + this BN's raw backward moments in one pass (no colstats)
+            part = torch.empty(nb, 2, C, dtype=torch.float32, device=y.device)
+            K.pool_bwd_stats(dp.data_ptr(), y.data_ptr(), dz.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), geom,
+                             ctx.act, part.data_ptr(), _native.stream(y), [y.numel(), dp.numel(), part.numel()])
+        else:
+            K.pool_bwd(dp.data_ptr(), y.data_ptr(), dz.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), geom,
+                       int(ctx.is_max), int(ctx.count_pad), ctx.act, _native.stream(y), [y.numel(), dp.numel()])
         y2, dz2 = y.reshape(-1, C), dz.reshape(-1, C)
-        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params)
+        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
                 dbeta if ctx.has_beta else None) + (None,) * 10
@@ -153,8 +173,11 @@ class BatchNormActPoolFn(torch.autograd.Function):
 def batchnorm_act(y5, gamma, beta, running_mean, running_var, training: bool, momentum: float = 0.1,
                   eps: float = 1e-5, act=None, stats_slab=None):
     if _native.use_native(y5):
+        # (grad mode is off inside Function.forward: decide here whether a backward will run)
+        tag = training and torch.is_grad_enabled() and (y5.requires_grad or any(
+            p is not None and p.requires_grad for p in (gamma, beta)))
         return BatchNormActFn.apply(y5.to(torch.bfloat16).contiguous(), gamma, beta, stats_slab, running_mean,
-                                    running_var, training, momentum, eps, act_code(act))
+                                    running_var, training, momentum, eps, act_code(act), tag)
     return ref.batchnorm_act(y5, gamma, beta, running_mean, running_var, training, momentum, eps, act)
 
 

@@ -1,0 +1,91 @@
+"""Cross-op fusion of a BN layer's backward statistics into the next conv's dgrad.
+
+A FeatureNet-3D block is ``conv -> BN -> act`` and the next block's conv reads
+``z = act(bn(y))``.  In backward that conv's dgrad writes ``dz``, and the BN
+backward then needs ``sum g`` and ``sum g * xhat`` (``g = dz * act'(z)``): one
+full pass over ``dz`` and ``y`` (``colstats``).  The big-tile dgrad kernel sums
+``g`` and ``g * y`` in its epilogue from registers instead (it reads ``y`` at the
+tile's positions; ``bn_finalize`` mode 2 centres the moments in fp64), so the
+pass disappears.
+
+Autograd runs the two ops as separate Functions, so they meet here:
+
+* :func:`tag_output` -- BN forward records ``z -> (y, prm, act)``;
+* :func:`source_of` -- the consuming conv's forward looks its input up;
+* :func:`offer` -- its backward hands ``(dz, slab)`` over;
+* :func:`take` -- the BN backward claims the slab for its ``dz`` (else it runs
+  ``colstats`` as before).
+
+Entries hold weak references and are matched on storage pointer, numel and the
+identity of ``y``, so a miss (a fork in the graph that sums gradients, the halo
+kernel chosen for dgrad, no-grad forward) only falls back to the separate pass.
+"""
+from __future__ import annotations
+
+import os
+import threading
+import weakref
+
+import torch
+
+_LOCK = threading.Lock()
+_FWD: dict = {}      # z.data_ptr() -> (ref z, ref y, ref prm, act)
+_BWD: dict = {}      # dz.data_ptr() -> (ref dz, slab, ref y)
+
+
+def enabled() -> bool:
+    """Off by default: measured slower on FeatureNet-3D (batch 128).  The statistics instance
+    of conv_tile needs 256 VGPRs + 136 B of scratch (the other instances fit in 242 with
+    none), and its spills cost the three dgrads 115-190 us each against the 248 us of
+    colstats passes they remove (docs/ARCHITECTURE.md, "rejected").  FN_BN_DGRAD_FUSE=1
+    turns it on; tests/test_bnfuse_gpu.py keeps it correct."""
+    return os.environ.get("FN_BN_DGRAD_FUSE", "0") == "1"
+
+
+def pool_stats_enabled() -> bool:
+    """BN-backward moments inside the max-pool backward (FN_POOL_BN_STATS, default on)."""
+    return os.environ.get("FN_POOL_BN_STATS", "1") != "0"
+
+
+def _purge(d: dict, limit: int = 256) -> None:
+    if len(d) > limit:
+        for k in [k for k, v in d.items() if v[0]() is None]:
+            d.pop(k, None)
+
+
+def tag_output(z: torch.Tensor, y: torch.Tensor, prm: torch.Tensor, act: int) -> None:
+    """BN forward (training): z = act(y * prm[2] + prm[3]), prm = (mean, invstd, scale, shift)."""
+    if not enabled():
+        return
+    with _LOCK:
+        _purge(_FWD)
+        _FWD[z.data_ptr()] = (weakref.ref(z), weakref.ref(y), weakref.ref(prm), act)
+
+
+def source_of(x: torch.Tensor):
+    """(y, prm, act) when ``x`` is (a same-extent view of) a tagged BN output, else None."""
+    e = _FWD.get(x.data_ptr())
+    if e is None:
+        return None
+    z, y, prm = e[0](), e[1](), e[2]()
+    if z is None or y is None or prm is None or z.numel() != x.numel() or not x.is_contiguous():
+        return None
+    return y, prm, e[3]
+
+
+def offer(dz: torch.Tensor, slab: torch.Tensor, y: torch.Tensor) -> None:
+    with _LOCK:
+        _purge(_BWD)
+        _BWD[dz.data_ptr()] = (weakref.ref(dz), slab, weakref.ref(y))
+
+
+def take(dz: torch.Tensor, y: torch.Tensor):
+    """The backward-statistics slab offered for this (dz, y) pair, or None."""
+    with _LOCK:
+        e = _BWD.pop(dz.data_ptr(), None)
+    if e is None:
+        return None
+    d, yy = e[0](), e[2]()
+    if d is None or yy is None or d.numel() != dz.numel() or yy.data_ptr() != y.data_ptr():
+        return None
+    return e[1]

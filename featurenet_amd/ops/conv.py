@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from . import bnfuse
 from . import conv_tile
 from . import conv_wtile
 from . import reference as ref
@@ -397,7 +398,19 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
     return y, stats
 
 
-def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=None):
+    """dx of the conv.  ``bn = (y, prm, act)`` (x was a BN+act output, :mod:`.bnfuse`): returns
+    ``(dx, slab)`` where ``slab`` holds that BN's backward sums from the tile kernel's
+    epilogue, or None when another kernel ran."""
+    if bn is not None:
+        tplan = conv_tile.dgrad_plan(spec)
+        plan = halo_dgrad_plan(spec)
+        if tplan is not None:
+            dy5 = dy5.contiguous()
+            if plan is None or conv_tile.choose("dgrad", spec, lambda: conv_tile.conv_dgrad(dy5, w, spec, tplan),
+                                                lambda: halo_conv_dgrad(dy5, w, spec, plan)):
+                return conv_tile.conv_dgrad(dy5, w, spec, tplan, bn=bn)
+        return native_conv_dgrad(dy5, w, spec), None
     tplan = conv_tile.dgrad_plan(spec)
     plan = halo_dgrad_plan(spec)
     if tplan is not None:
@@ -646,6 +659,10 @@ class ConvFn(torch.autograd.Function):
         ctx.spec, ctx.act, ctx.has_b, ctx.s2d = spec, act, b is not None, s2d
         ctx.set_materialize_grads(False)                # no zero-filled gradient for the stats output
         ctx.x_needs = ctx.needs_input_grad[0]
+        # x = act(bn(y)) of the previous layer: the dgrad epilogue sums that BN's backward
+        # statistics (ops/bnfuse.py) -- plain stride-1 convs on the tile kernel only
+        ctx.bn_src = (bnfuse.source_of(x_saved) if ctx.x_needs and not ctx.pw and s2d is None and
+                      conv_tile.dgrad_plan(spec) is not None else None)
         ctx.save_for_backward(x_saved, w, y if act else None)
         if stats is not None:
             ctx.mark_non_differentiable(stats)
@@ -666,7 +683,15 @@ class ConvFn(torch.autograd.Function):
             dw = pw_wgrad(dy2, x2).reshape(w.shape) if ctx.needs_input_grad[1] else None
             db = native_colsum(dy2) if (ctx.has_b and ctx.needs_input_grad[2]) else None
             return dx, dw, db, None, None, None
-        dx = native_conv_dgrad(dy, w.detach(), spec) if ctx.x_needs else None
+        dx = None
+        if ctx.x_needs:
+            if ctx.bn_src is not None:
+                dx, slab = native_conv_dgrad(dy, w.detach(), spec, bn=ctx.bn_src)
+                if slab is not None:
+                    bnfuse.offer(dx, slab, ctx.bn_src[0])
+                ctx.bn_src = None
+            else:
+                dx = native_conv_dgrad(dy, w.detach(), spec)
         dw = None
         if ctx.needs_input_grad[1]:
             if ctx.s2d is not None:      # x5 is the space-to-depth packed input (saved by forward)

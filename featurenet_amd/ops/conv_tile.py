@@ -304,14 +304,17 @@ def workers(p: TilePlan, geom: list, ncol: int) -> int:
 
 
 def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p: TilePlan, geom: list, kdims: tuple,
-        ncol: int, act: int) -> None:
+        ncol: int, act: int, bny=None, bnp=None) -> None:
     st = _native.stream(src5)
     rt = rowtab_tensor(p, kdims, src5.device)
     kt = ktab_tensor(p, kdims, src5.device)
+    ext = [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4]
+    if bny is not None:
+        ext += [bny.numel(), bnp.numel()]
     _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                 zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                 _native.ptr(stats), geom, ncol, act, p.MT, p.NT, sched(src5.device, st).data_ptr(),
-                                st, [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4])
+                                st, ext, _native.ptr(bny), _native.ptr(bnp))
 
 
 def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan):
@@ -328,15 +331,27 @@ def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats
     return y, stats
 
 
-def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan) -> torch.Tensor:
-    """dx = conv(dy, flip(W)^T) with leading pads K-1-p (stride 1) on the tile kernel."""
+def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None):
+    """dx = conv(dy, flip(W)^T) with leading pads K-1-p (stride 1) on the tile kernel.
+
+    ``bn = (y, prm, act)``: x was ``act(bn(y))`` with ``prm`` = (mean, invstd, scale, shift)
+    [4, C]; the epilogue then also sums that BN's raw backward moments (sum g, sum g*y,
+    g = dx * act'(z)) per workgroup and ``(dx, slab [workers, 2, C])`` is returned
+    (``bn_finalize`` mode 2 turns them into dbeta, dgamma)."""
     kd = (spec.KD, spec.KH, spec.KW)
     geom = geometry(p, (spec.N, spec.OD, spec.OH, spec.OW, spec.K), (spec.D, spec.H, spec.W), kd,
                     (spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw))
     wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
-    run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
-    return dx
+    lds_bws = 2 * p.BUF + 64 + RED_BYTES + (p.nks + PD + 2) * 16 + p.HPpad * 8 + p.NT * 16 * 16
+    if bn is None or lds_bws > LDS_MAX:          # (the statistics instance keeps the BN scale/shift in LDS)
+        run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
+        return dx if bn is None else (dx, None)
+    y, prm, act = bn
+    assert y.shape == dx.shape and y.dtype == torch.bfloat16 and y.is_contiguous() and prm.shape == (4, spec.C)
+    slab = torch.empty(workers(p, geom, spec.C), 2, spec.C, dtype=torch.float32, device=dy5.device)
+    run(dy5, wpk, None, dx, slab, p, geom, kd, spec.C, act, bny=y, bnp=prm.contiguous())
+    return dx, slab
 
 
 def fwd_plan(spec):

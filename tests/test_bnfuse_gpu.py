@@ -1,0 +1,93 @@
+"""BN-backward statistics fused into the consuming conv's dgrad epilogue (ops/bnfuse.py,
+conv_tile.hip BWS instance): the fused path must give the same parameter and input
+gradients as the separate colstats pass, and must actually take the fused branch."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from featurenet_amd import _native  # noqa: E402
+from featurenet_amd.ops import bn as bnmod  # noqa: E402
+from featurenet_amd.ops import bnfuse  # noqa: E402
+
+
+def _grads(model, x, fuse: bool, monkeypatch):
+    monkeypatch.setenv("FN_BN_DGRAD_FUSE", "1" if fuse else "0")
+    monkeypatch.setenv("FN_POOL_BN_STATS", "1" if fuse else "0")
+    model.zero_grad(set_to_none=True)
+    out = model(x)
+    loss = (out.float() * torch.linspace(-1, 1, out.shape[-1], device=x.device)).sum()
+    loss.backward()
+    return {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}
+
+
+def _count_fused(monkeypatch):
+    calls = {"fused": 0}
+    orig = bnfuse.take
+
+    def take(dz, y):
+        r = orig(dz, y)
+        calls["fused"] += r is not None
+        return r
+
+    monkeypatch.setattr(bnmod.bnfuse, "take", take)
+    return calls
+
+
+@pytest.mark.parametrize("N,S,cin,cmid,k", [(2, 20, 32, 32, 3), (3, 17, 16, 64, 4), (16, 24, 32, 64, 3)])
+def test_dgrad_bn_stats_match_colstats(monkeypatch, N, S, cin, cmid, k):
+    from torch import nn
+
+    from featurenet_amd.models.layers import Conv
+
+    assert _native.kernels() is not None
+    monkeypatch.setenv("FN_CONV_TILE", "2")      # the tile kernel (the fused epilogue lives there)
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    model = nn.Sequential(Conv(cin, cmid, k, 1, "valid", bn=True, act="relu", init="he"),
+                          Conv(cmid, 32, 3, 1, "valid", bn=True, act="relu", init="he")).to(dev)
+    x = torch.randn(N, S, S, S, cin, device=dev).to(torch.bfloat16)
+    calls = _count_fused(monkeypatch)
+    g0 = _grads(model, x, False, monkeypatch)
+    assert calls["fused"] == 0
+    g1 = _grads(model, x, True, monkeypatch)
+    assert calls["fused"] == 1, "the fused dgrad-epilogue statistics were not used"
+    for n in g0:
+        a, b = g0[n], g1[n]
+        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
+        assert err < 2e-3, f"{n}: rel err {err:.2e}"
+
+
+def test_featurenet3d_fused_bn_backward(monkeypatch):
+    """Production layer shapes (64^3, batch 8): every conv2..4 dgrad feeds its BN the fused sums."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3D
+
+    torch.manual_seed(1)
+    dev = torch.device("cuda", 0)
+    model = FeatureNet3D().to(dev)
+    x = (torch.rand(8, 64, 64, 64, 1, device=dev) < 0.3).to(torch.bfloat16)
+    calls = _count_fused(monkeypatch)
+    g0 = _grads(model, x, False, monkeypatch)
+    g1 = _grads(model, x, True, monkeypatch)
+    assert calls["fused"] >= 1
+    for n in g0:
+        a, b = g0[n], g1[n]
+        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
+        assert err < 5e-3, f"{n}: rel err {err:.2e}"
+
+
+@pytest.mark.parametrize("N,S,C", [(2, 20, 64), (4, 10, 32), (3, 8, 16)])
+def test_pool_bwd_bn_stats_match_colstats(monkeypatch, N, S, C):
+    """Max-pool backward with the BN-backward moments (pool_bwd_stats) vs pool_bwd + colstats."""
+    from featurenet_amd.models.layers import Conv
+
+    torch.manual_seed(2)
+    dev = torch.device("cuda", 0)
+    layer = Conv(C, C, 3, 1, "same", bn=True, act="relu", pool=(2, 2, 2), init="he").to(dev)
+    x = torch.randn(N, S, S, S, C, device=dev).to(torch.bfloat16)
+    g0 = _grads(layer, x, False, monkeypatch)
+    g1 = _grads(layer, x, True, monkeypatch)
+    for n in g0:
+        a, b = g0[n], g1[n]
+        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
+        assert err < 2e-3, f"{n}: rel err {err:.2e}"
