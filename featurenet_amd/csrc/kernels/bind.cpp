@@ -22,8 +22,9 @@ int fn_conv_halo(const void*, const void*, const float*, void*, float*, const in
                  hipStream_t);
 long long fn_conv_halo_lds(const int*, int);
 int fn_conv_halo_workers(const int*, int);
-int fn_pw_fwd(const void*, const void*, const float*, void*, long long, int, int, int, hipStream_t);
-int fn_pw_wgrad(const void*, const void*, float*, long long, int, int, hipStream_t);
+int fn_pw_fwd(const void*, const void*, const float*, void*, long long, int, int, int, hipStream_t, const float*,
+              const float*, int);
+int fn_pw_wgrad(const void*, const void*, float*, long long, int, int, hipStream_t, const float*, const float*, int);
 int fn_conv_halo_wgrad_yblocks(const int*, int);
 int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
                     int, int, hipStream_t);
@@ -69,6 +70,7 @@ int fn_bias_act(const void*, const float*, void*, long long, int, int, hipStream
 int fn_act_bwd(const void*, const void*, void*, long long, int, hipStream_t);
 int fn_dropout(const void*, void*, long long, float, unsigned, unsigned, hipStream_t);
 int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
+int fn_scale_unless_one(void*, int, const float*, long long, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                  const int*, int, int, int, int, int*, hipStream_t, const void*, const float*);
@@ -344,14 +346,22 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 17, "conv_halo_wgrad_yblocks");
     return fn_conv_halo_wgrad_yblocks(geom.data(), cout);
   });
+  // psc / psh / pact: optional input prologue x <- pact(x * psc[k] + psh[k]) (BN + act of the
+  // producing layer, never materialised)
   m.def("pw_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, long long M, int K, int N, int act,
-                     uintptr_t st) {
-    chk(fn_pw_fwd(P<const void*>(x), P<const void*>(w), P<const float*>(bias), P<void*>(y), M, K, N, act, S(st)),
+                     uintptr_t st, uintptr_t psc, uintptr_t psh, int pact) {
+    chk(fn_pw_fwd(P<const void*>(x), P<const void*>(w), P<const float*>(bias), P<void*>(y), M, K, N, act, S(st),
+                  P<const float*>(psc), P<const float*>(psh), pact),
         "pw_fwd");
-  });
-  m.def("pw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, long long M, int K, int N, uintptr_t st) {
-    chk(fn_pw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), M, K, N, S(st)), "pw_wgrad");
-  });
+  }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("M"), py::arg("K"), py::arg("N"),
+     py::arg("act"), py::arg("st"), py::arg("psc") = 0, py::arg("psh") = 0, py::arg("pact") = 0);
+  m.def("pw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, long long M, int K, int N, uintptr_t st,
+                       uintptr_t psc, uintptr_t psh, int pact) {
+    chk(fn_pw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), M, K, N, S(st), P<const float*>(psc),
+                    P<const float*>(psh), pact),
+        "pw_wgrad");
+  }, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("M"), py::arg("K"), py::arg("N"), py::arg("st"),
+     py::arg("psc") = 0, py::arg("psh") = 0, py::arg("pact") = 0);
   m.def("conv_halo_workers", [](std::vector<int> geom, int ncol) {
     need(geom, 17, "conv_halo_workers");
     return fn_conv_halo_workers(geom.data(), ncol);
@@ -475,6 +485,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("unpack_bits", [](uintptr_t bits, uintptr_t out, long long nbytes, uintptr_t st) {
     chk(fn_unpack_bits(P<const void*>(bits), P<void*>(out), nbytes, S(st)), "unpack_bits");
+  });
+  m.def("scale_unless_one", [](uintptr_t x, int is_bf16, uintptr_t s, long long n, uintptr_t st) {
+    chk(fn_scale_unless_one(P<void*>(x), is_bf16, P<const float*>(s), n, S(st)), "scale_unless_one");
   });
   m.def("cast_f32_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t st) {
     chk(fn_cast_f32_bf16(P<const float*>(x), P<void*>(y), n, S(st)), "cast_f32_bf16");

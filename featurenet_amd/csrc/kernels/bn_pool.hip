@@ -92,6 +92,49 @@ __global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ 
   }
 }
 
+// Column sums (MODE 0) of a [M][C] tensor whose C is not a multiple of 8 (bias gradients of
+// 25-class heads, odd NAS widths): 16-B vector loads over "super rows" of lcm(8, C) elements
+// = Q = C / gcd(8, C) chunks, in which chunk q always covers channels (8q + j) mod C -- so a
+// thread that keeps chunk position q keeps 8 fixed channels, like the VW = 8 path.  Needs
+// M * C to be whole super rows (the host checks) and Q <= 256.
+__global__ __launch_bounds__(256) void colstats_sr_kernel(const bf16* __restrict__ x, float* __restrict__ part,
+                                                          long long nsr, int C, int Q, long long sr_per_block) {
+  __shared__ float red[256][17];
+  const int tid = threadIdx.x;
+  const int rpp = 256 / Q;                   // super rows per pass
+  const bool active = tid < rpp * Q;
+  const int q = active ? tid % Q : 0, r0 = active ? tid / Q : 0;
+  const long long sbeg = (long long)blockIdx.x * sr_per_block;
+  long long send = sbeg + sr_per_block;
+  if (send > nsr) send = nsr;
+  float s0[8], s1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+  if (active) {
+#pragma unroll 4
+    for (long long r = sbeg + r0; r < send; r += rpp) {
+      Pack8 px;
+      px.u = *(const uint4*)(x + (r * Q + q) * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float v = bf2f(px.e[j]); s0[j] += v; s1[j] += v * v; }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[tid][j] = active ? s0[j] : 0.f; red[tid][8 + j] = active ? s1[j] : 0.f; }
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    float a = 0.f, b = 0.f;
+    for (int t = 0; t < rpp * Q; ++t) {
+      const int base = 8 * (t % Q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if ((base + j) % C == c) { a += red[t][j]; b += red[t][8 + j]; }
+    }
+    part[(long long)blockIdx.x * 2 * C + c] = a;
+    part[(long long)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Reduce [nb][2][C] slabs per channel in fp64 and finalise.
 //   MODE 0 (forward): mean, invstd, scale=gamma*invstd, shift=beta-mean*scale,
@@ -565,6 +608,18 @@ extern "C" int fn_colstats(const void* x, const void* dz, const float* scale, co
                            hipStream_t st) {
   const bool vec = (C % 8) == 0 && C / 8 <= 256;
   if (!vec && C > 256) return -2;
+  if (!vec && mode == 0) {                       // super-row vector path (see colstats_sr_kernel)
+    int gg = 8;
+    while (C % gg) gg >>= 1;                     // gcd(8, C)
+    const int Q = C / gg, rows_sr = 8 / gg;      // chunks / rows per super row
+    if (Q <= 256 && M % rows_sr == 0) {
+      const long long nsr = M / rows_sr;
+      hipLaunchKernelGGL(colstats_sr_kernel, dim3(nb), dim3(256), 0, st, (const bf16*)x, part, nsr, C, Q,
+                         (nsr + nb - 1) / nb);
+      FN_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   const long long rpb = (M + nb - 1) / nb;
   const bf16* xx = (const bf16*)x;
   const bf16* dd = (const bf16*)dz;

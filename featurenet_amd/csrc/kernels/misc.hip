@@ -15,6 +15,8 @@
 //   cast           : fp32 <-> bf16.
 #include "common.h"
 
+#include <type_traits>
+
 // ---------------------------------------------------------------------------
 // Dense-prediction form (per-voxel segmentation: millions of rows, NC ~ 25):
 // LPR lanes per row (8 for NC <= 64, so a wave covers 8 rows and the loads of a
@@ -486,6 +488,31 @@ extern "C" int fn_unpack_bits(const void* bits, void* out, long long nbytes, hip
 
 extern "C" int fn_cast_f32_bf16(const float* x, void* y, long long n, hipStream_t st) {
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(blocks_for(n)), dim3(256), 0, st, x, (bf16*)y, n);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// x *= *s in place, unless *s == 1 (the loss gradient of a plain loss.backward()): every
+// workgroup reads the device scalar first and leaves at once, so the common case costs one
+// near-empty launch instead of a pass over d(logits) -- no host sync, graph-capturable.
+// (SoftmaxXentFn.backward: 838M d(logits) elements for the 64^3 segmentation head.)
+template <typename T>
+__global__ __launch_bounds__(256) void scale_unless_one_kernel(T* __restrict__ x, const float* __restrict__ s,
+                                                               long long n) {
+  const float f = *s;
+  if (f == 1.0f) return;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    if constexpr (std::is_same<T, float>::value) x[i] *= f;
+    else x[i] = f2bf(bf2f(x[i]) * f);
+  }
+}
+
+extern "C" int fn_scale_unless_one(void* x, int is_bf16, const float* s, long long n, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (is_bf16)
+    hipLaunchKernelGGL(scale_unless_one_kernel<bf16>, dim3(blocks_for(n)), dim3(256), 0, st, (bf16*)x, s, n);
+  else
+    hipLaunchKernelGGL(scale_unless_one_kernel<float>, dim3(blocks_for(n)), dim3(256), 0, st, (float*)x, s, n);
   FN_CHECK_LAUNCH();
   return 0;
 }

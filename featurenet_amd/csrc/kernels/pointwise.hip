@@ -26,10 +26,12 @@ __device__ __forceinline__ int pw_tiles(long long M) { return (int)((M + PW_BM -
 
 // Y = act(X W^T + b).  KP / NP: K, N padded to 32 / 64.  Dynamic LDS: the A tile
 // [256][KP+8] and the output staging [256][NP+8] share one region (bf16).
-template <int KP, int NP, int ACT, bool HAS_BIAS>
+// PRO: -1 = plain input; ACT_NONE / ACT_RELU = input prologue x <- act(x * psc[k] + psh[k])
+template <int KP, int NP, int ACT, bool HAS_BIAS, int PRO = -1>
 __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
-                                                           long long M, int K, int N) {
+                                                           long long M, int K, int N, const float* __restrict__ psc,
+                                                           const float* __restrict__ psh) {
   constexpr int LDA = KP + 8, LDO = NP + 8;
   constexpr int KS = KP / 32, NT = NP / 16;
   constexpr int CH = KP / 8;                     // 16-B chunks per thread of a 256 x KP tile
@@ -64,6 +66,20 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
     bv[nt] = (HAS_BIAS && n < N) ? bias[n] : 0.f;
   }
 
+  // optional input prologue x <- act(x * psc[k] + psh[k]) (a BatchNorm + activation whose
+  // normalised output is never written): with K % 8 == 0 and 2048 % K == 0 (host check)
+  // every chunk this thread loads starts at channel (8 tid) mod K, so 8 scale/shift pairs
+  // in registers cover all of them
+  constexpr int NPV = PRO >= 0 ? 8 : 1;
+  float psv[NPV], phv[NPV];
+  if constexpr (PRO >= 0) {
+    const int pk0 = (tid * 8) % K;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      psv[j] = psc[pk0 + j];
+      phv[j] = psh[pk0 + j];
+    }
+  }
   const int ntiles = pw_tiles(M);
   uint4 rb[CH];
   auto load = [&](int t) {                       // tile t: 256*K contiguous bf16 (16-B aligned: 512*K*t)
@@ -88,7 +104,15 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
       if (c * 8 < rows * K) {
         int r = (c * 8) / K, k = c * 8 - r * K;   // one division per chunk, then walk
         if (K % 8 == 0) {                          // chunk inside one row: one 16-B LDS store
-          *(uint4*)(As + r * LDA + k) = rb[i];
+          if constexpr (PRO >= 0) {
+            Pack8 p;
+            p.u = rb[i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) p.e[j] = f2bf(act_fwd(bf2f(p.e[j]) * psv[j] + phv[j], PRO));
+            *(uint4*)(As + r * LDA + k) = p.u;
+          } else {
+            *(uint4*)(As + r * LDA + k) = rb[i];
+          }
         } else {
           Pack8 p;
           p.u = rb[i];
@@ -148,9 +172,11 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
 // dW[N][K] += sum_rows dY[row][n] * X[row][k].  Both tiles are scattered into LDS
 // TRANSPOSED ([channel][row]) so the MFMA operands (k = rows) are contiguous
 // 8-row runs; per-workgroup fp32 accumulators, one atomic per element at the end.
-template <int KP, int NP>
+template <int KP, int NP, int PRO = -1>
 __global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                             float* __restrict__ dw, long long M, int K, int N) {
+                                                             float* __restrict__ dw, long long M, int K, int N,
+                                                             const float* __restrict__ psc,
+                                                             const float* __restrict__ psh) {
   constexpr int LDR = PW_BM + 8;                 // row stride of the transposed tiles
   constexpr int NTN = NP / 16, NTK = KP / 16;
   extern __shared__ __attribute__((aligned(16))) unsigned char pw_dsm[];
@@ -181,6 +207,7 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __rest
       rb[i] = *(const uint4*)(src + e0 + (c * 8 < nel ? c * 8 : 0));
     }
   };
+  // optional prologue on x (as pw_fwd_kernel): x <- act(x * psc[k] + psh[k])
   auto scatter_t = [&](bf16* dst, const uint4* rb, int C, int rows, int nch) {
 #pragma unroll
     for (int i = 0; i < nch; ++i) {
@@ -208,6 +235,24 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __rest
       for (int i = tid; i < NP * (PW_BM - rows); i += PW_NTHR) Yt[(i / (PW_BM - rows)) * LDR + rows + i % (PW_BM - rows)] = f2bf(0.f);
     }
     __syncthreads();
+    if constexpr (PRO >= 0) {
+      // input prologue x <- act(x * psc[k] + psh[k]) on the transposed tile in LDS: channel k is
+      // one LDS row, so a thread takes 32 consecutive rows of one channel with two scalars
+      // (no per-element parameter registers; rows past a ragged tile's end meet dy = 0)
+      for (int k = tid >> 3; k < K; k += PW_NTHR / 8) {
+        const float a = psc[k], c = psh[k];
+        bf16* row = Xt + k * LDR + (tid & 7) * 32;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          Pack8 p;
+          p.u = *(const uint4*)(row + v * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) p.e[j] = f2bf(act_fwd(bf2f(p.e[j]) * a + c, PRO));
+          *(uint4*)(row + v * 8) = p.u;
+        }
+      }
+      __syncthreads();
+    }
     if (t + gridDim.x < ntiles) { load(dy, N, t + gridDim.x, ry, CY); load(x, K, t + gridDim.x, rx, CX); }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -249,12 +294,20 @@ static int pw_grid(long long M, int per_cu) {
 }
 
 // x: bf16 [M][K], w: bf16 [N][K] (row n = output channel), y: bf16 [M][N]; K, N <= 64
+// psc / psh (optional, fp32 [K]): input prologue x <- pact(x * psc + psh); needs K % 8 == 0 and
+// 2048 % K == 0
+static bool pw_pro_ok(const float* psc, const float* psh, int K) {
+  return !psc || (psh && K % 8 == 0 && 2048 % K == 0);
+}
+
 extern "C" int fn_pw_fwd(const void* x, const void* w, const float* bias, void* y, long long M, int K, int N, int act,
-                         hipStream_t st) {
+                         hipStream_t st, const float* psc, const float* psh, int pact) {
   if (K < 1 || K > 64 || N < 1 || N > 64 || M < 8 || M % 8) return -2;
+  if (!pw_pro_ok(psc, psh, K)) return -2;
   // ~110-200 VGPRs and <= 37 KB LDS: 4 workgroups per CU for the 32-channel variants
   const dim3 grid((unsigned)pw_grid(M, (K <= 32 && N <= 32) ? 4 : 2));
   const bool hb = bias != nullptr;
+  // (the 64-channel prologue instances need > 64 KB of LDS only for KP = NP = 64: not emitted)
 #define PWF(KP, NP, A, HB)                                                                                   \
   do {                                                                                                         \
     const size_t lds = (size_t)PW_BM * ((KP > NP ? KP : NP) + 8) * 2;                                        \
@@ -263,8 +316,28 @@ extern "C" int fn_pw_fwd(const void* x, const void* w, const float* bias, void* 
                             (int)lds) != hipSuccess)                                                           \
       return -4;                                                                                               \
     hipLaunchKernelGGL((pw_fwd_kernel<KP, NP, A, HB>), grid, dim3(PW_NTHR), lds, st, (const bf16*)x,          \
-                       (const bf16*)w, bias, (bf16*)y, M, K, N);                                               \
+                       (const bf16*)w, bias, (bf16*)y, M, K, N, nullptr, nullptr);                             \
   } while (0)
+  // prologue instances (the BN + act of the producing layer): identity output, bias or not,
+  // K <= 32 or 64, N <= 32 or 64
+#define PWP(KP, NP, HB, PA)                                                                                  \
+  hipLaunchKernelGGL((pw_fwd_kernel<KP, NP, ACT_NONE, HB, PA>), grid, dim3(PW_NTHR),                           \
+                     (size_t)PW_BM * ((KP > NP ? KP : NP) + 8) * 2, st, (const bf16*)x, (const bf16*)w, bias,    \
+                     (bf16*)y, M, K, N, psc, psh)
+  if (psc) {
+    if (act != ACT_NONE || (pact != ACT_NONE && pact != ACT_RELU)) return -2;
+#define PWP2(KP, NP)                                                                                         \
+    do {                                                                                                     \
+      if (pact == ACT_RELU) { if (hb) PWP(KP, NP, true, ACT_RELU); else PWP(KP, NP, false, ACT_RELU); }      \
+      else { if (hb) PWP(KP, NP, true, ACT_NONE); else PWP(KP, NP, false, ACT_NONE); }                       \
+    } while (0)
+    if (K <= 32) { if (N <= 32) PWP2(32, 32); else PWP2(32, 64); }
+    else { if (N <= 32) PWP2(64, 32); else PWP2(64, 64); }
+#undef PWP2
+#undef PWP
+    FN_CHECK_LAUNCH();
+    return 0;
+  }
 #define PWA(KP, NP)                                                          \
   do {                                                                       \
     if (act == ACT_RELU) { if (hb) PWF(KP, NP, ACT_RELU, true); else PWF(KP, NP, ACT_RELU, false); } \
@@ -282,8 +355,10 @@ extern "C" int fn_pw_fwd(const void* x, const void* w, const float* bias, void* 
 }
 
 // dw: fp32 [N][K], accumulated into (zero it for a fresh gradient)
-extern "C" int fn_pw_wgrad(const void* dy, const void* x, float* dw, long long M, int K, int N, hipStream_t st) {
+extern "C" int fn_pw_wgrad(const void* dy, const void* x, float* dw, long long M, int K, int N, hipStream_t st,
+                           const float* psc, const float* psh, int pact) {
   if (K < 1 || K > 64 || N < 1 || N > 64 || M < 8 || M % 8) return -2;
+  if (!pw_pro_ok(psc, psh, K)) return -2;
   const dim3 grid((unsigned)pw_grid(M, (K <= 32 && N <= 32) ? 3 : 2));
 #define PWW(KP, NP)                                                                                          \
   do {                                                                                                     \
@@ -292,9 +367,17 @@ extern "C" int fn_pw_wgrad(const void* dy, const void* x, float* dw, long long M
         hipFuncSetAttribute((const void*)pw_wgrad_kernel<KP, NP>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                             (int)lds) != hipSuccess)                                                       \
       return -4;                                                                                           \
-    hipLaunchKernelGGL((pw_wgrad_kernel<KP, NP>), grid, dim3(PW_NTHR), lds, st, (const bf16*)dy,          \
-                       (const bf16*)x, dw, M, K, N);                                                       \
+    if (!psc)                                                                                              \
+      hipLaunchKernelGGL((pw_wgrad_kernel<KP, NP>), grid, dim3(PW_NTHR), lds, st, (const bf16*)dy,        \
+                         (const bf16*)x, dw, M, K, N, nullptr, nullptr);                                   \
+    else if (pact == ACT_RELU)                                                                             \
+      hipLaunchKernelGGL((pw_wgrad_kernel<KP, NP, ACT_RELU>), grid, dim3(PW_NTHR), lds, st, (const bf16*)dy, \
+                         (const bf16*)x, dw, M, K, N, psc, psh);                                           \
+    else                                                                                                   \
+      hipLaunchKernelGGL((pw_wgrad_kernel<KP, NP, ACT_NONE>), grid, dim3(PW_NTHR), lds, st, (const bf16*)dy, \
+                         (const bf16*)x, dw, M, K, N, psc, psh);                                           \
   } while (0)
+  if (psc && pact != ACT_NONE && pact != ACT_RELU) return -2;
   if (K <= 32) { if (N <= 32) PWW(32, 32); else PWW(32, 64); }
   else { if (N <= 32) PWW(64, 32); else PWW(64, 64); }
 #undef PWW

@@ -25,6 +25,8 @@ from dataclasses import asdict, dataclass, field
 import torch
 from torch import nn
 
+from .. import ops
+from ..ops import bn as bn_ops
 from ..ops.elementwise import upsample2x
 from .layers import Conv, Dense
 
@@ -146,5 +148,13 @@ class FeatureNet3DSeg(nn.Module):
             x = x.unsqueeze(-1)
         for c in self.enc:
             x = c(x)
-        x = self.dec(upsample2x(x))        # nearest x2 upsample on the channels-last grid
-        return self.head(x)  # [N, S, S, S, classes]
+        x = upsample2x(x)                  # nearest x2 upsample on the channels-last grid
+        d, h = self.dec, self.head
+        if self.training and bn_ops.fused_pointwise_ok(x, d.cout, h.cout, d.act):
+            # training on the GPU: the decoder's BN + ReLU run inside the 1x1 head's pointwise
+            # kernels (forward and weight gradient), so its 64^3 x 32 output is never written
+            cs, _ = d.specs(tuple(x.shape))
+            y, slab = ops.conv(x, d.weight, None, cs, None, want_stats=True)
+            return bn_ops.batchnorm_act_pointwise(y, d.gamma, d.beta, d.running_mean, d.running_var, h.weight, h.bias,
+                                                  d.bn_momentum, d.bn_eps, d.act, stats_slab=slab)
+        return h(d(x))  # [N, S, S, S, classes]

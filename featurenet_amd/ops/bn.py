@@ -190,3 +190,64 @@ def batchnorm_act_pool(y5, gamma, beta, running_mean, running_var, training: boo
                                         count_pad)
     z = ref.batchnorm_act(y5, gamma, beta, running_mean, running_var, training, momentum, eps, act)
     return ref.pool(z, pspec, kind, count_pad)
+
+
+class BatchNormActPointwiseFn(torch.autograd.Function):
+    """out = act(bn(y)) @ W^T + b for a 1x1x1 conv head: the pointwise kernels apply BN + act
+    to their input tile in registers (forward and weight gradient), so act(bn(y)) -- the
+    segmentation decoder's 64^3 x 32 output -- is never written or re-read.  Backward: the
+    head's dgrad gives dz straight from dout, then the usual BN backward on (dz, y)."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, slab, rmean, rvar, momentum, eps, act, w, b):
+        from .conv import pw_fwd
+
+        C = y.shape[-1]
+        y2 = y.reshape(-1, C)
+        if slab is None:
+            slab = _stats_slab(y2)
+        prm = _finalize_fwd(slab, y2.shape[0], gamma, beta, rmean, rvar, momentum, eps)
+        N = w.shape[0]
+        w2 = w.detach().reshape(N, C)
+        bias = b.detach().float().contiguous() if b is not None else None
+        out = pw_fwd(y2, w2, bias, 0, pro=(prm[2], prm[3], act))
+        ctx.save_for_backward(y, prm, w)
+        ctx.act, ctx.has_b = act, b is not None
+        ctx.params = (beta, gamma)
+        return out.reshape(*y.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .conv import native_colsum, pw_fwd, pw_wgrad
+
+        y, prm, w = ctx.saved_tensors
+        C = y.shape[-1]
+        N = w.shape[0]
+        y2 = y.reshape(-1, C)
+        d2 = dout.contiguous().to(torch.bfloat16).reshape(-1, N)
+        w2 = w.detach().reshape(N, C)
+        dw = pw_wgrad(d2, y2, pro=(prm[2], prm[3], ctx.act)).reshape(w.shape) if ctx.needs_input_grad[9] else None
+        db = native_colsum(d2) if (ctx.has_b and ctx.needs_input_grad[10]) else None
+        dz2 = pw_fwd(d2, w2.t(), None, 0)                    # d(act(bn(y))) [M, C]
+        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params)
+        dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, True) if ctx.needs_input_grad[0] else None
+        return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.needs_input_grad[1] else None,
+                dbeta if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, dw, db)
+
+
+def batchnorm_act_pointwise(y5, gamma, beta, running_mean, running_var, w, b, momentum: float = 0.1,
+                            eps: float = 1e-5, act=None, stats_slab=None):
+    """Training-mode ``conv1x1(act(bn(y)))`` with the BN + act inside the 1x1 conv's kernels
+    (GPU; the caller checks :func:`fused_pointwise_ok`)."""
+    return BatchNormActPointwiseFn.apply(y5.to(torch.bfloat16).contiguous(), gamma, beta, stats_slab, running_mean,
+                                         running_var, momentum, eps, act_code(act), w, b)
+
+
+def fused_pointwise_ok(y5, C: int, N: int, act) -> bool:
+    from .conv import pw_prologue_ok
+
+    import os
+
+    M = y5.numel() // C
+    return (os.environ.get("FN_BN_PW_FUSE", "1") != "0" and _native.use_native(y5) and pw_prologue_ok(C)
+            and C <= 64 and N <= 64 and M % 8 == 0 and act in (None, "relu"))

@@ -599,25 +599,36 @@ def pointwise_ok(spec: ConvSpec, want_stats: bool = False) -> bool:
             and spec.M % 8 == 0 and spec.M >= 8)
 
 
-def pw_fwd(x2: torch.Tensor, w2: torch.Tensor, bias, act: int) -> torch.Tensor:
-    """[M, Kin] x [Nout, Kin]^T (+bias, act) -> bf16 [M, Nout] on the pointwise kernel."""
+def pw_fwd(x2: torch.Tensor, w2: torch.Tensor, bias, act: int, pro=None) -> torch.Tensor:
+    """[M, Kin] x [Nout, Kin]^T (+bias, act) -> bf16 [M, Nout] on the pointwise kernel.
+
+    ``pro = (scale, shift, act)``: the kernel reads ``act(x * scale + shift)`` (per input
+    channel) instead of x -- a BN + activation that is never written to memory."""
     M, Kin = x2.shape
     N = w2.shape[0]
     if act and bias is None:
         bias = torch.zeros(N, dtype=torch.float32, device=x2.device)
     y = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
     wb = w2.detach().to(torch.bfloat16).contiguous()
+    psc, psh, pact = pro if pro is not None else (None, None, 0)
     _native.kernels().pw_fwd(x2.data_ptr(), wb.data_ptr(), _native.ptr(bias), y.data_ptr(), M, Kin, N, act,
-                             _native.stream(x2))
+                             _native.stream(x2), _native.ptr(psc), _native.ptr(psh), pact)
     return y
 
 
-def pw_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
-    """fp32 dW [Nout, Kin] = dy^T x on the pointwise kernel."""
+def pw_prologue_ok(K: int) -> bool:
+    """Input channel counts the pointwise kernels' BN+act prologue supports."""
+    return K % 8 == 0 and 2048 % K == 0
+
+
+def pw_wgrad(dy2: torch.Tensor, x2: torch.Tensor, pro=None) -> torch.Tensor:
+    """fp32 dW [Nout, Kin] = dy^T x on the pointwise kernel (``pro``: as :func:`pw_fwd`)."""
     M, N = dy2.shape
     Kin = x2.shape[1]
     dw = torch.zeros(N, Kin, dtype=torch.float32, device=x2.device)
-    _native.kernels().pw_wgrad(dy2.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, Kin, N, _native.stream(x2))
+    psc, psh, pact = pro if pro is not None else (None, None, 0)
+    _native.kernels().pw_wgrad(dy2.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, Kin, N, _native.stream(x2),
+                               _native.ptr(psc), _native.ptr(psh), pact)
     return dw
 
 

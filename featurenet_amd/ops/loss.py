@@ -38,7 +38,15 @@ class SoftmaxXentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss, _dc):
         (dlog,) = ctx.saved_tensors
-        return (dlog * dloss.to(dlog.dtype)).to(ctx.in_dtype), None, None, None
+        if getattr(ctx, "scaled", False):              # a second backward (retain_graph): out of place
+            return (dlog * dloss.to(dlog.dtype)).to(ctx.in_dtype), None, None, None
+        ctx.scaled = True
+        # scale the stored d(logits) in place by dloss -- a near-empty launch when dloss == 1
+        # (every plain loss.backward()): the device-side check needs no host sync
+        s = dloss.detach().float().reshape(1).contiguous()
+        _native.kernels().scale_unless_one(dlog.data_ptr(), int(dlog.dtype == torch.bfloat16), s.data_ptr(),
+                                           dlog.numel(), _native.stream(dlog))
+        return dlog.to(ctx.in_dtype), None, None, None
 
 
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0, with_correct: bool = False):

@@ -91,3 +91,29 @@ def test_pool_bwd_bn_stats_match_colstats(monkeypatch, N, S, C):
         a, b = g0[n], g1[n]
         err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
         assert err < 2e-3, f"{n}: rel err {err:.2e}"
+
+
+@pytest.mark.parametrize("S", [16, 32])
+def test_seg_head_bn_in_pointwise_matches_unfused(monkeypatch, S):
+    """FeatureNet3DSeg training step with the decoder BN + ReLU inside the 1x1 head's pointwise
+    kernels (BatchNormActPointwiseFn) vs bn_apply + plain head: same logits and gradients."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3DSeg
+    from featurenet_amd.ops import softmax_xent
+
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    model = FeatureNet3DSeg(input_size=S).to(dev).train()
+    x = (torch.rand(2, S, S, S, 1, device=dev) < 0.3).to(torch.bfloat16)
+    lab = torch.randint(0, 25, (2, S, S, S), device=dev)
+    res = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("FN_BN_PW_FUSE", fuse)
+        model.zero_grad(set_to_none=True)
+        out = model(x)
+        softmax_xent(out, lab).backward()
+        res.append((out.detach().float(), {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}))
+    (o0, g0), (o1, g1) = res
+    assert (o0 - o1).abs().max().item() <= 2e-2 * o0.abs().max().item()
+    for n in g0:
+        err = (g0[n] - g1[n]).abs().max().item() / max(g0[n].abs().max().item(), 1e-6)
+        assert err < 2e-2, f"{n}: rel err {err:.2e}"
