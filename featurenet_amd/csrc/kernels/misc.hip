@@ -295,17 +295,20 @@ static unsigned blocks_for(long long work) {
 // segmentation decoder) and its backward (sum over each 2x2x2 block, fp32).
 // One thread per 8-channel source vector: forward = 1 load, 8 stores;
 // backward = 8 loads, 1 store.  C % 8 == 0.
+// Index decode in 32-bit (IDX = unsigned) when the chunk count fits: the 64-bit divisions of
+// the general form cost more VALU than the 16-B copies themselves (2.8 TB/s at 64^3 x 64).
+template <typename IDX>
 __global__ __launch_bounds__(256) void upsample2x_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int D,
                                                          int H, int W, int C, long long total) {
   const long long i = blockIdx.x * 256LL + threadIdx.x;
   if (i >= total) return;
-  const int cpr = C >> 3;
-  const int cv = (int)(i % cpr);
-  long long t = i / cpr;
-  const int w = (int)(t % W); t /= W;
-  const int h = (int)(t % H); t /= H;
-  const int d = (int)(t % D);
-  const long long n = t / D;
+  const IDX cpr = (IDX)(C >> 3);
+  IDX t = (IDX)i;
+  const int cv = (int)(t % cpr); t /= cpr;
+  const int w = (int)(t % (IDX)W); t /= (IDX)W;
+  const int h = (int)(t % (IDX)H); t /= (IDX)H;
+  const int d = (int)(t % (IDX)D);
+  const long long n = (long long)(t / (IDX)D);
   const uint4 v = *(const uint4*)(x + i * 8);
   const long long W2 = 2LL * W, H2 = 2LL * H;
 #pragma unroll
@@ -318,17 +321,18 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const bf16* __restrict_
     }
 }
 
+template <typename IDX>
 __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx,
                                                              int D, int H, int W, int C, long long total) {
   const long long i = blockIdx.x * 256LL + threadIdx.x;
   if (i >= total) return;
-  const int cpr = C >> 3;
-  const int cv = (int)(i % cpr);
-  long long t = i / cpr;
-  const int w = (int)(t % W); t /= W;
-  const int h = (int)(t % H); t /= H;
-  const int d = (int)(t % D);
-  const long long n = t / D;
+  const IDX cpr = (IDX)(C >> 3);
+  IDX t = (IDX)i;
+  const int cv = (int)(t % cpr); t /= cpr;
+  const int w = (int)(t % (IDX)W); t /= (IDX)W;
+  const int h = (int)(t % (IDX)H); t /= (IDX)H;
+  const int d = (int)(t % (IDX)D);
+  const long long n = (long long)(t / (IDX)D);
   const long long W2 = 2LL * W, H2 = 2LL * H;
   Pack8 p[8];
 #pragma unroll
@@ -355,12 +359,14 @@ extern "C" int fn_upsample2x(const void* x, void* y, int N, int D, int H, int W,
   if (C % 8) return -2;
   const long long total = (long long)N * D * H * W * (C / 8);
   const unsigned blocks = (unsigned)((total + 255) / 256);
-  if (backward)
-    hipLaunchKernelGGL(upsample2x_bwd_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)y, D, H, W, C,
-                       total);
-  else
-    hipLaunchKernelGGL(upsample2x_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)y, D, H, W, C,
-                       total);
+  const bool small = total < (1LL << 32);
+#define UP_LAUNCH(K, T) hipLaunchKernelGGL(K<T>, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)y, D, H, W, C, total)
+  if (backward) {
+    if (small) UP_LAUNCH(upsample2x_bwd_kernel, unsigned); else UP_LAUNCH(upsample2x_bwd_kernel, unsigned long long);
+  } else {
+    if (small) UP_LAUNCH(upsample2x_kernel, unsigned); else UP_LAUNCH(upsample2x_kernel, unsigned long long);
+  }
+#undef UP_LAUNCH
   FN_CHECK_LAUNCH();
   return 0;
 }
