@@ -151,23 +151,28 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_reduce_kernel(const floa
 // ---------------------------------------------------------------------------
 // dgrad: dx = g W   (C^T = W^T g^T: lane ends with dx[m][4 consecutive kk])
 // ---------------------------------------------------------------------------
-// grid (ceil(K/64), ceil(M/64)); block tile: 64 rows m x 64 columns kk; N % 32 == 0.
-// LDS (dynamic): W tile transposed to [64 kk][N + 8] bf16.
+// grid (ceil(K/64), ceil(M/64)); block tile: 64 rows m x 64 columns kk; any N (the MFMA k dim
+// is padded to NP = ceil(N/32)*32 with zero weights; g rows load as 16-B vectors when N % 8 == 0,
+// element-wise otherwise -- the 10 / 24 / 84-wide NAS heads).
+// LDS (dynamic): W tile transposed to [64 kk][NP + 8] bf16.
 __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __restrict__ g,
                                                                  const float* __restrict__ w,
                                                                  bf16* __restrict__ dx, int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
-  const int LDN = N + 8;                         // row pitch (bf16): 16-B aligned rows, bank shift
+  const int NP = (N + 31) & ~31;
+  const int LDN = NP + 8;                        // row pitch (bf16): 16-B aligned rows, bank shift
   bf16* wt = reinterpret_cast<bf16*>(dn_lds);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, gq = lane >> 4;
   const int kk0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
   // stage W[0:N][kk0:kk0+64] -> wt[kk][n] (bf16): thread = (n, 4 consecutive kk)
-  for (int idx = tid; idx < N * 16; idx += DN_THREADS) {
+  for (int idx = tid; idx < NP * 16; idx += DN_THREADS) {
     const int n = idx >> 4, q = idx & 15;
     const int kk = kk0 + 4 * q;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (kk + 4 <= K) {
+    if (n >= N) {
+      // zero rows of the padded k dimension
+    } else if (kk + 4 <= K) {
       v = *(const float4*)(w + (long long)n * K + kk);
     } else {
       float t[4] = {0.f, 0.f, 0.f, 0.f};
@@ -187,12 +192,21 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const bf16x8 zero8 = {};
-  for (int n0 = 0; n0 < N; n0 += 32) {
+  for (int n0 = 0; n0 < NP; n0 += 32) {
     const bf16x8 fa = *(const bf16x8*)(wt + (kkw + r) * LDN + n0 + 8 * gq);
+    const int nc = n0 + 8 * gq;                  // this lane group's 8 k (= n) values
+    const bool vec = (N & 7) == 0 && nc + 8 <= N;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + j * 16 + r;
-      const bf16x8 v = *(const bf16x8*)(g + (long long)(m < M ? m : 0) * N + n0 + 8 * gq);
+      const bf16* grow = g + (long long)(m < M ? m : 0) * N;
+      bf16x8 v = zero8;
+      if (vec) {
+        v = *(const bf16x8*)(grow + nc);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = nc + e < N ? grow[nc + e] : f2bf(0.f);
+      }
       acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, m < M ? v : zero8, acc[j], 0, 0, 0);
     }
   }
@@ -319,8 +333,8 @@ static int dn_lds_attr(const void* fn, size_t lds) {
 }
 
 extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, int N, int K, hipStream_t st) {
-  if (M <= 0 || K <= 0 || N <= 0 || N % 32 || K % 4) return -2;
-  const size_t lds = (size_t)64 * (N + 8) * 2;
+  if (M <= 0 || K <= 0 || N <= 0 || K % 4) return -2;
+  const size_t lds = (size_t)64 * (((N + 31) & ~31) + 8) * 2;
   if (lds > 160 * 1024) return -4;
   if (int e = dn_lds_attr((const void*)dense_dgrad_kernel, lds)) return e;
   hipLaunchKernelGGL(dense_dgrad_kernel, dim3((K + 63) / 64, (M + 63) / 64), dim3(DN_THREADS), lds, st,

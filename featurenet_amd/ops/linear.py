@@ -7,8 +7,8 @@ GPU: hand-written MFMA kernels (``csrc/kernels/dense.hip``): split-K forward
 that reads the fp32 master weights directly (no per-step bf16 weight copy) with
 bias + activation in the split reduction, a dgrad and a weight-gradient kernel
 that writes the fp32 ``dW`` (and ``db``) straight into the parameters' flat
-gradients.  Shapes outside the kernels' constraints (K % 8, N % 32 for dgrad,
-M % 32 for wgrad) fall back to hipBLASLt through torch for that product.
+gradients.  Shapes outside the kernels' constraints (K % 8 for the forward, K % 4 for
+dgrad, M % 32 for wgrad) fall back to hipBLASLt through torch for that product.
 """
 from __future__ import annotations
 
@@ -83,7 +83,8 @@ class LinearFn(torch.autograd.Function):
         wf = w.detach()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            if _NATIVE and N % 32 == 0 and K % 4 == 0 and wf.dtype == torch.float32 and 64 * (N + 8) * 2 <= 160 * 1024:
+            NP = -(-N // 32) * 32                      # (any N: the kernel pads its k dim to 32)
+            if _NATIVE and K % 4 == 0 and wf.dtype == torch.float32 and 64 * (NP + 8) * 2 <= 160 * 1024:
                 dx = torch.empty(M, K, dtype=torch.bfloat16, device=g.device)
                 Kn.dense_dgrad(g.data_ptr(), wf.data_ptr(), dx.data_ptr(), M, N, K, st,
                                [g.numel(), wf.numel(), dx.numel()])
