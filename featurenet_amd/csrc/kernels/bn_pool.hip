@@ -122,13 +122,25 @@ __global__ __launch_bounds__(256) void colstats_sr_kernel(const bf16* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) { red[tid][j] = active ? s0[j] : 0.f; red[tid][8 + j] = active ? s1[j] : 0.f; }
   __syncthreads();
+  // (1) per chunk position q: sum the rpp threads that held it (fixed order)
+  __shared__ float red2[256][17];
+  if (tid < Q) {
+    float a[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = 0.f;
+    for (int r = 0; r < rpp; ++r)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a[j] += red[r * Q + tid][j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) red2[tid][j] = a[j];
+  }
+  __syncthreads();
+  // (2) channel c sits at super-row offsets e = c + C*i, i < 8/gcd(8, C) (<= 8 terms)
   for (int c = tid; c < C; c += 256) {
     float a = 0.f, b = 0.f;
-    for (int t = 0; t < rpp * Q; ++t) {
-      const int base = 8 * (t % Q);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if ((base + j) % C == c) { a += red[t][j]; b += red[t][8 + j]; }
+    for (int e = c; e < 8 * Q; e += C) {
+      a += red2[e >> 3][e & 7];
+      b += red2[e >> 3][8 + (e & 7)];
     }
     part[(long long)blockIdx.x * 2 * C + c] = a;
     part[(long long)blockIdx.x * 2 * C + C + c] = b;

@@ -22,6 +22,7 @@
 #include "common.h"
 
 #define DN_THREADS 256
+#define DN_WG_MCH 512                            // weight gradient: batch rows per LDS chunk
 
 __device__ __forceinline__ bf16x8 dn_cvt8(const float4 a, const float4 b) {
   bf16x8 v;
@@ -34,7 +35,9 @@ __device__ __forceinline__ bf16x8 dn_cvt8(const float4 a, const float4 b) {
 // forward: split-K partials
 // ---------------------------------------------------------------------------
 // grid (ceil(N/64), ceil(M/128), S); slice s covers k in [s*kc, min(K, (s+1)*kc)), kc % 32 == 0.
-// Requires K % 8 == 0 (16-B rows).
+// VEC (K % 8 == 0): 16-B x rows and float4 weight loads; otherwise element loads masked at kend
+// (the 84-wide LeNet layers).
+template <bool VEC>
 __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* __restrict__ x,
                                                                     const float* __restrict__ w,
                                                                     float* __restrict__ part, int M, int N, int K,
@@ -72,18 +75,33 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
   auto load = [&](int k0) {
     const int k = k0 + 8 * gq;
     const int ks = k < kend ? k : 0;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) ra[i] = *(const bf16x8*)(xr[i] + ks);
+      for (int i = 0; i < 2; ++i) ra[i] = *(const bf16x8*)(xr[i] + ks);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4* p = (const float4*)(wr[j] + ks);
-      rb[j][0] = p[0];
-      rb[j][1] = p[1];
+      for (int j = 0; j < 4; ++j) {
+        const float4* p = (const float4*)(wr[j] + ks);
+        rb[j][0] = p[0];
+        rb[j][1] = p[1];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ra[i][e] = ks + e < kend ? xr[i][ks + e] : f2bf(0.f);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float t[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) t[e] = ks + e < kend ? wr[j][ks + e] : 0.f;
+        rb[j][0] = make_float4(t[0], t[1], t[2], t[3]);
+        rb[j][1] = make_float4(t[4], t[5], t[6], t[7]);
+      }
     }
   };
   if (kbeg < kend) load(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += 32) {
-    const bool kok = k0 + 8 * gq < kend;        // kend % 8 == 0 (K % 8 == 0, kc % 32 == 0)
+    const bool kok = k0 + 8 * gq < kend;        // (a chunk straddling kend was masked at load)
     bf16x8 fa[2], fb[4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) fa[i] = (rok[i] && kok) ? ra[i] : zero8;
@@ -231,53 +249,69 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
 // ---------------------------------------------------------------------------
 // wgrad: dW = g^T x (fp32, overwrite), db = colsum(g)
 // ---------------------------------------------------------------------------
-// grid (ceil(K/64), ceil(N/64)); block tile: 64 n x 64 kk; reduction over all M (M % 32 == 0).
+// grid (ceil(K/64), ceil(N/64)); block tile: 64 n x 64 kk; reduction over all M (padded with
+// zero rows to a multiple of 32); any K, N (element loads where rows are not 16-B aligned).
 // LDS (dynamic): x tile transposed [64 kk][M + 8], g tile transposed [64 n][M + 8].
 __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __restrict__ g,
                                                                  const bf16* __restrict__ x,
                                                                  float* __restrict__ dw, float* __restrict__ db,
                                                                  int M, int N, int K) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
-  const int LDM = M + 8;
+  // rows in chunks of up to DN_WG_MCH (LDS tiles), each padded with zero rows to a multiple of 32
+  const int MCH = M < DN_WG_MCH ? ((M + 31) & ~31) : DN_WG_MCH;
+  const int LDM = MCH + 8;
   bf16* xt = reinterpret_cast<bf16*>(dn_lds);
   bf16* gt = xt + 64 * LDM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, gq = lane >> 4;
   const int kk0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
-  // x[0:M][kk0:kk0+64] -> xt[kk][m]; g[0:M][n0:n0+64] -> gt[n][m]: thread = (m, 8 columns)
-  for (int idx = tid; idx < M * 8; idx += DN_THREADS) {
-    const int m = idx >> 3, q = idx & 7;
-    const int kk = kk0 + 8 * q, n = n0 + 8 * q;
-    Pack8 vx, vg;
-    if (kk + 8 <= K) {
-      vx.u = *(const uint4*)(x + (long long)m * K + kk);
-    } else {
-      for (int e = 0; e < 8; ++e) vx.e[e] = kk + e < K ? x[(long long)m * K + kk + e] : f2bf(0.f);
-    }
-    if (n + 8 <= N) {
-      vg.u = *(const uint4*)(g + (long long)m * N + n);
-    } else {
-      for (int e = 0; e < 8; ++e) vg.e[e] = n + e < N ? g[(long long)m * N + n + e] : f2bf(0.f);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      xt[(8 * q + e) * LDM + m] = vx.e[e];
-      gt[(8 * q + e) * LDM + m] = vg.e[e];
-    }
-  }
-  __syncthreads();
-  // C^T[kk][n] = sum_m x^T[kk][m] g[m][n]: wave = 16 kk rows x 64 n columns
   const int kkw = wave * 16;
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int mm = 0; mm < M; mm += 32) {
-    const bf16x8 fa = *(const bf16x8*)(xt + (kkw + r) * LDM + mm + 8 * gq);
+  float dbs = 0.f;                               // bias gradient (first column block, tid < 64)
+  for (int mb = 0; mb < M; mb += MCH) {
+    const int rows = M - mb < MCH ? M - mb : MCH;
+    const int MP = (rows + 31) & ~31;
+    if (mb > 0) __syncthreads();                 // previous chunk's MFMA / db reads are done
+    // x[mb:mb+rows][kk0:kk0+64] -> xt[kk][m]; g[..][n0:n0+64] -> gt[n][m]: thread = (m, 8 columns)
+    for (int idx = tid; idx < MP * 8; idx += DN_THREADS) {
+      const int ml = idx >> 3, q = idx & 7;
+      const int m = mb + ml;
+      const int kk = kk0 + 8 * q, n = n0 + 8 * q;
+      Pack8 vx, vg;
+      if (ml >= rows) {
+        vx.u = vg.u = make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        if ((K & 7) == 0 && kk + 8 <= K) {       // 16-B aligned rows only when K % 8 == 0
+          vx.u = *(const uint4*)(x + (long long)m * K + kk);
+        } else {
+          for (int e = 0; e < 8; ++e) vx.e[e] = kk + e < K ? x[(long long)m * K + kk + e] : f2bf(0.f);
+        }
+        if ((N & 7) == 0 && n + 8 <= N) {
+          vg.u = *(const uint4*)(g + (long long)m * N + n);
+        } else {
+          for (int e = 0; e < 8; ++e) vg.e[e] = n + e < N ? g[(long long)m * N + n + e] : f2bf(0.f);
+        }
+      }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bf16x8 fb = *(const bf16x8*)(gt + (j * 16 + r) * LDM + mm + 8 * gq);
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[j], 0, 0, 0);
+      for (int e = 0; e < 8; ++e) {
+        xt[(8 * q + e) * LDM + ml] = vx.e[e];
+        gt[(8 * q + e) * LDM + ml] = vg.e[e];
+      }
     }
+    __syncthreads();
+    // C^T[kk][n] = sum_m x^T[kk][m] g[m][n]: wave = 16 kk rows x 64 n columns
+    for (int mm = 0; mm < MP; mm += 32) {
+      const bf16x8 fa = *(const bf16x8*)(xt + (kkw + r) * LDM + mm + 8 * gq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8 fb = *(const bf16x8*)(gt + (j * 16 + r) * LDM + mm + 8 * gq);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[j], 0, 0, 0);
+      }
+    }
+    if (db && blockIdx.x == 0 && tid < 64 && n0 + tid < N)
+      for (int m = 0; m < rows; ++m) dbs += bf2f(gt[tid * LDM + m]);
   }
   // lane: n = n0 + 16j + r, kk = kk0 + kkw + 4gq .. +3 -> dW[n][kk..kk+3]
 #pragma unroll
@@ -293,12 +327,8 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
         if (kk + e < K) o[e] = acc[j][e];
     }
   }
-  // bias gradient: the first column block sums g over M for its 64 n
-  if (db && blockIdx.x == 0 && tid < 64 && n0 + tid < N) {
-    float s = 0.f;
-    for (int m = 0; m < M; ++m) s += bf2f(gt[tid * LDM + m]);
-    db[n0 + tid] = s;
-  }
+  // bias gradient: the first column block summed g over M for its 64 n
+  if (db && blockIdx.x == 0 && tid < 64 && n0 + tid < N) db[n0 + tid] = dbs;
 }
 
 // ---------------------------------------------------------------------------
@@ -313,12 +343,16 @@ extern "C" int fn_dense_splits(int M, int N, int K) {
 
 extern "C" int fn_dense_fwd(const void* x, const float* w, const float* bias, void* out, float* part, int M, int N,
                             int K, int S, int act, int out_fp32, hipStream_t st) {
-  if (M <= 0 || N <= 0 || K <= 0 || K % 8 || S < 1) return -2;
+  if (M <= 0 || N <= 0 || K <= 0 || S < 1) return -2;
   int kc = (K + S - 1) / S;
   kc = (kc + 31) / 32 * 32;
   const int Sr = (K + kc - 1) / kc;              // slices actually covering K
-  hipLaunchKernelGGL(dense_fwd_part_kernel, dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0, st,
-                     (const bf16*)x, w, part, M, N, K, kc);
+  if (K % 8 == 0)
+    hipLaunchKernelGGL(dense_fwd_part_kernel<true>, dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0,
+                       st, (const bf16*)x, w, part, M, N, K, kc);
+  else
+    hipLaunchKernelGGL(dense_fwd_part_kernel<false>, dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0,
+                       st, (const bf16*)x, w, part, M, N, K, kc);
   FN_CHECK_LAUNCH();
   const long long tot = (long long)M * N;
   hipLaunchKernelGGL(dense_fwd_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(DN_THREADS), 0, st,
@@ -345,8 +379,9 @@ extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, in
 
 extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db, int M, int N, int K,
                               hipStream_t st) {
-  if (M <= 0 || N <= 0 || K <= 0 || M % 32 || K % 8) return -2;
-  const size_t lds = (size_t)2 * 64 * (M + 8) * 2;
+  if (M <= 0 || N <= 0 || K <= 0) return -2;
+  const int mch = M < DN_WG_MCH ? ((M + 31) & ~31) : DN_WG_MCH;
+  const size_t lds = (size_t)2 * 64 * (mch + 8) * 2;
   if (lds > 160 * 1024) return -4;
   if (int e = dn_lds_attr((const void*)dense_wgrad_kernel, lds)) return e;
   hipLaunchKernelGGL(dense_wgrad_kernel, dim3((K + 63) / 64, (N + 63) / 64), dim3(DN_THREADS), lds, st,

@@ -7,8 +7,10 @@ GPU: hand-written MFMA kernels (``csrc/kernels/dense.hip``): split-K forward
 that reads the fp32 master weights directly (no per-step bf16 weight copy) with
 bias + activation in the split reduction, a dgrad and a weight-gradient kernel
 that writes the fp32 ``dW`` (and ``db``) straight into the parameters' flat
-gradients.  Shapes outside the kernels' constraints (K % 8 for the forward, K % 4 for
-dgrad, M % 32 for wgrad) fall back to hipBLASLt through torch for that product.
+gradients.  Any K / N / M: the kernels pad the MFMA dims with zeros and load unaligned rows
+element-wise, and the weight gradient walks the batch in 512-row LDS chunks.  Dgrad with
+K % 4 != 0 and weight gradients of batches over 512 rows (too few dW tiles to fill the GPU)
+fall back to hipBLASLt through torch.
 """
 from __future__ import annotations
 
@@ -45,7 +47,7 @@ class LinearFn(torch.autograd.Function):
         M = x2.shape[0]
         wf = w.detach()
         bias = b.detach().float().contiguous() if b is not None else None
-        native = _NATIVE and K % 8 == 0 and wf.dtype == torch.float32 and wf.is_contiguous()
+        native = _NATIVE and wf.dtype == torch.float32 and wf.is_contiguous()
         if native:
             Kn = _native.kernels()
             S = int(Kn.dense_splits(M, N, K))
@@ -93,7 +95,10 @@ class LinearFn(torch.autograd.Function):
             dx = dx.reshape(ctx.xshape)
         want_b = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            if _NATIVE and M % 32 == 0 and K % 8 == 0 and 2 * 64 * (M + 8) * 2 <= 160 * 1024:
+            # one workgroup per 64x64 tile of dW walks the whole batch: fine for the FeatureNet /
+            # NAS training batches (<= 512 rows); larger batches leave too few workgroups, so
+            # hipBLASLt takes them (measured: 1024-row LeNet heads 9x slower on the native kernel)
+            if _NATIVE and M <= 512:
                 dw = grad_target(w)
                 if dw is None:
                     dw = torch.empty(N, K, dtype=torch.float32, device=g.device)

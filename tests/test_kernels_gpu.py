@@ -737,7 +737,9 @@ def test_s2d_weight_map_matches_reference():
 @pytest.mark.parametrize("M,K,N,act,bias", [(128, 64000, 128, "relu", True), (128, 128, 24, None, True),
                                             (64, 2048, 256, "relu", False), (96, 520, 64, None, True),
                                             (32, 4096, 512, "relu", True), (64, 120, 84, "relu", True),
-                                            (64, 84, 10, None, True), (96, 400, 10, None, False)])
+                                            (64, 84, 10, None, True), (96, 400, 10, None, False),
+                                            (50, 84, 10, "relu", True), (20, 30, 7, None, True),
+                                            (1024, 400, 120, "relu", True), (700, 84, 10, None, True)])
 def test_dense_native_matches_fp32(M, K, N, act, bias):
     """Native Dense (split-K forward, dgrad, fp32 wgrad/db) vs the fp32 PyTorch reference."""
     from featurenet_amd.ops.linear import LinearFn
