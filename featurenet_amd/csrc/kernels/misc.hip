@@ -354,9 +354,81 @@ __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const bf16* __restr
   *(uint4*)(dx + i * 8) = o.u;
 }
 
+// Output-row-major variants (C / 8 a power of two <= 32): lane i covers output chunk (w2, cv) of
+// an output row, so every store (forward) / load (backward) instruction of a wave touches one
+// contiguous 1-KB run instead of 128-B pieces two voxels apart.  Forward: one input chunk ->
+// the same chunk of the four output rows (2d+a, 2h+b).  Backward: the four rows' chunks are
+// summed per lane, then the pair (w2 = 2w, 2w+1) -- lanes cpr apart in the same wave -- is
+// folded with one shuffle and the even lane stores dx.
+__global__ __launch_bounds__(256) void upsample2x_rows_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                              int D, int H, int W, int lcpr, unsigned total) {
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= total) return;
+  const unsigned cpr = 1u << lcpr, C = cpr * 8u, W2 = 2u * W;
+  const unsigned cv = i & (cpr - 1);
+  unsigned t = i >> lcpr;
+  const unsigned w2 = t % W2; t /= W2;
+  const unsigned h = t % (unsigned)H; t /= (unsigned)H;
+  const unsigned d = t % (unsigned)D;
+  const long long n = t / (unsigned)D;
+  const uint4 v = *(const uint4*)(x + ((((n * D + d) * H + h) * (long long)W + (w2 >> 1)) * C + cv * 8));
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      *(uint4*)(y + ((((n * 2 * D + 2 * d + a) * 2LL * H + 2 * h + b) * W2 + w2) * C + cv * 8)) = v;
+}
+
+__global__ __launch_bounds__(256) void upsample2x_rows_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx,
+                                                                  int D, int H, int W, int lcpr, unsigned total) {
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= total) return;                        // (total is a multiple of 2 cpr: pairs stay together)
+  const unsigned cpr = 1u << lcpr, C = cpr * 8u, W2 = 2u * W;
+  const unsigned cv = i & (cpr - 1);
+  unsigned t = i >> lcpr;
+  const unsigned w2 = t % W2; t /= W2;
+  const unsigned h = t % (unsigned)H; t /= (unsigned)H;
+  const unsigned d = t % (unsigned)D;
+  const long long n = t / (unsigned)D;
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      Pack8 p;
+      p.u = *(const uint4*)(dy + ((((n * 2 * D + 2 * d + a) * 2LL * H + 2 * h + b) * W2 + w2) * C + cv * 8));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += bf2f(p.e[j]);
+    }
+  Pack8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o.e[j] = f2bf(s[j] + __shfl_down(s[j], (int)cpr, 64));
+  if ((w2 & 1u) == 0)
+    *(uint4*)(dx + ((((n * D + d) * H + h) * (long long)W + (w2 >> 1)) * C + cv * 8)) = o.u;
+}
+
 extern "C" int fn_upsample2x(const void* x, void* y, int N, int D, int H, int W, int C, int backward,
                              hipStream_t st) {
   if (C % 8) return -2;
+  {
+    const int cpr = C / 8;
+    int lcpr = 0;
+    while ((1 << lcpr) < cpr) ++lcpr;
+    const long long tot_rows = (long long)N * D * H * (2LL * W) * cpr;
+    if ((1 << lcpr) == cpr && cpr <= 32 && tot_rows < (1LL << 32)) {
+      const unsigned blocks = (unsigned)((tot_rows + 255) / 256);
+      if (backward)
+        hipLaunchKernelGGL(upsample2x_rows_bwd_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)y, D, H,
+                           W, lcpr, (unsigned)tot_rows);
+      else
+        hipLaunchKernelGGL(upsample2x_rows_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)y, D, H, W,
+                           lcpr, (unsigned)tot_rows);
+      FN_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   const long long total = (long long)N * D * H * W * (C / 8);
   const unsigned blocks = (unsigned)((total + 255) / 256);
   const bool small = total < (1LL << 32);

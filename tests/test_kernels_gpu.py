@@ -697,13 +697,15 @@ def test_halo_pack_weights_matches_torch_layout(K, C, k):
         torch.testing.assert_close(Cm.halo_pack(w, spec, dgrad=True), ref_d, rtol=0, atol=0)
 
 
-def test_upsample2x_fwd_bwd():
-    """Nearest x2 upsample kernels vs the torch expand/reshape reference (fwd exact, bwd block sums)."""
+@pytest.mark.parametrize("C", [16, 64, 24, 256, 8])
+def test_upsample2x_fwd_bwd(C):
+    """Nearest x2 upsample kernels vs the torch expand/reshape reference (fwd exact, bwd block
+    sums); C / 8 a power of two <= 32 takes the output-row-major kernels, 24 the general ones."""
     _native_loaded()
     from featurenet_amd.ops.elementwise import upsample2x
 
     torch.manual_seed(9)
-    x = torch.randn(2, 3, 4, 5, 16, device="cuda").to(torch.bfloat16)
+    x = torch.randn(2, 3, 4, 5, C, device="cuda").to(torch.bfloat16)
     xn = x.clone().requires_grad_(True)
     y = upsample2x(xn)
     n, d, h, w, c = x.shape
