@@ -41,7 +41,8 @@ int fn_concat2(void*, void*, void*, long long, int, int, int, hipStream_t);
 int fn_pad3(void*, void*, const int*, int, hipStream_t);
 int fn_dense_fwd(const void*, const float*, const float*, void*, float*, int, int, int, int, int, int, hipStream_t);
 int fn_dense_dgrad(const void*, const float*, void*, int, int, int, hipStream_t);
-int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, hipStream_t);
+int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, float*, int, hipStream_t);
+int fn_dense_wgrad_slices(int, int, int);
 int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
@@ -294,15 +295,19 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_dense_dgrad(P<const void*>(g), P<const float*>(w), P<void*>(dx), M, N, K, S(st)), "dense_dgrad");
   }, py::arg("g"), py::arg("w"), py::arg("dx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("st"),
      py::arg("ext") = std::vector<long long>());
+  m.def("dense_wgrad_slices", &fn_dense_wgrad_slices);
+  // part: fp32 workspace of S * (N*K + N) elements when S > 1 (dense_wgrad_slices)
   m.def("dense_wgrad", [](uintptr_t g, uintptr_t x, uintptr_t dw, uintptr_t db, int M, int N, int K, uintptr_t st,
-                          std::vector<long long> ext) {
+                          std::vector<long long> ext, uintptr_t part, int slices) {
     fits(ext, 0, (long long)M * N, "dense_wgrad", "g");
     fits(ext, 1, (long long)M * K, "dense_wgrad", "x");
     fits(ext, 2, (long long)N * K, "dense_wgrad", "dw");
-    chk(fn_dense_wgrad(P<const void*>(g), P<const void*>(x), P<float*>(dw), P<float*>(db), M, N, K, S(st)),
+    if (slices > 1) fits(ext, 3, (long long)slices * ((long long)N * K + N), "dense_wgrad", "part");
+    chk(fn_dense_wgrad(P<const void*>(g), P<const void*>(x), P<float*>(dw), P<float*>(db), M, N, K, P<float*>(part),
+                       slices, S(st)),
         "dense_wgrad");
   }, py::arg("g"), py::arg("x"), py::arg("dw"), py::arg("db"), py::arg("M"), py::arg("N"), py::arg("K"),
-     py::arg("st"), py::arg("ext") = std::vector<long long>());
+     py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("part") = 0, py::arg("slices") = 1);
   m.def("s2d_weight_map", [](uintptr_t src, uintptr_t dst, std::vector<int> geom, int dir, uintptr_t st,
                              std::vector<long long> ext) {
     need(geom, 12, "s2d_weight_map");

@@ -255,10 +255,15 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
 __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __restrict__ g,
                                                                  const bf16* __restrict__ x,
                                                                  float* __restrict__ dw, float* __restrict__ db,
-                                                                 int M, int N, int K) {
+                                                                 int M, int N, int K, int mc) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
+  // split over the batch (blockIdx.z = slice of mc rows -> its own dW / db slab, summed by
+  // dense_wgrad_reduce_kernel in a fixed order) so small dW tiles still fill the GPU
+  const int mz0 = blockIdx.z * mc, mz1 = min(M, mz0 + mc);
+  dw += (long long)blockIdx.z * N * K;
+  if (db) db += (long long)blockIdx.z * N;
   // rows in chunks of up to DN_WG_MCH (LDS tiles), each padded with zero rows to a multiple of 32
-  const int MCH = M < DN_WG_MCH ? ((M + 31) & ~31) : DN_WG_MCH;
+  const int MCH = mc < DN_WG_MCH ? ((mc + 31) & ~31) : DN_WG_MCH;
   const int LDM = MCH + 8;
   bf16* xt = reinterpret_cast<bf16*>(dn_lds);
   bf16* gt = xt + 64 * LDM;
@@ -270,10 +275,10 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float dbs = 0.f;                               // bias gradient (first column block, tid < 64)
-  for (int mb = 0; mb < M; mb += MCH) {
-    const int rows = M - mb < MCH ? M - mb : MCH;
+  for (int mb = mz0; mb < mz1; mb += MCH) {
+    const int rows = mz1 - mb < MCH ? mz1 - mb : MCH;
     const int MP = (rows + 31) & ~31;
-    if (mb > 0) __syncthreads();                 // previous chunk's MFMA / db reads are done
+    if (mb > mz0) __syncthreads();               // previous chunk's MFMA / db reads are done
     // x[mb:mb+rows][kk0:kk0+64] -> xt[kk][m]; g[..][n0:n0+64] -> gt[n][m]: thread = (m, 8 columns)
     for (int idx = tid; idx < MP * 8; idx += DN_THREADS) {
       const int ml = idx >> 3, q = idx & 7;
@@ -377,15 +382,51 @@ extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, in
   return 0;
 }
 
-extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db, int M, int N, int K,
-                              hipStream_t st) {
-  if (M <= 0 || N <= 0 || K <= 0) return -2;
-  const int mch = M < DN_WG_MCH ? ((M + 31) & ~31) : DN_WG_MCH;
+// sum of S fp32 slabs [S][n] -> out[n] in slice order (deterministic)
+__global__ __launch_bounds__(256) void dense_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                                 long long n, int S) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += part[(long long)z * n + i];
+    out[i] = v;
+  }
+}
+
+// batch slices of the weight gradient: enough (dW tile, slice) workgroups for the 256 CUs, at
+// least 128 rows per slice (a 128-row batch -- FeatureNet-3D's FC layers -- stays one launch)
+extern "C" int fn_dense_wgrad_slices(int M, int N, int K) {
+  const int tiles = ((K + 63) / 64) * ((N + 63) / 64);
+  int S = (256 + tiles - 1) / tiles;
+  const int maxS = M / 128;
+  return S < 1 ? 1 : (S > maxS ? maxS : S);
+}
+
+// part: fp32 [S][N*K] + [S][N] workspace when S > 1 (fn_dense_wgrad_slices), else unused
+extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db, int M, int N, int K, float* part,
+                              int S, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || S < 1 || (S > 1 && !part)) return -2;
+  int mc = (M + S - 1) / S;
+  mc = (mc + 31) & ~31;
+  S = (M + mc - 1) / mc;                         // slices actually covering M
+  const int mch = mc < DN_WG_MCH ? mc : DN_WG_MCH;
   const size_t lds = (size_t)2 * 64 * (mch + 8) * 2;
   if (lds > 160 * 1024) return -4;
   if (int e = dn_lds_attr((const void*)dense_wgrad_kernel, lds)) return e;
-  hipLaunchKernelGGL(dense_wgrad_kernel, dim3((K + 63) / 64, (N + 63) / 64), dim3(DN_THREADS), lds, st,
-                     (const bf16*)g, (const bf16*)x, dw, db, M, N, K);
+  const long long NK = (long long)N * K;
+  float* pdw = S > 1 ? part : dw;
+  float* pdb = S > 1 ? (db ? part + (long long)S * NK : nullptr) : db;
+  hipLaunchKernelGGL(dense_wgrad_kernel, dim3((K + 63) / 64, (N + 63) / 64, S), dim3(DN_THREADS), lds, st,
+                     (const bf16*)g, (const bf16*)x, pdw, pdb, M, N, K, mc);
   FN_CHECK_LAUNCH();
+  if (S > 1) {
+    hipLaunchKernelGGL(dense_wgrad_reduce_kernel, dim3((unsigned)((NK + 255) / 256 < 2048 ? (NK + 255) / 256 : 2048)),
+                       dim3(256), 0, st, (const float*)part, dw, NK, S);
+    FN_CHECK_LAUNCH();
+    if (db) {
+      hipLaunchKernelGGL(dense_wgrad_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
+                         (const float*)(part + (long long)S * NK), db, (long long)N, S);
+      FN_CHECK_LAUNCH();
+    }
+  }
   return 0;
 }

@@ -8,9 +8,9 @@ that reads the fp32 master weights directly (no per-step bf16 weight copy) with
 bias + activation in the split reduction, a dgrad and a weight-gradient kernel
 that writes the fp32 ``dW`` (and ``db``) straight into the parameters' flat
 gradients.  Any K / N / M: the kernels pad the MFMA dims with zeros and load unaligned rows
-element-wise, and the weight gradient walks the batch in 512-row LDS chunks.  Dgrad with
-K % 4 != 0 and weight gradients of batches over 512 rows (too few dW tiles to fill the GPU)
-fall back to hipBLASLt through torch.
+element-wise; the weight gradient splits the batch into slices (own dW slabs, summed in a
+fixed order) so small dW matrices still fill the GPU.  Only dgrad with K % 4 != 0 falls back
+to hipBLASLt through torch.
 """
 from __future__ import annotations
 
@@ -95,10 +95,7 @@ class LinearFn(torch.autograd.Function):
             dx = dx.reshape(ctx.xshape)
         want_b = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
-            # one workgroup per 64x64 tile of dW walks the whole batch: fine for the FeatureNet /
-            # NAS training batches (<= 512 rows); larger batches leave too few workgroups, so
-            # hipBLASLt takes them (measured: 1024-row LeNet heads 9x slower on the native kernel)
-            if _NATIVE and M <= 512:
+            if _NATIVE:                                # (batch slices fill the GPU for small dW)
                 dw = grad_target(w)
                 if dw is None:
                     dw = torch.empty(N, K, dtype=torch.float32, device=g.device)
@@ -106,8 +103,11 @@ class LinearFn(torch.autograd.Function):
                     db = grad_target(ctx.bparam)
                     if db is None:
                         db = torch.empty(N, dtype=torch.float32, device=g.device)
+                S = int(Kn.dense_wgrad_slices(M, N, K))
+                part = torch.empty(S * (N * K + N), dtype=torch.float32, device=g.device) if S > 1 else None
                 Kn.dense_wgrad(g.data_ptr(), x2.data_ptr(), dw.data_ptr(), _native.ptr(db), M, N, K, st,
-                               [g.numel(), x2.numel(), dw.numel()])
+                               [g.numel(), x2.numel(), dw.numel()] + ([part.numel()] if S > 1 else []),
+                               _native.ptr(part), S)
             else:
                 dw = _wgrad_torch(g, x2)
         if want_b and db is None:
