@@ -397,7 +397,7 @@ __global__ __launch_bounds__(256) void dense_wgrad_reduce_kernel(const float* __
 extern "C" int fn_dense_wgrad_slices(int M, int N, int K) {
   const int tiles = ((K + 63) / 64) * ((N + 63) / 64);
   int S = (256 + tiles - 1) / tiles;
-  const int maxS = M / 128;
+  const int maxS = M / 128 > 1 ? M / 128 : 1;
   return S < 1 ? 1 : (S > maxS ? maxS : S);
 }
 
