@@ -23,7 +23,8 @@ int fn_conv_halo(const void*, const void*, const float*, void*, float*, const in
 long long fn_conv_halo_lds(const int*, int);
 int fn_conv_halo_workers(const int*, int);
 int fn_pw_fwd(const void*, const void*, const float*, void*, long long, int, int, int, hipStream_t, const float*,
-              const float*, int);
+              const float*, int, const void*, const float*, const float*, float*, int);
+int fn_pw_fwd_blocks(long long, int, int);
 int fn_pw_wgrad(const void*, const void*, float*, long long, int, int, hipStream_t, const float*, const float*, int);
 int fn_conv_halo_wgrad_yblocks(const int*, int);
 int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
@@ -353,13 +354,19 @@ PYBIND11_MODULE(_C, m) {
   });
   // psc / psh / pact: optional input prologue x <- pact(x * psc[k] + psh[k]) (BN + act of the
   // producing layer, never materialised)
+  // sy / ssc / ssh / spart / sact: BN-backward moments of the layer whose dz this call computes
+  // (spart fp32 [pw_fwd_blocks][2][N])
   m.def("pw_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t y, long long M, int K, int N, int act,
-                     uintptr_t st, uintptr_t psc, uintptr_t psh, int pact) {
+                     uintptr_t st, uintptr_t psc, uintptr_t psh, int pact, uintptr_t sy, uintptr_t ssc,
+                     uintptr_t ssh, uintptr_t spart, int sact) {
     chk(fn_pw_fwd(P<const void*>(x), P<const void*>(w), P<const float*>(bias), P<void*>(y), M, K, N, act, S(st),
-                  P<const float*>(psc), P<const float*>(psh), pact),
+                  P<const float*>(psc), P<const float*>(psh), pact, P<const void*>(sy), P<const float*>(ssc),
+                  P<const float*>(ssh), P<float*>(spart), sact),
         "pw_fwd");
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("M"), py::arg("K"), py::arg("N"),
-     py::arg("act"), py::arg("st"), py::arg("psc") = 0, py::arg("psh") = 0, py::arg("pact") = 0);
+     py::arg("act"), py::arg("st"), py::arg("psc") = 0, py::arg("psh") = 0, py::arg("pact") = 0, py::arg("sy") = 0,
+     py::arg("ssc") = 0, py::arg("ssh") = 0, py::arg("spart") = 0, py::arg("sact") = 0);
+  m.def("pw_fwd_blocks", &fn_pw_fwd_blocks);
   m.def("pw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, long long M, int K, int N, uintptr_t st,
                        uintptr_t psc, uintptr_t psh, int pact) {
     chk(fn_pw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), M, K, N, S(st), P<const float*>(psc),

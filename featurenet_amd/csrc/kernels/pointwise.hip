@@ -27,11 +27,19 @@ __device__ __forceinline__ int pw_tiles(long long M) { return (int)((M + PW_BM -
 // Y = act(X W^T + b).  KP / NP: K, N padded to 32 / 64.  Dynamic LDS: the A tile
 // [256][KP+8] and the output staging [256][NP+8] share one region (bf16).
 // PRO: -1 = plain input; ACT_NONE / ACT_RELU = input prologue x <- act(x * psc[k] + psh[k])
-template <int KP, int NP, int ACT, bool HAS_BIAS, int PRO = -1>
+// BWS: ACT_NONE / ACT_RELU = the output is the gradient dz of a BN+act layer whose pre-BN input
+//   sy [M][N] (scale ssc, shift ssh) is read alongside: each workgroup also sums that BN's raw
+//   backward moments (sum g, sum g*y), g = dz * act'(y*ssc+ssh), into spart[block][2][N]
+//   (bn_finalize MODE 2) -- the colstats pass over dz and y disappears (N % 8 == 0, 2048 % N == 0)
+template <int KP, int NP, int ACT, bool HAS_BIAS, int PRO = -1, int BWS = -1>
 __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            long long M, int K, int N, const float* __restrict__ psc,
-                                                           const float* __restrict__ psh) {
+                                                           const float* __restrict__ psh,
+                                                           const bf16* __restrict__ sy = nullptr,
+                                                           const float* __restrict__ ssc = nullptr,
+                                                           const float* __restrict__ ssh = nullptr,
+                                                           float* __restrict__ spart = nullptr) {
   constexpr int LDA = KP + 8, LDO = NP + 8;
   constexpr int KS = KP / 32, NT = NP / 16;
   constexpr int CH = KP / 8;                     // 16-B chunks per thread of a 256 x KP tile
@@ -78,6 +86,17 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
     for (int j = 0; j < 8; ++j) {
       psv[j] = psc[pk0 + j];
       phv[j] = psh[pk0 + j];
+    }
+  }
+  constexpr int NSV = BWS >= 0 ? 8 : 1;
+  float ssv[NSV], shv[NSV], sg[NSV], sgy[NSV];
+  if constexpr (BWS >= 0) {                      // this thread's output chunks start at channel 8 tid mod N
+    const int sn0 = (tid * 8) % N;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ssv[j] = ssc[sn0 + j];
+      shv[j] = ssh[sn0 + j];
+      sg[j] = sgy[j] = 0.f;
     }
   }
   const int ntiles = pw_tiles(M);
@@ -157,6 +176,17 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
       int r = (c * 8) / N, n = c * 8 - r * N;
       if (N % 8 == 0) {
         p.u = *(const uint4*)(Os + r * LDO + n);
+        if constexpr (BWS >= 0) {
+          Pack8 q;
+          q.u = *(const uint4*)(sy + o0 + c * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float yv = bf2f(q.e[j]);
+            const float gv = bf2f(p.e[j]) * act_bwd_from_out(act_fwd(yv * ssv[j] + shv[j], BWS), BWS);
+            sg[j] += gv;
+            sgy[j] += gv * yv;
+          }
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -165,6 +195,28 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
         }
       }
       *(uint4*)(y + o0 + c * 8) = p.u;           // rows * N is a multiple of 8 (M % 8 == 0)
+    }
+  }
+  if constexpr (BWS >= 0) {
+    // block reduction of the BN-backward moments (fixed order): thread t holds channels
+    // (8t mod N) .. +7; the dynamic LDS (>= 256 x 40 bf16) is free after the last tile
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(pw_dsm);   // [256][16]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[tid * 16 + j] = sg[j];
+      red[tid * 16 + 8 + j] = sgy[j];
+    }
+    __syncthreads();
+    const int cpr = N / 8;
+    for (int c = tid; c < N; c += PW_NTHR) {
+      float a = 0.f, b2 = 0.f;
+      for (int t2 = c / 8; t2 < PW_NTHR; t2 += cpr) {
+        a += red[t2 * 16 + (c & 7)];
+        b2 += red[t2 * 16 + 8 + (c & 7)];
+      }
+      spart[(long long)blockIdx.x * 2 * N + c] = a;
+      spart[(long long)blockIdx.x * 2 * N + N + c] = b2;
     }
   }
 }
@@ -300,12 +352,34 @@ static bool pw_pro_ok(const float* psc, const float* psh, int K) {
   return !psc || (psh && K % 8 == 0 && 2048 % K == 0);
 }
 
+// grid of the BWS (dgrad + BN-backward moments) launch = rows of its spart slab: 3 workgroups per
+// CU (165 VGPRs: occupancy 3, so a 4-per-CU persistent grid would leave a serial tail)
+extern "C" int fn_pw_fwd_blocks(long long M, int K, int N) {
+  (void)K; (void)N;
+  return pw_grid(M, 3);
+}
+
 extern "C" int fn_pw_fwd(const void* x, const void* w, const float* bias, void* y, long long M, int K, int N, int act,
-                         hipStream_t st, const float* psc, const float* psh, int pact) {
+                         hipStream_t st, const float* psc, const float* psh, int pact, const void* sy,
+                         const float* ssc, const float* ssh, float* spart, int sact) {
   if (K < 1 || K > 64 || N < 1 || N > 64 || M < 8 || M % 8) return -2;
   if (!pw_pro_ok(psc, psh, K)) return -2;
   // ~110-200 VGPRs and <= 37 KB LDS: 4 workgroups per CU for the 32-channel variants
   const dim3 grid((unsigned)pw_grid(M, (K <= 32 && N <= 32) ? 4 : 2));
+  if (sy) {                                      // dgrad + BN-backward moments (see BWS)
+    if (psc || bias || act != ACT_NONE || !ssc || !ssh || !spart || N % 8 || 2048 % N ||
+        (sact != ACT_NONE && sact != ACT_RELU) || K > 32 || N > 32)
+      return -2;
+#define PWS(SA)                                                                                              \
+  hipLaunchKernelGGL((pw_fwd_kernel<32, 32, ACT_NONE, false, -1, SA>), dim3((unsigned)fn_pw_fwd_blocks(M, K, N)),  \
+                     dim3(PW_NTHR),                                                                            \
+                     (size_t)PW_BM * (32 + 8) * 2, st, (const bf16*)x, (const bf16*)w, nullptr, (bf16*)y, M, K, N, \
+                     nullptr, nullptr, (const bf16*)sy, ssc, ssh, spart)
+    if (sact == ACT_RELU) PWS(ACT_RELU); else PWS(ACT_NONE);
+#undef PWS
+    FN_CHECK_LAUNCH();
+    return 0;
+  }
   const bool hb = bias != nullptr;
   // (the 64-channel prologue instances need > 64 KB of LDS only for KP = NP = 64: not emitted)
 #define PWF(KP, NP, A, HB)                                                                                   \

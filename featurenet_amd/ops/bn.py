@@ -228,8 +228,19 @@ class BatchNormActPointwiseFn(torch.autograd.Function):
         w2 = w.detach().reshape(N, C)
         dw = pw_wgrad(d2, y2, pro=(prm[2], prm[3], ctx.act)).reshape(w.shape) if ctx.needs_input_grad[9] else None
         db = native_colsum(d2) if (ctx.has_b and ctx.needs_input_grad[10]) else None
-        dz2 = pw_fwd(d2, w2.t(), None, 0)                    # d(act(bn(y))) [M, C]
-        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params)
+        M = y2.shape[0]
+        Kn = _native.kernels()
+        part = None
+        if C <= 32 and N <= 32 and C % 8 == 0 and 2048 % C == 0:
+            # d(act(bn(y))) [M, C] and this BN's raw backward moments in the same pass
+            part = torch.empty(Kn.pw_fwd_blocks(M, N, C), 2, C, dtype=torch.float32, device=y.device)
+            dz2 = torch.empty(M, C, dtype=torch.bfloat16, device=y.device)
+            wb = w2.t().to(torch.bfloat16).contiguous()
+            Kn.pw_fwd(d2.data_ptr(), wb.data_ptr(), 0, dz2.data_ptr(), M, N, C, 0, _native.stream(d2), 0, 0, 0,
+                      y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), part.data_ptr(), ctx.act)
+        else:
+            dz2 = pw_fwd(d2, w2.t(), None, 0)                # d(act(bn(y))) [M, C]
+        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, True) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.needs_input_grad[1] else None,
                 dbeta if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, dw, db)
