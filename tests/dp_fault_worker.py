@@ -39,4 +39,8 @@ def main() -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    code = main()
+    sys.stdout.flush()
+    # leave without tearing down the broken process group: its gloo threads can abort the
+    # interpreter's shutdown (seen under load: the exit code then hid the clean failure)
+    os._exit(code)
