@@ -42,7 +42,8 @@ def test_run_trial_inline_faults(fault, status):
 def test_scheduler_survives_hang_and_crash():
     """A hung and a crashed trial fail only themselves; the search continues."""
     specs = [_spec("a"), _spec("hang"), _spec("crash"), _spec("b")]
-    sched = TrialScheduler(devices=["cpu", "cpu"], timeout_s=20, mode="process")
+    # (45 s: a spawned worker importing torch on a loaded CI box can take most of 20 s)
+    sched = TrialScheduler(devices=["cpu", "cpu"], timeout_s=45, mode="process")
     res = sched.map(specs, _cfg(inject={"hang": "hang", "crash": "crash"}))
     by = {r.name: r for r in res}
     assert by["a"].status == "trained" and by["b"].status == "trained"
