@@ -375,8 +375,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
         const unsigned char* wl = ks + PD >= nks ? wnext : wbase;   // last turn: next job's steps
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
-          const int ko = ko_n;
-          ko_n = kofs(ks + u + 2);
+          const int ko = (DBG & 32) ? u * 16 * 37 : ko_n;   // (DBG 32, timing only: constant tap offsets)
+          if constexpr (!(DBG & 32)) ko_n = kofs(ks + u + 2);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -803,7 +803,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
 #define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, src, \
       (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, stamps);
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
-    CT_DBG(4, 23)
+    CT_DBG(4, 23) CT_DBG(2, 32) CT_DBG(4, 32)
 #undef CT_DBG
     if (rc) return rc;
     FN_CHECK_LAUNCH();

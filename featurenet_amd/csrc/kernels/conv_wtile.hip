@@ -34,9 +34,11 @@
 
 #include <cstdlib>
 
-#define WT_NCW 4
-#define WT_NTHR (64 * (WT_NCW + 1))
 #define WT_GEOM_LEN 24
+// NW = 4: 4 MFMA waves (one per SIMD) + 1 loader wave; NW = 8: 8 MFMA waves (two per SIMD,
+// twice the VALU/LDS issue slots of a lone wave) that LDS-DMA each job's halo and dy rows
+// themselves (1/8 each) -- no loader, and a workgroup covers twice the taps
+__host__ __device__ constexpr int wt_nthr(int NW) { return NW == 4 ? 64 * 5 : 64 * NW; }
 
 struct WGeom {
   int N, ID, IH, IW, C;      // x, channels-last
@@ -62,8 +64,8 @@ __device__ __forceinline__ bf16x8 wt_tr_pair(const unsigned char* lo, const unsi
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int MT, int NACC>
-__global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __restrict__ x,
+template <int MT, int NACC, int NW, int FAKE = 0>
+__global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* __restrict__ x,
                                                                 const bf16* __restrict__ dy,
                                                                 float* __restrict__ dw,   // partials
                                                                 const int2* __restrict__ rowtab,
@@ -85,9 +87,11 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
   const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH, twn = (g.OW + g.TW - 1) / g.TW;
   const int ntiles = g.N * tdn * thn * twn;
 
+  constexpr int NTHR = wt_nthr(NW);
+  constexpr bool HAS_LOADER = NW == 4;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool loader = wave == WT_NCW;
+  const bool loader = HAS_LOADER && wave == NW;
   // XCD-aware decomposition of the 1-D grid (gridDim.x = 8 * G * workers per group)
   const int xcd = blockIdx.x & 7, lid = blockIdx.x >> 3;
   const int grp = lid % g.G;
@@ -103,14 +107,14 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
   int* s_pos = reinterpret_cast<int*>(s_rows + ROWS);
   int* s_xoff = s_pos + g.HPpad;
   int* s_yoff = s_xoff + g.HPpad;
-  for (int i = tid; i < ROWS; i += WT_NTHR) {
+  for (int i = tid; i < ROWS; i += NTHR) {
     const int2 rt = rowtab[i];
     s_rows[i] = rt;
     // byte offset of the row's dy from the tile origin (interior tiles), -1 for a dummy row
     const int e = rt.y;
     s_yoff[i] = e < 0 ? -1 : (((e >> 16) * g.OH + ((e >> 8) & 255)) * g.OW + (e & 255)) * CO * 2;
   }
-  for (int i = tid; i < g.HPpad; i += WT_NTHR) {
+  for (int i = tid; i < g.HPpad; i += NTHR) {
     const int e = postab[i];
     s_pos[i] = e;
     // byte offset of the position from the halo origin (interior tiles; 0 past the halo:
@@ -128,10 +132,19 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
     const int t1 = t_lo + atomicAdd(cnt, 1);
     return t1 < t_hi ? t1 : -1;
   };
-  if (tid == 0) {
-    const int t0 = grab();
-    s_job[0] = t0;
-    s_job[1] = t0 >= 0 ? grab() : -1;
+  // NW = 8: static round-robin tiles (no atomic round trip on any wave's critical path):
+  // job j of worker wid of this (XCD, group) is tile t_lo + wid + j * nwk
+  const int nwk = (int)(gridDim.x >> 3) / g.G, wid = lid / g.G;
+  auto tile_of = [&](int j) -> int {
+    const int t = t_lo + wid + j * nwk;
+    return t < t_hi ? t : -1;
+  };
+  if constexpr (HAS_LOADER) {
+    if (tid == 0) {
+      const int t0 = grab();
+      s_job[0] = t0;
+      s_job[1] = t0 >= 0 ? grab() : -1;
+    }
   }
   tile_lds_barrier();
 
@@ -148,7 +161,7 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
   // dy rows of job `tile` in k order, DMA instructions first, first + step, ... (8 in
   // flight): slot s = CPR * row + chunk slot, holding source chunk slot ^ swizzle(row)
   const int ny = (ROWS * CPR) >> 6;
-  auto dma_dy = [&](int tile, int bufoff, int first, int step) {
+  auto dma_dy = [&](int tile, int bufoff, int first, int step, int mlo = 0, int mhi = 1 << 20) {
     tile = __builtin_amdgcn_readfirstlane(tile);
     int n, d0, h0, w0;
     decode(tile, n, d0, h0, w0);
@@ -157,7 +170,8 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
     const bool y_in = d0 + g.TD <= g.OD && h0 + g.TH <= g.OH && w0 + g.TW <= g.OW;
     const unsigned char* yo =
         reinterpret_cast<const unsigned char*>(ys + ((long long)(d0 * g.OH + h0) * g.OW + w0) * CO);
-    for (int j0 = first; j0 < ((dbg & 8) ? 0 : ny); j0 += 8 * step) {   // (dbg 8, timing only: no dy DMA)
+    const int jend = min((dbg & 8) ? 0 : ny, first + mhi * step);   // (dbg 8, timing only: no dy DMA)
+    for (int j0 = first + mlo * step; j0 < jend; j0 += 8 * step) {
       int o[8], e[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -168,14 +182,15 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int j = j0 + i * step;
-        if (j < ny) {
+        if (j < jend) {
           const int sl = 64 * j + lane;
           const int r = sl / CPR;
           const int c = (sl % CPR) ^ (2 * (((unsigned)r / R64) % NSW));
           bool ok = o[i] >= 0;
           if (!y_in) ok = ok && d0 + (e[i] >> 16) < g.OD && h0 + ((e[i] >> 8) & 255) < g.OH && w0 + (e[i] & 255) < g.OW;
           const void* src = ok ? (const void*)(yo + o[i] + c * 16) : (const void*)zp;
-          ct_glds16(src, dst0 + (unsigned)(j << 10));
+          if constexpr (HAS_LOADER) ct_glds16(src, dst0 + (unsigned)(j << 10));
+          else ct_glds16_nc(src, dst0 + (unsigned)(j << 10));
         }
       }
     }
@@ -186,7 +201,7 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
   // precomputed per-slot offsets from an SGPR base (table reads in batches of 8, one LDS
   // latency per batch); edge tiles check every slot against the input bounds and read
   // the zero page outside.
-  auto dma_x = [&](int tile, int bufoff, int first, int step) {
+  auto dma_x = [&](int tile, int bufoff, int first, int step, int mlo = 0, int mhi = 1 << 20) {
     tile = __builtin_amdgcn_readfirstlane(tile);
     bufoff = __builtin_amdgcn_readfirstlane(bufoff);
     int n, d0, h0, w0;
@@ -194,23 +209,24 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
     const int dlo = d0 - g.pd, hlo = h0 - g.ph, wlo = w0 - g.pw;
     const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
     const bf16* xs = x + (long long)n * g.ID * g.IH * g.IW * g.C + slice * 16;
-    const int nx = g.HPpad >> 5;               // DMA instructions of the x halo
+    const int nx = min(g.HPpad >> 5, first + mhi * step);   // DMA instructions of the x halo (this range)
     const bool x_in = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID && hlo + HH <= g.IH &&
                       wlo + HW <= g.IW;
     if (dbg & 4) {                             // (timing only: no x halo DMA)
     } else if (x_in) {
       const bf16* xo = xs + ((long long)(dlo * g.IH + hlo) * g.IW + wlo) * g.C;
-      for (int j0 = first; j0 < nx; j0 += 8 * step) {
+      for (int j0 = first + mlo * step; j0 < nx; j0 += 8 * step) {
         int o[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = s_xoff[((64 * min(j0 + i * step, nx - 1) + lane) >> 1)];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
           if (j0 + i * step < nx)
-            ct_glds16_s(xo, (unsigned)(o[i] + (lane & 1) * 16), dst0 + (unsigned)((j0 + i * step) << 10));
+            if constexpr (HAS_LOADER) ct_glds16_s(xo, (unsigned)(o[i] + (lane & 1) * 16), dst0 + (unsigned)((j0 + i * step) << 10));
+            else ct_glds16_s_nc(xo, (unsigned)(o[i] + (lane & 1) * 16), dst0 + (unsigned)((j0 + i * step) << 10));
       }
     } else {
-      for (int j0 = first; j0 < nx; j0 += 8 * step) {
+      for (int j0 = first + mlo * step; j0 < nx; j0 += 8 * step) {
         int e[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) e[i] = s_pos[((64 * min(j0 + i * step, nx - 1) + lane) >> 1)];
@@ -221,13 +237,21 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
             const bool ok = e[i] >= 0 && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
                             (unsigned)gw < (unsigned)g.IW;
             const bf16* src = ok ? xs + ((long long)(gd * g.IH + gh) * g.IW + gw) * g.C + (lane & 1) * 8 : zp;
-            ct_glds16(src, dst0 + (unsigned)((j0 + i * step) << 10));
+            if constexpr (HAS_LOADER) ct_glds16(src, dst0 + (unsigned)((j0 + i * step) << 10));
+            else ct_glds16_nc(src, dst0 + (unsigned)((j0 + i * step) << 10));
           }
         }
       }
     }
   };
 
+  if constexpr (!HAS_LOADER) {                  // job 0, 1/NW of it by each wave
+    const int t0 = tile_of(0);
+    if (t0 >= 0) {
+      dma_x(t0, 0, wave, NW);
+      dma_dy(t0, 0, wave, NW);
+    }
+  }
   if (loader) {
     // ======================= loader wave =======================
     int cur = __builtin_amdgcn_readfirstlane(s_job[0]);
@@ -259,13 +283,14 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
 
   // ======================= compute waves =======================
   const int G4 = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  const int tap0 = (tg * WT_NCW + wave) * NACC;
+  const int tap0 = (tg * NW + wave) * NACC;
   int toff[NACC];                                // byte offsets of this wave's taps in the halo
 #pragma unroll
   for (int i = 0; i < NACC; ++i) {
     const int t = tap0 + i < T ? tap0 + i : 0;   // dead taps read tap 0 (never stored)
     const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
     toff[i] = ((kd * HH + kh) * HW + kw) * 32;
+    if constexpr (FAKE != 0) toff[i] = i * 32 * 7;   // (timing experiment: compile-time tap offsets)
   }
   const bool live = tap0 < T;
   f32x4 acc[NACC][MT];
@@ -300,13 +325,29 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
     for (int mt = 0; mt < MT; ++mt) f[mt] = wt_tr_pair(yb + dy_addr(r_lo, mt), yb + dy_addr(r_lo + 16, mt));
   };
   int jc = 0;                                   // job index (s_job ring slot jc % 3)
+  int dnext = -1;                               // NW = 8: the tile this wave DMAs during the current job
+  // this wave's share of the next job's DMA instructions (x: j = wave + 8m, m < mx; dy alike)
+  const int mx = ((g.HPpad >> 5) - wave + NW - 1) / NW, my = (ny - wave + NW - 1) / NW;
+  // issued at k-step 0 by waves 0-3 and at mid-job by waves 4-7 (the two waves of a SIMD
+  // never both stop their MFMAs for the DMA burst at the same time)
+  const int kdma = wave < NW / 2 ? 0 : g.kst / 2;
+  auto dma_slice = [&](int k) {
+    if (dnext < 0 || k != kdma) return;
+    const int bo = (par ^ 1) * g.BUF;
+    dma_x(dnext, bo, wave, NW);
+    dma_dy(dnext, bo, wave, NW);
+  };
   auto start_job = [&]() -> bool {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's dy DMAs of the job about to start
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of the job about to start
     tile_lds_barrier();                          // A
-    const int tile = __builtin_amdgcn_readfirstlane(s_job[jc % 3]);
+    const int tile = HAS_LOADER ? __builtin_amdgcn_readfirstlane(s_job[jc % 3]) : tile_of(jc);
     if (tile < 0) return false;
-    const int nxt = __builtin_amdgcn_readfirstlane(s_job[(jc + 1) % 3]);
-    if (nxt >= 0 && !(dbg & 1)) dma_dy(nxt, (par ^ 1) * g.BUF, wave, WT_NCW);   // a quarter of job j+1's dy
+    const int nxt = HAS_LOADER ? __builtin_amdgcn_readfirstlane(s_job[(jc + 1) % 3]) : tile_of(jc + 1);
+    if constexpr (HAS_LOADER) {
+      if (nxt >= 0 && !(dbg & 1)) dma_dy(nxt, (par ^ 1) * g.BUF, wave, NW);   // a quarter of job j+1's dy
+    } else {
+      dnext = (dbg & 1) ? -1 : nxt;              // 1/NW of job j+1's halo and dy rows, a slice per k-step
+    }
     ++jc;
     xb = dsm + par * g.BUF;
     yb = xb + g.XB;
@@ -323,6 +364,7 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
       // the next k-step's rows and A fragments are read here, a whole k-step ahead
       // row offsets two k-steps ahead (read here, used for the next k-step's ring refill: a
       // read consumed in the same k-step made hipcc drain every LDS read in flight)
+      if constexpr (!HAS_LOADER) dma_slice(ks);
       const int ksn = ks + 1 < g.kst ? ks + 1 : ks;   // (a job's last k-steps re-read themselves: unused)
       const int ksnn = ks + 2 < g.kst ? ks + 2 : ksn;
       int plo_nn, phi_nn;
@@ -381,23 +423,49 @@ __global__ __launch_bounds__(WT_NTHR, 1) void conv_wtile_kernel(const bf16* __re
   }
 }
 
-// dw[e] (+)= sum over the partials p = 0 .. W-1 of part[p][e], in that order
+// dw[e] (+)= sum over the partials p = 0 .. W-1 of part[p][e], in a fixed order: each of the
+// 4 waves of a block sums a quarter of the partials for the block's 64 float4 columns, and
+// the quarters are added in wave order (deterministic; 4x the parallelism of one thread per
+// column walking all W partials)
 __global__ __launch_bounds__(256) void wtile_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
                                                            long long n, int W, int accumulate) {
-  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= n) return;
+  __shared__ float4 s_q[4][64];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const long long i = ((long long)blockIdx.x * 64 + l) * 4;
+  const int q = (W + 3) / 4, p0 = w * q, p1 = min(W, p0 + q);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i + 4 <= n) {
-    float4 a = accumulate ? *(const float4*)(dw + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int p = 0; p < W; ++p) {
+#pragma unroll 4
+    for (int p = p0; p < p1; ++p) {
       const float4 v = *(const float4*)(part + (long long)p * n + i);
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
-    *(float4*)(dw + i) = a;
-  } else {
-    for (long long j = i; j < n; ++j) {
-      float a = accumulate ? dw[j] : 0.f;
-      for (int p = 0; p < W; ++p) a += part[(long long)p * n + j];
-      dw[j] = a;
+  } else if (i < n) {
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int p = p0; p < p1; ++p)
+      for (long long j = i; j < n; ++j) t[j - i] += part[(long long)p * n + j];
+    a = make_float4(t[0], t[1], t[2], t[3]);
+  }
+  s_q[w][l] = a;
+  __syncthreads();
+  if (w == 0 && i < n) {
+    float4 r = accumulate ? (i + 4 <= n ? *(const float4*)(dw + i) : make_float4(0.f, 0.f, 0.f, 0.f))
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (accumulate && i + 4 > n) {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (long long j = i; j < n; ++j) t[j - i] = dw[j];
+      r = make_float4(t[0], t[1], t[2], t[3]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = s_q[k][l];
+      r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    }
+    if (i + 4 <= n) {
+      *(float4*)(dw + i) = r;
+    } else {
+      const float t[4] = {r.x, r.y, r.z, r.w};
+      for (long long j = i; j < n; ++j) dw[j] = t[j - i];
     }
   }
 }
@@ -421,6 +489,9 @@ static size_t wtile_lds(const WGeom& g) {
 }
 
 extern "C" int fn_conv_wtile_supported(int K, int nacc) {
+  const int nw = nacc >> 8;
+  nacc &= 255;
+  if (nw == 8) return (K == 32 && (nacc == 4 || nacc == 8 || nacc == 16)) || (K == 64 && (nacc == 4 || nacc == 8));
   return (K == 16 && nacc == 16) || (K == 32 && (nacc == 8 || nacc == 16)) || (K == 64 && nacc == 8);
 }
 
@@ -433,41 +504,55 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
                              const void* postab, const void* zp, const int* geom, int nacc, int workers, int* sched,
                              hipStream_t st) {
   const WGeom g = parse_wgeom(geom);
-  if (!fn_conv_wtile_supported(g.K, nacc) || g.C % 16 || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
+  static const int fake = [] { const char* e = getenv("FN_WTILE_FAKE"); return e ? atoi(e) : 0; }();
+  const int nw = (nacc >> 8) == 8 ? 8 + fake : 4;       // nacc | (8 << 8): the loaderless 8-wave variant
+  if (!fn_conv_wtile_supported(g.K, nacc)) return -2;
+  nacc &= 255;
+  if (g.C % 16 || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const long long HP = (long long)(g.TD + g.KD - 1) * HH * HW;
   const int T = g.KD * g.KH * g.KW;
   if (g.HPpad < HP || g.HPpad % 32 || g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
   if ((long long)g.TD * g.TH * g.TW > 32LL * g.kst || g.kst < 1 || g.kst > 32) return -3;
   if (g.XB != g.HPpad * 32 || g.BUF < g.XB + g.kst * 32 * g.K * 2 || g.BUF % 1024) return -3;
-  if (g.ntg != (T + 4 * nacc - 1) / (4 * nacc) || g.G != g.ntg * (g.C / 16) || 8 * g.G > 63) return -3;
+  if (g.ntg != (T + (nw & 12) * nacc - 1) / ((nw & 12) * nacc) || g.G != g.ntg * (g.C / 16) || 8 * g.G > 63) return -3;
   if ((g.kst * 32 * (g.K / 8)) % 64) return -3;
   const size_t lds = wtile_lds(g);
   if (lds > 160 * 1024) return -4;
   if (!sched || !zp || !part || workers < 1) return -6;
   const unsigned grid = 8u * (unsigned)g.G * (unsigned)workers;
   static const int dbg = [] { const char* e = getenv("FN_WTILE_DBG"); return e ? atoi(e) : 0; }();
-#define WT_CASE(M, A)                                                                                          \
-  if (g.K == M * 16 && nacc == A) {                                                                            \
+#define WT_CASE(M, A, W)                                                                                       \
+  if (g.K == M * 16 && nacc == A && nw == W) {                                                                 \
     static size_t cfg = 0;                                                                                     \
     if (lds > cfg) {                                                                                           \
-      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A>,                                 \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A, W>,                              \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
       if (e != hipSuccess) return (int)e;                                                                      \
       cfg = lds;                                                                                               \
     }                                                                                                          \
-    hipLaunchKernelGGL((conv_wtile_kernel<M, A>), dim3(grid), dim3(WT_NTHR), lds, st, (const bf16*)x,          \
+    hipLaunchKernelGGL((conv_wtile_kernel<M, A, W>), dim3(grid), dim3(wt_nthr(W)), lds, st, (const bf16*)x,    \
                        (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab, (const bf16*)zp, g, sched, \
                        dbg);                                                                                   \
   }
-  WT_CASE(1, 16)
-  WT_CASE(2, 8)
-  WT_CASE(2, 16)
-  WT_CASE(4, 8)
+  WT_CASE(1, 16, 4)
+  WT_CASE(2, 8, 4)
+  WT_CASE(2, 16, 4)
+  WT_CASE(4, 8, 4)
+  WT_CASE(2, 4, 8)
+  WT_CASE(2, 8, 8)
+  WT_CASE(2, 16, 8)
+  WT_CASE(4, 4, 8)
+  WT_CASE(4, 8, 8)
+  if (g.K == 32 && nacc == 16 && nw == 9) {
+    hipFuncSetAttribute((const void*)conv_wtile_kernel<2, 16, 8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((conv_wtile_kernel<2, 16, 8, 1>), dim3(grid), dim3(512), lds, st, (const bf16*)x,
+                       (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab, (const bf16*)zp, g, sched, dbg);
+  }
 #undef WT_CASE
   FN_CHECK_LAUNCH();
   const long long n = (long long)g.K * T * g.C;
-  hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n / 4 + 256) / 256)), dim3(256), 0, st, part, dw, n,
+  hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, dw, n,
                      8 * workers, 1);
   FN_CHECK_LAUNCH();
   return 0;

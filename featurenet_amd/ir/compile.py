@@ -158,6 +158,8 @@ class _Builder:
             if getattr(conv, "extra_pad", (0, 0, 0)) != (0, 0, 0):
                 continue
             ph, pw = arg
+            if not _pad_foldable(conv, (0, ph, pw)):
+                continue
             conv.extra_pad = (0, ph, pw)
             self.prog[i] = ("alias", None, ins)
 
@@ -374,6 +376,27 @@ def _conv_out(i: int, k: int, s: int, pad: str) -> int:
     if pad == "same":
         return -(-i // s)
     return (i - k) // s + 1
+
+
+def _pad_foldable(conv, extra) -> bool:
+    """A ZeroPadding folds into ``conv`` only while every total pad stays within the kernel
+    (lo, hi <= K - 1, stride 1, dilation 1): the stride-1 dgrad kernels run the transposed
+    conv with leading pads K - 1 - lo, which must not go negative (a 1x1 conv after a
+    fillSize-1 padding, or a 3x3 after padding 2, keeps the explicit pad op)."""
+    strides = conv.stride if isinstance(conv.stride, (tuple, list)) else (conv.stride,) * 3
+    dil = conv.dilation if isinstance(conv.dilation, (tuple, list)) else (conv.dilation,) * 3
+    if any(int(v) != 1 for v in strides) or any(int(v) != 1 for v in dil):
+        return False
+    for k, e in zip(conv.kernel, extra):
+        if conv.padding == "same":
+            lo, hi = (k - 1) // 2, k - 1 - (k - 1) // 2
+        elif conv.padding == "valid":
+            lo, hi = 0, 0
+        else:
+            return False
+        if lo + e > k - 1 or hi + e > k - 1:
+            return False
+    return True
 
 
 class CandidateNet(nn.Module):

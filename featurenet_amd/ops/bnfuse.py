@@ -16,9 +16,13 @@ Autograd runs the two ops as separate Functions, so they meet here:
 * :func:`take` -- the BN backward claims the slab for its ``dz`` (else it runs
   ``colstats`` as before).
 
-Entries hold weak references and are matched on storage pointer, numel and the
-identity of ``y``, so a miss (a fork in the graph that sums gradients, the halo
-kernel chosen for dgrad, no-grad forward) only falls back to the separate pass.
+Entries hold weak references and are matched on storage pointer, numel, the
+identity of ``y`` and the version counter of ``dz``: when the BN output has
+other consumers, autograd may add their gradients into the conv's ``dx`` in
+place (same storage, bumped version), and the slab then describes only the
+conv branch -- the version check turns that into a miss.  A miss (a fork in the
+graph, the halo kernel chosen for dgrad, no-grad forward) only falls back to the
+separate pass.
 """
 from __future__ import annotations
 
@@ -30,7 +34,7 @@ import torch
 
 _LOCK = threading.Lock()
 _FWD: dict = {}      # z.data_ptr() -> (ref z, ref y, ref prm, act)
-_BWD: dict = {}      # dz.data_ptr() -> (ref dz, slab, ref y)
+_BWD: dict = {}      # dz.data_ptr() -> (ref dz, slab, ref y, dz._version at offer)
 
 
 def enabled() -> bool:
@@ -76,7 +80,7 @@ def source_of(x: torch.Tensor):
 def offer(dz: torch.Tensor, slab: torch.Tensor, y: torch.Tensor) -> None:
     with _LOCK:
         _purge(_BWD)
-        _BWD[dz.data_ptr()] = (weakref.ref(dz), slab, weakref.ref(y))
+        _BWD[dz.data_ptr()] = (weakref.ref(dz), slab, weakref.ref(y), dz._version)
 
 
 def take(dz: torch.Tensor, y: torch.Tensor):
@@ -88,4 +92,6 @@ def take(dz: torch.Tensor, y: torch.Tensor):
     d, yy = e[0](), e[2]()
     if d is None or yy is None or d.numel() != dz.numel() or yy.data_ptr() != y.data_ptr():
         return None
+    if dz._version != e[3] or d._version != e[3]:
+        return None                               # modified since (another branch's gradient added)
     return e[1]

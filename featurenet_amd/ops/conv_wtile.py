@@ -45,6 +45,7 @@ class WPlan:
     workers: int
     BUF: int
     cost: float
+    nw: int = 4      # MFMA waves per workgroup: 4 (+ a loader wave) or 8 (no loader)
 
     @property
     def rows(self) -> int:
@@ -56,7 +57,14 @@ def mode() -> str:
     return os.environ.get("FN_WTILE", "1")
 
 
-def _nacc(K: int, T: int) -> int | None:
+def _nacc(K: int, T: int, nw: int = 4) -> int | None:
+    if nw == 8:                                   # 8 waves x nacc taps per workgroup
+        if K not in (32, 64):
+            return None
+        for a in ((4, 8, 16) if K == 32 else (4, 8)):
+            if T <= 8 * a:
+                return a
+        return 16 if K == 32 else 8
     if K == 16:
         return 16
     if K == 64:
@@ -80,13 +88,21 @@ def plan(spec) -> WPlan | None:
     return p
 
 
+def nwaves() -> int:
+    """FN_WTILE_NW: 8 (default) = the loaderless 8-MFMA-wave variant, 4 = 4 MFMA waves + loader."""
+    return int(os.environ.get("FN_WTILE_NW", "8"))
+
+
 def _plan(spec):
     K, C = spec.K, spec.C
     T = spec.KD * spec.KH * spec.KW
-    nacc = _nacc(K, T)
+    nw = nwaves()
+    nacc = _nacc(K, T, nw)
+    if nacc is None and nw == 8:
+        nw, nacc = 4, _nacc(K, T)
     if nacc is None or C % 16 or T < 2:
         return None
-    ntg = -(-T // (4 * nacc))
+    ntg = -(-T // (nw * nacc))
     G = ntg * (C // 16)
     if 8 * G > 63:
         return None
@@ -115,11 +131,11 @@ def _plan(spec):
                     continue
                 tiles = spec.N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
                 jobs = math.ceil(math.ceil(tiles / 8) / workers)
-                mfma = kst * nacc * MT * 16 + 400                 # per compute wave per job
+                mfma = kst * nacc * MT * 16 * (2 if nw == 8 else 1) + 400   # per SIMD per job
                 loader = 600 + (HPpad * 2 // 64 + kst * K // 16) * 60
                 cost = jobs * max(mfma, loader) * (1.0 + 0.02 * HP / rows)   # halo re-reads (L2 traffic)
                 if best is None or cost < best.cost:
-                    best = WPlan(TD, TH, TW, HPpad, kst, nacc, ntg, G, workers, BUF, float(cost))
+                    best = WPlan(TD, TH, TW, HPpad, kst, nacc, ntg, G, workers, BUF, float(cost), nw)
     return best
 
 
@@ -217,7 +233,7 @@ def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) ->
     dw = out if out is not None else torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=dev)
     part = _partials(dev, st, 8 * p.workers * dw.numel())
     _native.kernels().conv_wtile(x5.data_ptr(), dy5.data_ptr(), dw.data_ptr(), part.data_ptr(), rt.data_ptr(),
-                                 pt.data_ptr(), zp.data_ptr(), geometry(p, spec), p.nacc, p.workers, sched.data_ptr(),
+                                 pt.data_ptr(), zp.data_ptr(), geometry(p, spec), p.nacc | (p.nw << 8 if p.nw == 8 else 0), p.workers, sched.data_ptr(),
                                  st, [x5.numel(), dy5.numel(), dw.numel(), rt.numel() // 2, pt.numel(), part.numel()])
     return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
 

@@ -14,6 +14,21 @@ from .. import _native
 from . import reference as ref
 
 
+def _xent_rows(lg, labels, smoothing, want_correct):
+    """One pass of the fused kernel: (per-block loss partials, d(logits) with 1/B folded in,
+    per-row top-1 hits or None)."""
+    B, NC = lg.shape
+    K = _native.kernels()
+    nblk = K.softmax_xent_blocks(B, NC)
+    part = torch.empty(max(int(nblk), 1), dtype=torch.float32, device=lg.device)
+    dlog = torch.empty_like(lg)                         # 1/B folded in, logits' dtype
+    correct = torch.empty(B, dtype=torch.int32, device=lg.device) if want_correct else None
+    K.softmax_xent_rows(lg.data_ptr(), int(lg.dtype == torch.bfloat16), labels.data_ptr(),
+                        part.data_ptr(), dlog.data_ptr(), _native.ptr(correct), B, NC, 1.0 / B,
+                        float(smoothing), _native.stream(lg))
+    return part, dlog, correct
+
+
 class SoftmaxXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, labels, smoothing: float, want_correct: bool = True):
@@ -21,25 +36,25 @@ class SoftmaxXentFn(torch.autograd.Function):
         lg = logits.contiguous()
         if lg.dtype not in (torch.bfloat16, torch.float32):
             lg = lg.float()
-        K = _native.kernels()
-        nblk = K.softmax_xent_blocks(B, NC)
-        part = torch.empty(max(int(nblk), 1), dtype=torch.float32, device=lg.device)
-        dlog = torch.empty_like(lg)                     # 1/B folded in, logits' dtype
-        correct = torch.empty(B, dtype=torch.int32, device=lg.device) if want_correct else None
-        K.softmax_xent_rows(lg.data_ptr(), int(lg.dtype == torch.bfloat16), labels.contiguous().data_ptr(),
-                            part.data_ptr(), dlog.data_ptr(), _native.ptr(correct), B, NC, 1.0 / B,
-                            float(smoothing), _native.stream(lg))
-        ctx.save_for_backward(dlog)
+        labels = labels.contiguous()
+        part, dlog, correct = _xent_rows(lg, labels, smoothing, want_correct)
+        # logits / labels are kept only for a second backward (retain_graph), which recomputes
+        # d(logits): the first backward scales the stored one in place
+        ctx.save_for_backward(dlog, lg, labels)
         ctx.in_dtype = logits.dtype
+        ctx.smoothing = smoothing
         if correct is not None:
             ctx.mark_non_differentiable(correct)
         return part.sum() / B, correct
 
     @staticmethod
     def backward(ctx, dloss, _dc):
-        (dlog,) = ctx.saved_tensors
-        if getattr(ctx, "scaled", False):              # a second backward (retain_graph): out of place
-            return (dlog * dloss.to(dlog.dtype)).to(ctx.in_dtype), None, None, None
+        dlog, lg, labels = ctx.saved_tensors
+        if getattr(ctx, "scaled", False):
+            # a second backward (retain_graph): the stored d(logits) already carries the first
+            # call's dloss, so recompute it and scale out of place
+            _, base, _ = _xent_rows(lg, labels, ctx.smoothing, False)
+            return (base * dloss.to(base.dtype)).to(ctx.in_dtype), None, None, None
         ctx.scaled = True
         # scale the stored d(logits) in place by dloss -- a near-empty launch when dloss == 1
         # (every plain loss.backward()): the device-side check needs no host sync

@@ -49,6 +49,14 @@ def grad_target(p: torch.Tensor):
     return slot.view.view(slot.view.shape)   # a fresh alias: autograd adopts it without a copy
 
 
+def _adopt_hook(p) -> None:
+    """Post-accumulate-grad hook of every flat parameter: a module-level function (not a
+    bound method), so a hook left on a parameter never keeps a FlatParams alive."""
+    slot = _DIRECT.get(p.data_ptr())
+    if slot is not None and slot.flat is not None:
+        slot.flat._adopt(p)
+
+
 class FlatParams:
     def __init__(self, module: nn.Module, order: str = "reverse"):
         params = [p for p in module.parameters() if p.requires_grad]
@@ -66,6 +74,13 @@ class FlatParams:
         self.grad = torch.zeros(total, dtype=torch.float32, device=device)
         self.slices: list[tuple[nn.Parameter, int, int]] = []
         self._slots = []
+        self._hooks = []
+        # a FlatParams built again on the same parameters supersedes the old one: drop the
+        # old hooks (they would pile up and keep its buffers alive through the bound method)
+        for p in params:
+            old = _DIRECT.get(p.data_ptr())
+            if old is not None and old.flat is not None:
+                old.flat.release()
         with torch.no_grad():
             for p, off in zip(params, offs):
                 n = p.numel()
@@ -77,8 +92,20 @@ class FlatParams:
                 slot = _Slot(self, p, view)
                 self._slots.append(slot)
                 _DIRECT[p.data_ptr()] = slot
-                p.register_post_accumulate_grad_hook(self._adopt)
+                self._hooks.append(p.register_post_accumulate_grad_hook(_adopt_hook))
         self.module = module
+
+    def release(self) -> None:
+        """Detach this FlatParams from its parameters' gradient hooks and direct-gradient
+        slots (the parameters keep pointing into ``data``)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        for slot in self._slots:
+            if _DIRECT.get(slot.param.data_ptr()) is slot:
+                del _DIRECT[slot.param.data_ptr()]
+            slot.flat = None
+        self._slots = []
 
     @property
     def n_params(self) -> int:
@@ -90,7 +117,7 @@ class FlatParams:
             slot.param.grad = None
             slot.claimed = False
 
-    def _adopt(self, p) -> None:
+    def _adopt(self, p) -> None:  # noqa: D401 - see _adopt_hook
         """Post-accumulate hook: make ``p.grad`` the flat slice (copying a gradient autograd
         produced elsewhere).  Runs before any data-parallel bucket hook of ``p``."""
         slot = _DIRECT.get(p.data_ptr())

@@ -31,7 +31,7 @@ from ..ops import FlatAdam, FlatSGD, softmax_xent
 from ..parallel.ddp import DistributedFailure, GradBucketer
 from ..utils.events import default_log
 from .callbacks import Callback
-from .checkpoint import save_checkpoint
+from .checkpoint import capture_rng, read_checkpoint, read_rng, restore_rng, save_checkpoint
 from .data import DeviceLoader
 from .flat import FlatParams
 
@@ -110,6 +110,10 @@ class Trainer:
         self._graph = None
         self._gkey = None
         self._gwarm = 0
+        # resume state: epochs completed, and the fit loader's generator at the last epoch end
+        self.epochs_done = 0
+        self._loader = None
+        self._resume_loader_state = None
 
     # ------------------------------------------------------------------ lr
     def get_lr(self) -> float:
@@ -182,10 +186,18 @@ class Trainer:
     # ------------------------------------------------------------------ fit
     def fit(self, x, y, epochs: int = 1, batch_size: int = 128, validation_data=None, callbacks=None,
             augment: bool = False, packed_size: int | None = None, verbose: int = 1, shuffle: bool = True,
-            seed: int = 0) -> History:
+            seed: int = 0, initial_epoch: int = 0) -> History:
+        """Train epochs ``initial_epoch`` .. ``epochs - 1`` (Keras semantics).  After
+        :meth:`resume` from a checkpoint written at an epoch end, ``initial_epoch`` = the
+        checkpoint's epoch count continues the run bit-for-bit (same shuffle order, augment
+        draws, dropout masks) -- the loader's generator comes from the checkpoint."""
         callbacks: list[Callback] = list(callbacks or [])
         loader = DeviceLoader(x, y, batch_size, self.device, shuffle=shuffle, augment=augment,
                               packed_size=packed_size, rank=self.rank, world=self.world, seed=seed)
+        if self._resume_loader_state is not None:
+            loader.gen.set_state(self._resume_loader_state.to(torch.uint8))
+            self._resume_loader_state = None
+        self._loader = loader
         val_loader = None
         if validation_data is not None:   # uploaded once, not once per epoch
             val_loader = DeviceLoader(*validation_data, batch_size, self.device, shuffle=False,
@@ -195,7 +207,7 @@ class Trainer:
             cb.on_train_begin(self)
         t_start = time.time()
         try:
-            for epoch in range(epochs):
+            for epoch in range(initial_epoch, epochs):
                 for cb in callbacks:
                     cb.on_epoch_begin(self, epoch)
                 self.model.train()
@@ -226,6 +238,7 @@ class Trainer:
                 if not math.isfinite(logs["loss"]):
                     raise TrainingFailed("non-finite training loss")
                 self.history.log(epoch, logs)
+                self.epochs_done = epoch + 1
                 default_log().emit("epoch", epoch=epoch, world=self.world, **logs)
                 if verbose and self.rank == 0:
                     msg = " ".join(f"{k}={v:.4g}" for k, v in logs.items())
@@ -318,8 +331,39 @@ class Trainer:
         return torch.cat(out).numpy() if out else np.zeros((0,))
 
     # ------------------------------------------------------------------ io
-    def save(self, path, include_optimizer: bool = True):
+    def save(self, path, include_optimizer: bool = True, include_rng: bool = True):
+        """Weights (+ optimizer moments and step count) (+ every random generator's state and
+        the epoch counter: a :meth:`resume` continues the run bit-for-bit)."""
         meta = dict(self.meta)
         meta["history"] = self.history.history
         meta["optimizer_name"] = self.optimizer_name
-        return save_checkpoint(path, self.model, meta, self.opt if include_optimizer else None)
+        meta["train_state"] = {"epochs_done": self.epochs_done, "step": int(getattr(self.opt, "t", 0)),
+                               "history_epochs": list(self.history.epoch)}
+        rng = None
+        if include_rng:
+            gens = {"loader": self._loader.gen} if self._loader is not None else {}
+            rng = capture_rng(gens)
+        return save_checkpoint(path, self.model, meta, self.opt if include_optimizer else None, rng=rng)
+
+    def resume(self, path) -> int:
+        """Load weights, optimizer state, history and random-generator states written by
+        :meth:`save`; returns the number of completed epochs (pass it to ``fit`` as
+        ``initial_epoch``)."""
+        meta, state, opt_state = read_checkpoint(path)
+        self.model.load_state_dict(state)
+        self.flat.check_bound()
+        if opt_state:
+            ometa = meta.get("optimizer") or {}
+            self.opt.load_state_dict({**ometa, **{k: v.to(self.device) for k, v in opt_state.items()}})
+        ts = meta.get("train_state") or {}
+        self.epochs_done = int(ts.get("epochs_done", 0))
+        self.history = History()
+        hist = meta.get("history") or {}
+        self.history.history = {k: list(v) for k, v in hist.items()}
+        self.history.epoch = list(ts.get("history_epochs", []))
+        tensors, rmeta = read_rng(path)
+        if tensors or rmeta:
+            restore_rng(tensors, rmeta)
+            self._resume_loader_state = tensors.get("gen.loader")
+        self._graph = None                             # replays captured the old buffers' contents
+        return self.epochs_done

@@ -117,3 +117,34 @@ def test_seg_head_bn_in_pointwise_matches_unfused(monkeypatch, S):
     for n in g0:
         err = (g0[n] - g1[n]).abs().max().item() / max(g0[n].abs().max().item(), 1e-6)
         assert err < 2e-2, f"{n}: rel err {err:.2e}"
+
+
+def test_forked_bn_output_falls_back(monkeypatch):
+    """A BN output with two consumers (a conv and an identity branch): autograd adds the
+    identity branch's gradient into the conv's dx, so the dgrad-epilogue slab (conv branch
+    only) must not be used -- the gradients must equal the unfused path."""
+    from torch import nn
+
+    from featurenet_amd.models.layers import Conv
+
+    class Fork(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = Conv(32, 32, 3, 1, "valid", bn=True, act="relu", init="he")
+            self.b = Conv(32, 32, 3, 1, "same", bn=False, act=None, init="he")
+
+        def forward(self, x):
+            z = self.a(x)
+            return self.b(z) + z                # two consumers of the BN+ReLU output
+
+    monkeypatch.setenv("FN_CONV_TILE", "2")
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    model = Fork().to(dev)
+    x = torch.randn(2, 18, 18, 18, 32, device=dev).to(torch.bfloat16)
+    g0 = _grads(model, x, False, monkeypatch)
+    g1 = _grads(model, x, True, monkeypatch)
+    for n in g0:
+        a, b = g0[n], g1[n]
+        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
+        assert err < 2e-3, f"{n}: rel err {err:.2e}"

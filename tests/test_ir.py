@@ -43,11 +43,43 @@ def test_templates_compile(name, shape, ncls):
     assert net.flops_per_sample > 0
 
 
-def test_lenet5_param_count_pinned():
-    # Regression pin of our compile semantics for the reference LeNet-5 template on
-    # MNIST (parity with the TF build is unpinned: TF is not importable here).
-    net = compile_model(parse_feature_model("lenet5", name="lenet5"), (28, 28, 1), 10)
-    assert net.nb_params == 212902
+def _keras_lenet5_params(h: int, w: int, c: int, ncls: int) -> int:
+    """Keras parameter count of the reference ``lenet5_blocks()`` template (model/leNet.py:7-40),
+    derived by hand from the reference build semantics -- TF/Keras is not importable here, so
+    this arithmetic IS the parity oracle:
+
+    * block1 (stride 1x1, features 600 -> multiplier 6.0, model/block.py:31-35):
+      cell11 ConvolutionInput 5x5 'same' tanh with no own feature count, so the block's
+      multiplier applies: features = in_channels * 6 clamped to [6, 2048] (model/input.py:30-40)
+      -> Conv2D(6c, 5x5): 25*c*6c + 6c.  cell12 AveragePooling 2x2 -- its 'valid' padding is
+      not an accepted value and becomes 'same' (model/input.py:201-211), stride 1x1 from the
+      block -> h x w x 6c, no parameters.  cell12 reads cell11's output: the default OutCell
+      (index 1, model/output.py:81-95) is pushed on the stack front and counted down to 0
+      after cell11 (model/block.py:58-60, model/cell.py:49,76-82).
+    * block2 (stride 1x1, no multiplier): Conv2D(12, 5x5 'same') on 6c channels: 25*6c*12 + 12.
+    * block22 (stride 2x2): AveragePooling 2x2 'same' stride 2 -> ceil(h/2) x ceil(w/2).
+    * block3: ConvolutionInput 5x5 'valid' -> 'same' (model/input.py:264-275): Conv2D(120):
+      25*12*120 + 120.
+    * block4: DenseInput(84, tanh) on the 4-D tensor (last axis, model/input.py:190): 120*84 + 84.
+    * head: Flatten + Dense(ncls) (model/keras_model.py:118-124): ceil(h/2)*ceil(w/2)*84*ncls + ncls.
+    """
+    f1 = 6 * c
+    conv1 = 25 * c * f1 + f1
+    conv2 = 25 * f1 * 12 + 12
+    conv3 = 25 * 12 * 120 + 120
+    dense = 120 * 84 + 84
+    head = -(-h // 2) * -(-w // 2) * 84 * ncls + ncls
+    return conv1 + conv2 + conv3 + dense + head
+
+
+@pytest.mark.parametrize("shape,ncls", [((28, 28, 1), 10), ((32, 32, 3), 10), ((32, 32, 3), 100)])
+def test_lenet5_param_count_matches_hand_derived_keras(shape, ncls):
+    net = compile_model(parse_feature_model("lenet5", name="lenet5"), shape, ncls)
+    expected = _keras_lenet5_params(*shape, ncls)
+    assert net.nb_params == expected
+    if shape == (28, 28, 1):
+        # 156 + 1812 + 36120 + 10164 + 164650
+        assert expected == 212902
 
 
 def test_featurenet3d_template_compiles_3d():

@@ -848,3 +848,40 @@ def test_featurenet3d_training_trajectory_matches_fp32():
     # to the larger of the two losses (a round-1 blow-up would miss it by orders of magnitude)
     for a, b in zip(gpu, cpu):
         assert abs(a - b) < 0.1 + 0.25 * max(a, b), (gpu, cpu)
+
+
+@pytest.mark.parametrize("k,padding,extra", [((1, 3, 3), "valid", (0, 1, 1)), ((1, 3, 3), "valid", (0, 2, 2)),
+                                             ((1, 3, 3), "same", (0, 1, 1)), ((1, 5, 1), "same", (0, 2, 0)),
+                                             ((3, 3, 3), "valid", (0, 1, 2))])
+@pytest.mark.parametrize("C,K", [(16, 32), (6, 12)])
+def test_folded_zero_padding_matches_explicit_pad(k, padding, extra, C, K):
+    """A ZeroPadding folded into the next conv (ConvSpec extra pads, ir/compile.py fold_pads)
+    gives the same forward, dx and dW on the native kernels as the explicit pad followed by
+    the conv (every extra pad here is one the fold rule accepts: total pad <= K - 1)."""
+    _native_loaded()
+    from featurenet_amd.ir.compile import _pad_foldable
+    from featurenet_amd.models.layers import Conv
+    from featurenet_amd.ops.conv import ConvFn
+
+    assert _pad_foldable(Conv(C, K, k, 1, padding), extra)
+    torch.manual_seed(5)
+    x = torch.randn(2, 6, 13, 14, C, device="cuda").to(torch.bfloat16)
+    ed, eh, ew = extra
+    xp = torch.nn.functional.pad(x.float(), (0, 0, ew, ew, eh, eh, ed, ed)).to(torch.bfloat16)
+    s_fold = ConvSpec.make(tuple(x.shape), K, k, 1, padding, extra=extra)
+    s_pad = ConvSpec.make(tuple(xp.shape), K, k, 1, padding)
+    w = (torch.randn(K, *k, C, device="cuda") * 0.05).to(torch.bfloat16).float()
+    xa = x.clone().requires_grad_(True)
+    wa = w.clone().requires_grad_(True)
+    ya, _ = ConvFn.apply(xa, wa, None, s_fold, 0, False)
+    xb = xp.clone().requires_grad_(True)
+    wb = w.clone().requires_grad_(True)
+    yb, _ = ConvFn.apply(xb, wb, None, s_pad, 0, False)
+    assert ya.shape == yb.shape
+    close(ya, yb)
+    g = torch.randn_like(yb.float()).to(torch.bfloat16)
+    ya.backward(g)
+    yb.backward(g)
+    dx_ref = xb.grad.float()[:, ed:ed + x.shape[1], eh:eh + x.shape[2], ew:ew + x.shape[3]]
+    close(xa.grad, dx_ref)
+    close(wa.grad, wb.grad)

@@ -208,3 +208,51 @@ def test_s2d_padded_strided_conv_equals_direct(shape, k, s, pad):
     x2 = C.s2d_input(x, f, spec2, (spec.pd, spec.ph, spec.pw))
     y2 = R.conv(x2, C.s2d_weight(w, f, spec, spec2), None, spec2)
     torch.testing.assert_close(y2, R.conv(x, w, None, spec), rtol=1e-4, atol=1e-4)
+
+
+def test_pad_fold_rule_keeps_pads_beyond_the_kernel():
+    """ZeroPadding folds into the next conv only while every total pad stays <= K - 1
+    (the stride-1 dgrad runs with leading pads K - 1 - lo): a 1x1 conv after any padding,
+    and a 'same' 3x3 after a fillSize-2 padding, keep the explicit pad op."""
+    from featurenet_amd.ir.compile import _pad_foldable
+    from featurenet_amd.models.layers import Conv
+
+    assert _pad_foldable(Conv(8, 8, (1, 3, 3), 1, "valid"), (0, 1, 1))
+    assert _pad_foldable(Conv(8, 8, (1, 3, 3), 1, "valid"), (0, 2, 2))
+    assert _pad_foldable(Conv(8, 8, (1, 3, 3), 1, "same"), (0, 1, 1))
+    assert not _pad_foldable(Conv(8, 8, (1, 3, 3), 1, "same"), (0, 2, 2))
+    assert not _pad_foldable(Conv(8, 8, (1, 1, 1), 1, "valid"), (0, 1, 1))
+    assert not _pad_foldable(Conv(8, 8, (1, 3, 3), 2, "valid"), (0, 1, 1))
+    assert _pad_foldable(Conv(8, 8, (1, 5, 1), 1, "same"), (0, 2, 0))
+    assert not _pad_foldable(Conv(8, 8, (1, 5, 1), 1, "same"), (0, 2, 1))
+
+
+def test_flat_params_rebuild_releases_old_hooks():
+    """A FlatParams built again on the same module supersedes the old one: the old one's
+    hooks are removed (no pile-up, no reference keeping its buffers alive) and gradients
+    land in the new flat buffer only."""
+    import gc
+    import weakref
+
+    import torch
+    from torch import nn
+
+    from featurenet_amd.training.flat import FlatParams
+
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(4, 3), nn.Linear(3, 2))
+    f1 = FlatParams(m)
+    ref1 = weakref.ref(f1)
+    f2 = FlatParams(m)
+    del f1
+    gc.collect()
+    assert ref1() is None, "the superseded FlatParams is still referenced (hooks left behind)"
+    hooks = sum(len(p._post_accumulate_grad_hooks or {}) for p in m.parameters())
+    assert hooks == len(list(m.parameters()))
+    f2.zero_grad()
+    x = torch.randn(5, 4)
+    m(x).sum().backward()
+    for p, off, n in f2.slices:
+        assert p.grad.data_ptr() == f2.grad[off:off + n].data_ptr()
+        assert torch.equal(f2.grad[off:off + n].view(p.shape), p.grad)
+    assert f2.grad.abs().sum() > 0

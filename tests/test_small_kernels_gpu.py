@@ -33,3 +33,22 @@ def test_softmax_xent_backward_scales_by_dloss(scale, dtype):
     (torch.nn.functional.cross_entropy(ref_logits, labels) * scale).backward()
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
     assert torch.allclose(logits.grad.float(), ref_logits.grad, rtol=tol, atol=tol * 1e-2 * scale)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_softmax_xent_second_backward_with_scaled_dloss(dtype):
+    """retain_graph: a second backward after a first one whose upstream gradient was not 1
+    must not see the first call's scale (the first backward scales d(logits) in place)."""
+    from featurenet_amd.ops import softmax_xent
+
+    torch.manual_seed(2)
+    logits = torch.randn(300, 24, device="cuda").to(dtype).requires_grad_(True)
+    labels = torch.randint(0, 24, (300,), device="cuda")
+    loss = softmax_xent(logits, labels)
+    g1, = torch.autograd.grad(loss * 2.0, logits, retain_graph=True)
+    g2, = torch.autograd.grad(loss * 3.0, logits)
+    ref_logits = logits.detach().float().requires_grad_(True)
+    base, = torch.autograd.grad(torch.nn.functional.cross_entropy(ref_logits, labels), ref_logits)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert torch.allclose(g1.float(), 2.0 * base, rtol=tol, atol=tol * 2e-2)
+    assert torch.allclose(g2.float(), 3.0 * base, rtol=tol, atol=tol * 3e-2)

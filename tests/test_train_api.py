@@ -182,3 +182,56 @@ def test_fit_recalibrates_before_validation():
     tr.fit(ds.x_train, ds.y_train, epochs=2, batch_size=8, validation_data=(ds.x_test, ds.y_test),
            packed_size=32, verbose=0)
     assert len(calls) == 2 and tr._bn_fresh
+
+
+def test_resume_from_checkpoint_is_bit_identical(tmp_path):
+    """Checkpoint at an epoch end = weights + Adam moments/step + every random generator
+    (torch, numpy, python, the loader's shuffle generator).  A fresh trainer resumed from it
+    reproduces the remaining epochs' losses bit-for-bit (dropout masks and shuffle order
+    included) -- SURVEY 5.4; reference best-checkpoint reload helpers.py:88-97,169-170."""
+    import random
+
+    import numpy as np
+    import torch
+    from torch import nn
+
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+    from featurenet_amd.ops.elementwise import dropout
+    from featurenet_amd.training.callbacks import Callback
+    from featurenet_amd.training.trainer import Trainer
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.body = FeatureNet3D(FeatureNet3DConfig.tiny())
+
+        def forward(self, x):
+            f = self.body.features(x).reshape(x.shape[0], -1)
+            f = dropout(f, 0.3, self.training)          # torch's CPU generator on the CPU path
+            return self.body.fc2(self.body.fc1(f), out_fp32=True)
+
+    rs = np.random.RandomState(0)
+    x = (rs.rand(48, 16, 16, 16) < 0.3).astype(np.float32)
+    y = rs.randint(0, 2, 48).astype(np.int64)
+
+    class SaveAt(Callback):
+        def on_epoch_end(self, trainer, epoch, logs):
+            if epoch == 1:
+                trainer.save(tmp_path / "mid.fnk")
+
+    torch.manual_seed(0)
+    tr = Trainer(Net(), device="cpu", precise_bn=0)
+    h = tr.fit(x, y, epochs=4, batch_size=8, callbacks=[SaveAt()], verbose=0, seed=3)
+    full = h.history["loss"]
+
+    torch.manual_seed(123)                              # different init: everything must come from the file
+    random.seed(99)
+    np.random.seed(7)
+    tr2 = Trainer(Net(), device="cpu", precise_bn=0)
+    done = tr2.resume(tmp_path / "mid.fnk")
+    assert done == 2 and tr2.opt.t == tr.opt.t // 2
+    h2 = tr2.fit(x, y, epochs=4, batch_size=8, verbose=0, seed=3, initial_epoch=done)
+    assert h2.history["loss"][:2] == full[:2]          # the history came back with the weights
+    assert h2.history["loss"][2:] == full[2:], (h2.history["loss"], full)
+    for a, b in zip(tr.model.parameters(), tr2.model.parameters()):
+        assert torch.equal(a, b)
