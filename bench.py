@@ -230,7 +230,12 @@ def main():
     for i in range(args.warmup):
         step(i)
     sync()
+    if args.impl == "native" and dist.is_initialized():
+        from featurenet_amd.ops import tuning
+
+        tuning.sync_from_rank0()      # every rank runs rank 0's per-shape kernels (deterministic table)
     graph_used = False
+    graph_fallback = False
     if graph_on:
         # capture one step on static input buffers (the eager warmup above already ran the
         # per-shape kernel selection); every timed step = copy the batch in + one replay
@@ -252,6 +257,7 @@ def main():
             f = torch.tensor([1.0 if ok else 0.0], device=dev if backend == "nccl" else "cpu")
             dist.all_reduce(f, op=dist.ReduceOp.MIN)
             ok = bool(f.item() > 0.5)
+        graph_fallback = not ok
         if ok:
             graph_used = True
 
@@ -268,10 +274,14 @@ def main():
         loss = step(args.warmup + i)
     sync()
     elapsed = time.perf_counter() - t0
+    rank_ms = None
     if dist.is_initialized():
-        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        tdev = dev if backend == "nccl" else "cpu"
+        ts = [torch.zeros(1, device=tdev, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(ts, torch.tensor([elapsed], device=tdev, dtype=torch.float64))
+        per = [float(t.item()) for t in ts]
+        elapsed = max(per)                     # the job's time is the slowest rank's
+        rank_ms = [round(v / max(args.steps, 1) * 1e3, 3) for v in per]
     # communication diagnostics, measured AFTER the timed region: the bucketed
     # all-reduce of the whole gradient on its own (what the overlap has to hide)
     allreduce_ms = None
@@ -312,6 +322,7 @@ def main():
                 "impl": args.impl,
                 "optimizer": "adam", "graph": graph_used,
             },
+            "graph_fallback": graph_fallback,
             "final_loss": None if loss is None else round(float(loss.detach()), 4),
         }
         out["dist"] = {
@@ -321,6 +332,8 @@ def main():
             "bucket_mb": args.bucket_mb,
             "allreduce_ms": None if allreduce_ms is None else round(allreduce_ms, 3),
             "forced_single_rank": bool(args.force_allreduce and world == 1),
+            "rank_ms_per_step": rank_ms,
+            "rank_spread_pct": None if not rank_ms else round(100.0 * (max(rank_ms) - min(rank_ms)) / max(rank_ms), 2),
         }
         if flops:
             out["model_tflops_per_s"] = round(flops * value / 1e12, 2)

@@ -367,42 +367,22 @@ def dgrad_plan(spec):
 
 
 # ---------------------------------------------------------------------------
-# kernel selection: the big-tile kernel vs conv_halo, timed once per shape
+# kernel selection: the big-tile kernel vs conv_halo (deterministic, ops/tuning.py)
 # ---------------------------------------------------------------------------
-_CHOICE: dict = {}
-
-
-def _time_ms(fn, reps: int = 3) -> float:
-    fn()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
-        fn()
-    b.record()
-    b.synchronize()
-    return a.elapsed_time(b) / reps
-
-
 def choose(kind: str, spec, run_tile, run_other) -> bool:
     """True when the tile kernel should run ``kind`` ('fwd' / 'dgrad') of ``spec``.
 
-    ``FN_CONV_TILE`` = 1 (default) picks per shape by timing both kernels once (a few
-    launches on the current stream, outside any graph capture; the first call of a
-    shape during capture takes the tile kernel), 2 forces the tile kernel, 0 disables it."""
+    ``FN_CONV_TILE`` = 2 forces the tile kernel, 0 disables it; otherwise (default) the
+    deterministic per-shape selection of :mod:`.tuning` decides (committed table, then the
+    rule "tile whenever it plans"; ``FN_KERNEL_SELECT=autotune`` times unseen shapes)."""
     mode = os.environ.get("FN_CONV_TILE", "1")
     if mode == "0":
         return False
     if mode == "2":
         return True
-    key = (kind, spec)
-    c = _CHOICE.get(key)
-    if c is None:
-        if torch.cuda.is_current_stream_capturing():
-            return True
-        c = _time_ms(run_tile) <= _time_ms(run_other)
-        with _LOCK:
-            _CHOICE[key] = c
-    return c
+    from . import tuning
+
+    return tuning.select(kind, spec, run_tile, run_other)
 
 
 # ---------------------------------------------------------------------------

@@ -53,7 +53,8 @@ class WPlan:
 
 
 def mode() -> str:
-    """FN_WTILE: 1 (default) = per-shape timed choice vs conv_halo wgrad, 2 = always, 0 = off."""
+    """FN_WTILE: 1 (default) = deterministic per-shape choice vs conv_halo wgrad (ops/tuning.py),
+    2 = always, 0 = off."""
     return os.environ.get("FN_WTILE", "1")
 
 
@@ -238,21 +239,11 @@ def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) ->
     return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
 
 
-_CHOICE: dict = {}
-
-
 def choose(spec, run_wtile, run_halo) -> bool:
     """True when this kernel should run the weight gradient of ``spec``: FN_WTILE=2 always,
-    1 (default) by timing both kernels once per shape (outside graph capture; the first
-    call of a shape during capture takes this kernel)."""
+    otherwise the deterministic per-shape selection of :mod:`.tuning`."""
     if mode() == "2":
         return True
-    c = _CHOICE.get(spec)
-    if c is None:
-        if torch.cuda.is_current_stream_capturing():
-            return True
-        from .conv_tile import _time_ms
-        c = _time_ms(run_wtile) <= _time_ms(run_halo)
-        with _LOCK:
-            _CHOICE[spec] = c
-    return c
+    from . import tuning
+
+    return tuning.select("wgrad", spec, run_wtile, run_halo)

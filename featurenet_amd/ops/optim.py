@@ -31,20 +31,29 @@ class FlatAdam:
         self.shadow = shadow
         self.t = 0
         self._dev = None     # (hp, t) device state of the graph-capturable form
+        self._gscale = 1.0   # gradient scale of the device state (1/world under data parallelism)
 
     # ------------------------------------------------------------ graph mode
-    def enable_device_state(self) -> None:
-        """Keep lr / betas / step on the device so a captured step replays correctly."""
+    def enable_device_state(self, grad_scale: float | None = None) -> None:
+        """Keep lr / betas / step / gradient scale on the device so a captured step replays
+        correctly."""
+        if grad_scale is not None:
+            self._gscale = float(grad_scale)
         if self._dev is None:
-            hp = torch.tensor([self.lr, self.b1, self.b2, self.eps, self.wd, 1.0], dtype=torch.float32,
+            hp = torch.tensor([self.lr, self.b1, self.b2, self.eps, self.wd, self._gscale], dtype=torch.float32,
                               device=self.p.device)
             t = torch.tensor([self.t], dtype=torch.int32, device=self.p.device)
             self._dev = (hp, t)
+        else:
+            self.sync_device_state()
 
-    def sync_device_state(self, grad_scale: float = 1.0) -> None:
-        """Push host-side hyper-parameter changes (e.g. an lr callback) to the device copy."""
+    def sync_device_state(self, grad_scale: float | None = None) -> None:
+        """Push host-side hyper-parameter changes (e.g. an lr callback) to the device copy
+        (``grad_scale`` None keeps the current one)."""
+        if grad_scale is not None:
+            self._gscale = float(grad_scale)
         if self._dev is not None:
-            self._dev[0].copy_(torch.tensor([self.lr, self.b1, self.b2, self.eps, self.wd, grad_scale]))
+            self._dev[0].copy_(torch.tensor([self.lr, self.b1, self.b2, self.eps, self.wd, self._gscale]))
 
     def step_device(self) -> None:
         """One Adam step entirely driven by device state (safe inside hipGraph capture)."""
@@ -55,6 +64,8 @@ class FlatAdam:
 
     def step(self, grad_scale: float = 1.0) -> None:
         if self._dev is not None and _native.use_native(self.p):
+            if grad_scale != self._gscale:           # (eager steps only: a small host -> device copy)
+                self.sync_device_state(grad_scale)
             self.t += 1
             self.step_device()
             return

@@ -20,9 +20,11 @@ serialises behind the last layer's backward.  Default cap 32 MiB.  A bucket
 is closed BEFORE a tensor that would push it past the cap, and any tensor of
 at least half the cap gets a bucket of its own: FeatureNet-3D's 64000x128 FC1
 weight gradient (32.8 MB, produced by the very first backward GEMM) is
-therefore reduced alone while the whole conv stack is still in backward,
-and the conv gradients (~1 MB) form the tail bucket.  HBM is never the
-constraint (288 GB per GPU).
+therefore reduced alone while the whole conv stack is still in backward.
+The tail -- the gradients backward produces last -- is cut from the end into
+buckets of 0.25, 0.5, 1, ... MiB: conv4+conv3, conv2 and the stem reduce
+separately, conv2's while the stem's weight gradient still runs, so only the
+stem's tiny bucket is exposed.  HBM is never the constraint (288 GB per GPU).
 
 Failure handling: the process group is created with an
 explicit timeout (``FN_PG_TIMEOUT`` seconds, default 300) and, on RCCL, with
@@ -78,13 +80,32 @@ def init_from_env(backend: str | None = None, force: bool = False,
     return rank, world, local
 
 
-def plan_buckets(sizes: list[int], cap: int) -> list[list[int]]:
+def plan_buckets(sizes: list[int], cap: int, tail_cap: int | None = None) -> list[list[int]]:
     """Group consecutive tensors (element counts ``sizes``) into buckets of at most ``cap`` elements.
 
     A tensor of at least ``cap // 2`` elements is a bucket of its own; otherwise
     the open bucket is closed before a tensor that would push it past ``cap``.
+    ``tail_cap``: the LAST buckets (the gradients backward produces last, whose
+    all-reduce nothing can hide) are cut from the end with caps ``tail_cap``,
+    ``2 tail_cap``, ``4 tail_cap`` ... up to ``cap``, so the exposed final collective
+    is small and each earlier one overlaps the remaining backward.
     Returns lists of tensor indices, in order.
     """
+    if tail_cap and tail_cap < cap and sizes:
+        tail: list[list[int]] = []
+        c, i = tail_cap, len(sizes) - 1
+        while i >= 0 and c < cap:
+            cur, size = [], 0
+            while i >= 0 and sizes[i] < cap // 2 and (not cur or size + sizes[i] <= c):
+                cur.insert(0, i)
+                size += sizes[i]
+                i -= 1
+            if not cur:
+                break
+            tail.insert(0, cur)
+            c *= 2
+        head = plan_buckets(sizes[:i + 1], cap) if i >= 0 else []
+        return head + tail
     out: list[list[int]] = []
     cur: list[int] = []
     size = 0
@@ -107,7 +128,7 @@ def plan_buckets(sizes: list[int], cap: int) -> list[list[int]]:
 
 class GradBucketer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 32.0, overlap: bool = True,
-                 force: bool = False):
+                 force: bool = False, tail_mb: float | None = 0.25):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -121,7 +142,8 @@ class GradBucketer:
         self.members: list[list] = []
         self.param_bucket: dict[int, int] = {}
         # flat slices are contiguous in flat order: a bucket spans first offset .. last end
-        for idx in plan_buckets([n for _, _, n in flat.slices], self.cap):
+        tail = max(1, int(tail_mb * 1024 * 1024 / 4)) if tail_mb else None
+        for idx in plan_buckets([n for _, _, n in flat.slices], self.cap, tail):
             ps = [flat.slices[i] for i in idx]
             s = ps[0][1]
             e = ps[-1][1] + ps[-1][2]

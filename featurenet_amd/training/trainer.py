@@ -102,11 +102,15 @@ class Trainer:
         self._bn_fresh = False
         self.meta = dict(meta or {})
         self.history = History()
-        # hipGraph capture of the whole training step (forward + backward + Adam):
-        # NAS candidates on 28x28 / 32x32 inputs are launch-bound, one replay
-        # replaces ~100 kernel launches.  Single process, Adam, no dropout.
-        self.graph_mode = bool(graph) and self.device.type == "cuda" and self.world == 1 and \
+        # hipGraph capture of the whole training step (forward + backward + the bucketed
+        # RCCL all-reduces issued from the gradient hooks + Adam): the same step bench.py
+        # times.  NAS candidates on 28x28 / 32x32 inputs are launch-bound, one replay
+        # replaces ~100 kernel launches.  Adam, no dropout; one process or RCCL ranks (a
+        # rank whose capture fails makes every rank fall back to eager steps together).
+        dist_ok = self.world == 1 or (dist.is_initialized() and dist.get_backend() == "nccl")
+        self.graph_mode = bool(graph) and self.device.type == "cuda" and dist_ok and \
             optimizer == "adam" and not _has_dropout(self.model)
+        self.graph_fallback = False
         self._graph = None
         self._gkey = None
         self._gwarm = 0
@@ -122,7 +126,7 @@ class Trainer:
     def set_lr(self, lr: float) -> None:
         self.opt.lr = float(lr)
         if self.graph_mode:
-            self.opt.sync_device_state()
+            self.opt.sync_device_state()        # (keeps the 1/world gradient scale)
 
     # ------------------------------------------------------------------ steps
     def _prep(self, xb: torch.Tensor) -> torch.Tensor:
@@ -157,20 +161,39 @@ class Trainer:
             self._graph.replay()
             self.opt.t += 1
             return self._gloss, self._gcorr
-        self.opt.enable_device_state()
+        scale = 1.0 / self.world if self.bucketer.active else 1.0
+        self.opt.enable_device_state(grad_scale=scale)
         if self._gwarm < 3:                            # warm caches / kernel tables before capture
             self._gwarm += 1
             return self._eager_step(xb, yb)
+        if self.world > 1:                             # identical kernels on every rank
+            from ..ops import tuning
+
+            tuning.sync_from_rank0()
         self._sx, self._sy = xb.clone(), yb.clone()
         g = torch.cuda.CUDAGraph()
         torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g):
-            self.flat.zero_grad()
-            logits = self.model(self._prep(self._sx))
-            loss, correct = softmax_xent(logits, self._sy, self.label_smoothing, with_correct=True)
-            loss.backward()
-            self.opt.step_device()
-            self._gloss, self._gcorr = loss.detach(), correct
+        ok = True
+        try:
+            with torch.cuda.graph(g):
+                self.flat.zero_grad()
+                logits = self.model(self._prep(self._sx))
+                loss, correct = softmax_xent(logits, self._sy, self.label_smoothing, with_correct=True)
+                loss.backward()
+                self.bucketer.finish()
+                self.opt.step_device()
+                self._gloss, self._gcorr = loss.detach(), correct
+        except Exception as ex:  # noqa: BLE001 - every rank falls back together (below)
+            default_log().emit("graph_capture_failed", rank=self.rank, error=str(ex))
+            self.bucketer.reset()
+            ok = False
+        if self.world > 1:
+            f = torch.tensor([1.0 if ok else 0.0], device=self.device)
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok = bool(f.item() > 0.5)
+        if not ok:
+            self.graph_mode, self.graph_fallback = False, True
+            return self._eager_step(xb, yb)
         self._graph, self._gkey = g, key
         self._graph.replay()                           # capture records only; run this batch now
         self.opt.t += 1

@@ -227,3 +227,69 @@ def test_process_group_has_explicit_timeout(monkeypatch):
     monkeypatch.setenv("FN_PG_TIMEOUT", "42")
     ddp.init_from_env("gloo")
     assert seen["backend"] == "gloo" and seen["timeout"] == timedelta(seconds=42)
+
+
+def test_tail_buckets_split_the_conv_gradients():
+    """The gradients backward produces last are cut from the end into small buckets
+    (0.25, 0.5, 1 MiB ...): FeatureNet-3D's stem, conv2 and conv3+conv4 reduce separately, so
+    conv2's all-reduce overlaps the stem's weight gradient and only the stem's is exposed."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+    from featurenet_amd.parallel.ddp import GradBucketer, plan_buckets
+    from featurenet_amd.training.flat import FlatParams
+
+    assert plan_buckets([5, 5, 40, 3, 4, 2, 1], 100, tail_cap=4) == [[0, 1], [2], [3, 4], [5, 6]]
+    assert plan_buckets([5, 5, 40, 3, 4, 2, 1], 100, tail_cap=32) == [[0, 1, 2], [3, 4, 5, 6]]
+    assert plan_buckets([5, 5, 50, 3, 4, 2, 1], 100, tail_cap=4) == [[0, 1], [2], [3, 4], [5, 6]]
+    for sizes in ([3, 7, 1, 90, 45, 2, 60, 1], [1] * 50, [49, 51, 49, 51]):
+        plan = plan_buckets(sizes, 100, tail_cap=8)
+        assert [i for b in plan for i in b] == list(range(len(sizes)))
+    m = FeatureNet3D(FeatureNet3DConfig())
+    flat = FlatParams(m)
+    b = GradBucketer(flat, bucket_mb=32.0)
+    names = {id(p): n for n, p in m.named_parameters()}
+    groups = [[names[id(p)] for p in ps] for ps in b.members]
+    assert groups[-1] == ["convs.0.beta", "convs.0.gamma", "convs.0.weight"], groups
+    assert groups[-2] == ["convs.1.beta", "convs.1.gamma", "convs.1.weight"], groups
+    assert all(n.startswith(("convs.2", "convs.3")) for n in groups[-3]), groups
+
+
+def _select_worker(rank, tmp):
+    dist.init_process_group("gloo", init_method=f"file://{tmp}/rdzv", rank=rank, world_size=WORLD)
+    try:
+        from featurenet_amd.ops import tuning
+
+        tuning._DECIDED.clear()
+        # rank 1 decided differently (e.g. an autotuned timing); rank 0's decisions win
+        tuning._DECIDED[("fwd", (1, 2, 3))] = rank == 0
+        tuning._DECIDED[("wgrad", (4, 5, 6))] = rank != 0
+        n = tuning.sync_from_rank0()
+        torch.save({"n": n, "d": sorted(tuning.decisions().items())}, f"{tmp}/s{rank}.pt")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_kernel_choices_broadcast_from_rank0(tmp_path):
+    """Every rank runs rank 0's per-shape kernel choice (identical kernels and rounding)."""
+    import pickle  # noqa: F401 - (the files below are this test's own torch.save output)
+
+    mp.start_processes(_select_worker, args=(str(tmp_path),), nprocs=WORLD, start_method="spawn")
+    s = [torch.load(tmp_path / f"s{r}.pt", weights_only=False) for r in range(WORLD)]
+    assert s[0]["d"] == s[1]["d"] == [(("fwd", (1, 2, 3)), True), (("wgrad", (4, 5, 6)), False)]
+
+
+def test_kernel_selection_is_deterministic_without_timing(monkeypatch):
+    """Default selection never times kernels: the table, then the rule (tile kernel)."""
+    from featurenet_amd.ops import tuning
+    from featurenet_amd.ops.spec import ConvSpec
+
+    monkeypatch.delenv("FN_KERNEL_SELECT", raising=False)
+    spec = ConvSpec.make((4, 11, 12, 13, 32), 32, 3)
+
+    def boom():
+        raise AssertionError("timed a kernel")
+
+    tuning._DECIDED.pop(("fwd", tuning.shape_key(spec)), None)
+    assert tuning.select("fwd", spec, boom, boom) is True
+    monkeypatch.setitem(tuning.TABLE, ("dgrad",) + tuning.shape_key(spec), False)
+    tuning._DECIDED.pop(("dgrad", tuning.shape_key(spec)), None)
+    assert tuning.select("dgrad", spec, boom, boom) is False
