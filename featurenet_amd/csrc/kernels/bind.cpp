@@ -77,6 +77,9 @@ int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                  const int*, int, int, int, int, int*, hipStream_t, const void*, const float*);
 int fn_conv_tile_workers(const int*, int, int);
+int fn_conv_tile8(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
+                  const int*, int, int, int, int, hipStream_t);
+int fn_conv_tile8_supported(int, int, int);
 int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
                     float, const int*, int, int, int, int, int*, hipStream_t);
 int fn_conv_tile_f8_supported(int, int, int);
@@ -208,6 +211,20 @@ PYBIND11_MODULE(_C, m) {
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("bny") = 0,
      py::arg("bnp") = 0);
+  m.def("conv_tile8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
+                         uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
+                         uintptr_t st, std::vector<long long> ext) {
+    need(geom, 26, "conv_tile8");
+    check_tile(geom, ext, ncol, MT, "conv_tile8");
+    fits(ext, 4, geom[19] + 10LL, "conv_tile8", "ktab");    // nks + 2 PD + 2 entries
+    chk(fn_conv_tile8(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
+                      P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
+                      act, MT, NT, S(st)),
+        "conv_tile8");
+  }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
+     py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"), py::arg("st"),
+     py::arg("ext") = std::vector<long long>());
+  m.def("conv_tile8_supported", &fn_conv_tile8_supported);
   m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
                            uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,
                            int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext) {

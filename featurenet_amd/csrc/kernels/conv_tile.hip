@@ -615,6 +615,326 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
 }
 
 // ---------------------------------------------------------------------------
+// conv_tile8: 8 MFMA waves (two per SIMD), split-K pairs, no loader wave (round 3)
+// ---------------------------------------------------------------------------
+// The same tile, halo layout, row table, k-table, packed weights and epilogue as
+// conv_tile_kernel, but every SIMD runs TWO compute waves that own the same 16*MT output
+// rows x 32 columns and split each job's k-steps between them (wave w, w + 4: even / odd
+// k-steps).  A lone wave per SIMD was issue- and latency-bound (one ds_read_b128 + one
+// address add + one wait per MFMA pair at 4 cycles per VALU instruction: the k-loop ran at
+// ~72 % of MFMA issue); two waves interleave their MFMA streams and double the VALU issue
+// rate, at the same LDS and L2 traffic per MFMA.  The halo DMA is issued by the compute
+// waves themselves, 1/8 of the rows each, by waves 0-3 at their first k-step and by waves
+// 4-7 at mid-job (the two waves of a SIMD never pause their MFMAs together).  At a tile's
+// last slice the pair exchanges half its accumulators through the just-consumed halo
+// buffer (two rounds of 32 KiB) and each wave finalises half of the rows.  Tiles are
+// assigned statically (tile b, b + W, ...), so no atomics sit on any wave's critical path.
+template <int MT, int NT, int CPP>
+__global__ __launch_bounds__(512, 1) void conv_tile8_kernel(const unsigned char* __restrict__ src,
+                                                           const uint4* __restrict__ wp,
+                                                           const int2* __restrict__ rowtab,
+                                                           const int4* __restrict__ ktab,
+                                                           const unsigned char* __restrict__ zp,
+                                                           const float* __restrict__ bias, void* __restrict__ out,
+                                                           float* __restrict__ stats, TileGeom g, int Ncol, int act) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  constexpr int PD = 4;                          // B ring depth (this wave's k-steps in flight)
+  constexpr int MH = MT / 2;                     // rows blocks each wave of a pair finalises
+  static_assert(NT == 2 && MT % 4 == 0, "32-column blocks, MT a multiple of 4");
+  const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
+  const int HP = (g.TD + g.KD - 1) * HH * HW;
+  const int PLANE = g.HPpad * 16;
+  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH, twn = (g.OW + g.TW - 1) / g.TW;
+  const int ntiles = g.N * tdn * thn * twn;
+  const int nslice = g.C / g.CS;
+  const int nks = g.nks, nkw = nks >> 1;         // k-steps per job, per wave
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rg = wave & 3, hp = wave >> 2;       // row group, k-step parity
+  const int lr = lane & 15, lg = lane >> 4;
+  const int ct0 = blockIdx.y * NT;
+  // LDS: [buffer 0][buffer 1][BN partials 8 waves x 64][k-step offsets (nks + 2PD + 2) int4][positions]
+  float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF);
+  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 8 * 64 * 4);
+  int2* s_pos = reinterpret_cast<int2*>(s_kt + (nks + 2 * PD + 2));
+  for (int i = tid; i < nks + 2 * PD + 2; i += 512) s_kt[i] = ktab[i];
+  for (int i = tid; i < 8 * 64; i += 512) s_red[i] = 0.f;
+  for (int p = tid; p < g.HPpad; p += 512) {
+    const int pc = p < HP ? p : HP - 1;
+    const int hd = pc / (HH * HW), hh = (pc / HW) % HH, hw = pc % HW;
+    s_pos[p] = make_int2(((hd * g.IH + hh) * g.IW + hw) * g.C * 2, (hd << 16) | (hh << 8) | hw);
+  }
+  int lb[MT], roff[MT], rpk[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int2 rt = rowtab[(rg * MT + mt) * 16 + lr];
+    lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;
+    const int tw = rt.y % g.TW, th = (rt.y / g.TW) % g.TH, td = rt.y / (g.TW * g.TH);
+    roff[mt] = rt.y < 0 ? -1 : (td * g.OH + th) * g.OW + tw;
+    rpk[mt] = (td << 16) | (th << 8) | tw;
+  }
+  // static schedule: job j = (tile blockIdx.x + (j / nslice) * W, slice j % nslice)
+  const int W = (int)gridDim.x;
+  const int my_tiles = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / W + 1 : 0;
+  const int njobs = my_tiles * nslice;
+  auto job_tile = [&](int j) { return (int)blockIdx.x + (j / nslice) * W; };
+
+  // 1/8 of the halo rows of job (tile, slice) into the buffer at bufoff: rows wave, wave+8, ...
+  auto dma_job = [&](int tile, int slice, int bufoff) {
+    tile = __builtin_amdgcn_readfirstlane(tile);
+    slice = __builtin_amdgcn_readfirstlane(slice);
+    bufoff = __builtin_amdgcn_readfirstlane(bufoff);
+    int t = tile;
+    const int tw = t % twn; t /= twn;
+    const int th = t % thn; t /= thn;
+    const int td = t % tdn;
+    const int n = t / tdn;
+    const int dlo = td * g.TD - g.pd, hlo = th * g.TH - g.ph, wlo = tw * g.TW - g.pw;
+    const bool interior = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID &&
+                          hlo + HH <= g.IH && wlo + HW <= g.IW;
+    const unsigned char* base = src + ((long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS) * 2;
+    const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
+    const int NR = g.HPpad >> 6;
+    if (interior) {
+      const unsigned char* obase = base + (((long long)dlo * g.IH + hlo) * g.IW + wlo) * g.C * 2;
+      for (int r0 = wave; r0 < NR; r0 += 8 * 4) {
+        int po[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) po[i] = s_pos[(min(r0 + 8 * i, NR - 1) << 6) + lane].x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = r0 + 8 * i;
+          if (r < NR) {
+#pragma unroll
+            for (int c = 0; c < CPP; ++c)
+              ct_glds16_s(obase, (unsigned)(po[i] + c * 16), dst0 + (unsigned)(c * PLANE + (r << 10)));
+          }
+        }
+      }
+    } else {
+      for (int r0 = wave; r0 < NR; r0 += 8 * 4) {
+        int e[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) e[i] = s_pos[(min(r0 + 8 * i, NR - 1) << 6) + lane].y;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = r0 + 8 * i;
+          if (r < NR) {
+            const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
+            const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                            (unsigned)gw < (unsigned)g.IW;
+            const unsigned char* gsrc = ok ? base + (long long)((gd * g.IH + gh) * g.IW + gw) * g.C * 2 : zp;
+#pragma unroll
+            for (int c = 0; c < CPP; ++c)
+              ct_glds16(ok ? gsrc + c * 16 : zp, dst0 + (unsigned)(c * PLANE + (r << 10)));
+          }
+        }
+      }
+    }
+  };
+
+  tile_lds_barrier();                            // tables visible
+  if (njobs > 0) dma_job(job_tile(0), 0, 0);
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[MT];
+  bf16x8 fb[PD][NT];
+  const int gc8 = ct0 * 16 + 8 * lg;
+  constexpr unsigned FTILE = 64u * 16u;
+  const unsigned wstep = (unsigned)g.nct * FTILE;
+  unsigned voffb[PD];                            // this wave's ring slots: every other k-step
+#pragma unroll
+  for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * 16 + (unsigned)(2 * u + hp) * wstep;
+  auto load_b = [&](const unsigned char* base, int slot) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const bf16x8*)(base + voffb[slot] + nt * FTILE);
+  };
+  auto read_a = [&](int mt, int ko) -> bf16x8 { return *(const bf16x8*)(dsm + lb[mt] + ko); };
+  auto kofs = [&](int k) -> int { return *((const int*)(s_kt + k) + lg); };
+  const int emode = (stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0);
+  // ring prologue: job 0 (slice 0), this wave's first PD k-steps
+#pragma unroll
+  for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * FTILE, u);
+  // waves 0-3 issue the next job's DMA at their first turn, waves 4-7 at mid-job
+  const int kdma = hp == 0 ? 0 : ((nkw / 2) / PD) * PD;
+  int par = 0;
+  for (int j = 0; j < njobs; ++j) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's share of job j's halo
+    tile_lds_barrier();                          // A(j): job j's halo landed, the other buffer is free
+    const int tile = job_tile(j), slice = j % nslice;
+    const bool has_next = j + 1 < njobs;
+    const int ntile = has_next ? job_tile(j + 1) : 0, nslc = has_next ? (j + 1) % nslice : 0;
+    const unsigned char* wbase = reinterpret_cast<const unsigned char*>(wp) +
+                                 ((size_t)slice * nks * g.nct + ct0) * FTILE + 2 * PD * wstep;
+    const unsigned char* wnext =
+        reinterpret_cast<const unsigned char*>(wp) + ((size_t)nslc * nks * g.nct + ct0) * FTILE;
+    {
+      const int ko = kofs(hp);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) fa[mt] = read_a(mt, ko);
+    }
+    int ko_n = kofs(hp + 2);
+    for (int ks = 0; ks < nkw; ks += PD) {       // this wave's k-steps hp + 2 (ks + u)
+      if (ks == kdma && has_next) dma_job(ntile, nslc, (par ^ 1) * g.BUF);
+      const unsigned char* wl = ks + PD >= nkw ? wnext : wbase;
+#pragma unroll
+      for (int u = 0; u < PD; ++u) {
+        const int ko = ko_n;
+        ko_n = kofs(hp + 2 * (ks + u) + 4);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0);
+          fa[mt] = read_a(mt, ko);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        load_b(wl, u);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      wbase += 2 * PD * wstep;
+    }
+    if (slice == nslice - 1) {
+      // ---- split-K reduction: the pair exchanges half its accumulators through this job's
+      // (consumed) halo buffer, in two rounds of 32 KiB; wave (rg, hp) finalises row blocks
+      // [hp * MH, hp * MH + MH)
+      float4* xch = reinterpret_cast<float4*>(dsm + par * g.BUF);
+      // rounds of 64 KiB / RQ (RQ = 2 for buffers >= 32 KiB, 4 for the 16-32 KiB halos of CS = 8)
+      auto exchange = [&](auto hpc, auto rqc) {
+        constexpr int H = decltype(hpc)::value;
+        constexpr int RQ = decltype(rqc)::value, BR = MH / RQ;   // rounds, row blocks per round
+#pragma unroll
+        for (int q = 0; q < RQ; ++q) {
+          tile_lds_barrier();                    // every wave is done reading the buffer / last round
+#pragma unroll
+          for (int i = 0; i < BR; ++i) {         // export the partner's half: blocks (1-H)*MH + q*BR + i
+            const int mt = (1 - H) * MH + q * BR + i;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+              xch[(((H * 4 + rg) * BR + i) * NT + nt) * 64 + lane] =
+                  make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]);
+          }
+          tile_lds_barrier();
+#pragma unroll
+          for (int i = 0; i < BR; ++i) {         // import mine from the partner (parity 1 - H)
+            const int mt = H * MH + q * BR + i;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+              const float4 v = xch[((((1 - H) * 4 + rg) * BR + i) * NT + nt) * 64 + lane];
+              acc[mt][nt][0] += v.x;
+              acc[mt][nt][1] += v.y;
+              acc[mt][nt][2] += v.z;
+              acc[mt][nt][3] += v.w;
+            }
+          }
+        }
+      };
+      if (g.BUF >= 32768) {
+        if (hp == 0) exchange(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
+        else exchange(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
+      } else {
+        if (hp == 0) exchange(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+        else exchange(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
+      }
+      // ---- epilogue of this wave's half: (+bias) -> bf16 -> activation -> 16-B stores (+BN sums)
+      int t = tile;
+      const int tw_i = t % twn; t /= twn;
+      const int th_i = t % thn; t /= thn;
+      const int td_i = t % tdn;
+      const int n = t / tdn;
+      const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
+      const int ld = g.OD - d0, lh = g.OH - h0, lw = g.OW - w0;
+      const bool edge = ld < g.TD || lh < g.TH || lw < g.TW;
+      const long long obase_e = ((((long long)n * g.OD + d0) * g.OH + h0) * g.OW + w0) * Ncol + gc8;
+      bf16* obase = reinterpret_cast<bf16*>(out) + obase_e;
+      auto epilogue = [&](auto hpc, auto mode) {
+        constexpr int H = decltype(hpc)::value;
+        constexpr int M = decltype(mode)::value;
+        constexpr bool RELU = (M & 2) != 0, ST = (M & 1) != 0;
+        float bias8[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) bias8[jj] = (bias && gc8 + jj < Ncol) ? bias[gc8 + jj] : 0.f;
+        float ts[8], tq[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) ts[jj] = tq[jj] = 0.f;
+#pragma unroll
+        for (int i = 0; i < MH; ++i) {
+          const int mt = H * MH + i;
+          bool ok = roff[mt] >= 0 && gc8 < Ncol;
+          if (edge) ok = ok && (rpk[mt] >> 16) < ld && ((rpk[mt] >> 8) & 255) < lh && (rpk[mt] & 255) < lw;
+          float v[8];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            v[jj] = bf16_lo(bf16x2_pack(acc[mt][jj >> 2][jj & 3] + bias8[jj], 0.f));
+            if constexpr (RELU) v[jj] = fmaxf(v[jj], 0.f);
+          }
+          if constexpr (ST) {
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+              const float x = ok ? v[jj] : 0.f;
+              ts[jj] += x;
+              tq[jj] += x * x;
+            }
+          }
+          if (ok)
+            *(uint4*)(obase + (long long)roff[mt] * Ncol) = make_uint4(
+                bf16x2_pack(v[0], v[1]), bf16x2_pack(v[2], v[3]), bf16x2_pack(v[4], v[5]), bf16x2_pack(v[6], v[7]));
+        }
+        if constexpr (ST) {
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            ts[jj] = ct_sum16(ts[jj]);
+            tq[jj] = ct_sum16(tq[jj]);
+          }
+          if (lr == 0) {                         // fixed order per wave: deterministic statistics
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+              s_red[wave * 64 + 8 * lg + jj] += ts[jj];
+              s_red[wave * 64 + 32 + 8 * lg + jj] += tq[jj];
+            }
+          }
+        }
+      };
+      auto run = [&](auto hpc) {
+        switch (emode) {
+          case 0: epilogue(hpc, std::integral_constant<int, 0>{}); break;
+          case 1: epilogue(hpc, std::integral_constant<int, 1>{}); break;
+          case 2: epilogue(hpc, std::integral_constant<int, 2>{}); break;
+          default: epilogue(hpc, std::integral_constant<int, 3>{}); break;
+        }
+      };
+      if (hp == 0) run(std::integral_constant<int, 0>{});
+      else run(std::integral_constant<int, 1>{});
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) lb[mt] += (1 - 2 * par) * g.BUF;   // the other buffer
+    par ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last job's unused ring loads
+  tile_lds_barrier();
+  if (stats && tid < NT * 16 && ct0 * 16 + tid < Ncol) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      s1 += s_red[w * 64 + tid];
+      s2 += s_red[w * 64 + 32 + tid];
+    }
+    float* row = stats + (long long)blockIdx.x * 2 * Ncol;
+    row[ct0 * 16 + tid] = s1;
+    row[Ncol + ct0 * 16 + tid] = s2;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // weight packing: conv weight [K][T][C] (fp32) -> MFMA B fragments
 // ---------------------------------------------------------------------------
 // out[((slice * nks + ks) * nct + ct) * 64 + lane][j] (8 bf16 per lane) =
@@ -888,6 +1208,63 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   CT_F8_INSTANCES(CT_F8_CASE)
 #undef CT_F8_CASE
   if (rc) return rc;
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// conv_tile8 host launcher (same geometry / tables as fn_conv_tile; the k-table has
+// nks + 2 PD + 2 entries, nks a multiple of 8, MT = 8)
+// ---------------------------------------------------------------------------
+extern "C" int fn_conv_tile8_supported(int MT, int NT, int CPP) {
+  return MT == 8 && NT == 2 && (CPP == 1 || CPP == 2 || CPP == 4);
+}
+
+static size_t tile8_lds_total(const TileGeom& g) {
+  return 2 * (size_t)g.BUF + 8 * 64 * 4 + (size_t)(g.nks + 2 * 4 + 2) * 16 + (size_t)g.HPpad * 8;
+}
+
+extern "C" int fn_conv_tile8(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
+                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
+                             int NT, hipStream_t st) {
+  const TileGeom g = parse_tile(geom);
+  if (g.CS != 8 && g.CS != 16 && g.CS != 32) return -2;
+  const int CPP = g.CS / 8;
+  if (!fn_conv_tile8_supported(MT, NT, CPP)) return -2;
+  if (g.C % g.CS || g.TD * g.TH * g.TW > 64 * MT || g.TD < 1 || g.TH < 1 || g.TW < 1) return -3;
+  const long long HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
+  const long long HP = (g.TD + g.KD - 1) * HH * HW;
+  if (g.HPpad < HP || g.HPpad % 64) return -3;
+  if (g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
+  const int T = g.KD * g.KH * g.KW;
+  const int need_ks = g.CS >= 32 ? T * (g.CS / 32) : (g.CS == 16 ? (T + 1) / 2 : (T + 3) / 4);
+  if (g.nks % 8 || g.nks < need_ks || g.nks < 16 || g.nct < (Ncol + 15) / 16) return -3;
+  for (long long r = 0; r < 64LL * MT; ++r) {
+    const unsigned long long q = (r * (unsigned long long)g.mTW) >> 32;
+    if (q != (unsigned long long)(r / g.TW) || ((q * g.mTH) >> 32) != q / g.TH) return -3;
+  }
+  if ((size_t)g.BUF < (size_t)g.HPpad * CPP * 16 || g.BUF % 1024 || g.BUF < 16384) return -3;   // (16 KiB exchange rounds)
+  const size_t lds = tile8_lds_total(g);
+  if (lds > 160 * 1024) return -4;
+  const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
+  if (!zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
+  if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;
+  dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
+#define CT8_CASE(C)                                                                                           \
+  if (CPP == C) {                                                                                             \
+    static size_t cfg = 0;                                                                                    \
+    if (lds > cfg) {                                                                                          \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_tile8_kernel<8, 2, C>,                             \
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
+      if (e != hipSuccess) return (int)e;                                                                     \
+      cfg = lds;                                                                                              \
+    }                                                                                                         \
+    hipLaunchKernelGGL((conv_tile8_kernel<8, 2, C>), grid, dim3(512), lds, st, (const unsigned char*)src,      \
+                       (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, (const unsigned char*)zp, bias, \
+                       out, stats, g, Ncol, act);                                                             \
+  }
+  CT8_CASE(1) CT8_CASE(2) CT8_CASE(4)
+#undef CT8_CASE
   FN_CHECK_LAUNCH();
   return 0;
 }

@@ -64,7 +64,7 @@ __device__ __forceinline__ bf16x8 wt_tr_pair(const unsigned char* lo, const unsi
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int MT, int NACC, int NW, int FAKE = 0>
+template <int MT, int NACC, int NW, bool C8 = false>
 __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* __restrict__ x,
                                                                 const bf16* __restrict__ dy,
                                                                 float* __restrict__ dw,   // partials
@@ -77,10 +77,7 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   constexpr int CPR = CO / 8;                    // 16-B chunks per dy row
   constexpr int R64 = 256 / (CO * 2);            // dy rows per 64 banks
   constexpr int NSW = 8 / R64;                   // swizzle classes over 8 rows
-#ifndef WT_PF
-#define WT_PF 4
-#endif
-  constexpr int PF = NACC < WT_PF ? NACC : WT_PF;   // B fragments in flight (register ring)
+  constexpr int PF = NACC < 4 ? NACC : 4;       // B fragments in flight (register ring)
   const int ROWS = g.kst * 32;
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int T = g.KD * g.KH * g.KW;
@@ -290,7 +287,6 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
     const int t = tap0 + i < T ? tap0 + i : 0;   // dead taps read tap 0 (never stored)
     const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
     toff[i] = ((kd * HH + kh) * HW + kw) * 32;
-    if constexpr (FAKE != 0) toff[i] = i * 32 * 7;   // (timing experiment: compile-time tap offsets)
   }
   const bool live = tap0 < T;
   f32x4 acc[NACC][MT];
@@ -504,8 +500,7 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
                              const void* postab, const void* zp, const int* geom, int nacc, int workers, int* sched,
                              hipStream_t st) {
   const WGeom g = parse_wgeom(geom);
-  static const int fake = [] { const char* e = getenv("FN_WTILE_FAKE"); return e ? atoi(e) : 0; }();
-  const int nw = (nacc >> 8) == 8 ? 8 + fake : 4;       // nacc | (8 << 8): the loaderless 8-wave variant
+  const int nw = (nacc >> 8) == 8 ? 8 : 4;       // nacc | (8 << 8): the loaderless 8-wave variant
   if (!fn_conv_wtile_supported(g.K, nacc)) return -2;
   nacc &= 255;
   if (g.C % 16 || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
@@ -515,7 +510,7 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
   if (g.HPpad < HP || g.HPpad % 32 || g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
   if ((long long)g.TD * g.TH * g.TW > 32LL * g.kst || g.kst < 1 || g.kst > 32) return -3;
   if (g.XB != g.HPpad * 32 || g.BUF < g.XB + g.kst * 32 * g.K * 2 || g.BUF % 1024) return -3;
-  if (g.ntg != (T + (nw & 12) * nacc - 1) / ((nw & 12) * nacc) || g.G != g.ntg * (g.C / 16) || 8 * g.G > 63) return -3;
+  if (g.ntg != (T + nw * nacc - 1) / (nw * nacc) || g.G != g.ntg * (g.C / 16) || 8 * g.G > 63) return -3;
   if ((g.kst * 32 * (g.K / 8)) % 64) return -3;
   const size_t lds = wtile_lds(g);
   if (lds > 160 * 1024) return -4;
@@ -544,11 +539,6 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
   WT_CASE(2, 16, 8)
   WT_CASE(4, 4, 8)
   WT_CASE(4, 8, 8)
-  if (g.K == 32 && nacc == 16 && nw == 9) {
-    hipFuncSetAttribute((const void*)conv_wtile_kernel<2, 16, 8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((conv_wtile_kernel<2, 16, 8, 1>), dim3(grid), dim3(512), lds, st, (const bf16*)x,
-                       (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab, (const bf16*)zp, g, sched, dbg);
-  }
 #undef WT_CASE
   FN_CHECK_LAUNCH();
   const long long n = (long long)g.K * T * g.C;

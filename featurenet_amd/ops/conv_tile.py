@@ -45,6 +45,11 @@ def enabled() -> bool:
     return os.environ.get("FN_CONV_TILE", "1") != "0"
 
 
+def nwaves() -> int:
+    """FN_CONV_TILE_NW: 8 = the split-K 8-wave kernel (conv_tile8), 4 = 4 waves + loader."""
+    return int(os.environ.get("FN_CONV_TILE_NW", "4"))
+
+
 @dataclass(frozen=True)
 class TilePlan:
     TD: int
@@ -61,6 +66,7 @@ class TilePlan:
     mHHW: int
     cost: float      # modelled cycles (per wave, summed over the jobs of one CU)
     f8: bool = False  # fp8 (e4m3) inference variant: 16-channel chunks, 128-k steps, ring depth 2
+    nw: int = 4       # 4 MFMA waves + loader (conv_tile_kernel) or 8 split-K MFMA waves (conv_tile8_kernel)
 
     @property
     def rows(self) -> int:
@@ -89,16 +95,19 @@ def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int
     """Best TilePlan for an (N, OD, OH, OW) output of a (KD, KH, KW) stride-1 conv over
     ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply
     (``f8``: the e4m3 inference variant, 32- or 64-channel slices)."""
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8)
+    nw = 4 if f8 else nwaves()
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, nw)
     if key in _PLANS:
         return _PLANS[key]
-    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8)
+    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, nw)
+    if best is None and nw == 8:                 # shapes the 8-wave kernel cannot tile: 4 waves + loader
+        best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, 4)
     with _LOCK:
         _PLANS[key] = best
     return best
 
 
-def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False):
+def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
@@ -111,13 +120,15 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False):
     workers = max(1, n_cus // ncb)
     cands = []
     cs_only = int(os.environ.get("FN_TILE_CS", "0"))
-    mt_choices = (8,) if f8 else MT_CHOICES
+    mt_choices = (8,) if (f8 or nw == 8) else MT_CHOICES
     for CS in ((64, 32) if f8 else (32, 16, 8)):
         if Csrc % CS or (cs_only and CS != cs_only) or (CS == 8 and Csrc % 16 == 0):
             continue
         CPP = CS // 16 if f8 else CS // 8
         nslice = Csrc // CS
         nks = -(-math.ceil(T / (128 // CS)) // PD) * PD if f8 else _ksteps(T, CS, PD)   # f8: 128-k steps
+        if nw == 8:                              # k-steps split over a wave pair: a multiple of 2 PD
+            nks = max(16, -(-nks // 8) * 8)
         tw_opts = sorted({OW} | {-(-OW // k) for k in range(2, 5) if -(-OW // k) >= 8})
         for TW in tw_opts:
             for TD in range(1, OD + 1):
@@ -132,7 +143,12 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False):
                     HP = (TD + KD - 1) * HH * HW
                     HPpad = -(-HP // 64) * 64
                     BUF = HPpad * CPP * 16                     # the halo (a multiple of 2 KiB)
-                    lds = 2 * BUF + 64 + RED_BYTES + (nks + PD + 2) * 16 + HPpad * 8
+                    if nw == 8:
+                        lds = 2 * BUF + 8 * 64 * 4 + (nks + 2 * PD + 2) * 16 + HPpad * 8
+                        if BUF < 16384:                 # (the split-K exchange: 16 KiB rounds)
+                            continue
+                    else:
+                        lds = 2 * BUF + 64 + RED_BYTES + (nks + PD + 2) * 16 + HPpad * 8
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
@@ -144,7 +160,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False):
                     per_job = max(mfma + fixed + epi, loader)
                     cost = math.ceil(jobs / workers) * per_job
                     cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
-                                          float(cost), f8))
+                                          float(cost), f8, nw))
     # the cheapest few, re-costed with their row tables' residual bank conflicts (a
     # fragment whose 16 rows repeat a residue mod 16 reads at half rate)
     best = None
@@ -158,7 +174,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False):
         cost = c.cost * (1.0 + 0.5 * dups / res.size)
         if best is None or cost < best.cost:
             best = TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct", "BUF",
-                                                        "mHW", "mHHW")), cost, f8)
+                                                        "mHW", "mHHW")), cost, f8, nw)
     return best
 
 
@@ -250,7 +266,7 @@ PD_F8 = 2                                        # (fp8 variant: 2 k-steps of 12
 
 
 def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
-    """int32 [nks + PD + 2, 4]: LDS byte offset of the tap that lane group lg (lanes 16lg ..
+    """int32 [nks + 2 PD + 2, 4]: LDS byte offset of the tap that lane group lg (lanes 16lg ..
     16lg+15) reads in each k-step -- one tap for all four groups (CS >= 32: the groups take
     channel chunks of it), two taps (CS = 16: groups 0,1 / 2,3) or four (CS = 8); 0 past the
     last tap (zero weights).  fp8: four taps (CS = 32) or two (CS = 64, groups 0,1 / 2,3)."""
@@ -259,7 +275,7 @@ def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
     T = KD * KH * KW
     kd, kh, kw = np.meshgrid(np.arange(KD), np.arange(KH), np.arange(KW), indexing="ij")
     toff = (((kd * HH + kh) * HW + kw) * 16).reshape(-1)
-    tab = np.zeros((p.nks + PD + 2, 4), dtype=np.int32)
+    tab = np.zeros((p.nks + 2 * PD + 2, 4), dtype=np.int32)   # (the 8-wave kernel reads 2 PD + 2 ahead)
     plane = p.HPpad * 16
     for k in range(p.nks):
         for lg in range(4):
@@ -309,6 +325,11 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
     rt = rowtab_tensor(p, kdims, src5.device)
     kt = ktab_tensor(p, kdims, src5.device)
     ext = [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4]
+    if p.nw == 8 and bny is None:
+        _native.kernels().conv_tile8(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
+                                     zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
+                                     _native.ptr(stats), geom, ncol, act, p.MT, p.NT, st, ext)
+        return
     if bny is not None:
         ext += [bny.numel(), bnp.numel()]
     _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),

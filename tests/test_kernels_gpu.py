@@ -885,3 +885,86 @@ def test_folded_zero_padding_matches_explicit_pad(k, padding, extra, C, K):
     dx_ref = xb.grad.float()[:, ed:ed + x.shape[1], eh:eh + x.shape[2], ew:ew + x.shape[3]]
     close(xa.grad, dx_ref)
     close(wa.grad, wb.grad)
+
+
+def test_featurenet3d_per_layer_oracle_64cube():
+    """Composition oracle at the production input (64^3, batch 32, train-mode BN).
+
+    One native training step; each layer is then re-run in fp32 PyTorch on the GPU path's
+    OWN bf16 input and fed the GPU path's OWN upstream gradient, so bf16 ReLU-mask flips do
+    not compound from layer to layer.  Inside a layer the reference rounds what the native
+    path rounds -- the conv weights to bf16 (the kernels read bf16 copies of the fp32
+    masters) and the pre-BN conv output to bf16 (stored bf16; the BN statistics and the
+    ReLU mask come from the stored values) -- with straight-through gradients, so the ReLU
+    masks agree and what is left is accumulation-order noise.  Every layer's output, input
+    gradient and parameter gradients must match to a relative L2 error < 2e-2 (a 20 %
+    gradient bug in any one layer fails it; the end-to-end test above only bounds the
+    composed drift)."""
+    _native_loaded()
+    from featurenet_amd.models.featurenet3d import FeatureNet3D
+    from featurenet_amd.ops import softmax_xent
+
+    torch.manual_seed(11)
+    m = FeatureNet3D().cuda().train()
+    x = (torch.rand(32, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    y = torch.randint(0, 24, (32,), device="cuda")
+    layers = list(m.convs) + [m.fc1, m.fc2]
+    rec = {}
+
+    def hook(mod, inp, out):
+        i = inp[0]
+        if i.requires_grad:
+            i.retain_grad()
+        out.retain_grad()
+        rec[mod] = (i, out)
+
+    hs = [lay.register_forward_hook(hook) for lay in layers]
+    bn_state = [(c.running_mean.clone(), c.running_var.clone()) for c in m.convs]
+    logits = m(x)
+    softmax_xent(logits, y).backward()
+    for h in hs:
+        h.remove()
+
+    def rel(a, b):
+        a, b = a.detach().float(), b.detach().float()
+        return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+    report = []
+    for li, conv in enumerate(m.convs):
+        xin, out = rec[conv]
+        xr = xin.detach().float().requires_grad_(True)
+        wr = conv.weight.detach().clone().requires_grad_(True)
+        gr = conv.gamma.detach().clone().requires_grad_(True)
+        br = conv.beta.detach().clone().requires_grad_(True)
+        cs, ps = conv.specs(tuple(xin.shape))
+
+        def bf16_st(t):                          # bf16 rounding, straight-through gradient
+            return t + (t.to(torch.bfloat16).float() - t).detach()
+
+        yr = bf16_st(ref.conv(xr, bf16_st(wr), None, cs))
+        rm, rv = bn_state[li]
+        zr = ref.batchnorm_act(yr, gr, br, rm.clone(), rv.clone(), True, conv.bn_momentum, conv.bn_eps, conv.act)
+        if ps is not None:
+            zr = ref.pool(zr, ps, conv.pool_kind)
+        report.append((f"conv{li + 1}.out", rel(out, zr)))
+        zr.backward(out.grad.float())
+        report.append((f"conv{li + 1}.dW", rel(conv.weight.grad, wr.grad)))
+        report.append((f"conv{li + 1}.dgamma", rel(conv.gamma.grad, gr.grad)))
+        report.append((f"conv{li + 1}.dbeta", rel(conv.beta.grad, br.grad)))
+        if li > 0:
+            report.append((f"conv{li + 1}.dx", rel(xin.grad, xr.grad)))
+    for name, lay in (("fc1", m.fc1), ("fc2", m.fc2)):
+        xin, out = rec[lay]
+        xr = xin.detach().float().reshape(xin.shape[0], -1).requires_grad_(True)
+        wr = lay.weight.detach().clone().requires_grad_(True)
+        br = lay.bias.detach().clone().requires_grad_(True)
+        o = torch.nn.functional.linear(xr, wr, br)
+        if name == "fc1":
+            o = torch.relu(o)
+        report.append((f"{name}.out", rel(out, o)))
+        o.backward(out.grad.float())
+        report.append((f"{name}.dW", rel(lay.weight.grad, wr.grad)))
+        report.append((f"{name}.dx", rel(xin.grad.reshape(xr.shape), xr.grad)))
+    print("\n".join(f"{n:16s} rel={r:.2e}" for n, r in report))
+    bad = [(n, r) for n, r in report if not r < 2e-2]
+    assert not bad, bad
