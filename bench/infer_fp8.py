@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=128)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--only", choices=["bf16", "fp8"], default=None, help="time one precision (profiling)")
     a = ap.parse_args()
     from featurenet_amd.inference.fp8 import quantize_model
     from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
@@ -40,6 +41,8 @@ def main():
     with torch.no_grad():
         agree = (m(x).argmax(-1) == q(x).argmax(-1)).float().mean().item()
         for name, fn in (("bf16", m), ("fp8", q)):
+            if a.only and name != a.only:
+                continue
             for _ in range(a.warmup):
                 for _ in range(nchunks):
                     fn(x)
@@ -54,7 +57,8 @@ def main():
             print(json.dumps({"metric": f"samples/sec ({a.size}^3 voxel) inference", "precision": name,
                               "value": round(res[name], 1), "unit": "samples/s", "batch": a.batch,
                               "chunk": a.chunk, "ms_per_batch": round(dt / a.steps * 1e3, 2)}), flush=True)
-    print(json.dumps({"fp8_speedup": round(res["fp8"] / res["bf16"], 3), "top1_agreement_fp8_vs_bf16": agree}))
+    if len(res) == 2:
+        print(json.dumps({"fp8_speedup": round(res["fp8"] / res["bf16"], 3), "top1_agreement_fp8_vs_bf16": agree}))
 
 
 if __name__ == "__main__":
