@@ -78,6 +78,13 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   constexpr int R64 = 256 / (CO * 2);            // dy rows per 64 banks
   constexpr int NSW = 8 / R64;                   // swizzle classes over 8 rows
   constexpr int PF = NACC < 4 ? NACC : 4;       // B fragments in flight (register ring)
+  // C8 (8-channel input, the space-to-depth stem): 16-B halo positions, and each 16-column
+  // B fragment holds TWO taps x 8 channels (columns 0-7: tap 2i, 8-15: tap 2i + 1 of the
+  // wave's range -- lanes 4q + 2, 4q + 3 of a transposed read address the second tap)
+  static_assert(!C8 || NW == 8, "the 8-channel form is loaderless");
+  constexpr int XR = C8 ? 16 : 32;               // halo bytes per position
+  constexpr int XSH = C8 ? 0 : 1;                // DMA slot -> halo position shift
+  constexpr int TPF = C8 ? 2 : 1;                // taps per B fragment
   const int ROWS = g.kst * 32;
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int T = g.KD * g.KH * g.KW;
@@ -206,34 +213,39 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
     const int dlo = d0 - g.pd, hlo = h0 - g.ph, wlo = w0 - g.pw;
     const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
     const bf16* xs = x + (long long)n * g.ID * g.IH * g.IW * g.C + slice * 16;
-    const int nx = min(g.HPpad >> 5, first + mhi * step);   // DMA instructions of the x halo (this range)
+    const int nx = min((g.HPpad * XR) >> 10, first + mhi * step);   // DMA instructions of the x halo (this range)
     const bool x_in = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID && hlo + HH <= g.IH &&
                       wlo + HW <= g.IW;
     if (dbg & 4) {                             // (timing only: no x halo DMA)
     } else if (x_in) {
       const bf16* xo = xs + ((long long)(dlo * g.IH + hlo) * g.IW + wlo) * g.C;
+      {                                          // wave-uniform (an SGPR operand of the DMA)
+        const unsigned long long a = (unsigned long long)xo;
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+        xo = (const bf16*)(((unsigned long long)hi << 32) | lo);
+      }
       for (int j0 = first + mlo * step; j0 < nx; j0 += 8 * step) {
         int o[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = s_xoff[((64 * min(j0 + i * step, nx - 1) + lane) >> 1)];
+        for (int i = 0; i < 8; ++i) o[i] = s_xoff[((64 * min(j0 + i * step, nx - 1) + lane) >> XSH)];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
           if (j0 + i * step < nx)
             if constexpr (HAS_LOADER) ct_glds16_s(xo, (unsigned)(o[i] + (lane & 1) * 16), dst0 + (unsigned)((j0 + i * step) << 10));
-            else ct_glds16_s_nc(xo, (unsigned)(o[i] + (lane & 1) * 16), dst0 + (unsigned)((j0 + i * step) << 10));
+            else ct_glds16_s_nc(xo, (unsigned)(o[i] + (C8 ? 0 : (lane & 1) * 16)), dst0 + (unsigned)((j0 + i * step) << 10));
       }
     } else {
       for (int j0 = first + mlo * step; j0 < nx; j0 += 8 * step) {
         int e[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = s_pos[((64 * min(j0 + i * step, nx - 1) + lane) >> 1)];
+        for (int i = 0; i < 8; ++i) e[i] = s_pos[((64 * min(j0 + i * step, nx - 1) + lane) >> XSH)];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           if (j0 + i * step < nx) {
             const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
             const bool ok = e[i] >= 0 && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
                             (unsigned)gw < (unsigned)g.IW;
-            const bf16* src = ok ? xs + ((long long)(gd * g.IH + gh) * g.IW + gw) * g.C + (lane & 1) * 8 : zp;
+            const bf16* src = ok ? xs + ((long long)(gd * g.IH + gh) * g.IW + gw) * g.C + (C8 ? 0 : (lane & 1) * 8) : zp;
             if constexpr (HAS_LOADER) ct_glds16(src, dst0 + (unsigned)((j0 + i * step) << 10));
             else ct_glds16_nc(src, dst0 + (unsigned)((j0 + i * step) << 10));
           }
@@ -280,13 +292,14 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
 
   // ======================= compute waves =======================
   const int G4 = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  const int tap0 = (tg * NW + wave) * NACC;
+  const int tap0 = (tg * NW + wave) * NACC * TPF;
   int toff[NACC];                                // byte offsets of this wave's taps in the halo
 #pragma unroll
   for (int i = 0; i < NACC; ++i) {
-    const int t = tap0 + i < T ? tap0 + i : 0;   // dead taps read tap 0 (never stored)
+    const int ti = tap0 + TPF * i + (C8 ? (p4 >> 1) : 0);
+    const int t = ti < T ? ti : 0;               // dead taps read tap 0 (never stored)
     const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
-    toff[i] = ((kd * HH + kh) * HW + kw) * 32;
+    toff[i] = ((kd * HH + kh) * HW + kw) * XR;
   }
   const bool live = tap0 < T;
   f32x4 acc[NACC][MT];
@@ -311,8 +324,8 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   bf16x8 ring[PF], fa[MT];
   auto rows_of = [&](int k, int& lo, int& hi) {
     const int r_lo = k * 32 + 4 * G4 + q;
-    lo = s_rows[r_lo].x + 8 * p4;
-    hi = s_rows[r_lo + 16].x + 8 * p4;
+    lo = s_rows[r_lo].x + 8 * (C8 ? (p4 & 1) : p4);
+    hi = s_rows[r_lo + 16].x + 8 * (C8 ? (p4 & 1) : p4);
   };
   auto read_b = [&](int lo, int hi, int i) -> bf16x8 { return wt_tr_pair(xb + lo + toff[i], xb + hi + toff[i]); };
   auto read_a = [&](int k, bf16x8* f) {
@@ -322,8 +335,6 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   };
   int jc = 0;                                   // job index (s_job ring slot jc % 3)
   int dnext = -1;                               // NW = 8: the tile this wave DMAs during the current job
-  // this wave's share of the next job's DMA instructions (x: j = wave + 8m, m < mx; dy alike)
-  const int mx = ((g.HPpad >> 5) - wave + NW - 1) / NW, my = (ny - wave + NW - 1) / NW;
   // issued at k-step 0 by waves 0-3 and at mid-job by waves 4-7 (the two waves of a SIMD
   // never both stop their MFMAs for the DMA burst at the same time)
   const int kdma = wave < NW / 2 ? 0 : g.kst / 2;
@@ -354,6 +365,9 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
     for (int p = 0; p < PF; ++p) ring[p] = read_b(plo, phi, p);
     return true;
   };
+  // (Measured, C8 stem: alternating two A/B register sets so every read had a whole k-step
+  // to land changed nothing -- 191 vs 192 us; with 8 MFMAs per k-step that kernel is bound
+  // by the ~12 non-MFMA instructions issued per MFMA, SQ_INSTS_* in profiles/.)
   if (start_job()) {
     while (true) {
       // this k-step's A fragments were read during the previous one (or at the job start);
@@ -398,14 +412,15 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   if (live) {
 #pragma unroll
     for (int i = 0; i < NACC; ++i) {
-      const int t = tap0 + i;
+      const int t = tap0 + TPF * i + (C8 ? ((lane & 15) >> 3) : 0);
+      const int ci = C8 ? (lane & 7) : slice * 16 + (lane & 15);
       if (t < T) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int co = mt * 16 + G4 * 4 + r;
-            part[((long long)co * T + t) * g.C + slice * 16 + (lane & 15)] = acc[i][mt][r];
+            part[((long long)co * T + t) * g.C + ci] = acc[i][mt][r];
           }
       }
     }
@@ -485,8 +500,10 @@ static size_t wtile_lds(const WGeom& g) {
 }
 
 extern "C" int fn_conv_wtile_supported(int K, int nacc) {
-  const int nw = nacc >> 8;
+  const int c8 = (nacc >> 12) & 1;
+  const int nw = (nacc >> 8) & 15;
   nacc &= 255;
+  if (c8) return nw == 8 && (K == 32 || K == 64) && nacc == 4;
   if (nw == 8) return (K == 32 && (nacc == 4 || nacc == 8 || nacc == 16)) || (K == 64 && (nacc == 4 || nacc == 8));
   return (K == 16 && nacc == 16) || (K == 32 && (nacc == 8 || nacc == 16)) || (K == 64 && nacc == 8);
 }
@@ -500,45 +517,51 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
                              const void* postab, const void* zp, const int* geom, int nacc, int workers, int* sched,
                              hipStream_t st) {
   const WGeom g = parse_wgeom(geom);
-  const int nw = (nacc >> 8) == 8 ? 8 : 4;       // nacc | (8 << 8): the loaderless 8-wave variant
+  // nacc | (8 << 8): the loaderless 8-wave variant; | (1 << 12): its 8-input-channel form
+  const bool c8 = ((nacc >> 12) & 1) != 0;
+  const int nw = ((nacc >> 8) & 15) == 8 ? 8 : 4;
   if (!fn_conv_wtile_supported(g.K, nacc)) return -2;
   nacc &= 255;
-  if (g.C % 16 || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
+  const int xr = c8 ? 16 : 32, tpf = c8 ? 2 : 1;
+  if ((c8 ? g.C != 8 : g.C % 16) || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const long long HP = (long long)(g.TD + g.KD - 1) * HH * HW;
   const int T = g.KD * g.KH * g.KW;
-  if (g.HPpad < HP || g.HPpad % 32 || g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
+  if (g.HPpad < HP || g.HPpad % (c8 ? 64 : 32) || g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
   if ((long long)g.TD * g.TH * g.TW > 32LL * g.kst || g.kst < 1 || g.kst > 32) return -3;
-  if (g.XB != g.HPpad * 32 || g.BUF < g.XB + g.kst * 32 * g.K * 2 || g.BUF % 1024) return -3;
-  if (g.ntg != (T + nw * nacc - 1) / (nw * nacc) || g.G != g.ntg * (g.C / 16) || 8 * g.G > 63) return -3;
+  if (g.XB != g.HPpad * xr || g.BUF < g.XB + g.kst * 32 * g.K * 2 || g.BUF % 1024) return -3;
+  if (g.ntg != (T + nw * nacc * tpf - 1) / (nw * nacc * tpf) || g.G != g.ntg * (c8 ? 1 : g.C / 16) || 8 * g.G > 63)
+    return -3;
   if ((g.kst * 32 * (g.K / 8)) % 64) return -3;
   const size_t lds = wtile_lds(g);
   if (lds > 160 * 1024) return -4;
   if (!sched || !zp || !part || workers < 1) return -6;
   const unsigned grid = 8u * (unsigned)g.G * (unsigned)workers;
   static const int dbg = [] { const char* e = getenv("FN_WTILE_DBG"); return e ? atoi(e) : 0; }();
-#define WT_CASE(M, A, W)                                                                                       \
-  if (g.K == M * 16 && nacc == A && nw == W) {                                                                 \
+#define WT_CASE(M, A, W, C)                                                                                    \
+  if (g.K == M * 16 && nacc == A && nw == W && c8 == C) {                                                      \
     static size_t cfg = 0;                                                                                     \
     if (lds > cfg) {                                                                                           \
-      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A, W>,                              \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A, W, C>,                           \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
       if (e != hipSuccess) return (int)e;                                                                      \
       cfg = lds;                                                                                               \
     }                                                                                                          \
-    hipLaunchKernelGGL((conv_wtile_kernel<M, A, W>), dim3(grid), dim3(wt_nthr(W)), lds, st, (const bf16*)x,    \
+    hipLaunchKernelGGL((conv_wtile_kernel<M, A, W, C>), dim3(grid), dim3(wt_nthr(W)), lds, st, (const bf16*)x, \
                        (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab, (const bf16*)zp, g, sched, \
                        dbg);                                                                                   \
   }
-  WT_CASE(1, 16, 4)
-  WT_CASE(2, 8, 4)
-  WT_CASE(2, 16, 4)
-  WT_CASE(4, 8, 4)
-  WT_CASE(2, 4, 8)
-  WT_CASE(2, 8, 8)
-  WT_CASE(2, 16, 8)
-  WT_CASE(4, 4, 8)
-  WT_CASE(4, 8, 8)
+  WT_CASE(1, 16, 4, false)
+  WT_CASE(2, 8, 4, false)
+  WT_CASE(2, 16, 4, false)
+  WT_CASE(4, 8, 4, false)
+  WT_CASE(2, 4, 8, false)
+  WT_CASE(2, 8, 8, false)
+  WT_CASE(2, 16, 8, false)
+  WT_CASE(4, 4, 8, false)
+  WT_CASE(4, 8, 8, false)
+  WT_CASE(2, 4, 8, true)
+  WT_CASE(4, 4, 8, true)
 #undef WT_CASE
   FN_CHECK_LAUNCH();
   const long long n = (long long)g.K * T * g.C;

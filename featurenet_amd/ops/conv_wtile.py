@@ -46,6 +46,12 @@ class WPlan:
     BUF: int
     cost: float
     nw: int = 4      # MFMA waves per workgroup: 4 (+ a loader wave) or 8 (no loader)
+    c8: bool = False  # 8 input channels (the space-to-depth stem): two taps per B fragment
+
+    @property
+    def xr(self) -> int:
+        """Halo bytes per position."""
+        return 16 if self.c8 else 32
 
     @property
     def rows(self) -> int:
@@ -98,13 +104,21 @@ def _plan(spec):
     K, C = spec.K, spec.C
     T = spec.KD * spec.KH * spec.KW
     nw = nwaves()
-    nacc = _nacc(K, T, nw)
-    if nacc is None and nw == 8:
-        nw, nacc = 4, _nacc(K, T)
-    if nacc is None or C % 16 or T < 2:
+    c8 = C == 8 and nw == 8 and K in (32, 64)
+    if c8:                                        # 8 waves x 4 fragments x 2 taps per workgroup
+        nacc, tpf = 4, 2
+    else:
+        tpf = 1
+        nacc = _nacc(K, T, nw)
+        if nacc is None and nw == 8:
+            nw, nacc = 4, _nacc(K, T)
+        if nacc is None or C % 16:
+            return None
+    if T < 2:
         return None
-    ntg = -(-T // (nw * nacc))
-    G = ntg * (C // 16)
+    ntg = -(-T // (nw * nacc * tpf))
+    G = ntg * (1 if c8 else C // 16)
+    xr, hq = (16, 64) if c8 else (32, 32)
     if 8 * G > 63:
         return None
     workers = max(1, N_CUS // (8 * G))
@@ -125,27 +139,30 @@ def _plan(spec):
                 HP = (TD + spec.KD - 1) * HH * HW
                 if max(TD + spec.KD - 1, HH, HW) > 255:
                     continue
-                HPpad = -(-HP // 32) * 32
-                BUF = -(-(HPpad * 32 + kst * 32 * K * 2) // 1024) * 1024
+                HPpad = -(-HP // hq) * hq
+                BUF = -(-(HPpad * xr + kst * 32 * K * 2) // 1024) * 1024
                 lds = 2 * BUF + 64 + kst * 32 * 12 + HPpad * 8        # + row / position / offset tables
                 if lds > LDS_MAX:
                     continue
                 tiles = spec.N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
                 jobs = math.ceil(math.ceil(tiles / 8) / workers)
                 mfma = kst * nacc * MT * 16 * (2 if nw == 8 else 1) + 400   # per SIMD per job
-                loader = 600 + (HPpad * 2 // 64 + kst * K // 16) * 60
+                loader = 600 + (HPpad * xr // 1024 + kst * K // 16) * 60
                 cost = jobs * max(mfma, loader) * (1.0 + 0.02 * HP / rows)   # halo re-reads (L2 traffic)
                 if best is None or cost < best.cost:
-                    best = WPlan(TD, TH, TW, HPpad, kst, nacc, ntg, G, workers, BUF, float(cost), nw)
+                    best = WPlan(TD, TH, TW, HPpad, kst, nacc, ntg, G, workers, BUF, float(cost), nw, c8)
     return best
 
 
 def tables(p: WPlan, kdims: tuple) -> tuple[np.ndarray, np.ndarray]:
     """(rowtab int32 [kst*32, 2], postab int32 [HPpad]).
 
-    rowtab: per k-row (byte offset 32*hpos of its tap-0 halo position, packed tile coords
+    rowtab: per k-row (byte offset xr*hpos of its tap-0 halo position, packed tile coords
     td<<16 | th<<8 | tw, or -1 for a dummy row), ordered so every aligned group of 8 rows
-    has 8 distinct hpos mod 8; dummies take a missing residue (a real halo position).
+    (one LDS cycle of a transposed read) touches 64 distinct banks: 32-B positions need 8
+    distinct hpos mod 8; 16-B positions (c8) are read at hpos and hpos + 1 (the tap pair
+    2i, 2i + 1 of a fragment, adjacent in kw), so a group takes 8 distinct residues mod 16
+    of one parity.  Dummies take a missing residue (a real halo position).
     postab: packed halo coords hd<<16 | hh<<8 | hw per position, -1 past the halo."""
     key = (p, tuple(kdims))
     t = _TABS.get(key)
@@ -156,28 +173,43 @@ def tables(p: WPlan, kdims: tuple) -> tuple[np.ndarray, np.ndarray]:
     td, th, tw = np.meshgrid(np.arange(p.TD), np.arange(p.TH), np.arange(p.TW), indexing="ij")
     hpos = ((td * HH + th) * HW + tw).reshape(-1)
     pk = ((td << 16) | (th << 8) | tw).reshape(-1)
-    buckets = [list(zip(hpos[hpos % 8 == r].tolist(), pk[hpos % 8 == r].tolist())) for r in range(8)]
     ngroups = p.kst * 4
     groups = [[None] * 8 for _ in range(ngroups)]
     extra = []
-    for r in range(8):
-        for i, item in enumerate(buckets[r]):
-            if i < ngroups:
-                groups[i][r] = item
-            else:
-                extra.append(item)
+    if p.c8:
+        # group gi holds residues 2s + (gi & 1) (mod 16) in slot s
+        buckets = [list(zip(hpos[hpos % 16 == r].tolist(), pk[hpos % 16 == r].tolist())) for r in range(16)]
+        for r in range(16):
+            par, s = r & 1, r >> 1
+            for i, item in enumerate(buckets[r]):
+                gi = 2 * i + par
+                if gi < ngroups:
+                    groups[gi][s] = item
+                else:
+                    extra.append(item)
+        mod = 16
+    else:
+        buckets = [list(zip(hpos[hpos % 8 == r].tolist(), pk[hpos % 8 == r].tolist())) for r in range(8)]
+        for r in range(8):
+            for i, item in enumerate(buckets[r]):
+                if i < ngroups:
+                    groups[i][r] = item
+                else:
+                    extra.append(item)
+        mod = 8
     for gr in groups:                             # overflow rows fill free slots (a conflict, not an error)
         for s in range(8):
             if gr[s] is None and extra:
                 gr[s] = extra.pop()
     assert not extra, "row table overflow"
-    for gr in groups:
+    for gi, gr in enumerate(groups):
         for s in range(8):
             if gr[s] is None:
-                used = {x[0] % 8 for x in gr if x is not None}
-                cand = [r for r in range(8) if r not in used]
+                used = {x[0] % mod for x in gr if x is not None}
+                want = 2 * s + (gi & 1) if p.c8 else s
+                cand = [want] if want not in used else [r for r in range(mod) if r not in used]
                 gr[s] = ((cand[0] if cand else 0), -1)
-    rows = np.asarray([(h * 32, k) for gr in groups for (h, k) in gr], dtype=np.int32)
+    rows = np.asarray([(h * p.xr, k) for gr in groups for (h, k) in gr], dtype=np.int32)
     HP = (p.TD + KD - 1) * HH * HW
     pos = np.full(p.HPpad, -1, dtype=np.int32)
     q = np.arange(HP)
@@ -215,9 +247,14 @@ def _partials(dev, stream: int, n: int) -> torch.Tensor:
 
 
 def geometry(p: WPlan, spec) -> list[int]:
-    XB = p.HPpad * 32
+    XB = p.HPpad * p.xr
     return [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.K, spec.KD, spec.KH, spec.KW,
             spec.pd, spec.ph, spec.pw, p.TD, p.TH, p.TW, p.HPpad, p.kst, XB, p.BUF, p.G, p.ntg]
+
+
+def flags(p: WPlan) -> int:
+    """The launcher's variant word: nacc | 8 << 8 (8 waves) | 1 << 12 (8-channel form)."""
+    return p.nacc | (p.nw << 8 if p.nw == 8 else 0) | (1 << 12 if p.c8 else 0)
 
 
 def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) -> torch.Tensor:
@@ -234,7 +271,7 @@ def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) ->
     dw = out if out is not None else torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=dev)
     part = _partials(dev, st, 8 * p.workers * dw.numel())
     _native.kernels().conv_wtile(x5.data_ptr(), dy5.data_ptr(), dw.data_ptr(), part.data_ptr(), rt.data_ptr(),
-                                 pt.data_ptr(), zp.data_ptr(), geometry(p, spec), p.nacc | (p.nw << 8 if p.nw == 8 else 0), p.workers, sched.data_ptr(),
+                                 pt.data_ptr(), zp.data_ptr(), geometry(p, spec), flags(p), p.workers, sched.data_ptr(),
                                  st, [x5.numel(), dy5.numel(), dw.numel(), rt.numel() // 2, pt.numel(), part.numel()])
     return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
 

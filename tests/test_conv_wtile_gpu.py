@@ -32,6 +32,11 @@ CASES = [
     (3, 24, 24, 24, 64, 32, (3, 3, 3), "same"),      # segmentation decoder conv (padding, edge tiles)
     (4, 1, 40, 37, 32, 32, (1, 5, 5), "same"),       # 2-D conv
     (2, 14, 15, 16, 16, 16, (3, 3, 3), "same"),      # Cout 16
+    # 8 input channels (two taps per B fragment): the space-to-depth stem of FeatureNet-3D
+    # (7^3 stride 2 on 64^3 -> 4^3 stride 1 on 8 channels of a 32^3 grid)
+    (2, 32, 32, 32, 8, 32, (4, 4, 4), "valid"),
+    (24, 32, 32, 32, 8, 32, (4, 4, 4), "valid"),     # at a production batch
+    (3, 20, 21, 22, 8, 64, (3, 3, 3), "same"),       # odd kernel (tap pairs straddle kw rows), edges
 ]
 
 
