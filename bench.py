@@ -33,10 +33,12 @@ sys.path.insert(0, ROOT)
 # measured first-party baseline: stock PyTorch-ROCm eager on 1x MI355X, same config (bf16
 # autocast, channels-last, MIOpen find mode via torch.backends.cudnn.benchmark so MIOpen
 # times its solvers and keeps the fastest): `python bench.py --impl torch --torch-find`,
-# profiles/r2_bench_torch_miopen_find.log.  (Round 1 quoted 106.8 samples/s from MIOpen's
+# re-measured in round 3 on the same box and in the same call as the native bench
+# (profiles/r3_bench_torch_same_box.log: 6,068 samples/s, 21.1 ms/step; native on that box
+# 25,030, profiles/r3_bench_native_same_box.log; round 2: 6,100 on another box).  (Round 1 quoted 106.8 samples/s from MIOpen's
 # no-find fallback path -- a pathological baseline, withdrawn.)  The reference itself
 # publishes no number (BASELINE.json "published": {}).  vs_baseline = value / (this * n_gpus).
-TORCH_BASELINE_SAMPLES_PER_S_PER_GPU = 6100.15
+TORCH_BASELINE_SAMPLES_PER_S_PER_GPU = 6068.1
 
 
 def parse():
