@@ -254,7 +254,7 @@ PYBIND11_MODULE(_C, m) {
     fits(ext, 2, prod({geom[8], T, geom[4]}), "conv_wtile", "dw");
     fits(ext, 3, 32LL * geom[19], "conv_wtile", "rowtab");
     fits(ext, 4, geom[18], "conv_wtile", "postab");
-    fits(ext, 5, 8LL * workers * geom[8] * T * geom[4], "conv_wtile", "part");
+    fits(ext, 5, 8LL * workers * ((nacc >> 13) & 1 ? 2 : 1) * geom[8] * T * geom[4], "conv_wtile", "part");
     if (geom[5] > geom[1] + 2 * geom[12] || geom[6] > geom[2] + 2 * geom[13] || geom[7] > geom[3] + 2 * geom[14])
       throw std::runtime_error("conv_wtile: output larger than the padded input");
     chk(fn_conv_wtile(P<const void*>(x), P<const void*>(dy), P<float*>(dw), P<float*>(part), P<const void*>(rowtab),

@@ -64,7 +64,7 @@ __device__ __forceinline__ bf16x8 wt_tr_pair(const unsigned char* lo, const unsi
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int MT, int NACC, int NW, bool C8 = false>
+template <int MT, int NACC, int NW, bool C8 = false, bool KS2 = false>
 __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* __restrict__ x,
                                                                 const bf16* __restrict__ dy,
                                                                 float* __restrict__ dw,   // partials
@@ -85,6 +85,14 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   constexpr int XR = C8 ? 16 : 32;               // halo bytes per position
   constexpr int XSH = C8 ? 0 : 1;                // DMA slot -> halo position shift
   constexpr int TPF = C8 ? 2 : 1;                // taps per B fragment
+  // KS2: the k-steps of a job are split between the wave halves (waves 0-3 even, 4-7 odd
+  // k-steps; a wave and its SIMD partner w + 4 in different halves), each half covering
+  // all of the workgroup's taps with twice the fragments per wave: twice the MFMAs per
+  // k-step for the per-k-step bookkeeping (short k-steps were issue-bound).  The halves
+  // accumulate the same dW entries into separate partial slabs.
+  static_assert(!KS2 || NW == 8, "k-step split: loaderless form");
+  constexpr int WPT = KS2 ? NW / 2 : NW;         // waves sharing one k-step stream
+  constexpr int KSTEP = KS2 ? 2 : 1;
   const int ROWS = g.kst * 32;
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int T = g.KD * g.KH * g.KW;
@@ -292,7 +300,8 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
 
   // ======================= compute waves =======================
   const int G4 = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
-  const int tap0 = (tg * NW + wave) * NACC * TPF;
+  const int hp = KS2 ? (wave >= NW / 2 ? 1 : 0) : 0;   // first k-step of this wave
+  const int tap0 = (tg * WPT + (KS2 ? (wave & (NW / 2 - 1)) : wave)) * NACC * TPF;
   int toff[NACC];                                // byte offsets of this wave's taps in the halo
 #pragma unroll
   for (int i = 0; i < NACC; ++i) {
@@ -317,7 +326,7 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   // Every wave runs it (dead taps read tap 0 and are never stored).  B fragments run PF
   // taps ahead in a register ring, across the k-step boundary; a job starts with a ring
   // fill after its barrier.
-  int par = 0, ks = 0;
+  int par = 0, ks = hp;
   const unsigned char* xb = dsm;
   const unsigned char* yb = dsm;
   int plo = 0, phi = 0, plo_n = 0, phi_n = 0;   // row offsets of k-steps ks and ks + 1
@@ -337,7 +346,8 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   int dnext = -1;                               // NW = 8: the tile this wave DMAs during the current job
   // issued at k-step 0 by waves 0-3 and at mid-job by waves 4-7 (the two waves of a SIMD
   // never both stop their MFMAs for the DMA burst at the same time)
-  const int kdma = wave < NW / 2 ? 0 : g.kst / 2;
+  const int kdma = KS2 ? (hp == 0 ? 0 : ((g.kst / 2) | 1) < g.kst ? ((g.kst / 2) | 1) : 1)
+                      : (wave < NW / 2 ? 0 : g.kst / 2);
   auto dma_slice = [&](int k) {
     if (dnext < 0 || k != kdma) return;
     const int bo = (par ^ 1) * g.BUF;
@@ -358,9 +368,9 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
     ++jc;
     xb = dsm + par * g.BUF;
     yb = xb + g.XB;
-    rows_of(0, plo, phi);
-    rows_of(g.kst > 1 ? 1 : 0, plo_n, phi_n);
-    read_a(0, fa);
+    rows_of(hp, plo, phi);
+    rows_of(hp + KSTEP < g.kst ? hp + KSTEP : hp, plo_n, phi_n);
+    read_a(hp, fa);
 #pragma unroll
     for (int p = 0; p < PF; ++p) ring[p] = read_b(plo, phi, p);
     return true;
@@ -375,8 +385,8 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
       // row offsets two k-steps ahead (read here, used for the next k-step's ring refill: a
       // read consumed in the same k-step made hipcc drain every LDS read in flight)
       if constexpr (!HAS_LOADER) dma_slice(ks);
-      const int ksn = ks + 1 < g.kst ? ks + 1 : ks;   // (a job's last k-steps re-read themselves: unused)
-      const int ksnn = ks + 2 < g.kst ? ks + 2 : ksn;
+      const int ksn = ks + KSTEP < g.kst ? ks + KSTEP : ks;   // (a job's last k-steps re-read themselves: unused)
+      const int ksnn = ks + 2 * KSTEP < g.kst ? ks + 2 * KSTEP : ksn;
       int plo_nn, phi_nn;
       rows_of(ksnn, plo_nn, phi_nn);
       bf16x8 fa_n[MT];
@@ -397,8 +407,9 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
       phi = phi_n;
       plo_n = plo_nn;
       phi_n = phi_nn;
-      if (++ks == g.kst) {
-        ks = 0;
+      ks += KSTEP;
+      if (ks >= g.kst) {
+        ks = hp;
         par ^= 1;
         if (!start_job()) break;
       }
@@ -408,7 +419,7 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   // Plain stores into this workgroup's partial dW (partial = XCD x worker: the G
   // column-group workgroups of one (XCD, worker) write disjoint columns of it), summed
   // in a fixed order by wtile_reduce_kernel: deterministic, no atomics.
-  float* part = dw + (long long)(xcd * ((int)(gridDim.x >> 3) / g.G) + lid / g.G) * g.K * T * g.C;
+  float* part = dw + ((long long)(xcd * ((int)(gridDim.x >> 3) / g.G) + lid / g.G) * KSTEP + hp) * g.K * T * g.C;
   if (live) {
 #pragma unroll
     for (int i = 0; i < NACC; ++i) {
@@ -500,15 +511,16 @@ static size_t wtile_lds(const WGeom& g) {
 }
 
 extern "C" int fn_conv_wtile_supported(int K, int nacc) {
-  const int c8 = (nacc >> 12) & 1;
+  const int c8 = (nacc >> 12) & 1, ks2 = (nacc >> 13) & 1;
   const int nw = (nacc >> 8) & 15;
   nacc &= 255;
+  if (ks2) return nw == 8 && nacc == 8 && (K == 32 || (K == 64 && !c8));
   if (c8) return nw == 8 && (K == 32 || K == 64) && nacc == 4;
   if (nw == 8) return (K == 32 && (nacc == 4 || nacc == 8 || nacc == 16)) || (K == 64 && (nacc == 4 || nacc == 8));
   return (K == 16 && nacc == 16) || (K == 32 && (nacc == 8 || nacc == 16)) || (K == 64 && nacc == 8);
 }
 
-// dw: fp32 [K][T][C], accumulated into (+=); part: fp32 scratch [8 * workers][K][T][C]; rowtab int2[kst*32] (halo byte offset of
+// dw: fp32 [K][T][C], accumulated into (+=); part: fp32 scratch [8 * workers (x2 with ks2)][K][T][C]; rowtab int2[kst*32] (halo byte offset of
 // the row's tap-0 position, packed tile coords or -1), k order with distinct halo positions
 // mod 8 per aligned group of 8; postab int[HPpad] packed halo coords (-1 past the halo);
 // zp >= 16 zero bytes; sched int[64] zeroed (left zero); workers = workgroups per (XCD,
@@ -517,8 +529,9 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
                              const void* postab, const void* zp, const int* geom, int nacc, int workers, int* sched,
                              hipStream_t st) {
   const WGeom g = parse_wgeom(geom);
-  // nacc | (8 << 8): the loaderless 8-wave variant; | (1 << 12): its 8-input-channel form
-  const bool c8 = ((nacc >> 12) & 1) != 0;
+  // nacc | (8 << 8): the loaderless 8-wave variant; | (1 << 12): its 8-input-channel form;
+  // | (1 << 13): k-steps split between the wave halves
+  const bool c8 = ((nacc >> 12) & 1) != 0, ks2 = ((nacc >> 13) & 1) != 0;
   const int nw = ((nacc >> 8) & 15) == 8 ? 8 : 4;
   if (!fn_conv_wtile_supported(g.K, nacc)) return -2;
   nacc &= 255;
@@ -530,43 +543,48 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
   if (g.HPpad < HP || g.HPpad % (c8 ? 64 : 32) || g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
   if ((long long)g.TD * g.TH * g.TW > 32LL * g.kst || g.kst < 1 || g.kst > 32) return -3;
   if (g.XB != g.HPpad * xr || g.BUF < g.XB + g.kst * 32 * g.K * 2 || g.BUF % 1024) return -3;
-  if (g.ntg != (T + nw * nacc * tpf - 1) / (nw * nacc * tpf) || g.G != g.ntg * (c8 ? 1 : g.C / 16) || 8 * g.G > 63)
+  const int wpt = ks2 ? nw / 2 : nw;
+  if (g.ntg != (T + wpt * nacc * tpf - 1) / (wpt * nacc * tpf) || g.G != g.ntg * (c8 ? 1 : g.C / 16) || 8 * g.G > 63)
     return -3;
+  if (ks2 && g.kst < 2) return -3;
   if ((g.kst * 32 * (g.K / 8)) % 64) return -3;
   const size_t lds = wtile_lds(g);
   if (lds > 160 * 1024) return -4;
   if (!sched || !zp || !part || workers < 1) return -6;
   const unsigned grid = 8u * (unsigned)g.G * (unsigned)workers;
   static const int dbg = [] { const char* e = getenv("FN_WTILE_DBG"); return e ? atoi(e) : 0; }();
-#define WT_CASE(M, A, W, C)                                                                                    \
-  if (g.K == M * 16 && nacc == A && nw == W && c8 == C) {                                                      \
+#define WT_CASE(M, A, W, C, S)                                                                                 \
+  if (g.K == M * 16 && nacc == A && nw == W && c8 == C && ks2 == S) {                                          \
     static size_t cfg = 0;                                                                                     \
     if (lds > cfg) {                                                                                           \
-      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A, W, C>,                           \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A, W, C, S>,                        \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
       if (e != hipSuccess) return (int)e;                                                                      \
       cfg = lds;                                                                                               \
     }                                                                                                          \
-    hipLaunchKernelGGL((conv_wtile_kernel<M, A, W, C>), dim3(grid), dim3(wt_nthr(W)), lds, st, (const bf16*)x, \
-                       (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab, (const bf16*)zp, g, sched, \
-                       dbg);                                                                                   \
+    hipLaunchKernelGGL((conv_wtile_kernel<M, A, W, C, S>), dim3(grid), dim3(wt_nthr(W)), lds, st,              \
+                       (const bf16*)x, (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab,         \
+                       (const bf16*)zp, g, sched, dbg);                                                        \
   }
-  WT_CASE(1, 16, 4, false)
-  WT_CASE(2, 8, 4, false)
-  WT_CASE(2, 16, 4, false)
-  WT_CASE(4, 8, 4, false)
-  WT_CASE(2, 4, 8, false)
-  WT_CASE(2, 8, 8, false)
-  WT_CASE(2, 16, 8, false)
-  WT_CASE(4, 4, 8, false)
-  WT_CASE(4, 8, 8, false)
-  WT_CASE(2, 4, 8, true)
-  WT_CASE(4, 4, 8, true)
+  WT_CASE(1, 16, 4, false, false)
+  WT_CASE(2, 8, 4, false, false)
+  WT_CASE(2, 16, 4, false, false)
+  WT_CASE(4, 8, 4, false, false)
+  WT_CASE(2, 4, 8, false, false)
+  WT_CASE(2, 8, 8, false, false)
+  WT_CASE(2, 16, 8, false, false)
+  WT_CASE(4, 4, 8, false, false)
+  WT_CASE(4, 8, 8, false, false)
+  WT_CASE(2, 4, 8, true, false)
+  WT_CASE(4, 4, 8, true, false)
+  WT_CASE(2, 8, 8, false, true)
+  WT_CASE(4, 8, 8, false, true)
+  WT_CASE(2, 8, 8, true, true)
 #undef WT_CASE
   FN_CHECK_LAUNCH();
   const long long n = (long long)g.K * T * g.C;
   hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, dw, n,
-                     8 * workers, 1);
+                     8 * workers * (ks2 ? 2 : 1), 1);
   FN_CHECK_LAUNCH();
   return 0;
 }

@@ -47,6 +47,7 @@ class WPlan:
     cost: float
     nw: int = 4      # MFMA waves per workgroup: 4 (+ a loader wave) or 8 (no loader)
     c8: bool = False  # 8 input channels (the space-to-depth stem): two taps per B fragment
+    ks2: bool = False  # k-steps split between the wave halves (twice the fragments per wave)
 
     @property
     def xr(self) -> int:
@@ -95,6 +96,12 @@ def plan(spec) -> WPlan | None:
     return p
 
 
+def ks2_enabled() -> bool:
+    """FN_WTILE_KS2: 1 (default) = split the k-steps between the wave halves where a wave
+    would otherwise hold 4 fragments (T <= 32 taps, or the 8-channel stem), 0 = off."""
+    return os.environ.get("FN_WTILE_KS2", "1") != "0"
+
+
 def nwaves() -> int:
     """FN_WTILE_NW: 8 (default) = the loaderless 8-MFMA-wave variant, 4 = 4 MFMA waves + loader."""
     return int(os.environ.get("FN_WTILE_NW", "8"))
@@ -105,6 +112,7 @@ def _plan(spec):
     T = spec.KD * spec.KH * spec.KW
     nw = nwaves()
     c8 = C == 8 and nw == 8 and K in (32, 64)
+    ks2 = False
     if c8:                                        # 8 waves x 4 fragments x 2 taps per workgroup
         nacc, tpf = 4, 2
     else:
@@ -116,7 +124,9 @@ def _plan(spec):
             return None
     if T < 2:
         return None
-    ntg = -(-T // (nw * nacc * tpf))
+    if nw == 8 and nacc == 4 and ks2_enabled() and (K == 32 or (K == 64 and not c8)) and T <= 4 * 8 * tpf:
+        ks2, nacc = True, 8                       # 4 waves x 8 fragments per k-step stream
+    ntg = -(-T // ((nw // 2 if ks2 else nw) * nacc * tpf))
     G = ntg * (1 if c8 else C // 16)
     xr, hq = (16, 64) if c8 else (32, 32)
     if 8 * G > 63:
@@ -150,7 +160,7 @@ def _plan(spec):
                 loader = 600 + (HPpad * xr // 1024 + kst * K // 16) * 60
                 cost = jobs * max(mfma, loader) * (1.0 + 0.02 * HP / rows)   # halo re-reads (L2 traffic)
                 if best is None or cost < best.cost:
-                    best = WPlan(TD, TH, TW, HPpad, kst, nacc, ntg, G, workers, BUF, float(cost), nw, c8)
+                    best = WPlan(TD, TH, TW, HPpad, kst, nacc, ntg, G, workers, BUF, float(cost), nw, c8, ks2)
     return best
 
 
@@ -253,8 +263,9 @@ def geometry(p: WPlan, spec) -> list[int]:
 
 
 def flags(p: WPlan) -> int:
-    """The launcher's variant word: nacc | 8 << 8 (8 waves) | 1 << 12 (8-channel form)."""
-    return p.nacc | (p.nw << 8 if p.nw == 8 else 0) | (1 << 12 if p.c8 else 0)
+    """The launcher's variant word: nacc | 8 << 8 (8 waves) | 1 << 12 (8-channel form)
+    | 1 << 13 (k-steps split between the wave halves)."""
+    return p.nacc | (p.nw << 8 if p.nw == 8 else 0) | (1 << 12 if p.c8 else 0) | (1 << 13 if p.ks2 else 0)
 
 
 def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) -> torch.Tensor:
@@ -269,7 +280,7 @@ def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) ->
     st = _native.stream(x5)
     sched = _dev(_SCHED, (str(dev), st), lambda: torch.zeros(64, dtype=torch.int32, device=dev))
     dw = out if out is not None else torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=dev)
-    part = _partials(dev, st, 8 * p.workers * dw.numel())
+    part = _partials(dev, st, 8 * p.workers * (2 if p.ks2 else 1) * dw.numel())
     _native.kernels().conv_wtile(x5.data_ptr(), dy5.data_ptr(), dw.data_ptr(), part.data_ptr(), rt.data_ptr(),
                                  pt.data_ptr(), zp.data_ptr(), geometry(p, spec), flags(p), p.workers, sched.data_ptr(),
                                  st, [x5.numel(), dy5.numel(), dw.numel(), rt.numel() // 2, pt.numel(), part.numel()])

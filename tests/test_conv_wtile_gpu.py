@@ -76,3 +76,23 @@ def test_wtile_accumulates_into_out_and_repeats():
         cw.conv_wgrad(dy, x, spec, p, out=out)
     rel, mx = _rel(out.reshape(want.shape) / 3, want)
     assert rel < 5e-3 and mx < 2e-2, (rel, mx)
+
+
+@pytest.mark.parametrize("case", [CASES[2], CASES[4], CASES[5], CASES[6], CASES[8], CASES[9]])
+def test_wtile_kstep_split_matches_unsplit(case, monkeypatch):
+    """The k-step split (two partial slabs per worker) against the fp32 oracle, with the
+    unsplit plan of the same shape as a second opinion."""
+    x, dy, spec = _case(case, seed=5)
+    want = _ref_dw(x, dy, spec)
+    got = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("FN_WTILE_KS2", flag)
+        cw._PLANS.clear()
+        p = cw.plan(spec)
+        assert p is not None and p.ks2 == (flag == "1"), (case, p)
+        got[flag] = cw.conv_wgrad(dy, x, spec, p)
+        rel, mx = _rel(got[flag], want)
+        assert rel < 5e-3 and mx < 2e-2, (case, p, rel, mx)
+    cw._PLANS.clear()
+    rel, _ = _rel(got["1"], got["0"])
+    assert rel < 2e-3

@@ -52,8 +52,8 @@ def test_stem_geometry_is_launchable(monkeypatch):
     g = cw.geometry(p, spec)
     assert g[20] == p.HPpad * 16 and p.HPpad % 64 == 0       # XB: whole 64-position DMA instructions
     assert p.BUF >= g[20] + p.kst * 32 * spec.K * 2 and p.BUF % 1024 == 0
-    assert p.ntg == 1 and p.G == 1                           # 8 waves x 4 fragments x 2 taps = 64 taps
-    assert cw.flags(p) == 4 | (8 << 8) | (1 << 12)
+    assert p.ntg == 1 and p.G == 1                           # 4 waves x 8 fragments x 2 taps = 64 taps
+    assert p.ks2 and cw.flags(p) == 8 | (8 << 8) | (1 << 12) | (1 << 13)
     lds = 2 * p.BUF + 64 + p.kst * 32 * 12 + p.HPpad * 8
     assert lds <= cw.LDS_MAX
 
@@ -61,4 +61,22 @@ def test_stem_geometry_is_launchable(monkeypatch):
 def test_four_wave_mode_keeps_sixteen_channel_rule(monkeypatch):
     spec, p = _plan((128, 32, 32, 32, 8, 32, (4, 4, 4), "valid"), "4", monkeypatch)
     assert p is None                                          # the loader variant needs C % 16 == 0
+    cw._PLANS.clear()
+
+
+@pytest.mark.parametrize("case,ks2", [
+    ((128, 32, 32, 32, 8, 32, (4, 4, 4), "valid"), True),      # stem: 4 fragments of 2 taps -> 8
+    ((128, 22, 22, 22, 64, 64, (3, 3, 3), "valid"), True),     # conv4: T = 27 <= 32
+    ((128, 64, 64, 64, 64, 32, (3, 3, 3), "same"), True),      # seg decoder conv
+    ((128, 29, 29, 29, 32, 32, (5, 5, 5), "valid"), False),    # conv2: 16 fragments already
+    ((128, 25, 25, 25, 32, 64, (4, 4, 4), "valid"), False),    # conv3: 8 fragments of Cout 64
+])
+def test_kstep_split_selection(case, ks2, monkeypatch):
+    spec, p = _plan(case, "8", monkeypatch)
+    assert p.ks2 == ks2 and p.kst >= 2
+    wpt = 4 if p.ks2 else 8
+    assert p.ntg == -(-spec.taps // (wpt * p.nacc * (2 if p.c8 else 1)))
+    monkeypatch.setenv("FN_WTILE_KS2", "0")
+    cw._PLANS.clear()
+    assert not cw.plan(spec).ks2
     cw._PLANS.clear()
