@@ -55,6 +55,8 @@ int fn_bn_finalize(const float*, int, int, double, const float*, const float*, f
 int fn_bn_apply(const void*, const float*, const float*, void*, long long, int, int, hipStream_t);
 int fn_bn_bwd_apply(const void*, const void*, const float*, const float*, const float*, const float*, const float*,
                     const float*, void*, long long, int, float, int, hipStream_t);
+int fn_bn_bwd_apply_s2d(const void*, const void*, const float*, const float*, const float*, const float*,
+                        const float*, const float*, void*, int, int, int, int, int, float, int, hipStream_t);
 int fn_pool_fwd(const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd(const void*, const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd_stats_blocks(const int*);
@@ -150,6 +152,13 @@ static void check_halo(const std::vector<int>& g, const std::vector<long long>& 
 }
 
 // tile geometry: halo geometry (17) | CS HPpad nks nct mHW mHHW BUF mTW mTH; ext = {src, wpk, out, rowtab rows}
+// elements an output view (geometry entries 26-30: osn, ob, osd, osh, osw) spans
+static long long view_extent(const std::vector<int>& g, int ncol) {
+  if (g[26] < 0 || g[27] < 0 || g[28] < 0 || g[29] < 0 || g[30] < 0) throw std::runtime_error("conv_tile: bad output view");
+  return ((long long)(g[0] - 1) * g[26] + g[27] + (long long)(g[5] - 1) * g[28] + (long long)(g[6] - 1) * g[29] +
+          (long long)(g[7] - 1) * g[30] + 1) * ncol;
+}
+
 static void check_tile(const std::vector<int>& g, const std::vector<long long>& ext, int ncol, int MT,
                        const char* what) {
   if (g[4] <= 0 || ncol <= 0 || g[17] <= 0 || g[4] % g[17]) throw std::runtime_error(std::string(what) + ": bad slice");
@@ -157,7 +166,7 @@ static void check_tile(const std::vector<int>& g, const std::vector<long long>& 
     throw std::runtime_error(std::string(what) + ": output larger than the padded input");
   fits(ext, 0, prod({g[0], g[1], g[2], g[3], g[4]}), what, "src");
   fits(ext, 1, prod({g[4] / g[17] * g[19] + 4, g[20], 64, 8}), what, "wpk");   // + 4 zero ring k-steps
-  fits(ext, 2, prod({g[0], g[5], g[6], g[7], ncol}), what, "out");
+  fits(ext, 2, view_extent(g, ncol), what, "out");
   fits(ext, 3, 4LL * MT * 16, what, "rowtab");
   fits(ext, 4, g[19] + 6LL, what, "ktab");
 }
@@ -197,10 +206,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_tile", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                         uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
                         uintptr_t sched, uintptr_t st, std::vector<long long> ext, uintptr_t bny, uintptr_t bnp) {
-    need(geom, 26, "conv_tile");
+    need(geom, 31, "conv_tile");
     check_tile(geom, ext, ncol, MT, "conv_tile");
     if (bny) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
-      fits(ext, 5, prod({geom[0], geom[5], geom[6], geom[7], ncol}), "conv_tile", "bny");
+      fits(ext, 5, view_extent(geom, ncol), "conv_tile", "bny");
       fits(ext, 6, 4LL * ncol, "conv_tile", "bnp");
     }
     chk(fn_conv_tile(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
@@ -214,7 +223,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_tile8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                          uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
                          uintptr_t st, std::vector<long long> ext) {
-    need(geom, 26, "conv_tile8");
+    need(geom, 31, "conv_tile8");
     check_tile(geom, ext, ncol, MT, "conv_tile8");
     fits(ext, 4, geom[19] + 10LL, "conv_tile8", "ktab");    // nks + 2 PD + 2 entries
     chk(fn_conv_tile8(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
@@ -228,12 +237,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
                            uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,
                            int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext) {
-    need(geom, 26, "conv_tile_f8");
+    need(geom, 31, "conv_tile_f8");
     if (geom[4] <= 0 || ncol <= 0 || geom[17] <= 0 || geom[4] % geom[17])
       throw std::runtime_error("conv_tile_f8: bad slice");
     fits(ext, 0, prod({geom[0], geom[1], geom[2], geom[3], geom[4]}), "conv_tile_f8", "src");
     fits(ext, 1, prod({geom[4] / geom[17] * geom[19] + 4, geom[20], 64, 32}), "conv_tile_f8", "wpk");
-    fits(ext, 2, prod({geom[0], geom[5], geom[6], geom[7], ncol}), "conv_tile_f8", "out");
+    fits(ext, 2, view_extent(geom, ncol), "conv_tile_f8", "out");
     fits(ext, 3, 4LL * MT * 16, "conv_tile_f8", "rowtab");
     fits(ext, 4, geom[19] + 6LL, "conv_tile_f8", "ktab");
     chk(fn_conv_tile_f8(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
@@ -250,11 +259,16 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 24, "conv_wtile");
     const long long T = (long long)geom[9] * geom[10] * geom[11];
     fits(ext, 0, prod({geom[0], geom[1], geom[2], geom[3], geom[4]}), "conv_wtile", "x");
-    fits(ext, 1, prod({geom[0], geom[5], geom[6], geom[7], geom[8]}), "conv_wtile", "dy");
-    fits(ext, 2, prod({geom[8], T, geom[4]}), "conv_wtile", "dw");
+    const bool sp = (nacc >> 14) & 1;             // sub-pixel form: dy = [N, OD+1, OH+1, OW+1, 8 K]
+    if (sp)
+      fits(ext, 1, prod({geom[0], geom[5] + 1, geom[6] + 1, geom[7] + 1, 8 * geom[8]}), "conv_wtile", "dy");
+    else
+      fits(ext, 1, prod({geom[0], geom[5], geom[6], geom[7], geom[8]}), "conv_wtile", "dy");
+    const long long tw = sp ? 64 : T;             // (sub-pixel form: 8 classes x 8 folded taps)
+    fits(ext, 2, prod({geom[8], tw, geom[4]}), "conv_wtile", "dw");
     fits(ext, 3, 32LL * geom[19], "conv_wtile", "rowtab");
     fits(ext, 4, geom[18], "conv_wtile", "postab");
-    fits(ext, 5, 8LL * workers * ((nacc >> 13) & 1 ? 2 : 1) * geom[8] * T * geom[4], "conv_wtile", "part");
+    fits(ext, 5, 8LL * workers * ((nacc >> 13) & 1 ? 2 : 1) * geom[8] * tw * geom[4], "conv_wtile", "part");
     if (geom[5] > geom[1] + 2 * geom[12] || geom[6] > geom[2] + 2 * geom[13] || geom[7] > geom[3] + 2 * geom[14])
       throw std::runtime_error("conv_wtile: output larger than the padded input");
     chk(fn_conv_wtile(P<const void*>(x), P<const void*>(dy), P<float*>(dw), P<float*>(part), P<const void*>(rowtab),
@@ -265,7 +279,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("ext") = std::vector<long long>());
   m.def("conv_wtile_supported", &fn_conv_wtile_supported);
   m.def("conv_tile_workers", [](std::vector<int> geom, int ncol, int NT) {
-    need(geom, 26, "conv_tile_workers");
+    need(geom, 31, "conv_tile_workers");
     return fn_conv_tile_workers(geom.data(), ncol, NT);
   });
   m.def("tile_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int CS, int nks, int nct, int nslice,
@@ -434,6 +448,20 @@ PYBIND11_MODULE(_C, m) {
                         P<const float*>(dgamma), P<void*>(dy), total, C, inv_count, act, S(st)),
         "bn_bwd_apply");
   });
+  // ext = {dz / y numel, dsh numel}
+  m.def("bn_bwd_apply_s2d", [](uintptr_t dz, uintptr_t y, uintptr_t scale, uintptr_t shift, uintptr_t mean,
+                               uintptr_t invstd, uintptr_t dbeta, uintptr_t dgamma, uintptr_t dsh, int N, int FD,
+                               int FH, int FW, int C, float inv_count, int act, uintptr_t st,
+                               std::vector<long long> ext) {
+    fits(ext, 0, prod({N, FD, FH, FW, C}), "bn_bwd_apply_s2d", "dz/y");
+    fits(ext, 1, prod({N, FD / 2 + 1, FH / 2 + 1, FW / 2 + 1, 8LL * C}), "bn_bwd_apply_s2d", "dsh");
+    chk(fn_bn_bwd_apply_s2d(P<const void*>(dz), P<const void*>(y), P<const float*>(scale), P<const float*>(shift),
+                            P<const float*>(mean), P<const float*>(invstd), P<const float*>(dbeta),
+                            P<const float*>(dgamma), P<void*>(dsh), N, FD, FH, FW, C, inv_count, act, S(st)),
+        "bn_bwd_apply_s2d");
+  }, py::arg("dz"), py::arg("y"), py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"),
+     py::arg("dbeta"), py::arg("dgamma"), py::arg("dsh"), py::arg("N"), py::arg("FD"), py::arg("FH"), py::arg("FW"),
+     py::arg("C"), py::arg("inv_count"), py::arg("act"), py::arg("st"), py::arg("ext"));
   // pool geometry: N D H W C | OD OH OW | KD KH KW | sd sh sw | pd ph pw; ext = {x, out}
   auto check_pool = [](const std::vector<int>& g, const std::vector<long long>& ext, const char* what) {
     fits(ext, 0, prod({g[0], g[1], g[2], g[3], g[4]}), what, "x");

@@ -294,6 +294,69 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
   }
 }
 
+// The same BN backward, writing dy in the SHIFTED space-to-depth layout of the sub-pixel
+// decoder (ops/subpixel.py): output [N, FD/2+1, FH/2+1, FW/2+1, 8, C], cell c' sub-position
+// j' = full-resolution position q = 2c' - 1 + j' (zero where q is outside the grid).
+// Output-major: consecutive threads write consecutive 16-B chunks (the whole tensor, border
+// zeros included -- no separate fill); the reads are 64-B position rows, adjacent
+// sub-positions along W contiguous.  VW = 8 channels per thread, C / 8 dividing 256.
+template <int ACT>
+__global__ __launch_bounds__(256) void bn_bwd_apply_s2d_kernel(const bf16* __restrict__ dz, const bf16* __restrict__ y,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ invstd,
+                                                               const float* __restrict__ dbeta,
+                                                               const float* __restrict__ dgamma, bf16* __restrict__ dsh,
+                                                               int N, int FD, int FH, int FW, int C, float inv_count) {
+  constexpr int act = ACT;
+  const int cpr = C / 8;
+  const int D2 = FD / 2 + 1, H2 = FH / 2 + 1, W2 = FW / 2 + 1;
+  const long long nvec = (long long)N * D2 * H2 * W2 * 8 * cpr;
+  const long long stride = (long long)gridDim.x * 256;   // a multiple of cpr: the chunk is fixed
+  const long long i0 = blockIdx.x * 256LL + threadIdx.x;
+  const int k = (int)(threadIdx.x % cpr);
+  float sc[8], sh[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = k * 8 + j;
+    sc[j] = scale[c];
+    sh[j] = shift[c];
+    const float is = invstd[c];
+    k2[j] = -sc[j] * is * dgamma[c] * inv_count;
+    k3[j] = -sc[j] * (dbeta[c] * inv_count - mean[c] * is * dgamma[c] * inv_count);
+  }
+  for (long long i = i0; i < nvec; i += stride) {
+    const long long s = i / cpr;
+    const int jp = (int)(s & 7);
+    long long cell = s >> 3;
+    const int cw = (int)(cell % W2);
+    cell /= W2;
+    const int ch = (int)(cell % H2);
+    cell /= H2;
+    const int cd = (int)(cell % D2);
+    const int n = (int)(cell / D2);
+    const int qd = 2 * cd - 1 + (jp >> 2), qh = 2 * ch - 1 + ((jp >> 1) & 1), qw = 2 * cw - 1 + (jp & 1);
+    Pack8 po;
+    if ((unsigned)qd < (unsigned)FD && (unsigned)qh < (unsigned)FH && (unsigned)qw < (unsigned)FW) {
+      const long long off = ((((long long)n * FD + qd) * FH + qh) * FW + qw) * C + k * 8;
+      Pack8 py, pd;
+      py.u = *(const uint4*)(y + off);
+      pd.u = *(const uint4*)(dz + off);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float yv = bf2f(py.e[j]);
+        const float zv = act_fwd(yv * sc[j] + sh[j], act);
+        const float g = bf2f(pd.e[j]) * act_bwd_from_out(zv, act);
+        po.e[j] = f2bf(sc[j] * g + k2[j] * yv + k3[j]);
+      }
+    } else {
+      po.u = make_uint4(0u, 0u, 0u, 0u);
+    }
+    *(uint4*)(dsh + i * 8) = po.u;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Pooling (max / avg), 1-D/2-D/3-D channels-last with optional BN+act prologue.
 // geom: N, D, H, W, C, OD, OH, OW, KD, KH, KW, SD, SH, SW, PD, PH, PW
@@ -706,6 +769,24 @@ extern "C" int fn_bn_bwd_apply(const void* dz, const void* y, const float* scale
   if (C % 8 == 0) BB_ACT(8); else BB_ACT(1);
 #undef BB_ACT
 #undef BB_CASE
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_bn_bwd_apply_s2d(const void* dz, const void* y, const float* scale, const float* shift,
+                                   const float* mean, const float* invstd, const float* dbeta, const float* dgamma,
+                                   void* dsh, int N, int FD, int FH, int FW, int C, float inv_count, int act,
+                                   hipStream_t st) {
+  if (C % 8 || 256 % (C / 8) || FD % 2 || FH % 2 || FW % 2 || N < 1) return -2;
+  const long long nvec = (long long)N * (FD / 2 + 1) * (FH / 2 + 1) * (FW / 2 + 1) * 8 * (C / 8);
+#define BS_CASE(A)                                                                                      \
+  hipLaunchKernelGGL((bn_bwd_apply_s2d_kernel<A>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const bf16*)dz, \
+                     (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dsh, N, FD, FH, FW, C, inv_count)
+  if (act == ACT_RELU) BS_CASE(ACT_RELU);
+  else if (act == ACT_TANH) BS_CASE(ACT_TANH);
+  else if (act == ACT_SIGMOID) BS_CASE(ACT_SIGMOID);
+  else BS_CASE(ACT_NONE);
+#undef BS_CASE
   FN_CHECK_LAUNCH();
   return 0;
 }

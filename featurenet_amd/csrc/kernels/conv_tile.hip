@@ -57,6 +57,11 @@ struct TileGeom {
   unsigned mHW, mHHW;       // magic multipliers: p / HW == umulhi(p, mHW) (host-verified)
   int BUF;                  // bytes per LDS buffer (halo or epilogue staging), multiple of 16
   unsigned mTW, mTH;        // magic multipliers for the epilogue's tile-row decode
+  // output view: output position (n, d, h, w) is stored at position index
+  // n*osn + ob + d*osd + h*osh + w*osw (x Ncol elements); natural layout = (OD*OH*OW, 0,
+  // OH*OW, OW, 1).  A strided view writes one parity class of a sub-pixel (upsample x2)
+  // convolution straight into the full-resolution output.
+  int osn, ob, osd, osh, osw;
 };
 
 #define CT_NCW 4                       // compute (MFMA) waves
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     if constexpr (F8) lb[mt] = rt.x * 16 + (CPP == 4 ? 2 * (lg & 1) : 0) * PLANE;
     else lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;
     const int tw = rt.y % g.TW, th = (rt.y / g.TW) % g.TH, td = rt.y / (g.TW * g.TH);
-    roff[mt] = rt.y < 0 ? -1 : (td * g.OH + th) * g.OW + tw;
+    roff[mt] = rt.y < 0 ? -1 : td * g.osd + th * g.osh + tw * g.osw;
     rpk[mt] = (td << 16) | (th << 8) | tw;
   }
 
@@ -410,7 +415,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
         const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
         const int ld = g.OD - d0, lh = g.OH - h0, lw = g.OW - w0;   // in-bounds tile extent
         const bool edge = ld < g.TD || lh < g.TH || lw < g.TW;
-        const long long obase_e = ((((long long)n * g.OD + d0) * g.OH + h0) * g.OW + w0) * Ncol + gc8;
+        const long long obase_e =
+            ((long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh + w0 * g.osw) * Ncol + gc8;
         bf16* obase = reinterpret_cast<bf16*>(out) + obase_e;
         // straight-line variants per (statistics, activation): runtime branches inside the
         // unrolled per-tile loop made hipcc emit ~1000 basic blocks
@@ -671,7 +677,7 @@ __global__ __launch_bounds__(512, 1) void conv_tile8_kernel(const unsigned char*
     const int2 rt = rowtab[(rg * MT + mt) * 16 + lr];
     lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;
     const int tw = rt.y % g.TW, th = (rt.y / g.TW) % g.TH, td = rt.y / (g.TW * g.TH);
-    roff[mt] = rt.y < 0 ? -1 : (td * g.OH + th) * g.OW + tw;
+    roff[mt] = rt.y < 0 ? -1 : td * g.osd + th * g.osh + tw * g.osw;
     rpk[mt] = (td << 16) | (th << 8) | tw;
   }
   // static schedule: job j = (tile blockIdx.x + (j / nslice) * W, slice j % nslice)
@@ -850,7 +856,8 @@ __global__ __launch_bounds__(512, 1) void conv_tile8_kernel(const unsigned char*
       const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
       const int ld = g.OD - d0, lh = g.OH - h0, lw = g.OW - w0;
       const bool edge = ld < g.TD || lh < g.TH || lw < g.TW;
-      const long long obase_e = ((((long long)n * g.OD + d0) * g.OH + h0) * g.OW + w0) * Ncol + gc8;
+      const long long obase_e =
+          ((long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh + w0 * g.osw) * Ncol + gc8;
       bf16* obase = reinterpret_cast<bf16*>(out) + obase_e;
       auto epilogue = [&](auto hpc, auto mode) {
         constexpr int H = decltype(hpc)::value;
@@ -1005,7 +1012,7 @@ extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, in
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
-#define CT_GEOM_LEN 26
+#define CT_GEOM_LEN 31
 static TileGeom parse_tile(const int* v) {
   TileGeom g;
   g.N = v[0]; g.ID = v[1]; g.IH = v[2]; g.IW = v[3]; g.C = v[4];
@@ -1016,6 +1023,7 @@ static TileGeom parse_tile(const int* v) {
   g.CS = v[17]; g.HPpad = v[18]; g.nks = v[19]; g.nct = v[20];
   g.mHW = (unsigned)v[21]; g.mHHW = (unsigned)v[22]; g.BUF = v[23];
   g.mTW = (unsigned)v[24]; g.mTH = (unsigned)v[25];
+  g.osn = v[26]; g.ob = v[27]; g.osd = v[28]; g.osh = v[29]; g.osw = v[30];
   return g;
 }
 

@@ -64,7 +64,7 @@ __device__ __forceinline__ bf16x8 wt_tr_pair(const unsigned char* lo, const unsi
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int MT, int NACC, int NW, bool C8 = false, bool KS2 = false>
+template <int MT, int NACC, int NW, bool C8 = false, bool KS2 = false, bool SP = false>
 __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* __restrict__ x,
                                                                 const bf16* __restrict__ dy,
                                                                 float* __restrict__ dw,   // partials
@@ -74,9 +74,18 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
                                                                 int* __restrict__ sched, int dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int CO = MT * 16;
-  constexpr int CPR = CO / 8;                    // 16-B chunks per dy row
-  constexpr int R64 = 256 / (CO * 2);            // dy rows per 64 banks
+  // SP: the sub-pixel (upsample x2 + 3^3 conv) weight gradient.  Rows are low-resolution
+  // cells; wave w is parity class j = (w>>2, (w>>1)&1, w&1) and accumulates the 8 folded
+  // taps e of its class (low-res offsets j - 1 + e, inside a 3^3 footprint with pad 1) for
+  // two 16-channel x slices (two halo planes: 16 fragments).  The dy rows in LDS hold all 8
+  // classes (8 x 32 channels = 512 B per cell: full-resolution positions 2c + j, gathered
+  // from the shifted space-to-depth dy, ops/subpixel.py); wave w reads its class's 64 B.
+  static_assert(!SP || (NW == 8 && MT == 2 && NACC == 16 && !C8 && !KS2), "sub-pixel form");
+  constexpr int CO_L = SP ? 256 : CO;            // dy channels per LDS row
+  constexpr int CPR = CO_L / 8;                  // 16-B chunks per dy row
+  constexpr int R64 = SP ? 1 : 256 / (CO * 2);   // dy rows per 64 banks
   constexpr int NSW = 8 / R64;                   // swizzle classes over 8 rows
+  constexpr int XPL = SP ? 2 : 1;                // x halo planes (16-channel slices) per job
   constexpr int PF = NACC < 4 ? NACC : 4;       // B fragments in flight (register ring)
   // C8 (8-channel input, the space-to-depth stem): 16-B halo positions, and each 16-column
   // B fragment holds TWO taps x 8 channels (columns 0-7: tap 2i, 8-15: tap 2i + 1 of the
@@ -124,7 +133,10 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
     s_rows[i] = rt;
     // byte offset of the row's dy from the tile origin (interior tiles), -1 for a dummy row
     const int e = rt.y;
-    s_yoff[i] = e < 0 ? -1 : (((e >> 16) * g.OH + ((e >> 8) & 255)) * g.OW + (e & 255)) * CO * 2;
+    if constexpr (SP)   // dy grid = the shifted space-to-depth cells, one more per dimension
+      s_yoff[i] = e < 0 ? -1 : (((e >> 16) * (g.OH + 1) + ((e >> 8) & 255)) * (g.OW + 1) + (e & 255)) * CO_L * 2;
+    else
+      s_yoff[i] = e < 0 ? -1 : (((e >> 16) * g.OH + ((e >> 8) & 255)) * g.OW + (e & 255)) * CO * 2;
   }
   for (int i = tid; i < g.HPpad; i += NTHR) {
     const int e = postab[i];
@@ -178,10 +190,11 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
     int n, d0, h0, w0;
     decode(tile, n, d0, h0, w0);
     const unsigned dst0 = ct_lds_addr(dsm) + (unsigned)bufoff + (unsigned)g.XB;
-    const bf16* ys = dy + (long long)n * g.OD * g.OH * g.OW * CO;
+    const int YH = SP ? g.OH + 1 : g.OH, YW = SP ? g.OW + 1 : g.OW;
+    const bf16* ys = dy + (long long)n * (SP ? g.OD + 1 : g.OD) * YH * YW * CO_L;
     const bool y_in = d0 + g.TD <= g.OD && h0 + g.TH <= g.OH && w0 + g.TW <= g.OW;
     const unsigned char* yo =
-        reinterpret_cast<const unsigned char*>(ys + ((long long)(d0 * g.OH + h0) * g.OW + w0) * CO);
+        reinterpret_cast<const unsigned char*>(ys + ((long long)(d0 * YH + h0) * YW + w0) * CO_L);
     const int jend = min((dbg & 8) ? 0 : ny, first + mhi * step);   // (dbg 8, timing only: no dy DMA)
     for (int j0 = first + mlo * step; j0 < jend; j0 += 8 * step) {
       int o[8], e[8];
@@ -200,7 +213,14 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
           const int c = (sl % CPR) ^ (2 * (((unsigned)r / R64) % NSW));
           bool ok = o[i] >= 0;
           if (!y_in) ok = ok && d0 + (e[i] >> 16) < g.OD && h0 + ((e[i] >> 8) & 255) < g.OH && w0 + (e[i] & 255) < g.OW;
-          const void* src = ok ? (const void*)(yo + o[i] + c * 16) : (const void*)zp;
+          int co16 = c * 16;
+          if constexpr (SP) {
+            // chunk c = class j (c >> 2), quarter c & 3: full-res position 2 cell + j sits in
+            // shifted cell (cell + j), sub-position (1 - j)
+            const int j = c >> 2, jd = j >> 2, jh = (j >> 1) & 1, jw = j & 1;
+            co16 = (((jd * YH + jh) * YW + jw) * 8 + (7 - j)) * 64 + (c & 3) * 16;
+          }
+          const void* src = ok ? (const void*)(yo + o[i] + co16) : (const void*)zp;
           if constexpr (HAS_LOADER) ct_glds16(src, dst0 + (unsigned)(j << 10));
           else ct_glds16_nc(src, dst0 + (unsigned)(j << 10));
         }
@@ -220,8 +240,9 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
     decode(tile, n, d0, h0, w0);
     const int dlo = d0 - g.pd, hlo = h0 - g.ph, wlo = w0 - g.pw;
     const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
-    const bf16* xs = x + (long long)n * g.ID * g.IH * g.IW * g.C + slice * 16;
-    const int nx = min((g.HPpad * XR) >> 10, first + mhi * step);   // DMA instructions of the x halo (this range)
+    const bf16* xs = x + (long long)n * g.ID * g.IH * g.IW * g.C + slice * 16 * XPL;
+    const int nxp = (g.HPpad * XR) >> 10;        // DMA instructions per halo plane
+    const int nx = min(nxp * XPL, first + mhi * step);   // DMA instructions of the x halo (this range)
     const bool x_in = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID && hlo + HH <= g.IH &&
                       wlo + HW <= g.IW;
     if (dbg & 4) {                             // (timing only: no x halo DMA)
@@ -235,7 +256,11 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
       for (int j0 = first + mlo * step; j0 < nx; j0 += 8 * step) {
         int o[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = s_xoff[((64 * min(j0 + i * step, nx - 1) + lane) >> XSH)];
+        for (int i = 0; i < 8; ++i) {
+          const int jj = min(j0 + i * step, nx - 1);
+          const int pl = SP ? (jj >= nxp ? 1 : 0) : 0;   // (SP: plane = second 16-channel slice)
+          o[i] = s_xoff[((64 * (jj - pl * nxp) + lane) >> XSH)] + pl * 32;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i)
           if (j0 + i * step < nx)
@@ -246,14 +271,20 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
       for (int j0 = first + mlo * step; j0 < nx; j0 += 8 * step) {
         int e[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = s_pos[((64 * min(j0 + i * step, nx - 1) + lane) >> XSH)];
+        for (int i = 0; i < 8; ++i) {
+          const int jj = min(j0 + i * step, nx - 1);
+          const int pl = SP ? (jj >= nxp ? 1 : 0) : 0;
+          e[i] = s_pos[((64 * (jj - pl * nxp) + lane) >> XSH)];
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           if (j0 + i * step < nx) {
+            const int pl = SP ? (j0 + i * step >= nxp ? 1 : 0) : 0;
             const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
             const bool ok = e[i] >= 0 && (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
                             (unsigned)gw < (unsigned)g.IW;
-            const bf16* src = ok ? xs + ((long long)(gd * g.IH + gh) * g.IW + gw) * g.C + (C8 ? 0 : (lane & 1) * 8) : zp;
+            const bf16* src =
+                ok ? xs + ((long long)(gd * g.IH + gh) * g.IW + gw) * g.C + pl * 16 + (C8 ? 0 : (lane & 1) * 8) : zp;
             if constexpr (HAS_LOADER) ct_glds16(src, dst0 + (unsigned)((j0 + i * step) << 10));
             else ct_glds16_nc(src, dst0 + (unsigned)((j0 + i * step) << 10));
           }
@@ -305,12 +336,18 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   int toff[NACC];                                // byte offsets of this wave's taps in the halo
 #pragma unroll
   for (int i = 0; i < NACC; ++i) {
-    const int ti = tap0 + TPF * i + (C8 ? (p4 >> 1) : 0);
-    const int t = ti < T ? ti : 0;               // dead taps read tap 0 (never stored)
-    const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
-    toff[i] = ((kd * HH + kh) * HW + kw) * XR;
+    if constexpr (SP) {                          // class (wave) taps j + e in the 3^3 footprint, plane i >> 3
+      const int e = i & 7;
+      const int kd = (wave >> 2) + (e >> 2), kh = ((wave >> 1) & 1) + ((e >> 1) & 1), kw = (wave & 1) + (e & 1);
+      toff[i] = (i >> 3) * g.HPpad * XR + ((kd * HH + kh) * HW + kw) * XR;
+    } else {
+      const int ti = tap0 + TPF * i + (C8 ? (p4 >> 1) : 0);
+      const int t = ti < T ? ti : 0;             // dead taps read tap 0 (never stored)
+      const int kw = t % g.KW, kh = (t / g.KW) % g.KH, kd = t / (g.KW * g.KH);
+      toff[i] = ((kd * HH + kh) * HW + kw) * XR;
+    }
   }
-  const bool live = tap0 < T;
+  const bool live = SP || tap0 < T;
   f32x4 acc[NACC][MT];
 #pragma unroll
   for (int i = 0; i < NACC; ++i)
@@ -319,7 +356,8 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
 
   // dy fragment address of k-row r, 16-channel block mt: this lane's 4-channel quad
   auto dy_addr = [&](int r, int mt) -> int {
-    return r * (CO * 2) + (((2 * mt + (p4 >> 1)) ^ (2 * (((unsigned)r / R64) % NSW))) << 4) + (p4 & 1) * 8;
+    const int c = (SP ? wave * 4 : 0) + 2 * mt + (p4 >> 1);   // (SP: this wave's class)
+    return r * (CO_L * 2) + ((c ^ (2 * (((unsigned)r / R64) % NSW))) << 4) + (p4 & 1) * 8;
   };
   // One flat loop over (job, k-step): the accumulators are carried by a single loop (with
   // a job loop around a k-step loop, hipcc copied all of them at every job start).
@@ -419,10 +457,22 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   // Plain stores into this workgroup's partial dW (partial = XCD x worker: the G
   // column-group workgroups of one (XCD, worker) write disjoint columns of it), summed
   // in a fixed order by wtile_reduce_kernel: deterministic, no atomics.
-  float* part = dw + ((long long)(xcd * ((int)(gridDim.x >> 3) / g.G) + lid / g.G) * KSTEP + hp) * g.K * T * g.C;
+  float* part = dw + ((long long)(xcd * ((int)(gridDim.x >> 3) / g.G) + lid / g.G) * KSTEP + hp) *
+                         (SP ? 8LL * CO * 8 : (long long)g.K * T) * g.C;
   if (live) {
 #pragma unroll
     for (int i = 0; i < NACC; ++i) {
+      if constexpr (SP) {                        // part [class][co][e][ci] (T = 8 folded taps)
+        const int ci = (slice * 2 + (i >> 3)) * 16 + (lane & 15);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int co = wave * CO + mt * 16 + G4 * 4 + r;
+            part[((long long)co * 8 + (i & 7)) * g.C + ci] = acc[i][mt][r];
+          }
+        continue;
+      }
       const int t = tap0 + TPF * i + (C8 ? ((lane & 15) >> 3) : 0);
       const int ci = C8 ? (lane & 7) : slice * 16 + (lane & 15);
       if (t < T) {
@@ -511,9 +561,10 @@ static size_t wtile_lds(const WGeom& g) {
 }
 
 extern "C" int fn_conv_wtile_supported(int K, int nacc) {
-  const int c8 = (nacc >> 12) & 1, ks2 = (nacc >> 13) & 1;
+  const int c8 = (nacc >> 12) & 1, ks2 = (nacc >> 13) & 1, sp = (nacc >> 14) & 1;
   const int nw = (nacc >> 8) & 15;
   nacc &= 255;
+  if (sp) return nw == 8 && nacc == 16 && K == 32 && !c8 && !ks2;
   if (ks2) return nw == 8 && nacc == 8 && (K == 32 || (K == 64 && !c8));
   if (c8) return nw == 8 && (K == 32 || K == 64) && nacc == 4;
   if (nw == 8) return (K == 32 && (nacc == 4 || nacc == 8 || nacc == 16)) || (K == 64 && (nacc == 4 || nacc == 8));
@@ -530,59 +581,66 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
                              hipStream_t st) {
   const WGeom g = parse_wgeom(geom);
   // nacc | (8 << 8): the loaderless 8-wave variant; | (1 << 12): its 8-input-channel form;
-  // | (1 << 13): k-steps split between the wave halves
-  const bool c8 = ((nacc >> 12) & 1) != 0, ks2 = ((nacc >> 13) & 1) != 0;
+  // | (1 << 13): k-steps split between the wave halves; | (1 << 14): the sub-pixel form
+  // (K = 32 per parity class, dy = the shifted space-to-depth view with 8 x K channels per
+  // cell, a 3^3 footprint, dw = [8 classes][K][8 folded taps][C])
+  const bool c8 = ((nacc >> 12) & 1) != 0, ks2 = ((nacc >> 13) & 1) != 0, sp = ((nacc >> 14) & 1) != 0;
   const int nw = ((nacc >> 8) & 15) == 8 ? 8 : 4;
   if (!fn_conv_wtile_supported(g.K, nacc)) return -2;
   nacc &= 255;
   const int xr = c8 ? 16 : 32, tpf = c8 ? 2 : 1;
-  if ((c8 ? g.C != 8 : g.C % 16) || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
+  if ((c8 ? g.C != 8 : g.C % (sp ? 32 : 16)) || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
+  if (sp && (g.KD != 3 || g.KH != 3 || g.KW != 3)) return -2;
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const long long HP = (long long)(g.TD + g.KD - 1) * HH * HW;
   const int T = g.KD * g.KH * g.KW;
   if (g.HPpad < HP || g.HPpad % (c8 ? 64 : 32) || g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
   if ((long long)g.TD * g.TH * g.TW > 32LL * g.kst || g.kst < 1 || g.kst > 32) return -3;
-  if (g.XB != g.HPpad * xr || g.BUF < g.XB + g.kst * 32 * g.K * 2 || g.BUF % 1024) return -3;
+  const int kl = sp ? 8 * g.K : g.K;             // dy channels per LDS row
+  if (g.XB != g.HPpad * xr * (sp ? 2 : 1) || g.BUF < g.XB + g.kst * 32 * kl * 2 || g.BUF % 1024) return -3;
   const int wpt = ks2 ? nw / 2 : nw;
-  if (g.ntg != (T + wpt * nacc * tpf - 1) / (wpt * nacc * tpf) || g.G != g.ntg * (c8 ? 1 : g.C / 16) || 8 * g.G > 63)
+  if (sp ? (g.ntg != 1 || g.G != g.C / 32)
+         : (g.ntg != (T + wpt * nacc * tpf - 1) / (wpt * nacc * tpf) || g.G != g.ntg * (c8 ? 1 : g.C / 16)))
     return -3;
+  if (8 * g.G > 63) return -3;
   if (ks2 && g.kst < 2) return -3;
-  if ((g.kst * 32 * (g.K / 8)) % 64) return -3;
+  if ((g.kst * 32 * (kl / 8)) % 64) return -3;
   const size_t lds = wtile_lds(g);
   if (lds > 160 * 1024) return -4;
   if (!sched || !zp || !part || workers < 1) return -6;
   const unsigned grid = 8u * (unsigned)g.G * (unsigned)workers;
   static const int dbg = [] { const char* e = getenv("FN_WTILE_DBG"); return e ? atoi(e) : 0; }();
-#define WT_CASE(M, A, W, C, S)                                                                                 \
-  if (g.K == M * 16 && nacc == A && nw == W && c8 == C && ks2 == S) {                                          \
+#define WT_CASE(M, A, W, C, S, P)                                                                              \
+  if (g.K == M * 16 && nacc == A && nw == W && c8 == C && ks2 == S && sp == P) {                               \
     static size_t cfg = 0;                                                                                     \
     if (lds > cfg) {                                                                                           \
-      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A, W, C, S>,                        \
+      hipError_t e = hipFuncSetAttribute((const void*)conv_wtile_kernel<M, A, W, C, S, P>,                     \
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
       if (e != hipSuccess) return (int)e;                                                                      \
       cfg = lds;                                                                                               \
     }                                                                                                          \
-    hipLaunchKernelGGL((conv_wtile_kernel<M, A, W, C, S>), dim3(grid), dim3(wt_nthr(W)), lds, st,              \
+    hipLaunchKernelGGL((conv_wtile_kernel<M, A, W, C, S, P>), dim3(grid), dim3(wt_nthr(W)), lds, st,           \
                        (const bf16*)x, (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab,         \
                        (const bf16*)zp, g, sched, dbg);                                                        \
   }
-  WT_CASE(1, 16, 4, false, false)
-  WT_CASE(2, 8, 4, false, false)
-  WT_CASE(2, 16, 4, false, false)
-  WT_CASE(4, 8, 4, false, false)
-  WT_CASE(2, 4, 8, false, false)
-  WT_CASE(2, 8, 8, false, false)
-  WT_CASE(2, 16, 8, false, false)
-  WT_CASE(4, 4, 8, false, false)
-  WT_CASE(4, 8, 8, false, false)
-  WT_CASE(2, 4, 8, true, false)
-  WT_CASE(4, 4, 8, true, false)
-  WT_CASE(2, 8, 8, false, true)
-  WT_CASE(4, 8, 8, false, true)
-  WT_CASE(2, 8, 8, true, true)
+  WT_CASE(1, 16, 4, false, false, false)
+  WT_CASE(2, 8, 4, false, false, false)
+  WT_CASE(2, 16, 4, false, false, false)
+  WT_CASE(4, 8, 4, false, false, false)
+  WT_CASE(2, 4, 8, false, false, false)
+  WT_CASE(2, 8, 8, false, false, false)
+  WT_CASE(2, 16, 8, false, false, false)
+  WT_CASE(4, 4, 8, false, false, false)
+  WT_CASE(4, 8, 8, false, false, false)
+  WT_CASE(2, 4, 8, true, false, false)
+  WT_CASE(4, 4, 8, true, false, false)
+  WT_CASE(2, 8, 8, false, true, false)
+  WT_CASE(4, 8, 8, false, true, false)
+  WT_CASE(2, 8, 8, true, true, false)
+  WT_CASE(2, 16, 8, false, false, true)
 #undef WT_CASE
   FN_CHECK_LAUNCH();
-  const long long n = (long long)g.K * T * g.C;
+  const long long n = sp ? 64LL * g.K * g.C : (long long)g.K * T * g.C;
   hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, dw, n,
                      8 * workers * (ks2 ? 2 : 1), 1);
   FN_CHECK_LAUNCH();

@@ -27,6 +27,7 @@ from torch import nn
 
 from .. import ops
 from ..ops import bn as bn_ops
+from ..ops import subpixel
 from ..ops.elementwise import upsample2x
 from .layers import Conv, Dense
 
@@ -148,8 +149,15 @@ class FeatureNet3DSeg(nn.Module):
             x = x.unsqueeze(-1)
         for c in self.enc:
             x = c(x)
-        x = upsample2x(x)                  # nearest x2 upsample on the channels-last grid
         d, h = self.dec, self.head
+        if self.training and subpixel.gpu_ok(x, d.cout, x.shape[-1]) and \
+                bn_ops.fused_pointwise_ok(x, d.cout, h.cout, d.act):
+            # training on the GPU: upsample + decoder conv as 8 parity-class 2^3 convs (3.4x
+            # fewer FLOPs, the 2x-upsampled tensor never exists), the BN + ReLU inside the 1x1
+            # head's kernels, backward through the shifted space-to-depth dy (ops/subpixel.py)
+            return subpixel.decoder_head(x, d.weight, d.gamma, d.beta, d.running_mean, d.running_var, h.weight,
+                                         h.bias, d.bn_momentum, d.bn_eps, d.act)
+        x = upsample2x(x)                  # nearest x2 upsample on the channels-last grid
         if self.training and bn_ops.fused_pointwise_ok(x, d.cout, h.cout, d.act):
             # training on the GPU: the decoder's BN + ReLU run inside the 1x1 head's pointwise
             # kernels (forward and weight gradient), so its 64^3 x 32 output is never written

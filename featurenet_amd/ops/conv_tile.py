@@ -218,13 +218,28 @@ def row_table(p: TilePlan, kdims: tuple) -> np.ndarray:
     return tab
 
 
-def geometry(p: TilePlan, src_dims: tuple, out_dims: tuple, kdims: tuple, pads: tuple) -> list[int]:
+def natural_view(out_dims: tuple) -> tuple:
+    """(osn, ob, osd, osh, osw) of a contiguous [N, OD, OH, OW, C] output."""
+    OD, OH, OW = out_dims
+    return (OD * OH * OW, 0, OH * OW, OW, 1)
+
+
+def parity_view(full_dims: tuple, parity: tuple) -> tuple:
+    """Output view writing position (d, h, w) of one parity class to (2d + jd, 2h + jh, 2w + jw)
+    of a contiguous [N, FD, FH, FW, C] full-resolution output (sub-pixel upsample x2 convs)."""
+    FD, FH, FW = full_dims
+    jd, jh, jw = parity
+    return (FD * FH * FW, (jd * FH + jh) * FW + jw, 2 * FH * FW, 2 * FW, 2)
+
+
+def geometry(p: TilePlan, src_dims: tuple, out_dims: tuple, kdims: tuple, pads: tuple, view=None) -> list[int]:
     N, ID, IH, IW, C = src_dims
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     m = lambda v: int(np.int32(np.uint32(v)))    # noqa: E731 - unsigned magic as a signed int32
     return [N, ID, IH, IW, C, OD, OH, OW, KD, KH, KW, pads[0], pads[1], pads[2], p.TD, p.TH, p.TW,
-            p.CS, p.HPpad, p.nks, p.nct, m(p.mHW), m(p.mHHW), p.BUF, m(_magic(p.TW)), m(_magic(p.TH))]
+            p.CS, p.HPpad, p.nks, p.nct, m(p.mHW), m(p.mHHW), p.BUF, m(_magic(p.TW)), m(_magic(p.TH))] + \
+        list(view if view is not None else natural_view(out_dims))
 
 
 def _dev_cached(cache: dict, device, make):

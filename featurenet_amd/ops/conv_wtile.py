@@ -48,6 +48,7 @@ class WPlan:
     nw: int = 4      # MFMA waves per workgroup: 4 (+ a loader wave) or 8 (no loader)
     c8: bool = False  # 8 input channels (the space-to-depth stem): two taps per B fragment
     ks2: bool = False  # k-steps split between the wave halves (twice the fragments per wave)
+    sp: bool = False   # sub-pixel decoder form (ops/subpixel.py): wave = parity class, 2 slices
 
     @property
     def xr(self) -> int:
@@ -256,6 +257,72 @@ def _partials(dev, stream: int, n: int) -> torch.Tensor:
     return t
 
 
+def plan_subpixel(N: int, cells: tuple, C: int, K: int) -> WPlan | None:
+    """Tile plan of the sub-pixel decoder weight gradient: rows = low-res cells (all 8 parity
+    classes of a cell in one 512-B dy row), x halo = two 16-channel planes of the 3^3
+    footprint (pad 1), 16 fragments per wave (8 folded taps x 2 slices)."""
+    if K != 32 or C % 32 or nwaves() != 8:
+        return None
+    key = ("sp", N, tuple(cells), C, K)
+    if key in _PLANS:
+        return _PLANS[key]
+    OD, OH, OW = cells
+    G = C // 32
+    workers = max(1, N_CUS // (8 * G))
+    best = None
+    for TW in sorted({OW} | {-(-OW // k) for k in range(2, 6) if -(-OW // k) >= 8}):
+        for TD in range(1, OD + 1):
+            for TH in range(1, OH + 1):
+                rows = TD * TH * TW
+                if rows > 1024:
+                    break
+                kst = -(-rows // 32)
+                if rows < 0.85 * kst * 32 or rows < 64:
+                    continue
+                HP = (TD + 2) * (TH + 2) * (TW + 2)
+                HPpad = -(-HP // 32) * 32
+                BUF = -(-(2 * HPpad * 32 + kst * 32 * 8 * K * 2) // 1024) * 1024
+                lds = 2 * BUF + 64 + kst * 32 * 12 + HPpad * 8
+                if lds > LDS_MAX:
+                    continue
+                tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
+                jobs = math.ceil(math.ceil(tiles / 8) / workers)
+                mfma = kst * 16 * 2 * 16 * 2 + 400                  # per SIMD per job (2 waves)
+                dma = 600 + (2 * HPpad * 32 + kst * 32 * 8 * K * 2) // 1024 * 45
+                cost = jobs * max(mfma, dma) * (1.0 + 0.02 * HP / rows)
+                if best is None or cost < best.cost:
+                    best = WPlan(TD, TH, TW, HPpad, kst, 16, 1, G, workers, BUF, float(cost), 8, sp=True)
+    with _LOCK:
+        _PLANS[key] = best
+    return best
+
+
+def conv_wgrad_subpixel(dsh: torch.Tensor, x5: torch.Tensor, p: WPlan) -> torch.Tensor:
+    """Per-class folded weight gradients [8, K, 2, 2, 2, C] (fp32) of the sub-pixel decoder:
+    ``dsh`` = the shifted space-to-depth dy [N, D+1, H+1, W+1, 8K], ``x5`` = the low-res input
+    [N, D, H, W, C] (ops/subpixel.py; :func:`subpixel.fold_weight_grad` gives dW)."""
+    assert p.sp
+    N, D, H, W, C = x5.shape
+    K = dsh.shape[-1] // 8
+    assert dsh.shape == (N, D + 1, H + 1, W + 1, 8 * K) and dsh.is_contiguous() and x5.is_contiguous()
+    kd = (3, 3, 3)
+    dev = x5.device
+    rt_np, pt_np = tables(p, kd)
+    rt = _dev(_TABS, ("rt", p, kd, str(dev)), lambda: torch.from_numpy(rt_np).to(dev))
+    pt = _dev(_TABS, ("pt", p, kd, str(dev)), lambda: torch.from_numpy(pt_np).to(dev))
+    zp = _dev(_ZERO, str(dev), lambda: torch.zeros(64, dtype=torch.bfloat16, device=dev))
+    st = _native.stream(x5)
+    sched = _dev(_SCHED, (str(dev), st), lambda: torch.zeros(64, dtype=torch.int32, device=dev))
+    dw = torch.zeros(8 * K, 8, C, dtype=torch.float32, device=dev)
+    part = _partials(dev, st, 8 * p.workers * dw.numel())
+    geom = [N, D, H, W, C, D, H, W, K, 3, 3, 3, 1, 1, 1, p.TD, p.TH, p.TW, p.HPpad, p.kst, 2 * p.HPpad * 32, p.BUF,
+            p.G, p.ntg]
+    _native.kernels().conv_wtile(x5.data_ptr(), dsh.data_ptr(), dw.data_ptr(), part.data_ptr(), rt.data_ptr(),
+                                 pt.data_ptr(), zp.data_ptr(), geom, flags(p), p.workers, sched.data_ptr(), st,
+                                 [x5.numel(), dsh.numel(), dw.numel(), rt.numel() // 2, pt.numel(), part.numel()])
+    return dw.reshape(8, K, 2, 2, 2, C)
+
+
 def geometry(p: WPlan, spec) -> list[int]:
     XB = p.HPpad * p.xr
     return [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.K, spec.KD, spec.KH, spec.KW,
@@ -265,7 +332,8 @@ def geometry(p: WPlan, spec) -> list[int]:
 def flags(p: WPlan) -> int:
     """The launcher's variant word: nacc | 8 << 8 (8 waves) | 1 << 12 (8-channel form)
     | 1 << 13 (k-steps split between the wave halves)."""
-    return p.nacc | (p.nw << 8 if p.nw == 8 else 0) | (1 << 12 if p.c8 else 0) | (1 << 13 if p.ks2 else 0)
+    return (p.nacc | (p.nw << 8 if p.nw == 8 else 0) | (1 << 12 if p.c8 else 0) | (1 << 13 if p.ks2 else 0)
+            | (1 << 14 if p.sp else 0))
 
 
 def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) -> torch.Tensor:

@@ -1,0 +1,104 @@
+"""Sub-pixel segmentation decoder on the GPU (ops/subpixel.py): the 8 parity-class forward
+convs (tile kernel, strided output view), the BN backward written as the shifted
+space-to-depth dy, the decoder dgrad over it (tile kernel) and the sub-pixel weight
+gradient (conv_wtile SP form) against the fp32 references; then the whole
+decoder + BN + head autograd node against the materialised-upsample path."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from featurenet_amd import _native  # noqa: E402
+from featurenet_amd.ops import bn as bn_ops  # noqa: E402
+from featurenet_amd.ops import conv_wtile as cw  # noqa: E402
+from featurenet_amd.ops import subpixel as sp  # noqa: E402
+
+
+def _rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("N,S", [(2, 12), (3, 16)])
+def test_upconv_forward_and_stats(N, S):
+    assert _native.kernels_available()
+    torch.manual_seed(0)
+    x = _bf(torch.randn(N, S, S, S, 64, device="cuda"))
+    w = torch.randn(32, 3, 3, 3, 64, device="cuda") * 0.05
+    y, slab = sp.upconv_forward(x, w)
+    want = sp.ref_forward(x.float(), w)
+    assert _rel(y, want) < 1e-2
+    s = slab.sum(0)
+    yf = y.float().reshape(-1, 32)
+    torch.testing.assert_close(s[0], yf.sum(0), rtol=2e-3, atol=2e-1)
+    torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=2e-3, atol=2e-1)
+
+
+def test_bn_backward_shifted_layout_matches_natural():
+    torch.manual_seed(1)
+    N, F_, K = 2, 12, 32
+    y = _bf(torch.randn(N, F_, F_, F_, K, device="cuda"))
+    dz = _bf(torch.randn(N, F_, F_, F_, K, device="cuda"))
+    prm = torch.stack([torch.randn(K), torch.rand(K) + 0.5, torch.randn(K), torch.randn(K)]).cuda()
+    db, dg = torch.randn(K, device="cuda"), torch.randn(K, device="cuda")
+    y2, dz2 = y.reshape(-1, K), dz.reshape(-1, K)
+    nat = bn_ops._bwd_input(dz2, y2, prm, db, dg, 1, True).reshape(y.shape)
+    sh = sp.bn_bwd_to_shifted(dz2, y2, prm, db, dg, 1, y.shape)
+    assert torch.equal(sh.cpu(), sp.shift_s2d(nat.cpu()))
+
+
+@pytest.mark.parametrize("N,S", [(2, 12), (3, 16)])
+def test_upconv_dgrad(N, S):
+    torch.manual_seed(2)
+    w = torch.randn(32, 3, 3, 3, 64, device="cuda") * 0.05
+    dy = _bf(torch.randn(N, 2 * S, 2 * S, 2 * S, 32, device="cuda"))
+    dsh = sp.shift_s2d(dy).contiguous()
+    dx = sp.upconv_dgrad(dsh, w, (N, S, S, S, 64))
+    want = sp.ref_dgrad(dy.float(), w)
+    assert _rel(dx, want) < 1e-2
+
+
+@pytest.mark.parametrize("N,S", [(2, 12), (4, 16)])
+def test_subpixel_wgrad(N, S):
+    torch.manual_seed(3)
+    x = _bf(torch.randn(N, S, S, S, 64, device="cuda"))
+    dy = _bf(torch.randn(N, 2 * S, 2 * S, 2 * S, 32, device="cuda"))
+    p = cw.plan_subpixel(N, (S, S, S), 64, 32)
+    assert p is not None and p.sp
+    dwf = cw.conv_wgrad_subpixel(sp.shift_s2d(dy).contiguous(), x, p)
+    want = sp.ref_wgrad_classes(dy.float(), x.float())
+    assert _rel(dwf, want) < 5e-3
+    rel_fold = _rel(sp.fold_weight_grad(dwf), sp.fold_weight_grad(want))
+    assert rel_fold < 5e-3
+
+
+def test_decoder_head_matches_upsample_path():
+    """Forward logits and every gradient of the fused node vs upsample2x + conv + the fused
+    BN/head node (the previous path), same parameters."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3DSeg
+
+    torch.manual_seed(4)
+    N, S = 2, 24
+    m = FeatureNet3DSeg(input_size=S, num_classes=25).cuda().train()
+    x = (torch.rand(N, S, S, S, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    outs, grads = [], []
+    for flag in ("1", "0"):
+        import os
+        os.environ["FN_SUBPIXEL"] = flag
+        m.zero_grad(set_to_none=True)
+        torch.manual_seed(5)
+        out = m(x)
+        g = torch.randn_like(out.float())
+        (out.float() * g).sum().backward()
+        outs.append(out.float())
+        grads.append({k: p.grad.detach().float().clone() for k, p in m.named_parameters() if p.grad is not None})
+    os.environ.pop("FN_SUBPIXEL", None)
+    assert _rel(outs[0], outs[1]) < 2e-2
+    for k in grads[1]:
+        assert k in grads[0], k
+        r = _rel(grads[0][k], grads[1][k])
+        assert r < 5e-2, (k, r)
