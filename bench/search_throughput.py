@@ -2,8 +2,11 @@
 """NAS search throughput: candidates trained per hour.
 
 Trains ``--candidates`` mutants of the LeNet-5 template for ``--epochs`` on a
-synthetic MNIST-shaped set (no network), one trial per visible GPU through the
-TrialScheduler, with and without hipGraph-captured training steps.
+synthetic MNIST- or CIFAR-shaped set (no network) through the TrialScheduler, with and
+without hipGraph-captured training steps.  ``--workers-per-device N`` runs N worker
+processes per GPU (several small candidates share one MI355X).  The reference's unit of
+work is 25 epochs x 100 products (``pledge_evolution.py:20``); ``--candidates 32
+--epochs 5`` is the round-3 census workload.
 """
 import argparse
 import json
@@ -21,6 +24,9 @@ def main():
     ap.add_argument("--train", type=int, default=6000)
     ap.add_argument("--mode", default="inline", choices=["inline", "process"])
     ap.add_argument("--dataset", default="mnist", choices=["mnist", "cifar"])
+    ap.add_argument("--workers-per-device", type=int, default=1)
+    ap.add_argument("--graph", default="both", choices=["both", "on", "off"])
+    ap.add_argument("--batch", type=int, default=64)
     a = ap.parse_args()
     from featurenet_amd.ir.parse import parse_feature_model
     from featurenet_amd.search.mutation import MutationConfig, Mutator
@@ -31,9 +37,11 @@ def main():
     specs = [base] + [mut.generate_mutant(base, 0.1) for _ in range(a.candidates - 1)]
     for i, s in enumerate(specs):
         s.name = f"c{i}"
-    sched = TrialScheduler(mode=a.mode)
-    for graph in (False, True):
-        cfg = TrialConfig(dataset=a.dataset, epochs=a.epochs, batch_size=64, synthetic_sizes=(a.train, 1000),
+    mode = "process" if a.workers_per_device > 1 else a.mode
+    sched = TrialScheduler(mode=mode, workers_per_device=a.workers_per_device)
+    graphs = {"both": (False, True), "on": (True,), "off": (False,)}[a.graph]
+    for graph in graphs:
+        cfg = TrialConfig(dataset=a.dataset, epochs=a.epochs, batch_size=a.batch, synthetic_sizes=(a.train, 1000),
                           graph=graph)
         t0 = time.perf_counter()
         out = sched.map(specs, cfg)
@@ -41,7 +49,9 @@ def main():
         ok = sum(s.status == "trained" for s in out)
         print(json.dumps({"metric": "NAS candidates trained per hour", "graph": graph, "value": round(ok / dt * 3600, 1),
                           "candidates": len(specs), "trained": ok, "seconds": round(dt, 2),
-                          "devices": sched.devices, "epochs": a.epochs, "train_samples": a.train}), flush=True)
+                          "devices": sched.devices, "workers_per_device": a.workers_per_device,
+                          "dataset": a.dataset, "epochs": a.epochs, "train_samples": a.train, "batch": a.batch,
+                          "failed": [s.name for s in out if s.status != "trained"]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -146,9 +146,11 @@ def _worker(dev: str, tasks, results, ready):
 
 
 class TrialScheduler:
-    """Run trials on a set of devices, one worker process per device."""
+    """Run trials on a set of devices: ``workers_per_device`` worker processes per device
+    (several small candidates share one MI355X: each worker trains its own trial, the GPU
+    interleaves their kernels).  A device may also be listed more than once."""
 
-    def __init__(self, devices=None, timeout_s: float | None = None, mode: str = "auto"):
+    def __init__(self, devices=None, timeout_s: float | None = None, mode: str = "auto", workers_per_device: int = 1):
         if devices is None:
             try:
                 import torch
@@ -159,7 +161,13 @@ class TrialScheduler:
             devices = [str(i) for i in range(n)] or ["cpu"]
         self.devices = [str(d) for d in devices]
         self.timeout_s = timeout_s
-        self.mode = ("inline" if len(self.devices) == 1 and timeout_s is None else "process") if mode == "auto" else mode
+        self.workers_per_device = max(1, int(workers_per_device))
+        single = len(self.devices) == 1 and self.workers_per_device == 1
+        self.mode = ("inline" if single and timeout_s is None else "process") if mode == "auto" else mode
+
+    def slots(self) -> list[tuple[str, str]]:
+        """(worker key, device) of every worker process."""
+        return [(f"{d}/{i}/{k}", d) for i, d in enumerate(self.devices) for k in range(self.workers_per_device)]
 
     def map(self, specs: list[ModelSpec], cfg: TrialConfig) -> list[ModelSpec]:
         if not specs:
@@ -175,27 +183,29 @@ class TrialScheduler:
         workers: dict[str, dict] = {}
         retired: list[dict] = []
 
-        def start(dev):
+        devof = dict(self.slots())
+
+        def start(key):
             # every worker gets its OWN result queue, replaced with the worker: killing a
             # process while it writes a shared multiprocessing.Queue can corrupt that queue
             tq = ctx.Queue()
             rq = ctx.Queue()
             ready = ctx.Queue()
-            p = ctx.Process(target=_worker, args=(dev, tq, rq, ready), daemon=True)
+            p = ctx.Process(target=_worker, args=(devof[key], tq, rq, ready), daemon=True)
             p.start()
             # keep every queue referenced: a collected queue unlinks its semaphore
             # before the spawned child has unpickled it
-            if dev in workers:
-                retired.append(workers[dev])
-            workers[dev] = {"proc": p, "tasks": tq, "results": rq, "ready": ready, "busy": None, "t0": 0.0}
+            if key in workers:
+                retired.append(workers[key])
+            workers[key] = {"proc": p, "tasks": tq, "results": rq, "ready": ready, "busy": None, "t0": 0.0}
 
-        for d in self.devices:
-            start(d)
+        for key in devof:
+            start(key)
         pending = list(enumerate(specs))
         out: dict[int, ModelSpec] = {}
         cfgd = cfg.to_dict()
         while len(out) < len(specs):
-            for dev, w in workers.items():
+            for w in workers.values():
                 if w["busy"] is None and pending:
                     tid, s = pending.pop(0)
                     w["busy"], w["t0"] = tid, time.time()
@@ -215,8 +225,8 @@ class TrialScheduler:
             if not got:
                 time.sleep(0.05)
             # watchdog: hung or dead workers fail their trial and are restarted
-            for dev in list(workers):
-                w = workers[dev]
+            for key in list(workers):
+                w = workers[key]
                 tid = w["busy"]
                 if tid is None:
                     continue
@@ -230,7 +240,7 @@ class TrialScheduler:
                     s.status, s.accuracy = "failed", 0.0
                     s.error = "trial timed out" if hung else f"worker died (exit {w['proc'].exitcode})"
                     out[tid] = s
-                    start(dev)
+                    start(key)
         for w in workers.values():
             w["tasks"].put(None)
         for w in workers.values():

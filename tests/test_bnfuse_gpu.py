@@ -106,7 +106,8 @@ def test_seg_head_bn_in_pointwise_matches_unfused(monkeypatch, S):
     x = (torch.rand(2, S, S, S, 1, device=dev) < 0.3).to(torch.bfloat16)
     lab = torch.randint(0, 25, (2, S, S, S), device=dev)
     res = []
-    for fuse in ("0", "1"):
+    monkeypatch.setenv("FN_SUBPIXEL", "0")      # this pair isolates the BN-in-pointwise fusion
+    for fuse in ("0", "1"):                      # (the sub-pixel decoder: tests/test_subpixel_gpu.py)
         monkeypatch.setenv("FN_BN_PW_FUSE", fuse)
         model.zero_grad(set_to_none=True)
         out = model(x)

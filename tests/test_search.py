@@ -52,6 +52,17 @@ def test_scheduler_survives_hang_and_crash():
     assert [r.name for r in res] == ["a", "hang", "crash", "b"]
 
 
+def test_scheduler_runs_several_workers_per_device():
+    """workers_per_device = 2 on one device: two worker processes, every trial trained once,
+    results in submission order."""
+    sched = TrialScheduler(devices=["cpu"], timeout_s=60, mode="process", workers_per_device=2)
+    assert len(sched.slots()) == 2 and len({k for k, _ in sched.slots()}) == 2
+    specs = [_spec(n) for n in ("a", "b", "c")]
+    res = sched.map(specs, _cfg())
+    assert [r.name for r in res] == ["a", "b", "c"]
+    assert all(r.status == "trained" for r in res)
+
+
 def test_full_evolution_two_generations(tmp_path):
     from featurenet_amd.search.evolution import load_snapshot, run_evolution
 
