@@ -40,6 +40,7 @@ int fn_ew_binary(const void*, const void*, void*, long long, int, hipStream_t);
 int fn_ew_mul_bwd(const void*, const void*, const void*, void*, void*, long long, hipStream_t);
 int fn_concat2(void*, void*, void*, long long, int, int, int, hipStream_t);
 int fn_pad3(void*, void*, const int*, int, hipStream_t);
+int fn_pad_channels(void*, void*, long long, int, int, int, hipStream_t);
 int fn_dense_fwd(const void*, const float*, const float*, void*, float*, int, int, int, int, int, int, hipStream_t);
 int fn_dense_dgrad(const void*, const float*, void*, int, int, int, hipStream_t);
 int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, float*, int, hipStream_t);
@@ -305,6 +306,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("pad3", [](uintptr_t x, uintptr_t out, std::vector<int> geom, int dir, uintptr_t st) {
     need(geom, 8, "pad3");
     chk(fn_pad3(P<void*>(x), P<void*>(out), geom.data(), dir, S(st)), "pad3");
+  });
+  m.def("pad_channels", [](uintptr_t x, uintptr_t out, long long rows, int C, int CP, int dir, uintptr_t st) {
+    chk(fn_pad_channels(P<void*>(x), P<void*>(out), rows, C, CP, dir, S(st)), "pad_channels");
   });
   m.def("dense_splits", &fn_dense_splits);
   m.def("dense_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t part, int M, int N, int K,

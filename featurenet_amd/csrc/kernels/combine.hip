@@ -131,6 +131,35 @@ __global__ __launch_bounds__(CB_THREADS) void pad3_kernel(bf16* __restrict__ x, 
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
+// ---- channel padding: [rows][C] <-> [rows][CP] (CP a multiple of 8, CP >= C) ----------
+// dir 0: out[r][c] = c < C ? x[r][c] : 0 -- one 16-B store per thread (NAS convs with
+//        C % 8 != 0 then gather 16-B channel vectors instead of single elements);
+// dir 1: x[r][c] = out[r][c] for c < C (the gradient of the padding, a crop).
+__global__ __launch_bounds__(CB_THREADS) void pad_channels_kernel(bf16* __restrict__ x, bf16* __restrict__ out,
+                                                                  long long rows, int C, int CP, int dir) {
+  const int cc = CP >> 3;
+  const long long i = (long long)blockIdx.x * CB_THREADS + threadIdx.x;
+  if (i >= rows * cc) return;
+  const long long r = i / cc;
+  const int c0 = (int)(i - r * cc) * 8;
+  const unsigned short* xs = reinterpret_cast<const unsigned short*>(x) + r * C;
+  unsigned short* os = reinterpret_cast<unsigned short*>(out) + r * CP + c0;
+  if (dir == 0) {
+    unsigned short v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = c0 + j < C ? xs[c0 + j] : (unsigned short)0;
+    *reinterpret_cast<uint4*>(os) = make_uint4(v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
+                                               v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16));
+  } else {
+    const uint4 q = *reinterpret_cast<const uint4*>(os);
+    const unsigned w[4] = {q.x, q.y, q.z, q.w};
+    unsigned short* xd = reinterpret_cast<unsigned short*>(x) + r * C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (c0 + j < C) xd[c0 + j] = (unsigned short)(w[j >> 1] >> (16 * (j & 1)));
+  }
+}
+
 static unsigned cb_blocks(long long items) { return (unsigned)((items + CB_THREADS - 1) / CB_THREADS); }
 
 extern "C" int fn_ew_binary(const void* a, const void* b, void* out, long long n, int op, hipStream_t st) {
@@ -169,6 +198,14 @@ extern "C" int fn_pad3(void* x, void* out, const int* g8, int dir, hipStream_t s
                                    : (long long)N * D * H * W * cc;
   hipLaunchKernelGGL(pad3_kernel, dim3(cb_blocks(total)), dim3(CB_THREADS), 0, st, (bf16*)x, (bf16*)out, N, D, H, W,
                      C, pd, ph, pw, vec, dir);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_pad_channels(void* x, void* out, long long rows, int C, int CP, int dir, hipStream_t st) {
+  if (rows <= 0 || C <= 0 || CP < C || CP % 8 || (dir != 0 && dir != 1)) return -2;
+  hipLaunchKernelGGL(pad_channels_kernel, dim3(cb_blocks(rows * (CP / 8))), dim3(CB_THREADS), 0, st, (bf16*)x,
+                     (bf16*)out, rows, C, CP, dir);
   FN_CHECK_LAUNCH();
   return 0;
 }

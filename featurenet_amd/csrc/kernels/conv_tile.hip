@@ -149,6 +149,16 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // BWS: the BN's (scale, shift, mean, invstd) of this workgroup's 32 columns, read per use by
   // the epilogue (no live registers across the k-loop)
   float4* s_bn = reinterpret_cast<float4*>(s_pos + g.HPpad);
+  // F8: the dequantisation scale and bias of this workgroup's 32 columns ([scale 32][bias 32]),
+  // read by the epilogue from LDS (global loads there serialised every tile's stores)
+  float* s_sb = reinterpret_cast<float*>(s_pos + g.HPpad);
+  if constexpr (F8) {
+    if (tid < NT * 16) {
+      const int c = blockIdx.y * NT * 16 + tid;
+      s_sb[tid] = c < Ncol ? scale[c] : 0.f;
+      s_sb[NT * 16 + tid] = (bias && c < Ncol) ? bias[c] : 0.f;
+    }
+  }
   if constexpr (BWS) {
     if (tid < NT * 16) {
       const int c = blockIdx.y * NT * 16 + tid;
@@ -520,10 +530,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
         auto epilogue_f8 = [&](auto mode) {
           constexpr int M = decltype(mode)::value;   // bit 0 relu, bit 1 fp8 output
           float sc8[8], bs8[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            sc8[j] = gc8 + j < Ncol ? scale[gc8 + j] : 0.f;
-            bs8[j] = (bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
+          {
+            const float4* q = reinterpret_cast<const float4*>(s_sb + 8 * lg);
+            const float4 a = q[0], b = q[1], c = q[NT * 4], d = q[NT * 4 + 1];
+            sc8[0] = a.x; sc8[1] = a.y; sc8[2] = a.z; sc8[3] = a.w;
+            sc8[4] = b.x; sc8[5] = b.y; sc8[6] = b.z; sc8[7] = b.w;
+            bs8[0] = c.x; bs8[1] = c.y; bs8[2] = c.z; bs8[3] = c.w;
+            bs8[4] = d.x; bs8[5] = d.y; bs8[6] = d.z; bs8[7] = d.w;
           }
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
@@ -1074,7 +1087,7 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, bool bws = false) {
   const int PD = ct_pd(NT, f8);
   return 2 * (size_t)g.BUF + 64 + CT_RED_BYTES + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
-         (bws ? (size_t)NT * 16 * 16 : 0);
+         (bws ? (size_t)NT * 16 * 16 : 0) + (f8 ? (size_t)NT * 16 * 8 : 0);
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -1208,6 +1221,35 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   if (Ncol % 8) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
+  // FN_F8_DBG (timing experiments only, wrong results): 1 no weight loads, 2 no halo reads,
+  // 4 no halo DMA (and sums of them), 16 cycle stamps (barrier-A wait, job, epilogue)
+  static const int f8dbg = [] { const char* e = getenv("FN_F8_DBG"); return e ? atoi(e) : 0; }();
+  if (f8dbg) {
+    static long long* stamps = nullptr;
+    const size_t nst = (size_t)grid.x * grid.y * 16;
+    if ((f8dbg & 16) && !stamps && hipMalloc(&stamps, 256 * 64 * 16 * sizeof(long long)) != hipSuccess) return -5;
+    if ((f8dbg & 16) && hipMemsetAsync(stamps, 0, nst * sizeof(long long), st) != hipSuccess) return -5;
+#define CT_F8_DBG(C, D) if (MT == 8 && NT == 2 && CPP == C && f8dbg == D) \
+    rc = launch_tile<8, 2, C, D, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, \
+                                       zp, bias, out, nullptr, g, Ncol, relu ? ACT_RELU : ACT_NONE, sched, stamps, scale, oscale);
+    CT_F8_DBG(2, 1) CT_F8_DBG(2, 2) CT_F8_DBG(2, 3) CT_F8_DBG(2, 4) CT_F8_DBG(2, 7) CT_F8_DBG(2, 16)
+    CT_F8_DBG(4, 1) CT_F8_DBG(4, 2) CT_F8_DBG(4, 3) CT_F8_DBG(4, 4) CT_F8_DBG(4, 7) CT_F8_DBG(4, 16)
+#undef CT_F8_DBG
+    if (rc) return rc;
+    FN_CHECK_LAUNCH();
+    if (f8dbg & 16) {
+      std::vector<long long> h(nst);
+      if (hipStreamSynchronize(st) != hipSuccess ||
+          hipMemcpy(h.data(), stamps, nst * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return -5;
+      double m[16] = {0};
+      for (size_t i = 0; i < nst; ++i) m[i % 16] += (double)h[i] / (grid.x * grid.y);
+      for (int w = 0; w < 2; ++w)
+        fprintf(stderr, "[conv_tile_f8 stamps CPP%d %s] barrierA %.0f job %.0f epilogue %.0f | total %.0f\n", CPP,
+                w ? "loader" : "wave0 ", m[8 * w], m[8 * w + 1], m[8 * w + 2], m[8 * w + 6]);
+    }
+    return 0;
+  }
 #define CT_F8_CASE(M, N, C)                                                                                        \
   if (MT == M && NT == N && CPP == C)                                                                              \
     rc = launch_tile<M, N, C, 0, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, \

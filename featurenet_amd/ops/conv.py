@@ -19,12 +19,14 @@ GPU path:
 """
 from __future__ import annotations
 
+import dataclasses
 import math
 import os
 import threading
 
 import numpy as np
 import torch
+import torch.nn.functional as F
 
 from .. import _native
 from . import bnfuse
@@ -632,15 +634,75 @@ def pw_wgrad(dy2: torch.Tensor, x2: torch.Tensor, pro=None) -> torch.Tensor:
     return dw
 
 
+# ---------------------------------------------------------------------------
+# channel padding for NAS channel counts (C or Cout % 8 != 0)
+# ---------------------------------------------------------------------------
+def chan_pad_needed(spec: ConvSpec) -> bool:
+    """The forward / wgrad gather would fall back to single-element loads (GM_SCALAR)."""
+    return gather_mode(spec) == GM_SCALAR
+
+
+def pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
+    """bf16 channels-last copy of ``x`` with its channels zero-padded to ``cp`` (one native pass)."""
+    C = x.shape[-1]
+    if C == cp:
+        return x
+    x = x.contiguous()
+    out = torch.empty(*x.shape[:-1], cp, dtype=torch.bfloat16, device=x.device)
+    _native.kernels().pad_channels(x.data_ptr(), out.data_ptr(), x.numel() // C, C, cp, 0, _native.stream(x))
+    return out
+
+
+def pad_weight(w: torch.Tensor, cin: int | None = None, cout: int | None = None) -> torch.Tensor:
+    """Zero-pad a [K, KD, KH, KW, C] weight to ``cout`` rows / ``cin`` input channels."""
+    K, C = w.shape[0], w.shape[-1]
+    pc, pk = (cin or C) - C, (cout or K) - K
+    if pc == 0 and pk == 0:
+        return w
+    return F.pad(w, (0, pc, 0, 0, 0, 0, 0, 0, 0, pk))
+
+
+def _conv_bwd_padded(ctx, dy, xs, w, spec):
+    """ConvFn backward for channel-padded convs: ``xs`` is the (possibly channel-padded)
+    saved input, ``spec`` its spec; dy (already through the activation backward) is padded
+    to a multiple of 8 output channels when Cout % 8 != 0, the weight gets matching zero
+    rows / columns, and the gradients are cropped back to the real channels."""
+    C0 = w.shape[-1]
+    K0 = spec.K
+    kp = -(-K0 // 8) * 8
+    dyp = pad_channels(dy, kp)
+    sk = dataclasses.replace(spec, K=kp)
+    dx = dw = None
+    if ctx.x_needs:
+        wk = pad_weight(w.detach(), cout=kp)                     # real input channels: dx has C0 columns
+        dx = native_conv_dgrad(dyp, wk, dataclasses.replace(sk, C=C0))
+    if ctx.needs_input_grad[1]:
+        dwp = native_conv_wgrad(dyp, xs.contiguous(), sk)         # [kp, KD, KH, KW, spec.C]
+        dw = dwp[:K0, ..., :C0].contiguous() if (kp != K0 or spec.C != C0) else dwp
+    db = native_colsum(dy.reshape(-1, K0)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+    return dx, dw, db, None, None, None
+
+
 class ConvFn(torch.autograd.Function):
     """y = act(conv(x, w) + b); optional BN statistics slab as a 2nd output."""
 
     @staticmethod
     def forward(ctx, x5, w, b, spec: ConvSpec, act: int, want_stats: bool):
+        w0 = w
         bias = b.detach().float().contiguous() if b is not None else None
         s2d = s2d_plan(spec)
         x_saved = x5
         ctx.pw = pointwise_ok(spec, want_stats)
+        ctx.cpad = 0
+        if not ctx.pw and s2d is None and chan_pad_needed(spec):
+            # C % 8 != 0 (NAS convs: 12, 18, 120 ... channels): gather 16-B channel vectors of a
+            # zero-padded copy instead of single elements; the padded copy is what wgrad reads
+            cp = -(-spec.C // 8) * 8
+            x5 = pad_channels(x5, cp)
+            w = pad_weight(w.detach(), cin=cp)
+            spec = dataclasses.replace(spec, C=cp)
+            x_saved = x5
+            ctx.cpad = cp
         if ctx.pw:
             x5 = x5.contiguous()
             y = pw_fwd(x5.reshape(-1, spec.C), w.reshape(spec.K, spec.C), bias, act).reshape(spec.out_shape5)
@@ -667,14 +729,14 @@ class ConvFn(torch.autograd.Function):
         else:
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
-        ctx.spec, ctx.act, ctx.has_b, ctx.s2d = spec, act, b is not None, s2d
+        ctx.spec, ctx.act, ctx.has_b, ctx.s2d = spec, act, b is not None, s2d   # (channel-padded spec when cpad)
         ctx.set_materialize_grads(False)                # no zero-filled gradient for the stats output
         ctx.x_needs = ctx.needs_input_grad[0]
         # x = act(bn(y)) of the previous layer: the dgrad epilogue sums that BN's backward
         # statistics (ops/bnfuse.py) -- plain stride-1 convs on the tile kernel only
         ctx.bn_src = (bnfuse.source_of(x_saved) if ctx.x_needs and not ctx.pw and s2d is None and
                       conv_tile.dgrad_plan(spec) is not None else None)
-        ctx.save_for_backward(x_saved, w, y if act else None)
+        ctx.save_for_backward(x_saved, w0, y if act else None)
         if stats is not None:
             ctx.mark_non_differentiable(stats)
         return y, stats
@@ -694,6 +756,8 @@ class ConvFn(torch.autograd.Function):
             dw = pw_wgrad(dy2, x2).reshape(w.shape) if ctx.needs_input_grad[1] else None
             db = native_colsum(dy2) if (ctx.has_b and ctx.needs_input_grad[2]) else None
             return dx, dw, db, None, None, None
+        if ctx.cpad or (spec.K % 8 and ctx.s2d is None):
+            return _conv_bwd_padded(ctx, dy, x5, w, spec)
         dx = None
         if ctx.x_needs:
             if ctx.bn_src is not None:

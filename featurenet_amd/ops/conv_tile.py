@@ -148,7 +148,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4):
                         if BUF < 16384:                 # (the split-K exchange: 16 KiB rounds)
                             continue
                     else:
-                        lds = 2 * BUF + 64 + RED_BYTES + (nks + PD + 2) * 16 + HPpad * 8
+                        lds = 2 * BUF + 64 + RED_BYTES + (nks + PD + 2) * 16 + HPpad * 8 + (NT * 16 * 8 if f8 else 0)
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)

@@ -134,6 +134,50 @@ def test_conv_search_space_shapes(case):
 
 
 @pytest.mark.parametrize("case", [
+    # (x shape, Cout, kernel, stride, act): NAS channel counts that are not multiples of 8
+    ((16, 1, 16, 16, 12), 120, (1, 5, 5), 1, "relu"),
+    ((8, 1, 32, 32, 18), 108, (1, 3, 3), 1, "relu"),
+    ((8, 1, 32, 32, 48), 12, (1, 5, 5), 1, None),
+    ((4, 1, 8, 8, 36), 8, (1, 3, 3), 2, "relu"),
+    ((6, 1, 28, 28, 20), 6, (1, 3, 1), 1, None),
+    ((2, 9, 9, 9, 12), 20, (3, 3, 3), 1, "relu"),
+])
+def test_conv_channel_padded(case, monkeypatch):
+    """C or Cout % 8 != 0: the forward gathers a channel-padded copy of x, the backward a
+    channel-padded dy (16-B vectors instead of single elements); gradients cropped back."""
+    _native_loaded()
+    import importlib
+
+    from featurenet_amd.ops.spec import act_code
+
+    convmod = importlib.import_module("featurenet_amd.ops.conv")
+
+    calls = []
+    real = convmod.pad_channels
+    monkeypatch.setattr(convmod, "pad_channels", lambda x, cp: calls.append((x.shape[-1], cp)) or real(x, cp))
+    shape, K, k, s, act = case
+    torch.manual_seed(K + shape[-1])
+    x = torch.randn(*shape).to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, K, k, s, "same")
+    w = (torch.randn(K, spec.KD, spec.KH, spec.KW, shape[-1]) * 0.1).to(torch.bfloat16).float()
+    b = torch.randn(K) * 0.1
+    xr, wr, br = x.float().clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = ref.conv(xr, wr, br, spec, act)
+    xn = x.cuda().requires_grad_(True)
+    wn, bn = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    yn, _ = convmod.ConvFn.apply(xn, wn, bn, spec, act_code(act), False)
+    close(yn, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(g)
+    yn.backward(g.cuda().to(torch.bfloat16))
+    close(xn.grad, xr.grad)
+    close(wn.grad, wr.grad)
+    close(bn.grad, br.grad)
+    assert wn.grad.shape == w.shape and xn.grad.shape == x.shape
+    assert calls, "the channel-padded path did not run"
+
+
+@pytest.mark.parametrize("case", [
     ((2, 8, 8, 8, 32), 25, "none", True),       # segmentation classifier class: 32 -> 25 (+bias)
     ((4, 1, 14, 14, 24), 48, "relu", True),     # K % 8 == 0, N > 32
     ((2, 1, 8, 9, 6), 40, "none", False),       # 6 input channels: rows straddle 16-B chunks
