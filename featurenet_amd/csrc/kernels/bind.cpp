@@ -89,7 +89,7 @@ int fn_conv_tile_f8_supported(int, int, int);
 int fn_conv_wtile(const void*, const void*, float*, float*, const void*, const void*, const void*, const int*, int, int,
                   int*, hipStream_t);
 int fn_conv_wtile_supported(int, int);
-int fn_tile_pack_w(const float*, void*, int, int, int, int, int, int, int, int, hipStream_t);
+int fn_tile_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 }
 
 template <typename T>
@@ -284,8 +284,8 @@ PYBIND11_MODULE(_C, m) {
     return fn_conv_tile_workers(geom.data(), ncol, NT);
   });
   m.def("tile_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int CS, int nks, int nct, int nslice,
-                          int dgrad, uintptr_t st) {
-    chk(fn_tile_pack_w(P<const float*>(w), P<void*>(out), K, T, C, CS, nks, nct, nslice, dgrad, S(st)),
+                          int dgrad, uintptr_t st, int nt) {
+    chk(fn_tile_pack_w(P<const float*>(w), P<void*>(out), K, T, C, CS, nks, nct, nslice, dgrad, nt, S(st)),
         "tile_pack_w");
   });
   m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {

@@ -66,7 +66,8 @@ struct TileGeom {
 
 #define CT_NCW 4                       // compute (MFMA) waves
 #define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
-#define CT_RED_BYTES (CT_NCW * 2 * 32 * 4)   // per-compute-wave BN sums of 32 columns (NT = 2)
+// per-compute-wave BN sums of the workgroup's NT*16 columns
+__host__ __device__ constexpr int ct_red_bytes(int NT) { return CT_NCW * 2 * NT * 16 * 4; }
 
 // packed bf16 pairs (low half = element 0)
 __device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }
@@ -91,7 +92,7 @@ typedef int ct_i32x8 __attribute__((ext_vector_type(8)));
 
 // B-ring depth (k-steps in flight): a bf16 k-step is MT*NT 16-cycle MFMAs, an fp8 one
 // MT*NT 32-cycle block-scaled MFMAs, so 2 fp8 steps cover the latency 4 bf16 steps do
-__host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : (NT == 2 ? 4 : 3); }
+__host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : (NT == 2 ? 4 : 2); }
 
 // F8 = false: bf16 operands, v_mfma_f32_16x16x32_bf16, k-step 32; CPP = 16-B chunks (8
 //   channels) per halo position.
@@ -119,7 +120,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   constexpr int PD = ct_pd(NT, F8);
   constexpr int ESZ = F8 ? 1 : 2;                // bytes per element of the source / weights
   constexpr int FRAG = F8 ? 32 : 16;             // bytes per lane of one MFMA operand fragment
-  static_assert(NT == 2, "column order and s_red assume 32-column blocks");
+  // NT = 2: 32-column blocks (a lane stores 8 consecutive columns); NT = 4 (bf16, Ncol % 64 ==
+  // 0): 64 columns per workgroup, each halo fragment read feeds 4 MFMAs instead of 2 -- the
+  // one-wave-per-SIMD k-loop was issue-bound at 2 (one ds_read_b128 + address add per MFMA
+  // pair); a lane then stores 16 consecutive columns and the bias is read from LDS
+  static_assert(NT == 2 || (NT == 4 && !F8 && !BWS), "32-column blocks, or 64 for the plain bf16 kernel");
+  constexpr int RC = NT * 16;                    // columns of the workgroup (BN partial row length)
+  constexpr int NV = 4 * NT;                     // consecutive columns per lane in the epilogue
   static_assert(!F8 || CPP == 2 || CPP == 4, "fp8: 32- or 64-channel slices");
   using Frag = std::conditional_t<F8, ct_i32x8, bf16x8>;
 
@@ -138,20 +145,26 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   const bool loader = wave == CT_NCW;
   const int lr = lane & 15, lg = lane >> 4;
   const int ct0 = blockIdx.y * NT;               // first 16-column tile of this workgroup
-  // LDS: [buffer 0][buffer 1][job slots 64 B][BN partials][k-step offsets (nks+PD+2) int2]
+  // LDS: [buffer 0][buffer 1][job slots 64 B][BN partials][k-step offsets (nks+PD+2) int4]
   // [halo positions HPpad int2: (byte offset from the halo origin, packed hd|hh|hw)]
   int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);                    // [2][2] (tile, slice) by parity
   float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);           // [4 waves][2][32] BN partials
-  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + CT_RED_BYTES);
+  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + ct_red_bytes(NT));
   int2* s_pos = reinterpret_cast<int2*>(s_kt + (nks + PD + 2));
   for (int i = tid; i < nks + PD + 2; i += CT_NTHR) s_kt[i] = ktab[i];
-  for (int i = tid; i < CT_RED_BYTES / 4; i += CT_NTHR) s_red[i] = 0.f;
+  for (int i = tid; i < ct_red_bytes(NT) / 4; i += CT_NTHR) s_red[i] = 0.f;
   // BWS: the BN's (scale, shift, mean, invstd) of this workgroup's 32 columns, read per use by
   // the epilogue (no live registers across the k-loop)
   float4* s_bn = reinterpret_cast<float4*>(s_pos + g.HPpad);
   // F8: the dequantisation scale and bias of this workgroup's 32 columns ([scale 32][bias 32]),
   // read by the epilogue from LDS (global loads there serialised every tile's stores)
   float* s_sb = reinterpret_cast<float*>(s_pos + g.HPpad);
+  if constexpr (NT == 4) {                       // (NT = 4: the bias, [64])
+    if (tid < RC) {
+      const int c = blockIdx.y * RC + tid;
+      s_sb[tid] = (bias && c < Ncol) ? bias[c] : 0.f;
+    }
+  }
   if constexpr (F8) {
     if (tid < NT * 16) {
       const int c = blockIdx.y * NT * 16 + tid;
@@ -320,11 +333,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                                                  // after the NT MFMAs of (mt, k) consumed it
     Frag fb[PD][NT];
     // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
-    // ct0*16 + 8lg + 4nt + r: a lane ends with 8 consecutive columns of one position
-    const int gc8 = ct0 * 16 + 8 * lg;
-    float bias8[8];                              // (fp8: re-read per tile in the epilogue, no live
-#pragma unroll                                   // registers across the k-loop)
-    for (int j = 0; j < 8; ++j) bias8[j] = (!F8 && !BWS && bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
+    // ct0*16 + 4*NT*lg + 4nt + r: a lane ends with NV = 4*NT consecutive columns of one position
+    const int gc8 = ct0 * 16 + NV * lg;
+    float bias8[8];                              // (fp8 / NT = 4: read in the epilogue from LDS, no
+#pragma unroll                                   // live registers across the k-loop)
+    for (int j = 0; j < 8; ++j) bias8[j] = (NT == 2 && !F8 && !BWS && bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
     constexpr unsigned FTILE = 64u * FRAG;       // bytes of one 16-column fragment of a k-step
     const unsigned wstep = (unsigned)g.nct * FTILE;   // bytes per k-step of the packed weights
     unsigned voffb[PD];                          // per-lane B offsets of the PD ring slots
@@ -442,9 +455,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
           constexpr bool BW = (M & 4) != 0;
           constexpr bool RELU_OUT = !BW && (M & 2) != 0;
           constexpr bool ST = BW || (M & 1) != 0;
-          float ts[8], tq[8];                    // this tile's BN partial sums of the lane's 8 columns
-#pragma unroll
-          for (int j = 0; j < 8; ++j) ts[j] = tq[j] = 0.f;
           bool okm[MT];
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
@@ -474,53 +484,62 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
               bsh[j] = q.y;
             }
           }
+          // one pass per 8 consecutive columns of the lane (fragments 2h, 2h+1): one 16-B store
+          // per row and 8 + 8 live partial sums (NT = 4 with all 16 columns' sums live spilled)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const bool ok = okm[mt];
-            float v[8];
+          for (int h = 0; h < NT / 2; ++h) {
+            float ts[8], tq[8];                  // this tile's BN partial sums of the pass's 8 columns
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              v[j] = bf16_lo(bf16x2_pack(acc[mt][j >> 2][j & 3] + bias8[j], 0.f));   // the stored bf16 value
-              if constexpr (RELU_OUT) v[j] = fmaxf(v[j], 0.f);
-            }
-            if constexpr (BW) {
-              if (mt == MH) load_y(MH);
-              const uint4 yq = yb[mt % MH];
-              const unsigned yw[4] = {yq.x, yq.y, yq.z, yq.w};
+            for (int j = 0; j < 8; ++j) ts[j] = tq[j] = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) {
+              const bool ok = okm[mt];
+              float v[8];
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
-                const float y = (j & 1) ? bf16_hi(yw[j >> 1]) : bf16_lo(yw[j >> 1]);
-                float gv = ok ? v[j] : 0.f;
-                if constexpr ((M & 2) != 0) gv = (y * bsc[j] + bsh[j]) > 0.f ? gv : 0.f;
-                ts[j] += gv;
-                tq[j] += gv * y;
+                const float b = NT == 2 ? bias8[j] : s_sb[NV * lg + 8 * h + j];
+                v[j] = bf16_lo(bf16x2_pack(acc[mt][2 * h + (j >> 2)][j & 3] + b, 0.f));   // the stored bf16 value
+                if constexpr (RELU_OUT) v[j] = fmaxf(v[j], 0.f);
               }
-            } else if constexpr (ST) {
+              if constexpr (BW) {
+                if (mt == MH) load_y(MH);
+                const uint4 yq = yb[mt % MH];
+                const unsigned yw[4] = {yq.x, yq.y, yq.z, yq.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                  const float y = (j & 1) ? bf16_hi(yw[j >> 1]) : bf16_lo(yw[j >> 1]);
+                  float gv = ok ? v[j] : 0.f;
+                  if constexpr ((M & 2) != 0) gv = (y * bsc[j] + bsh[j]) > 0.f ? gv : 0.f;
+                  ts[j] += gv;
+                  tq[j] += gv * y;
+                }
+              } else if constexpr (ST) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                  const float x = ok ? v[j] : 0.f;
+                  ts[j] += x;
+                  tq[j] += x * x;
+                }
+              }
+              if (ok)
+                *(uint4*)(obase + (long long)roff[mt] * Ncol + 8 * h) = make_uint4(
+                    bf16x2_pack(v[0], v[1]), bf16x2_pack(v[2], v[3]), bf16x2_pack(v[4], v[5]), bf16x2_pack(v[6], v[7]));
+              acc[mt][2 * h] = (f32x4){0.f, 0.f, 0.f, 0.f};
+              acc[mt][2 * h + 1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+            }
+            if constexpr (ST) {
+              // over the 16 lanes holding the same columns (DPP), into the wave's LDS sums
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
-                const float x = ok ? v[j] : 0.f;
-                ts[j] += x;
-                tq[j] += x * x;
+                ts[j] = ct_sum16(ts[j]);
+                tq[j] = ct_sum16(tq[j]);
               }
-            }
-            if (ok)
-              *(uint4*)(obase + (long long)roff[mt] * Ncol) = make_uint4(
-                  bf16x2_pack(v[0], v[1]), bf16x2_pack(v[2], v[3]), bf16x2_pack(v[4], v[5]), bf16x2_pack(v[6], v[7]));
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-          }
-          if constexpr (ST) {
-            // over the 16 lanes holding the same columns (DPP), into the wave's LDS sums
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              ts[j] = ct_sum16(ts[j]);
-              tq[j] = ct_sum16(tq[j]);
-            }
-            if (lr == 0) {                       // one lane per column of this wave's row: plain
+              if (lr == 0) {                     // one lane per column of this wave's row: plain
 #pragma unroll                                   // adds, a fixed summation order (deterministic
-              for (int j = 0; j < 8; ++j) {      // statistics, run to run)
-                s_red[wave * 64 + 8 * lg + j] += ts[j];
-                s_red[wave * 64 + 32 + 8 * lg + j] += tq[j];
+                for (int j = 0; j < 8; ++j) {    // statistics, run to run)
+                  s_red[wave * 2 * RC + NV * lg + 8 * h + j] += ts[j];
+                  s_red[wave * 2 * RC + RC + NV * lg + 8 * h + j] += tq[j];
+                }
               }
             }
           }
@@ -601,12 +620,12 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       par ^= 1;
     }
     tile_lds_barrier();                          // R
-    if (!F8 && stats && tid < NT * 16 && ct0 * 16 + tid < Ncol) {
+    if (!F8 && stats && tid < RC && ct0 * 16 + tid < Ncol) {
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int w = 0; w < CT_NCW; ++w) {
-        s1 += s_red[w * 64 + tid];
-        s2 += s_red[w * 64 + 32 + tid];
+        s1 += s_red[w * 2 * RC + tid];
+        s2 += s_red[w * 2 * RC + RC + tid];
       }
       float* row = stats + (long long)blockIdx.x * 2 * Ncol;   // this workgroup's slab row
       row[ct0 * 16 + tid] = s1;
@@ -967,7 +986,7 @@ __global__ __launch_bounds__(512, 1) void conv_tile8_kernel(const unsigned char*
 // zero for tap >= T or col >= Ncol.
 __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restrict__ w, uint4* __restrict__ out, int K,
                                                           int T, int C, int CS, int nks, int nct, int nslice,
-                                                          int dgrad) {
+                                                          int dgrad, int nt) {
   const long long total = ((long long)nslice * nks + 4) * nct * 64;   // + the ring's 4 zero k-steps
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
@@ -982,11 +1001,11 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
   const int ks = (int)(r % nks);
   const int slice = (int)(r / nks);
   const int Ncol = dgrad ? C : K;
-  // column order inside each 32-column block: fragment ct&1, row i holds output column
-  // 8*(i/4) + 4*(ct&1) + i%4, so after the kernel's C^T MFMA a lane's two fragments give 8
-  // consecutive output columns (one 16-B store)
+  // column order inside each nt*16-column block: fragment ct%nt, row i holds output column
+  // 4nt*(i/4) + 4*(ct%nt) + i%4, so after the kernel's C^T MFMA a lane's nt fragments give 4nt
+  // consecutive output columns (one 16-B store per 8)
   const int fi = lane & 15;
-  const int col = (ct >> 1) * 32 + 8 * (fi >> 2) + 4 * (ct & 1) + (fi & 3);
+  const int col = (ct / nt) * nt * 16 + 4 * nt * (fi >> 2) + 4 * (ct % nt) + (fi & 3);
   int tap, ch0;
   if (CS >= 32) {
     const int sub = CS / 32;
@@ -1013,11 +1032,12 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
 }
 
 extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, int CS, int nks, int nct, int nslice,
-                              int dgrad, hipStream_t st) {
+                              int dgrad, int nt, hipStream_t st) {
   if (CS != 8 && CS != 16 && CS % 32 != 0) return -2;
+  if ((nt != 2 && nt != 4) || nct % nt) return -2;
   const long long total = ((long long)nslice * nks + 4) * nct * 64;
   hipLaunchKernelGGL(tile_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (uint4*)out, K, T,
-                     C, CS, nks, nct, nslice, dgrad);
+                     C, CS, nks, nct, nslice, dgrad, nt);
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -1075,7 +1095,8 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
 }
 
 // instantiations (MT, NT, CPP) -- the Python planner only emits these
-#define CT_INSTANCES(X) X(8, 2, 1) X(9, 2, 1) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4)
+#define CT_INSTANCES(X) X(8, 2, 1) X(9, 2, 1) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4) \
+  X(6, 4, 2) X(6, 4, 4) X(7, 4, 2) X(7, 4, 4) X(8, 4, 2) X(8, 4, 4)
 
 extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 #define CT_SUP(M, N, C) if (MT == M && NT == N && CPP == C) return 1;
@@ -1086,8 +1107,8 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, bool bws = false) {
   const int PD = ct_pd(NT, f8);
-  return 2 * (size_t)g.BUF + 64 + CT_RED_BYTES + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
-         (bws ? (size_t)NT * 16 * 16 : 0) + (f8 ? (size_t)NT * 16 * 8 : 0);
+  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
+         (bws ? (size_t)NT * 16 * 16 : 0) + (f8 ? (size_t)NT * 16 * 8 : 0) + (NT == 4 ? (size_t)NT * 16 * 4 : 0);
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -1111,7 +1132,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   const long long HP = (g.TD + g.KD - 1) * HH * HW;
   if (g.HPpad < HP || g.HPpad % 64) return -3;
   if (g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;   // packed 8-bit hd/hh/hw
-  const int PD = NT == 2 ? 4 : 3;
+  const int PD = ct_pd(NT, false);
   const int T = g.KD * g.KH * g.KW;
   const int need_ks = g.CS >= 32 ? T * (g.CS / 32) : (g.CS == 16 ? (T + 1) / 2 : (T + 3) / 4);
   if (g.nks % PD || g.nks < need_ks || g.nct < (Ncol + 15) / 16) return -3;
@@ -1132,6 +1153,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
   if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;   // 16-B column groups; relu or none
+  if (NT == 4 && (Ncol % 64 || bny)) return -2;                        // whole 64-column blocks, no BWS
   if ((bny != nullptr) != (bnp != nullptr) || (bny && (!stats || bias))) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
@@ -1164,7 +1186,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   }
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
-    rc = bny ? launch_tile<M, N, C, 0, false, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,    \
+    rc = bny ? launch_tile<M, N, C, 0, false, N == 2>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,  \
                                                     (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, \
                                                     nullptr, nullptr, 0.f, bny, bnp)                              \
              : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab,  \

@@ -32,8 +32,22 @@ from .. import _native
 
 LDS_MAX = 160 * 1024
 NTHR = 320          # 4 MFMA waves + 1 loader wave
-RED_BYTES = 4 * 2 * 32 * 4   # per-compute-wave BN sums in LDS
 MT_CHOICES = (8, 9)
+MT_CHOICES_NT4 = (6, 7)     # 64-column instances (register budget of 5 waves per CU: 256 VGPRs)
+
+
+def red_bytes(NT: int) -> int:
+    """LDS bytes of the per-compute-wave BN partial sums (4 waves x 2 x NT*16 columns)."""
+    return 4 * 2 * NT * 16 * 4
+
+
+def tile_nt() -> str:
+    """FN_TILE_NT: '4' plans 64-column workgroups (NT = 4) whenever Ncol % 64 == 0; '2'
+    (default) 32-column ones only.  NT = 4 halves the halo reads and DMA per MFMA but measured
+    3-4 % slower on conv3 / conv4 (fwd 375 / 261 vs 365 / 251 us, conv4 dgrad 304 vs 295): the
+    k-loop is not bound by the halo reads, and the 64-column instance only fits 96-112 rows
+    per wave in the 256 VGPRs of a 5-wave workgroup (ring depth 2)."""
+    return os.environ.get("FN_TILE_NT", "2")
 _LOCK = threading.Lock()
 _PLANS: dict = {}
 _ROWTAB: dict = {}
@@ -96,7 +110,7 @@ def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int
     ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply
     (``f8``: the e4m3 inference variant, 32- or 64-channel slices)."""
     nw = 4 if f8 else nwaves()
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, nw)
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, nw, tile_nt())
     if key in _PLANS:
         return _PLANS[key]
     best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, nw)
@@ -113,14 +127,17 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4):
     T = KD * KH * KW
     if Ncol < 16 or Ncol % 8 or Csrc % 8 or T < 2:
         return None
-    NT = 2                                       # 32-column blocks (register budget: 5 waves per CU)
+    # NT = 2: 32-column workgroups; NT = 4 (plain bf16, Ncol % 64 == 0): 64 columns, every halo
+    # fragment read feeds 4 MFMAs (the 2-MFMA k-loop is issue-bound), half the halo DMA per column
+    nt_mode = tile_nt()
+    NT = 4 if (not f8 and nw == 4 and Ncol % 64 == 0 and nt_mode == "4") else 2
     ncb = -(-Ncol // (NT * 16))
     nct = ncb * NT
     PD = PD_F8 if f8 else 4
     workers = max(1, n_cus // ncb)
     cands = []
     cs_only = int(os.environ.get("FN_TILE_CS", "0"))
-    mt_choices = (8,) if (f8 or nw == 8) else MT_CHOICES
+    mt_choices = (8,) if (f8 or nw == 8) else (MT_CHOICES_NT4 if NT == 4 else MT_CHOICES)
     for CS in ((64, 32) if f8 else (32, 16, 8)):
         if Csrc % CS or (cs_only and CS != cs_only) or (CS == 8 and Csrc % 16 == 0):
             continue
@@ -148,7 +165,8 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4):
                         if BUF < 16384:                 # (the split-K exchange: 16 KiB rounds)
                             continue
                     else:
-                        lds = 2 * BUF + 64 + RED_BYTES + (nks + PD + 2) * 16 + HPpad * 8 + (NT * 16 * 8 if f8 else 0)
+                        lds = 2 * BUF + 64 + red_bytes(NT) + (nks + PD + 2) * 16 + HPpad * 8 + (NT * 16 * 8 if f8 else 0) \
+                            + (NT * 16 * 4 if NT == 4 else 0)
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
@@ -326,7 +344,7 @@ def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bo
     out = torch.empty((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
     wf = w.detach().float().contiguous()
     _native.kernels().tile_pack_w(wf.data_ptr(), out.data_ptr(), K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad),
-                                  _native.stream(wf))
+                                  _native.stream(wf), p.NT)
     return out
 
 
@@ -379,8 +397,9 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None):
                     (spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw))
     wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
-    lds_bws = 2 * p.BUF + 64 + RED_BYTES + (p.nks + PD + 2) * 16 + p.HPpad * 8 + p.NT * 16 * 16
-    if bn is None or lds_bws > LDS_MAX:          # (the statistics instance keeps the BN scale/shift in LDS)
+    lds_bws = 2 * p.BUF + 64 + red_bytes(p.NT) + (p.nks + PD + 2) * 16 + p.HPpad * 8 + p.NT * 16 * 16
+    if bn is None or lds_bws > LDS_MAX or p.NT != 2:   # (the statistics instance: 32-column blocks, BN
+        # scale/shift in LDS)
         run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
         return dx if bn is None else (dx, None)
     y, prm, act = bn

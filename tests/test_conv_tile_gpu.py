@@ -31,15 +31,19 @@ CASES = [
     (24, 22, 22, 22, 64, 64, (3, 3, 3), "valid"),    # conv4, 2 slices per tile, 384 tiles
     (3, 11, 12, 13, 16, 48, (3, 3, 3), "same"),      # same padding, 48 columns (partial NT=4 block)
     (2, 9, 10, 11, 32, 96, (3, 3, 3), "same"),       # 2 column blocks
+    (2, 9, 10, 11, 32, 128, (3, 3, 3), "same"),      # 2 column blocks of 64 (NT = 4)
     (4, 1, 40, 37, 32, 32, (1, 5, 5), "same"),       # 2-D conv
     (6, 32, 32, 32, 8, 32, (4, 4, 4), "valid"),      # FeatureNet-3D stem after space-to-depth (CS = 8)
     (3, 10, 11, 12, 8, 16, (3, 3, 3), "same"),       # CS = 8, 27 taps (last k-step partial), padding
 ]
 
 
+@pytest.mark.parametrize("nt", ["4", "2"])
 @pytest.mark.parametrize("case", CASES)
-def test_conv_tile_fwd_dgrad(case):
+def test_conv_tile_fwd_dgrad(case, nt, monkeypatch):
+    """nt = 4: 64-column workgroups (NT = 4) where Ncol % 64 == 0; 2: 32-column ones only."""
     assert _native.kernels_available(), "HIP kernel library (_C) must be built and loadable on the GPU box"
+    monkeypatch.setenv("FN_TILE_NT", nt)
     N, D, H, W, C, K, k, pad = case
     torch.manual_seed(0)
     dev = "cuda"
@@ -49,6 +53,7 @@ def test_conv_tile_fwd_dgrad(case):
     b = torch.randn(K, device=dev) * 0.1
     pf, pd = ct.fwd_plan(spec), ct.dgrad_plan(spec)
     assert pf is not None and (pd is not None or C < 16), (pf, pd)   # dgrad needs >= 16 output columns
+    assert pf.NT == (4 if nt == "4" and K % 64 == 0 else 2), pf
 
     # forward with bias + relu
     y, _ = ct.conv_fwd(x, w, b, spec, 1, False, pf)

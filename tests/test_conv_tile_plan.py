@@ -14,7 +14,8 @@ def test_plans_fit_lds_and_cover_rows(out, k, c, n):
     p = ct.plan(128, out, k, c, n)
     assert p is not None
     assert p.BUF >= p.HPpad * (p.CS // 8) * 16
-    assert 2 * p.BUF + 64 + ct.RED_BYTES + (p.nks + ct.PD + 2) * 8 + p.HPpad * 8 <= ct.LDS_MAX
+    assert 2 * p.BUF + 64 + ct.red_bytes(p.NT) + (p.nks + ct.PD + 2) * 16 + p.HPpad * 8 + 256 <= ct.LDS_MAX
+    assert p.NT == 2
     HP = (p.TD + k[0] - 1) * (p.TH + k[1] - 1) * (p.TW + k[2] - 1)
     assert p.HPpad >= HP and p.HPpad % 64 == 0
     tab = ct.row_table(p, k)
@@ -59,7 +60,7 @@ def test_fp8_plans_and_weight_stream(out, k, c, n):
     T = k[0] * k[1] * k[2]
     tps = 128 // p.CS
     assert p.nks % ct.PD_F8 == 0 and p.nks * tps >= T
-    assert 2 * p.BUF + 64 + ct.RED_BYTES + (p.nks + ct.PD_F8 + 2) * 16 + p.HPpad * 8 <= ct.LDS_MAX
+    assert 2 * p.BUF + 64 + ct.red_bytes(p.NT) + (p.nks + ct.PD_F8 + 2) * 16 + p.HPpad * 8 <= ct.LDS_MAX
     g = torch.Generator().manual_seed(0)
     wq = torch.randint(1, 255, (n, T, c), generator=g, dtype=torch.uint8)
     wpk = ct.pack_weights_f8(wq, p)
