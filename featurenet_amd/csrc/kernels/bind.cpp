@@ -47,6 +47,7 @@ int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, floa
 int fn_dense_wgrad_slices(int, int, int);
 int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
+int fn_igemm_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
                    hipStream_t);
 int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
@@ -287,6 +288,13 @@ PYBIND11_MODULE(_C, m) {
                           int dgrad, uintptr_t st, int nt) {
     chk(fn_tile_pack_w(P<const float*>(w), P<void*>(out), K, T, C, CS, nks, nct, nslice, dgrad, nt, S(st)),
         "tile_pack_w");
+  });
+  m.def("igemm_pack_w", [](uintptr_t w, uintptr_t out, int K0, int C0, int K, int T, int C, int mode, int ld, int KW,
+                           int R, uintptr_t st, std::vector<long long> ext) {
+    // ext = {numel(w), numel(out)}
+    fits(ext, 0, (long long)K0 * T * C0, "igemm_pack_w", "w");
+    fits(ext, 1, (long long)(mode == 1 ? C : K) * ld, "igemm_pack_w", "out");
+    chk(fn_igemm_pack_w(P<const float*>(w), P<void*>(out), K0, C0, K, T, C, mode, ld, KW, R, S(st)), "igemm_pack_w");
   });
   m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {
     chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K, T, C, mode, stage_k, S(st)), "halo_pack_w");

@@ -594,3 +594,51 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const 
   FN_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// B-operand packing for the gather kernels: fp32 weight -> bf16 rows in one launch
+// (cast + transpose + zero padding of rows / channels / the row stride).
+// ---------------------------------------------------------------------------
+// w: fp32 [K0][T][C0] (the parameter, possibly fewer output / input channels than the
+// conv runs with).  out: bf16 [rows][ld] with
+//   mode 0 (forward): rows = K, element (k, t*C + c) = w[k][t][c]; kdim = T*C
+//   mode 1 (dgrad):   rows = C, element (c, t*K + k) = w[k][t][c] (the dgrad gather table
+//                     walks the taps mirrored itself)
+//   mode 2 (packed-W forward, C < 8): rows = K, row k = [KD*KH][R] with R >= KW*C, element
+//                     (k, r*R + p) = w[k][r*KW + p / C][p % C] for p < KW*C
+// and zeros for k >= K0, c >= C0 and the padding columns.
+__global__ __launch_bounds__(256) void igemm_pack_w_kernel(const float* __restrict__ w, bf16* __restrict__ out,
+                                                           int K0, int C0, int K, int T, int C, int mode, int ld,
+                                                           int KW, int R, long long total) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int row = (int)(i / ld), col = (int)(i % ld);
+  float v = 0.f;
+  if (mode == 0) {
+    const int t = col / C, c = col % C;
+    if (t < T && row < K0 && c < C0) v = w[((long long)row * T + t) * C0 + c];
+  } else if (mode == 1) {
+    const int t = col / K, k = col % K;
+    if (t < T && k < K0 && row < C0) v = w[((long long)k * T + t) * C0 + row];
+  } else {
+    const int r = col / R, p = col % R;
+    if (p < KW * C && row < K0) {
+      const int t = r * KW + p / C, c = p % C;
+      if (t < T && c < C0) v = w[((long long)row * T + t) * C0 + c];
+    }
+  }
+  out[i] = f2bf(v);
+}
+
+extern "C" int fn_igemm_pack_w(const float* w, void* out, int K0, int C0, int K, int T, int C, int mode, int ld, int KW,
+                               int R, hipStream_t st) {
+  if (K0 <= 0 || C0 <= 0 || K0 > K || C0 > C || T <= 0 || mode < 0 || mode > 2 || ld <= 0) return -2;
+  const int rows = mode == 1 ? C : K;
+  const long long need = mode == 0 ? (long long)T * C : (mode == 1 ? (long long)T * K : (long long)(T / KW) * R);
+  if (ld < need || (mode == 2 && (KW <= 0 || T % KW || R < KW * C || ld != (T / KW) * R))) return -2;
+  const long long total = (long long)rows * ld;
+  hipLaunchKernelGGL(igemm_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (bf16*)out, K0, C0,
+                     K, T, C, mode, ld, KW, R, total);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

@@ -212,7 +212,7 @@ class BatchNormActPointwiseFn(torch.autograd.Function):
         bias = b.detach().float().contiguous() if b is not None else None
         out = pw_fwd(y2, w2, bias, 0, pro=(prm[2], prm[3], act))
         ctx.save_for_backward(y, prm, w)
-        ctx.act, ctx.has_b = act, b is not None
+        ctx.act, ctx.has_b, ctx.bparam = act, b is not None, b
         ctx.params = (beta, gamma)
         return out.reshape(*y.shape[:-1], N)
 
@@ -226,8 +226,9 @@ class BatchNormActPointwiseFn(torch.autograd.Function):
         y2 = y.reshape(-1, C)
         d2 = dout.contiguous().to(torch.bfloat16).reshape(-1, N)
         w2 = w.detach().reshape(N, C)
-        dw = pw_wgrad(d2, y2, pro=(prm[2], prm[3], ctx.act)).reshape(w.shape) if ctx.needs_input_grad[9] else None
-        db = native_colsum(d2) if (ctx.has_b and ctx.needs_input_grad[10]) else None
+        dw = (pw_wgrad(d2, y2, pro=(prm[2], prm[3], ctx.act), out=grad_target(w)).reshape(w.shape)
+              if ctx.needs_input_grad[9] else None)
+        db = native_colsum(d2, out=grad_target(ctx.bparam)) if (ctx.has_b and ctx.needs_input_grad[10]) else None
         M = y2.shape[0]
         Kn = _native.kernels()
         part = None

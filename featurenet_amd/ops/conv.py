@@ -94,8 +94,36 @@ def kdim_gather(spec: ConvSpec) -> int:
     return spec.KD * spec.KH * packw_row(spec) if gather_mode(spec) == GM_PACKW else spec.kdim
 
 
+def _native_pack(w: torch.Tensor, spec: ConvSpec, mode: int) -> tuple[torch.Tensor, int]:
+    """One igemm_pack_w launch: fp32 ``w`` [K0, KD, KH, KW, C0] (K0 <= spec.K, C0 <= spec.C: the
+    missing rows / channels are zeros) -> the bf16 B rows of mode 0 (forward), 1 (dgrad:
+    [C][taps*K]) or 2 (packed-W forward), row stride padded to 8."""
+    wf = w.detach().float().contiguous()
+    T = spec.taps
+    if mode == 2:
+        R = packw_row(spec)
+        ld = spec.KD * spec.KH * R
+    else:
+        R = 0
+        ld = ((T * (spec.K if mode == 1 else spec.C)) + 7) // 8 * 8
+    rows = spec.C if mode == 1 else spec.K
+    out = torch.empty(rows, ld, dtype=torch.bfloat16, device=w.device)
+    _native.kernels().igemm_pack_w(wf.data_ptr(), out.data_ptr(), wf.shape[0], wf.shape[-1], spec.K, T, spec.C, mode, ld,
+                                   spec.KW, R, _native.stream(wf), [wf.numel(), out.numel()])
+    return out, ld
+
+
+def pad_to_spec(w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    """``w`` zero-padded to ``spec``'s output / input channel counts (no copy when they match)."""
+    return pad_weight(w, cin=spec.C, cout=spec.K)
+
+
 def pack_weight_rows(w: torch.Tensor, spec: ConvSpec) -> tuple[torch.Tensor, int]:
-    """Forward B operand [Cout, Kdim'] in the gather layout of ``spec``."""
+    """Forward B operand [Cout, Kdim'] in the gather layout of ``spec`` (``w`` may have fewer
+    output / input channels than ``spec``: zero rows / channels)."""
+    if w.is_cuda and _native.kernels_available():
+        return _native_pack(w, spec, 2 if gather_mode(spec) == GM_PACKW else 0)
+    w = pad_to_spec(w, spec)
     if gather_mode(spec) == GM_PACKW:
         R = packw_row(spec)
         out = torch.zeros(spec.K, spec.KD * spec.KH, R, dtype=torch.bfloat16, device=w.device)
@@ -403,7 +431,10 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
 def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=None):
     """dx of the conv.  ``bn = (y, prm, act)`` (x was a BN+act output, :mod:`.bnfuse`): returns
     ``(dx, slab)`` where ``slab`` holds that BN's backward sums from the tile kernel's
-    epilogue, or None when another kernel ran."""
+    epilogue, or None when another kernel ran.  ``w`` may have fewer output channels than
+    ``spec.K`` (channel-padded dy): zero rows, materialised only for the tile / halo kernels."""
+    if w.shape[0] != spec.K and (conv_tile.dgrad_plan(spec) is not None or halo_dgrad_plan(spec) is not None):
+        w = pad_to_spec(w, spec)
     if bn is not None:
         tplan = conv_tile.dgrad_plan(spec)
         plan = halo_dgrad_plan(spec)
@@ -431,9 +462,13 @@ def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=Non
     dy5 = dy5.contiguous()
     vec = GM_VEC if spec.K % 8 == 0 else GM_SCALAR
     tab = _table(spec, "dgrad", vec == GM_VEC, dy5.device)
-    # WT[ci][tap][co] = w[co][tap][ci]
-    wt = w.reshape(spec.K, spec.taps, spec.C).permute(2, 1, 0).reshape(spec.C, spec.taps * spec.K)
-    wt, ldw = _pack_rows(wt)
+    # WT[ci][tap][co] = w[co][tap][ci] (one cast + transpose launch; missing rows of w are zeros)
+    if w.is_cuda:
+        wt, ldw = _native_pack(w, spec, 1)
+    else:
+        w = pad_to_spec(w, spec)
+        wt = w.reshape(spec.K, spec.taps, spec.C).permute(2, 1, 0).reshape(spec.C, spec.taps * spec.K)
+        wt, ldw = _pack_rows(wt)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     M = spec.N * spec.D * spec.H * spec.W
     K.igemm_fwd(dy5.data_ptr(), wt.data_ptr(), 0, dx.data_ptr(), 0, tab.data_ptr(), _geom_dgrad(spec), M, spec.C,
@@ -466,26 +501,39 @@ def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=N
     tab = _table(spec, "fwd", gm, x5.device)
     splits = wgrad_splits(spec)
     kd = kdim_gather(spec)
-    dw = torch.zeros(spec.K, kd, dtype=torch.float32, device=x5.device)
+    # the kernel accumulates with atomics into a zeroed buffer: the flat gradient slice itself
+    # (``out``, zeroed by FlatParams) when the layouts agree
+    direct = (out is not None and gm != GM_PACKW and out.dtype == torch.float32 and out.is_contiguous()
+              and out.numel() == spec.K * kd)
+    dw = out.view(spec.K, kd) if direct else torch.zeros(spec.K, kd, dtype=torch.float32, device=x5.device)
     K.igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K,
                   kd, splits, gm, _native.stream(x5))
+    if direct:
+        return out
     if gm == GM_PACKW:
-        dw = dw.reshape(spec.K, spec.KD * spec.KH, -1)[:, :, : spec.KW * spec.C].contiguous()
-    return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
+        dw = dw.reshape(spec.K, spec.KD * spec.KH, -1)[:, :, : spec.KW * spec.C]
+    dw = dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
+    if out is not None:
+        return out.copy_(dw)
+    return dw.contiguous()
 
 
-def native_colsum(x2: torch.Tensor) -> torch.Tensor:
-    """Per-column sum of a [M, C] bf16 tensor in fp32 (bias gradients)."""
+def native_colsum(x2: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-column sum of a [M, C] bf16 tensor in fp32 (bias gradients); into ``out`` (fp32
+    [C], e.g. the bias's flat gradient slice) when given."""
     K = _native.kernels()
     M, C = x2.shape
     nb = int(max(1, min(1024, M // 64)))
     part = torch.empty(nb, 2, C, dtype=torch.float32, device=x2.device)
     st = _native.stream(x2)
     K.colstats(x2.data_ptr(), 0, 0, 0, 0, 0, part.data_ptr(), M, C, 0, 0, nb, st)
-    out = torch.empty(2, C, dtype=torch.float32, device=x2.device)
-    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, out[0].data_ptr(), out[1].data_ptr(), 0, 0,
+    tmp = torch.empty(2 if out is None else 1, C, dtype=torch.float32, device=x2.device)
+    if out is not None:
+        assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == C
+    o0 = out if out is not None else tmp[0]
+    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, o0.data_ptr(), tmp[-1].data_ptr(), 0, 0,
                   1, st)
-    return out[0]
+    return o0
 
 
 def native_act_bwd(dy: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
@@ -623,11 +671,15 @@ def pw_prologue_ok(K: int) -> bool:
     return K % 8 == 0 and 2048 % K == 0
 
 
-def pw_wgrad(dy2: torch.Tensor, x2: torch.Tensor, pro=None) -> torch.Tensor:
-    """fp32 dW [Nout, Kin] = dy^T x on the pointwise kernel (``pro``: as :func:`pw_fwd`)."""
+def pw_wgrad(dy2: torch.Tensor, x2: torch.Tensor, pro=None, out=None) -> torch.Tensor:
+    """fp32 dW [Nout, Kin] = dy^T x on the pointwise kernel (``pro``: as :func:`pw_fwd`); into
+    ``out`` (zeroed fp32 of N*Kin elements, e.g. the weight's flat gradient slice) when given."""
     M, N = dy2.shape
     Kin = x2.shape[1]
-    dw = torch.zeros(N, Kin, dtype=torch.float32, device=x2.device)
+    if out is not None and out.is_contiguous() and out.dtype == torch.float32 and out.numel() == N * Kin:
+        dw = out.view(N, Kin)
+    else:
+        dw = torch.zeros(N, Kin, dtype=torch.float32, device=x2.device)
     psc, psh, pact = pro if pro is not None else (None, None, 0)
     _native.kernels().pw_wgrad(dy2.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, Kin, N, _native.stream(x2),
                                _native.ptr(psc), _native.ptr(psh), pact)
@@ -673,13 +725,17 @@ def _conv_bwd_padded(ctx, dy, xs, w, spec):
     dyp = pad_channels(dy, kp)
     sk = dataclasses.replace(spec, K=kp)
     dx = dw = None
-    if ctx.x_needs:
-        wk = pad_weight(w.detach(), cout=kp)                     # real input channels: dx has C0 columns
-        dx = native_conv_dgrad(dyp, wk, dataclasses.replace(sk, C=C0))
+    if ctx.x_needs:                                              # real input channels: dx has C0 columns
+        dx = native_conv_dgrad(dyp, w.detach(), dataclasses.replace(sk, C=C0))   # (zero rows K0..kp)
     if ctx.needs_input_grad[1]:
-        dwp = native_conv_wgrad(dyp, xs.contiguous(), sk)         # [kp, KD, KH, KW, spec.C]
-        dw = dwp[:K0, ..., :C0].contiguous() if (kp != K0 or spec.C != C0) else dwp
-    db = native_colsum(dy.reshape(-1, K0)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        tgt = grad_target(w)
+        if kp != K0 or spec.C != C0:
+            dwp = native_conv_wgrad(dyp, xs.contiguous(), sk)     # [kp, KD, KH, KW, spec.C]
+            dw = tgt.copy_(dwp[:K0, ..., :C0]) if tgt is not None else dwp[:K0, ..., :C0].contiguous()
+        else:
+            dw = native_conv_wgrad(dyp, xs.contiguous(), sk, out=tgt)
+    db = (native_colsum(dy.reshape(-1, K0), out=grad_target(ctx.bparam))
+          if (ctx.has_b and ctx.needs_input_grad[2]) else None)
     return dx, dw, db, None, None, None
 
 
@@ -699,8 +755,8 @@ class ConvFn(torch.autograd.Function):
             # zero-padded copy instead of single elements; the padded copy is what wgrad reads
             cp = -(-spec.C // 8) * 8
             x5 = pad_channels(x5, cp)
-            w = pad_weight(w.detach(), cin=cp)
-            spec = dataclasses.replace(spec, C=cp)
+            spec = dataclasses.replace(spec, C=cp)              # (w keeps its C0 channels: zero-padded
+            #                                                     by the packing or pad_to_spec below)
             x_saved = x5
             ctx.cpad = cp
         if ctx.pw:
@@ -725,11 +781,13 @@ class ConvFn(torch.autograd.Function):
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
             x_saved = s2d_input(x5, f, spec2, (spec.pd, spec.ph, spec.pw)) if ctx.needs_input_grad[1] else x5
         elif halo_fwd_plan(spec) is not None or (conv_tile.fwd_plan(spec) is not None and act in (0, act_code("relu"))):
-            y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats, w=w.detach())
+            y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats,
+                                       w=pad_to_spec(w.detach(), spec))
         else:
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
         ctx.spec, ctx.act, ctx.has_b, ctx.s2d = spec, act, b is not None, s2d   # (channel-padded spec when cpad)
+        ctx.bparam = b
         ctx.set_materialize_grads(False)                # no zero-filled gradient for the stats output
         ctx.x_needs = ctx.needs_input_grad[0]
         # x = act(bn(y)) of the previous layer: the dgrad epilogue sums that BN's backward
@@ -753,8 +811,8 @@ class ConvFn(torch.autograd.Function):
         if ctx.pw:
             dy2, x2 = dy.reshape(-1, spec.K), x5.reshape(-1, spec.C)
             dx = pw_fwd(dy2, w.detach().reshape(spec.K, spec.C).t(), None, 0).reshape(x5.shape) if ctx.x_needs else None
-            dw = pw_wgrad(dy2, x2).reshape(w.shape) if ctx.needs_input_grad[1] else None
-            db = native_colsum(dy2) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+            dw = pw_wgrad(dy2, x2, out=grad_target(w)).reshape(w.shape) if ctx.needs_input_grad[1] else None
+            db = native_colsum(dy2, out=grad_target(ctx.bparam)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
             return dx, dw, db, None, None, None
         if ctx.cpad or (spec.K % 8 and ctx.s2d is None):
             return _conv_bwd_padded(ctx, dy, x5, w, spec)
@@ -775,7 +833,8 @@ class ConvFn(torch.autograd.Function):
             else:
                 # straight into the parameter's zeroed flat gradient when FlatParams offers it
                 dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w))
-        db = native_colsum(dy.reshape(-1, spec.K)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
+        db = (native_colsum(dy.reshape(-1, spec.K), out=grad_target(ctx.bparam))
+              if (ctx.has_b and ctx.needs_input_grad[2]) else None)
         return dx, dw, db, None, None, None
 
 
@@ -811,6 +870,7 @@ class DepthwiseFn(torch.autograd.Function):
         K.dw_fwd(x5.data_ptr(), wf.data_ptr(), _native.ptr(bias), y.data_ptr(), _dw_geom(spec), act,
                  _native.stream(x5))
         ctx.spec, ctx.act, ctx.has_b = spec, act, b is not None
+        ctx.wparam, ctx.bparam = w, b
         ctx.save_for_backward(x5, wf, y if act else None)
         return y
 
@@ -828,12 +888,17 @@ class DepthwiseFn(torch.autograd.Function):
             dx = torch.empty_like(x5)
             K.dw_dgrad(dy.data_ptr(), wf.data_ptr(), dx.data_ptr(), _dw_geom(spec), st)
         if ctx.needs_input_grad[1]:
-            dwf = torch.zeros(spec.C, spec.taps, dtype=torch.float32, device=x5.device)
+            tgt = grad_target(ctx.wparam)           # (zeroed flat slice: the kernel accumulates)
+            if tgt is not None and tgt.is_contiguous() and tgt.numel() == spec.C * spec.taps:
+                dwf = tgt.view(spec.C, spec.taps)
+            else:
+                dwf = torch.zeros(spec.C, spec.taps, dtype=torch.float32, device=x5.device)
             splits = int(max(1, min(256, spec.M // 2048)))
             K.dw_wgrad(dy.data_ptr(), x5.data_ptr(), dwf.data_ptr(), _dw_geom(spec), splits, st)
-            dw = dwf.reshape(spec.C, spec.KD, spec.KH, spec.KW, 1)
+            dw = tgt if dwf.data_ptr() == (tgt.data_ptr() if tgt is not None else -1) else \
+                dwf.reshape(spec.C, spec.KD, spec.KH, spec.KW, 1)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = native_colsum(dy.reshape(-1, spec.C))
+            db = native_colsum(dy.reshape(-1, spec.C), out=grad_target(ctx.bparam))
         return dx, dw, db, None, None
 
 

@@ -261,7 +261,7 @@ class SubpixelDecoderHeadFn(torch.autograd.Function):
         bias = hb.detach().float().contiguous() if hb is not None else None
         out = pw_fwd(y2, w2, bias, 0, pro=(prm[2], prm[3], act))
         ctx.save_for_backward(x, w, y, prm, hw)
-        ctx.act, ctx.has_b = act, hb is not None
+        ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
         ctx.params = (beta, gamma)
         return out.reshape(*y.shape[:-1], NC)
 
@@ -270,6 +270,7 @@ class SubpixelDecoderHeadFn(torch.autograd.Function):
         from .. import _native
         from . import bn as bn_ops
         from . import conv_wtile
+        from ..training.flat import grad_target
         from .conv import native_colsum, pw_fwd, pw_wgrad
 
         x, w, y, prm, hw = ctx.saved_tensors
@@ -278,8 +279,9 @@ class SubpixelDecoderHeadFn(torch.autograd.Function):
         y2 = y.reshape(-1, K)
         d2 = dout.contiguous().to(torch.bfloat16).reshape(-1, NC)
         w2 = hw.detach().reshape(NC, K)
-        dhw = pw_wgrad(d2, y2, pro=(prm[2], prm[3], ctx.act)).reshape(hw.shape) if ctx.needs_input_grad[9] else None
-        dhb = native_colsum(d2) if (ctx.has_b and ctx.needs_input_grad[10]) else None
+        dhw = (pw_wgrad(d2, y2, pro=(prm[2], prm[3], ctx.act), out=grad_target(hw)).reshape(hw.shape)
+               if ctx.needs_input_grad[9] else None)
+        dhb = native_colsum(d2, out=grad_target(ctx.bparam)) if (ctx.has_b and ctx.needs_input_grad[10]) else None
         M = y2.shape[0]
         Kn = _native.kernels()
         part = torch.empty(Kn.pw_fwd_blocks(M, NC, K), 2, K, dtype=torch.float32, device=y.device)

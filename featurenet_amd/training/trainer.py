@@ -70,6 +70,31 @@ class History:
             self.history.setdefault(k, []).append(v)
 
 
+
+class _EpochMetrics:
+    """Device-side running sums of an epoch's loss and correct predictions: one in-place add
+    each per step (the per-step reductions and casts were 5-7 tiny launches next to a NAS
+    candidate's ~50-kernel step), reduced once by :meth:`totals`."""
+
+    def __init__(self, device):
+        self.loss = torch.zeros((), dtype=torch.float64, device=device)
+        self.correct = None                      # int64 per-position counts (first batch's size)
+        self.extra = torch.zeros((), dtype=torch.int64, device=device)
+
+    def add(self, loss: torch.Tensor, corr: torch.Tensor, n: int) -> None:
+        self.loss.add_(loss.detach(), alpha=n)   # float64 += float32 * n in one kernel
+        c = corr.reshape(-1)
+        if self.correct is None and c.numel() <= 65536:
+            self.correct = torch.zeros(c.numel(), dtype=torch.int64, device=c.device)
+        if self.correct is not None and c.numel() <= self.correct.numel():
+            self.correct[:c.numel()].add_(c)
+        else:                                    # (per-voxel counts, or a batch larger than the first)
+            self.extra.add_(c.sum())
+
+    def totals(self):
+        corr = self.extra if self.correct is None else self.correct.sum() + self.extra
+        return self.loss, corr
+
 class Trainer:
     def __init__(self, model: torch.nn.Module, optimizer: str = "adam", lr: float = 1e-3, device=None,
                  keras_eps: bool = True, weight_decay: float = 0.0, momentum: float = 0.9,
@@ -235,17 +260,16 @@ class Trainer:
                     cb.on_epoch_begin(self, epoch)
                 self.model.train()
                 t0 = time.time()
-                loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
-                correct = torch.zeros((), dtype=torch.int64, device=self.device)
+                acc = _EpochMetrics(self.device)
                 seen = 0
                 for bi, (xb, yb) in enumerate(loader):
                     loss, corr = self.train_step(xb, yb)
-                    loss_sum += loss.double() * yb.numel()     # numel: per-voxel labels (segmentation)
-                    correct += corr.sum()
+                    acc.add(loss, corr, yb.numel())           # numel: per-voxel labels (segmentation)
                     seen += yb.numel()
                     if callbacks:
                         for cb in callbacks:
                             cb.on_batch_end(self, bi, {})
+                loss_sum, correct = acc.totals()
                 stats = self._reduce(torch.stack([loss_sum, correct.double(),
                                                   torch.tensor(float(seen), dtype=torch.float64, device=self.device)]))
                 logs = {"loss": float(stats[0] / max(stats[2], 1)), "acc": float(stats[1] / max(stats[2], 1)),
@@ -327,15 +351,14 @@ class Trainer:
         if loader is None:
             loader = DeviceLoader(x, y, batch_size, self.device, shuffle=False, packed_size=packed_size,
                                   rank=self.rank, world=self.world)
-        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
-        correct = torch.zeros((), dtype=torch.int64, device=self.device)
+        acc = _EpochMetrics(self.device)
         seen = 0
         for xb, yb in loader:
             logits = self.model(self._prep(xb))
             loss, corr = softmax_xent(logits, yb, with_correct=True)
-            loss_sum += loss.double() * yb.numel()
-            correct += corr.sum()
+            acc.add(loss, corr, yb.numel())
             seen += yb.numel()
+        loss_sum, correct = acc.totals()
         stats = self._reduce(torch.stack([loss_sum, correct.double(),
                                           torch.tensor(float(seen), dtype=torch.float64, device=self.device)]))
         self.model.train()
