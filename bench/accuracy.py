@@ -105,17 +105,22 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
         xb = torch.as_tensor(np.asarray(xs[i:i + n])).to(dev)
         return unpack_voxels(xb, size).to(torch.bfloat16)
 
-    q = quantize_model(model, batch(ds.x_train, 0, calib))
+    cx = batch(ds.x_train, 0, calib)
+    q = quantize_model(model, cx)                          # fp8 stem (tap-expanded space-to-depth)
+    qs = quantize_model(model, cx, fp8_stem=False)         # bf16 stem + quantisation pass
     y = np.asarray(ds.y_test)
-    pb, pq = [], []
+    pb, pq, ps = [], [], []
     for i in range(0, len(y), chunk):
         xb = batch(ds.x_test, i, chunk)
         pb.append(model(xb).float().argmax(-1).cpu())
         pq.append(q(xb).float().argmax(-1).cpu())
-    pb, pq = torch.cat(pb).numpy(), torch.cat(pq).numpy()
-    acc_b, acc_q = float((pb == y).mean()), float((pq == y).mean())
+        ps.append(qs(xb).float().argmax(-1).cpu())
+    pb, pq, ps = torch.cat(pb).numpy(), torch.cat(pq).numpy(), torch.cat(ps).numpy()
+    acc_b, acc_q, acc_s = float((pb == y).mean()), float((pq == y).mean()), float((ps == y).mean())
     return {"top1_bf16": round(acc_b, 4), "top1_fp8": round(acc_q, 4), "drop_pt": round(100 * (acc_b - acc_q), 2),
             "agreement": round(float((pb == pq).mean()), 4), "calib_samples": calib,
+            "bf16_stem": {"top1_fp8": round(acc_s, 4), "drop_pt": round(100 * (acc_b - acc_s), 2),
+                          "agreement": round(float((pb == ps).mean()), 4)},
             "kernel": ("conv_halo_f8" if os.environ.get("FN_F8_TILE", "1") == "0" else "conv_tile F8 variant")
                       + " (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3)"}
 

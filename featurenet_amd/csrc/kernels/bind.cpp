@@ -30,6 +30,7 @@ int fn_conv_halo_wgrad_yblocks(const int*, int);
 int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
                     int, int, hipStream_t);
 int fn_quant_fp8(const void*, void*, long long, float, hipStream_t);
+int fn_s2d_tap_f8(const void*, void*, int, int, int, int, int, int, int, int, float, hipStream_t);
 int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, hipStream_t);
 int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
@@ -244,7 +245,8 @@ PYBIND11_MODULE(_C, m) {
       throw std::runtime_error("conv_tile_f8: bad slice");
     fits(ext, 0, prod({geom[0], geom[1], geom[2], geom[3], geom[4]}), "conv_tile_f8", "src");
     fits(ext, 1, prod({geom[4] / geom[17] * geom[19] + 4, geom[20], 64, 32}), "conv_tile_f8", "wpk");
-    fits(ext, 2, view_extent(geom, ncol), "conv_tile_f8", "out");
+    fits(ext, 2, (relu & 2) ? prod({geom[0], geom[5] / 2, geom[6] / 2, geom[7] / 2, ncol}) : view_extent(geom, ncol),
+         "conv_tile_f8", "out");
     fits(ext, 3, 4LL * MT * 16, "conv_tile_f8", "rowtab");
     fits(ext, 4, geom[19] + 6LL, "conv_tile_f8", "ktab");
     chk(fn_conv_tile_f8(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
@@ -373,6 +375,15 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_conv_halo_f8(P<const void*>(src), P<const void*>(wt), P<const float*>(scale), P<const float*>(bias),
                         P<void*>(out), inv_out_scale, P<const int*>(toffs), geom.data(), ncol, out_f8, relu, S(st)),
         "conv_halo_f8");
+  });
+  m.def("s2d_tap_f8", [](uintptr_t x, uintptr_t y, std::vector<int> g, float inv_scale, uintptr_t st,
+                         std::vector<long long> ext) {
+    // g = {N, D, H, W, D2, H2, W2o, J}; ext = {numel(x), numel(y)}
+    need(g, 8, "s2d_tap_f8");
+    fits(ext, 0, prod({g[0], g[1], g[2], g[3]}), "s2d_tap_f8", "x");
+    fits(ext, 1, prod({g[0], g[4], g[5], g[6], 8LL * g[7]}), "s2d_tap_f8", "y");
+    chk(fn_s2d_tap_f8(P<const void*>(x), P<void*>(y), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], inv_scale, S(st)),
+        "s2d_tap_f8");
   });
   m.def("quant_fp8", [](uintptr_t x, uintptr_t y, long long n, float inv_scale, uintptr_t st) {
     chk(fn_quant_fp8(P<const void*>(x), P<void*>(y), n, inv_scale, S(st)), "quant_fp8");

@@ -296,3 +296,78 @@ extern "C" int fn_quant_fp8(const void* x, void* y, long long n, float inv_scale
   FN_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// fp8 stem input: space-to-depth (factor 2^3) of a 1-channel volume, with J consecutive
+// w-taps of the packed grid folded into the channels, quantised to e4m3.
+// ---------------------------------------------------------------------------
+// x: bf16 [N, D, H, W] (1 channel).  y: e4m3 [N, D2, H2, W2o, 8J] with
+//   y[n, d, h, w, 8j + (pd*4 + ph*2 + pw)] = e4m3(x[n, 2d+pd, 2h+ph, 2(w+j)+pw] * inv_scale)
+// (zero outside x).  A 2^3-stride conv of kernel k^3 over x is then a stride-1 conv of
+// taps (k2, k2, 1) over y (k2 = ceil(k/2), J = k2; the weight is the space-to-depth weight
+// [K][k2][k2][k2][8] viewed as [K][k2][k2][1][8 k2]): 8J = 32 channels fit the fp8 tile
+// kernel's 32-channel slices, where the plain space-to-depth input has 8.
+// Block = 4 packed rows (n, d, h) x 64 w: each thread quantises the 8 space-to-depth bytes of
+// ONE packed position (4 dword loads: two bf16 of each (pd, ph)) into LDS, then assembles
+// the 32 output bytes of its position from LDS slots w .. w+3 (the rows of 64 cover W2o + 3
+// <= 64 packed positions) -- every x element is loaded once, stores are 16 B.
+// Block = 4 packed rows (n, d, h) x 64 w: each thread quantises the 8 space-to-depth bytes of
+// ONE packed position (4 dword loads: two bf16 of each (pd, ph)) into LDS, then assembles
+// the 32 output bytes of its position from LDS slots w .. w+3 (the rows of 64 cover W2o + 3
+// <= 64 packed positions) -- every x element is loaded once, stores are 16 B.
+__global__ __launch_bounds__(256) void s2d_tap_f8_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ y,
+                                                         int N, int D, int H, int W, int D2, int H2, int W2o, int J,
+                                                         float inv_scale) {
+  __shared__ uint2 s8[4][64];
+  const int lane = threadIdx.x & 63, rw = threadIdx.x >> 6;
+  const long long row = (long long)blockIdx.x * 4 + rw;          // (n, d, h) packed row
+  const long long nrows = (long long)N * D2 * H2;
+  const int h = (int)(row % H2), d = (int)((row / H2) % D2), n = (int)(row / ((long long)H2 * D2));
+  unsigned char b[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) b[q] = 0;
+  const int xw = 2 * lane;
+  if (row < nrows) {
+#pragma unroll
+    for (int pd = 0; pd < 2; ++pd)
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        const int xd = 2 * d + pd, xh = 2 * h + ph;
+        if (xd >= D || xh >= H) continue;
+        const bf16* xr = x + (((long long)n * D + xd) * H + xh) * W;
+        float v0 = 0.f, v1 = 0.f;
+        if (xw + 1 < W && (W & 1) == 0) {        // (even W: a 4-byte aligned pair)
+          const unsigned u = *(const unsigned*)(xr + xw);
+          v0 = __uint_as_float(u << 16);
+          v1 = __uint_as_float(u & 0xffff0000u);
+        } else {
+          if (xw < W) v0 = bf2f(xr[xw]);
+          if (xw + 1 < W) v1 = bf2f(xr[xw + 1]);
+        }
+        b[pd * 4 + ph * 2] = f32_to_fp8(v0 * inv_scale);
+        b[pd * 4 + ph * 2 + 1] = f32_to_fp8(v1 * inv_scale);
+      }
+  }
+  s8[rw][lane] = make_uint2((unsigned)b[0] | ((unsigned)b[1] << 8) | ((unsigned)b[2] << 16) | ((unsigned)b[3] << 24),
+                            (unsigned)b[4] | ((unsigned)b[5] << 8) | ((unsigned)b[6] << 16) | ((unsigned)b[7] << 24));
+  __syncthreads();
+  if (row >= nrows || lane >= W2o) return;
+  uint2 t[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t[j] = (j < J && lane + j < 64) ? s8[rw][lane + j] : make_uint2(0u, 0u);
+  uint4* o = reinterpret_cast<uint4*>(y + (row * W2o + lane) * (8LL * J));
+  o[0] = make_uint4(t[0].x, t[0].y, t[1].x, t[1].y);
+  if (J == 4) o[1] = make_uint4(t[2].x, t[2].y, t[3].x, t[3].y);
+}
+
+extern "C" int fn_s2d_tap_f8(const void* x, void* y, int N, int D, int H, int W, int D2, int H2, int W2o, int J,
+                             float inv_scale, hipStream_t st) {
+  if (N <= 0 || D <= 0 || H <= 0 || W <= 0 || D2 <= 0 || H2 <= 0 || W2o <= 0 || (J != 2 && J != 4)) return -2;
+  if (2 * (D2 - 1) >= D || 2 * (H2 - 1) >= H || 2 * (W2o - 1) >= W) return -3;   // every position reads x
+  if (W2o + J - 1 > 64) return -2;               // one 64-lane row of packed positions per (n, d, h)
+  const long long rows = (long long)N * D2 * H2;
+  hipLaunchKernelGGL(s2d_tap_f8_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, (const bf16*)x,
+                     (unsigned char*)y, N, D, H, W, D2, H2, W2o, J, inv_scale);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

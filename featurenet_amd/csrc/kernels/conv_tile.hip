@@ -65,6 +65,7 @@ struct TileGeom {
 };
 
 #define CT_NCW 4                       // compute (MFMA) waves
+#define CT_F8_POOL 0x100               // fp8 act flag: fused 2^3 max-pool epilogue
 #define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
 // per-compute-wave BN sums of the workgroup's NT*16 columns
 __host__ __device__ constexpr int ct_red_bytes(int NT) { return CT_NCW * 2 * NT * 16 * 4; }
@@ -371,7 +372,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // (fp8: bit 0 relu, bit 1 fp8 output)
     // bf16 with bny (dgrad of the conv that consumes a BN+act output): bit 2, and bit 1 is the
     // BN's relu (the stored dx itself has no activation)
-    const int emode = F8 ? ((act == ACT_RELU ? 1 : 0) | (oscale > 0.f ? 2 : 0))
+    // (fp8: act bit CT_F8_POOL = the 2^3 max-pool epilogue, relu + bf16 output of the pooled grid)
+    const int emode = F8 ? (((act & 0xff) == ACT_RELU ? 1 : 0) | (oscale > 0.f ? 2 : 0) | ((act & CT_F8_POOL) ? 4 : 0))
                          : (BWS ? (4 | (act == ACT_RELU ? 2 : 0))
                                 : ((stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0)));   // (ACT_NONE / ACT_RELU only)
     // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
@@ -547,7 +549,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
         // fp8 inference epilogue: dequantise + bias (+ReLU) -> bf16 (16-B store) or e4m3 of
         // y * oscale (8-B store)
         auto epilogue_f8 = [&](auto mode) {
-          constexpr int M = decltype(mode)::value;   // bit 0 relu, bit 1 fp8 output
+          constexpr int M = decltype(mode)::value;   // bit 0 relu, bit 1 fp8 output, bit 2 max-pool
+          constexpr bool POOL = (M & 4) != 0;
           float sc8[8], bs8[8];
           {
             const float4* q = reinterpret_cast<const float4*>(s_sb + 8 * lg);
@@ -557,6 +560,21 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             bs8[0] = c.x; bs8[1] = c.y; bs8[2] = c.z; bs8[3] = c.w;
             bs8[4] = d.x; bs8[5] = d.y; bs8[6] = d.z; bs8[7] = d.w;
           }
+          if constexpr ((M & 2) != 0) {          // fp8 output: fold the requantisation scale into the
+#pragma unroll                                   // dequantisation (one FMA + one med3 per value)
+            for (int j = 0; j < 8; ++j) {
+              sc8[j] *= oscale;
+              bs8[j] *= oscale;
+            }
+          }
+          // POOL: the pool row table puts the 8 members of one 2^3 window in one lane, member m
+          // in fragment m (MT = 8): the lane's running max over the fragments is the pooled value
+          float pm[POOL ? 8 : 1];
+          if constexpr (POOL) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pm[j] = 0.f;   // (relu: pooled values are >= 0)
+          }
+          bool pok = false;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             bool ok = roff[mt] >= 0 && gc8 < Ncol;
@@ -565,18 +583,22 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               v[j] = acc[mt][j >> 2][j & 3] * sc8[j] + bs8[j];
-              if constexpr ((M & 1) != 0) v[j] = fmaxf(v[j], 0.f);
+              if constexpr ((M & 2) != 0)        // (already x oscale) relu / saturate in one med3
+                v[j] = __builtin_amdgcn_fmed3f(v[j], (M & 1) != 0 ? 0.f : -448.f, 448.f);
+              else if constexpr ((M & 1) != 0 || POOL)
+                v[j] = fmaxf(v[j], 0.f);
             }
-            if (ok) {
+            if constexpr (POOL) {
+              if (mt == 0) pok = ok;             // (windows lie wholly inside or outside the output)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) pm[j] = fmaxf(pm[j], v[j]);
+            } else if (ok) {
               if constexpr ((M & 2) != 0) {
                 unsigned wd[2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                  float q[4];
-#pragma unroll
-                  for (int j = 0; j < 4; ++j) q[j] = fminf(fmaxf(v[4 * h + j] * oscale, -448.f), 448.f);
-                  int p = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
-                  p = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], p, true);
+                  int p = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h], v[4 * h + 1], 0, false);
+                  p = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * h + 2], v[4 * h + 3], p, true);
                   wd[h] = (unsigned)p;
                 }
                 *(uint2*)(reinterpret_cast<unsigned char*>(out) + obase_e + (long long)roff[mt] * Ncol) =
@@ -590,13 +612,25 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
           }
+          if constexpr (POOL) {
+            if (pok) {                           // pooled grid [N][OD/2][OH/2][OW/2][Ncol]
+              const int PDm = g.OD >> 1, PHm = g.OH >> 1, PWm = g.OW >> 1;
+              const int pd_ = (d0 + (rpk[0] >> 16)) >> 1, ph_ = (h0 + ((rpk[0] >> 8) & 255)) >> 1,
+                        pw_ = (w0 + (rpk[0] & 255)) >> 1;
+              bf16* po = reinterpret_cast<bf16*>(out) +
+                         ((((long long)n * PDm + pd_) * PHm + ph_) * PWm + pw_) * Ncol + gc8;
+              *(uint4*)po = make_uint4(bf16x2_pack(pm[0], pm[1]), bf16x2_pack(pm[2], pm[3]),
+                                       bf16x2_pack(pm[4], pm[5]), bf16x2_pack(pm[6], pm[7]));
+            }
+          }
         };
         if constexpr (F8) {
           switch (emode) {
             case 0: epilogue_f8(std::integral_constant<int, 0>{}); break;
             case 1: epilogue_f8(std::integral_constant<int, 1>{}); break;
             case 2: epilogue_f8(std::integral_constant<int, 2>{}); break;
-            default: epilogue_f8(std::integral_constant<int, 3>{}); break;
+            case 3: epilogue_f8(std::integral_constant<int, 3>{}); break;
+            default: if constexpr (MT == 8) epilogue_f8(std::integral_constant<int, 5>{}); break;
           }
         } else if constexpr (BWS) {
           if (emode == 6) epilogue(std::integral_constant<int, 6>{});
@@ -1221,6 +1255,11 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   if (g.CS != 32 && g.CS != 64) return -2;
   const int CPP = g.CS / 16;
   if (!fn_conv_tile_f8_supported(MT, NT, CPP) || !scale || !(oscale >= 0.f)) return -2;
+  // relu: bit 0 relu, bit 1 the fused 2^3 max-pool (relu, bf16 output [N][OD/2][OH/2][OW/2][Ncol];
+  // even tile dims so every window lies in one tile, the pool row table, MT = 8)
+  const bool pool = (relu & 2) != 0;
+  if (pool && (MT != 8 || oscale != 0.f || (g.TD | g.TH | g.TW | g.OD | g.OH | g.OW) & 1)) return -2;
+  const int f8act = ((relu & 1) || pool ? ACT_RELU : ACT_NONE) | (pool ? CT_F8_POOL : 0);
   if (g.C % g.CS || g.TD * g.TH * g.TW > 64 * MT || g.TD < 1 || g.TH < 1 || g.TW < 1) return -3;
   const long long HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const long long HP = (g.TD + g.KD - 1) * HH * HW;
@@ -1253,7 +1292,7 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
     if ((f8dbg & 16) && hipMemsetAsync(stamps, 0, nst * sizeof(long long), st) != hipSuccess) return -5;
 #define CT_F8_DBG(C, D) if (MT == 8 && NT == 2 && CPP == C && f8dbg == D) \
     rc = launch_tile<8, 2, C, D, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, \
-                                       zp, bias, out, nullptr, g, Ncol, relu ? ACT_RELU : ACT_NONE, sched, stamps, scale, oscale);
+                                       zp, bias, out, nullptr, g, Ncol, f8act, sched, stamps, scale, oscale);
     CT_F8_DBG(2, 1) CT_F8_DBG(2, 2) CT_F8_DBG(2, 3) CT_F8_DBG(2, 4) CT_F8_DBG(2, 7) CT_F8_DBG(2, 16)
     CT_F8_DBG(4, 1) CT_F8_DBG(4, 2) CT_F8_DBG(4, 3) CT_F8_DBG(4, 4) CT_F8_DBG(4, 7) CT_F8_DBG(4, 16)
 #undef CT_F8_DBG
@@ -1275,7 +1314,7 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
 #define CT_F8_CASE(M, N, C)                                                                                        \
   if (MT == M && NT == N && CPP == C)                                                                              \
     rc = launch_tile<M, N, C, 0, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, \
-                                       zp, bias, out, nullptr, g, Ncol, relu ? ACT_RELU : ACT_NONE, sched, nullptr,   \
+                                       zp, bias, out, nullptr, g, Ncol, f8act, sched, nullptr,                     \
                                        scale, oscale);
   CT_F8_INSTANCES(CT_F8_CASE)
 #undef CT_F8_CASE

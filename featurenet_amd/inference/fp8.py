@@ -53,8 +53,10 @@ class Fp8Conv:
     A/B reference); folded BN, per-channel weight scales.  ``FN_F8_TILE=0`` forces the halo
     kernel."""
 
-    def __init__(self, conv, in_scale: float, out_scale: float | None, relu: bool = True):
-        w, b = _fold_bn(conv)
+    def __init__(self, conv, in_scale: float, out_scale: float | None, relu: bool = True, wb=None,
+                 padding: str | None = None):
+        # conv: the bf16 layer (BN folded here), or None with wb = (folded weight, bias)
+        w, b = _fold_bn(conv) if wb is None else wb
         K, KD, KH, KW, Cin = w.shape
         sw = w.abs().reshape(K, -1).amax(1).clamp_min(1e-12) / FP8_MAX
         wq = _to_fp8(w / sw.view(-1, 1, 1, 1, 1))
@@ -70,23 +72,34 @@ class Fp8Conv:
         self.bias = b.float().contiguous()
         self.out_scale, self.relu = out_scale, relu
         self.K, self.kernel, self.conv = K, (KD, KH, KW), conv
+        self.padding = padding if padding is not None else conv.padding
         self.w_dequant = wq.float() * sw.view(-1, 1, 1, 1, 1)     # for numerics tests
 
-    def tile_plan(self, spec):
+    def tile_plan(self, spec, pool: bool = False):
         if os.environ.get("FN_F8_TILE", "1") == "0":
             return None
         return conv_tile.plan(spec.N, (spec.OD, spec.OH, spec.OW), (spec.KD, spec.KH, spec.KW), spec.C, spec.K,
-                              f8=True)
+                              f8=True, pool=pool)
 
-    def __call__(self, xq: torch.Tensor, shape5: tuple) -> tuple[torch.Tensor, tuple]:
-        spec = ConvSpec.make(shape5, self.K, self.kernel, 1, self.conv.padding)
-        tp = self.tile_plan(spec)
+    def pool_plan(self, shape5: tuple):
+        """The tile plan with the fused 2^3 max-pool epilogue for this input, or None."""
+        if os.environ.get("FN_F8_POOL", "1") == "0" or self.out_scale is not None or not self.relu:
+            return None
+        return self.tile_plan(ConvSpec.make(shape5, self.K, self.kernel, 1, self.padding), pool=True)
+
+    def __call__(self, xq: torch.Tensor, shape5: tuple, pool: bool = False) -> tuple[torch.Tensor, tuple]:
+        """(y, y's shape); ``pool``: y = maxpool2^3(relu(conv)) from the fused epilogue (the
+        caller checked :meth:`pool_plan`)."""
+        spec = ConvSpec.make(shape5, self.K, self.kernel, 1, self.padding)
+        tp = self.tile_plan(spec, pool=pool)
+        if pool:
+            assert tp is not None and tp.pool
         if tp is not None:
             wpk = self._tile.get(tp)
             if wpk is None:
                 wpk = self._tile[tp] = conv_tile.pack_weights_f8(self.wq_ktc, tp)
             y = conv_tile.conv_fwd_f8(xq, wpk, self.scale, self.bias, spec, tp, self.relu, self.out_scale)
-            return y, spec.out_shape5
+            return y, tuple(y.shape)
         # fp8 halo = 16 B/position; halo_plan counts 32 B/position (bf16): <= 64 KiB of fp8 halo
         plan = halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, 128 * 1024, wsplit=False)
         if plan is None:
@@ -110,16 +123,66 @@ def quantize_fp8_act(x: torch.Tensor, scale: float) -> torch.Tensor:
     return y
 
 
-class Fp8FeatureNet3D:
-    """Inference-only fp8 FeatureNet-3D built from a trained (or random-init) bf16 model."""
+def stem_tap_plan(c1, in_shape5):
+    """(ConvSpec of the tap-expanded stem, packed grid dims) when the stem -- 1 input channel,
+    stride 2^3, 'valid', k^3 with ceil(k/2) = 4 -- can run as an fp8 conv: space-to-depth to
+    8 channels, then the 4 w-taps of the packed grid folded into 32 channels
+    (``s2d_tap_f8``), so the conv is taps (4, 4, 1) over 32 fp8 channels on the fp8 tile
+    kernel; else None (the bf16 stem + a quantisation pass)."""
+    N, D, H, W, C = in_shape5
+    k = tuple(c1.kernel) if isinstance(c1.kernel, (tuple, list)) else (c1.kernel,) * 3
+    st = tuple(c1.stride) if isinstance(c1.stride, (tuple, list)) else (c1.stride,) * 3
+    if os.environ.get("FN_F8_STEM", "1") == "0" or C != 1 or st != (2, 2, 2) or c1.padding != "valid" \
+            or any(-(-kk // 2) != 4 for kk in k):
+        return None
+    OD, OH, OW = ((D - k[0]) // 2 + 1, (H - k[1]) // 2 + 1, (W - k[2]) // 2 + 1)
+    D2, H2 = OD + 3, OH + 3                      # packed rows the 4 d / h taps reach
+    if 2 * (D2 - 1) >= D or 2 * (H2 - 1) >= H or 2 * (OW - 1 + 3) >= W:
+        return None
+    spec = ConvSpec.make((N, D2, H2, OW, 32), c1.cout, (4, 4, 1), 1, "valid")
+    if (spec.OD, spec.OH, spec.OW) != (OD, OH, OW):
+        return None
+    return spec
 
-    def __init__(self, model: FeatureNet3D, act_scales: list[float]):
+
+def stem_tap_weight(w: torch.Tensor) -> torch.Tensor:
+    """[K, k, k, k, 1] stem weight -> [K, 4, 4, 1, 32]: space-to-depth weight [K, 4, 4, 4, 8]
+    (tap 2t + p of each dim -> tap t, channel pd*4 + ph*2 + pw) with its w-taps folded into
+    the channels (8 j + c)."""
+    K = w.shape[0]
+    wp = torch.zeros(K, 8, 8, 8, 1, dtype=torch.float32, device=w.device)
+    wp[:, :w.shape[1], :w.shape[2], :w.shape[3]] = w.float()
+    w2 = wp.view(K, 4, 2, 4, 2, 4, 2).permute(0, 1, 3, 5, 2, 4, 6).reshape(K, 4, 4, 4, 8)
+    return w2.reshape(K, 4, 4, 1, 32).contiguous()
+
+
+def stem_tap_input(x5: torch.Tensor, spec: ConvSpec, in_scale: float) -> torch.Tensor:
+    """e4m3 [N, D2, H2, OW, 32] tap-expanded space-to-depth input of the stem (one launch)."""
+    N, D, H, W, _ = x5.shape
+    x5 = x5.to(torch.bfloat16).contiguous()
+    y = torch.empty(spec.N, spec.D, spec.H, spec.W, 32, dtype=torch.uint8, device=x5.device)
+    _native.kernels().s2d_tap_f8(x5.data_ptr(), y.data_ptr(), [N, D, H, W, spec.D, spec.H, spec.W, 4], 1.0 / in_scale,
+                                 _native.stream(x5), [x5.numel(), y.numel()])
+    return y
+
+
+class Fp8FeatureNet3D:
+    """Inference-only fp8 FeatureNet-3D built from a trained (or random-init) bf16 model.
+    With a calibrated input scale, the stem runs in fp8 too (tap-expanded space-to-depth,
+    :func:`stem_tap_plan`) and writes e4m3 straight into conv2's input."""
+
+    def __init__(self, model: FeatureNet3D, act_scales: list[float], in_scale: float | None = None):
         self.model = model.eval()
         convs = list(model.convs)
         c1 = convs[0]
         w1, b1 = _fold_bn(c1)
         self.c1_w, self.c1_b = w1, b1
         self.act_scales = act_scales
+        self.in_scale = in_scale
+        self.stem = None
+        if in_scale is not None:
+            self.stem = Fp8Conv(None, in_scale, act_scales[0], relu=True, wb=(stem_tap_weight(w1), b1),
+                                padding="valid")
         self.layers = []
         for i, conv in enumerate(convs[1:], start=1):
             last = i == len(convs) - 1
@@ -131,22 +194,40 @@ class Fp8FeatureNet3D:
         m = self.model
         if x.dim() == 4:
             x = x.unsqueeze(-1)
-        x = x.to(torch.bfloat16).contiguous()
         c1 = m.convs[0]
-        spec = ConvSpec.make(tuple(x.shape), c1.cout, c1.kernel, c1.stride, c1.padding)
-        y = ops.conv(x, self.c1_w, self.c1_b, spec, "relu")                   # bf16, BN folded, ReLU fused
-        xq = quantize_fp8_act(y, self.act_scales[0])
-        shape = spec.out_shape5
-        for layer in self.layers:
-            xq, shape = layer(xq, shape)
+        tspec = stem_tap_plan(c1, tuple(x.shape)) if self.stem is not None else None
+        if tspec is not None and self.stem.tile_plan(tspec) is not None:
+            xq, shape = self.stem(stem_tap_input(x, tspec, self.in_scale),              # fp8 in, fp8 out
+                                  (tspec.N, tspec.D, tspec.H, tspec.W, tspec.C))
+        else:
+            x = x.to(torch.bfloat16).contiguous()
+            spec = ConvSpec.make(tuple(x.shape), c1.cout, c1.kernel, c1.stride, c1.padding)
+            y = ops.conv(x, self.c1_w, self.c1_b, spec, "relu")               # bf16, BN folded, ReLU fused
+            xq = quantize_fp8_act(y, self.act_scales[0])
+            shape = spec.out_shape5
+        fused_pool = False
+        for li, layer in enumerate(self.layers):
+            last = li == len(self.layers) - 1
+            fused_pool = last and self._pool_fusable() and layer.pool_plan(shape) is not None
+            xq, shape = layer(xq, shape, pool=fused_pool)
         feat = xq                                                             # bf16 [N, D, H, W, 64]
-        if self.pool is not None:
+        if self.pool is not None and not fused_pool:
             ps = PoolSpec.make(tuple(feat.shape), self.pool, m.convs[-1].pool_stride, "valid")
             feat = ops.pool(feat, ps, "max")
         f = feat.reshape(feat.shape[0], -1)
         return m.fc2(m.fc1(f), out_fp32=True)
 
     __call__ = forward
+
+    def _pool_fusable(self) -> bool:
+        """The model's max-pool is 2^3 with stride 2 ('valid'): the last conv's fp8 epilogue can
+        pool (conv_tile pool plans)."""
+        c = self.model.convs[-1]
+        k = tuple(self.pool) if isinstance(self.pool, (tuple, list)) else (self.pool,) * 3
+        st = c.pool_stride if getattr(c, "pool_stride", None) is not None else k
+        st = tuple(st) if isinstance(st, (tuple, list)) else (st,) * 3
+        return (self.pool is not None and k == (2, 2, 2) and st == (2, 2, 2) and c.pool_kind == "max"
+                and c.pool_padding == "valid")
 
 
 @torch.no_grad()
@@ -164,8 +245,12 @@ def calibrate(model: FeatureNet3D, calib_x: torch.Tensor, margin: float = 1.0) -
     return scales
 
 
-def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor) -> Fp8FeatureNet3D:
-    return Fp8FeatureNet3D(model, calibrate(model, calib_x))
+def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem: bool = True) -> Fp8FeatureNet3D:
+    """fp8 model with activation scales from a bf16 pass over ``calib_x``; ``fp8_stem``: the
+    input is quantised too (scale amax / 448 of the calibration input: binary voxels map
+    exactly) and the stem runs on the fp8 kernel."""
+    in_scale = max(float(calib_x.float().abs().amax()), 1e-6) / FP8_MAX if fp8_stem else None
+    return Fp8FeatureNet3D(model, calibrate(model, calib_x), in_scale)
 
 
 _ = math

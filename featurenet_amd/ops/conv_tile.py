@@ -81,6 +81,7 @@ class TilePlan:
     cost: float      # modelled cycles (per wave, summed over the jobs of one CU)
     f8: bool = False  # fp8 (e4m3) inference variant: 16-channel chunks, 128-k steps, ring depth 2
     nw: int = 4       # 4 MFMA waves + loader (conv_tile_kernel) or 8 split-K MFMA waves (conv_tile8_kernel)
+    pool: bool = False  # fp8: fused 2^3 max-pool epilogue (even tile dims, window-per-lane row table)
 
     @property
     def rows(self) -> int:
@@ -105,15 +106,19 @@ def _ksteps(T: int, CS: int, PD: int) -> int:
     return -(-k // PD) * PD
 
 
-def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int = 256, f8: bool = False):
+def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int = 256, f8: bool = False,
+         pool: bool = False):
     """Best TilePlan for an (N, OD, OH, OW) output of a (KD, KH, KW) stride-1 conv over
     ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply
-    (``f8``: the e4m3 inference variant, 32- or 64-channel slices)."""
+    (``f8``: the e4m3 inference variant, 32- or 64-channel slices; ``pool``: with the fused
+    2^3 max-pool epilogue -- even output and tile dims)."""
     nw = 4 if f8 else nwaves()
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, nw, tile_nt())
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, nw, tile_nt(), pool)
     if key in _PLANS:
         return _PLANS[key]
-    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, nw)
+    if pool and (not f8 or any(d % 2 for d in out_dims)):
+        return None
+    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, nw, pool)
     if best is None and nw == 8:                 # shapes the 8-wave kernel cannot tile: 4 waves + loader
         best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, 4)
     with _LOCK:
@@ -121,7 +126,7 @@ def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int
     return best
 
 
-def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4):
+def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4, pool=False):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
@@ -153,6 +158,8 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4):
                     rows = TD * TH * TW
                     if rows > 64 * mt_choices[-1]:
                         break
+                    if pool and (TD % 2 or TH % 2 or TW % 2):
+                        continue
                     MT = max(mt_choices[0], -(-rows // 64))
                     if rows < 64 * mt_choices[0] * 0.75:
                         continue
@@ -178,7 +185,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4):
                     per_job = max(mfma + fixed + epi, loader)
                     cost = math.ceil(jobs / workers) * per_job
                     cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
-                                          float(cost), f8, nw))
+                                          float(cost), f8, nw, pool))
     # the cheapest few, re-costed with their row tables' residual bank conflicts (a
     # fragment whose 16 rows repeat a residue mod 16 reads at half rate)
     best = None
@@ -192,7 +199,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4):
         cost = c.cost * (1.0 + 0.5 * dups / res.size)
         if best is None or cost < best.cost:
             best = TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct", "BUF",
-                                                        "mHW", "mHHW")), cost, f8, nw)
+                                                        "mHW", "mHHW")), cost, f8, nw, pool)
     return best
 
 
@@ -205,6 +212,11 @@ def row_table(p: TilePlan, kdims: tuple) -> np.ndarray:
         return t
     KD, KH, KW = kdims
     HH, HW = p.TH + KH - 1, p.TW + KW - 1
+    if p.pool:
+        tab = _pool_row_table(p, HH, HW)
+        with _LOCK:
+            _ROWTAB[key] = tab
+        return tab
     td, th, tw = np.meshgrid(np.arange(p.TD), np.arange(p.TH), np.arange(p.TW), indexing="ij")
     nat = ((td * p.TH + th) * p.TW + tw).reshape(-1)
     hb = ((td * HH + th) * HW + tw).reshape(-1)
@@ -233,6 +245,30 @@ def row_table(p: TilePlan, kdims: tuple) -> np.ndarray:
     tab = np.asarray([x for f in frags for x in f], dtype=np.int32)
     with _LOCK:
         _ROWTAB[key] = tab
+    return tab
+
+
+def _pool_row_table(p: TilePlan, HH: int, HW: int) -> np.ndarray:
+    """Row table of the fused-pool fp8 epilogue: window i of the tile's (TD/2, TH/2, TW/2)
+    2^3 windows goes to wave i // 16, lane i % 16; its member m = (md, mh, mw) to fragment
+    m, so every lane holds one whole window (max over its 8 fragments).  Missing windows are
+    dummy rows (-1).  Bank slots are not permuted (members of a fragment are window bases
+    shifted by one fixed offset)."""
+    assert p.MT == 8 and p.TD % 2 == 0 and p.TH % 2 == 0 and p.TW % 2 == 0
+    wd, wh, ww = np.meshgrid(np.arange(p.TD // 2), np.arange(p.TH // 2), np.arange(p.TW // 2), indexing="ij")
+    wd, wh, ww = wd.reshape(-1), wh.reshape(-1), ww.reshape(-1)
+    nwin = wd.size
+    assert nwin <= 64, "more windows than lanes x waves"
+    tab = np.zeros((4 * 8 * 16, 2), dtype=np.int32)
+    for i in range(64):
+        wave, lr = divmod(i, 16)
+        for m in range(8):
+            r = (wave * 8 + m) * 16 + lr
+            if i < nwin:
+                d, h, w = 2 * wd[i] + (m >> 2), 2 * wh[i] + ((m >> 1) & 1), 2 * ww[i] + (m & 1)
+                tab[r] = ((d * HH + h) * HW + w, (d * p.TH + h) * p.TW + w)
+            else:
+                tab[r] = (0, -1)
     return tab
 
 
@@ -474,17 +510,24 @@ def pack_weights_f8(wq: torch.Tensor, p: TilePlan) -> torch.Tensor:
 def conv_fwd_f8(xq5: torch.Tensor, wpk: torch.Tensor, scale: torch.Tensor, bias: torch.Tensor, spec, p: TilePlan,
                 relu: bool, out_scale: float | None) -> torch.Tensor:
     """y = act(conv(x, w) * scale + bias) of e4m3 activations (uint8 [N, D, H, W, C]) on the fp8
-    tile kernel: bf16 output, or e4m3 of y / out_scale when ``out_scale`` is given."""
+    tile kernel: bf16 output, or e4m3 of y / out_scale when ``out_scale`` is given.  A ``pool``
+    plan returns maxpool2^3(relu(...)) instead: bf16 [N, OD/2, OH/2, OW/2, K]."""
     kd = (spec.KD, spec.KH, spec.KW)
     geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
                     (spec.pd, spec.ph, spec.pw))
-    y = torch.empty(spec.out_shape5, dtype=torch.uint8 if out_scale else torch.bfloat16, device=xq5.device)
+    if p.pool:
+        assert out_scale is None and relu
+        y = torch.empty(spec.N, spec.OD // 2, spec.OH // 2, spec.OW // 2, spec.K, dtype=torch.bfloat16,
+                        device=xq5.device)
+    else:
+        y = torch.empty(spec.out_shape5, dtype=torch.uint8 if out_scale else torch.bfloat16, device=xq5.device)
     st = _native.stream(xq5)
     rt = rowtab_tensor(p, kd, xq5.device)
     kt = ktab_tensor(p, kd, xq5.device)
     _native.kernels().conv_tile_f8(xq5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                    zero_page(xq5.device).data_ptr(), scale.data_ptr(), _native.ptr(bias), y.data_ptr(),
-                                   1.0 / out_scale if out_scale else 0.0, geom, spec.K, int(relu), p.MT, p.NT, st,
+                                   1.0 / out_scale if out_scale else 0.0, geom, spec.K, int(relu) | (2 if p.pool else 0),
+                                   p.MT, p.NT, st,
                                    sched(xq5.device, st).data_ptr(),
                                    [xq5.numel(), wpk.numel(), y.numel(), rt.numel() // 2, kt.numel() // 4])
     return y

@@ -82,3 +82,27 @@ def test_fp8_plans_and_weight_stream(out, k, c, n):
     kh, kw = divmod(r, k[2])
     ks, lg = (t // 4, t % 4) if p.CS == 32 else (t // 2, 2 * (t % 2))
     assert kt[ks, lg] == ((kd * HH + kh) * HW + kw) * 16
+
+
+@pytest.mark.parametrize("out,k,c,n", [((52, 52, 52), (3, 3, 3), 64, 64), ((20, 20, 20), (3, 3, 3), 64, 64),
+                                       ((10, 12, 14), (3, 3, 3), 32, 32)])
+def test_fp8_pool_plans_hold_whole_windows_per_lane(out, k, c, n):
+    """Fused-pool fp8 plans: even tile dims, and lane lr of wave w holds the 8 members of one
+    2^3 window in fragments 0..7 (each tile row exactly once)."""
+    p = ct.plan(64, out, k, c, n, f8=True, pool=True)
+    assert p is not None and p.pool and p.MT == 8
+    assert p.TD % 2 == 0 and p.TH % 2 == 0 and p.TW % 2 == 0
+    tab = ct.row_table(p, k)
+    nat = tab[:, 1][tab[:, 1] >= 0]
+    assert sorted(nat.tolist()) == list(range(p.rows))
+    t = tab[:, 1].reshape(4, 8, 16)                  # [wave][fragment][lane]
+    for wv in range(4):
+        for lr in range(16):
+            rows = t[wv, :, lr]
+            if rows[0] < 0:
+                assert (rows < 0).all()
+                continue
+            tw, th, td = rows % p.TW, (rows // p.TW) % p.TH, rows // (p.TW * p.TH)
+            assert len({(a // 2, b // 2, e // 2) for a, b, e in zip(td, th, tw)}) == 1   # one window
+            assert td[0] % 2 == 0 and th[0] % 2 == 0 and tw[0] % 2 == 0                  # member 0 = base
+    assert ct.plan(64, (21, 20, 20), k, c, n, f8=True, pool=True) is None           # odd output dim
