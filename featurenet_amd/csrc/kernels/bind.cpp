@@ -80,7 +80,7 @@ int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int fn_scale_unless_one(void*, int, const float*, long long, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
-                 const int*, int, int, int, int, int*, hipStream_t, const void*, const float*);
+                 const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float);
 int fn_conv_tile_workers(const int*, int, int);
 int fn_conv_tile8(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                   const int*, int, int, int, int, hipStream_t);
@@ -208,7 +208,8 @@ PYBIND11_MODULE(_C, m) {
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>());
   m.def("conv_tile", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                         uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
-                        uintptr_t sched, uintptr_t st, std::vector<long long> ext, uintptr_t bny, uintptr_t bnp) {
+                        uintptr_t sched, uintptr_t st, std::vector<long long> ext, uintptr_t bny, uintptr_t bnp,
+                        float oscale) {
     need(geom, 31, "conv_tile");
     check_tile(geom, ext, ncol, MT, "conv_tile");
     if (bny) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
@@ -217,12 +218,12 @@ PYBIND11_MODULE(_C, m) {
     }
     chk(fn_conv_tile(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
                      P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
-                     act, MT, NT, P<int*>(sched), S(st), P<const void*>(bny), P<const float*>(bnp)),
+                     act, MT, NT, P<int*>(sched), S(st), P<const void*>(bny), P<const float*>(bnp), oscale),
         "conv_tile");
   }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("bny") = 0,
-     py::arg("bnp") = 0);
+     py::arg("bnp") = 0, py::arg("oscale") = 0.f);
   m.def("conv_tile8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                          uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
                          uintptr_t st, std::vector<long long> ext) {

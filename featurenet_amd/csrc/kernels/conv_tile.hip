@@ -104,7 +104,9 @@ __host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : (NT =
 //   or re-quantised e4m3 (x oscale).
 // BWS: the dgrad instance with the BN-backward statistics epilogue (its own register
 // allocation: the extra epilogue operands must not cost the other instances registers)
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false>
+// Q8O: the bf16 instance with an e4m3 output epilogue (fp8 inference: the bf16 stem writes the
+// fp8 layers' input; its own register allocation, like BWS)
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false, bool Q8O = false>
 __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
@@ -375,7 +377,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // (fp8: act bit CT_F8_POOL = the 2^3 max-pool epilogue, relu + bf16 output of the pooled grid)
     const int emode = F8 ? (((act & 0xff) == ACT_RELU ? 1 : 0) | (oscale > 0.f ? 2 : 0) | ((act & CT_F8_POOL) ? 4 : 0))
                          : (BWS ? (4 | (act == ACT_RELU ? 2 : 0))
-                                : ((stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0)));   // (ACT_NONE / ACT_RELU only)
+                                : ((stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0) | (Q8O ? 8 : 0)));   // (ACT_NONE /
+                                                                                          // ACT_RELU only; 8: e4m3 out)
     // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
     // the previous job's last turn, so no job starts on an exposed L2 latency
 #pragma unroll
@@ -457,6 +460,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
           constexpr bool BW = (M & 4) != 0;
           constexpr bool RELU_OUT = !BW && (M & 2) != 0;
           constexpr bool ST = BW || (M & 1) != 0;
+          // bit 3: e4m3 output of v * oscale (saturated; fp8 inference: the bf16 stem writes the
+          // fp8 layers' input directly), 8-B stores; no statistics
+          constexpr bool Q8 = (M & 8) != 0;
           bool okm[MT];
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
@@ -523,7 +529,23 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                   tq[j] += x * x;
                 }
               }
-              if (ok)
+              if constexpr (Q8) {
+                if (ok) {
+                  unsigned wd[2];
+#pragma unroll
+                  for (int q = 0; q < 2; ++q) {
+                    float e[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                      e[j] = __builtin_amdgcn_fmed3f(v[4 * q + j] * oscale, RELU_OUT ? 0.f : -448.f, 448.f);
+                    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(e[0], e[1], 0, false);
+                    pk = __builtin_amdgcn_cvt_pk_fp8_f32(e[2], e[3], pk, true);
+                    wd[q] = (unsigned)pk;
+                  }
+                  *(uint2*)(reinterpret_cast<unsigned char*>(out) + obase_e + (long long)roff[mt] * Ncol + 8 * h) =
+                      make_uint2(wd[0], wd[1]);
+                }
+              } else if (ok)
                 *(uint4*)(obase + (long long)roff[mt] * Ncol + 8 * h) = make_uint4(
                     bf16x2_pack(v[0], v[1]), bf16x2_pack(v[2], v[3]), bf16x2_pack(v[4], v[5]), bf16x2_pack(v[6], v[7]));
               acc[mt][2 * h] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -640,7 +662,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             case 0: epilogue(std::integral_constant<int, 0>{}); break;
             case 1: epilogue(std::integral_constant<int, 1>{}); break;
             case 2: epilogue(std::integral_constant<int, 2>{}); break;
-            default: epilogue(std::integral_constant<int, 3>{}); break;
+            case 3: epilogue(std::integral_constant<int, 3>{}); break;
+            case 8: if constexpr (Q8O) epilogue(std::integral_constant<int, 8>{}); break;
+            default: if constexpr (Q8O) epilogue(std::integral_constant<int, 10>{}); break;
           }
         }
         lap(st_e);
@@ -1110,19 +1134,19 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false>
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false, bool Q8O = false>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
                        float oscale = 0.f, const void* bny = nullptr, const float* bnp = nullptr) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS, Q8O>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS>), grid, dim3(CT_NTHR), lds, st,
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS, Q8O>), grid, dim3(CT_NTHR), lds, st,
                      (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
                      stamps, scale, oscale, (const bf16*)bny, bnp);
   return 0;
@@ -1130,7 +1154,7 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
 
 // instantiations (MT, NT, CPP) -- the Python planner only emits these
 #define CT_INSTANCES(X) X(8, 2, 1) X(9, 2, 1) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4) \
-  X(6, 4, 2) X(6, 4, 4) X(7, 4, 2) X(7, 4, 4) X(8, 4, 2) X(8, 4, 4)
+  X(6, 4, 2) X(6, 4, 4) X(7, 4, 2) X(7, 4, 4)
 
 extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 #define CT_SUP(M, N, C) if (MT == M && NT == N && CPP == C) return 1;
@@ -1156,7 +1180,7 @@ static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false,
 // BN's activation (none / relu), not an activation of the output.
 extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
-                            int NT, int* sched, hipStream_t st, const void* bny, const float* bnp) {
+                            int NT, int* sched, hipStream_t st, const void* bny, const float* bnp, float oscale) {
   const TileGeom g = parse_tile(geom);
   if (g.CS != 8 && g.CS != 16 && g.CS != 32 && g.CS != 64) return -2;
   const int CPP = g.CS / 8;
@@ -1188,6 +1212,9 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
   if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;   // 16-B column groups; relu or none
   if (NT == 4 && (Ncol % 64 || bny)) return -2;                        // whole 64-column blocks, no BWS
+  // oscale > 0: e4m3 output of y * oscale (no statistics; the 8-channel-slice instances: the
+  // space-to-depth stem of the fp8 inference path)
+  if (!(oscale >= 0.f) || (oscale > 0.f && (stats || bny || NT != 2 || CPP != 1))) return -2;
   if ((bny != nullptr) != (bnp != nullptr) || (bny && (!stats || bias))) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
@@ -1223,8 +1250,11 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     rc = bny ? launch_tile<M, N, C, 0, false, N == 2>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,  \
                                                     (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, \
                                                     nullptr, nullptr, 0.f, bny, bnp)                              \
-             : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab,  \
-                                    zp, bias, out, stats, g, Ncol, act, sched);
+             : (oscale > 0.f ? launch_tile<M, N, C, 0, false, false, C == 1 && N == 2>(                          \
+                                   grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp,  \
+                                   bias, out, stats, g, Ncol, act, sched, nullptr, nullptr, oscale)                   \
+                             : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,         \
+                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched));
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;

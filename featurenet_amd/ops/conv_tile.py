@@ -389,12 +389,12 @@ def workers(p: TilePlan, geom: list, ncol: int) -> int:
 
 
 def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p: TilePlan, geom: list, kdims: tuple,
-        ncol: int, act: int, bny=None, bnp=None) -> None:
+        ncol: int, act: int, bny=None, bnp=None, oscale: float = 0.0) -> None:
     st = _native.stream(src5)
     rt = rowtab_tensor(p, kdims, src5.device)
     kt = ktab_tensor(p, kdims, src5.device)
     ext = [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4]
-    if p.nw == 8 and bny is None:
+    if p.nw == 8 and bny is None and not oscale:
         _native.kernels().conv_tile8(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                      zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                      _native.ptr(stats), geom, ncol, act, p.MT, p.NT, st, ext)
@@ -404,20 +404,23 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
     _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                 zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                 _native.ptr(stats), geom, ncol, act, p.MT, p.NT, sched(src5.device, st).data_ptr(),
-                                st, ext, _native.ptr(bny), _native.ptr(bnp))
+                                st, ext, _native.ptr(bny), _native.ptr(bnp), float(oscale))
 
 
-def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan):
-    """y = act(conv(x, w) + b) (+ BN statistics slab) for a stride-1 conv on the tile kernel."""
+def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan,
+             out_scale: float | None = None):
+    """y = act(conv(x, w) + b) (+ BN statistics slab) for a stride-1 conv on the tile kernel;
+    ``out_scale``: e4m3 bytes of y / out_scale instead (fp8 inference input, no statistics)."""
     kd = (spec.KD, spec.KH, spec.KW)
     geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
                     (spec.pd, spec.ph, spec.pw))
     wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=False)
-    y = torch.empty(spec.out_shape5, dtype=torch.bfloat16, device=x5.device)
+    y = torch.empty(spec.out_shape5, dtype=torch.uint8 if out_scale else torch.bfloat16, device=x5.device)
     stats = None
     if want_stats:
+        assert not out_scale, "statistics with an fp8 output"
         stats = torch.empty(workers(p, geom, spec.K), 2, spec.K, dtype=torch.float32, device=x5.device)
-    run(x5, wpk, bias, y, stats, p, geom, kd, spec.K, act)
+    run(x5, wpk, bias, y, stats, p, geom, kd, spec.K, act, oscale=1.0 / out_scale if out_scale else 0.0)
     return y, stats
 
 

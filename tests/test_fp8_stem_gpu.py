@@ -114,3 +114,23 @@ def test_tile_f8_matches_halo_f8_model(monkeypatch):
     assert ((a - b).norm() / b.norm()).item() < 2e-2
     la, lb = outs["1"][1], outs["0"][1]
     assert ((la - lb).norm() / lb.norm()).item() < 2e-2
+
+
+def test_bf16_stem_e4m3_epilogue_matches_quant_pass(monkeypatch):
+    """The default fp8 model's bf16 stem writes e4m3 from the tile epilogue: same bytes as the
+    bf16 stem output followed by the quantisation pass (FN_F8_STEM_Q8=0)."""
+    torch.manual_seed(4)
+    m = FeatureNet3D(FeatureNet3DConfig(input_size=64, num_classes=24)).cuda().eval()
+    x = (torch.rand(4, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    q = F8.quantize_model(m, x)
+    assert q.stem is None
+    from featurenet_amd.ops.spec import ConvSpec
+    c1 = m.convs[0]
+    spec = ConvSpec.make(tuple(x.shape), c1.cout, c1.kernel, c1.stride, c1.padding)
+    with torch.no_grad():
+        a = q._bf16_stem_fp8_out(x, spec)
+        from featurenet_amd import ops
+        b = F8.quantize_fp8_act(ops.conv(x, q.c1_w, q.c1_b, spec, "relu"), q.act_scales[0])
+    assert a is not None and a.shape == b.shape and a.dtype == torch.uint8
+    same = (a == b).float().mean().item()
+    assert same > 0.999, same
