@@ -66,6 +66,7 @@ struct TileGeom {
 
 #define CT_NCW 4                       // compute (MFMA) waves
 #define CT_F8_POOL 0x100               // fp8 act flag: fused 2^3 max-pool epilogue
+#define CT_PRIO 0x200                  // act flag: s_setprio 1 on the compute waves
 #define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
 // per-compute-wave BN sums of the workgroup's NT*16 columns
 __host__ __device__ constexpr int ct_red_bytes(int NT) { return CT_NCW * 2 * NT * 16 * 4; }
@@ -324,6 +325,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     tile_lds_barrier();                          // R: the compute waves' BN partials (uniform count)
   } else {
     // ======================= compute waves =======================
+    // FN_TILE_PRIO=1 (CT_PRIO in act): compute waves over the loader wave in SIMD issue
+    // arbitration.  Layer timings moved 1-2 % (noise level), the training step not at all
+    // (26,012 vs 26,069 samples/s over 3 alternating runs each): off by default
+    if ((DBG & 64) != 0 || (act & CT_PRIO) != 0) __builtin_amdgcn_s_setprio(1);
     // MFMA with the weights as A (16 output channels) and the halo as B (16 positions):
     // acc[mt][nt] = C^T, lane (lr, lg) holds channels (ct0+nt)*16 + 4lg + r of position
     // lr of tile mt -- 4 consecutive channels of one output row, stored as one 8-B write
@@ -376,8 +381,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // BN's relu (the stored dx itself has no activation)
     // (fp8: act bit CT_F8_POOL = the 2^3 max-pool epilogue, relu + bf16 output of the pooled grid)
     const int emode = F8 ? (((act & 0xff) == ACT_RELU ? 1 : 0) | (oscale > 0.f ? 2 : 0) | ((act & CT_F8_POOL) ? 4 : 0))
-                         : (BWS ? (4 | (act == ACT_RELU ? 2 : 0))
-                                : ((stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0) | (Q8O ? 8 : 0)));   // (ACT_NONE /
+                         : (BWS ? (4 | ((act & 0xff) == ACT_RELU ? 2 : 0))
+                                : ((stats ? 1 : 0) | ((act & 0xff) == ACT_RELU ? 2 : 0) | (Q8O ? 8 : 0)));   // (ACT_NONE /
                                                                                           // ACT_RELU only; 8: e4m3 out)
     // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
     // the previous job's last turn, so no job starts on an exposed L2 latency
@@ -421,8 +426,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0);
             }
             if constexpr (!(DBG & 2)) fa[mt] = read_a(mt, ko);
-            __builtin_amdgcn_sched_barrier(0);
-          }
+            if constexpr (!(DBG & 128)) __builtin_amdgcn_sched_barrier(0);   // (DBG 128: free scheduling
+          }                                                                  //  within a k-step)
           // k-step ks+u+PD, or the next job's step u (BWS: not before an epilogue -- the ring
           // registers are the statistics epilogue's; it refills the ring after the stores)
           if constexpr (!(DBG & 1)) {
@@ -1211,6 +1216,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
   if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;   // 16-B column groups; relu or none
+  static const int prio = [] { const char* e = getenv("FN_TILE_PRIO"); return e && atoi(e) == 1 ? CT_PRIO : 0; }();
   if (NT == 4 && (Ncol % 64 || bny)) return -2;                        // whole 64-column blocks, no BWS
   // oscale > 0: e4m3 output of y * oscale (no statistics; the 8-channel-slice instances: the
   // space-to-depth stem of the fp8 inference path)
@@ -1219,7 +1225,8 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();
-  if (dbg && MT == 8 && NT == 2 && !bny) {              // experiment variants (timing only; 1-7 give wrong results)
+  if (dbg && MT == 8 && NT == 2 && !bny && oscale == 0.f) {   // experiment variants (timing only; 1-7, 32 give
+                                                              // wrong results; 64, 128, 192 schedule variants)
     static long long* stamps = nullptr;
     const size_t nst = (size_t)grid.x * grid.y * 16;
     if ((dbg & 16) && !stamps && hipMalloc(&stamps, 256 * 64 * 16 * sizeof(long long)) != hipSuccess) return -5;
@@ -1228,6 +1235,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
       (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, stamps);
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
     CT_DBG(4, 23) CT_DBG(2, 32) CT_DBG(4, 32)
+    CT_DBG(2, 64) CT_DBG(2, 128) CT_DBG(2, 192) CT_DBG(4, 64) CT_DBG(4, 128) CT_DBG(4, 192)   // (correct results)
 #undef CT_DBG
     if (rc) return rc;
     FN_CHECK_LAUNCH();
@@ -1248,13 +1256,13 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
     rc = bny ? launch_tile<M, N, C, 0, false, N == 2>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,  \
-                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, \
+                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act | prio, sched, \
                                                     nullptr, nullptr, 0.f, bny, bnp)                              \
              : (oscale > 0.f ? launch_tile<M, N, C, 0, false, false, C == 1 && N == 2>(                          \
                                    grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp,  \
-                                   bias, out, stats, g, Ncol, act, sched, nullptr, nullptr, oscale)                   \
+                                   bias, out, stats, g, Ncol, act | prio, sched, nullptr, nullptr, oscale)                   \
                              : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,         \
-                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched));
+                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act | prio, sched));
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;
