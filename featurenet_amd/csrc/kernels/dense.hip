@@ -36,8 +36,10 @@ __device__ __forceinline__ bf16x8 dn_cvt8(const float4 a, const float4 b) {
 // ---------------------------------------------------------------------------
 // grid (ceil(N/64), ceil(M/128), S); slice s covers k in [s*kc, min(K, (s+1)*kc)), kc % 32 == 0.
 // VEC (K % 8 == 0): 16-B x rows and float4 weight loads; otherwise element loads masked at kend
-// (the 84-wide LeNet layers).
-template <bool VEC>
+// (the 84-wide LeNet layers).  D k-steps of raw operands in flight (a register ring): with one
+// step ahead the loop waited a full memory latency per 32-k step (FC1 at 128^3 inference:
+// 1100 steps per slice, 2.4 ms for 3.4 GB)
+template <bool VEC, int D>
 __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* __restrict__ x,
                                                                     const float* __restrict__ w,
                                                                     float* __restrict__ part, int M, int N, int K,
@@ -68,51 +70,70 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
     wr[j] = w + (long long)(cok[j] ? n : 0) * K;
   }
   const bf16x8 zero8 = {};
-  // one k-step of operands in flight ahead of the MFMAs (raw loads; conversion and masking
-  // happen when the step is consumed)
-  bf16x8 ra[2];
-  float4 rb[4][2];
-  auto load = [&](int k0) {
+  // D k-steps of operands in flight ahead of the MFMAs (raw loads; conversion and masking
+  // happen when the step is consumed; steps past kend read chunk 0 and are never consumed)
+  bf16x8 ra[D][2];
+  float4 rb[D][4][2];
+  auto load = [&](int st, int k0) {
     const int k = k0 + 8 * gq;
     const int ks = k < kend ? k : 0;
     if constexpr (VEC) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) ra[i] = *(const bf16x8*)(xr[i] + ks);
+      for (int i = 0; i < 2; ++i) ra[st][i] = *(const bf16x8*)(xr[i] + ks);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float4* p = (const float4*)(wr[j] + ks);
-        rb[j][0] = p[0];
-        rb[j][1] = p[1];
+        rb[st][j][0] = p[0];
+        rb[st][j][1] = p[1];
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) ra[i][e] = ks + e < kend ? xr[i][ks + e] : f2bf(0.f);
+        for (int e = 0; e < 8; ++e) ra[st][i][e] = ks + e < kend ? xr[i][ks + e] : f2bf(0.f);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float t[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) t[e] = ks + e < kend ? wr[j][ks + e] : 0.f;
-        rb[j][0] = make_float4(t[0], t[1], t[2], t[3]);
-        rb[j][1] = make_float4(t[4], t[5], t[6], t[7]);
+        rb[st][j][0] = make_float4(t[0], t[1], t[2], t[3]);
+        rb[st][j][1] = make_float4(t[4], t[5], t[6], t[7]);
       }
     }
   };
-  if (kbeg < kend) load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += 32) {
-    const bool kok = k0 + 8 * gq < kend;        // (a chunk straddling kend was masked at load)
-    bf16x8 fa[2], fb[4];
+  // branch-free ring: every group of D steps loads and multiplies unconditionally (steps past
+  // kend read chunk 0 and are zeroed by kok): hipcc's vmcnt counting stays exact (a conditional
+  // load or step made it wait for the whole ring)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) fa[i] = (rok[i] && kok) ? ra[i] : zero8;
+  for (int st = 0; st < D; ++st) load(st, kbeg + 32 * st);
+  __builtin_amdgcn_sched_barrier(0);             // (the scheduler otherwise sinks every load to its use)
+  for (int k0 = kbeg; k0 < kend; k0 += 32 * D) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = (cok[j] && kok) ? dn_cvt8(rb[j][0], rb[j][1]) : zero8;
-    if (k0 + 32 < kend) load(k0 + 32);
+    for (int st = 0; st < D; ++st) {
+      const int kk = k0 + 32 * st;
+      {
+        // rows / columns past M / N read row / column 0 and their outputs are never stored: only
+        // chunks past kend (the tail of K) need zeroing.  Conversion first, then a select: a
+        // conditional conversion became an exec-masked branch with a vmcnt(0) wait inside,
+        // which drained the whole ring every step
+        const bool kok = kk + 8 * gq < kend;
+        bf16x8 fa[2], fb[4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i) fa[i] = kok ? ra[st][i] : zero8;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          const bf16x8 t = dn_cvt8(rb[st][j][0], rb[st][j][1]);
+          fb[j] = kok ? t : zero8;
+        }
+        load(st, kk + 32 * D);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
   }
   float* ps = part + (long long)blockIdx.z * M * N;
 #pragma unroll
@@ -353,10 +374,10 @@ extern "C" int fn_dense_fwd(const void* x, const float* w, const float* bias, vo
   kc = (kc + 31) / 32 * 32;
   const int Sr = (K + kc - 1) / kc;              // slices actually covering K
   if (K % 8 == 0)
-    hipLaunchKernelGGL(dense_fwd_part_kernel<true>, dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0,
+    hipLaunchKernelGGL((dense_fwd_part_kernel<true, 4>), dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0,
                        st, (const bf16*)x, w, part, M, N, K, kc);
   else
-    hipLaunchKernelGGL(dense_fwd_part_kernel<false>, dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0,
+    hipLaunchKernelGGL((dense_fwd_part_kernel<false, 1>), dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0,
                        st, (const bf16*)x, w, part, M, N, K, kc);
   FN_CHECK_LAUNCH();
   const long long tot = (long long)M * N;
