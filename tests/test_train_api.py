@@ -235,3 +235,28 @@ def test_resume_from_checkpoint_is_bit_identical(tmp_path):
     assert h2.history["loss"][2:] == full[2:], (h2.history["loss"], full)
     for a, b in zip(tr.model.parameters(), tr2.model.parameters()):
         assert torch.equal(a, b)
+
+
+def test_epoch_metrics_accumulate_like_the_per_step_reductions():
+    """Trainer's device-side epoch sums (one add per step) equal the reference per-step sums,
+    including a smaller last batch and per-voxel correct maps (the scalar fallback)."""
+    import torch
+
+    from featurenet_amd.training.trainer import _EpochMetrics
+
+    torch.manual_seed(0)
+    m = _EpochMetrics(torch.device("cpu"))
+    ref_loss, ref_corr = 0.0, 0
+    for n in (64, 64, 17):
+        loss = torch.rand(())
+        corr = torch.randint(0, 2, (n,), dtype=torch.int32)
+        m.add(loss, corr, n)
+        ref_loss += float(loss) * n
+        ref_corr += int(corr.sum())
+    big = torch.randint(0, 2, (70000,), dtype=torch.int32)        # per-voxel: beyond the vector size
+    m.add(torch.tensor(0.5), big, big.numel())
+    ref_loss += 0.5 * big.numel()
+    ref_corr += int(big.sum())
+    ls, cs = m.totals()
+    assert abs(float(ls) - ref_loss) < 1e-6 * ref_loss
+    assert int(cs) == ref_corr
