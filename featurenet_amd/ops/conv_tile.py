@@ -113,7 +113,8 @@ def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int
     (``f8``: the e4m3 inference variant, 32- or 64-channel slices; ``pool``: with the fused
     2^3 max-pool epilogue -- even output and tile dims)."""
     nw = 4 if f8 else nwaves()
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, nw, tile_nt(), pool)
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, nw, tile_nt(), pool,
+           os.environ.get("FN_TILE_PLAN_RANK", "0"))
     if key in _PLANS:
         return _PLANS[key]
     if pool and (not f8 or any(d % 2 for d in out_dims)):
@@ -188,7 +189,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4, pool=False):
                                           float(cost), f8, nw, pool))
     # the cheapest few, re-costed with their row tables' residual bank conflicts (a
     # fragment whose 16 rows repeat a residue mod 16 reads at half rate)
-    best = None
+    ranked = []
     for c in sorted(cands, key=lambda c: c.cost)[:12]:
         HH, HW = c.TH + KH - 1, c.TW + KW - 1
         if not _magic_ok(HH, HW, c.HPpad):
@@ -197,10 +198,14 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4, pool=False):
         res = tab[:, 0].reshape(-1, 16) % 16
         dups = sum(16 - len(set(r.tolist())) for r in res)
         cost = c.cost * (1.0 + 0.5 * dups / res.size)
-        if best is None or cost < best.cost:
-            best = TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct", "BUF",
-                                                        "mHW", "mHHW")), cost, f8, nw, pool)
-    return best
+        ranked.append(TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct",
+                                                          "BUF", "mHW", "mHHW")), cost, f8, nw, pool))
+    if not ranked:
+        return None
+    ranked.sort(key=lambda c: c.cost)
+    # FN_TILE_PLAN_RANK=k: the k-th cheapest plan of the model (timing sweeps of the cost model)
+    k = int(os.environ.get("FN_TILE_PLAN_RANK", "0"))
+    return ranked[min(k, len(ranked) - 1)]
 
 
 def row_table(p: TilePlan, kdims: tuple) -> np.ndarray:
