@@ -82,9 +82,9 @@ int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                  const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float);
 int fn_conv_tile_workers(const int*, int, int);
-int fn_conv_tile8(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
-                  const int*, int, int, int, int, hipStream_t);
-int fn_conv_tile8_supported(int, int, int);
+int fn_conv_tile32(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
+                   const int*, int, int, int, int*, hipStream_t, float);
+int fn_conv_tile32_supported(int, int);
 int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
                     float, const int*, int, int, int, int, int*, hipStream_t);
 int fn_conv_tile_f8_supported(int, int, int);
@@ -224,20 +224,19 @@ PYBIND11_MODULE(_C, m) {
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("bny") = 0,
      py::arg("bnp") = 0, py::arg("oscale") = 0.f);
-  m.def("conv_tile8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
-                         uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
-                         uintptr_t st, std::vector<long long> ext) {
-    need(geom, 31, "conv_tile8");
-    check_tile(geom, ext, ncol, MT, "conv_tile8");
-    fits(ext, 4, geom[19] + 10LL, "conv_tile8", "ktab");    // nks + 2 PD + 2 entries
-    chk(fn_conv_tile8(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
-                      P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
-                      act, MT, NT, S(st)),
-        "conv_tile8");
+  m.def("conv_tile32", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
+                          uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MB,
+                          uintptr_t sched, uintptr_t st, std::vector<long long> ext, float oscale) {
+    need(geom, 31, "conv_tile32");
+    check_tile(geom, ext, ncol, 2 * MB, "conv_tile32");   // (row table: 4 waves x 2MB 16-row fragments)
+    chk(fn_conv_tile32(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
+                       P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
+                       act, MB, P<int*>(sched), S(st), oscale),
+        "conv_tile32");
   }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
-     py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"), py::arg("st"),
-     py::arg("ext") = std::vector<long long>());
-  m.def("conv_tile8_supported", &fn_conv_tile8_supported);
+     py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MB"), py::arg("sched"),
+     py::arg("st"), py::arg("ext"), py::arg("oscale") = 0.f);
+  m.def("conv_tile32_supported", &fn_conv_tile32_supported);
   m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
                            uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,
                            int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext) {
@@ -318,9 +317,14 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 8, "pad3");
     chk(fn_pad3(P<void*>(x), P<void*>(out), geom.data(), dir, S(st)), "pad3");
   });
-  m.def("pad_channels", [](uintptr_t x, uintptr_t out, long long rows, int C, int CP, int dir, uintptr_t st) {
+  m.def("pad_channels", [](uintptr_t x, uintptr_t out, long long rows, int C, int CP, int dir, uintptr_t st,
+                           std::vector<long long> ext) {
+    // dir 0: x [rows, C] -> out [rows, CP]; dir 1: x [rows, CP] -> out [rows, C]
+    fits(ext, 0, rows * (dir == 0 ? C : CP), "pad_channels", "x");
+    fits(ext, 1, rows * (dir == 0 ? CP : C), "pad_channels", "out");
     chk(fn_pad_channels(P<void*>(x), P<void*>(out), rows, C, CP, dir, S(st)), "pad_channels");
-  });
+  }, py::arg("x"), py::arg("out"), py::arg("rows"), py::arg("C"), py::arg("CP"), py::arg("dir"), py::arg("st"),
+     py::arg("ext"));
   m.def("dense_splits", &fn_dense_splits);
   m.def("dense_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t part, int M, int N, int K,
                         int nsplit, int act, int out_fp32, uintptr_t st, std::vector<long long> ext) {

@@ -37,64 +37,11 @@
 // (CS >= 32), two taps x 16 channels (CS = 16) or four taps x 8 channels (CS = 8).
 //
 // Dgrad uses the same kernel: dx = conv(dy, flip(W)^T) with leading pads K-1-p.
-#include "common.h"
-#include "tile_dma.h"
+#include "conv_tile_shared.h"
 
 #include <cstdio>
 #include <type_traits>
 #include <vector>
-
-struct TileGeom {
-  int N, ID, IH, IW, C;     // gathered source (x for fwd, dy for dgrad), channels-last
-  int OD, OH, OW;           // output dims
-  int KD, KH, KW;           // kernel
-  int pd, ph, pw;           // leading pads (stride 1)
-  int TD, TH, TW;           // output tile
-  int CS;                   // channels per halo slice (jobs per tile = C / CS)
-  int HPpad;                // halo positions rounded up to a multiple of 64 (whole DMA rows)
-  int nks;                  // k-steps per job (multiple of the B prefetch depth)
-  int nct;                  // 16-column tiles of the packed weights (ceil(Ncol / 16))
-  unsigned mHW, mHHW;       // magic multipliers: p / HW == umulhi(p, mHW) (host-verified)
-  int BUF;                  // bytes per LDS buffer (halo or epilogue staging), multiple of 16
-  unsigned mTW, mTH;        // magic multipliers for the epilogue's tile-row decode
-  // output view: output position (n, d, h, w) is stored at position index
-  // n*osn + ob + d*osd + h*osh + w*osw (x Ncol elements); natural layout = (OD*OH*OW, 0,
-  // OH*OW, OW, 1).  A strided view writes one parity class of a sub-pixel (upsample x2)
-  // convolution straight into the full-resolution output.
-  int osn, ob, osd, osh, osw;
-};
-
-#define CT_NCW 4                       // compute (MFMA) waves
-#define CT_F8_POOL 0x100               // fp8 act flag: fused 2^3 max-pool epilogue
-#define CT_PRIO 0x200                  // act flag: s_setprio 1 on the compute waves
-#define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
-// per-compute-wave BN sums of the workgroup's NT*16 columns
-__host__ __device__ constexpr int ct_red_bytes(int NT) { return CT_NCW * 2 * NT * 16 * 4; }
-
-// packed bf16 pairs (low half = element 0)
-__device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }
-__device__ __forceinline__ float bf16_hi(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
-__device__ __forceinline__ unsigned bf16x2_pack(float lo, float hi) {
-  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  const bf16x2_t p = {f2bf(lo), f2bf(hi)};
-  return __builtin_bit_cast(unsigned, p);
-}
-
-// sum over the 16 lanes of a DPP row (every lane of the row gets it): quad swaps, then
-// half-row and row mirrors
-__device__ __forceinline__ float ct_sum16(float x) {
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));    // quad [1,0,3,2]
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));    // quad [2,3,0,1]
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));   // row_half_mirror
-  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));   // row_mirror
-  return x;
-}
-
-typedef int ct_i32x8 __attribute__((ext_vector_type(8)));
-
-// B-ring depth (k-steps in flight): a bf16 k-step is MT*NT 16-cycle MFMAs, an fp8 one
-// MT*NT 32-cycle block-scaled MFMAs, so 2 fp8 steps cover the latency 4 bf16 steps do
-__host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : (NT == 2 ? 4 : 2); }
 
 // F8 = false: bf16 operands, v_mfma_f32_16x16x32_bf16, k-step 32; CPP = 16-B chunks (8
 //   channels) per halo position.
@@ -124,11 +71,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   constexpr int PD = ct_pd(NT, F8);
   constexpr int ESZ = F8 ? 1 : 2;                // bytes per element of the source / weights
   constexpr int FRAG = F8 ? 32 : 16;             // bytes per lane of one MFMA operand fragment
-  // NT = 2: 32-column blocks (a lane stores 8 consecutive columns); NT = 4 (bf16, Ncol % 64 ==
-  // 0): 64 columns per workgroup, each halo fragment read feeds 4 MFMAs instead of 2 -- the
-  // one-wave-per-SIMD k-loop was issue-bound at 2 (one ds_read_b128 + address add per MFMA
-  // pair); a lane then stores 16 consecutive columns and the bias is read from LDS
-  static_assert(NT == 2 || (NT == 4 && !F8 && !BWS), "32-column blocks, or 64 for the plain bf16 kernel");
+  // NT = 2: 32-column blocks (a lane stores 8 consecutive columns).  (Round 3 measured 64-column
+  // NT = 4 workgroups 3-4 % slower -- 256 VGPRs for 5 waves per CU -- and round 4 removed them;
+  // conv_tile32_kernel takes wide tiles on the 32x32x16 MFMA instead.)
+  static_assert(NT == 2, "32-column blocks");
   constexpr int RC = NT * 16;                    // columns of the workgroup (BN partial row length)
   constexpr int NV = 4 * NT;                     // consecutive columns per lane in the epilogue
   static_assert(!F8 || CPP == 2 || CPP == 4, "fp8: 32- or 64-channel slices");
@@ -163,12 +109,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // F8: the dequantisation scale and bias of this workgroup's 32 columns ([scale 32][bias 32]),
   // read by the epilogue from LDS (global loads there serialised every tile's stores)
   float* s_sb = reinterpret_cast<float*>(s_pos + g.HPpad);
-  if constexpr (NT == 4) {                       // (NT = 4: the bias, [64])
-    if (tid < RC) {
-      const int c = blockIdx.y * RC + tid;
-      s_sb[tid] = (bias && c < Ncol) ? bias[c] : 0.f;
-    }
-  }
   if constexpr (F8) {
     if (tid < NT * 16) {
       const int c = blockIdx.y * NT * 16 + tid;
@@ -209,56 +149,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // address math per DMA row; halos crossing the input boundary check every position
   // and read the zero page outside.
   auto dma_job = [&](int tile, int slice, int bufoff) {
-    tile = __builtin_amdgcn_readfirstlane(tile);   // (wave-uniform: the SGPR operands need proof)
-    slice = __builtin_amdgcn_readfirstlane(slice);
-    bufoff = __builtin_amdgcn_readfirstlane(bufoff);
-    int t = tile;
-    const int tw = t % twn; t /= twn;
-    const int th = t % thn; t /= thn;
-    const int td = t % tdn;
-    const int n = t / tdn;
-    const int dlo = td * g.TD - g.pd, hlo = th * g.TH - g.ph, wlo = tw * g.TW - g.pw;
-    const bool interior = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID &&
-                          hlo + HH <= g.IH && wlo + HW <= g.IW;
-    const unsigned char* base = src + ((long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS) * ESZ;
-    const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
-    // position rows in batches of 8: the s_pos reads of a batch are in flight together
-    // (one LDS latency per batch, not per DMA row)
-    const int NR = g.HPpad >> 6;
-    if (interior) {
-      const unsigned char* obase = base + (((long long)dlo * g.IH + hlo) * g.IW + wlo) * g.C * ESZ;
-      for (int r0 = 0; r0 < NR; r0 += 8) {
-        int po[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) po[i] = s_pos[((r0 + i < NR ? r0 + i : NR - 1) << 6) + lane].x;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (r0 + i < NR) {
-#pragma unroll
-            for (int c = 0; c < CPP; ++c)
-              ct_glds16_s(obase, (unsigned)(po[i] + c * 16), dst0 + (unsigned)(c * PLANE + ((r0 + i) << 10)));
-          }
-        }
-      }
-    } else {
-      for (int r0 = 0; r0 < NR; r0 += 8) {
-        int e[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = s_pos[((r0 + i < NR ? r0 + i : NR - 1) << 6) + lane].y;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (r0 + i < NR) {
-            const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
-            const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-                            (unsigned)gw < (unsigned)g.IW;
-            const unsigned char* gsrc = ok ? base + (long long)((gd * g.IH + gh) * g.IW + gw) * g.C * ESZ : zp;
-#pragma unroll
-            for (int c = 0; c < CPP; ++c)
-              ct_glds16(ok ? gsrc + c * 16 : zp, dst0 + (unsigned)(c * PLANE + ((r0 + i) << 10)));
-          }
-        }
-      }
-    }
+    ct_dma_job<CPP, ESZ>(g, src, zp, dsm, s_pos, tile, slice, bufoff, lane, tdn, thn, twn);
   };
 
   // DBG & 16: cycle stamps of wave 0 and the loader (barrier-A wait, job work, tile end)
@@ -325,10 +216,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     tile_lds_barrier();                          // R: the compute waves' BN partials (uniform count)
   } else {
     // ======================= compute waves =======================
-    // FN_TILE_PRIO=1 (CT_PRIO in act): compute waves over the loader wave in SIMD issue
-    // arbitration.  Layer timings moved 1-2 % (noise level), the training step not at all
-    // (26,012 vs 26,069 samples/s over 3 alternating runs each): off by default
-    if ((DBG & 64) != 0 || (act & CT_PRIO) != 0) __builtin_amdgcn_s_setprio(1);
+    if constexpr ((DBG & 64) != 0) __builtin_amdgcn_s_setprio(1);   // (timing variant: compute waves first)
     // MFMA with the weights as A (16 output channels) and the halo as B (16 positions):
     // acc[mt][nt] = C^T, lane (lr, lg) holds channels (ct0+nt)*16 + 4lg + r of position
     // lr of tile mt -- 4 consecutive channels of one output row, stored as one 8-B write
@@ -343,9 +231,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
     // ct0*16 + 4*NT*lg + 4nt + r: a lane ends with NV = 4*NT consecutive columns of one position
     const int gc8 = ct0 * 16 + NV * lg;
-    float bias8[8];                              // (fp8 / NT = 4: read in the epilogue from LDS, no
-#pragma unroll                                   // live registers across the k-loop)
-    for (int j = 0; j < 8; ++j) bias8[j] = (NT == 2 && !F8 && !BWS && bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
+    float bias8[8];                              // (fp8: read in the epilogue from LDS, no live
+#pragma unroll                                   // registers across the k-loop)
+    for (int j = 0; j < 8; ++j) bias8[j] = (!F8 && !BWS && bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
     constexpr unsigned FTILE = 64u * FRAG;       // bytes of one 16-column fragment of a k-step
     const unsigned wstep = (unsigned)g.nct * FTILE;   // bytes per k-step of the packed weights
     unsigned voffb[PD];                          // per-lane B offsets of the PD ring slots
@@ -498,7 +386,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             }
           }
           // one pass per 8 consecutive columns of the lane (fragments 2h, 2h+1): one 16-B store
-          // per row and 8 + 8 live partial sums (NT = 4 with all 16 columns' sums live spilled)
+          // per row and 8 + 8 live partial sums
 #pragma unroll
           for (int h = 0; h < NT / 2; ++h) {
             float ts[8], tq[8];                  // this tile's BN partial sums of the pass's 8 columns
@@ -510,7 +398,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
               float v[8];
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
-                const float b = NT == 2 ? bias8[j] : s_sb[NV * lg + 8 * h + j];
+                const float b = bias8[j];
                 v[j] = bf16_lo(bf16x2_pack(acc[mt][2 * h + (j >> 2)][j & 3] + b, 0.f));   // the stored bf16 value
                 if constexpr (RELU_OUT) v[j] = fmaxf(v[j], 0.f);
               }
@@ -716,327 +604,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
 }
 
 // ---------------------------------------------------------------------------
-// conv_tile8: 8 MFMA waves (two per SIMD), split-K pairs, no loader wave (round 3)
-// ---------------------------------------------------------------------------
-// The same tile, halo layout, row table, k-table, packed weights and epilogue as
-// conv_tile_kernel, but every SIMD runs TWO compute waves that own the same 16*MT output
-// rows x 32 columns and split each job's k-steps between them (wave w, w + 4: even / odd
-// k-steps).  A lone wave per SIMD was issue- and latency-bound (one ds_read_b128 + one
-// address add + one wait per MFMA pair at 4 cycles per VALU instruction: the k-loop ran at
-// ~72 % of MFMA issue); two waves interleave their MFMA streams and double the VALU issue
-// rate, at the same LDS and L2 traffic per MFMA.  The halo DMA is issued by the compute
-// waves themselves, 1/8 of the rows each, by waves 0-3 at their first k-step and by waves
-// 4-7 at mid-job (the two waves of a SIMD never pause their MFMAs together).  At a tile's
-// last slice the pair exchanges half its accumulators through the just-consumed halo
-// buffer (two rounds of 32 KiB) and each wave finalises half of the rows.  Tiles are
-// assigned statically (tile b, b + W, ...), so no atomics sit on any wave's critical path.
-template <int MT, int NT, int CPP>
-__global__ __launch_bounds__(512, 1) void conv_tile8_kernel(const unsigned char* __restrict__ src,
-                                                           const uint4* __restrict__ wp,
-                                                           const int2* __restrict__ rowtab,
-                                                           const int4* __restrict__ ktab,
-                                                           const unsigned char* __restrict__ zp,
-                                                           const float* __restrict__ bias, void* __restrict__ out,
-                                                           float* __restrict__ stats, TileGeom g, int Ncol, int act) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  constexpr int PD = 4;                          // B ring depth (this wave's k-steps in flight)
-  constexpr int MH = MT / 2;                     // rows blocks each wave of a pair finalises
-  static_assert(NT == 2 && MT % 4 == 0, "32-column blocks, MT a multiple of 4");
-  const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
-  const int HP = (g.TD + g.KD - 1) * HH * HW;
-  const int PLANE = g.HPpad * 16;
-  const int tdn = (g.OD + g.TD - 1) / g.TD, thn = (g.OH + g.TH - 1) / g.TH, twn = (g.OW + g.TW - 1) / g.TW;
-  const int ntiles = g.N * tdn * thn * twn;
-  const int nslice = g.C / g.CS;
-  const int nks = g.nks, nkw = nks >> 1;         // k-steps per job, per wave
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int rg = wave & 3, hp = wave >> 2;       // row group, k-step parity
-  const int lr = lane & 15, lg = lane >> 4;
-  const int ct0 = blockIdx.y * NT;
-  // LDS: [buffer 0][buffer 1][BN partials 8 waves x 64][k-step offsets (nks + 2PD + 2) int4][positions]
-  float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF);
-  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 8 * 64 * 4);
-  int2* s_pos = reinterpret_cast<int2*>(s_kt + (nks + 2 * PD + 2));
-  for (int i = tid; i < nks + 2 * PD + 2; i += 512) s_kt[i] = ktab[i];
-  for (int i = tid; i < 8 * 64; i += 512) s_red[i] = 0.f;
-  for (int p = tid; p < g.HPpad; p += 512) {
-    const int pc = p < HP ? p : HP - 1;
-    const int hd = pc / (HH * HW), hh = (pc / HW) % HH, hw = pc % HW;
-    s_pos[p] = make_int2(((hd * g.IH + hh) * g.IW + hw) * g.C * 2, (hd << 16) | (hh << 8) | hw);
-  }
-  int lb[MT], roff[MT], rpk[MT];
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const int2 rt = rowtab[(rg * MT + mt) * 16 + lr];
-    lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;
-    const int tw = rt.y % g.TW, th = (rt.y / g.TW) % g.TH, td = rt.y / (g.TW * g.TH);
-    roff[mt] = rt.y < 0 ? -1 : td * g.osd + th * g.osh + tw * g.osw;
-    rpk[mt] = (td << 16) | (th << 8) | tw;
-  }
-  // static schedule: job j = (tile blockIdx.x + (j / nslice) * W, slice j % nslice)
-  const int W = (int)gridDim.x;
-  const int my_tiles = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / W + 1 : 0;
-  const int njobs = my_tiles * nslice;
-  auto job_tile = [&](int j) { return (int)blockIdx.x + (j / nslice) * W; };
-
-  // 1/8 of the halo rows of job (tile, slice) into the buffer at bufoff: rows wave, wave+8, ...
-  auto dma_job = [&](int tile, int slice, int bufoff) {
-    tile = __builtin_amdgcn_readfirstlane(tile);
-    slice = __builtin_amdgcn_readfirstlane(slice);
-    bufoff = __builtin_amdgcn_readfirstlane(bufoff);
-    int t = tile;
-    const int tw = t % twn; t /= twn;
-    const int th = t % thn; t /= thn;
-    const int td = t % tdn;
-    const int n = t / tdn;
-    const int dlo = td * g.TD - g.pd, hlo = th * g.TH - g.ph, wlo = tw * g.TW - g.pw;
-    const bool interior = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID &&
-                          hlo + HH <= g.IH && wlo + HW <= g.IW;
-    const unsigned char* base = src + ((long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS) * 2;
-    const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
-    const int NR = g.HPpad >> 6;
-    if (interior) {
-      const unsigned char* obase = base + (((long long)dlo * g.IH + hlo) * g.IW + wlo) * g.C * 2;
-      for (int r0 = wave; r0 < NR; r0 += 8 * 4) {
-        int po[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) po[i] = s_pos[(min(r0 + 8 * i, NR - 1) << 6) + lane].x;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = r0 + 8 * i;
-          if (r < NR) {
-#pragma unroll
-            for (int c = 0; c < CPP; ++c)
-              ct_glds16_s(obase, (unsigned)(po[i] + c * 16), dst0 + (unsigned)(c * PLANE + (r << 10)));
-          }
-        }
-      }
-    } else {
-      for (int r0 = wave; r0 < NR; r0 += 8 * 4) {
-        int e[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) e[i] = s_pos[(min(r0 + 8 * i, NR - 1) << 6) + lane].y;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = r0 + 8 * i;
-          if (r < NR) {
-            const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
-            const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-                            (unsigned)gw < (unsigned)g.IW;
-            const unsigned char* gsrc = ok ? base + (long long)((gd * g.IH + gh) * g.IW + gw) * g.C * 2 : zp;
-#pragma unroll
-            for (int c = 0; c < CPP; ++c)
-              ct_glds16(ok ? gsrc + c * 16 : zp, dst0 + (unsigned)(c * PLANE + (r << 10)));
-          }
-        }
-      }
-    }
-  };
-
-  tile_lds_barrier();                            // tables visible
-  if (njobs > 0) dma_job(job_tile(0), 0, 0);
-
-  f32x4 acc[MT][NT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[MT];
-  bf16x8 fb[PD][NT];
-  const int gc8 = ct0 * 16 + 8 * lg;
-  constexpr unsigned FTILE = 64u * 16u;
-  const unsigned wstep = (unsigned)g.nct * FTILE;
-  unsigned voffb[PD];                            // this wave's ring slots: every other k-step
-#pragma unroll
-  for (int u = 0; u < PD; ++u) voffb[u] = (unsigned)lane * 16 + (unsigned)(2 * u + hp) * wstep;
-  auto load_b = [&](const unsigned char* base, int slot) {
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) fb[slot][nt] = *(const bf16x8*)(base + voffb[slot] + nt * FTILE);
-  };
-  auto read_a = [&](int mt, int ko) -> bf16x8 { return *(const bf16x8*)(dsm + lb[mt] + ko); };
-  auto kofs = [&](int k) -> int { return *((const int*)(s_kt + k) + lg); };
-  const int emode = (stats ? 1 : 0) | (act == ACT_RELU ? 2 : 0);
-  // ring prologue: job 0 (slice 0), this wave's first PD k-steps
-#pragma unroll
-  for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * FTILE, u);
-  // waves 0-3 issue the next job's DMA at their first turn, waves 4-7 at mid-job
-  const int kdma = hp == 0 ? 0 : ((nkw / 2) / PD) * PD;
-  int par = 0;
-  for (int j = 0; j < njobs; ++j) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's share of job j's halo
-    tile_lds_barrier();                          // A(j): job j's halo landed, the other buffer is free
-    const int tile = job_tile(j), slice = j % nslice;
-    const bool has_next = j + 1 < njobs;
-    const int ntile = has_next ? job_tile(j + 1) : 0, nslc = has_next ? (j + 1) % nslice : 0;
-    const unsigned char* wbase = reinterpret_cast<const unsigned char*>(wp) +
-                                 ((size_t)slice * nks * g.nct + ct0) * FTILE + 2 * PD * wstep;
-    const unsigned char* wnext =
-        reinterpret_cast<const unsigned char*>(wp) + ((size_t)nslc * nks * g.nct + ct0) * FTILE;
-    {
-      const int ko = kofs(hp);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) fa[mt] = read_a(mt, ko);
-    }
-    int ko_n = kofs(hp + 2);
-    for (int ks = 0; ks < nkw; ks += PD) {       // this wave's k-steps hp + 2 (ks + u)
-      if (ks == kdma && has_next) dma_job(ntile, nslc, (par ^ 1) * g.BUF);
-      const unsigned char* wl = ks + PD >= nkw ? wnext : wbase;
-#pragma unroll
-      for (int u = 0; u < PD; ++u) {
-        const int ko = ko_n;
-        ko_n = kofs(hp + 2 * (ks + u) + 4);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0);
-          fa[mt] = read_a(mt, ko);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        load_b(wl, u);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      wbase += 2 * PD * wstep;
-    }
-    if (slice == nslice - 1) {
-      // ---- split-K reduction: the pair exchanges half its accumulators through this job's
-      // (consumed) halo buffer, in two rounds of 32 KiB; wave (rg, hp) finalises row blocks
-      // [hp * MH, hp * MH + MH)
-      float4* xch = reinterpret_cast<float4*>(dsm + par * g.BUF);
-      // rounds of 64 KiB / RQ (RQ = 2 for buffers >= 32 KiB, 4 for the 16-32 KiB halos of CS = 8)
-      auto exchange = [&](auto hpc, auto rqc) {
-        constexpr int H = decltype(hpc)::value;
-        constexpr int RQ = decltype(rqc)::value, BR = MH / RQ;   // rounds, row blocks per round
-#pragma unroll
-        for (int q = 0; q < RQ; ++q) {
-          tile_lds_barrier();                    // every wave is done reading the buffer / last round
-#pragma unroll
-          for (int i = 0; i < BR; ++i) {         // export the partner's half: blocks (1-H)*MH + q*BR + i
-            const int mt = (1 - H) * MH + q * BR + i;
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
-              xch[(((H * 4 + rg) * BR + i) * NT + nt) * 64 + lane] =
-                  make_float4(acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]);
-          }
-          tile_lds_barrier();
-#pragma unroll
-          for (int i = 0; i < BR; ++i) {         // import mine from the partner (parity 1 - H)
-            const int mt = H * MH + q * BR + i;
-#pragma unroll
-            for (int nt = 0; nt < NT; ++nt) {
-              const float4 v = xch[((((1 - H) * 4 + rg) * BR + i) * NT + nt) * 64 + lane];
-              acc[mt][nt][0] += v.x;
-              acc[mt][nt][1] += v.y;
-              acc[mt][nt][2] += v.z;
-              acc[mt][nt][3] += v.w;
-            }
-          }
-        }
-      };
-      if (g.BUF >= 32768) {
-        if (hp == 0) exchange(std::integral_constant<int, 0>{}, std::integral_constant<int, 2>{});
-        else exchange(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
-      } else {
-        if (hp == 0) exchange(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
-        else exchange(std::integral_constant<int, 1>{}, std::integral_constant<int, 4>{});
-      }
-      // ---- epilogue of this wave's half: (+bias) -> bf16 -> activation -> 16-B stores (+BN sums)
-      int t = tile;
-      const int tw_i = t % twn; t /= twn;
-      const int th_i = t % thn; t /= thn;
-      const int td_i = t % tdn;
-      const int n = t / tdn;
-      const int d0 = td_i * g.TD, h0 = th_i * g.TH, w0 = tw_i * g.TW;
-      const int ld = g.OD - d0, lh = g.OH - h0, lw = g.OW - w0;
-      const bool edge = ld < g.TD || lh < g.TH || lw < g.TW;
-      const long long obase_e =
-          ((long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh + w0 * g.osw) * Ncol + gc8;
-      bf16* obase = reinterpret_cast<bf16*>(out) + obase_e;
-      auto epilogue = [&](auto hpc, auto mode) {
-        constexpr int H = decltype(hpc)::value;
-        constexpr int M = decltype(mode)::value;
-        constexpr bool RELU = (M & 2) != 0, ST = (M & 1) != 0;
-        float bias8[8];
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) bias8[jj] = (bias && gc8 + jj < Ncol) ? bias[gc8 + jj] : 0.f;
-        float ts[8], tq[8];
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) ts[jj] = tq[jj] = 0.f;
-#pragma unroll
-        for (int i = 0; i < MH; ++i) {
-          const int mt = H * MH + i;
-          bool ok = roff[mt] >= 0 && gc8 < Ncol;
-          if (edge) ok = ok && (rpk[mt] >> 16) < ld && ((rpk[mt] >> 8) & 255) < lh && (rpk[mt] & 255) < lw;
-          float v[8];
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) {
-            v[jj] = bf16_lo(bf16x2_pack(acc[mt][jj >> 2][jj & 3] + bias8[jj], 0.f));
-            if constexpr (RELU) v[jj] = fmaxf(v[jj], 0.f);
-          }
-          if constexpr (ST) {
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-              const float x = ok ? v[jj] : 0.f;
-              ts[jj] += x;
-              tq[jj] += x * x;
-            }
-          }
-          if (ok)
-            *(uint4*)(obase + (long long)roff[mt] * Ncol) = make_uint4(
-                bf16x2_pack(v[0], v[1]), bf16x2_pack(v[2], v[3]), bf16x2_pack(v[4], v[5]), bf16x2_pack(v[6], v[7]));
-        }
-        if constexpr (ST) {
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) {
-            ts[jj] = ct_sum16(ts[jj]);
-            tq[jj] = ct_sum16(tq[jj]);
-          }
-          if (lr == 0) {                         // fixed order per wave: deterministic statistics
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-              s_red[wave * 64 + 8 * lg + jj] += ts[jj];
-              s_red[wave * 64 + 32 + 8 * lg + jj] += tq[jj];
-            }
-          }
-        }
-      };
-      auto run = [&](auto hpc) {
-        switch (emode) {
-          case 0: epilogue(hpc, std::integral_constant<int, 0>{}); break;
-          case 1: epilogue(hpc, std::integral_constant<int, 1>{}); break;
-          case 2: epilogue(hpc, std::integral_constant<int, 2>{}); break;
-          default: epilogue(hpc, std::integral_constant<int, 3>{}); break;
-        }
-      };
-      if (hp == 0) run(std::integral_constant<int, 0>{});
-      else run(std::integral_constant<int, 1>{});
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) lb[mt] += (1 - 2 * par) * g.BUF;   // the other buffer
-    par ^= 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the last job's unused ring loads
-  tile_lds_barrier();
-  if (stats && tid < NT * 16 && ct0 * 16 + tid < Ncol) {
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      s1 += s_red[w * 64 + tid];
-      s2 += s_red[w * 64 + 32 + tid];
-    }
-    float* row = stats + (long long)blockIdx.x * 2 * Ncol;
-    row[ct0 * 16 + tid] = s1;
-    row[Ncol + ct0 * 16 + tid] = s2;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // weight packing: conv weight [K][T][C] (fp32) -> MFMA B fragments
 // ---------------------------------------------------------------------------
 // out[((slice * nks + ks) * nct + ct) * 64 + lane][j] (8 bf16 per lane) =
@@ -1067,9 +634,28 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
   // column order inside each nt*16-column block: fragment ct%nt, row i holds output column
   // 4nt*(i/4) + 4*(ct%nt) + i%4, so after the kernel's C^T MFMA a lane's nt fragments give 4nt
   // consecutive output columns (one 16-B store per 8)
+  int tap, ch0, col;
+  if (nt == 32) {
+    // conv_tile32 (v_mfma_f32_32x32x16_bf16, weights = A): fragment ct = 2 * (32-column block) + j
+    // (k half of the 32-k step); lane l holds MFMA row m = l & 31 -- output column
+    // 16((m>>2)&1) + (m&3) + 4(m>>3) of the block, so a lane half's accumulator holds 16
+    // consecutive columns -- and k = 8(l >> 5) + e
+    const int m = lane & 31, h = lane >> 5, j = ct & 1;
+    col = (ct >> 1) * 32 + 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3);
+    if (CS >= 32) {
+      const int sub = CS / 32;
+      tap = ks / sub;
+      ch0 = slice * CS + (ks % sub) * 32 + 16 * j + 8 * h;
+    } else if (CS == 16) {
+      tap = 2 * ks + j;
+      ch0 = slice * 16 + 8 * h;
+    } else {                                     // CS = 8: taps 4ks + 2j + h
+      tap = 4 * ks + 2 * j + h;
+      ch0 = slice * 8;
+    }
+  } else {
   const int fi = lane & 15;
-  const int col = (ct / nt) * nt * 16 + 4 * nt * (fi >> 2) + 4 * (ct % nt) + (fi & 3);
-  int tap, ch0;
+  col = (ct / nt) * nt * 16 + 4 * nt * (fi >> 2) + 4 * (ct % nt) + (fi & 3);
   if (CS >= 32) {
     const int sub = CS / 32;
     tap = ks / sub;
@@ -1080,6 +666,7 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
   } else {                                       // CS = 8: four taps per k-step
     tap = 4 * ks + (lane >> 4);
     ch0 = slice * 8;
+  }
   }
   Pack8 v;
 #pragma unroll
@@ -1097,7 +684,7 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
 extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, int CS, int nks, int nct, int nslice,
                               int dgrad, int nt, hipStream_t st) {
   if (CS != 8 && CS != 16 && CS % 32 != 0) return -2;
-  if ((nt != 2 && nt != 4) || nct % nt) return -2;
+  if ((nt != 2 && nt != 32) || nct % 2) return -2;   // 2: conv_tile_kernel, 32: conv_tile32_kernel
   const long long total = ((long long)nslice * nks + 4) * nct * 64;
   hipLaunchKernelGGL(tile_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (uint4*)out, K, T,
                      C, CS, nks, nct, nslice, dgrad, nt);
@@ -1108,20 +695,6 @@ extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, in
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
-#define CT_GEOM_LEN 31
-static TileGeom parse_tile(const int* v) {
-  TileGeom g;
-  g.N = v[0]; g.ID = v[1]; g.IH = v[2]; g.IW = v[3]; g.C = v[4];
-  g.OD = v[5]; g.OH = v[6]; g.OW = v[7];
-  g.KD = v[8]; g.KH = v[9]; g.KW = v[10];
-  g.pd = v[11]; g.ph = v[12]; g.pw = v[13];
-  g.TD = v[14]; g.TH = v[15]; g.TW = v[16];
-  g.CS = v[17]; g.HPpad = v[18]; g.nks = v[19]; g.nct = v[20];
-  g.mHW = (unsigned)v[21]; g.mHHW = (unsigned)v[22]; g.BUF = v[23];
-  g.mTW = (unsigned)v[24]; g.mTH = (unsigned)v[25];
-  g.osn = v[26]; g.ob = v[27]; g.osd = v[28]; g.osh = v[29]; g.osw = v[30];
-  return g;
-}
 
 static int g_tile_cus = 0;
 
@@ -1158,8 +731,7 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
 }
 
 // instantiations (MT, NT, CPP) -- the Python planner only emits these
-#define CT_INSTANCES(X) X(8, 2, 1) X(9, 2, 1) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4) \
-  X(6, 4, 2) X(6, 4, 4) X(7, 4, 2) X(7, 4, 4)
+#define CT_INSTANCES(X) X(8, 2, 1) X(9, 2, 1) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4)
 
 extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 #define CT_SUP(M, N, C) if (MT == M && NT == N && CPP == C) return 1;
@@ -1171,7 +743,7 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, bool bws = false) {
   const int PD = ct_pd(NT, f8);
   return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
-         (bws ? (size_t)NT * 16 * 16 : 0) + (f8 ? (size_t)NT * 16 * 8 : 0) + (NT == 4 ? (size_t)NT * 16 * 4 : 0);
+         (bws ? (size_t)NT * 16 * 16 : 0) + (f8 ? (size_t)NT * 16 * 8 : 0);
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -1216,8 +788,6 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
   if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;   // 16-B column groups; relu or none
-  static const int prio = [] { const char* e = getenv("FN_TILE_PRIO"); return e && atoi(e) == 1 ? CT_PRIO : 0; }();
-  if (NT == 4 && (Ncol % 64 || bny)) return -2;                        // whole 64-column blocks, no BWS
   // oscale > 0: e4m3 output of y * oscale (no statistics; the 8-channel-slice instances: the
   // space-to-depth stem of the fp8 inference path)
   if (!(oscale >= 0.f) || (oscale > 0.f && (stats || bny || NT != 2 || CPP != 1))) return -2;
@@ -1256,13 +826,13 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
     rc = bny ? launch_tile<M, N, C, 0, false, N == 2>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,  \
-                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act | prio, sched, \
+                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, \
                                                     nullptr, nullptr, 0.f, bny, bnp)                              \
              : (oscale > 0.f ? launch_tile<M, N, C, 0, false, false, C == 1 && N == 2>(                          \
                                    grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp,  \
-                                   bias, out, stats, g, Ncol, act | prio, sched, nullptr, nullptr, oscale)                   \
+                                   bias, out, stats, g, Ncol, act, sched, nullptr, nullptr, oscale)                   \
                              : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,         \
-                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act | prio, sched));
+                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched));
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;
@@ -1357,63 +927,6 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   CT_F8_INSTANCES(CT_F8_CASE)
 #undef CT_F8_CASE
   if (rc) return rc;
-  FN_CHECK_LAUNCH();
-  return 0;
-}
-
-// ---------------------------------------------------------------------------
-// conv_tile8 host launcher (same geometry / tables as fn_conv_tile; the k-table has
-// nks + 2 PD + 2 entries, nks a multiple of 8, MT = 8)
-// ---------------------------------------------------------------------------
-extern "C" int fn_conv_tile8_supported(int MT, int NT, int CPP) {
-  return MT == 8 && NT == 2 && (CPP == 1 || CPP == 2 || CPP == 4);
-}
-
-static size_t tile8_lds_total(const TileGeom& g) {
-  return 2 * (size_t)g.BUF + 8 * 64 * 4 + (size_t)(g.nks + 2 * 4 + 2) * 16 + (size_t)g.HPpad * 8;
-}
-
-extern "C" int fn_conv_tile8(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
-                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
-                             int NT, hipStream_t st) {
-  const TileGeom g = parse_tile(geom);
-  if (g.CS != 8 && g.CS != 16 && g.CS != 32) return -2;
-  const int CPP = g.CS / 8;
-  if (!fn_conv_tile8_supported(MT, NT, CPP)) return -2;
-  if (g.C % g.CS || g.TD * g.TH * g.TW > 64 * MT || g.TD < 1 || g.TH < 1 || g.TW < 1) return -3;
-  const long long HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
-  const long long HP = (g.TD + g.KD - 1) * HH * HW;
-  if (g.HPpad < HP || g.HPpad % 64) return -3;
-  if (g.TD + g.KD - 1 > 255 || HH > 255 || HW > 255) return -3;
-  const int T = g.KD * g.KH * g.KW;
-  const int need_ks = g.CS >= 32 ? T * (g.CS / 32) : (g.CS == 16 ? (T + 1) / 2 : (T + 3) / 4);
-  if (g.nks % 8 || g.nks < need_ks || g.nks < 16 || g.nct < (Ncol + 15) / 16) return -3;
-  for (long long r = 0; r < 64LL * MT; ++r) {
-    const unsigned long long q = (r * (unsigned long long)g.mTW) >> 32;
-    if (q != (unsigned long long)(r / g.TW) || ((q * g.mTH) >> 32) != q / g.TH) return -3;
-  }
-  if ((size_t)g.BUF < (size_t)g.HPpad * CPP * 16 || g.BUF % 1024 || g.BUF < 16384) return -3;   // (16 KiB exchange rounds)
-  const size_t lds = tile8_lds_total(g);
-  if (lds > 160 * 1024) return -4;
-  const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
-  if (!zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
-  if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;
-  dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
-#define CT8_CASE(C)                                                                                           \
-  if (CPP == C) {                                                                                             \
-    static size_t cfg = 0;                                                                                    \
-    if (lds > cfg) {                                                                                          \
-      hipError_t e = hipFuncSetAttribute((const void*)conv_tile8_kernel<8, 2, C>,                             \
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
-      if (e != hipSuccess) return (int)e;                                                                     \
-      cfg = lds;                                                                                              \
-    }                                                                                                         \
-    hipLaunchKernelGGL((conv_tile8_kernel<8, 2, C>), grid, dim3(512), lds, st, (const unsigned char*)src,      \
-                       (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, (const unsigned char*)zp, bias, \
-                       out, stats, g, Ncol, act);                                                             \
-  }
-  CT8_CASE(1) CT8_CASE(2) CT8_CASE(4)
-#undef CT8_CASE
   FN_CHECK_LAUNCH();
   return 0;
 }

@@ -1,0 +1,137 @@
+// Shared pieces of the big-tile LDS-halo conv kernels (conv_tile.hip: the 16x16x32 bf16 and
+// the fp8 kernels; conv_tile32.hip: the 32x32x16 bf16 kernel): the tile geometry, the halo DMA
+// of one job, small helpers.
+#pragma once
+#include "common.h"
+#include "tile_dma.h"
+
+struct TileGeom {
+  int N, ID, IH, IW, C;     // gathered source (x for fwd, dy for dgrad), channels-last
+  int OD, OH, OW;           // output dims
+  int KD, KH, KW;           // kernel
+  int pd, ph, pw;           // leading pads (stride 1)
+  int TD, TH, TW;           // output tile
+  int CS;                   // channels per halo slice (jobs per tile = C / CS)
+  int HPpad;                // halo positions rounded up to a multiple of 64 (whole DMA rows)
+  int nks;                  // k-steps per job (multiple of the B prefetch depth)
+  int nct;                  // 16-column tiles of the packed weights (ceil(Ncol / 16))
+  unsigned mHW, mHHW;       // magic multipliers: p / HW == umulhi(p, mHW) (host-verified)
+  int BUF;                  // bytes per LDS buffer (halo or epilogue staging), multiple of 16
+  unsigned mTW, mTH;        // magic multipliers for the epilogue's tile-row decode
+  // output view: output position (n, d, h, w) is stored at position index
+  // n*osn + ob + d*osd + h*osh + w*osw (x Ncol elements); natural layout = (OD*OH*OW, 0,
+  // OH*OW, OW, 1).  A strided view writes one parity class of a sub-pixel (upsample x2)
+  // convolution straight into the full-resolution output.
+  int osn, ob, osd, osh, osw;
+};
+
+#define CT_NCW 4                       // compute (MFMA) waves
+#define CT_F8_POOL 0x100               // fp8 act flag: fused 2^3 max-pool epilogue
+#define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
+// per-compute-wave BN sums of the workgroup's NT*16 columns
+__host__ __device__ constexpr int ct_red_bytes(int NT) { return CT_NCW * 2 * NT * 16 * 4; }
+
+// packed bf16 pairs (low half = element 0)
+__device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ unsigned bf16x2_pack(float lo, float hi) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t p = {f2bf(lo), f2bf(hi)};
+  return __builtin_bit_cast(unsigned, p);
+}
+
+// sum over the 16 lanes of a DPP row (every lane of the row gets it): quad swaps, then
+// half-row and row mirrors
+__device__ __forceinline__ float ct_sum16(float x) {
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));    // quad [1,0,3,2]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));    // quad [2,3,0,1]
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));   // row_half_mirror
+  x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));   // row_mirror
+  return x;
+}
+
+typedef int ct_i32x8 __attribute__((ext_vector_type(8)));
+
+// B-ring depth (k-steps in flight): a bf16 k-step is MT*NT 16-cycle MFMAs, an fp8 one
+// MT*NT 32-cycle block-scaled MFMAs, so 2 fp8 steps cover the latency 4 bf16 steps do
+__host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : 4; }
+
+// Halo of job (tile, slice) into the LDS buffer at bufoff, issued by one wave (the
+// loader): interior halos (the common case for unpadded convs) use SGPR base + the
+// per-position byte offsets of s_pos, no address math per DMA row; halos crossing the input
+// boundary check every position and read the zero page outside.
+template <int CPP, int ESZ>
+__device__ __forceinline__ void ct_dma_job(const TileGeom& g, const unsigned char* __restrict__ src,
+                                           const unsigned char* __restrict__ zp, unsigned char* dsm,
+                                           const int2* s_pos, int tile, int slice, int bufoff, int lane, int tdn,
+                                           int thn, int twn) {
+  const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
+  const int PLANE = g.HPpad * 16;
+  tile = __builtin_amdgcn_readfirstlane(tile);   // (wave-uniform: the SGPR operands need proof)
+  slice = __builtin_amdgcn_readfirstlane(slice);
+  bufoff = __builtin_amdgcn_readfirstlane(bufoff);
+  int t = tile;
+  const int tw = t % twn; t /= twn;
+  const int th = t % thn; t /= thn;
+  const int td = t % tdn;
+  const int n = t / tdn;
+  const int dlo = td * g.TD - g.pd, hlo = th * g.TH - g.ph, wlo = tw * g.TW - g.pw;
+  const bool interior = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID &&
+                        hlo + HH <= g.IH && wlo + HW <= g.IW;
+  const unsigned char* base = src + ((long long)n * g.ID * g.IH * g.IW * g.C + slice * g.CS) * ESZ;
+  const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
+  // position rows in batches of 8: the s_pos reads of a batch are in flight together
+  // (one LDS latency per batch, not per DMA row)
+  const int NR = g.HPpad >> 6;
+  if (interior) {
+    const unsigned char* obase = base + (((long long)dlo * g.IH + hlo) * g.IW + wlo) * g.C * ESZ;
+    for (int r0 = 0; r0 < NR; r0 += 8) {
+      int po[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) po[i] = s_pos[((r0 + i < NR ? r0 + i : NR - 1) << 6) + lane].x;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (r0 + i < NR) {
+#pragma unroll
+          for (int c = 0; c < CPP; ++c)
+            ct_glds16_s(obase, (unsigned)(po[i] + c * 16), dst0 + (unsigned)(c * PLANE + ((r0 + i) << 10)));
+        }
+      }
+    }
+  } else {
+    for (int r0 = 0; r0 < NR; r0 += 8) {
+      int e[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = s_pos[((r0 + i < NR ? r0 + i : NR - 1) << 6) + lane].y;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (r0 + i < NR) {
+          const int gd = dlo + (e[i] >> 16), gh = hlo + ((e[i] >> 8) & 255), gw = wlo + (e[i] & 255);
+          const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                          (unsigned)gw < (unsigned)g.IW;
+          const unsigned char* gsrc = ok ? base + (long long)((gd * g.IH + gh) * g.IW + gw) * g.C * ESZ : zp;
+#pragma unroll
+          for (int c = 0; c < CPP; ++c)
+            ct_glds16(ok ? gsrc + c * 16 : zp, dst0 + (unsigned)(c * PLANE + ((r0 + i) << 10)));
+        }
+      }
+    }
+  }
+}
+
+#define CT_GEOM_LEN 31
+static inline TileGeom parse_tile(const int* v) {
+  TileGeom g;
+  g.N = v[0]; g.ID = v[1]; g.IH = v[2]; g.IW = v[3]; g.C = v[4];
+  g.OD = v[5]; g.OH = v[6]; g.OW = v[7];
+  g.KD = v[8]; g.KH = v[9]; g.KW = v[10];
+  g.pd = v[11]; g.ph = v[12]; g.pw = v[13];
+  g.TD = v[14]; g.TH = v[15]; g.TW = v[16];
+  g.CS = v[17]; g.HPpad = v[18]; g.nks = v[19]; g.nct = v[20];
+  g.mHW = (unsigned)v[21]; g.mHHW = (unsigned)v[22]; g.BUF = v[23];
+  g.mTW = (unsigned)v[24]; g.mTH = (unsigned)v[25];
+  g.osn = v[26]; g.ob = v[27]; g.osd = v[28]; g.osh = v[29]; g.osw = v[30];
+  return g;
+}
+
+extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT);

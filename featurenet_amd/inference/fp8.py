@@ -232,7 +232,7 @@ class Fp8FeatureNet3D:
             return None
         f, spec2 = s2d
         tp = conv_tile.fwd_plan(spec2)
-        if tp is None or tp.NT != 2 or tp.nw != 4 or tp.CS != 8:   # (the e4m3-output instances: 8-channel
+        if tp is None or tp.NT != 2 or tp.CS != 8:   # (the e4m3-output instances: 8-channel
             return None                                            #  slices, the space-to-depth stem)
         key = (f, spec2.C, spec2.KD, spec2.KH, spec2.KW)
         w2 = self._stem_w2.get(key)

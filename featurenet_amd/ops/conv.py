@@ -701,7 +701,8 @@ def pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
         return x
     x = x.contiguous()
     out = torch.empty(*x.shape[:-1], cp, dtype=torch.bfloat16, device=x.device)
-    _native.kernels().pad_channels(x.data_ptr(), out.data_ptr(), x.numel() // C, C, cp, 0, _native.stream(x))
+    _native.kernels().pad_channels(x.data_ptr(), out.data_ptr(), x.numel() // C, C, cp, 0, _native.stream(x),
+                                   [x.numel(), out.numel()])
     return out
 
 

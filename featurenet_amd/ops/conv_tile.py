@@ -33,7 +33,14 @@ from .. import _native
 LDS_MAX = 160 * 1024
 NTHR = 320          # 4 MFMA waves + 1 loader wave
 MT_CHOICES = (8, 9)
-MT_CHOICES_NT4 = (6, 7)     # 64-column instances (register budget of 5 waves per CU: 256 VGPRs)
+MT_CHOICES_32 = (8, 10)     # conv_tile32: MB = MT / 2 blocks of 32 rows per wave
+
+
+def m32_enabled() -> bool:
+    """FN_TILE_M32: '1' (default) plans bf16 convs with whole 32-column blocks on the
+    v_mfma_f32_32x32x16_bf16 kernel (conv_tile32.hip), '0' keeps every plan on the
+    16x16x32 kernel."""
+    return os.environ.get("FN_TILE_M32", "1") != "0"
 
 
 def red_bytes(NT: int) -> int:
@@ -41,13 +48,6 @@ def red_bytes(NT: int) -> int:
     return 4 * 2 * NT * 16 * 4
 
 
-def tile_nt() -> str:
-    """FN_TILE_NT: '4' plans 64-column workgroups (NT = 4) whenever Ncol % 64 == 0; '2'
-    (default) 32-column ones only.  NT = 4 halves the halo reads and DMA per MFMA but measured
-    3-4 % slower on conv3 / conv4 (fwd 375 / 261 vs 365 / 251 us, conv4 dgrad 304 vs 295): the
-    k-loop is not bound by the halo reads, and the 64-column instance only fits 96-112 rows
-    per wave in the 256 VGPRs of a 5-wave workgroup (ring depth 2)."""
-    return os.environ.get("FN_TILE_NT", "2")
 _LOCK = threading.Lock()
 _PLANS: dict = {}
 _ROWTAB: dict = {}
@@ -59,11 +59,6 @@ def enabled() -> bool:
     return os.environ.get("FN_CONV_TILE", "1") != "0"
 
 
-def nwaves() -> int:
-    """FN_CONV_TILE_NW: 8 = the split-K 8-wave kernel (conv_tile8), 4 = 4 waves + loader."""
-    return int(os.environ.get("FN_CONV_TILE_NW", "4"))
-
-
 @dataclass(frozen=True)
 class TilePlan:
     TD: int
@@ -71,7 +66,7 @@ class TilePlan:
     TW: int
     CS: int          # channels per halo slice
     MT: int          # 16-row MFMA tiles per wave
-    NT: int          # 16-col MFMA tiles per workgroup (2 or 4)
+    NT: int          # 16-col MFMA tiles per workgroup (2: 32-column blocks)
     HPpad: int
     nks: int         # k-steps per job
     nct: int         # 16-col tiles of the packed weights
@@ -80,8 +75,12 @@ class TilePlan:
     mHHW: int
     cost: float      # modelled cycles (per wave, summed over the jobs of one CU)
     f8: bool = False  # fp8 (e4m3) inference variant: 16-channel chunks, 128-k steps, ring depth 2
-    nw: int = 4       # 4 MFMA waves + loader (conv_tile_kernel) or 8 split-K MFMA waves (conv_tile8_kernel)
     pool: bool = False  # fp8: fused 2^3 max-pool epilogue (even tile dims, window-per-lane row table)
+    m32: bool = False   # bf16 on conv_tile32_kernel (32x32x16 MFMA, MT / 2 blocks of 32 rows per wave)
+
+    @property
+    def MB(self) -> int:
+        return self.MT // 2
 
     @property
     def rows(self) -> int:
@@ -112,46 +111,38 @@ def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int
     ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply
     (``f8``: the e4m3 inference variant, 32- or 64-channel slices; ``pool``: with the fused
     2^3 max-pool epilogue -- even output and tile dims)."""
-    nw = 4 if f8 else nwaves()
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, nw, tile_nt(), pool,
-           os.environ.get("FN_TILE_PLAN_RANK", "0"))
+    m32 = not f8 and Ncol % 32 == 0 and m32_enabled()
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, pool, m32, os.environ.get("FN_TILE_PLAN_RANK", "0"))
     if key in _PLANS:
         return _PLANS[key]
     if pool and (not f8 or any(d % 2 for d in out_dims)):
         return None
-    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, nw, pool)
-    if best is None and nw == 8:                 # shapes the 8-wave kernel cannot tile: 4 waves + loader
-        best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, 4)
+    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, pool, m32)
     with _LOCK:
         _PLANS[key] = best
     return best
 
 
-def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4, pool=False):
+def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
     if Ncol < 16 or Ncol % 8 or Csrc % 8 or T < 2:
         return None
-    # NT = 2: 32-column workgroups; NT = 4 (plain bf16, Ncol % 64 == 0): 64 columns, every halo
-    # fragment read feeds 4 MFMAs (the 2-MFMA k-loop is issue-bound), half the halo DMA per column
-    nt_mode = tile_nt()
-    NT = 4 if (not f8 and nw == 4 and Ncol % 64 == 0 and nt_mode == "4") else 2
+    NT = 2                                       # 32-column workgroups
     ncb = -(-Ncol // (NT * 16))
     nct = ncb * NT
     PD = PD_F8 if f8 else 4
     workers = max(1, n_cus // ncb)
     cands = []
     cs_only = int(os.environ.get("FN_TILE_CS", "0"))
-    mt_choices = (8,) if (f8 or nw == 8) else (MT_CHOICES_NT4 if NT == 4 else MT_CHOICES)
+    mt_choices = (8,) if f8 else (MT_CHOICES_32 if m32 else MT_CHOICES)
     for CS in ((64, 32) if f8 else (32, 16, 8)):
         if Csrc % CS or (cs_only and CS != cs_only) or (CS == 8 and Csrc % 16 == 0):
             continue
         CPP = CS // 16 if f8 else CS // 8
         nslice = Csrc // CS
         nks = -(-math.ceil(T / (128 // CS)) // PD) * PD if f8 else _ksteps(T, CS, PD)   # f8: 128-k steps
-        if nw == 8:                              # k-steps split over a wave pair: a multiple of 2 PD
-            nks = max(16, -(-nks // 8) * 8)
         tw_opts = sorted({OW} | {-(-OW // k) for k in range(2, 5) if -(-OW // k) >= 8})
         for TW in tw_opts:
             for TD in range(1, OD + 1):
@@ -162,19 +153,16 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4, pool=False):
                     if pool and (TD % 2 or TH % 2 or TW % 2):
                         continue
                     MT = max(mt_choices[0], -(-rows // 64))
+                    if m32:
+                        MT += MT & 1                            # whole 32-row blocks
                     if rows < 64 * mt_choices[0] * 0.75:
                         continue
                     HH, HW = TH + KH - 1, TW + KW - 1
                     HP = (TD + KD - 1) * HH * HW
                     HPpad = -(-HP // 64) * 64
                     BUF = HPpad * CPP * 16                     # the halo (a multiple of 2 KiB)
-                    if nw == 8:
-                        lds = 2 * BUF + 8 * 64 * 4 + (nks + 2 * PD + 2) * 16 + HPpad * 8
-                        if BUF < 16384:                 # (the split-K exchange: 16 KiB rounds)
-                            continue
-                    else:
-                        lds = 2 * BUF + 64 + red_bytes(NT) + (nks + PD + 2) * 16 + HPpad * 8 + (NT * 16 * 8 if f8 else 0) \
-                            + (NT * 16 * 4 if NT == 4 else 0)
+                    lds = 2 * BUF + 64 + red_bytes(NT) + (nks + PD + 2) * 16 + HPpad * 8 + (NT * 16 * 8 if f8 else 0) \
+                        + (128 if m32 else 0)
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
@@ -186,7 +174,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4, pool=False):
                     per_job = max(mfma + fixed + epi, loader)
                     cost = math.ceil(jobs / workers) * per_job
                     cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
-                                          float(cost), f8, nw, pool))
+                                          float(cost), f8, pool, m32))
     # the cheapest few, re-costed with their row tables' residual bank conflicts (a
     # fragment whose 16 rows repeat a residue mod 16 reads at half rate)
     ranked = []
@@ -199,7 +187,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, nw=4, pool=False):
         dups = sum(16 - len(set(r.tolist())) for r in res)
         cost = c.cost * (1.0 + 0.5 * dups / res.size)
         ranked.append(TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct",
-                                                          "BUF", "mHW", "mHHW")), cost, f8, nw, pool))
+                                                          "BUF", "mHW", "mHHW")), cost, f8, pool, m32))
     if not ranked:
         return None
     ranked.sort(key=lambda c: c.cost)
@@ -349,8 +337,23 @@ def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
     T = KD * KH * KW
     kd, kh, kw = np.meshgrid(np.arange(KD), np.arange(KH), np.arange(KW), indexing="ij")
     toff = (((kd * HH + kh) * HW + kw) * 16).reshape(-1)
-    tab = np.zeros((p.nks + 2 * PD + 2, 4), dtype=np.int32)   # (the 8-wave kernel reads 2 PD + 2 ahead)
+    tab = np.zeros((p.nks + 2 * PD + 2, 4), dtype=np.int32)
     plane = p.HPpad * 16
+    if p.m32:
+        # conv_tile32: entry [k][2h + j] = the offset lane half h reads in sub-step j (16 k each)
+        for k in range(p.nks):
+            for h in range(2):
+                for j in range(2):
+                    if p.CS >= 32:
+                        t, sub = divmod(k, p.CS // 32)
+                        off = (4 * sub + 2 * j + h) * plane
+                    elif p.CS == 16:
+                        t, off = 2 * k + j, h * plane
+                    else:
+                        t, off = 4 * k + 2 * j + h, 0
+                    if t < T:
+                        tab[k, 2 * h + j] = toff[t] + off
+        return tab
     for k in range(p.nks):
         for lg in range(4):
             if p.f8:                                 # lane group: 32 bytes of one tap (planes in lb)
@@ -385,7 +388,7 @@ def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bo
     out = torch.empty((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
     wf = w.detach().float().contiguous()
     _native.kernels().tile_pack_w(wf.data_ptr(), out.data_ptr(), K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad),
-                                  _native.stream(wf), p.NT)
+                                  _native.stream(wf), 32 if p.m32 else p.NT)
     return out
 
 
@@ -399,10 +402,12 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
     rt = rowtab_tensor(p, kdims, src5.device)
     kt = ktab_tensor(p, kdims, src5.device)
     ext = [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4]
-    if p.nw == 8 and bny is None and not oscale:
-        _native.kernels().conv_tile8(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
-                                     zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
-                                     _native.ptr(stats), geom, ncol, act, p.MT, p.NT, st, ext)
+    if p.m32:
+        assert bny is None, "the BN-statistics dgrad epilogue is a conv_tile_kernel instance"
+        _native.kernels().conv_tile32(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
+                                      zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
+                                      _native.ptr(stats), geom, ncol, act, p.MB, sched(src5.device, st).data_ptr(),
+                                      st, ext, float(oscale))
         return
     if bny is not None:
         ext += [bny.numel(), bnp.numel()]
@@ -442,7 +447,7 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None):
     wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     lds_bws = 2 * p.BUF + 64 + red_bytes(p.NT) + (p.nks + PD + 2) * 16 + p.HPpad * 8 + p.NT * 16 * 16
-    if bn is None or lds_bws > LDS_MAX or p.NT != 2:   # (the statistics instance: 32-column blocks, BN
+    if bn is None or lds_bws > LDS_MAX or p.NT != 2 or p.m32:   # (the statistics instance: 32-column blocks, BN
         # scale/shift in LDS)
         run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
         return dx if bn is None else (dx, None)

@@ -32,6 +32,7 @@ class FlatAdam:
         self.t = 0
         self._dev = None     # (hp, t) device state of the graph-capturable form
         self._gscale = 1.0   # gradient scale of the device state (1/world under data parallelism)
+        self._pushed = None  # the host hyper-parameters last copied to the device state
 
     # ------------------------------------------------------------ graph mode
     def enable_device_state(self, grad_scale: float | None = None) -> None:
@@ -44,6 +45,7 @@ class FlatAdam:
                               device=self.p.device)
             t = torch.tensor([self.t], dtype=torch.int32, device=self.p.device)
             self._dev = (hp, t)
+            self._pushed = self._host_hp()
         else:
             self.sync_device_state()
 
@@ -53,7 +55,11 @@ class FlatAdam:
         if grad_scale is not None:
             self._gscale = float(grad_scale)
         if self._dev is not None:
-            self._dev[0].copy_(torch.tensor([self.lr, self.b1, self.b2, self.eps, self.wd, self._gscale]))
+            self._pushed = self._host_hp()
+            self._dev[0].copy_(torch.tensor(list(self._pushed)))
+
+    def _host_hp(self) -> tuple:
+        return (float(self.lr), float(self.b1), float(self.b2), float(self.eps), float(self.wd), float(self._gscale))
 
     def step_device(self) -> None:
         """One Adam step entirely driven by device state (safe inside hipGraph capture)."""
@@ -64,7 +70,9 @@ class FlatAdam:
 
     def step(self, grad_scale: float = 1.0) -> None:
         if self._dev is not None and _native.use_native(self.p):
-            if grad_scale != self._gscale:           # (eager steps only: a small host -> device copy)
+            # eager steps with the device state (e.g. after a graph-capture fallback): push any
+            # host-side change -- a new lr from a callback, another gradient scale -- first
+            if grad_scale != self._gscale or self._host_hp() != self._pushed:
                 self.sync_device_state(grad_scale)
             self.t += 1
             self.step_device()

@@ -95,13 +95,15 @@ def plan_buckets(sizes: list[int], cap: int, tail_cap: int | None = None) -> lis
         tail: list[list[int]] = []
         c, i = tail_cap, len(sizes) - 1
         while i >= 0 and c < cap:
+            if sizes[i] >= cap // 2:                 # a large tensor is a bucket of its own; the
+                tail.insert(0, [i])                  # tail walk goes on past it at the same cap
+                i -= 1
+                continue
             cur, size = [], 0
             while i >= 0 and sizes[i] < cap // 2 and (not cur or size + sizes[i] <= c):
                 cur.insert(0, i)
                 size += sizes[i]
                 i -= 1
-            if not cur:
-                break
             tail.insert(0, cur)
             c *= 2
         head = plan_buckets(sizes[:i + 1], cap) if i >= 0 else []

@@ -217,18 +217,30 @@ def augment_images(x: torch.Tensor, shift: float = 0.1, hflip: bool = True,
 
 
 class DeviceLoader:
-    """Shuffled mini-batches from device-resident arrays (optionally sharded by rank)."""
+    """Shuffled mini-batches from device-resident arrays.
+
+    Data parallelism (reference ``model/keras_model.py:137-146``: ``multi_gpu_model``
+    slices every batch of a Keras ``fit`` that reshuffles each epoch, so every replica
+    sees a random cross-section of the whole set): every rank holds the WHOLE set on
+    its device (bit-packed voxels are 32 KB per 64^3 grid; HBM is 288 GB) and, each
+    epoch, takes the rank-strided slice ``perm[rank::world]`` of ONE global permutation
+    drawn from ``(seed, epoch)`` -- identical on every rank, so the shards partition the
+    epoch and change between epochs, whatever order the set is stored in (e.g. the
+    class-sorted :func:`binvox_folder`).  Training shards are cut to ``n // world``
+    samples (equal step counts on every rank: the per-step gradient all-reduce needs
+    them); ``even=False`` (evaluation) keeps every sample exactly once instead.
+
+    ``gen`` (seeded ``seed + rank``) drives the augmentation draws only; the shuffle is
+    a pure function of ``(seed, epoch)`` (:meth:`set_epoch`), so a resumed run needs the
+    epoch count, not a generator state, to reproduce the order."""
 
     def __init__(self, x, y, batch_size: int, device, shuffle: bool = True, augment: bool = False,
                  packed_size: int | None = None, rank: int = 0, world: int = 1, drop_last: bool = False,
-                 seed: int = 0, dtype=None):
+                 seed: int = 0, dtype=None, even: bool = True):
         self.device = torch.device(device)
         self.packed_size = packed_size
         xt = torch.as_tensor(np.asarray(x)) if not isinstance(x, torch.Tensor) else x
         yt = torch.as_tensor(np.asarray(y)) if not isinstance(y, torch.Tensor) else y
-        if world > 1:   # contiguous shard per rank, equal sizes (drop the tail)
-            per = len(xt) // world
-            xt, yt = xt[rank * per:(rank + 1) * per], yt[rank * per:(rank + 1) * per]
         if dtype is None:
             dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
         if packed_size is None and xt.dtype != torch.uint8:
@@ -237,27 +249,55 @@ class DeviceLoader:
         self.y = yt.long().to(self.device)
         self.batch_size, self.shuffle, self.augment, self.drop_last = batch_size, shuffle, augment, drop_last
         self.dtype = dtype
+        self.rank, self.world, self.seed, self.even = int(rank), max(1, int(world)), int(seed), bool(even)
+        self.epoch = 0
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed + rank)
 
     def derived(self, shuffle: bool = True, seed: int = 0, augment: bool = False) -> "DeviceLoader":
         """Another loader over the SAME device-resident tensors (no re-upload of the set):
-        own shuffle order / generator, e.g. PreciseBN recalibration batches during fit."""
+        own shuffle seed / epoch / augmentation generator, e.g. PreciseBN recalibration
+        batches during fit."""
         d = object.__new__(DeviceLoader)
         d.__dict__.update(self.__dict__)
-        d.shuffle, d.augment = shuffle, augment
+        d.shuffle, d.augment, d.seed, d.epoch = shuffle, augment, int(seed), 0
         d.gen = torch.Generator(device=self.device)
-        d.gen.manual_seed(seed)
+        d.gen.manual_seed(seed + self.rank)
         return d
 
-    def __len__(self) -> int:
+    def set_epoch(self, epoch: int) -> None:
+        """The epoch whose global permutation the next iteration uses."""
+        self.epoch = int(epoch)
+
+    def shard_size(self) -> int:
         n = len(self.x)
+        if self.world == 1:
+            return n
+        return n // self.world if self.even else len(range(self.rank, n, self.world))
+
+    def indices(self, epoch: int | None = None) -> torch.Tensor:
+        """This rank's sample indices of ``epoch`` (default: the next one), in batch order (CPU)."""
+        n = len(self.x)
+        e = self.epoch if epoch is None else int(epoch)
+        if self.shuffle:
+            g = torch.Generator()                # CPU: bit-identical on every rank and device type
+            g.manual_seed((self.seed * 1_000_003 + e * 7_919 + 12_345) & 0x7FFF_FFFF_FFFF_FFFF)
+            idx = torch.randperm(n, generator=g)
+        else:
+            idx = torch.arange(n)
+        if self.world > 1:
+            idx = idx[self.rank::self.world]
+            if self.even:
+                idx = idx[:n // self.world]
+        return idx
+
+    def __len__(self) -> int:
+        n = self.shard_size()
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def __iter__(self):
-        n = len(self.x)
-        idx = torch.randperm(n, device=self.device, generator=self.gen) if self.shuffle else \
-            torch.arange(n, device=self.device)
+        idx = self.indices().to(self.device)
+        self.epoch += 1
         for i in range(len(self)):
             sel = idx[i * self.batch_size:(i + 1) * self.batch_size]
             xb = self.x[sel]

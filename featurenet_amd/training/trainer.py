@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import math
 import time
+from pathlib import Path
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -95,6 +96,21 @@ class _EpochMetrics:
         corr = self.extra if self.correct is None else self.correct.sum() + self.extra
         return self.loss, corr
 
+def _gather_rank_rng(rng: tuple[dict, dict], world: int) -> tuple[dict, dict]:
+    """Every rank's :func:`capture_rng` snapshot, gathered for rank 0's checkpoint: rank 0's own
+    under the plain ``rng.*`` keys (single-process readers) and rank r's under ``rng.rank<r>.*``;
+    the header records the world size and each rank's json part."""
+    tensors, meta = rng
+    local = ({k: v.detach().cpu() for k, v in tensors.items()}, meta)
+    allr: list = [None] * world
+    dist.all_gather_object(allr, local)
+    out = dict(local[0])
+    for r, (t, _) in enumerate(allr):
+        for k, v in t.items():
+            out["rng.rank%d.%s" % (r, k[len("rng."):])] = v
+    return out, {**meta, "world": world, "ranks": [m for _, m in allr]}
+
+
 class Trainer:
     def __init__(self, model: torch.nn.Module, optimizer: str = "adam", lr: float = 1e-3, device=None,
                  keras_eps: bool = True, weight_decay: float = 0.0, momentum: float = 0.9,
@@ -150,8 +166,10 @@ class Trainer:
 
     def set_lr(self, lr: float) -> None:
         self.opt.lr = float(lr)
-        if self.graph_mode:
-            self.opt.sync_device_state()        # (keeps the 1/world gradient scale)
+        if getattr(self.opt, "_dev", None) is not None:
+            # the device-state Adam (graph mode, and the eager steps after a capture fallback)
+            # reads lr from its device copy (keeps the 1/world gradient scale)
+            self.opt.sync_device_state()
 
     # ------------------------------------------------------------------ steps
     def _prep(self, xb: torch.Tensor) -> torch.Tensor:
@@ -237,11 +255,13 @@ class Trainer:
             seed: int = 0, initial_epoch: int = 0) -> History:
         """Train epochs ``initial_epoch`` .. ``epochs - 1`` (Keras semantics).  After
         :meth:`resume` from a checkpoint written at an epoch end, ``initial_epoch`` = the
-        checkpoint's epoch count continues the run bit-for-bit (same shuffle order, augment
-        draws, dropout masks) -- the loader's generator comes from the checkpoint."""
+        checkpoint's epoch count continues the run bit-for-bit (same shuffle order -- a function
+        of (seed, epoch) -- augment draws and dropout masks: this rank's generators come from the
+        checkpoint).  Under data parallelism every rank trains on its strided slice of one
+        global per-epoch permutation (:class:`DeviceLoader`)."""
         callbacks: list[Callback] = list(callbacks or [])
         loader = DeviceLoader(x, y, batch_size, self.device, shuffle=shuffle, augment=augment,
-                              packed_size=packed_size, rank=self.rank, world=self.world, seed=seed)
+                              packed_size=packed_size, rank=self.rank, world=self.world, seed=seed, even=True)
         if self._resume_loader_state is not None:
             loader.gen.set_state(self._resume_loader_state.to(torch.uint8))
             self._resume_loader_state = None
@@ -249,7 +269,7 @@ class Trainer:
         val_loader = None
         if validation_data is not None:   # uploaded once, not once per epoch
             val_loader = DeviceLoader(*validation_data, batch_size, self.device, shuffle=False,
-                                      packed_size=packed_size, rank=self.rank, world=self.world)
+                                      packed_size=packed_size, rank=self.rank, world=self.world, even=False)
         self.stop_training = False
         for cb in callbacks:
             cb.on_train_begin(self)
@@ -262,6 +282,7 @@ class Trainer:
                 t0 = time.time()
                 acc = _EpochMetrics(self.device)
                 seen = 0
+                loader.set_epoch(epoch)
                 for bi, (xb, yb) in enumerate(loader):
                     loss, corr = self.train_step(xb, yb)
                     acc.add(loss, corr, yb.numel())           # numel: per-voxel labels (segmentation)
@@ -278,7 +299,7 @@ class Trainer:
                 self._bn_fresh = False
                 if self.precise_bn and (validation_data is not None or epoch == epochs - 1):
                     self.recalibrate_bn(x, y, self.precise_bn, batch_size, packed_size, seed + epoch,
-                                        loader=loader.derived(seed=seed + epoch + 7919 * (self.rank + 1)))
+                                        loader=loader.derived(seed=seed + epoch + 7919))
                 if val_loader is not None:
                     vl, va = self.evaluate(None, None, loader=val_loader)
                     logs["val_loss"], logs["val_acc"] = vl, va
@@ -296,7 +317,7 @@ class Trainer:
                     break
             if self.precise_bn and not self._bn_fresh:    # stopped early without validation
                 self.recalibrate_bn(x, y, self.precise_bn, batch_size, packed_size, seed,
-                                    loader=loader.derived(seed=seed + 7919 * (self.rank + 1)))
+                                    loader=loader.derived(seed=seed + 7919))
         except torch.cuda.OutOfMemoryError as e:   # reference: ResourceExhaustedError -> candidate dropped
             raise TrainingFailed(f"out of device memory: {e}") from e
         finally:
@@ -350,7 +371,7 @@ class Trainer:
         self.model.eval()
         if loader is None:
             loader = DeviceLoader(x, y, batch_size, self.device, shuffle=False, packed_size=packed_size,
-                                  rank=self.rank, world=self.world)
+                                  rank=self.rank, world=self.world, even=False)
         acc = _EpochMetrics(self.device)
         seen = 0
         for xb, yb in loader:
@@ -389,6 +410,10 @@ class Trainer:
         if include_rng:
             gens = {"loader": self._loader.gen} if self._loader is not None else {}
             rng = capture_rng(gens)
+            if self.world > 1:
+                rng = _gather_rank_rng(rng, self.world)   # (a collective: every rank calls save)
+        if self.world > 1 and self.rank != 0:          # one writer: rank 0 holds every rank's state
+            return Path(path)
         return save_checkpoint(path, self.model, meta, self.opt if include_optimizer else None, rng=rng)
 
     def resume(self, path) -> int:
@@ -408,6 +433,18 @@ class Trainer:
         self.history.history = {k: list(v) for k, v in hist.items()}
         self.history.epoch = list(ts.get("history_epochs", []))
         tensors, rmeta = read_rng(path)
+        saved_world = int(rmeta.get("world", 1)) if rmeta else 1
+        if saved_world > 1:
+            if saved_world == self.world:                # this rank's own generators
+                pre = f"rank{self.rank}."
+                tensors = {k[len(pre):]: v for k, v in tensors.items() if k.startswith(pre)}
+                rmeta = rmeta["ranks"][self.rank]
+            else:                                        # another world size: the shuffle order still
+                default_log().emit("resume_rng_skipped", saved_world=saved_world, world=self.world)
+                tensors, rmeta = {}, {}                  # follows (seed, epoch); augment draws do not
+        elif self.world > 1 and tensors:                 # a single-process checkpoint: not per rank
+            default_log().emit("resume_rng_skipped", saved_world=1, world=self.world)
+            tensors, rmeta = {}, {}
         if tensors or rmeta:
             restore_rng(tensors, rmeta)
             self._resume_loader_state = tensors.get("gen.loader")

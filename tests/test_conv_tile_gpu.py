@@ -1,4 +1,5 @@
-"""Big-tile conv kernel (``csrc/kernels/conv_tile.hip``) vs the fp32 PyTorch reference.
+"""Big-tile conv kernels (``csrc/kernels/conv_tile.hip`` on v_mfma_f32_16x16x32_bf16,
+``conv_tile32.hip`` on v_mfma_f32_32x32x16_bf16) vs the fp32 PyTorch reference.
 
 Forward (bias + activation epilogue, BN statistics epilogue) and dgrad at the
 FeatureNet-3D layer shapes, at a small batch and at a production-size batch
@@ -29,21 +30,24 @@ CASES = [
     (2, 22, 22, 22, 64, 64, (3, 3, 3), "valid"),     # conv4
     (16, 29, 29, 29, 32, 32, (5, 5, 5), "valid"),    # conv2, 400 tiles > 256 workgroups
     (24, 22, 22, 22, 64, 64, (3, 3, 3), "valid"),    # conv4, 2 slices per tile, 384 tiles
-    (3, 11, 12, 13, 16, 48, (3, 3, 3), "same"),      # same padding, 48 columns (partial NT=4 block)
+    (3, 11, 12, 13, 16, 48, (3, 3, 3), "same"),      # same padding, 48 columns (16x16 kernel only)
     (2, 9, 10, 11, 32, 96, (3, 3, 3), "same"),       # 2 column blocks
-    (2, 9, 10, 11, 32, 128, (3, 3, 3), "same"),      # 2 column blocks of 64 (NT = 4)
+    (2, 9, 10, 11, 32, 128, (3, 3, 3), "same"),      # 4 column blocks of 32
+    (4, 29, 29, 29, 32, 32, (5, 5, 5), "valid"),     # conv2, CS = 16 plans
+    (2, 9, 10, 11, 64, 64, (3, 3, 3), "same"),       # 64 input channels: CS = 64 / 32 slices
     (4, 1, 40, 37, 32, 32, (1, 5, 5), "same"),       # 2-D conv
     (6, 32, 32, 32, 8, 32, (4, 4, 4), "valid"),      # FeatureNet-3D stem after space-to-depth (CS = 8)
     (3, 10, 11, 12, 8, 16, (3, 3, 3), "same"),       # CS = 8, 27 taps (last k-step partial), padding
 ]
 
 
-@pytest.mark.parametrize("nt", ["4", "2"])
+@pytest.mark.parametrize("m32", ["1", "0"])
 @pytest.mark.parametrize("case", CASES)
-def test_conv_tile_fwd_dgrad(case, nt, monkeypatch):
-    """nt = 4: 64-column workgroups (NT = 4) where Ncol % 64 == 0; 2: 32-column ones only."""
+def test_conv_tile_fwd_dgrad(case, m32, monkeypatch):
+    """m32 = 1: whole 32-column blocks on the 32x32x16 kernel (conv_tile32); 0: every plan on
+    the 16x16x32 kernel."""
     assert _native.kernels_available(), "HIP kernel library (_C) must be built and loadable on the GPU box"
-    monkeypatch.setenv("FN_TILE_NT", nt)
+    monkeypatch.setenv("FN_TILE_M32", m32)
     N, D, H, W, C, K, k, pad = case
     torch.manual_seed(0)
     dev = "cuda"
@@ -53,7 +57,9 @@ def test_conv_tile_fwd_dgrad(case, nt, monkeypatch):
     b = torch.randn(K, device=dev) * 0.1
     pf, pd = ct.fwd_plan(spec), ct.dgrad_plan(spec)
     assert pf is not None and (pd is not None or C < 16), (pf, pd)   # dgrad needs >= 16 output columns
-    assert pf.NT == (4 if nt == "4" and K % 64 == 0 else 2), pf
+    assert pf.m32 == (m32 == "1" and K % 32 == 0), pf
+    if pd is not None:
+        assert pd.m32 == (m32 == "1" and C % 32 == 0), pd
 
     # forward with bias + relu
     y, _ = ct.conv_fwd(x, w, b, spec, 1, False, pf)
