@@ -83,7 +83,7 @@ int fn_conv_tile(const void*, const void*, const void*, const void*, const void*
                  const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float);
 int fn_conv_tile_workers(const int*, int, int);
 int fn_conv_tile32(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
-                   const int*, int, int, int, int*, hipStream_t, float);
+                   const int*, int, int, int, int*, hipStream_t, float, const void*, const float*);
 int fn_conv_tile32_supported(int, int);
 int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
                     float, const int*, int, int, int, int, int*, hipStream_t);
@@ -226,16 +226,21 @@ PYBIND11_MODULE(_C, m) {
      py::arg("bnp") = 0, py::arg("oscale") = 0.f);
   m.def("conv_tile32", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                           uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MB,
-                          uintptr_t sched, uintptr_t st, std::vector<long long> ext, float oscale) {
+                          uintptr_t sched, uintptr_t st, std::vector<long long> ext, float oscale, uintptr_t bny,
+                          uintptr_t bnp) {
     need(geom, 31, "conv_tile32");
     check_tile(geom, ext, ncol, 2 * MB, "conv_tile32");   // (row table: 4 waves x 2MB 16-row fragments)
+    if (bny) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
+      fits(ext, 5, view_extent(geom, ncol), "conv_tile32", "bny");
+      fits(ext, 6, 4LL * ncol, "conv_tile32", "bnp");
+    }
     chk(fn_conv_tile32(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
                        P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
-                       act, MB, P<int*>(sched), S(st), oscale),
+                       act, MB, P<int*>(sched), S(st), oscale, P<const void*>(bny), P<const float*>(bnp)),
         "conv_tile32");
   }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MB"), py::arg("sched"),
-     py::arg("st"), py::arg("ext"), py::arg("oscale") = 0.f);
+     py::arg("st"), py::arg("ext"), py::arg("oscale") = 0.f, py::arg("bny") = 0, py::arg("bnp") = 0);
   m.def("conv_tile32_supported", &fn_conv_tile32_supported);
   m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
                            uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,

@@ -37,7 +37,11 @@ __device__ __forceinline__ float c32_sum32(float x) {
 
 // MB: 32-row MFMA blocks per compute wave (tile rows <= 128 MB); CPP: 16-B chunks per halo position
 // of a slice (CS / 8); Q8O: e4m3 output of v * oscale (the fp8 inference stem), no statistics.
-template <int MB, int CPP, bool Q8O = false>
+// BWS: the dgrad of a conv whose input was act(bn(y)) (ops/bnfuse.py): the stored dx is that BN's
+// dz, and the epilogue also sums the BN's raw backward moments (sum g, sum g*y; g = dz * act'(z))
+// from y (bny) at the tile's positions and the BN's scale / shift (bnp rows 2, 3) -- the separate
+// colstats pass over dz and y disappears (bn_finalize mode 2 centres the moments in fp64).
+template <int MB, int CPP, bool Q8O = false, bool BWS = false>
 __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned char* __restrict__ src,
                                                                  const uint4* __restrict__ wp,
                                                                  const int2* __restrict__ rowtab,
@@ -45,7 +49,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned 
                                                                  const unsigned char* __restrict__ zp,
                                                                  const float* __restrict__ bias, void* __restrict__ out,
                                                                  float* __restrict__ stats, TileGeom g, int Ncol,
-                                                                 int act, int* __restrict__ sched, float oscale) {
+                                                                 int act, int* __restrict__ sched, float oscale,
+                                                                 const bf16* __restrict__ bny,
+                                                                 const float* __restrict__ bnp) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int PD = C32_PD;
   constexpr int RC = 32;                         // columns of the workgroup
@@ -63,17 +69,19 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned 
   const int r32 = lane & 31, hf = lane >> 5;     // position row of the block, k / channel half
   const int ct0 = blockIdx.y * 2;                // first 16-column fragment of the workgroup
   // LDS: [buffer 0][buffer 1][job slots 64 B][BN partials 4 x 2 x 32][k-table (nks+PD+2) int4]
-  // [halo positions HPpad int2][bias 32 floats]
+  // [halo positions HPpad int2][bias 32 floats][BWS: (scale, shift) 32 float2]
   int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);
   float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);
   int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + ct_red_bytes(2));
   int2* s_pos = reinterpret_cast<int2*>(s_kt + (nks + PD + 2));
   float* s_bias = reinterpret_cast<float*>(s_pos + g.HPpad);
+  float2* s_bn = reinterpret_cast<float2*>(s_bias + RC);
   for (int i = tid; i < nks + PD + 2; i += CT_NTHR) s_kt[i] = ktab[i];
   for (int i = tid; i < ct_red_bytes(2) / 4; i += CT_NTHR) s_red[i] = 0.f;
   if (tid < RC) {
     const int c = blockIdx.y * RC + tid;
     s_bias[tid] = (bias && c < Ncol) ? bias[c] : 0.f;
+    if constexpr (BWS) s_bn[tid] = c < Ncol ? make_float2(bnp[2 * Ncol + c], bnp[3 * Ncol + c]) : make_float2(0.f, 0.f);
   }
   for (int p = tid; p < g.HPpad; p += CT_NTHR) {  // positions past HP repeat the last one
     const int pc = p < HP ? p : HP - 1;
@@ -156,7 +164,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned 
     // halo reads interleaved with the MFMAs (see conv_tile_kernel)
     auto kofs = [&](int k) -> int2 { return *reinterpret_cast<const int2*>((const int*)(s_kt + k) + 2 * hf); };
     const int emode = Q8O ? (8 | ((act & 0xff) == ACT_RELU ? 2 : 0))
-                          : ((stats ? 1 : 0) | ((act & 0xff) == ACT_RELU ? 2 : 0));
+                          : (BWS ? (4 | ((act & 0xff) == ACT_RELU ? 2 : 0))
+                                 : ((stats ? 1 : 0) | ((act & 0xff) == ACT_RELU ? 2 : 0)));
 #pragma unroll
     for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * FTILE, u);
     int par = 0;
@@ -212,8 +221,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned 
         const long long obase_e =
             ((long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh + w0 * g.osw) * Ncol + gc;
         auto epilogue = [&](auto mode) {
-          constexpr int M = decltype(mode)::value;   // bit 0 BN statistics, bit 1 relu, bit 3 e4m3 out
-          constexpr bool ST = (M & 1) != 0, RELU = (M & 2) != 0, Q8 = (M & 8) != 0;
+          // bit 0 BN statistics, bit 1 relu, bit 2 BN-backward moments (bit 1 is then the BN's relu,
+          // dx itself has no activation), bit 3 e4m3 out
+          constexpr int M = decltype(mode)::value;
+          constexpr bool BW = (M & 4) != 0;
+          constexpr bool ST = BW || (M & 1) != 0, RELU = !BW && (M & 2) != 0, Q8 = (M & 8) != 0;
           bool okm[MB];
 #pragma unroll
           for (int mb = 0; mb < MB; ++mb) {
@@ -229,6 +241,22 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned 
             if constexpr (ST) {
 #pragma unroll
               for (int j = 0; j < 8; ++j) ts[j] = tq[j] = 0.f;
+            }
+            // BW: the BN input y of this pass's 8 columns at every block's position (all MB loads
+            // in flight together) and the BN's scale / shift (the relu mask)
+            uint4 yb[BW ? MB : 1];
+            float bsc[BW ? 8 : 1], bsh[BW ? 8 : 1];
+            if constexpr (BW) {
+#pragma unroll
+              for (int mb = 0; mb < MB; ++mb)
+                yb[mb] = okm[mb] ? *(const uint4*)(bny + obase_e + (long long)roff[mb] * Ncol + 8 * p)
+                                 : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const float2 q = s_bn[16 * hf + 8 * p + j];
+                bsc[j] = q.x;
+                bsh[j] = q.y;
+              }
             }
             float bb[8];
             {
@@ -247,7 +275,17 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned 
                 if constexpr (RELU) x = fmaxf(x, 0.f);
                 v[j] = x;
               }
-              if constexpr (ST) {
+              if constexpr (BW) {
+                const unsigned yw[4] = {yb[mb].x, yb[mb].y, yb[mb].z, yb[mb].w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                  const float y = (j & 1) ? bf16_hi(yw[j >> 1]) : bf16_lo(yw[j >> 1]);
+                  float gv = ok ? v[j] : 0.f;
+                  if constexpr ((M & 2) != 0) gv = (y * bsc[j] + bsh[j]) > 0.f ? gv : 0.f;
+                  ts[j] += gv;
+                  tq[j] += gv * y;
+                }
+              } else if constexpr (ST) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                   const float x = ok ? v[j] : 0.f;
@@ -297,7 +335,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned 
             }
           }
         };
-        switch (emode) {
+        if constexpr (BWS) {
+          if (emode == 6) epilogue(std::integral_constant<int, 6>{});
+          else epilogue(std::integral_constant<int, 4>{});
+        } else switch (emode) {
           case 0: epilogue(std::integral_constant<int, 0>{}); break;
           case 1: epilogue(std::integral_constant<int, 1>{}); break;
           case 2: epilogue(std::integral_constant<int, 2>{}); break;
@@ -348,31 +389,36 @@ extern "C" int fn_conv_tile32_supported(int MB, int CPP) {
 }
 
 static size_t tile32_lds_total(const TileGeom& g) {
-  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(2) + (size_t)(g.nks + C32_PD + 2) * 16 + (size_t)g.HPpad * 8 + 32 * 4;
+  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(2) + (size_t)(g.nks + C32_PD + 2) * 16 + (size_t)g.HPpad * 8 + 32 * 4 +
+         32 * 8;
 }
 
-template <int MB, int CPP, bool Q8O>
+template <int MB, int CPP, bool Q8O, bool BWS = false>
 static int launch_tile32(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                          const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
-                         int Ncol, int act, int* sched, float oscale) {
+                         int Ncol, int act, int* sched, float oscale, const void* bny = nullptr,
+                         const float* bnp = nullptr) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile32_kernel<MB, CPP, Q8O>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile32_kernel<MB, CPP, Q8O, BWS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile32_kernel<MB, CPP, Q8O>), grid, dim3(CT_NTHR), lds, st, (const unsigned char*)s, w, rt,
-                     kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched, oscale);
+  hipLaunchKernelGGL((conv_tile32_kernel<MB, CPP, Q8O, BWS>), grid, dim3(CT_NTHR), lds, st, (const unsigned char*)s, w,
+                     rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched, oscale, (const bf16*)bny, bnp);
   return 0;
 }
 
 // As fn_conv_tile (same geometry vector, row table of 4 * 2MB 16-row fragments, sched / zero
 // page), for the 32x32x16 kernel: wp packed by fn_tile_pack_w mode 32, ktab int4[nks + PD + 2]
 // = per k-step {h0 j0, h0 j1, h1 j0, h1 j1} byte offsets; Ncol % 32 == 0; oscale > 0: e4m3 out.
+// bny / bnp (dgrad only, with stats): as fn_conv_tile -- the BN input y [out shape] and (mean,
+// invstd, scale, shift) [4][Ncol] of the BN+act layer whose output the conv consumed; stats then
+// receives that BN's raw backward sums and act is the BN's activation (none / relu).
 extern "C" int fn_conv_tile32(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                               const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MB,
-                              int* sched, hipStream_t st, float oscale) {
+                              int* sched, hipStream_t st, float oscale, const void* bny, const float* bnp) {
   const TileGeom g = parse_tile(geom);
   if (g.CS != 8 && g.CS != 16 && g.CS != 32 && g.CS != 64) return -2;
   const int CPP = g.CS / 8;
@@ -396,12 +442,16 @@ extern "C" int fn_conv_tile32(const void* src, const void* wp, const void* rowta
   const int ncb = Ncol / 32;
   if (!sched || !zp || !ktab || ncb > 63 || ncb * 2 > g.nct) return -6;
   if (Ncol % 32 || (act != ACT_NONE && act != ACT_RELU)) return -2;   // whole 32-column blocks
-  if (!(oscale >= 0.f) || (oscale > 0.f && (stats || CPP != 1))) return -2;   // (e4m3 out: the s2d stem)
+  if (!(oscale >= 0.f) || (oscale > 0.f && (stats || CPP != 1 || bny))) return -2;   // (e4m3 out: the s2d stem)
+  if ((bny != nullptr) != (bnp != nullptr) || (bny && (!stats || bias))) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, 2), (unsigned)ncb);
   int rc = -2;
 #define C32_CASE(M, C)                                                                                            \
   if (MB == M && CPP == C)                                                                                        \
-    rc = oscale > 0.f ? launch_tile32<M, C, C == 1>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,     \
+    rc = bny ? launch_tile32<M, C, false, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,        \
+                                                 (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, 0.f, \
+                                                 bny, bnp) :                                                       \
+         oscale > 0.f ? launch_tile32<M, C, C == 1>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,     \
                                                      (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched,  \
                                                      oscale)                                                        \
                       : launch_tile32<M, C, false>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,      \

@@ -38,12 +38,23 @@ _BWD: dict = {}      # dz.data_ptr() -> (ref dz, slab, ref y, dz._version at off
 
 
 def enabled() -> bool:
-    """Off by default: measured slower on FeatureNet-3D (batch 128).  The statistics instance
-    of conv_tile needs 256 VGPRs + 136 B of scratch (the other instances fit in 242 with
-    none), and its spills cost the three dgrads 115-190 us each against the 248 us of
-    colstats passes they remove (docs/ARCHITECTURE.md, "rejected").  FN_BN_DGRAD_FUSE=1
-    turns it on; tests/test_bnfuse_gpu.py keeps it correct."""
-    return os.environ.get("FN_BN_DGRAD_FUSE", "0") == "1"
+    """Whether BN forwards tag their outputs for the consuming conv's dgrad.  ``FN_BN_DGRAD_FUSE``:
+    'auto' (default) = whenever the 32x32x16 tile kernel is on (``FN_TILE_M32``): its dgrad
+    epilogue reads y at the tile's positions with every load of a pass in flight together and
+    has the registers for it (209-247 VGPRs, no scratch); '1' also fuses into the 16x16x32
+    kernel's statistics instance, measured slower there (its spills cost the three dgrads
+    115-190 us each against the colstats passes they remove); '0' never."""
+    mode = os.environ.get("FN_BN_DGRAD_FUSE", "auto")
+    if mode == "auto":
+        from .conv_tile import m32_enabled
+
+        return m32_enabled()
+    return mode == "1"
+
+
+def tile16_enabled() -> bool:
+    """The statistics epilogue on the 16x16x32 kernel (opt-in: FN_BN_DGRAD_FUSE=1)."""
+    return os.environ.get("FN_BN_DGRAD_FUSE", "auto") == "1"
 
 
 def pool_stats_enabled() -> bool:

@@ -402,15 +402,14 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
     rt = rowtab_tensor(p, kdims, src5.device)
     kt = ktab_tensor(p, kdims, src5.device)
     ext = [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4]
+    if bny is not None:
+        ext += [bny.numel(), bnp.numel()]
     if p.m32:
-        assert bny is None, "the BN-statistics dgrad epilogue is a conv_tile_kernel instance"
         _native.kernels().conv_tile32(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                       zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                       _native.ptr(stats), geom, ncol, act, p.MB, sched(src5.device, st).data_ptr(),
-                                      st, ext, float(oscale))
+                                      st, ext, float(oscale), _native.ptr(bny), _native.ptr(bnp))
         return
-    if bny is not None:
-        ext += [bny.numel(), bnp.numel()]
     _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                 zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                 _native.ptr(stats), geom, ncol, act, p.MT, p.NT, sched(src5.device, st).data_ptr(),
@@ -447,7 +446,12 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None):
     wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     lds_bws = 2 * p.BUF + 64 + red_bytes(p.NT) + (p.nks + PD + 2) * 16 + p.HPpad * 8 + p.NT * 16 * 16
-    if bn is None or lds_bws > LDS_MAX or p.NT != 2 or p.m32:   # (the statistics instance: 32-column blocks, BN
+    # the statistics epilogue: every conv_tile32 plan (its LDS holds the BN scale / shift already),
+    # the conv_tile_kernel instance only when asked for (FN_BN_DGRAD_FUSE=1: measured slower)
+    from . import bnfuse
+
+    fuse = p.m32 or (bnfuse.tile16_enabled() and lds_bws <= LDS_MAX and p.NT == 2)
+    if bn is None or not fuse:   # (the statistics instance: 32-column blocks, BN
         # scale/shift in LDS)
         run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
         return dx if bn is None else (dx, None)
