@@ -5,9 +5,11 @@ namespace py = pybind11;
 
 void register_sampler(py::module_& m);
 void register_voxel(py::module_& m);
+void register_weibull(py::module_& m);
 
 PYBIND11_MODULE(_rt, m) {
-  m.doc() = "featurenet_amd native host runtime (sampler, voxel pipeline)";
+  m.doc() = "featurenet_amd native host runtime (sampler, voxel pipeline, CLEVER Weibull fits)";
   register_sampler(m);
   register_voxel(m);
+  register_weibull(m);
 }

@@ -79,8 +79,8 @@ def _bwd_input(dz2, y2, prm, dbeta, dgamma, act, training):
     dy = torch.empty_like(y2)
     if training:
         db, dg, inv = dbeta, dgamma, 1.0 / M
-    else:
-        db = dg = torch.zeros_like(dbeta)
+    else:                                        # eval: the statistics are constants
+        db = dg = torch.zeros(C, dtype=torch.float32, device=y2.device)
         inv = 0.0
     _native.kernels().bn_bwd_apply(dz2.data_ptr(), y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(),
                                    prm[0].data_ptr(), prm[1].data_ptr(), db.data_ptr(), dg.data_ptr(), dy.data_ptr(),
@@ -117,7 +117,11 @@ class BatchNormActFn(torch.autograd.Function):
         y2 = y.reshape(-1, C)
         dz2 = dz.contiguous().to(torch.bfloat16).reshape(-1, C)
         part = bnfuse.take(dz2, y) if ctx.training else None
-        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
+        dbeta = dgamma = None
+        if ctx.training or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            # (eval mode with frozen parameters -- input gradients of robustness attacks -- needs
+            # neither: no colstats pass)
+            dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
                 dbeta if ctx.has_beta else None, None, None, None, None, None, None, None, None)
@@ -164,7 +168,9 @@ class BatchNormActPoolFn(torch.autograd.Function):
             K.pool_bwd(dp.data_ptr(), y.data_ptr(), dz.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), geom,
                        int(ctx.is_max), int(ctx.count_pad), ctx.act, _native.stream(y), [y.numel(), dp.numel()])
         y2, dz2 = y.reshape(-1, C), dz.reshape(-1, C)
-        dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
+        dbeta = dgamma = None
+        if ctx.training or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
                 dbeta if ctx.has_beta else None) + (None,) * 10

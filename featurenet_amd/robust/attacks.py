@@ -7,9 +7,16 @@ parameters of ``tensorflow_generator.py:151-173`` (norm 2; PGD eps 1, step
 Input gradients flow through the same HIP kernels as training (the conv
 dgrad kernel computes d(loss)/d(input)); every attack runs on whole batches,
 not per-sample Python loops.
+
+Attacks need d(loss)/d(input) only: every gradient here is taken under
+:func:`no_param_grad`, so the conv / dense backward never launches a weight-gradient kernel
+(``needs_input_grad`` of the weights is False) and nothing is written into the training
+gradient buffer (``FlatParams`` slots) -- about a third of each PGD / CW / CLEVER iteration's
+kernels in round 3.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -18,6 +25,20 @@ import torch.nn.functional as F
 
 def _logits(model, x: torch.Tensor) -> torch.Tensor:
     return model(x).float()
+
+
+@contextlib.contextmanager
+def no_param_grad(model):
+    """Input-gradient-only autograd through ``model``: parameters stop requiring grad for the
+    duration (restored on exit, also after an exception)."""
+    ps = [p for p in model.parameters() if p.requires_grad]
+    for p in ps:
+        p.requires_grad_(False)
+    try:
+        yield
+    finally:
+        for p in ps:
+            p.requires_grad_(True)
 
 
 def predict(model, x: torch.Tensor, batch_size: int = 256) -> torch.Tensor:
@@ -49,29 +70,39 @@ def _direction(g: torch.Tensor, norm) -> torch.Tensor:
 
 def loss_gradient(model, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     xg = x.detach().float().clone().requires_grad_(True)
-    loss = F.cross_entropy(_logits(model, xg), y, reduction="sum")
-    (g,) = torch.autograd.grad(loss, xg)
+    with no_param_grad(model):
+        loss = F.cross_entropy(_logits(model, xg), y, reduction="sum")
+        (g,) = torch.autograd.grad(loss, xg)
     return g
 
 
-def class_gradients(model, x: torch.Tensor, classes: torch.Tensor | None = None) -> torch.Tensor:
+def class_gradients(model, x: torch.Tensor, classes: torch.Tensor | None = None,
+                    max_rows: int = 16384) -> torch.Tensor:
     """d logit_c / d x for every class c (or the listed ones): [B, C, *x.shape[1:]].
 
-    All classes are obtained from ONE backward pass: the batch is replicated
-    per class and each replica back-propagates its own one-hot seed.
-    """
+    All classes are obtained from ONE backward pass per chunk: the batch is replicated per
+    class and each replica back-propagates its own one-hot seed; chunks of at most
+    ``max_rows`` replicated rows bound the activation memory of large pools (CLEVER over a
+    whole robustness set)."""
     B = x.shape[0]
     with torch.no_grad():
         nc = _logits(model, x[:1]).shape[-1]
     cls = torch.arange(nc, device=x.device) if classes is None else classes.to(x.device)
     C = len(cls)
-    xr = x.detach().float().unsqueeze(1).expand(B, C, *x.shape[1:]).reshape(B * C, *x.shape[1:]).clone()
-    xr.requires_grad_(True)
-    z = _logits(model, xr)
-    seed = torch.zeros_like(z)
-    seed[torch.arange(B * C, device=x.device), cls.repeat(B)] = 1.0
-    (g,) = torch.autograd.grad(z, xr, grad_outputs=seed)
-    return g.reshape(B, C, *x.shape[1:])
+    step = max(1, max_rows // max(C, 1))
+    out = []
+    with no_param_grad(model):
+        for i in range(0, B, step):
+            xb = x[i:i + step].detach().float()
+            b = xb.shape[0]
+            xr = xb.unsqueeze(1).expand(b, C, *x.shape[1:]).reshape(b * C, *x.shape[1:]).clone()
+            xr.requires_grad_(True)
+            z = _logits(model, xr)
+            seed = torch.zeros_like(z)
+            seed[torch.arange(b * C, device=x.device), cls.repeat(b)] = 1.0
+            (g,) = torch.autograd.grad(z, xr, grad_outputs=seed)
+            out.append(g.reshape(b, C, *x.shape[1:]))
+    return out[0] if len(out) == 1 else torch.cat(out)
 
 
 def fgsm(model, x: torch.Tensor, y: torch.Tensor | None = None, eps: float = 0.3, norm=float("inf"),
@@ -162,6 +193,13 @@ def carlini_l2(model, x: torch.Tensor, y: torch.Tensor | None = None, confidence
     best_adv = x.clone()
     nc = predict(model, x[:1]).shape[-1]
     onehot = F.one_hot(y, nc).float()
+    with no_param_grad(model):
+        return _cw_search(model, x, y, confidence, learning_rate, binary_search_steps, max_iter, lo, span, B, shape,
+                          w0, c, c_lo, c_hi, best_l2, best_adv, onehot)
+
+
+def _cw_search(model, x, y, confidence, learning_rate, binary_search_steps, max_iter, lo, span, B, shape, w0, c,
+               c_lo, c_hi, best_l2, best_adv, onehot):
     for _ in range(binary_search_steps):
         w = w0.clone().requires_grad_(True)
         opt = torch.optim.Adam([w], lr=learning_rate)
@@ -174,9 +212,8 @@ def carlini_l2(model, x: torch.Tensor, y: torch.Tensor | None = None, confidence
             f = torch.clamp(real - other + confidence, min=0.0)
             l2 = ((adv - x) ** 2).reshape(B, -1).sum(1)
             loss = (l2 + c * f).sum()
-            # gradient w.r.t. the attack variable only: loss.backward() would also run every
-            # layer's weight-gradient pass into the training gradient buffer (and, under DP,
-            # fire the all-reduce hooks outside a training step)
+            # gradient w.r.t. the attack variable only (and no parameter requires grad: no
+            # weight-gradient kernels, no writes into the training gradient buffer, no DP hooks)
             (w.grad,) = torch.autograd.grad(loss, [w])
             opt.step()
             with torch.no_grad():

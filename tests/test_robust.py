@@ -88,3 +88,67 @@ def test_eval_robustness_policy():
     assert clean == 1.0 and adv <= clean and math.isfinite(score)
     assert out["score"] == out["fgsm"][0]
     assert eval_robustness(m, (x, y), ["fgsm"], accuracy=0.4)["skipped"]
+
+
+def test_native_weibull_fit_matches_scipy():
+    """csrc/runtime/weibull.cpp runs scipy's estimator (weibull_min.fit with a shape guess,
+    optimizer fmin) step for step: same parameters on random CLEVER-like problems."""
+    from scipy.stats import weibull_min
+
+    from featurenet_amd import _native
+    from featurenet_amd.robust.metrics import _fmin, weibull_locs
+
+    rng = np.random.default_rng(1)
+    maxes = np.stack([rng.random(10) * rng.uniform(0.05, 5) + rng.uniform(0, 3) for _ in range(40)])
+    ref = np.array([weibull_min.fit(-m, 1.0, optimizer=_fmin) for m in maxes])
+    if _native.runtime_available():
+        fit = _native.runtime().weibull_min_fit_batch(-maxes, 1.0, 1e-6, 1e-4, 1000, 2)
+        np.testing.assert_allclose(fit, ref, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(weibull_locs(maxes, 1.0), ref[:, 1], rtol=1e-9, atol=1e-12)
+
+
+class _Small(torch.nn.Module):
+    """A nonlinear 3-class model on 2x3x3x1 inputs (class gradients vary over the pool)."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)
+        self.w1 = torch.nn.Parameter(torch.randn(18, 8, generator=g))
+        self.w2 = torch.nn.Parameter(torch.randn(8, 3, generator=g))
+
+    def forward(self, x):
+        return torch.tanh(x.reshape(len(x), -1) @ self.w1) @ self.w2
+
+
+def test_clever_batch_equals_per_sample_reference_loop():
+    """The batched CLEVER (all samples' pools in one gradient pass, one batched fit) gives the
+    reference's per-sample loop (fresh seed-0 generator per sample) exactly."""
+    from featurenet_amd.robust.metrics import _clever_scores_rng, clever_batch, clever_u_batch
+
+    m = _Small()
+    xs = torch.rand(7, 2, 3, 3, 1, generator=torch.Generator().manual_seed(2))
+    batched = clever_batch(m, xs, nb_batches=10, batch_size=5, radius=2.0, norm=2, pool_factor=3, clip=(0.0, 1.0),
+                           chunk_samples=3)
+    for i in range(len(xs)):
+        ref = _clever_scores_rng(m, xs[i], 10, 5, 2.0, 2, None, 1.0, 3, (0.0, 1.0), np.random.default_rng(0))
+        assert batched[i].keys() == ref.keys()
+        for j in ref:
+            assert batched[i][j] == pytest.approx(ref[j], rel=1e-6, abs=1e-9)
+    u = clever_u_batch(m, xs, 10, 5, 2.0, 2, pool_factor=3, clip=(0.0, 1.0))
+    assert u == pytest.approx([min(d.values()) for d in batched])
+
+
+def test_attacks_take_no_parameter_gradients():
+    """Input gradients only: parameters end with requires_grad restored and no .grad written
+    (on the GPU the same switch keeps every weight-gradient kernel from launching)."""
+    m = _Small()
+    x = torch.rand(4, 2, 3, 3, 1)
+    y = torch.tensor([0, 1, 2, 0])
+    g = A.loss_gradient(m, x, y)
+    assert g.shape == x.shape and torch.isfinite(g).all()
+    cg = A.class_gradients(m, x, max_rows=6)                       # 2 chunks of 2 samples x 3 classes
+    full = A.class_gradients(m, x)
+    torch.testing.assert_close(cg, full)
+    A.carlini_l2(m, x, y, binary_search_steps=2, max_iter=3)
+    A.pgd(m, x, y, max_iter=3)
+    assert all(p.requires_grad and p.grad is None for p in m.parameters())
