@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--workers-per-device", type=int, default=1)
     ap.add_argument("--graph", default="both", choices=["both", "on", "off"])
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--attacks", default="", help="comma list (e.g. cw,pgd): robustness evaluation of every trained "
+                    "candidate with accuracy >= 0.5, as FullEvolution does (full_evolution.py:244-258)")
+    ap.add_argument("--robustness-set", type=int, default=500)
     a = ap.parse_args()
     from featurenet_amd.ir.parse import parse_feature_model
     from featurenet_amd.search.mutation import MutationConfig, Mutator
@@ -41,8 +44,9 @@ def main():
     sched = TrialScheduler(mode=mode, workers_per_device=a.workers_per_device)
     graphs = {"both": (False, True), "on": (True,), "off": (False,)}[a.graph]
     for graph in graphs:
+        attacks = [t for t in a.attacks.split(",") if t]
         cfg = TrialConfig(dataset=a.dataset, epochs=a.epochs, batch_size=a.batch, synthetic_sizes=(a.train, 1000),
-                          graph=graph)
+                          graph=graph, attacks=attacks, robustness_set_size=a.robustness_set)
         t0 = time.perf_counter()
         out = sched.map(specs, cfg)
         dt = time.perf_counter() - t0
@@ -51,7 +55,14 @@ def main():
                           "candidates": len(specs), "trained": ok, "seconds": round(dt, 2),
                           "devices": sched.devices, "workers_per_device": a.workers_per_device,
                           "dataset": a.dataset, "epochs": a.epochs, "train_samples": a.train, "batch": a.batch,
-                          "failed": [s.name for s in out if s.status != "trained"]}), flush=True)
+                          "attacks": attacks, "robustness_set": a.robustness_set if attacks else None,
+                          "robustness_evaluated": sum(s.status == "trained" and (s.accuracy or 0) >= 0.5
+                                                      for s in out) if attacks else None,
+                          # every candidate that did not train, with its status and reason (e.g. c33:
+                          # 'invalid', > 20M parameters -- the reference's cap, model/keras_model.py:127)
+                          "not_trained": [{"name": s.name, "status": s.status,
+                                           "error": (s.error or "").splitlines()[0][:200]}
+                                          for s in out if s.status != "trained"]}), flush=True)
 
 
 if __name__ == "__main__":
