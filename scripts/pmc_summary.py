@@ -10,6 +10,8 @@ all 256 CUs / 1024 SIMDs of an MI355X:
 * wait / wave = SQ_WAIT_ANY / SQ_WAVE_CYCLES  (waves parked on s_waitcnt / barrier)
 * stall/wave  = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES (issue stalls)
 * HBM GB/s    = FETCH_SIZE (KB read from HBM via the TCC/EA) / kernel time, when collected
+* with a second pass holding them: effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time,
+  LDS and VALU instructions per MFMA, LDS-issue stall share (SQ_WAIT_INST_LDS / wave cycles)
 
 Several CSVs (one per counter pass of the same program) are merged per (kernel, grid);
 times come from the first pass.
@@ -41,9 +43,11 @@ def main():
                 if i == 0:
                     durs[key][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     print(f"Counters normalised at {a.ghz} GHz over 1024 SIMDs / 256 CUs.\n")
+    extra = any("GRBM_GUI_ACTIVE" in c for c in agg.values())
     print("| kernel | grid (threads) | time ms | MFMA util | LDS util | bank conflict / LDS cyc | wait / wave cyc | "
-          "issue stall / wave cyc | HBM read GB/s |")
-    print("|---|---|---|---|---|---|---|---|---|")
+          "issue stall / wave cyc | HBM read GB/s |" + (" clock GHz | LDS inst / MFMA | VALU inst / MFMA | "
+                                                         "LDS stall / wave cyc |" if extra else ""))
+    print("|---|---|---|---|---|---|---|---|---|" + ("---|---|---|---|" if extra else ""))
     rows = sorted((kv for kv in agg.items() if kv[0] in durs), key=lambda kv: -sum(durs[kv[0]].values()))[: a.top]
     for (name, grid), c in rows:
         ns = sum(durs[(name, grid)].values())
@@ -53,7 +57,11 @@ def main():
         print(f"| `{name}` | {grid} | {ns / 1e6:.3f} | {c.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / (cyc * 1024):.3f} | "
               f"{lds / (cyc * 256):.3f} | {c.get('SQ_LDS_BANK_CONFLICT', 0) / max(lds, 1):.3f} | "
               f"{c.get('SQ_WAIT_ANY', 0) / wc:.3f} | {c.get('SQ_WAIT_INST_ANY', 0) / wc:.3f} | "
-              f"{(c['FETCH_SIZE'] * 1024 / ns if 'FETCH_SIZE' in c else float('nan')):.0f} |")
+              f"{(c['FETCH_SIZE'] * 1024 / ns if 'FETCH_SIZE' in c else float('nan')):.0f} |" +
+              (f" {c.get('GRBM_GUI_ACTIVE', 0) / 8 / ns:.2f} | "
+               f"{c.get('SQ_INSTS_LDS', 0) / max(c.get('SQ_INSTS_MFMA', 0), 1):.2f} | "
+               f"{c.get('SQ_INSTS_VALU', 0) / max(c.get('SQ_INSTS_MFMA', 0), 1):.2f} | "
+               f"{c.get('SQ_WAIT_INST_LDS', 0) / wc:.3f} |" if extra else ""))
 
 
 if __name__ == "__main__":
