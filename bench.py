@@ -177,10 +177,14 @@ def main():
         bucketer = GradBucketer(flat, bucket_mb=args.bucket_mb, force=args.force_allreduce)
         bucketer.broadcast_from(0)
 
+        def loss_of(x, y):
+            # the model's own loss where it has one (the segmentation head computes the per-voxel
+            # cross-entropy in its epilogue: no logits tensor), else softmax_xent of the logits
+            return model.loss(x, y) if hasattr(model, "loss") else softmax_xent(model(x), y)
+
         def step(i):
             flat.zero_grad()
-            logits = model(xs[i % args.pool])
-            loss = softmax_xent(logits, ys[i % args.pool])
+            loss = loss_of(xs[i % args.pool], ys[i % args.pool])
             loss.backward()
             scale = bucketer.finish()
             opt.step(grad_scale=scale)
@@ -247,7 +251,7 @@ def main():
         try:
             with torch.cuda.graph(g):
                 flat.zero_grad()
-                gl = softmax_xent(model(sx), sy)
+                gl = loss_of(sx, sy)
                 gl.backward()
                 bucketer.finish()
                 opt.step_device()

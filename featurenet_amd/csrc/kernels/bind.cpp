@@ -24,6 +24,9 @@ long long fn_conv_halo_lds(const int*, int);
 int fn_conv_halo_workers(const int*, int);
 int fn_pw_fwd(const void*, const void*, const float*, void*, long long, int, int, int, hipStream_t, const float*,
               const float*, int, const void*, const float*, const float*, float*, int);
+int fn_pw_xent_blocks(long long);
+int fn_pw_fwd_xent(const void*, const void*, const float*, void*, long long, int, int, const float*, const float*, int,
+                   const long long*, float*, float, float, hipStream_t);
 int fn_pw_fwd_blocks(long long, int, int);
 int fn_pw_wgrad(const void*, const void*, float*, long long, int, int, hipStream_t, const float*, const float*, int);
 int fn_conv_halo_wgrad_yblocks(const int*, int);
@@ -431,6 +434,21 @@ PYBIND11_MODULE(_C, m) {
      py::arg("act"), py::arg("st"), py::arg("psc") = 0, py::arg("psh") = 0, py::arg("pact") = 0, py::arg("sy") = 0,
      py::arg("ssc") = 0, py::arg("ssh") = 0, py::arg("spart") = 0, py::arg("sact") = 0);
   m.def("pw_fwd_blocks", &fn_pw_fwd_blocks);
+  m.def("pw_xent_blocks", &fn_pw_xent_blocks);
+  m.def("pw_fwd_xent", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t dlog, long long M, int K, int N,
+                          uintptr_t psc, uintptr_t psh, int pact, uintptr_t labels, uintptr_t xpart, float xscale,
+                          float smoothing, uintptr_t st, std::vector<long long> ext) {
+    fits(ext, 0, M * K, "pw_fwd_xent", "x");
+    fits(ext, 1, M * N, "pw_fwd_xent", "dlog");
+    fits(ext, 2, M, "pw_fwd_xent", "labels");
+    fits(ext, 3, 2LL * fn_pw_xent_blocks(M), "pw_fwd_xent", "xpart");
+    chk(fn_pw_fwd_xent(P<const void*>(x), P<const void*>(w), P<const float*>(bias), P<void*>(dlog), M, K, N,
+                       P<const float*>(psc), P<const float*>(psh), pact, P<const long long*>(labels), P<float*>(xpart),
+                       xscale, smoothing, S(st)),
+        "pw_fwd_xent");
+  }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("dlog"), py::arg("M"), py::arg("K"), py::arg("N"),
+     py::arg("psc"), py::arg("psh"), py::arg("pact"), py::arg("labels"), py::arg("xpart"), py::arg("xscale"),
+     py::arg("smoothing"), py::arg("st"), py::arg("ext"));
   m.def("pw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, long long M, int K, int N, uintptr_t st,
                        uintptr_t psc, uintptr_t psh, int pact) {
     chk(fn_pw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), M, K, N, S(st), P<const float*>(psc),

@@ -31,7 +31,13 @@ __device__ __forceinline__ int pw_tiles(long long M) { return (int)((M + PW_BM -
 //   sy [M][N] (scale ssc, shift ssh) is read alongside: each workgroup also sums that BN's raw
 //   backward moments (sum g, sum g*y), g = dz * act'(y*ssc+ssh), into spart[block][2][N]
 //   (bn_finalize MODE 2) -- the colstats pass over dz and y disappears (N % 8 == 0, 2048 % N == 0)
-template <int KP, int NP, int ACT, bool HAS_BIAS, int PRO = -1, int BWS = -1>
+// XENT: the layer is a classifier head whose logits feed softmax + categorical cross-entropy against
+//   int64 labels[M] (the per-voxel segmentation loss): every thread takes one row of the staged
+//   logit tile, computes its log-sum-exp loss, top-1 hit and d(logits) = (softmax - target) * xscale
+//   (label smoothing as softmax_xent_tile_kernel), and the tile's d(logits) -- not the logits --
+//   are stored; per-workgroup (loss sum, hits) go to xpart[block][2].  The logits never reach HBM
+//   and the separate loss kernel (one read of the logits + one write of d(logits)) disappears.
+template <int KP, int NP, int ACT, bool HAS_BIAS, int PRO = -1, int BWS = -1, bool XENT = false>
 __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
                                                            const float* __restrict__ bias, bf16* __restrict__ y,
                                                            long long M, int K, int N, const float* __restrict__ psc,
@@ -39,7 +45,10 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
                                                            const bf16* __restrict__ sy = nullptr,
                                                            const float* __restrict__ ssc = nullptr,
                                                            const float* __restrict__ ssh = nullptr,
-                                                           float* __restrict__ spart = nullptr) {
+                                                           float* __restrict__ spart = nullptr,
+                                                           const long long* __restrict__ labels = nullptr,
+                                                           float* __restrict__ xpart = nullptr, float xscale = 0.f,
+                                                           float smoothing = 0.f) {
   constexpr int LDA = KP + 8, LDO = NP + 8;
   constexpr int KS = KP / 32, NT = NP / 16;
   constexpr int CH = KP / 8;                     // 16-B chunks per thread of a 256 x KP tile
@@ -100,6 +109,7 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
     }
   }
   const int ntiles = pw_tiles(M);
+  float xl = 0.f, xc = 0.f;                      // XENT: this thread's loss / top-1 hit sums
   uint4 rb[CH];
   auto load = [&](int t) {                       // tile t: 256*K contiguous bf16 (16-B aligned: 512*K*t)
     const long long e0 = (long long)t * PW_BM * K;
@@ -168,6 +178,39 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
         for (int r = 0; r < 4; ++r)
           Os[(wave * 64 + mt * 16 + lg * 4 + r) * LDO + nt * 16 + lr] = f2bf(act_fwd(acc[mt][nt][r] + bv[nt], ACT));
     __syncthreads();
+    if constexpr (XENT) {
+      // one row per thread, from the stored bf16 logits (the values the unfused loss would read)
+      if (tid < rows) {
+        bf16* orow = Os + tid * LDO;
+        const long long yl = labels[(long long)t * PW_BM + tid];
+        const float off = smoothing / (float)N, on = 1.f - smoothing + off;
+        float v[NP];
+        float mx = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int c = 0; c < NP; ++c) {
+          v[c] = c < N ? bf2f(orow[c]) : -INFINITY;
+          if (v[c] > mx) { mx = v[c]; am = c; }
+        }
+        float se = 0.f;
+#pragma unroll
+        for (int c = 0; c < NP; ++c) se += c < N ? __expf(v[c] - mx) : 0.f;
+        const float lse = mx + __logf(se);
+        float lrow = 0.f;
+#pragma unroll
+        for (int c = 0; c < NP; ++c) {
+          if (c < N) {
+            const float lp = v[c] - lse;
+            const float tgt = (c == yl) ? on : off;
+            lrow -= tgt * lp;
+            orow[c] = f2bf((__expf(lp) - tgt) * xscale);   // own row only: no race
+          }
+        }
+        xl += lrow;
+        xc += (am == yl) ? 1.f : 0.f;
+      }
+      __syncthreads();
+    }
     // gather padded rows -> flat 256*N run, 16-B stores
     const long long o0 = (long long)t * PW_BM * N;
     const int nel = rows * N;
@@ -195,6 +238,22 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
         }
       }
       *(uint4*)(y + o0 + c * 8) = p.u;           // rows * N is a multiple of 8 (M % 8 == 0)
+    }
+  }
+  if constexpr (XENT) {
+    // (loss sum, hits) of the workgroup, fixed order: waves, then the 4 wave sums
+    xl = wave_sum(xl);
+    xc = wave_sum(xc);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(pw_dsm);
+    if (lane == 0) {
+      red[wave] = xl;
+      red[4 + wave] = xc;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      xpart[2 * blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+      xpart[2 * blockIdx.x + 1] = (red[4] + red[5]) + (red[6] + red[7]);
     }
   }
   if constexpr (BWS >= 0) {
@@ -424,6 +483,32 @@ extern "C" int fn_pw_fwd(const void* x, const void* w, const float* bias, void* 
   else { if (N <= 32) PWA(64, 32); else PWA(64, 64); }
 #undef PWA
 #undef PWF
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// Classifier head + softmax cross-entropy (XENT instances): dlog [M][N] bf16 = d(mean loss)/d(logits)
+// with xscale = 1/M folded in (the unscaled loss is sum(xpart[:, 0]) * xscale ... / M), labels
+// int64 [M] (no ignore index), xpart fp32 [fn_pw_xent_blocks(M)][2] = per-workgroup (loss sum, top-1
+// hits).  K, N <= 32, identity activation; psc / psh: the optional BN + act input prologue.
+extern "C" int fn_pw_xent_blocks(long long M) { return pw_grid(M, 3); }   // (143-159 VGPRs: 3 per CU)
+
+extern "C" int fn_pw_fwd_xent(const void* x, const void* w, const float* bias, void* dlog, long long M, int K, int N,
+                              const float* psc, const float* psh, int pact, const long long* labels, float* xpart,
+                              float xscale, float smoothing, hipStream_t st) {
+  if (K < 1 || K > 32 || N < 2 || N > 32 || M < 8 || M % 8 || !labels || !xpart) return -2;
+  if (!pw_pro_ok(psc, psh, K) || (psc && pact != ACT_NONE && pact != ACT_RELU)) return -2;
+  const dim3 grid((unsigned)fn_pw_xent_blocks(M));
+  const size_t lds = (size_t)PW_BM * (32 + 8) * 2;
+  const bool hb = bias != nullptr;
+#define PWX(HB, PA)                                                                                          \
+  hipLaunchKernelGGL((pw_fwd_kernel<32, 32, ACT_NONE, HB, PA, -1, true>), grid, dim3(PW_NTHR), lds, st,       \
+                     (const bf16*)x, (const bf16*)w, bias, (bf16*)dlog, M, K, N, psc, psh, nullptr, nullptr,     \
+                     nullptr, nullptr, labels, xpart, xscale, smoothing)
+  if (!psc) { if (hb) PWX(true, -1); else PWX(false, -1); }
+  else if (pact == ACT_RELU) { if (hb) PWX(true, ACT_RELU); else PWX(false, ACT_RELU); }
+  else { if (hb) PWX(true, ACT_NONE); else PWX(false, ACT_NONE); }
+#undef PWX
   FN_CHECK_LAUNCH();
   return 0;
 }

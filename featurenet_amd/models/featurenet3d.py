@@ -149,6 +149,9 @@ class FeatureNet3DSeg(nn.Module):
             x = x.unsqueeze(-1)
         for c in self.enc:
             x = c(x)
+        return self._decode(x)
+
+    def _decode(self, x: torch.Tensor) -> torch.Tensor:
         d, h = self.dec, self.head
         if self.training and subpixel.gpu_ok(x, d.cout, x.shape[-1]) and \
                 bn_ops.fused_pointwise_ok(x, d.cout, h.cout, d.act):
@@ -166,3 +169,26 @@ class FeatureNet3DSeg(nn.Module):
             return bn_ops.batchnorm_act_pointwise(y, d.gamma, d.beta, d.running_mean, d.running_var, h.weight, h.bias,
                                                   d.bn_momentum, d.bn_eps, d.act, stats_slab=slab)
         return h(d(x))  # [N, S, S, S, classes]
+
+    def loss(self, x: torch.Tensor, labels: torch.Tensor, smoothing: float = 0.0, with_correct: bool = False):
+        """Mean per-voxel softmax cross-entropy against ``labels`` [N, S, S, S] (+ the number of
+        top-1 hits when ``with_correct``).  Training on the GPU's sub-pixel path computes the loss
+        in the 1x1 head's epilogue (``subpixel.decoder_head_xent``: the logits are never stored);
+        otherwise ``softmax_xent(self(x), labels)``."""
+        from ..ops import softmax_xent
+
+        if x.dim() == 4:
+            x = x.unsqueeze(-1)
+        d, h = self.dec, self.head
+        if self.training:
+            z = x
+            for c in self.enc:
+                z = c(z)
+            if subpixel.gpu_ok(z, d.cout, z.shape[-1]) and bn_ops.fused_pointwise_ok(z, d.cout, h.cout, d.act) \
+                    and subpixel.xent_ok(d.cout, h.cout):
+                loss, hits = subpixel.decoder_head_xent(z, d.weight, d.gamma, d.beta, d.running_mean, d.running_var,
+                                                        h.weight, h.bias, labels, d.bn_momentum, d.bn_eps, d.act,
+                                                        smoothing)
+                return (loss, hits) if with_correct else loss
+            return softmax_xent(self._decode(z), labels, smoothing, with_correct)
+        return softmax_xent(self(x), labels, smoothing, with_correct)

@@ -236,6 +236,54 @@ def bn_bwd_to_shifted(dz2, y2, prm, dbeta, dgamma, act: int, full_shape) -> torc
     return dsh
 
 
+def _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb):
+    """Decoder forward up to the head's input: (y, its BN parameters, head weight [NC, K], bias)."""
+    from . import bn as bn_ops
+
+    y, slab = upconv_forward(x, w)
+    K = y.shape[-1]
+    prm = bn_ops._finalize_fwd(slab, y.numel() // K, gamma, beta, rmean, rvar, momentum, eps)
+    w2 = hw.detach().reshape(hw.shape[0], K)
+    bias = hb.detach().float().contiguous() if hb is not None else None
+    return y, prm, w2, bias
+
+
+def _head_backward(ctx, d2):
+    """Backward of decoder + head from d(logits) d2 [M, NC] (bf16): the input and parameter
+    gradients in SubpixelDecoderHeadFn.backward's order."""
+    from .. import _native
+    from . import bn as bn_ops
+    from . import conv_wtile
+    from ..training.flat import grad_target
+    from .conv import native_colsum, pw_wgrad
+
+    x, w, y, prm, hw = ctx.saved_tensors
+    K = y.shape[-1]
+    NC = hw.shape[0]
+    y2 = y.reshape(-1, K)
+    w2 = hw.detach().reshape(NC, K)
+    dhw = (pw_wgrad(d2, y2, pro=(prm[2], prm[3], ctx.act), out=grad_target(hw)).reshape(hw.shape)
+           if ctx.needs_input_grad[9] else None)
+    dhb = native_colsum(d2, out=grad_target(ctx.bparam)) if (ctx.has_b and ctx.needs_input_grad[10]) else None
+    M = y2.shape[0]
+    Kn = _native.kernels()
+    part = torch.empty(Kn.pw_fwd_blocks(M, NC, K), 2, K, dtype=torch.float32, device=y.device)
+    dz2 = torch.empty(M, K, dtype=torch.bfloat16, device=y.device)
+    wb = w2.t().to(torch.bfloat16).contiguous()
+    Kn.pw_fwd(d2.data_ptr(), wb.data_ptr(), 0, dz2.data_ptr(), M, NC, K, 0, _native.stream(d2), 0, 0, 0,
+              y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), part.data_ptr(), ctx.act)
+    dbeta, dgamma = bn_ops._bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
+    dsh = bn_bwd_to_shifted(dz2, y2, prm, dbeta, dgamma, ctx.act, y.shape)
+    dx = upconv_dgrad(dsh, w, x.shape) if ctx.needs_input_grad[0] else None
+    dw = None
+    if ctx.needs_input_grad[1]:
+        N, D, H, W, C = x.shape
+        p = conv_wtile.plan_subpixel(N, (D, H, W), C, K)
+        dw = fold_weight_grad(conv_wtile.conv_wgrad_subpixel(dsh, x, p)).reshape(w.shape)
+    return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
+            None, None, None, None, None, dhw, dhb)
+
+
 class SubpixelDecoderHeadFn(torch.autograd.Function):
     """logits = head(relu(bn(conv3^3_same(upsample2x(x))))) without materialising upsample2x(x)
     or relu(bn(.)) (FeatureNet3DSeg's decoder + 1x1 head, training mode).
@@ -249,56 +297,70 @@ class SubpixelDecoderHeadFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, rmean, rvar, momentum, eps, act, hw, hb):
-        from . import bn as bn_ops
         from .conv import pw_fwd
 
-        y, slab = upconv_forward(x, w)
-        K = y.shape[-1]
-        y2 = y.reshape(-1, K)
-        prm = bn_ops._finalize_fwd(slab, y2.shape[0], gamma, beta, rmean, rvar, momentum, eps)
-        NC = hw.shape[0]
-        w2 = hw.detach().reshape(NC, K)
-        bias = hb.detach().float().contiguous() if hb is not None else None
-        out = pw_fwd(y2, w2, bias, 0, pro=(prm[2], prm[3], act))
+        y, prm, w2, bias = _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb)
+        out = pw_fwd(y.reshape(-1, y.shape[-1]), w2, bias, 0, pro=(prm[2], prm[3], act))
         ctx.save_for_backward(x, w, y, prm, hw)
         ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
         ctx.params = (beta, gamma)
-        return out.reshape(*y.shape[:-1], NC)
+        return out.reshape(*y.shape[:-1], hw.shape[0])
 
     @staticmethod
     def backward(ctx, dout):
-        from .. import _native
-        from . import bn as bn_ops
-        from . import conv_wtile
-        from ..training.flat import grad_target
-        from .conv import native_colsum, pw_fwd, pw_wgrad
+        return _head_backward(ctx, dout.contiguous().to(torch.bfloat16).reshape(-1, ctx.saved_tensors[4].shape[0]))
 
-        x, w, y, prm, hw = ctx.saved_tensors
+
+class SubpixelDecoderHeadXentFn(torch.autograd.Function):
+    """(mean softmax cross-entropy, top-1 hits) of the per-voxel logits of
+    :class:`SubpixelDecoderHeadFn` against int64 ``labels`` -- with the loss in the head's
+    epilogue (``pw_fwd_kernel`` XENT instance): the forward stores d(loss)/d(logits) instead of
+    the 838M logits of a 128 x 64^3 batch, and the separate loss kernel disappears (reference:
+    the softmax head + categorical cross-entropy, ``model/keras_model.py:124``,
+    ``tensorflow_generator.py:232-235``)."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, rmean, rvar, momentum, eps, act, hw, hb, labels, smoothing):
+        from .. import _native
+
+        y, prm, w2, bias = _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb)
         K = y.shape[-1]
-        NC = hw.shape[0]
         y2 = y.reshape(-1, K)
-        d2 = dout.contiguous().to(torch.bfloat16).reshape(-1, NC)
-        w2 = hw.detach().reshape(NC, K)
-        dhw = (pw_wgrad(d2, y2, pro=(prm[2], prm[3], ctx.act), out=grad_target(hw)).reshape(hw.shape)
-               if ctx.needs_input_grad[9] else None)
-        dhb = native_colsum(d2, out=grad_target(ctx.bparam)) if (ctx.has_b and ctx.needs_input_grad[10]) else None
-        M = y2.shape[0]
+        M, NC = y2.shape[0], w2.shape[0]
         Kn = _native.kernels()
-        part = torch.empty(Kn.pw_fwd_blocks(M, NC, K), 2, K, dtype=torch.float32, device=y.device)
-        dz2 = torch.empty(M, K, dtype=torch.bfloat16, device=y.device)
-        wb = w2.t().to(torch.bfloat16).contiguous()
-        Kn.pw_fwd(d2.data_ptr(), wb.data_ptr(), 0, dz2.data_ptr(), M, NC, K, 0, _native.stream(d2), 0, 0, 0,
-                  y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), part.data_ptr(), ctx.act)
-        dbeta, dgamma = bn_ops._bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
-        dsh = bn_bwd_to_shifted(dz2, y2, prm, dbeta, dgamma, ctx.act, y.shape)
-        dx = upconv_dgrad(dsh, w, x.shape) if ctx.needs_input_grad[0] else None
-        dw = None
-        if ctx.needs_input_grad[1]:
-            N, D, H, W, C = x.shape
-            p = conv_wtile.plan_subpixel(N, (D, H, W), C, K)
-            dw = fold_weight_grad(conv_wtile.conv_wgrad_subpixel(dsh, x, p)).reshape(w.shape)
-        return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, dhw, dhb)
+        lab = labels.reshape(-1).contiguous()
+        dlog = torch.empty(M, NC, dtype=torch.bfloat16, device=y.device)
+        xpart = torch.empty(Kn.pw_xent_blocks(M), 2, dtype=torch.float32, device=y.device)
+        wb = w2.to(torch.bfloat16).contiguous()
+        Kn.pw_fwd_xent(y2.data_ptr(), wb.data_ptr(), _native.ptr(bias), dlog.data_ptr(), M, K, NC,
+                       prm[2].data_ptr(), prm[3].data_ptr(), act, lab.data_ptr(), xpart.data_ptr(), 1.0 / M,
+                       float(smoothing), _native.stream(y2), [y2.numel(), dlog.numel(), lab.numel(), xpart.numel()])
+        ctx.save_for_backward(x, w, y, prm, hw, dlog)
+        ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
+        ctx.params = (beta, gamma)
+        hits = xpart[:, 1].sum().round().long()
+        ctx.mark_non_differentiable(hits)
+        return xpart[:, 0].sum() / M, hits
+
+    @staticmethod
+    def backward(ctx, dloss, _dhits):
+        from .. import _native
+
+        dlog = ctx.saved_tensors[5]
+        # d(logits) carries 1/M; scale by dloss in place -- a near-empty launch when dloss == 1
+        s = dloss.detach().float().reshape(1).contiguous()
+        _native.kernels().scale_unless_one(dlog.data_ptr(), 1, s.data_ptr(), dlog.numel(), _native.stream(dlog))
+        g = _head_backward(_SavedView(ctx), dlog)
+        return g + (None, None)
+
+
+class _SavedView:
+    """ctx stand-in for :func:`_head_backward` (its first five saved tensors, the same flags)."""
+
+    def __init__(self, ctx):
+        self.saved_tensors = ctx.saved_tensors[:5]
+        self.needs_input_grad = ctx.needs_input_grad
+        self.act, self.has_b, self.bparam, self.params = ctx.act, ctx.has_b, ctx.bparam, ctx.params
 
 
 def decoder_head(x5, w, gamma, beta, running_mean, running_var, hw, hb, momentum=0.1, eps=1e-5, act="relu"):
@@ -308,3 +370,21 @@ def decoder_head(x5, w, gamma, beta, running_mean, running_var, hw, hb, momentum
 
     return SubpixelDecoderHeadFn.apply(x5.to(torch.bfloat16).contiguous(), w, gamma, beta, running_mean,
                                        running_var, momentum, eps, act_code(act), hw, hb)
+
+
+def decoder_head_xent(x5, w, gamma, beta, running_mean, running_var, hw, hb, labels, momentum=0.1, eps=1e-5,
+                      act="relu", smoothing: float = 0.0):
+    """:func:`decoder_head` + mean softmax cross-entropy against per-voxel ``labels`` -> (loss, hits)
+    (caller checks :func:`gpu_ok` and :func:`xent_ok`)."""
+    from .spec import act_code
+
+    return SubpixelDecoderHeadXentFn.apply(x5.to(torch.bfloat16).contiguous(), w, gamma, beta, running_mean,
+                                           running_var, momentum, eps, act_code(act), hw, hb, labels.long(),
+                                           float(smoothing))
+
+
+def xent_ok(K: int, NC: int) -> bool:
+    """Shapes the fused head + loss kernel takes (K, NC <= 32; FN_SEG_XENT=0 turns it off)."""
+    import os
+
+    return os.environ.get("FN_SEG_XENT", "1") != "0" and K <= 32 and 2 <= NC <= 32

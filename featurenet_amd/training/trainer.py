@@ -179,10 +179,18 @@ class Trainer:
             xb = xb.float()
         return xb
 
+    def _loss(self, xb: torch.Tensor, yb: torch.Tensor):
+        """(mean loss, top-1 hits): the model's own fused loss when it has one (e.g.
+        FeatureNet3DSeg.loss, the cross-entropy inside the head's kernel), else softmax_xent
+        of its logits."""
+        lossf = getattr(self.model, "loss", None)
+        if callable(lossf):
+            return lossf(self._prep(xb), yb, self.label_smoothing, with_correct=True)
+        return softmax_xent(self.model(self._prep(xb)), yb, self.label_smoothing, with_correct=True)
+
     def _eager_step(self, xb: torch.Tensor, yb: torch.Tensor):
         self.flat.zero_grad()
-        logits = self.model(self._prep(xb))
-        loss, correct = softmax_xent(logits, yb, self.label_smoothing, with_correct=True)
+        loss, correct = self._loss(xb, yb)
         loss.backward()
         try:
             scale = self.bucketer.finish()
@@ -220,8 +228,7 @@ class Trainer:
         try:
             with torch.cuda.graph(g):
                 self.flat.zero_grad()
-                logits = self.model(self._prep(self._sx))
-                loss, correct = softmax_xent(logits, self._sy, self.label_smoothing, with_correct=True)
+                loss, correct = self._loss(self._sx, self._sy)
                 loss.backward()
                 self.bucketer.finish()
                 self.opt.step_device()

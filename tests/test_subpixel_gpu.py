@@ -102,3 +102,33 @@ def test_decoder_head_matches_upsample_path():
         assert k in grads[0], k
         r = _rel(grads[0][k], grads[1][k])
         assert r < 5e-2, (k, r)
+
+
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_fused_head_xent_matches_softmax_xent(monkeypatch, smoothing):
+    """FeatureNet3DSeg.loss with the cross-entropy in the head's epilogue (pw_fwd XENT
+    instance: d(logits) stored instead of the logits) vs the unfused head + softmax_xent:
+    same loss, top-1 hits and every parameter gradient; a second call scaled by 3 checks the
+    dloss scaling of the stored d(logits)."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3DSeg
+
+    torch.manual_seed(6)
+    N, S = 2, 24
+    m = FeatureNet3DSeg(input_size=S, num_classes=25).cuda().train()
+    x = (torch.rand(N, S, S, S, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    lab = torch.randint(0, 25, (N, S, S, S), device="cuda")
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("FN_SEG_XENT", flag)
+        m.zero_grad(set_to_none=True)
+        loss, hits = m.loss(x, lab, smoothing, with_correct=True)
+        (loss * 3.0).backward()
+        res.append((float(loss), int(hits.sum()), {k: p.grad.detach().float().clone() for k, p in m.named_parameters()
+                                                    if p.grad is not None}))
+    (l1, h1, g1), (l0, h0, g0) = res
+    assert l1 == pytest.approx(l0, rel=1e-4)
+    assert abs(h1 - h0) <= max(2, h0 // 1000)        # (identical logits up to bf16 ties)
+    for k in g0:
+        assert k in g1, k
+        r = _rel(g1[k], g0[k])
+        assert r < 2e-2, (k, r)
