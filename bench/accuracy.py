@@ -106,21 +106,26 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
         return unpack_voxels(xb, size).to(torch.bfloat16)
 
     cx = batch(ds.x_train, 0, calib)
-    q = quantize_model(model, cx)                          # fp8 stem (tap-expanded space-to-depth)
-    qs = quantize_model(model, cx, fp8_stem=False)         # bf16 stem + quantisation pass
+    q = quantize_model(model, cx)                          # the default stem (FN_F8_STEM)
+    qs = quantize_model(model, cx, fp8_stem=False)         # bf16 stem writing e4m3 from its epilogue
+    qi = quantize_model(model, cx, fp8_stem="i8")          # int8 stem (v_mfma_i32_16x16x64_i8)
     y = np.asarray(ds.y_test)
-    pb, pq, ps = [], [], []
+    pb, pq, ps, pi = [], [], [], []
     for i in range(0, len(y), chunk):
         xb = batch(ds.x_test, i, chunk)
         pb.append(model(xb).float().argmax(-1).cpu())
         pq.append(q(xb).float().argmax(-1).cpu())
         ps.append(qs(xb).float().argmax(-1).cpu())
-    pb, pq, ps = torch.cat(pb).numpy(), torch.cat(pq).numpy(), torch.cat(ps).numpy()
-    acc_b, acc_q, acc_s = float((pb == y).mean()), float((pq == y).mean()), float((ps == y).mean())
+        pi.append(qi(xb).float().argmax(-1).cpu())
+    pb, pq, ps, pi = (torch.cat(t).numpy() for t in (pb, pq, ps, pi))
+    acc_b, acc_q, acc_s, acc_i = (float((t == y).mean()) for t in (pb, pq, ps, pi))
     return {"top1_bf16": round(acc_b, 4), "top1_fp8": round(acc_q, 4), "drop_pt": round(100 * (acc_b - acc_q), 2),
             "agreement": round(float((pb == pq).mean()), 4), "calib_samples": calib,
+            "stem": q.stem and ("i8" if q.stem.int8 else "e4m3") or "bf16",
             "bf16_stem": {"top1_fp8": round(acc_s, 4), "drop_pt": round(100 * (acc_b - acc_s), 2),
                           "agreement": round(float((pb == ps).mean()), 4)},
+            "i8_stem": {"top1_fp8": round(acc_i, 4), "drop_pt": round(100 * (acc_b - acc_i), 2),
+                        "agreement": round(float((pb == pi).mean()), 4)},
             "kernel": ("conv_halo_f8" if os.environ.get("FN_F8_TILE", "1") == "0" else "conv_tile F8 variant")
                       + " (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3)"}
 

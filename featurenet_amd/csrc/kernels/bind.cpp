@@ -33,7 +33,7 @@ int fn_conv_halo_wgrad_yblocks(const int*, int);
 int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
                     int, int, hipStream_t);
 int fn_quant_fp8(const void*, void*, long long, float, hipStream_t);
-int fn_s2d_tap_f8(const void*, void*, int, int, int, int, int, int, int, int, float, hipStream_t);
+int fn_s2d_tap_f8(const void*, void*, int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, hipStream_t);
 int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
@@ -390,12 +390,12 @@ PYBIND11_MODULE(_C, m) {
         "conv_halo_f8");
   });
   m.def("s2d_tap_f8", [](uintptr_t x, uintptr_t y, std::vector<int> g, float inv_scale, uintptr_t st,
-                         std::vector<long long> ext) {
+                         std::vector<long long> ext, int i8) {
     // g = {N, D, H, W, D2, H2, W2o, J}; ext = {numel(x), numel(y)}
     need(g, 8, "s2d_tap_f8");
     fits(ext, 0, prod({g[0], g[1], g[2], g[3]}), "s2d_tap_f8", "x");
     fits(ext, 1, prod({g[0], g[4], g[5], g[6], 8LL * g[7]}), "s2d_tap_f8", "y");
-    chk(fn_s2d_tap_f8(P<const void*>(x), P<void*>(y), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], inv_scale, S(st)),
+    chk(fn_s2d_tap_f8(P<const void*>(x), P<void*>(y), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], inv_scale, i8, S(st)),
         "s2d_tap_f8");
   });
   m.def("quant_fp8", [](uintptr_t x, uintptr_t y, long long n, float inv_scale, uintptr_t st) {

@@ -311,10 +311,9 @@ extern "C" int fn_quant_fp8(const void* x, void* y, long long n, float inv_scale
 // ONE packed position (4 dword loads: two bf16 of each (pd, ph)) into LDS, then assembles
 // the 32 output bytes of its position from LDS slots w .. w+3 (the rows of 64 cover W2o + 3
 // <= 64 packed positions) -- every x element is loaded once, stores are 16 B.
-// Block = 4 packed rows (n, d, h) x 64 w: each thread quantises the 8 space-to-depth bytes of
-// ONE packed position (4 dword loads: two bf16 of each (pd, ph)) into LDS, then assembles
-// the 32 output bytes of its position from LDS slots w .. w+3 (the rows of 64 cover W2o + 3
-// <= 64 packed positions) -- every x element is loaded once, stores are 16 B.
+// I8: int8 bytes of rint(x * inv_scale) saturated to [-127, 127] instead of e4m3 (the int8 stem:
+// binary voxels are exact either way).
+template <bool I8>
 __global__ __launch_bounds__(256) void s2d_tap_f8_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ y,
                                                          int N, int D, int H, int W, int D2, int H2, int W2o, int J,
                                                          float inv_scale) {
@@ -344,8 +343,13 @@ __global__ __launch_bounds__(256) void s2d_tap_f8_kernel(const bf16* __restrict_
           if (xw < W) v0 = bf2f(xr[xw]);
           if (xw + 1 < W) v1 = bf2f(xr[xw + 1]);
         }
-        b[pd * 4 + ph * 2] = f32_to_fp8(v0 * inv_scale);
-        b[pd * 4 + ph * 2 + 1] = f32_to_fp8(v1 * inv_scale);
+        if constexpr (I8) {
+          b[pd * 4 + ph * 2] = (unsigned char)(signed char)(int)fminf(fmaxf(rintf(v0 * inv_scale), -127.f), 127.f);
+          b[pd * 4 + ph * 2 + 1] = (unsigned char)(signed char)(int)fminf(fmaxf(rintf(v1 * inv_scale), -127.f), 127.f);
+        } else {
+          b[pd * 4 + ph * 2] = f32_to_fp8(v0 * inv_scale);
+          b[pd * 4 + ph * 2 + 1] = f32_to_fp8(v1 * inv_scale);
+        }
       }
   }
   s8[rw][lane] = make_uint2((unsigned)b[0] | ((unsigned)b[1] << 8) | ((unsigned)b[2] << 16) | ((unsigned)b[3] << 24),
@@ -361,13 +365,17 @@ __global__ __launch_bounds__(256) void s2d_tap_f8_kernel(const bf16* __restrict_
 }
 
 extern "C" int fn_s2d_tap_f8(const void* x, void* y, int N, int D, int H, int W, int D2, int H2, int W2o, int J,
-                             float inv_scale, hipStream_t st) {
+                             float inv_scale, int i8, hipStream_t st) {
   if (N <= 0 || D <= 0 || H <= 0 || W <= 0 || D2 <= 0 || H2 <= 0 || W2o <= 0 || (J != 2 && J != 4)) return -2;
   if (2 * (D2 - 1) >= D || 2 * (H2 - 1) >= H || 2 * (W2o - 1) >= W) return -3;   // every position reads x
   if (W2o + J - 1 > 64) return -2;               // one 64-lane row of packed positions per (n, d, h)
   const long long rows = (long long)N * D2 * H2;
-  hipLaunchKernelGGL(s2d_tap_f8_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, (const bf16*)x,
-                     (unsigned char*)y, N, D, H, W, D2, H2, W2o, J, inv_scale);
+  if (i8)
+    hipLaunchKernelGGL(s2d_tap_f8_kernel<true>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, (const bf16*)x,
+                       (unsigned char*)y, N, D, H, W, D2, H2, W2o, J, inv_scale);
+  else
+    hipLaunchKernelGGL(s2d_tap_f8_kernel<false>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, (const bf16*)x,
+                       (unsigned char*)y, N, D, H, W, D2, H2, W2o, J, inv_scale);
   FN_CHECK_LAUNCH();
   return 0;
 }

@@ -54,7 +54,13 @@
 // allocation: the extra epilogue operands must not cost the other instances registers)
 // Q8O: the bf16 instance with an e4m3 output epilogue (fp8 inference: the bf16 stem writes the
 // fp8 layers' input; its own register allocation, like BWS)
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false, bool Q8O = false>
+// I8 (with F8: the fp8 kernel's 32-byte fragments holding int8 instead): two
+//   v_mfma_i32_16x16x64_i8 per fragment pair (bytes 0-15 and 16-31 of every lane: A and B split
+//   the same way, so the k sum is complete), exact int32 accumulation, converted to float in
+//   the epilogue before the dequantisation -- the binary-voxel stem of the fp8 inference path
+//   (0/1 inputs are exact; per-channel int8 weights keep ~8 bits, where e4m3 kept 4).
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false, bool Q8O = false,
+          bool I8 = false>
 __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
@@ -307,7 +313,16 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
           for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-              if constexpr (F8)   // e4m3 x e4m3 (formats 0, 0), E8M0 scales 127 = 1.0
+              if constexpr (F8 && I8) {   // int8 x int8 -> int32 (the accumulator's bits)
+                typedef int ct_i32x4 __attribute__((ext_vector_type(4)));
+                const ct_i32x8 b8 = fb[u][nt], a8 = fa[mt];
+                ct_i32x4 c = __builtin_bit_cast(ct_i32x4, acc[mt][nt]);
+                c = __builtin_amdgcn_mfma_i32_16x16x64_i8((ct_i32x4){b8[0], b8[1], b8[2], b8[3]},
+                                                         (ct_i32x4){a8[0], a8[1], a8[2], a8[3]}, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_i32_16x16x64_i8((ct_i32x4){b8[4], b8[5], b8[6], b8[7]},
+                                                         (ct_i32x4){a8[4], a8[5], a8[6], a8[7]}, c, 0, 0, 0);
+                acc[mt][nt] = __builtin_bit_cast(f32x4, c);
+              } else if constexpr (F8)   // e4m3 x e4m3 (formats 0, 0), E8M0 scales 127 = 1.0
                 acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[u][nt], fa[mt], acc[mt][nt], 0, 0,
                                                                                  0, 127, 0, 127);
               else
@@ -497,7 +512,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              v[j] = acc[mt][j >> 2][j & 3] * sc8[j] + bs8[j];
+              const float a = I8 ? (float)__builtin_bit_cast(int, acc[mt][j >> 2][j & 3]) : acc[mt][j >> 2][j & 3];
+              v[j] = a * sc8[j] + bs8[j];
               if constexpr ((M & 2) != 0)        // (already x oscale) relu / saturate in one med3
                 v[j] = __builtin_amdgcn_fmed3f(v[j], (M & 1) != 0 ? 0.f : -448.f, 448.f);
               else if constexpr ((M & 1) != 0 || POOL)
@@ -712,19 +728,20 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false, bool Q8O = false>
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false, bool Q8O = false,
+          bool I8 = false>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
                        float oscale = 0.f, const void* bny = nullptr, const float* bnp = nullptr) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS, Q8O>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS, Q8O, I8>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS, Q8O>), grid, dim3(CT_NTHR), lds, st,
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS, Q8O, I8>), grid, dim3(CT_NTHR), lds, st,
                      (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
                      stamps, scale, oscale, (const bf16*)bny, bnp);
   return 0;
@@ -864,8 +881,11 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   const int CPP = g.CS / 16;
   if (!fn_conv_tile_f8_supported(MT, NT, CPP) || !scale || !(oscale >= 0.f)) return -2;
   // relu: bit 0 relu, bit 1 the fused 2^3 max-pool (relu, bf16 output [N][OD/2][OH/2][OW/2][Ncol];
-  // even tile dims so every window lies in one tile, the pool row table, MT = 8)
+  // even tile dims so every window lies in one tile, the pool row table, MT = 8), bit 2 int8
+  // operands (src / wp hold int8, scale dequantises the int32 sums; 32-channel slices, no pool)
   const bool pool = (relu & 2) != 0;
+  const bool i8 = (relu & 4) != 0;
+  if (i8 && (pool || CPP != 2 || MT != 8 || NT != 2)) return -2;
   if (pool && (MT != 8 || oscale != 0.f || (g.TD | g.TH | g.TW | g.OD | g.OH | g.OW) & 1)) return -2;
   const int f8act = ((relu & 1) || pool ? ACT_RELU : ACT_NONE) | (pool ? CT_F8_POOL : 0);
   if (g.C % g.CS || g.TD * g.TH * g.TW > 64 * MT || g.TD < 1 || g.TH < 1 || g.TW < 1) return -3;
@@ -921,9 +941,13 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   }
 #define CT_F8_CASE(M, N, C)                                                                                        \
   if (MT == M && NT == N && CPP == C)                                                                              \
-    rc = launch_tile<M, N, C, 0, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, \
-                                       zp, bias, out, nullptr, g, Ncol, f8act, sched, nullptr,                     \
-                                       scale, oscale);
+    rc = i8 ? launch_tile<M, N, C, 0, true, false, false, C == 2>(grid, lds, st, src, (const uint4*)wp,              \
+                                                                  (const int2*)rowtab, (const int4*)ktab, zp, bias, \
+                                                                  out, nullptr, g, Ncol, f8act, sched, nullptr,    \
+                                                                  scale, oscale)                                   \
+            : launch_tile<M, N, C, 0, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,              \
+                                            (const int4*)ktab, zp, bias, out, nullptr, g, Ncol, f8act, sched,      \
+                                            nullptr, scale, oscale);
   CT_F8_INSTANCES(CT_F8_CASE)
 #undef CT_F8_CASE
   if (rc) return rc;

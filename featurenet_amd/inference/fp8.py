@@ -31,6 +31,7 @@ from ..ops.conv import halo_plan, halo_tap_offsets
 from ..ops.spec import ConvSpec, PoolSpec
 
 FP8_MAX = 448.0
+I8_MAX = 127.0
 
 
 def _fold_bn(conv) -> tuple[torch.Tensor, torch.Tensor]:
@@ -54,18 +55,26 @@ class Fp8Conv:
     kernel."""
 
     def __init__(self, conv, in_scale: float, out_scale: float | None, relu: bool = True, wb=None,
-                 padding: str | None = None):
+                 padding: str | None = None, int8: bool = False):
         # conv: the bf16 layer (BN folded here), or None with wb = (folded weight, bias)
+        # int8: int8 operands (per-channel weights amax / 127; the input quantised with in_scale
+        # the same way) on the tile kernel's int8 MFMA instance -- the binary-voxel stem
         w, b = _fold_bn(conv) if wb is None else wb
         K, KD, KH, KW, Cin = w.shape
-        sw = w.abs().reshape(K, -1).amax(1).clamp_min(1e-12) / FP8_MAX
-        wq = _to_fp8(w / sw.view(-1, 1, 1, 1, 1))
-        # fp8 weights in the halo kernel's k order ([K][C/16][T8][16] bytes)
         T = KD * KH * KW
-        T8 = (T + 7) // 8 * 8
-        lay = torch.zeros(K, Cin // 16, T8, 16, dtype=torch.float8_e4m3fn, device=w.device)
-        lay[:, :, :T] = wq.reshape(K, T, Cin // 16, 16).permute(0, 2, 1, 3)
-        self.wq = lay.reshape(K, -1).view(torch.uint8).contiguous()
+        self.int8 = bool(int8)
+        if self.int8:
+            sw = w.abs().reshape(K, -1).amax(1).clamp_min(1e-12) / I8_MAX
+            wq = torch.round(w / sw.view(-1, 1, 1, 1, 1)).clamp(-I8_MAX, I8_MAX).to(torch.int8)
+            self.wq = None                                   # (tile kernel only)
+        else:
+            sw = w.abs().reshape(K, -1).amax(1).clamp_min(1e-12) / FP8_MAX
+            wq = _to_fp8(w / sw.view(-1, 1, 1, 1, 1))
+            # fp8 weights in the halo kernel's k order ([K][C/16][T8][16] bytes)
+            T8 = (T + 7) // 8 * 8
+            lay = torch.zeros(K, Cin // 16, T8, 16, dtype=torch.float8_e4m3fn, device=w.device)
+            lay[:, :, :T] = wq.reshape(K, T, Cin // 16, 16).permute(0, 2, 1, 3)
+            self.wq = lay.reshape(K, -1).view(torch.uint8).contiguous()
         self.wq_ktc = wq.reshape(K, T, Cin).view(torch.uint8).contiguous()   # [K][T][C] for the tile packing
         self._tile = {}
         self.scale = (in_scale * sw).float().contiguous()
@@ -98,8 +107,11 @@ class Fp8Conv:
             wpk = self._tile.get(tp)
             if wpk is None:
                 wpk = self._tile[tp] = conv_tile.pack_weights_f8(self.wq_ktc, tp)
-            y = conv_tile.conv_fwd_f8(xq, wpk, self.scale, self.bias, spec, tp, self.relu, self.out_scale)
+            y = conv_tile.conv_fwd_f8(xq, wpk, self.scale, self.bias, spec, tp, self.relu, self.out_scale,
+                                      i8=self.int8)
             return y, tuple(y.shape)
+        if self.int8:
+            raise RuntimeError(f"no int8 tile plan for {spec}")
         # fp8 halo = 16 B/position; halo_plan counts 32 B/position (bf16): <= 64 KiB of fp8 halo
         plan = halo_plan(spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW, 128 * 1024, wsplit=False)
         if plan is None:
@@ -156,13 +168,13 @@ def stem_tap_weight(w: torch.Tensor) -> torch.Tensor:
     return w2.reshape(K, 4, 4, 1, 32).contiguous()
 
 
-def stem_tap_input(x5: torch.Tensor, spec: ConvSpec, in_scale: float) -> torch.Tensor:
-    """e4m3 [N, D2, H2, OW, 32] tap-expanded space-to-depth input of the stem (one launch)."""
+def stem_tap_input(x5: torch.Tensor, spec: ConvSpec, in_scale: float, int8: bool = False) -> torch.Tensor:
+    """e4m3 (or int8) [N, D2, H2, OW, 32] tap-expanded space-to-depth input of the stem (one launch)."""
     N, D, H, W, _ = x5.shape
     x5 = x5.to(torch.bfloat16).contiguous()
     y = torch.empty(spec.N, spec.D, spec.H, spec.W, 32, dtype=torch.uint8, device=x5.device)
     _native.kernels().s2d_tap_f8(x5.data_ptr(), y.data_ptr(), [N, D, H, W, spec.D, spec.H, spec.W, 4], 1.0 / in_scale,
-                                 _native.stream(x5), [x5.numel(), y.numel()])
+                                 _native.stream(x5), [x5.numel(), y.numel()], int(int8))
     return y
 
 
@@ -171,7 +183,8 @@ class Fp8FeatureNet3D:
     With a calibrated input scale, the stem runs in fp8 too (tap-expanded space-to-depth,
     :func:`stem_tap_plan`) and writes e4m3 straight into conv2's input."""
 
-    def __init__(self, model: FeatureNet3D, act_scales: list[float], in_scale: float | None = None):
+    def __init__(self, model: FeatureNet3D, act_scales: list[float], in_scale: float | None = None,
+                 stem_int8: bool = False):
         self.model = model.eval()
         convs = list(model.convs)
         c1 = convs[0]
@@ -181,9 +194,10 @@ class Fp8FeatureNet3D:
         self.in_scale = in_scale
         self._stem_w2 = {}
         self.stem = None
+        self.stem_int8 = bool(stem_int8)
         if in_scale is not None:
             self.stem = Fp8Conv(None, in_scale, act_scales[0], relu=True, wb=(stem_tap_weight(w1), b1),
-                                padding="valid")
+                                padding="valid", int8=self.stem_int8)
         self.layers = []
         for i, conv in enumerate(convs[1:], start=1):
             last = i == len(convs) - 1
@@ -198,7 +212,7 @@ class Fp8FeatureNet3D:
         c1 = m.convs[0]
         tspec = stem_tap_plan(c1, tuple(x.shape)) if self.stem is not None else None
         if tspec is not None and self.stem.tile_plan(tspec) is not None:
-            xq, shape = self.stem(stem_tap_input(x, tspec, self.in_scale),              # fp8 in, fp8 out
+            xq, shape = self.stem(stem_tap_input(x, tspec, self.in_scale, self.stem_int8),   # fp8 / int8 in, fp8 out
                                   (tspec.N, tspec.D, tspec.H, tspec.W, tspec.C))
         else:
             x = x.to(torch.bfloat16).contiguous()
@@ -268,18 +282,29 @@ def calibrate(model: FeatureNet3D, calib_x: torch.Tensor, margin: float = 1.0) -
     return scales
 
 
-def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem: bool | None = None) -> Fp8FeatureNet3D:
+def stem_mode() -> str:
+    """FN_F8_STEM: '0' the bf16 stem writing e4m3 from its epilogue, '1' / 'e4m3' the stem on the
+    fp8 kernel with per-channel e4m3 weights, 'i8' the stem on the int8 MFMA instance."""
+    m = os.environ.get("FN_F8_STEM", "0")
+    return {"1": "e4m3", "e4m3": "e4m3", "i8": "i8", "int8": "i8"}.get(m, "bf16")
+
+
+def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem=None) -> Fp8FeatureNet3D:
     """fp8 model with activation scales from a bf16 pass over ``calib_x``.
 
-    ``fp8_stem`` (FN_F8_STEM=1; off by default): the input is quantised too (scale amax / 448 of the
-    calibration input: binary voxels map exactly) and the stem runs on the fp8 kernel.  Off
-    by default: per-channel e4m3 stem weights cost a trained model ~16 points of top-1 on the
-    held-out set (the stem output error 6 % vs 3 %), so the stem stays bf16 and writes e4m3
-    from its epilogue (the same speed: no bf16 output, no quantisation pass)."""
+    ``fp8_stem`` (default :func:`stem_mode`): 'bf16' keeps the stem on the bf16 tile kernel,
+    writing e4m3 from its epilogue; 'e4m3' (or True) quantises the input too (scale amax / 448
+    of the calibration input: binary voxels map exactly) and runs the stem on the fp8 kernel --
+    per-channel e4m3 stem weights cost a trained model ~16 points of top-1 on the held-out set
+    (the stem output error 6 % vs 3 %); 'i8' runs it on the int8 MFMA (v_mfma_i32_16x16x64_i8,
+    2x the bf16 rate): binary inputs are exact in int8 and per-channel int8 weights keep ~8
+    bits of each weight, the precision the e4m3 stem lacked."""
     if fp8_stem is None:
-        fp8_stem = os.environ.get("FN_F8_STEM", "0") == "1"
-    in_scale = max(float(calib_x.float().abs().amax()), 1e-6) / FP8_MAX if fp8_stem else None
-    return Fp8FeatureNet3D(model, calibrate(model, calib_x), in_scale)
+        fp8_stem = stem_mode()
+    mode = {True: "e4m3", False: "bf16"}.get(fp8_stem, fp8_stem)
+    amax = max(float(calib_x.float().abs().amax()), 1e-6)
+    in_scale = {"e4m3": amax / FP8_MAX, "i8": amax / I8_MAX}.get(mode)
+    return Fp8FeatureNet3D(model, calibrate(model, calib_x), in_scale, stem_int8=mode == "i8")
 
 
 _ = math

@@ -525,9 +525,10 @@ def pack_weights_f8(wq: torch.Tensor, p: TilePlan) -> torch.Tensor:
 
 
 def conv_fwd_f8(xq5: torch.Tensor, wpk: torch.Tensor, scale: torch.Tensor, bias: torch.Tensor, spec, p: TilePlan,
-                relu: bool, out_scale: float | None) -> torch.Tensor:
+                relu: bool, out_scale: float | None, i8: bool = False) -> torch.Tensor:
     """y = act(conv(x, w) * scale + bias) of e4m3 activations (uint8 [N, D, H, W, C]) on the fp8
-    tile kernel: bf16 output, or e4m3 of y / out_scale when ``out_scale`` is given.  A ``pool``
+    tile kernel: bf16 output, or e4m3 of y / out_scale when ``out_scale`` is given.  ``i8``: the
+    operands are int8 instead (x, wpk hold int8 bytes; the int8 MFMA instance).  A ``pool``
     plan returns maxpool2^3(relu(...)) instead: bf16 [N, OD/2, OH/2, OW/2, K]."""
     kd = (spec.KD, spec.KH, spec.KW)
     geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
@@ -543,7 +544,8 @@ def conv_fwd_f8(xq5: torch.Tensor, wpk: torch.Tensor, scale: torch.Tensor, bias:
     kt = ktab_tensor(p, kd, xq5.device)
     _native.kernels().conv_tile_f8(xq5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                    zero_page(xq5.device).data_ptr(), scale.data_ptr(), _native.ptr(bias), y.data_ptr(),
-                                   1.0 / out_scale if out_scale else 0.0, geom, spec.K, int(relu) | (2 if p.pool else 0),
+                                   1.0 / out_scale if out_scale else 0.0, geom, spec.K,
+                                   int(relu) | (2 if p.pool else 0) | (4 if i8 else 0),
                                    p.MT, p.NT, st,
                                    sched(xq5.device, st).data_ptr(),
                                    [xq5.numel(), wpk.numel(), y.numel(), rt.numel() // 2, kt.numel() // 4])

@@ -134,3 +134,42 @@ def test_bf16_stem_e4m3_epilogue_matches_quant_pass(monkeypatch):
     assert a is not None and a.shape == b.shape and a.dtype == torch.uint8
     same = (a == b).float().mean().item()
     assert same > 0.999, same
+
+
+def test_int8_tile_kernel_exact():
+    """The int8 instance of the fp8 tile kernel (two v_mfma_i32_16x16x64_i8 per fragment pair)
+    against an exact integer conv: int8 x, int8 w, int32 sums, then scale + bias + relu."""
+    from featurenet_amd.ops import conv_tile as ct
+    from featurenet_amd.ops.spec import ConvSpec
+
+    torch.manual_seed(7)
+    N, S, C, K = 2, 12, 32, 32
+    xi = torch.randint(-20, 21, (N, S, S, S, C), device="cuda", dtype=torch.int8)
+    wi = torch.randint(-127, 128, (K, 4, 4, 1, C), device="cuda", dtype=torch.int8)
+    spec = ConvSpec.make((N, S, S, S, C), K, (4, 4, 1), 1, "valid")
+    p = ct.plan(N, (spec.OD, spec.OH, spec.OW), (4, 4, 1), C, K, f8=True)
+    assert p is not None
+    scale = torch.rand(K, device="cuda") * 1e-3 + 1e-4
+    bias = torch.randn(K, device="cuda") * 0.1
+    wpk = ct.pack_weights_f8(wi.view(torch.uint8).reshape(K, 16, C), p)
+    y = ct.conv_fwd_f8(xi.view(torch.uint8), wpk, scale, bias, spec, p, True, None, i8=True)
+    acc = torch.nn.functional.conv3d(xi.double().permute(0, 4, 1, 2, 3), wi.double().permute(0, 4, 1, 2, 3))
+    ref = torch.relu(acc.permute(0, 2, 3, 4, 1) * scale.double() + bias.double())
+    torch.testing.assert_close(y.double(), ref, rtol=8e-3, atol=1e-3)   # (bf16 output rounding)
+
+
+def test_int8_stem_model_matches_bf16_model():
+    """The fp8 model with the int8 stem (FN_F8_STEM=i8): closer to the bf16 model than the e4m3
+    stem, as close as the bf16 stem."""
+    torch.manual_seed(0)
+    m = FeatureNet3D(FeatureNet3DConfig(input_size=64, num_classes=24)).cuda().eval()
+    x = (torch.rand(8, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    qi = F8.quantize_model(m, x[:4], fp8_stem="i8")
+    qb = F8.quantize_model(m, x[:4], fp8_stem="bf16")
+    assert qi.stem is not None and qi.stem.int8
+    with torch.no_grad():
+        ref = m(x).float()
+        a = qi(x).float()
+        b = qb(x).float()
+    cos = lambda u, v: torch.nn.functional.cosine_similarity(u.flatten(), v.flatten(), dim=0).item()  # noqa: E731
+    assert cos(a, b) > 0.995 and cos(a, ref) >= cos(b, ref) - 0.01, (cos(a, b), cos(a, ref), cos(b, ref))
