@@ -1,0 +1,344 @@
+// Segmentation classifier head + per-voxel softmax cross-entropy + the head's whole backward in ONE
+// streaming pass (FeatureNet3DSeg training, ops/subpixel.py SubpixelDecoderHeadLossFn).
+//
+// The 1x1x1 head maps the decoder output z = act(bn(y)) [M][32] to per-voxel logits [M][NC] and
+// the loss is their mean cross-entropy.  Unfused, a training step writes the logits (1.7 GB at
+// 128 x 64^3), the loss kernel reads them and writes d(logits), and the backward reads
+// d(logits) three more times: head weight gradient (with z), bias gradient, head dgrad (with y,
+// plus the decoder BN's backward moments).  Everything the backward needs from d(logits) is
+// linear in it and local to a voxel row, so this kernel computes it while the tile is in LDS:
+//
+//   per 256-row tile:  y (raw, for the BN moments) and z = act(y*sc + sh) into LDS
+//                      logits = z W^T + b            (MFMA 16x16x32, W^T fragments in registers)
+//                      one row per thread: log-sum-exp loss, top-1 hit,
+//                      d = (softmax - target) * xscale  (bf16, the unfused kernel's values)
+//                      dW^T += z^T d, db += 1^T d    (MFMA; both operands ds_read_b64_tr_b16)
+//                      dz = d W                      (MFMA; W fragments in registers)
+//                      BN moments: g = dz * act'(y*sc + sh), sum g, sum g * y per channel
+//                      dz -> HBM (16-B stores through LDS)
+//
+// HBM traffic: y and the labels in, dz out -- the logits and d(logits) never exist.  Partials are
+// per workgroup (fixed-order reductions: deterministic); the host sums them.
+//
+// Reference parity: the softmax head + categorical cross-entropy (reference
+// model/keras_model.py:124, tensorflow_generator.py:232-235), Keras Conv (1,1) head
+// (model/input.py:294).
+#include "common.h"
+
+#define SH_BM 256
+#define SH_NTHR 256
+#define SH_K 32                                  // decoder channels (the head's input)
+#define SH_LD 40                                 // LDS row stride (bf16): 80 B
+
+typedef short sh_s4 __attribute__((ext_vector_type(4)));
+typedef short sh_s8 __attribute__((ext_vector_type(8)));
+
+// 8 consecutive rows of one column (rows lo..lo+3 and hi..hi+3 of the lane's 16-lane group) as
+// an MFMA operand fragment: lane 4q+p of the group addresses row q, columns 4p..4p+3
+__device__ __forceinline__ bf16x8 sh_tr8(const bf16* lo, const bf16* hi) {
+  sh_s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sh_s4*)(lo));
+  sh_s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sh_s4*)(hi));
+  sh_s8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ sh_s4 sh_tr4(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) sh_s4*)(p));
+}
+
+__device__ __forceinline__ float sh_bf(short s) { return __uint_as_float(((unsigned)(unsigned short)s) << 16); }
+__device__ __forceinline__ float bf16_round(float x) { return bf2f(f2bf(x)); }
+
+// ACT: the decoder BN's activation (ACT_NONE / ACT_RELU).
+// y [M][32] bf16; sc / sh [32]; w [NC][32] bf16; bias [NC] fp32 or null; labels int64 [M];
+// dz [M][32] bf16 out; part: per workgroup [loss, hits | db[32] | dWt[32][32] | msum[32] | msq[32]]
+// (fp32; dWt[ch][cls] = sum z[r][ch] d[r][cls]).
+template <int ACT>
+__global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __restrict__ y,
+                                                                 const float* __restrict__ sc,
+                                                                 const float* __restrict__ shf,
+                                                                 const bf16* __restrict__ w,
+                                                                 const float* __restrict__ bias,
+                                                                 const long long* __restrict__ labels,
+                                                                 bf16* __restrict__ dz, float* __restrict__ part,
+                                                                 long long M, int NC, float xscale, float smoothing) {
+  __shared__ __attribute__((aligned(16))) bf16 Ys[SH_BM * SH_LD];   // raw y
+  __shared__ __attribute__((aligned(16))) bf16 Zs[SH_BM * SH_LD];   // z = act(y*sc + sh)
+  __shared__ __attribute__((aligned(16))) bf16 Os[SH_BM * SH_LD];   // logits -> d -> dz staging
+  constexpr int PW = 2 + 32 + 32 * 32 + 64;      // partial floats per wave / workgroup
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int q = (lane & 15) >> 2, pp = lane & 3;                    // tr_b16 address roles
+  const int ntiles = (int)((M + SH_BM - 1) / SH_BM);
+
+  // head weights as MFMA fragments: logits B[k = ch][n = cls] = w[cls][ch] (8 consecutive ch of
+  // row cls: 16-B loads), dz B[k = cls][n = ch] = w[cls][ch] (a column gather, once)
+  bf16x8 wl[2], wd[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int cls = 16 * nb + lr;
+    Pack8 p, r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      p.e[j] = cls < NC ? w[cls * SH_K + 8 * lg + j] : f2bf(0.f);
+      const int c2 = 8 * lg + j;                                     // class of the dz B fragment
+      r.e[j] = c2 < NC ? w[c2 * SH_K + 16 * nb + lr] : f2bf(0.f);
+    }
+    wl[nb] = __builtin_bit_cast(bf16x8, p.u);
+    wd[nb] = __builtin_bit_cast(bf16x8, r.u);
+  }
+  float bl[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) bl[nb] = (bias && 16 * nb + lr < NC) ? bias[16 * nb + lr] : 0.f;
+  // this thread's input chunks always start at channel 8 (tid mod 4): 8 (scale, shift) pairs
+  float psc[8], psh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    psc[j] = sc[8 * (tid & 3) + j];
+    psh[j] = shf[8 * (tid & 3) + j];
+  }
+  // the moments' columns: 16 nb + lr
+  float msc[2], msh[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    msc[nb] = sc[16 * nb + lr];
+    msh[nb] = shf[16 * nb + lr];
+  }
+  Pack8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones.e[j] = f2bf(1.f);
+  const bf16x8 fone = __builtin_bit_cast(bf16x8, ones.u);
+
+  f32x4 adw[2][2], adb[2];                       // dW^T [ch block][cls block], db [cls block]
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    adb[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) adw[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  float ms[2] = {0.f, 0.f}, mq[2] = {0.f, 0.f};   // BN moments of columns 16 nb + lr
+  float xl = 0.f, xc = 0.f;                       // loss, hits (row threads)
+
+  uint4 rb[4];
+  auto load = [&](int t) {                       // tile t: 256 x 32 contiguous bf16 = 1024 chunks
+    const long long e0 = (long long)t * SH_BM * SH_K;
+    const long long nel = (M - (long long)t * SH_BM < SH_BM ? M - (long long)t * SH_BM : SH_BM) * SH_K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = i * SH_NTHR + tid;
+      rb[i] = *(const uint4*)(y + e0 + (c * 8 < nel ? c * 8 : 0));
+    }
+  };
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (; t < ntiles; t += gridDim.x) {
+    const int rows = (int)(M - (long long)t * SH_BM < SH_BM ? M - (long long)t * SH_BM : SH_BM);
+    __syncthreads();                             // the previous tile's LDS readers are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = i * SH_NTHR + tid, r = c >> 2, k = (c & 3) * 8;
+      Pack8 raw, zz;
+      raw.u = rb[i];
+      if (r >= rows) raw.u = make_uint4(0u, 0u, 0u, 0u);   // (partial tile: zero rows)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) zz.e[j] = f2bf(act_fwd(bf2f(raw.e[j]) * psc[j] + psh[j], ACT));
+      if (r >= rows) zz.u = make_uint4(0u, 0u, 0u, 0u);
+      *(uint4*)(Ys + r * SH_LD + k) = raw.u;
+      *(uint4*)(Zs + r * SH_LD + k) = zz.u;
+    }
+    __syncthreads();
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);   // next tile in flight
+    // ---- logits = z W^T + b: wave rows 64 wave + 16 mt ----
+    {
+      f32x4 acc[4][2];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8 fa = *(const bf16x8*)(Zs + (64 * wave + 16 * mt + lr) * SH_LD + 8 * lg);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mt][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, wl[nb], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            Os[(64 * wave + 16 * mt + 4 * lg + i) * SH_LD + 16 * nb + lr] = f2bf(acc[mt][nb][i] + bl[nb]);
+    }
+    __syncthreads();
+    // ---- softmax cross-entropy, one row per thread: d (bf16) replaces the logits ----
+    {
+      bf16* orow = Os + tid * SH_LD;
+      if (tid < rows) {
+        const long long yl = labels[(long long)t * SH_BM + tid];
+        const float off = smoothing / (float)NC, on = 1.f - smoothing + off;
+        float v[32];
+        float mx = -INFINITY;
+        int am = 0;
+#pragma unroll
+        for (int c = 0; c < 32; ++c) {
+          v[c] = c < NC ? bf2f(orow[c]) : -INFINITY;
+          if (v[c] > mx) { mx = v[c]; am = c; }
+        }
+        float se = 0.f;
+#pragma unroll
+        for (int c = 0; c < 32; ++c) se += c < NC ? __expf(v[c] - mx) : 0.f;
+        const float lse = mx + __logf(se);
+        float lrow = 0.f;
+#pragma unroll
+        for (int c = 0; c < 32; ++c) {
+          float d = 0.f;
+          if (c < NC) {
+            const float lp = v[c] - lse;
+            const float tgt = (c == yl) ? on : off;
+            lrow -= tgt * lp;
+            d = (__expf(lp) - tgt) * xscale;
+          }
+          orow[c] = f2bf(d);                     // (padded classes: 0)
+        }
+        xl += lrow;
+        xc += (am == yl) ? 1.f : 0.f;
+      } else {
+#pragma unroll
+        for (int c = 0; c < 32; ++c) orow[c] = f2bf(0.f);
+      }
+    }
+    __syncthreads();
+    // ---- dW^T += z^T d and db += 1^T d over the wave's 64 rows (2 k-steps of 32 rows) ----
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r0 = 64 * wave + 32 * ks + 8 * lg;      // this lane group's 8 rows
+      bf16x8 fz[2], fd[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        fz[b] = sh_tr8(Zs + (r0 + q) * SH_LD + 16 * b + 4 * pp, Zs + (r0 + 4 + q) * SH_LD + 16 * b + 4 * pp);
+        fd[b] = sh_tr8(Os + (r0 + q) * SH_LD + 16 * b + 4 * pp, Os + (r0 + 4 + q) * SH_LD + 16 * b + 4 * pp);
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          adw[cb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fz[cb], fd[nb], adw[cb][nb], 0, 0, 0);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) adb[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fone, fd[nb], adb[nb], 0, 0, 0);
+    }
+    // ---- dz = d W (rows 64 wave + 16 mt), the BN moments from y ----
+    f32x4 dzc[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const bf16x8 fa = *(const bf16x8*)(Os + (64 * wave + 16 * mt + lr) * SH_LD + 8 * lg);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        dzc[mt][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, wd[nb], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int rb0 = 64 * wave + 16 * mt + 4 * lg;   // the C fragment's 4 rows
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const sh_s4 yv = sh_tr4(Ys + (rb0 + q) * SH_LD + 16 * nb + 4 * pp);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float g0 = bf16_round(dzc[mt][nb][i]);   // the stored dz
+          const float yy = sh_bf(yv[i]);
+          const float g = act_bwd_from_out(act_fwd(yy * msc[nb] + msh[nb], ACT), ACT) * g0;
+          ms[nb] += g;
+          mq[nb] += g * yy;
+        }
+      }
+    }
+    __syncthreads();                             // every wave is done with d (Os) of this tile
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          Os[(64 * wave + 16 * mt + 4 * lg + i) * SH_LD + 16 * nb + lr] = f2bf(dzc[mt][nb][i]);
+    __syncthreads();
+    // dz rows -> HBM: 256 x 32 contiguous bf16, 16-B chunks
+    {
+      bf16* dst = dz + (long long)t * SH_BM * SH_K;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = i * SH_NTHR + tid, r = c >> 2, k = (c & 3) * 8;
+        if (r < rows) *(uint4*)(dst + c * 8) = *(const uint4*)(Os + r * SH_LD + k);
+      }
+    }
+  }
+  // ---- workgroup partials (fixed order) ----
+  // moments: lanes lr, lr+16, lr+32, lr+48 hold column 16 nb + lr
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    ms[nb] += __shfl_xor(ms[nb], 16, 64);
+    ms[nb] += __shfl_xor(ms[nb], 32, 64);
+    mq[nb] += __shfl_xor(mq[nb], 16, 64);
+    mq[nb] += __shfl_xor(mq[nb], 32, 64);
+  }
+  xl = wave_sum(xl);
+  xc = wave_sum(xc);
+  __syncthreads();                               // (Ys / Zs are free: the per-wave partials go there)
+  float* red = reinterpret_cast<float*>(Ys);     // [4][PW] floats = 18 KB of the 40 KB of Ys + Zs
+  float* rw = red + wave * PW;
+  if (lane == 0) {
+    rw[0] = xl;
+    rw[1] = xc;
+  }
+  // db: every row of the C fragment holds the column sums; lanes of group 0 row 0
+  if (lg == 0) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) rw[2 + 16 * nb + lr] = adb[nb][0];
+  }
+  // dW^T [ch][cls]: C row = ch = 16 cb + 4 lg + i, column = cls = 16 nb + lr
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rw[34 + (16 * cb + 4 * lg + i) * 32 + 16 * nb + lr] = adw[cb][nb][i];
+  if (lg == 0) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      rw[34 + 1024 + 16 * nb + lr] = ms[nb];
+      rw[34 + 1024 + 32 + 16 * nb + lr] = mq[nb];
+    }
+  }
+  __syncthreads();
+  float* out = part + (long long)blockIdx.x * PW;
+  for (int i = tid; i < PW; i += SH_NTHR) out[i] = (red[i] + red[PW + i]) + (red[2 * PW + i] + red[3 * PW + i]);
+}
+
+extern "C" int fn_seghead_part_len() { return 2 + 32 + 32 * 32 + 64; }
+
+extern "C" int fn_seghead_blocks(long long M) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const long long tiles = (M + SH_BM - 1) / SH_BM;
+  const long long g = 2LL * cus;                 // (~60 KB of LDS: 2 workgroups per CU)
+  return (int)(tiles < g ? (tiles > 0 ? tiles : 1) : g);
+}
+
+// y [M][32] bf16 (M % 8 == 0), sc / sh [32], w [NC][32] bf16 (NC <= 32), bias [NC] or null,
+// labels int64 [M], dz [M][32] bf16, part fp32 [fn_seghead_blocks(M)][fn_seghead_part_len()]
+extern "C" int fn_seghead_loss(const void* y, const float* sc, const float* sh, const void* w, const float* bias,
+                               const long long* labels, void* dz, float* part, long long M, int K, int NC, int act,
+                               float xscale, float smoothing, hipStream_t st) {
+  if (K != SH_K || NC < 2 || NC > 32 || M < 8 || M % 8 || !sc || !sh || !labels || !part) return -2;
+  const dim3 grid((unsigned)fn_seghead_blocks(M));
+  if (act == ACT_RELU)
+    hipLaunchKernelGGL(seghead_loss_kernel<ACT_RELU>, grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,
+                       (const bf16*)w, bias, labels, (bf16*)dz, part, M, NC, xscale, smoothing);
+  else if (act == ACT_NONE)
+    hipLaunchKernelGGL(seghead_loss_kernel<ACT_NONE>, grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,
+                       (const bf16*)w, bias, labels, (bf16*)dz, part, M, NC, xscale, smoothing);
+  else
+    return -2;
+  FN_CHECK_LAUNCH();
+  return 0;
+}

@@ -37,10 +37,12 @@ MT_CHOICES_32 = (8, 10)     # conv_tile32: MB = MT / 2 blocks of 32 rows per wav
 
 
 def m32_enabled() -> bool:
-    """FN_TILE_M32: '1' (default) plans bf16 convs with whole 32-column blocks on the
-    v_mfma_f32_32x32x16_bf16 kernel (conv_tile32.hip), '0' keeps every plan on the
-    16x16x32 kernel."""
-    return os.environ.get("FN_TILE_M32", "1") != "0"
+    """FN_TILE_M32: '1' plans bf16 convs with whole 32-column blocks on the
+    v_mfma_f32_32x32x16_bf16 kernel (conv_tile32.hip); '0' (default) keeps every plan on the
+    16x16x32 kernel.  Round 4 measured the 32x32x16 k-loop 2-8 % slower on the FeatureNet-3D
+    layers (conv2 fwd 539 vs 513 us, dgrad 707 vs 669; the step 5.13 vs 4.97 ms on one box,
+    profiles/r4_m32_ab.md), the exception being conv3's dgrad with 640-row tiles."""
+    return os.environ.get("FN_TILE_M32", "0") == "1"
 
 
 def red_bytes(NT: int) -> int:

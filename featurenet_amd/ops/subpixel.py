@@ -354,6 +354,76 @@ class SubpixelDecoderHeadXentFn(torch.autograd.Function):
         return g + (None, None)
 
 
+class SubpixelDecoderHeadLossFn(torch.autograd.Function):
+    """(mean softmax cross-entropy, top-1 hits) of FeatureNet3DSeg's decoder + head with the
+    head's ENTIRE backward done in the forward pass (``csrc/kernels/seghead.hip``): one
+    streaming kernel computes logits, loss, d(logits), the head weight / bias gradient partials,
+    dz = d(logits) W and the decoder BN's backward moments while each 256-voxel tile is in LDS,
+    and writes only dz.  The backward sums the partials, scales by dloss (a near-empty launch
+    when it is 1) and continues with the BN backward and the decoder.  K = 32 decoder channels,
+    NC <= 32 classes."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, rmean, rvar, momentum, eps, act, hw, hb, labels, smoothing):
+        from .. import _native
+
+        y, prm, w2, bias = _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb)
+        K = y.shape[-1]
+        y2 = y.reshape(-1, K)
+        M, NC = y2.shape[0], w2.shape[0]
+        Kn = _native.kernels()
+        lab = labels.reshape(-1).contiguous()
+        dz = torch.empty(M, K, dtype=torch.bfloat16, device=y.device)
+        nb = Kn.seghead_blocks(M)
+        part = torch.empty(nb, Kn.seghead_part_len(), dtype=torch.float32, device=y.device)
+        wb = w2.to(torch.bfloat16).contiguous()
+        Kn.seghead_loss(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), wb.data_ptr(), _native.ptr(bias),
+                        lab.data_ptr(), dz.data_ptr(), part.data_ptr(), M, K, NC, act, 1.0 / M, float(smoothing),
+                        _native.stream(y2), [y2.numel(), wb.numel(), lab.numel(), dz.numel(), part.numel()])
+        ctx.save_for_backward(x, w, y, prm, hw, dz, part)
+        ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
+        ctx.params = (beta, gamma)
+        tot = part.sum(0)
+        hits = tot[1].round().long()
+        ctx.mark_non_differentiable(hits)
+        return tot[0] / M, hits
+
+    @staticmethod
+    def backward(ctx, dloss, _dhits):
+        from .. import _native
+        from . import bn as bn_ops
+        from . import conv_wtile
+        from ..training.flat import grad_target
+
+        x, w, y, prm, hw, dz, part = ctx.saved_tensors
+        K = y.shape[-1]
+        NC = hw.shape[0]
+        y2 = y.reshape(-1, K)
+        s = dloss.detach().float().reshape(1).contiguous()
+        _native.kernels().scale_unless_one(dz.data_ptr(), 1, s.data_ptr(), dz.numel(), _native.stream(dz))
+        tot = part[:, 2:].sum(0) * s                  # [db 32 | dWt 32 x 32 | msum 32 | msq 32], x dloss
+        dhw = dhb = None
+        if ctx.needs_input_grad[9]:
+            dwt = tot[32:32 + 32 * 32].view(32, 32)[:K, :NC]    # [ch][cls]
+            tgt = grad_target(hw)
+            dhw = tgt.view(NC, K).copy_(dwt.t()) if tgt is not None else dwt.t().contiguous()
+            dhw = dhw.reshape(hw.shape)
+        if ctx.has_b and ctx.needs_input_grad[10]:
+            tgt = grad_target(ctx.bparam)
+            dhb = tgt.copy_(tot[:NC]) if tgt is not None else tot[:NC].clone()
+        mom = tot[32 + 32 * 32:].view(1, 2, 32)[:, :, :K].contiguous()   # (sum g, sum g*y) of the BN
+        dbeta, dgamma = bn_ops._bwd_param_grads(dz, y2, prm, ctx.act, *ctx.params, part=mom)
+        dsh = bn_bwd_to_shifted(dz, y2, prm, dbeta, dgamma, ctx.act, y.shape)
+        dx = upconv_dgrad(dsh, w, x.shape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            N, D, H, W, C = x.shape
+            p = conv_wtile.plan_subpixel(N, (D, H, W), C, K)
+            dw = fold_weight_grad(conv_wtile.conv_wgrad_subpixel(dsh, x, p)).reshape(w.shape)
+        return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
+                None, None, None, None, None, dhw, dhb, None, None)
+
+
 class _SavedView:
     """ctx stand-in for :func:`_head_backward` (its first five saved tensors, the same flags)."""
 
@@ -375,9 +445,17 @@ def decoder_head(x5, w, gamma, beta, running_mean, running_var, hw, hb, momentum
 def decoder_head_xent(x5, w, gamma, beta, running_mean, running_var, hw, hb, labels, momentum=0.1, eps=1e-5,
                       act="relu", smoothing: float = 0.0):
     """:func:`decoder_head` + mean softmax cross-entropy against per-voxel ``labels`` -> (loss, hits)
-    (caller checks :func:`gpu_ok` and :func:`xent_ok`)."""
+    (caller checks :func:`gpu_ok` and :func:`xent_ok`): the head's whole backward inside the
+    forward kernel (:class:`SubpixelDecoderHeadLossFn`) for 32 decoder channels
+    (``FN_SEG_XENT=2`` keeps the loss-only epilogue, :class:`SubpixelDecoderHeadXentFn`)."""
+    import os
+
     from .spec import act_code
 
+    if hw.shape[-1] == 32 and os.environ.get("FN_SEG_XENT", "1") != "2":
+        return SubpixelDecoderHeadLossFn.apply(x5.to(torch.bfloat16).contiguous(), w, gamma, beta, running_mean,
+                                               running_var, momentum, eps, act_code(act), hw, hb, labels.long(),
+                                               float(smoothing))
     return SubpixelDecoderHeadXentFn.apply(x5.to(torch.bfloat16).contiguous(), w, gamma, beta, running_mean,
                                            running_var, momentum, eps, act_code(act), hw, hb, labels.long(),
                                            float(smoothing))

@@ -1,4 +1,4 @@
-"""Deterministic per-shape kernel selection for gfx950 (the committed tuning table).
+"""Deterministic per-shape kernel selection for gfx950: a rule plus measured exceptions.
 
 Several convolution shapes have two native implementations -- the big-tile kernels
 (``conv_tile.hip`` forward / dgrad, ``conv_wtile.hip`` weight gradient) and the
@@ -8,12 +8,14 @@ could run different kernels (different bf16 rounding, run-to-run variance).
 
 Selection is now a pure function of the shape:
 
-1. :data:`TABLE` -- measured choices for shapes where the default rule is wrong
-   (``scripts/bench_conv_layers.py`` on 1x MI355X, batch 128; the entries cite the
-   profile that decided them);
+1. :data:`EXCEPTIONS` -- measured choices for shapes where the rule is wrong
+   (``scripts/bench_conv_layers.py`` on 1x MI355X, batch 128; each entry cites the
+   profile that decided it).  It is empty: on every FeatureNet-3D and search-space
+   shape measured in rounds 2-4 the big-tile kernels beat the halo kernels
+   (``profiles/r4_m32_ab.md`` has the round-4 layer times of both);
 2. the rule: the big-tile kernel whenever it can plan the shape.
 
-``FN_KERNEL_SELECT=autotune`` restores per-shape timing for shapes not in the table
+``FN_KERNEL_SELECT=autotune`` restores per-shape timing for shapes without an exception
 (research / new shapes); under data parallelism :func:`sync_from_rank0` then makes
 every rank adopt rank 0's decisions before the step is captured.  Every decision is
 logged once per shape (``kernel_choice`` events, :mod:`featurenet_amd.utils.events`).
@@ -33,8 +35,8 @@ _DECIDED: dict = {}      # (kind, shape key) -> bool, every decision taken in th
 _LOGGED: set = set()
 
 # (kind, D, H, W, C, K, KD, KH, KW, sd, sh, sw, pd, ph, pw) -> True (big-tile kernel) / False (halo)
-# Only exceptions to the rule "big-tile whenever it plans" are listed.
-TABLE: dict = {
+# Only exceptions to the rule "big-tile whenever it plans" are listed (none measured so far).
+EXCEPTIONS: dict = {
 }
 
 
@@ -81,8 +83,8 @@ def select(kind: str, spec, run_tile=None, run_other=None) -> bool:
         return c
     src = "table"
     tk = (kind,) + key[1]
-    if tk in TABLE:
-        c = bool(TABLE[tk])
+    if tk in EXCEPTIONS:
+        c = bool(EXCEPTIONS[tk])
     elif mode() == "autotune" and run_tile is not None and run_other is not None and \
             not torch.cuda.is_current_stream_capturing():
         c = _time_ms(run_tile) <= _time_ms(run_other)

@@ -312,6 +312,6 @@ def test_kernel_selection_is_deterministic_without_timing(monkeypatch):
 
     tuning._DECIDED.pop(("fwd", tuning.shape_key(spec)), None)
     assert tuning.select("fwd", spec, boom, boom) is True
-    monkeypatch.setitem(tuning.TABLE, ("dgrad",) + tuning.shape_key(spec), False)
+    monkeypatch.setitem(tuning.EXCEPTIONS, ("dgrad",) + tuning.shape_key(spec), False)
     tuning._DECIDED.pop(("dgrad", tuning.shape_key(spec)), None)
     assert tuning.select("dgrad", spec, boom, boom) is False

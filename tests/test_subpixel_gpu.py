@@ -104,12 +104,14 @@ def test_decoder_head_matches_upsample_path():
         assert r < 5e-2, (k, r)
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
 @pytest.mark.parametrize("smoothing", [0.0, 0.1])
-def test_fused_head_xent_matches_softmax_xent(monkeypatch, smoothing):
-    """FeatureNet3DSeg.loss with the cross-entropy in the head's epilogue (pw_fwd XENT
-    instance: d(logits) stored instead of the logits) vs the unfused head + softmax_xent:
-    same loss, top-1 hits and every parameter gradient; a second call scaled by 3 checks the
-    dloss scaling of the stored d(logits)."""
+def test_fused_head_xent_matches_softmax_xent(monkeypatch, smoothing, mode):
+    """FeatureNet3DSeg.loss with the loss fused into the head vs the unfused head + softmax_xent:
+    mode 1 = the head's whole backward in the forward kernel (seghead.hip: dz, weight / bias
+    gradient and BN-moment partials), mode 2 = the loss-only epilogue (pw_fwd XENT instance:
+    d(logits) stored).  Same loss, top-1 hits and every parameter gradient; the loss is scaled by
+    3 before backward to check the dloss scaling of what the forward stored."""
     from featurenet_amd.models.featurenet3d import FeatureNet3DSeg
 
     torch.manual_seed(6)
@@ -118,7 +120,7 @@ def test_fused_head_xent_matches_softmax_xent(monkeypatch, smoothing):
     x = (torch.rand(N, S, S, S, 1, device="cuda") < 0.3).to(torch.bfloat16)
     lab = torch.randint(0, 25, (N, S, S, S), device="cuda")
     res = []
-    for flag in ("1", "0"):
+    for flag in (mode, "0"):
         monkeypatch.setenv("FN_SEG_XENT", flag)
         m.zero_grad(set_to_none=True)
         loss, hits = m.loss(x, lab, smoothing, with_correct=True)
