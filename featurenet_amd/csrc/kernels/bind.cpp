@@ -49,7 +49,7 @@ int fn_ew_mul_bwd(const void*, const void*, const void*, void*, void*, long long
 int fn_concat2(void*, void*, void*, long long, int, int, int, hipStream_t);
 int fn_pad3(void*, void*, const int*, int, hipStream_t);
 int fn_pad_channels(void*, void*, long long, int, int, int, hipStream_t);
-int fn_dense_fwd(const void*, const float*, const float*, void*, float*, int, int, int, int, int, int, hipStream_t);
+int fn_dense_fwd(const void*, const void*, const float*, void*, float*, int, int, int, int, int, int, int, hipStream_t);
 int fn_dense_dgrad(const void*, const float*, void*, int, int, int, hipStream_t);
 int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, float*, int, hipStream_t);
 int fn_dense_wgrad_slices(int, int, int);
@@ -70,6 +70,8 @@ int fn_bn_bwd_apply_s2d(const void*, const void*, const float*, const float*, co
 int fn_pool_fwd(const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd(const void*, const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd_stats_blocks(const int*);
+int fn_pool_bn_bwd_apply(const void*, const void*, const float*, const float*, const float*, const float*,
+                         const float*, const float*, void*, const int*, int, float, hipStream_t);
 int fn_pool_bwd_stats(const void*, const void*, void*, const float*, const float*, const int*, int, float*,
                       hipStream_t);
 int fn_softmax_xent_blocks(long long, int);
@@ -339,17 +341,17 @@ PYBIND11_MODULE(_C, m) {
      py::arg("ext"));
   m.def("dense_splits", &fn_dense_splits);
   m.def("dense_fwd", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t out, uintptr_t part, int M, int N, int K,
-                        int nsplit, int act, int out_fp32, uintptr_t st, std::vector<long long> ext) {
+                        int nsplit, int act, int out_fp32, uintptr_t st, std::vector<long long> ext, int wbf16) {
     fits(ext, 0, (long long)M * K, "dense_fwd", "x");
     fits(ext, 1, (long long)N * K, "dense_fwd", "w");
     fits(ext, 2, (long long)M * N, "dense_fwd", "out");
     fits(ext, 3, (long long)nsplit * M * N, "dense_fwd", "part");
-    chk(fn_dense_fwd(P<const void*>(x), P<const float*>(w), P<const float*>(bias), P<void*>(out), P<float*>(part), M,
-                     N, K, nsplit, act, out_fp32, S(st)),
+    chk(fn_dense_fwd(P<const void*>(x), P<const void*>(w), P<const float*>(bias), P<void*>(out), P<float*>(part), M,
+                     N, K, nsplit, act, out_fp32, wbf16, S(st)),
         "dense_fwd");
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("part"), py::arg("M"), py::arg("N"),
      py::arg("K"), py::arg("S"), py::arg("act"), py::arg("out_fp32"), py::arg("st"),
-     py::arg("ext") = std::vector<long long>());
+     py::arg("ext") = std::vector<long long>(), py::arg("wbf16") = 0);
   m.def("dense_dgrad", [](uintptr_t g, uintptr_t w, uintptr_t dx, int M, int N, int K, uintptr_t st,
                           std::vector<long long> ext) {
     fits(ext, 0, (long long)M * N, "dense_dgrad", "g");
@@ -572,6 +574,19 @@ PYBIND11_MODULE(_C, m) {
         "pool_bwd_stats");
   }, py::arg("dout"), py::arg("x"), py::arg("dx"), py::arg("scale"), py::arg("shift"), py::arg("geom"),
      py::arg("act"), py::arg("part"), py::arg("st"), py::arg("ext") = std::vector<long long>());
+  m.def("pool_bn_bwd_apply", [check_pool](uintptr_t dout, uintptr_t y, uintptr_t scale, uintptr_t shift,
+                                uintptr_t mean, uintptr_t invstd, uintptr_t dbeta, uintptr_t dgamma, uintptr_t dy,
+                                std::vector<int> geom, int act, float inv_count, uintptr_t st,
+                                std::vector<long long> ext) {
+    need(geom, 17, "pool_bn_bwd_apply");
+    check_pool(geom, ext, "pool_bn_bwd_apply");   // ext = {y (and dy), dout}
+    chk(fn_pool_bn_bwd_apply(P<const void*>(dout), P<const void*>(y), P<const float*>(scale), P<const float*>(shift),
+                             P<const float*>(mean), P<const float*>(invstd), P<const float*>(dbeta),
+                             P<const float*>(dgamma), P<void*>(dy), geom.data(), act, inv_count, S(st)),
+        "pool_bn_bwd_apply");
+  }, py::arg("dout"), py::arg("y"), py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"),
+     py::arg("dbeta"), py::arg("dgamma"), py::arg("dy"), py::arg("geom"), py::arg("act"), py::arg("inv_count"),
+     py::arg("st"), py::arg("ext") = std::vector<long long>());
   m.def("upsample2x", [](uintptr_t x, uintptr_t y, int N, int D, int H, int W, int C, int backward, uintptr_t st) {
     chk(fn_upsample2x(P<const void*>(x), P<void*>(y), N, D, H, W, C, backward, S(st)), "upsample2x");
   });

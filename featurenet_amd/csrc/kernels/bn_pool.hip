@@ -644,12 +644,14 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
         }
       }
     }
-    for (int w = 0; w < win; ++w) {
-      Pack8 p;
+    if (!STATS || dx) {                          // (STATS with dx null: the moments only -- the
+      for (int w = 0; w < win; ++w) {            //  fused apply below recomputes dx)
+        Pack8 p;
 #pragma unroll
-      for (int j = 0; j < VW; ++j) p.e[j] = f2bf(is_max ? (arg[j] == w ? go[j] : 0.f) : go[j] * inv);
-      const long long b = base_of(w);
-      if constexpr (VW == 8) *(uint4*)(dx + b) = p.u; else dx[b] = p.e[0];
+        for (int j = 0; j < VW; ++j) p.e[j] = f2bf(is_max ? (arg[j] == w ? go[j] : 0.f) : go[j] * inv);
+        const long long b = base_of(w);
+        if constexpr (VW == 8) *(uint4*)(dx + b) = p.u; else dx[b] = p.e[0];
+      }
     }
   }
   if constexpr (STATS) {
@@ -664,6 +666,81 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
       for (int t = chk; t < 256; t += cpr) { a += red[t][j]; b += red[t][VW + j]; }
       part[(long long)blockIdx.x * 2 * g.C + c] = a;
       part[(long long)blockIdx.x * 2 * g.C + g.C + c] = b;
+    }
+  }
+}
+
+// Max-pool backward and the BN backward's input gradient in one pass (non-overlapping windows
+// of <= 8 positions, C % 8 == 0): one thread per (window, 8-channel chunk) reads the window's y
+// once, recomputes z = act(bn(y)) and the first arg-max, and writes
+//   dy = scale*g + k2*y + k3,  g = dout * act'(z) at the arg-max, 0 elsewhere
+// for the whole window (bn_bwd_apply_kernel's k2 / k3).  Replaces pool_bwd (writes the sparse
+// dz) + bn_bwd_apply (reads dz and y again): two full-size passes fewer -- the moments come
+// from pool_bwd_tiled_kernel<8, true> with dx = null beforehand.
+__global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(
+    const bf16* __restrict__ dout, const bf16* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ dbeta, const float* __restrict__ dgamma, bf16* __restrict__ dy, PoolGeom g, int act,
+    float inv_count) {
+  const int cpr = g.C / 8;
+  const long long total = (long long)g.N * g.OD * g.OH * g.OW * cpr;
+  const int win = g.KD * g.KH * g.KW;            // (<= 8: host-checked)
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int ch = (int)(i % cpr);
+    long long t = i / cpr;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH); t /= g.OH;
+    const int od = (int)(t % g.OD);
+    const long long n = t / g.OD;
+    float go[8], sc[8], sh[8], k2[8], k3[8], best[8];
+    int arg[8];
+    Pack8 pg;
+    pg.u = *(const uint4*)(dout + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = ch * 8 + j;
+      go[j] = bf2f(pg.e[j]);
+      best[j] = -INFINITY;
+      arg[j] = 0;
+      sc[j] = scale[c];
+      sh[j] = shift[c];
+      const float is = invstd[c];
+      k2[j] = -sc[j] * is * dgamma[c] * inv_count;
+      k3[j] = -sc[j] * (dbeta[c] * inv_count - mean[c] * is * dgamma[c] * inv_count);
+    }
+    long long base[8];
+    Pack8 py[8];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      if (w < win) {
+        const int kw = w % g.KW, kh = (w / g.KW) % g.KH, kd = w / (g.KW * g.KH);
+        base[w] = ((((n * g.D + od * g.KD + kd) * g.H + oh * g.KH + kh) * (long long)g.W + ow * g.KW + kw) * g.C) +
+                  ch * 8;
+        py[w].u = *(const uint4*)(y + base[w]);
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      if (w < win) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = act_fwd(bf2f(py[w].e[j]) * sc[j] + sh[j], act);
+          if (v > best[j]) { best[j] = v; arg[j] = w; }
+        }
+      }
+    }
+    float gm[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gm[j] = go[j] * act_bwd_from_out(best[j], act);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      if (w < win) {
+        Pack8 po;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          po.e[j] = f2bf(sc[j] * (arg[j] == w ? gm[j] : 0.f) + k2[j] * bf2f(py[w].e[j]) + k3[j]);
+        *(uint4*)(dy + base[w]) = po.u;
+      }
     }
   }
 }
@@ -848,6 +925,23 @@ extern "C" int fn_pool_bwd_stats(const void* dout, const void* x, void* dx, cons
   if (nb <= 0 || !scale || !shift || !part) return -2;
   hipLaunchKernelGGL((pool_bwd_tiled_kernel<8, true>), dim3(nb), dim3(256), 0, st, (const bf16*)dout, (const bf16*)x,
                      (bf16*)dx, scale, shift, g, 1, act, part);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// dy of BN+act+max-pool in one pass (pool_bn_bwd_apply_kernel); the tiled-window geometry of
+// fn_pool_bwd_stats with windows of <= 8 positions
+extern "C" int fn_pool_bn_bwd_apply(const void* dout, const void* y, const float* scale, const float* shift,
+                                    const float* mean, const float* invstd, const float* dbeta, const float* dgamma,
+                                    void* dy, const int* geom17, int act, float inv_count, hipStream_t st) {
+  const PoolGeom g = pool_geom(geom17);
+  const bool tiled = g.sd == g.KD && g.sh == g.KH && g.sw == g.KW && g.pd == 0 && g.ph == 0 && g.pw == 0 &&
+                     g.D == g.OD * g.KD && g.H == g.OH * g.KH && g.W == g.OW * g.KW;
+  if (!tiled || g.C % 8 || g.KD * g.KH * g.KW > 8) return -2;
+  const long long outs = (long long)g.N * g.OD * g.OH * g.OW;
+  hipLaunchKernelGGL(pool_bn_bwd_apply_kernel, dim3(ew_blocks(outs * (g.C / 8))), dim3(256), 0, st,
+                     (const bf16*)dout, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, g, act,
+                     inv_count);
   FN_CHECK_LAUNCH();
   return 0;
 }

@@ -5,9 +5,10 @@
 // K huge); NAS candidates put Dense layers of up to 2048 features after small feature maps.
 //
 //   dense_fwd_part  split-K partial products, x bf16 [M][K] x W fp32 [N][K] (the fp32 master
-//                   weights converted to bf16 on the fly: no per-step weight cast pass), fp32
-//                   partial slabs [S][M][N]; 128x64 output tile per workgroup, 4 waves x
-//                   (32 rows x 64 cols), operands straight from global (16-B loads, no LDS)
+//                   weights converted to bf16 on the fly: no per-step weight cast pass) or a
+//                   bf16 W copy (inference), fp32 partial slabs [S][M][N]; 128x64 or 128x128
+//                   output tile per workgroup, 4 or 8 waves x (32 rows x 64 cols), operands
+//                   straight from global (16-B loads, no LDS)
 //   dense_fwd_reduce  y = act(sum_s part[s] + b) -> bf16 or fp32 (one pass over M*N)
 //   dense_dgrad     dx [M][K] = g [M][N] W [N][K] -> bf16.  C^T form: A = W^T from an LDS
 //                   tile written transposed ([kk][n], converted to bf16), B = g rows from
@@ -34,19 +35,25 @@ __device__ __forceinline__ bf16x8 dn_cvt8(const float4 a, const float4 b) {
 // ---------------------------------------------------------------------------
 // forward: split-K partials
 // ---------------------------------------------------------------------------
-// grid (ceil(N/64), ceil(M/128), S); slice s covers k in [s*kc, min(K, (s+1)*kc)), kc % 32 == 0.
-// VEC (K % 8 == 0): 16-B x rows and float4 weight loads; otherwise element loads masked at kend
-// (the 84-wide LeNet layers).  D k-steps of raw operands in flight (a register ring): with one
-// step ahead the loop waited a full memory latency per 32-k step (FC1 at 128^3 inference:
-// 1100 steps per slice, 2.4 ms for 3.4 GB)
-template <bool VEC, int D>
-__global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* __restrict__ x,
-                                                                    const float* __restrict__ w,
-                                                                    float* __restrict__ part, int M, int N, int K,
-                                                                    int kc) {
+// grid (ceil(N/(64 NCW)), ceil(M/128), S); slice s covers k in [s*kc, min(K, (s+1)*kc)),
+// kc % 32 == 0.  4 NCW waves: wave w takes rows 32 (w & 3).., columns 64 (w >> 2)..  -- with
+// NCW = 2 (N > 64) a workgroup covers 128 columns, so each x row is fetched from HBM once and
+// shared by the two column waves through the CU's L1 / L2 (with 64-column workgroups the two
+// column tiles of a row landed on different XCDs and x, 2.3 GB at 128^3 inference, came from
+// HBM twice).
+// VEC (K % 8 == 0): 16-B x rows and 16-B weight loads; otherwise element loads masked at kend
+// (the 84-wide LeNet layers).  WB: bf16 weights (the inference copy, half the weight bytes, no
+// conversion), else the fp32 master weights converted on the fly.  D k-steps of raw operands
+// in flight (a register ring): with one step ahead the loop waited a full memory latency per
+// 32-k step (FC1 at 128^3 inference: 1100 steps per slice)
+template <bool VEC, int D, bool WB, int NCW>
+__global__ __launch_bounds__(DN_THREADS * NCW) void dense_fwd_part_kernel(const bf16* __restrict__ x,
+                                                                          const void* __restrict__ wv,
+                                                                          float* __restrict__ part, int M, int N,
+                                                                          int K, int kc) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, gq = lane >> 4;
-  const int row0 = blockIdx.y * 128 + wave * 32, col0 = blockIdx.x * 64;
+  const int row0 = blockIdx.y * 128 + (wave & 3) * 32, col0 = (blockIdx.x * NCW + (wave >> 2)) * 64;
   const int kbeg = blockIdx.z * kc, kend = min(K, kbeg + kc);
   f32x4 acc[2][4];
 #pragma unroll
@@ -57,6 +64,7 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
   bool rok[2], cok[4];
   const bf16* xr[2];
   const float* wr[4];
+  const bf16* wh[4];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int m = row0 + i * 16 + r;
@@ -67,13 +75,15 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
   for (int j = 0; j < 4; ++j) {
     const int n = col0 + j * 16 + r;
     cok[j] = n < N;
-    wr[j] = w + (long long)(cok[j] ? n : 0) * K;
+    wr[j] = (const float*)wv + (long long)(cok[j] ? n : 0) * K;
+    wh[j] = (const bf16*)wv + (long long)(cok[j] ? n : 0) * K;
   }
   const bf16x8 zero8 = {};
   // D k-steps of operands in flight ahead of the MFMAs (raw loads; conversion and masking
   // happen when the step is consumed; steps past kend read chunk 0 and are never consumed)
   bf16x8 ra[D][2];
   float4 rb[D][4][2];
+  bf16x8 rh[D][4];
   auto load = [&](int st, int k0) {
     const int k = k0 + 8 * gq;
     const int ks = k < kend ? k : 0;
@@ -82,9 +92,13 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
       for (int i = 0; i < 2; ++i) ra[st][i] = *(const bf16x8*)(xr[i] + ks);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float4* p = (const float4*)(wr[j] + ks);
-        rb[st][j][0] = p[0];
-        rb[st][j][1] = p[1];
+        if constexpr (WB) {
+          rh[st][j] = *(const bf16x8*)(wh[j] + ks);
+        } else {
+          const float4* p = (const float4*)(wr[j] + ks);
+          rb[st][j][0] = p[0];
+          rb[st][j][1] = p[1];
+        }
       }
     } else {
 #pragma unroll
@@ -93,11 +107,16 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
         for (int e = 0; e < 8; ++e) ra[st][i][e] = ks + e < kend ? xr[i][ks + e] : f2bf(0.f);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float t[8];
+        if constexpr (WB) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) t[e] = ks + e < kend ? wr[j][ks + e] : 0.f;
-        rb[st][j][0] = make_float4(t[0], t[1], t[2], t[3]);
-        rb[st][j][1] = make_float4(t[4], t[5], t[6], t[7]);
+          for (int e = 0; e < 8; ++e) rh[st][j][e] = ks + e < kend ? wh[j][ks + e] : f2bf(0.f);
+        } else {
+          float t[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t[e] = ks + e < kend ? wr[j][ks + e] : 0.f;
+          rb[st][j][0] = make_float4(t[0], t[1], t[2], t[3]);
+          rb[st][j][1] = make_float4(t[4], t[5], t[6], t[7]);
+        }
       }
     }
   };
@@ -122,7 +141,9 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_part_kernel(const bf16* 
         for (int i = 0; i < 2; ++i) fa[i] = kok ? ra[st][i] : zero8;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const bf16x8 t = dn_cvt8(rb[st][j][0], rb[st][j][1]);
+          bf16x8 t;
+          if constexpr (WB) t = rh[st][j];
+          else t = dn_cvt8(rb[st][j][0], rb[st][j][1]);
           fb[j] = kok ? t : zero8;
         }
         load(st, kk + 32 * D);
@@ -360,25 +381,45 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
+// column waves per forward workgroup: 2 (128 columns, x rows read once) when N > 64
+static int dn_ncw(int N) { return N > 64 ? 2 : 1; }
+
 extern "C" int fn_dense_splits(int M, int N, int K) {
-  const int tiles = ((N + 63) / 64) * ((M + 127) / 128);
-  int S = (512 + tiles - 1) / tiles;
+  const int ncw = dn_ncw(N);
+  const int tiles = ((N + 64 * ncw - 1) / (64 * ncw)) * ((M + 127) / 128);
+  const int target = 512 / ncw;                  // ~2048 waves: 2 per SIMD
+  int S = (target + tiles - 1) / tiles;
   const int maxS = K / 256 > 0 ? K / 256 : 1;   // >= 256 k per slice
   return S < 1 ? 1 : (S > maxS ? maxS : S);
 }
 
-extern "C" int fn_dense_fwd(const void* x, const float* w, const float* bias, void* out, float* part, int M, int N,
-                            int K, int S, int act, int out_fp32, hipStream_t st) {
+template <bool WB, int NCW>
+static void dn_fwd_part(const void* x, const void* w, float* part, int M, int N, int K, int kc, int Sr,
+                        hipStream_t st) {
+  const dim3 grid((N + 64 * NCW - 1) / (64 * NCW), (M + 127) / 128, Sr), blk(DN_THREADS * NCW);
+  if (K % 8 == 0)
+    hipLaunchKernelGGL((dense_fwd_part_kernel<true, 4, WB, NCW>), grid, blk, 0, st, (const bf16*)x, w, part, M, N,
+                       K, kc);
+  else
+    hipLaunchKernelGGL((dense_fwd_part_kernel<false, 1, WB, NCW>), grid, blk, 0, st, (const bf16*)x, w, part, M, N,
+                       K, kc);
+}
+
+// w: fp32 [N][K] (training: the master weights) or, wbf16, a bf16 copy (inference)
+extern "C" int fn_dense_fwd(const void* x, const void* w, const float* bias, void* out, float* part, int M, int N,
+                            int K, int S, int act, int out_fp32, int wbf16, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || S < 1) return -2;
   int kc = (K + S - 1) / S;
   kc = (kc + 31) / 32 * 32;
   const int Sr = (K + kc - 1) / kc;              // slices actually covering K
-  if (K % 8 == 0)
-    hipLaunchKernelGGL((dense_fwd_part_kernel<true, 4>), dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0,
-                       st, (const bf16*)x, w, part, M, N, K, kc);
-  else
-    hipLaunchKernelGGL((dense_fwd_part_kernel<false, 1>), dim3((N + 63) / 64, (M + 127) / 128, Sr), dim3(DN_THREADS), 0,
-                       st, (const bf16*)x, w, part, M, N, K, kc);
+  const int ncw = dn_ncw(N);
+  if (wbf16) {
+    if (ncw == 2) dn_fwd_part<true, 2>(x, w, part, M, N, K, kc, Sr, st);
+    else dn_fwd_part<true, 1>(x, w, part, M, N, K, kc, Sr, st);
+  } else {
+    if (ncw == 2) dn_fwd_part<false, 2>(x, w, part, M, N, K, kc, Sr, st);
+    else dn_fwd_part<false, 1>(x, w, part, M, N, K, kc, Sr, st);
+  }
   FN_CHECK_LAUNCH();
   const long long tot = (long long)M * N;
   hipLaunchKernelGGL(dense_fwd_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(DN_THREADS), 0, st,

@@ -14,7 +14,8 @@ Post-training quantisation, inference only:
   (+ requantise to fp8) in the epilogue.  conv1 (1-channel, stride 2) stays on
   the bf16 path (space-to-depth tile kernel) with the folded BN + ReLU fused,
   followed by one quantisation pass; conv4 writes bf16 for the max-pool and the
-  two dense layers (native split-K MFMA kernels, bf16).
+  two dense layers (native split-K MFMA kernels on bf16 weight copies, 128-column
+  workgroups: ``csrc/kernels/dense.hip``).
 """
 from __future__ import annotations
 
@@ -203,6 +204,18 @@ class Fp8FeatureNet3D:
             last = i == len(convs) - 1
             self.layers.append(Fp8Conv(conv, act_scales[i - 1], None if last else act_scales[i], relu=True))
         self.pool = convs[-1].pool
+        # the dense layers read bf16 weight copies (FN_F8_FC_BF16=0: the fp32 master weights)
+        self.fc_w = None
+        if os.environ.get("FN_F8_FC_BF16", "1") != "0":
+            self.fc_w = [fc.weight.detach().to(torch.bfloat16).contiguous() for fc in (model.fc1, model.fc2)]
+
+    def _dense(self, f: torch.Tensor) -> torch.Tensor:
+        m = self.model
+        if self.fc_w is None or not _native.use_native(f):
+            return m.fc2(m.fc1(f), out_fp32=True)
+        from ..ops.linear import linear_infer
+        h = linear_infer(f, self.fc_w[0], m.fc1.bias, m.fc1.act)
+        return linear_infer(h, self.fc_w[1], m.fc2.bias, m.fc2.act, out_fp32=True)
 
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -232,7 +245,7 @@ class Fp8FeatureNet3D:
             ps = PoolSpec.make(tuple(feat.shape), self.pool, m.convs[-1].pool_stride, "valid")
             feat = ops.pool(feat, ps, "max")
         f = feat.reshape(feat.shape[0], -1)
-        return m.fc2(m.fc1(f), out_fp32=True)
+        return self._dense(f)
 
     __call__ = forward
 

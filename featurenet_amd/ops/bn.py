@@ -153,12 +153,28 @@ class BatchNormActPoolFn(torch.autograd.Function):
     def backward(ctx, dp):
         y, prm = ctx.saved_tensors
         C = y.shape[-1]
-        dz = torch.empty_like(y)
         dp = dp.contiguous().to(torch.bfloat16)
         K = _native.kernels()
         geom = ctx.pspec.geom17()
         nb = K.pool_bwd_stats_blocks(geom) if (ctx.is_max and ctx.training and bnfuse.pool_stats_enabled()) else 0
         part = None
+        ps = ctx.pspec
+        if nb > 0 and bnfuse.pool_apply_enabled() and ps.KD * ps.KH * ps.KW <= 8 and C % 8 == 0:
+            # the moments without writing dz, then dy straight from (dp, y): no sparse dz pass
+            part = torch.empty(nb, 2, C, dtype=torch.float32, device=y.device)
+            K.pool_bwd_stats(dp.data_ptr(), y.data_ptr(), 0, prm[2].data_ptr(), prm[3].data_ptr(), geom, ctx.act,
+                             part.data_ptr(), _native.stream(y), [y.numel(), dp.numel(), part.numel()])
+            y2 = y.reshape(-1, C)
+            dbeta, dgamma = _bwd_param_grads(None, y2, prm, ctx.act, *ctx.params, part=part)
+            dy = None
+            if ctx.needs_input_grad[0]:
+                dy = torch.empty_like(y)
+                K.pool_bn_bwd_apply(dp.data_ptr(), y.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(),
+                                    prm[0].data_ptr(), prm[1].data_ptr(), dbeta.data_ptr(), dgamma.data_ptr(),
+                                    dy.data_ptr(), geom, ctx.act, 1.0 / y2.shape[0], _native.stream(y),
+                                    [y.numel(), dp.numel()])
+            return (dy, dgamma if ctx.has_gamma else None, dbeta if ctx.has_beta else None) + (None,) * 10
+        dz = torch.empty_like(y)
         if nb > 0:
             # max-pool backward + this BN's raw backward moments in one pass (no colstats)
             part = torch.empty(nb, 2, C, dtype=torch.float32, device=y.device)

@@ -62,6 +62,12 @@ def pool_stats_enabled() -> bool:
     return os.environ.get("FN_POOL_BN_STATS", "1") != "0"
 
 
+def pool_apply_enabled() -> bool:
+    """BN backward's input gradient computed inside the max-pool backward (the moments pass then
+    writes nothing; ``pool_bn_bwd_apply``) -- FN_POOL_BN_APPLY, default on."""
+    return os.environ.get("FN_POOL_BN_APPLY", "1") != "0"
+
+
 def _purge(d: dict, limit: int = 256) -> None:
     if len(d) > limit:
         for k in [k for k, v in d.items() if v[0]() is None]:

@@ -96,6 +96,39 @@ def test_pool_bwd_bn_stats_match_colstats(monkeypatch, N, S, C):
         assert err < 2e-3, f"{n}: rel err {err:.2e}"
 
 
+@pytest.mark.parametrize("N,S,C", [(2, 20, 64), (3, 8, 16), (4, 6, 8)])
+def test_pool_bn_bwd_apply_matches_separate_passes(monkeypatch, N, S, C):
+    """BN+ReLU+max-pool backward in one pass (pool_bn_bwd_apply: no sparse dz tensor) vs
+    pool_bwd + bn_bwd_apply: same input and parameter gradients."""
+    from featurenet_amd.models.layers import Conv
+
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    layer = Conv(C, C, 3, 1, "same", bn=True, act="relu", pool=(2, 2, 2), init="he").to(dev)
+    x0 = torch.randn(N, S, S, S, C, device=dev).to(torch.bfloat16)
+    Kn = _native.kernels()
+    calls = {"n": 0}
+    orig = Kn.pool_bn_bwd_apply
+
+    def counted(*a, **k):
+        calls["n"] += 1
+        return orig(*a, **k)
+
+    monkeypatch.setattr(Kn, "pool_bn_bwd_apply", counted)
+    res = {}
+    for apply in ("0", "1"):
+        monkeypatch.setenv("FN_POOL_BN_APPLY", apply)
+        x = x0.clone().requires_grad_(True)
+        g = _grads(layer, x, True, monkeypatch)
+        g["x"] = x.grad.detach().float().clone()
+        res[apply] = g
+    for n in res["0"]:
+        a, b = res["0"][n], res["1"][n]
+        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
+        assert err < 2e-3, f"{n}: rel err {err:.2e}"
+    assert calls["n"] == 1
+
+
 @pytest.mark.parametrize("S", [16, 32])
 def test_seg_head_bn_in_pointwise_matches_unfused(monkeypatch, S):
     """FeatureNet3DSeg training step with the decoder BN + ReLU inside the 1x1 head's pointwise

@@ -814,6 +814,24 @@ def test_dense_native_matches_fp32(M, K, N, act, bias):
         assert e < 2e-2, e
 
 
+@pytest.mark.parametrize("M,K,N,act", [(1024, 140608, 128, "relu"), (128, 64000, 128, None), (64, 84, 10, None),
+                                        (300, 520, 200, "relu"), (33, 4096, 64, None)])
+def test_dense_infer_bf16_weights(M, K, N, act):
+    """Inference Dense on a bf16 weight copy (128-column workgroups when N > 64) vs fp32 PyTorch."""
+    from featurenet_amd.ops.linear import linear_infer
+
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device="cuda") * 0.1
+    y = linear_infer(x, w, b, act, out_fp32=True)
+    yr = x.float() @ w.float().t() + b
+    if act == "relu":
+        yr = torch.relu(yr)
+    assert y.dtype == torch.float32 and y.shape == (M, N)
+    assert ((y - yr).norm() / yr.norm()).item() < 1e-4
+
+
 @pytest.mark.parametrize("shape", [(2, 3, 5, 7, 16), (3, 1, 4, 6, 5)])
 def test_combine_kernels_match_torch(shape):
     """Native add / multiply (+fused backward), two-way concat (+split) and zero padding
