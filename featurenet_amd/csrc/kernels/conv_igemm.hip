@@ -353,7 +353,7 @@ template <int BCO, int GM, bool VECN>
 __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ src, float* __restrict__ dw,
     const int4* __restrict__ tab, GatherGeom g, long long M, int Cout, int Kdim, long long rows_per_split,
-    int gx, int gy) {
+    int gx, int gy, int ccrop, int cpad) {
   constexpr int LDY = WgLds<BCO>::LDY;
   constexpr int X_STAGE = WG_BR * WG_LDX;
   constexpr int Y_STAGE = WG_BR * LDY;
@@ -487,15 +487,27 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
   // Split-m partial sums are folded straight into the fp32 dW with no-return
   // float atomics (S x Cout x Kdim x 4 B of atomic traffic, well under the
   // ~1.3 TB/s chip-wide atomic rate for the split counts used).
+  // ccrop > 0: k = t*cpad + c lands at dw[co][t*ccrop + c] of the real weight, columns
+  // c >= ccrop dropped -- the zero channels of a channel-padded input (cpad = its channels,
+  // ccrop = the real ones) or the row padding of the packed-W layout (cpad = R, ccrop = KW*C):
+  // straight into the parameter's zeroed flat gradient (no padded dW buffer, fill or crop copy)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int k = kc0 + wave * 64 + nt * 16 + (lane & 15);
+      long long kdst = k;
+      bool kok = k < Kdim;
+      if (ccrop > 0) {
+        const int t = k / cpad, c = k - t * cpad;
+        kok = kok && c < ccrop;
+        kdst = (long long)t * ccrop + c;
+      }
+      const long long ldo = ccrop > 0 ? (long long)(Kdim / cpad) * ccrop : Kdim;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + mt * 16 + (lane >> 4) * 4 + r;
-        if (co < Cout && k < Kdim) atomicAdd(dw + (long long)co * Kdim + k, acc[mt][nt][r]);
+        if (co < Cout && kok) atomicAdd(dw + (long long)co * ldo + kdst, acc[mt][nt][r]);
       }
     }
 }
@@ -563,9 +575,13 @@ extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, 
 
 extern "C" int fn_igemm_fwd_mblocks(long long M) { return (int)((M + FWD_BM - 1) / FWD_BM); }
 
+// ccrop > 0: dw is the real [Cout][Kdim / cpad][ccrop] weight gradient; column t*cpad + c of the
+// gather layout (c < ccrop) maps to t*ccrop + c (channel-padded inputs; the packed-W rows)
 extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const int* tab, const int* geom14,
-                              long long M, int Cout, int Kdim, int splits, int gm, hipStream_t st) {
+                              long long M, int Cout, int Kdim, int splits, int gm, hipStream_t st, int ccrop,
+                              int cpad) {
   const GatherGeom g = parse_geom(geom14);
+  if (ccrop > 0 && (cpad < ccrop || Kdim % cpad)) return -2;
   const int BCO = Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64);
   const long long rps = ((M + splits - 1) / splits + WG_BR - 1) / WG_BR * WG_BR;
   const int gx = (Kdim + WG_BK - 1) / WG_BK, gy = (Cout + BCO - 1) / BCO;
@@ -575,7 +591,8 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const 
   const bf16* s = (const bf16*)src;
   const int4* t = (const int4*)tab;
 #define WG_CASE(B, V, VN) \
-  hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, dw, t, g, M, Cout, Kdim, rps, gx, gy)
+  hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, dw, t, g, M, Cout, Kdim, rps, gx, gy, \
+                     ccrop, cpad)
 #define WG_GM(GMV)                                                                        \
   do {                                                                                    \
     if (vecn) {                                                                           \

@@ -820,6 +820,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     if ((dbg & 16) && hipMemsetAsync(stamps, 0, nst * sizeof(long long), st) != hipSuccess) return -5;
 #define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, src, \
       (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, stamps);
+    CT_DBG(1, 1) CT_DBG(1, 2) CT_DBG(1, 4) CT_DBG(1, 16)   // (the space-to-depth stem)
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
     CT_DBG(4, 23) CT_DBG(2, 32) CT_DBG(4, 32)
     CT_DBG(2, 64) CT_DBG(2, 128) CT_DBG(2, 192) CT_DBG(4, 64) CT_DBG(4, 128) CT_DBG(4, 192)   // (correct results)

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(const TIn* __res
                                                                 const long long* __restrict__ labels,
                                                                 float* __restrict__ block_loss, TIn* __restrict__ dlogits,
                                                                 int* __restrict__ correct, long long B, int NC,
-                                                                float gscale, float smoothing) {
+                                                                float gscale, float smoothing, float lscale) {
   // EPL > 0: the row (<= LPR*EPL classes) is read ONCE into registers; EPL = 0: any NC,
   // re-read per pass
   constexpr int RPB = 256 / LPR;
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(const TIn* __res
   acc = wave_sum(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) block_loss[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) block_loss[blockIdx.x] = (red[0] + red[1] + red[2] + red[3]) * lscale;
 }
 
 // Tile form for bf16 logits with NC <= NCMAX (the per-voxel segmentation loss):
@@ -115,7 +115,8 @@ __global__ __launch_bounds__(256) void softmax_xent_tile_kernel(const bf16* __re
                                                                 const long long* __restrict__ labels,
                                                                 float* __restrict__ block_loss,
                                                                 bf16* __restrict__ dlogits, int* __restrict__ correct,
-                                                                long long B, int NC, float gscale, float smoothing) {
+                                                                long long B, int NC, float gscale, float smoothing,
+                                                                float lscale) {
   __shared__ __attribute__((aligned(16))) bf16 tile[256 * NCMAX];
   __shared__ float red[4];
   const int tid = threadIdx.x;
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(256) void softmax_xent_tile_kernel(const bf16* __re
   acc = wave_sum(acc);
   if ((tid & 63) == 0) red[tid >> 6] = acc;
   __syncthreads();
-  if (tid == 0) block_loss[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) block_loss[blockIdx.x] = (red[0] + red[1] + red[2] + red[3]) * lscale;
 }
 
 // ---------------------------------------------------------------------------
@@ -446,21 +447,26 @@ extern "C" int fn_upsample2x(const void* x, void* y, int N, int D, int H, int W,
 static int sx_lpr(int NC) { return NC <= 64 ? 8 : 64; }
 
 // number of partial loss sums softmax_xent_rows writes (= its grid); the bf16 tile
-// kernel (NC <= 32) covers 256 rows per block, the lane-group kernel 256/LPR
+// kernel (NC <= 32) covers 256 rows per block, the lane-group kernel 256/LPR.  Classifier
+// batches (<= 2048 rows) take ONE block: its partial is then the mean loss itself (no reduction
+// and division launches after the loss kernel)
 extern "C" int fn_softmax_xent_blocks(long long B, int NC) {
+  if (B <= 2048) return 1;
   const long long rpb = NC <= 32 ? 256 : 256 / sx_lpr(NC);
   const long long need = (B + rpb - 1) / rpb;
   return (int)(need < 8192 ? (need > 0 ? need : 1) : 8192);
 }
 
-// logits / dlogits bf16 (in_bf16 = 1) or fp32; block_loss: fp32 [fn_softmax_xent_blocks]
+// logits / dlogits bf16 (in_bf16 = 1) or fp32; block_loss: fp32 [fn_softmax_xent_blocks] partial
+// sums, or with one block the sum x gscale (the mean loss when gscale = 1/B)
 extern "C" int fn_softmax_xent_rows(const void* logits, int in_bf16, const long long* labels, float* block_loss,
                                     void* dlogits, int* correct, long long B, int NC, float gscale, float smoothing,
                                     hipStream_t st) {
   const unsigned blocks = (unsigned)fn_softmax_xent_blocks(B, NC);
+  const float lscale = blocks == 1 ? gscale : 1.f;
 #define SX(T, L, E)                                                                                                \
   hipLaunchKernelGGL((softmax_xent_rows_kernel<T, L, E>), dim3(blocks), dim3(256), 0, st, (const T*)logits, labels, \
-                     block_loss, (T*)dlogits, correct, B, NC, gscale, smoothing)
+                     block_loss, (T*)dlogits, correct, B, NC, gscale, smoothing, lscale)
 #define SX_T(T)                                         \
   do {                                                  \
     if (NC <= 32) SX(T, 8, 4);                          \
@@ -469,7 +475,7 @@ extern "C" int fn_softmax_xent_rows(const void* logits, int in_bf16, const long 
   } while (0)
   if (in_bf16 && NC <= 32)
     hipLaunchKernelGGL(softmax_xent_tile_kernel<32>, dim3(blocks), dim3(256), 0, st, (const bf16*)logits, labels,
-                       block_loss, (bf16*)dlogits, correct, B, NC, gscale, smoothing);
+                       block_loss, (bf16*)dlogits, correct, B, NC, gscale, smoothing, lscale);
   else if (in_bf16) SX_T(bf16);
   else SX_T(float);
 #undef SX_T

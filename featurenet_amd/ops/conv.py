@@ -498,6 +498,10 @@ def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=N
         return halo_conv_wgrad(dy5.contiguous(), x5.contiguous(), spec, plan, out=out)
     K = _native.kernels()
     gm = gather_mode(spec)
+    if gm == GM_PACKW:                   # (the epilogue drops the packed rows' padding columns)
+        dw = igemm_wgrad_cropped(dy5, x5, spec, spec.C, out=out)
+        if dw is not None:
+            return dw
     tab = _table(spec, "fwd", gm, x5.device)
     splits = wgrad_splits(spec)
     kd = kdim_gather(spec)
@@ -516,6 +520,39 @@ def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=N
     if out is not None:
         return out.copy_(dw)
     return dw.contiguous()
+
+
+def igemm_wgrad_cropped(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, c0: int, out=None):
+    """fp32 dW [K, KD, KH, KW, c0] on the gather kernel, accumulated straight into ``out``
+    (zeroed, e.g. the parameter's flat gradient) with every padding column of the gather
+    layout dropped in the epilogue: the zero channels c0..spec.C of a channel-padded input,
+    or the row padding of the packed-W layout (C < 8: rows of KW*C rounded up to 8).
+    ``dy5`` has the real ``spec.K`` channels (any count, no padded copy).  None when the
+    shape belongs to another weight-gradient kernel."""
+    sk = dataclasses.replace(spec, K=-(-spec.K // 8) * 8)        # (what the padded path would run)
+    if any(p is not None for p in (halo_wgrad_plan(spec), conv_wtile.plan(spec), halo_wgrad_plan(sk),
+                                   conv_wtile.plan(sk))):
+        return None
+    gm = gather_mode(spec)
+    if spec.C < c0:
+        return None
+    if gm == GM_PACKW:
+        if c0 != spec.C:
+            return None
+        cpad, ccrop = packw_row(spec), spec.KW * spec.C   # row r*R + p -> r*KW*C + p, p < KW*C
+    else:
+        cpad, ccrop = spec.C, c0                          # tap t*C + c -> t*c0 + c, c < c0
+    kd = kdim_gather(spec)
+    if kd % cpad:
+        return None
+    shape = (spec.K, spec.KD, spec.KH, spec.KW, c0)
+    if out is None or out.dtype != torch.float32 or not out.is_contiguous() or tuple(out.shape) != shape:
+        out = torch.zeros(shape, dtype=torch.float32, device=x5.device)
+    tab = _table(spec, "fwd", gm, x5.device)
+    dy5, x5 = dy5.contiguous(), x5.contiguous()
+    _native.kernels().igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), out.data_ptr(), tab.data_ptr(), _geom_fwd(spec),
+                                  spec.M, spec.K, kd, wgrad_splits(spec), gm, _native.stream(x5), ccrop, cpad)
+    return out
 
 
 def native_colsum(x2: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -723,17 +760,23 @@ def _conv_bwd_padded(ctx, dy, xs, w, spec):
     C0 = w.shape[-1]
     K0 = spec.K
     kp = -(-K0 // 8) * 8
-    dyp = pad_channels(dy, kp)
     sk = dataclasses.replace(spec, K=kp)
+    dyp = None
     dx = dw = None
     if ctx.x_needs:                                              # real input channels: dx has C0 columns
+        dyp = pad_channels(dy, kp)
         dx = native_conv_dgrad(dyp, w.detach(), dataclasses.replace(sk, C=C0))   # (zero rows K0..kp)
     if ctx.needs_input_grad[1]:
         tgt = grad_target(w)
         if kp != K0 or spec.C != C0:
-            dwp = native_conv_wgrad(dyp, xs.contiguous(), sk)     # [kp, KD, KH, KW, spec.C]
-            dw = tgt.copy_(dwp[:K0, ..., :C0]) if tgt is not None else dwp[:K0, ..., :C0].contiguous()
+            # the gather kernel drops the padded channels itself and reads the unpadded dy
+            dw = igemm_wgrad_cropped(dy, xs, spec, C0, out=tgt)
+            if dw is None:
+                dyp = pad_channels(dy, kp) if dyp is None else dyp
+                dwp = native_conv_wgrad(dyp, xs.contiguous(), sk)     # [kp, KD, KH, KW, spec.C]
+                dw = tgt.copy_(dwp[:K0, ..., :C0]) if tgt is not None else dwp[:K0, ..., :C0].contiguous()
         else:
+            dyp = pad_channels(dy, kp) if dyp is None else dyp
             dw = native_conv_wgrad(dyp, xs.contiguous(), sk, out=tgt)
     db = (native_colsum(dy.reshape(-1, K0), out=grad_target(ctx.bparam))
           if (ctx.has_b and ctx.needs_input_grad[2]) else None)

@@ -15,8 +15,8 @@ from . import reference as ref
 
 
 def _xent_rows(lg, labels, smoothing, want_correct):
-    """One pass of the fused kernel: (per-block loss partials, d(logits) with 1/B folded in,
-    per-row top-1 hits or None)."""
+    """One pass of the fused kernel: (per-block loss partials -- or, with one block, the mean
+    loss itself --, d(logits) with 1/B folded in, per-row top-1 hits or None)."""
     B, NC = lg.shape
     K = _native.kernels()
     nblk = K.softmax_xent_blocks(B, NC)
@@ -45,7 +45,8 @@ class SoftmaxXentFn(torch.autograd.Function):
         ctx.smoothing = smoothing
         if correct is not None:
             ctx.mark_non_differentiable(correct)
-        return part.sum() / B, correct
+        # one block (classifier batches): the kernel wrote the mean itself
+        return (part.view(()) if part.numel() == 1 else part.sum() / B), correct
 
     @staticmethod
     def backward(ctx, dloss, _dc):

@@ -18,7 +18,11 @@ step() {
 step i8dbg 120 python3 scripts/r4/i8_debug.py; cat gpurun_out/b5_i8dbg.log | grep -v amdgpu.ids
 step tests 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
   tests/test_bnfuse_gpu.py "tests/test_kernels_gpu.py::test_dense_infer_bf16_weights" \
-  "tests/test_kernels_gpu.py::test_dense_native_matches_fp32"
+  "tests/test_kernels_gpu.py::test_dense_native_matches_fp32" \
+  "tests/test_kernels_gpu.py::test_conv_padded_wgrad_cropped_in_kernel" \
+  "tests/test_kernels_gpu.py::test_conv_channel_padded" "tests/test_kernels_gpu.py::test_conv_search_space_shapes" \
+  "tests/test_kernels_gpu.py::test_conv_fwd_bwd" "tests/test_kernels_gpu.py::test_softmax_xent_dense_bf16" \
+  "tests/test_kernels_gpu.py::test_softmax_xent"
 grep -E "passed|failed" gpurun_out/b5_tests.log | tail -2; grep -E "^FAILED|Error:" gpurun_out/b5_tests.log | head -10
 for a in 1 0 1 0; do
   FN_POOL_BN_APPLY=$a step bench 300 python3 bench.py --steps 30 --warmup 5

@@ -178,6 +178,50 @@ def test_conv_channel_padded(case, monkeypatch):
 
 
 @pytest.mark.parametrize("case", [
+    # LeNet-5 conv1 / conv2 (packed-W gather: C < 8), a channel-padded input (C = 12 -> 16) with
+    # Cout % 8 != 0: (x shape, Cout, kernel, padding)
+    ((16, 1, 32, 32, 3), 6, (1, 5, 5), "valid"),
+    ((16, 1, 14, 14, 6), 16, (1, 5, 5), "valid"),
+    ((4, 6, 7, 8, 5), 12, (1, 1, 7), "same"),
+    ((8, 1, 20, 20, 12), 20, (1, 3, 1), "same"),
+])
+def test_conv_padded_wgrad_cropped_in_kernel(case, monkeypatch):
+    """Weight gradients on the gather kernel written straight into the real [K, taps, C] shape:
+    the epilogue drops the padding columns of the gather layout (packed-W rows, padded input
+    channels) and reads the unpadded dy (no padded dy / dW copies, no fill, no crop copy) --
+    same dW / db as the fp32 oracle."""
+    _native_loaded()
+    import importlib
+
+    convmod = importlib.import_module("featurenet_amd.ops.conv")
+    calls = []
+    real = convmod.igemm_wgrad_cropped
+    def counted(*a, **k):
+        r = real(*a, **k)
+        calls.append(r is not None)
+        return r
+
+    monkeypatch.setattr(convmod, "igemm_wgrad_cropped", counted)
+    shape, K, k, pad = case
+    torch.manual_seed(K * 3 + shape[-1])
+    x = torch.randn(*shape).to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, K, k, 1, pad)
+    w = (torch.randn(K, spec.KD, spec.KH, spec.KW, shape[-1]) * 0.1).to(torch.bfloat16).float()
+    b = torch.randn(K) * 0.1
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = ref.conv(x.float(), wr, br, spec, "relu")
+    wn, bn = w.cuda().requires_grad_(True), b.cuda().requires_grad_(True)
+    yn, _ = convmod.ConvFn.apply(x.cuda(), wn, bn, spec, 1, False)
+    close(yn, yr)
+    g = torch.randn_like(yr).to(torch.bfloat16).float()
+    yr.backward(g)
+    yn.backward(g.cuda().to(torch.bfloat16))
+    close(wn.grad, wr.grad)
+    close(bn.grad, br.grad)
+    assert calls and all(calls), "the cropped weight-gradient path did not run"
+
+
+@pytest.mark.parametrize("case", [
     ((2, 8, 8, 8, 32), 25, "none", True),       # segmentation classifier class: 32 -> 25 (+bias)
     ((4, 1, 14, 14, 24), 48, "relu", True),     # K % 8 == 0, N > 32
     ((2, 1, 8, 9, 6), 40, "none", False),       # 6 input channels: rows straddle 16-B chunks
