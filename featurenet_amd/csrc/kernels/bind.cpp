@@ -50,14 +50,14 @@ int fn_concat2(void*, void*, void*, long long, int, int, int, hipStream_t);
 int fn_pad3(void*, void*, const int*, int, hipStream_t);
 int fn_pad_channels(void*, void*, long long, int, int, int, hipStream_t);
 int fn_dense_fwd(const void*, const void*, const float*, void*, float*, int, int, int, int, int, int, int, hipStream_t);
-int fn_dense_dgrad(const void*, const float*, void*, int, int, int, hipStream_t);
-int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, float*, int, hipStream_t);
+int fn_dense_dgrad(const void*, const float*, void*, int, int, int, hipStream_t, const void*, int);
+int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, float*, int, hipStream_t, const void*, int);
 int fn_dense_wgrad_slices(int, int, int);
 int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
-                   hipStream_t, int, int);
+                   hipStream_t, int, int, const void*, int, float*);
 int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
                 int, int, int, int, hipStream_t);
 int fn_bn_finalize(const float*, int, int, double, const float*, const float*, float*, float*, float, float, float*,
@@ -352,27 +352,32 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("out"), py::arg("part"), py::arg("M"), py::arg("N"),
      py::arg("K"), py::arg("S"), py::arg("act"), py::arg("out_fp32"), py::arg("st"),
      py::arg("ext") = std::vector<long long>(), py::arg("wbf16") = 0);
+  // ya / act: g is dy and the layer's activation backward is applied as it is loaded (ya =
+  // the activation output [M][N], the same extent as g)
   m.def("dense_dgrad", [](uintptr_t g, uintptr_t w, uintptr_t dx, int M, int N, int K, uintptr_t st,
-                          std::vector<long long> ext) {
+                          std::vector<long long> ext, uintptr_t ya, int act) {
     fits(ext, 0, (long long)M * N, "dense_dgrad", "g");
     fits(ext, 1, (long long)N * K, "dense_dgrad", "w");
     fits(ext, 2, (long long)M * K, "dense_dgrad", "dx");
-    chk(fn_dense_dgrad(P<const void*>(g), P<const float*>(w), P<void*>(dx), M, N, K, S(st)), "dense_dgrad");
+    if (ya) fits(ext, 3, (long long)M * N, "dense_dgrad", "ya");
+    chk(fn_dense_dgrad(P<const void*>(g), P<const float*>(w), P<void*>(dx), M, N, K, S(st), P<const void*>(ya), act),
+        "dense_dgrad");
   }, py::arg("g"), py::arg("w"), py::arg("dx"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("st"),
-     py::arg("ext") = std::vector<long long>());
+     py::arg("ext") = std::vector<long long>(), py::arg("ya") = 0, py::arg("act") = 0);
   m.def("dense_wgrad_slices", &fn_dense_wgrad_slices);
   // part: fp32 workspace of S * (N*K + N) elements when S > 1 (dense_wgrad_slices)
   m.def("dense_wgrad", [](uintptr_t g, uintptr_t x, uintptr_t dw, uintptr_t db, int M, int N, int K, uintptr_t st,
-                          std::vector<long long> ext, uintptr_t part, int slices) {
+                          std::vector<long long> ext, uintptr_t part, int slices, uintptr_t ya, int act) {
     fits(ext, 0, (long long)M * N, "dense_wgrad", "g");
     fits(ext, 1, (long long)M * K, "dense_wgrad", "x");
     fits(ext, 2, (long long)N * K, "dense_wgrad", "dw");
     if (slices > 1) fits(ext, 3, (long long)slices * ((long long)N * K + N), "dense_wgrad", "part");
     chk(fn_dense_wgrad(P<const void*>(g), P<const void*>(x), P<float*>(dw), P<float*>(db), M, N, K, P<float*>(part),
-                       slices, S(st)),
+                       slices, S(st), P<const void*>(ya), act),
         "dense_wgrad");
   }, py::arg("g"), py::arg("x"), py::arg("dw"), py::arg("db"), py::arg("M"), py::arg("N"), py::arg("K"),
-     py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("part") = 0, py::arg("slices") = 1);
+     py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("part") = 0, py::arg("slices") = 1,
+     py::arg("ya") = 0, py::arg("act") = 0);
   m.def("s2d_weight_map", [](uintptr_t src, uintptr_t dst, std::vector<int> geom, int dir, uintptr_t st,
                              std::vector<long long> ext) {
     need(geom, 12, "s2d_weight_map");
@@ -488,13 +493,15 @@ PYBIND11_MODULE(_C, m) {
     return fn_conv_halo_lds(geom.data(), ncol);
   });
   m.def("igemm_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t part, uintptr_t tab, std::vector<int> geom,
-                          long long M, int Cout, int K, int splits, int vec, uintptr_t st, int ccrop, int cpad) {
+                          long long M, int Cout, int K, int splits, int vec, uintptr_t st, int ccrop, int cpad,
+                          uintptr_t ya, int act, uintptr_t db) {
     need(geom, 14, "igemm_wgrad");
     chk(fn_igemm_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(part), P<const int*>(tab), geom.data(), M,
-                       Cout, K, splits, vec, S(st), ccrop, cpad),
+                       Cout, K, splits, vec, S(st), ccrop, cpad, P<const void*>(ya), act, P<float*>(db)),
         "igemm_wgrad");
   }, py::arg("dy"), py::arg("src"), py::arg("part"), py::arg("tab"), py::arg("geom"), py::arg("M"), py::arg("Cout"),
-     py::arg("K"), py::arg("splits"), py::arg("vec"), py::arg("st"), py::arg("ccrop") = 0, py::arg("cpad") = 0);
+     py::arg("K"), py::arg("splits"), py::arg("vec"), py::arg("st"), py::arg("ccrop") = 0, py::arg("cpad") = 0,
+     py::arg("ya") = 0, py::arg("act") = 0, py::arg("db") = 0);
   m.def("colstats", [](uintptr_t x, uintptr_t dz, uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd,
                        uintptr_t part, long long M, int C, int act, int mode, int nb, uintptr_t st) {
     chk(fn_colstats(P<const void*>(x), P<const void*>(dz), P<const float*>(scale), P<const float*>(shift),

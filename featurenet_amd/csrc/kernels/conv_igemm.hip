@@ -353,7 +353,7 @@ template <int BCO, int GM, bool VECN>
 __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ src, float* __restrict__ dw,
     const int4* __restrict__ tab, GatherGeom g, long long M, int Cout, int Kdim, long long rows_per_split,
-    int gx, int gy, int ccrop, int cpad) {
+    int gx, int gy, int ccrop, int cpad, const bf16* __restrict__ ya, int act, float* __restrict__ db) {
   constexpr int LDY = WgLds<BCO>::LDY;
   constexpr int X_STAGE = WG_BR * WG_LDX;
   constexpr int Y_STAGE = WG_BR * LDY;
@@ -422,6 +422,14 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
         const bool okc = ok && co < Cout;
         const uint4 v = *(const uint4*)(dy + (okc ? m * Cout + co : 0));
         ry[i] = okc ? v : make_uint4(0, 0, 0, 0);
+        if (ya && okc) {                         // dy * act'(y): the activation backward on load
+          Pack8 p, q;
+          p.u = ry[i];
+          q.u = *(const uint4*)(ya + m * Cout + co);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) p.e[j] = f2bf(bf2f(p.e[j]) * act_bwd_from_out(bf2f(q.e[j]), act));
+          ry[i] = p.u;
+        }
       } else {
         Pack8 p;
 #pragma unroll
@@ -429,6 +437,7 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
           const bool okj = ok && co + j < Cout;
           const bf16 x = dy[okj ? m * Cout + co + j : 0];
           p.e[j] = okj ? x : (bf16)0.f;
+          if (ya && okj) p.e[j] = f2bf(bf2f(p.e[j]) * act_bwd_from_out(bf2f(ya[m * Cout + co + j]), act));
         }
         ry[i] = p.u;
       }
@@ -454,6 +463,11 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  // db (optional): the bias gradient = column sums of (activated) dy, taken from the LDS dy tile by
+  // the first column-tile's workgroups (one thread per output channel), one atomic per channel
+  // and workgroup into the zeroed db -- no separate column-sum pass
+  const bool dsum = db != nullptr && bx == 0 && tid < BCO;
+  float dbs = 0.f;
   const long long nst = (mend - mbeg + WG_BR - 1) / WG_BR;
   if (nst > 0) {
     load_stage(mbeg);
@@ -462,6 +476,8 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
   __syncthreads();
   for (long long s = 0; s < nst; ++s) {
     const bool more = s + 1 < nst;
+    if (dsum)
+      for (int row = 0; row < WG_BR; ++row) dbs += bf2f(Ys[row * LDY + tid]);
     if (more) load_stage(mbeg + (s + 1) * WG_BR);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -487,6 +503,7 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
   // Split-m partial sums are folded straight into the fp32 dW with no-return
   // float atomics (S x Cout x Kdim x 4 B of atomic traffic, well under the
   // ~1.3 TB/s chip-wide atomic rate for the split counts used).
+  if (dsum && co0 + tid < Cout) atomicAdd(db + co0 + tid, dbs);
   // ccrop > 0: k = t*cpad + c lands at dw[co][t*ccrop + c] of the real weight, columns
   // c >= ccrop dropped -- the zero channels of a channel-padded input (cpad = its channels,
   // ccrop = the real ones) or the row padding of the packed-W layout (cpad = R, ccrop = KW*C):
@@ -577,9 +594,12 @@ extern "C" int fn_igemm_fwd_mblocks(long long M) { return (int)((M + FWD_BM - 1)
 
 // ccrop > 0: dw is the real [Cout][Kdim / cpad][ccrop] weight gradient; column t*cpad + c of the
 // gather layout (c < ccrop) maps to t*ccrop + c (channel-padded inputs; the packed-W rows)
+// ya / act (optional): dy is the gradient of the activation output ya (the activation backward
+// is applied as dy is loaded); db (optional, zeroed): receives the bias gradient (column sums of
+// the activated dy)
 extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const int* tab, const int* geom14,
                               long long M, int Cout, int Kdim, int splits, int gm, hipStream_t st, int ccrop,
-                              int cpad) {
+                              int cpad, const void* ya, int act, float* db) {
   const GatherGeom g = parse_geom(geom14);
   if (ccrop > 0 && (cpad < ccrop || Kdim % cpad)) return -2;
   const int BCO = Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64);
@@ -592,7 +612,7 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const 
   const int4* t = (const int4*)tab;
 #define WG_CASE(B, V, VN) \
   hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, dw, t, g, M, Cout, Kdim, rps, gx, gy, \
-                     ccrop, cpad)
+                     ccrop, cpad, (const bf16*)ya, act, db)
 #define WG_GM(GMV)                                                                        \
   do {                                                                                    \
     if (vecn) {                                                                           \

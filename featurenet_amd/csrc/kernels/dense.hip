@@ -9,7 +9,8 @@
 //                   bf16 W copy (inference), fp32 partial slabs [S][M][N]; 128x64 or 128x128
 //                   output tile per workgroup, 4 or 8 waves x (32 rows x 64 cols), operands
 //                   straight from global (16-B loads, no LDS)
-//   dense_fwd_reduce  y = act(sum_s part[s] + b) -> bf16 or fp32 (one pass over M*N)
+//   dense_fwd_reduce  y = act(sum_s part[s] + b) -> bf16 or fp32 (one pass over M*N); with one
+//                   slice the partial kernel's epilogue writes y itself (no slab, no reduction)
 //   dense_dgrad     dx [M][K] = g [M][N] W [N][K] -> bf16.  C^T form: A = W^T from an LDS
 //                   tile written transposed ([kk][n], converted to bf16), B = g rows from
 //                   global; a lane ends with 4 consecutive kk of one row (8-B stores)
@@ -46,11 +47,14 @@ __device__ __forceinline__ bf16x8 dn_cvt8(const float4 a, const float4 b) {
 // conversion), else the fp32 master weights converted on the fly.  D k-steps of raw operands
 // in flight (a register ring): with one step ahead the loop waited a full memory latency per
 // 32-k step (FC1 at 128^3 inference: 1100 steps per slice)
-template <bool VEC, int D, bool WB, int NCW>
+// FINAL (one slice, gridDim.z == 1): the epilogue writes y = act(acc + b) itself (bf16 or fp32)
+// -- no partial slab and no reduction launch (the small Dense layers of NAS candidates)
+template <bool VEC, int D, bool WB, int NCW, bool FINAL = false>
 __global__ __launch_bounds__(DN_THREADS * NCW) void dense_fwd_part_kernel(const bf16* __restrict__ x,
                                                                           const void* __restrict__ wv,
                                                                           float* __restrict__ part, int M, int N,
-                                                                          int K, int kc) {
+                                                                          int K, int kc, const float* __restrict__ bias,
+                                                                          int act, int out_fp32) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, gq = lane >> 4;
   const int row0 = blockIdx.y * 128 + (wave & 3) * 32, col0 = (blockIdx.x * NCW + (wave >> 2)) * 64;
@@ -156,6 +160,25 @@ __global__ __launch_bounds__(DN_THREADS * NCW) void dense_fwd_part_kernel(const 
       }
     }
   }
+  if constexpr (FINAL) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = col0 + j * 16 + r;
+      const float b = (bias && n < N) ? bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = row0 + i * 16 + 4 * gq + q;
+          if (m < M && n < N) {
+            const float v = act_fwd(acc[i][j][q] + b, act);
+            if (out_fp32) ((float*)part)[(long long)m * N + n] = v;
+            else ((bf16*)part)[(long long)m * N + n] = f2bf(v);
+          }
+        }
+    }
+    return;
+  }
   float* ps = part + (long long)blockIdx.z * M * N;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -215,9 +238,12 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_reduce_kernel(const floa
 // is padded to NP = ceil(N/32)*32 with zero weights; g rows load as 16-B vectors when N % 8 == 0,
 // element-wise otherwise -- the 10 / 24 / 84-wide NAS heads).
 // LDS (dynamic): W tile transposed to [64 kk][NP + 8] bf16.
+// ya (optional): the layer's activation output -- g is then dy * act'(y) (the activation
+// backward applied as g is loaded, no separate pass)
 __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __restrict__ g,
                                                                  const float* __restrict__ w,
-                                                                 bf16* __restrict__ dx, int M, int N, int K) {
+                                                                 bf16* __restrict__ dx, int M, int N, int K,
+                                                                 const bf16* __restrict__ ya, int act) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
   const int NP = (N + 31) & ~31;
   const int LDN = NP + 8;                        // row pitch (bf16): 16-B aligned rows, bank shift
@@ -267,6 +293,12 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = nc + e < N ? grow[nc + e] : f2bf(0.f);
       }
+      if (ya) {
+        const bf16* yrow = ya + (long long)(m < M ? m : 0) * N;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (nc + e < N) v[e] = f2bf(bf2f(v[e]) * act_bwd_from_out(bf2f(yrow[nc + e]), act));
+      }
       acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, m < M ? v : zero8, acc[j], 0, 0, 0);
     }
   }
@@ -297,7 +329,8 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
 __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __restrict__ g,
                                                                  const bf16* __restrict__ x,
                                                                  float* __restrict__ dw, float* __restrict__ db,
-                                                                 int M, int N, int K, int mc) {
+                                                                 int M, int N, int K, int mc,
+                                                                 const bf16* __restrict__ ya, int act) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
   // split over the batch (blockIdx.z = slice of mc rows -> its own dW / db slab, summed by
   // dense_wgrad_reduce_kernel in a fixed order) so small dW tiles still fill the GPU
@@ -339,6 +372,10 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
           vg.u = *(const uint4*)(g + (long long)m * N + n);
         } else {
           for (int e = 0; e < 8; ++e) vg.e[e] = n + e < N ? g[(long long)m * N + n + e] : f2bf(0.f);
+        }
+        if (ya) {                                // g = dy * act'(y) (see dense_dgrad_kernel)
+          for (int e = 0; e < 8; ++e)
+            if (n + e < N) vg.e[e] = f2bf(bf2f(vg.e[e]) * act_bwd_from_out(bf2f(ya[(long long)m * N + n + e]), act));
         }
       }
 #pragma unroll
@@ -393,16 +430,29 @@ extern "C" int fn_dense_splits(int M, int N, int K) {
   return S < 1 ? 1 : (S > maxS ? maxS : S);
 }
 
-template <bool WB, int NCW>
-static void dn_fwd_part(const void* x, const void* w, float* part, int M, int N, int K, int kc, int Sr,
-                        hipStream_t st) {
+template <bool WB, int NCW, bool FINAL>
+static void dn_fwd_part(const void* x, const void* w, void* part, int M, int N, int K, int kc, int Sr,
+                        const float* bias, int act, int out_fp32, hipStream_t st) {
   const dim3 grid((N + 64 * NCW - 1) / (64 * NCW), (M + 127) / 128, Sr), blk(DN_THREADS * NCW);
   if (K % 8 == 0)
-    hipLaunchKernelGGL((dense_fwd_part_kernel<true, 4, WB, NCW>), grid, blk, 0, st, (const bf16*)x, w, part, M, N,
-                       K, kc);
+    hipLaunchKernelGGL((dense_fwd_part_kernel<true, 4, WB, NCW, FINAL>), grid, blk, 0, st, (const bf16*)x, w,
+                       (float*)part, M, N, K, kc, bias, act, out_fp32);
   else
-    hipLaunchKernelGGL((dense_fwd_part_kernel<false, 1, WB, NCW>), grid, blk, 0, st, (const bf16*)x, w, part, M, N,
-                       K, kc);
+    hipLaunchKernelGGL((dense_fwd_part_kernel<false, 1, WB, NCW, FINAL>), grid, blk, 0, st, (const bf16*)x, w,
+                       (float*)part, M, N, K, kc, bias, act, out_fp32);
+}
+
+template <bool WB, int NCW>
+static void dn_fwd(const void* x, const void* w, const float* bias, void* out, float* part, int M, int N, int K,
+                   int kc, int Sr, int act, int out_fp32, hipStream_t st) {
+  if (Sr == 1) {                                 // one slice: bias + activation in the epilogue
+    dn_fwd_part<WB, NCW, true>(x, w, out, M, N, K, kc, 1, bias, act, out_fp32, st);
+    return;
+  }
+  dn_fwd_part<WB, NCW, false>(x, w, part, M, N, K, kc, Sr, nullptr, 0, 0, st);
+  const long long tot = (long long)M * N;
+  hipLaunchKernelGGL(dense_fwd_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(DN_THREADS), 0, st,
+                     (const float*)part, bias, out, M, N, Sr, act, out_fp32);
 }
 
 // w: fp32 [N][K] (training: the master weights) or, wbf16, a bf16 copy (inference)
@@ -414,16 +464,12 @@ extern "C" int fn_dense_fwd(const void* x, const void* w, const float* bias, voi
   const int Sr = (K + kc - 1) / kc;              // slices actually covering K
   const int ncw = dn_ncw(N);
   if (wbf16) {
-    if (ncw == 2) dn_fwd_part<true, 2>(x, w, part, M, N, K, kc, Sr, st);
-    else dn_fwd_part<true, 1>(x, w, part, M, N, K, kc, Sr, st);
+    if (ncw == 2) dn_fwd<true, 2>(x, w, bias, out, part, M, N, K, kc, Sr, act, out_fp32, st);
+    else dn_fwd<true, 1>(x, w, bias, out, part, M, N, K, kc, Sr, act, out_fp32, st);
   } else {
-    if (ncw == 2) dn_fwd_part<false, 2>(x, w, part, M, N, K, kc, Sr, st);
-    else dn_fwd_part<false, 1>(x, w, part, M, N, K, kc, Sr, st);
+    if (ncw == 2) dn_fwd<false, 2>(x, w, bias, out, part, M, N, K, kc, Sr, act, out_fp32, st);
+    else dn_fwd<false, 1>(x, w, bias, out, part, M, N, K, kc, Sr, act, out_fp32, st);
   }
-  FN_CHECK_LAUNCH();
-  const long long tot = (long long)M * N;
-  hipLaunchKernelGGL(dense_fwd_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(DN_THREADS), 0, st,
-                     (const float*)part, bias, out, M, N, Sr, act, out_fp32);
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -433,13 +479,15 @@ static int dn_lds_attr(const void* fn, size_t lds) {
   return (int)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
-extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, int N, int K, hipStream_t st) {
+// ya / act: see dense_dgrad_kernel (null: g is the gradient itself)
+extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, int N, int K, hipStream_t st,
+                              const void* ya, int act) {
   if (M <= 0 || K <= 0 || N <= 0 || K % 4) return -2;
   const size_t lds = (size_t)64 * (((N + 31) & ~31) + 8) * 2;
   if (lds > 160 * 1024) return -4;
   if (int e = dn_lds_attr((const void*)dense_dgrad_kernel, lds)) return e;
   hipLaunchKernelGGL(dense_dgrad_kernel, dim3((K + 63) / 64, (M + 63) / 64), dim3(DN_THREADS), lds, st,
-                     (const bf16*)g, w, (bf16*)dx, M, N, K);
+                     (const bf16*)g, w, (bf16*)dx, M, N, K, (const bf16*)ya, act);
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -465,7 +513,7 @@ extern "C" int fn_dense_wgrad_slices(int M, int N, int K) {
 
 // part: fp32 [S][N*K] + [S][N] workspace when S > 1 (fn_dense_wgrad_slices), else unused
 extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db, int M, int N, int K, float* part,
-                              int S, hipStream_t st) {
+                              int S, hipStream_t st, const void* ya, int act) {
   if (M <= 0 || N <= 0 || K <= 0 || S < 1 || (S > 1 && !part)) return -2;
   int mc = (M + S - 1) / S;
   mc = (mc + 31) & ~31;
@@ -478,7 +526,7 @@ extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db
   float* pdw = S > 1 ? part : dw;
   float* pdb = S > 1 ? (db ? part + (long long)S * NK : nullptr) : db;
   hipLaunchKernelGGL(dense_wgrad_kernel, dim3((K + 63) / 64, (N + 63) / 64, S), dim3(DN_THREADS), lds, st,
-                     (const bf16*)g, (const bf16*)x, pdw, pdb, M, N, K, mc);
+                     (const bf16*)g, (const bf16*)x, pdw, pdb, M, N, K, mc, (const bf16*)ya, act);
   FN_CHECK_LAUNCH();
   if (S > 1) {
     hipLaunchKernelGGL(dense_wgrad_reduce_kernel, dim3((unsigned)((NK + 255) / 256 < 2048 ? (NK + 255) / 256 : 2048)),

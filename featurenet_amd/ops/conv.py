@@ -522,16 +522,26 @@ def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=N
     return dw.contiguous()
 
 
-def igemm_wgrad_cropped(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, c0: int, out=None):
+def igemm_wgrad_takes(spec: ConvSpec) -> bool:
+    """The weight gradient of ``spec`` (and of its 8-padded-Cout form) runs on the gather kernel
+    (no halo / tile weight-gradient plan)."""
+    sk = dataclasses.replace(spec, K=-(-spec.K // 8) * 8)
+    return all(p is None for p in (halo_wgrad_plan(spec), conv_wtile.plan(spec), halo_wgrad_plan(sk),
+                                   conv_wtile.plan(sk)))
+
+
+def igemm_wgrad_cropped(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, c0: int, out=None, ya=None,
+                        act: int = 0, bias_param=None, with_db: bool = False):
     """fp32 dW [K, KD, KH, KW, c0] on the gather kernel, accumulated straight into ``out``
     (zeroed, e.g. the parameter's flat gradient) with every padding column of the gather
     layout dropped in the epilogue: the zero channels c0..spec.C of a channel-padded input,
     or the row padding of the packed-W layout (C < 8: rows of KW*C rounded up to 8).
-    ``dy5`` has the real ``spec.K`` channels (any count, no padded copy).  None when the
+    ``dy5`` has the real ``spec.K`` channels (any count, no padded copy).  ``ya`` / ``act``: dy5
+    is the gradient of the activation output ``ya`` (the activation backward runs as dy is
+    loaded); ``with_db``: the bias gradient from the same dy tiles too, into ``bias_param``'s
+    zeroed flat-gradient slot when it offers one -- returns ``(dW, db)`` then.  None when the
     shape belongs to another weight-gradient kernel."""
-    sk = dataclasses.replace(spec, K=-(-spec.K // 8) * 8)        # (what the padded path would run)
-    if any(p is not None for p in (halo_wgrad_plan(spec), conv_wtile.plan(spec), halo_wgrad_plan(sk),
-                                   conv_wtile.plan(sk))):
+    if not igemm_wgrad_takes(spec):
         return None
     gm = gather_mode(spec)
     if spec.C < c0:
@@ -550,9 +560,14 @@ def igemm_wgrad_cropped(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, c0:
         out = torch.zeros(shape, dtype=torch.float32, device=x5.device)
     tab = _table(spec, "fwd", gm, x5.device)
     dy5, x5 = dy5.contiguous(), x5.contiguous()
+    if ya is not None:
+        ya = ya.contiguous()
+        assert ya.dtype == torch.bfloat16 and ya.numel() == dy5.numel()
+    db = _zeroed_grad(bias_param, spec.K, x5.device) if with_db else None
     _native.kernels().igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), out.data_ptr(), tab.data_ptr(), _geom_fwd(spec),
-                                  spec.M, spec.K, kd, wgrad_splits(spec), gm, _native.stream(x5), ccrop, cpad)
-    return out
+                                  spec.M, spec.K, kd, wgrad_splits(spec), gm, _native.stream(x5), ccrop, cpad,
+                                  _native.ptr(ya), act if ya is not None else 0, _native.ptr(db))
+    return (out, db) if with_db else out
 
 
 def native_colsum(x2: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -752,34 +767,53 @@ def pad_weight(w: torch.Tensor, cin: int | None = None, cout: int | None = None)
     return F.pad(w, (0, pc, 0, 0, 0, 0, 0, 0, 0, pk))
 
 
-def _conv_bwd_padded(ctx, dy, xs, w, spec):
+def _zeroed_grad(p, n: int, device) -> torch.Tensor:
+    """The parameter's zeroed flat-gradient slot, or a zeroed fp32 buffer of ``n``."""
+    t = grad_target(p)
+    return t if t is not None else torch.zeros(n, dtype=torch.float32, device=device)
+
+
+def _conv_bwd_padded(ctx, dy, xs, w, spec, y=None):
     """ConvFn backward for channel-padded convs: ``xs`` is the (possibly channel-padded)
     saved input, ``spec`` its spec; dy (already through the activation backward) is padded
     to a multiple of 8 output channels when Cout % 8 != 0, the weight gets matching zero
-    rows / columns, and the gradients are cropped back to the real channels."""
+    rows / columns, and the gradients are cropped back to the real channels.  ``y`` (the
+    activation output, first layers only): dy is still pre-activation-backward, and the gather
+    weight-gradient kernel applies it (and sums the bias gradient) as it loads dy."""
     C0 = w.shape[-1]
     K0 = spec.K
     kp = -(-K0 // 8) * 8
     sk = dataclasses.replace(spec, K=kp)
     dyp = None
-    dx = dw = None
+    dx = dw = db = None
     if ctx.x_needs:                                              # real input channels: dx has C0 columns
         dyp = pad_channels(dy, kp)
         dx = native_conv_dgrad(dyp, w.detach(), dataclasses.replace(sk, C=C0))   # (zero rows K0..kp)
+    want_db = ctx.has_b and ctx.needs_input_grad[2]
+    if y is not None and not ctx.needs_input_grad[1]:
+        dy, y = native_act_bwd(dy, y, ctx.act), None
     if ctx.needs_input_grad[1]:
         tgt = grad_target(w)
+        if y is not None and not (kp != K0 or spec.C != C0):
+            dy, y = native_act_bwd(dy, y, ctx.act), None
         if kp != K0 or spec.C != C0:
             # the gather kernel drops the padded channels itself and reads the unpadded dy
-            dw = igemm_wgrad_cropped(dy, xs, spec, C0, out=tgt)
+            r = igemm_wgrad_cropped(dy, xs, spec, C0, out=tgt, ya=y, act=ctx.act if y is not None else 0,
+                                    bias_param=ctx.bparam, with_db=want_db)
+            if r is not None:
+                dw, db = r if want_db else (r, None)
             if dw is None:
+                if y is not None:                # (the fused activation backward did not run)
+                    dy = native_act_bwd(dy, y, ctx.act)
+                    y = None
                 dyp = pad_channels(dy, kp) if dyp is None else dyp
                 dwp = native_conv_wgrad(dyp, xs.contiguous(), sk)     # [kp, KD, KH, KW, spec.C]
                 dw = tgt.copy_(dwp[:K0, ..., :C0]) if tgt is not None else dwp[:K0, ..., :C0].contiguous()
         else:
             dyp = pad_channels(dy, kp) if dyp is None else dyp
             dw = native_conv_wgrad(dyp, xs.contiguous(), sk, out=tgt)
-    db = (native_colsum(dy.reshape(-1, K0), out=grad_target(ctx.bparam))
-          if (ctx.has_b and ctx.needs_input_grad[2]) else None)
+    if want_db and db is None:
+        db = native_colsum(dy.reshape(-1, K0), out=grad_target(ctx.bparam))
     return dx, dw, db, None, None, None
 
 
@@ -850,16 +884,22 @@ class ConvFn(torch.autograd.Function):
         x5, w, y = ctx.saved_tensors
         spec, act = ctx.spec, ctx.act
         dy = dy.contiguous().to(torch.bfloat16)
-        if act:
+        padded = ctx.cpad or (spec.K % 8 and ctx.s2d is None)
+        # the gather weight-gradient kernel is dy's only consumer (no input gradient: a first
+        # layer): it applies the activation backward and sums the bias gradient as it loads dy
+        wg_igemm = (not ctx.pw and ctx.s2d is None and ctx.needs_input_grad[1] and igemm_wgrad_takes(spec)
+                    and (not padded or ctx.cpad or spec.C == w.shape[-1]))
+        fuse_act = bool(act) and wg_igemm and not ctx.x_needs
+        if act and not fuse_act:
             dy = native_act_bwd(dy, y, act)
+        if padded:
+            return _conv_bwd_padded(ctx, dy, x5, w, spec, y=y if fuse_act else None)
         if ctx.pw:
             dy2, x2 = dy.reshape(-1, spec.K), x5.reshape(-1, spec.C)
             dx = pw_fwd(dy2, w.detach().reshape(spec.K, spec.C).t(), None, 0).reshape(x5.shape) if ctx.x_needs else None
             dw = pw_wgrad(dy2, x2, out=grad_target(w)).reshape(w.shape) if ctx.needs_input_grad[1] else None
             db = native_colsum(dy2, out=grad_target(ctx.bparam)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
             return dx, dw, db, None, None, None
-        if ctx.cpad or (spec.K % 8 and ctx.s2d is None):
-            return _conv_bwd_padded(ctx, dy, x5, w, spec)
         dx = None
         if ctx.x_needs:
             if ctx.bn_src is not None:
@@ -869,16 +909,27 @@ class ConvFn(torch.autograd.Function):
                 ctx.bn_src = None
             else:
                 dx = native_conv_dgrad(dy, w.detach(), spec)
-        dw = None
+        dw = db = None
+        want_db = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             if ctx.s2d is not None:      # x5 is the space-to-depth packed input (saved by forward)
                 f, spec2 = ctx.s2d
                 dw = s2d_weight_grad(native_conv_wgrad(dy, x5, spec2), f, spec, out=grad_target(w))
+            elif wg_igemm:               # (+ the bias gradient, + the activation backward if fused)
+                tgt = grad_target(w)
+                r = igemm_wgrad_cropped(dy, x5, spec, spec.C, out=tgt, ya=y if fuse_act else None,
+                                        act=act if fuse_act else 0, bias_param=ctx.bparam, with_db=want_db)
+                if r is not None:
+                    dw, db = r if want_db else (r, None)
+                else:                    # (not taken after all: the separate passes)
+                    if fuse_act:
+                        dy = native_act_bwd(dy, y, act)
+                    dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=tgt)
             else:
                 # straight into the parameter's zeroed flat gradient when FlatParams offers it
                 dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w))
-        db = (native_colsum(dy.reshape(-1, spec.K), out=grad_target(ctx.bparam))
-              if (ctx.has_b and ctx.needs_input_grad[2]) else None)
+        if want_db and db is None:
+            db = native_colsum(dy.reshape(-1, spec.K), out=grad_target(ctx.bparam))
         return dx, dw, db, None, None, None
 
 

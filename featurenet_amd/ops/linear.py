@@ -75,21 +75,31 @@ class LinearFn(torch.autograd.Function):
         M, K = x2.shape
         N = w.shape[0]
         g = dy.reshape(M, N).to(torch.bfloat16).contiguous()
+        wf = w.detach()
+        NP = -(-N // 32) * 32                          # (any N: the dgrad kernel pads its k dim to 32)
+        dgrad_native = _NATIVE and K % 4 == 0 and wf.dtype == torch.float32 and 64 * (NP + 8) * 2 <= 160 * 1024
+        # the activation backward inside the dgrad / wgrad kernels (g = dy * act'(y) as they load
+        # it) when both run natively and the wgrad kernel produces db: no separate pass
+        ya = None
         if ctx.act:
-            g2 = torch.empty_like(g)
-            _native.kernels().act_bwd(g.data_ptr(), y.reshape(M, N).to(torch.bfloat16).contiguous().data_ptr(),
-                                      g2.data_ptr(), g.numel(), ctx.act, _native.stream(g))
-            g = g2
+            if (_NATIVE and ctx.needs_input_grad[1] and (dgrad_native or not ctx.needs_input_grad[0])
+                    and y.dtype == torch.bfloat16):
+                ya = y.reshape(M, N).contiguous()
+            else:
+                g2 = torch.empty_like(g)
+                _native.kernels().act_bwd(g.data_ptr(), y.reshape(M, N).to(torch.bfloat16).contiguous().data_ptr(),
+                                          g2.data_ptr(), g.numel(), ctx.act, _native.stream(g))
+                g = g2
+        yp, yact = (_native.ptr(ya), ctx.act) if ya is not None else (0, 0)
         Kn = _native.kernels()
         st = _native.stream(g)
-        wf = w.detach()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            NP = -(-N // 32) * 32                      # (any N: the kernel pads its k dim to 32)
-            if _NATIVE and K % 4 == 0 and wf.dtype == torch.float32 and 64 * (NP + 8) * 2 <= 160 * 1024:
+            if dgrad_native:
                 dx = torch.empty(M, K, dtype=torch.bfloat16, device=g.device)
                 Kn.dense_dgrad(g.data_ptr(), wf.data_ptr(), dx.data_ptr(), M, N, K, st,
-                               [g.numel(), wf.numel(), dx.numel()])
+                               [g.numel(), wf.numel(), dx.numel()] + ([ya.numel()] if ya is not None else []), yp,
+                               yact)
             else:
                 dx = torch.matmul(g, wf.to(torch.bfloat16))
             dx = dx.reshape(ctx.xshape)
@@ -107,7 +117,7 @@ class LinearFn(torch.autograd.Function):
                 part = torch.empty(S * (N * K + N), dtype=torch.float32, device=g.device) if S > 1 else None
                 Kn.dense_wgrad(g.data_ptr(), x2.data_ptr(), dw.data_ptr(), _native.ptr(db), M, N, K, st,
                                [g.numel(), x2.numel(), dw.numel()] + ([part.numel()] if S > 1 else []),
-                               _native.ptr(part), S)
+                               _native.ptr(part), S, yp, yact)
             else:
                 dw = _wgrad_torch(g, x2)
         if want_b and db is None:
