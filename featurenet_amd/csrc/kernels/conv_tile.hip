@@ -50,17 +50,17 @@
 //   32, CPP = 2 chunks of 16 channels) or tap 2ks+lg/2 x channels 32(lg&1).. (CS = 64, CPP =
 //   4); the epilogue dequantises (acc * scale[co] + bias[co]), applies ReLU and stores bf16
 //   or re-quantised e4m3 (x oscale).
-// BWS: the dgrad instance with the BN-backward statistics epilogue (its own register
-// allocation: the extra epilogue operands must not cost the other instances registers)
 // Q8O: the bf16 instance with an e4m3 output epilogue (fp8 inference: the bf16 stem writes the
-// fp8 layers' input; its own register allocation, like BWS)
+// fp8 layers' input; its own register allocation)
+// (The BN-backward statistics epilogue for dgrad -- the statistics of the BN whose output this
+// conv consumed -- lives in conv_tile32_kernel only: on this kernel it measured 5.37 vs 5.00 ms
+// per step in round 4 and 5.14 vs 4.80 in round 3, and was removed.)
 // I8 (with F8: the fp8 kernel's 32-byte fragments holding int8 instead): two
 //   v_mfma_i32_16x16x64_i8 per fragment pair (bytes 0-15 and 16-31 of every lane: A and B split
 //   the same way, so the k sum is complete), exact int32 accumulation, converted to float in
 //   the epilogue before the dequantisation -- the binary-voxel stem of the fp8 inference path
 //   (0/1 inputs are exact; per-channel int8 weights keep ~8 bits, where e4m3 kept 4).
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false, bool Q8O = false,
-          bool I8 = false>
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false>
 __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
@@ -70,9 +70,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                                                                float* __restrict__ stats, TileGeom g, int Ncol,
                                                                int act, int* __restrict__ sched,
                                                                long long* __restrict__ stamps,
-                                                               const float* __restrict__ scale, float oscale,
-                                                               const bf16* __restrict__ bny,
-                                                               const float* __restrict__ bnp) {
+                                                               const float* __restrict__ scale, float oscale) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int PD = ct_pd(NT, F8);
   constexpr int ESZ = F8 ? 1 : 2;                // bytes per element of the source / weights
@@ -109,9 +107,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   int2* s_pos = reinterpret_cast<int2*>(s_kt + (nks + PD + 2));
   for (int i = tid; i < nks + PD + 2; i += CT_NTHR) s_kt[i] = ktab[i];
   for (int i = tid; i < ct_red_bytes(NT) / 4; i += CT_NTHR) s_red[i] = 0.f;
-  // BWS: the BN's (scale, shift, mean, invstd) of this workgroup's 32 columns, read per use by
-  // the epilogue (no live registers across the k-loop)
-  float4* s_bn = reinterpret_cast<float4*>(s_pos + g.HPpad);
   // F8: the dequantisation scale and bias of this workgroup's 32 columns ([scale 32][bias 32]),
   // read by the epilogue from LDS (global loads there serialised every tile's stores)
   float* s_sb = reinterpret_cast<float*>(s_pos + g.HPpad);
@@ -120,13 +115,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       const int c = blockIdx.y * NT * 16 + tid;
       s_sb[tid] = c < Ncol ? scale[c] : 0.f;
       s_sb[NT * 16 + tid] = (bias && c < Ncol) ? bias[c] : 0.f;
-    }
-  }
-  if constexpr (BWS) {
-    if (tid < NT * 16) {
-      const int c = blockIdx.y * NT * 16 + tid;
-      s_bn[tid] = c < Ncol ? make_float4(bnp[2 * Ncol + c], bnp[3 * Ncol + c], bnp[c], bnp[Ncol + c])
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
   for (int p = tid; p < g.HPpad; p += CT_NTHR) {  // positions past HP repeat the last one
@@ -239,7 +227,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     const int gc8 = ct0 * 16 + NV * lg;
     float bias8[8];                              // (fp8: read in the epilogue from LDS, no live
 #pragma unroll                                   // registers across the k-loop)
-    for (int j = 0; j < 8; ++j) bias8[j] = (!F8 && !BWS && bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
+    for (int j = 0; j < 8; ++j) bias8[j] = (!F8 && bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
     constexpr unsigned FTILE = 64u * FRAG;       // bytes of one 16-column fragment of a k-step
     const unsigned wstep = (unsigned)g.nct * FTILE;   // bytes per k-step of the packed weights
     unsigned voffb[PD];                          // per-lane B offsets of the PD ring slots
@@ -271,13 +259,20 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     auto kofs = [&](int k) -> int { return *((const int*)(s_kt + k) + lg); };
     // epilogue variant (wave-uniform); columns come in whole 8-column groups (Ncol % 8 == 0)
     // (fp8: bit 0 relu, bit 1 fp8 output)
-    // bf16 with bny (dgrad of the conv that consumes a BN+act output): bit 2, and bit 1 is the
-    // BN's relu (the stored dx itself has no activation)
     // (fp8: act bit CT_F8_POOL = the 2^3 max-pool epilogue, relu + bf16 output of the pooled grid)
     const int emode = F8 ? (((act & 0xff) == ACT_RELU ? 1 : 0) | (oscale > 0.f ? 2 : 0) | ((act & CT_F8_POOL) ? 4 : 0))
-                         : (BWS ? (4 | ((act & 0xff) == ACT_RELU ? 2 : 0))
-                                : ((stats ? 1 : 0) | ((act & 0xff) == ACT_RELU ? 2 : 0) | (Q8O ? 8 : 0)));   // (ACT_NONE /
+                         : ((stats ? 1 : 0) | ((act & 0xff) == ACT_RELU ? 2 : 0) | (Q8O ? 8 : 0));   // (ACT_NONE /
                                                                                           // ACT_RELU only; 8: e4m3 out)
+    // BN partial sums of this lane's columns over every tile the workgroup runs (the epilogues
+    // add into them; one DPP + LDS reduction after the last tile instead of one per tile:
+    // stem fwd epilogue ~40 % of its cycles in round 4 stamps).  MT = 9 keeps the per-tile
+    // reduction (16 more live registers made it spill)
+    constexpr bool RSACC = MT <= 8;
+    float rsum[NT / 2][8], rsq[NT / 2][8];
+#pragma unroll
+    for (int h = 0; h < NT / 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rsum[h][j] = rsq[h][j] = 0.f;
     // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
     // the previous job's last turn, so no job starts on an exposed L2 latency
 #pragma unroll
@@ -331,11 +326,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             if constexpr (!(DBG & 2)) fa[mt] = read_a(mt, ko);
             if constexpr (!(DBG & 128)) __builtin_amdgcn_sched_barrier(0);   // (DBG 128: free scheduling
           }                                                                  //  within a k-step)
-          // k-step ks+u+PD, or the next job's step u (BWS: not before an epilogue -- the ring
-          // registers are the statistics epilogue's; it refills the ring after the stores)
-          if constexpr (!(DBG & 1)) {
-            if (!BWS || slice != nslice - 1 || ks + PD < nks) load_b(wl, u);
-          }
+          // k-step ks+u+PD, or the next job's step u
+          if constexpr (!(DBG & 1)) load_b(wl, u);
           __builtin_amdgcn_sched_barrier(0);
         }
         wbase += PD * wstep;
@@ -358,16 +350,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
         // unrolled per-tile loop made hipcc emit ~1000 basic blocks
         auto epilogue = [&](auto mode) {
           // bit 0: forward BN statistics (sum v, sum v^2) of the stored values; bit 1: relu.
-          // bit 2: BN-BACKWARD statistics of the layer whose BN+act output fed this conv: the
-          // stored dx is that layer's dz, so with its pre-BN y (bny, same layout) and scale /
-          // shift (bnp rows 2, 3) the tile sums g = dz * act'(z) and g * y (bn_finalize MODE 2
-          // centres them: sum g*xhat = invstd * (sum g*y - mean * sum g)) -- the colstats pass
-          // over dz and y disappears; bit 1 is then the BN's relu and dx is stored without
-          // activation
           constexpr int M = decltype(mode)::value;
-          constexpr bool BW = (M & 4) != 0;
-          constexpr bool RELU_OUT = !BW && (M & 2) != 0;
-          constexpr bool ST = BW || (M & 1) != 0;
+          constexpr bool RELU_OUT = (M & 2) != 0;
+          constexpr bool ST = (M & 1) != 0;
           // bit 3: e4m3 output of v * oscale (saturated; fp8 inference: the bf16 stem writes the
           // fp8 layers' input directly), 8-B stores; no statistics
           constexpr bool Q8 = (M & 8) != 0;
@@ -378,35 +363,15 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             if (edge) ok = ok && (rpk[mt] >> 16) < ld && ((rpk[mt] >> 8) & 255) < lh && (rpk[mt] & 255) < lw;
             okm[mt] = ok;
           }
-          // BW: the BN input y at the tile's positions, loaded in two halves of the row blocks
-          // (16 registers), and the BN's scale / shift (the relu mask); the sums are the raw
-          // moments (sum g, sum g*y), centred by the finalize step
-          constexpr int MH = (MT + 1) / 2;
-          uint4 yb[BW ? MH : 1];
-          float bsc[BW ? 8 : 1], bsh[BW ? 8 : 1];
-          auto load_y = [&](int m0) {
-#pragma unroll
-            for (int i = 0; i < MH; ++i)
-              if (m0 + i < MT)
-                yb[i] = okm[m0 + i] ? *(const uint4*)(bny + obase_e + (long long)roff[m0 + i] * Ncol)
-                                    : make_uint4(0u, 0u, 0u, 0u);
-          };
-          if constexpr (BW) {
-            load_y(0);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float4 q = s_bn[8 * lg + j];
-              bsc[j] = q.x;
-              bsh[j] = q.y;
-            }
-          }
           // one pass per 8 consecutive columns of the lane (fragments 2h, 2h+1): one 16-B store
-          // per row and 8 + 8 live partial sums
+          // per row; the BN partial sums go into the lane's running sums (rsum / rsq)
 #pragma unroll
           for (int h = 0; h < NT / 2; ++h) {
-            float ts[8], tq[8];                  // this tile's BN partial sums of the pass's 8 columns
+            float tsl[8], tql[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) ts[j] = tq[j] = 0.f;
+            for (int j = 0; j < 8; ++j) tsl[j] = tql[j] = 0.f;
+            float* ts = RSACC ? rsum[h] : tsl;
+            float* tq = RSACC ? rsq[h] : tql;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
               const bool ok = okm[mt];
@@ -417,19 +382,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                 v[j] = bf16_lo(bf16x2_pack(acc[mt][2 * h + (j >> 2)][j & 3] + b, 0.f));   // the stored bf16 value
                 if constexpr (RELU_OUT) v[j] = fmaxf(v[j], 0.f);
               }
-              if constexpr (BW) {
-                if (mt == MH) load_y(MH);
-                const uint4 yq = yb[mt % MH];
-                const unsigned yw[4] = {yq.x, yq.y, yq.z, yq.w};
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                  const float y = (j & 1) ? bf16_hi(yw[j >> 1]) : bf16_lo(yw[j >> 1]);
-                  float gv = ok ? v[j] : 0.f;
-                  if constexpr ((M & 2) != 0) gv = (y * bsc[j] + bsh[j]) > 0.f ? gv : 0.f;
-                  ts[j] += gv;
-                  tq[j] += gv * y;
-                }
-              } else if constexpr (ST) {
+              if constexpr (ST) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                   const float x = ok ? v[j] : 0.f;
@@ -459,18 +412,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
               acc[mt][2 * h] = (f32x4){0.f, 0.f, 0.f, 0.f};
               acc[mt][2 * h + 1] = (f32x4){0.f, 0.f, 0.f, 0.f};
             }
-            if constexpr (ST) {
-              // over the 16 lanes holding the same columns (DPP), into the wave's LDS sums
+            if constexpr (ST && !RSACC) {        // (per-tile: DPP over the 16 lanes, LDS adds)
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
-                ts[j] = ct_sum16(ts[j]);
-                tq[j] = ct_sum16(tq[j]);
-              }
-              if (lr == 0) {                     // one lane per column of this wave's row: plain
-#pragma unroll                                   // adds, a fixed summation order (deterministic
-                for (int j = 0; j < 8; ++j) {    // statistics, run to run)
-                  s_red[wave * 2 * RC + NV * lg + 8 * h + j] += ts[j];
-                  s_red[wave * 2 * RC + RC + NV * lg + 8 * h + j] += tq[j];
+                const float a = ct_sum16(ts[j]), b = ct_sum16(tq[j]);
+                if (lr == 0) {
+                  s_red[wave * 2 * RC + NV * lg + 8 * h + j] += a;
+                  s_red[wave * 2 * RC + RC + NV * lg + 8 * h + j] += b;
                 }
               }
             }
@@ -563,9 +511,6 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             case 3: epilogue_f8(std::integral_constant<int, 3>{}); break;
             default: if constexpr (MT == 8) epilogue_f8(std::integral_constant<int, 5>{}); break;
           }
-        } else if constexpr (BWS) {
-          if (emode == 6) epilogue(std::integral_constant<int, 6>{});
-          else epilogue(std::integral_constant<int, 4>{});
         } else {
           switch (emode) {
             case 0: epilogue(std::integral_constant<int, 0>{}); break;
@@ -577,14 +522,25 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
           }
         }
         lap(st_e);
-        if constexpr (BWS) {
-#pragma unroll
-          for (int u = 0; u < PD; ++u) load_b(wnext, u);
-        }
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) lb[mt] += (1 - 2 * par) * g.BUF;   // the other buffer
       par ^= 1;
+    }
+    if (!F8 && RSACC && stats) {
+      // the lane's running sums over the 16 lanes holding the same columns (DPP), into the wave's
+      // LDS row: a fixed summation order (deterministic statistics, run to run)
+#pragma unroll
+      for (int h = 0; h < NT / 2; ++h) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = ct_sum16(rsum[h][j]), b = ct_sum16(rsq[h][j]);
+          if (lr == 0) {
+            s_red[wave * 2 * RC + NV * lg + 8 * h + j] = a;
+            s_red[wave * 2 * RC + RC + NV * lg + 8 * h + j] = b;
+          }
+        }
+      }
     }
     tile_lds_barrier();                          // R
     if (!F8 && stats && tid < RC && ct0 * 16 + tid < Ncol) {
@@ -728,22 +684,21 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool BWS = false, bool Q8O = false,
-          bool I8 = false>
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
-                       float oscale = 0.f, const void* bny = nullptr, const float* bnp = nullptr) {
+                       float oscale = 0.f) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS, Q8O, I8>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, BWS, Q8O, I8>), grid, dim3(CT_NTHR), lds, st,
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8>), grid, dim3(CT_NTHR), lds, st,
                      (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
-                     stamps, scale, oscale, (const bf16*)bny, bnp);
+                     stamps, scale, oscale);
   return 0;
 }
 
@@ -757,10 +712,10 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
   return 0;
 }
 
-static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, bool bws = false) {
+static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false) {
   const int PD = ct_pd(NT, f8);
   return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
-         (bws ? (size_t)NT * 16 * 16 : 0) + (f8 ? (size_t)NT * 16 * 8 : 0);
+         (f8 ? (size_t)NT * 16 * 8 : 0);
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -768,10 +723,8 @@ static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false,
 // int2[4 * MT * 16] (halo position of the row, natural tile row or -1); ktab: int4[nks + PD
 // + 2] byte offsets of the tap each lane group reads per k-step (zero past nks);
 // zp: >= 16 zero bytes; sched: int[64] zeroed counters (left zero); stats: fp32
-// [workers][2][Ncol], or null.  bny / bnp (dgrad only, with stats): the BN input y [out shape]
-// and (mean, invstd, scale, shift) [4][Ncol] of the BN+act layer whose output this conv
-// consumed; stats then receives that BN's raw backward sums (sum g, sum g*y) and act is the
-// BN's activation (none / relu), not an activation of the output.
+// [workers][2][Ncol], or null.  bny / bnp: must be null (the BN-backward statistics epilogue is
+// conv_tile32's, fn_conv_tile32).
 extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
                             int NT, int* sched, hipStream_t st, const void* bny, const float* bnp, float oscale) {
@@ -800,19 +753,19 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   }
   const size_t halo = (size_t)g.HPpad * CPP * 16;
   if ((size_t)g.BUF < halo || g.BUF % 1024) return -3;
-  const size_t lds = tile_lds_total(g, MT, NT, false, bny != nullptr);
+  if (bny || bnp) return -2;
+  const size_t lds = tile_lds_total(g, MT, NT, false);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
   if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;   // 16-B column groups; relu or none
   // oscale > 0: e4m3 output of y * oscale (no statistics; the 8-channel-slice instances: the
   // space-to-depth stem of the fp8 inference path)
-  if (!(oscale >= 0.f) || (oscale > 0.f && (stats || bny || NT != 2 || CPP != 1))) return -2;
-  if ((bny != nullptr) != (bnp != nullptr) || (bny && (!stats || bias))) return -2;
+  if (!(oscale >= 0.f) || (oscale > 0.f && (stats || NT != 2 || CPP != 1))) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();
-  if (dbg && MT == 8 && NT == 2 && !bny && oscale == 0.f) {   // experiment variants (timing only; 1-7, 32 give
+  if (dbg && MT == 8 && NT == 2 && oscale == 0.f) {   // experiment variants (timing only; 1-7, 32 give
                                                               // wrong results; 64, 128, 192 schedule variants)
     static long long* stamps = nullptr;
     const size_t nst = (size_t)grid.x * grid.y * 16;
@@ -843,14 +796,11 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   }
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
-    rc = bny ? launch_tile<M, N, C, 0, false, N == 2>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,  \
-                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, \
-                                                    nullptr, nullptr, 0.f, bny, bnp)                              \
-             : (oscale > 0.f ? launch_tile<M, N, C, 0, false, false, C == 1 && N == 2>(                          \
-                                   grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp,  \
-                                   bias, out, stats, g, Ncol, act, sched, nullptr, nullptr, oscale)                   \
-                             : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,         \
-                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched));
+    rc = oscale > 0.f ? launch_tile<M, N, C, 0, false, C == 1 && N == 2>(                                        \
+                            grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, \
+                            stats, g, Ncol, act, sched, nullptr, nullptr, oscale)                                   \
+                      : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,                 \
+                                             (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched);
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;
@@ -942,7 +892,7 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   }
 #define CT_F8_CASE(M, N, C)                                                                                        \
   if (MT == M && NT == N && CPP == C)                                                                              \
-    rc = i8 ? launch_tile<M, N, C, 0, true, false, false, C == 2>(grid, lds, st, src, (const uint4*)wp,              \
+    rc = i8 ? launch_tile<M, N, C, 0, true, false, C == 2>(grid, lds, st, src, (const uint4*)wp,                     \
                                                                   (const int2*)rowtab, (const int4*)ktab, zp, bias, \
                                                                   out, nullptr, g, Ncol, f8act, sched, nullptr,    \
                                                                   scale, oscale)                                   \

@@ -41,20 +41,16 @@ def enabled() -> bool:
     """Whether BN forwards tag their outputs for the consuming conv's dgrad.  ``FN_BN_DGRAD_FUSE``:
     'auto' (default) = whenever the 32x32x16 tile kernel is on (``FN_TILE_M32``): its dgrad
     epilogue reads y at the tile's positions with every load of a pass in flight together and
-    has the registers for it (209-247 VGPRs, no scratch); '1' also fuses into the 16x16x32
-    kernel's statistics instance, measured slower there (its spills cost the three dgrads
-    115-190 us each against the colstats passes they remove); '0' never."""
+    has the registers for it (209-247 VGPRs, no scratch); '1' always tags (the fusion still
+    happens only on the 32x32x16 kernel: the 16x16x32 kernel's statistics instance measured
+    slower in rounds 3 and 4 -- 5.14 vs 4.80 and 5.37 vs 5.00 ms per step -- and was removed);
+    '0' never."""
     mode = os.environ.get("FN_BN_DGRAD_FUSE", "auto")
     if mode == "auto":
         from .conv_tile import m32_enabled
 
         return m32_enabled()
     return mode == "1"
-
-
-def tile16_enabled() -> bool:
-    """The statistics epilogue on the 16x16x32 kernel (opt-in: FN_BN_DGRAD_FUSE=1)."""
-    return os.environ.get("FN_BN_DGRAD_FUSE", "auto") == "1"
 
 
 def pool_stats_enabled() -> bool:

@@ -447,14 +447,9 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None):
                     (spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw))
     wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
-    lds_bws = 2 * p.BUF + 64 + red_bytes(p.NT) + (p.nks + PD + 2) * 16 + p.HPpad * 8 + p.NT * 16 * 16
-    # the statistics epilogue: every conv_tile32 plan (its LDS holds the BN scale / shift already),
-    # the conv_tile_kernel instance only when asked for (FN_BN_DGRAD_FUSE=1: measured slower)
-    from . import bnfuse
-
-    fuse = p.m32 or (bnfuse.tile16_enabled() and lds_bws <= LDS_MAX and p.NT == 2)
-    if bn is None or not fuse:   # (the statistics instance: 32-column blocks, BN
-        # scale/shift in LDS)
+    # the statistics epilogue: conv_tile32 plans (their LDS holds the BN scale / shift already)
+    fuse = p.m32
+    if bn is None or not fuse:
         run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
         return dx if bn is None else (dx, None)
     y, prm, act = bn

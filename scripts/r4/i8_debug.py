@@ -1,9 +1,13 @@
 """Diagnostics for the int8 instance of the fp8 tile kernel: structured inputs whose exact
 outputs are known (constant operands, channel halves, single taps), printed side by side."""
-import torch
+import os
+import sys
 
-from featurenet_amd.ops import conv_tile as ct
-from featurenet_amd.ops.spec import ConvSpec
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+from featurenet_amd.ops import conv_tile as ct  # noqa: E402
+from featurenet_amd.ops.spec import ConvSpec  # noqa: E402
 
 N, S, C, K = 2, 12, 32, 32
 spec = ConvSpec.make((N, S, S, S, C), K, (4, 4, 1), 1, "valid")

@@ -1,7 +1,7 @@
 """BN-backward statistics fused into the consuming conv's dgrad epilogue (ops/bnfuse.py;
-conv_tile32.hip BWS instances, and the opt-in conv_tile.hip one): the fused path must give the
-same parameter and input gradients as the separate colstats pass, and must actually take the
-fused branch."""
+conv_tile32.hip BWS instances -- the 16x16x32 kernel has none since round 4): the fused path must
+give the same parameter and input gradients as the separate colstats pass, and must actually
+take the fused branch."""
 import pytest
 import torch
 
@@ -35,16 +35,15 @@ def _count_fused(monkeypatch):
     return calls
 
 
-@pytest.mark.parametrize("m32", ["1", "0"])
 @pytest.mark.parametrize("N,S,cin,cmid,k", [(2, 20, 32, 32, 3), (3, 17, 16, 64, 4), (16, 24, 32, 64, 3)])
-def test_dgrad_bn_stats_match_colstats(monkeypatch, N, S, cin, cmid, k, m32):
+def test_dgrad_bn_stats_match_colstats(monkeypatch, N, S, cin, cmid, k):
     from torch import nn
 
     from featurenet_amd.models.layers import Conv
 
     assert _native.kernels() is not None
     monkeypatch.setenv("FN_CONV_TILE", "2")      # the tile kernel (the fused epilogue lives there)
-    monkeypatch.setenv("FN_TILE_M32", m32)       # 32x32x16 kernel (default) or the 16x16x32 one
+    monkeypatch.setenv("FN_TILE_M32", "1")       # the 32x32x16 kernel (its dgrad has the epilogue)
     torch.manual_seed(0)
     dev = torch.device("cuda", 0)
     model = nn.Sequential(Conv(cin, cmid, k, 1, "valid", bn=True, act="relu", init="he"),
@@ -66,6 +65,7 @@ def test_featurenet3d_fused_bn_backward(monkeypatch):
     from featurenet_amd.models.featurenet3d import FeatureNet3D
 
     torch.manual_seed(1)
+    monkeypatch.setenv("FN_TILE_M32", "1")
     dev = torch.device("cuda", 0)
     model = FeatureNet3D().to(dev)
     x = (torch.rand(8, 64, 64, 64, 1, device=dev) < 0.3).to(torch.bfloat16)
