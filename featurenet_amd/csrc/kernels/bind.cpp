@@ -57,7 +57,7 @@ int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
-                   hipStream_t, int, int, const void*, int, float*);
+                   hipStream_t, int, int, const void*, int, float*, int);
 int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
                 int, int, int, int, hipStream_t);
 int fn_bn_finalize(const float*, int, int, double, const float*, const float*, float*, float*, float, float, float*,
@@ -494,14 +494,14 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("igemm_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t part, uintptr_t tab, std::vector<int> geom,
                           long long M, int Cout, int K, int splits, int vec, uintptr_t st, int ccrop, int cpad,
-                          uintptr_t ya, int act, uintptr_t db) {
+                          uintptr_t ya, int act, uintptr_t db, int kout) {
     need(geom, 14, "igemm_wgrad");
     chk(fn_igemm_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(part), P<const int*>(tab), geom.data(), M,
-                       Cout, K, splits, vec, S(st), ccrop, cpad, P<const void*>(ya), act, P<float*>(db)),
+                       Cout, K, splits, vec, S(st), ccrop, cpad, P<const void*>(ya), act, P<float*>(db), kout),
         "igemm_wgrad");
   }, py::arg("dy"), py::arg("src"), py::arg("part"), py::arg("tab"), py::arg("geom"), py::arg("M"), py::arg("Cout"),
      py::arg("K"), py::arg("splits"), py::arg("vec"), py::arg("st"), py::arg("ccrop") = 0, py::arg("cpad") = 0,
-     py::arg("ya") = 0, py::arg("act") = 0, py::arg("db") = 0);
+     py::arg("ya") = 0, py::arg("act") = 0, py::arg("db") = 0, py::arg("kout") = 0);
   m.def("colstats", [](uintptr_t x, uintptr_t dz, uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd,
                        uintptr_t part, long long M, int C, int act, int mode, int nb, uintptr_t st) {
     chk(fn_colstats(P<const void*>(x), P<const void*>(dz), P<const float*>(scale), P<const float*>(shift),

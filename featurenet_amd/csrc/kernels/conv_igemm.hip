@@ -353,7 +353,7 @@ template <int BCO, int GM, bool VECN>
 __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ src, float* __restrict__ dw,
     const int4* __restrict__ tab, GatherGeom g, long long M, int Cout, int Kdim, long long rows_per_split,
-    int gx, int gy, int ccrop, int cpad, const bf16* __restrict__ ya, int act, float* __restrict__ db) {
+    int gx, int gy, int ccrop, int cpad, const bf16* __restrict__ ya, int act, float* __restrict__ db, int kout) {
   constexpr int LDY = WgLds<BCO>::LDY;
   constexpr int X_STAGE = WG_BR * WG_LDX;
   constexpr int Y_STAGE = WG_BR * LDY;
@@ -503,7 +503,7 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
   // Split-m partial sums are folded straight into the fp32 dW with no-return
   // float atomics (S x Cout x Kdim x 4 B of atomic traffic, well under the
   // ~1.3 TB/s chip-wide atomic rate for the split counts used).
-  if (dsum && co0 + tid < Cout) atomicAdd(db + co0 + tid, dbs);
+  if (dsum && co0 + tid < kout) atomicAdd(db + co0 + tid, dbs);
   // ccrop > 0: k = t*cpad + c lands at dw[co][t*ccrop + c] of the real weight, columns
   // c >= ccrop dropped -- the zero channels of a channel-padded input (cpad = its channels,
   // ccrop = the real ones) or the row padding of the packed-W layout (cpad = R, ccrop = KW*C):
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + mt * 16 + (lane >> 4) * 4 + r;
-        if (co < Cout && kok) atomicAdd(dw + (long long)co * ldo + kdst, acc[mt][nt][r]);
+        if (co < kout && kok) atomicAdd(dw + (long long)co * ldo + kdst, acc[mt][nt][r]);
       }
     }
 }
@@ -596,10 +596,13 @@ extern "C" int fn_igemm_fwd_mblocks(long long M) { return (int)((M + FWD_BM - 1)
 // gather layout (c < ccrop) maps to t*ccrop + c (channel-padded inputs; the packed-W rows)
 // ya / act (optional): dy is the gradient of the activation output ya (the activation backward
 // is applied as dy is loaded); db (optional, zeroed): receives the bias gradient (column sums of
-// the activated dy)
+// the activated dy).  kout (0 = Cout): only output channels co < kout are written (dy channel-
+// padded to Cout for 16-B loads, dW / db of the real kout channels)
 extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const int* tab, const int* geom14,
                               long long M, int Cout, int Kdim, int splits, int gm, hipStream_t st, int ccrop,
-                              int cpad, const void* ya, int act, float* db) {
+                              int cpad, const void* ya, int act, float* db, int kout) {
+  if (kout <= 0) kout = Cout;
+  if (kout > Cout) return -2;
   const GatherGeom g = parse_geom(geom14);
   if (ccrop > 0 && (cpad < ccrop || Kdim % cpad)) return -2;
   const int BCO = Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64);
@@ -612,7 +615,7 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const 
   const int4* t = (const int4*)tab;
 #define WG_CASE(B, V, VN) \
   hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, dw, t, g, M, Cout, Kdim, rps, gx, gy, \
-                     ccrop, cpad, (const bf16*)ya, act, db)
+                     ccrop, cpad, (const bf16*)ya, act, db, kout)
 #define WG_GM(GMV)                                                                        \
   do {                                                                                    \
     if (vecn) {                                                                           \

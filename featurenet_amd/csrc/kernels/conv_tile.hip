@@ -460,7 +460,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             float v[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              const float a = I8 ? (float)__builtin_bit_cast(int, acc[mt][j >> 2][j & 3]) : acc[mt][j >> 2][j & 3];
+              // (the element is copied out first: __builtin_bit_cast of a vector-element lvalue
+              // compiled to element 0 of the vector -- every lane's 4 columns got column 0's sum)
+              const float ae = acc[mt][j >> 2][j & 3];
+              const float a = I8 ? (float)__builtin_bit_cast(int, ae) : ae;
               v[j] = a * sc8[j] + bs8[j];
               if constexpr ((M & 2) != 0)        // (already x oscale) relu / saturate in one med3
                 v[j] = __builtin_amdgcn_fmed3f(v[j], (M & 1) != 0 ? 0.f : -448.f, 448.f);

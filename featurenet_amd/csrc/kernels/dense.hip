@@ -295,9 +295,15 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
       }
       if (ya) {
         const bf16* yrow = ya + (long long)(m < M ? m : 0) * N;
+        bf16x8 yv = zero8;
+        if (vec) {
+          yv = *(const bf16x8*)(yrow + nc);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (nc + e < N) v[e] = f2bf(bf2f(v[e]) * act_bwd_from_out(bf2f(yrow[nc + e]), act));
+          for (int e = 0; e < 8; ++e) yv[e] = nc + e < N ? yrow[nc + e] : f2bf(0.f);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) * act_bwd_from_out(bf2f(yv[e]), act));
       }
       acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, m < M ? v : zero8, acc[j], 0, 0, 0);
     }
@@ -374,8 +380,14 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
           for (int e = 0; e < 8; ++e) vg.e[e] = n + e < N ? g[(long long)m * N + n + e] : f2bf(0.f);
         }
         if (ya) {                                // g = dy * act'(y) (see dense_dgrad_kernel)
-          for (int e = 0; e < 8; ++e)
-            if (n + e < N) vg.e[e] = f2bf(bf2f(vg.e[e]) * act_bwd_from_out(bf2f(ya[(long long)m * N + n + e]), act));
+          Pack8 vy;
+          if ((N & 7) == 0 && n + 8 <= N) {
+            vy.u = *(const uint4*)(ya + (long long)m * N + n);
+          } else {
+            for (int e = 0; e < 8; ++e) vy.e[e] = n + e < N ? ya[(long long)m * N + n + e] : f2bf(0.f);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) vg.e[e] = f2bf(bf2f(vg.e[e]) * act_bwd_from_out(bf2f(vy.e[e]), act));
         }
       }
 #pragma unroll

@@ -536,7 +536,8 @@ def igemm_wgrad_cropped(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, c0:
     (zeroed, e.g. the parameter's flat gradient) with every padding column of the gather
     layout dropped in the epilogue: the zero channels c0..spec.C of a channel-padded input,
     or the row padding of the packed-W layout (C < 8: rows of KW*C rounded up to 8).
-    ``dy5`` has the real ``spec.K`` channels (any count, no padded copy).  ``ya`` / ``act``: dy5
+    ``dy5`` has the real ``spec.K`` channels (padded here to a multiple of 8 for the kernel's
+    16-B loads; the epilogue drops the padded rows).  ``ya`` / ``act``: dy5
     is the gradient of the activation output ``ya`` (the activation backward runs as dy is
     loaded); ``with_db``: the bias gradient from the same dy tiles too, into ``bias_param``'s
     zeroed flat-gradient slot when it offers one -- returns ``(dW, db)`` then.  None when the
@@ -563,10 +564,17 @@ def igemm_wgrad_cropped(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, c0:
     if ya is not None:
         ya = ya.contiguous()
         assert ya.dtype == torch.bfloat16 and ya.numel() == dy5.numel()
+    kp = -(-spec.K // 8) * 8
+    if kp != spec.K:
+        # Cout % 8 != 0: dy channel-padded for 16-B row loads (single-element loads made this
+        # kernel 1.45x slower on LeNet's 6-channel conv1), rows past K dropped by the epilogue
+        if ya is not None:
+            dy5, ya = native_act_bwd(dy5, ya, act), None
+        dy5 = pad_channels(dy5, kp)
     db = _zeroed_grad(bias_param, spec.K, x5.device) if with_db else None
     _native.kernels().igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), out.data_ptr(), tab.data_ptr(), _geom_fwd(spec),
-                                  spec.M, spec.K, kd, wgrad_splits(spec), gm, _native.stream(x5), ccrop, cpad,
-                                  _native.ptr(ya), act if ya is not None else 0, _native.ptr(db))
+                                  spec.M, kp, kd, wgrad_splits(spec), gm, _native.stream(x5), ccrop, cpad,
+                                  _native.ptr(ya), act if ya is not None else 0, _native.ptr(db), spec.K)
     return (out, db) if with_db else out
 
 

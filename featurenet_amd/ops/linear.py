@@ -79,10 +79,12 @@ class LinearFn(torch.autograd.Function):
         NP = -(-N // 32) * 32                          # (any N: the dgrad kernel pads its k dim to 32)
         dgrad_native = _NATIVE and K % 4 == 0 and wf.dtype == torch.float32 and 64 * (NP + 8) * 2 <= 160 * 1024
         # the activation backward inside the dgrad / wgrad kernels (g = dy * act'(y) as they load
-        # it) when both run natively and the wgrad kernel produces db: no separate pass
+        # it) when both run natively and the wgrad kernel produces db: no separate pass.  Small
+        # layers only (K <= 4096): every dgrad / wgrad workgroup re-applies it to the g rows it
+        # reads, which for FC1 (K = 64000: 1000 column workgroups) cost more than the pass
         ya = None
         if ctx.act:
-            if (_NATIVE and ctx.needs_input_grad[1] and (dgrad_native or not ctx.needs_input_grad[0])
+            if (_NATIVE and K <= 4096 and ctx.needs_input_grad[1] and (dgrad_native or not ctx.needs_input_grad[0])
                     and y.dtype == torch.bfloat16):
                 ya = y.reshape(M, N).contiguous()
             else:
