@@ -70,6 +70,7 @@ int fn_bn_bwd_apply_s2d(const void*, const void*, const float*, const float*, co
 int fn_pool_fwd(const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd(const void*, const void*, void*, const float*, const float*, const int*, int, int, int, hipStream_t);
 int fn_pool_bwd_stats_blocks(const int*);
+int fn_colstats_blocks(long long, int, int, int);
 int fn_pool_bn_bwd_apply(const void*, const void*, const float*, const float*, const float*, const float*,
                          const float*, const float*, void*, const int*, int, float, hipStream_t);
 int fn_pool_bwd_stats(const void*, const void*, void*, const float*, const float*, const int*, int, float*,
@@ -508,6 +509,7 @@ PYBIND11_MODULE(_C, m) {
                     P<const float*>(mean), P<const float*>(invstd), P<float*>(part), M, C, act, mode, nb, S(st)),
         "colstats");
   });
+  m.def("colstats_blocks", &fn_colstats_blocks, py::arg("M"), py::arg("C"), py::arg("mode"), py::arg("act"));
   m.def("bn_finalize", [](uintptr_t part, int nb, int C, double count, uintptr_t gamma, uintptr_t beta,
                           uintptr_t rmean, uintptr_t rvar, float momentum, float eps, uintptr_t o0, uintptr_t o1,
                           uintptr_t o2, uintptr_t o3, int mode, uintptr_t st) {

@@ -437,14 +437,10 @@ __global__ __launch_bounds__(256) void pool2_fwd_kernel(const bf16* __restrict__
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
                                                         PoolGeom g, int is_max, int act, int total) {
   const int cpr = g.C >> 3;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int ch = i % cpr;
-  int t = i / cpr;
-  const int ow = t % g.OW; t /= g.OW;
-  const int oh = t % g.OH; t /= g.OH;
-  const int od = t % g.OD;
-  const int n = t / g.OD;
+  // grid-stride over a resident-sized grid (the stride is a multiple of 256, so with
+  // 256 % cpr == 0 -- host-checked -- a thread keeps its 8-channel chunk and the BN parameters
+  // are loaded once); the next window's loads are issued before this one is reduced
+  const int ch = threadIdx.x % cpr;
   float sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -452,27 +448,47 @@ __global__ __launch_bounds__(256) void pool2_fwd_kernel(const bf16* __restrict__
     sh[j] = scale ? shift[ch * 8 + j] : 0.f;
   }
   const long long rowW = (long long)g.W * g.C, plane = (long long)g.H * rowW;
-  const long long b0 = ((long long)(n * g.D + od * KD) * g.H + oh * 2) * rowW + (long long)ow * 2 * g.C + ch * 8;
+  auto origin = [&](int ii) -> long long {
+    int t = ii / cpr;
+    const int ow = t % g.OW; t /= g.OW;
+    const int oh = t % g.OH; t /= g.OH;
+    const int od = t % g.OD;
+    const int n = t / g.OD;
+    return ((long long)(n * g.D + od * KD) * g.H + oh * 2) * rowW + (long long)ow * 2 * g.C + ch * 8;
+  };
+  auto fetch = [&](long long b0, Pack8* p) {
+#pragma unroll
+    for (int kd = 0; kd < KD; ++kd)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 2; ++kw) p[(kd * 2 + kh) * 2 + kw].u = *(const uint4*)(x + b0 + kd * plane + kh * rowW + kw * g.C);
+  };
+  const int stride = gridDim.x * 256;
+  int i = blockIdx.x * 256 + threadIdx.x;
   Pack8 p[KD * 4];
+  if (i < total) fetch(origin(i), p);
+  while (i < total) {
+    const int inx = i + stride;
+    Pack8 p2[KD * 4];
+    fetch(origin(inx < total ? inx : i), p2);
+    Pack8 o;
 #pragma unroll
-  for (int kd = 0; kd < KD; ++kd)
+    for (int j = 0; j < 8; ++j) {
+      float acc = is_max ? -INFINITY : 0.f;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 2; ++kw) p[(kd * 2 + kh) * 2 + kw].u = *(const uint4*)(x + b0 + kd * plane + kh * rowW + kw * g.C);
-  Pack8 o;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float acc = is_max ? -INFINITY : 0.f;
-#pragma unroll
-    for (int w = 0; w < KD * 4; ++w) {
-      float v = bf2f(p[w].e[j]);
-      if (scale) v = act_fwd(v * sc[j] + sh[j], act);
-      acc = is_max ? fmaxf(acc, v) : acc + v;
+      for (int w = 0; w < KD * 4; ++w) {
+        float v = bf2f(p[w].e[j]);
+        if (scale) v = act_fwd(v * sc[j] + sh[j], act);
+        acc = is_max ? fmaxf(acc, v) : acc + v;
+      }
+      o.e[j] = f2bf(is_max ? acc : acc * (1.f / (KD * 4)));
     }
-    o.e[j] = f2bf(is_max ? acc : acc * (1.f / (KD * 4)));
+    *(uint4*)(out + (long long)i * 8) = o.u;
+#pragma unroll
+    for (int w = 0; w < KD * 4; ++w) p[w] = p2[w];
+    i = inx;
   }
-  *(uint4*)(out + (long long)i * 8) = o.u;
 }
 
 // Gather-form backward: every input element collects from the windows that
@@ -670,6 +686,91 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
   }
 }
 
+// BN backward moments of a BN+act+max-pool block without writing dz (the fused apply below
+// recomputes it): pool_bwd_tiled_kernel<8, true> with dx = null, restructured for bandwidth --
+// all <= 8 window loads of a thread in flight together (the generic kernel's runtime window
+// loop issued one 16-B load at a time: 2.6 TB/s), 32-bit index math (I = int when the host
+// checked the sizes), a grid-stride loop over a resident-sized grid.
+template <typename I>
+__global__ __launch_bounds__(256) void pool_bn_moments8_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, PoolGeom g, int act,
+                                                               float* __restrict__ part) {
+  const int cpr = g.C / 8;
+  const I total = (I)g.N * g.OD * g.OH * g.OW * cpr;
+  const int win = g.KD * g.KH * g.KW;            // (<= 8: host-checked)
+  const int ch = (int)(threadIdx.x % cpr);       // fixed: the stride is a multiple of cpr (256 % cpr == 0)
+  float sc[8], sh[8], s0[8], s1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[ch * 8 + j];
+    sh[j] = shift[ch * 8 + j];
+    s0[j] = s1[j] = 0.f;
+  }
+  I wofs[8];                                     // window member offsets from the window origin
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    const int ww = w < win ? w : 0;
+    const int kw = ww % g.KW, kh = (ww / g.KW) % g.KH, kd = ww / (g.KW * g.KH);
+    wofs[w] = (((I)kd * g.H + kh) * g.W + kw) * g.C;
+  }
+  // software-pipelined: the next window's 9 loads are issued before this one is reduced (an
+  // index past the end re-loads the current window: unconditional loads, so hipcc's wait
+  // counts stay exact)
+  auto fetch = [&](I ii, Pack8& q, Pack8* qy) {
+    I t = ii / cpr;
+    const int ow = (int)(t % g.OW); t /= g.OW;
+    const int oh = (int)(t % g.OH); t /= g.OH;
+    const int od = (int)(t % g.OD);
+    const I n = t / g.OD;
+    const I b0 = (((n * g.D + (I)od * g.KD) * g.H + (I)oh * g.KH) * g.W + (I)ow * g.KW) * g.C + ch * 8;
+    q.u = *(const uint4*)(dout + ii * 8);
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+      if (w < win) qy[w].u = *(const uint4*)(y + b0 + wofs[w]);
+  };
+  const I stride = (I)gridDim.x * 256;
+  I i = (I)blockIdx.x * 256 + threadIdx.x;
+  Pack8 pg, py[8];
+  if (i < total) fetch(i, pg, py);
+  while (i < total) {
+    const I inx = i + stride;
+    Pack8 pg2, py2[8];
+    fetch(inx < total ? inx : i, pg2, py2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float best = -INFINITY, yarg = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        if (w < win) {
+          const float yv = bf2f(py[w].e[j]);
+          const float v = act_fwd(yv * sc[j] + sh[j], act);
+          if (v > best) { best = v; yarg = yv; }   // (first arg-max, as the forward's scan)
+        }
+      }
+      const float gv = bf2f(pg.e[j]) * act_bwd_from_out(best, act);
+      s0[j] += gv;
+      s1[j] += gv * yarg;
+    }
+    pg = pg2;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) py[w] = py2[w];
+    i = inx;
+  }
+  __shared__ float red[256][17];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[tid][j] = s0[j]; red[tid][8 + j] = s1[j]; }
+  __syncthreads();
+  for (int c = tid; c < g.C; c += 256) {
+    const int chk = c / 8, j = c % 8;
+    float a = 0.f, b = 0.f;
+    for (int u = chk; u < 256; u += cpr) { a += red[u][j]; b += red[u][8 + j]; }
+    part[(long long)blockIdx.x * 2 * g.C + c] = a;
+    part[(long long)blockIdx.x * 2 * g.C + g.C + c] = b;
+  }
+}
+
 // Max-pool backward and the BN backward's input gradient in one pass (non-overlapping windows
 // of <= 8 positions, C % 8 == 0): one thread per (window, 8-channel chunk) reads the window's y
 // once, recomputes z = act(bn(y)) and the first arg-max, and writes
@@ -677,47 +778,72 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
 // for the whole window (bn_bwd_apply_kernel's k2 / k3).  Replaces pool_bwd (writes the sparse
 // dz) + bn_bwd_apply (reads dz and y again): two full-size passes fewer -- the moments come
 // from pool_bwd_tiled_kernel<8, true> with dx = null beforehand.
+// (I = int: 32-bit index math, when the host checked that every offset fits)
+template <typename I>
 __global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(
     const bf16* __restrict__ dout, const bf16* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ dbeta, const float* __restrict__ dgamma, bf16* __restrict__ dy, PoolGeom g, int act,
     float inv_count) {
   const int cpr = g.C / 8;
-  const long long total = (long long)g.N * g.OD * g.OH * g.OW * cpr;
+  const I total = (I)g.N * g.OD * g.OH * g.OW * cpr;
   const int win = g.KD * g.KH * g.KW;            // (<= 8: host-checked)
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int ch = (int)(i % cpr);
-    long long t = i / cpr;
+  // a fixed 8-channel chunk per thread (256 % cpr == 0 and the grid stride a multiple of 256,
+  // host-checked): the per-channel constants are loaded once, not per window
+  const int ch = (int)(threadIdx.x % cpr);
+  float sc[8], sh[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = ch * 8 + j;
+    sc[j] = scale[c];
+    sh[j] = shift[c];
+    const float is = invstd[c];
+    k2[j] = -sc[j] * is * dgamma[c] * inv_count;
+    k3[j] = -sc[j] * (dbeta[c] * inv_count - mean[c] * is * dgamma[c] * inv_count);
+  }
+  I wofs[8];                                     // window member offsets from the window origin
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    const int ww = w < win ? w : 0;
+    const int kw = ww % g.KW, kh = (ww / g.KW) % g.KH, kd = ww / (g.KW * g.KH);
+    wofs[w] = (((I)kd * g.H + kh) * g.W + kw) * g.C;
+  }
+  auto origin = [&](I ii) -> I {
+    I t = ii / cpr;
     const int ow = (int)(t % g.OW); t /= g.OW;
     const int oh = (int)(t % g.OH); t /= g.OH;
     const int od = (int)(t % g.OD);
-    const long long n = t / g.OD;
-    float go[8], sc[8], sh[8], k2[8], k3[8], best[8];
+    const I n = t / g.OD;
+    return (((n * g.D + (I)od * g.KD) * g.H + (I)oh * g.KH) * g.W + (I)ow * g.KW) * g.C + ch * 8;
+  };
+  // software-pipelined as pool_bn_moments8_kernel: the next window's loads are in flight
+  // while this one is reduced and stored
+  auto fetch = [&](I ii, I b0, Pack8& q, Pack8* qy) {
+    q.u = *(const uint4*)(dout + ii * 8);
+#pragma unroll
+    for (int w = 0; w < 8; ++w)
+      if (w < win) qy[w].u = *(const uint4*)(y + b0 + wofs[w]);
+  };
+  const I stride = (I)gridDim.x * 256;
+  I i = (I)blockIdx.x * 256 + threadIdx.x;
+  Pack8 pg, py[8];
+  I b0 = 0;
+  if (i < total) {
+    b0 = origin(i);
+    fetch(i, b0, pg, py);
+  }
+  while (i < total) {
+    const I inx = i + stride;
+    const I in2 = inx < total ? inx : i;
+    const I b1 = origin(in2);
+    Pack8 pg2, py2[8];
+    fetch(in2, b1, pg2, py2);
+    float best[8], gm[8];
     int arg[8];
-    Pack8 pg;
-    pg.u = *(const uint4*)(dout + i * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = ch * 8 + j;
-      go[j] = bf2f(pg.e[j]);
       best[j] = -INFINITY;
       arg[j] = 0;
-      sc[j] = scale[c];
-      sh[j] = shift[c];
-      const float is = invstd[c];
-      k2[j] = -sc[j] * is * dgamma[c] * inv_count;
-      k3[j] = -sc[j] * (dbeta[c] * inv_count - mean[c] * is * dgamma[c] * inv_count);
-    }
-    long long base[8];
-    Pack8 py[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      if (w < win) {
-        const int kw = w % g.KW, kh = (w / g.KW) % g.KH, kd = w / (g.KW * g.KH);
-        base[w] = ((((n * g.D + od * g.KD + kd) * g.H + oh * g.KH + kh) * (long long)g.W + ow * g.KW + kw) * g.C) +
-                  ch * 8;
-        py[w].u = *(const uint4*)(y + base[w]);
-      }
     }
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
@@ -729,9 +855,8 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(
         }
       }
     }
-    float gm[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gm[j] = go[j] * act_bwd_from_out(best[j], act);
+    for (int j = 0; j < 8; ++j) gm[j] = bf2f(pg.e[j]) * act_bwd_from_out(best[j], act);
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
       if (w < win) {
@@ -739,20 +864,60 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           po.e[j] = f2bf(sc[j] * (arg[j] == w ? gm[j] : 0.f) + k2[j] * bf2f(py[w].e[j]) + k3[j]);
-        *(uint4*)(dy + base[w]) = po.u;
+        *(uint4*)(dy + b0 + wofs[w]) = po.u;
       }
     }
+    pg = pg2;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) py[w] = py2[w];
+    b0 = b1;
+    i = inx;
   }
 }
 
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
+// workgroups of `kernel` (256 threads, no dynamic LDS) resident on the whole device at once
+// (0 when the runtime cannot say)
+static int bn_resident_blocks(const void* kernel) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 256, 0) != hipSuccess)
+    return 0;
+  return cus > 0 && per > 0 ? cus * per : 0;
+}
+
 static unsigned ew_blocks(long long work) {
   long long b = (work + 255) / 256;
   if (b < 1) b = 1;
   if (b > 8192) b = 8192;
   return (unsigned)b;
+}
+
+// Workgroups for a colstats launch over M rows: one per 256 rows, capped at what the device
+// holds resident at once (the kernel walks its rows in a loop; a grid of 2048 over 768 resident
+// slots -- 134 VGPRs, 3 workgroups per CU -- spent its last third at 2/3 occupancy)
+extern "C" int fn_colstats_blocks(long long M, int C, int mode, int act) {
+  long long nb = M / 256;
+  if (nb < 1) nb = 1;
+  long long cap = 2048;
+  if (C % 8 == 0 && C / 8 <= 256) {
+    static int res[2][4] = {{-1, -1, -1, -1}, {-1, -1, -1, -1}};
+    const int m = mode ? 1 : 0;
+    const int a = mode == 0 ? 0 : (act == ACT_RELU ? 1 : act == ACT_TANH ? 2 : act == ACT_SIGMOID ? 3 : 0);
+    if (res[m][a] < 0) {
+      const void* k = mode == 0 ? (const void*)colstats_kernel<8, 0, ACT_NONE>
+                    : a == 1 ? (const void*)colstats_kernel<8, 1, ACT_RELU>
+                    : a == 2 ? (const void*)colstats_kernel<8, 1, ACT_TANH>
+                    : a == 3 ? (const void*)colstats_kernel<8, 1, ACT_SIGMOID>
+                             : (const void*)colstats_kernel<8, 1, ACT_NONE>;
+      res[m][a] = bn_resident_blocks(k);
+    }
+    if (res[m][a] > 0) cap = res[m][a];
+  }
+  return (int)(nb > cap ? cap : nb);
 }
 
 extern "C" int fn_colstats(const void* x, const void* dz, const float* scale, const float* shift, const float* mean,
@@ -884,14 +1049,21 @@ extern "C" int fn_pool_fwd(const void* x, void* out, const float* scale, const f
   const long long outs = (long long)g.N * g.OD * g.OH * g.OW;
   const bool win2 = g.KH == 2 && g.KW == 2 && (g.KD == 2 || g.KD == 1) && g.sd == g.KD && g.sh == 2 && g.sw == 2 &&
                     g.pd == 0 && g.ph == 0 && g.pw == 0 && g.D >= g.OD * g.KD && g.H >= g.OH * 2 &&
-                    g.W >= g.OW * 2 && g.C % 8 == 0 && outs * (g.C / 8) < (1LL << 31);
+                    g.W >= g.OW * 2 && g.C % 8 == 0 && 256 % (g.C / 8) == 0 &&
+                    outs * (g.C / 8) + 256LL * 8192 < (1LL << 31);
   if (win2) {
     const int total = (int)(outs * (g.C / 8));
+    static const int res2 = bn_resident_blocks((const void*)pool2_fwd_kernel<2>);
+    static const int res1 = bn_resident_blocks((const void*)pool2_fwd_kernel<1>);
+    const int res = g.KD == 2 ? res2 : res1;
+    long long nbl = (total + 255) / 256;
+    if (res > 0 && nbl > res) nbl = res;
+    const unsigned nb = (unsigned)(nbl < 1 ? 1 : (nbl > 8192 ? 8192 : nbl));
     if (g.KD == 2)
-      hipLaunchKernelGGL(pool2_fwd_kernel<2>, dim3((total + 255) / 256), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
+      hipLaunchKernelGGL(pool2_fwd_kernel<2>, dim3(nb), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
                          scale, shift, g, is_max, act, total);
     else
-      hipLaunchKernelGGL(pool2_fwd_kernel<1>, dim3((total + 255) / 256), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
+      hipLaunchKernelGGL(pool2_fwd_kernel<1>, dim3(nb), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
                          scale, shift, g, is_max, act, total);
   } else if (g.C % 8 == 0)
     hipLaunchKernelGGL(pool_fwd_kernel<8>, dim3(ew_blocks(outs * (g.C / 8))), dim3(256), 0, st, (const bf16*)x,
@@ -901,6 +1073,13 @@ extern "C" int fn_pool_fwd(const void* x, void* out, const float* scale, const f
                        scale, shift, g, is_max, count_pad, act);
   FN_CHECK_LAUNCH();
   return 0;
+}
+
+// every element offset of the pool's input / output (and the loop bound) fits a 32-bit int
+static bool pool_i32(const PoolGeom& g) {
+  const long long ins = (long long)g.N * g.D * g.H * g.W * g.C;
+  const long long outs = (long long)g.N * g.OD * g.OH * g.OW * g.C;
+  return ins + 256LL * 8192 * 8 < (1LL << 31) && outs + 256LL * 8192 * 8 < (1LL << 31);
 }
 
 static bool pool_bwd_stats_ok(const PoolGeom& g) {
@@ -913,7 +1092,13 @@ extern "C" int fn_pool_bwd_stats_blocks(const int* geom17) {
   const PoolGeom g = pool_geom(geom17);
   if (!pool_bwd_stats_ok(g)) return 0;
   const long long w = ((long long)g.N * g.OD * g.OH * g.OW * (g.C / 8) + 255) / 256;
-  return (int)(w < 1 ? 1 : (w > 2048 ? 2048 : w));
+  long long cap = 2048;
+  if (g.KD * g.KH * g.KW <= 8) {
+    // the moments kernel's grid-stride loop: one resident wave of workgroups (no tail round)
+    static const int res = bn_resident_blocks((const void*)pool_bn_moments8_kernel<int>);
+    if (res > 0) cap = res;
+  }
+  return (int)(w < 1 ? 1 : (w > cap ? cap : w));
 }
 
 // max-pool backward of a BN+act output plus that BN's raw backward moments (see
@@ -923,8 +1108,16 @@ extern "C" int fn_pool_bwd_stats(const void* dout, const void* x, void* dx, cons
   const PoolGeom g = pool_geom(geom17);
   const int nb = fn_pool_bwd_stats_blocks(geom17);
   if (nb <= 0 || !scale || !shift || !part) return -2;
-  hipLaunchKernelGGL((pool_bwd_tiled_kernel<8, true>), dim3(nb), dim3(256), 0, st, (const bf16*)dout, (const bf16*)x,
-                     (bf16*)dx, scale, shift, g, 1, act, part);
+  if (!dx && g.KD * g.KH * g.KW <= 8) {          // moments only: the bandwidth form
+    if (pool_i32(g))
+      hipLaunchKernelGGL(pool_bn_moments8_kernel<int>, dim3(nb), dim3(256), 0, st, (const bf16*)dout, (const bf16*)x,
+                         scale, shift, g, act, part);
+    else
+      hipLaunchKernelGGL(pool_bn_moments8_kernel<long long>, dim3(nb), dim3(256), 0, st, (const bf16*)dout,
+                         (const bf16*)x, scale, shift, g, act, part);
+  } else
+    hipLaunchKernelGGL((pool_bwd_tiled_kernel<8, true>), dim3(nb), dim3(256), 0, st, (const bf16*)dout, (const bf16*)x,
+                       (bf16*)dx, scale, shift, g, 1, act, part);
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -937,11 +1130,20 @@ extern "C" int fn_pool_bn_bwd_apply(const void* dout, const void* y, const float
   const PoolGeom g = pool_geom(geom17);
   const bool tiled = g.sd == g.KD && g.sh == g.KH && g.sw == g.KW && g.pd == 0 && g.ph == 0 && g.pw == 0 &&
                      g.D == g.OD * g.KD && g.H == g.OH * g.KH && g.W == g.OW * g.KW;
-  if (!tiled || g.C % 8 || g.KD * g.KH * g.KW > 8) return -2;
+  if (!tiled || g.C % 8 || 256 % (g.C / 8) || g.KD * g.KH * g.KW > 8) return -2;
   const long long outs = (long long)g.N * g.OD * g.OH * g.OW;
-  hipLaunchKernelGGL(pool_bn_bwd_apply_kernel, dim3(ew_blocks(outs * (g.C / 8))), dim3(256), 0, st,
-                     (const bf16*)dout, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, g, act,
-                     inv_count);
+  static const int res = bn_resident_blocks((const void*)pool_bn_bwd_apply_kernel<int>);
+  long long nbl = (outs * (g.C / 8) + 255) / 256;
+  if (res > 0 && nbl > res) nbl = res;           // one resident wave of workgroups, grid-stride
+  const unsigned nb = (unsigned)(nbl < 1 ? 1 : (nbl > 8192 ? 8192 : nbl));
+  if (pool_i32(g))
+    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<int>, dim3(nb), dim3(256), 0, st,
+                       (const bf16*)dout, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, g, act,
+                       inv_count);
+  else
+    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<long long>, dim3(nb), dim3(256), 0, st,
+                       (const bf16*)dout, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, g, act,
+                       inv_count);
   FN_CHECK_LAUNCH();
   return 0;
 }

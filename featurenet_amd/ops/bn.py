@@ -23,7 +23,7 @@ from .spec import PoolSpec, act_code
 
 def _stats_slab(y2: torch.Tensor) -> torch.Tensor:
     M, C = y2.shape
-    nb = int(max(1, min(2048, M // 256)))
+    nb = _native.kernels().colstats_blocks(M, C, 0, 0)
     part = torch.empty(nb, 2, C, dtype=torch.float32, device=y2.device)
     _native.kernels().colstats(y2.data_ptr(), 0, 0, 0, 0, 0, part.data_ptr(), M, C, 0, 0, nb, _native.stream(y2))
     return part
@@ -60,7 +60,7 @@ def _bwd_param_grads(dz2, y2, prm, act, beta=None, gamma=None, part=None):
     mode = 2                                     # dgrad-epilogue slabs: raw moments (sum g, sum g*y)
     if part is None:
         mode = 1                                 # colstats: (sum g, sum g*xhat)
-        nb = int(max(1, min(2048, M // 256)))
+        nb = K.colstats_blocks(M, C, 1, act)
         part = torch.empty(nb, 2, C, dtype=torch.float32, device=y2.device)
         K.colstats(y2.data_ptr(), dz2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), prm[0].data_ptr(),
                    prm[1].data_ptr(), part.data_ptr(), M, C, act, 1, nb, st)

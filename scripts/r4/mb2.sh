@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round-4 (session 2): pipelined pool kernels (tests, bench, trace) + stem epilogue timing variants.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/mb2_$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  if [ $rc -ge 124 ]; then tail -20 "gpurun_out/mb2_$name.log"; exit $rc; fi
+  return $rc
+}
+step tests 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider \
+  tests/test_bnfuse_gpu.py tests/test_kernels_gpu.py -k "bn or pool or batchnorm or featurenet"
+grep -E "passed|failed" gpurun_out/mb2_tests.log | tail -2; grep -E "^FAILED|Error" gpurun_out/mb2_tests.log | head -10
+for d in 0 16 8 24; do
+  FN_TILE_DBG=$d step stem_$d 120 python3 scripts/bench_conv_layers.py --batch 128 --reps 10 --only stem_s2d,conv2
+  echo "dbg=$d"; grep -o '"layer": "[a-z0-9_]*"\|"tile_fwd_us": [0-9.]*' gpurun_out/mb2_stem_$d.log | paste - - ; grep stamps gpurun_out/mb2_stem_$d.log | sort | uniq -c | head -6
+done
+for i in 1 2; do
+  step bench 300 python3 bench.py --steps 30 --warmup 5
+  echo "bench $(grep -o '"value": [0-9.]*' gpurun_out/mb2_bench.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/mb2_bench.log)"
+done
+rm -rf gpurun_out/prof_mb2
+step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_mb2 -o run -- \
+  python3 bench.py --steps 5 --warmup 3
+python3 scripts/step_breakdown.py gpurun_out/prof_mb2/run_kernel_trace.csv --min-us 0 > gpurun_out/step_mb2.md 2>&1 || true
+tail -2 gpurun_out/step_mb2.md
+grep -E "pool|colstats" gpurun_out/step_mb2.md
