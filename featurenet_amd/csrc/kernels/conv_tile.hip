@@ -225,9 +225,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
     // ct0*16 + 4*NT*lg + 4nt + r: a lane ends with NV = 4*NT consecutive columns of one position
     const int gc8 = ct0 * 16 + NV * lg;
-    float bias8[8];                              // (fp8: read in the epilogue from LDS, no live
+    ct_f32x2 bias2[4];                           // (fp8: read in the epilogue from LDS, no live
 #pragma unroll                                   // registers across the k-loop)
-    for (int j = 0; j < 8; ++j) bias8[j] = (!F8 && bias && gc8 + j < Ncol) ? bias[gc8 + j] : 0.f;
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) bias2[q][e] = (!F8 && bias && gc8 + 2 * q + e < Ncol) ? bias[gc8 + 2 * q + e] : 0.f;
     constexpr unsigned FTILE = 64u * FRAG;       // bytes of one 16-column fragment of a k-step
     const unsigned wstep = (unsigned)g.nct * FTILE;   // bytes per k-step of the packed weights
     unsigned voffb[PD];                          // per-lane B offsets of the PD ring slots
@@ -268,11 +270,12 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // stem fwd epilogue ~40 % of its cycles in round 4 stamps).  MT = 9 keeps the per-tile
     // reduction (16 more live registers made it spill)
     constexpr bool RSACC = MT <= 8;
-    float rsum[NT / 2][8], rsq[NT / 2][8];
+    // (column pairs: the epilogue's adds are packed v_pk_add / v_pk_fma of two columns)
+    ct_f32x2 rsum[NT / 2][4], rsq[NT / 2][4];
 #pragma unroll
     for (int h = 0; h < NT / 2; ++h)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) rsum[h][j] = rsq[h][j] = 0.f;
+      for (int q = 0; q < 4; ++q) rsum[h][q] = rsq[h][q] = (ct_f32x2){0.f, 0.f};
     // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
     // the previous job's last turn, so no job starts on an exposed L2 latency
 #pragma unroll
@@ -364,58 +367,66 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             okm[mt] = ok;
           }
           // one pass per 8 consecutive columns of the lane (fragments 2h, 2h+1): one 16-B store
-          // per row; the BN partial sums go into the lane's running sums (rsum / rsq)
+          // per row; the BN partial sums go into the lane's running sums (rsum / rsq).  Column
+          // pairs throughout: packed bias add, one v_cvt_pk_bf16_f32 per pair gives the stored
+          // word (relu on the packed bf16 as a signed 16-bit max), the statistics unpack that
+          // word (the stored values) into packed adds -- ~3 VALU per value instead of ~6
 #pragma unroll
           for (int h = 0; h < NT / 2; ++h) {
-            float tsl[8], tql[8];
+            ct_f32x2 tsl[4], tql[4];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) tsl[j] = tql[j] = 0.f;
-            float* ts = RSACC ? rsum[h] : tsl;
-            float* tq = RSACC ? rsq[h] : tql;
+            for (int q = 0; q < 4; ++q) tsl[q] = tql[q] = (ct_f32x2){0.f, 0.f};
+            ct_f32x2* ts = RSACC ? rsum[h] : tsl;
+            ct_f32x2* tq = RSACC ? rsq[h] : tql;
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
               const bool ok = okm[mt];
-              float v[8];
+              unsigned pw[4];                    // the stored bf16 pairs (columns 2q, 2q+1)
 #pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const float b = bias8[j];
-                v[j] = bf16_lo(bf16x2_pack(acc[mt][2 * h + (j >> 2)][j & 3] + b, 0.f));   // the stored bf16 value
-                if constexpr (RELU_OUT) v[j] = fmaxf(v[j], 0.f);
+              for (int q = 0; q < 4; ++q) {
+                const f32x4 a4 = acc[mt][2 * h + (q >> 1)];
+                const ct_f32x2 v = (ct_f32x2){a4[(2 * q) & 3], a4[(2 * q + 1) & 3]} + bias2[q];
+                unsigned w = bf16x2_pack(v[0], v[1]);
+                if constexpr (RELU_OUT) w = ct_relu_bf16x2(w);
+                pw[q] = w;
               }
               if constexpr (ST) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                  const float x = ok ? v[j] : 0.f;
-                  ts[j] += x;
-                  tq[j] += x * x;
+                for (int q = 0; q < 4; ++q) {
+                  const unsigned w = ok ? pw[q] : 0u;
+                  const ct_f32x2 x = (ct_f32x2){bf16_lo(w), bf16_hi(w)};
+                  ts[q] += x;
+                  tq[q] += x * x;
                 }
               }
               if constexpr (Q8) {
                 if (ok) {
                   unsigned wd[2];
 #pragma unroll
-                  for (int q = 0; q < 2; ++q) {
+                  for (int qq = 0; qq < 2; ++qq) {
                     float e[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                      e[j] = __builtin_amdgcn_fmed3f(v[4 * q + j] * oscale, RELU_OUT ? 0.f : -448.f, 448.f);
+                    for (int j = 0; j < 4; ++j) {
+                      const unsigned w = pw[2 * qq + (j >> 1)];
+                      const float v = (j & 1) ? bf16_hi(w) : bf16_lo(w);
+                      e[j] = __builtin_amdgcn_fmed3f(v * oscale, RELU_OUT ? 0.f : -448.f, 448.f);
+                    }
                     int pk = __builtin_amdgcn_cvt_pk_fp8_f32(e[0], e[1], 0, false);
                     pk = __builtin_amdgcn_cvt_pk_fp8_f32(e[2], e[3], pk, true);
-                    wd[q] = (unsigned)pk;
+                    wd[qq] = (unsigned)pk;
                   }
                   *(uint2*)(reinterpret_cast<unsigned char*>(out) + obase_e + (long long)roff[mt] * Ncol + 8 * h) =
                       make_uint2(wd[0], wd[1]);
                 }
-              } else if (ok)
-                *(uint4*)(obase + (long long)roff[mt] * Ncol + 8 * h) = make_uint4(
-                    bf16x2_pack(v[0], v[1]), bf16x2_pack(v[2], v[3]), bf16x2_pack(v[4], v[5]), bf16x2_pack(v[6], v[7]));
+              } else if (ok && !(DBG & 8))      // (DBG 8, timing only: no output stores)
+                *(uint4*)(obase + (long long)roff[mt] * Ncol + 8 * h) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
               acc[mt][2 * h] = (f32x4){0.f, 0.f, 0.f, 0.f};
               acc[mt][2 * h + 1] = (f32x4){0.f, 0.f, 0.f, 0.f};
             }
             if constexpr (ST && !RSACC) {        // (per-tile: DPP over the 16 lanes, LDS adds)
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
-                const float a = ct_sum16(ts[j]), b = ct_sum16(tq[j]);
+                const float a = ct_sum16(ts[j >> 1][j & 1]), b = ct_sum16(tq[j >> 1][j & 1]);
                 if (lr == 0) {
                   s_red[wave * 2 * RC + NV * lg + 8 * h + j] += a;
                   s_red[wave * 2 * RC + RC + NV * lg + 8 * h + j] += b;
@@ -537,7 +548,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       for (int h = 0; h < NT / 2; ++h) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float a = ct_sum16(rsum[h][j]), b = ct_sum16(rsq[h][j]);
+          const float a = ct_sum16(rsum[h][j >> 1][j & 1]), b = ct_sum16(rsq[h][j >> 1][j & 1]);
           if (lr == 0) {
             s_red[wave * 2 * RC + NV * lg + 8 * h + j] = a;
             s_red[wave * 2 * RC + RC + NV * lg + 8 * h + j] = b;
@@ -777,6 +788,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
 #define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, src, \
       (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, stamps);
     CT_DBG(1, 1) CT_DBG(1, 2) CT_DBG(1, 4) CT_DBG(1, 16)   // (the space-to-depth stem)
+    CT_DBG(1, 8) CT_DBG(1, 24) CT_DBG(2, 8) CT_DBG(2, 24)
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
     CT_DBG(4, 23) CT_DBG(2, 32) CT_DBG(4, 32)
     CT_DBG(2, 64) CT_DBG(2, 128) CT_DBG(2, 192) CT_DBG(4, 64) CT_DBG(4, 128) CT_DBG(4, 192)   // (correct results)

@@ -51,6 +51,15 @@ __device__ __forceinline__ float ct_sum16(float x) {
 }
 
 typedef int ct_i32x8 __attribute__((ext_vector_type(8)));
+typedef float ct_f32x2 __attribute__((ext_vector_type(2)));
+typedef short ct_s16x2 __attribute__((ext_vector_type(2)));
+
+// relu of a packed bf16 pair: a negative bf16 (sign bit set) is a negative int16, so a signed
+// 16-bit max with 0 zeroes it (-0.0 -> +0.0) and keeps every non-negative value (one v_pk_max_i16)
+__device__ __forceinline__ unsigned ct_relu_bf16x2(unsigned w) {
+  const ct_s16x2 s = __builtin_elementwise_max(__builtin_bit_cast(ct_s16x2, w), (ct_s16x2){0, 0});
+  return __builtin_bit_cast(unsigned, s);
+}
 
 // B-ring depth (k-steps in flight): a bf16 k-step is MT*NT 16-cycle MFMAs, an fp8 one
 // MT*NT 32-cycle block-scaled MFMAs, so 2 fp8 steps cover the latency 4 bf16 steps do
