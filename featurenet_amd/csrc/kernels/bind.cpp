@@ -62,7 +62,13 @@ int fn_colstats(const void*, const void*, const float*, const float*, const floa
                 int, int, int, int, hipStream_t);
 int fn_bn_finalize(const float*, int, int, double, const float*, const float*, float*, float*, float, float, float*,
                    float*, float*, float*, int, hipStream_t);
-int fn_bn_apply(const void*, const float*, const float*, void*, long long, int, int, hipStream_t);
+int fn_bn_apply(const void*, const float*, const float*, void*, long long, int, int, hipStream_t, void*);
+int fn_bn_wdot(const float*, const float*, float*, int, int, int, hipStream_t);
+int fn_bn_bwd_prep(const float*, int, const float*, int, int, double, const float*, const float*, const float*,
+                   const float*, float*, float*, hipStream_t);
+int fn_bn_bwd_apply_k_blocks(long long, int);
+int fn_bn_bwd_apply_k(const void*, const void*, const float*, const float*, const float*, void*, long long, int,
+                      float*, int, hipStream_t);
 int fn_bn_bwd_apply(const void*, const void*, const float*, const float*, const float*, const float*, const float*,
                     const float*, void*, long long, int, float, int, hipStream_t);
 int fn_bn_bwd_apply_s2d(const void*, const void*, const float*, const float*, const float*, const float*,
@@ -222,9 +228,11 @@ PYBIND11_MODULE(_C, m) {
                         float oscale) {
     need(geom, 31, "conv_tile");
     check_tile(geom, ext, ncol, MT, "conv_tile");
-    if (bny) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
+    if (bny && bnp) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
       fits(ext, 5, view_extent(geom, ncol), "conv_tile", "bny");
       fits(ext, 6, 4LL * ncol, "conv_tile", "bnp");
+    } else if (bny) {   // the relu-mask bytes: ext[5] = their count (one per 8 output columns)
+      fits(ext, 5, view_extent(geom, ncol) / 8, "conv_tile", "mask");
     }
     chk(fn_conv_tile(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
                      P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
@@ -509,6 +517,14 @@ PYBIND11_MODULE(_C, m) {
                     P<const float*>(mean), P<const float*>(invstd), P<float*>(part), M, C, act, mode, nb, S(st)),
         "colstats");
   });
+  m.def("experiments_built", [] {
+    // FN_BUILD_EXPERIMENTS=1 builds: conv_tile32, the int8 fp8-stem instance, timing variants
+#ifdef FN_EXPERIMENTS
+    return true;
+#else
+    return false;
+#endif
+  });
   m.def("colstats_blocks", &fn_colstats_blocks, py::arg("M"), py::arg("C"), py::arg("mode"), py::arg("act"));
   m.def("bn_finalize", [](uintptr_t part, int nb, int C, double count, uintptr_t gamma, uintptr_t beta,
                           uintptr_t rmean, uintptr_t rvar, float momentum, float eps, uintptr_t o0, uintptr_t o1,
@@ -519,10 +535,42 @@ PYBIND11_MODULE(_C, m) {
         "bn_finalize");
   });
   m.def("bn_apply", [](uintptr_t y, uintptr_t scale, uintptr_t shift, uintptr_t z, long long total, int C, int act,
-                       uintptr_t st) {
+                       uintptr_t st, uintptr_t mask, long long mask_numel) {
+    // mask: optional uint8 [total / 8] relu-mask bytes (one per 8-channel chunk)
+    if (mask && mask_numel * 8 != total) throw std::runtime_error("bn_apply: mask needs total / 8 bytes");
     chk(fn_bn_apply(P<const void*>(y), P<const float*>(scale), P<const float*>(shift), P<void*>(z), total, C, act,
-                    S(st)),
+                    S(st), P<void*>(mask)),
         "bn_apply");
+  }, py::arg("y"), py::arg("scale"), py::arg("shift"), py::arg("z"), py::arg("total"), py::arg("C"), py::arg("act"),
+     py::arg("st"), py::arg("mask") = 0, py::arg("mask_numel") = 0);
+  m.def("bn_wdot", [](uintptr_t w, uintptr_t dw, uintptr_t part, int R, int C, int nb, uintptr_t st,
+                      std::vector<long long> ext) {
+    fits(ext, 0, (long long)R * C, "bn_wdot", "w");
+    fits(ext, 1, (long long)R * C, "bn_wdot", "dw");
+    fits(ext, 2, (long long)nb * C, "bn_wdot", "part");
+    chk(fn_bn_wdot(P<const float*>(w), P<const float*>(dw), P<float*>(part), R, C, nb, S(st)), "bn_wdot");
+  });
+  m.def("bn_bwd_prep", [](uintptr_t gslab, int nbg, uintptr_t wpart, int nbw, int C, double count, uintptr_t beta,
+                          uintptr_t mean, uintptr_t invstd, uintptr_t scale, uintptr_t dbeta, uintptr_t kc, uintptr_t st,
+                          std::vector<long long> ext) {
+    fits(ext, 0, 2LL * nbg * C, "bn_bwd_prep", "gslab");
+    fits(ext, 1, (long long)nbw * C, "bn_bwd_prep", "wpart");
+    fits(ext, 2, 3LL * C, "bn_bwd_prep", "kc");
+    chk(fn_bn_bwd_prep(P<const float*>(gslab), nbg, P<const float*>(wpart), nbw, C, count, P<const float*>(beta),
+                       P<const float*>(mean), P<const float*>(invstd), P<const float*>(scale), P<float*>(dbeta),
+                       P<float*>(kc), S(st)),
+        "bn_bwd_prep");
+  });
+  m.def("bn_bwd_apply_k_blocks", &fn_bn_bwd_apply_k_blocks);
+  m.def("bn_bwd_apply_k", [](uintptr_t g, uintptr_t y, uintptr_t kc, uintptr_t mean, uintptr_t invstd, uintptr_t dy,
+                             long long M, int C, uintptr_t part, int nb, uintptr_t st, std::vector<long long> ext) {
+    fits(ext, 0, M * C, "bn_bwd_apply_k", "g");
+    fits(ext, 1, M * C, "bn_bwd_apply_k", "y");
+    fits(ext, 2, M * C, "bn_bwd_apply_k", "dy");
+    fits(ext, 3, 2LL * nb * C, "bn_bwd_apply_k", "part");
+    chk(fn_bn_bwd_apply_k(P<const void*>(g), P<const void*>(y), P<const float*>(kc), P<const float*>(mean),
+                          P<const float*>(invstd), P<void*>(dy), M, C, P<float*>(part), nb, S(st)),
+        "bn_bwd_apply_k");
   });
   m.def("bn_bwd_apply", [](uintptr_t dz, uintptr_t y, uintptr_t scale, uintptr_t shift, uintptr_t mean,
                            uintptr_t invstd, uintptr_t dbeta, uintptr_t dgamma, uintptr_t dy, long long total, int C,

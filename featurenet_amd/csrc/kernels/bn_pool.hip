@@ -209,10 +209,13 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
 // thread keeps ONE channel chunk for the whole grid-stride loop, so the
 // per-channel parameters live in registers and no 64-bit modulo runs per
 // element.
+// mask (VW = 8, fixed-chunk path only; host-checked): also one byte per 8-channel chunk, bit j =
+// (z_j > 0) -- the relu mask of the BN-backward statistics identity (bn_bwd_prep_kernel), which
+// the consuming conv's dgrad epilogue applies to dz
 template <int VW, int ACT>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ y, const float* __restrict__ scale,
                                                        const float* __restrict__ shift, bf16* __restrict__ z,
-                                                       long long total, int C) {
+                                                       long long total, int C, unsigned char* __restrict__ mask) {
   constexpr int act = ACT;
   const long long nvec = total / VW;
   const int cpr = C / VW;
@@ -227,9 +230,15 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16* __restrict__ 
     for (long long i = i0; i < nvec; i += stride) {
       Pack8 p;
       if constexpr (VW == 8) p.u = *(const uint4*)(y + i * 8); else p.e[0] = y[i];
+      unsigned bits = 0;
 #pragma unroll
-      for (int j = 0; j < VW; ++j) p.e[j] = f2bf(act_fwd(bf2f(p.e[j]) * sc[j] + sh[j], act));
+      for (int j = 0; j < VW; ++j) {
+        const float v = act_fwd(bf2f(p.e[j]) * sc[j] + sh[j], act);
+        bits |= (v > 0.f ? 1u : 0u) << j;
+        p.e[j] = f2bf(v);
+      }
       if constexpr (VW == 8) *(uint4*)(z + i * 8) = p.u; else z[i] = p.e[0];
+      if (mask) mask[i] = (unsigned char)bits;
     }
     return;
   }
@@ -291,6 +300,132 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
     }
     if constexpr (VW == 8) *(uint4*)(dy + i * 8) = po.u;
     else dy[i] = po.e[0];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BN backward without the colstats pass over (dz, y): the statistics identity.
+//
+// z = relu(bn(y)) feeds a conv (weights W [K][T][C], weight gradient dW, both fp32 [K*T][C]);
+// its dgrad gives dz = conv^T(dy', W).  Per input channel c the adjoint identity
+//     sum_p dz[p,c] * z[p,c] = sum_{k,t} W[k,t,c] * dW[k,t,c]
+// holds exactly (dW = sum_q dy'[q,k] z[q+t,c]), so with g = dz * relu'(z) and, where
+// relu' = 1, z = gamma * xhat + beta:
+//     gamma * sum g*xhat = S - beta * sum g,      S = sum_{k,t} W * dW
+// The consuming conv's dgrad epilogue writes g (dz masked by the bit mask bn_apply wrote) and
+// its column sums (sum g); bn_wdot_kernel gives S; bn_bwd_prep_kernel the apply constants
+//     dy = k1*g + k2*y + k3,  k1 = scale, k2 = -invstd^2 * G / M,
+//                            k3 = -scale * sum g / M + mean * invstd^2 * G / M,  G = S - beta sum g
+// (no division by gamma: the input gradient is exact for any gamma).  dgamma itself, only read
+// by the optimizer, is summed exactly from (g, y) inside the apply pass (bn_bwd_apply_k_kernel).
+// W is rounded to bf16 as the dgrad's packed weights are.
+// ---------------------------------------------------------------------------
+
+// per-block partial sums part[block][c] = sum_rows bf16(W[r][c]) * dW[r][c] over rows of [R][C]
+// (C divides 256: a thread keeps one channel)
+__global__ __launch_bounds__(256) void bn_wdot_kernel(const float* __restrict__ w, const float* __restrict__ dw,
+                                                      float* __restrict__ part, int R, int C, int rows_per_block) {
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  const int c = tid % C, r0 = tid / C, rpp = 256 / C;
+  const int rb = blockIdx.x * rows_per_block;
+  int re = rb + rows_per_block;
+  if (re > R) re = R;
+  float a = 0.f;
+  for (int r = rb + r0; r < re; r += rpp) {
+    const long long o = (long long)r * C + c;
+    a += (float)(bf16)w[o] * dw[o];
+  }
+  red[tid] = a;
+  __syncthreads();
+  if (tid < C) {
+    float t = 0.f;
+    for (int i = 0; i < rpp; ++i) t += red[i * C + tid];
+    part[(long long)blockIdx.x * C + tid] = t;
+  }
+}
+
+// One block per channel: sum g (the dgrad epilogue's slab rows, [nbg][2][C] row 0) and S (the
+// wdot partials [nbw][C]) in fp64 -> dbeta = sum g and the apply constants kc[3][C].
+__global__ __launch_bounds__(256) void bn_bwd_prep_kernel(const float* __restrict__ gslab, int nbg,
+                                                          const float* __restrict__ wpart, int nbw, int C,
+                                                          double count, const float* __restrict__ beta,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd,
+                                                          const float* __restrict__ scale, float* __restrict__ dbeta,
+                                                          float* __restrict__ kc) {
+  __shared__ double sa[256], sb[256];
+  const int c = blockIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int i = threadIdx.x; i < nbg; i += 256) a += (double)gslab[(long long)i * 2 * C + c];
+  for (int i = threadIdx.x; i < nbw; i += 256) b += (double)wpart[(long long)i * C + c];
+  sa[threadIdx.x] = a;
+  sb[threadIdx.x] = b;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (threadIdx.x < st) {
+      sa[threadIdx.x] += sa[threadIdx.x + st];
+      sb[threadIdx.x] += sb[threadIdx.x + st];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double sg = sa[0], S = sb[0];
+    const double bt = beta ? (double)beta[c] : 0.0;
+    const double is = (double)invstd[c], sc = (double)scale[c];
+    const double G = S - bt * sg;                // gamma * sum g*xhat
+    dbeta[c] = (float)sg;
+    kc[c] = (float)sc;
+    kc[C + c] = (float)(-is * is * G / count);
+    kc[2 * C + c] = (float)(-sc * sg / count + (double)mean[c] * is * is * G / count);
+  }
+}
+
+// dy = k1*g + k2*y + k3 (g: the masked dz) and the exact dgamma partials sum g*(y-mean)*invstd as
+// rows part[block][2][C] (row 0 zero; bn_finalize mode 1 turns row 1 into dgamma).  8 channels
+// per thread, fixed (C / 8 divides 256, the stride a multiple of 256); grid-stride over a
+// resident-sized grid.
+__global__ __launch_bounds__(256) void bn_bwd_apply_k_kernel(const bf16* __restrict__ g, const bf16* __restrict__ y,
+                                                             const float* __restrict__ kc,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ invstd, bf16* __restrict__ dy,
+                                                             long long nvec, int C, float* __restrict__ part) {
+  const int cpr = C / 8;
+  const int tid = threadIdx.x;
+  const int c0 = (tid % cpr) * 8;
+  float k1[8], k2[8], k3[8], mu[8], s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k1[j] = kc[c0 + j];
+    k2[j] = kc[C + c0 + j];
+    k3[j] = kc[2 * C + c0 + j];
+    mu[j] = mean[c0 + j];
+    s[j] = 0.f;
+  }
+  const long long stride = (long long)gridDim.x * 256;
+#pragma unroll 2
+  for (long long i = blockIdx.x * 256LL + tid; i < nvec; i += stride) {
+    Pack8 pg, py, po;
+    pg.u = *(const uint4*)(g + i * 8);
+    py.u = *(const uint4*)(y + i * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gv = bf2f(pg.e[j]), yv = bf2f(py.e[j]);
+      po.e[j] = f2bf(k1[j] * gv + k2[j] * yv + k3[j]);
+      s[j] += gv * (yv - mu[j]);
+    }
+    *(uint4*)(dy + i * 8) = po.u;
+  }
+  __shared__ float red[256][9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[tid][j] = s[j] * invstd[c0 + j];
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    const int chk = c / 8, j = c % 8;
+    float b = 0.f;
+    for (int t = chk; t < 256; t += cpr) b += red[t][j];
+    part[(long long)blockIdx.x * 2 * C + c] = 0.f;
+    part[(long long)blockIdx.x * 2 * C + C + c] = b;
   }
 }
 
@@ -976,10 +1111,11 @@ extern "C" int fn_bn_finalize(const float* part, int nb, int C, double count, co
 }
 
 extern "C" int fn_bn_apply(const void* y, const float* scale, const float* shift, void* z, long long total, int C,
-                           int act, hipStream_t st) {
+                           int act, hipStream_t st, void* mask) {
+  if (mask && (C % 8 || 256 % (C / 8))) return -2;   // (the fixed-chunk path writes the mask)
 #define BA_CASE(VW, A)                                                                                  \
   hipLaunchKernelGGL((bn_apply_kernel<VW, A>), dim3(ew_blocks(total / VW)), dim3(256), 0, st, (const bf16*)y, scale, \
-                     shift, (bf16*)z, total, C)
+                     shift, (bf16*)z, total, C, (unsigned char*)mask)
 #define BA_ACT(VW)                                                                                      \
   do {                                                                                                  \
     if (act == ACT_RELU) BA_CASE(VW, ACT_RELU);                                                         \
@@ -1171,6 +1307,43 @@ extern "C" int fn_pool_bwd(const void* dout, const void* x, void* dx, const floa
   else
     hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(ew_blocks(ins * g.C)), dim3(256), 0, st, (const bf16*)dout,
                        (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, count_pad, act);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// S partials of the statistics identity: part[nb][C], W / dW fp32 [R][C] (R = K * taps)
+extern "C" int fn_bn_wdot(const float* w, const float* dw, float* part, int R, int C, int nb, hipStream_t st) {
+  if (C <= 0 || C > 256 || 256 % C || nb < 1) return -2;
+  const int rpb = (R + nb - 1) / nb;
+  hipLaunchKernelGGL(bn_wdot_kernel, dim3(nb), dim3(256), 0, st, w, dw, part, R, C, rpb);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fn_bn_bwd_prep(const float* gslab, int nbg, const float* wpart, int nbw, int C, double count,
+                              const float* beta, const float* mean, const float* invstd, const float* scale,
+                              float* dbeta, float* kc, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_prep_kernel, dim3(C), dim3(256), 0, st, gslab, nbg, wpart, nbw, C, count, beta, mean,
+                     invstd, scale, dbeta, kc);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// workgroups of bn_bwd_apply_k (its partial-sum rows): one resident wave of them
+extern "C" int fn_bn_bwd_apply_k_blocks(long long M, int C) {
+  static const int res = bn_resident_blocks((const void*)bn_bwd_apply_k_kernel);
+  long long nb = (M * (C / 8) + 255) / 256;
+  const long long cap = res > 0 ? res : 2048;
+  if (nb > cap) nb = cap;
+  return (int)(nb < 1 ? 1 : nb);
+}
+
+extern "C" int fn_bn_bwd_apply_k(const void* g, const void* y, const float* kc, const float* mean,
+                                 const float* invstd, void* dy, long long M, int C, float* part, int nb,
+                                 hipStream_t st) {
+  if (C % 8 || 256 % (C / 8) || nb < 1) return -2;
+  hipLaunchKernelGGL(bn_bwd_apply_k_kernel, dim3(nb), dim3(256), 0, st, (const bf16*)g, (const bf16*)y, kc, mean,
+                     invstd, (bf16*)dy, M * (C / 8), C, part);
   FN_CHECK_LAUNCH();
   return 0;
 }

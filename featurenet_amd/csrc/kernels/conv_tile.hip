@@ -70,7 +70,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                                                                float* __restrict__ stats, TileGeom g, int Ncol,
                                                                int act, int* __restrict__ sched,
                                                                long long* __restrict__ stamps,
-                                                               const float* __restrict__ scale, float oscale) {
+                                                               const float* __restrict__ scale, float oscale,
+                                                               const unsigned char* __restrict__ gmask) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int PD = ct_pd(NT, F8);
   constexpr int ESZ = F8 ? 1 : 2;                // bytes per element of the source / weights
@@ -110,6 +111,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // F8: the dequantisation scale and bias of this workgroup's 32 columns ([scale 32][bias 32]),
   // read by the epilogue from LDS (global loads there serialised every tile's stores)
   float* s_sb = reinterpret_cast<float*>(s_pos + g.HPpad);
+  // relu-mask dgrad (gmask): two buffers (by job parity) of the tile's mask bytes,
+  // [natural tile row][Ncol / 8], after everything else
+  const int mask_off = 64 + ct_red_bytes(NT) + (nks + PD + 2) * 16 + g.HPpad * 8 + (F8 ? NT * 16 * 8 : 0);
+  const int mask_bytes = ct_mask_bytes(rows, Ncol, gmask != nullptr);
   if constexpr (F8) {
     if (tid < NT * 16) {
       const int c = blockIdx.y * NT * 16 + tid;
@@ -145,6 +150,31 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   auto dma_job = [&](int tile, int slice, int bufoff) {
     ct_dma_job<CPP, ESZ>(g, src, zp, dsm, s_pos, tile, slice, bufoff, lane, tdn, thn, twn);
   };
+  // the mask bytes of `tile` into mask buffer mpar, with the halo of the tile's last job: one
+  // dword per lane (Ncol / 32 per position), natural row order; rows past the tile or the
+  // output read the tile origin's bytes (never used)
+  auto dma_mask = [&](int tile, int mpar) {
+    if (!gmask) return;
+    int t = __builtin_amdgcn_readfirstlane(tile);
+    const int tw_ = t % twn; t /= twn;
+    const int th_ = t % thn; t /= thn;
+    const int td_ = t % tdn;
+    const int n = t / tdn;
+    const int d0 = td_ * g.TD, h0 = th_ * g.TH, w0 = tw_ * g.TW;
+    const long long pb = (long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh + w0 * g.osw;
+    const int dpp = Ncol >> 5;
+    const int ndw = rows * dpp;
+    const unsigned dst = ct_lds_addr(dsm) + 2 * g.BUF + mask_off + mpar * mask_bytes;
+    for (int k0 = 0; k0 < ndw; k0 += 64) {
+      const int dd = k0 + lane;
+      int r = dd / dpp;
+      if (r >= rows) r = rows - 1;
+      const int tw = r % g.TW, th = (r / g.TW) % g.TH, td = r / (g.TW * g.TH);
+      const bool in = d0 + td < g.OD && h0 + th < g.OH && w0 + tw < g.OW;
+      const long long pos = pb + (in ? (long long)td * g.osd + (long long)th * g.osh + (long long)tw * g.osw : 0);
+      ct_glds4(gmask + pos * (Ncol >> 3) + (dd % dpp) * 4, dst + (unsigned)(k0 * 4));
+    }
+  };
 
   // DBG & 16: cycle stamps of wave 0 and the loader (barrier-A wait, job work, tile end)
   long long st_a = 0, st_k = 0, st_e = 0, st_0 = 0, st_1 = 0;
@@ -175,6 +205,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     int tile = __builtin_amdgcn_readfirstlane(s_job[0]), slice = 0, t_next = -1;
     if (tile >= 0) {
       dma_job(tile, 0, 0);
+      if (nslice == 1) dma_mask(tile, 0);
       if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
       t_next = __builtin_amdgcn_readfirstlane(t_next);
       if (t_next >= ntiles) t_next = -1;
@@ -196,6 +227,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
         s_job[2 * (par ^ 1) + 1] = nslc;
       }
       if (!(DBG & 4) && ntile >= 0) dma_job(ntile, nslc, (par ^ 1) * g.BUF);
+      if (ntile >= 0 && nslc == nslice - 1) dma_mask(ntile, par ^ 1);
       if (nslc == 0 && ntile >= 0) {
         if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
         t_next = __builtin_amdgcn_readfirstlane(t_next);
@@ -265,6 +297,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     const int emode = F8 ? (((act & 0xff) == ACT_RELU ? 1 : 0) | (oscale > 0.f ? 2 : 0) | ((act & CT_F8_POOL) ? 4 : 0))
                          : ((stats ? 1 : 0) | ((act & 0xff) == ACT_RELU ? 2 : 0) | (Q8O ? 8 : 0));   // (ACT_NONE /
                                                                                           // ACT_RELU only; 8: e4m3 out)
+    // relu-mask dgrad (stats, no activation; host-checked) -- selected inside case 1, so every
+    // emode value still reaches an epilogue (a reachable no-epilogue path kept the accumulators
+    // live across it: 227 -> 256 VGPRs with spills)
+    const bool msk = !F8 && gmask != nullptr;
     // BN partial sums of this lane's columns over every tile the workgroup runs (the epilogues
     // add into them; one DPP + LDS reduction after the last tile instead of one per tile:
     // stem fwd epilogue ~40 % of its cycles in round 4 stamps).  MT = 9 keeps the per-tile
@@ -359,6 +395,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
           // bit 3: e4m3 output of v * oscale (saturated; fp8 inference: the bf16 stem writes the
           // fp8 layers' input directly), 8-B stores; no statistics
           constexpr bool Q8 = (M & 8) != 0;
+          // bit 4: relu-mask dgrad -- the stored values are g = dx * relu'(z), z's mask bits in mbits
+          constexpr bool MSK = (M & 16) != 0;
+          // (MSK: the loader DMA'd the tile's mask bytes into the LDS mask buffer of this job's
+          // parity, [natural tile row][Ncol / 8]; dummy rows read row 0)
+          const unsigned char* mb = dsm + 2 * g.BUF + mask_off + par * mask_bytes + (gc8 >> 3);
           bool okm[MT];
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
@@ -381,6 +422,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
               const bool ok = okm[mt];
+              unsigned mrow = 0;
+              if constexpr (MSK) {
+                const int nat = roff[mt] < 0 ? 0 : ((rpk[mt] >> 16) * g.TH + ((rpk[mt] >> 8) & 255)) * g.TW + (rpk[mt] & 255);
+                mrow = mb[nat * (Ncol >> 3)];
+              }
               unsigned pw[4];                    // the stored bf16 pairs (columns 2q, 2q+1)
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
@@ -388,6 +434,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                 const ct_f32x2 v = (ct_f32x2){a4[(2 * q) & 3], a4[(2 * q + 1) & 3]} + bias2[q];
                 unsigned w = bf16x2_pack(v[0], v[1]);
                 if constexpr (RELU_OUT) w = ct_relu_bf16x2(w);
+                if constexpr (MSK) {                 // bits 2q, 2q+1 of this row's mask byte
+                  const unsigned b = mrow >> (2 * q);
+                  w &= ((b & 1u) ? 0x0000ffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
+                }
                 pw[q] = w;
               }
               if constexpr (ST) {
@@ -528,7 +578,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
         } else {
           switch (emode) {
             case 0: epilogue(std::integral_constant<int, 0>{}); break;
-            case 1: epilogue(std::integral_constant<int, 1>{}); break;
+            case 1:
+              if (msk) epilogue(std::integral_constant<int, 17>{});
+              else epilogue(std::integral_constant<int, 1>{});
+              break;
             case 2: epilogue(std::integral_constant<int, 2>{}); break;
             case 3: epilogue(std::integral_constant<int, 3>{}); break;
             case 8: if constexpr (Q8O) epilogue(std::integral_constant<int, 8>{}); break;
@@ -702,7 +755,7 @@ template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = fals
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
-                       float oscale = 0.f) {
+                       float oscale = 0.f, const void* gmask = nullptr) {
   static size_t configured = 0;
   if (lds > configured) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8>,
@@ -712,7 +765,7 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
   }
   hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8>), grid, dim3(CT_NTHR), lds, st,
                      (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
-                     stamps, scale, oscale);
+                     stamps, scale, oscale, (const unsigned char*)gmask);
   return 0;
 }
 
@@ -726,10 +779,10 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
   return 0;
 }
 
-static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false) {
+static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, int Ncol = 0, bool mask = false) {
   const int PD = ct_pd(NT, f8);
   return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
-         (f8 ? (size_t)NT * 16 * 8 : 0);
+         (f8 ? (size_t)NT * 16 * 8 : 0) + 2 * (size_t)ct_mask_bytes(g.TD * g.TH * g.TW, Ncol, mask);
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -737,8 +790,10 @@ static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false)
 // int2[4 * MT * 16] (halo position of the row, natural tile row or -1); ktab: int4[nks + PD
 // + 2] byte offsets of the tap each lane group reads per k-step (zero past nks);
 // zp: >= 16 zero bytes; sched: int[64] zeroed counters (left zero); stats: fp32
-// [workers][2][Ncol], or null.  bny / bnp: must be null (the BN-backward statistics epilogue is
-// conv_tile32's, fn_conv_tile32).
+// [workers][2][Ncol], or null.  bny (bnp null): the relu-mask bytes [output positions][Ncol / 8]
+// of the BN whose output this dgrad's conv consumed -- the epilogue stores g = dx * mask and
+// (with stats) sums it; act none.  (The raw-moment BN-backward statistics epilogue, bny + bnp,
+// is conv_tile32's, fn_conv_tile32.)
 extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
                             int NT, int* sched, hipStream_t st, const void* bny, const float* bnp, float oscale) {
@@ -767,8 +822,8 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   }
   const size_t halo = (size_t)g.HPpad * CPP * 16;
   if ((size_t)g.BUF < halo || g.BUF % 1024) return -3;
-  if (bny || bnp) return -2;
-  const size_t lds = tile_lds_total(g, MT, NT, false);
+  if (bnp || (bny && (act != ACT_NONE || oscale != 0.f || Ncol % 32 || !stats))) return -2;
+  const size_t lds = tile_lds_total(g, MT, NT, false, Ncol, bny != nullptr);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
@@ -778,6 +833,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   if (!(oscale >= 0.f) || (oscale > 0.f && (stats || NT != 2 || CPP != 1))) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
+#ifdef FN_EXPERIMENTS
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();
   if (dbg && MT == 8 && NT == 2 && oscale == 0.f) {   // experiment variants (timing only; 1-7, 32 give
                                                               // wrong results; 64, 128, 192 schedule variants)
@@ -809,13 +865,15 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     }
     return 0;
   }
+#endif  // FN_EXPERIMENTS
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
     rc = oscale > 0.f ? launch_tile<M, N, C, 0, false, C == 1 && N == 2>(                                        \
                             grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, \
                             stats, g, Ncol, act, sched, nullptr, nullptr, oscale)                                   \
                       : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,                 \
-                                             (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched);
+                                             (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, nullptr,     \
+                                             nullptr, 0.f, bny);
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;
@@ -878,6 +936,7 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   int rc = -2;
   // FN_F8_DBG (timing experiments only, wrong results): 1 no weight loads, 2 no halo reads,
   // 4 no halo DMA (and sums of them), 16 cycle stamps (barrier-A wait, job, epilogue)
+#ifdef FN_EXPERIMENTS
   static const int f8dbg = [] { const char* e = getenv("FN_F8_DBG"); return e ? atoi(e) : 0; }();
   if (f8dbg) {
     static long long* stamps = nullptr;
@@ -905,6 +964,8 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
     }
     return 0;
   }
+#endif  // FN_EXPERIMENTS
+#ifdef FN_EXPERIMENTS
 #define CT_F8_CASE(M, N, C)                                                                                        \
   if (MT == M && NT == N && CPP == C)                                                                              \
     rc = i8 ? launch_tile<M, N, C, 0, true, false, C == 2>(grid, lds, st, src, (const uint4*)wp,                     \
@@ -914,6 +975,14 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
             : launch_tile<M, N, C, 0, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,              \
                                             (const int4*)ktab, zp, bias, out, nullptr, g, Ncol, f8act, sched,      \
                                             nullptr, scale, oscale);
+#else   // (the int8 stem instance is an experiment build: measured no faster, and seed-dependent top-1)
+  if (i8) return -2;
+#define CT_F8_CASE(M, N, C)                                                                                        \
+  if (MT == M && NT == N && CPP == C)                                                                              \
+    rc = launch_tile<M, N, C, 0, true>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,                   \
+                                       (const int4*)ktab, zp, bias, out, nullptr, g, Ncol, f8act, sched, nullptr,  \
+                                       scale, oscale);
+#endif
   CT_F8_INSTANCES(CT_F8_CASE)
 #undef CT_F8_CASE
   if (rc) return rc;

@@ -382,6 +382,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile32_kernel(const unsigned 
 #define C32_INSTANCES(X) X(4, 1) X(5, 1) X(4, 2) X(5, 2) X(4, 4) X(5, 4)
 
 extern "C" int fn_conv_tile32_supported(int MB, int CPP) {
+#ifndef FN_EXPERIMENTS
+  return 0;   // (measured 3.5 % slower per step, profiles/r4_m32_ab.md: an experiment build only)
+#endif
 #define C32_SUP(M, C) if (MB == M && CPP == C) return 1;
   C32_INSTANCES(C32_SUP)
 #undef C32_SUP
@@ -456,7 +459,9 @@ extern "C" int fn_conv_tile32(const void* src, const void* wp, const void* rowta
                                                      oscale)                                                        \
                       : launch_tile32<M, C, false>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,      \
                                                    (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, 0.f);
+#ifdef FN_EXPERIMENTS
   C32_INSTANCES(C32_CASE)
+#endif
 #undef C32_CASE
   if (rc) return rc;
   FN_CHECK_LAUNCH();

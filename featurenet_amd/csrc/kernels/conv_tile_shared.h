@@ -128,6 +128,12 @@ __device__ __forceinline__ void ct_dma_job(const TileGeom& g, const unsigned cha
   }
 }
 
+// bytes of one LDS mask buffer of the relu-mask dgrad epilogue: rows x Ncol / 8, rounded up to
+// whole 64-dword DMA rows
+__host__ __device__ constexpr int ct_mask_bytes(int rows, int Ncol, bool on) {
+  return on ? (rows * (Ncol >> 3) + 255) / 256 * 256 : 0;
+}
+
 #define CT_GEOM_LEN 31
 static inline TileGeom parse_tile(const int* v) {
   TileGeom g;

@@ -28,6 +28,15 @@ __device__ __forceinline__ void ct_glds16_s(const void* sbase, unsigned voff, un
                : "memory");
 }
 
+// LDS-DMA of one dword per lane into lds_dst + 4 * lane (lds_dst wave-uniform)
+__device__ __forceinline__ void ct_glds4(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
 __device__ __forceinline__ unsigned ct_lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
 }

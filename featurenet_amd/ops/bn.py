@@ -74,6 +74,35 @@ def _bwd_param_grads(dz2, y2, prm, act, beta=None, gamma=None, part=None):
     return db, dg
 
 
+def _bwd_identity(g2, y2, prm, beta, gamma, gslab, wpart):
+    """BN(+relu) backward from the statistics identity (``bn_pool.hip`` bn_bwd_prep_kernel):
+    ``g2`` = dz * relu'(z) [M, C] from the consuming conv's dgrad, ``gslab`` its column sums
+    [nbg, 2, C] (row 0), ``wpart`` the partials of S = sum W . dW [nbw, C].  Returns
+    (dy, dbeta, dgamma); dbeta / dgamma go straight into the flat gradients when offered."""
+    M, C = y2.shape
+    K = _native.kernels()
+    st = _native.stream(y2)
+    db, dg = grad_target(beta), grad_target(gamma)
+    tmp = torch.empty(3, C, dtype=torch.float32, device=y2.device)
+    if db is None or db.numel() != C:
+        db = tmp[0]
+    if dg is None or dg.numel() != C:
+        dg = tmp[1]
+    kc = torch.empty(3, C, dtype=torch.float32, device=y2.device)
+    K.bn_bwd_prep(gslab.data_ptr(), gslab.shape[0], wpart.data_ptr(), wpart.shape[0], C, float(M),
+                  _native.ptr(beta), prm[0].data_ptr(), prm[1].data_ptr(), prm[2].data_ptr(), db.data_ptr(),
+                  kc.data_ptr(), st, [gslab.numel(), wpart.numel(), kc.numel()])
+    dy = torch.empty_like(y2)
+    nb = K.bn_bwd_apply_k_blocks(M, C)
+    part = torch.empty(nb, 2, C, dtype=torch.float32, device=y2.device)
+    K.bn_bwd_apply_k(g2.data_ptr(), y2.data_ptr(), kc.data_ptr(), prm[0].data_ptr(), prm[1].data_ptr(), dy.data_ptr(),
+                     M, C, part.data_ptr(), nb, st, [g2.numel(), y2.numel(), dy.numel(), part.numel()])
+    # dgamma = sum g * xhat, summed exactly from (g, y) by the apply pass (row 1 of its slab)
+    K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, tmp[2].data_ptr(), dg.data_ptr(), 0, 0, 1,
+                  st)
+    return dy, db, dg
+
+
 def _bwd_input(dz2, y2, prm, dbeta, dgamma, act, training):
     M, C = y2.shape
     dy = torch.empty_like(y2)
@@ -100,10 +129,15 @@ class BatchNormActFn(torch.autograd.Function):
         else:
             prm = _eval_params(gamma, beta, rmean, rvar, eps, C, y.device)
         z = torch.empty_like(y)
+        # the relu-mask bytes of the statistics identity (ops/bnfuse.py): the consuming conv's
+        # dgrad applies them, so the backward needs no colstats pass
+        mask = (torch.empty(y2.numel() // 8, dtype=torch.uint8, device=y.device)
+                if tag and bnfuse.identity_ok(C, act) else None)
         _native.kernels().bn_apply(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), z.data_ptr(), y2.numel(), C,
-                                   act, _native.stream(y))
+                                   act, _native.stream(y), _native.ptr(mask), 0 if mask is None else mask.numel())
         if tag and act in (0, 1):                # none / relu: the dgrad epilogue's forms
-            bnfuse.tag_output(z, y, prm, act)
+            bnfuse.tag_output(z, y, prm, act, mask)
+        ctx.mask = mask                          # (alive until the backward: the conv's dgrad reads it)
         ctx.save_for_backward(y, prm)
         ctx.act, ctx.training = act, training
         ctx.has_gamma, ctx.has_beta = gamma is not None, beta is not None
@@ -117,6 +151,14 @@ class BatchNormActFn(torch.autograd.Function):
         y2 = y.reshape(-1, C)
         dz2 = dz.contiguous().to(torch.bfloat16).reshape(-1, C)
         part = bnfuse.take(dz2, y) if ctx.training else None
+        ctx.mask = None
+        if isinstance(part, tuple) and ctx.needs_input_grad[0]:
+            dy, dbeta, dgamma = _bwd_identity(dz2, y2, prm, *ctx.params, gslab=part[1], wpart=part[2])
+            return (dy.reshape(y.shape), dgamma if ctx.has_gamma else None, dbeta if ctx.has_beta else None,
+                    None, None, None, None, None, None, None, None)
+        if isinstance(part, tuple):
+            part = None                          # (no input gradient wanted: the colstats pass;
+            #                                       dz2 is g -- masked -- which it masks again)
         dbeta = dgamma = None
         if ctx.training or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             # (eval mode with frozen parameters -- input gradients of robustness attacks -- needs

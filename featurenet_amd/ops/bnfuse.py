@@ -53,6 +53,21 @@ def enabled() -> bool:
     return mode == "1"
 
 
+def identity_enabled() -> bool:
+    """BN backward without the colstats pass (``FN_BN_IDENTITY``, default on): the BN forward
+    writes its relu mask, the consuming conv's 16x16x32 tile dgrad stores g = dz * mask and its
+    column sums, and ``sum g * xhat`` comes from the adjoint identity
+    ``sum_p dz z = sum W * dW`` over the conv's weights and weight gradient
+    (``bn_pool.hip`` bn_bwd_prep_kernel)."""
+    return os.environ.get("FN_BN_IDENTITY", "0") != "0"
+
+
+def identity_ok(C: int, act: int) -> bool:
+    """The identity path's shape conditions: relu (the mask), 32-channel multiples (whole mask
+    dwords per position for the dgrad loader's DMA), 8-channel chunks dividing 256."""
+    return identity_enabled() and act == 1 and C % 32 == 0 and 256 % (C // 8) == 0
+
+
 def pool_stats_enabled() -> bool:
     """BN-backward moments inside the max-pool backward (FN_POOL_BN_STATS, default on)."""
     return os.environ.get("FN_POOL_BN_STATS", "1") != "0"
@@ -70,34 +85,40 @@ def _purge(d: dict, limit: int = 256) -> None:
             d.pop(k, None)
 
 
-def tag_output(z: torch.Tensor, y: torch.Tensor, prm: torch.Tensor, act: int) -> None:
-    """BN forward (training): z = act(y * prm[2] + prm[3]), prm = (mean, invstd, scale, shift)."""
-    if not enabled():
+def tag_output(z: torch.Tensor, y: torch.Tensor, prm: torch.Tensor, act: int, mask=None) -> None:
+    """BN forward (training): z = act(y * prm[2] + prm[3]), prm = (mean, invstd, scale, shift);
+    ``mask``: z's relu-mask bytes (the identity path; the BN keeps it alive until its backward)."""
+    if not (enabled() or mask is not None):
         return
     with _LOCK:
         _purge(_FWD)
-        _FWD[z.data_ptr()] = (weakref.ref(z), weakref.ref(y), weakref.ref(prm), act)
+        _FWD[z.data_ptr()] = (weakref.ref(z), weakref.ref(y), weakref.ref(prm), act,
+                              weakref.ref(mask) if mask is not None else None)
 
 
 def source_of(x: torch.Tensor):
-    """(y, prm, act) when ``x`` is (a same-extent view of) a tagged BN output, else None."""
+    """(y, prm, act, mask) when ``x`` is (a same-extent view of) a tagged BN output, else None
+    (mask: the relu-mask bytes, or None)."""
     e = _FWD.get(x.data_ptr())
     if e is None:
         return None
     z, y, prm = e[0](), e[1](), e[2]()
     if z is None or y is None or prm is None or z.numel() != x.numel() or not x.is_contiguous():
         return None
-    return y, prm, e[3]
+    mask = e[4]() if e[4] is not None else None
+    return y, prm, e[3], mask
 
 
-def offer(dz: torch.Tensor, slab: torch.Tensor, y: torch.Tensor) -> None:
+def offer(dz: torch.Tensor, slab, y: torch.Tensor) -> None:
+    """``slab``: the raw-moment slab [nb, 2, C] (conv_tile32), or ``("identity", gslab, wpart)``
+    (the 16x16x32 dgrad's sum-g slab and the S partials of the conv's W . dW)."""
     with _LOCK:
         _purge(_BWD)
         _BWD[dz.data_ptr()] = (weakref.ref(dz), slab, weakref.ref(y), dz._version)
 
 
 def take(dz: torch.Tensor, y: torch.Tensor):
-    """The backward-statistics slab offered for this (dz, y) pair, or None."""
+    """What :func:`offer` handed over for this (dz, y) pair, or None."""
     with _LOCK:
         e = _BWD.pop(dz.data_ptr(), None)
     if e is None:

@@ -578,6 +578,19 @@ def igemm_wgrad_cropped(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, c0:
     return (out, db) if with_db else out
 
 
+def bn_wdot(w: torch.Tensor, dw: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
+    """Per-block partial sums [nb, C] of sum_{k,t} bf16(W[k,t,c]) * dW[k,t,c] (fp32 weights and
+    weight gradient of a conv over C input channels; ``bn_pool.hip`` bn_wdot_kernel)."""
+    C = w.shape[-1]
+    R = w.numel() // C
+    w2 = w.float().contiguous()
+    nb = int(max(1, min(64, -(-R // (256 // C)))))
+    part = torch.empty(nb, C, dtype=torch.float32, device=w.device)
+    _native.kernels().bn_wdot(w2.data_ptr(), dw.data_ptr(), part.data_ptr(), R, C, nb, _native.stream(w2),
+                              [w2.numel(), dw.numel(), part.numel()])
+    return part
+
+
 def native_colsum(x2: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """Per-column sum of a [M, C] bf16 tensor in fp32 (bias gradients); into ``out`` (fp32
     [C], e.g. the bias's flat gradient slice) when given."""
@@ -909,11 +922,16 @@ class ConvFn(torch.autograd.Function):
             db = native_colsum(dy2, out=grad_target(ctx.bparam)) if (ctx.has_b and ctx.needs_input_grad[2]) else None
             return dx, dw, db, None, None, None
         dx = None
+        ident = None                     # the statistics identity's sum-g slab (bnfuse)
+        bn_y = None
         if ctx.x_needs:
             if ctx.bn_src is not None:
+                bn_y = ctx.bn_src[0]
                 dx, slab = native_conv_dgrad(dy, w.detach(), spec, bn=ctx.bn_src)
-                if slab is not None:
-                    bnfuse.offer(dx, slab, ctx.bn_src[0])
+                if isinstance(slab, tuple):
+                    ident = slab[1]              # (offered below, with S from this conv's dW)
+                elif slab is not None:
+                    bnfuse.offer(dx, slab, bn_y)
                 ctx.bn_src = None
             else:
                 dx = native_conv_dgrad(dy, w.detach(), spec)
@@ -938,6 +956,13 @@ class ConvFn(torch.autograd.Function):
                 dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w))
         if want_db and db is None:
             db = native_colsum(dy.reshape(-1, spec.K), out=grad_target(ctx.bparam))
+        if ident is not None:
+            if dw is not None and dw.dtype == torch.float32 and dw.is_contiguous() and dw.numel() == w.numel():
+                # S = sum W . dW per input channel, read before any data-parallel all-reduce of dW
+                # (its hook fires after this backward returns)
+                bnfuse.offer(dx, ("identity", ident, bn_wdot(w.detach(), dw, spec)), bn_y)
+            # (else: no offer -- the BN backward's colstats pass reads the masked dx, which its
+            # relu mask leaves unchanged)
         return dx, dw, db, None, None, None
 
 

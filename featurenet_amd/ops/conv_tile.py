@@ -41,8 +41,18 @@ def m32_enabled() -> bool:
     v_mfma_f32_32x32x16_bf16 kernel (conv_tile32.hip); '0' (default) keeps every plan on the
     16x16x32 kernel.  Round 4 measured the 32x32x16 k-loop 2-8 % slower on the FeatureNet-3D
     layers (conv2 fwd 539 vs 513 us, dgrad 707 vs 669; the step 5.13 vs 4.97 ms on one box,
-    profiles/r4_m32_ab.md), the exception being conv3's dgrad with 640-row tiles."""
-    return os.environ.get("FN_TILE_M32", "0") == "1"
+    profiles/r4_m32_ab.md), the exception being conv3's dgrad with 640-row tiles -- so the
+    kernel is only in experiment builds (``FN_BUILD_EXPERIMENTS=1``)."""
+    return os.environ.get("FN_TILE_M32", "0") == "1" and experiments_built()
+
+
+def experiments_built() -> bool:
+    """The kernel library was built with ``FN_BUILD_EXPERIMENTS=1`` (conv_tile32, the int8
+    fp8-stem instance, the timing-only variants)."""
+    try:
+        return bool(_native.kernels().experiments_built())
+    except Exception:                            # noqa: BLE001 - no library (CPU): nothing built
+        return False
 
 
 def red_bytes(NT: int) -> int:
@@ -394,6 +404,16 @@ def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bo
     return out
 
 
+def mask_dgrad_ok(p: TilePlan, ncol: int) -> bool:
+    """The relu-mask dgrad epilogue fits: whole mask dwords per position and the two LDS mask
+    buffers (rows x ncol / 8 bytes each, 256-B rounded) within the CU's LDS."""
+    if ncol % 32:
+        return False
+    mb = -(-p.rows * (ncol // 8) // 256) * 256
+    lds = 2 * p.BUF + 64 + red_bytes(p.NT) + (p.nks + 4 + 2) * 16 + p.HPpad * 8 + 2 * mb
+    return lds <= LDS_MAX
+
+
 def workers(p: TilePlan, geom: list, ncol: int) -> int:
     return int(_native.kernels().conv_tile_workers(geom, ncol, p.NT))
 
@@ -405,7 +425,7 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
     kt = ktab_tensor(p, kdims, src5.device)
     ext = [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4]
     if bny is not None:
-        ext += [bny.numel(), bnp.numel()]
+        ext += [bny.numel()] + ([bnp.numel()] if bnp is not None else [])
     if p.m32:
         _native.kernels().conv_tile32(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                       zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
@@ -447,12 +467,20 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None):
                     (spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw))
     wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
-    # the statistics epilogue: conv_tile32 plans (their LDS holds the BN scale / shift already)
+    mask = bn[3] if bn is not None else None
+    if bn is not None and not p.m32 and mask is not None and mask_dgrad_ok(p, spec.C):
+        # the relu-mask epilogue (statistics identity, ops/bnfuse.py): dx holds g = dz * relu'(z)
+        # and the slab's row 0 its column sums
+        assert mask.numel() * 8 == dx.numel() and mask.dtype == torch.uint8
+        slab = torch.empty(workers(p, geom, spec.C), 2, spec.C, dtype=torch.float32, device=dy5.device)
+        run(dy5, wpk, None, dx, slab, p, geom, kd, spec.C, 0, bny=mask)
+        return dx, ("identity", slab)
+    # the raw-moment statistics epilogue: conv_tile32 plans (their LDS holds the BN scale / shift)
     fuse = p.m32
     if bn is None or not fuse:
         run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
         return dx if bn is None else (dx, None)
-    y, prm, act = bn
+    y, prm, act = bn[:3]
     assert y.shape == dx.shape and y.dtype == torch.bfloat16 and y.is_contiguous() and prm.shape == (4, spec.C)
     slab = torch.empty(workers(p, geom, spec.C), 2, spec.C, dtype=torch.float32, device=dy5.device)
     run(dy5, wpk, None, dx, slab, p, geom, kd, spec.C, act, bny=y, bnp=prm.contiguous())

@@ -42,6 +42,10 @@ def test_dgrad_bn_stats_match_colstats(monkeypatch, N, S, cin, cmid, k):
     from featurenet_amd.models.layers import Conv
 
     assert _native.kernels() is not None
+    from featurenet_amd.ops import conv_tile as ct
+
+    if not ct.experiments_built():
+        pytest.skip("conv_tile32 (its raw-moment dgrad epilogue) is an experiment build")
     monkeypatch.setenv("FN_CONV_TILE", "2")      # the tile kernel (the fused epilogue lives there)
     monkeypatch.setenv("FN_TILE_M32", "1")       # the 32x32x16 kernel (its dgrad has the epilogue)
     torch.manual_seed(0)
@@ -63,7 +67,10 @@ def test_dgrad_bn_stats_match_colstats(monkeypatch, N, S, cin, cmid, k):
 def test_featurenet3d_fused_bn_backward(monkeypatch):
     """Production layer shapes (64^3, batch 8): every conv2..4 dgrad feeds its BN the fused sums."""
     from featurenet_amd.models.featurenet3d import FeatureNet3D
+    from featurenet_amd.ops import conv_tile as ct
 
+    if not ct.experiments_built():
+        pytest.skip("conv_tile32 (its raw-moment dgrad epilogue) is an experiment build")
     torch.manual_seed(1)
     monkeypatch.setenv("FN_TILE_M32", "1")
     dev = torch.device("cuda", 0)
@@ -185,3 +192,78 @@ def test_forked_bn_output_falls_back(monkeypatch):
         a, b = g0[n], g1[n]
         err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
         assert err < 2e-3, f"{n}: rel err {err:.2e}"
+
+
+def _count_identity(monkeypatch):
+    from featurenet_amd.ops import bn as bnm
+
+    calls = {"identity": 0}
+    orig = bnm._bwd_identity
+
+    def wrapped(*a, **k):
+        calls["identity"] += 1
+        return orig(*a, **k)
+
+    monkeypatch.setattr(bnm, "_bwd_identity", wrapped)
+    return calls
+
+
+def _grads_ident(model, x, on: bool, monkeypatch):
+    monkeypatch.setenv("FN_BN_IDENTITY", "1" if on else "0")
+    monkeypatch.setenv("FN_BN_DGRAD_FUSE", "0")
+    model.zero_grad(set_to_none=True)
+    out = model(x)
+    loss = (out.float() * torch.linspace(-1, 1, out.shape[-1], device=x.device)).sum()
+    loss.backward()
+    return {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}
+
+
+def test_identity_featurenet3d_matches_colstats(monkeypatch):
+    """Production shapes (64^3, batch 8): the BN backward of conv1-3's BNs from the statistics
+    identity (relu mask in the dgrad epilogue, S = sum W . dW) against the colstats pass."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3D
+
+    monkeypatch.setenv("FN_TILE_M32", "0")
+    torch.manual_seed(2)
+    dev = torch.device("cuda", 0)
+    model = FeatureNet3D().to(dev)
+    x = (torch.rand(8, 64, 64, 64, 1, device=dev) < 0.3).to(torch.bfloat16)
+    calls = _count_identity(monkeypatch)
+    g0 = _grads_ident(model, x, False, monkeypatch)
+    assert calls["identity"] == 0
+    g1 = _grads_ident(model, x, True, monkeypatch)
+    assert calls["identity"] == 3, f"identity path taken {calls['identity']} times (conv2-4 inputs)"
+    for n in g0:
+        a, b = g0[n], g1[n]
+        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
+        assert err < 5e-3, f"{n}: rel err {err:.2e}"
+
+
+@pytest.mark.parametrize("gscale", [1.0, -0.5, 1e-4])
+def test_identity_any_gamma(monkeypatch, gscale):
+    """conv -> BN(relu) -> conv with gamma positive, negative or ~0 and large beta: the identity
+    path's gradients equal the colstats path's (no division by gamma anywhere)."""
+    from torch import nn
+
+    from featurenet_amd.models.layers import Conv
+
+    monkeypatch.setenv("FN_CONV_TILE", "2")
+    monkeypatch.setenv("FN_TILE_M32", "0")
+    torch.manual_seed(3)
+    dev = torch.device("cuda", 0)
+    model = nn.Sequential(Conv(16, 32, 3, 1, "valid", bn=True, act="relu", init="he"),
+                          Conv(32, 32, 3, 1, "valid", bn=True, act="relu", init="he")).to(dev)
+    with torch.no_grad():
+        for m in model.modules():
+            if getattr(m, "gamma", None) is not None:
+                m.gamma.mul_(gscale)
+                m.beta.add_(torch.linspace(-2, 3, m.beta.numel(), device=dev))
+    x = torch.randn(4, 20, 20, 20, 16, device=dev).to(torch.bfloat16)
+    calls = _count_identity(monkeypatch)
+    g0 = _grads_ident(model, x, False, monkeypatch)
+    g1 = _grads_ident(model, x, True, monkeypatch)
+    assert calls["identity"] >= 1
+    for n in g0:
+        a, b = g0[n], g1[n]
+        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
+        assert err < 1e-2, f"{n}: rel err {err:.2e}"

@@ -47,6 +47,8 @@ def test_conv_tile_fwd_dgrad(case, m32, monkeypatch):
     """m32 = 1: whole 32-column blocks on the 32x32x16 kernel (conv_tile32); 0: every plan on
     the 16x16x32 kernel."""
     assert _native.kernels_available(), "HIP kernel library (_C) must be built and loadable on the GPU box"
+    if m32 == "1" and not ct.experiments_built():
+        pytest.skip("conv_tile32 (32x32x16 MFMA) is an experiment build (FN_BUILD_EXPERIMENTS=1)")
     monkeypatch.setenv("FN_TILE_M32", m32)
     N, D, H, W, C, K, k, pad = case
     torch.manual_seed(0)

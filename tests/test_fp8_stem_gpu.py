@@ -136,6 +136,8 @@ def test_bf16_stem_e4m3_epilogue_matches_quant_pass(monkeypatch):
     assert same > 0.999, same
 
 
+@pytest.mark.skipif(not __import__("featurenet_amd.ops.conv_tile", fromlist=["x"]).experiments_built(),
+                    reason="the int8 stem instance is an experiment build (FN_BUILD_EXPERIMENTS=1)")
 def test_int8_tile_kernel_exact():
     """The int8 instance of the fp8 tile kernel (two v_mfma_i32_16x16x64_i8 per fragment pair)
     against an exact integer conv: int8 x, int8 w, int32 sums, then scale + bias + relu."""
@@ -158,6 +160,8 @@ def test_int8_tile_kernel_exact():
     torch.testing.assert_close(y.double(), ref, rtol=8e-3, atol=1e-3)   # (bf16 output rounding)
 
 
+@pytest.mark.skipif(not __import__("featurenet_amd.ops.conv_tile", fromlist=["x"]).experiments_built(),
+                    reason="the int8 stem instance is an experiment build (FN_BUILD_EXPERIMENTS=1)")
 def test_int8_stem_model_matches_bf16_model():
     """The fp8 model with the int8 stem (FN_F8_STEM=i8): closer to the bf16 model than the e4m3
     stem, as close as the bf16 stem."""
