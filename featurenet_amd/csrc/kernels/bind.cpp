@@ -65,10 +65,11 @@ int fn_bn_finalize(const float*, int, int, double, const float*, const float*, f
 int fn_bn_apply(const void*, const float*, const float*, void*, long long, int, int, hipStream_t, void*);
 int fn_bn_wdot(const float*, const float*, float*, int, int, int, hipStream_t);
 int fn_bn_bwd_prep(const float*, int, const float*, int, int, double, const float*, const float*, const float*,
-                   const float*, float*, float*, hipStream_t);
+                   const float*, const float*, const float*, float*, float*, const void*, const void*, long long,
+                   hipStream_t);
 int fn_bn_bwd_apply_k_blocks(long long, int);
-int fn_bn_bwd_apply_k(const void*, const void*, const float*, const float*, const float*, void*, long long, int,
-                      float*, int, hipStream_t);
+int fn_bn_bwd_apply_k(const void*, const void*, const float*, const float*, const float*, const float*, void*,
+                      long long, int, float*, int, hipStream_t);
 int fn_bn_bwd_apply(const void*, const void*, const float*, const float*, const float*, const float*, const float*,
                     const float*, void*, long long, int, float, int, hipStream_t);
 int fn_bn_bwd_apply_s2d(const void*, const void*, const float*, const float*, const float*, const float*,
@@ -108,6 +109,7 @@ int fn_conv_wtile(const void*, const void*, float*, float*, const void*, const v
                   int*, hipStream_t);
 int fn_conv_wtile_supported(int, int);
 int fn_tile_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int fn_tile_pack_w2(const float*, void*, void*, int, int, int, const int*, const int*, hipStream_t);
 }
 
 template <typename T>
@@ -313,6 +315,17 @@ PYBIND11_MODULE(_C, m) {
                           int dgrad, uintptr_t st, int nt) {
     chk(fn_tile_pack_w(P<const float*>(w), P<void*>(out), K, T, C, CS, nks, nct, nslice, dgrad, nt, S(st)),
         "tile_pack_w");
+  });
+  m.def("tile_pack_w2", [](uintptr_t w, uintptr_t out0, uintptr_t out1, int K, int T, int C, std::vector<int> p0,
+                           std::vector<int> p1, uintptr_t st, std::vector<long long> ext) {
+    // p = {CS, nks, nct, nslice, dgrad, nt}; ext = {numel(w), numel(out0) and numel(out1) in uint4 x 2 bf16x4}
+    need(p0, 6, "tile_pack_w2");
+    need(p1, 6, "tile_pack_w2");
+    fits(ext, 0, (long long)K * T * C, "tile_pack_w2", "w");
+    fits(ext, 1, ((long long)p0[3] * p0[1] + 4) * p0[2] * 64 * 8, "tile_pack_w2", "out0");
+    fits(ext, 2, ((long long)p1[3] * p1[1] + 4) * p1[2] * 64 * 8, "tile_pack_w2", "out1");
+    chk(fn_tile_pack_w2(P<const float*>(w), P<void*>(out0), P<void*>(out1), K, T, C, p0.data(), p1.data(), S(st)),
+        "tile_pack_w2");
   });
   m.def("igemm_pack_w", [](uintptr_t w, uintptr_t out, int K0, int C0, int K, int T, int C, int mode, int ld, int KW,
                            int R, uintptr_t st, std::vector<long long> ext) {
@@ -550,26 +563,32 @@ PYBIND11_MODULE(_C, m) {
     fits(ext, 2, (long long)nb * C, "bn_wdot", "part");
     chk(fn_bn_wdot(P<const float*>(w), P<const float*>(dw), P<float*>(part), R, C, nb, S(st)), "bn_wdot");
   });
-  m.def("bn_bwd_prep", [](uintptr_t gslab, int nbg, uintptr_t wpart, int nbw, int C, double count, uintptr_t beta,
-                          uintptr_t mean, uintptr_t invstd, uintptr_t scale, uintptr_t dbeta, uintptr_t kc, uintptr_t st,
+  m.def("bn_bwd_prep", [](uintptr_t gslab, int nbg, uintptr_t wpart, int nbw, int C, double count, uintptr_t gamma,
+                          uintptr_t beta, uintptr_t mean, uintptr_t invstd, uintptr_t scale, uintptr_t shift,
+                          uintptr_t dbeta, uintptr_t kc, uintptr_t g, uintptr_t y, long long M, uintptr_t st,
                           std::vector<long long> ext) {
     fits(ext, 0, 2LL * nbg * C, "bn_bwd_prep", "gslab");
     fits(ext, 1, (long long)nbw * C, "bn_bwd_prep", "wpart");
     fits(ext, 2, 3LL * C, "bn_bwd_prep", "kc");
-    chk(fn_bn_bwd_prep(P<const float*>(gslab), nbg, P<const float*>(wpart), nbw, C, count, P<const float*>(beta),
-                       P<const float*>(mean), P<const float*>(invstd), P<const float*>(scale), P<float*>(dbeta),
-                       P<float*>(kc), S(st)),
+    fits(ext, 3, M * C, "bn_bwd_prep", "g");
+    fits(ext, 4, M * C, "bn_bwd_prep", "y");
+    chk(fn_bn_bwd_prep(P<const float*>(gslab), nbg, P<const float*>(wpart), nbw, C, count, P<const float*>(gamma),
+                       P<const float*>(beta), P<const float*>(mean), P<const float*>(invstd), P<const float*>(scale),
+                       P<const float*>(shift), P<float*>(dbeta), P<float*>(kc), P<const void*>(g), P<const void*>(y),
+                       M, S(st)),
         "bn_bwd_prep");
   });
   m.def("bn_bwd_apply_k_blocks", &fn_bn_bwd_apply_k_blocks);
-  m.def("bn_bwd_apply_k", [](uintptr_t g, uintptr_t y, uintptr_t kc, uintptr_t mean, uintptr_t invstd, uintptr_t dy,
-                             long long M, int C, uintptr_t part, int nb, uintptr_t st, std::vector<long long> ext) {
+  m.def("bn_bwd_apply_k", [](uintptr_t g, uintptr_t y, uintptr_t kc, uintptr_t mean, uintptr_t invstd,
+                             uintptr_t shift, uintptr_t dy, long long M, int C, uintptr_t part, int nb, uintptr_t st,
+                             std::vector<long long> ext) {
     fits(ext, 0, M * C, "bn_bwd_apply_k", "g");
     fits(ext, 1, M * C, "bn_bwd_apply_k", "y");
     fits(ext, 2, M * C, "bn_bwd_apply_k", "dy");
     fits(ext, 3, 2LL * nb * C, "bn_bwd_apply_k", "part");
     chk(fn_bn_bwd_apply_k(P<const void*>(g), P<const void*>(y), P<const float*>(kc), P<const float*>(mean),
-                          P<const float*>(invstd), P<void*>(dy), M, C, P<float*>(part), nb, S(st)),
+                          P<const float*>(invstd), P<const float*>(shift), P<void*>(dy), M, C, P<float*>(part), nb,
+                          S(st)),
         "bn_bwd_apply_k");
   });
   m.def("bn_bwd_apply", [](uintptr_t dz, uintptr_t y, uintptr_t scale, uintptr_t shift, uintptr_t mean,

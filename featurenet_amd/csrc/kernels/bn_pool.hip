@@ -312,12 +312,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
 // holds exactly (dW = sum_q dy'[q,k] z[q+t,c]), so with g = dz * relu'(z) and, where
 // relu' = 1, z = gamma * xhat + beta:
 //     gamma * sum g*xhat = S - beta * sum g,      S = sum_{k,t} W * dW
-// The consuming conv's dgrad epilogue writes g (dz masked by the bit mask bn_apply wrote) and
-// its column sums (sum g); bn_wdot_kernel gives S; bn_bwd_prep_kernel the apply constants
+// The consuming conv's dgrad epilogue sums g (dz masked by the bit mask bn_apply wrote; dz is
+// stored unmasked, the true gradient of z); bn_wdot_kernel gives S; bn_bwd_prep_kernel the
+// apply constants
 //     dy = k1*g + k2*y + k3,  k1 = scale, k2 = -invstd^2 * G / M,
 //                            k3 = -scale * sum g / M + mean * invstd^2 * G / M,  G = S - beta sum g
-// (no division by gamma: the input gradient is exact for any gamma).  dgamma itself, only read
-// by the optimizer, is summed exactly from (g, y) inside the apply pass (bn_bwd_apply_k_kernel).
+// (no division by gamma; channels whose gamma is too small against beta for z's bf16 resolution
+// take G from (g, y) directly, see bn_bwd_prep_kernel).  dgamma itself, only read by the
+// optimizer, is summed exactly from (g, y) inside the apply pass (bn_bwd_apply_k_kernel).
 // W is rounded to bf16 as the dgrad's packed weights are.
 // ---------------------------------------------------------------------------
 
@@ -347,18 +349,38 @@ __global__ __launch_bounds__(256) void bn_wdot_kernel(const float* __restrict__ 
 
 // One block per channel: sum g (the dgrad epilogue's slab rows, [nbg][2][C] row 0) and S (the
 // wdot partials [nbw][C]) in fp64 -> dbeta = sum g and the apply constants kc[3][C].
+// Conditioning: z is stored in bf16, so S = sum dz * z carries ~2^-9 |z| of rounding per term,
+// and G = S - beta * sum g cancels down to gamma * sum g * xhat -- a channel whose |gamma| is
+// small against |beta| (z ~ beta: gamma * xhat below z's bf16 resolution) cannot get G from the
+// identity.  Such a channel (|gamma| < |beta| / 4) sums g * (y - mean) exactly from g and y
+// itself (a strided pass over that one channel: rare, and only the unsafe channels pay it).
 __global__ __launch_bounds__(256) void bn_bwd_prep_kernel(const float* __restrict__ gslab, int nbg,
                                                           const float* __restrict__ wpart, int nbw, int C,
-                                                          double count, const float* __restrict__ beta,
+                                                          double count, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd,
-                                                          const float* __restrict__ scale, float* __restrict__ dbeta,
-                                                          float* __restrict__ kc) {
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, float* __restrict__ dbeta,
+                                                          float* __restrict__ kc, const bf16* __restrict__ g,
+                                                          const bf16* __restrict__ y, long long M) {
   __shared__ double sa[256], sb[256];
   const int c = blockIdx.x;
+  const double gm = gamma ? (double)gamma[c] : 1.0, bt = beta ? (double)beta[c] : 0.0;
+  const bool exact = fabs(gm) < 0.25 * fabs(bt);
   double a = 0.0, b = 0.0;
   for (int i = threadIdx.x; i < nbg; i += 256) a += (double)gslab[(long long)i * 2 * C + c];
-  for (int i = threadIdx.x; i < nbw; i += 256) b += (double)wpart[(long long)i * C + c];
+  if (exact) {
+    const float mu = mean[c], scf = scale[c], shf = shift[c];
+    float t = 0.f;
+    for (long long m = threadIdx.x; m < M; m += 256) {
+      const float yv = bf2f(y[m * C + c]);
+      if (yv * scf + shf > 0.f) t += bf2f(g[m * C + c]) * (yv - mu);
+    }
+    b = (double)t;                              // sum g * (y - mean), g = dz * relu'
+  } else {
+    for (int i = threadIdx.x; i < nbw; i += 256) b += (double)wpart[(long long)i * C + c];
+  }
   sa[threadIdx.x] = a;
   sb[threadIdx.x] = b;
   __syncthreads();
@@ -370,10 +392,10 @@ __global__ __launch_bounds__(256) void bn_bwd_prep_kernel(const float* __restric
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double sg = sa[0], S = sb[0];
-    const double bt = beta ? (double)beta[c] : 0.0;
+    const double sg = sa[0];
     const double is = (double)invstd[c], sc = (double)scale[c];
-    const double G = S - bt * sg;                // gamma * sum g*xhat
+    // G = gamma * sum g * xhat: from the identity, or exactly (gamma * invstd * sum g (y - mean))
+    const double G = exact ? gm * is * sb[0] : sb[0] - bt * sg;
     dbeta[c] = (float)sg;
     kc[c] = (float)sc;
     kc[C + c] = (float)(-is * is * G / count);
@@ -381,25 +403,28 @@ __global__ __launch_bounds__(256) void bn_bwd_prep_kernel(const float* __restric
   }
 }
 
-// dy = k1*g + k2*y + k3 (g: the masked dz) and the exact dgamma partials sum g*(y-mean)*invstd as
+// dy = k1*g + k2*y + k3 (g = dz * relu'(y * scale + shift)) and the exact dgamma partials
+// sum g*(y-mean)*invstd as
 // rows part[block][2][C] (row 0 zero; bn_finalize mode 1 turns row 1 into dgamma).  8 channels
 // per thread, fixed (C / 8 divides 256, the stride a multiple of 256); grid-stride over a
 // resident-sized grid.
 __global__ __launch_bounds__(256) void bn_bwd_apply_k_kernel(const bf16* __restrict__ g, const bf16* __restrict__ y,
                                                              const float* __restrict__ kc,
                                                              const float* __restrict__ mean,
-                                                             const float* __restrict__ invstd, bf16* __restrict__ dy,
+                                                             const float* __restrict__ invstd,
+                                                             const float* __restrict__ shift, bf16* __restrict__ dy,
                                                              long long nvec, int C, float* __restrict__ part) {
   const int cpr = C / 8;
   const int tid = threadIdx.x;
   const int c0 = (tid % cpr) * 8;
-  float k1[8], k2[8], k3[8], mu[8], s[8];
+  float k1[8], k2[8], k3[8], mu[8], sh[8], s[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    k1[j] = kc[c0 + j];
+    k1[j] = kc[c0 + j];                          // (= scale)
     k2[j] = kc[C + c0 + j];
     k3[j] = kc[2 * C + c0 + j];
     mu[j] = mean[c0 + j];
+    sh[j] = shift[c0 + j];
     s[j] = 0.f;
   }
   const long long stride = (long long)gridDim.x * 256;
@@ -410,7 +435,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k_kernel(const bf16* __restr
     py.u = *(const uint4*)(y + i * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float gv = bf2f(pg.e[j]), yv = bf2f(py.e[j]);
+      const float yv = bf2f(py.e[j]);
+      const float gv = yv * k1[j] + sh[j] > 0.f ? bf2f(pg.e[j]) : 0.f;   // relu' of z (k1 = scale)
       po.e[j] = f2bf(k1[j] * gv + k2[j] * yv + k3[j]);
       s[j] += gv * (yv - mu[j]);
     }
@@ -1321,10 +1347,11 @@ extern "C" int fn_bn_wdot(const float* w, const float* dw, float* part, int R, i
 }
 
 extern "C" int fn_bn_bwd_prep(const float* gslab, int nbg, const float* wpart, int nbw, int C, double count,
-                              const float* beta, const float* mean, const float* invstd, const float* scale,
-                              float* dbeta, float* kc, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_prep_kernel, dim3(C), dim3(256), 0, st, gslab, nbg, wpart, nbw, C, count, beta, mean,
-                     invstd, scale, dbeta, kc);
+                              const float* gamma, const float* beta, const float* mean, const float* invstd,
+                              const float* scale, const float* shift, float* dbeta, float* kc, const void* g,
+                              const void* y, long long M, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_prep_kernel, dim3(C), dim3(256), 0, st, gslab, nbg, wpart, nbw, C, count, gamma, beta,
+                     mean, invstd, scale, shift, dbeta, kc, (const bf16*)g, (const bf16*)y, M);
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -1339,11 +1366,11 @@ extern "C" int fn_bn_bwd_apply_k_blocks(long long M, int C) {
 }
 
 extern "C" int fn_bn_bwd_apply_k(const void* g, const void* y, const float* kc, const float* mean,
-                                 const float* invstd, void* dy, long long M, int C, float* part, int nb,
-                                 hipStream_t st) {
+                                 const float* invstd, const float* shift, void* dy, long long M, int C, float* part,
+                                 int nb, hipStream_t st) {
   if (C % 8 || 256 % (C / 8) || nb < 1) return -2;
   hipLaunchKernelGGL(bn_bwd_apply_k_kernel, dim3(nb), dim3(256), 0, st, (const bf16*)g, (const bf16*)y, kc, mean,
-                     invstd, (bf16*)dy, M * (C / 8), C, part);
+                     invstd, shift, (bf16*)dy, M * (C / 8), C, part);
   FN_CHECK_LAUNCH();
   return 0;
 }

@@ -114,7 +114,23 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // relu-mask dgrad (gmask): two buffers (by job parity) of the tile's mask bytes,
   // [natural tile row][Ncol / 8], after everything else
   const int mask_off = 64 + ct_red_bytes(NT) + (nks + PD + 2) * 16 + g.HPpad * 8 + (F8 ? NT * 16 * 8 : 0);
-  const int mask_bytes = ct_mask_bytes(rows, Ncol, gmask != nullptr);
+  // (the buffers hold the bytes in FRAGMENT order -- slot f = (wave * MT + mt) * 16 + lr -- so
+  // the epilogue reads slot (wave * MT + mt) * 16 + lr: a per-lane base plus a constant per mt)
+  const int mask_bytes = ct_mask_bytes(4 * MT * 16, Ncol, gmask != nullptr);
+  // ... and after them each fragment slot's (output offset from the tile origin in positions,
+  // packed td|th|tw; dummy rows: the origin) for the loader's mask DMA, built once per kernel
+  int2* s_mrow = reinterpret_cast<int2*>(dsm + 2 * g.BUF + mask_off + 2 * mask_bytes);
+  if (!F8 && gmask) {
+    for (int f = tid; f < 4 * MT * 16; f += CT_NTHR) {
+      const int r = rowtab[f].y;
+      if (r < 0) {
+        s_mrow[f] = make_int2(0, 0);
+      } else {
+        const int tw = r % g.TW, th = (r / g.TW) % g.TH, td = r / (g.TW * g.TH);
+        s_mrow[f] = make_int2(td * g.osd + th * g.osh + tw * g.osw, (td << 16) | (th << 8) | tw);
+      }
+    }
+  }
   if constexpr (F8) {
     if (tid < NT * 16) {
       const int c = blockIdx.y * NT * 16 + tid;
@@ -162,17 +178,17 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     const int n = t / tdn;
     const int d0 = td_ * g.TD, h0 = th_ * g.TH, w0 = tw_ * g.TW;
     const long long pb = (long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh + w0 * g.osw;
-    const int dpp = Ncol >> 5;
-    const int ndw = rows * dpp;
+    const int lg2 = Ncol == 64 ? 1 : 0;          // log2 dwords per position (Ncol 32 / 64)
+    const int nslot = 4 * MT * 16;
+    const int ndw = nslot << lg2;
+    const int ld = g.OD - d0, lh = g.OH - h0, lw = g.OW - w0;
+    const unsigned char* mb0 = gmask + pb * (Ncol >> 3);
     const unsigned dst = ct_lds_addr(dsm) + 2 * g.BUF + mask_off + mpar * mask_bytes;
     for (int k0 = 0; k0 < ndw; k0 += 64) {
       const int dd = k0 + lane;
-      int r = dd / dpp;
-      if (r >= rows) r = rows - 1;
-      const int tw = r % g.TW, th = (r / g.TW) % g.TH, td = r / (g.TW * g.TH);
-      const bool in = d0 + td < g.OD && h0 + th < g.OH && w0 + tw < g.OW;
-      const long long pos = pb + (in ? (long long)td * g.osd + (long long)th * g.osh + (long long)tw * g.osw : 0);
-      ct_glds4(gmask + pos * (Ncol >> 3) + (dd % dpp) * 4, dst + (unsigned)(k0 * 4));
+      const int2 e = s_mrow[dd >> lg2];             // (ndw is a whole number of DMA rows)
+      const bool in = (e.y >> 16) < ld && ((e.y >> 8) & 255) < lh && (e.y & 255) < lw;
+      ct_glds4(mb0 + (long long)(in ? e.x : 0) * (Ncol >> 3) + (dd & ((1 << lg2) - 1)) * 4, dst + (unsigned)(k0 * 4));
     }
   };
 
@@ -395,11 +411,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
           // bit 3: e4m3 output of v * oscale (saturated; fp8 inference: the bf16 stem writes the
           // fp8 layers' input directly), 8-B stores; no statistics
           constexpr bool Q8 = (M & 8) != 0;
-          // bit 4: relu-mask dgrad -- the stored values are g = dx * relu'(z), z's mask bits in mbits
+          // bit 4: relu-mask dgrad -- the column sums are of g = dx * relu'(z) (z's mask bits, from
+          // LDS); dx itself is stored unmasked (it is the true gradient of z)
           constexpr bool MSK = (M & 16) != 0;
           // (MSK: the loader DMA'd the tile's mask bytes into the LDS mask buffer of this job's
-          // parity, [natural tile row][Ncol / 8]; dummy rows read row 0)
-          const unsigned char* mb = dsm + 2 * g.BUF + mask_off + par * mask_bytes + (gc8 >> 3);
+          // parity, [fragment slot][Ncol / 8])
+          const unsigned char* mb = dsm + 2 * g.BUF + mask_off + par * mask_bytes +
+                                    ((wave * MT * 16 + lr) * (Ncol >> 3) + (gc8 >> 3));
           bool okm[MT];
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
@@ -423,10 +441,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             for (int mt = 0; mt < MT; ++mt) {
               const bool ok = okm[mt];
               unsigned mrow = 0;
-              if constexpr (MSK) {
-                const int nat = roff[mt] < 0 ? 0 : ((rpk[mt] >> 16) * g.TH + ((rpk[mt] >> 8) & 255)) * g.TW + (rpk[mt] & 255);
-                mrow = mb[nat * (Ncol >> 3)];
-              }
+              if constexpr (MSK) mrow = mb[mt * 16 * (Ncol >> 3)];
               unsigned pw[4];                    // the stored bf16 pairs (columns 2q, 2q+1)
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
@@ -434,16 +449,16 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                 const ct_f32x2 v = (ct_f32x2){a4[(2 * q) & 3], a4[(2 * q + 1) & 3]} + bias2[q];
                 unsigned w = bf16x2_pack(v[0], v[1]);
                 if constexpr (RELU_OUT) w = ct_relu_bf16x2(w);
-                if constexpr (MSK) {                 // bits 2q, 2q+1 of this row's mask byte
-                  const unsigned b = mrow >> (2 * q);
-                  w &= ((b & 1u) ? 0x0000ffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
-                }
                 pw[q] = w;
               }
               if constexpr (ST) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                  const unsigned w = ok ? pw[q] : 0u;
+                  unsigned w = ok ? pw[q] : 0u;
+                  if constexpr (MSK) {               // the sums see g = dx * relu'(z): bits 2q, 2q+1
+                    const unsigned b = mrow >> (2 * q);   // of the row's mask byte (dx is stored whole)
+                    w &= ((b & 1u) ? 0x0000ffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
+                  }
                   const ct_f32x2 x = (ct_f32x2){bf16_lo(w), bf16_hi(w)};
                   ts[q] += x;
                   tq[q] += x * x;
@@ -653,12 +668,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
 //   forward: Wsrc[col][tap][ch] = w[col][tap][ch]          (Ncol = K, Csrc = C)
 //   dgrad:   Wsrc[col][tap][ch] = w[ch][T-1-tap][col]      (Ncol = C, Csrc = K)
 // zero for tap >= T or col >= Ncol.
-__global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restrict__ w, uint4* __restrict__ out, int K,
-                                                          int T, int C, int CS, int nks, int nct, int nslice,
-                                                          int dgrad, int nt) {
-  const long long total = ((long long)nslice * nks + 4) * nct * 64;   // + the ring's 4 zero k-steps
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
+__device__ __forceinline__ void tile_pack_w_one(const float* __restrict__ w, uint4* __restrict__ out, int K, int T,
+                                                int C, int CS, int nks, int nct, int nslice, int dgrad, int nt,
+                                                long long i) {
   if (i >= (long long)nslice * nks * nct * 64) {
     out[i] = make_uint4(0u, 0u, 0u, 0u);
     return;
@@ -718,6 +730,51 @@ __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restric
     v.e[j] = f2bf(f);
   }
   out[i] = v.u;
+}
+
+__global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restrict__ w, uint4* __restrict__ out, int K,
+                                                          int T, int C, int CS, int nks, int nct, int nslice,
+                                                          int dgrad, int nt) {
+  const long long total = ((long long)nslice * nks + 4) * nct * 64;   // + the ring's 4 zero k-steps
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < total) tile_pack_w_one(w, out, K, T, C, CS, nks, nct, nslice, dgrad, nt, i);
+}
+
+// The forward and the dgrad packing of one weight in one launch (the conv's forward packs its
+// backward's dgrad operand too: one graph node fewer on the backward's critical path)
+struct TilePackJob {
+  uint4* out;
+  int CS, nks, nct, nslice, dgrad, nt;
+};
+
+__global__ __launch_bounds__(256) void tile_pack_w2_kernel(const float* __restrict__ w, int K, int T, int C,
+                                                           TilePackJob j0, TilePackJob j1) {
+  const long long t0 = ((long long)j0.nslice * j0.nks + 4) * j0.nct * 64;
+  const long long t1 = ((long long)j1.nslice * j1.nks + 4) * j1.nct * 64;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < t0)
+    tile_pack_w_one(w, j0.out, K, T, C, j0.CS, j0.nks, j0.nct, j0.nslice, j0.dgrad, j0.nt, i);
+  else if (i < t0 + t1)
+    tile_pack_w_one(w, j1.out, K, T, C, j1.CS, j1.nks, j1.nct, j1.nslice, j1.dgrad, j1.nt, i - t0);
+}
+
+// two packings of one weight (p = {CS, nks, nct, nslice, dgrad, nt} each) in one launch
+extern "C" int fn_tile_pack_w2(const float* w, void* out0, void* out1, int K, int T, int C, const int* p0,
+                               const int* p1, hipStream_t st) {
+  const int* ps[2] = {p0, p1};
+  TilePackJob j[2];
+  long long total = 0;
+  for (int q = 0; q < 2; ++q) {
+    const int* p = ps[q];
+    if (p[0] != 8 && p[0] != 16 && p[0] % 32 != 0) return -2;
+    if ((p[5] != 2 && p[5] != 32) || p[2] % 2) return -2;
+    j[q] = TilePackJob{(uint4*)(q ? out1 : out0), p[0], p[1], p[2], p[3], p[4], p[5]};
+    total += ((long long)p[3] * p[1] + 4) * p[2] * 64;
+  }
+  hipLaunchKernelGGL(tile_pack_w2_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, K, T, C, j[0],
+                     j[1]);
+  FN_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, int CS, int nks, int nct, int nslice,
@@ -782,7 +839,7 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, int Ncol = 0, bool mask = false) {
   const int PD = ct_pd(NT, f8);
   return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
-         (f8 ? (size_t)NT * 16 * 8 : 0) + 2 * (size_t)ct_mask_bytes(g.TD * g.TH * g.TW, Ncol, mask);
+         (f8 ? (size_t)NT * 16 * 8 : 0) + (size_t)ct_mask_lds(4 * MT * 16, Ncol, mask);
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -791,8 +848,8 @@ static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false,
 // + 2] byte offsets of the tap each lane group reads per k-step (zero past nks);
 // zp: >= 16 zero bytes; sched: int[64] zeroed counters (left zero); stats: fp32
 // [workers][2][Ncol], or null.  bny (bnp null): the relu-mask bytes [output positions][Ncol / 8]
-// of the BN whose output this dgrad's conv consumed -- the epilogue stores g = dx * mask and
-// (with stats) sums it; act none.  (The raw-moment BN-backward statistics epilogue, bny + bnp,
+// of the BN whose output this dgrad's conv consumed -- the epilogue's column sums are of
+// g = dx * mask (dx stored as is); stats required, act none.  (The raw-moment BN-backward statistics epilogue, bny + bnp,
 // is conv_tile32's, fn_conv_tile32.)
 extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
@@ -822,7 +879,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   }
   const size_t halo = (size_t)g.HPpad * CPP * 16;
   if ((size_t)g.BUF < halo || g.BUF % 1024) return -3;
-  if (bnp || (bny && (act != ACT_NONE || oscale != 0.f || Ncol % 32 || !stats))) return -2;
+  if (bnp || (bny && (act != ACT_NONE || oscale != 0.f || (Ncol != 32 && Ncol != 64) || !stats))) return -2;
   const size_t lds = tile_lds_total(g, MT, NT, false, Ncol, bny != nullptr);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);

@@ -128,10 +128,14 @@ __device__ __forceinline__ void ct_dma_job(const TileGeom& g, const unsigned cha
   }
 }
 
-// bytes of one LDS mask buffer of the relu-mask dgrad epilogue: rows x Ncol / 8, rounded up to
-// whole 64-dword DMA rows
+// bytes of one LDS mask buffer of the relu-mask dgrad epilogue: slots (4 waves x MT x 16 fragment
+// rows) x Ncol / 8, rounded up to whole 64-dword DMA rows
 __host__ __device__ constexpr int ct_mask_bytes(int rows, int Ncol, bool on) {
   return on ? (rows * (Ncol >> 3) + 255) / 256 * 256 : 0;
+}
+// LDS bytes of the relu-mask dgrad: the two mask buffers and the slot table (int2 per slot)
+__host__ __device__ constexpr int ct_mask_lds(int rows, int Ncol, bool on) {
+  return on ? 2 * ct_mask_bytes(rows, Ncol, on) + rows * 8 : 0;
 }
 
 #define CT_GEOM_LEN 31

@@ -76,7 +76,8 @@ def _bwd_param_grads(dz2, y2, prm, act, beta=None, gamma=None, part=None):
 
 def _bwd_identity(g2, y2, prm, beta, gamma, gslab, wpart):
     """BN(+relu) backward from the statistics identity (``bn_pool.hip`` bn_bwd_prep_kernel):
-    ``g2`` = dz * relu'(z) [M, C] from the consuming conv's dgrad, ``gslab`` its column sums
+    ``g2`` = dz [M, C] from the consuming conv's dgrad, ``gslab`` the column sums of
+    g = dz * relu'(z) its epilogue made
     [nbg, 2, C] (row 0), ``wpart`` the partials of S = sum W . dW [nbw, C].  Returns
     (dy, dbeta, dgamma); dbeta / dgamma go straight into the flat gradients when offered."""
     M, C = y2.shape
@@ -90,13 +91,15 @@ def _bwd_identity(g2, y2, prm, beta, gamma, gslab, wpart):
         dg = tmp[1]
     kc = torch.empty(3, C, dtype=torch.float32, device=y2.device)
     K.bn_bwd_prep(gslab.data_ptr(), gslab.shape[0], wpart.data_ptr(), wpart.shape[0], C, float(M),
-                  _native.ptr(beta), prm[0].data_ptr(), prm[1].data_ptr(), prm[2].data_ptr(), db.data_ptr(),
-                  kc.data_ptr(), st, [gslab.numel(), wpart.numel(), kc.numel()])
+                  _native.ptr(gamma), _native.ptr(beta), prm[0].data_ptr(), prm[1].data_ptr(), prm[2].data_ptr(),
+                  prm[3].data_ptr(), db.data_ptr(), kc.data_ptr(), g2.data_ptr(), y2.data_ptr(), M, st,
+                  [gslab.numel(), wpart.numel(), kc.numel(), g2.numel(), y2.numel()])
     dy = torch.empty_like(y2)
     nb = K.bn_bwd_apply_k_blocks(M, C)
     part = torch.empty(nb, 2, C, dtype=torch.float32, device=y2.device)
-    K.bn_bwd_apply_k(g2.data_ptr(), y2.data_ptr(), kc.data_ptr(), prm[0].data_ptr(), prm[1].data_ptr(), dy.data_ptr(),
-                     M, C, part.data_ptr(), nb, st, [g2.numel(), y2.numel(), dy.numel(), part.numel()])
+    K.bn_bwd_apply_k(g2.data_ptr(), y2.data_ptr(), kc.data_ptr(), prm[0].data_ptr(), prm[1].data_ptr(),
+                     prm[3].data_ptr(), dy.data_ptr(), M, C, part.data_ptr(), nb, st,
+                     [g2.numel(), y2.numel(), dy.numel(), part.numel()])
     # dgamma = sum g * xhat, summed exactly from (g, y) by the apply pass (row 1 of its slab)
     K.bn_finalize(part.data_ptr(), nb, C, float(M), 0, 0, 0, 0, 0.0, 0.0, tmp[2].data_ptr(), dg.data_ptr(), 0, 0, 1,
                   st)
@@ -157,8 +160,7 @@ class BatchNormActFn(torch.autograd.Function):
             return (dy.reshape(y.shape), dgamma if ctx.has_gamma else None, dbeta if ctx.has_beta else None,
                     None, None, None, None, None, None, None, None)
         if isinstance(part, tuple):
-            part = None                          # (no input gradient wanted: the colstats pass;
-            #                                       dz2 is g -- masked -- which it masks again)
+            part = None                          # (no input gradient wanted: the colstats pass)
         dbeta = dgamma = None
         if ctx.training or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             # (eval mode with frozen parameters -- input gradients of robustness attacks -- needs

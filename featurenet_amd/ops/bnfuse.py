@@ -59,13 +59,13 @@ def identity_enabled() -> bool:
     column sums, and ``sum g * xhat`` comes from the adjoint identity
     ``sum_p dz z = sum W * dW`` over the conv's weights and weight gradient
     (``bn_pool.hip`` bn_bwd_prep_kernel)."""
-    return os.environ.get("FN_BN_IDENTITY", "0") != "0"
+    return os.environ.get("FN_BN_IDENTITY", "1") != "0"
 
 
 def identity_ok(C: int, act: int) -> bool:
-    """The identity path's shape conditions: relu (the mask), 32-channel multiples (whole mask
-    dwords per position for the dgrad loader's DMA), 8-channel chunks dividing 256."""
-    return identity_enabled() and act == 1 and C % 32 == 0 and 256 % (C // 8) == 0
+    """The identity path's shape conditions: relu (the mask) and 32 or 64 channels (one or two
+    mask dwords per position for the dgrad loader's DMA)."""
+    return identity_enabled() and act == 1 and C in (32, 64)
 
 
 def pool_stats_enabled() -> bool:

@@ -403,14 +403,14 @@ def halo_conv_dgrad(dy5, w, spec: ConvSpec, plan):
 # raw native calls
 # ---------------------------------------------------------------------------
 def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: ConvSpec, act: int,
-                    want_stats: bool, w: torch.Tensor | None = None):
+                    want_stats: bool, w: torch.Tensor | None = None, dstash: dict | None = None):
     # the tile kernel's epilogue has the identity and relu only
     tplan = conv_tile.fwd_plan(spec) if w is not None and act in (0, act_code("relu")) else None
     plan = halo_fwd_plan(spec) if w is not None else None
     if tplan is not None and (plan is None or conv_tile.choose(
             "fwd", spec, lambda: conv_tile.conv_fwd(x5, w, bias, spec, act, want_stats, tplan),
             lambda: halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan))):
-        return conv_tile.conv_fwd(x5, w, bias, spec, act, want_stats, tplan)
+        return conv_tile.conv_fwd(x5, w, bias, spec, act, want_stats, tplan, dstash=dstash)
     if plan is not None:
         return halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan)
     K = _native.kernels()
@@ -428,7 +428,7 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
     return y, stats
 
 
-def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=None):
+def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=None, wpk=None):
     """dx of the conv.  ``bn = (y, prm, act)`` (x was a BN+act output, :mod:`.bnfuse`): returns
     ``(dx, slab)`` where ``slab`` holds that BN's backward sums from the tile kernel's
     epilogue, or None when another kernel ran.  ``w`` may have fewer output channels than
@@ -442,15 +442,15 @@ def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=Non
             dy5 = dy5.contiguous()
             if plan is None or conv_tile.choose("dgrad", spec, lambda: conv_tile.conv_dgrad(dy5, w, spec, tplan),
                                                 lambda: halo_conv_dgrad(dy5, w, spec, plan)):
-                return conv_tile.conv_dgrad(dy5, w, spec, tplan, bn=bn)
-        return native_conv_dgrad(dy5, w, spec), None
+                return conv_tile.conv_dgrad(dy5, w, spec, tplan, bn=bn, wpk=wpk)
+        return native_conv_dgrad(dy5, w, spec, wpk=wpk), None
     tplan = conv_tile.dgrad_plan(spec)
     plan = halo_dgrad_plan(spec)
     if tplan is not None:
         dy5 = dy5.contiguous()
         if plan is None or conv_tile.choose("dgrad", spec, lambda: conv_tile.conv_dgrad(dy5, w, spec, tplan),
                                             lambda: halo_conv_dgrad(dy5, w, spec, plan)):
-            return conv_tile.conv_dgrad(dy5, w, spec, tplan)
+            return conv_tile.conv_dgrad(dy5, w, spec, tplan, wpk=wpk)
     if plan is not None:
         return halo_conv_dgrad(dy5.contiguous(), w, spec, plan)
     K = _native.kernels()
@@ -838,6 +838,14 @@ def _conv_bwd_padded(ctx, dy, xs, w, spec, y=None):
     return dx, dw, db, None, None, None
 
 
+def _stashed(ctx):
+    """The dgrad's packed weights the forward made (conv_tile.conv_fwd ``dstash``), or None;
+    released once taken."""
+    st = getattr(ctx, "dstash", None)
+    ctx.dstash = None
+    return st.get("wpk") if st else None
+
+
 class ConvFn(torch.autograd.Function):
     """y = act(conv(x, w) + b); optional BN statistics slab as a 2nd output."""
 
@@ -880,8 +888,10 @@ class ConvFn(torch.autograd.Function):
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
             x_saved = s2d_input(x5, f, spec2, (spec.pd, spec.ph, spec.pw)) if ctx.needs_input_grad[1] else x5
         elif halo_fwd_plan(spec) is not None or (conv_tile.fwd_plan(spec) is not None and act in (0, act_code("relu"))):
+            # (the tile forward also packs the backward's dgrad weights, in the same launch)
+            ctx.dstash = {} if ctx.needs_input_grad[0] else None
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats,
-                                       w=pad_to_spec(w.detach(), spec))
+                                       w=pad_to_spec(w.detach(), spec), dstash=ctx.dstash)
         else:
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
@@ -927,14 +937,14 @@ class ConvFn(torch.autograd.Function):
         if ctx.x_needs:
             if ctx.bn_src is not None:
                 bn_y = ctx.bn_src[0]
-                dx, slab = native_conv_dgrad(dy, w.detach(), spec, bn=ctx.bn_src)
+                dx, slab = native_conv_dgrad(dy, w.detach(), spec, bn=ctx.bn_src, wpk=_stashed(ctx))
                 if isinstance(slab, tuple):
                     ident = slab[1]              # (offered below, with S from this conv's dW)
                 elif slab is not None:
                     bnfuse.offer(dx, slab, bn_y)
                 ctx.bn_src = None
             else:
-                dx = native_conv_dgrad(dy, w.detach(), spec)
+                dx = native_conv_dgrad(dy, w.detach(), spec, wpk=_stashed(ctx))
         dw = db = None
         want_db = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:

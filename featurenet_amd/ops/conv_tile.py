@@ -407,11 +407,30 @@ def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bo
 def mask_dgrad_ok(p: TilePlan, ncol: int) -> bool:
     """The relu-mask dgrad epilogue fits: whole mask dwords per position and the two LDS mask
     buffers (rows x ncol / 8 bytes each, 256-B rounded) within the CU's LDS."""
-    if ncol % 32:
+    if ncol not in (32, 64):
         return False
-    mb = -(-p.rows * (ncol // 8) // 256) * 256
-    lds = 2 * p.BUF + 64 + red_bytes(p.NT) + (p.nks + 4 + 2) * 16 + p.HPpad * 8 + 2 * mb
+    slots = 4 * p.MT * 16                        # (fragment-ordered mask slots)
+    mb = -(-slots * (ncol // 8) // 256) * 256
+    lds = 2 * p.BUF + 64 + red_bytes(p.NT) + (p.nks + 4 + 2) * 16 + p.HPpad * 8 + 2 * mb + 8 * slots
     return lds <= LDS_MAX
+
+
+def _pack_params(p: TilePlan, Csrc: int, dgrad: bool) -> list[int]:
+    return [p.CS, p.nks, p.nct, Csrc // p.CS, int(dgrad), 32 if p.m32 else p.NT]
+
+
+def pack_pair(w: torch.Tensor, K: int, T: int, C: int, pf: TilePlan, pd: TilePlan):
+    """(forward, dgrad) packed B streams of one weight in one launch (:func:`pack_weights`
+    twice): the forward packs its backward's dgrad operand too."""
+    outs = []
+    for p, dg in ((pf, False), (pd, True)):
+        Csrc = K if dg else C
+        outs.append(torch.empty(((Csrc // p.CS) * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device))
+    wf = w.detach().float().contiguous()
+    _native.kernels().tile_pack_w2(wf.data_ptr(), outs[0].data_ptr(), outs[1].data_ptr(), K, T, C,
+                                   _pack_params(pf, C, False), _pack_params(pd, K, True), _native.stream(wf),
+                                   [wf.numel(), outs[0].numel(), outs[1].numel()])
+    return outs[0], outs[1]
 
 
 def workers(p: TilePlan, geom: list, ncol: int) -> int:
@@ -439,13 +458,20 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
 
 
 def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan,
-             out_scale: float | None = None):
+             out_scale: float | None = None, dstash: dict | None = None):
     """y = act(conv(x, w) + b) (+ BN statistics slab) for a stride-1 conv on the tile kernel;
-    ``out_scale``: e4m3 bytes of y / out_scale instead (fp8 inference input, no statistics)."""
+    ``out_scale``: e4m3 bytes of y / out_scale instead (fp8 inference input, no statistics).
+    ``dstash`` (a dict kept by the caller until its backward): the dgrad's packed weights are made
+    in the same launch and left there as ``(plan, packed)`` for :func:`conv_dgrad`."""
     kd = (spec.KD, spec.KH, spec.KW)
     geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
                     (spec.pd, spec.ph, spec.pw))
-    wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=False)
+    pd = dgrad_plan(spec) if dstash is not None and not out_scale else None
+    if pd is not None:
+        wpk, wpk_d = pack_pair(w, spec.K, spec.taps, spec.C, p, pd)
+        dstash["wpk"] = (pd, wpk_d)
+    else:
+        wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=False)
     y = torch.empty(spec.out_shape5, dtype=torch.uint8 if out_scale else torch.bfloat16, device=x5.device)
     stats = None
     if want_stats:
@@ -455,7 +481,7 @@ def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats
     return y, stats
 
 
-def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None):
+def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None, wpk=None):
     """dx = conv(dy, flip(W)^T) with leading pads K-1-p (stride 1) on the tile kernel.
 
     ``bn = (y, prm, act)``: x was ``act(bn(y))`` with ``prm`` = (mean, invstd, scale, shift)
@@ -465,12 +491,13 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None):
     kd = (spec.KD, spec.KH, spec.KW)
     geom = geometry(p, (spec.N, spec.OD, spec.OH, spec.OW, spec.K), (spec.D, spec.H, spec.W), kd,
                     (spec.KD - 1 - spec.pd, spec.KH - 1 - spec.ph, spec.KW - 1 - spec.pw))
-    wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
+    # ``wpk``: (plan, packed) left by the forward (:func:`conv_fwd` dstash), used when the plan matches
+    wpk = wpk[1] if wpk is not None and wpk[0] == p else pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     mask = bn[3] if bn is not None else None
     if bn is not None and not p.m32 and mask is not None and mask_dgrad_ok(p, spec.C):
-        # the relu-mask epilogue (statistics identity, ops/bnfuse.py): dx holds g = dz * relu'(z)
-        # and the slab's row 0 its column sums
+        # the relu-mask epilogue (statistics identity, ops/bnfuse.py): the slab's row 0 holds the
+        # column sums of g = dx * relu'(z); dx itself is stored unmasked
         assert mask.numel() * 8 == dx.numel() and mask.dtype == torch.uint8
         slab = torch.empty(workers(p, geom, spec.C), 2, spec.C, dtype=torch.float32, device=dy5.device)
         run(dy5, wpk, None, dx, slab, p, geom, kd, spec.C, 0, bny=mask)

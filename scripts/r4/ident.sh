@@ -24,9 +24,10 @@ for i in 1 2; do
   done
 done
 rm -rf gpurun_out/prof_id
-step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_id -o run -- \
+step dgstats 200 python3 scripts/r4/dgrad_stats_ab.py; grep layer gpurun_out/id_dgstats.log
+FN_BN_IDENTITY=1 step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_id -o run -- \
   python3 bench.py --steps 5 --warmup 3
 python3 scripts/step_breakdown.py gpurun_out/prof_id/run_kernel_trace.csv --min-us 0 > gpurun_out/step_id.md 2>&1 || true
 tail -2 gpurun_out/step_id.md
-step seg 300 python3 bench.py --model seg --steps 10 --warmup 3
+FN_BN_IDENTITY=1 step seg 300 python3 bench.py --model seg --steps 10 --warmup 3
 echo "seg $(grep -o '"value": [0-9.]*' gpurun_out/id_seg.log) $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/id_seg.log)"

@@ -229,14 +229,24 @@ def test_identity_featurenet3d_matches_colstats(monkeypatch):
     model = FeatureNet3D().to(dev)
     x = (torch.rand(8, 64, 64, 64, 1, device=dev) < 0.3).to(torch.bfloat16)
     calls = _count_identity(monkeypatch)
+    # (a warm-up step first: in a process that ran other tests before, the first step's gradients
+    # differ from every later one -- off vs off -- by up to 1.5e-2 on conv4's weight)
+    _grads_ident(model, x, False, monkeypatch)
     g0 = _grads_ident(model, x, False, monkeypatch)
     assert calls["identity"] == 0
     g1 = _grads_ident(model, x, True, monkeypatch)
     assert calls["identity"] == 3, f"identity path taken {calls['identity']} times (conv2-4 inputs)"
-    for n in g0:
-        a, b = g0[n], g1[n]
-        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
-        assert err < 5e-3, f"{n}: rel err {err:.2e}"
+    g2 = _grads_ident(model, x, False, monkeypatch)
+    # relative L2 errors: the forward's BN statistics come from dynamically scheduled tiles, so
+    # their fp32 summation order -- and bf16 roundings downstream -- vary run to run once other
+    # kernels have run in the process (off vs off: max-element differences up to 3.6e-2 on conv4's
+    # weight gradient, a few elements); the identity pieces are checked exactly in
+    # test_identity_pieces_exact
+    rl2 = lambda u, v: ((u - v).norm() / u.norm().clamp_min(1e-12)).item()  # noqa: E731
+    errs = {n: (rl2(g0[n], g1[n]), rl2(g0[n], g2[n])) for n in g0}
+    print({n: f"{e[0]:.2e} (off/off {e[1]:.2e})" for n, e in errs.items()})
+    for n, (e, e0) in errs.items():
+        assert e < 1e-2, f"{n}: rel L2 err {e:.2e} (off/off run-to-run {e0:.2e})"
 
 
 @pytest.mark.parametrize("gscale", [1.0, -0.5, 1e-4])
@@ -260,6 +270,7 @@ def test_identity_any_gamma(monkeypatch, gscale):
                 m.beta.add_(torch.linspace(-2, 3, m.beta.numel(), device=dev))
     x = torch.randn(4, 20, 20, 20, 16, device=dev).to(torch.bfloat16)
     calls = _count_identity(monkeypatch)
+    _grads_ident(model, x, False, monkeypatch)   # (warm-up, as above)
     g0 = _grads_ident(model, x, False, monkeypatch)
     g1 = _grads_ident(model, x, True, monkeypatch)
     assert calls["identity"] >= 1
@@ -267,3 +278,41 @@ def test_identity_any_gamma(monkeypatch, gscale):
         a, b = g0[n], g1[n]
         err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
         assert err < 1e-2, f"{n}: rel err {err:.2e}"
+
+
+@pytest.mark.parametrize("N,S,C,K,k", [(8, 22, 64, 64, 3), (4, 29, 32, 32, 5), (4, 25, 32, 64, 4)])
+def test_identity_pieces_exact(N, S, C, K, k):
+    """The statistics identity's pieces on one conv (FeatureNet-3D conv2-4 shapes): the masked
+    dgrad stores dz unchanged and the column sums of dz * relu'(z), the conv's weight gradient is
+    unchanged by it, bn_wdot equals torch's sum bf16(W) * dW, and that sum equals sum dz * z."""
+    import importlib
+
+    from featurenet_amd.ops import conv_tile as ct
+    from featurenet_amd.ops.spec import ConvSpec
+
+    cv = importlib.import_module("featurenet_amd.ops.conv")
+    torch.manual_seed(0)
+    x = torch.relu(torch.randn(N, S, S, S, C, device="cuda")).to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, K, k, 1, "valid")
+    w = torch.randn(K, k, k, k, C, device="cuda") * 0.05
+    dy = torch.randn(spec.out_shape5, device="cuda").to(torch.bfloat16)
+    bits = (x.reshape(-1, 8) > 0).to(torch.uint8)
+    mask = (bits * (2 ** torch.arange(8, device="cuda", dtype=torch.uint8))).sum(-1).to(torch.uint8).contiguous()
+    p = ct.dgrad_plan(spec)
+    assert p is not None and ct.mask_dgrad_ok(p, C)
+    dz = ct.conv_dgrad(dy, w, spec, p)
+    dw0 = cv.native_conv_wgrad(dy, x, spec).clone()
+    g, ident = ct.conv_dgrad(dy, w, spec, p, bn=(x, None, 1, mask))
+    assert isinstance(ident, tuple) and ident[0] == "identity"
+    dw1 = cv.native_conv_wgrad(dy, x, spec).clone()
+    ref = dz.float() * (x.float() > 0)
+    assert torch.equal(g, dz)                    # dx stored whole (the true gradient of z)
+    sg = ident[1][:, 0].sum(0)
+    rs = ref.reshape(-1, C).sum(0)
+    assert ((sg - rs).abs().max() / rs.abs().max()).item() < 1e-5
+    assert torch.equal(dw0, dw1)
+    S_k = cv.bn_wdot(w, dw0, spec).sum(0)
+    S_t = (w.to(torch.bfloat16).float() * dw0).reshape(-1, C).sum(0)
+    S_z = (dz.float() * x.float()).reshape(-1, C).sum(0)
+    assert ((S_k - S_t).abs().max() / S_t.abs().max()).item() < 1e-5
+    assert ((S_k - S_z).abs().max() / S_z.abs().max()).item() < 5e-3   # (dz rounded to bf16 here)
