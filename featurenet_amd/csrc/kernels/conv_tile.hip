@@ -316,7 +316,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // relu-mask dgrad (stats, no activation; host-checked) -- selected inside case 1, so every
     // emode value still reaches an epilogue (a reachable no-epilogue path kept the accumulators
     // live across it: 227 -> 256 VGPRs with spills)
-    const bool msk = !F8 && gmask != nullptr;
+    const bool msk = !F8 && gmask != nullptr && !(act & 0x200);   // (0x200: timing only, DMA without the mask epilogue)
     // BN partial sums of this lane's columns over every tile the workgroup runs (the epilogues
     // add into them; one DPP + LDS reduction after the last tile instead of one per tile:
     // stem fwd epilogue ~40 % of its cycles in round 4 stamps).  MT = 9 keeps the per-tile
@@ -418,6 +418,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
           // parity, [fragment slot][Ncol / 8])
           const unsigned char* mb = dsm + 2 * g.BUF + mask_off + par * mask_bytes +
                                     ((wave * MT * 16 + lr) * (Ncol >> 3) + (gc8 >> 3));
+          unsigned mrows[MSK ? MT : 1];          // (all MT byte reads in flight together)
+          if constexpr (MSK) {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) mrows[mt] = mb[mt * 16 * (Ncol >> 3)];
+          }
           bool okm[MT];
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
@@ -440,8 +445,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
               const bool ok = okm[mt];
-              unsigned mrow = 0;
-              if constexpr (MSK) mrow = mb[mt * 16 * (Ncol >> 3)];
+              const unsigned mrow = MSK ? mrows[mt] : 0u;
               unsigned pw[4];                    // the stored bf16 pairs (columns 2q, 2q+1)
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
@@ -461,7 +465,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                   }
                   const ct_f32x2 x = (ct_f32x2){bf16_lo(w), bf16_hi(w)};
                   ts[q] += x;
-                  tq[q] += x * x;
+                  if constexpr (!MSK) tq[q] += x * x;      // (the identity needs sum g only)
                 }
               }
               if constexpr (Q8) {
@@ -879,12 +883,12 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   }
   const size_t halo = (size_t)g.HPpad * CPP * 16;
   if ((size_t)g.BUF < halo || g.BUF % 1024) return -3;
-  if (bnp || (bny && (act != ACT_NONE || oscale != 0.f || (Ncol != 32 && Ncol != 64) || !stats))) return -2;
+  if (bnp || (bny && ((act & 0xff) != ACT_NONE || oscale != 0.f || (Ncol != 32 && Ncol != 64) || !stats))) return -2;
   const size_t lds = tile_lds_total(g, MT, NT, false, Ncol, bny != nullptr);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
-  if (Ncol % 8 || (act != ACT_NONE && act != ACT_RELU)) return -2;   // 16-B column groups; relu or none
+  if (Ncol % 8 || ((act & 0xff) != ACT_NONE && (act & 0xff) != ACT_RELU)) return -2;   // 16-B column groups
   // oscale > 0: e4m3 output of y * oscale (no statistics; the 8-channel-slice instances: the
   // space-to-depth stem of the fp8 inference path)
   if (!(oscale >= 0.f) || (oscale > 0.f && (stats || NT != 2 || CPP != 1))) return -2;

@@ -243,14 +243,17 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_reduce_kernel(const floa
 __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __restrict__ g,
                                                                  const float* __restrict__ w,
                                                                  bf16* __restrict__ dx, int M, int N, int K,
-                                                                 const bf16* __restrict__ ya, int act) {
+                                                                 const bf16* __restrict__ ya, int act, int mrep) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
   const int NP = (N + 31) & ~31;
   const int LDN = NP + 8;                        // row pitch (bf16): 16-B aligned rows, bank shift
   bf16* wt = reinterpret_cast<bf16*>(dn_lds);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, gq = lane >> 4;
-  const int kk0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  // a workgroup covers mrep consecutive 64-row blocks with one staged W tile (the W tile is the
+  // expensive part: FC1's 128 x 64000 weights were read -- and LDS-transposed -- once per row
+  // block before)
+  const int kk0 = blockIdx.x * 64;
   // stage W[0:N][kk0:kk0+64] -> wt[kk][n] (bf16): thread = (n, 4 consecutive kk)
   for (int idx = tid; idx < NP * 16; idx += DN_THREADS) {
     const int n = idx >> 4, q = idx & 15;
@@ -274,10 +277,13 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
   __syncthreads();
   // wave: 16 kk rows (A = W^T rows kk) x 64 m columns (B = g^T columns m): 4 tiles
   const int kkw = wave * 16;
+  const bf16x8 zero8 = {};
+  for (int mi = 0; mi < mrep; ++mi) {
+  const int m0 = (blockIdx.y * mrep + mi) * 64;
+  if (m0 >= M) break;
   f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bf16x8 zero8 = {};
   for (int n0 = 0; n0 < NP; n0 += 32) {
     const bf16x8 fa = *(const bf16x8*)(wt + (kkw + r) * LDN + n0 + 8 * gq);
     const int nc = n0 + 8 * gq;                  // this lane group's 8 k (= n) values
@@ -324,6 +330,7 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
         if (kk + e < K) o[e] = f2bf(acc[j][e]);
     }
   }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -332,6 +339,9 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
 // grid (ceil(K/64), ceil(N/64)); block tile: 64 n x 64 kk; reduction over all M (padded with
 // zero rows to a multiple of 32); any K, N (element loads where rows are not 16-B aligned).
 // LDS (dynamic): x tile transposed [64 kk][M + 8], g tile transposed [64 n][M + 8].
+// NB = 2: 128 n columns per workgroup (the x tile -- FC1's 16 MB activation -- staged once for
+// both 64-column halves instead of once per half; a wave then holds 8 accumulator tiles)
+template <int NB>
 __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __restrict__ g,
                                                                  const bf16* __restrict__ x,
                                                                  float* __restrict__ dw, float* __restrict__ db,
@@ -350,26 +360,31 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
   bf16* gt = xt + 64 * LDM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, gq = lane >> 4;
-  const int kk0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int kk0 = blockIdx.x * 64, n0 = blockIdx.y * 64 * NB;
   const int kkw = wave * 16;
-  f32x4 acc[4];
+  f32x4 acc[4 * NB];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  float dbs = 0.f;                               // bias gradient (first column block, tid < 64)
+  for (int j = 0; j < 4 * NB; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float dbs[NB];                                 // bias gradient (first column block, tid < 64)
+#pragma unroll
+  for (int b = 0; b < NB; ++b) dbs[b] = 0.f;
   for (int mb = mz0; mb < mz1; mb += MCH) {
     const int rows = mz1 - mb < MCH ? mz1 - mb : MCH;
     const int MP = (rows + 31) & ~31;
     if (mb > mz0) __syncthreads();               // previous chunk's MFMA / db reads are done
-    // x[mb:mb+rows][kk0:kk0+64] -> xt[kk][m]; g[..][n0:n0+64] -> gt[n][m]: thread = (m, 8 columns)
-    for (int idx = tid; idx < MP * 8; idx += DN_THREADS) {
-      const int ml = idx >> 3, q = idx & 7;
+    // x[mb:mb+rows][kk0:kk0+64] -> xt[kk][m]; g[..][n0:n0+64 NB] -> gt[n][m]: thread = (m, 8 columns)
+    for (int idx = tid; idx < MP * 8 * NB; idx += DN_THREADS) {
+      const int ml = idx / (8 * NB), q = idx % (8 * NB);
       const int m = mb + ml;
       const int kk = kk0 + 8 * q, n = n0 + 8 * q;
+      const bool xq = q < 8;                     // (NB = 2: columns 8..15 stage g only)
       Pack8 vx, vg;
       if (ml >= rows) {
         vx.u = vg.u = make_uint4(0u, 0u, 0u, 0u);
       } else {
-        if ((K & 7) == 0 && kk + 8 <= K) {       // 16-B aligned rows only when K % 8 == 0
+        if (!xq) {
+          vx.u = make_uint4(0u, 0u, 0u, 0u);
+        } else if ((K & 7) == 0 && kk + 8 <= K) {   // 16-B aligned rows only when K % 8 == 0
           vx.u = *(const uint4*)(x + (long long)m * K + kk);
         } else {
           for (int e = 0; e < 8; ++e) vx.e[e] = kk + e < K ? x[(long long)m * K + kk + e] : f2bf(0.f);
@@ -392,26 +407,30 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        xt[(8 * q + e) * LDM + ml] = vx.e[e];
+        if (xq) xt[(8 * q + e) * LDM + ml] = vx.e[e];
         gt[(8 * q + e) * LDM + ml] = vg.e[e];
       }
     }
     __syncthreads();
-    // C^T[kk][n] = sum_m x^T[kk][m] g[m][n]: wave = 16 kk rows x 64 n columns
+    // C^T[kk][n] = sum_m x^T[kk][m] g[m][n]: wave = 16 kk rows x 64 NB n columns
     for (int mm = 0; mm < MP; mm += 32) {
       const bf16x8 fa = *(const bf16x8*)(xt + (kkw + r) * LDM + mm + 8 * gq);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4 * NB; ++j) {
         const bf16x8 fb = *(const bf16x8*)(gt + (j * 16 + r) * LDM + mm + 8 * gq);
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[j], 0, 0, 0);
       }
     }
-    if (db && blockIdx.x == 0 && tid < 64 && n0 + tid < N)
-      for (int m = 0; m < rows; ++m) dbs += bf2f(gt[tid * LDM + m]);
+    if (db && blockIdx.x == 0 && tid < 64) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        if (n0 + 64 * b + tid < N)
+          for (int m = 0; m < rows; ++m) dbs[b] += bf2f(gt[(64 * b + tid) * LDM + m]);
+    }
   }
   // lane: n = n0 + 16j + r, kk = kk0 + kkw + 4gq .. +3 -> dW[n][kk..kk+3]
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 4 * NB; ++j) {
     const int n = n0 + j * 16 + r;
     const int kk = kk0 + kkw + 4 * gq;
     if (n >= N) continue;
@@ -423,8 +442,12 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
         if (kk + e < K) o[e] = acc[j][e];
     }
   }
-  // bias gradient: the first column block summed g over M for its 64 n
-  if (db && blockIdx.x == 0 && tid < 64 && n0 + tid < N) db[n0 + tid] = dbs;
+  // bias gradient: the first column block summed g over M for its 64 NB n
+  if (db && blockIdx.x == 0 && tid < 64) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (n0 + 64 * b + tid < N) db[n0 + 64 * b + tid] = dbs[b];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -498,8 +521,11 @@ extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, in
   const size_t lds = (size_t)64 * (((N + 31) & ~31) + 8) * 2;
   if (lds > 160 * 1024) return -4;
   if (int e = dn_lds_attr((const void*)dense_dgrad_kernel, lds)) return e;
-  hipLaunchKernelGGL(dense_dgrad_kernel, dim3((K + 63) / 64, (M + 63) / 64), dim3(DN_THREADS), lds, st,
-                     (const bf16*)g, w, (bf16*)dx, M, N, K, (const bf16*)ya, act);
+  // row blocks per workgroup: up to 4 when the K tiles alone fill the GPU
+  const int mblk = (M + 63) / 64;
+  const int mrep = (K + 63) / 64 >= 512 ? (mblk < 4 ? mblk : 4) : 1;
+  hipLaunchKernelGGL(dense_dgrad_kernel, dim3((K + 63) / 64, (mblk + mrep - 1) / mrep), dim3(DN_THREADS), lds, st,
+                     (const bf16*)g, w, (bf16*)dx, M, N, K, (const bf16*)ya, act, mrep);
   FN_CHECK_LAUNCH();
   return 0;
 }
@@ -531,14 +557,23 @@ extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db
   mc = (mc + 31) & ~31;
   S = (M + mc - 1) / mc;                         // slices actually covering M
   const int mch = mc < DN_WG_MCH ? mc : DN_WG_MCH;
-  const size_t lds = (size_t)2 * 64 * (mch + 8) * 2;
+  // 128-column workgroups when N > 64 and the K tiles alone fill the GPU (FC1: 1000 tiles)
+  // (NB = 2 -- x staged once for both 64-column halves -- measured slower on FC1: 42.8 vs 29.6 us)
+  const int nb = 1;
+  const size_t lds = (size_t)(64 + 64 * nb) * (mch + 8) * 2;
   if (lds > 160 * 1024) return -4;
-  if (int e = dn_lds_attr((const void*)dense_wgrad_kernel, lds)) return e;
   const long long NK = (long long)N * K;
   float* pdw = S > 1 ? part : dw;
   float* pdb = S > 1 ? (db ? part + (long long)S * NK : nullptr) : db;
-  hipLaunchKernelGGL(dense_wgrad_kernel, dim3((K + 63) / 64, (N + 63) / 64, S), dim3(DN_THREADS), lds, st,
-                     (const bf16*)g, (const bf16*)x, pdw, pdb, M, N, K, mc, (const bf16*)ya, act);
+  if (nb == 2) {
+    if (int e = dn_lds_attr((const void*)dense_wgrad_kernel<2>, lds)) return e;
+    hipLaunchKernelGGL(dense_wgrad_kernel<2>, dim3((K + 63) / 64, (N + 127) / 128, S), dim3(DN_THREADS), lds, st,
+                       (const bf16*)g, (const bf16*)x, pdw, pdb, M, N, K, mc, (const bf16*)ya, act);
+  } else {
+    if (int e = dn_lds_attr((const void*)dense_wgrad_kernel<1>, lds)) return e;
+    hipLaunchKernelGGL(dense_wgrad_kernel<1>, dim3((K + 63) / 64, (N + 63) / 64, S), dim3(DN_THREADS), lds, st,
+                       (const bf16*)g, (const bf16*)x, pdw, pdb, M, N, K, mc, (const bf16*)ya, act);
+  }
   FN_CHECK_LAUNCH();
   if (S > 1) {
     hipLaunchKernelGGL(dense_wgrad_reduce_kernel, dim3((unsigned)((NK + 255) / 256 < 2048 ? (NK + 255) / 256 : 2048)),

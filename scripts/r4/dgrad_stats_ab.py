@@ -42,9 +42,10 @@ for name, S, C, K, k in LAYERS:
     t1 = timeit(lambda: ct.run(dy, wpk, None, dx, slab, p, geom, kd, C, 0))
     mask = torch.randint(0, 256, (dx.numel() // 8,), dtype=torch.uint8, device="cuda")
     t2 = timeit(lambda: ct.run(dy, wpk, None, dx, slab, p, geom, kd, C, 0, bny=mask))
+    t3 = timeit(lambda: ct.run(dy, wpk, None, dx, slab, p, geom, kd, C, 0x200, bny=mask))   # DMA, no mask epilogue
     t0 = timeit(lambda: ct.run(dy, wpk, None, dx, None, p, geom, kd, C, 0))      # (again: clock ramp)
     ref = dx.float().reshape(-1, C).sum(0)
     err = (slab[:, 0].sum(0) - ref).abs().max().item() / ref.abs().max().item()
     print(json.dumps({"layer": name, "dgrad_us": round(t0, 1), "dgrad_stats_us": round(t1, 1),
-                      "dgrad_mask_us": round(t2, 1),
+                      "dgrad_mask_us": round(t2, 1), "dgrad_maskdma_only_us": round(t3, 1),
                       "stats_rel_err": err}), flush=True)
