@@ -108,7 +108,10 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
     cx = batch(ds.x_train, 0, calib)
     q = quantize_model(model, cx)                          # the default stem (FN_F8_STEM)
     qs = quantize_model(model, cx, fp8_stem=False)         # bf16 stem writing e4m3 from its epilogue
-    qi = quantize_model(model, cx, fp8_stem="i8")          # int8 stem (v_mfma_i32_16x16x64_i8)
+    from featurenet_amd.ops.conv_tile import experiments_built
+
+    # int8 stem (v_mfma_i32_16x16x64_i8): an experiment build only (FN_BUILD_EXPERIMENTS=1)
+    qi = quantize_model(model, cx, fp8_stem="i8") if experiments_built() else None
     y = np.asarray(ds.y_test)
     pb, pq, ps, pi = [], [], [], []
     for i in range(0, len(y), chunk):
@@ -116,16 +119,22 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
         pb.append(model(xb).float().argmax(-1).cpu())
         pq.append(q(xb).float().argmax(-1).cpu())
         ps.append(qs(xb).float().argmax(-1).cpu())
-        pi.append(qi(xb).float().argmax(-1).cpu())
-    pb, pq, ps, pi = (torch.cat(t).numpy() for t in (pb, pq, ps, pi))
-    acc_b, acc_q, acc_s, acc_i = (float((t == y).mean()) for t in (pb, pq, ps, pi))
+        if qi is not None:
+            pi.append(qi(xb).float().argmax(-1).cpu())
+    pb, pq, ps = (torch.cat(t).numpy() for t in (pb, pq, ps))
+    acc_b, acc_q, acc_s = (float((t == y).mean()) for t in (pb, pq, ps))
+    i8 = None
+    if qi is not None:
+        pi = torch.cat(pi).numpy()
+        acc_i = float((pi == y).mean())
+        i8 = {"top1_fp8": round(acc_i, 4), "drop_pt": round(100 * (acc_b - acc_i), 2),
+              "agreement": round(float((pb == pi).mean()), 4)}
     return {"top1_bf16": round(acc_b, 4), "top1_fp8": round(acc_q, 4), "drop_pt": round(100 * (acc_b - acc_q), 2),
             "agreement": round(float((pb == pq).mean()), 4), "calib_samples": calib,
             "stem": q.stem and ("i8" if q.stem.int8 else "e4m3") or "bf16",
             "bf16_stem": {"top1_fp8": round(acc_s, 4), "drop_pt": round(100 * (acc_b - acc_s), 2),
                           "agreement": round(float((pb == ps).mean()), 4)},
-            "i8_stem": {"top1_fp8": round(acc_i, 4), "drop_pt": round(100 * (acc_b - acc_i), 2),
-                        "agreement": round(float((pb == pi).mean()), 4)},
+            "i8_stem": i8,
             "kernel": ("conv_halo_f8" if os.environ.get("FN_F8_TILE", "1") == "0" else "conv_tile F8 variant")
                       + " (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3)"}
 
