@@ -188,7 +188,10 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
                     cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
                                           float(cost), f8, pool, m32))
     # the cheapest few, re-costed with their row tables' residual bank conflicts (a
-    # fragment whose 16 rows repeat a residue mod 16 reads at half rate)
+    # fragment whose 16 rows repeat a residue mod 16 reads at half rate).  (A finer term --
+    # bank_ways, the simulated ways of every ds_read_b128 lane group -- was tried: conv4 fwd's
+    # 2.1-way plan times equal to its conflict-free alternatives and the stem's conflict-free
+    # plans need MT = 9, 7 % slower; profiles/r4_tile_plan_bank_sweep.md)
     ranked = []
     for c in sorted(cands, key=lambda c: c.cost)[:12]:
         HH, HW = c.TH + KH - 1, c.TW + KW - 1
@@ -251,6 +254,47 @@ def row_table(p: TilePlan, kdims: tuple) -> np.ndarray:
     with _LOCK:
         _ROWTAB[key] = tab
     return tab
+
+
+# the lanes of each ds_read_b128 bank group (MI355X: four non-contiguous 16-lane groups)
+_B128_GROUPS = np.array([[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
+                         [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31]])
+_B128_GROUPS = np.concatenate([_B128_GROUPS, _B128_GROUPS + 32])
+_WAYS: dict = {}
+
+
+def bank_ways(p: TilePlan, kdims: tuple) -> float:
+    """Mean ways of the kernel's halo-fragment reads (ds_read_b128: bank of byte address a is
+    (a / 4) mod 64, so a lane's 16-B read takes slot (a / 16) mod 16) over every fragment, every
+    distinct k-step tap pattern and the four lane groups the LDS serves together; 1.0 =
+    conflict-free.  Lane l = (lane group lg = l / 16, fragment row lr = l % 16) reads halo
+    position rowtab[lr] at the plane and tap offset of lg (``lb`` / ``s_kt`` in conv_tile.hip).
+    The groups mix rows of two lane groups ({0-3, 12-15} of one with {4-11} of the next), so a
+    k-step whose lane groups read different taps (CS = 8, fp8) shifts one half's residues."""
+    key = (p, tuple(kdims))
+    w = _WAYS.get(key)
+    if w is not None:
+        return w
+    tab = row_table(p, kdims)
+    kt = k_table(p, kdims)[:p.nks]
+    hb = tab[:, 0].reshape(-1, 16).astype(np.int64)               # [fragments, 16 rows]
+    lg, lr = _B128_GROUPS // 16, _B128_GROUPS % 16                 # [4, 16]
+    cpp = p.CS // 16 if p.f8 else p.CS // 8
+    if p.f8:
+        pl = 2 * (lg & 1) if cpp == 4 else 0 * lg
+    else:
+        pl = lg if cpp >= 4 else ((lg & 1) if cpp == 2 else 0 * lg)
+    pats = np.unique(kt.astype(np.int64), axis=0)                  # distinct k-step offset rows
+    a = hb[:, lr][:, None] * 16 + (pl * p.HPpad * 16)[None, None] + pats[:, lg][None]   # [F, P, 4, 16]
+    a = np.sort(a, axis=-1)
+    same = np.zeros(a.shape, dtype=bool)                            # one address: a broadcast
+    same[..., 1:] = a[..., 1:] == a[..., :-1]
+    slot = (a // 16) % 16
+    cnt = ((slot[..., None] == np.arange(16)) & ~same[..., None]).sum(-2)
+    w = float(cnt.max(-1).mean())
+    with _LOCK:
+        _WAYS[key] = w
+    return w
 
 
 def _pool_row_table(p: TilePlan, HH: int, HW: int) -> np.ndarray:

@@ -44,6 +44,20 @@ def test_row_table_conflict_free_when_residues_allow():
     assert all(len(set(r.tolist())) == 16 for r in res)
 
 
+def test_bank_ways_matches_row_residues():
+    """bank_ways: 1.0 for a fragment set with 16 distinct residues and one tap per lane group
+    pair (CS = 32); a plan whose fragments repeat residues reads more than 1-way; CS = 8 (four
+    taps per k-step, the ds_read_b128 groups mixing two lane groups) shifts residues."""
+    p = ct.TilePlan(5, 5, 20, 32, 8, 2, 1088, 28, 4, 1088 * 64, ct._magic(22), ct._magic(7 * 22), 0.0)
+    assert ct.bank_ways(p, (3, 3, 3)) == 1.0
+    q = ct.plan(128, (20, 20, 20), (3, 3, 3), 64, 64)           # conv4 fwd: 5x10x10, 44 repeated slots
+    res = ct.row_table(q, (3, 3, 3))[:, 0].reshape(-1, 16) % 16
+    if any(len(set(r.tolist())) < 16 for r in res):
+        assert ct.bank_ways(q, (3, 3, 3)) > 1.0
+    s = ct.plan(128, (29, 29, 29), (4, 4, 4), 8, 32)             # the stem (CS = 8)
+    assert 1.0 <= ct.bank_ways(s, (4, 4, 4)) <= 4.0
+
+
 def test_magic_division_exact():
     for HH, HW in [(9, 29), (14, 25), (7, 22), (13, 28), (15, 33)]:
         assert ct._magic_ok(HH, HW, 4096)
