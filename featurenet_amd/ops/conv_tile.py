@@ -197,10 +197,15 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
         HH, HW = c.TH + KH - 1, c.TW + KW - 1
         if not _magic_ok(HH, HW, c.HPpad):
             continue
-        tab = row_table(c, kdims)
-        res = tab[:, 0].reshape(-1, 16) % 16
-        dups = sum(16 - len(set(r.tolist())) for r in res)
-        cost = c.cost * (1.0 + 0.5 * dups / res.size)
+        if f8:
+            # fp8: the simulated ways of its reads (the parity tables below repeat residues by
+            # design); the fused-pool conv4 went 2.8 -> 1.0 ways and 9 % faster
+            cost = c.cost * (1.0 + 0.5 * (bank_ways(c, kdims) - 1.0))
+        else:
+            tab = row_table(c, kdims)
+            res = tab[:, 0].reshape(-1, 16) % 16
+            dups = sum(16 - len(set(r.tolist())) for r in res)
+            cost = c.cost * (1.0 + 0.5 * dups / res.size)
         ranked.append(TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct",
                                                           "BUF", "mHW", "mHHW")), cost, f8, pool, m32))
     if not ranked:
@@ -225,20 +230,28 @@ def row_table(p: TilePlan, kdims: tuple) -> np.ndarray:
         with _LOCK:
             _ROWTAB[key] = tab
         return tab
+    tab = _std_row_table(p, HH, HW)
+    if p.f8 and p.CS == 32:
+        # fp8 32-channel slices read 4 taps per k-step, one per lane group, and a ds_read_b128
+        # group mixes two lane groups: rows {0-3, 12-15} of one tap with rows {4-11} of the
+        # next.  Distinct residues per fragment do not survive that shift; fragments of one
+        # residue parity (each half holding all 8 residues of it) do, for every odd tap step.
+        alt = _parity_row_table(p, HH, HW)
+        if _table_ways(alt, p, kdims) < _table_ways(tab, p, kdims):
+            tab = alt
+    with _LOCK:
+        _ROWTAB[key] = tab
+    return tab
+
+
+def _rows_and_positions(p: TilePlan, HH: int, HW: int):
     td, th, tw = np.meshgrid(np.arange(p.TD), np.arange(p.TH), np.arange(p.TW), indexing="ij")
     nat = ((td * p.TH + th) * p.TW + tw).reshape(-1)
     hb = ((td * HH + th) * HW + tw).reshape(-1)
-    nfrag = 4 * p.MT
-    buckets = [list(zip(hb[hb % 16 == r].tolist(), nat[hb % 16 == r].tolist())) for r in range(16)]
-    frags = [[None] * 16 for _ in range(nfrag)]
-    extra = []
-    for r in range(16):
-        for i, item in enumerate(buckets[r]):
-            if i < nfrag:
-                frags[i][r] = item
-            else:
-                extra.append(item)
-    maxhb = int(hb.max())
+    return nat, hb
+
+
+def _fill_rest(frags: list, extra: list, maxhb: int) -> np.ndarray:
     for f in frags:                              # overflow rows fill free slots (a conflict, not an error)
         for s in range(16):
             if f[s] is None and extra:
@@ -250,10 +263,42 @@ def row_table(p: TilePlan, kdims: tuple) -> np.ndarray:
                 used = {x[0] % 16 for x in f if x is not None}
                 cand = [r for r in range(16) if r not in used and r <= maxhb]
                 f[s] = ((cand[0] if cand else 0), -1)
-    tab = np.asarray([x for f in frags for x in f], dtype=np.int32)
-    with _LOCK:
-        _ROWTAB[key] = tab
-    return tab
+    return np.asarray([x for f in frags for x in f], dtype=np.int32)
+
+
+def _parity_row_table(p: TilePlan, HH: int, HW: int) -> np.ndarray:
+    """Fragments of one residue parity: lanes {0-3, 12-15} and {4-11} each take one row of
+    every residue of the fragment's parity (the parity with more rows left)."""
+    nat, hb = _rows_and_positions(p, HH, HW)
+    buckets = [list(zip(hb[hb % 16 == r].tolist(), nat[hb % 16 == r].tolist())) for r in range(16)]
+    halves = ((0, 1, 2, 3, 12, 13, 14, 15), (4, 5, 6, 7, 8, 9, 10, 11))
+    frags = []
+    for _ in range(4 * p.MT):
+        even = sum(len(buckets[r]) for r in range(0, 16, 2))
+        odd = sum(len(buckets[r]) for r in range(1, 16, 2))
+        par = 0 if even >= odd else 1
+        f = [None] * 16
+        for lanes in halves:
+            for k, lr in enumerate(lanes):
+                if buckets[par + 2 * k]:
+                    f[lr] = buckets[par + 2 * k].pop()
+        frags.append(f)
+    return _fill_rest(frags, [x for b in buckets for x in b], int(hb.max()))
+
+
+def _std_row_table(p: TilePlan, HH: int, HW: int) -> np.ndarray:
+    nat, hb = _rows_and_positions(p, HH, HW)
+    nfrag = 4 * p.MT
+    buckets = [list(zip(hb[hb % 16 == r].tolist(), nat[hb % 16 == r].tolist())) for r in range(16)]
+    frags = [[None] * 16 for _ in range(nfrag)]
+    extra = []
+    for r in range(16):
+        for i, item in enumerate(buckets[r]):
+            if i < nfrag:
+                frags[i][r] = item
+            else:
+                extra.append(item)
+    return _fill_rest(frags, extra, int(hb.max()))
 
 
 # the lanes of each ds_read_b128 bank group (MI355X: four non-contiguous 16-lane groups)
@@ -273,9 +318,14 @@ def bank_ways(p: TilePlan, kdims: tuple) -> float:
     k-step whose lane groups read different taps (CS = 8, fp8) shifts one half's residues."""
     key = (p, tuple(kdims))
     w = _WAYS.get(key)
-    if w is not None:
-        return w
-    tab = row_table(p, kdims)
+    if w is None:
+        w = _table_ways(row_table(p, kdims), p, kdims)
+        with _LOCK:
+            _WAYS[key] = w
+    return w
+
+
+def _table_ways(tab: np.ndarray, p: TilePlan, kdims: tuple) -> float:
     kt = k_table(p, kdims)[:p.nks]
     hb = tab[:, 0].reshape(-1, 16).astype(np.int64)               # [fragments, 16 rows]
     lg, lr = _B128_GROUPS // 16, _B128_GROUPS % 16                 # [4, 16]
@@ -291,34 +341,100 @@ def bank_ways(p: TilePlan, kdims: tuple) -> float:
     same[..., 1:] = a[..., 1:] == a[..., :-1]
     slot = (a // 16) % 16
     cnt = ((slot[..., None] == np.arange(16)) & ~same[..., None]).sum(-2)
-    w = float(cnt.max(-1).mean())
-    with _LOCK:
-        _WAYS[key] = w
-    return w
+    return float(cnt.max(-1).mean())
 
 
 def _pool_row_table(p: TilePlan, HH: int, HW: int) -> np.ndarray:
-    """Row table of the fused-pool fp8 epilogue: window i of the tile's (TD/2, TH/2, TW/2)
-    2^3 windows goes to wave i // 16, lane i % 16; its member m = (md, mh, mw) to fragment
-    m, so every lane holds one whole window (max over its 8 fragments).  Missing windows are
-    dummy rows (-1).  Bank slots are not permuted (members of a fragment are window bases
-    shifted by one fixed offset)."""
+    """Row table of the fused-pool fp8 epilogue: every lane holds the 8 members of one 2^3
+    window, one member per fragment (MT = 8), so the lane's running max over its fragments is
+    the pooled value (the epilogue takes the window from any member's coordinates halved).
+    Missing windows are dummy rows (-1).
+
+    Bank slots: a ds_read_b128 lane group reads halo position hb at slot hb mod 16, and window
+    bases are all even positions, so one member order for every lane puts a fragment's 16 rows
+    on at most 8 slots (2.8 ways on the 128^3 conv4 plan, bank_ways).  Instead the windows are
+    dealt to the 4 waves round-robin by base residue (so no slot is reachable from more than
+    8 (lane, member) pairs of a wave), and each wave's bipartite multigraph lane -> slot (an
+    edge per member, dummy lanes taking the slots' remaining degree) is 8-regular: it splits
+    into 8 perfect matchings (Koenig), one per fragment -- 16 distinct slots in every fragment.
+    Where the degrees do not allow it, the plain order (member m in fragment m) is kept."""
     assert p.MT == 8 and p.TD % 2 == 0 and p.TH % 2 == 0 and p.TW % 2 == 0
     wd, wh, ww = np.meshgrid(np.arange(p.TD // 2), np.arange(p.TH // 2), np.arange(p.TW // 2), indexing="ij")
     wd, wh, ww = wd.reshape(-1), wh.reshape(-1), ww.reshape(-1)
     nwin = wd.size
     assert nwin <= 64, "more windows than lanes x waves"
+    md, mh, mw = np.arange(8) >> 2, (np.arange(8) >> 1) & 1, np.arange(8) & 1
+    moff = (md * HH + mh) * HW + mw                              # halo offset of member m
+    base = (2 * wd * HH + 2 * wh) * HW + 2 * ww
+
+    def member_row(i, m):
+        d, h, w = 2 * wd[i] + md[m], 2 * wh[i] + mh[m], 2 * ww[i] + mw[m]
+        return ((d * HH + h) * HW + w, (d * p.TH + h) * p.TW + w)
+
     tab = np.zeros((4 * 8 * 16, 2), dtype=np.int32)
-    for i in range(64):
-        wave, lr = divmod(i, 16)
-        for m in range(8):
-            r = (wave * 8 + m) * 16 + lr
-            if i < nwin:
-                d, h, w = 2 * wd[i] + (m >> 2), 2 * wh[i] + ((m >> 1) & 1), 2 * ww[i] + (m & 1)
-                tab[r] = ((d * HH + h) * HW + w, (d * p.TH + h) * p.TW + w)
-            else:
-                tab[r] = (0, -1)
+    tab[:, 1] = -1
+    colored = _pool_coloring(base, moff, nwin)
+    if colored is None:                           # plain order: window i -> wave i // 16, lane i % 16
+        for i in range(nwin):
+            wave, lr = divmod(i, 16)
+            for m in range(8):
+                tab[(wave * 8 + m) * 16 + lr] = member_row(i, m)
+        return tab
+    for wave, lanes, frag in colored:             # frag[f][lr] = (window, member) or (-1, slot)
+        for f in range(8):
+            for lr in range(16):
+                i, m = frag[f][lr]
+                tab[(wave * 8 + f) * 16 + lr] = member_row(i, m) if i >= 0 else (m, -1)
     return tab
+
+
+def _pool_coloring(base: np.ndarray, moff: np.ndarray, nwin: int):
+    """[(wave, windows, frag[8][16] of (window, member) | (-1, dummy slot))] or None (a slot
+    reachable from more than 8 (lane, member) pairs of one wave)."""
+    order = sorted(range(nwin), key=lambda i: (int(base[i]) % 16, i))
+    waves = [order[w::4] for w in range(4)]
+    out = []
+    for wave, wins in enumerate(waves):
+        if len(wins) > 16:
+            return None
+        # edges lane -> slot: (member list per (lane, slot)); lanes 0..len-1 are windows
+        edges = [[[] for _ in range(16)] for _ in range(16)]
+        deg = np.zeros(16, dtype=int)
+        for lr, i in enumerate(wins):
+            for m in range(8):
+                r = int(base[i] + moff[m]) % 16
+                edges[lr][r].append(m)
+                deg[r] += 1
+        if deg.max() > 8:
+            return None
+        spare = [r for r in range(16) for _ in range(8 - int(deg[r]))]   # 8 per dummy lane
+        for k, lr in enumerate(range(len(wins), 16)):
+            for r in spare[8 * k:8 * k + 8]:
+                edges[lr][r].append(-1)
+        frag = []
+        for f in range(8):
+            match_r = [-1] * 16                   # slot -> lane
+            for lr in range(16):
+                if not _augment(lr, edges, match_r, [False] * 16):
+                    return None
+            row = [None] * 16
+            for r, lr in enumerate(match_r):
+                m = edges[lr][r].pop()
+                row[lr] = (wins[lr], m) if m >= 0 else (-1, r)
+            frag.append(row)
+        out.append((wave, wins, frag))
+    return out
+
+
+def _augment(lr, edges, match_r, seen) -> bool:
+    """Kuhn's augmenting path from lane lr over slots with remaining edges."""
+    for r in range(16):
+        if edges[lr][r] and not seen[r]:
+            seen[r] = True
+            if match_r[r] < 0 or _augment(match_r[r], edges, match_r, seen):
+                match_r[r] = lr
+                return True
+    return False
 
 
 def natural_view(out_dims: tuple) -> tuple:

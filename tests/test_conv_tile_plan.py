@@ -102,7 +102,8 @@ def test_fp8_plans_and_weight_stream(out, k, c, n):
                                        ((10, 12, 14), (3, 3, 3), 32, 32)])
 def test_fp8_pool_plans_hold_whole_windows_per_lane(out, k, c, n):
     """Fused-pool fp8 plans: even tile dims, and lane lr of wave w holds the 8 members of one
-    2^3 window in fragments 0..7 (each tile row exactly once)."""
+    2^3 window in fragments 0..7 (each tile row exactly once, any member order); the
+    edge-coloured table reads conflict-free (16 distinct slots per fragment)."""
     p = ct.plan(64, out, k, c, n, f8=True, pool=True)
     assert p is not None and p.pool and p.MT == 8
     assert p.TD % 2 == 0 and p.TH % 2 == 0 and p.TW % 2 == 0
@@ -118,5 +119,7 @@ def test_fp8_pool_plans_hold_whole_windows_per_lane(out, k, c, n):
                 continue
             tw, th, td = rows % p.TW, (rows // p.TW) % p.TH, rows // (p.TW * p.TH)
             assert len({(a // 2, b // 2, e // 2) for a, b, e in zip(td, th, tw)}) == 1   # one window
-            assert td[0] % 2 == 0 and th[0] % 2 == 0 and tw[0] % 2 == 0                  # member 0 = base
+            assert len({(a % 2, b % 2, e % 2) for a, b, e in zip(td, th, tw)}) == 8      # 8 members
+    if p.CS == 64:
+        assert ct.bank_ways(p, k) == 1.0
     assert ct.plan(64, (21, 20, 20), k, c, n, f8=True, pool=True) is None           # odd output dim

@@ -60,7 +60,7 @@ def test_fp8_stem_model_matches_bf16_stem_path():
     assert cos_ab > 0.99 and cos_ref > 0.97, (cos_ab, cos_ref)
 
 
-@pytest.mark.parametrize("N,S,C,K", [(2, 22, 64, 64), (3, 14, 32, 32)])
+@pytest.mark.parametrize("N,S,C,K", [(2, 22, 64, 64), (3, 14, 32, 32), (2, 54, 64, 64)])
 def test_fp8_fused_pool_matches_unfused(N, S, C, K):
     """conv_tile F8 with the fused 2^3 max-pool epilogue == the plain F8 kernel (bf16 output)
     followed by relu + max-pool in torch (identical conv arithmetic; bf16 rounding of the max)."""
