@@ -10,7 +10,9 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
 
-import featurenet_amd.ops.conv as C  # noqa: E402
+import importlib  # noqa: E402
+
+C = importlib.import_module("featurenet_amd.ops.conv")   # (ops.conv is also a function name)
 
 STATS = collections.defaultdict(lambda: [0, 0.0])
 
