@@ -208,19 +208,77 @@ def upconv_forward(x5: torch.Tensor, w: torch.Tensor):
     return y, slab
 
 
-def upconv_dgrad(dsh: torch.Tensor, w: torch.Tensor, x_shape) -> torch.Tensor:
-    """dx [N, D, H, W, C] = the 2^3 'valid' conv over the shifted view with :func:`dgrad_weights`."""
+def _dgrad_plan(x_shape, K: int):
+    from . import conv_tile
+
+    N, D, H, W, C = x_shape
+    return conv_tile.plan(N, (D, H, W), (2, 2, 2), 8 * K, C)
+
+
+def upconv_dgrad(dsh: torch.Tensor, w: torch.Tensor, x_shape, mask=None):
+    """dx [N, D, H, W, C] = the 2^3 'valid' conv over the shifted view with :func:`dgrad_weights`.
+    ``mask`` (x = relu(bn(y)) with its relu-mask bytes, the BN statistics identity of
+    ops/bnfuse.py): returns ``(dx, slab)``, the slab's row 0 the column sums of dx * relu'(x)."""
     from . import conv_tile
 
     N, D, H, W, C = x_shape
     K = w.shape[0]
-    p = conv_tile.plan(N, (D, H, W), (2, 2, 2), 8 * K, C)
+    p = _dgrad_plan(x_shape, K)
     kd = dgrad_weights(w.detach().float()).reshape(C, 8, 8 * K)
     wpk = conv_tile.pack_weights(kd, C, 8, 8 * K, p, dgrad=False)
     geom = conv_tile.geometry(p, (N, D + 1, H + 1, W + 1, 8 * K), (D, H, W), (2, 2, 2), (0, 0, 0))
     dx = torch.empty(N, D, H, W, C, dtype=torch.bfloat16, device=dsh.device)
-    conv_tile.run(dsh, wpk, None, dx, None, p, geom, (2, 2, 2), C, 0)
-    return dx
+    if mask is None:
+        conv_tile.run(dsh, wpk, None, dx, None, p, geom, (2, 2, 2), C, 0)
+        return dx
+    assert mask.numel() * 8 == dx.numel() and mask.dtype == torch.uint8
+    slab = torch.empty(conv_tile.workers(p, geom, C), 2, C, dtype=torch.float32, device=dsh.device)
+    conv_tile.run(dsh, wpk, None, dx, slab, p, geom, (2, 2, 2), C, 0, bny=mask)
+    return dx, slab
+
+
+def _bn_source(ctx, x: torch.Tensor, K: int) -> None:
+    """Forward: when the decoder's input is a tagged relu(bn(y)) with its relu mask (the
+    encoder's last BN, ops/bnfuse.py) and the dgrad plan takes the mask epilogue, keep the
+    source for the backward's statistics identity."""
+    from . import bnfuse, conv_tile
+
+    ctx.bn_src = None
+    if not ctx.needs_input_grad[0]:
+        return
+    src = bnfuse.source_of(x)
+    if src is None or src[3] is None or src[2] != 1:
+        return
+    p = _dgrad_plan(tuple(x.shape), K)
+    if p is not None and not p.m32 and conv_tile.mask_dgrad_ok(p, x.shape[-1]):
+        ctx.bn_src = src
+
+
+def _decoder_backward(ctx, dsh: torch.Tensor, w: torch.Tensor, x: torch.Tensor, K: int):
+    """(dx, dw) of the sub-pixel decoder conv from the shifted dy; with a BN source
+    (:func:`_bn_source`) the dgrad sums that BN's g = dx * relu' and, once the class weight
+    gradients exist, S = sum W_class . dW_class (the adjoint identity holds class by class: the
+    dgrad's weights are the class weights re-indexed) goes to the BN backward with it."""
+    from . import bnfuse, conv_wtile
+    from .conv import bn_wdot
+
+    src, ctx.bn_src = getattr(ctx, "bn_src", None), None
+    dx = slab = None
+    if ctx.needs_input_grad[0]:
+        if src is not None:
+            dx, slab = upconv_dgrad(dsh, w, x.shape, mask=src[3])
+        else:
+            dx = upconv_dgrad(dsh, w, x.shape)
+    dw = None
+    if ctx.needs_input_grad[1]:
+        N, D, H, W, C = x.shape
+        p = conv_wtile.plan_subpixel(N, (D, H, W), C, K)
+        dwf = conv_wtile.conv_wgrad_subpixel(dsh, x, p)
+        if slab is not None:
+            wf = forward_weights(w.detach().float()).reshape(-1, C).contiguous()
+            bnfuse.offer(dx, ("identity", slab, bn_wdot(wf, dwf.reshape(-1, C), None)), src[0])
+        dw = fold_weight_grad(dwf).reshape(w.shape)
+    return dx, dw
 
 
 def bn_bwd_to_shifted(dz2, y2, prm, dbeta, dgamma, act: int, full_shape) -> torch.Tensor:
@@ -253,7 +311,6 @@ def _head_backward(ctx, d2):
     gradients in SubpixelDecoderHeadFn.backward's order."""
     from .. import _native
     from . import bn as bn_ops
-    from . import conv_wtile
     from ..training.flat import grad_target
     from .conv import native_colsum, pw_wgrad
 
@@ -274,12 +331,7 @@ def _head_backward(ctx, d2):
               y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), part.data_ptr(), ctx.act)
     dbeta, dgamma = bn_ops._bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
     dsh = bn_bwd_to_shifted(dz2, y2, prm, dbeta, dgamma, ctx.act, y.shape)
-    dx = upconv_dgrad(dsh, w, x.shape) if ctx.needs_input_grad[0] else None
-    dw = None
-    if ctx.needs_input_grad[1]:
-        N, D, H, W, C = x.shape
-        p = conv_wtile.plan_subpixel(N, (D, H, W), C, K)
-        dw = fold_weight_grad(conv_wtile.conv_wgrad_subpixel(dsh, x, p)).reshape(w.shape)
+    dx, dw = _decoder_backward(ctx, dsh, w, x, K)
     return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
             None, None, None, None, None, dhw, dhb)
 
@@ -300,6 +352,7 @@ class SubpixelDecoderHeadFn(torch.autograd.Function):
         from .conv import pw_fwd
 
         y, prm, w2, bias = _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb)
+        _bn_source(ctx, x, w.shape[0])
         out = pw_fwd(y.reshape(-1, y.shape[-1]), w2, bias, 0, pro=(prm[2], prm[3], act))
         ctx.save_for_backward(x, w, y, prm, hw)
         ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
@@ -324,6 +377,7 @@ class SubpixelDecoderHeadXentFn(torch.autograd.Function):
         from .. import _native
 
         y, prm, w2, bias = _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb)
+        _bn_source(ctx, x, w.shape[0])
         K = y.shape[-1]
         y2 = y.reshape(-1, K)
         M, NC = y2.shape[0], w2.shape[0]
@@ -368,6 +422,7 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         from .. import _native
 
         y, prm, w2, bias = _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb)
+        _bn_source(ctx, x, w.shape[0])
         K = y.shape[-1]
         y2 = y.reshape(-1, K)
         M, NC = y2.shape[0], w2.shape[0]
@@ -392,7 +447,6 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
     def backward(ctx, dloss, _dhits):
         from .. import _native
         from . import bn as bn_ops
-        from . import conv_wtile
         from ..training.flat import grad_target
 
         x, w, y, prm, hw, dz, part = ctx.saved_tensors
@@ -414,12 +468,7 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         mom = tot[32 + 32 * 32:].view(1, 2, 32)[:, :, :K].contiguous()   # (sum g, sum g*y) of the BN
         dbeta, dgamma = bn_ops._bwd_param_grads(dz, y2, prm, ctx.act, *ctx.params, part=mom)
         dsh = bn_bwd_to_shifted(dz, y2, prm, dbeta, dgamma, ctx.act, y.shape)
-        dx = upconv_dgrad(dsh, w, x.shape) if ctx.needs_input_grad[0] else None
-        dw = None
-        if ctx.needs_input_grad[1]:
-            N, D, H, W, C = x.shape
-            p = conv_wtile.plan_subpixel(N, (D, H, W), C, K)
-            dw = fold_weight_grad(conv_wtile.conv_wgrad_subpixel(dsh, x, p)).reshape(w.shape)
+        dx, dw = _decoder_backward(ctx, dsh, w, x, K)
         return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
                 None, None, None, None, None, dhw, dhb, None, None)
 
@@ -431,6 +480,7 @@ class _SavedView:
         self.saved_tensors = ctx.saved_tensors[:5]
         self.needs_input_grad = ctx.needs_input_grad
         self.act, self.has_b, self.bparam, self.params = ctx.act, ctx.has_b, ctx.bparam, ctx.params
+        self.bn_src, ctx.bn_src = getattr(ctx, "bn_src", None), None
 
 
 def decoder_head(x5, w, gamma, beta, running_mean, running_var, hw, hb, momentum=0.1, eps=1e-5, act="relu"):

@@ -134,3 +134,35 @@ def test_fused_head_xent_matches_softmax_xent(monkeypatch, smoothing, mode):
         assert k in g1, k
         r = _rel(g1[k], g0[k])
         assert r < 2e-2, (k, r)
+
+
+def test_decoder_bn_identity_matches_colstats(monkeypatch):
+    """The encoder's last BN (relu(bn(y)) feeding the sub-pixel decoder) takes its backward from
+    the statistics identity: the decoder dgrad sums g = dx * mask and S = sum W_class . dW_class
+    comes from the class weight gradients.  Every parameter gradient matches the colstats path
+    (FN_BN_IDENTITY=0), and the identity offer is actually made."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3DSeg
+    from featurenet_amd.ops import bnfuse
+
+    torch.manual_seed(7)
+    N, S = 2, 24
+    m = FeatureNet3DSeg(input_size=S, num_classes=25).cuda().train()
+    x = (torch.rand(N, S, S, S, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    lab = torch.randint(0, 25, (N, S, S, S), device="cuda")
+    offers = []
+    orig = bnfuse.offer
+    monkeypatch.setattr(bnfuse, "offer", lambda dz, slab, y: (offers.append(slab[0] if isinstance(slab, tuple)
+                                                                             else "raw"), orig(dz, slab, y)))
+    monkeypatch.setenv("FN_SEG_XENT", "1")
+    res = []
+    for flag in ("0", "1", "1"):                     # (warm-up pass, then the identity pass compared)
+        monkeypatch.setenv("FN_BN_IDENTITY", flag)
+        m.zero_grad(set_to_none=True)
+        loss = m.loss(x, lab)
+        loss.backward()
+        res.append({k: p.grad.detach().float().clone() for k, p in m.named_parameters() if p.grad is not None})
+    assert offers.count("identity") >= 2 * 4 - 2      # 3 encoder convs + the decoder, per identity pass
+    g0, g1 = res[0], res[2]
+    for k in g0:
+        r = _rel(g1[k], g0[k])
+        assert r < 2e-2, (k, r)
