@@ -273,11 +273,16 @@ def test_identity_any_gamma(monkeypatch, gscale):
     _grads_ident(model, x, False, monkeypatch)   # (warm-up, as above)
     g0 = _grads_ident(model, x, False, monkeypatch)
     g1 = _grads_ident(model, x, True, monkeypatch)
+    g2 = _grads_ident(model, x, False, monkeypatch)
     assert calls["identity"] >= 1
+    # (gamma 1e-4: the gradients below the second BN are ~1e-4 of their usual scale and carry the
+    # run-to-run rounding differences of the forward's BN statistics (dynamically scheduled tiles)
+    # at O(1) relative size -- the colstats path against itself too; a division by gamma would
+    # be off by orders of magnitude, so the bound is 1e-2 or 4x the off/off spread)
+    rel = lambda u, v: (u - v).abs().max().item() / max(u.abs().max().item(), 1e-6)  # noqa: E731
     for n in g0:
-        a, b = g0[n], g1[n]
-        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
-        assert err < 1e-2, f"{n}: rel err {err:.2e}"
+        err, err0 = rel(g0[n], g1[n]), rel(g0[n], g2[n])
+        assert err < max(1e-2, 4 * err0), f"{n}: rel err {err:.2e} (off/off {err0:.2e})"
 
 
 @pytest.mark.parametrize("N,S,C,K,k", [(8, 22, 64, 64, 3), (4, 29, 32, 32, 5), (4, 25, 32, 64, 4)])

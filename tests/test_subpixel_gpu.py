@@ -38,11 +38,13 @@ def test_upconv_forward_and_stats(N, S):
     torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=2e-3, atol=2e-1)
 
 
-def test_bn_backward_shifted_layout_matches_natural():
+@pytest.mark.parametrize("shape", [(2, 12, 12, 12, 32), (3, 10, 14, 8, 64), (4, 64, 64, 64, 32)])
+def test_bn_backward_shifted_layout_matches_natural(shape):
+    """bn_bwd_apply_s2d == the natural BN backward, shifted (incl. non-cubic grids, 64 channels)."""
     torch.manual_seed(1)
-    N, F_, K = 2, 12, 32
-    y = _bf(torch.randn(N, F_, F_, F_, K, device="cuda"))
-    dz = _bf(torch.randn(N, F_, F_, F_, K, device="cuda"))
+    K = shape[-1]
+    y = _bf(torch.randn(*shape, device="cuda"))
+    dz = _bf(torch.randn(*shape, device="cuda"))
     prm = torch.stack([torch.randn(K), torch.rand(K) + 0.5, torch.randn(K), torch.randn(K)]).cuda()
     db, dg = torch.randn(K, device="cuda"), torch.randn(K, device="cuda")
     y2, dz2 = y.reshape(-1, K), dz.reshape(-1, K)
