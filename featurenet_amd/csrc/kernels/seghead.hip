@@ -47,6 +47,11 @@ __device__ __forceinline__ sh_s4 sh_tr4(const bf16* p) {
 }
 
 __device__ __forceinline__ float sh_bf(short s) { return __uint_as_float(((unsigned)(unsigned short)s) << 16); }
+__device__ __forceinline__ unsigned sh_pack2(float lo, float hi) {
+  typedef __bf16 sh_b2 __attribute__((ext_vector_type(2)));
+  const sh_b2 p = {f2bf(lo), f2bf(hi)};
+  return __builtin_bit_cast(unsigned, p);
+}
 __device__ __forceinline__ float bf16_round(float x) { return bf2f(f2bf(x)); }
 
 // ACT: the decoder BN's activation (ACT_NONE / ACT_RELU).
@@ -87,9 +92,17 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
     wl[nb] = __builtin_bit_cast(bf16x8, p.u);
     wd[nb] = __builtin_bit_cast(bf16x8, r.u);
   }
-  float bl[2];
+  // (the MFMAs take the weights as A and the voxel rows as B: a lane's accumulator holds 4
+  // consecutive classes / channels 16 nb + 4 lg + i of one voxel row 16 mt + lr -- one 8-B LDS
+  // store per fragment instead of four 2-B ones)
+  float bl[2][4];
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) bl[nb] = (bias && 16 * nb + lr < NC) ? bias[16 * nb + lr] : 0.f;
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cls = 16 * nb + 4 * lg + i;
+      bl[nb][i] = (bias && cls < NC) ? bias[cls] : 0.f;
+    }
   // this thread's input chunks always start at channel 8 (tid mod 4): 8 (scale, shift) pairs
   float psc[8], psh[8];
 #pragma unroll
@@ -97,13 +110,15 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
     psc[j] = sc[8 * (tid & 3) + j];
     psh[j] = shf[8 * (tid & 3) + j];
   }
-  // the moments' columns: 16 nb + lr
-  float msc[2], msh[2];
+  // the moments' columns: 16 nb + 4 lg + i
+  float msc[2][4], msh[2][4];
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
-    msc[nb] = sc[16 * nb + lr];
-    msh[nb] = shf[16 * nb + lr];
-  }
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      msc[nb][i] = sc[16 * nb + 4 * lg + i];
+      msh[nb][i] = shf[16 * nb + 4 * lg + i];
+    }
   Pack8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones.e[j] = f2bf(1.f);
@@ -116,7 +131,11 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
 #pragma unroll
     for (int j = 0; j < 2; ++j) adw[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  float ms[2] = {0.f, 0.f}, mq[2] = {0.f, 0.f};   // BN moments of columns 16 nb + lr
+  float ms[2][4], mq[2][4];                      // BN moments of columns 16 nb + 4 lg + i
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ms[nb][i] = mq[nb][i] = 0.f;
   float xl = 0.f, xc = 0.f;                       // loss, hits (row threads)
 
   uint4 rb[4];
@@ -156,29 +175,34 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
         const bf16x8 fa = *(const bf16x8*)(Zs + (64 * wave + 16 * mt + lr) * SH_LD + 8 * lg);
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb)
-          acc[mt][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, wl[nb], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          acc[mt][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl[nb], fa, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       }
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            Os[(64 * wave + 16 * mt + 4 * lg + i) * SH_LD + 16 * nb + lr] = f2bf(acc[mt][nb][i] + bl[nb]);
+          *(uint2*)(Os + (64 * wave + 16 * mt + lr) * SH_LD + 16 * nb + 4 * lg) =
+              make_uint2(sh_pack2(acc[mt][nb][0] + bl[nb][0], acc[mt][nb][1] + bl[nb][1]),
+                         sh_pack2(acc[mt][nb][2] + bl[nb][2], acc[mt][nb][3] + bl[nb][3]));
     }
     __syncthreads();
     // ---- softmax cross-entropy, one row per thread: d (bf16) replaces the logits ----
     {
+      // (the row moves as four 16-B LDS accesses each way: rows are 80 B apart, so the 16-lane
+      // groups of ds_read_b128 hit 16 distinct bank slots; scalar 2-B accesses were 4-way)
       bf16* orow = Os + tid * SH_LD;
       if (tid < rows) {
         const long long yl = labels[(long long)t * SH_BM + tid];
         const float off = smoothing / (float)NC, on = 1.f - smoothing + off;
+        Pack8 lv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lv[j].u = *(const uint4*)(orow + 8 * j);
         float v[32];
         float mx = -INFINITY;
         int am = 0;
 #pragma unroll
         for (int c = 0; c < 32; ++c) {
-          v[c] = c < NC ? bf2f(orow[c]) : -INFINITY;
+          v[c] = c < NC ? bf2f(lv[c >> 3].e[c & 7]) : -INFINITY;
           if (v[c] > mx) { mx = v[c]; am = c; }
         }
         float se = 0.f;
@@ -195,13 +219,15 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
             lrow -= tgt * lp;
             d = (__expf(lp) - tgt) * xscale;
           }
-          orow[c] = f2bf(d);                     // (padded classes: 0)
+          lv[c >> 3].e[c & 7] = f2bf(d);         // (padded classes: 0)
         }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *(uint4*)(orow + 8 * j) = lv[j].u;
         xl += lrow;
         xc += (am == yl) ? 1.f : 0.f;
       } else {
 #pragma unroll
-        for (int c = 0; c < 32; ++c) orow[c] = f2bf(0.f);
+        for (int j = 0; j < 4; ++j) *(uint4*)(orow + 8 * j) = make_uint4(0u, 0u, 0u, 0u);
       }
     }
     __syncthreads();
@@ -230,21 +256,22 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
       const bf16x8 fa = *(const bf16x8*)(Os + (64 * wave + 16 * mt + lr) * SH_LD + 8 * lg);
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
-        dzc[mt][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, wd[nb], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        dzc[mt][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wd[nb], fa, (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const int rb0 = 64 * wave + 16 * mt + 4 * lg;   // the C fragment's 4 rows
+      const int row = 64 * wave + 16 * mt + lr;      // the lane's voxel row, channels 16 nb + 4 lg + i
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const sh_s4 yv = sh_tr4(Ys + (rb0 + q) * SH_LD + 16 * nb + 4 * pp);
+        const uint2 y4 = *(const uint2*)(Ys + row * SH_LD + 16 * nb + 4 * lg);
+        const unsigned yw[2] = {y4.x, y4.y};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float g0 = bf16_round(dzc[mt][nb][i]);   // the stored dz
-          const float yy = sh_bf(yv[i]);
-          const float g = act_bwd_from_out(act_fwd(yy * msc[nb] + msh[nb], ACT), ACT) * g0;
-          ms[nb] += g;
-          mq[nb] += g * yy;
+          const float yy = (i & 1) ? __uint_as_float(yw[i >> 1] & 0xffff0000u) : __uint_as_float(yw[i >> 1] << 16);
+          const float g = act_bwd_from_out(act_fwd(yy * msc[nb][i] + msh[nb][i], ACT), ACT) * g0;
+          ms[nb][i] += g;
+          mq[nb][i] += g * yy;
         }
       }
     }
@@ -253,9 +280,8 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          Os[(64 * wave + 16 * mt + 4 * lg + i) * SH_LD + 16 * nb + lr] = f2bf(dzc[mt][nb][i]);
+        *(uint2*)(Os + (64 * wave + 16 * mt + lr) * SH_LD + 16 * nb + 4 * lg) =
+            make_uint2(sh_pack2(dzc[mt][nb][0], dzc[mt][nb][1]), sh_pack2(dzc[mt][nb][2], dzc[mt][nb][3]));
     __syncthreads();
     // dz rows -> HBM: 256 x 32 contiguous bf16, 16-B chunks
     {
@@ -268,14 +294,16 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
     }
   }
   // ---- workgroup partials (fixed order) ----
-  // moments: lanes lr, lr+16, lr+32, lr+48 hold column 16 nb + lr
+  // moments: the 16 lanes lr of lane group lg hold columns 16 nb + 4 lg + i
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
-    ms[nb] += __shfl_xor(ms[nb], 16, 64);
-    ms[nb] += __shfl_xor(ms[nb], 32, 64);
-    mq[nb] += __shfl_xor(mq[nb], 16, 64);
-    mq[nb] += __shfl_xor(mq[nb], 32, 64);
-  }
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        ms[nb][i] += __shfl_xor(ms[nb][i], o, 64);
+        mq[nb][i] += __shfl_xor(mq[nb][i], o, 64);
+      }
   xl = wave_sum(xl);
   xc = wave_sum(xc);
   __syncthreads();                               // (Ys / Zs are free: the per-wave partials go there)
@@ -297,12 +325,14 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) rw[34 + (16 * cb + 4 * lg + i) * 32 + 16 * nb + lr] = adw[cb][nb][i];
-  if (lg == 0) {
+  if (lr == 0) {
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      rw[34 + 1024 + 16 * nb + lr] = ms[nb];
-      rw[34 + 1024 + 32 + 16 * nb + lr] = mq[nb];
-    }
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        rw[34 + 1024 + 16 * nb + 4 * lg + i] = ms[nb][i];
+        rw[34 + 1024 + 32 + 16 * nb + 4 * lg + i] = mq[nb][i];
+      }
   }
   __syncthreads();
   float* out = part + (long long)blockIdx.x * PW;
