@@ -205,20 +205,22 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
           v[c] = c < NC ? bf2f(lv[c >> 3].e[c & 7]) : -INFINITY;
           if (v[c] > mx) { mx = v[c]; am = c; }
         }
-        float se = 0.f;
-#pragma unroll
-        for (int c = 0; c < 32; ++c) se += c < NC ? __expf(v[c] - mx) : 0.f;
-        const float lse = mx + __logf(se);
-        float lrow = 0.f;
+        // one exp per class: e_c = exp(v_c - max) serves the sum and the softmax (e_c / sum); the
+        // loss -sum_c tgt_c (v_c - lse) = lse - sum_c tgt_c v_c (the targets sum to 1)
+        float se = 0.f, sv = 0.f;
 #pragma unroll
         for (int c = 0; c < 32; ++c) {
-          float d = 0.f;
           if (c < NC) {
-            const float lp = v[c] - lse;
-            const float tgt = (c == yl) ? on : off;
-            lrow -= tgt * lp;
-            d = (__expf(lp) - tgt) * xscale;
+            sv += ((c == yl) ? on : off) * v[c];
+            v[c] = __expf(v[c] - mx);
+            se += v[c];
           }
+        }
+        const float lse = mx + __logf(se), inv = 1.f / se;
+        const float lrow = lse - sv;
+#pragma unroll
+        for (int c = 0; c < 32; ++c) {
+          const float d = c < NC ? (v[c] * inv - ((c == yl) ? on : off)) * xscale : 0.f;
           lv[c >> 3].e[c & 7] = f2bf(d);         // (padded classes: 0)
         }
 #pragma unroll
