@@ -75,3 +75,21 @@ def stream(t: torch.Tensor | None = None) -> int:
 
 def ptr(t: torch.Tensor | None) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+def copy_in(dst0: torch.Tensor, src0: torch.Tensor, dst1: torch.Tensor | None = None,
+            src1: torch.Tensor | None = None) -> None:
+    """``dst0.copy_(src0)`` (and ``dst1.copy_(src1)``) as ONE native launch (``misc.hip``
+    copy2_kernel) when both pairs are same-dtype, same-size, contiguous, 16-B aligned device
+    tensors -- the training step's batch copy-in; otherwise torch's copies."""
+    pairs = [(dst0, src0)] + ([(dst1, src1)] if dst1 is not None else [])
+    ok = all(d.is_cuda and s.is_cuda and d.dtype == s.dtype and d.numel() == s.numel() and d.is_contiguous()
+             and s.is_contiguous() and d.device == s.device and (d.data_ptr() | s.data_ptr()) % 16 == 0
+             for d, s in pairs) and kernels_available()
+    if not ok:
+        for d, s in pairs:
+            d.copy_(s)
+        return
+    nb = [d.numel() * d.element_size() for d, _ in pairs]
+    d1, s1, n1 = (pairs[1][0].data_ptr(), pairs[1][1].data_ptr(), nb[1]) if len(pairs) > 1 else (0, 0, 0)
+    kernels().copy2(dst0.data_ptr(), src0.data_ptr(), nb[0], d1, s1, n1, stream(dst0))

@@ -95,6 +95,7 @@ int fn_act_bwd(const void*, const void*, void*, long long, int, hipStream_t);
 int fn_dropout(const void*, void*, long long, float, unsigned, unsigned, hipStream_t);
 int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int fn_scale_unless_one(void*, int, const float*, long long, hipStream_t);
+int fn_copy2(void*, const void*, long long, void*, const void*, long long, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                  const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float);
@@ -706,6 +707,9 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("unpack_bits", [](uintptr_t bits, uintptr_t out, long long nbytes, uintptr_t st) {
     chk(fn_unpack_bits(P<const void*>(bits), P<void*>(out), nbytes, S(st)), "unpack_bits");
+  });
+  m.def("copy2", [](uintptr_t d0, uintptr_t s0, long long n0, uintptr_t d1, uintptr_t s1, long long n1, uintptr_t st) {
+    chk(fn_copy2(P<void*>(d0), P<const void*>(s0), n0, P<void*>(d1), P<const void*>(s1), n1, S(st)), "copy2");
   });
   m.def("scale_unless_one", [](uintptr_t x, int is_bf16, uintptr_t s, long long n, uintptr_t st) {
     chk(fn_scale_unless_one(P<void*>(x), is_bf16, P<const float*>(s), n, S(st)), "scale_unless_one");

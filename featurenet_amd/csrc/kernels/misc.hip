@@ -600,3 +600,51 @@ extern "C" int fn_scale_unless_one(void* x, int is_bf16, const float* s, long lo
   FN_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Batch copy-in: up to two device buffers (the step's input voxels and labels) in ONE launch,
+// 16-B vector loads with four chunks in flight per thread over a resident-sized grid (the
+// runtime's blit kernel moved the 33.5 MB FeatureNet-3D batch at ~1.3 TB/s in 25 us, plus a
+// second launch for the labels).  Pointers 16-B aligned (host-checked); tail bytes one by one.
+struct CopyJob {
+  unsigned char* d;
+  const unsigned char* s;
+  long long n;
+};
+
+__global__ __launch_bounds__(256) void copy2_kernel(CopyJob a, CopyJob b) {
+  const long long stride = (long long)gridDim.x * 256;
+  const long long t0 = (long long)blockIdx.x * 256 + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const CopyJob c = j == 0 ? a : b;
+    const long long nv = c.n >> 4;
+    const uint4* sv = reinterpret_cast<const uint4*>(c.s);
+    uint4* dv = reinterpret_cast<uint4*>(c.d);
+    long long i = t0;
+    for (; i + 3 * stride < nv; i += 4 * stride) {
+      const uint4 v0 = sv[i], v1 = sv[i + stride], v2 = sv[i + 2 * stride], v3 = sv[i + 3 * stride];
+      dv[i] = v0;
+      dv[i + stride] = v1;
+      dv[i + 2 * stride] = v2;
+      dv[i + 3 * stride] = v3;
+    }
+    for (; i < nv; i += stride) dv[i] = sv[i];
+    for (long long k = nv * 16 + t0; k < c.n; k += stride) c.d[k] = c.s[k];
+  }
+}
+
+extern "C" int fn_copy2(void* d0, const void* s0, long long n0, void* d1, const void* s1, long long n1,
+                        hipStream_t st) {
+  if (n0 < 0 || n1 < 0 || ((uintptr_t)d0 | (uintptr_t)s0) % 16 || (n1 > 0 && ((uintptr_t)d1 | (uintptr_t)s1) % 16))
+    return -2;
+  const long long nv = ((n0 > n1 ? n0 : n1) + 15) / 16;
+  long long blocks = (nv + 4 * 256 - 1) / (4 * 256);
+  if (blocks > 2048) blocks = 2048;              // 8 per CU, grid-stride beyond
+  if (blocks < 1) blocks = 1;
+  const CopyJob a{(unsigned char*)d0, (const unsigned char*)s0, n0};
+  const CopyJob b{(unsigned char*)d1, (const unsigned char*)s1, n1 > 0 ? n1 : 0};
+  hipLaunchKernelGGL(copy2_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, b);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

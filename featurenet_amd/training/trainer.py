@@ -28,6 +28,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .. import _native
 from ..ops import FlatAdam, FlatSGD, softmax_xent
 from ..parallel.ddp import DistributedFailure, GradBucketer
 from ..utils.events import default_log
@@ -207,8 +208,7 @@ class Trainer:
         if self._graph is not None:
             if key != self._gkey:                      # e.g. the last partial batch of an epoch
                 return self._eager_step(xb, yb)
-            self._sx.copy_(xb)
-            self._sy.copy_(yb)
+            _native.copy_in(self._sx, xb, self._sy, yb)   # (one launch for both)
             self._graph.replay()
             self.opt.t += 1
             return self._gloss, self._gcorr
