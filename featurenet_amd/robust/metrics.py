@@ -3,10 +3,11 @@
 Reference: the vendored ART metrics module ``model/metrics.py:57-324``
 (``empirical_robustness``, ``loss_sensitivity``, ``clever``, ``clever_u``,
 ``clever_t``).  Gradients are computed in batches on the GPU
-(:func:`featurenet_amd.robust.attacks.class_gradients` gets every class
-gradient of a whole random pool from one backward pass); the reverse-Weibull
-maximum-likelihood fits of every (sample, target) problem run in one batched call of the
-native runtime (scipy's exact estimator in C++, ``csrc/runtime/weibull.cpp``).
+(CLEVER: every (sample, target) problem draws its own pool and batches from one generator in
+the reference's order, and the gradients of many problems' pools come from one backward pass,
+each point seeding its own logit difference); the reverse-Weibull maximum-likelihood fits of
+every (sample, target) problem run in one batched call of the native runtime (scipy's exact
+estimator in C++, ``csrc/runtime/weibull.cpp``).
 """
 from __future__ import annotations
 
@@ -105,109 +106,144 @@ def _dual(norm):
     return np.inf if norm == 1 else (1 if norm in (np.inf, float("inf")) else 2)
 
 
+def _pair_gradients(model, pts: torch.Tensor, seeds: torch.Tensor) -> torch.Tensor:
+    """d(z . seed)/dx for every row of ``pts`` [B, ...] with its own logit seed [B, nc]: with seed
+    = e_pred - e_target this is grad_pred - grad_target of the reference's ``clever_t``
+    (``model/metrics.py:305-309``) in ONE backward pass, parameter gradients off."""
+    xg = pts.detach().float().clone().requires_grad_(True)
+    with A.no_param_grad(model):
+        z = A._logits(model, xg)
+        (g,) = torch.autograd.grad(z, xg, grad_outputs=seeds.to(z.dtype))
+    return g
+
+
 def clever_batch(model, xs: torch.Tensor, nb_batches: int, batch_size: int, radius: float, norm=2,
                  targets=None, c_init: float = 1.0, pool_factor: int = 10, clip=None, seed: int = 0,
-                 chunk_samples: int | None = None) -> list[dict]:
+                 rng=None, chunk_points: int | None = None) -> list[dict]:
     """CLEVER targeted scores of EVERY sample of ``xs`` [S, ...] for every target class (or
     ``targets``): one list entry ``{target: score}`` per sample.
 
-    The reference loops over samples (``tensorflow_generator.py:182-203``), each with a fresh
-    generator seeded 0 (one random pool of ``pool_factor * batch_size`` points in the Lp ball
-    and ``nb_batches`` random batches per target), a class-gradient pass of its pool and one
-    reverse-Weibull fit per target.  Here the same draws (every sample's generator starts at
-    seed 0, so the pool directions and batch indices are shared) feed batched gradient passes
-    over many samples' pools at once (:func:`~featurenet_amd.robust.attacks.class_gradients`,
-    parameter gradients off) and ONE batched fit of every (sample, target) problem."""
+    Reference semantics (``model/metrics.py:205-324`` driven by ``tensorflow_generator.py:
+    200-201``): for each sample, for each target class j != pred in class order, ``clever_t``
+    draws a FRESH pool of ``pool_factor * batch_size`` points in the Lp ball around the sample
+    (``random_sphere``), then ``nb_batches`` index batches of ``batch_size`` from that pool, all
+    from ONE global generator that runs on across targets and samples; the estimate is the
+    reverse-Weibull location of the per-batch maxima of ||grad_pred - grad_j||_q.  Here the
+    generator is ``rng`` (default ``np.random.default_rng(seed)``; pass
+    ``np.random.RandomState(s)`` for the reference's legacy ``np.random`` stream -- same calls, same
+    order, so the same pools and batches) and the draws follow exactly that order, but the
+    gradients of many (sample, target) pools run as one batched backward per chunk (each pool
+    point seeds its own logit difference e_pred - e_j, so one pass gives grad_pred - grad_j), the
+    next chunk's draws are made while the GPU works on the current one, and every (sample,
+    target) fit runs in ONE native batched call."""
     xs = xs.detach().float()
     S = xs.shape[0]
     if S == 0:
         return []
+    rng = np.random.default_rng(seed) if rng is None else rng
     z0 = A.predict(model, xs)                                   # [S, nc]
     preds = z0.argmax(-1).tolist()
     nc = z0.shape[1]
     dim = xs[0].numel()
     n_pool = pool_factor * batch_size
-    rng = np.random.default_rng(seed)
-    sphere = random_sphere(n_pool, dim, radius, norm, rng).reshape((n_pool,) + tuple(xs.shape[1:]))
-    sphere = torch.as_tensor(sphere, dtype=torch.float32, device=xs.device)
-    tgts = [[j for j in (range(nc) if targets is None else targets) if j != p] for p in preds]
-    ntg = max((len(t) for t in tgts), default=0)
-    # the batches each target position draws from a seed-0 generator after the pool
-    choice = np.stack([np.stack([rng.choice(n_pool, batch_size) for _ in range(nb_batches)]) for _ in range(ntg)]) \
-        if ntg else np.zeros((0, nb_batches, batch_size), dtype=np.int64)
+    probs = [(s_i, j) for s_i in range(S) for j in (range(nc) if targets is None else targets) if j != preds[s_i]]
+    Q = len(probs)
     q = _dual(norm)
-    step = chunk_samples or max(1, 16384 // max(n_pool * nc, 1))
-    norms = np.zeros((S, nc, n_pool), dtype=np.float64)          # ||grad_pred - grad_j|| over the pool
-    for i in range(0, S, step):
-        xb = xs[i:i + step]
-        b = xb.shape[0]
-        pool = (sphere.unsqueeze(0) + xb.unsqueeze(1)).reshape((b * n_pool,) + tuple(xs.shape[1:]))
+    # pool points per backward pass: ~64 MB of fp32 inputs (whole pools per chunk)
+    cp = chunk_points or max(n_pool, (16 << 20) // max(dim, 1))
+    per = max(1, cp // n_pool)
+    dev = xs.device
+    maxes = np.zeros((Q, nb_batches), dtype=np.float64)
+
+    def draw(lo: int, hi: int):
+        pools = np.empty((hi - lo, n_pool, dim), dtype=np.float32)
+        picks = np.empty((hi - lo, nb_batches, batch_size), dtype=np.int64)
+        for k in range(hi - lo):                  # the reference's order: pool, then the batches
+            pools[k] = random_sphere(n_pool, dim, radius, norm, rng)
+            for b in range(nb_batches):
+                picks[k, b] = rng.choice(n_pool, batch_size)
+        return pools, picks
+
+    def launch(lo: int, hi: int, pools: np.ndarray):
+        si = torch.as_tensor([probs[k][0] for k in range(lo, hi)], device=dev)
+        tj = torch.as_tensor([probs[k][1] for k in range(lo, hi)], device=dev)
+        pts = torch.as_tensor(pools, device=dev).reshape((hi - lo, n_pool) + tuple(xs.shape[1:]))
+        pts = (pts + xs[si].unsqueeze(1)).reshape(((hi - lo) * n_pool,) + tuple(xs.shape[1:]))
         if clip is not None:
-            pool = pool.clamp(*clip)
-        g = A.class_gradients(model, pool).reshape(b, n_pool, nc, -1)   # [b, P, C, dim]
-        pr = torch.as_tensor(preds[i:i + b], device=xs.device)
-        gp = g[torch.arange(b, device=xs.device), :, pr]            # [b, P, dim]
-        diff = gp.unsqueeze(2) - g                                  # [b, P, C, dim]
+            pts = pts.clamp(*clip)
+        sd = torch.zeros(hi - lo, nc, device=dev)
+        r = torch.arange(hi - lo, device=dev)
+        sd[r, torch.as_tensor(preds, device=dev)[si]] = 1.0
+        sd[r, tj] -= 1.0
+        g = _pair_gradients(model, pts, sd.repeat_interleave(n_pool, 0)).reshape(hi - lo, n_pool, -1)
         if q == 2:
-            gn = diff.norm(dim=-1)
-        elif q == 1:
-            gn = diff.abs().sum(-1)
-        else:
-            gn = diff.abs().amax(-1)
-        norms[i:i + b] = gn.permute(0, 2, 1).double().cpu().numpy()
-    rows, keys = [], []
-    for s_i in range(S):
-        for t, j in enumerate(tgts[s_i]):
-            gn = norms[s_i, j]
-            rows.append([gn[choice[t, k]].max() for k in range(nb_batches)])
-            keys.append((s_i, j))
-    locs = weibull_locs(np.asarray(rows, dtype=np.float64), c_init) if rows else np.zeros(0)
+            return g.norm(dim=-1)
+        return g.abs().sum(-1) if q == 1 else g.abs().amax(-1)
+
+    pending = None
+    lo = 0
+    nxt = draw(0, min(per, Q)) if Q else None
+    while lo < Q:
+        hi = min(lo + per, Q)
+        pools, picks = nxt
+        gn = launch(lo, hi, pools)                # (asynchronous on the GPU)
+        if hi < Q:
+            nxt = draw(hi, min(hi + per, Q))      # the next chunk's draws overlap this chunk's pass
+        if pending is not None:
+            plo, phi, pg, pp = pending
+            maxes[plo:phi] = np.take_along_axis(pg.double().cpu().numpy()[:, None, :],
+                                                pp.reshape(phi - plo, 1, -1), 2).reshape(
+                phi - plo, nb_batches, batch_size).max(-1)
+        pending = (lo, hi, gn, picks)
+        lo = hi
+    if pending is not None:
+        plo, phi, pg, pp = pending
+        maxes[plo:phi] = np.take_along_axis(pg.double().cpu().numpy()[:, None, :], pp.reshape(phi - plo, 1, -1),
+                                            2).reshape(phi - plo, nb_batches, batch_size).max(-1)
+    locs = weibull_locs(maxes, c_init) if Q else np.zeros(0)
     z0c = z0.double().cpu().numpy()
     out: list[dict] = [dict() for _ in range(S)]
-    for (s_i, j), loc in zip(keys, locs):
+    for (s_i, j), loc in zip(probs, locs):
         value = float(z0c[s_i, preds[s_i]] - z0c[s_i, j])
         out[s_i][j] = min(-value / loc, radius) if loc != 0 else radius
     return out
 
 
 def clever_scores(model, x: torch.Tensor, nb_batches: int, batch_size: int, radius: float, norm=2,
-                  targets=None, c_init: float = 1.0, pool_factor: int = 10, clip=None,
-                  rng: np.random.Generator | None = None) -> dict:
-    """CLEVER targeted scores of ONE sample ``x`` for every target class (or ``targets``)."""
-    if rng is not None:
-        return _clever_scores_rng(model, x, nb_batches, batch_size, radius, norm, targets, c_init, pool_factor, clip,
-                                  rng)
+                  targets=None, c_init: float = 1.0, pool_factor: int = 10, clip=None, rng=None) -> dict:
+    """CLEVER targeted scores of ONE sample ``x`` for every target class (or ``targets``); ``rng``
+    (optional) is the generator the draws continue from (the reference's global stream)."""
     return clever_batch(model, x.unsqueeze(0), nb_batches, batch_size, radius, norm, targets, c_init, pool_factor,
-                        clip)[0]
+                        clip, rng=rng)[0]
 
 
-def _clever_scores_rng(model, x, nb_batches, batch_size, radius, norm, targets, c_init, pool_factor, clip, rng):
-    """One sample with a caller-supplied generator (its draws continue across calls)."""
+def clever_t_literal(model, x: torch.Tensor, target: int, nb_batches: int, batch_size: int, radius: float, norm,
+                     c_init: float, pool_factor: int, clip, rng) -> float:
+    """The reference's ``clever_t`` line by line (``model/metrics.py:242-324``): pool, batches,
+    class gradients of each batch, per-batch max norm, reverse-Weibull fit -- one target of one
+    sample, unbatched.  The test oracle of :func:`clever_batch`."""
     xs = x.detach().float()
-    z0 = A.predict(model, xs.unsqueeze(0))[0]
+    z0 = A.predict(model, xs.unsqueeze(0))[0].double()
     pred = int(z0.argmax())
-    nc = z0.shape[0]
-    tgt = [j for j in (range(nc) if targets is None else targets) if j != pred]
+    if target == pred:
+        raise ValueError("The targeted class is the predicted class.")
     dim = xs.numel()
     n_pool = pool_factor * batch_size
-    pool = random_sphere(n_pool, dim, radius, norm, rng).reshape((n_pool,) + tuple(xs.shape))
-    pool = torch.as_tensor(pool, dtype=torch.float32, device=xs.device) + xs.unsqueeze(0)
+    pool = random_sphere(n_pool, dim, radius, norm, rng).astype(np.float32).reshape((n_pool,) + tuple(xs.shape))
+    pool = torch.as_tensor(pool, device=xs.device) + xs.unsqueeze(0)
     if clip is not None:
         pool = pool.clamp(*clip)
-    grads = A.class_gradients(model, pool)                    # [P, C, ...]
-    gp = grads[:, pred]
     q = _dual(norm)
-    rows = []
-    for j in tgt:
-        diff = (gp - grads[:, j]).reshape(n_pool, -1)
-        gn = (diff.norm(dim=1) if q == 2 else diff.abs().sum(1) if q == 1 else diff.abs().amax(1)).cpu().numpy()
-        rows.append([gn[rng.choice(n_pool, batch_size)].max() for _ in range(nb_batches)])
-    locs = weibull_locs(np.asarray(rows, dtype=np.float64), c_init) if rows else []
-    out = {}
-    for j, loc in zip(tgt, locs):
-        value = float(z0[pred] - z0[j])
-        out[j] = min(-value / loc, radius) if loc != 0 else radius
-    return out
+    gmax = []
+    for _ in range(nb_batches):
+        pick = torch.as_tensor(rng.choice(n_pool, batch_size), device=xs.device)
+        grads = A.class_gradients(model, pool[pick])              # [bs, C, ...]
+        d = (grads[:, pred] - grads[:, target]).reshape(batch_size, -1)
+        gn = d.norm(dim=1) if q == 2 else (d.abs().sum(1) if q == 1 else d.abs().amax(1))
+        gmax.append(float(gn.max()))
+    loc = _weibull_loc(np.asarray(gmax), c_init)
+    value = float(z0[pred] - z0[target])
+    return min(-value / loc, radius) if loc != 0 else radius
 
 
 def clever_t(model, x, target_class, nb_batches, batch_size, radius, norm=2, c_init=1.0, pool_factor=10, **kw):

@@ -121,21 +121,59 @@ class _Small(torch.nn.Module):
 
 
 def test_clever_batch_equals_per_sample_reference_loop():
-    """The batched CLEVER (all samples' pools in one gradient pass, one batched fit) gives the
-    reference's per-sample loop (fresh seed-0 generator per sample) exactly."""
-    from featurenet_amd.robust.metrics import _clever_scores_rng, clever_batch, clever_u_batch
+    """The batched CLEVER gives the reference's literal loop exactly: for each sample, for each
+    target class, a fresh pool and fresh batch draws from ONE generator advanced in the
+    reference's order (``model/metrics.py:284-302`` under ``tensorflow_generator.py:200-201``),
+    with the default generator and with the legacy ``np.random`` stream (RandomState)."""
+    from featurenet_amd.robust.metrics import clever_batch, clever_t_literal, clever_u_batch
 
     m = _Small()
     xs = torch.rand(7, 2, 3, 3, 1, generator=torch.Generator().manual_seed(2))
-    batched = clever_batch(m, xs, nb_batches=10, batch_size=5, radius=2.0, norm=2, pool_factor=3, clip=(0.0, 1.0),
-                           chunk_samples=3)
-    for i in range(len(xs)):
-        ref = _clever_scores_rng(m, xs[i], 10, 5, 2.0, 2, None, 1.0, 3, (0.0, 1.0), np.random.default_rng(0))
-        assert batched[i].keys() == ref.keys()
-        for j in ref:
-            assert batched[i][j] == pytest.approx(ref[j], rel=1e-6, abs=1e-9)
+    preds = A.predict(m, xs).argmax(-1).tolist()
+    for mk in (lambda: np.random.default_rng(0), lambda: np.random.RandomState(5)):
+        batched = clever_batch(m, xs, nb_batches=10, batch_size=5, radius=2.0, norm=2, pool_factor=3,
+                               clip=(0.0, 1.0), rng=mk(), chunk_points=30)      # 2 problems per chunk
+        rng = mk()
+        for i in range(len(xs)):
+            tg = [j for j in range(3) if j != preds[i]]
+            assert sorted(batched[i]) == tg
+            for j in tg:
+                ref = clever_t_literal(m, xs[i], j, 10, 5, 2.0, 2, 1.0, 3, (0.0, 1.0), rng)
+                assert batched[i][j] == pytest.approx(ref, rel=1e-5, abs=1e-7)
     u = clever_u_batch(m, xs, 10, 5, 2.0, 2, pool_factor=3, clip=(0.0, 1.0))
-    assert u == pytest.approx([min(d.values()) for d in batched])
+    again = clever_batch(m, xs, 10, 5, 2.0, 2, pool_factor=3, clip=(0.0, 1.0))
+    assert u == pytest.approx([min(d.values()) for d in again])
+
+
+class _CountingRng:
+    """A generator wrapper that records the pool draws (their first values)."""
+
+    def __init__(self, seed):
+        self.g, self.pools, self.choices = np.random.default_rng(seed), [], 0
+
+    def standard_normal(self, shape):
+        a = self.g.standard_normal(shape)
+        self.pools.append(a[0, 0])
+        return a
+
+    def choice(self, n, k):
+        self.choices += 1
+        return self.g.choice(n, k)
+
+
+def test_clever_pools_are_distinct_per_sample_and_target():
+    """Every (sample, target) problem draws its own pool and its own nb_batches index batches
+    (round 4 shared one seed-0 pool and one draw table across all problems)."""
+    from featurenet_amd.robust.metrics import clever_batch
+
+    m = _Small()
+    xs = torch.rand(4, 2, 3, 3, 1, generator=torch.Generator().manual_seed(3))
+    rng = _CountingRng(1)
+    out = clever_batch(m, xs, nb_batches=10, batch_size=5, radius=2.0, norm=2, pool_factor=3, rng=rng)
+    q = sum(len(d) for d in out)
+    assert q == 4 * 2
+    assert len(rng.pools) == q and len(set(rng.pools)) == q
+    assert rng.choices == q * 10
 
 
 def test_attacks_take_no_parameter_gradients():
