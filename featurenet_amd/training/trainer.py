@@ -419,9 +419,23 @@ class Trainer:
             rng = capture_rng(gens)
             if self.world > 1:
                 rng = _gather_rank_rng(rng, self.world)   # (a collective: every rank calls save)
-        if self.world > 1 and self.rank != 0:          # one writer: rank 0 holds every rank's state
-            return Path(path)
-        return save_checkpoint(path, self.model, meta, self.opt if include_optimizer else None, rng=rng)
+        if self.world <= 1:
+            return save_checkpoint(path, self.model, meta, self.opt if include_optimizer else None, rng=rng)
+        # one writer (rank 0 holds every rank's generator state), then the outcome goes to every
+        # rank: a failed write raises everywhere, and no rank returns before the file is complete
+        # (ranks read it back through a shared filesystem -- resume() / api.load on other nodes
+        # need the path on storage they all see)
+        err, out = None, Path(path)
+        if self.rank == 0:
+            try:
+                out = save_checkpoint(path, self.model, meta, self.opt if include_optimizer else None, rng=rng)
+            except Exception as e:  # noqa: BLE001 - re-raised on every rank below
+                err = f"{type(e).__name__}: {e}"
+        flag = [err]
+        dist.broadcast_object_list(flag, src=0)
+        if flag[0] is not None:
+            raise RuntimeError(f"checkpoint write failed on rank 0: {flag[0]}")
+        return out
 
     def resume(self, path) -> int:
         """Load weights, optimizer state, history and random-generator states written by

@@ -194,3 +194,32 @@ def test_resume_world2_restores_each_ranks_generators(tmp_path):
         b = torch.load(tmp_path / f"r{r}_1.pt", weights_only=True)
         assert a["loss"] == b["loss"], (a["loss"], b["loss"])
         assert torch.equal(a["p"], b["p"])
+
+
+def _save_fail_worker(rank, tmp):
+    dist.init_process_group("gloo", init_method=f"file://{tmp}/rdzv_save", rank=rank, world_size=2)
+    try:
+        torch.set_num_threads(1)
+        from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+        from featurenet_amd.training.trainer import Trainer
+
+        torch.manual_seed(0)
+        tr = Trainer(FeatureNet3D(FeatureNet3DConfig.tiny()), device="cpu", precise_bn=0)
+        p = tr.save(f"{tmp}/ok.fnk")                     # every rank returns after the file exists
+        assert os.path.exists(p) and os.path.getsize(p) > 0
+        try:
+            tr.save(f"{tmp}/ok.fnk/x.fnk")                # under a regular file: rank 0 fails ...
+            raise AssertionError("save into a missing directory returned")
+        except RuntimeError as e:                        # ... and every rank raises
+            assert "rank 0" in str(e)
+        with open(f"{tmp}/raised{rank}", "w") as f:
+            f.write("1")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_save_world2_reports_rank0_failure_on_every_rank(tmp_path):
+    """Advisor r4: with one writer, the other ranks must neither return before the checkpoint
+    exists nor miss a failed write -- rank 0's outcome is broadcast."""
+    mp.start_processes(_save_fail_worker, args=(str(tmp_path),), nprocs=2, start_method="spawn")
+    assert (tmp_path / "raised0").exists() and (tmp_path / "raised1").exists()
