@@ -32,7 +32,9 @@ int fn_pw_xent_blocks(long long);
 int fn_pw_fwd_xent(const void*, const void*, const float*, void*, long long, int, int, const float*, const float*, int,
                    const long long*, float*, float, float, hipStream_t);
 int fn_pw_fwd_blocks(long long, int, int);
-int fn_pw_wgrad(const void*, const void*, float*, long long, int, int, hipStream_t, const float*, const float*, int);
+int fn_pw_wgrad(const void*, const void*, float*, long long, int, int, hipStream_t, const float*, const float*, int,
+                float*);
+int fn_pw_wgrad_blocks(long long, int, int);
 int fn_conv_halo_wgrad_yblocks(const int*, int);
 int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
                     int, int, hipStream_t);
@@ -40,8 +42,9 @@ int fn_quant_fp8(const void*, void*, long long, float, hipStream_t);
 int fn_s2d_tap_f8(const void*, void*, int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, hipStream_t);
 int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
-int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t);
-int fn_conv_halo_wgrad(const void*, const void*, float*, const int*, int, int, int*, hipStream_t);
+int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t, float*);
+int fn_conv_halo_wgrad(const void*, const void*, float*, float*, const int*, int, int, hipStream_t);
+int fn_conv_halo_wgrad_gx(const int*, int);
 int fn_s2d_pack(const void*, void*, const int*, int, hipStream_t);
 int fn_dense_splits(int, int, int);
 int fn_ew_binary(const void*, const void*, void*, long long, int, hipStream_t);
@@ -57,7 +60,8 @@ int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
-                   hipStream_t, int, int, const void*, int, float*, int);
+                   hipStream_t, int, int, const void*, int, float*, int, float*);
+long long fn_igemm_wgrad_part(int, int, int, int, int, int, int);
 int fn_colstats(const void*, const void*, const float*, const float*, const float*, const float*, float*, long long,
                 int, int, int, int, hipStream_t);
 int fn_bn_finalize(const float*, int, int, double, const float*, const float*, float*, float*, float, float, float*,
@@ -98,13 +102,13 @@ int fn_scale_unless_one(void*, int, const float*, long long, hipStream_t);
 int fn_copy2(void*, const void*, long long, void*, const void*, long long, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
-                 const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float);
+                 const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float, void*);
 int fn_conv_tile_workers(const int*, int, int);
 int fn_conv_tile32(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                    const int*, int, int, int, int*, hipStream_t, float, const void*, const float*);
 int fn_conv_tile32_supported(int, int);
 int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
-                    float, const int*, int, int, int, int, int*, hipStream_t);
+                    float, const int*, int, int, int, int, int*, hipStream_t, const void*, void*);
 int fn_conv_tile_f8_supported(int, int, int);
 int fn_conv_wtile(const void*, const void*, float*, float*, const void*, const void*, const void*, const int*, int, int,
                   int*, hipStream_t);
@@ -216,21 +220,31 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("src"), py::arg("wt"), py::arg("bias"), py::arg("out"), py::arg("stats"), py::arg("toffs"),
      py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("sched"), py::arg("st"),
      py::arg("ext") = std::vector<long long>());
-  m.def("conv_halo_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t dw, std::vector<int> geom, int cout,
-                              int grid_x, uintptr_t sched, uintptr_t st, std::vector<long long> ext) {
+  // part: fp32 scratch of conv_halo_wgrad_gx(geom, grid_x) x cout x taps x C (the per-workgroup
+  // partial weight gradients, added into dw in a fixed order); ext = {dy, src, dw, part}
+  m.def("conv_halo_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t dw, uintptr_t part, std::vector<int> geom,
+                              int cout, int grid_x, uintptr_t st, std::vector<long long> ext) {
     need(geom, 17, "conv_halo_wgrad");
     check_halo(geom, ext, cout, true, "conv_halo_wgrad");
-    chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), geom.data(), cout, grid_x,
-                           P<int*>(sched), S(st)),
+    const int gx = fn_conv_halo_wgrad_gx(geom.data(), grid_x);
+    fits(ext, 3, prod({gx, cout, geom[8] * geom[9] * geom[10], geom[4]}), "conv_halo_wgrad", "part");
+    chk(fn_conv_halo_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), P<float*>(part), geom.data(), cout,
+                           grid_x, S(st)),
         "conv_halo_wgrad");
-  }, py::arg("dy"), py::arg("src"), py::arg("dw"), py::arg("geom"), py::arg("cout"), py::arg("grid_x"),
-     py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>());
+  }, py::arg("dy"), py::arg("src"), py::arg("dw"), py::arg("part"), py::arg("geom"), py::arg("cout"),
+     py::arg("grid_x"), py::arg("st"), py::arg("ext") = std::vector<long long>());
+  m.def("conv_halo_wgrad_gx", [](std::vector<int> geom, int grid_x) {
+    need(geom, 17, "conv_halo_wgrad_gx");
+    return fn_conv_halo_wgrad_gx(geom.data(), grid_x);
+  });
   m.def("conv_tile", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                         uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
                         uintptr_t sched, uintptr_t st, std::vector<long long> ext, uintptr_t bny, uintptr_t bnp,
-                        float oscale) {
+                        float oscale, uintptr_t osc, long long osc_n) {
     need(geom, 31, "conv_tile");
     check_tile(geom, ext, ncol, MT, "conv_tile");
+    // osc: block scales of an e4m3 output, one dword per output position
+    if (osc && osc_n < view_extent(geom, 1)) throw std::runtime_error("conv_tile: osc smaller than the output");
     if (bny && bnp) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
       fits(ext, 5, view_extent(geom, ncol), "conv_tile", "bny");
       fits(ext, 6, 4LL * ncol, "conv_tile", "bnp");
@@ -239,12 +253,13 @@ PYBIND11_MODULE(_C, m) {
     }
     chk(fn_conv_tile(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
                      P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
-                     act, MT, NT, P<int*>(sched), S(st), P<const void*>(bny), P<const float*>(bnp), oscale),
+                     act, MT, NT, P<int*>(sched), S(st), P<const void*>(bny), P<const float*>(bnp), oscale,
+                     P<void*>(osc)),
         "conv_tile");
   }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("bny") = 0,
-     py::arg("bnp") = 0, py::arg("oscale") = 0.f);
+     py::arg("bnp") = 0, py::arg("oscale") = 0.f, py::arg("osc") = 0, py::arg("osc_n") = 0);
   m.def("conv_tile32", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                           uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MB,
                           uintptr_t sched, uintptr_t st, std::vector<long long> ext, float oscale, uintptr_t bny,
@@ -265,8 +280,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_tile32_supported", &fn_conv_tile32_supported);
   m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
                            uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,
-                           int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext) {
+                           int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext,
+                           uintptr_t xsc, uintptr_t osc) {
     need(geom, 31, "conv_tile_f8");
+    // xsc / osc: block scales (a dword per input / output position): ext[5] / ext[6] their counts
+    if (xsc) fits(ext, 5, prod({geom[0], geom[1], geom[2], geom[3]}), "conv_tile_f8", "xsc");
+    if (osc) fits(ext, 6, view_extent(geom, 1), "conv_tile_f8", "osc");
     if (geom[4] <= 0 || ncol <= 0 || geom[17] <= 0 || geom[4] % geom[17])
       throw std::runtime_error("conv_tile_f8: bad slice");
     fits(ext, 0, prod({geom[0], geom[1], geom[2], geom[3], geom[4]}), "conv_tile_f8", "src");
@@ -277,11 +296,12 @@ PYBIND11_MODULE(_C, m) {
     fits(ext, 4, geom[19] + 6LL, "conv_tile_f8", "ktab");
     chk(fn_conv_tile_f8(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
                         P<const void*>(zp), P<const float*>(scale), P<const float*>(bias), P<void*>(out), oscale,
-                        geom.data(), ncol, relu, MT, NT, P<int*>(sched), S(st)),
+                        geom.data(), ncol, relu, MT, NT, P<int*>(sched), S(st), P<const void*>(xsc), P<void*>(osc)),
         "conv_tile_f8");
   }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("scale"),
      py::arg("bias"), py::arg("out"), py::arg("oscale"), py::arg("geom"), py::arg("ncol"), py::arg("relu"),
-     py::arg("MT"), py::arg("NT"), py::arg("st"), py::arg("sched"), py::arg("ext") = std::vector<long long>());
+     py::arg("MT"), py::arg("NT"), py::arg("st"), py::arg("sched"), py::arg("ext") = std::vector<long long>(),
+     py::arg("xsc") = 0, py::arg("osc") = 0);
   m.def("conv_tile_f8_supported", &fn_conv_tile_f8_supported);
   m.def("conv_wtile", [](uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t part, uintptr_t rowtab, uintptr_t postab,
                          uintptr_t zp, std::vector<int> geom, int nacc, int workers, uintptr_t sched, uintptr_t st,
@@ -395,6 +415,7 @@ PYBIND11_MODULE(_C, m) {
     fits(ext, 1, (long long)M * K, "dense_wgrad", "x");
     fits(ext, 2, (long long)N * K, "dense_wgrad", "dw");
     if (slices > 1) fits(ext, 3, (long long)slices * ((long long)N * K + N), "dense_wgrad", "part");
+    if (ya) fits(ext, 4, (long long)M * N, "dense_wgrad", "ya");   // (the activation output dy is taken through)
     chk(fn_dense_wgrad(P<const void*>(g), P<const void*>(x), P<float*>(dw), P<float*>(db), M, N, K, P<float*>(part),
                        slices, S(st), P<const void*>(ya), act),
         "dense_wgrad");
@@ -445,9 +466,14 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 20, "dw_dgrad");
     chk(fn_dw_dgrad(P<const void*>(dy), P<const float*>(w), P<void*>(dx), geom.data(), S(st)), "dw_dgrad");
   });
-  m.def("dw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, std::vector<int> geom, int splits, uintptr_t st) {
+  // part: fp32 scratch [splits][C][taps] (the per-split partials, added into dw in a fixed order)
+  m.def("dw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, std::vector<int> geom, int splits, uintptr_t st,
+                       uintptr_t part, long long part_n) {
     need(geom, 20, "dw_wgrad");
-    chk(fn_dw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), geom.data(), splits, S(st)), "dw_wgrad");
+    if (part_n < prod({splits, geom[4], geom[8] * geom[9] * geom[10]}))
+      throw std::runtime_error("dw_wgrad: part scratch too small");
+    chk(fn_dw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), geom.data(), splits, S(st), P<float*>(part)),
+        "dw_wgrad");
   });
   m.def("conv_halo_wgrad_yblocks", [](std::vector<int> geom, int cout) {
     need(geom, 17, "conv_halo_wgrad_yblocks");
@@ -500,13 +526,16 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("dlog"), py::arg("M"), py::arg("K"), py::arg("N"),
      py::arg("psc"), py::arg("psh"), py::arg("pact"), py::arg("labels"), py::arg("xpart"), py::arg("xscale"),
      py::arg("smoothing"), py::arg("st"), py::arg("ext"));
+  // part: fp32 scratch of pw_wgrad_blocks(M, K, N) x N x K floats (per-workgroup partials)
   m.def("pw_wgrad", [](uintptr_t dy, uintptr_t x, uintptr_t dw, long long M, int K, int N, uintptr_t st,
-                       uintptr_t psc, uintptr_t psh, int pact) {
+                       uintptr_t psc, uintptr_t psh, int pact, uintptr_t part, long long part_n) {
+    if (part_n < (long long)fn_pw_wgrad_blocks(M, K, N) * N * K) throw std::runtime_error("pw_wgrad: part scratch too small");
     chk(fn_pw_wgrad(P<const void*>(dy), P<const void*>(x), P<float*>(dw), M, K, N, S(st), P<const float*>(psc),
-                    P<const float*>(psh), pact),
+                    P<const float*>(psh), pact, P<float*>(part)),
         "pw_wgrad");
   }, py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("M"), py::arg("K"), py::arg("N"), py::arg("st"),
-     py::arg("psc") = 0, py::arg("psh") = 0, py::arg("pact") = 0);
+     py::arg("psc") = 0, py::arg("psh") = 0, py::arg("pact") = 0, py::arg("part") = 0, py::arg("part_n") = 0);
+  m.def("pw_wgrad_blocks", &fn_pw_wgrad_blocks);
   m.def("conv_halo_workers", [](std::vector<int> geom, int ncol) {
     need(geom, 17, "conv_halo_workers");
     return fn_conv_halo_workers(geom.data(), ncol);
@@ -515,16 +544,22 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 17, "conv_halo_lds");
     return fn_conv_halo_lds(geom.data(), ncol);
   });
-  m.def("igemm_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t part, uintptr_t tab, std::vector<int> geom,
+  // dw (and db) are accumulated into from the split partials in `scratch` (igemm_wgrad_part floats)
+  m.def("igemm_wgrad", [](uintptr_t dy, uintptr_t src, uintptr_t dw, uintptr_t tab, std::vector<int> geom,
                           long long M, int Cout, int K, int splits, int vec, uintptr_t st, int ccrop, int cpad,
-                          uintptr_t ya, int act, uintptr_t db, int kout) {
+                          uintptr_t ya, int act, uintptr_t db, int kout, uintptr_t scratch, long long scratch_n) {
     need(geom, 14, "igemm_wgrad");
-    chk(fn_igemm_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(part), P<const int*>(tab), geom.data(), M,
-                       Cout, K, splits, vec, S(st), ccrop, cpad, P<const void*>(ya), act, P<float*>(db), kout),
+    if (scratch_n < fn_igemm_wgrad_part(Cout, K, splits, ccrop, cpad, kout, db ? 1 : 0))
+      throw std::runtime_error("igemm_wgrad: partial scratch too small");
+    chk(fn_igemm_wgrad(P<const void*>(dy), P<const void*>(src), P<float*>(dw), P<const int*>(tab), geom.data(), M,
+                       Cout, K, splits, vec, S(st), ccrop, cpad, P<const void*>(ya), act, P<float*>(db), kout,
+                       P<float*>(scratch)),
         "igemm_wgrad");
-  }, py::arg("dy"), py::arg("src"), py::arg("part"), py::arg("tab"), py::arg("geom"), py::arg("M"), py::arg("Cout"),
+  }, py::arg("dy"), py::arg("src"), py::arg("dw"), py::arg("tab"), py::arg("geom"), py::arg("M"), py::arg("Cout"),
      py::arg("K"), py::arg("splits"), py::arg("vec"), py::arg("st"), py::arg("ccrop") = 0, py::arg("cpad") = 0,
-     py::arg("ya") = 0, py::arg("act") = 0, py::arg("db") = 0, py::arg("kout") = 0);
+     py::arg("ya") = 0, py::arg("act") = 0, py::arg("db") = 0, py::arg("kout") = 0, py::arg("scratch") = 0,
+     py::arg("scratch_n") = 0);
+  m.def("igemm_wgrad_part", &fn_igemm_wgrad_part);
   m.def("colstats", [](uintptr_t x, uintptr_t dz, uintptr_t scale, uintptr_t shift, uintptr_t mean, uintptr_t invstd,
                        uintptr_t part, long long M, int C, int act, int mode, int nb, uintptr_t st) {
     chk(fn_colstats(P<const void*>(x), P<const void*>(dz), P<const float*>(scale), P<const float*>(shift),

@@ -76,3 +76,9 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + idx;
 }
+
+// dst[e] (+)= sum over p = 0 .. W-1 of part[p * n + e], in a fixed order (conv_wtile.hip): the
+// deterministic replacement of per-workgroup float atomics -- kernels store their partial
+// weight gradients into rows of `part` and this pass adds the rows, so the result is bitwise
+// the same run to run whatever the workgroup timing
+extern "C" int fn_part_reduce(const float* part, float* dst, long long n, int W, int accumulate, hipStream_t st);

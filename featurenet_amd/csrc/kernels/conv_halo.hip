@@ -137,7 +137,8 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   // resident workgroups simply take more of them.  The last workgroup to finish
   // (sched[0] counts finished ones) resets the counters for the next launch.
   // chunk < 0: static partition instead (one contiguous run of -chunk tiles per
-  // workgroup, XCD-aware order) -- kept for A/B measurements
+  // workgroup, XCD-aware order) -- the host's choice whenever BN statistics are taken
+  // (per-workgroup partials over a fixed tile set: repeatable run to run)
   const bool dyn = chunk > 0;
   const int run = dyn ? chunk : -chunk;
   int nstatic = 0;
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
   };
   auto finish = [&]() {
     write_stats();
-    if (tid == 0) {
+    if (tid == 0 && dyn) {
       __threadfence();
       if (atomicAdd(sched, 1) == (int)(gridDim.x * gridDim.y) - 1) {
         for (int i = 0; i < (int)gridDim.y; ++i) atomicExch(sched + 1 + i, 0);
@@ -468,7 +469,9 @@ __global__ __launch_bounds__(H_NTHR, 4) void conv_halo_kernel(const bf16* __rest
 // staged in LDS once; both MFMA operands are read with ds_read_b64_tr_b16
 // (k = tile rows is the slow axis of both), the x operand at per-lane halo
 // positions row -> pos(row) + tapoff.  fp32 accumulators live across all the
-// workgroup's tiles and are folded into dW with one atomic add per element.
+// workgroup's tiles (a static set) and are stored into the workgroup's partial
+// dW row (part[blockIdx.x]); fn_part_reduce adds the rows in a fixed order, so
+// dW is bitwise repeatable (no float atomics).
 template <int MT>
 __device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
   typedef short s4 __attribute__((ext_vector_type(4)));
@@ -492,8 +495,7 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16* lo, const bf16* hi) {
 template <int MT, int CS, int DIV>
 __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __restrict__ dy,
                                                                  const bf16* __restrict__ src,
-                                                                 float* __restrict__ dw, HaloGeom g, int Cout,
-                                                                 int* __restrict__ sched, int nstatic_tiles) {
+                                                                 float* __restrict__ dw, HaloGeom g, int Cout) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   // 16x16 accumulator column blocks per (wave, co block); both slice widths give a
   // wave the same taps (CS = 8 packs two taps per block, so half the blocks)
@@ -523,25 +525,22 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
   const int G = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
   const int slice = blockIdx.z;
   const int tap0 = (blockIdx.y * 4 + wave) * TPW;          // uniform: tap offsets stay in SGPRs
-  // Hybrid schedule.  The first nstatic_tiles tiles are split statically: one
-  // contiguous run per workgroup x, so the grid.y/grid.z workgroups (tap groups,
-  // slices) of a tile walk it in near lockstep and share its dy / halo in L2.  The
-  // remaining tail is taken in single tiles from a per-(y, z) counter, so workgroups
-  // that start late (CU slots held by a concurrent RCCL kernel) do not stretch the
-  // kernel by a whole run.  The last workgroup out resets the counters.
-  const int per = nstatic_tiles / (int)gridDim.x;
-  int* cnt = sched + 1 + blockIdx.z * gridDim.y + blockIdx.y;
+  // Static schedule: one contiguous run of ntiles / gridDim.x tiles per workgroup x (the
+  // grid.y/grid.z workgroups -- tap groups, slices -- of a tile walk it in near lockstep and
+  // share its dy / halo in L2), then at most one of the remaining tiles (tile per * gx + x).
+  // The workgroup's tile set is fixed, so its partial dW is the same run to run.  (Through
+  // round 4 the remainder and the last 1/8 were taken from a counter: dW changed in the last
+  // bits with the schedule.)
+  const int per = ntiles / (int)gridDim.x;
   int ngrab = 0;
-  __shared__ int s_grab;
   auto grab = [&](int& end) -> int {
-    if (ngrab++ == 0 && per > 0) {
+    const int k = ngrab++;
+    if (k == 0 && per > 0) {
       end = (int)(blockIdx.x + 1) * per;
       return (int)blockIdx.x * per;
     }
-    if (tid == 0) s_grab = per * (int)gridDim.x + atomicAdd(cnt, 1);
-    lds_barrier();
-    const int t0 = __builtin_amdgcn_readfirstlane(s_grab);
-    lds_barrier();
+    if (k > 1 || (k == 1 && per == 0)) return -1;
+    const int t0 = per * (int)gridDim.x + (int)blockIdx.x;
     end = t0 + 1;
     return t0 < ntiles ? t0 : -1;
   };
@@ -708,16 +707,11 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
     tile = ntile;
     cend = ncend;
   }
-  if (tid == 0) {                  // the last workgroup out resets the tail counters
-    __threadfence();
-    const int total = (int)(gridDim.x * gridDim.y * gridDim.z);
-    if (atomicAdd(sched, 1) == total - 1) {
-      for (int i = 0; i < (int)(gridDim.y * gridDim.z); ++i) atomicExch(sched + 1 + i, 0);
-      atomicExch(sched, 0);
-    }
-  }
   // D[row=co][col=n]: lane holds co = mt*16 + (lane>>4)*4 + r, n = lane & 15
-  // (CS=16: n = input channel; CS=8: n = (tap of the pair) * 8 + channel)
+  // (CS=16: n = input channel; CS=8: n = (tap of the pair) * 8 + channel); plain stores into
+  // this workgroup's partial row (the (y, z) workgroups of one x write disjoint (tap, channel)
+  // columns of it, every element exactly once)
+  float* part = dw + (long long)blockIdx.x * Cout * T * g.C;
 #pragma unroll
   for (int i = 0; i < NACC; ++i) {
     const int t = CS == 16 ? tap0 + i : tap0 + 2 * i + ((lane & 15) >> 3);
@@ -728,8 +722,7 @@ __global__ __launch_bounds__(256, 2) void conv_halo_wgrad_kernel(const bf16* __r
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = mt * 16 + (lane >> 4) * 4 + r;
-          if (co < Cout)
-            atomicAdd(dw + ((long long)co * T + t) * g.C + slice * CS + ci, acc[i][mt][r]);
+          if (co < Cout) part[((long long)co * T + t) * g.C + slice * CS + ci] = acc[i][mt][r];
         }
     }
   }
@@ -823,7 +816,9 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   // ~4 chunks per workgroup: enough slack to absorb late or missing workgroups,
   // few enough that consecutive tiles (shared halo rows) stay on one workgroup
   int chunk = ntiles_all / (4 * workers) > 1 ? ntiles_all / (4 * workers) : 1;
-  if (g_halo_static) chunk = -((ntiles_all + workers - 1) / workers);
+  // BN statistics: one partial row per workgroup, so its tiles must not depend on the dynamic
+  // schedule (bitwise-repeatable statistics): the static partition
+  if (g_halo_static || stats) chunk = -((ntiles_all + workers - 1) / workers);
   dim3 grid((unsigned)workers, ncb);
   const bf16* s = (const bf16*)src;
   const bf16* w = (const bf16*)wt;
@@ -903,10 +898,18 @@ extern "C" int fn_conv_halo_wgrad_yblocks(const int* geom17, int Cout) {
   return (T + 4 * tpw - 1) / (4 * tpw);
 }
 
-// dw: fp32 [Cout][T][C], zero-initialised by the caller (atomics accumulate).
-// sched: int[1 + grid.y * grid.z] zeroed counters (left zero again, see fn_conv_halo)
-extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, const int* geom17, int Cout,
-                                  int grid_x, int* sched, hipStream_t st) {
+// effective grid.x of fn_conv_halo_wgrad (the partial rows `part` must hold)
+extern "C" int fn_conv_halo_wgrad_gx(const int* geom17, int grid_x) {
+  const HaloGeom g = parse_halo(geom17);
+  if (g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
+  const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) * ((g.OW + g.TW - 1) / g.TW);
+  return grid_x < ntiles ? (grid_x > 0 ? grid_x : 1) : ntiles;
+}
+
+// dw: fp32 [Cout][T][C], accumulated into (+=); part: fp32 scratch [fn_conv_halo_wgrad_gx][Cout][T][C]
+// (every element written by the kernel, then summed over the rows in a fixed order)
+extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, float* part, const int* geom17, int Cout,
+                                  int grid_x, hipStream_t st) {
   const HaloGeom g = parse_halo(geom17);
   const int CS = halo_cs(g.C);
   if (CS == 0 || g.TD * g.TH * g.TW > H_BM || g.TW < 1 || g.TW > g.OW || Cout > 64 || Cout % 8 != 0) return -2;
@@ -919,9 +922,7 @@ extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, co
   const int ntiles = g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) * ((g.OW + g.TW - 1) / g.TW);
   const int gx = grid_x < ntiles ? (grid_x > 0 ? grid_x : 1) : ntiles;
   dim3 grid((unsigned)gx, (unsigned)((T + 4 * TPW - 1) / (4 * TPW)), (unsigned)(g.C / CS));
-  if (!sched || grid.y * grid.z > 63) return -6;
-  // 7/8 of the tiles in static runs (whole runs per workgroup), the rest as a dynamic tail
-  const int nstatic = g_halo_static ? ntiles : ntiles / gx * 7 / 8 * gx;
+  if (!part) return -6;
   const bf16* d = (const bf16*)dy;
   const bf16* s = (const bf16*)src;
 #define WCASE1(M, C, D)                                                                                    \
@@ -933,8 +934,7 @@ extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, co
       if (e != hipSuccess) return (int)e;                                                                  \
       cfg = lds;                                                                                           \
     }                                                                                                      \
-    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M, C, D>), grid, dim3(256), lds, st, d, s, dw, g, Cout, sched, \
-                       nstatic);                                                                           \
+    hipLaunchKernelGGL((conv_halo_wgrad_kernel<M, C, D>), grid, dim3(256), lds, st, d, s, part, g, Cout);  \
   } while (0)
 #define WCASE(M, C) do { if (DIV == 2) WCASE1(M, C, 2); else WCASE1(M, C, 1); } while (0)
   if (CS == 16) {
@@ -945,7 +945,7 @@ extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, co
 #undef WCASE
 #undef WCASE1
   FN_CHECK_LAUNCH();
-  return 0;
+  return fn_part_reduce(part, dw, (long long)Cout * T * g.C, gx, 1, st);
 }
 
 // ---------------------------------------------------------------------------

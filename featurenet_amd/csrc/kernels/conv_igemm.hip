@@ -5,7 +5,7 @@
 //   dgrad: dx[m][ci] = sum_k' A'[m][k'] * WT[ci][k']  A' = "im2col" of dy with
 //          negated tap offsets (stride-1 transposed conv; stride-2 layers are
 //          handled by the caller through zero insertion of dy)
-//   wgrad: dW[co][k] = sum_m dy[m][co] * A[m][k]     (split over m, fp32 atomics)
+//   wgrad: dW[co][k] = sum_m dy[m][co] * A[m][k]     (split over m, fixed-order partial sums)
 //
 // Nothing is materialised: the gather is driven by a per-layer tap table
 // (built once on the host and cached) whose entries hold the element offset of
@@ -500,10 +500,12 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
   }
 
   // D[row=co][col=k]: lane holds rows (lane>>4)*4+r, col lane&15.
-  // Split-m partial sums are folded straight into the fp32 dW with no-return
-  // float atomics (S x Cout x Kdim x 4 B of atomic traffic, well under the
-  // ~1.3 TB/s chip-wide atomic rate for the split counts used).
-  if (dsum && co0 + tid < kout) atomicAdd(db + co0 + tid, dbs);
+  // Split-m partial sums are stored into this split's partial rows (dw / db point at the
+  // partial slabs [splits][kout][ldo] / [splits][kout]); fn_part_reduce adds the splits in a
+  // fixed order (bitwise repeatable; through round 4 these were float atomics into dW).
+  const long long ldo = ccrop > 0 ? (long long)(Kdim / cpad) * ccrop : Kdim;
+  dw += (long long)bz * kout * ldo;
+  if (dsum && co0 + tid < kout) db[(long long)bz * kout + co0 + tid] = dbs;
   // ccrop > 0: k = t*cpad + c lands at dw[co][t*ccrop + c] of the real weight, columns
   // c >= ccrop dropped -- the zero channels of a channel-padded input (cpad = its channels,
   // ccrop = the real ones) or the row padding of the packed-W layout (cpad = R, ccrop = KW*C):
@@ -520,11 +522,10 @@ __global__ __launch_bounds__(256, 2) void igemm_wgrad_kernel(
         kok = kok && c < ccrop;
         kdst = (long long)t * ccrop + c;
       }
-      const long long ldo = ccrop > 0 ? (long long)(Kdim / cpad) * ccrop : Kdim;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + mt * 16 + (lane >> 4) * 4 + r;
-        if (co < kout && kok) atomicAdd(dw + (long long)co * ldo + kdst, acc[mt][nt][r]);
+        if (co < kout && kok) dw[(long long)co * ldo + kdst] = acc[mt][nt][r];
       }
     }
 }
@@ -592,19 +593,32 @@ extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, 
 
 extern "C" int fn_igemm_fwd_mblocks(long long M) { return (int)((M + FWD_BM - 1) / FWD_BM); }
 
+// fp32 floats of the partial slab fn_igemm_wgrad needs: splits x kout x (columns of dw) (+ splits x
+// kout for the bias gradient)
+extern "C" long long fn_igemm_wgrad_part(int Cout, int Kdim, int splits, int ccrop, int cpad, int kout, int with_db) {
+  if (kout <= 0) kout = Cout;
+  const long long ldo = ccrop > 0 ? (long long)(Kdim / cpad) * ccrop : Kdim;
+  return (long long)splits * kout * (ldo + (with_db ? 1 : 0));
+}
+
 // ccrop > 0: dw is the real [Cout][Kdim / cpad][ccrop] weight gradient; column t*cpad + c of the
 // gather layout (c < ccrop) maps to t*ccrop + c (channel-padded inputs; the packed-W rows)
 // ya / act (optional): dy is the gradient of the activation output ya (the activation backward
-// is applied as dy is loaded); db (optional, zeroed): receives the bias gradient (column sums of
+// is applied as dy is loaded); db (optional): receives (+=) the bias gradient (column sums of
 // the activated dy).  kout (0 = Cout): only output channels co < kout are written (dy channel-
-// padded to Cout for 16-B loads, dW / db of the real kout channels)
+// padded to Cout for 16-B loads, dW / db of the real kout channels).  dw and db are accumulated
+// into (+=) from the split partials in `part` (fn_igemm_wgrad_part floats), in a fixed order.
 extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const int* tab, const int* geom14,
                               long long M, int Cout, int Kdim, int splits, int gm, hipStream_t st, int ccrop,
-                              int cpad, const void* ya, int act, float* db, int kout) {
+                              int cpad, const void* ya, int act, float* db, int kout, float* part) {
   if (kout <= 0) kout = Cout;
   if (kout > Cout) return -2;
   const GatherGeom g = parse_geom(geom14);
   if (ccrop > 0 && (cpad < ccrop || Kdim % cpad)) return -2;
+  if (!part || splits < 1) return -6;
+  const long long ldo = ccrop > 0 ? (long long)(Kdim / cpad) * ccrop : Kdim;
+  float* pdw = part;
+  float* pdb = db ? part + (long long)splits * kout * ldo : nullptr;
   const int BCO = Cout <= 16 ? 16 : (Cout <= 32 ? 32 : 64);
   const long long rps = ((M + splits - 1) / splits + WG_BR - 1) / WG_BR * WG_BR;
   const int gx = (Kdim + WG_BK - 1) / WG_BK, gy = (Cout + BCO - 1) / BCO;
@@ -614,8 +628,8 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const 
   const bf16* s = (const bf16*)src;
   const int4* t = (const int4*)tab;
 #define WG_CASE(B, V, VN) \
-  hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, dw, t, g, M, Cout, Kdim, rps, gx, gy, \
-                     ccrop, cpad, (const bf16*)ya, act, db, kout)
+  hipLaunchKernelGGL((igemm_wgrad_kernel<B, V, VN>), grid, dim3(256), 0, st, d, s, pdw, t, g, M, Cout, Kdim, rps, gx, gy, \
+                     ccrop, cpad, (const bf16*)ya, act, pdb, kout)
 #define WG_GM(GMV)                                                                        \
   do {                                                                                    \
     if (vecn) {                                                                           \
@@ -632,7 +646,9 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const 
 #undef WG_GM
 #undef WG_CASE
   FN_CHECK_LAUNCH();
-  return 0;
+  int rc = fn_part_reduce(pdw, dw, (long long)kout * ldo, splits, 1, st);
+  if (rc == 0 && db) rc = fn_part_reduce(pdb, db, kout, splits, 1, st);
+  return rc;
 }
 
 // ---------------------------------------------------------------------------

@@ -60,7 +60,12 @@
 //   the same way, so the k sum is complete), exact int32 accumulation, converted to float in
 //   the epilogue before the dequantisation -- the binary-voxel stem of the fp8 inference path
 //   (0/1 inputs are exact; per-channel int8 weights keep ~8 bits, where e4m3 kept 4).
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false>
+// BS (block-scaled fp8, OCP MX style): with F8 the e4m3 input carries one E8M0 scale per (position,
+//   32-channel block) -- xsc: a dword per position, byte j = block j -- that the loader LDS-DMAs with
+//   each job's halo and every MFMA takes as its B-operand scale (the halo is the B operand); with an
+//   e4m3 output (F8 fp8 output, or Q8O) the epilogue scales every (position, 32-column block) by its
+//   own power of two and writes the scale byte into osc (the same dword-per-position layout)
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false>
 __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
@@ -71,8 +76,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                                                                int act, int* __restrict__ sched,
                                                                long long* __restrict__ stamps,
                                                                const float* __restrict__ scale, float oscale,
-                                                               const unsigned char* __restrict__ gmask) {
+                                                               const unsigned char* __restrict__ gmask,
+                                                               const unsigned* __restrict__ xsc,
+                                                               unsigned char* __restrict__ osc) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  static_assert(!BS || F8 || Q8O, "block scales: fp8 operands or an e4m3 output");
   constexpr int PD = ct_pd(NT, F8);
   constexpr int ESZ = F8 ? 1 : 2;                // bytes per element of the source / weights
   constexpr int FRAG = F8 ? 32 : 16;             // bytes per lane of one MFMA operand fragment
@@ -117,6 +125,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // (the buffers hold the bytes in FRAGMENT order -- slot f = (wave * MT + mt) * 16 + lr -- so
   // the epilogue reads slot (wave * MT + mt) * 16 + lr: a per-lane base plus a constant per mt)
   const int mask_bytes = ct_mask_bytes(4 * MT * 16, Ncol, gmask != nullptr);
+  // BS (F8): two planes (by job parity) of the halo positions' scale dwords, after s_sb
+  const int scl_off = 2 * g.BUF + 64 + ct_red_bytes(NT) + (nks + PD + 2) * 16 + g.HPpad * 8 + NT * 16 * 8;
   // ... and after them each fragment slot's (output offset from the tile origin in positions,
   // packed td|th|tw; dummy rows: the origin) for the loader's mask DMA, built once per kernel
   int2* s_mrow = reinterpret_cast<int2*>(dsm + 2 * g.BUF + mask_off + 2 * mask_bytes);
@@ -147,9 +157,11 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // offset lb (toggled between the buffers per job), its output offset relative to the
   // tile origin (-1: dummy row) and its packed tile coordinates (edge-tile bounds)
   int lb[MT], roff[MT], rpk[MT];
+  int sofs[(F8 && BS) ? MT : 1];                 // BS: byte offset of the row's scale dword in a plane
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int2 rt = rowtab[((loader ? 0 : wave) * MT + mt) * 16 + lr];
+    if constexpr (F8 && BS) sofs[mt] = rt.x * 4;
     // this lane group's (first) plane
     if constexpr (F8) lb[mt] = rt.x * 16 + (CPP == 4 ? 2 * (lg & 1) : 0) * PLANE;
     else lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;
@@ -165,6 +177,27 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // and read the zero page outside.
   auto dma_job = [&](int tile, int slice, int bufoff) {
     ct_dma_job<CPP, ESZ>(g, src, zp, dsm, s_pos, tile, slice, bufoff, lane, tdn, thn, twn);
+  };
+  // BS: the scale dwords of the job's halo positions into scale plane `which` (64 positions per
+  // DMA row; positions outside the input read the zero page: scale 2^-127 on zero data)
+  auto dma_scl = [&](int tile, int which) {
+    if constexpr (F8 && BS) {
+      int t = __builtin_amdgcn_readfirstlane(tile);
+      const int tw_ = t % twn; t /= twn;
+      const int th_ = t % thn; t /= thn;
+      const int td_ = t % tdn;
+      const int n = t / tdn;
+      const int dlo = td_ * g.TD - g.pd, hlo = th_ * g.TH - g.ph, wlo = tw_ * g.TW - g.pw;
+      const unsigned dst0 = ct_lds_addr(dsm) + (unsigned)(scl_off + which * g.HPpad * 4);
+      const unsigned* base = xsc + (long long)n * g.ID * g.IH * g.IW;
+      for (int r = 0; r < (g.HPpad >> 6); ++r) {
+        const int e = s_pos[(r << 6) + lane].y;
+        const int gd = dlo + (e >> 16), gh = hlo + ((e >> 8) & 255), gw = wlo + (e & 255);
+        const bool ok = (unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH && (unsigned)gw < (unsigned)g.IW;
+        ct_glds4(ok ? (const void*)(base + ((long long)gd * g.IH + gh) * g.IW + gw) : (const void*)zp,
+                 dst0 + (unsigned)(r << 8));
+      }
+    }
   };
   // the mask bytes of `tile` into mask buffer mpar, with the halo of the tile's last job: one
   // dword per lane (Ncol / 32 per position), natural row order; rows past the tile or the
@@ -209,22 +242,36 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // The loader publishes job j+1 in slot par^1 right after barrier A(j) and lands its
   // halo before barrier A(j+1); every wave reads its job after barrier A.  The compute
   // waves never wait on anything else: the epilogue stores straight from registers.
+  // Tile schedule.  With BN statistics (stats != null) the partial sums of a workgroup must
+  // not depend on which tiles it happened to grab, or the statistics -- and everything
+  // downstream -- would change in the last bits run to run: the workgroup then walks a
+  // STATIC tile sequence (job k = tile k * G + slot, slots XCD-major so that the tiles running
+  // together on one XCD are neighbours sharing halo rows in its L2).  Without statistics
+  // every output element is written by exactly one tile whatever the order, and the tiles
+  // are handed out dynamically from a counter (the tail balances across late workgroups).
+  const bool stat_sched = stats != nullptr;
+  const int G = (int)gridDim.x;
+  const int slot = (G & 7) == 0 ? ((int)blockIdx.x & 7) * (G >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
+  auto next_tile = [&](int k) -> int {           // tile of this workgroup's job k (-1: none)
+    const int t = stat_sched ? k * G + slot : atomicAdd(sched + 1 + blockIdx.y, 1);
+    return t < ntiles ? t : -1;
+  };
   if (tid == 0) {
-    const int t0 = atomicAdd(sched + 1 + blockIdx.y, 1);
-    s_job[0] = t0 < ntiles ? t0 : -1;
+    s_job[0] = next_tile(0);
     s_job[1] = 0;
   }
   tile_lds_barrier();
 
   if (loader) {
     // ======================= loader wave =======================
-    int tile = __builtin_amdgcn_readfirstlane(s_job[0]), slice = 0, t_next = -1;
+    int tile = __builtin_amdgcn_readfirstlane(s_job[0]), slice = 0, t_next = -1, kjob = 1;
     if (tile >= 0) {
       dma_job(tile, 0, 0);
+      dma_scl(tile, 0);
       if (nslice == 1) dma_mask(tile, 0);
-      if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
+      if (lane == 0) t_next = next_tile(kjob);
+      ++kjob;
       t_next = __builtin_amdgcn_readfirstlane(t_next);
-      if (t_next >= ntiles) t_next = -1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int par = 0;
@@ -243,11 +290,12 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
         s_job[2 * (par ^ 1) + 1] = nslc;
       }
       if (!(DBG & 4) && ntile >= 0) dma_job(ntile, nslc, (par ^ 1) * g.BUF);
+      if (ntile >= 0) dma_scl(ntile, par ^ 1);
       if (ntile >= 0 && nslc == nslice - 1) dma_mask(ntile, par ^ 1);
       if (nslc == 0 && ntile >= 0) {
-        if (lane == 0) t_next = atomicAdd(sched + 1 + blockIdx.y, 1);
+        if (lane == 0) t_next = next_tile(kjob);
+        ++kjob;
         t_next = __builtin_amdgcn_readfirstlane(t_next);
-        if (t_next >= ntiles) t_next = -1;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lap(st_k);
@@ -269,6 +317,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     Frag fa[MT];                                 // rotating: fragment mt of k-step k+1 is read right
                                                  // after the NT MFMAs of (mt, k) consumed it
+    unsigned fs[(F8 && BS) ? MT : 1];            // BS: fragment mt's E8M0 scale (low byte), read with it
+    int scl_job = 0, ssh = 0;                    // BS: the job's scale plane, the lane's byte in a dword
     Frag fb[PD][NT];
     // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
     // ct0*16 + 4*NT*lg + 4nt + r: a lane ends with NV = 4*NT consecutive columns of one position
@@ -307,6 +357,12 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // keeps the halo reads interleaved with the MFMAs (with a wave-uniform offset it
     // hoisted a turn's reads into a double-buffered block)
     auto kofs = [&](int k) -> int { return *((const int*)(s_kt + k) + lg); };
+    // BS: the scale of fragment mt's rows at k-step offset ko (the dword of the row's tap position,
+    // its block byte shifted down)
+    auto read_s = [&](int mt, int ko) -> unsigned {
+      if constexpr (F8 && BS) return *(const unsigned*)(dsm + scl_job + sofs[mt] + (ko >> 2)) >> ssh;
+      else return 127u;
+    };
     // epilogue variant (wave-uniform); columns come in whole 8-column groups (Ncol % 8 == 0)
     // (fp8: bit 0 relu, bit 1 fp8 output)
     // (fp8: act bit CT_F8_POOL = the 2^3 max-pool epilogue, relu + bf16 output of the pooled grid)
@@ -341,6 +397,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       const int slice = __builtin_amdgcn_readfirstlane(s_job[2 * par + 1]);
       if (tile < 0) break;
       const int nslc = slice + 1 == nslice ? 0 : slice + 1;
+      if constexpr (F8 && BS) {
+        scl_job = scl_off + par * g.HPpad * 4;
+        ssh = 8 * (CPP == 4 ? 2 * slice + (lg & 1) : slice);   // 32-channel block of this lane group
+      }
       // ---- k-loop: MFMA + A reads + B loads, nothing else ----
       const unsigned char* wbase = reinterpret_cast<const unsigned char*>(wp) +
                                    ((size_t)slice * nks * g.nct + ct0) * FTILE + PD * wstep;
@@ -350,7 +410,10 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       {
         const int ko = kofs(0);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) fa[mt] = read_a(mt, ko);
+        for (int mt = 0; mt < MT; ++mt) {
+          fa[mt] = read_a(mt, ko);
+          if constexpr (F8 && BS) fs[mt] = read_s(mt, ko);
+        }
       }
       int ko_n = kofs(1);                        // offsets of the next k-step
       for (int ks = 0; ks < nks; ks += PD) {
@@ -372,13 +435,19 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                 c = __builtin_amdgcn_mfma_i32_16x16x64_i8((ct_i32x4){b8[4], b8[5], b8[6], b8[7]},
                                                          (ct_i32x4){a8[4], a8[5], a8[6], a8[7]}, c, 0, 0, 0);
                 acc[mt][nt] = __builtin_bit_cast(f32x4, c);
-              } else if constexpr (F8)   // e4m3 x e4m3 (formats 0, 0), E8M0 scales 127 = 1.0
+              } else if constexpr (F8 && BS)   // e4m3 x e4m3, weights unscaled (127 = 1.0; per-channel
+                acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(   // scale in the epilogue),
+                    fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0, 127, 0, (int)fs[mt]);  // halo block-scaled
+              else if constexpr (F8)   // e4m3 x e4m3 (formats 0, 0), E8M0 scales 127 = 1.0
                 acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[u][nt], fa[mt], acc[mt][nt], 0, 0,
                                                                                  0, 127, 0, 127);
               else
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0);
             }
-            if constexpr (!(DBG & 2)) fa[mt] = read_a(mt, ko);
+            if constexpr (!(DBG & 2)) {
+              fa[mt] = read_a(mt, ko);
+              if constexpr (F8 && BS) fs[mt] = read_s(mt, ko);
+            }
             if constexpr (!(DBG & 128)) __builtin_amdgcn_sched_barrier(0);   // (DBG 128: free scheduling
           }                                                                  //  within a k-step)
           // k-step ks+u+PD, or the next job's step u
@@ -469,6 +538,21 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                 }
               }
               if constexpr (Q8) {
+                float qs = oscale;               // BS: 2^-e of the (row, 32-column) block instead
+                if constexpr (BS) {
+                  float am = 0.f;
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) am = fmaxf(am, fmaxf(fabsf(bf16_lo(pw[q])), fabsf(bf16_hi(pw[q]))));
+                  am = fmaxf(am, __shfl_xor(am, 16, 64));
+                  am = fmaxf(am, __shfl_xor(am, 32, 64));
+                  const int e = ct_e8m0_exp(am);
+                  qs = ct_exp2_neg(e);
+                  if (ok && lg == 0) {
+                    const long long pos = (long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh +
+                                          w0 * g.osw + roff[mt];
+                    osc[pos * 4 + blockIdx.y] = (unsigned char)(e + 127);
+                  }
+                }
                 if (ok) {
                   unsigned wd[2];
 #pragma unroll
@@ -478,7 +562,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                     for (int j = 0; j < 4; ++j) {
                       const unsigned w = pw[2 * qq + (j >> 1)];
                       const float v = (j & 1) ? bf16_hi(w) : bf16_lo(w);
-                      e[j] = __builtin_amdgcn_fmed3f(v * oscale, RELU_OUT ? 0.f : -448.f, 448.f);
+                      e[j] = __builtin_amdgcn_fmed3f(v * qs, RELU_OUT ? 0.f : -448.f, 448.f);
                     }
                     int pk = __builtin_amdgcn_cvt_pk_fp8_f32(e[0], e[1], 0, false);
                     pk = __builtin_amdgcn_cvt_pk_fp8_f32(e[2], e[3], pk, true);
@@ -518,13 +602,16 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             bs8[0] = c.x; bs8[1] = c.y; bs8[2] = c.z; bs8[3] = c.w;
             bs8[4] = d.x; bs8[5] = d.y; bs8[6] = d.z; bs8[7] = d.w;
           }
-          if constexpr ((M & 2) != 0) {          // fp8 output: fold the requantisation scale into the
+          if constexpr ((M & 2) != 0 && !BS) {   // fp8 output: fold the requantisation scale into the
 #pragma unroll                                   // dequantisation (one FMA + one med3 per value)
             for (int j = 0; j < 8; ++j) {
               sc8[j] *= oscale;
               bs8[j] *= oscale;
             }
           }
+          // BS fp8 output: position index of the tile origin (the output view), for the scale bytes
+          const long long pbase = (long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh +
+                                  w0 * g.osw;
           // POOL: the pool row table puts the 8 members of one 2^3 window in one lane, member m
           // in fragment m (MT = 8): the lane's running max over the fragments is the pooled value
           float pm[POOL ? 8 : 1];
@@ -545,10 +632,23 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
               const float ae = acc[mt][j >> 2][j & 3];
               const float a = I8 ? (float)__builtin_bit_cast(int, ae) : ae;
               v[j] = a * sc8[j] + bs8[j];
-              if constexpr ((M & 2) != 0)        // (already x oscale) relu / saturate in one med3
+              if constexpr ((M & 2) != 0 && !BS)   // (already x oscale) relu / saturate in one med3
                 v[j] = __builtin_amdgcn_fmed3f(v[j], (M & 1) != 0 ? 0.f : -448.f, 448.f);
               else if constexpr ((M & 1) != 0 || POOL)
                 v[j] = fmaxf(v[j], 0.f);
+            }
+            if constexpr ((M & 2) != 0 && BS) {
+              // block scale of (row, the workgroup's 32 columns): the 4 lanes lr + 16 lg hold them
+              float am = 0.f;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v[j]));
+              am = fmaxf(am, __shfl_xor(am, 16, 64));
+              am = fmaxf(am, __shfl_xor(am, 32, 64));
+              const int e = ct_e8m0_exp(am);
+              const float inv = ct_exp2_neg(e);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = __builtin_amdgcn_fmed3f(v[j] * inv, -448.f, 448.f);
+              if (ok && lg == 0) osc[(pbase + roff[mt]) * 4 + blockIdx.y] = (unsigned char)(e + 127);
             }
             if constexpr (POOL) {
               if (mt == 0) pok = ok;             // (windows lie wholly inside or outside the output)
@@ -615,7 +715,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     }
     if (!F8 && RSACC && stats) {
       // the lane's running sums over the 16 lanes holding the same columns (DPP), into the wave's
-      // LDS row: a fixed summation order (deterministic statistics, run to run)
+      // LDS row.  The workgroup's tiles are a static sequence when statistics are on (see the
+      // tile schedule), so every partial -- and the finalize's fixed-order sum over the slab
+      // rows -- is the same run to run
 #pragma unroll
       for (int h = 0; h < NT / 2; ++h) {
 #pragma unroll
@@ -652,8 +754,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       d[6] = stamp() - st_0;
     }
   }
-  if (tid == 0) {                                // the last workgroup out resets the counters
-    __threadfence();
+  if (tid == 0 && !stat_sched) {                 // the last workgroup out resets the counters
+    __threadfence();                             // (static schedules never touch them)
     if (atomicAdd(sched, 1) == (int)(gridDim.x * gridDim.y) - 1) {
       for (int i = 0; i < (int)gridDim.y; ++i) atomicExch(sched + 1 + i, 0);
       atomicExch(sched, 0);
@@ -812,21 +914,23 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false>
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
-                       float oscale = 0.f, const void* gmask = nullptr) {
+                       float oscale = 0.f, const void* gmask = nullptr, const void* xsc = nullptr,
+                       void* osc = nullptr) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8>), grid, dim3(CT_NTHR), lds, st,
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS>), grid, dim3(CT_NTHR), lds, st,
                      (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
-                     stamps, scale, oscale, (const unsigned char*)gmask);
+                     stamps, scale, oscale, (const unsigned char*)gmask, (const unsigned*)xsc,
+                     (unsigned char*)osc);
   return 0;
 }
 
@@ -840,10 +944,12 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
   return 0;
 }
 
-static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, int Ncol = 0, bool mask = false) {
+static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, int Ncol = 0, bool mask = false,
+                             bool bs = false) {
   const int PD = ct_pd(NT, f8);
   return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
-         (f8 ? (size_t)NT * 16 * 8 : 0) + (size_t)ct_mask_lds(4 * MT * 16, Ncol, mask);
+         (f8 ? (size_t)NT * 16 * 8 : 0) + (size_t)ct_mask_lds(4 * MT * 16, Ncol, mask) +
+         (f8 && bs ? 2 * (size_t)g.HPpad * 4 : 0);    // (BS: the two scale planes)
 }
 
 // geom: halo geometry (17) + CS, HPpad, nks, nct, mHW, mHHW, BUF (see TileGeom).
@@ -855,9 +961,12 @@ static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false,
 // of the BN whose output this dgrad's conv consumed -- the epilogue's column sums are of
 // g = dx * mask (dx stored as is); stats required, act none.  (The raw-moment BN-backward statistics epilogue, bny + bnp,
 // is conv_tile32's, fn_conv_tile32.)
+// osc (oscale > 0 only): block-scaled e4m3 output -- one E8M0 byte per (position, 32-column block)
+// into the dword-per-position array osc (byte j = block j); oscale is then only the flag
 extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
-                            int NT, int* sched, hipStream_t st, const void* bny, const float* bnp, float oscale) {
+                            int NT, int* sched, hipStream_t st, const void* bny, const float* bnp, float oscale,
+                            void* osc) {
   const TileGeom g = parse_tile(geom);
   if (g.CS != 8 && g.CS != 16 && g.CS != 32 && g.CS != 64) return -2;
   const int CPP = g.CS / 8;
@@ -892,6 +1001,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   // oscale > 0: e4m3 output of y * oscale (no statistics; the 8-channel-slice instances: the
   // space-to-depth stem of the fp8 inference path)
   if (!(oscale >= 0.f) || (oscale > 0.f && (stats || NT != 2 || CPP != 1))) return -2;
+  if (osc && (oscale <= 0.f || Ncol > 128)) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
 #ifdef FN_EXPERIMENTS
@@ -929,9 +1039,13 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
 #endif  // FN_EXPERIMENTS
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
-    rc = oscale > 0.f ? launch_tile<M, N, C, 0, false, C == 1 && N == 2>(                                        \
-                            grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, \
-                            stats, g, Ncol, act, sched, nullptr, nullptr, oscale)                                   \
+    rc = oscale > 0.f ? (osc ? launch_tile<M, N, C, 0, false, C == 1 && N == 2, false, C == 1 && N == 2>(        \
+                                   grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp,  \
+                                   bias, out, stats, g, Ncol, act, sched, nullptr, nullptr, oscale, nullptr, nullptr, \
+                                   osc)                                                                           \
+                             : launch_tile<M, N, C, 0, false, C == 1 && N == 2>(                                  \
+                                   grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp,  \
+                                   bias, out, stats, g, Ncol, act, sched, nullptr, nullptr, oscale))              \
                       : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,                 \
                                              (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, nullptr,     \
                                              nullptr, 0.f, bny);
@@ -958,9 +1072,12 @@ extern "C" int fn_conv_tile_f8_supported(int MT, int NT, int CPP) {
   return 0;
 }
 
+// xsc (optional): block-scaled input -- one E8M0 byte per (input position, 32-channel block) in a
+// dword per position; scale then holds the weights' per-column dequantisation only.  osc (with
+// xsc, oscale > 0): block-scaled e4m3 output (the same layout; oscale is then only the flag).
 extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                                const float* scale, const float* bias, void* out, float oscale, const int* geom, int Ncol,
-                               int relu, int MT, int NT, int* sched, hipStream_t st) {
+                               int relu, int MT, int NT, int* sched, hipStream_t st, const void* xsc, void* osc) {
   const TileGeom g = parse_tile(geom);
   if (g.CS != 32 && g.CS != 64) return -2;
   const int CPP = g.CS / 16;
@@ -971,6 +1088,8 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   const bool pool = (relu & 2) != 0;
   const bool i8 = (relu & 4) != 0;
   if (i8 && (pool || CPP != 2 || MT != 8 || NT != 2)) return -2;
+  const bool bs = xsc != nullptr;
+  if ((bs && (i8 || g.C > 128)) || (osc && (!bs || oscale <= 0.f || Ncol > 128))) return -2;
   if (pool && (MT != 8 || oscale != 0.f || (g.TD | g.TH | g.TW | g.OD | g.OH | g.OW) & 1)) return -2;
   const int f8act = ((relu & 1) || pool ? ACT_RELU : ACT_NONE) | (pool ? CT_F8_POOL : 0);
   if (g.C % g.CS || g.TD * g.TH * g.TW > 64 * MT || g.TD < 1 || g.TH < 1 || g.TW < 1) return -3;
@@ -988,11 +1107,26 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
     if (hd != (unsigned long long)(p / (HH * HW)) || (((rem * g.mHW) >> 32) != rem / HW)) return -3;
   }
   if ((size_t)g.BUF < (size_t)g.HPpad * CPP * 16 || g.BUF % 1024) return -3;
-  const size_t lds = tile_lds_total(g, MT, NT, true);
+  const size_t lds = tile_lds_total(g, MT, NT, true, 0, false, bs);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
   if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
   if (Ncol % 8) return -2;
+  if (bs) {                                      // (block-scaled operands: the production instances only)
+#define CT_F8_BS(M, N, C)                                                                                          \
+    if (MT == M && NT == N && CPP == C)                                                                            \
+      rc = launch_tile<M, N, C, 0, true, false, false, true>(grid, lds, st, src, (const uint4*)wp,                  \
+                                                             (const int2*)rowtab, (const int4*)ktab, zp, bias, out, \
+                                                             nullptr, g, Ncol, f8act, sched, nullptr, scale, oscale, \
+                                                             nullptr, xsc, osc);
+    dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
+    int rc = -2;
+    CT_F8_INSTANCES(CT_F8_BS)
+#undef CT_F8_BS
+    if (rc) return rc;
+    FN_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   int rc = -2;
   // FN_F8_DBG (timing experiments only, wrong results): 1 no weight loads, 2 no halo reads,

@@ -50,6 +50,18 @@ __device__ __forceinline__ float ct_sum16(float x) {
   return x;
 }
 
+// OCP MX block scale of a block whose largest magnitude is amax: the E8M0 exponent e = ceil(log2(amax /
+// 448)) (the smallest power of two that maps the block into e4m3's range), clamped to [-127, 126]
+// (byte e + 127: never 0xFF, the E8M0 NaN; 2^-e stays a normal float); amax 0 gives -127
+__device__ __forceinline__ int ct_e8m0_exp(float amax) {
+  const unsigned b = __float_as_uint(amax * (1.f / 448.f));
+  int e = (int)((b >> 23) & 255u) - 127 + ((b & 0x7fffffu) != 0u ? 1 : 0);
+  if ((b & 0x7f800000u) == 0u) e = -127;          // zero / subnormal block
+  return e < -127 ? -127 : (e > 126 ? 126 : e);
+}
+// 2^-e for e in [-127, 126]
+__device__ __forceinline__ float ct_exp2_neg(int e) { return __uint_as_float((unsigned)(127 - e) << 23); }
+
 typedef int ct_i32x8 __attribute__((ext_vector_type(8)));
 typedef float ct_f32x2 __attribute__((ext_vector_type(2)));
 typedef short ct_s16x2 __attribute__((ext_vector_type(2)));

@@ -9,7 +9,8 @@
 //   B = x     (32 positions x 16 input channels) at tap offset t, NACC fragments
 // and a wave accumulates MT x NACC 16x16 blocks: all Cout rows x NACC taps of one
 // 16-channel input slice, over every tile its workgroup processes; the blocks are
-// folded into dW with fp32 atomics once, at the end.
+// stored into this workgroup's partial dW once, at the end (summed in a fixed order by
+// wtile_reduce_kernel).
 //
 // Structure (as conv_tile.hip): one workgroup per CU = 4 MFMA waves (one per SIMD) + 1
 // loader wave.  A job is one output tile; its x halo (the slice's 16 channels, 32 B per
@@ -119,7 +120,6 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   const int tg = grp % g.ntg, slice = grp / g.ntg;
   const int per = (ntiles + 7) / 8;
   const int t_lo = xcd * per, t_hi = min(ntiles, t_lo + per);
-  int* cnt = sched + 1 + xcd * g.G + grp;
 
   // LDS: [buffer 0][buffer 1][s_job 64 B][rows int2 ROWS][positions int HPpad]
   //      [x offsets int HPpad][dy row offsets int ROWS]
@@ -152,12 +152,12 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   // compute waves -- after reading jobs j and j+1, before running job j -- DMA a quarter
   // each of job j+1's dy rows (one wave alone could not keep the LDS fed at this job
   // size; giving the compute waves part of the x halo as well measured slower).
-  auto grab = [&]() -> int {
-    const int t1 = t_lo + atomicAdd(cnt, 1);
-    return t1 < t_hi ? t1 : -1;
-  };
-  // NW = 8: static round-robin tiles (no atomic round trip on any wave's critical path):
-  // job j of worker wid of this (XCD, group) is tile t_lo + wid + j * nwk
+  // Static round-robin tiles for both forms: job j of worker wid of this (XCD, group) is tile
+  // t_lo + wid + j * nwk.  The workgroup's partial dW is then a sum over a fixed tile set in a
+  // fixed order, and wtile_reduce_kernel adds the partials in a fixed order: the weight
+  // gradient is bitwise the same run to run (no atomic round trip on any wave's critical path
+  // either).  (The 4-wave loader form took tiles from a per-(XCD, group) counter through round
+  // 4, which made its partials -- and dW -- depend on the dynamic schedule.)
   const int nwk = (int)(gridDim.x >> 3) / g.G, wid = lid / g.G;
   auto tile_of = [&](int j) -> int {
     const int t = t_lo + wid + j * nwk;
@@ -165,9 +165,8 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   };
   if constexpr (HAS_LOADER) {
     if (tid == 0) {
-      const int t0 = grab();
-      s_job[0] = t0;
-      s_job[1] = t0 >= 0 ? grab() : -1;
+      s_job[0] = tile_of(0);
+      s_job[1] = tile_of(1);
     }
   }
   tile_lds_barrier();
@@ -315,11 +314,10 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
       if (cur < 0) break;
       int t2 = -1;
       if (nxt >= 0) {
-        if (lane == 0) t2 = grab();              // job j+2 (its round trip overlaps the DMAs)
+        t2 = tile_of(j + 2);                     // job j+2
         if (!(dbg & 1)) dma_x(nxt, (par ^ 1) * g.BUF, 0, 1);   // (dbg 1: timing only, stale data)
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      t2 = __builtin_amdgcn_readfirstlane(t2);
       if (lane == 0) s_job[(j + 2) % 3] = t2;
       cur = nxt;
       nxt = t2;
@@ -486,13 +484,6 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
       }
     }
   }
-  if (tid == 0) {                                // the last workgroup out resets the counters
-    __threadfence();
-    if (atomicAdd(sched, 1) == (int)gridDim.x - 1) {
-      for (int i = 0; i < 8 * g.G; ++i) atomicExch(sched + 1 + i, 0);
-      atomicExch(sched, 0);
-    }
-  }
 }
 
 // dw[e] (+)= sum over the partials p = 0 .. W-1 of part[p][e], in a fixed order: each of the
@@ -540,6 +531,15 @@ __global__ __launch_bounds__(256) void wtile_reduce_kernel(const float* __restri
       for (long long j = i; j < n; ++j) dw[j] = t[j - i];
     }
   }
+}
+
+extern "C" int fn_part_reduce(const float* part, float* dst, long long n, int W, int accumulate, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (!part || !dst || W < 1) return -6;
+  hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, dst, n, W,
+                     accumulate);
+  FN_CHECK_LAUNCH();
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -641,8 +641,5 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
 #undef WT_CASE
   FN_CHECK_LAUNCH();
   const long long n = sp ? 64LL * g.K * g.C : (long long)g.K * T * g.C;
-  hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, dw, n,
-                     8 * workers * (ks2 ? 2 : 1), 1);
-  FN_CHECK_LAUNCH();
-  return 0;
+  return fn_part_reduce(part, dw, n, 8 * workers * (ks2 ? 2 : 1), 1, st);
 }

@@ -6,7 +6,7 @@
 // with clamped-address loads, and fuses bias + activation.
 //   fwd  : y[m][c]  = act(b[c] + sum_tap x[pos(m)+tap][c] * w[c][tap])
 //   dgrad: dx[p][c] = sum_tap sum_{o: o*s - pad + tap*dil = p} dy[o][c] * w[c][tap]
-//   wgrad: dw[c][tap] = sum_m dy[m][c] * x[pos(m)+tap][c]  (block-reduced, 1 atomic / WG)
+//   wgrad: dw[c][tap] = sum_m dy[m][c] * x[pos(m)+tap][c]  (block-reduced, per-split partials)
 #include "common.h"
 
 struct DwGeom {
@@ -164,7 +164,8 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const bf16* __restrict__ 
   __syncthreads();
   if (threadIdx.x < VW) {
     const int j = threadIdx.x;
-    atomicAdd(dw + (long long)(c0 + j) * T + t, red[j][0] + red[j][1] + red[j][2] + red[j][3]);
+    // this split's partial row (fn_part_reduce adds the splits in a fixed order)
+    dw[(long long)blockIdx.z * g.C * T + (long long)(c0 + j) * T + t] = red[j][0] + red[j][1] + red[j][2] + red[j][3];
   }
 }
 
@@ -218,15 +219,17 @@ extern "C" int fn_dw_dgrad(const void* dy, const float* w, void* dx, const int* 
   return 0;
 }
 
-// dw: fp32 [C][taps], zero-initialised by the caller.
-extern "C" int fn_dw_wgrad(const void* dy, const void* x, float* dw, const int* geom20, int splits, hipStream_t st) {
+// dw: fp32 [C][taps], accumulated into (+=); part: fp32 scratch [splits][C][taps]
+extern "C" int fn_dw_wgrad(const void* dy, const void* x, float* dw, const int* geom20, int splits, hipStream_t st,
+                           float* part) {
   const DwGeom g = parse_dw(geom20);
+  if (!part || splits < 1) return -6;
   const bool v8 = g.C % 8 == 0;
   const long long M = (long long)g.N * g.OD * g.OH * g.OW;
   const long long per = (M + splits - 1) / splits;
   const dim3 grid((unsigned)(g.KD * g.KH * g.KW), (unsigned)(v8 ? g.C / 8 : g.C), (unsigned)splits);
-  if (v8) hipLaunchKernelGGL((dw_wgrad_kernel<8>), grid, dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, dw, g, M, per);
-  else hipLaunchKernelGGL((dw_wgrad_kernel<1>), grid, dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, dw, g, M, per);
+  if (v8) hipLaunchKernelGGL((dw_wgrad_kernel<8>), grid, dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, part, g, M, per);
+  else hipLaunchKernelGGL((dw_wgrad_kernel<1>), grid, dim3(256), 0, st, (const bf16*)dy, (const bf16*)x, part, g, M, per);
   FN_CHECK_LAUNCH();
-  return 0;
+  return fn_part_reduce(part, dw, (long long)g.C * g.KD * g.KH * g.KW, splits, 1, st);
 }

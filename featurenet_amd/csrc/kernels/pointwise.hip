@@ -282,7 +282,9 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_fwd_kernel(const bf16* __restri
 
 // dW[N][K] += sum_rows dY[row][n] * X[row][k].  Both tiles are scattered into LDS
 // TRANSPOSED ([channel][row]) so the MFMA operands (k = rows) are contiguous
-// 8-row runs; per-workgroup fp32 accumulators, one atomic per element at the end.
+// 8-row runs; per-wave fp32 accumulators over a static (strided) tile set, added across the
+// waves in a fixed order and stored into the workgroup's partial row of `dw` ([gridDim.x][N][K]),
+// summed by fn_part_reduce in a fixed order (bitwise repeatable).
 template <int KP, int NP, int PRO = -1>
 __global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                              float* __restrict__ dw, long long M, int K, int N,
@@ -379,16 +381,24 @@ __global__ __launch_bounds__(PW_NTHR, 2) void pw_wgrad_kernel(const bf16* __rest
         for (int b = 0; b < NTK; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
     }
   }
-  // D[row = n][col = k]: lane holds n = a*16 + lg*4 + r, k = b*16 + lr
+  // D[row = n][col = k]: lane holds n = a*16 + lg*4 + r, k = b*16 + lr.  Every wave holds a partial
+  // of the WHOLE [N][K] block (its quarter of the rows): the four are added through LDS in wave
+  // order (4 x NP x KP fp32 fit in the tiles' LDS), then stored as the workgroup's partial row
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(pw_dsm);
 #pragma unroll
   for (int a = 0; a < NTN; ++a)
 #pragma unroll
     for (int b = 0; b < NTK; ++b)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = a * 16 + lg * 4 + r, k = b * 16 + lr;
-        if (n < N && k < K) atomicAdd(dw + (long long)n * K + k, acc[a][b][r]);
-      }
+      for (int r = 0; r < 4; ++r) red[(wave * NP + a * 16 + lg * 4 + r) * KP + b * 16 + lr] = acc[a][b][r];
+  __syncthreads();
+  for (int i = tid; i < NP * KP; i += PW_NTHR) {
+    const int n = i / KP, k = i % KP;
+    if (n < N && k < K)
+      dw[((long long)blockIdx.x * N + n) * K + k] =
+          ((red[i] + red[NP * KP + i]) + red[2 * NP * KP + i]) + red[3 * NP * KP + i];
+  }
 }
 
 static int g_pw_cus = 0;
@@ -513,12 +523,17 @@ extern "C" int fn_pw_fwd_xent(const void* x, const void* w, const float* bias, v
   return 0;
 }
 
-// dw: fp32 [N][K], accumulated into (zero it for a fresh gradient)
+// rows of the partial slab fn_pw_wgrad needs ([rows][N][K] fp32)
+extern "C" int fn_pw_wgrad_blocks(long long M, int K, int N) { return pw_grid(M, (K <= 32 && N <= 32) ? 3 : 2); }
+
+// dw: fp32 [N][K], accumulated into (zero it for a fresh gradient); part: fp32 scratch
+// [fn_pw_wgrad_blocks][N][K]
 extern "C" int fn_pw_wgrad(const void* dy, const void* x, float* dw, long long M, int K, int N, hipStream_t st,
-                           const float* psc, const float* psh, int pact) {
+                           const float* psc, const float* psh, int pact, float* part) {
   if (K < 1 || K > 64 || N < 1 || N > 64 || M < 8 || M % 8) return -2;
   if (!pw_pro_ok(psc, psh, K)) return -2;
-  const dim3 grid((unsigned)pw_grid(M, (K <= 32 && N <= 32) ? 3 : 2));
+  if (!part) return -6;
+  const dim3 grid((unsigned)fn_pw_wgrad_blocks(M, K, N));
 #define PWW(KP, NP)                                                                                          \
   do {                                                                                                     \
     const size_t lds = (size_t)(KP + NP) * (PW_BM + 8) * 2;                                                \
@@ -528,18 +543,18 @@ extern "C" int fn_pw_wgrad(const void* dy, const void* x, float* dw, long long M
       return -4;                                                                                           \
     if (!psc)                                                                                              \
       hipLaunchKernelGGL((pw_wgrad_kernel<KP, NP>), grid, dim3(PW_NTHR), lds, st, (const bf16*)dy,        \
-                         (const bf16*)x, dw, M, K, N, nullptr, nullptr);                                   \
+                         (const bf16*)x, part, M, K, N, nullptr, nullptr);                                 \
     else if (pact == ACT_RELU)                                                                             \
       hipLaunchKernelGGL((pw_wgrad_kernel<KP, NP, ACT_RELU>), grid, dim3(PW_NTHR), lds, st, (const bf16*)dy, \
-                         (const bf16*)x, dw, M, K, N, psc, psh);                                           \
+                         (const bf16*)x, part, M, K, N, psc, psh);                                         \
     else                                                                                                   \
       hipLaunchKernelGGL((pw_wgrad_kernel<KP, NP, ACT_NONE>), grid, dim3(PW_NTHR), lds, st, (const bf16*)dy, \
-                         (const bf16*)x, dw, M, K, N, psc, psh);                                           \
+                         (const bf16*)x, part, M, K, N, psc, psh);                                         \
   } while (0)
   if (psc && pact != ACT_NONE && pact != ACT_RELU) return -2;
   if (K <= 32) { if (N <= 32) PWW(32, 32); else PWW(32, 64); }
   else { if (N <= 32) PWW(64, 32); else PWW(64, 64); }
 #undef PWW
   FN_CHECK_LAUNCH();
-  return 0;
+  return fn_part_reduce(part, dw, (long long)N * K, (int)grid.x, 1, st);
 }

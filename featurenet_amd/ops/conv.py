@@ -13,8 +13,8 @@ GPU path:
   dgrad   -> ``conv_halo`` on dy with the flipped, transposed kernel (stride 1)
              or ``igemm_fwd`` in transposed-conv mode (negated tap table)
   wgrad   -> ``conv_halo_wgrad`` (stride 1, Cout <= 64: halo tiles, persistent
-             workgroups, fp32 atomics once per workgroup) or ``igemm_wgrad``
-             (split-m, fp32 atomics)
+             workgroups, per-workgroup partials summed in a fixed order) or ``igemm_wgrad``
+             (split-m partials, summed in a fixed order)
 ``FEATURENET_CONV_HALO=0`` disables the halo path (A/B checks).
 """
 from __future__ import annotations
@@ -335,6 +335,13 @@ def halo_wgrad_plan(spec: ConvSpec):
 _SCHED: dict = {}
 
 
+def part_scratch(n: int, device) -> torch.Tensor:
+    """fp32 scratch for the per-workgroup partial weight gradients of the wgrad kernels (every
+    element is written by the kernel, then the rows are added into dW in a fixed order by
+    ``fn_part_reduce``: bitwise-repeatable gradients, no float atomics)."""
+    return torch.empty(max(1, int(n)), dtype=torch.float32, device=device)
+
+
 def halo_sched(device, stream: int) -> torch.Tensor:
     """int32[64] tile-schedule counters of the halo kernel (one buffer per device and stream:
     kernels on one stream run in order, and every launch leaves the counters zero)."""
@@ -354,12 +361,15 @@ def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512, out=No
     geom = [spec.N, spec.D, spec.H, spec.W, spec.C, spec.OD, spec.OH, spec.OW, spec.KD, spec.KH, spec.KW,
             spec.pd, spec.ph, spec.pw, TD, TH, TW]
     cs = halo_cs(spec.C)
-    per_tile = int(_native.kernels().conv_halo_wgrad_yblocks(geom, spec.K)) * (spec.C // cs)
+    K = _native.kernels()
+    per_tile = int(K.conv_halo_wgrad_yblocks(geom, spec.K)) * (spec.C // cs)
     dw = out if out is not None else torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=x5.device)
     st = _native.stream(x5)
-    _native.kernels().conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), geom, spec.K,
-                                      max(1, target_wgs // per_tile), halo_sched(x5.device, st).data_ptr(), st,
-                                      [dy5.numel(), x5.numel(), dw.numel()])
+    gx = max(1, target_wgs // per_tile)
+    # per-workgroup partial weight gradients, added into dw in a fixed order (repeatable bits)
+    part = part_scratch(int(K.conv_halo_wgrad_gx(geom, gx)) * spec.K * spec.taps * spec.C, x5.device)
+    K.conv_halo_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), part.data_ptr(), geom, spec.K, gx, st,
+                      [dy5.numel(), x5.numel(), dw.numel(), part.numel()])
     return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
 
 
@@ -510,8 +520,9 @@ def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=N
     direct = (out is not None and gm != GM_PACKW and out.dtype == torch.float32 and out.is_contiguous()
               and out.numel() == spec.K * kd)
     dw = out.view(spec.K, kd) if direct else torch.zeros(spec.K, kd, dtype=torch.float32, device=x5.device)
+    part = part_scratch(int(K.igemm_wgrad_part(spec.K, kd, splits, 0, 0, 0, 0)), x5.device)
     K.igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), dw.data_ptr(), tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K,
-                  kd, splits, gm, _native.stream(x5))
+                  kd, splits, gm, _native.stream(x5), 0, 0, 0, 0, 0, 0, part.data_ptr(), part.numel())
     if direct:
         return out
     if gm == GM_PACKW:
@@ -572,9 +583,12 @@ def igemm_wgrad_cropped(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, c0:
             dy5, ya = native_act_bwd(dy5, ya, act), None
         dy5 = pad_channels(dy5, kp)
     db = _zeroed_grad(bias_param, spec.K, x5.device) if with_db else None
-    _native.kernels().igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), out.data_ptr(), tab.data_ptr(), _geom_fwd(spec),
-                                  spec.M, kp, kd, wgrad_splits(spec), gm, _native.stream(x5), ccrop, cpad,
-                                  _native.ptr(ya), act if ya is not None else 0, _native.ptr(db), spec.K)
+    K = _native.kernels()
+    splits = wgrad_splits(spec)
+    part = part_scratch(int(K.igemm_wgrad_part(kp, kd, splits, ccrop, cpad, spec.K, int(db is not None))), x5.device)
+    K.igemm_wgrad(dy5.data_ptr(), x5.data_ptr(), out.data_ptr(), tab.data_ptr(), _geom_fwd(spec), spec.M, kp, kd,
+                  splits, gm, _native.stream(x5), ccrop, cpad, _native.ptr(ya), act if ya is not None else 0,
+                  _native.ptr(db), spec.K, part.data_ptr(), part.numel())
     return (out, db) if with_db else out
 
 
@@ -754,8 +768,10 @@ def pw_wgrad(dy2: torch.Tensor, x2: torch.Tensor, pro=None, out=None) -> torch.T
     else:
         dw = torch.zeros(N, Kin, dtype=torch.float32, device=x2.device)
     psc, psh, pact = pro if pro is not None else (None, None, 0)
-    _native.kernels().pw_wgrad(dy2.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, Kin, N, _native.stream(x2),
-                               _native.ptr(psc), _native.ptr(psh), pact)
+    K = _native.kernels()
+    part = part_scratch(int(K.pw_wgrad_blocks(M, Kin, N)) * N * Kin, x2.device)
+    K.pw_wgrad(dy2.data_ptr(), x2.data_ptr(), dw.data_ptr(), M, Kin, N, _native.stream(x2), _native.ptr(psc),
+               _native.ptr(psh), pact, part.data_ptr(), part.numel())
     return dw
 
 
@@ -1032,7 +1048,9 @@ class DepthwiseFn(torch.autograd.Function):
             else:
                 dwf = torch.zeros(spec.C, spec.taps, dtype=torch.float32, device=x5.device)
             splits = int(max(1, min(256, spec.M // 2048)))
-            K.dw_wgrad(dy.data_ptr(), x5.data_ptr(), dwf.data_ptr(), _dw_geom(spec), splits, st)
+            part = part_scratch(splits * spec.C * spec.taps, x5.device)
+            K.dw_wgrad(dy.data_ptr(), x5.data_ptr(), dwf.data_ptr(), _dw_geom(spec), splits, st, part.data_ptr(),
+                       part.numel())
             dw = tgt if dwf.data_ptr() == (tgt.data_ptr() if tgt is not None else -1) else \
                 dwf.reshape(spec.C, spec.KD, spec.KH, spec.KW, 1)
         if ctx.has_b and ctx.needs_input_grad[2]:

@@ -118,8 +118,8 @@ class LinearFn(torch.autograd.Function):
                 S = int(Kn.dense_wgrad_slices(M, N, K))
                 part = torch.empty(S * (N * K + N), dtype=torch.float32, device=g.device) if S > 1 else None
                 Kn.dense_wgrad(g.data_ptr(), x2.data_ptr(), dw.data_ptr(), _native.ptr(db), M, N, K, st,
-                               [g.numel(), x2.numel(), dw.numel()] + ([part.numel()] if S > 1 else []),
-                               _native.ptr(part), S, yp, yact)
+                               [g.numel(), x2.numel(), dw.numel(), part.numel() if S > 1 else 0,
+                                ya.numel() if ya is not None else 0], _native.ptr(part), S, yp, yact)
             else:
                 dw = _wgrad_torch(g, x2)
         if want_b and db is None:

@@ -392,7 +392,7 @@ class SubpixelDecoderHeadXentFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, y, prm, hw, dlog)
         ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
         ctx.params = (beta, gamma)
-        hits = xpart[:, 1].sum().round().long()
+        hits = xpart[:, 1].double().sum().round().long()   # (fp64: > 2^24 voxels per batch)
         ctx.mark_non_differentiable(hits)
         return xpart[:, 0].sum() / M, hits
 
@@ -439,7 +439,7 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
         ctx.params = (beta, gamma)
         tot = part.sum(0)
-        hits = tot[1].round().long()
+        hits = part[:, 1].double().sum().round().long()    # (fp64: > 2^24 voxels per batch)
         ctx.mark_non_differentiable(hits)
         return tot[0] / M, hits
 

@@ -9,12 +9,21 @@ if ROOT not in sys.path:
 
 
 def _ensure_native_built():
-    """Build the in-tree native modules (gitignored) when a fresh checkout lacks them."""
+    """Build the in-tree native modules (gitignored) when a fresh checkout lacks them or a source
+    is newer than the built library (the object cache under build/ does not travel to a GPU box:
+    an up-to-date library there is used as it is, never rebuilt)."""
     try:
         from featurenet_amd import _build
 
-        _build.build_runtime()
-        _build.build_kernels()
+        def stale(lib: str, sub: str) -> bool:
+            so = _build.PKG / f"{lib}{_build.EXT}"
+            srcs = [p for p in (_build.PKG / "csrc" / sub).iterdir() if p.suffix in (".hip", ".cpp", ".h")]
+            return not so.exists() or any(p.stat().st_mtime > so.stat().st_mtime for p in srcs)
+
+        if stale("_rt", "runtime"):
+            _build.build_runtime()
+        if stale("_C", "kernels"):
+            _build.build_kernels()
     except Exception as e:  # a missing toolchain only skips the native tests
         print(f"[conftest] native build skipped: {e}")
 

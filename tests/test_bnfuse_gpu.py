@@ -150,17 +150,20 @@ def test_seg_head_bn_in_pointwise_matches_unfused(monkeypatch, S):
     lab = torch.randint(0, 25, (2, S, S, S), device=dev)
     res = []
     monkeypatch.setenv("FN_SUBPIXEL", "0")      # this pair isolates the BN-in-pointwise fusion
-    for fuse in ("0", "1"):                      # (the sub-pixel decoder: tests/test_subpixel_gpu.py)
+    for fuse in ("0", "0", "1"):                 # (the sub-pixel decoder: tests/test_subpixel_gpu.py)
         monkeypatch.setenv("FN_BN_PW_FUSE", fuse)
         model.zero_grad(set_to_none=True)
         out = model(x)
         softmax_xent(out, lab).backward()
         res.append((out.detach().float(), {n: p.grad.detach().float().clone() for n, p in model.named_parameters()}))
-    (o0, g0), (o1, g1) = res
-    assert (o0 - o1).abs().max().item() <= 2e-2 * o0.abs().max().item()
-    for n in g0:
-        err = (g0[n] - g1[n]).abs().max().item() / max(g0[n].abs().max().item(), 1e-6)
-        assert err < 2e-2, f"{n}: rel err {err:.2e}"
+    (o0, g0), (o0b, g0b), (o1, g1) = res
+    # the unfused path against itself: bitwise (deterministic kernels, tests/test_determinism_gpu.py)
+    assert torch.equal(o0, o0b) and all(torch.equal(g0[n], g0b[n]) for n in g0)
+    assert (o0 - o1).abs().max().item() <= 5e-3 * o0.abs().max().item()
+    errs = {n: (g0[n] - g1[n]).abs().max().item() / max(g0[n].abs().max().item(), 1e-6) for n in g0}
+    print({n: f"{e:.2e}" for n, e in errs.items()})
+    for n, err in errs.items():
+        assert err < 5e-3, f"{n}: rel err {err:.2e}"
 
 
 def test_forked_bn_output_falls_back(monkeypatch):

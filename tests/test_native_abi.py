@@ -43,7 +43,7 @@ class _FakeK:
         def f(*args):
             assert lo <= len(args) <= hi, f"{name}: called with {len(args)} args, binding takes {lo}..{hi}"
             self.calls.append(name)
-            if name.endswith(("_lds", "mblocks", "_workers", "_blocks", "_yblocks")):
+            if name.endswith(("_lds", "mblocks", "_workers", "_blocks", "_yblocks", "_gx", "_part")):
                 return 1
             return None
         return f
@@ -130,7 +130,7 @@ def test_halo_extent_check_rejects_undersized_tensors():
     with pytest.raises(RuntimeError, match="out has"):
         K.conv_halo(0, 0, 0, 0, 0, 0, geom, 32, 0, 0, 0, [src, wt, out // 2, 128])
     with pytest.raises(RuntimeError, match="dw has"):
-        K.conv_halo_wgrad(0, 0, 0, geom, 32, 1, 0, 0, [out, src, 32 * 125 * 32 - 1])
+        K.conv_halo_wgrad(0, 0, 0, 0, geom, 32, 1, 0, [out, src, 32 * 125 * 32 - 1, 32 * 125 * 32])
     bad = list(geom)
     bad[5] = 40                                           # output larger than the input allows
     with pytest.raises(RuntimeError, match="larger than"):
