@@ -39,6 +39,7 @@ int fn_conv_halo_wgrad_yblocks(const int*, int);
 int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*, float, const int*, const int*, int,
                     int, int, hipStream_t);
 int fn_quant_fp8(const void*, void*, long long, float, hipStream_t);
+int fn_quant_fp8_block(const void*, void*, void*, long long, int, hipStream_t);
 int fn_s2d_tap_f8(const void*, void*, int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, hipStream_t);
 int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
@@ -453,6 +454,15 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_s2d_tap_f8(P<const void*>(x), P<void*>(y), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], inv_scale, i8, S(st)),
         "s2d_tap_f8");
   });
+  // block-scaled e4m3 of a bf16 [M][C] tensor: y [M][C] bytes, sc a scale dword per row (ext = {x, y, sc})
+  m.def("quant_fp8_block", [](uintptr_t x, uintptr_t y, uintptr_t sc, long long M, int C, uintptr_t st,
+                              std::vector<long long> ext) {
+    fits(ext, 0, M * C, "quant_fp8_block", "x");
+    fits(ext, 1, M * C, "quant_fp8_block", "y");
+    fits(ext, 2, M, "quant_fp8_block", "sc");
+    chk(fn_quant_fp8_block(P<const void*>(x), P<void*>(y), P<void*>(sc), M, C, S(st)), "quant_fp8_block");
+  }, py::arg("x"), py::arg("y"), py::arg("sc"), py::arg("M"), py::arg("C"), py::arg("st"),
+     py::arg("ext") = std::vector<long long>());
   m.def("quant_fp8", [](uintptr_t x, uintptr_t y, long long n, float inv_scale, uintptr_t st) {
     chk(fn_quant_fp8(P<const void*>(x), P<void*>(y), n, inv_scale, S(st)), "quant_fp8");
   });

@@ -297,6 +297,55 @@ extern "C" int fn_quant_fp8(const void* x, void* y, long long n, float inv_scale
   return 0;
 }
 
+// x (bf16 [M][C], C % 32 == 0, C <= 128) -> OCP MX-style block-scaled e4m3: per (row, 32-channel
+// block) the E8M0 exponent e = ceil(log2(amax / 448)), y = e4m3(x * 2^-e), and byte j of the row's
+// scale dword = e_j + 127 (the layout the block-scaled fp8 conv kernels read).  One thread per
+// (row, block): 64 B in, 32 B + 1 scale byte out.
+__global__ void quant_fp8_block_kernel(const bf16* __restrict__ x, unsigned char* __restrict__ y,
+                                       unsigned char* __restrict__ sc, long long M, int C) {
+  const int nb = C >> 5;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * nb) return;
+  const long long row = i / nb;
+  const int b = (int)(i - row * nb);
+  const bf16* xs = x + row * C + 32 * b;
+  Pack8 p[4];
+  float am = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    p[q].u = *(const uint4*)(xs + 8 * q);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(bf2f(p[q].e[j])));
+  }
+  const unsigned bits = __float_as_uint(am * (1.f / 448.f));
+  int e = (int)((bits >> 23) & 255u) - 127 + ((bits & 0x7fffffu) != 0u ? 1 : 0);
+  if ((bits & 0x7f800000u) == 0u) e = -127;
+  e = e < -127 ? -127 : (e > 126 ? 126 : e);
+  const float inv = __uint_as_float((unsigned)(127 - e) << 23);
+  unsigned char* ys = y + row * C + 32 * b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lo |= (unsigned)f32_to_fp8(bf2f(p[q].e[j]) * inv) << (8 * j);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) hi |= (unsigned)f32_to_fp8(bf2f(p[q].e[4 + j]) * inv) << (8 * j);
+    *(uint2*)(ys + 8 * q) = make_uint2(lo, hi);
+  }
+  sc[row * 4 + b] = (unsigned char)(e + 127);
+}
+
+// sc: uint32 [M] (one scale dword per row; bytes past C/32 are left as they are)
+extern "C" int fn_quant_fp8_block(const void* x, void* y, void* sc, long long M, int C, hipStream_t st) {
+  if (C % 32 || C > 128 || M < 0) return -2;
+  const long long n = M * (C / 32);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(quant_fp8_block_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const bf16*)x,
+                     (unsigned char*)y, (unsigned char*)sc, M, C);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // fp8 stem input: space-to-depth (factor 2^3) of a 1-channel volume, with J consecutive
 // w-taps of the packed grid folded into the channels, quantised to e4m3.

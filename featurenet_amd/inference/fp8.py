@@ -4,8 +4,13 @@ Post-training quantisation, inference only:
 
 * BatchNorm is folded into the conv weights and bias (eval statistics);
 * weights are quantised per output channel to OCP e4m3 (amax / 448);
-* activations between layers are quantised per tensor with scales calibrated
-  from a bf16 forward pass (``amax / 448`` of each layer's post-ReLU output);
+* activations between layers are OCP MX-style block-scaled e4m3 (default, ``FN_F8_BLOCK=1``): every
+  (position, 32-channel block) carries its own E8M0 power-of-two scale, written by the producing
+  epilogue (``osc``) and applied inside ``v_mfma_scale_f32_16x16x128_f8f6f4`` by the consumer (its
+  loader LDS-DMAs the scale dwords with each halo) -- no calibration, and a position with small
+  activations keeps e4m3's full relative precision however large the tensor's maximum is;
+  ``FN_F8_BLOCK=0`` (or a shape without a block-scaled tile plan) quantises per tensor with scales
+  calibrated from a bf16 forward pass (``amax / 448`` of each layer's post-ReLU output);
 * conv2..conv4 run the fp8 variant of the big-tile kernel (``conv_tile.hip``,
   ``conv_tile_kernel<8, 2, CPP, 0, true>``: LDS-DMA'd e4m3 halo, weights streamed in
   MFMA-fragment order, ``v_mfma_scale_f32_16x16x128_f8f6f4``, dequantise + bias + ReLU
@@ -79,31 +84,46 @@ class Fp8Conv:
         self.wq_ktc = wq.reshape(K, T, Cin).view(torch.uint8).contiguous()   # [K][T][C] for the tile packing
         self._tile = {}
         self.scale = (in_scale * sw).float().contiguous()
+        self.wscale = sw.float().contiguous()          # (block-scaled inputs: the weights' dequantisation only)
         self.bias = b.float().contiguous()
         self.out_scale, self.relu = out_scale, relu
         self.K, self.kernel, self.conv = K, (KD, KH, KW), conv
         self.padding = padding if padding is not None else conv.padding
         self.w_dequant = wq.float() * sw.view(-1, 1, 1, 1, 1)     # for numerics tests
 
-    def tile_plan(self, spec, pool: bool = False):
+    def tile_plan(self, spec, pool: bool = False, block: bool = False):
         if os.environ.get("FN_F8_TILE", "1") == "0":
             return None
+        if block and (self.int8 or spec.C % 32 or spec.C > 128 or spec.K > 128):
+            return None
         return conv_tile.plan(spec.N, (spec.OD, spec.OH, spec.OW), (spec.KD, spec.KH, spec.KW), spec.C, spec.K,
-                              f8=True, pool=pool)
+                              f8=True, pool=pool, bs=block)
 
-    def pool_plan(self, shape5: tuple):
+    def pool_plan(self, shape5: tuple, block: bool = False):
         """The tile plan with the fused 2^3 max-pool epilogue for this input, or None."""
         if os.environ.get("FN_F8_POOL", "1") == "0" or self.out_scale is not None or not self.relu:
             return None
-        return self.tile_plan(ConvSpec.make(shape5, self.K, self.kernel, 1, self.padding), pool=True)
+        return self.tile_plan(ConvSpec.make(shape5, self.K, self.kernel, 1, self.padding), pool=True, block=block)
 
-    def __call__(self, xq: torch.Tensor, shape5: tuple, pool: bool = False) -> tuple[torch.Tensor, tuple]:
+    def __call__(self, xq, shape5: tuple, pool: bool = False) -> tuple:
         """(y, y's shape); ``pool``: y = maxpool2^3(relu(conv)) from the fused epilogue (the
-        caller checked :meth:`pool_plan`)."""
+        caller checked :meth:`pool_plan`).  Block-scaled mode: ``xq`` is ``(e4m3 bytes, scale
+        dwords)`` and so is y unless it is the bf16 output of the last layer (tile kernel only)."""
         spec = ConvSpec.make(shape5, self.K, self.kernel, 1, self.padding)
-        tp = self.tile_plan(spec, pool=pool)
+        block = isinstance(xq, tuple)
+        tp = self.tile_plan(spec, pool=pool, block=block)
         if pool:
             assert tp is not None and tp.pool
+        if block:
+            if tp is None:
+                raise RuntimeError(f"no block-scaled fp8 tile plan for {spec}")
+            wpk = self._tile.get(tp)
+            if wpk is None:
+                wpk = self._tile[tp] = conv_tile.pack_weights_f8(self.wq_ktc, tp)
+            out_block = self.out_scale is not None and not pool
+            y = conv_tile.conv_fwd_f8(xq[0], wpk, self.wscale, self.bias, spec, tp, self.relu, None, xsc=xq[1],
+                                      out_block=out_block)
+            return y, tuple((y[0] if out_block else y).shape)
         if tp is not None:
             wpk = self._tile.get(tp)
             if wpk is None:
@@ -134,6 +154,27 @@ def quantize_fp8_act(x: torch.Tensor, scale: float) -> torch.Tensor:
     y = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
     _native.kernels().quant_fp8(x.data_ptr(), y.data_ptr(), x.numel(), 1.0 / scale, _native.stream(x))
     return y
+
+
+def quantize_fp8_block(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """bf16 channels-last activation [..., C] (C % 32 == 0, C <= 128) -> OCP MX-style block-scaled
+    e4m3: (bytes [..., C], int32 scale dwords [...]: byte j = the E8M0 scale of channels 32j..)."""
+    x = x.to(torch.bfloat16).contiguous()
+    C = x.shape[-1]
+    M = x.numel() // C
+    y = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    sc = torch.zeros(x.shape[:-1], dtype=torch.int32, device=x.device)
+    _native.kernels().quant_fp8_block(x.data_ptr(), y.data_ptr(), sc.data_ptr(), M, C, _native.stream(x),
+                                      [x.numel(), y.numel(), sc.numel()])
+    return y, sc
+
+
+def dequantize_fp8_block(y: torch.Tensor, sc: torch.Tensor) -> torch.Tensor:
+    """fp32 values of a block-scaled e4m3 tensor (:func:`quantize_fp8_block` layout)."""
+    C = y.shape[-1]
+    v = y.view(torch.float8_e4m3fn).float().reshape(*y.shape[:-1], C // 32, 32)
+    e = ((sc.unsqueeze(-1) >> (8 * torch.arange(C // 32, device=sc.device))) & 255).float() - 127.0
+    return (v * torch.exp2(e).unsqueeze(-1)).reshape(y.shape)
 
 
 def stem_tap_plan(c1, in_shape5):
@@ -194,6 +235,7 @@ class Fp8FeatureNet3D:
         self.act_scales = act_scales
         self.in_scale = in_scale
         self._stem_w2 = {}
+        self._block_ok = {}
         self.stem = None
         self.stem_int8 = bool(stem_int8)
         if in_scale is not None:
@@ -217,12 +259,37 @@ class Fp8FeatureNet3D:
         h = linear_infer(f, self.fc_w[0], m.fc1.bias, m.fc1.act)
         return linear_infer(h, self.fc_w[1], m.fc2.bias, m.fc2.act, out_fp32=True)
 
+    def block_mode(self, in_shape5: tuple) -> bool:
+        """Block-scaled activations for this input: ``FN_F8_BLOCK`` on (default), the bf16 stem, and a
+        block-scaled tile plan for every fp8 layer (else the per-tensor path)."""
+        if os.environ.get("FN_F8_BLOCK", "1") == "0" or self.stem is not None:
+            return False
+        key = tuple(in_shape5)
+        ok = self._block_ok.get(key)
+        if ok is None:
+            c1 = self.model.convs[0]
+            shape = ConvSpec.make(key, c1.cout, c1.kernel, c1.stride, c1.padding).out_shape5
+            ok = True
+            for li, layer in enumerate(self.layers):
+                spec = ConvSpec.make(shape, layer.K, layer.kernel, 1, layer.padding)
+                last = li == len(self.layers) - 1
+                tp = (layer.pool_plan(shape, block=True) if last and self._pool_fusable() else None) or \
+                    layer.tile_plan(spec, block=True)
+                if tp is None:
+                    ok = False
+                    break
+                shape = spec.out_shape5 if not tp.pool else (spec.N, spec.OD // 2, spec.OH // 2, spec.OW // 2, spec.K)
+            self._block_ok[key] = ok
+        return ok
+
     @torch.no_grad()
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         m = self.model
         if x.dim() == 4:
             x = x.unsqueeze(-1)
         c1 = m.convs[0]
+        if self.block_mode(tuple(x.shape)):
+            return self._forward_block(x)
         tspec = stem_tap_plan(c1, tuple(x.shape)) if self.stem is not None else None
         if tspec is not None and self.stem.tile_plan(tspec) is not None:
             xq, shape = self.stem(stem_tap_input(x, tspec, self.in_scale, self.stem_int8),   # fp8 / int8 in, fp8 out
@@ -249,7 +316,29 @@ class Fp8FeatureNet3D:
 
     __call__ = forward
 
-    def _bf16_stem_fp8_out(self, x: torch.Tensor, spec: ConvSpec):
+    def _forward_block(self, x: torch.Tensor) -> torch.Tensor:
+        """Block-scaled fp8 forward: the bf16 stem writes (e4m3, scales) from its epilogue, every fp8
+        layer reads them through the scaled MFMA and writes its own, the last one (fused pool) bf16."""
+        m = self.model
+        c1 = m.convs[0]
+        x = x.to(torch.bfloat16).contiguous()
+        spec = ConvSpec.make(tuple(x.shape), c1.cout, c1.kernel, c1.stride, c1.padding)
+        xq = self._bf16_stem_fp8_out(x, spec, block=True)
+        if xq is None:
+            xq = quantize_fp8_block(ops.conv(x, self.c1_w, self.c1_b, spec, "relu"))
+        shape = spec.out_shape5
+        fused_pool = False
+        for li, layer in enumerate(self.layers):
+            last = li == len(self.layers) - 1
+            fused_pool = last and self._pool_fusable() and layer.pool_plan(shape, block=True) is not None
+            xq, shape = layer(xq, shape, pool=fused_pool)
+        feat = xq
+        if self.pool is not None and not fused_pool:
+            ps = PoolSpec.make(tuple(feat.shape), self.pool, m.convs[-1].pool_stride, "valid")
+            feat = ops.pool(feat, ps, "max")
+        return self._dense(feat.reshape(feat.shape[0], -1))
+
+    def _bf16_stem_fp8_out(self, x: torch.Tensor, spec: ConvSpec, block: bool = False):
         """The bf16 stem (space-to-depth tile kernel, BN folded, ReLU) writing e4m3 of its output
         / act_scales[0] from the epilogue -- conv2's input without a bf16 tensor or a
         quantisation pass -- or None where that kernel does not take the stem."""
@@ -266,6 +355,8 @@ class Fp8FeatureNet3D:
         if w2 is None:
             w2 = self._stem_w2[key] = s2d_weight(self.c1_w, f, spec, spec2)
         x2 = s2d_input(x, f, spec2, (spec.pd, spec.ph, spec.pw))
+        if block:                                # (block-scaled e4m3 + scale dwords)
+            return conv_tile.conv_fwd_q8_block(x2, w2, self.c1_b, spec2, 1, tp)
         y, _ = conv_tile.conv_fwd(x2, w2, self.c1_b, spec2, 1, False, tp, out_scale=self.act_scales[0])
         return y
 

@@ -118,24 +118,27 @@ def _ksteps(T: int, CS: int, PD: int) -> int:
 
 
 def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int = 256, f8: bool = False,
-         pool: bool = False):
+         pool: bool = False, bs: bool = False):
     """Best TilePlan for an (N, OD, OH, OW) output of a (KD, KH, KW) stride-1 conv over
     ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply
     (``f8``: the e4m3 inference variant, 32- or 64-channel slices; ``pool``: with the fused
-    2^3 max-pool epilogue -- even output and tile dims)."""
+    2^3 max-pool epilogue -- even output and tile dims; ``bs``: block-scaled fp8 operands, the
+    LDS also holds two planes of the halo positions' scale dwords)."""
     m32 = not f8 and Ncol % 32 == 0 and m32_enabled()
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, pool, m32, os.environ.get("FN_TILE_PLAN_RANK", "0"))
+    bs = bool(bs and f8)
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, pool, m32, bs,
+           os.environ.get("FN_TILE_PLAN_RANK", "0"))
     if key in _PLANS:
         return _PLANS[key]
     if pool and (not f8 or any(d % 2 for d in out_dims)):
         return None
-    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, pool, m32)
+    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, pool, m32, bs)
     with _LOCK:
         _PLANS[key] = best
     return best
 
 
-def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False):
+def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False, bs=False):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
@@ -174,7 +177,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
                     HPpad = -(-HP // 64) * 64
                     BUF = HPpad * CPP * 16                     # the halo (a multiple of 2 KiB)
                     lds = 2 * BUF + 64 + red_bytes(NT) + (nks + PD + 2) * 16 + HPpad * 8 + (NT * 16 * 8 if f8 else 0) \
-                        + (128 if m32 else 0)
+                        + (128 if m32 else 0) + (2 * HPpad * 4 if bs else 0)
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
@@ -598,7 +601,7 @@ def workers(p: TilePlan, geom: list, ncol: int) -> int:
 
 
 def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p: TilePlan, geom: list, kdims: tuple,
-        ncol: int, act: int, bny=None, bnp=None, oscale: float = 0.0) -> None:
+        ncol: int, act: int, bny=None, bnp=None, oscale: float = 0.0, osc=None) -> None:
     st = _native.stream(src5)
     rt = rowtab_tensor(p, kdims, src5.device)
     kt = ktab_tensor(p, kdims, src5.device)
@@ -614,7 +617,8 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
     _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                 zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                 _native.ptr(stats), geom, ncol, act, p.MT, p.NT, sched(src5.device, st).data_ptr(),
-                                st, ext, _native.ptr(bny), _native.ptr(bnp), float(oscale))
+                                st, ext, _native.ptr(bny), _native.ptr(bnp), float(oscale), _native.ptr(osc),
+                                osc.numel() if osc is not None else 0)
 
 
 def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan,
@@ -639,6 +643,20 @@ def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats
         stats = torch.empty(workers(p, geom, spec.K), 2, spec.K, dtype=torch.float32, device=x5.device)
     run(x5, wpk, bias, y, stats, p, geom, kd, spec.K, act, oscale=1.0 / out_scale if out_scale else 0.0)
     return y, stats
+
+
+def conv_fwd_q8_block(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, p: TilePlan):
+    """The bf16 tile forward writing OCP MX-style block-scaled e4m3: (y bytes [N, OD, OH, OW, K],
+    scales int32 [N, OD, OH, OW] -- byte j = E8M0 scale of channels 32j..32j+31).  The fp8 inference
+    input of the next layer, from the epilogue (the space-to-depth stem instances)."""
+    kd = (spec.KD, spec.KH, spec.KW)
+    geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
+                    (spec.pd, spec.ph, spec.pw))
+    wpk = pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=False)
+    y = torch.empty(spec.out_shape5, dtype=torch.uint8, device=x5.device)
+    ysc = torch.zeros(spec.out_shape5[:4], dtype=torch.int32, device=x5.device)
+    run(x5, wpk, bias, y, None, p, geom, kd, spec.K, act, oscale=1.0, osc=ysc)
+    return y, ysc
 
 
 def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None, wpk=None):
@@ -737,11 +755,16 @@ def pack_weights_f8(wq: torch.Tensor, p: TilePlan) -> torch.Tensor:
 
 
 def conv_fwd_f8(xq5: torch.Tensor, wpk: torch.Tensor, scale: torch.Tensor, bias: torch.Tensor, spec, p: TilePlan,
-                relu: bool, out_scale: float | None, i8: bool = False) -> torch.Tensor:
+                relu: bool, out_scale: float | None, i8: bool = False, xsc: torch.Tensor | None = None,
+                out_block: bool = False):
     """y = act(conv(x, w) * scale + bias) of e4m3 activations (uint8 [N, D, H, W, C]) on the fp8
     tile kernel: bf16 output, or e4m3 of y / out_scale when ``out_scale`` is given.  ``i8``: the
     operands are int8 instead (x, wpk hold int8 bytes; the int8 MFMA instance).  A ``pool``
-    plan returns maxpool2^3(relu(...)) instead: bf16 [N, OD/2, OH/2, OW/2, K]."""
+    plan returns maxpool2^3(relu(...)) instead: bf16 [N, OD/2, OH/2, OW/2, K].
+
+    ``xsc`` (int32 [N, D, H, W]): block-scaled input -- byte j of a position's dword is the E8M0
+    scale of its channels 32j..32j+31, applied by the scaled MFMA; ``scale`` then dequantises the
+    weights only.  ``out_block`` (with xsc): block-scaled e4m3 output, returns ``(y, ysc)``."""
     kd = (spec.KD, spec.KH, spec.KW)
     geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
                     (spec.pd, spec.ph, spec.pw))
@@ -750,15 +773,21 @@ def conv_fwd_f8(xq5: torch.Tensor, wpk: torch.Tensor, scale: torch.Tensor, bias:
         y = torch.empty(spec.N, spec.OD // 2, spec.OH // 2, spec.OW // 2, spec.K, dtype=torch.bfloat16,
                         device=xq5.device)
     else:
-        y = torch.empty(spec.out_shape5, dtype=torch.uint8 if out_scale else torch.bfloat16, device=xq5.device)
+        y = torch.empty(spec.out_shape5, dtype=torch.uint8 if (out_scale or out_block) else torch.bfloat16,
+                        device=xq5.device)
+    assert not out_block or (xsc is not None and not p.pool)
+    ysc = torch.zeros(spec.out_shape5[:4], dtype=torch.int32, device=xq5.device) if out_block else None
     st = _native.stream(xq5)
     rt = rowtab_tensor(p, kd, xq5.device)
     kt = ktab_tensor(p, kd, xq5.device)
+    oscale = 1.0 if out_block else (1.0 / out_scale if out_scale else 0.0)
     _native.kernels().conv_tile_f8(xq5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                    zero_page(xq5.device).data_ptr(), scale.data_ptr(), _native.ptr(bias), y.data_ptr(),
-                                   1.0 / out_scale if out_scale else 0.0, geom, spec.K,
+                                   oscale, geom, spec.K,
                                    int(relu) | (2 if p.pool else 0) | (4 if i8 else 0),
                                    p.MT, p.NT, st,
                                    sched(xq5.device, st).data_ptr(),
-                                   [xq5.numel(), wpk.numel(), y.numel(), rt.numel() // 2, kt.numel() // 4])
-    return y
+                                   [xq5.numel(), wpk.numel(), y.numel(), rt.numel() // 2, kt.numel() // 4,
+                                    xsc.numel() if xsc is not None else 0, ysc.numel() if ysc is not None else 0],
+                                   _native.ptr(xsc), _native.ptr(ysc))
+    return (y, ysc) if out_block else y

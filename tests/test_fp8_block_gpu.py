@@ -1,0 +1,146 @@
+"""Block-scaled fp8 inference (OCP MX style): e4m3 activations with one E8M0 power-of-two scale per
+(position, 32-channel block), applied inside ``v_mfma_scale_f32_16x16x128_f8f6f4`` as the halo
+operand's scale (``conv_tile.hip`` BS instances), written by the producing epilogues.
+
+Every check compares against an fp32 emulation of the same quantised operands: the block
+quantiser against its definition (e = ceil(log2(amax / 448))), the scaled-MFMA conv against the
+fp32 conv of the dequantised input and weights, the epilogue's block-scaled output against the
+quantiser applied to the bf16 output.  (BASELINE.json config 5: 128^3 fp8 inference.)
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from featurenet_amd import _native  # noqa: E402
+from featurenet_amd.ops import reference as ref  # noqa: E402
+from featurenet_amd.ops.spec import ConvSpec  # noqa: E402
+
+
+def _spread(shape, lo=-8.0, hi=8.0, seed=0):
+    """Activations whose magnitude varies by 2^16 across positions (one factor per position)."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(*shape, device="cuda", generator=g)
+    f = torch.exp2(torch.rand(*shape[:-1], 1, device="cuda", generator=g) * (hi - lo) + lo)
+    return (x * f).to(torch.bfloat16)
+
+
+def test_block_quantiser_definition():
+    from featurenet_amd.inference.fp8 import dequantize_fp8_block, quantize_fp8_block
+
+    assert _native.kernels_available()
+    x = _spread((4, 9, 10, 11, 64))
+    x[0, 0, 0, 0] = 0                                   # an all-zero position
+    q, sc = quantize_fp8_block(x)
+    xf = x.float().reshape(-1, 2, 32)
+    amax = xf.abs().amax(-1)
+    e_ref = torch.ceil(torch.log2(amax / 448.0)).clamp(-127, 126)
+    e_ref[amax == 0] = -127
+    e = torch.stack([(sc.reshape(-1) >> (8 * j)) & 255 for j in range(2)], -1).float() - 127
+    assert torch.equal(e, e_ref)
+    d = dequantize_fp8_block(q, sc).reshape(-1, 2, 32)
+    err = (d - xf).abs()
+    # e4m3: 3 mantissa bits (half-ulp 2^-4 relative) down to the subnormal step 2^-9 x 2^e
+    assert torch.all(err <= 0.0625 * xf.abs() + torch.exp2(e).unsqueeze(-1) * 2.0 ** -9)
+    assert torch.all(d.abs() <= 448.0 * torch.exp2(e).unsqueeze(-1))
+
+
+@pytest.mark.parametrize("cin,cout,k,dims,out_block", [
+    (32, 32, 5, (3, 17, 16, 15), True),       # conv2-like: CS = 32, 4 taps per 128-k step, edge tiles
+    (32, 64, 4, (2, 14, 13, 12), True),       # conv3-like
+    (64, 64, 3, (2, 12, 13, 14), False),      # conv4-like: CS = 64, 2 taps per step, bf16 output
+])
+def test_block_scaled_conv_matches_emulation(cin, cout, k, dims, out_block):
+    """The scaled-MFMA conv on block-scaled input vs the fp32 conv of the dequantised operands."""
+    from featurenet_amd.inference.fp8 import Fp8Conv, dequantize_fp8_block, quantize_fp8_block
+    from featurenet_amd.models.layers import Conv
+
+    torch.manual_seed(4)
+    conv = Conv(cin, cout, (k, k, k), 1, "valid", bias=True).cuda()
+    with torch.no_grad():
+        conv.bias.normal_(0, 0.1)
+    x = _spread((*dims, cin), seed=1)
+    xq, xs = quantize_fp8_block(x)
+    layer = Fp8Conv(conv, 1.0, 1.0 if out_block else None, relu=True)
+    spec = ConvSpec.make(x.shape, cout, (k, k, k))
+    assert layer.tile_plan(spec, block=True) is not None, spec
+    y, shape = layer((xq, xs), tuple(x.shape))
+    yr = torch.relu(ref.conv(dequantize_fp8_block(xq, xs), layer.w_dequant, layer.bias, spec))
+    if out_block:
+        yq, ys = y
+        assert yq.shape == tuple(shape) and ys.shape == tuple(shape[:-1])
+        yd = dequantize_fp8_block(yq, ys)
+        # e4m3 rounding of the output (3 mantissa bits) on top of the conv's accumulation order
+        bound = 0.07 * yr.abs() + 1e-3 * yr.abs().amax(-1, keepdim=True)
+        assert torch.all((yd - yr).abs() <= bound), ((yd - yr).abs() - bound).max()
+    else:
+        err = (y.float() - yr).abs().max().item()
+        assert err <= 1e-2 * yr.abs().max().item(), err
+
+
+def test_block_scales_keep_small_positions():
+    """One position ~2^17 larger than the rest: per-tensor e4m3 pushes the others below e4m3's
+    normal range (2^-6 of 448), the block-scaled path keeps them at e4m3 precision (the failure
+    mode of a per-tensor scale)."""
+    from featurenet_amd.inference.fp8 import Fp8Conv, dequantize_fp8_block, quantize_fp8_block
+    from featurenet_amd.models.layers import Conv
+
+    torch.manual_seed(5)
+    conv = Conv(32, 32, (3, 3, 3), 1, "valid", bias=True).cuda()
+    x = (torch.randn(2, 12, 12, 12, 32, device="cuda") * 0.01).to(torch.bfloat16)
+    x[0, 0, 0, 0] = 2000.0                                # the outlier (sample 0 only)
+    spec = ConvSpec.make(x.shape, 32, (3, 3, 3))
+    xq, xs = quantize_fp8_block(x)
+    lb = Fp8Conv(conv, 1.0, None, relu=False)
+    yb, _ = lb((xq, xs), tuple(x.shape))
+    ts = float(x.float().abs().amax()) / 448.0
+    lt = Fp8Conv(conv, ts, None, relu=False)
+    yt, _ = lt((x.float() / ts).to(torch.float8_e4m3fn).view(torch.uint8), tuple(x.shape))
+    yr = ref.conv(x.float(), lb.w_dequant, lb.bias, spec)
+    far = (slice(1, 2),)                                  # the second sample never sees the outlier
+    eb = ((yb.float() - yr)[far].norm() / yr[far].norm()).item()
+    et = ((yt.float() - yr)[far].norm() / yr[far].norm()).item()
+    assert eb < 0.05 and eb * 4 < et, (eb, et)
+    torch.testing.assert_close(dequantize_fp8_block(xq, xs)[1], x.float()[1], rtol=0.07, atol=1e-4)
+
+
+def test_stem_block_output_equals_quantiser():
+    """The bf16 stem's epilogue writing block-scaled e4m3 (Q8O BS instance) = the block quantiser
+    applied to the stem's bf16 output, byte for byte."""
+    from featurenet_amd.inference.fp8 import quantize_fp8_block
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+    from featurenet_amd.ops import conv_tile
+    from featurenet_amd.ops.conv import s2d_input, s2d_plan, s2d_weight
+
+    torch.manual_seed(6)
+    m = FeatureNet3D(FeatureNet3DConfig(input_size=48, num_classes=24)).cuda().eval()
+    c1 = m.convs[0]
+    x = (torch.rand(3, 48, 48, 48, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    spec = ConvSpec.make(tuple(x.shape), c1.cout, c1.kernel, c1.stride, c1.padding)
+    f, spec2 = s2d_plan(spec)
+    tp = conv_tile.fwd_plan(spec2)
+    assert tp is not None and tp.CS == 8
+    w2 = s2d_weight(c1.weight.detach().float(), f, spec, spec2)
+    b = torch.randn(c1.cout, device="cuda") * 0.1
+    x2 = s2d_input(x, f, spec2, (spec.pd, spec.ph, spec.pw))
+    yq, ys = conv_tile.conv_fwd_q8_block(x2, w2, b, spec2, 1, tp)
+    y, _ = conv_tile.conv_fwd(x2, w2, b, spec2, 1, False, tp)
+    rq, rs = quantize_fp8_block(y)
+    assert torch.equal(ys, rs)
+    assert torch.equal(yq, rq)
+
+
+def test_fp8_featurenet3d_block_matches_bf16():
+    from featurenet_amd.inference.fp8 import quantize_model
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+
+    torch.manual_seed(0)
+    m = FeatureNet3D(FeatureNet3DConfig(input_size=32, num_classes=24)).cuda().eval()
+    x = (torch.rand(16, 32, 32, 32, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    q = quantize_model(m, x[:8])
+    assert q.block_mode(tuple(x.unsqueeze(-1).shape if x.dim() == 4 else x.shape))
+    with torch.no_grad():
+        ref_logits = m(x).float()
+        got = q(x).float()
+    cos = torch.nn.functional.cosine_similarity(got.flatten(), ref_logits.flatten(), dim=0).item()
+    assert cos > 0.98, cos

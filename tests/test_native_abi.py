@@ -114,6 +114,27 @@ def test_fp8_inference_calls_match_bindings(fake, monkeypatch):
     assert {"conv_tile_f8", "conv_halo_f8", "quant_fp8"} <= set(fake.calls)
 
 
+def test_fp8_block_scaled_calls_match_bindings(fake):
+    from featurenet_amd.inference.fp8 import Fp8Conv, quantize_fp8_block
+    from featurenet_amd.models.layers import Conv
+    from featurenet_amd.ops import conv_tile
+
+    conv = Conv(32, 64, (3, 3, 3), 1, "valid", bias=True)
+    layer = Fp8Conv(conv, 1.0, 1.0)
+    xq, xs = quantize_fp8_block(torch.zeros(2, 10, 10, 10, 32, dtype=torch.bfloat16))
+    assert xq.dtype == torch.uint8 and xs.shape == (2, 10, 10, 10)
+    (yq, ys), shape = layer((xq, xs), tuple(xq.shape))         # block-scaled in and out
+    assert shape == (2, 8, 8, 8, 64) and ys.shape == (2, 8, 8, 8)
+    from featurenet_amd.ops.spec import ConvSpec
+
+    spec = ConvSpec.make((2, 12, 12, 12, 8), 32, 4, 1, "valid")      # (a space-to-depth stem shape)
+    tp = conv_tile.fwd_plan(spec)
+    yq, ys = conv_tile.conv_fwd_q8_block(torch.zeros(2, 12, 12, 12, 8, dtype=torch.bfloat16),
+                                         torch.zeros(32, 4, 4, 4, 8), torch.zeros(32), spec, 1, tp)
+    assert ys.shape == (2, 9, 9, 9)
+    assert {"conv_tile_f8", "quant_fp8_block", "conv_tile"} <= set(fake.calls)
+
+
 def test_halo_extent_check_rejects_undersized_tensors():
     """bind.cpp validates operand extents implied by the geometry before any HIP call."""
     if not _native.kernels_available():
