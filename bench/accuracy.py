@@ -113,7 +113,7 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
     # int8 stem (v_mfma_i32_16x16x64_i8): an experiment build only (FN_BUILD_EXPERIMENTS=1)
     qi = quantize_model(model, cx, fp8_stem="i8") if experiments_built() else None
     y = np.asarray(ds.y_test)
-    pb, pq, ps, pi = [], [], [], []
+    pb, pq, ps, pi, pt = [], [], [], [], []
     for i in range(0, len(y), chunk):
         xb = batch(ds.x_test, i, chunk)
         pb.append(model(xb).float().argmax(-1).cpu())
@@ -121,8 +121,13 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
         ps.append(qs(xb).float().argmax(-1).cpu())
         if qi is not None:
             pi.append(qi(xb).float().argmax(-1).cpu())
-    pb, pq, ps = (torch.cat(t).numpy() for t in (pb, pq, ps))
-    acc_b, acc_q, acc_s = (float((t == y).mean()) for t in (pb, pq, ps))
+        os.environ["FN_F8_BLOCK"] = "0"                 # the per-tensor activation scales, same model
+        try:
+            pt.append(qs(xb).float().argmax(-1).cpu())
+        finally:
+            os.environ.pop("FN_F8_BLOCK")
+    pb, pq, ps, pt = (torch.cat(t).numpy() for t in (pb, pq, ps, pt))
+    acc_b, acc_q, acc_s, acc_t = (float((t == y).mean()) for t in (pb, pq, ps, pt))
     i8 = None
     if qi is not None:
         pi = torch.cat(pi).numpy()
@@ -132,8 +137,13 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
     return {"top1_bf16": round(acc_b, 4), "top1_fp8": round(acc_q, 4), "drop_pt": round(100 * (acc_b - acc_q), 2),
             "agreement": round(float((pb == pq).mean()), 4), "calib_samples": calib,
             "stem": q.stem and ("i8" if q.stem.int8 else "e4m3") or "bf16",
+            "activations": "block-scaled (E8M0 per position x 32 channels)" if q.block_mode(
+                (1, size, size, size, 1)) else "per-tensor",
             "bf16_stem": {"top1_fp8": round(acc_s, 4), "drop_pt": round(100 * (acc_b - acc_s), 2),
                           "agreement": round(float((pb == ps).mean()), 4)},
+            "per_tensor": {"top1_fp8": round(acc_t, 4), "drop_pt": round(100 * (acc_b - acc_t), 2),
+                           "agreement": round(float((pb == pt).mean()), 4)},
+            "calib_agreement": q.calib_agreement,
             "i8_stem": i8,
             "kernel": ("conv_halo_f8" if os.environ.get("FN_F8_TILE", "1") == "0" else "conv_tile F8 variant")
                       + " (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3)"}

@@ -40,6 +40,7 @@ int fn_conv_halo_f8(const void*, const void*, const float*, const float*, void*,
                     int, int, hipStream_t);
 int fn_quant_fp8(const void*, void*, long long, float, hipStream_t);
 int fn_quant_fp8_block(const void*, void*, void*, long long, int, hipStream_t);
+int fn_mfma_scale_probe(const void*, const void*, const int*, const int*, float*, hipStream_t);
 int fn_s2d_tap_f8(const void*, void*, int, int, int, int, int, int, int, int, float, int, hipStream_t);
 int fn_dw_fwd(const void*, const float*, const float*, void*, const int*, int, hipStream_t);
 int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
@@ -463,6 +464,12 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_quant_fp8_block(P<const void*>(x), P<void*>(y), P<void*>(sc), M, C, S(st)), "quant_fp8_block");
   }, py::arg("x"), py::arg("y"), py::arg("sc"), py::arg("M"), py::arg("C"), py::arg("st"),
      py::arg("ext") = std::vector<long long>());
+  // one v_mfma_scale_f32_16x16x128_f8f6f4 on one wave (a, b: 64 x 32 bytes; sa, sb: 64 int32; d: 64 x 4 fp32)
+  m.def("mfma_scale_probe", [](uintptr_t a, uintptr_t b, uintptr_t sa, uintptr_t sb, uintptr_t d, uintptr_t st) {
+    chk(fn_mfma_scale_probe(P<const void*>(a), P<const void*>(b), P<const int*>(sa), P<const int*>(sb), P<float*>(d),
+                            S(st)),
+        "mfma_scale_probe");
+  });
   m.def("quant_fp8", [](uintptr_t x, uintptr_t y, long long n, float inv_scale, uintptr_t st) {
     chk(fn_quant_fp8(P<const void*>(x), P<void*>(y), n, inv_scale, S(st)), "quant_fp8");
   });

@@ -428,3 +428,34 @@ extern "C" int fn_s2d_tap_f8(const void* x, void* y, int N, int D, int H, int W,
   FN_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Probe of v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3) on one wave: lane l supplies the 32 A
+// bytes a[l][0..31], the 32 B bytes b[l][0..31], the scale dwords sa[l] / sb[l] (opsel 0: low
+// byte) and gets its 4 accumulator values d[l][0..3] -- the numerics test pins the operand
+// K-layout and the block-scale lane mapping against an fp32 emulation (tests/test_fp8_block_gpu.py)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void mfma_scale_probe_kernel(const unsigned char* __restrict__ a,
+                                                              const unsigned char* __restrict__ b,
+                                                              const int* __restrict__ sa, const int* __restrict__ sb,
+                                                              float* __restrict__ d) {
+  const int l = threadIdx.x;
+  i32x8 va, vb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    va[j] = *(const int*)(a + l * 32 + 4 * j);
+    vb[j] = *(const int*)(b + l * 32 + 4 * j);
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(va, vb, acc, 0, 0, 0, sa[l], 0, sb[l]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) d[l * 4 + r] = acc[r];
+}
+
+extern "C" int fn_mfma_scale_probe(const void* a, const void* b, const int* sa, const int* sb, float* d,
+                                   hipStream_t st) {
+  hipLaunchKernelGGL(mfma_scale_probe_kernel, dim3(1), dim3(64), 0, st, (const unsigned char*)a,
+                     (const unsigned char*)b, sa, sb, d);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

@@ -112,21 +112,24 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // [halo positions HPpad int2: (byte offset from the halo origin, packed hd|hh|hw)]
   int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);                    // [2][2] (tile, slice) by parity
   float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);           // [4 waves][2][32] BN partials
+  // BS (F8): two int4 per k-step -- the tap offset of the scale each lane group supplies, then the
+  // lane group's packed (lo | hi << 16) data offsets (the block-scaled operand layout, below)
+  constexpr int KTW = (F8 && BS) ? 2 : 1;
   int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + ct_red_bytes(NT));
-  int2* s_pos = reinterpret_cast<int2*>(s_kt + (nks + PD + 2));
-  for (int i = tid; i < nks + PD + 2; i += CT_NTHR) s_kt[i] = ktab[i];
+  int2* s_pos = reinterpret_cast<int2*>(s_kt + KTW * (nks + PD + 2));
+  for (int i = tid; i < KTW * (nks + PD + 2); i += CT_NTHR) s_kt[i] = ktab[i];
   for (int i = tid; i < ct_red_bytes(NT) / 4; i += CT_NTHR) s_red[i] = 0.f;
   // F8: the dequantisation scale and bias of this workgroup's 32 columns ([scale 32][bias 32]),
   // read by the epilogue from LDS (global loads there serialised every tile's stores)
   float* s_sb = reinterpret_cast<float*>(s_pos + g.HPpad);
   // relu-mask dgrad (gmask): two buffers (by job parity) of the tile's mask bytes,
   // [natural tile row][Ncol / 8], after everything else
-  const int mask_off = 64 + ct_red_bytes(NT) + (nks + PD + 2) * 16 + g.HPpad * 8 + (F8 ? NT * 16 * 8 : 0);
+  const int mask_off = 64 + ct_red_bytes(NT) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + (F8 ? NT * 16 * 8 : 0);
   // (the buffers hold the bytes in FRAGMENT order -- slot f = (wave * MT + mt) * 16 + lr -- so
   // the epilogue reads slot (wave * MT + mt) * 16 + lr: a per-lane base plus a constant per mt)
   const int mask_bytes = ct_mask_bytes(4 * MT * 16, Ncol, gmask != nullptr);
   // BS (F8): two planes (by job parity) of the halo positions' scale dwords, after s_sb
-  const int scl_off = 2 * g.BUF + 64 + ct_red_bytes(NT) + (nks + PD + 2) * 16 + g.HPpad * 8 + NT * 16 * 8;
+  const int scl_off = 2 * g.BUF + 64 + ct_red_bytes(NT) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + NT * 16 * 8;
   // ... and after them each fragment slot's (output offset from the tile origin in positions,
   // packed td|th|tw; dummy rows: the origin) for the loader's mask DMA, built once per kernel
   int2* s_mrow = reinterpret_cast<int2*>(dsm + 2 * g.BUF + mask_off + 2 * mask_bytes);
@@ -163,7 +166,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     const int2 rt = rowtab[((loader ? 0 : wave) * MT + mt) * 16 + lr];
     if constexpr (F8 && BS) sofs[mt] = rt.x * 4;
     // this lane group's (first) plane
-    if constexpr (F8) lb[mt] = rt.x * 16 + (CPP == 4 ? 2 * (lg & 1) : 0) * PLANE;
+    // (BS: lane group lg reads chunk plane lg & 1 (CPP 2) or lg (CPP 4) of two taps, see read_a)
+    if constexpr (F8 && BS) lb[mt] = rt.x * 16 + (CPP == 4 ? lg : (lg & 1)) * PLANE;
+    else if constexpr (F8) lb[mt] = rt.x * 16 + (CPP == 4 ? 2 * (lg & 1) : 0) * PLANE;
     else lb[mt] = rt.x * 16 + (CPP >= 4 ? lg : (CPP == 2 ? (lg & 1) : 0)) * PLANE;
     const int tw = rt.y % g.TW, th = (rt.y / g.TW) % g.TH, td = rt.y / (g.TW * g.TH);
     roff[mt] = rt.y < 0 ? -1 : td * g.osd + th * g.osh + tw * g.osw;
@@ -342,8 +347,18 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     };
     // A fragment of row block mt at k-step offset ko: one 16-B read (bf16) or the lane
     // group's two consecutive chunk planes (fp8)
+    // BS: v_mfma_scale_f32_16x16x128_f8f6f4 reads a lane's bytes 0-15 as k = 16 lg .. and bytes 16-31 as
+    // k = 64 + 16 lg .., and takes the scale of 32-k block j from lane group j
+    // (tests/test_fp8_block_gpu.py::test_scaled_mfma_operand_layout), so every block must be one
+    // (position, 32-channel block): lane group lg reads its low 16 B at the packed offset's low half
+    // and its high 16 B at the high half (two taps, one chunk plane), and supplies the scale of
+    // block lg (kofs_s)
     auto read_a = [&](int mt, int ko) -> Frag {
-      if constexpr (F8) {
+      if constexpr (F8 && BS) {
+        const uint4 lo = *(const uint4*)(dsm + lb[mt] + (ko & 0xffff));
+        const uint4 hi = *(const uint4*)(dsm + lb[mt] + (ko >> 16));
+        return (ct_i32x8){(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+      } else if constexpr (F8) {
         const uint4 lo = *(const uint4*)(dsm + lb[mt] + ko);
         const uint4 hi = *(const uint4*)(dsm + lb[mt] + ko + PLANE);
         return (ct_i32x8){(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
@@ -356,7 +371,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // them per lane keeps the offset a per-lane value even where it is uniform: hipcc then
     // keeps the halo reads interleaved with the MFMAs (with a wave-uniform offset it
     // hoisted a turn's reads into a double-buffered block)
-    auto kofs = [&](int k) -> int { return *((const int*)(s_kt + k) + lg); };
+    auto kofs = [&](int k) -> int { return *((const int*)(s_kt + KTW * k + (KTW - 1)) + lg); };
+    auto kofs_s = [&](int k) -> int { return *((const int*)(s_kt + KTW * k) + lg); };   // (BS: scale tap)
     // BS: the scale of fragment mt's rows at k-step offset ko (the dword of the row's tap position,
     // its block byte shifted down)
     auto read_s = [&](int mt, int ko) -> unsigned {
@@ -408,20 +424,23 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       const unsigned char* wnext =
           reinterpret_cast<const unsigned char*>(wp) + ((size_t)nslc * nks * g.nct + ct0) * FTILE;
       {
-        const int ko = kofs(0);
+        const int ko = kofs(0), kos = kofs_s(0);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           fa[mt] = read_a(mt, ko);
-          if constexpr (F8 && BS) fs[mt] = read_s(mt, ko);
+          if constexpr (F8 && BS) fs[mt] = read_s(mt, kos);
         }
       }
       int ko_n = kofs(1);                        // offsets of the next k-step
+      int kos_n = (F8 && BS) ? kofs_s(1) : 0;
       for (int ks = 0; ks < nks; ks += PD) {
         const unsigned char* wl = ks + PD >= nks ? wnext : wbase;   // last turn: next job's steps
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
           const int ko = (DBG & 32) ? u * 16 * 37 : ko_n;   // (DBG 32, timing only: constant tap offsets)
+          const int kos = kos_n;
           if constexpr (!(DBG & 32)) ko_n = kofs(ks + u + 2);
+          if constexpr (F8 && BS) kos_n = kofs_s(ks + u + 2);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -446,7 +465,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             }
             if constexpr (!(DBG & 2)) {
               fa[mt] = read_a(mt, ko);
-              if constexpr (F8 && BS) fs[mt] = read_s(mt, ko);
+              if constexpr (F8 && BS) fs[mt] = read_s(mt, kos);
             }
             if constexpr (!(DBG & 128)) __builtin_amdgcn_sched_barrier(0);   // (DBG 128: free scheduling
           }                                                                  //  within a k-step)
@@ -947,7 +966,8 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, int Ncol = 0, bool mask = false,
                              bool bs = false) {
   const int PD = ct_pd(NT, f8);
-  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 + (size_t)g.HPpad * 8 +
+  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 * (f8 && bs ? 2 : 1) +
+         (size_t)g.HPpad * 8 +
          (f8 ? (size_t)NT * 16 * 8 : 0) + (size_t)ct_mask_lds(4 * MT * 16, Ncol, mask) +
          (f8 && bs ? 2 * (size_t)g.HPpad * 4 : 0);    // (BS: the two scale planes)
 }

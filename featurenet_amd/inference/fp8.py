@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import math
 import os
+import warnings
 
 import torch
 
@@ -38,6 +39,7 @@ from ..ops.spec import ConvSpec, PoolSpec
 
 FP8_MAX = 448.0
 I8_MAX = 127.0
+AGREEMENT_WARN = 0.97      # calibration-set top-1 agreement below which quantize_model warns
 
 
 def _fold_bn(conv) -> tuple[torch.Tensor, torch.Tensor]:
@@ -236,6 +238,7 @@ class Fp8FeatureNet3D:
         self.in_scale = in_scale
         self._stem_w2 = {}
         self._block_ok = {}
+        self.calib_agreement = None
         self.stem = None
         self.stem_int8 = bool(stem_int8)
         if in_scale is not None:
@@ -264,11 +267,11 @@ class Fp8FeatureNet3D:
         block-scaled tile plan for every fp8 layer (else the per-tensor path)."""
         if os.environ.get("FN_F8_BLOCK", "1") == "0" or self.stem is not None:
             return False
-        key = tuple(in_shape5)
+        key = (tuple(in_shape5), os.environ.get("FN_F8_TILE", "1"), os.environ.get("FN_F8_POOL", "1"))
         ok = self._block_ok.get(key)
         if ok is None:
             c1 = self.model.convs[0]
-            shape = ConvSpec.make(key, c1.cout, c1.kernel, c1.stride, c1.padding).out_shape5
+            shape = ConvSpec.make(key[0], c1.cout, c1.kernel, c1.stride, c1.padding).out_shape5
             ok = True
             for li, layer in enumerate(self.layers):
                 spec = ConvSpec.make(shape, layer.K, layer.kernel, 1, layer.padding)
@@ -414,7 +417,18 @@ def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem=None) ->
                              "no faster than the bf16 stem, and 23.8 points of top-1 lost on one of two seeds")
     amax = max(float(calib_x.float().abs().amax()), 1e-6)
     in_scale = {"e4m3": amax / FP8_MAX, "i8": amax / I8_MAX}.get(mode)
-    return Fp8FeatureNet3D(model, calibrate(model, calib_x), in_scale, stem_int8=mode == "i8")
+    q = Fp8FeatureNet3D(model, calibrate(model, calib_x), in_scale, stem_int8=mode == "i8")
+    # post-quantisation check on the calibration set: top-1 agreement of the fp8 and bf16 models
+    # (a model whose activations the chosen scales do not fit shows up here, not in deployment)
+    with torch.no_grad():
+        x = calib_x if calib_x.dim() == 5 else calib_x.unsqueeze(-1)
+        a = model(x.to(torch.bfloat16)).float().argmax(-1)
+        b = q(x).float().argmax(-1)
+        q.calib_agreement = round(float((a == b).float().mean()), 4)
+    if q.calib_agreement < AGREEMENT_WARN:
+        warnings.warn(f"fp8 model agrees with bf16 on {q.calib_agreement:.1%} of the calibration set "
+                      f"(< {AGREEMENT_WARN:.0%}): keep this model in bf16", RuntimeWarning)
+    return q
 
 
 _ = math

@@ -89,6 +89,8 @@ class TilePlan:
     f8: bool = False  # fp8 (e4m3) inference variant: 16-channel chunks, 128-k steps, ring depth 2
     pool: bool = False  # fp8: fused 2^3 max-pool epilogue (even tile dims, window-per-lane row table)
     m32: bool = False   # bf16 on conv_tile32_kernel (32x32x16 MFMA, MT / 2 blocks of 32 rows per wave)
+    bs: bool = False    # fp8 with block-scaled activations: the block-scaled operand layout (k_table,
+    #                     pack_weights_f8), two k-table rows per k-step, the LDS scale planes
 
     @property
     def MB(self) -> int:
@@ -176,8 +178,8 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
                     HP = (TD + KD - 1) * HH * HW
                     HPpad = -(-HP // 64) * 64
                     BUF = HPpad * CPP * 16                     # the halo (a multiple of 2 KiB)
-                    lds = 2 * BUF + 64 + red_bytes(NT) + (nks + PD + 2) * 16 + HPpad * 8 + (NT * 16 * 8 if f8 else 0) \
-                        + (128 if m32 else 0) + (2 * HPpad * 4 if bs else 0)
+                    lds = 2 * BUF + 64 + red_bytes(NT) + (nks + PD + 2) * 16 * (2 if bs else 1) + HPpad * 8 \
+                        + (NT * 16 * 8 if f8 else 0) + (128 if m32 else 0) + (2 * HPpad * 4 if bs else 0)
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
@@ -188,8 +190,10 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
                     loader = 1500 + (CPP * HPpad // 64) * 130   # DMA issue + landing of one job's halo
                     per_job = max(mfma + fixed + epi, loader)
                     cost = math.ceil(jobs / workers) * per_job
+                    if bs and HP * 16 >= 65536:
+                        continue                               # (packed 16-bit data offsets)
                     cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
-                                          float(cost), f8, pool, m32))
+                                          float(cost), f8, pool, m32, bs))
     # the cheapest few, re-costed with their row tables' residual bank conflicts (a
     # fragment whose 16 rows repeat a residue mod 16 reads at half rate).  (A finer term --
     # bank_ways, the simulated ways of every ds_read_b128 lane group -- was tried: conv4 fwd's
@@ -210,7 +214,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
             dups = sum(16 - len(set(r.tolist())) for r in res)
             cost = c.cost * (1.0 + 0.5 * dups / res.size)
         ranked.append(TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct",
-                                                          "BUF", "mHW", "mHHW")), cost, f8, pool, m32))
+                                                          "BUF", "mHW", "mHHW")), cost, f8, pool, m32, bs))
     if not ranked:
         return None
     ranked.sort(key=lambda c: c.cost)
@@ -514,6 +518,22 @@ def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
     toff = (((kd * HH + kh) * HW + kw) * 16).reshape(-1)
     tab = np.zeros((p.nks + 2 * PD + 2, 4), dtype=np.int32)
     plane = p.HPpad * 16
+    if p.f8 and p.bs:
+        # block-scaled operand layout: row 2k = the tap offset of the scale lane group lg supplies
+        # (32-k block lg of the MFMA), row 2k+1 = lg's packed data offsets lo | hi << 16 -- bytes 0-15
+        # and 16-31 of its operand, two taps of one chunk plane (see conv_tile.hip read_a)
+        tab2 = np.zeros((p.nks + 2 * PD + 2, 8), dtype=np.int64)
+        off = lambda t: int(toff[t]) if t < T else 0   # noqa: E731
+        for k in range(p.nks):
+            for lg in range(4):
+                if p.CS == 32:
+                    st, lo, hi = 4 * k + lg, 4 * k + (lg >> 1), 4 * k + 2 + (lg >> 1)
+                else:
+                    st, lo, hi = 2 * k + (lg >> 1), 2 * k, 2 * k + 1
+                assert off(lo) < 65536 and off(hi) < 65536
+                tab2[k, lg] = off(st)
+                tab2[k, 4 + lg] = off(lo) | (off(hi) << 16)
+        return tab2.astype(np.uint32).view(np.int32).reshape(-1, 4)
     if p.m32:
         # conv_tile32: entry [k][2h + j] = the offset lane half h reads in sub-step j (16 k each)
         for k in range(p.nks):
@@ -730,7 +750,8 @@ def pack_weights_f8(wq: torch.Tensor, p: TilePlan) -> torch.Tensor:
     """e4m3 weight bytes [K, taps, C] (uint8) -> the fp8 kernel's fragment stream: uint8
     [(nslice * nks + 4) * nct * 64 * 32] -- per (slice, k-step, 16-column tile, lane) the 32
     bytes lane group lg multiplies (tap 4ks+lg x 32 channels for CS = 32, tap 2ks+lg/2 x
-    channels 32(lg&1).. for CS = 64), columns in the bf16 kernel's permuted order, zeros past
+    channels 32(lg&1).. for CS = 64; block-scaled plans: bytes 0-15 / 16-31 of two taps, the
+    halo's layout, see :func:`k_table`), columns in the bf16 kernel's permuted order, zeros past
     the last tap / column and 4 zero k-steps for the ring's over-the-end loads."""
     assert p.f8
     K, T, C = wq.shape
@@ -739,18 +760,22 @@ def pack_weights_f8(wq: torch.Tensor, p: TilePlan) -> torch.Tensor:
     Tp = p.nks * tps
     wpad = torch.zeros(p.nct * 16, Tp, C, dtype=torch.uint8, device=wq.device)
     wpad[:K, :T] = wq
-    sl, ks, ct, ln = np.meshgrid(np.arange(nslice), np.arange(p.nks), np.arange(p.nct), np.arange(64), indexing="ij")
+    sl, ks, ct, ln, i = np.meshgrid(np.arange(nslice), np.arange(p.nks), np.arange(p.nct), np.arange(64),
+                                    np.arange(32), indexing="ij")
     fi, lg = ln & 15, ln >> 4
     col = (ct >> 1) * 32 + 8 * (fi >> 2) + 4 * (ct & 1) + (fi & 3)
-    if p.CS == 32:
-        tap, ch0 = 4 * ks + lg, sl * 32
+    hi, b = i >> 4, i & 15
+    if p.bs and p.CS == 32:
+        tap, ch = 4 * ks + 2 * hi + (lg >> 1), sl * 32 + 16 * (lg & 1) + b
+    elif p.bs:
+        tap, ch = 2 * ks + hi, sl * 64 + 16 * lg + b
+    elif p.CS == 32:
+        tap, ch = 4 * ks + lg, sl * 32 + i
     else:
-        tap, ch0 = 2 * ks + (lg >> 1), sl * 64 + 32 * (lg & 1)
+        tap, ch = 2 * ks + (lg >> 1), sl * 64 + 32 * (lg & 1) + i
     dev = wq.device
-    ci = torch.from_numpy(col.reshape(-1)).to(dev)[:, None]
-    ti = torch.from_numpy(tap.reshape(-1)).to(dev)[:, None]
-    chi = torch.from_numpy(ch0.reshape(-1)).to(dev)[:, None] + torch.arange(32, device=dev)[None, :]
-    body = wpad[ci, ti, chi].reshape(-1)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a.reshape(-1))).to(dev)   # noqa: E731
+    body = wpad[t(col), t(tap), t(ch)]
     return torch.cat([body, torch.zeros(4 * p.nct * 64 * 32, dtype=torch.uint8, device=dev)]).contiguous()
 
 

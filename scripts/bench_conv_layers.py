@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="")
+    ap.add_argument("--tile-only", action="store_true", help="skip the conv_halo kernels")
     args = ap.parse_args()
     torch.manual_seed(0)
     rows = []
@@ -63,14 +64,20 @@ def main():
         res = {"layer": name, "gflop": round(gf, 1), "tile_fwd_plan": str(pf), "tile_dgrad_plan": str(pd)}
         hf, hd, hw = cv.halo_fwd_plan(spec), cv.halo_dgrad_plan(spec), cv.halo_wgrad_plan(spec)
         pw = cw.plan(spec)
+        # the training step's dgrad: the relu-mask statistics epilogue (static tile schedule)
+        bits = (x.reshape(-1, 8) > 0).to(torch.uint8)
+        mask = (bits * (2 ** torch.arange(8, device="cuda", dtype=torch.uint8))).sum(-1).to(torch.uint8).contiguous()
+        mask_ok = pd is not None and ct.mask_dgrad_ok(pd, spec.C)
         runs = {"halo_fwd": (hf, lambda: cv.halo_conv_fwd(x, w, None, spec, 0, True, hf)),
                 "tile_fwd": (pf, lambda: ct.conv_fwd(x, w, None, spec, 0, True, pf)),
                 "halo_dgrad": (hd, lambda: cv.halo_conv_dgrad(dy, w, spec, hd)),
                 "tile_dgrad": (pd, lambda: ct.conv_dgrad(dy, w, spec, pd)),
+                "tile_dgrad_mask": (pd if mask_ok else None,
+                                    lambda: ct.conv_dgrad(dy, w, spec, pd, bn=(x, None, 1, mask))),
                 "halo_wgrad": (hw, lambda: cv.halo_conv_wgrad(dy, x, spec, hw)),
                 "wtile_wgrad": (pw, lambda: cw.conv_wgrad(dy, x, spec, pw))}
         for kk, (pl, fn) in runs.items():
-            if pl is None:
+            if pl is None or (args.tile_only and kk.startswith("halo")):
                 continue
             res[kk + "_us"] = round(timeit(fn, args.reps), 1)
             res[kk + "_tflops"] = round(gf / res[kk + "_us"] * 1e3, 1)

@@ -135,12 +135,81 @@ def test_fp8_featurenet3d_block_matches_bf16():
     from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
 
     torch.manual_seed(0)
-    m = FeatureNet3D(FeatureNet3DConfig(input_size=32, num_classes=24)).cuda().eval()
-    x = (torch.rand(16, 32, 32, 32, 1, device="cuda") < 0.3).to(torch.bfloat16)
-    q = quantize_model(m, x[:8])
-    assert q.block_mode(tuple(x.unsqueeze(-1).shape if x.dim() == 4 else x.shape))
+    m = FeatureNet3D(FeatureNet3DConfig(input_size=64, num_classes=24)).cuda().eval()
+    x = (torch.rand(6, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    q = quantize_model(m, x[:4])
+    assert q.block_mode(tuple(x.shape))
     with torch.no_grad():
         ref_logits = m(x).float()
         got = q(x).float()
     cos = torch.nn.functional.cosine_similarity(got.flatten(), ref_logits.flatten(), dim=0).item()
     assert cos > 0.98, cos
+
+
+def _e4m3(v: torch.Tensor) -> torch.Tensor:
+    return v.to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def _probe(a, b, sa, sb):
+    d = torch.empty(64, 4, device="cuda")
+    _native.kernels().mfma_scale_probe(a.data_ptr(), b.data_ptr(), sa.data_ptr(), sb.data_ptr(), d.data_ptr(),
+                                       _native.stream(a))
+    torch.cuda.synchronize()
+    return d
+
+
+def _emulate(a, b, sa, sb, kmap):
+    """D[m][n] = sum_k A[m][k] B[k][n] 2^(sa(m, k/32) - 127) 2^(sb(n, k/32) - 127) with lane (r, g) byte
+    i holding k = kmap(g, i) of row / column r, and the scale of (row r, block j) in lane r + 16 j."""
+    av = a.view(torch.float8_e4m3fn).float().cpu()
+    bv = b.view(torch.float8_e4m3fn).float().cpu()
+    A = torch.zeros(16, 128)
+    B = torch.zeros(128, 16)
+    for lane in range(64):
+        r, g = lane & 15, lane >> 4
+        for i in range(32):
+            k = kmap(g, i)
+            A[r, k] = av[lane, i]
+            B[k, r] = bv[lane, i]
+    esa = (sa.cpu() & 255).float() - 127
+    esb = (sb.cpu() & 255).float() - 127
+    blk = torch.arange(128) // 32
+    SA = torch.exp2(esa.view(4, 16).t()[:, blk])          # [m][k]: lane m + 16 * (k // 32)
+    SB = torch.exp2(esb.view(4, 16).t()[:, blk])          # [n][k]
+    D = (A * SA) @ (B * SB.t())
+    out = torch.empty(64, 4)
+    for lane in range(64):                                  # C layout: col = lane & 15, row = 4 (lane >> 4) + r
+        for r in range(4):
+            out[lane, r] = D[4 * (lane >> 4) + r, lane & 15]
+    return out
+
+
+KMAPS = {
+    "contiguous": lambda g, i: 32 * g + i,                               # lane group g = k block g
+    "split_halves": lambda g, i: 16 * g + i if i < 16 else 64 + 16 * g + (i - 16),
+    "quads": lambda g, i: 8 * g + 32 * (i // 8) + i % 8,
+}
+
+
+def test_scaled_mfma_operand_layout():
+    """One v_mfma_scale_f32_16x16x128_f8f6f4 with random e4m3 operands and random per-lane E8M0
+    scales against an fp32 emulation: pins which K index each (lane, byte) holds and which lane's
+    scale serves which 32-k block (the layout the block-scaled conv kernels are built on)."""
+    torch.manual_seed(8)
+    a = _e4m3(torch.randn(64, 32, device="cuda"))
+    b = _e4m3(torch.randn(64, 32, device="cuda"))
+    one = torch.full((64,), 127, dtype=torch.int32, device="cuda")
+    d1 = _probe(a, b, one, one)
+    sa = torch.randint(121, 134, (64,), dtype=torch.int32, device="cuda")
+    sb = torch.randint(121, 134, (64,), dtype=torch.int32, device="cuda")
+    d = _probe(a, b, sa, sb)
+    res = {}
+    for name, km in KMAPS.items():
+        e1 = _emulate(a, b, one, one, km)
+        e = _emulate(a, b, sa, sb, km)
+        res[name] = ((d1.cpu() - e1).abs().max().item(), (d.cpu() - e).abs().max().item() / e.abs().max().item())
+    print(res)
+    assert res["contiguous"][0] < 1e-3 * d1.abs().max().item()          # the unscaled dot products
+    # bytes 0-15 of lane group g are k = 16g.., bytes 16-31 are k = 64 + 16g..; block j's scale is
+    # lane group j's (measured on MI355X; the block-scaled conv layout is built on this)
+    assert res["split_halves"][1] < 1e-4, res

@@ -86,12 +86,15 @@ def test_fp8_fused_pool_matches_unfused(N, S, C, K):
 def test_tile_f8_matches_halo_f8_model(monkeypatch):
     """Same quantised model through the fp8 tile kernel and the fp8 halo kernel (bf16 stem,
     unfused pool in both): identical fp8 products, fp32 accumulation in a different order --
-    the logits agree to ~1e-2 relative and the intermediate fp8 activations almost exactly."""
+    the logits agree to ~1e-2 relative and the intermediate fp8 activations almost exactly.
+    Per-tensor activation scales in both (the halo kernel has no block-scaled form; the block
+    path is checked against its own emulation in test_fp8_block_gpu.py)."""
     torch.manual_seed(3)
     m = FeatureNet3D(FeatureNet3DConfig(input_size=64, num_classes=24)).cuda().eval()
     x = (torch.rand(8, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
     q = F8.quantize_model(m, x[:4], fp8_stem=False)
     monkeypatch.setenv("FN_F8_POOL", "0")
+    monkeypatch.setenv("FN_F8_BLOCK", "0")
     outs = {}
     for tile in ("1", "0"):
         monkeypatch.setenv("FN_F8_TILE", tile)
