@@ -161,6 +161,7 @@ def main():
     if args.impl == "native":
         from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
         from featurenet_amd.ops import FlatAdam, softmax_xent
+        from featurenet_amd.ops.loss import backward as loss_backward   # (unit-seeded: no fill launch)
         from featurenet_amd.parallel.ddp import GradBucketer
         from featurenet_amd.training.flat import FlatParams
 
@@ -185,7 +186,7 @@ def main():
         def step(i):
             flat.zero_grad()
             loss = loss_of(xs[i % args.pool], ys[i % args.pool])
-            loss.backward()
+            loss_backward(loss)
             scale = bucketer.finish()
             opt.step(grad_scale=scale)
             return loss
@@ -254,7 +255,7 @@ def main():
             with torch.cuda.graph(g):
                 flat.zero_grad()
                 gl = loss_of(sx, sy)
-                gl.backward()
+                loss_backward(gl)
                 bucketer.finish()
                 opt.step_device()
         except Exception as ex:  # noqa: BLE001 - report and fall back to eager steps

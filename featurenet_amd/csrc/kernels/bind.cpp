@@ -113,7 +113,7 @@ int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const vo
                     float, const int*, int, int, int, int, int*, hipStream_t, const void*, void*);
 int fn_conv_tile_f8_supported(int, int, int);
 int fn_conv_wtile(const void*, const void*, float*, float*, const void*, const void*, const void*, const int*, int, int,
-                  int*, hipStream_t);
+                  int*, hipStream_t, const float*, float*);
 int fn_conv_wtile_supported(int, int);
 int fn_tile_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int fn_tile_pack_w2(const float*, void*, void*, int, int, int, const int*, const int*, hipStream_t);
@@ -307,7 +307,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_tile_f8_supported", &fn_conv_tile_f8_supported);
   m.def("conv_wtile", [](uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t part, uintptr_t rowtab, uintptr_t postab,
                          uintptr_t zp, std::vector<int> geom, int nacc, int workers, uintptr_t sched, uintptr_t st,
-                         std::vector<long long> ext) {
+                         std::vector<long long> ext, uintptr_t wsrc, uintptr_t wdp) {
     need(geom, 24, "conv_wtile");
     const long long T = (long long)geom[9] * geom[10] * geom[11];
     fits(ext, 0, prod({geom[0], geom[1], geom[2], geom[3], geom[4]}), "conv_wtile", "x");
@@ -321,14 +321,19 @@ PYBIND11_MODULE(_C, m) {
     fits(ext, 3, 32LL * geom[19], "conv_wtile", "rowtab");
     fits(ext, 4, geom[18], "conv_wtile", "postab");
     fits(ext, 5, 8LL * workers * ((nacc >> 13) & 1 ? 2 : 1) * geom[8] * tw * geom[4], "conv_wtile", "part");
+    if (wsrc) {                                   // S = sum W . dW partials: [ceil(dW / 256)][C], W like dW
+      fits(ext, 6, prod({geom[8], tw, geom[4]}), "conv_wtile", "wsrc");
+      fits(ext, 7, (prod({geom[8], tw, geom[4]}) + 255) / 256 * geom[4], "conv_wtile", "wdp");
+    }
     if (geom[5] > geom[1] + 2 * geom[12] || geom[6] > geom[2] + 2 * geom[13] || geom[7] > geom[3] + 2 * geom[14])
       throw std::runtime_error("conv_wtile: output larger than the padded input");
     chk(fn_conv_wtile(P<const void*>(x), P<const void*>(dy), P<float*>(dw), P<float*>(part), P<const void*>(rowtab),
-                      P<const void*>(postab), P<const void*>(zp), geom.data(), nacc, workers, P<int*>(sched), S(st)),
+                      P<const void*>(postab), P<const void*>(zp), geom.data(), nacc, workers, P<int*>(sched), S(st),
+                      P<const float*>(wsrc), P<float*>(wdp)),
         "conv_wtile");
   }, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("part"), py::arg("rowtab"), py::arg("postab"), py::arg("zp"),
      py::arg("geom"), py::arg("nacc"), py::arg("workers"), py::arg("sched"), py::arg("st"),
-     py::arg("ext") = std::vector<long long>());
+     py::arg("ext") = std::vector<long long>(), py::arg("wsrc") = 0, py::arg("wdp") = 0);
   m.def("conv_wtile_supported", &fn_conv_wtile_supported);
   m.def("conv_tile_workers", [](std::vector<int> geom, int ncol, int NT) {
     need(geom, 31, "conv_tile_workers");

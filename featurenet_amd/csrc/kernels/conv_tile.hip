@@ -160,11 +160,9 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // offset lb (toggled between the buffers per job), its output offset relative to the
   // tile origin (-1: dummy row) and its packed tile coordinates (edge-tile bounds)
   int lb[MT], roff[MT], rpk[MT];
-  int sofs[(F8 && BS) ? MT : 1];                 // BS: byte offset of the row's scale dword in a plane
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int2 rt = rowtab[((loader ? 0 : wave) * MT + mt) * 16 + lr];
-    if constexpr (F8 && BS) sofs[mt] = rt.x * 4;
     // this lane group's (first) plane
     // (BS: lane group lg reads chunk plane lg & 1 (CPP 2) or lg (CPP 4) of two taps, see read_a)
     if constexpr (F8 && BS) lb[mt] = rt.x * 16 + (CPP == 4 ? lg : (lg & 1)) * PLANE;
@@ -322,8 +320,13 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
     Frag fa[MT];                                 // rotating: fragment mt of k-step k+1 is read right
                                                  // after the NT MFMAs of (mt, k) consumed it
-    unsigned fs[(F8 && BS) ? MT : 1];            // BS: fragment mt's E8M0 scale (low byte), read with it
-    int scl_job = 0, ssh = 0;                    // BS: the job's scale plane, the lane's byte in a dword
+    // BS: E8M0 scales (low byte) of fragment rows, a ring of SR read SR - 1 fragments ahead of their
+    // MFMAs (not a full k-step like fa: 8 more live registers made the kernel spill)
+    static_assert(!(F8 && BS) || MT % 4 == 0, "block-scaled instances: MT a multiple of the scale ring");
+    constexpr int SR = (F8 && BS) ? 4 : 1;
+    unsigned fs[SR];
+    int scl_job = 0;                             // BS: the lane's scale byte of the job's scale plane
+                                                 // (less the lane's halo plane offset, see read_s)
     Frag fb[PD][NT];
     // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
     // ct0*16 + 4*NT*lg + 4nt + r: a lane ends with NV = 4*NT consecutive columns of one position
@@ -373,10 +376,14 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // hoisted a turn's reads into a double-buffered block)
     auto kofs = [&](int k) -> int { return *((const int*)(s_kt + KTW * k + (KTW - 1)) + lg); };
     auto kofs_s = [&](int k) -> int { return *((const int*)(s_kt + KTW * k) + lg); };   // (BS: scale tap)
-    // BS: the scale of fragment mt's rows at k-step offset ko (the dword of the row's tap position,
-    // its block byte shifted down)
+    // BS: the scale of fragment mt's rows at k-step scale offset ko (the dword of the row's tap
+    // position, its block byte shifted down).  lb[mt] = 16 row + halo plane + buffer, ko = 16 tap:
+    // (lb + ko) / 4 is the dword index 4 (row + tap) plus terms scl_job takes back off.  One byte
+    // read (ds_read_u8, zero-extended: the MFMA takes the low byte), no shift after it -- a shift
+    // right behind each read made hipcc wait for every scale read on the spot (lgkmcnt(0) per
+    // fragment: the block-scaled kernel ran 1.47x the per-tensor one)
     auto read_s = [&](int mt, int ko) -> unsigned {
-      if constexpr (F8 && BS) return *(const unsigned*)(dsm + scl_job + sofs[mt] + (ko >> 2)) >> ssh;
+      if constexpr (F8 && BS) return *(const unsigned char*)(dsm + scl_job + ((lb[mt] + ko) >> 2));
       else return 127u;
     };
     // epilogue variant (wave-uniform); columns come in whole 8-column groups (Ncol % 8 == 0)
@@ -414,8 +421,8 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       if (tile < 0) break;
       const int nslc = slice + 1 == nslice ? 0 : slice + 1;
       if constexpr (F8 && BS) {
-        scl_job = scl_off + par * g.HPpad * 4;
-        ssh = 8 * (CPP == 4 ? 2 * slice + (lg & 1) : slice);   // 32-channel block of this lane group
+        scl_job = scl_off + par * g.HPpad * 4 - (((CPP == 4 ? lg : (lg & 1)) * PLANE + par * g.BUF) >> 2) +
+                  (CPP == 4 ? 2 * slice + (lg & 1) : slice);   // (+ the byte of this lane group's 32-channel block)
       }
       // ---- k-loop: MFMA + A reads + B loads, nothing else ----
       const unsigned char* wbase = reinterpret_cast<const unsigned char*>(wp) +
@@ -423,24 +430,24 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       // weights of the next job: its slice (slice 0 for a new tile, whatever the tile)
       const unsigned char* wnext =
           reinterpret_cast<const unsigned char*>(wp) + ((size_t)nslc * nks * g.nct + ct0) * FTILE;
+      int kos_c = (F8 && BS) ? kofs_s(0) : 0;   // BS: scale offsets of the current k-step
       {
-        const int ko = kofs(0), kos = kofs_s(0);
+        const int ko = kofs(0);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          fa[mt] = read_a(mt, ko);
-          if constexpr (F8 && BS) fs[mt] = read_s(mt, kos);
+        for (int mt = 0; mt < MT; ++mt) fa[mt] = read_a(mt, ko);
+        if constexpr (F8 && BS) {
+#pragma unroll
+          for (int mt = 0; mt < SR - 1; ++mt) fs[mt] = read_s(mt, kos_c);
         }
       }
       int ko_n = kofs(1);                        // offsets of the next k-step
-      int kos_n = (F8 && BS) ? kofs_s(1) : 0;
       for (int ks = 0; ks < nks; ks += PD) {
         const unsigned char* wl = ks + PD >= nks ? wnext : wbase;   // last turn: next job's steps
 #pragma unroll
         for (int u = 0; u < PD; ++u) {
           const int ko = (DBG & 32) ? u * 16 * 37 : ko_n;   // (DBG 32, timing only: constant tap offsets)
-          const int kos = kos_n;
+          const int kos_x = (F8 && BS) ? kofs_s(ks + u + 1) : 0;   // (BS: the next k-step's)
           if constexpr (!(DBG & 32)) ko_n = kofs(ks + u + 2);
-          if constexpr (F8 && BS) kos_n = kofs_s(ks + u + 2);
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
@@ -456,7 +463,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                 acc[mt][nt] = __builtin_bit_cast(f32x4, c);
               } else if constexpr (F8 && BS)   // e4m3 x e4m3, weights unscaled (127 = 1.0; per-channel
                 acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(   // scale in the epilogue),
-                    fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0, 127, 0, (int)fs[mt]);  // halo block-scaled
+                    fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0, 127, 0, (int)fs[mt % SR]);  // halo block-scaled
               else if constexpr (F8)   // e4m3 x e4m3 (formats 0, 0), E8M0 scales 127 = 1.0
                 acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[u][nt], fa[mt], acc[mt][nt], 0, 0,
                                                                                  0, 127, 0, 127);
@@ -465,12 +472,16 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
             }
             if constexpr (!(DBG & 2)) {
               fa[mt] = read_a(mt, ko);
-              if constexpr (F8 && BS) fs[mt] = read_s(mt, kos);
+              if constexpr (F8 && BS) {          // row mt + SR - 1: this k-step's or (wrapped) the next's
+                const int r = mt + SR - 1;
+                fs[r % SR] = read_s(r < MT ? r : r - MT, r < MT ? kos_c : kos_x);
+              }
             }
             if constexpr (!(DBG & 128)) __builtin_amdgcn_sched_barrier(0);   // (DBG 128: free scheduling
           }                                                                  //  within a k-step)
           // k-step ks+u+PD, or the next job's step u
           if constexpr (!(DBG & 1)) load_b(wl, u);
+          if constexpr (F8 && BS) kos_c = kos_x;
           __builtin_amdgcn_sched_barrier(0);
         }
         wbase += PD * wstep;

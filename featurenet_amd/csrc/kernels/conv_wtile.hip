@@ -490,9 +490,15 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
 // 4 waves of a block sums a quarter of the partials for the block's 64 float4 columns, and
 // the quarters are added in wave order (deterministic; 4x the parallelism of one thread per
 // column walking all W partials)
+// wsrc (optional, C | 256): also the per-block partials wdp[block][c] = sum over the block's 256
+// elements of channel c of bf16(wsrc) * dW (the BN statistics identity's S = sum W . dW, which
+// bn_wdot_kernel would otherwise compute in a launch of its own after this one)
 __global__ __launch_bounds__(256) void wtile_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
-                                                           long long n, int W, int accumulate) {
+                                                           long long n, int W, int accumulate,
+                                                           const float* __restrict__ wsrc, float* __restrict__ wdp,
+                                                           int C) {
   __shared__ float4 s_q[4][64];
+  __shared__ float s_p[256];
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const long long i = ((long long)blockIdx.x * 64 + l) * 4;
   const int q = (W + 3) / 4, p0 = w * q, p1 = min(W, p0 + q);
@@ -530,16 +536,38 @@ __global__ __launch_bounds__(256) void wtile_reduce_kernel(const float* __restri
       const float t[4] = {r.x, r.y, r.z, r.w};
       for (long long j = i; j < n; ++j) dw[j] = t[j - i];
     }
+    if (wsrc) {
+      const float t[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_p[4 * l + k] = i + k < n ? (float)(bf16)wsrc[i + k] * t[k] : 0.f;
+    }
+  } else if (w == 0 && wsrc) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_p[4 * l + k] = 0.f;
+  }
+  if (wsrc) {                                    // (uniform: every thread reaches the barrier)
+    __syncthreads();
+    if ((int)threadIdx.x < C) {
+      float t = 0.f;
+      for (int e = threadIdx.x; e < 256; e += C) t += s_p[e];
+      wdp[(long long)blockIdx.x * C + threadIdx.x] = t;
+    }
   }
 }
 
-extern "C" int fn_part_reduce(const float* part, float* dst, long long n, int W, int accumulate, hipStream_t st) {
+extern "C" int fn_part_reduce_wdot(const float* part, float* dst, long long n, int W, int accumulate,
+                                  const float* wsrc, float* wdp, int C, hipStream_t st) {
   if (n <= 0) return 0;
   if (!part || !dst || W < 1) return -6;
+  if (wsrc && (!wdp || C < 1 || 256 % C || n % C)) return -2;
   hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, dst, n, W,
-                     accumulate);
+                     accumulate, wsrc, wdp, C);
   FN_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int fn_part_reduce(const float* part, float* dst, long long n, int W, int accumulate, hipStream_t st) {
+  return fn_part_reduce_wdot(part, dst, n, W, accumulate, nullptr, nullptr, 0, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -576,9 +604,11 @@ extern "C" int fn_conv_wtile_supported(int K, int nacc) {
 // mod 8 per aligned group of 8; postab int[HPpad] packed halo coords (-1 past the halo);
 // zp >= 16 zero bytes; sched int[64] zeroed (left zero); workers = workgroups per (XCD,
 // column group).
+// wsrc / wdp (optional): the reduce also writes the S = sum W . dW partials [ceil(n / 256)][C]
+// (fn_part_reduce_wdot)
 extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* part, const void* rowtab,
                              const void* postab, const void* zp, const int* geom, int nacc, int workers, int* sched,
-                             hipStream_t st) {
+                             hipStream_t st, const float* wsrc, float* wdp) {
   const WGeom g = parse_wgeom(geom);
   // nacc | (8 << 8): the loaderless 8-wave variant; | (1 << 12): its 8-input-channel form;
   // | (1 << 13): k-steps split between the wave halves; | (1 << 14): the sub-pixel form
@@ -641,5 +671,5 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
 #undef WT_CASE
   FN_CHECK_LAUNCH();
   const long long n = sp ? 64LL * g.K * g.C : (long long)g.K * T * g.C;
-  return fn_part_reduce(part, dw, n, 8 * workers * (ks2 ? 2 : 1), 1, st);
+  return fn_part_reduce_wdot(part, dw, n, 8 * workers * (ks2 ? 2 : 1), 1, sp ? nullptr : wsrc, wdp, g.C, st);
 }

@@ -493,9 +493,11 @@ def wgrad_splits(spec: ConvSpec, target_blocks: int = 1024) -> int:
     return int(min(s, max(1, spec.M // 256)))
 
 
-def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=None) -> torch.Tensor:
+def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=None, wdot=None):
     """fp32 dW [K, KD, KH, KW, C]; ``out`` (zeroed, contiguous, that shape) receives it in place
-    where the kernel allows."""
+    where the kernel allows.  ``wdot`` (the fp32 weights): returns ``(dW, S partials or None)``
+    -- the big-tile kernel's reduce also sums S = W . dW per input channel (see
+    :func:`conv_wtile.conv_wgrad`); None where another kernel ran."""
     plan = halo_wgrad_plan(spec)
     wplan = conv_wtile.plan(spec)
     if wplan is not None:
@@ -503,7 +505,9 @@ def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=N
         use = plan is None or conv_wtile.choose(
             spec, lambda: conv_wtile.conv_wgrad(dy5, x5, spec, wplan), lambda: halo_conv_wgrad(dy5, x5, spec, plan))
         if use:
-            return conv_wtile.conv_wgrad(dy5, x5, spec, wplan, out=out)
+            return conv_wtile.conv_wgrad(dy5, x5, spec, wplan, out=out, wdot=wdot)
+    if wdot is not None:
+        return native_conv_wgrad(dy5, x5, spec, out=out), None
     if plan is not None:
         return halo_conv_wgrad(dy5.contiguous(), x5.contiguous(), spec, plan, out=out)
     K = _native.kernels()
@@ -962,6 +966,7 @@ class ConvFn(torch.autograd.Function):
             else:
                 dx = native_conv_dgrad(dy, w.detach(), spec, wpk=_stashed(ctx))
         dw = db = None
+        wpart = None
         want_db = ctx.has_b and ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1]:
             if ctx.s2d is not None:      # x5 is the space-to-depth packed input (saved by forward)
@@ -977,6 +982,9 @@ class ConvFn(torch.autograd.Function):
                     if fuse_act:
                         dy = native_act_bwd(dy, y, act)
                     dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=tgt)
+            elif ident is not None and w.dtype == torch.float32:
+                # (+ S = sum W . dW for the statistics identity from the reduce pass, when it can)
+                dw, wpart = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w), wdot=w.detach())
             else:
                 # straight into the parameter's zeroed flat gradient when FlatParams offers it
                 dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w))
@@ -986,7 +994,9 @@ class ConvFn(torch.autograd.Function):
             if dw is not None and dw.dtype == torch.float32 and dw.is_contiguous() and dw.numel() == w.numel():
                 # S = sum W . dW per input channel, read before any data-parallel all-reduce of dW
                 # (its hook fires after this backward returns)
-                bnfuse.offer(dx, ("identity", ident, bn_wdot(w.detach(), dw, spec)), bn_y)
+                if wpart is None:
+                    wpart = bn_wdot(w.detach(), dw, spec)
+                bnfuse.offer(dx, ("identity", ident, wpart), bn_y)
             # (else: no offer -- the BN backward's colstats pass reads the masked dx, which its
             # relu mask leaves unchanged)
         return dx, dw, db, None, None, None

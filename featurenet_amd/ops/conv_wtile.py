@@ -336,9 +336,12 @@ def flags(p: WPlan) -> int:
             | (1 << 14 if p.sp else 0))
 
 
-def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) -> torch.Tensor:
+def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None, wdot=None):
     """dW fp32 [K, KD, KH, KW, C] on the big-tile wgrad kernel (accumulated into ``out``
-    when given: a zeroed contiguous fp32 tensor of that size, e.g. the flat gradient)."""
+    when given: a zeroed contiguous fp32 tensor of that size, e.g. the flat gradient).
+    ``wdot`` (the layer's fp32 weights, that layout): returns ``(dW, S partials)`` where the
+    partial slab [blocks, C] of S = sum W . dW comes from the kernel's reduce pass (the BN
+    statistics identity, ``bn_pool.hip``; no separate bn_wdot launch)."""
     kd = (spec.KD, spec.KH, spec.KW)
     dev = x5.device
     rt_np, pt_np = tables(p, kd)
@@ -349,10 +352,18 @@ def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None) ->
     sched = _dev(_SCHED, (str(dev), st), lambda: torch.zeros(64, dtype=torch.int32, device=dev))
     dw = out if out is not None else torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=dev)
     part = _partials(dev, st, 8 * p.workers * (2 if p.ks2 else 1) * dw.numel())
+    wsrc = wdp = None
+    if wdot is not None and 256 % spec.C == 0:
+        wsrc = wdot.detach().float().contiguous()
+        wdp = torch.empty(-(-dw.numel() // 256), spec.C, dtype=torch.float32, device=dev)
+    ext = [x5.numel(), dy5.numel(), dw.numel(), rt.numel() // 2, pt.numel(), part.numel()]
+    if wsrc is not None:
+        ext += [wsrc.numel(), wdp.numel()]
     _native.kernels().conv_wtile(x5.data_ptr(), dy5.data_ptr(), dw.data_ptr(), part.data_ptr(), rt.data_ptr(),
                                  pt.data_ptr(), zp.data_ptr(), geometry(p, spec), flags(p), p.workers, sched.data_ptr(),
-                                 st, [x5.numel(), dy5.numel(), dw.numel(), rt.numel() // 2, pt.numel(), part.numel()])
-    return dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
+                                 st, ext, _native.ptr(wsrc), _native.ptr(wdp))
+    dw = dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
+    return dw if wdot is None else (dw, wdp)
 
 
 def choose(spec, run_wtile, run_halo) -> bool:

@@ -14,6 +14,33 @@ from .. import _native
 from . import reference as ref
 
 
+_UNIT: dict = {}
+
+
+def unit_grad(t: torch.Tensor) -> torch.Tensor:
+    """A cached device scalar 1.0 of ``t``'s dtype: ``loss.backward(unit_grad(loss))`` seeds the
+    backward with a gradient the fused losses recognise (:func:`is_unit`) -- no ``ones_like`` fill
+    launch, and no in-place scale of the stored d(logits)."""
+    key = (str(t.device), t.dtype)
+    u = _UNIT.get(key)
+    if u is None:
+        u = _UNIT[key] = torch.ones((), dtype=t.dtype, device=t.device)
+    return u
+
+
+def is_unit(d: torch.Tensor | None) -> bool:
+    """True when ``d`` is the :func:`unit_grad` scalar itself (identity, not value: no sync)."""
+    if d is None or d.dim() != 0:
+        return False
+    u = _UNIT.get((str(d.device), d.dtype))
+    return u is not None and u.data_ptr() == d.data_ptr()
+
+
+def backward(loss: torch.Tensor) -> None:
+    """``loss.backward()`` seeded with :func:`unit_grad` (scalar losses)."""
+    loss.backward(unit_grad(loss) if loss.dim() == 0 and loss.is_floating_point() else None)
+
+
 def _xent_rows(lg, labels, smoothing, want_correct):
     """One pass of the fused kernel: (per-block loss partials -- or, with one block, the mean
     loss itself --, d(logits) with 1/B folded in, per-row top-1 hits or None)."""
@@ -57,11 +84,13 @@ class SoftmaxXentFn(torch.autograd.Function):
             _, base, _ = _xent_rows(lg, labels, ctx.smoothing, False)
             return (base * dloss.to(base.dtype)).to(ctx.in_dtype), None, None, None
         ctx.scaled = True
-        # scale the stored d(logits) in place by dloss -- a near-empty launch when dloss == 1
-        # (every plain loss.backward()): the device-side check needs no host sync
-        s = dloss.detach().float().reshape(1).contiguous()
-        _native.kernels().scale_unless_one(dlog.data_ptr(), int(dlog.dtype == torch.bfloat16), s.data_ptr(),
-                                           dlog.numel(), _native.stream(dlog))
+        # scale the stored d(logits) in place by dloss -- nothing at all for the unit seed
+        # (loss.backward(unit_grad(loss))), else a near-empty launch when dloss == 1 (a plain
+        # loss.backward()): the device-side check needs no host sync
+        if not is_unit(dloss):
+            s = dloss.detach().float().reshape(1).contiguous()
+            _native.kernels().scale_unless_one(dlog.data_ptr(), int(dlog.dtype == torch.bfloat16), s.data_ptr(),
+                                               dlog.numel(), _native.stream(dlog))
         return dlog.to(ctx.in_dtype), None, None, None
 
 

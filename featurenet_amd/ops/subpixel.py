@@ -402,8 +402,11 @@ class SubpixelDecoderHeadXentFn(torch.autograd.Function):
 
         dlog = ctx.saved_tensors[5]
         # d(logits) carries 1/M; scale by dloss in place -- a near-empty launch when dloss == 1
-        s = dloss.detach().float().reshape(1).contiguous()
-        _native.kernels().scale_unless_one(dlog.data_ptr(), 1, s.data_ptr(), dlog.numel(), _native.stream(dlog))
+        from .loss import is_unit
+
+        if not is_unit(dloss):                   # (the unit seed: nothing to scale)
+            s = dloss.detach().float().reshape(1).contiguous()
+            _native.kernels().scale_unless_one(dlog.data_ptr(), 1, s.data_ptr(), dlog.numel(), _native.stream(dlog))
         g = _head_backward(_SavedView(ctx), dlog)
         return g + (None, None)
 
@@ -453,8 +456,11 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         K = y.shape[-1]
         NC = hw.shape[0]
         y2 = y.reshape(-1, K)
+        from .loss import is_unit
+
         s = dloss.detach().float().reshape(1).contiguous()
-        _native.kernels().scale_unless_one(dz.data_ptr(), 1, s.data_ptr(), dz.numel(), _native.stream(dz))
+        if not is_unit(dloss):
+            _native.kernels().scale_unless_one(dz.data_ptr(), 1, s.data_ptr(), dz.numel(), _native.stream(dz))
         tot = part[:, 2:].sum(0) * s                  # [db 32 | dWt 32 x 32 | msum 32 | msq 32], x dloss
         dhw = dhb = None
         if ctx.needs_input_grad[9]:

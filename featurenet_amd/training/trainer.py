@@ -30,6 +30,7 @@ import torch.distributed as dist
 
 from .. import _native
 from ..ops import FlatAdam, FlatSGD, softmax_xent
+from ..ops.loss import backward as loss_backward
 from ..parallel.ddp import DistributedFailure, GradBucketer
 from ..utils.events import default_log
 from .callbacks import Callback
@@ -192,7 +193,7 @@ class Trainer:
     def _eager_step(self, xb: torch.Tensor, yb: torch.Tensor):
         self.flat.zero_grad()
         loss, correct = self._loss(xb, yb)
-        loss.backward()
+        loss_backward(loss)
         try:
             scale = self.bucketer.finish()
         except DistributedFailure as e:              # fail fast: log and let the process exit non-zero
@@ -229,7 +230,7 @@ class Trainer:
             with torch.cuda.graph(g):
                 self.flat.zero_grad()
                 loss, correct = self._loss(self._sx, self._sy)
-                loss.backward()
+                loss_backward(loss)
                 self.bucketer.finish()
                 self.opt.step_device()
                 self._gloss, self._gcorr = loss.detach(), correct
