@@ -375,15 +375,16 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     // keeps the halo reads interleaved with the MFMAs (with a wave-uniform offset it
     // hoisted a turn's reads into a double-buffered block)
     auto kofs = [&](int k) -> int { return *((const int*)(s_kt + KTW * k + (KTW - 1)) + lg); };
-    auto kofs_s = [&](int k) -> int { return *((const int*)(s_kt + KTW * k) + lg); };   // (BS: scale tap)
-    // BS: the scale of fragment mt's rows at k-step scale offset ko (the dword of the row's tap
-    // position, its block byte shifted down).  lb[mt] = 16 row + halo plane + buffer, ko = 16 tap:
-    // (lb + ko) / 4 is the dword index 4 (row + tap) plus terms scl_job takes back off.  One byte
+    // (BS: the scale tap, as kq = the lane's scale byte base + tap / 4 -- read_s adds lb / 4)
+    auto kofs_s = [&](int k) -> int { return scl_job + (*((const int*)(s_kt + KTW * k) + lg) >> 2); };
+    // BS: the scale of fragment mt's rows at k-step scale base ko = kq (kofs_s: the byte of the
+    // row's tap position dword).  lb[mt] = 16 row + halo plane + buffer, tap offsets 16 tap:
+    // lb / 4 + tap / 4 is the dword index 4 (row + tap) plus terms scl_job takes back off.  One byte
     // read (ds_read_u8, zero-extended: the MFMA takes the low byte), no shift after it -- a shift
     // right behind each read made hipcc wait for every scale read on the spot (lgkmcnt(0) per
     // fragment: the block-scaled kernel ran 1.47x the per-tensor one)
     auto read_s = [&](int mt, int ko) -> unsigned {
-      if constexpr (F8 && BS) return *(const unsigned char*)(dsm + scl_job + ((lb[mt] + ko) >> 2));
+      if constexpr (F8 && BS) return *(const unsigned char*)(dsm + ko + (lb[mt] >> 2));   // (ko: kq, below)
       else return 127u;
     };
     // epilogue variant (wave-uniform); columns come in whole 8-column groups (Ncol % 8 == 0)

@@ -495,17 +495,18 @@ extern "C" int fn_adam_flat(float* p, const float* g, float* m, float* v, void* 
 
 // Graph-capturable Adam: hyper-parameters and the step counter live in device
 // memory, so a captured training step replays with the current lr / step.
-// hp = {lr, b1, b2, eps, wd, grad_scale}; t = {step, finished blocks}: every block runs step
-// t[0] + 1, and the last block to finish stores it back (and re-zeroes the count) -- after
-// every block has read t[0] (no separate increment launch before this one)
+// hp = {lr, b1, b2, eps, wd, grad_scale}; *t is incremented by the 1-thread kernel that
+// precedes this one in the same stream.  (A finished-block count with the last block storing the
+// step back, to save that launch, serialised 8192 same-address atomics: 40 -> 407 us.)
+__global__ void step_inc_kernel(int* t) { *t += 1; }
+
 __global__ __launch_bounds__(256) void adam_flat_dev_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                             float* __restrict__ m, float* __restrict__ v,
                                                             bf16* __restrict__ pb, long long n,
-                                                            const float* __restrict__ hp, int* __restrict__ t,
+                                                            const float* __restrict__ hp, const int* __restrict__ t,
                                                             int keras_eps) {
   const float lr = hp[0], b1 = hp[1], b2 = hp[2], eps = hp[3], wd = hp[4], gscale = hp[5];
-  const int step = t[0] + 1;
-  const float tf = (float)step;
+  const float tf = (float)*t;
   const float bc1 = 1.f - powf(b1, tf), bc2 = 1.f - powf(b2, tf);
   const float rb2 = rsqrtf(bc2);
   const float lr_t = lr * sqrtf(bc2) / bc1;
@@ -521,18 +522,11 @@ __global__ __launch_bounds__(256) void adam_flat_dev_kernel(float* __restrict__ 
     p[i] = pi;
     if (pb) pb[i] = f2bf(pi);
   }
-  __syncthreads();                               // (every thread of the block has read t[0])
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(t + 1, 1) == (int)gridDim.x - 1) {
-      t[0] = step;
-      t[1] = 0;
-    }
-  }
 }
 
 extern "C" int fn_adam_flat_dev(float* p, const float* g, float* m, float* v, void* pb, long long n, const float* hp,
                                 int* t, int keras_eps, hipStream_t st) {
+  hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, t);
   hipLaunchKernelGGL(adam_flat_dev_kernel, dim3(blocks_for(n)), dim3(256), 0, st, p, g, m, v, (bf16*)pb, n, hp, t,
                      keras_eps);
   FN_CHECK_LAUNCH();

@@ -43,9 +43,7 @@ class FlatAdam:
         if self._dev is None:
             hp = torch.tensor([self.lr, self.b1, self.b2, self.eps, self.wd, self._gscale], dtype=torch.float32,
                               device=self.p.device)
-            # [step, finished-block count]: the Adam kernel's last block advances the step (no
-            # separate increment launch; misc.hip adam_flat_dev_kernel)
-            t = torch.tensor([self.t, 0], dtype=torch.int32, device=self.p.device)
+            t = torch.tensor([self.t], dtype=torch.int32, device=self.p.device)
             self._dev = (hp, t)
             self._pushed = self._host_hp()
         else:
@@ -112,7 +110,7 @@ class FlatAdam:
         self.t = int(sd["t"])
         self.lr = float(sd.get("lr", self.lr))
         if self._dev is not None:
-            self._dev[1][0].fill_(self.t)
+            self._dev[1].fill_(self.t)
             self.sync_device_state()
 
 

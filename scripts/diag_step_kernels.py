@@ -50,15 +50,18 @@ def main():
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
         step()
         torch.cuda.synchronize()
-    # map each device kernel to its launching CPU op's stack (correlation through the profiler's
-    # event tree: a kernel is a child of the runtime launch event whose parent chain has the stack)
+    # each kernel under the innermost op that launched it (its CPU event), in launch order
     evs = prof.profiler.function_events
     rows = []
     for e in evs:
+        if not e.kernels:
+            continue
+        if any(c.kernels for c in e.cpu_children):
+            continue                              # (a parent op: its children carry the kernels)
+        stack = [s for s in (e.stack or []) if ("featurenet_amd" in s or "bench" in s or "scripts" in s)]
+        where = stack[0] if stack else ""
         for k in e.kernels:
-            stack = [s for s in (e.stack or []) if ("featurenet_amd" in s or "bench" in s or "scripts" in s)]
-            where = stack[0] if stack else (e.name)
-            rows.append((k.time_range.start, k.name, k.duration, e.name, where))
+            rows.append((e.time_range.start, k.name, k.duration, e.name, where))
     rows.sort()
     tot = 0.0
     for _, name, dur, op, where in rows:

@@ -22,6 +22,6 @@ run infer_block 300 python bench/infer_fp8.py --size 128 --batch 1024 --chunk 10
 FN_F8_BLOCK=0 run infer_tensor 300 python bench/infer_fp8.py --size 128 --batch 1024 --chunk 1024 --only fp8
 rc=$?; if fatal $rc; then exit $rc; fi
 for s in ${SEEDS:-0 1 2 3}; do
-  run acc_seed$s 400 python bench/accuracy.py --fp8 --seed $s; rc=$?; if fatal $rc; then exit $rc; fi
+  run acc_seed$s 400 python bench/accuracy.py --fp8 --epochs 16 --train-per-class 1000 --seed $s; rc=$?; if fatal $rc; then exit $rc; fi
 done
 exit 0
