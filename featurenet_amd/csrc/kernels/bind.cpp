@@ -16,7 +16,8 @@ namespace py = pybind11;
 
 extern "C" {
 int fn_igemm_fwd(const void*, const void*, const float*, void*, float*, const int*, const int*, long long, int, int,
-                 int, int, int, hipStream_t);
+                 int, int, int, hipStream_t, float*, int);
+int fn_igemm_fwd_splits(long long, int, int);
 int fn_igemm_fwd_mblocks(long long);
 int fn_conv_halo(const void*, const void*, const float*, void*, float*, const int*, const int*, int, int, int*,
                  hipStream_t);
@@ -203,13 +204,21 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "featurenet_amd gfx950 HIP kernels";
   m.attr("ARCH") = "gfx950";
 
+  // part / splits (optional): the split-K form (fn_igemm_fwd_splits), part = splits x M x N floats
   m.def("igemm_fwd", [](uintptr_t src, uintptr_t wt, uintptr_t bias, uintptr_t out, uintptr_t stats, uintptr_t tab,
-                        std::vector<int> geom, long long M, int N, int K, int ldw, int vec, int act, uintptr_t st) {
+                        std::vector<int> geom, long long M, int N, int K, int ldw, int vec, int act, uintptr_t st,
+                        uintptr_t part, int splits, long long part_elems) {
     need(geom, 14, "igemm_fwd");
+    if (splits > 1 && part_elems < (long long)splits * M * N)
+      throw std::runtime_error("igemm_fwd: part has " + std::to_string(part_elems) + " elements, split-K needs " +
+                               std::to_string((long long)splits * M * N));
     chk(fn_igemm_fwd(P<const void*>(src), P<const void*>(wt), P<const float*>(bias), P<void*>(out), P<float*>(stats),
-                     P<const int*>(tab), geom.data(), M, N, K, ldw, vec, act, S(st)),
+                     P<const int*>(tab), geom.data(), M, N, K, ldw, vec, act, S(st), P<float*>(part), splits),
         "igemm_fwd");
-  });
+  }, py::arg("src"), py::arg("wt"), py::arg("bias"), py::arg("out"), py::arg("stats"), py::arg("tab"), py::arg("geom"),
+     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("ldw"), py::arg("vec"), py::arg("act"), py::arg("st"),
+     py::arg("part") = 0, py::arg("splits") = 1, py::arg("part_elems") = 0);
+  m.def("igemm_fwd_splits", &fn_igemm_fwd_splits);
   m.def("igemm_fwd_mblocks", &fn_igemm_fwd_mblocks);
   m.def("conv_halo", [](uintptr_t src, uintptr_t wt, uintptr_t bias, uintptr_t out, uintptr_t stats,
                         uintptr_t toffs, std::vector<int> geom, int ncol, int act, uintptr_t sched, uintptr_t st,

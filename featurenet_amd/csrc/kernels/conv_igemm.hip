@@ -146,11 +146,17 @@ __device__ __forceinline__ int4 entry_for(const int4* __restrict__ tab, int k0, 
 #define FWD_BM 256
 #define FWD_BK 64
 
-template <int BN, int GM, int ACT, bool HAS_BIAS, bool STATS>
+// SPLIT (split-K, ACT_NONE / no bias / no stats): workgroup z takes k-stages [z * spz, (z+1) * spz)
+// and writes its fp32 partial tile to part[z][M][Ncol] straight from the accumulators; the slices
+// are added in slice order by dense_fwd_reduce_kernel (+ bias, activation, bf16).  For the small-M,
+// deep-K layers of NAS candidates (the dgrad of a 5x5x16 -> 120 LeNet conv: 7 row blocks for a
+// 3000-deep reduction ran 67 us on 7 CUs)
+template <int BN, int GM, int ACT, bool HAS_BIAS, bool STATS, bool SPLIT = false>
 __global__ __launch_bounds__(256, (BN >= 64 || GM != GM_VEC ? 3 : 4)) void igemm_fwd_kernel(
     const bf16* __restrict__ src, const bf16* __restrict__ wt, const float* __restrict__ bias,
     bf16* __restrict__ out, float* __restrict__ stats, const int4* __restrict__ tab, GatherGeom g,
-    long long M, int Ncol, int Kdim, int ldw) {
+    long long M, int Ncol, int Kdim, int ldw, float* __restrict__ part = nullptr, int spz = 0) {
+  static_assert(!SPLIT || (ACT == ACT_NONE && !HAS_BIAS && !STATS), "split-K: the reduce applies bias / act");
   constexpr int A_STAGE = FWD_BM * FWD_BK;      // elements
   constexpr int B_STAGE = BN * FWD_BK;
   constexpr int LDO = BN + 8;                   // epilogue staging row (16-B aligned)
@@ -214,16 +220,18 @@ __global__ __launch_bounds__(256, (BN >= 64 || GM != GM_VEC ? 3 : 4)) void igemm
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (Kdim + FWD_BK - 1) / FWD_BK;
-  fetch_entries(0);
-  load_stage(0);
-  if (nk > 1) fetch_entries(1);
+  const int nk_all = (Kdim + FWD_BK - 1) / FWD_BK;
+  const int kt0 = SPLIT ? (int)blockIdx.z * spz : 0;
+  const int nk = SPLIT ? min(nk_all, kt0 + spz) : nk_all;   // (stage index range [kt0, nk))
+  fetch_entries(kt0);
+  load_stage(kt0);
+  if (nk > kt0 + 1) fetch_entries(kt0 + 1);
   write_stage();
   __syncthreads();
 
   const int lr = lane & 15;     // row inside a 16-row fragment
   const int lg = lane >> 4;     // k-group (8 elements each)
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = kt0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) {
       load_stage(kt + 1);                 // gathers in flight during the MFMAs below
@@ -256,6 +264,21 @@ __global__ __launch_bounds__(256, (BN >= 64 || GM != GM_VEC ? 3 : 4)) void igemm
     }
   }
 
+  if constexpr (SPLIT) {                        // fp32 partial tile, straight from the accumulators
+    float* ps = part + (long long)blockIdx.z * M * Ncol;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int col = n0 + nt * 16 + lr;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long long m = m0 + wave * 64 + mt * 16 + lg * 4 + r;
+          if (m < M && col < Ncol) ps[m * Ncol + col] = acc[mt][nt][r];
+        }
+    }
+    return;
+  }
   // ---- epilogue: bias + activation, bf16 staging in LDS, BN partial stats ----
   bf16* Os = smem;  // reuse the A stage (all waves passed the final barrier)
   float csum[NT], csq[NT];
@@ -564,9 +587,24 @@ static void launch_fwd_bn(dim3 grid, hipStream_t st, const bf16* src, const bf16
 #undef FWD_ARGS
 }
 
+extern "C" int fn_dense_fwd_reduce(const float* part, const float* bias, void* out, int M, int N, int S, int act,
+                                   int out_fp32, hipStream_t st);
+
+// k-slices of the split-K form for (M, Ncol, Kdim): enough workgroups for the 256 CUs, >= 4
+// k-stages per slice, 1 = no split (the caller sizes part = splits x M x Ncol floats)
+extern "C" int fn_igemm_fwd_splits(long long M, int Ncol, int Kdim) {
+  const int BN = Ncol <= 16 ? 16 : (Ncol <= 32 ? 32 : 64);
+  const long long tiles = (M + FWD_BM - 1) / FWD_BM * ((Ncol + BN - 1) / BN);
+  const int nk = (Kdim + FWD_BK - 1) / FWD_BK;
+  if (tiles >= 128 || nk < 8) return 1;
+  int s = (int)((256 + tiles - 1) / tiles);
+  if (s > nk / 4) s = nk / 4;
+  return s < 2 ? 1 : s;
+}
+
 extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, void* out, float* stats,
                             const int* tab, const int* geom14, long long M, int Ncol, int Kdim, int ldw, int gm,
-                            int act, hipStream_t st) {
+                            int act, hipStream_t st, float* part, int splits) {
   const GatherGeom g = parse_geom(geom14);
   if (stats && act != ACT_NONE) return -1;  // stats are taken on the pre-BN output
   if (ldw % 8 != 0) return -3;
@@ -577,6 +615,27 @@ extern "C" int fn_igemm_fwd(const void* src, const void* wt, const float* bias, 
   const bf16* w = (const bf16*)wt;
   bf16* o = (bf16*)out;
   const int4* t = (const int4*)tab;
+  if (splits > 1 && !stats) {
+    if (!part) return -6;
+    const int nk = (Kdim + FWD_BK - 1) / FWD_BK;
+    const int spz = (nk + splits - 1) / splits;
+    const int sr = (nk + spz - 1) / spz;        // slices actually covering the k-stages
+    grid.z = (unsigned)sr;
+#define SPLIT_CASE(BNV, GMV)                                                                              \
+  hipLaunchKernelGGL((igemm_fwd_kernel<BNV, GMV, ACT_NONE, false, false, true>), grid, dim3(256), 0, st, s, w, \
+                     nullptr, o, nullptr, t, g, M, Ncol, Kdim, ldw, part, spz)
+#define SPLIT_GM(GMV)                                                                                     \
+  do {                                                                                                  \
+    if (BN == 16) SPLIT_CASE(16, GMV); else if (BN == 32) SPLIT_CASE(32, GMV); else SPLIT_CASE(64, GMV);   \
+  } while (0)
+    if (gm == GM_VEC) SPLIT_GM(GM_VEC);
+    else if (gm == GM_PACKW) SPLIT_GM(GM_PACKW);
+    else SPLIT_GM(GM_SCALAR);
+#undef SPLIT_GM
+#undef SPLIT_CASE
+    FN_CHECK_LAUNCH();
+    return fn_dense_fwd_reduce(part, bias, out, (int)M, Ncol, sr, act, 0, st);
+  }
 #define FWD_GM(GMV)                                                                                      \
   do {                                                                                                   \
     if (BN == 16) launch_fwd_bn<16, GMV>(grid, st, s, w, bias, o, stats, t, g, M, Ncol, Kdim, ldw, act);      \

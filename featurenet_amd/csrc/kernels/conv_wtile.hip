@@ -555,11 +555,52 @@ __global__ __launch_bounds__(256) void wtile_reduce_kernel(const float* __restri
   }
 }
 
+// Few outputs, many slices (the small layers of NAS candidates: a 4K-element dW over 1K
+// partial rows ran 23 us in the 256-element blocks above, each thread walking a quarter of
+// the rows): E elements per block, the 256 / E thread groups take every (256 / E)-th row, then
+// the groups' sums are added in group order -- fixed for a given (n, W), so still repeatable.
+template <int E>
+__global__ __launch_bounds__(256) void part_reduce_narrow_kernel(const float* __restrict__ part, float* __restrict__ dst,
+                                                                 long long n, int W, int accumulate) {
+  constexpr int G = 256 / E;
+  __shared__ float s_r[G][E];
+  const int e = threadIdx.x % E, gq = threadIdx.x / E;
+  const long long i = (long long)blockIdx.x * E + e;
+  float a0 = 0.f, a1 = 0.f;
+  if (i < n) {
+    int p = gq;
+    for (; p + G < W; p += 2 * G) {
+      a0 += part[(long long)p * n + i];
+      a1 += part[(long long)(p + G) * n + i];
+    }
+    if (p < W) a0 += part[(long long)p * n + i];
+  }
+  s_r[gq][e] = a0 + a1;
+  __syncthreads();
+  if (threadIdx.x < E && i < n) {
+    float r = accumulate ? dst[i] : 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) r += s_r[g][threadIdx.x];
+    dst[i] = r;
+  }
+}
+
 extern "C" int fn_part_reduce_wdot(const float* part, float* dst, long long n, int W, int accumulate,
                                   const float* wsrc, float* wdp, int C, hipStream_t st) {
   if (n <= 0) return 0;
   if (!part || !dst || W < 1) return -6;
   if (wsrc && (!wdp || C < 1 || 256 % C || n % C)) return -2;
+  if (!wsrc && W >= 16 && (n + 255) / 256 < 192) {   // (narrow form: at least ~192 blocks)
+    if (n <= 192 * 16) {
+      hipLaunchKernelGGL(part_reduce_narrow_kernel<16>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, part, dst,
+                         n, W, accumulate);
+    } else {
+      hipLaunchKernelGGL(part_reduce_narrow_kernel<64>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, dst,
+                         n, W, accumulate);
+    }
+    FN_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(wtile_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, dst, n, W,
                      accumulate, wsrc, wdp, C);
   FN_CHECK_LAUNCH();

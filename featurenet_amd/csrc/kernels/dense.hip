@@ -349,7 +349,7 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
                                                                  const bf16* __restrict__ ya, int act) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dn_lds[];
   // split over the batch (blockIdx.z = slice of mc rows -> its own dW / db slab, summed by
-  // dense_wgrad_reduce_kernel in a fixed order) so small dW tiles still fill the GPU
+  // fn_part_reduce in a fixed order) so small dW tiles still fill the GPU
   const int mz0 = blockIdx.z * mc, mz1 = min(M, mz0 + mc);
   dw += (long long)blockIdx.z * N * K;
   if (db) db += (long long)blockIdx.z * N;
@@ -490,6 +490,17 @@ static void dn_fwd(const void* x, const void* w, const float* bias, void* out, f
                      (const float*)part, bias, out, M, N, Sr, act, out_fp32);
 }
 
+// y = act(sum of S fp32 slabs [S][M][N] + b) -> bf16 (or fp32), slices added in order
+extern "C" int fn_dense_fwd_reduce(const float* part, const float* bias, void* out, int M, int N, int S, int act,
+                                   int out_fp32, hipStream_t st) {
+  const long long tot = (long long)M * N;
+  if (tot <= 0) return 0;
+  hipLaunchKernelGGL(dense_fwd_reduce_kernel, dim3((unsigned)((tot + 63) / 64)), dim3(DN_THREADS), 0, st, part, bias,
+                     out, M, N, S, act, out_fp32);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
 // w: fp32 [N][K] (training: the master weights) or, wbf16, a bf16 copy (inference)
 extern "C" int fn_dense_fwd(const void* x, const void* w, const float* bias, void* out, float* part, int M, int N,
                             int K, int S, int act, int out_fp32, int wbf16, hipStream_t st) {
@@ -530,16 +541,6 @@ extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, in
   return 0;
 }
 
-// sum of S fp32 slabs [S][n] -> out[n] in slice order (deterministic)
-__global__ __launch_bounds__(256) void dense_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                                 long long n, int S) {
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    float v = 0.f;
-    for (int z = 0; z < S; ++z) v += part[(long long)z * n + i];
-    out[i] = v;
-  }
-}
-
 // batch slices of the weight gradient: enough (dW tile, slice) workgroups for the 256 CUs, at
 // least 128 rows per slice (a 128-row batch -- FeatureNet-3D's FC layers -- stays one launch)
 extern "C" int fn_dense_wgrad_slices(int M, int N, int K) {
@@ -575,15 +576,9 @@ extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db
                        (const bf16*)g, (const bf16*)x, pdw, pdb, M, N, K, mc, (const bf16*)ya, act);
   }
   FN_CHECK_LAUNCH();
-  if (S > 1) {
-    hipLaunchKernelGGL(dense_wgrad_reduce_kernel, dim3((unsigned)((NK + 255) / 256 < 2048 ? (NK + 255) / 256 : 2048)),
-                       dim3(256), 0, st, (const float*)part, dw, NK, S);
-    FN_CHECK_LAUNCH();
-    if (db) {
-      hipLaunchKernelGGL(dense_wgrad_reduce_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st,
-                         (const float*)(part + (long long)S * NK), db, (long long)N, S);
-      FN_CHECK_LAUNCH();
-    }
+  if (S > 1) {                                   // (fixed slice order: fn_part_reduce, overwrite)
+    if (int e = fn_part_reduce(part, dw, NK, S, 0, st)) return e;
+    if (db) return fn_part_reduce(part + (long long)S * NK, db, (long long)N, S, 0, st);
   }
   return 0;
 }

@@ -432,10 +432,19 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
     if want_stats:
         nmb = K.igemm_fwd_mblocks(spec.M)
         stats = torch.empty(nmb, 2, spec.K, dtype=torch.float32, device=x5.device)
-    K.igemm_fwd(x5.data_ptr(), wmat.data_ptr(), _native.ptr(bias), y.data_ptr(), _native.ptr(stats),
-                tab.data_ptr(), _geom_fwd(spec), spec.M, spec.K, kdim_gather(spec), ldw, gm, act,
-                _native.stream(x5))
+    _igemm_fwd_call(K, x5, wmat, bias, y, stats, tab, _geom_fwd(spec), spec.M, spec.K, kdim_gather(spec), ldw, gm,
+                    act)
     return y, stats
+
+
+def _igemm_fwd_call(K, src, wt, bias, out, stats, tab, geom, M, N, kdim, ldw, gm, act):
+    """igemm_fwd, in its split-K form (fp32 partial slabs, one reduce launch) where few row
+    blocks meet a deep reduction and no statistics are wanted (``fn_igemm_fwd_splits``)."""
+    splits = 1 if stats is not None else int(K.igemm_fwd_splits(M, N, kdim))
+    part = part_scratch(splits * M * N, src.device) if splits > 1 else None
+    K.igemm_fwd(src.data_ptr(), wt.data_ptr(), _native.ptr(bias), out.data_ptr(), _native.ptr(stats), tab.data_ptr(),
+                geom, M, N, kdim, ldw, gm, act, _native.stream(src), _native.ptr(part), splits,
+                0 if part is None else part.numel())
 
 
 def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=None, wpk=None):
@@ -481,8 +490,7 @@ def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=Non
         wt, ldw = _pack_rows(wt)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     M = spec.N * spec.D * spec.H * spec.W
-    K.igemm_fwd(dy5.data_ptr(), wt.data_ptr(), 0, dx.data_ptr(), 0, tab.data_ptr(), _geom_dgrad(spec), M, spec.C,
-                spec.taps * spec.K, ldw, vec, 0, _native.stream(dy5))
+    _igemm_fwd_call(K, dy5, wt, None, dx, None, tab, _geom_dgrad(spec), M, spec.C, spec.taps * spec.K, ldw, vec, 0)
     return dx
 
 

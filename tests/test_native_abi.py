@@ -43,7 +43,7 @@ class _FakeK:
         def f(*args):
             assert lo <= len(args) <= hi, f"{name}: called with {len(args)} args, binding takes {lo}..{hi}"
             self.calls.append(name)
-            if name.endswith(("_lds", "mblocks", "_workers", "_blocks", "_yblocks", "_gx", "_part")):
+            if name.endswith(("_lds", "mblocks", "_workers", "_blocks", "_yblocks", "_gx", "_part", "_splits")):
                 return 1
             return None
         return f
