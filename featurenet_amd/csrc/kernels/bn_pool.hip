@@ -1330,6 +1330,9 @@ extern "C" int fn_pool_bwd(const void* dout, const void* x, void* dx, const floa
   if (g.C % 8 == 0)
     hipLaunchKernelGGL(pool_bwd_kernel<8>, dim3(ew_blocks(ins * (g.C / 8))), dim3(256), 0, st, (const bf16*)dout,
                        (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, count_pad, act);
+  else if (g.C % 2 == 0)                         // (channel pairs: the window walk once per two, e.g.
+    hipLaunchKernelGGL(pool_bwd_kernel<2>, dim3(ew_blocks(ins * (g.C / 2))), dim3(256), 0, st,   // LeNet's 18)
+                       (const bf16*)dout, (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, count_pad, act);
   else
     hipLaunchKernelGGL(pool_bwd_kernel<1>, dim3(ew_blocks(ins * g.C)), dim3(256), 0, st, (const bf16*)dout,
                        (const bf16*)x, (bf16*)dx, scale, shift, g, is_max, count_pad, act);

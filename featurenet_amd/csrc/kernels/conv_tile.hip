@@ -1049,7 +1049,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     CT_DBG(1, 1) CT_DBG(1, 2) CT_DBG(1, 4) CT_DBG(1, 16)   // (the space-to-depth stem)
     CT_DBG(1, 8) CT_DBG(1, 24) CT_DBG(2, 8) CT_DBG(2, 24)
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
-    CT_DBG(4, 23) CT_DBG(2, 32) CT_DBG(4, 32)
+    CT_DBG(4, 23) CT_DBG(2, 32) CT_DBG(4, 32) CT_DBG(4, 1) CT_DBG(4, 2) CT_DBG(4, 3) CT_DBG(4, 4) CT_DBG(4, 8)
     CT_DBG(2, 64) CT_DBG(2, 128) CT_DBG(2, 192) CT_DBG(4, 64) CT_DBG(4, 128) CT_DBG(4, 192)   // (correct results)
 #undef CT_DBG
     if (rc) return rc;

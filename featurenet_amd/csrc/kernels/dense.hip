@@ -33,6 +33,38 @@ __device__ __forceinline__ bf16x8 dn_cvt8(const float4 a, const float4 b) {
   return v;
 }
 
+// 8 consecutive bf16 of a row of n elements from column c (zeros past n), as wide as the row
+// pitch allows: one 16-B load (n % 8 == 0), two 8-B loads (n % 4 == 0: the 84-wide Dense of the
+// LeNet template, whose element loads ran its dgrad at 30 us), 4-B loads (n even), else elements
+__device__ inline bf16x8 dn_load8(const bf16* __restrict__ row, int c, int n) {
+  bf16x8 v = {};
+  if ((n & 7) == 0 && c + 8 <= n) return *(const bf16x8*)(row + c);
+  if ((n & 3) == 0) {
+    if (c + 4 <= n) {
+      const bf16x4 a = *(const bf16x4*)(row + c);
+      v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    }
+    if (c + 8 <= n) {
+      const bf16x4 b = *(const bf16x4*)(row + c + 4);
+      v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+    }
+    return v;
+  }
+  if ((n & 1) == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; e += 2)
+      if (c + e + 2 <= n) {
+        const unsigned u = *(const unsigned*)(row + c + e);
+        v[e] = __builtin_bit_cast(bf16, (unsigned short)(u & 0xffffu));
+        v[e + 1] = __builtin_bit_cast(bf16, (unsigned short)(u >> 16));
+      }
+    return v;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = c + e < n ? row[c + e] : f2bf(0.f);
+  return v;
+}
+
 // ---------------------------------------------------------------------------
 // forward: split-K partials
 // ---------------------------------------------------------------------------
@@ -292,22 +324,10 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + j * 16 + r;
       const bf16* grow = g + (long long)(m < M ? m : 0) * N;
-      bf16x8 v = zero8;
-      if (vec) {
-        v = *(const bf16x8*)(grow + nc);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = nc + e < N ? grow[nc + e] : f2bf(0.f);
-      }
+      bf16x8 v = vec ? *(const bf16x8*)(grow + nc) : dn_load8(grow, nc, N);
       if (ya) {
         const bf16* yrow = ya + (long long)(m < M ? m : 0) * N;
-        bf16x8 yv = zero8;
-        if (vec) {
-          yv = *(const bf16x8*)(yrow + nc);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) yv[e] = nc + e < N ? yrow[nc + e] : f2bf(0.f);
-        }
+        const bf16x8 yv = vec ? *(const bf16x8*)(yrow + nc) : dn_load8(yrow, nc, N);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = f2bf(bf2f(v[e]) * act_bwd_from_out(bf2f(yv[e]), act));
       }
@@ -384,23 +404,13 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
       } else {
         if (!xq) {
           vx.u = make_uint4(0u, 0u, 0u, 0u);
-        } else if ((K & 7) == 0 && kk + 8 <= K) {   // 16-B aligned rows only when K % 8 == 0
-          vx.u = *(const uint4*)(x + (long long)m * K + kk);
-        } else {
-          for (int e = 0; e < 8; ++e) vx.e[e] = kk + e < K ? x[(long long)m * K + kk + e] : f2bf(0.f);
+        } else {                                 // (16-B loads when K % 8 == 0, narrower otherwise)
+          vx.v = dn_load8(x + (long long)m * K, kk, K);
         }
-        if ((N & 7) == 0 && n + 8 <= N) {
-          vg.u = *(const uint4*)(g + (long long)m * N + n);
-        } else {
-          for (int e = 0; e < 8; ++e) vg.e[e] = n + e < N ? g[(long long)m * N + n + e] : f2bf(0.f);
-        }
+        vg.v = dn_load8(g + (long long)m * N, n, N);
         if (ya) {                                // g = dy * act'(y) (see dense_dgrad_kernel)
           Pack8 vy;
-          if ((N & 7) == 0 && n + 8 <= N) {
-            vy.u = *(const uint4*)(ya + (long long)m * N + n);
-          } else {
-            for (int e = 0; e < 8; ++e) vy.e[e] = n + e < N ? ya[(long long)m * N + n + e] : f2bf(0.f);
-          }
+          vy.v = dn_load8(ya + (long long)m * N, n, N);
 #pragma unroll
           for (int e = 0; e < 8; ++e) vg.e[e] = f2bf(bf2f(vg.e[e]) * act_bwd_from_out(bf2f(vy.e[e]), act));
         }

@@ -79,7 +79,11 @@ def main():
         for kk, (pl, fn) in runs.items():
             if pl is None or (args.tile_only and kk.startswith("halo")):
                 continue
-            res[kk + "_us"] = round(timeit(fn, args.reps), 1)
+            try:
+                res[kk + "_us"] = round(timeit(fn, args.reps), 1)
+            except RuntimeError as e:                # (e.g. no timing instance of this variant)
+                res[kk + "_error"] = str(e).splitlines()[-1][:80]
+                continue
             res[kk + "_tflops"] = round(gf / res[kk + "_us"] * 1e3, 1)
         rows.append(res)
         print(json.dumps(res), flush=True)

@@ -9,9 +9,10 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 FN_BUILD_EXPERIMENTS=1 timeout -k 10 600 python -m featurenet_amd._build > gpurun_out/build_exp.log 2>&1 || { tail gpurun_out/build_exp.log; exit 1; }
-for d in ${DBGS:-0 16 1 2 4 8 32 64 128}; do
+for d in ${DBGS:-0 1 2 3 4 8 32 64 128}; do
   FN_TILE_DBG=$d timeout -k 10 180 python -u scripts/bench_conv_layers.py --batch 128 --reps 3 --tile-only \
     > gpurun_out/budget_$d.log 2>&1 || { echo "dbg $d failed"; tail -5 gpurun_out/budget_$d.log; exit 1; }
+  [ "$d" = 0 ] && cp gpurun_out/budget_0.log gpurun_out/budget_base.log
   echo "== dbg=$d"
   grep -o '"layer": "[a-z0-9_]*"\|"tile_[a-z_]*_us": [0-9.]*\|\[conv_tile stamps.*' gpurun_out/budget_$d.log | tr '\n' ' '
   echo
