@@ -747,7 +747,8 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16* __restrict__ 
       for (int j = 0; j < 8; ++j) p.e[j] = f2bf(gacc[j]);
       *(uint4*)(dx + i * 8) = p.u;
     } else {
-      dx[i] = f2bf(gacc[0]);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) dx[i * VW + j] = f2bf(gacc[j]);
     }
   }
 }

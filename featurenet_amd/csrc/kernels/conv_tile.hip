@@ -65,8 +65,12 @@
 //   each job's halo and every MFMA takes as its B-operand scale (the halo is the B operand); with an
 //   e4m3 output (F8 fp8 output, or Q8O) the epilogue scales every (position, 32-column block) by its
 //   own power of two and writes the scale byte into osc (the same dword-per-position layout)
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false>
-__global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
+// NCW: compute waves (4: one per SIMD, MT fragments each; 8: two per SIMD at MT / 2 -- the same
+// 4 * 8 fragment rows, so the same row tables -- where a partner wave can issue while the other
+// waits: the one-wave-per-SIMD k-loop ran its MFMAs at 72 % of its cycles)
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false,
+          int NCW = CT_NCW>
+__global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
                                                                const int4* __restrict__ ktab,
@@ -81,6 +85,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
                                                                unsigned char* __restrict__ osc) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   static_assert(!BS || F8 || Q8O, "block scales: fp8 operands or an e4m3 output");
+  constexpr int NTHR = 64 * (NCW + 1);
   constexpr int PD = ct_pd(NT, F8);
   constexpr int ESZ = F8 ? 1 : 2;                // bytes per element of the source / weights
   constexpr int FRAG = F8 ? 32 : 16;             // bytes per lane of one MFMA operand fragment
@@ -105,7 +110,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool loader = wave == CT_NCW;
+  const bool loader = wave == NCW;
   const int lr = lane & 15, lg = lane >> 4;
   const int ct0 = blockIdx.y * NT;               // first 16-column tile of this workgroup
   // LDS: [buffer 0][buffer 1][job slots 64 B][BN partials][k-step offsets (nks+PD+2) int4]
@@ -115,26 +120,26 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
   // BS (F8): two int4 per k-step -- the tap offset of the scale each lane group supplies, then the
   // lane group's packed (lo | hi << 16) data offsets (the block-scaled operand layout, below)
   constexpr int KTW = (F8 && BS) ? 2 : 1;
-  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + ct_red_bytes(NT));
+  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + ct_red_bytes(NT, NCW));
   int2* s_pos = reinterpret_cast<int2*>(s_kt + KTW * (nks + PD + 2));
-  for (int i = tid; i < KTW * (nks + PD + 2); i += CT_NTHR) s_kt[i] = ktab[i];
-  for (int i = tid; i < ct_red_bytes(NT) / 4; i += CT_NTHR) s_red[i] = 0.f;
+  for (int i = tid; i < KTW * (nks + PD + 2); i += NTHR) s_kt[i] = ktab[i];
+  for (int i = tid; i < ct_red_bytes(NT, NCW) / 4; i += NTHR) s_red[i] = 0.f;
   // F8: the dequantisation scale and bias of this workgroup's 32 columns ([scale 32][bias 32]),
   // read by the epilogue from LDS (global loads there serialised every tile's stores)
   float* s_sb = reinterpret_cast<float*>(s_pos + g.HPpad);
   // relu-mask dgrad (gmask): two buffers (by job parity) of the tile's mask bytes,
   // [natural tile row][Ncol / 8], after everything else
-  const int mask_off = 64 + ct_red_bytes(NT) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + (F8 ? NT * 16 * 8 : 0);
+  const int mask_off = 64 + ct_red_bytes(NT, NCW) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + (F8 ? NT * 16 * 8 : 0);
   // (the buffers hold the bytes in FRAGMENT order -- slot f = (wave * MT + mt) * 16 + lr -- so
   // the epilogue reads slot (wave * MT + mt) * 16 + lr: a per-lane base plus a constant per mt)
-  const int mask_bytes = ct_mask_bytes(4 * MT * 16, Ncol, gmask != nullptr);
+  const int mask_bytes = ct_mask_bytes(NCW * MT * 16, Ncol, gmask != nullptr);
   // BS (F8): two planes (by job parity) of the halo positions' scale dwords, after s_sb
-  const int scl_off = 2 * g.BUF + 64 + ct_red_bytes(NT) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + NT * 16 * 8;
+  const int scl_off = 2 * g.BUF + 64 + ct_red_bytes(NT, NCW) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + NT * 16 * 8;
   // ... and after them each fragment slot's (output offset from the tile origin in positions,
   // packed td|th|tw; dummy rows: the origin) for the loader's mask DMA, built once per kernel
   int2* s_mrow = reinterpret_cast<int2*>(dsm + 2 * g.BUF + mask_off + 2 * mask_bytes);
   if (!F8 && gmask) {
-    for (int f = tid; f < 4 * MT * 16; f += CT_NTHR) {
+    for (int f = tid; f < NCW * MT * 16; f += NTHR) {
       const int r = rowtab[f].y;
       if (r < 0) {
         s_mrow[f] = make_int2(0, 0);
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
       s_sb[NT * 16 + tid] = (bias && c < Ncol) ? bias[c] : 0.f;
     }
   }
-  for (int p = tid; p < g.HPpad; p += CT_NTHR) {  // positions past HP repeat the last one
+  for (int p = tid; p < g.HPpad; p += NTHR) {  // positions past HP repeat the last one
     const int pc = p < HP ? p : HP - 1;
     const int hd = pc / (HH * HW), hh = (pc / HW) % HH, hw = pc % HW;
     s_pos[p] = make_int2(((hd * g.IH + hh) * g.IW + hw) * g.C * ESZ, (hd << 16) | (hh << 8) | hw);
@@ -215,7 +220,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     const int d0 = td_ * g.TD, h0 = th_ * g.TH, w0 = tw_ * g.TW;
     const long long pb = (long long)n * g.osn + g.ob + (long long)d0 * g.osd + (long long)h0 * g.osh + w0 * g.osw;
     const int lg2 = Ncol == 64 ? 1 : 0;          // log2 dwords per position (Ncol 32 / 64)
-    const int nslot = 4 * MT * 16;
+    const int nslot = NCW * MT * 16;
     const int ndw = nslot << lg2;
     const int ld = g.OD - d0, lh = g.OH - h0, lw = g.OW - w0;
     const unsigned char* mb0 = gmask + pb * (Ncol >> 3);
@@ -765,7 +770,7 @@ __global__ __launch_bounds__(CT_NTHR, 1) void conv_tile_kernel(const unsigned ch
     if (!F8 && stats && tid < RC && ct0 * 16 + tid < Ncol) {
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < CT_NCW; ++w) {
+      for (int w = 0; w < NCW; ++w) {
         s1 += s_red[w * 2 * RC + tid];
         s2 += s_red[w * 2 * RC + RC + tid];
       }
@@ -945,7 +950,8 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
-template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false>
+template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false,
+          int NCW = CT_NCW>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
@@ -953,12 +959,12 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
                        void* osc = nullptr) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS>), grid, dim3(CT_NTHR), lds, st,
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW>), grid, dim3(64 * (NCW + 1)), lds, st,
                      (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
                      stamps, scale, oscale, (const unsigned char*)gmask, (const unsigned*)xsc,
                      (unsigned char*)osc);
@@ -976,11 +982,11 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 }
 
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, int Ncol = 0, bool mask = false,
-                             bool bs = false) {
+                             bool bs = false, int ncw = CT_NCW) {
   const int PD = ct_pd(NT, f8);
-  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT) + (size_t)(g.nks + PD + 2) * 16 * (f8 && bs ? 2 : 1) +
+  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT, ncw) + (size_t)(g.nks + PD + 2) * 16 * (f8 && bs ? 2 : 1) +
          (size_t)g.HPpad * 8 +
-         (f8 ? (size_t)NT * 16 * 8 : 0) + (size_t)ct_mask_lds(4 * MT * 16, Ncol, mask) +
+         (f8 ? (size_t)NT * 16 * 8 : 0) + (size_t)ct_mask_lds(ncw * MT * 16, Ncol, mask) +
          (f8 && bs ? 2 * (size_t)g.HPpad * 4 : 0);    // (BS: the two scale planes)
 }
 
@@ -1069,6 +1075,23 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     return 0;
   }
 #endif  // FN_EXPERIMENTS
+  // FN_TILE_W8=1: the bf16 MT = 8 plans on 8 compute waves of MT = 4 (same rows, same tables)
+  static const bool w8 = [] { const char* e = getenv("FN_TILE_W8"); return e && atoi(e) == 1; }();
+  if (w8 && MT == 8 && NT == 2 && oscale == 0.f && !osc) {
+    const size_t lds8 = tile_lds_total(g, 4, NT, false, Ncol, bny != nullptr, false, 8);
+    if (lds8 <= 160 * 1024) {
+#define CT_W8(C)                                                                                                  \
+  if (CPP == C)                                                                                                   \
+    rc = launch_tile<4, 2, C, 0, false, false, false, false, 8>(grid, lds8, st, src, (const uint4*)wp,               \
+                                                                (const int2*)rowtab, (const int4*)ktab, zp, bias, out, \
+                                                                stats, g, Ncol, act, sched, nullptr, nullptr, 0.f, bny);
+      CT_W8(1) CT_W8(2) CT_W8(4)
+#undef CT_W8
+      if (rc) return rc;
+      FN_CHECK_LAUNCH();
+      return 0;
+    }
+  }
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
     rc = oscale > 0.f ? (osc ? launch_tile<M, N, C, 0, false, C == 1 && N == 2, false, C == 1 && N == 2>(        \

@@ -29,7 +29,7 @@ struct TileGeom {
 #define CT_F8_POOL 0x100               // fp8 act flag: fused 2^3 max-pool epilogue
 #define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
 // per-compute-wave BN sums of the workgroup's NT*16 columns
-__host__ __device__ constexpr int ct_red_bytes(int NT) { return CT_NCW * 2 * NT * 16 * 4; }
+__host__ __device__ constexpr int ct_red_bytes(int NT, int ncw = CT_NCW) { return ncw * 2 * NT * 16 * 4; }
 
 // packed bf16 pairs (low half = element 0)
 __device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }
