@@ -60,6 +60,7 @@ int fn_dense_dgrad(const void*, const float*, void*, int, int, int, hipStream_t,
 int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, float*, int, hipStream_t, const void*, int);
 int fn_dense_wgrad_slices(int, int, int);
 int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
+int fn_subpixel_wmap(const float*, float*, int, int, int, hipStream_t);
 int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
 int fn_igemm_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
@@ -438,6 +439,15 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("g"), py::arg("x"), py::arg("dw"), py::arg("db"), py::arg("M"), py::arg("N"), py::arg("K"),
      py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("part") = 0, py::arg("slices") = 1,
      py::arg("ya") = 0, py::arg("act") = 0);
+  // sub-pixel decoder weight maps (conv_halo.hip): mode 0 class weights [8][K][8][C] from w
+  // [K][27][C], 1 dgrad weights [C][8][8][K], 2 the folded weight gradient [K][27][C] from [8][K][8][C]
+  m.def("subpixel_wmap", [](uintptr_t src, uintptr_t dst, int K, int C, int mode, uintptr_t st,
+                            std::vector<long long> ext) {
+    const long long small = 27LL * K * C, big = 64LL * K * C;
+    fits(ext, 0, mode == 2 ? big : small, "subpixel_wmap", "src");
+    fits(ext, 1, mode == 2 ? small : big, "subpixel_wmap", "dst");
+    chk(fn_subpixel_wmap(P<const float*>(src), P<float*>(dst), K, C, mode, S(st)), "subpixel_wmap");
+  });
   m.def("s2d_weight_map", [](uintptr_t src, uintptr_t dst, std::vector<int> geom, int dir, uintptr_t st,
                              std::vector<long long> ext) {
     need(geom, 12, "s2d_weight_map");

@@ -1054,6 +1054,88 @@ __global__ __launch_bounds__(256) void s2d_weight_map_kernel(const float* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// sub-pixel decoder weight maps (ops/subpixel.py: conv3^3_same(upsample2x(x)) as 8 parity-class
+// 2^3 convs).  1-D selections, per dimension: forward S[j][e][t] = 1 iff e = floor((j + t - 1) / 2)
+// - (j - 1) (parity j output, low-res offset e, full-res tap t); dgrad D[e][j'][t] = 1 iff
+// 0 <= 2e + j' + t - 2 <= 1 (shifted cell offset e, sub-position j').  One launch per map instead
+// of an einsum (a hipBLASLt GEMM and its copies) plus a contiguous copy per class:
+//   mode 0  wf [8 classes (jd,jh,jw)][K][8 offsets (ed,eh,ew)][C] = sum_t S S S w[K][3][3][3][C]
+//   mode 1  wd [C][8 offsets][8 sub-positions (jd,jh,jw)][K]     = sum_t D D D w
+//   mode 2  dW [K][3][3][3][C] = sum over classes and offsets of S S S dwf[8][K][8][C] (mode 0's
+//           adjoint, the per-class weight gradients folded back)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool sp_sel_fwd(int j, int e, int t) { return e == ((j + t - 1) >> 1) - (j - 1); }
+__device__ __forceinline__ bool sp_sel_dgrad(int e, int j, int t) {
+  const int v = 2 * e + j + t - 2;
+  return v >= 0 && v <= 1;
+}
+
+__global__ __launch_bounds__(256) void subpixel_wmap_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                            int K, int C, int mode) {
+  const long long total = mode == 2 ? 27LL * K * C : 64LL * K * C;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % C);
+  float v = 0.f;
+  if (mode == 0) {
+    long long r = i / C;
+    const int e = (int)(r % 8); r /= 8;
+    const int k = (int)(r % K);
+    const int j = (int)(r / K);
+    const int jd = j >> 2, jh = (j >> 1) & 1, jw = j & 1, ed = e >> 2, eh = (e >> 1) & 1, ew = e & 1;
+    for (int x = 0; x < 3; ++x) {
+      if (!sp_sel_fwd(jd, ed, x)) continue;
+      for (int y = 0; y < 3; ++y) {
+        if (!sp_sel_fwd(jh, eh, y)) continue;
+        for (int z = 0; z < 3; ++z)
+          if (sp_sel_fwd(jw, ew, z)) v += src[(((long long)k * 3 + x) * 3 + y) * 3 * C + (long long)z * C + c];
+      }
+    }
+  } else if (mode == 1) {
+    // dst[c][e][j][k]: the fastest index is k here
+    const int k = (int)(i % K);
+    long long r = i / K;
+    const int j = (int)(r % 8); r /= 8;
+    const int e = (int)(r % 8);
+    const int ci = (int)(r / 8);
+    const int jd = j >> 2, jh = (j >> 1) & 1, jw = j & 1, ed = e >> 2, eh = (e >> 1) & 1, ew = e & 1;
+    for (int x = 0; x < 3; ++x) {
+      if (!sp_sel_dgrad(ed, jd, x)) continue;
+      for (int y = 0; y < 3; ++y) {
+        if (!sp_sel_dgrad(eh, jh, y)) continue;
+        for (int z = 0; z < 3; ++z)
+          if (sp_sel_dgrad(ew, jw, z)) v += src[(((long long)k * 3 + x) * 3 + y) * 3 * C + (long long)z * C + ci];
+      }
+    }
+    dst[i] = v;
+    return;
+  } else {
+    long long r = i / C;
+    const int t = (int)(r % 27);
+    const int k = (int)(r / 27);
+    const int x = t / 9, y = (t / 3) % 3, z = t % 3;
+    for (int j = 0; j < 8; ++j) {
+      const int jd = j >> 2, jh = (j >> 1) & 1, jw = j & 1;
+      for (int e = 0; e < 8; ++e) {
+        const int ed = e >> 2, eh = (e >> 1) & 1, ew = e & 1;
+        if (sp_sel_fwd(jd, ed, x) && sp_sel_fwd(jh, eh, y) && sp_sel_fwd(jw, ew, z))
+          v += src[(((long long)j * K + k) * 8 + e) * C + c];
+      }
+    }
+  }
+  dst[i] = v;
+}
+
+extern "C" int fn_subpixel_wmap(const float* src, float* dst, int K, int C, int mode, hipStream_t st) {
+  if (K < 1 || C < 1 || mode < 0 || mode > 2) return -2;
+  const long long total = mode == 2 ? 27LL * K * C : 64LL * K * C;
+  hipLaunchKernelGGL(subpixel_wmap_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, src, dst, K, C,
+                     mode);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int fn_s2d_weight_map(const float* src, float* dst, const int* geom13, int dir, hipStream_t st) {
   const int K = geom13[0], KD = geom13[1], KH = geom13[2], KW = geom13[3], C = geom13[4];
   const int sd = geom13[5], sh = geom13[6], sw = geom13[7], kd = geom13[8], kh = geom13[9], kw = geom13[10];

@@ -78,8 +78,25 @@ def _sel_dgrad(device=None, dtype=torch.float32) -> torch.Tensor:
     return _cached("dgrad", _sel_dgrad_cpu, device or "cpu", dtype)
 
 
+def _wmap(src: torch.Tensor, K: int, C: int, mode: int, shape: tuple):
+    """The native weight map (``conv_halo.hip`` subpixel_wmap) for fp32 GPU tensors, else None."""
+    from .. import _native
+
+    if not (src.is_cuda and src.dtype == torch.float32 and _native.kernels_available()):
+        return None
+    src = src.contiguous()
+    out = torch.empty(shape, dtype=torch.float32, device=src.device)
+    _native.kernels().subpixel_wmap(src.data_ptr(), out.data_ptr(), K, C, mode, _native.stream(src),
+                                    [src.numel(), out.numel()])
+    return out
+
+
 def forward_weights(w: torch.Tensor) -> torch.Tensor:
     """W [K, 3, 3, 3, C] -> per-class folded weights [8, K, 2, 2, 2, C] (class = parity index)."""
+    K, C = w.shape[0], w.shape[-1]
+    out = _wmap(w, K, C, 0, (8, K, 2, 2, 2, C))
+    if out is not None:
+        return out
     s = _sel_fwd(w.device, w.dtype)
     # out[jd, jh, jw, k, ed, eh, ew, c]
     out = torch.einsum("adx,bey,cfz,kxyzi->abckdefi", s, s, s, w)
@@ -88,6 +105,10 @@ def forward_weights(w: torch.Tensor) -> torch.Tensor:
 
 def fold_weight_grad(dwf: torch.Tensor) -> torch.Tensor:
     """Adjoint of :func:`forward_weights`: per-class [8, K, 2, 2, 2, C] -> dW [K, 3, 3, 3, C]."""
+    K, C = dwf.shape[1], dwf.shape[-1]
+    out = _wmap(dwf, K, C, 2, (K, 3, 3, 3, C))
+    if out is not None:
+        return out
     s = _sel_fwd(dwf.device, dwf.dtype)
     d = dwf.reshape(2, 2, 2, *dwf.shape[1:])
     return torch.einsum("adx,bey,cfz,abckdefi->kxyzi", s, s, s, d)
@@ -96,8 +117,11 @@ def fold_weight_grad(dwf: torch.Tensor) -> torch.Tensor:
 def dgrad_weights(w: torch.Tensor) -> torch.Tensor:
     """W [K, 3, 3, 3, C] -> the weights of the dgrad conv over the shifted view:
     [C (output), 2, 2, 2, 8 * K (input channel = j' * K + co)]."""
-    s = _sel_dgrad(w.device, w.dtype)
     K, C = w.shape[0], w.shape[-1]
+    out = _wmap(w, K, C, 1, (C, 2, 2, 2, 8 * K))
+    if out is not None:
+        return out
+    s = _sel_dgrad(w.device, w.dtype)
     # out[i, ed, eh, ew, jd, jh, jw, k]
     out = torch.einsum("dax,eby,fcz,kxyzi->idefabck", s, s, s, w)
     return out.reshape(C, 2, 2, 2, 8 * K)

@@ -168,3 +168,19 @@ def test_decoder_bn_identity_matches_colstats(monkeypatch):
     for k in g0:
         r = _rel(g1[k], g0[k])
         assert r < 2e-2, (k, r)
+
+
+def test_weight_maps_native_match_einsum():
+    """The native sub-pixel weight maps (class weights, dgrad weights, folded weight gradient;
+    conv_halo.hip subpixel_wmap) against the einsum forms on the CPU."""
+    from featurenet_amd.ops import subpixel as sp
+
+    torch.manual_seed(21)
+    K, C = 32, 64
+    w = torch.randn(K, 3, 3, 3, C)
+    dwf = torch.randn(8, K, 2, 2, 2, C)
+    for fn, arg in ((sp.forward_weights, w), (sp.dgrad_weights, w), (sp.fold_weight_grad, dwf)):
+        ref = fn(arg)
+        got = fn(arg.cuda()).cpu()
+        assert got.shape == ref.shape, fn.__name__
+        torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-5)
