@@ -154,7 +154,8 @@ def main():
     xs = [(torch.rand(B, S, S, S, 1, device=dev) < 0.3).to(torch.bfloat16) for _ in range(args.pool)]
     if args.model == "seg":
         NC = 25
-        ys = [torch.randint(0, NC, (B, S, S, S), device=dev) for _ in range(args.pool)]
+        # per-voxel class labels as bytes (25 classes): an eighth of int64's bytes to copy in and read
+        ys = [torch.randint(0, NC, (B, S, S, S), device=dev, dtype=torch.uint8) for _ in range(args.pool)]
     else:
         ys = [torch.randint(0, NC, (B,), device=dev) for _ in range(args.pool)]
 

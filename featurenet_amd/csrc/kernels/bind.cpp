@@ -27,8 +27,8 @@ int fn_pw_fwd(const void*, const void*, const float*, void*, long long, int, int
               const float*, int, const void*, const float*, const float*, float*, int);
 int fn_seghead_part_len();
 int fn_seghead_blocks(long long);
-int fn_seghead_loss(const void*, const float*, const float*, const void*, const float*, const long long*, void*, float*,
-                    long long, int, int, int, float, float, hipStream_t);
+int fn_seghead_loss(const void*, const float*, const float*, const void*, const float*, const void*, void*, float*,
+                    long long, int, int, int, float, float, hipStream_t, int);
 int fn_pw_xent_blocks(long long);
 int fn_pw_fwd_xent(const void*, const void*, const float*, void*, long long, int, int, const float*, const float*, int,
                    const long long*, float*, float, float, hipStream_t);
@@ -190,12 +190,15 @@ static long long view_extent(const std::vector<int>& g, int ncol) {
 }
 
 static void check_tile(const std::vector<int>& g, const std::vector<long long>& ext, int ncol, int MT,
-                       const char* what) {
+                       const char* what, int NT = 2) {
   if (g[4] <= 0 || ncol <= 0 || g[17] <= 0 || g[4] % g[17]) throw std::runtime_error(std::string(what) + ": bad slice");
   if (g[5] > g[1] + 2 * g[11] + g[8] || g[6] > g[2] + 2 * g[12] + g[9] || g[7] > g[3] + 2 * g[13] + g[10])
     throw std::runtime_error(std::string(what) + ": output larger than the padded input");
   fits(ext, 0, prod({g[0], g[1], g[2], g[3], g[4]}), what, "src");
-  fits(ext, 1, prod({g[4] / g[17] * g[19] + 4, g[20], 64, 8}), what, "wpk");   // + 4 zero ring k-steps
+  // the stream's rows (+ 4 zero ring k-steps) x nct fragments, of which the last row is read up to the
+  // ncol columns' fragments (a view may start inside a wider stream: the sub-pixel class weights)
+  const long long ncb = (ncol + NT * 16 - 1) / (NT * 16);
+  fits(ext, 1, ((long long)(g[4] / g[17] * g[19] + 3) * g[20] + ncb * NT) * 64 * 8, what, "wpk");
   fits(ext, 2, view_extent(g, ncol), what, "out");
   fits(ext, 3, 4LL * MT * 16, what, "rowtab");
   fits(ext, 4, g[19] + 6LL, what, "ktab");
@@ -254,7 +257,7 @@ PYBIND11_MODULE(_C, m) {
                         uintptr_t sched, uintptr_t st, std::vector<long long> ext, uintptr_t bny, uintptr_t bnp,
                         float oscale, uintptr_t osc, long long osc_n) {
     need(geom, 31, "conv_tile");
-    check_tile(geom, ext, ncol, MT, "conv_tile");
+    check_tile(geom, ext, ncol, MT, "conv_tile", NT);
     // osc: block scales of an e4m3 output, one dword per output position
     if (osc && osc_n < view_extent(geom, 1)) throw std::runtime_error("conv_tile: osc smaller than the output");
     if (bny && bnp) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
@@ -540,19 +543,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("seghead_blocks", &fn_seghead_blocks);
   m.def("seghead_loss", [](uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t w, uintptr_t bias, uintptr_t labels,
                            uintptr_t dz, uintptr_t part, long long M, int K, int NC, int act, float xscale,
-                           float smoothing, uintptr_t st, std::vector<long long> ext) {
+                           float smoothing, uintptr_t st, std::vector<long long> ext, int lab8) {
     fits(ext, 0, M * K, "seghead_loss", "y");
     fits(ext, 1, (long long)NC * K, "seghead_loss", "w");
     fits(ext, 2, M, "seghead_loss", "labels");
     fits(ext, 3, M * K, "seghead_loss", "dz");
     fits(ext, 4, (long long)fn_seghead_blocks(M) * fn_seghead_part_len(), "seghead_loss", "part");
     chk(fn_seghead_loss(P<const void*>(y), P<const float*>(sc), P<const float*>(sh), P<const void*>(w),
-                        P<const float*>(bias), P<const long long*>(labels), P<void*>(dz), P<float*>(part), M, K, NC,
-                        act, xscale, smoothing, S(st)),
+                        P<const float*>(bias), P<const void*>(labels), P<void*>(dz), P<float*>(part), M, K, NC,
+                        act, xscale, smoothing, S(st), lab8),
         "seghead_loss");
   }, py::arg("y"), py::arg("sc"), py::arg("sh"), py::arg("w"), py::arg("bias"), py::arg("labels"), py::arg("dz"),
      py::arg("part"), py::arg("M"), py::arg("K"), py::arg("NC"), py::arg("act"), py::arg("xscale"),
-     py::arg("smoothing"), py::arg("st"), py::arg("ext"));
+     py::arg("smoothing"), py::arg("st"), py::arg("ext"), py::arg("lab8") = 0);
   m.def("pw_fwd_xent", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t dlog, long long M, int K, int N,
                           uintptr_t psc, uintptr_t psh, int pact, uintptr_t labels, uintptr_t xpart, float xscale,
                           float smoothing, uintptr_t st, std::vector<long long> ext) {

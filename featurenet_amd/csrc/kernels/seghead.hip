@@ -54,17 +54,18 @@ __device__ __forceinline__ unsigned sh_pack2(float lo, float hi) {
 }
 __device__ __forceinline__ float bf16_round(float x) { return bf2f(f2bf(x)); }
 
-// ACT: the decoder BN's activation (ACT_NONE / ACT_RELU).
-// y [M][32] bf16; sc / sh [32]; w [NC][32] bf16; bias [NC] fp32 or null; labels int64 [M];
+// ACT: the decoder BN's activation (ACT_NONE / ACT_RELU); LT: the label type (int64, or uint8 --
+// NC <= 32 classes fit a byte: 8x fewer label bytes to copy in and read).
+// y [M][32] bf16; sc / sh [32]; w [NC][32] bf16; bias [NC] fp32 or null; labels LT [M];
 // dz [M][32] bf16 out; part: per workgroup [loss, hits | db[32] | dWt[32][32] | msum[32] | msq[32]]
 // (fp32; dWt[ch][cls] = sum z[r][ch] d[r][cls]).
-template <int ACT>
+template <int ACT, typename LT>
 __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __restrict__ y,
                                                                  const float* __restrict__ sc,
                                                                  const float* __restrict__ shf,
                                                                  const bf16* __restrict__ w,
                                                                  const float* __restrict__ bias,
-                                                                 const long long* __restrict__ labels,
+                                                                 const LT* __restrict__ labels,
                                                                  bf16* __restrict__ dz, float* __restrict__ part,
                                                                  long long M, int NC, float xscale, float smoothing) {
   __shared__ __attribute__((aligned(16))) bf16 Ys[SH_BM * SH_LD];   // raw y
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
       // groups of ds_read_b128 hit 16 distinct bank slots; scalar 2-B accesses were 4-way)
       bf16* orow = Os + tid * SH_LD;
       if (tid < rows) {
-        const long long yl = labels[(long long)t * SH_BM + tid];
+        const long long yl = (long long)labels[(long long)t * SH_BM + tid];
         const float off = smoothing / (float)NC, on = 1.f - smoothing + off;
         Pack8 lv[4];
 #pragma unroll
@@ -357,20 +358,23 @@ extern "C" int fn_seghead_blocks(long long M) {
 }
 
 // y [M][32] bf16 (M % 8 == 0), sc / sh [32], w [NC][32] bf16 (NC <= 32), bias [NC] or null,
-// labels int64 [M], dz [M][32] bf16, part fp32 [fn_seghead_blocks(M)][fn_seghead_part_len()]
+// labels int64 [M] (lab8 = 0) or uint8 [M] (lab8 = 1), dz [M][32] bf16, part fp32
+// [fn_seghead_blocks(M)][fn_seghead_part_len()]
 extern "C" int fn_seghead_loss(const void* y, const float* sc, const float* sh, const void* w, const float* bias,
-                               const long long* labels, void* dz, float* part, long long M, int K, int NC, int act,
-                               float xscale, float smoothing, hipStream_t st) {
+                               const void* labels, void* dz, float* part, long long M, int K, int NC, int act,
+                               float xscale, float smoothing, hipStream_t st, int lab8) {
   if (K != SH_K || NC < 2 || NC > 32 || M < 8 || M % 8 || !sc || !sh || !labels || !part) return -2;
+  if (act != ACT_RELU && act != ACT_NONE) return -2;
   const dim3 grid((unsigned)fn_seghead_blocks(M));
-  if (act == ACT_RELU)
-    hipLaunchKernelGGL(seghead_loss_kernel<ACT_RELU>, grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,
-                       (const bf16*)w, bias, labels, (bf16*)dz, part, M, NC, xscale, smoothing);
-  else if (act == ACT_NONE)
-    hipLaunchKernelGGL(seghead_loss_kernel<ACT_NONE>, grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,
-                       (const bf16*)w, bias, labels, (bf16*)dz, part, M, NC, xscale, smoothing);
-  else
-    return -2;
+#define SH_LAUNCH(A, T)                                                                                       \
+  hipLaunchKernelGGL((seghead_loss_kernel<A, T>), grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,           \
+                     (const bf16*)w, bias, (const T*)labels, (bf16*)dz, part, M, NC, xscale, smoothing)
+  if (act == ACT_RELU) {
+    if (lab8) SH_LAUNCH(ACT_RELU, unsigned char); else SH_LAUNCH(ACT_RELU, long long);
+  } else {
+    if (lab8) SH_LAUNCH(ACT_NONE, unsigned char); else SH_LAUNCH(ACT_NONE, long long);
+  }
+#undef SH_LAUNCH
   FN_CHECK_LAUNCH();
   return 0;
 }

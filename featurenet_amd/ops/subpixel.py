@@ -214,21 +214,29 @@ def upconv_forward(x5: torch.Tensor, w: torch.Tensor):
     parity-class 2^3 convs on the tile kernel writing straight into the full-res output."""
     from . import conv_tile
 
+    import dataclasses
+
     N, D, H, W, C = x5.shape
     K = w.shape[0]
     p = conv_tile.plan(N, (D, H, W), (2, 2, 2), C, K)
-    wf = forward_weights(w.detach().float()).reshape(8, K, 8, C)
+    # the 8 classes' weights as ONE packed stream of 8 K columns (one pack launch, not eight): class
+    # ci's columns are fragment block ci of every k-step row, so its conv reads the stream from
+    # fragment ci * nct on with the row pitch of all 8 (geometry nct = 8 nct)
+    p8 = dataclasses.replace(p, nct=8 * p.nct)
+    wf = forward_weights(w.detach().float()).reshape(8 * K, 8, C)
+    wall = conv_tile.pack_weights(wf, 8 * K, 8, C, p8, dgrad=False)
     y = torch.empty(N, 2 * D, 2 * H, 2 * W, K, dtype=torch.bfloat16, device=x5.device)
     geoms = []
     for j in PARITIES:
         lo, _ = class_pads(j)
-        geoms.append(conv_tile.geometry(p, (N, D, H, W, C), (D, H, W), (2, 2, 2), lo,
+        geoms.append(conv_tile.geometry(p8, (N, D, H, W, C), (D, H, W), (2, 2, 2), lo,
                                         view=conv_tile.parity_view((2 * D, 2 * H, 2 * W), j)))
-    nw = conv_tile.workers(p, geoms[0], K)
+    nw = conv_tile.workers(p8, geoms[0], K)
     slab = torch.empty(8 * nw, 2, K, dtype=torch.float32, device=x5.device)
+    frag = 64 * 8                                # bf16 elements per packed fragment
     for ci in range(8):
-        wpk = conv_tile.pack_weights(wf[ci], K, 8, C, p, dgrad=False)
-        conv_tile.run(x5, wpk, None, y, slab[ci * nw:(ci + 1) * nw], p, geoms[ci], (2, 2, 2), K, 0)
+        conv_tile.run(x5, wall[ci * p.nct * frag:], None, y, slab[ci * nw:(ci + 1) * nw], p8, geoms[ci], (2, 2, 2), K,
+                      0)
     return y, slab
 
 
@@ -461,7 +469,8 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         wb = w2.to(torch.bfloat16).contiguous()
         Kn.seghead_loss(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), wb.data_ptr(), _native.ptr(bias),
                         lab.data_ptr(), dz.data_ptr(), part.data_ptr(), M, K, NC, act, 1.0 / M, float(smoothing),
-                        _native.stream(y2), [y2.numel(), wb.numel(), lab.numel(), dz.numel(), part.numel()])
+                        _native.stream(y2), [y2.numel(), wb.numel(), lab.numel(), dz.numel(), part.numel()],
+                        int(lab.dtype == torch.uint8))
         ctx.save_for_backward(x, w, y, prm, hw, dz, part)
         ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
         ctx.params = (beta, gamma)
@@ -533,8 +542,10 @@ def decoder_head_xent(x5, w, gamma, beta, running_mean, running_var, hw, hb, lab
     from .spec import act_code
 
     if hw.shape[-1] == 32 and os.environ.get("FN_SEG_XENT", "1") != "2":
+        # (uint8 labels stay uint8: the kernel reads either, a byte is 8x fewer label bytes)
+        lab = labels if labels.dtype == torch.uint8 else labels.long()
         return SubpixelDecoderHeadLossFn.apply(x5.to(torch.bfloat16).contiguous(), w, gamma, beta, running_mean,
-                                               running_var, momentum, eps, act_code(act), hw, hb, labels.long(),
+                                               running_var, momentum, eps, act_code(act), hw, hb, lab,
                                                float(smoothing))
     return SubpixelDecoderHeadXentFn.apply(x5.to(torch.bfloat16).contiguous(), w, gamma, beta, running_mean,
                                            running_var, momentum, eps, act_code(act), hw, hb, labels.long(),

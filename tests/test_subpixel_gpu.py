@@ -184,3 +184,25 @@ def test_weight_maps_native_match_einsum():
         got = fn(arg.cuda()).cpu()
         assert got.shape == ref.shape, fn.__name__
         torch.testing.assert_close(got, ref, rtol=1e-6, atol=1e-5)
+
+
+def test_fused_head_loss_uint8_labels_match_int64():
+    """The fused head + loss with uint8 per-voxel labels (the seg bench's label format) gives the
+    same loss, hits and gradients bit for bit as with int64 labels."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3DSeg
+
+    torch.manual_seed(7)
+    N, S = 2, 24
+    m = FeatureNet3DSeg(input_size=S, num_classes=25).cuda().train()
+    x = (torch.rand(N, S, S, S, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    lab = torch.randint(0, 25, (N, S, S, S), device="cuda")
+    res = []
+    for lb in (lab, lab.to(torch.uint8)):
+        m.zero_grad(set_to_none=True)
+        loss, hits = m.loss(x, lb, 0.0, with_correct=True)
+        loss.backward()
+        res.append((loss.detach().clone(), hits.clone(),
+                    {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    for k in res[0][2]:
+        assert torch.equal(res[0][2][k], res[1][2][k]), k
