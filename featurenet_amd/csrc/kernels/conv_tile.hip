@@ -1075,12 +1075,13 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     return 0;
   }
 #endif  // FN_EXPERIMENTS
-  // the bf16 MT = 8 plans on 8 compute waves of MT = 4 (same rows, same tables): FN_TILE_W8 = 1
-  // always, 0 never, unset = the 8-channel-slice stem only -- measured (profiles/r5_conv_tile_budget.md):
-  // stem fwd -6 %, conv2 / conv3 fwd -1..-3 %, but dgrad and conv4 +1..+10 % (every compute wave
-  // loads the workgroup's weight fragments itself: eight copies through L1 instead of four)
-  static const int w8e = [] { const char* e = getenv("FN_TILE_W8"); return e ? atoi(e) : -1; }();
-  const bool w8 = w8e == 1 || (w8e < 0 && CPP == 1);
+  // FN_TILE_W8=1: the bf16 MT = 8 plans on 8 compute waves of MT = 4 (same rows, same tables) --
+  // measured, not the default (profiles/r5_conv_tile_budget.md): the stem forward alone -7 %, but
+  // the dgrad / CPP 4 plans +1..+10 % (every compute wave loads the workgroup's weight fragments
+  // itself: eight copies through L1 instead of four), and whole steps never faster (training
+  // 4.67-4.70 vs 4.70-4.71 ms with it on the short-tile convs only, segmentation 19.0-19.1 vs
+  // 19.3-19.4 ms)
+  static const bool w8 = [] { const char* e = getenv("FN_TILE_W8"); return e && atoi(e) == 1; }();
   if (w8 && MT == 8 && NT == 2 && oscale == 0.f && !osc) {
     const size_t lds8 = tile_lds_total(g, 4, NT, false, Ncol, bny != nullptr, false, 8);
     if (lds8 <= 160 * 1024) {

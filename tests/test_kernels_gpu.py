@@ -39,6 +39,7 @@ CONV_CASES = [
     (2, 9, 10, 11, 16, 48, (3, 3, 3), 1, "same"),         # halo path: same padding, partial col block
     (2, 1, 20, 23, 48, 32, (1, 5, 5), 1, "same"),         # halo path: 2-D, 3 channel slices
     (1, 6, 7, 30, 32, 16, (2, 3, 3), 1, "valid"),         # halo path: even kernel, Cout 16
+    (4, 1, 16, 16, 12, 120, (1, 5, 5), 1, "same"),        # LeNet conv3: split-K gather fwd + dgrad
 ]
 
 
