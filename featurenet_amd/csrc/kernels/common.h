@@ -82,5 +82,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // weight gradients into rows of `part` and this pass adds the rows, so the result is bitwise
 // the same run to run whatever the workgroup timing
 extern "C" int fn_part_reduce(const float* part, float* dst, long long n, int W, int accumulate, hipStream_t st);
+extern "C" int fn_part_reduce2(const float* part, float* dst, long long n, const float* part2, float* dst2,
+                               long long n2, int W, int accumulate, hipStream_t st);
 extern "C" int fn_part_reduce_wdot(const float* part, float* dst, long long n, int W, int accumulate,
                                   const float* wsrc, float* wdp, int C, hipStream_t st);

@@ -705,8 +705,7 @@ extern "C" int fn_igemm_wgrad(const void* dy, const void* src, float* dw, const 
 #undef WG_GM
 #undef WG_CASE
   FN_CHECK_LAUNCH();
-  int rc = fn_part_reduce(pdw, dw, (long long)kout * ldo, splits, 1, st);
-  if (rc == 0 && db) rc = fn_part_reduce(pdb, db, kout, splits, 1, st);
+  int rc = fn_part_reduce2(pdw, dw, (long long)kout * ldo, db ? pdb : nullptr, db, db ? kout : 0, splits, 1, st);
   return rc;
 }
 

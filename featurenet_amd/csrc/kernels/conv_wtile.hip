@@ -559,13 +559,25 @@ __global__ __launch_bounds__(256) void wtile_reduce_kernel(const float* __restri
 // partial rows ran 23 us in the 256-element blocks above, each thread walking a quarter of
 // the rows): E elements per block, the 256 / E thread groups take every (256 / E)-th row, then
 // the groups' sums are added in group order -- fixed for a given (n, W), so still repeatable.
+// (a second job -- part2 / dst2 / n2, the bias gradient beside a weight gradient -- takes the
+// blocks past the first job's: one launch for both)
 template <int E>
 __global__ __launch_bounds__(256) void part_reduce_narrow_kernel(const float* __restrict__ part, float* __restrict__ dst,
-                                                                 long long n, int W, int accumulate) {
+                                                                 long long n, int W, int accumulate,
+                                                                 const float* __restrict__ part2 = nullptr,
+                                                                 float* __restrict__ dst2 = nullptr, long long n2 = 0) {
   constexpr int G = 256 / E;
   __shared__ float s_r[G][E];
   const int e = threadIdx.x % E, gq = threadIdx.x / E;
-  const long long i = (long long)blockIdx.x * E + e;
+  long long b = blockIdx.x;
+  const long long nb1 = (n + E - 1) / E;
+  if (b >= nb1) {                                // (uniform per block)
+    part = part2;
+    dst = dst2;
+    n = n2;
+    b -= nb1;
+  }
+  const long long i = b * E + e;
   float a0 = 0.f, a1 = 0.f;
   if (i < n) {
     int p = gq;
@@ -609,6 +621,23 @@ extern "C" int fn_part_reduce_wdot(const float* part, float* dst, long long n, i
 
 extern "C" int fn_part_reduce(const float* part, float* dst, long long n, int W, int accumulate, hipStream_t st) {
   return fn_part_reduce_wdot(part, dst, n, W, accumulate, nullptr, nullptr, 0, st);
+}
+
+// two reductions over the same slice count (a weight gradient and its bias gradient) in one
+// launch when both take the narrow form, else two
+extern "C" int fn_part_reduce2(const float* part, float* dst, long long n, const float* part2, float* dst2,
+                               long long n2, int W, int accumulate, hipStream_t st) {
+  if (!part2 || !dst2 || n2 <= 0) return fn_part_reduce(part, dst, n, W, accumulate, st);
+  if (n <= 0 || !part || !dst || W < 1) return -6;
+  if (W >= 16 && (n + 255) / 256 < 192 && n <= 192 * 16 && n2 <= 192 * 16) {
+    const unsigned nb = (unsigned)((n + 15) / 16 + (n2 + 15) / 16);
+    hipLaunchKernelGGL(part_reduce_narrow_kernel<16>, dim3(nb), dim3(256), 0, st, part, dst, n, W, accumulate, part2,
+                       dst2, n2);
+    FN_CHECK_LAUNCH();
+    return 0;
+  }
+  if (int e = fn_part_reduce(part, dst, n, W, accumulate, st)) return e;
+  return fn_part_reduce(part2, dst2, n2, W, accumulate, st);
 }
 
 // ---------------------------------------------------------------------------

@@ -464,7 +464,11 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
 // host launchers
 // ---------------------------------------------------------------------------
 // column waves per forward workgroup: 2 (128 columns, x rows read once) when N > 64
-static int dn_ncw(int N) { return N > 64 ? 2 : 1; }
+static int dn_ncw(int N) {
+  static const int forced = [] { const char* e = getenv("FN_DENSE_NCW"); return e ? atoi(e) : 0; }();   // (A/B)
+  if (forced == 1 || forced == 2) return forced;
+  return N > 64 ? 2 : 1;
+}
 
 extern "C" int fn_dense_splits(int M, int N, int K) {
   const int ncw = dn_ncw(N);
@@ -587,8 +591,7 @@ extern "C" int fn_dense_wgrad(const void* g, const void* x, float* dw, float* db
   }
   FN_CHECK_LAUNCH();
   if (S > 1) {                                   // (fixed slice order: fn_part_reduce, overwrite)
-    if (int e = fn_part_reduce(part, dw, NK, S, 0, st)) return e;
-    if (db) return fn_part_reduce(part + (long long)S * NK, db, (long long)N, S, 0, st);
+    return fn_part_reduce2(part, dw, NK, db ? part + (long long)S * NK : nullptr, db, db ? (long long)N : 0, S, 0, st);
   }
   return 0;
 }

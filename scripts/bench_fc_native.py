@@ -46,7 +46,7 @@ def main():
     g = torch.randn(M, N, device="cuda").to(torch.bfloat16)
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     res = {"S_default": int(Kn.dense_splits(M, N, K))}
-    for S in sorted({16, 32, 64, 125, 250, res["S_default"]}):
+    for S in sorted({32, 64, 125, 250, 500, 1000, res["S_default"]}):
         part = torch.empty(S, M, N, device="cuda")
         res[f"fwd_S{S}"] = timeit(lambda: Kn.dense_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(),
                                                         part.data_ptr(), M, N, K, S, 1, 0, st), a.reps)
