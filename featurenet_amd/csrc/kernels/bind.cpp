@@ -61,8 +61,9 @@ int fn_dense_wgrad(const void*, const void*, float*, float*, int, int, int, floa
 int fn_dense_wgrad_slices(int, int, int);
 int fn_s2d_weight_map(const float*, float*, const int*, int, hipStream_t);
 int fn_subpixel_wmap(const float*, float*, int, int, int, hipStream_t);
-int fn_halo_pack_w(const float*, void*, int, int, int, int, int, hipStream_t);
+int fn_halo_pack_w(const float*, void*, int, int, int, int, int, int, int, hipStream_t);
 int fn_igemm_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+int fn_pack_w_multi(const long long*, int, hipStream_t);
 int fn_igemm_wgrad(const void*, const void*, float*, const int*, const int*, long long, int, int, int, int,
                    hipStream_t, int, int, const void*, int, float*, int, float*);
 long long fn_igemm_wgrad_part(int, int, int, int, int, int, int);
@@ -375,8 +376,34 @@ PYBIND11_MODULE(_C, m) {
     fits(ext, 1, (long long)(mode == 1 ? C : K) * ld, "igemm_pack_w", "out");
     chk(fn_igemm_pack_w(P<const float*>(w), P<void*>(out), K0, C0, K, T, C, mode, ld, KW, R, S(st)), "igemm_pack_w");
   });
-  m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int mode, int stage_k, uintptr_t st) {
-    chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K, T, C, mode, stage_k, S(st)), "halo_pack_w");
+  m.def("pack_w_multi", [](std::vector<long long> jobs, uintptr_t st, std::vector<long long> ext) {
+    // jobs: n rows of (w, out, kind, a0..a8) (pack_w.h PackJob); ext: n rows of (numel(w), numel(out))
+    if (jobs.size() % 12 || ext.size() != jobs.size() / 6)
+      throw std::invalid_argument("pack_w_multi: 12 values per job and 2 extents per job");
+    const int n = (int)(jobs.size() / 12);
+    for (int k = 0; k < n; ++k) {
+      const long long* r = jobs.data() + 12 * k;
+      const long long kind = r[2];
+      long long wn, on;
+      if (kind >= 0 && kind <= 2) {                // K0, C0, K, T, C, ld
+        wn = r[3] * r[6] * r[4];
+        on = (kind == 1 ? r[7] : r[5]) * r[8];
+      } else {                                     // K0, C0, K, T, C, CS, Tp
+        wn = r[3] * r[6] * r[4];
+        on = r[5] * r[7] * r[9];
+      }
+      std::vector<long long> e = {ext[2 * k], ext[2 * k + 1]};
+      fits(e, 0, wn, "pack_w_multi", "w");
+      fits(e, 1, on, "pack_w_multi", "out");
+    }
+    chk(fn_pack_w_multi(jobs.data(), n, S(st)), "pack_w_multi");
+  });
+  m.def("halo_pack_w", [](uintptr_t w, uintptr_t out, int K0, int C0, int K, int T, int C, int mode, int stage_k,
+                          uintptr_t st, std::vector<long long> ext) {
+    // ext = {numel(w), numel(out)}; out holds K * C * (taps padded to the stage) elements
+    fits(ext, 0, (long long)K0 * T * C0, "halo_pack_w", "w");
+    fits(ext, 1, (long long)K * C * T, "halo_pack_w", "out");
+    chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K0, C0, K, T, C, mode, stage_k, S(st)), "halo_pack_w");
   });
   m.def("ew_binary", [](uintptr_t a, uintptr_t b, uintptr_t out, long long n, int op, uintptr_t st) {
     chk(fn_ew_binary(P<const void*>(a), P<const void*>(b), P<void*>(out), n, op, S(st)), "ew_binary");

@@ -23,6 +23,7 @@
 // consecutive halo positions, so a ds_read_b128 lane group {lr 0-3,12-15 @ lg,
 // lr 4-11 @ lg^1} touches 16 distinct 16-B slots of a 256-B bank line.
 #include "common.h"
+#include "pack_w.h"
 
 struct HaloGeom {
   int N, ID, IH, IW, C;    // gathered source (x for fwd, dy for dgrad), channels-last
@@ -1151,37 +1152,26 @@ extern "C" int fn_s2d_weight_map(const float* src, float* dst, const int* geom13
 // ---------------------------------------------------------------------------
 // weight packing for the halo kernels (one launch instead of zero-fill + copies)
 // ---------------------------------------------------------------------------
-// w: fp32 (or bf16 when w_bf16) [K][T][C] (the conv weight, taps kd-kh-kw major).
-// mode 0 (forward):  out[n = co][p][t][j] = w[co][t][p*CS + j]            n < K,  src C channels
-// mode 1 (dgrad):    out[n = ci][p][t][j] = w[p*CS + j][T-1-t][ci]        n < C,  src K channels
-// t in [0, Tp) (taps >= T are zero), CS = channels per halo slice of the source.
-__global__ __launch_bounds__(256) void halo_pack_w_kernel(const float* __restrict__ w, bf16* __restrict__ out, int K,
-                                                          int T, int C, int CS, int Tp, int mode) {
-  const int Ncol = mode == 0 ? K : C, Csrc = mode == 0 ? C : K;
-  const long long total = (long long)Ncol * Csrc * Tp;
+// w: fp32 [K][T][C] (the conv weight, taps kd-kh-kw major); the layouts: pack_w.h halo_pack_val
+__global__ __launch_bounds__(256) void halo_pack_w_kernel(const float* __restrict__ w, bf16* __restrict__ out, int K0,
+                                                          int C0, int K, int T, int C, int CS, int Tp, int mode) {
+  const long long total = (long long)K * C * Tp;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
-  const int j = (int)(i % CS);
-  long long r = i / CS;
-  const int t = (int)(r % Tp);
-  r /= Tp;
-  const int p = (int)(r % (Csrc / CS));
-  const int n = (int)(r / (Csrc / CS));
-  const int cs = p * CS + j;
-  float v = 0.f;
-  if (t < T) v = mode == 0 ? w[((long long)n * T + t) * C + cs] : w[((long long)cs * T + (T - 1 - t)) * C + n];
-  out[i] = f2bf(v);
+  out[i] = f2bf(halo_pack_val(w, K0, C0, K, T, C, CS, Tp, mode, i));
 }
 
-extern "C" int fn_halo_pack_w(const float* w, void* out, int K, int T, int C, int mode, int stage_k, hipStream_t st) {
+// w: [K0][T][C0] fp32 (K0 <= K, C0 <= C)
+extern "C" int fn_halo_pack_w(const float* w, void* out, int K0, int C0, int K, int T, int C, int mode, int stage_k,
+                              hipStream_t st) {
   const int Csrc = mode == 0 ? C : K;
   const int CS = Csrc % 16 == 0 ? 16 : (Csrc % 8 == 0 ? 8 : 0);
-  if (CS == 0 || stage_k % CS) return -2;
+  if (CS == 0 || stage_k % CS || K0 <= 0 || C0 <= 0 || K0 > K || C0 > C) return -2;
   const int tps = stage_k / CS;
   const int Tp = (T + tps - 1) / tps * tps;
-  const long long total = (long long)(mode == 0 ? K : C) * Csrc * Tp;
-  hipLaunchKernelGGL(halo_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (bf16*)out, K, T,
-                     C, CS, Tp, mode);
+  const long long total = (long long)K * C * Tp;
+  hipLaunchKernelGGL(halo_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (bf16*)out, K0, C0,
+                     K, T, C, CS, Tp, mode);
   FN_CHECK_LAUNCH();
   return 0;
 }

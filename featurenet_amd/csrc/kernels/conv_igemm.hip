@@ -37,6 +37,7 @@
 //   * XCD-aware block remap so neighbouring tiles (which share input halos /
 //     the same rows of x) run on the same XCD's L2.
 #include "common.h"
+#include "pack_w.h"
 
 struct GatherGeom {
   int RD, RH, RW;          // row decode dims: m -> (n, r1, r2, r3)
@@ -726,22 +727,23 @@ __global__ __launch_bounds__(256) void igemm_pack_w_kernel(const float* __restri
                                                            int KW, int R, long long total) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
-  const int row = (int)(i / ld), col = (int)(i % ld);
-  float v = 0.f;
-  if (mode == 0) {
-    const int t = col / C, c = col % C;
-    if (t < T && row < K0 && c < C0) v = w[((long long)row * T + t) * C0 + c];
-  } else if (mode == 1) {
-    const int t = col / K, k = col % K;
-    if (t < T && k < K0 && row < C0) v = w[((long long)k * T + t) * C0 + row];
-  } else {
-    const int r = col / R, p = col % R;
-    if (p < KW * C && row < K0) {
-      const int t = r * KW + p / C, c = p % C;
-      if (t < T && c < C0) v = w[((long long)row * T + t) * C0 + c];
-    }
-  }
-  out[i] = f2bf(v);
+  out[i] = f2bf(ig_pack_val(w, K0, C0, K, T, C, mode, ld, KW, R, i));
+}
+
+// Many weight packs in one launch (a model's forward and dgrad B operands at the start of its
+// forward, ops/conv.py pack_scope): thread i finds its job by a scan of the (<= 24) job starts
+// -- the NAS candidate step ran one 3-5 us launch per conv per direction
+__global__ __launch_bounds__(256) void pack_w_multi_kernel(const PackJobs js) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= js.total) return;
+  int k = 0;
+  while (k + 1 < js.n && i >= js.j[k + 1].start) ++k;
+  const PackJob& jb = js.j[k];
+  const long long e = i - jb.start;
+  const int* a = jb.a;
+  const float v = jb.kind <= 2 ? ig_pack_val(jb.w, a[0], a[1], a[2], a[3], a[4], jb.kind, a[5], a[6], a[7], e)
+                               : halo_pack_val(jb.w, a[0], a[1], a[2], a[3], a[4], a[5], a[6], jb.kind - 3, e);
+  jb.out[e] = f2bf(v);
 }
 
 extern "C" int fn_igemm_pack_w(const float* w, void* out, int K0, int C0, int K, int T, int C, int mode, int ld, int KW,
@@ -753,6 +755,46 @@ extern "C" int fn_igemm_pack_w(const float* w, void* out, int K0, int C0, int K,
   const long long total = (long long)rows * ld;
   hipLaunchKernelGGL(igemm_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (bf16*)out, K0, C0,
                      K, T, C, mode, ld, KW, R, total);
+  FN_CHECK_LAUNCH();
+  return 0;
+}
+
+// jobs: n rows of 12 int64 (w, out, kind, a[0..8]); the element counts follow from kind and a
+// (checked as fn_igemm_pack_w / fn_halo_pack_w check their arguments)
+extern "C" int fn_pack_w_multi(const long long* jobs, int n, hipStream_t st) {
+  if (n <= 0 || n > FN_PACK_MAXJ) return -2;
+  PackJobs js{};
+  long long start = 0;
+  for (int k = 0; k < n; ++k) {
+    const long long* r = jobs + 12 * k;
+    PackJob& jb = js.j[k];
+    jb.w = reinterpret_cast<const float*>(r[0]);
+    jb.out = reinterpret_cast<bf16*>(r[1]);
+    jb.kind = (int)r[2];
+    for (int q = 0; q < 9; ++q) jb.a[q] = (int)r[3 + q];
+    const int* a = jb.a;
+    long long cnt;
+    if (jb.kind <= 2) {
+      const int K0 = a[0], C0 = a[1], K = a[2], T = a[3], C = a[4], mode = jb.kind, ld = a[5], KW = a[6], R = a[7];
+      if (K0 <= 0 || C0 <= 0 || K0 > K || C0 > C || T <= 0 || ld <= 0) return -2;
+      const long long need = mode == 0 ? (long long)T * C : (mode == 1 ? (long long)T * K : (long long)(T / KW) * R);
+      if (ld < need || (mode == 2 && (KW <= 0 || T % KW || R < KW * C || ld != (T / KW) * R))) return -2;
+      cnt = (long long)(mode == 1 ? C : K) * ld;
+    } else if (jb.kind <= 4) {
+      const int K0 = a[0], C0 = a[1], K = a[2], T = a[3], C = a[4], CS = a[5], Tp = a[6];
+      const int Csrc = jb.kind == 3 ? C : K;
+      if (K0 <= 0 || C0 <= 0 || K0 > K || C0 > C || CS <= 0 || Csrc % CS || T <= 0 || Tp < T) return -2;
+      cnt = (long long)(jb.kind == 3 ? K : C) * Csrc * Tp;
+    } else {
+      return -2;
+    }
+    if (!jb.w || !jb.out) return -2;
+    jb.start = start;
+    start += cnt;
+  }
+  js.n = n;
+  js.total = start;
+  hipLaunchKernelGGL(pack_w_multi_kernel, dim3((unsigned)((start + 255) / 256)), dim3(256), 0, st, js);
   FN_CHECK_LAUNCH();
   return 0;
 }

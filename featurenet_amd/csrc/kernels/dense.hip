@@ -271,7 +271,9 @@ __global__ __launch_bounds__(DN_THREADS) void dense_fwd_reduce_kernel(const floa
 // element-wise otherwise -- the 10 / 24 / 84-wide NAS heads).
 // LDS (dynamic): W tile transposed to [64 kk][NP + 8] bf16.
 // ya (optional): the layer's activation output -- g is then dy * act'(y) (the activation
-// backward applied as g is loaded, no separate pass)
+// backward applied as g is loaded, no separate pass).  (Batched, double-buffered g loads -- all
+// 16 fragments of a 128-wide n chunk issued together, the first during the W staging -- ran
+// FC1's dgrad at 31.1 us against 24.7 us: 196 registers, half the waves per SIMD)
 __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __restrict__ g,
                                                                  const float* __restrict__ w,
                                                                  bf16* __restrict__ dx, int M, int N, int K,
@@ -360,7 +362,8 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
 // zero rows to a multiple of 32); any K, N (element loads where rows are not 16-B aligned).
 // LDS (dynamic): x tile transposed [64 kk][M + 8], g tile transposed [64 n][M + 8].
 // NB = 2: 128 n columns per workgroup (the x tile -- FC1's 16 MB activation -- staged once for
-// both 64-column halves instead of once per half; a wave then holds 8 accumulator tiles)
+// both 64-column halves instead of once per half; a wave then holds 8 accumulator tiles).
+// (Staging four items' loads before their LDS writes ran FC1's wgrad at 29.1 us against 25.0 us.)
 template <int NB>
 __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __restrict__ g,
                                                                  const bf16* __restrict__ x,
@@ -463,17 +466,22 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
-// column waves per forward workgroup: 2 (128 columns, x rows read once) when N > 64
-static int dn_ncw(int N) {
+// column waves per forward workgroup: 2 (128 columns, x rows read once) when N > 64 and the
+// batch spans row blocks (inference chunks); one 128-row block (FC1 at training batch 128) takes
+// 64-column workgroups -- 250 of them over K, one per CU: 30.6 us against 37.8 us for 128-column
+// workgroups over 250 K slices (scripts/bench_fc_native.py, FN_DENSE_NCW A/B)
+static int dn_ncw(int M, int N) {
   static const int forced = [] { const char* e = getenv("FN_DENSE_NCW"); return e ? atoi(e) : 0; }();   // (A/B)
   if (forced == 1 || forced == 2) return forced;
-  return N > 64 ? 2 : 1;
+  return N > 64 && M > 128 ? 2 : 1;
 }
 
 extern "C" int fn_dense_splits(int M, int N, int K) {
-  const int ncw = dn_ncw(N);
+  const int ncw = dn_ncw(M, N);
   const int tiles = ((N + 64 * ncw - 1) / (64 * ncw)) * ((M + 127) / 128);
-  const int target = 512 / ncw;                  // ~2048 waves: 2 per SIMD
+  // workgroups: ~256 (one per CU) for one row block -- longer K per slice, half the partial
+  // slab (the same FC1 A/B: 500 workgroups 39.2 us, 250 30.6 us) -- else ~2048 waves, 2 per SIMD
+  const int target = M <= 128 ? 256 : 512 / ncw;
   int S = (target + tiles - 1) / tiles;
   const int maxS = K / 256 > 0 ? K / 256 : 1;   // >= 256 k per slice
   return S < 1 ? 1 : (S > maxS ? maxS : S);
@@ -522,7 +530,7 @@ extern "C" int fn_dense_fwd(const void* x, const void* w, const float* bias, voi
   int kc = (K + S - 1) / S;
   kc = (kc + 31) / 32 * 32;
   const int Sr = (K + kc - 1) / kc;              // slices actually covering K
-  const int ncw = dn_ncw(N);
+  const int ncw = dn_ncw(M, N);
   if (wbf16) {
     if (ncw == 2) dn_fwd<true, 2>(x, w, bias, out, part, M, N, K, kc, Sr, act, out_fp32, st);
     else dn_fwd<true, 1>(x, w, bias, out, part, M, N, K, kc, Sr, act, out_fp32, st);

@@ -34,6 +34,7 @@ reference's "build returns None" semantics.
 """
 from __future__ import annotations
 
+import importlib
 import math
 from dataclasses import dataclass
 
@@ -43,6 +44,8 @@ from torch import nn
 from .. import ops
 from ..models.layers import AxisBatchNorm, Conv, Dense, DepthwiseConv, Pool, SeparableConv
 from .spec import CellSpec, InputSpec, ModelSpec, OpSpec
+
+conv_ops = importlib.import_module("..ops.conv", __package__)   # (the module: ops.conv is the conv function)
 
 MIN_FEATURES, MAX_FEATURES = 6, 2048
 MAX_PARAMS = 20_000_000
@@ -433,6 +436,12 @@ class CandidateNet(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda and x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
+        # every conv weight pack of the candidate in one launch (ops/conv.py pack_scope; a no-op
+        # on the CPU)
+        with conv_ops.pack_scope(self):
+            return self._run(x)
+
+    def _run(self, x: torch.Tensor) -> torch.Tensor:
         vals: list = [None] * len(self.prog)
         for i, (kind, arg, ins) in enumerate(self.prog):
             if kind == "input":

@@ -23,6 +23,7 @@ import dataclasses
 import math
 import os
 import threading
+import weakref
 
 import numpy as np
 import torch
@@ -94,23 +95,175 @@ def kdim_gather(spec: ConvSpec) -> int:
     return spec.KD * spec.KH * packw_row(spec) if gather_mode(spec) == GM_PACKW else spec.kdim
 
 
+def _ig_pack_geom(spec: ConvSpec, mode: int) -> tuple[int, int, int]:
+    """(rows, ld, R) of the igemm_pack_w layout ``mode``."""
+    if mode == 2:
+        R = packw_row(spec)
+        return spec.K, spec.KD * spec.KH * R, R
+    return (spec.C if mode == 1 else spec.K), ((spec.taps * (spec.K if mode == 1 else spec.C)) + 7) // 8 * 8, 0
+
+
 def _native_pack(w: torch.Tensor, spec: ConvSpec, mode: int) -> tuple[torch.Tensor, int]:
     """One igemm_pack_w launch: fp32 ``w`` [K0, KD, KH, KW, C0] (K0 <= spec.K, C0 <= spec.C: the
     missing rows / channels are zeros) -> the bf16 B rows of mode 0 (forward), 1 (dgrad:
-    [C][taps*K]) or 2 (packed-W forward), row stride padded to 8."""
+    [C][taps*K]) or 2 (packed-W forward), row stride padded to 8.  Inside a :class:`pack_scope`
+    the model's forward has made it already (one launch for every layer)."""
+    hit = _pack_lookup(w, spec, mode)
+    if hit is not None:
+        return hit
     wf = w.detach().float().contiguous()
-    T = spec.taps
-    if mode == 2:
-        R = packw_row(spec)
-        ld = spec.KD * spec.KH * R
-    else:
-        R = 0
-        ld = ((T * (spec.K if mode == 1 else spec.C)) + 7) // 8 * 8
-    rows = spec.C if mode == 1 else spec.K
+    rows, ld, R = _ig_pack_geom(spec, mode)
     out = torch.empty(rows, ld, dtype=torch.bfloat16, device=w.device)
-    _native.kernels().igemm_pack_w(wf.data_ptr(), out.data_ptr(), wf.shape[0], wf.shape[-1], spec.K, T, spec.C, mode, ld,
-                                   spec.KW, R, _native.stream(wf), [wf.numel(), out.numel()])
+    _native.kernels().igemm_pack_w(wf.data_ptr(), out.data_ptr(), wf.shape[0], wf.shape[-1], spec.K, spec.taps, spec.C,
+                                   mode, ld, spec.KW, R, _native.stream(wf), [wf.numel(), out.numel()])
+    _pack_record(w, spec, mode)
     return out, ld
+
+
+# ---------------------------------------------------------------------------
+# a model forward's weight packs in one launch
+# ---------------------------------------------------------------------------
+# NAS candidates run one 3-5 us pack launch per conv and direction (forward B rows, dgrad B
+# rows; gather and halo layouts): ~4 of a LeNet step's ~43 kernels.  A model forward run in a
+# pack_scope makes every pack its layers made before -- recorded the first time they miss --
+# in ONE pack_w_multi launch up front; the layers (and their backward: ConvFn keeps the forward's
+# generation in ctx) take the packed operands from that generation's cache.  A generation's
+# cache is dropped when the model's next scope opens, so a pack never outlives the weights it
+# was made from (the optimizer step comes between two forwards).
+_PK_MAXJ = 24                           # jobs per launch (csrc pack_w.h FN_PACK_MAXJ)
+_PK_LOCK = threading.Lock()
+_PK_NEXT = [0]
+
+
+class _PackGen:
+    """One scope's packs: cache {key: packed (igemm: (out, ld))}, the model's plan and its
+    parameters by data pointer.  Held by the model (the current one only) and reachable by
+    generation number through a weak map, so a dropped candidate takes its packs with it."""
+    __slots__ = ("cache", "plan", "params", "__weakref__")
+
+    def __init__(self, plan, params):
+        self.cache, self.plan, self.params = {}, plan, params
+
+
+_PK_GENS = weakref.WeakValueDictionary()   # generation -> _PackGen
+
+
+class _PackTLS(threading.local):
+    gen = None                          # the generation this thread's conv calls belong to
+
+
+_PK_TLS = _PackTLS()
+
+
+def _pack_key(w: torch.Tensor, spec: ConvSpec, kind: int):
+    return (w.data_ptr(), tuple(w.shape), spec, kind)
+
+
+def _pack_lookup(w: torch.Tensor, spec: ConvSpec, kind: int):
+    gen = _PK_TLS.gen
+    g = _PK_GENS.get(gen) if gen is not None else None
+    return None if g is None else g.cache.get(_pack_key(w, spec, kind))
+
+
+def _pack_record(w: torch.Tensor, spec: ConvSpec, kind: int):
+    """A pack made outside the cache: the scope's model makes it up front from now on (model
+    parameters only -- fp32, contiguous; a per-step temporary is not recorded)."""
+    gen = _PK_TLS.gen
+    g = _PK_GENS.get(gen) if gen is not None else None
+    if g is None:
+        return
+    p = g.params.get(w.data_ptr())
+    if p is None or tuple(p.shape) != tuple(w.shape):
+        return
+    with _PK_LOCK:
+        g.plan.setdefault(_pack_key(w, spec, kind), (p, spec, kind))
+
+
+def _pack_job(p: torch.Tensor, spec: ConvSpec, kind: int):
+    """(job row, output, cache value) of one recorded pack."""
+    K0, C0 = p.shape[0], p.shape[-1]
+    T = spec.taps
+    if kind <= 2:
+        rows, ld, R = _ig_pack_geom(spec, kind)
+        out = torch.empty(rows, ld, dtype=torch.bfloat16, device=p.device)
+        a = [K0, C0, spec.K, T, spec.C, ld, spec.KW, R, 0]
+        val = (out, ld)
+    else:
+        dgrad = kind == 4
+        ncol, csrc = (spec.C, spec.K) if dgrad else (spec.K, spec.C)
+        cs = halo_cs(csrc)
+        tps = 128 // cs
+        Tp = (T + tps - 1) // tps * tps
+        out = torch.empty(ncol, csrc * Tp, dtype=torch.bfloat16, device=p.device)
+        a = [K0, C0, spec.K, T, spec.C, cs, Tp, 0, 0]
+        val = out
+    return [p.data_ptr(), out.data_ptr(), kind] + a, out, val
+
+
+class pack_scope:
+    """``with pack_scope(model): y = <model body>`` -- the weight packs of the model's convs in
+    one launch at the start (see above).  No-op on the CPU or without the native kernels."""
+
+    def __init__(self, model: torch.nn.Module):
+        self.model = model
+        self.prev = None
+
+    def __enter__(self):
+        m = self.model
+        self.prev = _PK_TLS.gen
+        plist = [p for p in m.parameters() if p.is_cuda]
+        if not plist or not _native.kernels_available():
+            _PK_TLS.gen = None
+            return self
+        params = {p.data_ptr(): p for p in plist if p.dtype == torch.float32 and p.is_contiguous()}
+        plan = m.__dict__.setdefault("_pack_plan", {})
+        g = _PackGen(plan, params)
+        with _PK_LOCK:
+            _PK_NEXT[0] += 1
+            gen = _PK_NEXT[0]
+            _PK_GENS[gen] = g
+        m.__dict__["_pack_gen"] = gen
+        m.__dict__["_pack_gen_obj"] = g          # (the previous generation's packs go with it)
+        jobs, ext, cache = [], [], g.cache
+        grad = torch.is_grad_enabled()
+        for key, (p, spec, kind) in list(plan.items()):
+            if p.data_ptr() != key[0] or params.get(key[0]) is not p:
+                plan.pop(key, None)              # (the parameter moved: re-recorded on its next miss)
+                continue
+            if kind in (1, 4) and not grad:
+                continue                         # (no backward under no_grad)
+            row, out, val = _pack_job(p, spec, kind)
+            jobs.append(row)
+            ext.append((p.numel(), out.numel()))
+            cache[key] = val
+        st = _native.stream(plist[0]) if jobs else None
+        for i in range(0, len(jobs), _PK_MAXJ):
+            chunk = jobs[i:i + _PK_MAXJ]
+            _native.kernels().pack_w_multi([v for r in chunk for v in r], st,
+                                           [v for e in ext[i:i + _PK_MAXJ] for v in e])
+        _PK_TLS.gen = gen
+        return self
+
+    def __exit__(self, *exc):
+        _PK_TLS.gen = self.prev
+        return False
+
+
+class _pack_gen_as:
+    """The conv calls of a backward belong to its forward's generation."""
+
+    def __init__(self, gen):
+        self.gen = gen
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = _PK_TLS.gen
+        _PK_TLS.gen = self.gen
+        return self
+
+    def __exit__(self, *exc):
+        _PK_TLS.gen = self.prev
+        return False
 
 
 def pad_to_spec(w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
@@ -275,18 +428,25 @@ def halo_dgrad_plan(spec: ConvSpec):
 
 
 def halo_pack(w: torch.Tensor, spec: ConvSpec, dgrad: bool) -> torch.Tensor:
-    """Halo-kernel B operand of a conv weight [K, KD, KH, KW, C]: forward layout, or the
-    dgrad layout (taps reversed, K <-> C); one HIP launch on GPU."""
+    """Halo-kernel B operand of a conv weight [K0, KD, KH, KW, C0] (K0 <= spec.K, C0 <= spec.C:
+    missing output / input channels are zeros): forward layout, or the dgrad layout (taps
+    reversed, K <-> C); one HIP launch on GPU (or from the :class:`pack_scope` cache)."""
     if w.is_cuda and _native.kernels_available():
+        kind = 4 if dgrad else 3
+        hit = _pack_lookup(w, spec, kind)
+        if hit is not None:
+            return hit
         wf = w.detach().float().contiguous()
         ncol, csrc = (spec.C, spec.K) if dgrad else (spec.K, spec.C)
         cs = halo_cs(csrc)
         tps = 128 // cs
         Tp = (spec.taps + tps - 1) // tps * tps
         out = torch.empty(ncol, csrc * Tp, dtype=torch.bfloat16, device=w.device)
-        _native.kernels().halo_pack_w(wf.data_ptr(), out.data_ptr(), spec.K, spec.taps, spec.C, int(dgrad), 128,
-                                      _native.stream(wf))
+        _native.kernels().halo_pack_w(wf.data_ptr(), out.data_ptr(), wf.shape[0], wf.shape[-1], spec.K, spec.taps, spec.C,
+                                      int(dgrad), 128, _native.stream(wf), [wf.numel(), out.numel()])
+        _pack_record(w, spec, kind)
         return out
+    w = pad_to_spec(w, spec)
     w3 = w.reshape(spec.K, spec.taps, spec.C)
     return halo_weights(w3.flip(1).permute(2, 1, 0) if dgrad else w3)
 
@@ -417,10 +577,12 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
     # the tile kernel's epilogue has the identity and relu only
     tplan = conv_tile.fwd_plan(spec) if w is not None and act in (0, act_code("relu")) else None
     plan = halo_fwd_plan(spec) if w is not None else None
+    # (``w`` may have fewer channels than spec: the halo packing zero-fills them itself, the tile
+    # kernel takes the padded weight)
     if tplan is not None and (plan is None or conv_tile.choose(
-            "fwd", spec, lambda: conv_tile.conv_fwd(x5, w, bias, spec, act, want_stats, tplan),
+            "fwd", spec, lambda: conv_tile.conv_fwd(x5, pad_to_spec(w, spec), bias, spec, act, want_stats, tplan),
             lambda: halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan))):
-        return conv_tile.conv_fwd(x5, w, bias, spec, act, want_stats, tplan, dstash=dstash)
+        return conv_tile.conv_fwd(x5, pad_to_spec(w, spec), bias, spec, act, want_stats, tplan, dstash=dstash)
     if plan is not None:
         return halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan)
     K = _native.kernels()
@@ -451,8 +613,9 @@ def native_conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec: ConvSpec, bn=Non
     """dx of the conv.  ``bn = (y, prm, act)`` (x was a BN+act output, :mod:`.bnfuse`): returns
     ``(dx, slab)`` where ``slab`` holds that BN's backward sums from the tile kernel's
     epilogue, or None when another kernel ran.  ``w`` may have fewer output channels than
-    ``spec.K`` (channel-padded dy): zero rows, materialised only for the tile / halo kernels."""
-    if w.shape[0] != spec.K and (conv_tile.dgrad_plan(spec) is not None or halo_dgrad_plan(spec) is not None):
+    ``spec.K`` (channel-padded dy): zero rows, materialised only for the tile kernel (the halo
+    and gather packings zero-fill them)."""
+    if w.shape[0] != spec.K and conv_tile.dgrad_plan(spec) is not None:
         w = pad_to_spec(w, spec)
     if bn is not None:
         tplan = conv_tile.dgrad_plan(spec)
@@ -919,11 +1082,12 @@ class ConvFn(torch.autograd.Function):
             # (the tile forward also packs the backward's dgrad weights, in the same launch)
             ctx.dstash = {} if ctx.needs_input_grad[0] else None
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats,
-                                       w=pad_to_spec(w.detach(), spec), dstash=ctx.dstash)
+                                       w=w.detach(), dstash=ctx.dstash)
         else:
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
         ctx.spec, ctx.act, ctx.has_b, ctx.s2d = spec, act, b is not None, s2d   # (channel-padded spec when cpad)
+        ctx.pack_gen = _PK_TLS.gen                      # (the backward's packs: this forward's scope)
         ctx.bparam = b
         ctx.set_materialize_grads(False)                # no zero-filled gradient for the stats output
         ctx.x_needs = ctx.needs_input_grad[0]
@@ -940,6 +1104,11 @@ class ConvFn(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         if dy is None:
             return None, None, None, None, None, None
+        with _pack_gen_as(ctx.pack_gen):
+            return ConvFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         x5, w, y = ctx.saved_tensors
         spec, act = ctx.spec, ctx.act
         dy = dy.contiguous().to(torch.bfloat16)

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--template", default="lenet5")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--list", action="store_true")
+    ap.add_argument("--stacks", action="store_true", help="with --list: the package frames that launched torch glue")
     a = ap.parse_args()
     from featurenet_amd.ir.compile import compile_model
     from featurenet_amd.ir.parse import parse_feature_model
@@ -50,19 +51,36 @@ def main():
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
 
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=a.stacks) as prof:
         step()
         torch.cuda.synchronize()
     rows = []
     for e in prof.profiler.function_events:
-        if not e.kernels or any(c.kernels for c in e.cpu_children):
-            continue                              # (kernels sit under the innermost launching op)
+        # an op's own launches: a kernel a child op lists as well belongs to the child (the
+        # native kernels of an autograd node with torch glue inside it are its own -- skipping
+        # every op with a launching child dropped them)
+        child = {(k.name, k.duration) for c in e.cpu_children for k in c.kernels}
         for k in e.kernels:
-            rows.append((e.time_range.start, k.name, k.duration, e.name))
-    rows.sort()
+            if (k.name, k.duration) not in child:
+                rows.append((e.time_range.start, k.name, k.duration, e.name, e))
+    rows.sort(key=lambda r: r[0])
     if a.list:
-        for _, name, dur, op in rows:
+        for _, name, dur, op, ev in rows:
             print(f"{dur:8.1f} us  {name[:70]:70s}  {op[:40]}")
+            if a.stacks and op.startswith("aten::"):
+                # (the launching op's nearest parents with a Python stack: the package frames)
+                e2, fr = ev, []
+                while e2 is not None and not fr:
+                    fr = [f for f in (e2.stack or []) if "featurenet_amd" in f]
+                    e2 = e2.cpu_parent
+                for f in fr[:4]:
+                    print(f"              <- {f}")
+                if not fr:                        # (no Python stacks recorded: the op chain)
+                    chain, e2 = [], ev.cpu_parent
+                    while e2 is not None and len(chain) < 6:
+                        chain.append(e2.name)
+                        e2 = e2.cpu_parent
+                    print(f"              <- {' <- '.join(chain)}")
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         step()
