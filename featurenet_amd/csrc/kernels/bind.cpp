@@ -388,9 +388,12 @@ PYBIND11_MODULE(_C, m) {
       if (kind >= 0 && kind <= 2) {                // K0, C0, K, T, C, ld
         wn = r[3] * r[6] * r[4];
         on = (kind == 1 ? r[7] : r[5]) * r[8];
-      } else {                                     // K0, C0, K, T, C, CS, Tp
+      } else if (kind <= 4) {                      // K0, C0, K, T, C, CS, Tp
         wn = r[3] * r[6] * r[4];
         on = r[5] * r[7] * r[9];
+      } else {                                     // K, T, C, CS, nks, nct, nslice, dgrad, nt: bf16 x 8 per index
+        wn = r[3] * r[4] * r[5];
+        on = (r[9] * r[7] + 4) * r[8] * 64 * 8;
       }
       std::vector<long long> e = {ext[2 * k], ext[2 * k + 1]};
       fits(e, 0, wn, "pack_w_multi", "w");

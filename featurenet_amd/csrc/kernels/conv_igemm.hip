@@ -733,14 +733,22 @@ __global__ __launch_bounds__(256) void igemm_pack_w_kernel(const float* __restri
 // Many weight packs in one launch (a model's forward and dgrad B operands at the start of its
 // forward, ops/conv.py pack_scope): thread i finds its job by a scan of the (<= 24) job starts
 // -- the NAS candidate step ran one 3-5 us launch per conv per direction
+// Every job starts on a 256-element boundary, so a workgroup lies in one job: the job search and
+// the job's parameters are wave-uniform (scalar loads; a per-lane search over the by-value job
+// table made the FeatureNet-3D pack launch as slow as the three it replaced)
 __global__ __launch_bounds__(256) void pack_w_multi_kernel(const PackJobs js) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= js.total) return;
+  const long long b0 = (long long)blockIdx.x * 256;
   int k = 0;
-  while (k + 1 < js.n && i >= js.j[k + 1].start) ++k;
+  while (k + 1 < js.n && b0 >= js.j[k + 1].start) ++k;
+  k = __builtin_amdgcn_readfirstlane(k);
   const PackJob& jb = js.j[k];
-  const long long e = i - jb.start;
+  const long long e = b0 - jb.start + threadIdx.x;
+  if (e >= jb.count) return;
   const int* a = jb.a;
+  if (jb.kind == 5) {                            // (tile stream: one uint4 per index)
+    tile_pack_w_one(jb.w, reinterpret_cast<uint4*>(jb.out), a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8], e);
+    return;
+  }
   const float v = jb.kind <= 2 ? ig_pack_val(jb.w, a[0], a[1], a[2], a[3], a[4], jb.kind, a[5], a[6], a[7], e)
                                : halo_pack_val(jb.w, a[0], a[1], a[2], a[3], a[4], a[5], a[6], jb.kind - 3, e);
   jb.out[e] = f2bf(v);
@@ -760,7 +768,7 @@ extern "C" int fn_igemm_pack_w(const float* w, void* out, int K0, int C0, int K,
 }
 
 // jobs: n rows of 12 int64 (w, out, kind, a[0..8]); the element counts follow from kind and a
-// (checked as fn_igemm_pack_w / fn_halo_pack_w check their arguments)
+// (checked as fn_igemm_pack_w / fn_halo_pack_w / fn_tile_pack_w check their arguments)
 extern "C" int fn_pack_w_multi(const long long* jobs, int n, hipStream_t st) {
   if (n <= 0 || n > FN_PACK_MAXJ) return -2;
   PackJobs js{};
@@ -785,12 +793,18 @@ extern "C" int fn_pack_w_multi(const long long* jobs, int n, hipStream_t st) {
       const int Csrc = jb.kind == 3 ? C : K;
       if (K0 <= 0 || C0 <= 0 || K0 > K || C0 > C || CS <= 0 || Csrc % CS || T <= 0 || Tp < T) return -2;
       cnt = (long long)(jb.kind == 3 ? K : C) * Csrc * Tp;
+    } else if (jb.kind == 5) {                   // (fn_tile_pack_w's checks)
+      const int CS = a[3], nks = a[4], nct = a[5], nslice = a[6], nt = a[8];
+      if (CS != 8 && CS != 16 && CS % 32 != 0) return -2;
+      if ((nt != 2 && nt != 32) || nct % 2 || nks <= 0 || nslice <= 0) return -2;
+      cnt = ((long long)nslice * nks + 4) * nct * 64;
     } else {
       return -2;
     }
     if (!jb.w || !jb.out) return -2;
     jb.start = start;
-    start += cnt;
+    jb.count = cnt;
+    start += (cnt + 255) / 256 * 256;              // (workgroup-aligned job starts)
   }
   js.n = n;
   js.total = start;

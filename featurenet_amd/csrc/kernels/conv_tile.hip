@@ -38,6 +38,7 @@
 //
 // Dgrad uses the same kernel: dx = conv(dy, flip(W)^T) with leading pads K-1-p.
 #include "conv_tile_shared.h"
+#include "pack_w.h"
 
 #include <cstdio>
 #include <type_traits>
@@ -802,78 +803,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
 // ---------------------------------------------------------------------------
 // weight packing: conv weight [K][T][C] (fp32) -> MFMA B fragments
 // ---------------------------------------------------------------------------
-// out[((slice * nks + ks) * nct + ct) * 64 + lane][j] (8 bf16 per lane) =
-//   Wsrc[col = ct*16 + (lane & 15)][tap][ch], k-step ks of slice:
-//     CS >= 32: tap = ks / (CS/32), ch = slice*CS + (ks % (CS/32))*32 + (lane>>4)*8 + j
-//     CS == 16: tap = 2*ks + (lane>>5), ch = slice*16 + ((lane>>4)&1)*8 + j
-//     CS == 8:  tap = 4*ks + (lane>>4), ch = slice*8 + j
-//   forward: Wsrc[col][tap][ch] = w[col][tap][ch]          (Ncol = K, Csrc = C)
-//   dgrad:   Wsrc[col][tap][ch] = w[ch][T-1-tap][col]      (Ncol = C, Csrc = K)
-// zero for tap >= T or col >= Ncol.
-__device__ __forceinline__ void tile_pack_w_one(const float* __restrict__ w, uint4* __restrict__ out, int K, int T,
-                                                int C, int CS, int nks, int nct, int nslice, int dgrad, int nt,
-                                                long long i) {
-  if (i >= (long long)nslice * nks * nct * 64) {
-    out[i] = make_uint4(0u, 0u, 0u, 0u);
-    return;
-  }
-  const int lane = (int)(i % 64);
-  long long r = i / 64;
-  const int ct = (int)(r % nct);
-  r /= nct;
-  const int ks = (int)(r % nks);
-  const int slice = (int)(r / nks);
-  const int Ncol = dgrad ? C : K;
-  // column order inside each nt*16-column block: fragment ct%nt, row i holds output column
-  // 4nt*(i/4) + 4*(ct%nt) + i%4, so after the kernel's C^T MFMA a lane's nt fragments give 4nt
-  // consecutive output columns (one 16-B store per 8)
-  int tap, ch0, col;
-  if (nt == 32) {
-    // conv_tile32 (v_mfma_f32_32x32x16_bf16, weights = A): fragment ct = 2 * (32-column block) + j
-    // (k half of the 32-k step); lane l holds MFMA row m = l & 31 -- output column
-    // 16((m>>2)&1) + (m&3) + 4(m>>3) of the block, so a lane half's accumulator holds 16
-    // consecutive columns -- and k = 8(l >> 5) + e
-    const int m = lane & 31, h = lane >> 5, j = ct & 1;
-    col = (ct >> 1) * 32 + 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3);
-    if (CS >= 32) {
-      const int sub = CS / 32;
-      tap = ks / sub;
-      ch0 = slice * CS + (ks % sub) * 32 + 16 * j + 8 * h;
-    } else if (CS == 16) {
-      tap = 2 * ks + j;
-      ch0 = slice * 16 + 8 * h;
-    } else {                                     // CS = 8: taps 4ks + 2j + h
-      tap = 4 * ks + 2 * j + h;
-      ch0 = slice * 8;
-    }
-  } else {
-  const int fi = lane & 15;
-  col = (ct / nt) * nt * 16 + 4 * nt * (fi >> 2) + 4 * (ct % nt) + (fi & 3);
-  if (CS >= 32) {
-    const int sub = CS / 32;
-    tap = ks / sub;
-    ch0 = slice * CS + (ks % sub) * 32 + (lane >> 4) * 8;
-  } else if (CS == 16) {
-    tap = 2 * ks + (lane >> 5);
-    ch0 = slice * 16 + ((lane >> 4) & 1) * 8;
-  } else {                                       // CS = 8: four taps per k-step
-    tap = 4 * ks + (lane >> 4);
-    ch0 = slice * 8;
-  }
-  }
-  Pack8 v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float f = 0.f;
-    if (tap < T && col < Ncol) {
-      const int ch = ch0 + j;
-      f = dgrad ? w[((long long)ch * T + (T - 1 - tap)) * C + col] : w[((long long)col * T + tap) * C + ch];
-    }
-    v.e[j] = f2bf(f);
-  }
-  out[i] = v.u;
-}
-
+// (the element map: pack_w.h tile_pack_w_one)
 __global__ __launch_bounds__(256) void tile_pack_w_kernel(const float* __restrict__ w, uint4* __restrict__ out, int K,
                                                           int T, int C, int CS, int nks, int nct, int nslice,
                                                           int dgrad, int nt) {

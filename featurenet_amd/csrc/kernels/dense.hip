@@ -470,14 +470,18 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
 // batch spans row blocks (inference chunks); one 128-row block (FC1 at training batch 128) takes
 // 64-column workgroups -- 250 of them over K, one per CU: 30.6 us against 37.8 us for 128-column
 // workgroups over 250 K slices (scripts/bench_fc_native.py, FN_DENSE_NCW A/B)
-static int dn_ncw(int M, int N) {
+// -- and so does a layer too shallow to split over K whose 128-column tiles would leave CUs idle
+// (LeNet's 120 -> 84 Dense on 16,384 rows: 128 workgroups of 128 columns)
+static int dn_ncw(int M, int N, int K) {
   static const int forced = [] { const char* e = getenv("FN_DENSE_NCW"); return e ? atoi(e) : 0; }();   // (A/B)
   if (forced == 1 || forced == 2) return forced;
-  return N > 64 && M > 128 ? 2 : 1;
+  if (N <= 64 || M <= 128) return 1;
+  if (K < 512 && ((N + 127) / 128) * ((M + 127) / 128) < 256) return 1;
+  return 2;
 }
 
 extern "C" int fn_dense_splits(int M, int N, int K) {
-  const int ncw = dn_ncw(M, N);
+  const int ncw = dn_ncw(M, N, K);
   const int tiles = ((N + 64 * ncw - 1) / (64 * ncw)) * ((M + 127) / 128);
   // workgroups: ~256 (one per CU) for one row block -- longer K per slice, half the partial
   // slab (the same FC1 A/B: 500 workgroups 39.2 us, 250 30.6 us) -- else ~2048 waves, 2 per SIMD
@@ -530,7 +534,7 @@ extern "C" int fn_dense_fwd(const void* x, const void* w, const float* bias, voi
   int kc = (K + S - 1) / S;
   kc = (kc + 31) / 32 * 32;
   const int Sr = (K + kc - 1) / kc;              // slices actually covering K
-  const int ncw = dn_ncw(M, N);
+  const int ncw = dn_ncw(M, N, K);
   if (wbf16) {
     if (ncw == 2) dn_fwd<true, 2>(x, w, bias, out, part, M, N, K, kc, Sr, act, out_fp32, st);
     else dn_fwd<true, 1>(x, w, bias, out, part, M, N, K, kc, Sr, act, out_fp32, st);

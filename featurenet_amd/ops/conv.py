@@ -23,7 +23,6 @@ import dataclasses
 import math
 import os
 import threading
-import weakref
 
 import numpy as np
 import torch
@@ -33,6 +32,7 @@ from .. import _native
 from . import bnfuse
 from . import conv_tile
 from . import conv_wtile
+from . import packs
 from . import reference as ref
 from ..training.flat import grad_target
 from .spec import ConvSpec, act_code
@@ -120,67 +120,16 @@ def _native_pack(w: torch.Tensor, spec: ConvSpec, mode: int) -> tuple[torch.Tens
     return out, ld
 
 
-# ---------------------------------------------------------------------------
-# a model forward's weight packs in one launch
-# ---------------------------------------------------------------------------
-# NAS candidates run one 3-5 us pack launch per conv and direction (forward B rows, dgrad B
-# rows; gather and halo layouts): ~4 of a LeNet step's ~43 kernels.  A model forward run in a
-# pack_scope makes every pack its layers made before -- recorded the first time they miss --
-# in ONE pack_w_multi launch up front; the layers (and their backward: ConvFn keeps the forward's
-# generation in ctx) take the packed operands from that generation's cache.  A generation's
-# cache is dropped when the model's next scope opens, so a pack never outlives the weights it
-# was made from (the optimizer step comes between two forwards).
-_PK_MAXJ = 24                           # jobs per launch (csrc pack_w.h FN_PACK_MAXJ)
-_PK_LOCK = threading.Lock()
-_PK_NEXT = [0]
-
-
-class _PackGen:
-    """One scope's packs: cache {key: packed (igemm: (out, ld))}, the model's plan and its
-    parameters by data pointer.  Held by the model (the current one only) and reachable by
-    generation number through a weak map, so a dropped candidate takes its packs with it."""
-    __slots__ = ("cache", "plan", "params", "__weakref__")
-
-    def __init__(self, plan, params):
-        self.cache, self.plan, self.params = {}, plan, params
-
-
-_PK_GENS = weakref.WeakValueDictionary()   # generation -> _PackGen
-
-
-class _PackTLS(threading.local):
-    gen = None                          # the generation this thread's conv calls belong to
-
-
-_PK_TLS = _PackTLS()
-
-
-def _pack_key(w: torch.Tensor, spec: ConvSpec, kind: int):
-    return (w.data_ptr(), tuple(w.shape), spec, kind)
-
-
-def _pack_lookup(w: torch.Tensor, spec: ConvSpec, kind: int):
-    gen = _PK_TLS.gen
-    g = _PK_GENS.get(gen) if gen is not None else None
-    return None if g is None else g.cache.get(_pack_key(w, spec, kind))
-
-
-def _pack_record(w: torch.Tensor, spec: ConvSpec, kind: int):
-    """A pack made outside the cache: the scope's model makes it up front from now on (model
-    parameters only -- fp32, contiguous; a per-step temporary is not recorded)."""
-    gen = _PK_TLS.gen
-    g = _PK_GENS.get(gen) if gen is not None else None
-    if g is None:
-        return
-    p = g.params.get(w.data_ptr())
-    if p is None or tuple(p.shape) != tuple(w.shape):
-        return
-    with _PK_LOCK:
-        g.plan.setdefault(_pack_key(w, spec, kind), (p, spec, kind))
+# one-launch packing of a model forward's weights (ops/packs.py): the gather / halo layouts
+# (kinds 0-2: igemm_pack_w modes, 3 / 4: halo forward / dgrad)
+_pack_lookup = packs.lookup
+_pack_record = packs.record
+pack_scope = packs.pack_scope
+_PK_GENS, _PK_TLS = packs.GENS, packs.TLS
 
 
 def _pack_job(p: torch.Tensor, spec: ConvSpec, kind: int):
-    """(job row, output, cache value) of one recorded pack."""
+    """(job row, output, cache value) of one recorded gather / halo pack."""
     K0, C0 = p.shape[0], p.shape[-1]
     T = spec.taps
     if kind <= 2:
@@ -200,70 +149,7 @@ def _pack_job(p: torch.Tensor, spec: ConvSpec, kind: int):
     return [p.data_ptr(), out.data_ptr(), kind] + a, out, val
 
 
-class pack_scope:
-    """``with pack_scope(model): y = <model body>`` -- the weight packs of the model's convs in
-    one launch at the start (see above).  No-op on the CPU or without the native kernels."""
-
-    def __init__(self, model: torch.nn.Module):
-        self.model = model
-        self.prev = None
-
-    def __enter__(self):
-        m = self.model
-        self.prev = _PK_TLS.gen
-        plist = [p for p in m.parameters() if p.is_cuda]
-        if not plist or not _native.kernels_available():
-            _PK_TLS.gen = None
-            return self
-        params = {p.data_ptr(): p for p in plist if p.dtype == torch.float32 and p.is_contiguous()}
-        plan = m.__dict__.setdefault("_pack_plan", {})
-        g = _PackGen(plan, params)
-        with _PK_LOCK:
-            _PK_NEXT[0] += 1
-            gen = _PK_NEXT[0]
-            _PK_GENS[gen] = g
-        m.__dict__["_pack_gen"] = gen
-        m.__dict__["_pack_gen_obj"] = g          # (the previous generation's packs go with it)
-        jobs, ext, cache = [], [], g.cache
-        grad = torch.is_grad_enabled()
-        for key, (p, spec, kind) in list(plan.items()):
-            if p.data_ptr() != key[0] or params.get(key[0]) is not p:
-                plan.pop(key, None)              # (the parameter moved: re-recorded on its next miss)
-                continue
-            if kind in (1, 4) and not grad:
-                continue                         # (no backward under no_grad)
-            row, out, val = _pack_job(p, spec, kind)
-            jobs.append(row)
-            ext.append((p.numel(), out.numel()))
-            cache[key] = val
-        st = _native.stream(plist[0]) if jobs else None
-        for i in range(0, len(jobs), _PK_MAXJ):
-            chunk = jobs[i:i + _PK_MAXJ]
-            _native.kernels().pack_w_multi([v for r in chunk for v in r], st,
-                                           [v for e in ext[i:i + _PK_MAXJ] for v in e])
-        _PK_TLS.gen = gen
-        return self
-
-    def __exit__(self, *exc):
-        _PK_TLS.gen = self.prev
-        return False
-
-
-class _pack_gen_as:
-    """The conv calls of a backward belong to its forward's generation."""
-
-    def __init__(self, gen):
-        self.gen = gen
-        self.prev = None
-
-    def __enter__(self):
-        self.prev = _PK_TLS.gen
-        _PK_TLS.gen = self.gen
-        return self
-
-    def __exit__(self, *exc):
-        _PK_TLS.gen = self.prev
-        return False
+packs.register((0, 1, 2, 3, 4), lambda p, spec, kind: _pack_job(p, spec, kind), lambda spec, kind: kind in (1, 4))
 
 
 def pad_to_spec(w: torch.Tensor, spec: ConvSpec) -> torch.Tensor:
@@ -1104,7 +990,7 @@ class ConvFn(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         if dy is None:
             return None, None, None, None, None, None
-        with _pack_gen_as(ctx.pack_gen):
+        with packs.gen_as(ctx.pack_gen):
             return ConvFn._backward(ctx, dy)
 
     @staticmethod

@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from . import packs
 
 LDS_MAX = 160 * 1024
 NTHR = 320          # 4 MFMA waves + 1 loader wave
@@ -577,14 +578,32 @@ def ktab_tensor(p: TilePlan, kdims: tuple, device) -> torch.Tensor:
 
 def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bool) -> torch.Tensor:
     """Conv weight [K, taps, C] -> the kernel's fragment-ordered B stream (bf16), plus PD
-    zero k-steps that the ring's over-the-end loads read."""
+    zero k-steps that the ring's over-the-end loads read (inside a ``packs.pack_scope``: from
+    the model forward's one pack launch once recorded)."""
+    desc = (K, T, C, p, bool(dgrad))
+    hit = packs.lookup(w, desc, 5)
+    if hit is not None:
+        return hit
     Csrc = K if dgrad else C
     nslice = Csrc // p.CS
     out = torch.empty((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
     wf = w.detach().float().contiguous()
     _native.kernels().tile_pack_w(wf.data_ptr(), out.data_ptr(), K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad),
                                   _native.stream(wf), 32 if p.m32 else p.NT)
+    packs.record(w, desc, 5)
     return out
+
+
+def _pack_job(w: torch.Tensor, desc, kind: int):
+    """(job row, output, cache value) of one recorded tile-stream pack (packs.py kind 5)."""
+    K, T, C, p, dgrad = desc
+    nslice = (K if dgrad else C) // p.CS
+    out = torch.empty((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
+    row = [w.data_ptr(), out.data_ptr(), 5, K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad), 32 if p.m32 else p.NT]
+    return row, out, out
+
+
+packs.register((5,), _pack_job, lambda desc, kind: desc[4])
 
 
 def mask_dgrad_ok(p: TilePlan, ncol: int) -> bool:
@@ -604,7 +623,12 @@ def _pack_params(p: TilePlan, Csrc: int, dgrad: bool) -> list[int]:
 
 def pack_pair(w: torch.Tensor, K: int, T: int, C: int, pf: TilePlan, pd: TilePlan):
     """(forward, dgrad) packed B streams of one weight in one launch (:func:`pack_weights`
-    twice): the forward packs its backward's dgrad operand too."""
+    twice): the forward packs its backward's dgrad operand too (or both come from the scope's
+    up-front launch)."""
+    df, dd = (K, T, C, pf, False), (K, T, C, pd, True)
+    hf, hd = packs.lookup(w, df, 5), packs.lookup(w, dd, 5)
+    if hf is not None and hd is not None:
+        return hf, hd
     outs = []
     for p, dg in ((pf, False), (pd, True)):
         Csrc = K if dg else C
@@ -613,6 +637,8 @@ def pack_pair(w: torch.Tensor, K: int, T: int, C: int, pf: TilePlan, pd: TilePla
     _native.kernels().tile_pack_w2(wf.data_ptr(), outs[0].data_ptr(), outs[1].data_ptr(), K, T, C,
                                    _pack_params(pf, C, False), _pack_params(pd, K, True), _native.stream(wf),
                                    [wf.numel(), outs[0].numel(), outs[1].numel()])
+    packs.record(w, df, 5)
+    packs.record(w, dd, 5)
     return outs[0], outs[1]
 
 

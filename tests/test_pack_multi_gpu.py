@@ -119,3 +119,73 @@ def test_scope_cache_dropped_with_next_forward():
     g2 = model.__dict__["_pack_gen"]
     assert g2 != g1 and g1 not in cv._PK_GENS and g2 in cv._PK_GENS
     assert cv._PK_TLS.gen is None
+
+
+def test_pack_w_multi_tile_streams_match():
+    """Kind 5 (the conv_tile B stream, forward and dgrad) from the many-layer launch == the
+    single-layer tile packing."""
+    ct = importlib.import_module("featurenet_amd.ops.conv_tile")
+    torch.manual_seed(4)
+    rows, outs, ext, singles, ws = [], [], [], [], []
+    for shp, K, k in (((8, 29, 29, 29, 32), 32, 5), ((8, 22, 22, 22, 64), 64, 3)):
+        spec = ConvSpec.make(shp, K, (k, k, k), 1, "valid")
+        w = torch.randn(K, k, k, k, shp[-1], device="cuda")
+        ws.append(w)                                     # (the job rows hold raw pointers: keep w alive)
+        for p, dg in ((ct.fwd_plan(spec), False), (ct.dgrad_plan(spec), True)):
+            assert p is not None
+            singles.append(ct.pack_weights(w, K, spec.taps, spec.C, p, dg))
+            row, out, _ = ct._pack_job(w, (K, spec.taps, spec.C, p, dg), 5)
+            rows.append(row)
+            outs.append(out)
+            ext.append((w.numel(), out.numel()))
+    _native.kernels().pack_w_multi([v for r in rows for v in r], _native.stream(outs[0]), [v for e in ext for v in e])
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(outs, singles)):
+        assert a.shape == b.shape and torch.equal(a, b), i
+
+
+def test_featurenet3d_scope_matches_per_layer_packs(monkeypatch):
+    """FeatureNet-3D training steps (tile-kernel convs: forward + dgrad streams recorded, then made
+    by the scope's one launch) == the same steps with every layer packing its own weights."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+    from featurenet_amd.ops import softmax_xent
+
+    packs = importlib.import_module("featurenet_amd.ops.packs")
+    res, hits = [], []
+    orig = packs.lookup
+
+    def counting(w, desc, kind):
+        r = orig(w, desc, kind)
+        if r is not None:
+            hits.append(kind)
+        return r
+
+    for scoped in (False, True):
+        if not scoped:
+            monkeypatch.setattr(packs, "pack_scope", lambda m: contextlib.nullcontext())
+        else:
+            monkeypatch.setattr(packs, "lookup", counting)
+        torch.manual_seed(5)
+        m = FeatureNet3D(FeatureNet3DConfig(input_size=64, num_classes=24)).cuda()
+        x = (torch.rand(8, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
+        y = torch.randint(0, 24, (8,), device="cuda")
+        run = []
+        for _ in range(3):
+            m.zero_grad(set_to_none=True)
+            loss = softmax_xent(m(x), y)
+            loss.backward()
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.add_(p.grad, alpha=-1e-3)
+            torch.cuda.synchronize()
+            run.append((loss.detach().clone(), {n: p.detach().clone() for n, p in m.named_parameters()}))
+        monkeypatch.undo()
+        if scoped:
+            kinds = [k[3] for k in m.__dict__.get("_pack_plan", {})]
+            assert kinds.count(5) >= 6, kinds           # conv2-4: forward + dgrad streams
+            assert hits.count(5) >= 2 * 6, hits         # steps 2 and 3 took them from the scope
+        res.append(run)
+    for i, ((la, pa), (lb, pb)) in enumerate(zip(*res)):
+        assert torch.equal(la, lb), (i, la.item(), lb.item())
+        for n in pa:
+            assert torch.equal(pa[n], pb[n]), (i, n)
