@@ -3,8 +3,9 @@
 
 Forward (bias + activation epilogue, BN statistics epilogue) and dgrad at the
 FeatureNet-3D layer shapes, at a small batch and at a production-size batch
-whose tile count is many times the 256 persistent workgroups (dynamic tile
-schedule, halo double buffering across jobs, multi-slice jobs), plus
+whose tile count is many times the 256 persistent workgroups (the static tile schedule
+with BN statistics, the dynamic one without, halo double buffering across jobs, multi-slice
+jobs), plus
 same-padded / 2-D / multi-column-block shapes from the NAS search space.
 """
 import pytest

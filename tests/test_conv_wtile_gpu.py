@@ -1,10 +1,10 @@
 """Big-tile weight-gradient kernel (``csrc/kernels/conv_wtile.hip``) vs the fp32 reference.
 
 FeatureNet-3D layer shapes at a small batch and at production-size batches whose tile
-count is many times the workgroups of every (XCD, column group) (dynamic per-XCD tile
-counters, double-buffered jobs), the segmentation decoder conv ('same' padding, 64 input
+count is many times the workgroups of every (XCD, column group) (static per-workgroup tile
+sets, double-buffered jobs), the segmentation decoder conv ('same' padding, 64 input
 channels = 4 slices), a 2-D conv, Cout 16, in-place accumulation into ``out`` and
-repeated launches (the tile counters reset themselves).
+repeated launches (accumulating into the same output).
 """
 import pytest
 import torch
@@ -72,7 +72,7 @@ def test_wtile_accumulates_into_out_and_repeats():
     p = cw.plan(spec)
     want = _ref_dw(x, dy, spec)
     out = torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device="cuda")
-    for _ in range(3):                               # three launches accumulate 3x (counters reset)
+    for _ in range(3):                               # three launches accumulate 3x
         cw.conv_wgrad(dy, x, spec, p, out=out)
     rel, mx = _rel(out.reshape(want.shape) / 3, want)
     assert rel < 5e-3 and mx < 2e-2, (rel, mx)
