@@ -48,7 +48,7 @@ int fn_dw_dgrad(const void*, const float*, void*, const int*, hipStream_t);
 int fn_dw_wgrad(const void*, const void*, float*, const int*, int, hipStream_t, float*);
 int fn_conv_halo_wgrad(const void*, const void*, float*, float*, const int*, int, int, hipStream_t);
 int fn_conv_halo_wgrad_gx(const int*, int);
-int fn_s2d_pack(const void*, void*, const int*, int, hipStream_t);
+int fn_s2d_pack(const void*, void*, const int*, int, hipStream_t, int);
 int fn_dense_splits(int, int, int);
 int fn_ew_binary(const void*, const void*, void*, long long, int, hipStream_t);
 int fn_ew_mul_bwd(const void*, const void*, const void*, void*, void*, long long, hipStream_t);
@@ -491,9 +491,10 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_s2d_weight_map(P<const float*>(src), P<float*>(dst), geom.data(), dir, S(st)), "s2d_weight_map");
   }, py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("dir"), py::arg("st"),
      py::arg("ext") = std::vector<long long>());
-  m.def("s2d_pack", [](uintptr_t x, uintptr_t out, std::vector<int> geom, uintptr_t st) {
+  m.def("s2d_pack", [](uintptr_t x, uintptr_t out, std::vector<int> geom, uintptr_t st, int u8) {
+    // u8: x holds uint8 voxels (binary occupancy), else bf16
     if (geom.size() != 12 && geom.size() != 15) throw std::runtime_error("s2d_pack: geometry of 12 or 15 ints");
-    chk(fn_s2d_pack(P<const void*>(x), P<void*>(out), geom.data(), (int)geom.size(), S(st)), "s2d_pack");
+    chk(fn_s2d_pack(P<const void*>(x), P<void*>(out), geom.data(), (int)geom.size(), S(st), u8), "s2d_pack");
   });
   m.def("conv_halo_f8", [](uintptr_t src, uintptr_t wt, uintptr_t scale, uintptr_t bias, uintptr_t out,
                            float inv_out_scale, uintptr_t toffs, std::vector<int> geom, int ncol, int out_f8, int relu,

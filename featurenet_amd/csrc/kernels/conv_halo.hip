@@ -956,7 +956,13 @@ extern "C" int fn_conv_halo_wgrad(const void* dy, const void* src, float* dw, fl
 // ((a * sh + b) * sw + c) * C + ci = x[n][d2*sd + a][h2*sh + b][w2*sw + c][ci]
 // (zero outside x).  One thread per output position, one 16-B store per 8
 // channels; a 1-channel stride-2 stem reads 4 bf16 pairs per position.
-__global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
+// T: bf16, or uint8 (binary voxel occupancy stored as bytes -- a quarter of the copy-in and of this
+// kernel's reads; 0 / 1 convert exactly)
+__device__ __forceinline__ float s2d_in(bf16 v) { return bf2f(v); }
+__device__ __forceinline__ float s2d_in(unsigned char v) { return (float)v; }
+
+template <typename T>
+__global__ __launch_bounds__(256) void s2d_pack_kernel(const T* __restrict__ x, bf16* __restrict__ out,
                                                         int N, int D, int H, int W, int C, int sd, int sh, int sw,
                                                         int D2, int H2, int W2, int CO, int pd, int ph, int pw) {
   const long long npos = (long long)N * D2 * H2 * W2;
@@ -966,15 +972,21 @@ __global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ 
   const long long n = p / ((long long)W2 * H2 * D2);
   const int creal = sd * sh * sw * C;
   if (C == 1 && sd == 2 && sh == 2 && sw == 2 && 2 * D2 == D && 2 * H2 == H && 2 * W2 == W && !(pd | ph | pw)) {
-    // the 1-channel stride-2 stem: 4 aligned bf16 pairs (w, w+1) -> one 16-B store
-    const unsigned* xr = reinterpret_cast<const unsigned*>(x);
-    uint4 v;
+    // the 1-channel stride-2 stem: 4 aligned element pairs (w, w+1) -> one 16-B store
     const long long b00 = ((n * D + 2 * d2) * H + 2 * h2) * (long long)W + 2 * w2;
-    v.x = xr[b00 >> 1];
-    v.y = xr[(b00 + W) >> 1];
-    v.z = xr[(b00 + (long long)H * W) >> 1];
-    v.w = xr[(b00 + (long long)H * W + W) >> 1];
-    *(uint4*)(out + p * CO) = v;
+    const long long offs[4] = {b00, b00 + W, b00 + (long long)H * W, b00 + (long long)H * W + W};
+    unsigned q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if constexpr (sizeof(T) == 2) {
+        q[k] = reinterpret_cast<const unsigned*>(x)[offs[k] >> 1];
+      } else {
+        const unsigned short b = reinterpret_cast<const unsigned short*>(x)[offs[k] >> 1];
+        q[k] = (unsigned)__builtin_bit_cast(unsigned short, f2bf((float)(b & 0xffu))) |
+               ((unsigned)__builtin_bit_cast(unsigned short, f2bf((float)(b >> 8))) << 16);
+      }
+    }
+    *(uint4*)(out + p * CO) = make_uint4(q[0], q[1], q[2], q[3]);
     if (CO == 16) *(uint4*)(out + p * CO + 8) = make_uint4(0, 0, 0, 0);
     return;
   }
@@ -990,7 +1002,7 @@ __global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ 
         // (leading zero pads of a padded strided conv: the packed grid covers the padded input)
         const int d = d2 * sd + a - pd, h = h2 * sh + b - ph, w = w2 * sw + c - pw;
         if ((unsigned)d < (unsigned)D && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
-          f = bf2f(x[(((n * D + d) * H + h) * W + w) * C + ci]);
+          f = s2d_in(x[(((n * D + d) * H + h) * W + w) * C + ci]);
       }
       v.e[j] = f2bf(f);
     }
@@ -998,8 +1010,8 @@ __global__ __launch_bounds__(256) void s2d_pack_kernel(const bf16* __restrict__ 
   }
 }
 
-// geom: N D H W C sd sh sw D2 H2 W2 CO [pd ph pw] (leading pads, default 0)
-extern "C" int fn_s2d_pack(const void* x, void* out, const int* geom, int glen, hipStream_t st) {
+// geom: N D H W C sd sh sw D2 H2 W2 CO [pd ph pw] (leading pads, default 0); u8: x is uint8
+extern "C" int fn_s2d_pack(const void* x, void* out, const int* geom, int glen, hipStream_t st, int u8) {
   const int N = geom[0], D = geom[1], H = geom[2], W = geom[3], C = geom[4];
   const int sd = geom[5], sh = geom[6], sw = geom[7], D2 = geom[8], H2 = geom[9], W2 = geom[10];
   const int CO = geom[11];
@@ -1009,8 +1021,12 @@ extern "C" int fn_s2d_pack(const void* x, void* out, const int* geom, int glen, 
     return -2;
   const long long npos = (long long)N * D2 * H2 * W2;
   const unsigned blocks = (unsigned)((npos + 255) / 256);
-  hipLaunchKernelGGL(s2d_pack_kernel, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)out, N, D, H, W, C, sd,
-                     sh, sw, D2, H2, W2, CO, pd, ph, pw);
+  if (u8)
+    hipLaunchKernelGGL(s2d_pack_kernel<unsigned char>, dim3(blocks), dim3(256), 0, st, (const unsigned char*)x,
+                       (bf16*)out, N, D, H, W, C, sd, sh, sw, D2, H2, W2, CO, pd, ph, pw);
+  else
+    hipLaunchKernelGGL(s2d_pack_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (const bf16*)x, (bf16*)out, N, D, H, W,
+                       C, sd, sh, sw, D2, H2, W2, CO, pd, ph, pw);
   FN_CHECK_LAUNCH();
   return 0;
 }

@@ -27,7 +27,6 @@ from torch import nn
 
 from .. import ops
 from ..ops import bn as bn_ops
-from ..ops import packs
 from ..ops import subpixel
 from ..ops.elementwise import upsample2x
 from .layers import Conv, Dense
@@ -102,11 +101,13 @@ class FeatureNet3D(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         """x: [N, S, S, S, 1] (or [N, S, S, S]) -> fp32 logits [N, num_classes]."""
-        with packs.pack_scope(self):               # (the convs' weight packs in one launch)
-            f = self.features(x)
-            f = f.reshape(f.shape[0], -1)
-            h = self.fc1(f)
-            return self.fc2(h, out_fp32=True)
+        # (no packs.pack_scope here: the three tile-stream packs in one launch measured neutral on
+        # this step -- 4.633 vs 4.632 ms -- and the seg step slower, 19.05 vs 18.91 ms; NAS
+        # candidates, with one 3-5 us pack per conv and direction, gain 2.5 %)
+        f = self.features(x)
+        f = f.reshape(f.shape[0], -1)
+        h = self.fc1(f)
+        return self.fc2(h, out_fp32=True)
 
     def train_flops_per_sample(self) -> int:
         """Analytic FLOPs of one training sample (fwd + dgrad + wgrad)."""
@@ -149,10 +150,9 @@ class FeatureNet3DSeg(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.dim() == 4:
             x = x.unsqueeze(-1)
-        with packs.pack_scope(self):               # (the convs' weight packs in one launch)
-            for c in self.enc:
-                x = c(x)
-            return self._decode(x)
+        for c in self.enc:
+            x = c(x)
+        return self._decode(x)
 
     def _decode(self, x: torch.Tensor) -> torch.Tensor:
         d, h = self.dec, self.head
@@ -184,15 +184,14 @@ class FeatureNet3DSeg(nn.Module):
             x = x.unsqueeze(-1)
         d, h = self.dec, self.head
         if self.training:
-            with packs.pack_scope(self):           # (the convs' weight packs in one launch)
-                z = x
-                for c in self.enc:
-                    z = c(z)
-                if subpixel.gpu_ok(z, d.cout, z.shape[-1]) and bn_ops.fused_pointwise_ok(z, d.cout, h.cout, d.act) \
-                        and subpixel.xent_ok(d.cout, h.cout):
-                    loss, hits = subpixel.decoder_head_xent(z, d.weight, d.gamma, d.beta, d.running_mean,
-                                                            d.running_var, h.weight, h.bias, labels, d.bn_momentum,
-                                                            d.bn_eps, d.act, smoothing)
-                    return (loss, hits) if with_correct else loss
-                return softmax_xent(self._decode(z), labels, smoothing, with_correct)
+            z = x
+            for c in self.enc:
+                z = c(z)
+            if subpixel.gpu_ok(z, d.cout, z.shape[-1]) and bn_ops.fused_pointwise_ok(z, d.cout, h.cout, d.act) \
+                    and subpixel.xent_ok(d.cout, h.cout):
+                loss, hits = subpixel.decoder_head_xent(z, d.weight, d.gamma, d.beta, d.running_mean, d.running_var,
+                                                        h.weight, h.bias, labels, d.bn_momentum, d.bn_eps, d.act,
+                                                        smoothing)
+                return (loss, hits) if with_correct else loss
+            return softmax_xent(self._decode(z), labels, smoothing, with_correct)
         return softmax_xent(self(x), labels, smoothing, with_correct)

@@ -735,10 +735,12 @@ def s2d_input(x5: torch.Tensor, f, spec2: ConvSpec, pads=(0, 0, 0)) -> torch.Ten
     pd, ph, pw = pads
     D2, H2, W2 = spec2.D, spec2.H, spec2.W
     if x5.is_cuda and _native.kernels_available():
-        x5 = x5.to(torch.bfloat16).contiguous()
+        u8 = x5.dtype == torch.uint8              # (binary voxels as bytes: converted as they are read)
+        x5 = x5.contiguous() if u8 else x5.to(torch.bfloat16).contiguous()
         out = torch.empty(N, D2, H2, W2, spec2.C, dtype=torch.bfloat16, device=x5.device)
         _native.kernels().s2d_pack(x5.data_ptr(), out.data_ptr(),
-                                   [N, D, H, W, C, sd, sh, sw, D2, H2, W2, spec2.C, pd, ph, pw], _native.stream(x5))
+                                   [N, D, H, W, C, sd, sh, sw, D2, H2, W2, spec2.C, pd, ph, pw], _native.stream(x5),
+                                   int(u8))
         return out
     xp = torch.zeros(N, D2 * sd, H2 * sh, W2 * sw, C, dtype=x5.dtype, device=x5.device)
     xp[:, pd:pd + D, ph:ph + H, pw:pw + W] = x5[:, :D2 * sd - pd, :H2 * sh - ph, :W2 * sw - pw]
@@ -1073,10 +1075,22 @@ def conv(x5: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, spec: ConvSp
     per-block (sum, sumsq) slab consumed by :func:`ops.bn.batchnorm_act`).
     """
     if _native.use_native(x5):
-        y, stats = ConvFn.apply(x5.to(torch.bfloat16), w, b, spec, act_code(act), want_stats)
+        # uint8 input (binary voxel occupancy) goes to the space-to-depth stem as is: its packing
+        # kernel reads the bytes (a quarter of the bf16 traffic); every other conv takes bf16
+        xin = x5 if x5.dtype == torch.uint8 and u8_input_ok(spec) else x5.to(torch.bfloat16)
+        y, stats = ConvFn.apply(xin, w, b, spec, act_code(act), want_stats)
         return (y, stats) if want_stats else y
+    if not x5.is_floating_point():
+        x5 = x5.to(w.dtype)                       # (uint8 voxels on the reference path)
     y = ref.conv(x5, w.to(x5.dtype), None if b is None else b.to(x5.dtype), spec, act)
     return (y, None) if want_stats else y
+
+
+def u8_input_ok(spec: ConvSpec) -> bool:
+    """The conv reads its input only through the space-to-depth packing (ConvFn's s2d branch):
+    a uint8 input may be passed as is."""
+    s2d = s2d_plan(spec)
+    return s2d is not None and not pointwise_ok(spec) and s2d[1].kdim <= S2D_FWD_RATIO * spec.kdim
 
 
 def _dw_geom(spec: ConvSpec) -> list[int]:

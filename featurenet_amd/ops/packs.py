@@ -15,7 +15,9 @@ from (the optimizer step comes between two forwards), and the cache is owned by 
 weak map finds it by generation): a dropped NAS candidate takes its packs with it.
 
 Layout kinds (the builders register themselves): 0-2 gather forward / dgrad / packed-W and 3 / 4
-halo forward / dgrad (``ops/conv.py``), 5 tile-kernel stream (``ops/conv_tile.py``).
+halo forward / dgrad (``ops/conv.py``), 5 tile-kernel stream (``ops/conv_tile.py``).  NAS
+candidates (``ir/compile.py`` CandidateNet) run in a scope: 2.5 % off a LeNet step.  The
+FeatureNet-3D models do not: their three tile-stream packs in one launch measured neutral.
 """
 from __future__ import annotations
 

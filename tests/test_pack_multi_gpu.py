@@ -145,8 +145,9 @@ def test_pack_w_multi_tile_streams_match():
 
 
 def test_featurenet3d_scope_matches_per_layer_packs(monkeypatch):
-    """FeatureNet-3D training steps (tile-kernel convs: forward + dgrad streams recorded, then made
-    by the scope's one launch) == the same steps with every layer packing its own weights."""
+    """FeatureNet-3D training steps in a pack scope (tile-kernel convs: forward + dgrad streams
+    recorded, then made by the scope's one launch) == the same steps with every layer packing its
+    own weights."""
     from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
     from featurenet_amd.ops import softmax_xent
 
@@ -161,9 +162,7 @@ def test_featurenet3d_scope_matches_per_layer_packs(monkeypatch):
         return r
 
     for scoped in (False, True):
-        if not scoped:
-            monkeypatch.setattr(packs, "pack_scope", lambda m: contextlib.nullcontext())
-        else:
+        if scoped:
             monkeypatch.setattr(packs, "lookup", counting)
         torch.manual_seed(5)
         m = FeatureNet3D(FeatureNet3DConfig(input_size=64, num_classes=24)).cuda()
@@ -172,7 +171,9 @@ def test_featurenet3d_scope_matches_per_layer_packs(monkeypatch):
         run = []
         for _ in range(3):
             m.zero_grad(set_to_none=True)
-            loss = softmax_xent(m(x), y)
+            # (the model does not open a scope itself -- measured neutral there -- so the test does)
+            with (packs.pack_scope(m) if scoped else contextlib.nullcontext()):
+                loss = softmax_xent(m(x), y)
             loss.backward()
             with torch.no_grad():
                 for p in m.parameters():
