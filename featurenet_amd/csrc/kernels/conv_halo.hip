@@ -971,17 +971,23 @@ __global__ __launch_bounds__(256) void s2d_pack_kernel(const T* __restrict__ x, 
   const int w2 = (int)(p % W2), h2 = (int)((p / W2) % H2), d2 = (int)((p / ((long long)W2 * H2)) % D2);
   const long long n = p / ((long long)W2 * H2 * D2);
   const int creal = sd * sh * sw * C;
-  if (C == 1 && sd == 2 && sh == 2 && sw == 2 && 2 * D2 == D && 2 * H2 == H && 2 * W2 == W && !(pd | ph | pw)) {
-    // the 1-channel stride-2 stem: 4 aligned element pairs (w, w+1) -> one 16-B store
-    const long long b00 = ((n * D + 2 * d2) * H + 2 * h2) * (long long)W + 2 * w2;
-    const long long offs[4] = {b00, b00 + W, b00 + (long long)H * W, b00 + (long long)H * W + W};
+  if (C == 1 && sd == 2 && sh == 2 && sw == 2 && !((D | H | W | pd | ph | pw) & 1)) {
+    // the 1-channel stride-2 stem with even extents and even leading pads (FeatureNet-3D's valid
+    // stem, the seg model's 'same' one): every (w, w+1) pair is aligned and wholly inside or
+    // outside the input -- 4 pair loads -> one 16-B store
+    const int d0 = 2 * d2 - pd, h0 = 2 * h2 - ph, w0 = 2 * w2 - pw;
+    const bool wok = (unsigned)w0 < (unsigned)W;
     unsigned q[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      const int d = d0 + (k >> 1), h = h0 + (k & 1);
+      q[k] = 0u;
+      if (!wok || (unsigned)d >= (unsigned)D || (unsigned)h >= (unsigned)H) continue;
+      const long long off = ((n * D + d) * H + h) * (long long)W + w0;
       if constexpr (sizeof(T) == 2) {
-        q[k] = reinterpret_cast<const unsigned*>(x)[offs[k] >> 1];
+        q[k] = reinterpret_cast<const unsigned*>(x)[off >> 1];
       } else {
-        const unsigned short b = reinterpret_cast<const unsigned short*>(x)[offs[k] >> 1];
+        const unsigned short b = reinterpret_cast<const unsigned short*>(x)[off >> 1];
         q[k] = (unsigned)__builtin_bit_cast(unsigned short, f2bf((float)(b & 0xffu))) |
                ((unsigned)__builtin_bit_cast(unsigned short, f2bf((float)(b >> 8))) << 16);
       }
