@@ -322,7 +322,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None if vs is None else round(vs, 3),
             "dtype": "fp32" if (not use_cuda or (args.impl == "torch" and args.torch_amp == "off")) else "bf16",
-            "data": f"synthetic (random {args.size}^3 binary voxels, random labels, random-init weights)",
+            "data": f"synthetic (random {args.size}^3 binary voxels{' stored as uint8' if xs[0].dtype == torch.uint8 else ''}, "
+                    f"random labels, random-init weights)",
             "config": {
                 "model": model_name,
                 "global_batch": B * world,

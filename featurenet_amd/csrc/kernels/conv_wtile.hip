@@ -557,18 +557,21 @@ __global__ __launch_bounds__(256) void wtile_reduce_kernel(const float* __restri
 
 // Few outputs, many slices (the small layers of NAS candidates: a 4K-element dW over 1K
 // partial rows ran 23 us in the 256-element blocks above, each thread walking a quarter of
-// the rows): E elements per block, the 256 / E thread groups take every (256 / E)-th row, then
-// the groups' sums are added in group order -- fixed for a given (n, W), so still repeatable.
+// the rows): E elements per block in vectors of V (16-B loads when V = 4), the 256 V / E thread
+// groups take every (256 V / E)-th row, then the groups' sums are added in group order -- fixed
+// for a given (n, W), so still repeatable.  (Scalar loads -- V = 1 -- made the FeatureNet-3D stem's
+// 16K-element reduce over its 1K+ partial rows 19.2 us against 11.7 us in the 256-element form.)
 // (a second job -- part2 / dst2 / n2, the bias gradient beside a weight gradient -- takes the
 // blocks past the first job's: one launch for both)
-template <int E>
+template <int E, int V>
 __global__ __launch_bounds__(256) void part_reduce_narrow_kernel(const float* __restrict__ part, float* __restrict__ dst,
                                                                  long long n, int W, int accumulate,
                                                                  const float* __restrict__ part2 = nullptr,
                                                                  float* __restrict__ dst2 = nullptr, long long n2 = 0) {
-  constexpr int G = 256 / E;
+  constexpr int T = E / V;                       // threads per row group
+  constexpr int G = 256 / T;                     // row groups
   __shared__ float s_r[G][E];
-  const int e = threadIdx.x % E, gq = threadIdx.x / E;
+  const int t = threadIdx.x % T, gq = threadIdx.x / T;
   long long b = blockIdx.x;
   const long long nb1 = (n + E - 1) / E;
   if (b >= nb1) {                                // (uniform per block)
@@ -577,23 +580,35 @@ __global__ __launch_bounds__(256) void part_reduce_narrow_kernel(const float* __
     n = n2;
     b -= nb1;
   }
-  const long long i = b * E + e;
-  float a0 = 0.f, a1 = 0.f;
+  const long long i = b * E + (long long)t * V;  // (V > 1: n % V == 0, whole vectors)
+  float a0[V], a1[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) a0[v] = a1[v] = 0.f;
+  auto add = [&](float (&acc)[V], int p) {
+    if constexpr (V == 4) {
+      const float4 x = *(const float4*)(part + (long long)p * n + i);
+      acc[0] += x.x; acc[1] += x.y; acc[2] += x.z; acc[3] += x.w;
+    } else {
+      acc[0] += part[(long long)p * n + i];
+    }
+  };
   if (i < n) {
     int p = gq;
     for (; p + G < W; p += 2 * G) {
-      a0 += part[(long long)p * n + i];
-      a1 += part[(long long)(p + G) * n + i];
+      add(a0, p);
+      add(a1, p + G);
     }
-    if (p < W) a0 += part[(long long)p * n + i];
+    if (p < W) add(a0, p);
   }
-  s_r[gq][e] = a0 + a1;
+#pragma unroll
+  for (int v = 0; v < V; ++v) s_r[gq][t * V + v] = a0[v] + a1[v];
   __syncthreads();
-  if (threadIdx.x < E && i < n) {
-    float r = accumulate ? dst[i] : 0.f;
+  const long long o = b * E + threadIdx.x;
+  if (threadIdx.x < E && o < n) {
+    float r = accumulate ? dst[o] : 0.f;
 #pragma unroll
     for (int g = 0; g < G; ++g) r += s_r[g][threadIdx.x];
-    dst[i] = r;
+    dst[o] = r;
   }
 }
 
@@ -603,12 +618,14 @@ extern "C" int fn_part_reduce_wdot(const float* part, float* dst, long long n, i
   if (!part || !dst || W < 1) return -6;
   if (wsrc && (!wdp || C < 1 || 256 % C || n % C)) return -2;
   if (!wsrc && W >= 16 && (n + 255) / 256 < 192) {   // (narrow form: at least ~192 blocks)
+    const bool v4 = n % 4 == 0 && ((uintptr_t)part & 15) == 0;
+    const unsigned nb16 = (unsigned)((n + 15) / 16), nb64 = (unsigned)((n + 63) / 64);
     if (n <= 192 * 16) {
-      hipLaunchKernelGGL(part_reduce_narrow_kernel<16>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, part, dst,
-                         n, W, accumulate);
+      if (v4) hipLaunchKernelGGL((part_reduce_narrow_kernel<16, 4>), dim3(nb16), dim3(256), 0, st, part, dst, n, W, accumulate);
+      else hipLaunchKernelGGL((part_reduce_narrow_kernel<16, 1>), dim3(nb16), dim3(256), 0, st, part, dst, n, W, accumulate);
     } else {
-      hipLaunchKernelGGL(part_reduce_narrow_kernel<64>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, dst,
-                         n, W, accumulate);
+      if (v4) hipLaunchKernelGGL((part_reduce_narrow_kernel<64, 4>), dim3(nb64), dim3(256), 0, st, part, dst, n, W, accumulate);
+      else hipLaunchKernelGGL((part_reduce_narrow_kernel<64, 1>), dim3(nb64), dim3(256), 0, st, part, dst, n, W, accumulate);
     }
     FN_CHECK_LAUNCH();
     return 0;
@@ -631,8 +648,12 @@ extern "C" int fn_part_reduce2(const float* part, float* dst, long long n, const
   if (n <= 0 || !part || !dst || W < 1) return -6;
   if (W >= 16 && (n + 255) / 256 < 192 && n <= 192 * 16 && n2 <= 192 * 16) {
     const unsigned nb = (unsigned)((n + 15) / 16 + (n2 + 15) / 16);
-    hipLaunchKernelGGL(part_reduce_narrow_kernel<16>, dim3(nb), dim3(256), 0, st, part, dst, n, W, accumulate, part2,
-                       dst2, n2);
+    if (n % 4 == 0 && n2 % 4 == 0 && !(((uintptr_t)part | (uintptr_t)part2) & 15))
+      hipLaunchKernelGGL((part_reduce_narrow_kernel<16, 4>), dim3(nb), dim3(256), 0, st, part, dst, n, W, accumulate,
+                         part2, dst2, n2);
+    else
+      hipLaunchKernelGGL((part_reduce_narrow_kernel<16, 1>), dim3(nb), dim3(256), 0, st, part, dst, n, W, accumulate,
+                         part2, dst2, n2);
     FN_CHECK_LAUNCH();
     return 0;
   }
