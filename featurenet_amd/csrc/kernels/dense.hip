@@ -225,95 +225,6 @@ __global__ __launch_bounds__(DN_THREADS * NCW) void dense_fwd_part_kernel(const 
     }
 }
 
-// Inference Dense on the bf16 weight copy with K permuted inside 128-k super-steps: lane group g
-// takes k = 32g .. 32g + 31 of the super-step (four 16-B loads: one contiguous 64-B run of its row
-// per operand fragment) and MFMA step c multiplies chunk c of every lane group -- A and B lanes
-// pair the same k, so the products are the same, summed in another order.  A row's 256 B of a
-// super-step arrive together instead of 64 B per 32-k step (FC1 at 128^3 inference: 1024 rows
-// x 1.12M features streamed at 1.44 TB/s in the 32-k form).  kc is a multiple of 128; chunks past
-// kend read chunk 0 of the row and are zeroed (K % 8 == 0).
-template <int NCW, bool FINAL>
-__global__ __launch_bounds__(DN_THREADS * NCW) void dense_fwd_part_pk_kernel(const bf16* __restrict__ x,
-                                                                             const bf16* __restrict__ w,
-                                                                             float* __restrict__ part, int M, int N,
-                                                                             int K, int kc, const float* __restrict__ bias,
-                                                                             int act, int out_fp32) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r = lane & 15, gq = lane >> 4;
-  const int row0 = blockIdx.y * 128 + (wave & 3) * 32, col0 = (blockIdx.x * NCW + (wave >> 2)) * 64;
-  const int kbeg = blockIdx.z * kc, kend = min(K, kbeg + kc);
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bf16* xr[2];
-  const bf16* wh[4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = row0 + i * 16 + r;
-    xr[i] = x + (long long)(m < M ? m : 0) * K;
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = col0 + j * 16 + r;
-    wh[j] = w + (long long)(n < N ? n : 0) * K;
-  }
-  const bf16x8 zero8 = {};
-  bf16x8 ra[2][4], rb[4][4];                     // [fragment][chunk] of one super-step in flight
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int k = k0 + 32 * gq + 8 * c;
-      const int ks = k < kend ? k : 0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) ra[i][c] = *(const bf16x8*)(xr[i] + ks);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) rb[j][c] = *(const bf16x8*)(wh[j] + ks);
-    }
-  };
-  load(kbeg);
-  __builtin_amdgcn_sched_barrier(0);
-  for (int k0 = kbeg; k0 < kend; k0 += 128) {
-    bf16x8 fa[2][4], fb[4][4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const bool kok = k0 + 32 * gq + 8 * c < kend;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i][c] = kok ? ra[i][c] : zero8;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j][c] = kok ? rb[j][c] : zero8;
-    }
-    load(k0 + 128);                              // (the next super-step while these multiply)
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][c], fb[j][c], acc[i][j], 0, 0, 0);
-  }
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = col0 + j * 16 + r;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = row0 + i * 16 + 4 * gq + q;
-        if (m >= M || n >= N) continue;
-        if constexpr (FINAL) {
-          const float v = act_fwd(acc[i][j][q] + ((bias) ? bias[n] : 0.f), act);
-          if (out_fp32) ((float*)part)[(long long)m * N + n] = v;
-          else ((bf16*)part)[(long long)m * N + n] = f2bf(v);
-        } else {
-          part[(long long)blockIdx.z * M * N + (long long)m * N + n] = acc[i][j][q];
-        }
-      }
-    }
-}
-
 // y[m][n] = act(sum_s part[s][m][n] + b[n]); bf16 or fp32 output.  A workgroup takes 64
 // outputs; its 4 waves sum every 4th slice (coalesced 256-B rows, 4 loads in flight per
 // lane) and combine through LDS -- one thread per output with a serial walk over hundreds
@@ -580,20 +491,11 @@ extern "C" int fn_dense_splits(int M, int N, int K) {
   return S < 1 ? 1 : (S > maxS ? maxS : S);
 }
 
-// the K-permuted form of the bf16-weight forward (dense_fwd_part_pk_kernel): FN_DENSE_PK=1 (A/B)
-static bool dn_pk() {
-  static const bool on = [] { const char* e = getenv("FN_DENSE_PK"); return e && atoi(e) == 1; }();
-  return on;
-}
-
 template <bool WB, int NCW, bool FINAL>
 static void dn_fwd_part(const void* x, const void* w, void* part, int M, int N, int K, int kc, int Sr,
                         const float* bias, int act, int out_fp32, hipStream_t st) {
   const dim3 grid((N + 64 * NCW - 1) / (64 * NCW), (M + 127) / 128, Sr), blk(DN_THREADS * NCW);
-  if (WB && K % 8 == 0 && kc % 128 == 0 && dn_pk())
-    hipLaunchKernelGGL((dense_fwd_part_pk_kernel<NCW, FINAL>), grid, blk, 0, st, (const bf16*)x, (const bf16*)w,
-                       (float*)part, M, N, K, kc, bias, act, out_fp32);
-  else if (K % 8 == 0)
+  if (K % 8 == 0)
     hipLaunchKernelGGL((dense_fwd_part_kernel<true, 4, WB, NCW, FINAL>), grid, blk, 0, st, (const bf16*)x, w,
                        (float*)part, M, N, K, kc, bias, act, out_fp32);
   else
@@ -630,8 +532,7 @@ extern "C" int fn_dense_fwd(const void* x, const void* w, const float* bias, voi
                             int K, int S, int act, int out_fp32, int wbf16, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || S < 1) return -2;
   int kc = (K + S - 1) / S;
-  const int kq = wbf16 && K % 8 == 0 && dn_pk() ? 128 : 32;   // (the K-permuted form: 128-k super-steps)
-  kc = (kc + kq - 1) / kq * kq;
+  kc = (kc + 31) / 32 * 32;
   const int Sr = (K + kc - 1) / kc;              // slices actually covering K
   const int ncw = dn_ncw(M, N, K);
   if (wbf16) {
