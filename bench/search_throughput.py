@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--attacks", default="", help="comma list (e.g. cw,pgd): robustness evaluation of every trained "
                     "candidate with accuracy >= 0.5, as FullEvolution does (full_evolution.py:244-258)")
     ap.add_argument("--robustness-set", type=int, default=500)
+    ap.add_argument("--warm", action="store_true",
+                    help="start the worker pool (one 1-epoch trial per worker) before the clock: the steady "
+                         "state of a multi-generation search, whose workers persist across generations")
     a = ap.parse_args()
     from featurenet_amd.ir.parse import parse_feature_model
     from featurenet_amd.search.mutation import MutationConfig, Mutator
@@ -47,11 +50,16 @@ def main():
         attacks = [t for t in a.attacks.split(",") if t]
         cfg = TrialConfig(dataset=a.dataset, epochs=a.epochs, batch_size=a.batch, synthetic_sizes=(a.train, 1000),
                           graph=graph, attacks=attacks, robustness_set_size=a.robustness_set)
+        if a.warm:
+            nw = len(sched.slots()) if sched.mode == "process" else 1
+            wcfg = TrialConfig(**{**cfg.to_dict(), "epochs": 1, "attacks": []})
+            sched.map([s.clone() for s in specs[:nw]], wcfg)
         t0 = time.perf_counter()
         out = sched.map(specs, cfg)
         dt = time.perf_counter() - t0
         ok = sum(s.status == "trained" for s in out)
         print(json.dumps({"metric": "NAS candidates trained per hour", "graph": graph, "value": round(ok / dt * 3600, 1),
+                          "warm_workers": bool(a.warm),
                           "candidates": len(specs), "trained": ok, "seconds": round(dt, 2),
                           "devices": sched.devices, "workers_per_device": a.workers_per_device,
                           "dataset": a.dataset, "epochs": a.epochs, "train_samples": a.train, "batch": a.batch,

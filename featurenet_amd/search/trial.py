@@ -148,9 +148,16 @@ def _worker(dev: str, tasks, results, ready):
 class TrialScheduler:
     """Run trials on a set of devices: ``workers_per_device`` worker processes per device
     (several small candidates share one MI355X: each worker trains its own trial, the GPU
-    interleaves their kernels).  A device may also be listed more than once."""
+    interleaves their kernels).  A device may also be listed more than once.
 
-    def __init__(self, devices=None, timeout_s: float | None = None, mode: str = "auto", workers_per_device: int = 1):
+    ``persistent`` (default): the worker processes outlive a :meth:`map` call and serve the next
+    one -- an evolution calls ``map`` once per generation, and each fresh worker pays process
+    spawn, ``import torch``, HIP initialisation and the first candidate's kernel tables (~2 s of a
+    32-candidate generation at 4 workers per GPU).  :meth:`close` (or the context manager, or the
+    interpreter's exit: the workers are daemons) ends them."""
+
+    def __init__(self, devices=None, timeout_s: float | None = None, mode: str = "auto", workers_per_device: int = 1,
+                 persistent: bool = True):
         if devices is None:
             try:
                 import torch
@@ -164,6 +171,43 @@ class TrialScheduler:
         self.workers_per_device = max(1, int(workers_per_device))
         single = len(self.devices) == 1 and self.workers_per_device == 1
         self.mode = ("inline" if single and timeout_s is None else "process") if mode == "auto" else mode
+        self.persistent = bool(persistent)
+        self._workers: dict[str, dict] = {}      # the live pool (persistent mode)
+        self._retired: list[dict] = []           # replaced workers' queues, kept referenced
+        self._next_tid = 0                       # task ids unique across map calls
+
+    def __enter__(self):
+        return self
+
+    def __del__(self):
+        # (a scheduler dropped without close() -- e.g. the one a search function made for itself
+        # -- takes its workers with it)
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown: the daemons end anyway
+            pass
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def pids(self) -> list[int]:
+        """PIDs of the live worker processes (persistent mode)."""
+        return [w["proc"].pid for w in self._workers.values() if w["proc"].is_alive()]
+
+    def close(self):
+        """End the worker processes (they finish the task they hold first)."""
+        workers, self._workers = self._workers, {}
+        for w in workers.values():
+            try:
+                w["tasks"].put(None)
+            except Exception:  # noqa: BLE001 - a broken queue: the process is killed below
+                pass
+        for w in workers.values():
+            w["proc"].join(timeout=30)
+            if w["proc"].is_alive():
+                w["proc"].kill()
+        self._retired.clear()
 
     def slots(self) -> list[tuple[str, str]]:
         """(worker key, device) of every worker process."""
@@ -180,8 +224,8 @@ class TrialScheduler:
 
     def _map_processes(self, specs, cfg):
         ctx = mp.get_context("spawn")
-        workers: dict[str, dict] = {}
-        retired: list[dict] = []
+        workers = self._workers if self.persistent else {}
+        retired = self._retired
 
         devof = dict(self.slots())
 
@@ -200,8 +244,11 @@ class TrialScheduler:
             workers[key] = {"proc": p, "tasks": tq, "results": rq, "ready": ready, "busy": None, "t0": 0.0}
 
         for key in devof:
-            start(key)
-        pending = list(enumerate(specs))
+            if key not in workers or not workers[key]["proc"].is_alive():
+                start(key)
+        base = self._next_tid
+        self._next_tid += len(specs)
+        pending = [(base + i, s) for i, s in enumerate(specs)]
         out: dict[int, ModelSpec] = {}
         cfgd = cfg.to_dict()
         while len(out) < len(specs):
@@ -236,15 +283,17 @@ class TrialScheduler:
                     if not dead:
                         w["proc"].kill()
                     w["proc"].join(timeout=10)
-                    s = specs[tid].clone()
+                    s = specs[tid - base].clone()
                     s.status, s.accuracy = "failed", 0.0
                     s.error = "trial timed out" if hung else f"worker died (exit {w['proc'].exitcode})"
                     out[tid] = s
                     start(key)
-        for w in workers.values():
-            w["tasks"].put(None)
-        for w in workers.values():
-            w["proc"].join(timeout=30)
-            if w["proc"].is_alive():
-                w["proc"].kill()
-        return [out[i] for i in range(len(specs))]
+        if not self.persistent:
+            for w in workers.values():
+                w["tasks"].put(None)
+            for w in workers.values():
+                w["proc"].join(timeout=30)
+                if w["proc"].is_alive():
+                    w["proc"].kill()
+            retired.clear()
+        return [out[base + i] for i in range(len(specs))]

@@ -54,10 +54,10 @@ def run_task(store: TaskStore, task_id: str, base_path: str, template: str | Non
         cfg = TrialConfig(dataset=dataset, epochs=int(task.get("nb_training_iterations", 2)),
                           save_dir=products, fill_defaults=True,
                           synthetic_sizes=tuple(task.get("synthetic_sizes", (6000, 1000))))
-        sched = TrialScheduler(devices=devices)
-        pe.run(base, fm, out, nb_base_products=nb[2], dataset=dataset, training_epochs=cfg.epochs,
-               evolution_epochs=int(task.get("nb_evolution_epochs", 0)), attacks=(), scheduler=sched, trial=cfg,
-               pledge_duration_s=float(task.get("max_sampling_time", 30)), verbose=0)
+        with TrialScheduler(devices=devices) as sched:
+            pe.run(base, fm, out, nb_base_products=nb[2], dataset=dataset, training_epochs=cfg.epochs,
+                   evolution_epochs=int(task.get("nb_evolution_epochs", 0)), attacks=(), scheduler=sched, trial=cfg,
+                   pledge_duration_s=float(task.get("max_sampling_time", 30)), verbose=0)
     except Exception as e:
         return store.update(task_id, "generation_failed", error=f"{type(e).__name__}: {e}\n{traceback.format_exc()}")
     return store.update(task_id, "generation_complete")

@@ -43,8 +43,8 @@ def test_scheduler_survives_hang_and_crash():
     """A hung and a crashed trial fail only themselves; the search continues."""
     specs = [_spec("a"), _spec("hang"), _spec("crash"), _spec("b")]
     # (45 s: a spawned worker importing torch on a loaded CI box can take most of 20 s)
-    sched = TrialScheduler(devices=["cpu", "cpu"], timeout_s=45, mode="process")
-    res = sched.map(specs, _cfg(inject={"hang": "hang", "crash": "crash"}))
+    with TrialScheduler(devices=["cpu", "cpu"], timeout_s=45, mode="process") as sched:
+        res = sched.map(specs, _cfg(inject={"hang": "hang", "crash": "crash"}))
     by = {r.name: r for r in res}
     assert by["a"].status == "trained" and by["b"].status == "trained"
     assert by["hang"].status == "failed" and "timed out" in by["hang"].error
@@ -55,12 +55,27 @@ def test_scheduler_survives_hang_and_crash():
 def test_scheduler_runs_several_workers_per_device():
     """workers_per_device = 2 on one device: two worker processes, every trial trained once,
     results in submission order."""
-    sched = TrialScheduler(devices=["cpu"], timeout_s=60, mode="process", workers_per_device=2)
-    assert len(sched.slots()) == 2 and len({k for k, _ in sched.slots()}) == 2
-    specs = [_spec(n) for n in ("a", "b", "c")]
-    res = sched.map(specs, _cfg())
-    assert [r.name for r in res] == ["a", "b", "c"]
-    assert all(r.status == "trained" for r in res)
+    with TrialScheduler(devices=["cpu"], timeout_s=60, mode="process", workers_per_device=2) as sched:
+        assert len(sched.slots()) == 2 and len({k for k, _ in sched.slots()}) == 2
+        specs = [_spec(n) for n in ("a", "b", "c")]
+        res = sched.map(specs, _cfg())
+        assert [r.name for r in res] == ["a", "b", "c"]
+        assert all(r.status == "trained" for r in res)
+
+
+def test_scheduler_workers_persist_across_maps():
+    """Two map calls (two generations) run on the same worker processes; after close() none is
+    left.  A crash in the second map replaces only that worker."""
+    with TrialScheduler(devices=["cpu", "cpu"], timeout_s=60, mode="process") as sched:
+        r1 = sched.map([_spec("a"), _spec("b")], _cfg())
+        pids = sorted(sched.pids())
+        assert len(pids) == 2 and all(r.status == "trained" for r in r1)
+        r2 = sched.map([_spec("c"), _spec("crash"), _spec("d")], _cfg(inject={"crash": "crash"}))
+        assert [r.name for r in r2] == ["c", "crash", "d"]
+        assert r2[0].status == "trained" and r2[2].status == "trained" and r2[1].status == "failed"
+        assert len(set(sched.pids()) & set(pids)) >= 1         # (the crashed one was replaced)
+        procs = [w["proc"] for w in sched._workers.values()]
+    assert not sched.pids() and all(not p.is_alive() for p in procs)
 
 
 def test_full_evolution_two_generations(tmp_path):
