@@ -34,8 +34,9 @@ def main():
     torch.manual_seed(0)
     dev = torch.device("cuda")
     m = FeatureNet3D(FeatureNet3DConfig(input_size=a.size, num_classes=24)).to(dev).eval()
-    x = (torch.rand(a.chunk, a.size, a.size, a.size, 1, device=dev) < 0.3).to(torch.bfloat16)
-    q = quantize_model(m, x[: min(32, a.chunk)])
+    # binary voxels as uint8 (the space-to-depth stem packing reads the bytes); calibration in bf16
+    x = (torch.rand(a.chunk, a.size, a.size, a.size, 1, device=dev) < 0.3).to(torch.uint8)
+    q = quantize_model(m, x[: min(32, a.chunk)].to(torch.bfloat16))
     nchunks = max(1, a.batch // a.chunk)
     res = {}
     with torch.no_grad():

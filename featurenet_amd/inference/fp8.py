@@ -298,7 +298,8 @@ class Fp8FeatureNet3D:
             xq, shape = self.stem(stem_tap_input(x, tspec, self.in_scale, self.stem_int8),   # fp8 / int8 in, fp8 out
                                   (tspec.N, tspec.D, tspec.H, tspec.W, tspec.C))
         else:
-            x = x.to(torch.bfloat16).contiguous()
+            # (uint8 voxels stay bytes: the space-to-depth packing reads them)
+            x = x.contiguous() if x.dtype == torch.uint8 else x.to(torch.bfloat16).contiguous()
             spec = ConvSpec.make(tuple(x.shape), c1.cout, c1.kernel, c1.stride, c1.padding)
             xq = self._bf16_stem_fp8_out(x, spec)
             if xq is None:
@@ -324,7 +325,7 @@ class Fp8FeatureNet3D:
         layer reads them through the scaled MFMA and writes its own, the last one (fused pool) bf16."""
         m = self.model
         c1 = m.convs[0]
-        x = x.to(torch.bfloat16).contiguous()
+        x = x.contiguous() if x.dtype == torch.uint8 else x.to(torch.bfloat16).contiguous()
         spec = ConvSpec.make(tuple(x.shape), c1.cout, c1.kernel, c1.stride, c1.padding)
         xq = self._bf16_stem_fp8_out(x, spec, block=True)
         if xq is None:
