@@ -20,7 +20,7 @@ reference configuration and the per-voxel segmentation variant
 """
 from __future__ import annotations
 
-from dataclasses import asdict, dataclass, field
+from dataclasses import asdict, dataclass
 
 import torch
 from torch import nn
