@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--only", choices=["bf16", "fp8"], default=None, help="time one precision (profiling)")
+    ap.add_argument("--voxels", choices=["uint8", "bf16"], default="uint8", help="input voxel storage")
     a = ap.parse_args()
     from featurenet_amd.inference.fp8 import quantize_model
     from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
@@ -35,7 +36,7 @@ def main():
     dev = torch.device("cuda")
     m = FeatureNet3D(FeatureNet3DConfig(input_size=a.size, num_classes=24)).to(dev).eval()
     # binary voxels as uint8 (the space-to-depth stem packing reads the bytes); calibration in bf16
-    x = (torch.rand(a.chunk, a.size, a.size, a.size, 1, device=dev) < 0.3).to(torch.uint8)
+    x = (torch.rand(a.chunk, a.size, a.size, a.size, 1, device=dev) < 0.3).to({"uint8": torch.uint8, "bf16": torch.bfloat16}[a.voxels])
     q = quantize_model(m, x[: min(32, a.chunk)].to(torch.bfloat16))
     nchunks = max(1, a.batch // a.chunk)
     res = {}
