@@ -40,6 +40,7 @@ class SearchConfig:
     batch_size: int = 64
     devices: str = ""                    # "" = every visible GPU (or cpu); "0,1" / "cpu"
     trial_timeout_s: float = 0.0         # 0 = no watchdog
+    workers_per_device: int = 0          # trial worker processes per GPU; 0 = auto (4 per GPU, 1 on the CPU)
     seed: int = 0
     synthetic_sizes: list = field(default_factory=lambda: [6000, 1000])   # when a dataset is not on disk
 

@@ -141,13 +141,16 @@ def run_evolution(base_path: str = "runs", last_pdts_path: str = "", nb_base_pro
         candidates = evolve(parents, per_parent, mutator, mutation_rate, breed, evo)
         todo = [c for c in candidates if c.status != "trained"]
         tcfg.save_prefix = f"e{evo}_"
+        t0 = time.perf_counter()
         trained = {id(c): r for c, r in zip(todo, scheduler.map(todo, tcfg))}
+        dt = time.perf_counter() - t0
         candidates = [trained.get(id(c), c) for c in candidates]
         append_population(sp / f"e{evo}.json", candidates)
         population = sorted([c for c in candidates if c.accuracy > 0.1], key=lambda c: c.accuracy, reverse=True)
         save_snapshot(sp / f"{nb_base_products}products_e{evo}.json", population)
         top = population[0].accuracy if population else 0.0
         history.append({"generation": evo, "size": len(population), "top_accuracy": top,
-                        "invalid": sum(c.status == "invalid" for c in candidates)})
+                        "invalid": sum(c.status == "invalid" for c in candidates),
+                        "trained": len(todo), "seconds": round(dt, 2)})   # (the generation's trial wall time)
         log(f"generation {evo}: {len(population)} individuals, top accuracy {top:.4f}")
     return EvolutionResult(str(sp), population, len(history), history)
