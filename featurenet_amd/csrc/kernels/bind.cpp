@@ -26,6 +26,7 @@ int fn_conv_halo_workers(const int*, int);
 int fn_pw_fwd(const void*, const void*, const float*, void*, long long, int, int, int, hipStream_t, const float*,
               const float*, int, const void*, const float*, const float*, float*, int);
 int fn_seghead_part_len();
+int fn_part_reduce(const float*, float*, long long, int, int, hipStream_t);
 int fn_seghead_blocks(long long);
 int fn_seghead_loss(const void*, const float*, const float*, const void*, const float*, const void*, void*, float*,
                     long long, int, int, int, float, float, hipStream_t, int);
@@ -570,6 +571,13 @@ PYBIND11_MODULE(_C, m) {
      py::arg("ssc") = 0, py::arg("ssh") = 0, py::arg("spart") = 0, py::arg("sact") = 0);
   m.def("pw_fwd_blocks", &fn_pw_fwd_blocks);
   m.def("pw_xent_blocks", &fn_pw_xent_blocks);
+  m.def("part_reduce", [](uintptr_t part, uintptr_t dst, long long n, int W, int accumulate, uintptr_t st,
+                          std::vector<long long> ext) {
+    // dst[i] (+)= sum over the W partial rows part[w][i], added in row order; ext = {numel(part), numel(dst)}
+    fits(ext, 0, n * W, "part_reduce", "part");
+    fits(ext, 1, n, "part_reduce", "dst");
+    chk(fn_part_reduce(P<const float*>(part), P<float*>(dst), n, W, accumulate, S(st)), "part_reduce");
+  });
   m.def("seghead_part_len", &fn_seghead_part_len);
   m.def("seghead_blocks", &fn_seghead_blocks);
   m.def("seghead_loss", [](uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t w, uintptr_t bias, uintptr_t labels,

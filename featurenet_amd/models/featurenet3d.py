@@ -191,7 +191,7 @@ class FeatureNet3DSeg(nn.Module):
                     and subpixel.xent_ok(d.cout, h.cout):
                 loss, hits = subpixel.decoder_head_xent(z, d.weight, d.gamma, d.beta, d.running_mean, d.running_var,
                                                         h.weight, h.bias, labels, d.bn_momentum, d.bn_eps, d.act,
-                                                        smoothing)
+                                                        smoothing, want_hits=with_correct)
                 return (loss, hits) if with_correct else loss
             return softmax_xent(self._decode(z), labels, smoothing, with_correct)
         return softmax_xent(self(x), labels, smoothing, with_correct)

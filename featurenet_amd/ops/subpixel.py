@@ -405,7 +405,7 @@ class SubpixelDecoderHeadXentFn(torch.autograd.Function):
     ``tensorflow_generator.py:232-235``)."""
 
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, rmean, rvar, momentum, eps, act, hw, hb, labels, smoothing):
+    def forward(ctx, x, w, gamma, beta, rmean, rvar, momentum, eps, act, hw, hb, labels, smoothing, want_hits=True):
         from .. import _native
 
         y, prm, w2, bias = _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb)
@@ -453,7 +453,7 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
     NC <= 32 classes."""
 
     @staticmethod
-    def forward(ctx, x, w, gamma, beta, rmean, rvar, momentum, eps, act, hw, hb, labels, smoothing):
+    def forward(ctx, x, w, gamma, beta, rmean, rvar, momentum, eps, act, hw, hb, labels, smoothing, want_hits=True):
         from .. import _native
 
         y, prm, w2, bias = _head_forward(x, w, gamma, beta, rmean, rvar, momentum, eps, hw, hb)
@@ -471,11 +471,17 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
                         lab.data_ptr(), dz.data_ptr(), part.data_ptr(), M, K, NC, act, 1.0 / M, float(smoothing),
                         _native.stream(y2), [y2.numel(), wb.numel(), lab.numel(), dz.numel(), part.numel()],
                         int(lab.dtype == torch.uint8))
-        ctx.save_for_backward(x, w, y, prm, hw, dz, part)
+        # the workgroups' partials summed once, in row order (one launch), for the loss here and the
+        # head / BN-moment gradients in the backward
+        tot = torch.empty(part.shape[1], dtype=torch.float32, device=y.device)
+        Kn.part_reduce(part.data_ptr(), tot.data_ptr(), part.shape[1], part.shape[0], 0, _native.stream(y2),
+                       [part.numel(), tot.numel()])
+        ctx.save_for_backward(x, w, y, prm, hw, dz, tot)
         ctx.act, ctx.has_b, ctx.bparam = act, hb is not None, hb
         ctx.params = (beta, gamma)
-        tot = part.sum(0)
-        hits = part[:, 1].double().sum().round().long()    # (fp64: > 2^24 voxels per batch)
+        # top-1 hits only when asked for (fp64: > 2^24 voxels per batch; four small launches)
+        hits = part[:, 1].double().sum().round().long() if want_hits else torch.empty(0, dtype=torch.long,
+                                                                                        device=y.device)
         ctx.mark_non_differentiable(hits)
         return tot[0] / M, hits
 
@@ -485,7 +491,7 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         from . import bn as bn_ops
         from ..training.flat import grad_target
 
-        x, w, y, prm, hw, dz, part = ctx.saved_tensors
+        x, w, y, prm, hw, dz, tot = ctx.saved_tensors
         K = y.shape[-1]
         NC = hw.shape[0]
         y2 = y.reshape(-1, K)
@@ -494,7 +500,7 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         s = dloss.detach().float().reshape(1).contiguous()
         if not is_unit(dloss):
             _native.kernels().scale_unless_one(dz.data_ptr(), 1, s.data_ptr(), dz.numel(), _native.stream(dz))
-        tot = part[:, 2:].sum(0) * s                  # [db 32 | dWt 32 x 32 | msum 32 | msq 32], x dloss
+        tot = tot[2:] if is_unit(dloss) else tot[2:] * s   # [db 32 | dWt 32 x 32 | msum 32 | msq 32], x dloss
         dhw = dhb = None
         if ctx.needs_input_grad[9]:
             dwt = tot[32:32 + 32 * 32].view(32, 32)[:K, :NC]    # [ch][cls]
@@ -509,7 +515,7 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         dsh = bn_bwd_to_shifted(dz, y2, prm, dbeta, dgamma, ctx.act, y.shape)
         dx, dw = _decoder_backward(ctx, dsh, w, x, K)
         return (dx, dw, dgamma if ctx.needs_input_grad[2] else None, dbeta if ctx.needs_input_grad[3] else None,
-                None, None, None, None, None, dhw, dhb, None, None)
+                None, None, None, None, None, dhw, dhb, None, None, None)
 
 
 class _SavedView:
@@ -532,7 +538,7 @@ def decoder_head(x5, w, gamma, beta, running_mean, running_var, hw, hb, momentum
 
 
 def decoder_head_xent(x5, w, gamma, beta, running_mean, running_var, hw, hb, labels, momentum=0.1, eps=1e-5,
-                      act="relu", smoothing: float = 0.0):
+                      act="relu", smoothing: float = 0.0, want_hits: bool = True):
     """:func:`decoder_head` + mean softmax cross-entropy against per-voxel ``labels`` -> (loss, hits)
     (caller checks :func:`gpu_ok` and :func:`xent_ok`): the head's whole backward inside the
     forward kernel (:class:`SubpixelDecoderHeadLossFn`) for 32 decoder channels
@@ -546,7 +552,7 @@ def decoder_head_xent(x5, w, gamma, beta, running_mean, running_var, hw, hb, lab
         lab = labels if labels.dtype == torch.uint8 else labels.long()
         return SubpixelDecoderHeadLossFn.apply(x5.to(torch.bfloat16).contiguous(), w, gamma, beta, running_mean,
                                                running_var, momentum, eps, act_code(act), hw, hb, lab,
-                                               float(smoothing))
+                                               float(smoothing), bool(want_hits))
     return SubpixelDecoderHeadXentFn.apply(x5.to(torch.bfloat16).contiguous(), w, gamma, beta, running_mean,
                                            running_var, momentum, eps, act_code(act), hw, hb, labels.long(),
                                            float(smoothing))
