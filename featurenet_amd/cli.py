@@ -67,6 +67,8 @@ def cmd_run(a) -> int:
     if a.breed is not None:
         cfg.breed = a.breed not in ("0", "false", "False", "")
     nb = cfg.nb_tuple
+    # the trial worker pool starts now: its start-up overlaps the product sampling below
+    sched = _scheduler(cfg.devices, cfg.trial_timeout_s, cfg.workers_per_device).start()
     ms = MutationStrategies.ALL if cfg.mutation_strategy == "all" else MutationStrategies.CHOICE
     ss = {"pareto": SelectionStrategies.PARETO, "elitist": SelectionStrategies.ELITIST,
           "hybrid": SelectionStrategies.HYBRID}[cfg.selection_strategy]
@@ -85,8 +87,8 @@ def cmd_run(a) -> int:
                         survival_rate=cfg.survival_rate, breed=cfg.breed, evolution_epochs=cfg.evolution_epochs,
                         model=cfg.model, attacks=tuple(cfg.attacks), mutation_strategy=ms, selection_strategy=ss,
                         max_nb_cells=cfg.max_nb_cells, max_nb_blocks=cfg.max_nb_blocks,
-                        scheduler=_scheduler(cfg.devices, cfg.trial_timeout_s, cfg.workers_per_device), trial=trial,
-                        seed=cfg.seed)
+                        scheduler=sched, trial=trial, seed=cfg.seed)
+    sched.close()
     print(json.dumps({"session": res.session_path, "generations": res.generations, "history": res.history}))
     return 0
 

@@ -222,28 +222,40 @@ class TrialScheduler:
             return [run_trial(s, cfg, device) for s in specs]
         return self._map_processes(specs, cfg)
 
-    def _map_processes(self, specs, cfg):
+    def _spawn(self, key: str, workers: dict) -> None:
         ctx = mp.get_context("spawn")
+        # every worker gets its OWN result queue, replaced with the worker: killing a
+        # process while it writes a shared multiprocessing.Queue can corrupt that queue
+        tq = ctx.Queue()
+        rq = ctx.Queue()
+        ready = ctx.Queue()
+        p = ctx.Process(target=_worker, args=(dict(self.slots())[key], tq, rq, ready), daemon=True)
+        p.start()
+        # keep every queue referenced: a collected queue unlinks its semaphore
+        # before the spawned child has unpickled it
+        if key in workers:
+            self._retired.append(workers[key])
+        workers[key] = {"proc": p, "tasks": tq, "results": rq, "ready": ready, "busy": None, "t0": 0.0}
+
+    def start(self) -> "TrialScheduler":
+        """Spawn the worker pool now (persistent process mode), so that its start-up -- process
+        spawn, ``import torch``, HIP initialisation -- overlaps the caller's own preparation
+        (product sampling, model specs) instead of the first generation."""
+        if self.mode == "process" and self.persistent:
+            for key, _ in self.slots():
+                w = self._workers.get(key)
+                if w is None or not w["proc"].is_alive():
+                    self._spawn(key, self._workers)
+        return self
+
+    def _map_processes(self, specs, cfg):
         workers = self._workers if self.persistent else {}
         retired = self._retired
 
-        devof = dict(self.slots())
-
         def start(key):
-            # every worker gets its OWN result queue, replaced with the worker: killing a
-            # process while it writes a shared multiprocessing.Queue can corrupt that queue
-            tq = ctx.Queue()
-            rq = ctx.Queue()
-            ready = ctx.Queue()
-            p = ctx.Process(target=_worker, args=(devof[key], tq, rq, ready), daemon=True)
-            p.start()
-            # keep every queue referenced: a collected queue unlinks its semaphore
-            # before the spawned child has unpickled it
-            if key in workers:
-                retired.append(workers[key])
-            workers[key] = {"proc": p, "tasks": tq, "results": rq, "ready": ready, "busy": None, "t0": 0.0}
+            self._spawn(key, workers)
 
-        for key in devof:
+        for key, _ in self.slots():
             if key not in workers or not workers[key]["proc"].is_alive():
                 start(key)
         base = self._next_tid

@@ -63,6 +63,15 @@ def test_scheduler_runs_several_workers_per_device():
         assert all(r.status == "trained" for r in res)
 
 
+def test_scheduler_start_spawns_the_pool_before_map():
+    """start() spawns the persistent pool up front; the first map then uses those processes."""
+    with TrialScheduler(devices=["cpu", "cpu"], timeout_s=60, mode="process") as sched:
+        pids = sorted(sched.start().pids())
+        assert len(pids) == 2
+        res = sched.map([_spec("a"), _spec("b")], _cfg())
+        assert all(r.status == "trained" for r in res) and sorted(sched.pids()) == pids
+
+
 def test_scheduler_workers_persist_across_maps():
     """Two map calls (two generations) run on the same worker processes; after close() none is
     left.  A crash in the second map replaces only that worker."""
