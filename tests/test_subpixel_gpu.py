@@ -99,11 +99,16 @@ def test_decoder_head_matches_upsample_path():
         outs.append(out.float())
         grads.append({k: p.grad.detach().float().clone() for k, p in m.named_parameters() if p.grad is not None})
     os.environ.pop("FN_SUBPIXEL", None)
-    assert _rel(outs[0], outs[1]) < 2e-2
+    # (measured, scripts/diag_model_tolerances.py: outputs 4.7e-3 apart; every upstream gradient
+    # 2.8-4.5e-2 apart -- the decoder BN's backward removes the mean components of a random dz and
+    # amplifies the two paths' different bf16 roundings; BOTH paths are 13-18 % from the same model
+    # run in fp32 on the CPU and 4.4e-2 from each other, so neither carries an error of its own.
+    # The gradient bound leaves 1.8x margin for boxes whose schedules round differently.)
+    assert _rel(outs[0], outs[1]) < 1e-2
     for k in grads[1]:
         assert k in grads[0], k
         r = _rel(grads[0][k], grads[1][k])
-        assert r < 5e-2, (k, r)
+        assert r < 8e-2, (k, r)
 
 
 @pytest.mark.parametrize("mode", ["1", "2"])
