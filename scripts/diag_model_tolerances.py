@@ -93,3 +93,33 @@ def against_fp32():
 
 if __name__ == "__main__" and os.environ.get("FP32", "1") == "1":
     against_fp32()
+
+
+def classifier_against_fp32():
+    """FeatureNet-3D (64^3, batch 4) on the GPU kernels vs the same model in fp32 on the CPU, with
+    the training loss (softmax cross-entropy on labels) rather than a random output gradient."""
+    import copy
+
+    from featurenet_amd.models.featurenet3d import FeatureNet3D
+    from featurenet_amd.ops import softmax_xent
+
+    torch.manual_seed(6)
+    m = FeatureNet3D().cuda().train()
+    mc = copy.deepcopy(m).cpu().float().train()
+    occ = torch.rand(4, 64, 64, 64, 1) < 0.3
+    y = torch.randint(0, 24, (4,))
+    mc.zero_grad(set_to_none=True)
+    lc = softmax_xent(mc(occ.float()), y)
+    lc.backward()
+    ref = grads(mc)
+    m.zero_grad(set_to_none=True)
+    lg = softmax_xent(m(occ.to(torch.uint8).cuda()), y.cuda())
+    lg.backward()
+    gg = grads(m)
+    e = {k: rel(gg[k].cpu(), ref[k]) for k in ref}
+    print(f"FeatureNet-3D vs fp32 CPU: loss {float(lg):.5f} vs {float(lc):.5f}; grads max {max(e.values()):.2e} "
+          f"({max(e, key=e.get)}); " + ", ".join(f"{k} {v:.1e}" for k, v in sorted(e.items(), key=lambda kv: -kv[1])))
+
+
+if __name__ == "__main__" and os.environ.get("FP32CLS", "1") == "1":
+    classifier_against_fp32()
