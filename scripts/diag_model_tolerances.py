@@ -113,9 +113,23 @@ def classifier_against_fp32():
     lc.backward()
     ref = grads(mc)
     m.zero_grad(set_to_none=True)
+    zs = {}
+    hooks = [c.register_forward_hook(lambda mod, inp, out, i=i, tag="g": zs.__setitem__((tag, i), out.detach()))
+             for i, c in enumerate(m.convs[:3])]
     lg = softmax_xent(m(occ.to(torch.uint8).cuda()), y.cuda())
+    for h in hooks:
+        h.remove()
     lg.backward()
     gg = grads(m)
+    hooks = [c.register_forward_hook(lambda mod, inp, out, i=i: zs.__setitem__(("c", i), out.detach()))
+             for i, c in enumerate(mc.convs[:3])]
+    with torch.no_grad():
+        mc(occ.float())
+    for h in hooks:
+        h.remove()
+    for i in range(3):
+        a, b = zs[("g", i)].float().cpu() > 0, zs[("c", i)] > 0
+        print(f"relu mask of conv{i + 1}'s output: {100.0 * (a != b).float().mean().item():.2f} % of the elements differ")
     e = {k: rel(gg[k].cpu(), ref[k]) for k in ref}
     print(f"FeatureNet-3D vs fp32 CPU: loss {float(lg):.5f} vs {float(lc):.5f}; grads max {max(e.values()):.2e} "
           f"({max(e, key=e.get)}); " + ", ".join(f"{k} {v:.1e}" for k, v in sorted(e.items(), key=lambda kv: -kv[1])))
