@@ -95,16 +95,18 @@ if __name__ == "__main__" and os.environ.get("FP32", "1") == "1":
     against_fp32()
 
 
-def classifier_against_fp32():
+def classifier_against_fp32(pool: int = 2):
     """FeatureNet-3D (64^3, batch 4) on the GPU kernels vs the same model in fp32 on the CPU, with
-    the training loss (softmax cross-entropy on labels) rather than a random output gradient."""
+    the training loss (softmax cross-entropy on labels) rather than a random output gradient
+    (``pool`` 1: the same network without its max-pool -- how much of the difference is the pool's
+    arg-max)."""
     import copy
 
-    from featurenet_amd.models.featurenet3d import FeatureNet3D
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
     from featurenet_amd.ops import softmax_xent
 
     torch.manual_seed(6)
-    m = FeatureNet3D().cuda().train()
+    m = FeatureNet3D(FeatureNet3DConfig(pool=pool)).cuda().train()
     mc = copy.deepcopy(m).cpu().float().train()
     occ = torch.rand(4, 64, 64, 64, 1) < 0.3
     y = torch.randint(0, 24, (4,))
@@ -131,9 +133,10 @@ def classifier_against_fp32():
         a, b = zs[("g", i)].float().cpu() > 0, zs[("c", i)] > 0
         print(f"relu mask of conv{i + 1}'s output: {100.0 * (a != b).float().mean().item():.2f} % of the elements differ")
     e = {k: rel(gg[k].cpu(), ref[k]) for k in ref}
-    print(f"FeatureNet-3D vs fp32 CPU: loss {float(lg):.5f} vs {float(lc):.5f}; grads max {max(e.values()):.2e} "
+    print(f"FeatureNet-3D (pool {pool}) vs fp32 CPU: loss {float(lg):.5f} vs {float(lc):.5f}; grads max {max(e.values()):.2e} "
           f"({max(e, key=e.get)}); " + ", ".join(f"{k} {v:.1e}" for k, v in sorted(e.items(), key=lambda kv: -kv[1])))
 
 
 if __name__ == "__main__" and os.environ.get("FP32CLS", "1") == "1":
     classifier_against_fp32()
+    classifier_against_fp32(pool=1)
