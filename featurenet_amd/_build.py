@@ -63,9 +63,9 @@ def build_kernels(force: bool = False, workers: int | None = None, verbose: bool
     out = PKG / f"_C{EXT}"
     OBJ.mkdir(parents=True, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"] + _py_includes()
-    # FN_BUILD_EXPERIMENTS=1: also the measured-slower / timing-only kernel variants (the
-    # 32x32x16 conv_tile32 kernel, the int8 fp8-stem instance, the FN_TILE_DBG / FN_F8_DBG timing
-    # instances) -- off by default (compile time, code size, test surface)
+    # FN_BUILD_EXPERIMENTS=1: also the measured-slower / timing-only kernel variants (the int8
+    # fp8-stem instance, the FN_TILE_DBG / FN_F8_DBG timing instances) -- off by default (compile
+    # time, code size, test surface)
     if os.environ.get("FN_BUILD_EXPERIMENTS", "0") == "1":
         flags.append("-DFN_EXPERIMENTS=1")
     stamp = OBJ / "kernel_flags.txt"

@@ -106,13 +106,13 @@ int fn_dropout(const void*, void*, long long, float, unsigned, unsigned, hipStre
 int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int fn_scale_unless_one(void*, int, const float*, long long, hipStream_t);
 int fn_copy2(void*, const void*, long long, void*, const void*, long long, hipStream_t);
+int fn_cu_occupy(int, int, int, void*, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                  const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float, void*);
 int fn_conv_tile_workers(const int*, int, int);
-int fn_conv_tile32(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
-                   const int*, int, int, int, int*, hipStream_t, float, const void*, const float*);
-int fn_conv_tile32_supported(int, int);
+int fn_conv_tile_slab_rows(const int*, int, int);
+void fn_conv_tile_grid_cap(int);
 int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
                     float, const int*, int, int, int, int, int*, hipStream_t, const void*, void*);
 int fn_conv_tile_f8_supported(int, int, int);
@@ -277,24 +277,6 @@ PYBIND11_MODULE(_C, m) {
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("bny") = 0,
      py::arg("bnp") = 0, py::arg("oscale") = 0.f, py::arg("osc") = 0, py::arg("osc_n") = 0);
-  m.def("conv_tile32", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
-                          uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MB,
-                          uintptr_t sched, uintptr_t st, std::vector<long long> ext, float oscale, uintptr_t bny,
-                          uintptr_t bnp) {
-    need(geom, 31, "conv_tile32");
-    check_tile(geom, ext, ncol, 2 * MB, "conv_tile32");   // (row table: 4 waves x 2MB 16-row fragments)
-    if (bny) {   // ext[5] = numel of the BN input (the output's shape), ext[6] = numel of bnp
-      fits(ext, 5, view_extent(geom, ncol), "conv_tile32", "bny");
-      fits(ext, 6, 4LL * ncol, "conv_tile32", "bnp");
-    }
-    chk(fn_conv_tile32(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
-                       P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
-                       act, MB, P<int*>(sched), S(st), oscale, P<const void*>(bny), P<const float*>(bnp)),
-        "conv_tile32");
-  }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
-     py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MB"), py::arg("sched"),
-     py::arg("st"), py::arg("ext"), py::arg("oscale") = 0.f, py::arg("bny") = 0, py::arg("bnp") = 0);
-  m.def("conv_tile32_supported", &fn_conv_tile32_supported);
   m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
                            uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,
                            int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext,
@@ -354,6 +336,12 @@ PYBIND11_MODULE(_C, m) {
     need(geom, 31, "conv_tile_workers");
     return fn_conv_tile_workers(geom.data(), ncol, NT);
   });
+  m.def("conv_tile_grid_cap", [](int cap) { fn_conv_tile_grid_cap(cap); });   // (tests: grid independence)
+  m.def("conv_tile_slab_rows", [](std::vector<int> geom, int ncol, int NT) {
+    // rows of the BN-statistics slab a conv_tile launch with statistics writes (one per tile chunk)
+    need(geom, 31, "conv_tile_slab_rows");
+    return fn_conv_tile_slab_rows(geom.data(), ncol, NT);
+  });
   m.def("tile_pack_w", [](uintptr_t w, uintptr_t out, int K, int T, int C, int CS, int nks, int nct, int nslice,
                           int dgrad, uintptr_t st, int nt) {
     chk(fn_tile_pack_w(P<const float*>(w), P<void*>(out), K, T, C, CS, nks, nct, nslice, dgrad, nt, S(st)),
@@ -406,7 +394,15 @@ PYBIND11_MODULE(_C, m) {
                           uintptr_t st, std::vector<long long> ext) {
     // ext = {numel(w), numel(out)}; out holds K * C * (taps padded to the stage) elements
     fits(ext, 0, (long long)K0 * T * C0, "halo_pack_w", "w");
-    fits(ext, 1, (long long)K * C * T, "halo_pack_w", "out");
+    // (the kernel writes K * C * Tp elements: the tap count padded to whole stages, as
+    // fn_halo_pack_w derives it -- checking K * C * T would let an output sized by T overrun)
+    {
+      const int Csrc = mode == 0 ? C : K;
+      const int CS = Csrc % 16 == 0 ? 16 : (Csrc % 8 == 0 ? 8 : 0);
+      const int tps = CS > 0 && stage_k > 0 ? stage_k / CS : 0;
+      const long long Tp = tps > 0 ? (long long)(T + tps - 1) / tps * tps : T;
+      fits(ext, 1, (long long)K * C * Tp, "halo_pack_w", "out");
+    }
     chk(fn_halo_pack_w(P<const float*>(w), P<void*>(out), K0, C0, K, T, C, mode, stage_k, S(st)), "halo_pack_w");
   });
   m.def("ew_binary", [](uintptr_t a, uintptr_t b, uintptr_t out, long long n, int op, uintptr_t st) {
@@ -650,7 +646,7 @@ PYBIND11_MODULE(_C, m) {
         "colstats");
   });
   m.def("experiments_built", [] {
-    // FN_BUILD_EXPERIMENTS=1 builds: conv_tile32, the int8 fp8-stem instance, timing variants
+    // FN_BUILD_EXPERIMENTS=1 builds: the int8 fp8-stem instance, timing variants
 #ifdef FN_EXPERIMENTS
     return true;
 #else
@@ -793,6 +789,10 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_softmax_xent_rows(P<const void*>(logits), in_bf16, P<const long long*>(labels), P<float*>(block_loss),
                              P<void*>(dlogits), P<int*>(correct), B, NC, gscale, smoothing, S(st)),
         "softmax_xent_rows");
+  });
+  m.def("cu_occupy", [](int nwg, int usec, int lds, uintptr_t sink, uintptr_t st) {
+    // (measurement only: pins nwg CUs on the given stream for usec microseconds; sink >= 1 KB)
+    chk(fn_cu_occupy(nwg, usec, lds, P<void*>(sink), S(st)), "cu_occupy");
   });
   m.def("adam_flat_dev", [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t v, uintptr_t pb, long long n,
                             uintptr_t hp, uintptr_t t, int keras_eps, uintptr_t st) {

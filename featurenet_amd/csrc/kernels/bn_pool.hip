@@ -164,6 +164,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
   __shared__ double sa[256], sb[256];
   const int c = blockIdx.x;
   double a = 0.0, b = 0.0;
+#pragma unroll 4   // (the conv_tile chunk slabs have thousands of rows: keep several loads in flight)
   for (int i = threadIdx.x; i < nb; i += 256) {
     a += (double)part[(long long)i * 2 * C + c];
     b += (double)part[(long long)i * 2 * C + C + c];
@@ -369,6 +370,7 @@ __global__ __launch_bounds__(256) void bn_bwd_prep_kernel(const float* __restric
   const double gm = gamma ? (double)gamma[c] : 1.0, bt = beta ? (double)beta[c] : 0.0;
   const bool exact = fabs(gm) < 0.25 * fabs(bt);
   double a = 0.0, b = 0.0;
+#pragma unroll 4
   for (int i = threadIdx.x; i < nbg; i += 256) a += (double)gslab[(long long)i * 2 * C + c];
   if (exact) {
     const float mu = mean[c], scf = scale[c], shf = shift[c];

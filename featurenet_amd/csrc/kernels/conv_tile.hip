@@ -40,7 +40,9 @@
 #include "conv_tile_shared.h"
 #include "pack_w.h"
 
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -53,9 +55,9 @@
 //   or re-quantised e4m3 (x oscale).
 // Q8O: the bf16 instance with an e4m3 output epilogue (fp8 inference: the bf16 stem writes the
 // fp8 layers' input; its own register allocation)
-// (The BN-backward statistics epilogue for dgrad -- the statistics of the BN whose output this
-// conv consumed -- lives in conv_tile32_kernel only: on this kernel it measured 5.37 vs 5.00 ms
-// per step in round 4 and 5.14 vs 4.80 in round 3, and was removed.)
+// (A raw-moment BN-backward statistics epilogue for dgrad -- the statistics of the BN whose output
+// this conv consumed, read from y at the tile's positions -- measured 5.37 vs 5.00 ms per step in
+// round 4 and 5.14 vs 4.80 in round 3, and was removed; the relu-mask epilogue (MSK) replaced it.)
 // I8 (with F8: the fp8 kernel's 32-byte fragments holding int8 instead): two
 //   v_mfma_i32_16x16x64_i8 per fragment pair (bytes 0-15 and 16-31 of every lane: A and B split
 //   the same way, so the k sum is complete), exact int32 accumulation, converted to float in
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
                                                                const float* __restrict__ scale, float oscale,
                                                                const unsigned char* __restrict__ gmask,
                                                                const unsigned* __restrict__ xsc,
-                                                               unsigned char* __restrict__ osc) {
+                                                               unsigned char* __restrict__ osc, int chunk) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   static_assert(!BS || F8 || Q8O, "block scales: fp8 operands or an e4m3 output");
   constexpr int NTHR = 64 * (NCW + 1);
@@ -92,7 +94,8 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   constexpr int FRAG = F8 ? 32 : 16;             // bytes per lane of one MFMA operand fragment
   // NT = 2: 32-column blocks (a lane stores 8 consecutive columns).  (Round 3 measured 64-column
   // NT = 4 workgroups 3-4 % slower -- 256 VGPRs for 5 waves per CU -- and round 4 removed them;
-  // conv_tile32_kernel takes wide tiles on the 32x32x16 MFMA instead.)
+  // a 32x32x16-MFMA form of this kernel measured 2-8 % slower per layer in round 4,
+  // profiles/r4_m32_ab.md, and was removed in round 6.)
   static_assert(NT == 2, "32-column blocks");
   constexpr int RC = NT * 16;                    // columns of the workgroup (BN partial row length)
   constexpr int NV = 4 * NT;                     // consecutive columns per lane in the epilogue
@@ -116,26 +119,28 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   const int ct0 = blockIdx.y * NT;               // first 16-column tile of this workgroup
   // LDS: [buffer 0][buffer 1][job slots 64 B][BN partials][k-step offsets (nks+PD+2) int4]
   // [halo positions HPpad int2: (byte offset from the halo origin, packed hd|hh|hw)]
-  int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);                    // [2][2] (tile, slice) by parity
-  float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);           // [4 waves][2][32] BN partials
+  int* s_job = reinterpret_cast<int*>(dsm + 2 * g.BUF);                    // [2][4] (tile, slice, flush) by parity
+  // BN partials: [0] the waves' running per-tile sums (MT = 9), [1 + parity] the chunk flush rows;
+  // each [4 waves][2][32]
+  float* s_red = reinterpret_cast<float*>(dsm + 2 * g.BUF + 64);
   // BS (F8): two int4 per k-step -- the tap offset of the scale each lane group supplies, then the
   // lane group's packed (lo | hi << 16) data offsets (the block-scaled operand layout, below)
   constexpr int KTW = (F8 && BS) ? 2 : 1;
-  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + ct_red_bytes(NT, NCW));
+  int4* s_kt = reinterpret_cast<int4*>(dsm + 2 * g.BUF + 64 + ct_red_bytes(NT, NCW, F8));
   int2* s_pos = reinterpret_cast<int2*>(s_kt + KTW * (nks + PD + 2));
   for (int i = tid; i < KTW * (nks + PD + 2); i += NTHR) s_kt[i] = ktab[i];
-  for (int i = tid; i < ct_red_bytes(NT, NCW) / 4; i += NTHR) s_red[i] = 0.f;
+  for (int i = tid; i < ct_red_bytes(NT, NCW, F8) / 4; i += NTHR) s_red[i] = 0.f;
   // F8: the dequantisation scale and bias of this workgroup's 32 columns ([scale 32][bias 32]),
   // read by the epilogue from LDS (global loads there serialised every tile's stores)
   float* s_sb = reinterpret_cast<float*>(s_pos + g.HPpad);
   // relu-mask dgrad (gmask): two buffers (by job parity) of the tile's mask bytes,
   // [natural tile row][Ncol / 8], after everything else
-  const int mask_off = 64 + ct_red_bytes(NT, NCW) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + (F8 ? NT * 16 * 8 : 0);
+  const int mask_off = 64 + ct_red_bytes(NT, NCW, F8) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + (F8 ? NT * 16 * 8 : 0);
   // (the buffers hold the bytes in FRAGMENT order -- slot f = (wave * MT + mt) * 16 + lr -- so
   // the epilogue reads slot (wave * MT + mt) * 16 + lr: a per-lane base plus a constant per mt)
   const int mask_bytes = ct_mask_bytes(NCW * MT * 16, Ncol, gmask != nullptr);
   // BS (F8): two planes (by job parity) of the halo positions' scale dwords, after s_sb
-  const int scl_off = 2 * g.BUF + 64 + ct_red_bytes(NT, NCW) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + NT * 16 * 8;
+  const int scl_off = 2 * g.BUF + 64 + ct_red_bytes(NT, NCW, F8) + KTW * (nks + PD + 2) * 16 + g.HPpad * 8 + NT * 16 * 8;
   // ... and after them each fragment slot's (output offset from the tile origin in positions,
   // packed td|th|tw; dummy rows: the origin) for the loader's mask DMA, built once per kernel
   int2* s_mrow = reinterpret_cast<int2*>(dsm + 2 * g.BUF + mask_off + 2 * mask_bytes);
@@ -247,64 +252,119 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   st_0 = stamp();
 
   // ---- job protocol ---------------------------------------------------------
-  // s_job[2*par] = (tile, slice) of the job whose halo sits in buffer par (tile -1: done).
-  // The loader publishes job j+1 in slot par^1 right after barrier A(j) and lands its
-  // halo before barrier A(j+1); every wave reads its job after barrier A.  The compute
-  // waves never wait on anything else: the epilogue stores straight from registers.
-  // Tile schedule.  With BN statistics (stats != null) the partial sums of a workgroup must
-  // not depend on which tiles it happened to grab, or the statistics -- and everything
-  // downstream -- would change in the last bits run to run: the workgroup then walks a
-  // STATIC tile sequence (job k = tile k * G + slot, slots XCD-major so that the tiles running
-  // together on one XCD are neighbours sharing halo rows in its L2).  Without statistics
-  // every output element is written by exactly one tile whatever the order, and the tiles
-  // are handed out dynamically from a counter (the tail balances across late workgroups).
-  const bool stat_sched = stats != nullptr;
+  // s_job[4*par ..] = (tile, slice, flush) of the job whose halo sits in buffer par (tile -1:
+  // done; flush: see below).  The loader publishes job j+1 in slot par^1 right after barrier
+  // A(j) and lands its halo before barrier A(j+1); every wave reads its job after barrier A.
+  // The compute waves never wait on anything else: the epilogue stores straight from registers.
+  // Tile schedule.  Without BN statistics every output element is written by exactly one tile
+  // whatever the order, and tiles are handed out one at a time from a counter.  With statistics
+  // (stats != null) the partial sums must not depend on which workgroup ran which tiles, or the
+  // statistics -- and everything downstream -- would change in the last bits run to run:
+  //   * chunk > 0 (the default): the tiles are cut into fixed CHUNKS of `chunk` consecutive
+  //     tiles (the host sizes them from the tile count alone, never from the grid or the CU
+  //     count); workgroups grab whole chunks from a counter, and each compute wave writes its
+  //     partial sums over a chunk into the chunk's own slab row (chunk * NCW + wave) when the
+  //     chunk's last job ends (s_job flush = the chunk id).  The sums are fixed per chunk and
+  //     the finalize adds the rows in a fixed order, so the result is the same bits whatever
+  //     the grab order -- and a workgroup that starts late (its CU held by another kernel, e.g.
+  //     an RCCL ring of the data-parallel all-reduce) simply takes fewer chunks
+  //     (profiles/r6_dp_interference.md);
+  //   * chunk == 0: the round-5 STATIC schedule (job k = tile k * G + slot, slots XCD-major;
+  //     per-workgroup partial rows), kept for the A/B of that measurement: a CU held by another
+  //     kernel there delays its workgroup's whole fixed share.
+  const bool stat_static = stats != nullptr && chunk <= 0;
+  const bool stat_chunk = stats != nullptr && chunk > 0;
   const int G = (int)gridDim.x;
   const int slot = (G & 7) == 0 ? ((int)blockIdx.x & 7) * (G >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
+  const int nchunk = stat_chunk ? (ntiles + chunk - 1) / chunk : 0;
+  // loader state of the chunk walk (wave-uniform): the chunk being handed out, its next tile, its end
+  int ch_id = -1, ch_next = 0, ch_end = 0;
   auto next_tile = [&](int k) -> int {           // tile of this workgroup's job k (-1: none)
-    const int t = stat_sched ? k * G + slot : atomicAdd(sched + 1 + blockIdx.y, 1);
+    if (stat_chunk) {
+      if (ch_next >= ch_end) {
+        int c = 0;
+        if (lane == 0) c = atomicAdd(sched + 1 + blockIdx.y, 1);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (c >= nchunk) return -1;
+        ch_id = c;
+        ch_next = c * chunk;
+        ch_end = min(ntiles, ch_next + chunk);
+      }
+      return ch_next++;
+    }
+    int t = 0;
+    if (stat_static) t = k * G + slot;
+    else if (lane == 0) t = atomicAdd(sched + 1 + blockIdx.y, 1);
+    t = __builtin_amdgcn_readfirstlane(t);
     return t < ntiles ? t : -1;
   };
-  if (tid == 0) {
-    s_job[0] = next_tile(0);
-    s_job[1] = 0;
+  // the chunk to flush after job (tile, slice): its id when this is the chunk's last job, else -1
+  auto flush_of = [&](int tile, int slice) -> int {
+    return (stat_chunk && tile >= 0 && tile == ch_end - 1 && slice == nslice - 1) ? ch_id : -1;
+  };
+  if (loader) {                                  // (the loader runs the tile walk; its first job here)
+    const int t0 = next_tile(0);
+    if (lane == 0) {
+      s_job[0] = t0;
+      s_job[1] = 0;
+      s_job[2] = flush_of(t0, 0);
+    }
   }
   tile_lds_barrier();
 
   if (loader) {
     // ======================= loader wave =======================
     int tile = __builtin_amdgcn_readfirstlane(s_job[0]), slice = 0, t_next = -1, kjob = 1;
+    // (the chunk walk hands out the next tile only once the current one is published: t_next is
+    // taken when the loader moves to a new tile, so flush_of sees the chunk of the published job)
     if (tile >= 0) {
       dma_job(tile, 0, 0);
       dma_scl(tile, 0);
       if (nslice == 1) dma_mask(tile, 0);
-      if (lane == 0) t_next = next_tile(kjob);
+      if (!stat_chunk) t_next = next_tile(kjob);
       ++kjob;
-      t_next = __builtin_amdgcn_readfirstlane(t_next);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int par = 0;
+    int fl_prev = -1;                            // flush (chunk id) of the job before the current one
+    int fl_cur = __builtin_amdgcn_readfirstlane(s_job[2]);
     while (true) {
       st_1 = stamp();
       tile_lds_barrier();                        // A: job halo landed; the other buffer is free
       lap(st_a);
+      if (!F8 && fl_prev >= 0) {
+        // the chunk that ended with the previous job: its 4 waves' flush rows (that job's parity,
+        // par ^ 1 now), added in wave order, into the chunk's slab row
+        const float* fl = s_red + (1 + (par ^ 1)) * NCW * 2 * RC;
+        float* row = stats + (long long)fl_prev * 2 * Ncol;
+        for (int i = lane; i < 2 * RC; i += 64) {
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < NCW; ++w) v += fl[w * 2 * RC + i];
+          const int c = ct0 * 16 + (i < RC ? i : i - RC);
+          if (c < Ncol) row[(i < RC ? 0 : Ncol) + c] = v;
+        }
+      }
+      fl_prev = fl_cur;
       if (tile < 0) break;
       int ntile = tile, nslc = slice + 1;
       if (nslc == nslice) {
         nslc = 0;
-        ntile = t_next;
+        ntile = stat_chunk ? next_tile(kjob) : t_next;
       }
+      const int nfl = flush_of(ntile, nslc);
+      fl_cur = nfl;
       if (lane == 0) {
-        s_job[2 * (par ^ 1)] = ntile;
-        s_job[2 * (par ^ 1) + 1] = nslc;
+        s_job[4 * (par ^ 1)] = ntile;
+        s_job[4 * (par ^ 1) + 1] = nslc;
+        s_job[4 * (par ^ 1) + 2] = nfl;
       }
       if (!(DBG & 4) && ntile >= 0) dma_job(ntile, nslc, (par ^ 1) * g.BUF);
       if (ntile >= 0) dma_scl(ntile, par ^ 1);
       if (ntile >= 0 && nslc == nslice - 1) dma_mask(ntile, par ^ 1);
       if (nslc == 0 && ntile >= 0) {
-        if (lane == 0) t_next = next_tile(kjob);
+        if (!stat_chunk) t_next = next_tile(kjob);
         ++kjob;
-        t_next = __builtin_amdgcn_readfirstlane(t_next);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lap(st_k);
@@ -423,8 +483,9 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       st_1 = stamp();
       tile_lds_barrier();                        // A
       lap(st_a);
-      const int tile = __builtin_amdgcn_readfirstlane(s_job[2 * par]);
-      const int slice = __builtin_amdgcn_readfirstlane(s_job[2 * par + 1]);
+      const int tile = __builtin_amdgcn_readfirstlane(s_job[4 * par]);
+      const int slice = __builtin_amdgcn_readfirstlane(s_job[4 * par + 1]);
+      const int flush = __builtin_amdgcn_readfirstlane(s_job[4 * par + 2]);
       if (tile < 0) break;
       const int nslc = slice + 1 == nslice ? 0 : slice + 1;
       if constexpr (F8 && BS) {
@@ -745,16 +806,41 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
           }
         }
         lap(st_e);
+        if (!F8 && stat_chunk && flush >= 0) {
+          // the chunk's last job: this wave's partial sums over the chunk into its LDS flush row
+          // of this job's parity; after the next barrier A the loader adds the 4 waves' rows in
+          // wave order and stores the chunk's slab row (every row written once per column block)
+          float* fl = s_red + (1 + par) * NCW * 2 * RC + wave * 2 * RC;
+          if constexpr (RSACC) {
+#pragma unroll
+            for (int h = 0; h < NT / 2; ++h) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const float a = ct_sum16(rsum[h][j >> 1][j & 1]), b = ct_sum16(rsq[h][j >> 1][j & 1]);
+                if (lr == 0) {
+                  fl[NV * lg + 8 * h + j] = a;
+                  fl[RC + NV * lg + 8 * h + j] = b;
+                }
+              }
+#pragma unroll
+              for (int q = 0; q < 4; ++q) rsum[h][q] = rsq[h][q] = (ct_f32x2){0.f, 0.f};
+            }
+          } else {                               // (per-tile sums in this wave's own LDS row)
+            for (int i = lane; i < 2 * RC; i += 64) {
+              fl[i] = s_red[wave * 2 * RC + i];
+              s_red[wave * 2 * RC + i] = 0.f;
+            }
+          }
+        }
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) lb[mt] += (1 - 2 * par) * g.BUF;   // the other buffer
       par ^= 1;
     }
-    if (!F8 && RSACC && stats) {
-      // the lane's running sums over the 16 lanes holding the same columns (DPP), into the wave's
-      // LDS row.  The workgroup's tiles are a static sequence when statistics are on (see the
-      // tile schedule), so every partial -- and the finalize's fixed-order sum over the slab
-      // rows -- is the same run to run
+    if (!F8 && RSACC && stat_static) {
+      // (static schedule) the lane's running sums over the 16 lanes holding the same columns
+      // (DPP), into the wave's LDS row: the workgroup's tiles are a fixed sequence, so every
+      // partial -- and the finalize's fixed-order sum over the slab rows -- is the same run to run
 #pragma unroll
       for (int h = 0; h < NT / 2; ++h) {
 #pragma unroll
@@ -768,7 +854,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       }
     }
     tile_lds_barrier();                          // R
-    if (!F8 && stats && tid < RC && ct0 * 16 + tid < Ncol) {
+    if (!F8 && stat_static && tid < RC && ct0 * 16 + tid < Ncol) {
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int w = 0; w < NCW; ++w) {
@@ -791,7 +877,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       d[6] = stamp() - st_0;
     }
   }
-  if (tid == 0 && !stat_sched) {                 // the last workgroup out resets the counters
+  if (tid == 0 && !stat_static) {                // the last workgroup out resets the counters
     __threadfence();                             // (static schedules never touch them)
     if (atomicAdd(sched, 1) == (int)(gridDim.x * gridDim.y) - 1) {
       for (int i = 0; i < (int)gridDim.y; ++i) atomicExch(sched + 1 + i, 0);
@@ -839,7 +925,7 @@ extern "C" int fn_tile_pack_w2(const float* w, void* out0, void* out1, int K, in
   for (int q = 0; q < 2; ++q) {
     const int* p = ps[q];
     if (p[0] != 8 && p[0] != 16 && p[0] % 32 != 0) return -2;
-    if ((p[5] != 2 && p[5] != 32) || p[2] % 2) return -2;
+    if (p[5] != 2 || p[2] % 2) return -2;
     j[q] = TilePackJob{(uint4*)(q ? out1 : out0), p[0], p[1], p[2], p[3], p[4], p[5]};
     total += ((long long)p[3] * p[1] + 4) * p[2] * 64;
   }
@@ -852,7 +938,7 @@ extern "C" int fn_tile_pack_w2(const float* w, void* out0, void* out1, int K, in
 extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, int CS, int nks, int nct, int nslice,
                               int dgrad, int nt, hipStream_t st) {
   if (CS != 8 && CS != 16 && CS % 32 != 0) return -2;
-  if ((nt != 2 && nt != 32) || nct % 2) return -2;   // 2: conv_tile_kernel, 32: conv_tile32_kernel
+  if (nt != 2 || nct % 2) return -2;
   const long long total = ((long long)nslice * nks + 4) * nct * 64;
   hipLaunchKernelGGL(tile_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (uint4*)out, K, T,
                      C, CS, nks, nct, nslice, dgrad, nt);
@@ -865,6 +951,9 @@ extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, in
 // ---------------------------------------------------------------------------
 
 static int g_tile_cus = 0;
+static int g_tile_grid_cap = 0;   // tests: at most this many workgroups per column block (0: none)
+
+extern "C" void fn_conv_tile_grid_cap(int cap) { g_tile_grid_cap = cap > 0 ? cap : 0; }
 
 extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   const TileGeom g = parse_tile(geom);
@@ -880,13 +969,41 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
+// Statistics chunks of conv_tile_kernel's chunked schedule: tiles per chunk from the tile count
+// alone (never the grid or the CU count: the partial rows -- so the statistics' bits -- are the
+// same on every box), at most CT_MAX_CHUNKS chunks, so every workgroup takes dozens and the tail
+// of the dynamic grab is about one tile.  FN_TILE_STATIC=1: the round-5 static schedule (A/B of
+// profiles/r6_dp_interference.md only).
+#define CT_MAX_CHUNKS 8192
+static bool tile_stat_static() {
+  static const bool v = [] { const char* e = getenv("FN_TILE_STATIC"); return e && atoi(e) == 1; }();
+  return v;
+}
+static int tile_chunk(const TileGeom& g) {
+  if (tile_stat_static()) return 0;
+  const long long nt = (long long)g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) *
+                       ((g.OW + g.TW - 1) / g.TW);
+  return (int)std::max(1LL, (nt + CT_MAX_CHUNKS - 1) / CT_MAX_CHUNKS);
+}
+
+// rows of the BN-statistics slab [rows][2][Ncol] a statistics launch writes: one per chunk (or, with
+// the static schedule, one per workgroup)
+extern "C" int fn_conv_tile_slab_rows(const int* geom, int Ncol, int NT) {
+  const TileGeom g = parse_tile(geom);
+  const int c = tile_chunk(g);
+  if (c == 0) return fn_conv_tile_workers(geom, Ncol, NT);
+  const long long nt = (long long)g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) *
+                       ((g.OW + g.TW - 1) / g.TW);
+  return (int)((nt + c - 1) / c);
+}
+
 template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false,
           int NCW = CT_NCW>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
                        float oscale = 0.f, const void* gmask = nullptr, const void* xsc = nullptr,
-                       void* osc = nullptr) {
+                       void* osc = nullptr, int chunk = 0) {
   static size_t configured = 0;
   if (lds > configured) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW>,
@@ -897,7 +1014,7 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
   hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW>), grid, dim3(64 * (NCW + 1)), lds, st,
                      (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
                      stamps, scale, oscale, (const unsigned char*)gmask, (const unsigned*)xsc,
-                     (unsigned char*)osc);
+                     (unsigned char*)osc, chunk);
   return 0;
 }
 
@@ -914,7 +1031,7 @@ extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false, int Ncol = 0, bool mask = false,
                              bool bs = false, int ncw = CT_NCW) {
   const int PD = ct_pd(NT, f8);
-  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT, ncw) + (size_t)(g.nks + PD + 2) * 16 * (f8 && bs ? 2 : 1) +
+  return 2 * (size_t)g.BUF + 64 + ct_red_bytes(NT, ncw, f8) + (size_t)(g.nks + PD + 2) * 16 * (f8 && bs ? 2 : 1) +
          (size_t)g.HPpad * 8 +
          (f8 ? (size_t)NT * 16 * 8 : 0) + (size_t)ct_mask_lds(ncw * MT * 16, Ncol, mask) +
          (f8 && bs ? 2 * (size_t)g.HPpad * 4 : 0);    // (BS: the two scale planes)
@@ -925,10 +1042,9 @@ static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false,
 // int2[4 * MT * 16] (halo position of the row, natural tile row or -1); ktab: int4[nks + PD
 // + 2] byte offsets of the tap each lane group reads per k-step (zero past nks);
 // zp: >= 16 zero bytes; sched: int[64] zeroed counters (left zero); stats: fp32
-// [workers][2][Ncol], or null.  bny (bnp null): the relu-mask bytes [output positions][Ncol / 8]
-// of the BN whose output this dgrad's conv consumed -- the epilogue's column sums are of
-// g = dx * mask (dx stored as is); stats required, act none.  (The raw-moment BN-backward statistics epilogue, bny + bnp,
-// is conv_tile32's, fn_conv_tile32.)
+// [fn_conv_tile_slab_rows][2][Ncol], or null.  bny (bnp null): the relu-mask bytes [output
+// positions][Ncol / 8] of the BN whose output this dgrad's conv consumed -- the epilogue's column
+// sums are of g = dx * mask (dx stored as is); stats required, act none.
 // osc (oscale > 0 only): block-scaled e4m3 output -- one E8M0 byte per (position, 32-column block)
 // into the dword-per-position array osc (byte j = block j); oscale is then only the flag
 extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
@@ -971,6 +1087,8 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   if (!(oscale >= 0.f) || (oscale > 0.f && (stats || NT != 2 || CPP != 1))) return -2;
   if (osc && (oscale <= 0.f || Ncol > 128)) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
+  // (tests: a smaller grid must give the same bits -- only the dynamic schedules take it)
+  if (g_tile_grid_cap > 0 && (!stats || tile_chunk(g) > 0)) grid.x = std::min<unsigned>(grid.x, g_tile_grid_cap);
   int rc = -2;
 #ifdef FN_EXPERIMENTS
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();
@@ -1005,28 +1123,6 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     return 0;
   }
 #endif  // FN_EXPERIMENTS
-  // FN_TILE_W8=1: the bf16 MT = 8 plans on 8 compute waves of MT = 4 (same rows, same tables) --
-  // measured, not the default (profiles/r5_conv_tile_budget.md): the stem forward alone -7 %, but
-  // the dgrad / CPP 4 plans +1..+10 % (every compute wave loads the workgroup's weight fragments
-  // itself: eight copies through L1 instead of four), and whole steps never faster (training
-  // 4.67-4.70 vs 4.70-4.71 ms with it on the short-tile convs only, segmentation 19.0-19.1 vs
-  // 19.3-19.4 ms)
-  static const bool w8 = [] { const char* e = getenv("FN_TILE_W8"); return e && atoi(e) == 1; }();
-  if (w8 && MT == 8 && NT == 2 && oscale == 0.f && !osc) {
-    const size_t lds8 = tile_lds_total(g, 4, NT, false, Ncol, bny != nullptr, false, 8);
-    if (lds8 <= 160 * 1024) {
-#define CT_W8(C)                                                                                                  \
-  if (CPP == C)                                                                                                   \
-    rc = launch_tile<4, 2, C, 0, false, false, false, false, 8>(grid, lds8, st, src, (const uint4*)wp,               \
-                                                                (const int2*)rowtab, (const int4*)ktab, zp, bias, out, \
-                                                                stats, g, Ncol, act, sched, nullptr, nullptr, 0.f, bny);
-      CT_W8(1) CT_W8(2) CT_W8(4)
-#undef CT_W8
-      if (rc) return rc;
-      FN_CHECK_LAUNCH();
-      return 0;
-    }
-  }
 #define CT_CASE(M, N, C)                                                                                          \
   if (MT == M && NT == N && CPP == C)                                                                             \
     rc = oscale > 0.f ? (osc ? launch_tile<M, N, C, 0, false, C == 1 && N == 2, false, C == 1 && N == 2>(        \
@@ -1038,7 +1134,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
                                    bias, out, stats, g, Ncol, act, sched, nullptr, nullptr, oscale))              \
                       : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,                 \
                                              (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, nullptr,     \
-                                             nullptr, 0.f, bny);
+                                             nullptr, 0.f, bny, nullptr, nullptr, stats ? tile_chunk(g) : 0);
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;

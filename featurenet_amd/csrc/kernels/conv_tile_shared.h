@@ -1,6 +1,5 @@
 // Shared pieces of the big-tile LDS-halo conv kernels (conv_tile.hip: the 16x16x32 bf16 and
-// the fp8 kernels; conv_tile32.hip: the 32x32x16 bf16 kernel): the tile geometry, the halo DMA
-// of one job, small helpers.
+// the fp8 kernels): the tile geometry, the halo DMA of one job, small helpers.
 #pragma once
 #include "common.h"
 #include "tile_dma.h"
@@ -28,8 +27,12 @@ struct TileGeom {
 #define CT_NCW 4                       // compute (MFMA) waves
 #define CT_F8_POOL 0x100               // fp8 act flag: fused 2^3 max-pool epilogue
 #define CT_NTHR (64 * (CT_NCW + 1))     // + one loader wave
-// per-compute-wave BN sums of the workgroup's NT*16 columns
-__host__ __device__ constexpr int ct_red_bytes(int NT, int ncw = CT_NCW) { return ncw * 2 * NT * 16 * 4; }
+// per-compute-wave BN sums of the workgroup's NT*16 columns: the running sums and the chunk flush
+// rows of the two job parities (conv_tile.hip's chunked statistics schedule)
+// (fp8 inference instances: no statistics, one set)
+__host__ __device__ constexpr int ct_red_bytes(int NT, int ncw = CT_NCW, bool f8 = false) {
+  return (f8 ? 1 : 3) * ncw * 2 * NT * 16 * 4;
+}
 
 // packed bf16 pairs (low half = element 0)
 __device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }

@@ -649,3 +649,32 @@ extern "C" int fn_copy2(void* d0, const void* s0, long long n0, void* d1, const 
   FN_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// CU occupier (measurement only: scripts/dp_interference.py).  `nwg` workgroups of 256 threads,
+// each holding `lds` bytes of LDS and spinning VALU work for `usec` microseconds of wall time
+// (s_memrealtime, 100 MHz), so that a side stream pins that many CUs the way an RCCL ring
+// kernel does while the training step runs on the main stream.  lds >= 16 KB keeps a big-tile
+// conv workgroup (>= 144 KB) off the CU for the whole spin; lds = 0 only shares its issue
+// slots.  Every wave leaves after `usec` (bounded: no flag, no dependence on other work); a
+// nonzero `sink` word is written only if the impossible happens, so the loop is not dead code.
+__global__ __launch_bounds__(256) void cu_occupy_kernel(int usec, unsigned* __restrict__ sink) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long dt = (unsigned long long)usec * 100ull;   // 100 MHz ticks
+  float a = (float)threadIdx.x, b = 1.0001f;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < dt) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) a = a * b + 1e-7f;
+  }
+  if (a == -1.f) sink[threadIdx.x] = 1u;          // never true: keeps the spin alive
+}
+
+extern "C" int fn_cu_occupy(int nwg, int usec, int lds, void* sink, hipStream_t st) {
+  if (nwg <= 0 || nwg > 1024 || usec <= 0 || usec > 200000 || lds < 0 || lds > 160 * 1024) return -2;
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)cu_occupy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    return -5;
+  hipLaunchKernelGGL(cu_occupy_kernel, dim3((unsigned)nwg), dim3(256), (size_t)lds, st, usec, (unsigned*)sink);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

@@ -74,28 +74,9 @@ __device__ __forceinline__ void tile_pack_w_one(const float* __restrict__ w, uin
   // column order inside each nt*16-column block: fragment ct%nt, row i holds output column
   // 4nt*(i/4) + 4*(ct%nt) + i%4, so after the kernel's C^T MFMA a lane's nt fragments give 4nt
   // consecutive output columns (one 16-B store per 8)
-  int tap, ch0, col;
-  if (nt == 32) {
-    // conv_tile32 (v_mfma_f32_32x32x16_bf16, weights = A): fragment ct = 2 * (32-column block) + j
-    // (k half of the 32-k step); lane l holds MFMA row m = l & 31 -- output column
-    // 16((m>>2)&1) + (m&3) + 4(m>>3) of the block, so a lane half's accumulator holds 16
-    // consecutive columns -- and k = 8(l >> 5) + e
-    const int m = lane & 31, h = lane >> 5, j = ct & 1;
-    col = (ct >> 1) * 32 + 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3);
-    if (CS >= 32) {
-      const int sub = CS / 32;
-      tap = ks / sub;
-      ch0 = slice * CS + (ks % sub) * 32 + 16 * j + 8 * h;
-    } else if (CS == 16) {
-      tap = 2 * ks + j;
-      ch0 = slice * 16 + 8 * h;
-    } else {                                     // CS = 8: taps 4ks + 2j + h
-      tap = 4 * ks + 2 * j + h;
-      ch0 = slice * 8;
-    }
-  } else {
+  int tap, ch0;
   const int fi = lane & 15;
-  col = (ct / nt) * nt * 16 + 4 * nt * (fi >> 2) + 4 * (ct % nt) + (fi & 3);
+  const int col = (ct / nt) * nt * 16 + 4 * nt * (fi >> 2) + 4 * (ct % nt) + (fi & 3);
   if (CS >= 32) {
     const int sub = CS / 32;
     tap = ks / sub;
@@ -106,7 +87,6 @@ __device__ __forceinline__ void tile_pack_w_one(const float* __restrict__ w, uin
   } else {                                       // CS = 8: four taps per k-step
     tap = 4 * ks + (lane >> 4);
     ch0 = slice * 8;
-  }
   }
   Pack8 v;
 #pragma unroll

@@ -397,6 +397,9 @@ def stem_mode() -> str:
     return {"1": "e4m3", "e4m3": "e4m3", "i8": "i8", "int8": "i8"}.get(m, "bf16")
 
 
+CHECK_CHUNK = 64          # samples per forward of quantize_model's agreement check
+
+
 def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem=None) -> Fp8FeatureNet3D:
     """fp8 model with activation scales from a bf16 pass over ``calib_x``.
 
@@ -421,11 +424,18 @@ def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem=None) ->
     q = Fp8FeatureNet3D(model, calibrate(model, calib_x), in_scale, stem_int8=mode == "i8")
     # post-quantisation check on the calibration set: top-1 agreement of the fp8 and bf16 models
     # (a model whose activations the chosen scales do not fit shows up here, not in deployment)
+    # (in chunks of CHECK_CHUNK samples: two full-batch forwards over a 128^3 calibration set would
+    # double calibrate()'s peak activation memory)
     with torch.no_grad():
         x = calib_x if calib_x.dim() == 5 else calib_x.unsqueeze(-1)
-        a = model(x.to(torch.bfloat16)).float().argmax(-1)
-        b = q(x).float().argmax(-1)
-        q.calib_agreement = round(float((a == b).float().mean()), 4)
+        hits = 0
+        for i in range(0, x.shape[0], CHECK_CHUNK):
+            xc = x[i:i + CHECK_CHUNK]
+            a = model(xc.to(torch.bfloat16)).float().argmax(-1)
+            b = q(xc).float().argmax(-1)
+            hits += int((a == b).sum())
+            del a, b
+        q.calib_agreement = round(hits / max(1, x.shape[0]), 4)
     if q.calib_agreement < AGREEMENT_WARN:
         warnings.warn(f"fp8 model agrees with bf16 on {q.calib_agreement:.1%} of the calibration set "
                       f"(< {AGREEMENT_WARN:.0%}): keep this model in bf16", RuntimeWarning)

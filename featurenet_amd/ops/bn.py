@@ -52,12 +52,13 @@ def _eval_params(gamma, beta, rmean, rvar, eps, C, device):
 def _bwd_param_grads(dz2, y2, prm, act, beta=None, gamma=None, part=None):
     """(dbeta, dgamma) = (sum g, sum g*xhat), written straight into the parameters' flat
     gradients when :func:`grad_target` offers them.  ``part``: per-block partial sums
-    [nb, 2, C] already produced by the dgrad epilogue of the conv that consumed this
-    layer's output (:mod:`.bnfuse`); otherwise ``colstats`` computes them."""
+    [nb, 2, C] of the raw backward moments (sum g, sum g*y) already produced by the pass that
+    wrote dz (the max-pool backward, the pointwise head's dgrad); otherwise ``colstats``
+    computes them."""
     M, C = y2.shape
     K = _native.kernels()
     st = _native.stream(y2)
-    mode = 2                                     # dgrad-epilogue slabs: raw moments (sum g, sum g*y)
+    mode = 2                                     # raw moments (sum g, sum g*y)
     if part is None:
         mode = 1                                 # colstats: (sum g, sum g*xhat)
         nb = K.colstats_blocks(M, C, 1, act)
@@ -159,13 +160,11 @@ class BatchNormActFn(torch.autograd.Function):
             dy, dbeta, dgamma = _bwd_identity(dz2, y2, prm, *ctx.params, gslab=part[1], wpart=part[2])
             return (dy.reshape(y.shape), dgamma if ctx.has_gamma else None, dbeta if ctx.has_beta else None,
                     None, None, None, None, None, None, None, None)
-        if isinstance(part, tuple):
-            part = None                          # (no input gradient wanted: the colstats pass)
         dbeta = dgamma = None
         if ctx.training or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            # (eval mode with frozen parameters -- input gradients of robustness attacks -- needs
-            # neither: no colstats pass)
-            dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params, part=part)
+            # (no identity slab, or no input gradient wanted: the colstats pass.  Eval mode with
+            # frozen parameters -- input gradients of robustness attacks -- needs neither)
+            dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
                 dbeta if ctx.has_beta else None, None, None, None, None, None, None, None, None)

@@ -3,16 +3,16 @@
 A FeatureNet-3D block is ``conv -> BN -> act`` and the next block's conv reads
 ``z = act(bn(y))``.  In backward that conv's dgrad writes ``dz``, and the BN
 backward then needs ``sum g`` and ``sum g * xhat`` (``g = dz * act'(z)``): one
-full pass over ``dz`` and ``y`` (``colstats``).  The big-tile dgrad kernel sums
-``g`` and ``g * y`` in its epilogue from registers instead (it reads ``y`` at the
-tile's positions; ``bn_finalize`` mode 2 centres the moments in fp64), so the
-pass disappears.
+full pass over ``dz`` and ``y`` (``colstats``).  Instead the BN forward writes its relu
+mask, the big-tile dgrad's epilogue sums ``g`` from registers (its loader DMAs the mask
+bytes), and ``sum g * xhat`` follows from the adjoint identity ``sum_p dz z = sum W . dW``
+over the conv's weights and weight gradient (:func:`identity_ok`), so the pass disappears.
 
 Autograd runs the two ops as separate Functions, so they meet here:
 
-* :func:`tag_output` -- BN forward records ``z -> (y, prm, act)``;
+* :func:`tag_output` -- BN forward records ``z -> (y, prm, act, mask)``;
 * :func:`source_of` -- the consuming conv's forward looks its input up;
-* :func:`offer` -- its backward hands ``(dz, slab)`` over;
+* :func:`offer` -- its backward hands ``(dz, ("identity", sum-g slab, S partials))`` over;
 * :func:`take` -- the BN backward claims the slab for its ``dz`` (else it runs
   ``colstats`` as before).
 
@@ -35,22 +35,6 @@ import torch
 _LOCK = threading.Lock()
 _FWD: dict = {}      # z.data_ptr() -> (ref z, ref y, ref prm, act)
 _BWD: dict = {}      # dz.data_ptr() -> (ref dz, slab, ref y, dz._version at offer)
-
-
-def enabled() -> bool:
-    """Whether BN forwards tag their outputs for the consuming conv's dgrad.  ``FN_BN_DGRAD_FUSE``:
-    'auto' (default) = whenever the 32x32x16 tile kernel is on (``FN_TILE_M32``): its dgrad
-    epilogue reads y at the tile's positions with every load of a pass in flight together and
-    has the registers for it (209-247 VGPRs, no scratch); '1' always tags (the fusion still
-    happens only on the 32x32x16 kernel: the 16x16x32 kernel's statistics instance measured
-    slower in rounds 3 and 4 -- 5.14 vs 4.80 and 5.37 vs 5.00 ms per step -- and was removed);
-    '0' never."""
-    mode = os.environ.get("FN_BN_DGRAD_FUSE", "auto")
-    if mode == "auto":
-        from .conv_tile import m32_enabled
-
-        return m32_enabled()
-    return mode == "1"
 
 
 def identity_enabled() -> bool:
@@ -88,7 +72,7 @@ def _purge(d: dict, limit: int = 256) -> None:
 def tag_output(z: torch.Tensor, y: torch.Tensor, prm: torch.Tensor, act: int, mask=None) -> None:
     """BN forward (training): z = act(y * prm[2] + prm[3]), prm = (mean, invstd, scale, shift);
     ``mask``: z's relu-mask bytes (the identity path; the BN keeps it alive until its backward)."""
-    if not (enabled() or mask is not None):
+    if mask is None:
         return
     with _LOCK:
         _purge(_FWD)
@@ -110,8 +94,8 @@ def source_of(x: torch.Tensor):
 
 
 def offer(dz: torch.Tensor, slab, y: torch.Tensor) -> None:
-    """``slab``: the raw-moment slab [nb, 2, C] (conv_tile32), or ``("identity", gslab, wpart)``
-    (the 16x16x32 dgrad's sum-g slab and the S partials of the conv's W . dW)."""
+    """``slab``: ``("identity", gslab, wpart)`` -- the tile dgrad's sum-g slab and the S partials of
+    the conv's W . dW."""
     with _LOCK:
         _purge(_BWD)
         _BWD[dz.data_ptr()] = (weakref.ref(dz), slab, weakref.ref(y), dz._version)

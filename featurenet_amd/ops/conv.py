@@ -1025,8 +1025,6 @@ class ConvFn(torch.autograd.Function):
                 dx, slab = native_conv_dgrad(dy, w.detach(), spec, bn=ctx.bn_src, wpk=_stashed(ctx))
                 if isinstance(slab, tuple):
                     ident = slab[1]              # (offered below, with S from this conv's dW)
-                elif slab is not None:
-                    bnfuse.offer(dx, slab, bn_y)
                 ctx.bn_src = None
             else:
                 dx = native_conv_dgrad(dy, w.detach(), spec, wpk=_stashed(ctx))

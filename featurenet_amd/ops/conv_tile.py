@@ -34,31 +34,21 @@ from . import packs
 LDS_MAX = 160 * 1024
 NTHR = 320          # 4 MFMA waves + 1 loader wave
 MT_CHOICES = (8, 9)
-MT_CHOICES_32 = (8, 10)     # conv_tile32: MB = MT / 2 blocks of 32 rows per wave
-
-
-def m32_enabled() -> bool:
-    """FN_TILE_M32: '1' plans bf16 convs with whole 32-column blocks on the
-    v_mfma_f32_32x32x16_bf16 kernel (conv_tile32.hip); '0' (default) keeps every plan on the
-    16x16x32 kernel.  Round 4 measured the 32x32x16 k-loop 2-8 % slower on the FeatureNet-3D
-    layers (conv2 fwd 539 vs 513 us, dgrad 707 vs 669; the step 5.13 vs 4.97 ms on one box,
-    profiles/r4_m32_ab.md), the exception being conv3's dgrad with 640-row tiles -- so the
-    kernel is only in experiment builds (``FN_BUILD_EXPERIMENTS=1``)."""
-    return os.environ.get("FN_TILE_M32", "0") == "1" and experiments_built()
 
 
 def experiments_built() -> bool:
-    """The kernel library was built with ``FN_BUILD_EXPERIMENTS=1`` (conv_tile32, the int8
-    fp8-stem instance, the timing-only variants)."""
+    """The kernel library was built with ``FN_BUILD_EXPERIMENTS=1`` (the int8 fp8-stem instance,
+    the timing-only variants)."""
     try:
         return bool(_native.kernels().experiments_built())
     except Exception:                            # noqa: BLE001 - no library (CPU): nothing built
         return False
 
 
-def red_bytes(NT: int) -> int:
-    """LDS bytes of the per-compute-wave BN partial sums (4 waves x 2 x NT*16 columns)."""
-    return 4 * 2 * NT * 16 * 4
+def red_bytes(NT: int, f8: bool = False) -> int:
+    """LDS bytes of the per-compute-wave BN partial sums (4 waves x 2 x NT*16 columns: the running
+    sums and the chunk flush rows of both job parities -- csrc conv_tile_shared.h ct_red_bytes)."""
+    return (1 if f8 else 3) * 4 * 2 * NT * 16 * 4
 
 
 _LOCK = threading.Lock()
@@ -89,13 +79,8 @@ class TilePlan:
     cost: float      # modelled cycles (per wave, summed over the jobs of one CU)
     f8: bool = False  # fp8 (e4m3) inference variant: 16-channel chunks, 128-k steps, ring depth 2
     pool: bool = False  # fp8: fused 2^3 max-pool epilogue (even tile dims, window-per-lane row table)
-    m32: bool = False   # bf16 on conv_tile32_kernel (32x32x16 MFMA, MT / 2 blocks of 32 rows per wave)
     bs: bool = False    # fp8 with block-scaled activations: the block-scaled operand layout (k_table,
     #                     pack_weights_f8), two k-table rows per k-step, the LDS scale planes
-
-    @property
-    def MB(self) -> int:
-        return self.MT // 2
 
     @property
     def rows(self) -> int:
@@ -127,21 +112,20 @@ def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int
     (``f8``: the e4m3 inference variant, 32- or 64-channel slices; ``pool``: with the fused
     2^3 max-pool epilogue -- even output and tile dims; ``bs``: block-scaled fp8 operands, the
     LDS also holds two planes of the halo positions' scale dwords)."""
-    m32 = not f8 and Ncol % 32 == 0 and m32_enabled()
     bs = bool(bs and f8)
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, pool, m32, bs,
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, pool, bs,
            os.environ.get("FN_TILE_PLAN_RANK", "0"))
     if key in _PLANS:
         return _PLANS[key]
     if pool and (not f8 or any(d % 2 for d in out_dims)):
         return None
-    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, pool, m32, bs)
+    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, pool, bs)
     with _LOCK:
         _PLANS[key] = best
     return best
 
 
-def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False, bs=False):
+def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, bs=False):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
@@ -154,7 +138,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
     workers = max(1, n_cus // ncb)
     cands = []
     cs_only = int(os.environ.get("FN_TILE_CS", "0"))
-    mt_choices = (8,) if f8 else (MT_CHOICES_32 if m32 else MT_CHOICES)
+    mt_choices = (8,) if f8 else MT_CHOICES
     for CS in ((64, 32) if f8 else (32, 16, 8)):
         if Csrc % CS or (cs_only and CS != cs_only) or (CS == 8 and Csrc % 16 == 0):
             continue
@@ -171,16 +155,14 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
                     if pool and (TD % 2 or TH % 2 or TW % 2):
                         continue
                     MT = max(mt_choices[0], -(-rows // 64))
-                    if m32:
-                        MT += MT & 1                            # whole 32-row blocks
                     if rows < 64 * mt_choices[0] * 0.75:
                         continue
                     HH, HW = TH + KH - 1, TW + KW - 1
                     HP = (TD + KD - 1) * HH * HW
                     HPpad = -(-HP // 64) * 64
                     BUF = HPpad * CPP * 16                     # the halo (a multiple of 2 KiB)
-                    lds = 2 * BUF + 64 + red_bytes(NT) + (nks + PD + 2) * 16 * (2 if bs else 1) + HPpad * 8 \
-                        + (NT * 16 * 8 if f8 else 0) + (128 if m32 else 0) + (2 * HPpad * 4 if bs else 0)
+                    lds = 2 * BUF + 64 + red_bytes(NT, f8) + (nks + PD + 2) * 16 * (2 if bs else 1) + HPpad * 8 \
+                        + (NT * 16 * 8 if f8 else 0) + (2 * HPpad * 4 if bs else 0)
                     if lds > LDS_MAX:
                         continue
                     tiles = N * -(-OD // TD) * -(-OH // TH) * -(-OW // TW)
@@ -194,7 +176,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
                     if bs and HP * 16 >= 65536:
                         continue                               # (packed 16-bit data offsets)
                     cands.append(TilePlan(TD, TH, TW, CS, MT, NT, HPpad, nks, nct, BUF, _magic(HW), _magic(HH * HW),
-                                          float(cost), f8, pool, m32, bs))
+                                          float(cost), f8, pool, bs))
     # the cheapest few, re-costed with their row tables' residual bank conflicts (a
     # fragment whose 16 rows repeat a residue mod 16 reads at half rate).  (A finer term --
     # bank_ways, the simulated ways of every ds_read_b128 lane group -- was tried: conv4 fwd's
@@ -215,7 +197,7 @@ def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, m32=False
             dups = sum(16 - len(set(r.tolist())) for r in res)
             cost = c.cost * (1.0 + 0.5 * dups / res.size)
         ranked.append(TilePlan(*(getattr(c, f) for f in ("TD", "TH", "TW", "CS", "MT", "NT", "HPpad", "nks", "nct",
-                                                          "BUF", "mHW", "mHHW")), cost, f8, pool, m32, bs))
+                                                          "BUF", "mHW", "mHHW")), cost, f8, pool, bs))
     if not ranked:
         return None
     ranked.sort(key=lambda c: c.cost)
@@ -535,21 +517,6 @@ def k_table(p: TilePlan, kdims: tuple) -> np.ndarray:
                 tab2[k, lg] = off(st)
                 tab2[k, 4 + lg] = off(lo) | (off(hi) << 16)
         return tab2.astype(np.uint32).view(np.int32).reshape(-1, 4)
-    if p.m32:
-        # conv_tile32: entry [k][2h + j] = the offset lane half h reads in sub-step j (16 k each)
-        for k in range(p.nks):
-            for h in range(2):
-                for j in range(2):
-                    if p.CS >= 32:
-                        t, sub = divmod(k, p.CS // 32)
-                        off = (4 * sub + 2 * j + h) * plane
-                    elif p.CS == 16:
-                        t, off = 2 * k + j, h * plane
-                    else:
-                        t, off = 4 * k + 2 * j + h, 0
-                    if t < T:
-                        tab[k, 2 * h + j] = toff[t] + off
-        return tab
     for k in range(p.nks):
         for lg in range(4):
             if p.f8:                                 # lane group: 32 bytes of one tap (planes in lb)
@@ -589,7 +556,7 @@ def pack_weights(w: torch.Tensor, K: int, T: int, C: int, p: TilePlan, dgrad: bo
     out = torch.empty((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
     wf = w.detach().float().contiguous()
     _native.kernels().tile_pack_w(wf.data_ptr(), out.data_ptr(), K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad),
-                                  _native.stream(wf), 32 if p.m32 else p.NT)
+                                  _native.stream(wf), p.NT)
     packs.record(w, desc, 5)
     return out
 
@@ -599,7 +566,7 @@ def _pack_job(w: torch.Tensor, desc, kind: int):
     K, T, C, p, dgrad = desc
     nslice = (K if dgrad else C) // p.CS
     out = torch.empty((nslice * p.nks + PD) * p.nct * 64 * 8, dtype=torch.bfloat16, device=w.device)
-    row = [w.data_ptr(), out.data_ptr(), 5, K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad), 32 if p.m32 else p.NT]
+    row = [w.data_ptr(), out.data_ptr(), 5, K, T, C, p.CS, p.nks, p.nct, nslice, int(dgrad), p.NT]
     return row, out, out
 
 
@@ -618,7 +585,7 @@ def mask_dgrad_ok(p: TilePlan, ncol: int) -> bool:
 
 
 def _pack_params(p: TilePlan, Csrc: int, dgrad: bool) -> list[int]:
-    return [p.CS, p.nks, p.nct, Csrc // p.CS, int(dgrad), 32 if p.m32 else p.NT]
+    return [p.CS, p.nks, p.nct, Csrc // p.CS, int(dgrad), p.NT]
 
 
 def pack_pair(w: torch.Tensor, K: int, T: int, C: int, pf: TilePlan, pd: TilePlan):
@@ -643,7 +610,9 @@ def pack_pair(w: torch.Tensor, K: int, T: int, C: int, pf: TilePlan, pd: TilePla
 
 
 def workers(p: TilePlan, geom: list, ncol: int) -> int:
-    return int(_native.kernels().conv_tile_workers(geom, ncol, p.NT))
+    """Rows of the BN-statistics slab a launch with statistics writes: one per chunk of tiles
+    (conv_tile.hip's chunked deterministic schedule; the chunking depends on the tile count only)."""
+    return int(_native.kernels().conv_tile_slab_rows(geom, ncol, p.NT))
 
 
 def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p: TilePlan, geom: list, kdims: tuple,
@@ -654,12 +623,6 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
     ext = [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4]
     if bny is not None:
         ext += [bny.numel()] + ([bnp.numel()] if bnp is not None else [])
-    if p.m32:
-        _native.kernels().conv_tile32(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
-                                      zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
-                                      _native.ptr(stats), geom, ncol, act, p.MB, sched(src5.device, st).data_ptr(),
-                                      st, ext, float(oscale), _native.ptr(bny), _native.ptr(bnp))
-        return
     _native.kernels().conv_tile(src5.data_ptr(), wpk.data_ptr(), rt.data_ptr(), kt.data_ptr(),
                                 zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                 _native.ptr(stats), geom, ncol, act, p.MT, p.NT, sched(src5.device, st).data_ptr(),
@@ -719,23 +682,15 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None, w
     wpk = wpk[1] if wpk is not None and wpk[0] == p else pack_weights(w, spec.K, spec.taps, spec.C, p, dgrad=True)
     dx = torch.empty(spec.N, spec.D, spec.H, spec.W, spec.C, dtype=torch.bfloat16, device=dy5.device)
     mask = bn[3] if bn is not None else None
-    if bn is not None and not p.m32 and mask is not None and mask_dgrad_ok(p, spec.C):
+    if bn is not None and mask is not None and mask_dgrad_ok(p, spec.C):
         # the relu-mask epilogue (statistics identity, ops/bnfuse.py): the slab's row 0 holds the
         # column sums of g = dx * relu'(z); dx itself is stored unmasked
         assert mask.numel() * 8 == dx.numel() and mask.dtype == torch.uint8
         slab = torch.empty(workers(p, geom, spec.C), 2, spec.C, dtype=torch.float32, device=dy5.device)
         run(dy5, wpk, None, dx, slab, p, geom, kd, spec.C, 0, bny=mask)
         return dx, ("identity", slab)
-    # the raw-moment statistics epilogue: conv_tile32 plans (their LDS holds the BN scale / shift)
-    fuse = p.m32
-    if bn is None or not fuse:
-        run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
-        return dx if bn is None else (dx, None)
-    y, prm, act = bn[:3]
-    assert y.shape == dx.shape and y.dtype == torch.bfloat16 and y.is_contiguous() and prm.shape == (4, spec.C)
-    slab = torch.empty(workers(p, geom, spec.C), 2, spec.C, dtype=torch.float32, device=dy5.device)
-    run(dy5, wpk, None, dx, slab, p, geom, kd, spec.C, act, bny=y, bnp=prm.contiguous())
-    return dx, slab
+    run(dy5, wpk, None, dx, None, p, geom, kd, spec.C, 0)
+    return dx if bn is None else (dx, None)
 
 
 def fwd_plan(spec):

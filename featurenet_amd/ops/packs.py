@@ -66,10 +66,18 @@ def key(w: torch.Tensor, desc, kind: int):
 
 
 def lookup(w: torch.Tensor, desc, kind: int):
-    """The packed operand this scope's up-front launch made, or None."""
+    """The packed operand this scope's up-front launch made, or None -- also None when the
+    parameter was changed in place since (its version counter moved: an EMA / SWA swap, a
+    ``load_state_dict`` copy, a clamp between a forward and its backward), so the caller packs
+    the current values instead of using a stale pack."""
     gen = TLS.gen
     g = GENS.get(gen) if gen is not None else None
-    return None if g is None else g.cache.get(key(w, desc, kind))
+    if g is None:
+        return None
+    hit = g.cache.get(key(w, desc, kind))
+    if hit is None or hit[1] != w._version:
+        return None
+    return hit[0]
 
 
 def record(w: torch.Tensor, desc, kind: int):
@@ -123,7 +131,7 @@ class pack_scope:
             row, out, val = build(p, desc, kind)
             jobs.append(row)
             ext.append((p.numel(), out.numel()))
-            g.cache[k] = val
+            g.cache[k] = (val, p._version)       # (lookup checks the version: no stale packs)
         st = _native.stream(plist[0]) if jobs else None
         for i in range(0, len(jobs), MAXJ):
             _native.kernels().pack_w_multi([v for r in jobs[i:i + MAXJ] for v in r], st,

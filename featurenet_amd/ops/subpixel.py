@@ -282,7 +282,7 @@ def _bn_source(ctx, x: torch.Tensor, K: int) -> None:
     if src is None or src[3] is None or src[2] != 1:
         return
     p = _dgrad_plan(tuple(x.shape), K)
-    if p is not None and not p.m32 and conv_tile.mask_dgrad_ok(p, x.shape[-1]):
+    if p is not None and conv_tile.mask_dgrad_ok(p, x.shape[-1]):
         ctx.bn_src = src
 
 

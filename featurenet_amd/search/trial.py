@@ -16,7 +16,8 @@ GPU (8 concurrent candidates on an 8x MI355X node), with
 * invalid-candidate semantics: compile errors -> ``status="invalid"``,
   accuracy 0; OOM / non-finite loss -> ``status="failed"``;
 * fault-injection hooks for tests (``cfg.inject = {spec_name: "build" | "oom" |
-  "hang" | "crash"}``).
+  "hang" | "crash" | "device"}``; "device": a HIP runtime error that poisons the
+  worker's context -- the trial fails and the worker is replaced).
 """
 from __future__ import annotations
 
@@ -80,6 +81,8 @@ def run_trial(spec: ModelSpec, cfg: TrialConfig, device=None) -> ModelSpec:
         spec.nb_params, spec.nb_layers, spec.nb_flops = model.nb_params, model.nb_layers, model.flops_per_sample
         if fault == "oom":
             raise TrainingFailed("out of device memory: injected")
+        if fault == "device":
+            raise RuntimeError("HIP error: an illegal memory access was encountered (injected)")
         trainer = Trainer(model, lr=cfg.lr, device=device, graph=cfg.graph, meta={"model_kind": "candidate", "spec": spec.to_dict(),
                                                                   "input_shape": list(ds.input_shape),
                                                                   "num_classes": ds.num_classes,
@@ -127,6 +130,19 @@ def run_trial(spec: ModelSpec, cfg: TrialConfig, device=None) -> ModelSpec:
 # ---------------------------------------------------------------------------
 # process pool
 # ---------------------------------------------------------------------------
+# Error texts of a device runtime failure that leaves the process's HIP context unusable
+# (a faulting kernel, a device-side assert, a lost device): every later trial in that process
+# would fail the same way, so the worker reports the trial and exits, and the pool replaces it.
+_POISON_MARKERS = ("hip error", "hiperror", "cuda error", "device-side assert", "illegal memory access",
+                   "memory access fault", "hsa_status", "unspecified launch failure", "device lost")
+
+
+def device_poisoned(error: str | None) -> bool:
+    """True when a trial's error text names a device runtime failure (see ``_POISON_MARKERS``)."""
+    e = (error or "").lower()
+    return any(m in e for m in _POISON_MARKERS)
+
+
 def _worker(dev: str, tasks, results, ready):
     os.environ.setdefault("OMP_NUM_THREADS", "4")
     import torch
@@ -142,7 +158,14 @@ def _worker(dev: str, tasks, results, ready):
             return
         tid, spec_json, cfg = item
         out = run_trial(ModelSpec.from_json(spec_json), TrialConfig(**cfg), device)
-        results.put((tid, out.to_json()))
+        leaving = out.status == "failed" and device_poisoned(out.error)
+        results.put((tid, out.to_json(), leaving))
+        if leaving:
+            # the context is gone for every later trial: flush the result, then leave with a
+            # non-zero code (the result says so: the scheduler starts a fresh worker right away)
+            results.close()
+            results.join_thread()
+            os._exit(3)
 
 
 class TrialScheduler:
@@ -263,43 +286,77 @@ class TrialScheduler:
         pending = [(base + i, s) for i, s in enumerate(specs)]
         out: dict[int, ModelSpec] = {}
         cfgd = cfg.to_dict()
-        while len(out) < len(specs):
-            for w in workers.values():
-                if w["busy"] is None and pending:
-                    tid, s = pending.pop(0)
-                    w["busy"], w["t0"] = tid, time.time()
-                    w["tasks"].put((tid, s.to_json(), cfgd))
-            got = False
-            for w in list(workers.values()):
-                try:
-                    tid, js = w["results"].get_nowait()
-                except queue.Empty:
-                    continue
-                got = True
-                # only the trial this worker is running counts: a result that arrives after
-                # the watchdog already failed (and restarted) it is dropped
-                if w["busy"] == tid and tid not in out:
-                    out[tid] = ModelSpec.from_json(js)
-                    w["busy"] = None
-            if not got:
-                time.sleep(0.05)
-            # watchdog: hung or dead workers fail their trial and are restarted
-            for key in list(workers):
-                w = workers[key]
-                tid = w["busy"]
-                if tid is None:
-                    continue
-                dead = not w["proc"].is_alive()
-                hung = self.timeout_s is not None and time.time() - w["t0"] > self.timeout_s
-                if dead or hung:
-                    if not dead:
+        finished = False
+        try:
+            while len(out) < len(specs):
+                for key in list(workers):
+                    w = workers[key]
+                    if w["busy"] is None and pending:
+                        if not w["proc"].is_alive():       # (a worker that left after reporting a
+                            start(key)                       # device failure: a fresh one takes the task)
+                            w = workers[key]
+                        tid, s = pending.pop(0)
+                        w["busy"], w["t0"] = tid, time.time()
+                        w["tasks"].put((tid, s.to_json(), cfgd))
+                got = False
+                for key in list(workers):
+                    w = workers[key]
+                    try:
+                        tid, js, leaving = w["results"].get_nowait()
+                    except queue.Empty:
+                        continue
+                    got = True
+                    # only the trial this worker is running, of this call, counts: a result that
+                    # arrives after the watchdog already failed (and restarted) it is dropped
+                    if w["busy"] == tid and base <= tid < base + len(specs) and tid not in out:
+                        out[tid] = ModelSpec.from_json(js)
+                        w["busy"] = None
+                    if leaving:                          # (its device context is gone: replace it)
+                        w["proc"].join(timeout=30)
+                        if w["proc"].is_alive():
+                            w["proc"].kill()
+                            w["proc"].join(timeout=10)
+                        w["busy"] = None
+                        start(key)
+                if not got:
+                    time.sleep(0.05)
+                # watchdog: hung or dead workers fail their trial and are restarted
+                for key in list(workers):
+                    w = workers[key]
+                    tid = w["busy"]
+                    if tid is None:
+                        continue
+                    dead = not w["proc"].is_alive()
+                    hung = self.timeout_s is not None and time.time() - w["t0"] > self.timeout_s
+                    if dead or hung:
+                        if dead:                          # (its result may have landed just before
+                            try:                          #  it exited: take it if so)
+                                rtid, js, _ = w["results"].get(timeout=0.5)
+                                if rtid == tid and tid not in out:
+                                    out[tid] = ModelSpec.from_json(js)
+                            except queue.Empty:
+                                pass
+                        if not dead:
+                            w["proc"].kill()
+                        w["proc"].join(timeout=10)
+                        if tid not in out:
+                            s = specs[tid - base].clone()
+                            s.status, s.accuracy = "failed", 0.0
+                            s.error = "trial timed out" if hung else f"worker died (exit {w['proc'].exitcode})"
+                            out[tid] = s
+                        start(key)
+            finished = True
+        finally:
+            if not finished:
+                # abnormal exit (KeyboardInterrupt, a bad result, ...): a worker still busy with a
+                # task of this call would later report into the next call -- end it, so the next
+                # map() starts a fresh one
+                for key in list(workers):
+                    w = workers[key]
+                    if w["busy"] is not None:
                         w["proc"].kill()
-                    w["proc"].join(timeout=10)
-                    s = specs[tid - base].clone()
-                    s.status, s.accuracy = "failed", 0.0
-                    s.error = "trial timed out" if hung else f"worker died (exit {w['proc'].exitcode})"
-                    out[tid] = s
-                    start(key)
+                        w["proc"].join(timeout=10)
+                        w["busy"] = None
         if not self.persistent:
             for w in workers.values():
                 w["tasks"].put(None)

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round 6, first box: conv_tile tests after the chunked statistics schedule, the RCCL GPU tests,
+# the 1-GPU bench (chunked vs the round-5 static schedule, alternating), and the CU-interference
+# sweep (scripts/dp_interference.py) of both schedules.  Each GPU step has its own time limit; a
+# crash, abort or timeout ends the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+step() {
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 12 "gpurun_out/$name.log"
+  return $rc
+}
+step tests 900 python -u -m pytest tests/test_determinism_gpu.py tests/test_conv_tile_gpu.py tests/test_rccl_gpu.py tests/test_bnfuse_gpu.py tests/test_subpixel_gpu.py -x -v -s -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider || exit $?
+for i in 1 2; do
+  step bench_chunk_$i 200 python bench.py --steps 30 --warmup 5 || exit $?
+  FN_TILE_STATIC=1 step bench_static_$i 200 python bench.py --steps 30 --warmup 5 || exit $?
+done
+step interf_chunk 400 python -u scripts/dp_interference.py --cus 0 8 16 32 --lds 98304 0 --steps 15 || exit $?
+FN_TILE_STATIC=1 step interf_static 400 python -u scripts/dp_interference.py --cus 0 8 16 32 --lds 98304 0 --steps 15 || exit $?
+step interf_bwd_chunk 300 python -u scripts/dp_interference.py --cus 0 16 --lds 98304 --steps 15 --phase backward || exit $?
+FN_TILE_STATIC=1 step interf_bwd_static 300 python -u scripts/dp_interference.py --cus 0 16 --lds 98304 --steps 15 --phase backward || exit $?

@@ -8,16 +8,16 @@ from featurenet_amd.ops import bnfuse
 
 
 def test_source_and_take_match_only_the_tagged_pair(monkeypatch):
-    monkeypatch.setenv("FN_BN_DGRAD_FUSE", "1")
     y = torch.randn(2, 4, 4, 4, 8)
     prm = torch.randn(4, 8)
     z = torch.relu(y)
-    bnfuse.tag_output(z, y, prm, 1)
+    mask = torch.zeros(z.numel() // 8, dtype=torch.uint8)
+    bnfuse.tag_output(z, y, prm, 1, mask)
     src = bnfuse.source_of(z.reshape(2, 4, 4, 4, 8))      # a same-extent view matches
-    assert src is not None and src[0] is y and src[1] is prm and src[2] == 1
+    assert src is not None and src[0] is y and src[1] is prm and src[2] == 1 and src[3] is mask
     assert bnfuse.source_of(torch.empty_like(z)) is None  # another tensor does not
     dz = torch.randn_like(z)
-    slab = torch.randn(3, 2, 8)
+    slab = ("identity", torch.randn(3, 2, 8), torch.randn(2, 8))
     bnfuse.offer(dz, slab, y)
     assert bnfuse.take(dz, torch.empty_like(y)) is None   # wrong y: no slab (and the entry is consumed)
     bnfuse.offer(dz, slab, y)
@@ -26,25 +26,22 @@ def test_source_and_take_match_only_the_tagged_pair(monkeypatch):
 
 
 def test_dead_outputs_do_not_match(monkeypatch):
-    monkeypatch.setenv("FN_BN_DGRAD_FUSE", "1")
     y = torch.randn(64)
     prm = torch.randn(4, 1)
     z = torch.relu(y)
     ptr = z.data_ptr()
-    bnfuse.tag_output(z, y, prm, 1)
+    bnfuse.tag_output(z, y, prm, 1, torch.zeros(8, dtype=torch.uint8))
     del z
     gc.collect()
     w = torch.empty(64)
     if w.data_ptr() == ptr:                               # allocator reuse must not resurrect the entry
         assert bnfuse.source_of(w) is None
-    monkeypatch.setenv("FN_BN_DGRAD_FUSE", "0")
     z2 = torch.relu(y)
     bnfuse.tag_output(z2, y, prm, 1)
-    assert bnfuse.source_of(z2) is None                   # disabled: nothing is recorded
+    assert bnfuse.source_of(z2) is None                   # no relu mask (no identity path): nothing recorded
 
 
 def test_identity_tag_keeps_mask(monkeypatch):
-    monkeypatch.setenv("FN_BN_DGRAD_FUSE", "0")
     monkeypatch.setenv("FN_BN_IDENTITY", "1")
     y = torch.randn(2, 4, 4, 4, 32)
     prm = torch.randn(4, 32)

@@ -1,7 +1,7 @@
-"""BN-backward statistics fused into the consuming conv's dgrad epilogue (ops/bnfuse.py;
-conv_tile32.hip BWS instances -- the 16x16x32 kernel has none since round 4): the fused path must
-give the same parameter and input gradients as the separate colstats pass, and must actually
-take the fused branch."""
+"""BN-backward statistics fused into the consuming conv's dgrad (ops/bnfuse.py: the relu-mask
+epilogue and the statistics identity, the max-pool backward's moments): the fused paths must give
+the same parameter and input gradients as the separate colstats pass, and must actually take the
+fused branch."""
 import pytest
 import torch
 
@@ -13,7 +13,6 @@ from featurenet_amd.ops import bnfuse  # noqa: E402
 
 
 def _grads(model, x, fuse: bool, monkeypatch):
-    monkeypatch.setenv("FN_BN_DGRAD_FUSE", "1" if fuse else "0")
     monkeypatch.setenv("FN_POOL_BN_STATS", "1" if fuse else "0")
     model.zero_grad(set_to_none=True)
     out = model(x)
@@ -33,57 +32,6 @@ def _count_fused(monkeypatch):
 
     monkeypatch.setattr(bnmod.bnfuse, "take", take)
     return calls
-
-
-@pytest.mark.parametrize("N,S,cin,cmid,k", [(2, 20, 32, 32, 3), (3, 17, 16, 64, 4), (16, 24, 32, 64, 3)])
-def test_dgrad_bn_stats_match_colstats(monkeypatch, N, S, cin, cmid, k):
-    from torch import nn
-
-    from featurenet_amd.models.layers import Conv
-
-    assert _native.kernels() is not None
-    from featurenet_amd.ops import conv_tile as ct
-
-    if not ct.experiments_built():
-        pytest.skip("conv_tile32 (its raw-moment dgrad epilogue) is an experiment build")
-    monkeypatch.setenv("FN_CONV_TILE", "2")      # the tile kernel (the fused epilogue lives there)
-    monkeypatch.setenv("FN_TILE_M32", "1")       # the 32x32x16 kernel (its dgrad has the epilogue)
-    torch.manual_seed(0)
-    dev = torch.device("cuda", 0)
-    model = nn.Sequential(Conv(cin, cmid, k, 1, "valid", bn=True, act="relu", init="he"),
-                          Conv(cmid, 32, 3, 1, "valid", bn=True, act="relu", init="he")).to(dev)
-    x = torch.randn(N, S, S, S, cin, device=dev).to(torch.bfloat16)
-    calls = _count_fused(monkeypatch)
-    g0 = _grads(model, x, False, monkeypatch)
-    assert calls["fused"] == 0
-    g1 = _grads(model, x, True, monkeypatch)
-    assert calls["fused"] == 1, "the fused dgrad-epilogue statistics were not used"
-    for n in g0:
-        a, b = g0[n], g1[n]
-        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
-        assert err < 2e-3, f"{n}: rel err {err:.2e}"
-
-
-def test_featurenet3d_fused_bn_backward(monkeypatch):
-    """Production layer shapes (64^3, batch 8): every conv2..4 dgrad feeds its BN the fused sums."""
-    from featurenet_amd.models.featurenet3d import FeatureNet3D
-    from featurenet_amd.ops import conv_tile as ct
-
-    if not ct.experiments_built():
-        pytest.skip("conv_tile32 (its raw-moment dgrad epilogue) is an experiment build")
-    torch.manual_seed(1)
-    monkeypatch.setenv("FN_TILE_M32", "1")
-    dev = torch.device("cuda", 0)
-    model = FeatureNet3D().to(dev)
-    x = (torch.rand(8, 64, 64, 64, 1, device=dev) < 0.3).to(torch.bfloat16)
-    calls = _count_fused(monkeypatch)
-    g0 = _grads(model, x, False, monkeypatch)
-    g1 = _grads(model, x, True, monkeypatch)
-    assert calls["fused"] >= 1
-    for n in g0:
-        a, b = g0[n], g1[n]
-        err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
-        assert err < 5e-3, f"{n}: rel err {err:.2e}"
 
 
 @pytest.mark.parametrize("N,S,C", [(2, 20, 64), (4, 10, 32), (3, 8, 16)])
@@ -168,8 +116,8 @@ def test_seg_head_bn_in_pointwise_matches_unfused(monkeypatch, S):
 
 def test_forked_bn_output_falls_back(monkeypatch):
     """A BN output with two consumers (a conv and an identity branch): autograd adds the
-    identity branch's gradient into the conv's dx, so the dgrad-epilogue slab (conv branch
-    only) must not be used -- the gradients must equal the unfused path."""
+    identity branch's gradient into the conv's dx, so the dgrad-epilogue slab of the statistics
+    identity (conv branch only) must not be used -- the gradients must equal the colstats path."""
     from torch import nn
 
     from featurenet_amd.models.layers import Conv
@@ -189,8 +137,8 @@ def test_forked_bn_output_falls_back(monkeypatch):
     dev = torch.device("cuda", 0)
     model = Fork().to(dev)
     x = torch.randn(2, 18, 18, 18, 32, device=dev).to(torch.bfloat16)
-    g0 = _grads(model, x, False, monkeypatch)
-    g1 = _grads(model, x, True, monkeypatch)
+    g0 = _grads_ident(model, x, False, monkeypatch)
+    g1 = _grads_ident(model, x, True, monkeypatch)
     for n in g0:
         a, b = g0[n], g1[n]
         err = (a - b).abs().max().item() / max(a.abs().max().item(), 1e-6)
@@ -213,7 +161,6 @@ def _count_identity(monkeypatch):
 
 def _grads_ident(model, x, on: bool, monkeypatch):
     monkeypatch.setenv("FN_BN_IDENTITY", "1" if on else "0")
-    monkeypatch.setenv("FN_BN_DGRAD_FUSE", "0")
     model.zero_grad(set_to_none=True)
     out = model(x)
     loss = (out.float() * torch.linspace(-1, 1, out.shape[-1], device=x.device)).sum()
@@ -226,7 +173,6 @@ def test_identity_featurenet3d_matches_colstats(monkeypatch):
     identity (relu mask in the dgrad epilogue, S = sum W . dW) against the colstats pass."""
     from featurenet_amd.models.featurenet3d import FeatureNet3D
 
-    monkeypatch.setenv("FN_TILE_M32", "0")
     torch.manual_seed(2)
     dev = torch.device("cuda", 0)
     model = FeatureNet3D().to(dev)
@@ -260,7 +206,6 @@ def test_identity_any_gamma(monkeypatch, gscale):
     from featurenet_amd.models.layers import Conv
 
     monkeypatch.setenv("FN_CONV_TILE", "2")
-    monkeypatch.setenv("FN_TILE_M32", "0")
     torch.manual_seed(3)
     dev = torch.device("cuda", 0)
     model = nn.Sequential(Conv(16, 32, 3, 1, "valid", bn=True, act="relu", init="he"),

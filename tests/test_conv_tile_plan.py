@@ -74,7 +74,7 @@ def test_fp8_plans_and_weight_stream(out, k, c, n):
     T = k[0] * k[1] * k[2]
     tps = 128 // p.CS
     assert p.nks % ct.PD_F8 == 0 and p.nks * tps >= T
-    assert 2 * p.BUF + 64 + ct.red_bytes(p.NT) + (p.nks + ct.PD_F8 + 2) * 16 + p.HPpad * 8 <= ct.LDS_MAX
+    assert 2 * p.BUF + 64 + ct.red_bytes(p.NT, True) + (p.nks + ct.PD_F8 + 2) * 16 + p.HPpad * 8 <= ct.LDS_MAX
     g = torch.Generator().manual_seed(0)
     wq = torch.randint(1, 255, (n, T, c), generator=g, dtype=torch.uint8)
     wpk = ct.pack_weights_f8(wq, p)

@@ -207,3 +207,31 @@ def test_wgrad_kernels_bitwise_repeatable_and_correct():
     wr = w4.detach().float().reshape(16, 1, 3, 3).clone().requires_grad_(True)
     torch.nn.functional.conv2d(xr, wr, padding=1, groups=16).sum().backward()
     assert rel(res[0].reshape(16, 3, 3), wr.grad.reshape(16, 3, 3)) < 1e-2
+
+
+def test_tile_statistics_do_not_depend_on_the_grid():
+    """The chunked dynamic schedule of conv_tile's BN-statistics launches (fixed chunks of tiles,
+    one partial row per chunk, rows added in a fixed order): the same step on a grid of 37 or 100
+    workgroups instead of one per CU -- other workgroups running other chunks, in another order,
+    as when RCCL kernels hold CUs during data-parallel backward -- gives the same bits."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3D
+    from featurenet_amd.ops import softmax_xent
+
+    K = _native.kernels()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(16)
+    model = FeatureNet3D().to(dev)
+    x = (torch.rand(16, 64, 64, 64, 1, device=dev) < 0.3).to(torch.bfloat16)
+    y = torch.randint(0, 24, (16,), device=dev)
+    runs = []
+    try:
+        for cap in (0, 37, 100):
+            K.conv_tile_grid_cap(cap)
+            model.zero_grad(set_to_none=True)
+            loss = softmax_xent(model(x), y)
+            loss.backward()
+            torch.cuda.synchronize()
+            runs.append((loss.detach().clone(), _grads(model)))
+    finally:
+        K.conv_tile_grid_cap(0)
+    _assert_same(runs)

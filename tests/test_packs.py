@@ -29,13 +29,26 @@ def test_record_only_parameters_and_lookup_by_generation():
         packs.record(tmp, ("desc",), 0)
         packs.record(w.detach().reshape(4, -1), ("desc",), 0)   # (same storage, other shape)
     assert list(plan) == [packs.key(w, ("desc",), 0)]
-    g.cache[packs.key(w, ("desc",), 0)] = "packed"
+    g.cache[packs.key(w, ("desc",), 0)] = ("packed", w._version)
     with packs.gen_as(gid):
         assert packs.lookup(w.detach(), ("desc",), 0) == "packed"
         assert packs.lookup(w.detach(), ("other",), 0) is None
         assert packs.lookup(w.detach(), ("desc",), 1) is None
     assert packs.lookup(w, ("desc",), 0) is None      # outside the generation
     assert packs.TLS.gen is None
+
+
+def test_in_place_change_invalidates_the_pack():
+    """A parameter changed in place between the scope's packing and a lookup (an EMA swap, a
+    load_state_dict copy, a clamp) misses, so the layer packs its current values."""
+    w = torch.nn.Parameter(torch.randn(4, 3))
+    gid, g, _ = _gen([w])
+    g.cache[packs.key(w, ("d",), 0)] = ("packed", w._version)
+    with packs.gen_as(gid):
+        assert packs.lookup(w.detach(), ("d",), 0) == "packed"
+        with torch.no_grad():
+            w.clamp_(-0.5, 0.5)
+        assert packs.lookup(w.detach(), ("d",), 0) is None
 
 
 def test_dropped_generation_leaves_the_weak_map():

@@ -87,6 +87,44 @@ def test_scheduler_workers_persist_across_maps():
     assert not sched.pids() and all(not p.is_alive() for p in procs)
 
 
+def test_scheduler_replaces_worker_after_device_error():
+    """A trial that fails with a HIP runtime error (a poisoned context) is reported as failed and
+    its worker exits; the next trials run on a fresh worker instead of failing one after another."""
+    from featurenet_amd.search.trial import device_poisoned
+
+    assert device_poisoned("RuntimeError: HIP error: an illegal memory access was encountered")
+    assert not device_poisoned("TrainingFailed: loss is nan")
+    with TrialScheduler(devices=["cpu"], timeout_s=60, mode="process") as sched:
+        pid0 = sched.start().pids()
+        res = sched.map([_spec("dev"), _spec("b"), _spec("c")], _cfg(inject={"dev": "device"}))
+        assert [r.name for r in res] == ["dev", "b", "c"]
+        assert res[0].status == "failed" and "HIP error" in res[0].error
+        assert res[1].status == "trained" and res[2].status == "trained"
+        assert sched.pids() and set(sched.pids()).isdisjoint(pid0)
+
+
+def test_scheduler_abnormal_exit_leaves_no_stale_task(monkeypatch):
+    """map() leaving by an exception ends the workers still busy with its tasks, so the next map()
+    neither accepts their late results nor waits on a slot with no task behind it."""
+    import featurenet_amd.search.trial as tr
+
+    with TrialScheduler(devices=["cpu"], timeout_s=60, mode="process") as sched:
+        real = tr.ModelSpec.from_json
+        calls = {"n": 0}
+
+        def boom(js):
+            calls["n"] += 1
+            raise KeyboardInterrupt("injected")
+
+        monkeypatch.setattr(tr.ModelSpec, "from_json", staticmethod(boom))
+        with pytest.raises(KeyboardInterrupt):
+            sched.map([_spec("a"), _spec("b")], _cfg())
+        monkeypatch.setattr(tr.ModelSpec, "from_json", staticmethod(real))
+        assert all(w["busy"] is None for w in sched._workers.values())
+        res = sched.map([_spec("c"), _spec("d")], _cfg())
+        assert [r.name for r in res] == ["c", "d"] and all(r.status == "trained" for r in res)
+
+
 def test_full_evolution_two_generations(tmp_path):
     from featurenet_amd.search.evolution import load_snapshot, run_evolution
 
