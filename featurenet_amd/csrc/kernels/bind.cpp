@@ -113,6 +113,8 @@ int fn_conv_tile(const void*, const void*, const void*, const void*, const void*
 int fn_conv_tile_workers(const int*, int, int);
 int fn_conv_tile_slab_rows(const int*, int, int);
 void fn_conv_tile_grid_cap(int);
+void fn_conv_tile_set_wlds(int);
+int fn_conv_tile_wring(const int*, int, int, int, int);
 int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
                     float, const int*, int, int, int, int, int*, hipStream_t, const void*, void*);
 int fn_conv_tile_f8_supported(int, int, int);
@@ -337,6 +339,12 @@ PYBIND11_MODULE(_C, m) {
     return fn_conv_tile_workers(geom.data(), ncol, NT);
   });
   m.def("conv_tile_grid_cap", [](int cap) { fn_conv_tile_grid_cap(cap); });   // (tests: grid independence)
+  // the LDS weight ring: -1 = FN_TILE_WLDS (default on), 0 off, 1 on (tests / A/B in one process)
+  m.def("conv_tile_set_wlds", [](int mode) { fn_conv_tile_set_wlds(mode); });
+  m.def("conv_tile_wring", [](std::vector<int> geom, int ncol, int MT, int NT, int mask) {
+    need(geom, 31, "conv_tile_wring");
+    return fn_conv_tile_wring(geom.data(), ncol, MT, NT, mask);
+  });
   m.def("conv_tile_slab_rows", [](std::vector<int> geom, int ncol, int NT) {
     // rows of the BN-statistics slab a conv_tile launch with statistics writes (one per tile chunk)
     need(geom, 31, "conv_tile_slab_rows");

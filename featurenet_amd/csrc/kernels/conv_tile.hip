@@ -71,8 +71,12 @@
 // NCW: compute waves (4: one per SIMD, MT fragments each; 8: two per SIMD at MT / 2 -- the same
 // 4 * 8 fragment rows, so the same row tables -- where a partner wave can issue while the other
 // waits: the one-wave-per-SIMD k-loop ran its MFMAs at 72 % of its cycles)
+// WL (bf16): the weight fragments through an LDS ring of `wring` k-step slots that the loader wave
+// LDS-DMAs (one copy per workgroup instead of one per compute wave through L1), with per-k-step
+// counters in LDS for the hand-off (see the loader); wring = 0 / WL false: every compute wave
+// streams the fragments global -> VGPRs itself (the PD-deep register ring).
 template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false,
-          int NCW = CT_NCW>
+          int NCW = CT_NCW, bool WL = false>
 __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
@@ -85,7 +89,8 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
                                                                const float* __restrict__ scale, float oscale,
                                                                const unsigned char* __restrict__ gmask,
                                                                const unsigned* __restrict__ xsc,
-                                                               unsigned char* __restrict__ osc, int chunk) {
+                                                               unsigned char* __restrict__ osc, int chunk,
+                                                               int wring) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   static_assert(!BS || F8 || Q8O, "block scales: fp8 operands or an e4m3 output");
   constexpr int NTHR = 64 * (NCW + 1);
@@ -155,6 +160,18 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       }
     }
   }
+  // WL: the weight ring after everything else; counters in the job area: [8] k-steps published
+  // (landed in the ring) by the loader, [12 + w] k-steps whose fragments compute wave w has read
+  static_assert(!WL || !F8, "the LDS weight ring is the bf16 kernel's");
+  constexpr unsigned WSLOT = NT * 1024u;         // bytes of one ring slot (NT 1-KB bf16 fragments)
+  const int ring_off = 2 * g.BUF + mask_off + ct_mask_lds(NCW * MT * 16, Ncol, gmask != nullptr);
+  int* s_wrdy = s_job + 8;
+  int* s_wdone = s_job + 12;
+  int* s_wabort = s_job + 9;                     // set by a wave whose bounded wait ran out: no more waits
+  // (relaxed workgroup-scope atomics: plain ds_read / ds_write that the compiler may not merge,
+  // drop or hoist out of a polling loop, and -- unlike volatile -- with no wait behind them)
+  auto ld_cnt = [](int* p) -> int { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+  auto st_cnt = [](int* p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
   if constexpr (F8) {
     if (tid < NT * 16) {
       const int c = blockIdx.y * NT * 16 + tid;
@@ -191,6 +208,9 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   // and read the zero page outside.
   auto dma_job = [&](int tile, int slice, int bufoff) {
     ct_dma_job<CPP, ESZ>(g, src, zp, dsm, s_pos, tile, slice, bufoff, lane, tdn, thn, twn);
+  };
+  auto dma_job_rows = [&](int tile, int slice, int bufoff, int r_lo, int r_hi) {
+    ct_dma_job<CPP, ESZ>(g, src, zp, dsm, s_pos, tile, slice, bufoff, lane, tdn, thn, twn, r_lo, r_hi);
   };
   // BS: the scale dwords of the job's halo positions into scale plane `which` (64 positions per
   // DMA row; positions outside the input read the zero page: scale 2^-127 on zero data)
@@ -309,10 +329,138 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       s_job[1] = 0;
       s_job[2] = flush_of(t0, 0);
     }
+    if (WL && lane < 2 + NCW) s_job[lane == 0 ? 8 : (lane == 1 ? 9 : 10 + lane)] = 0;   // (ring counters, abort)
   }
   tile_lds_barrier();
 
-  if (loader) {
+  if (WL && loader) {
+    // ================ loader wave, LDS weight ring (WL) ================
+    // The weights are one cyclic stream: job j runs slice j % nslice (a tile's jobs are its slices in
+    // order), so k-step q of the workgroup is packed row (slice (q / nks) % nslice, k-step q % nks)
+    // whatever the tiles.  Step q goes to ring slot q % wring once every compute wave has read the
+    // step wring before it (s_wdone); after its DMA has landed the loader publishes it (s_wrdy).
+    // The next job's halo rows are interleaved with the weight steps, one per step, so a wait for
+    // landed weights never waits behind a whole halo.
+    int tile = __builtin_amdgcn_readfirstlane(s_job[0]), slice = 0, t_next = -1, kjob = 1;
+    const int NR = g.HPpad >> 6;
+    const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024;
+    const unsigned ring0 = ct_lds_addr(dsm) + (unsigned)ring_off;
+    int qi = 0, wsl = 0, wk = 0, wslot = 0;      // next step to issue: its slice, k-step, ring slot
+    auto issue_w = [&]() {
+      const unsigned char* src = wsrc + ((size_t)(wsl * nks + wk) * g.nct) * 1024;
+      const unsigned dst = ring0 + (unsigned)wslot * WSLOT;
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) ct_glds16_s(src + nt * 1024, (unsigned)lane * 16u, dst + (unsigned)nt * 1024u);
+      ++qi;
+      if (++wk == nks) {
+        wk = 0;
+        if (++wsl == nslice) wsl = 0;
+      }
+      if (++wslot == wring) wslot = 0;
+    };
+    auto credit = [&]() -> int {                 // steps the ring can hold now: the slowest reader + wring
+      int m = ld_cnt(s_wdone);
+#pragma unroll
+      for (int w = 1; w < NCW; ++w) m = min(m, ld_cnt(s_wdone + w));
+      return __builtin_amdgcn_readfirstlane(m) + wring;
+    };
+    auto publish = [&]() {                       // every DMA issued so far has landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) st_cnt(s_wrdy, qi);
+    };
+    if (tile >= 0) {
+      dma_job(tile, 0, 0);
+      if (nslice == 1) dma_mask(tile, 0);
+      if (!stat_chunk) t_next = next_tile(kjob);
+      ++kjob;
+    }
+    while (qi < wring) issue_w();                // (credit: nothing read yet)
+    publish();
+    int par = 0, jcur = 0;
+    int fl_prev = -1;
+    int fl_cur = __builtin_amdgcn_readfirstlane(s_job[2]);
+    while (true) {
+      tile_lds_barrier();                        // A: job halo landed; the other buffer is free
+      if (fl_prev >= 0) {
+        const float* fl = s_red + (1 + (par ^ 1)) * NCW * 2 * RC;
+        float* row = stats + (long long)fl_prev * 2 * Ncol;
+        for (int i = lane; i < 2 * RC; i += 64) {
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < NCW; ++w) v += fl[w * 2 * RC + i];
+          const int c = ct0 * 16 + (i < RC ? i : i - RC);
+          if (c < Ncol) row[(i < RC ? 0 : Ncol) + c] = v;
+        }
+      }
+      fl_prev = fl_cur;
+      if (tile < 0) break;
+      int ntile = tile, nslc = slice + 1;
+      if (nslc == nslice) {
+        nslc = 0;
+        ntile = stat_chunk ? next_tile(kjob) : t_next;
+      }
+      const int nfl = flush_of(ntile, nslc);
+      fl_cur = nfl;
+      if (lane == 0) {
+        s_job[4 * (par ^ 1)] = ntile;
+        s_job[4 * (par ^ 1) + 1] = nslc;
+        s_job[4 * (par ^ 1) + 2] = nfl;
+      }
+      // this period: job jcur's steps (and the compute waves' read-ahead of the next job's first)
+      // must all be issued before barrier A(jcur + 1); the loader goes on to the most the compute
+      // waves can release before it (everything up to their read-ahead + wring), so the next job
+      // starts on a full ring.  The next job's halo rows go in one per issued step (two when no
+      // step can be issued), and must have landed before the barrier.
+      const int qneed = (jcur + 1) * nks + 1;
+      const int qmax = qneed + wring - 1;
+      const int bo = (par ^ 1) * g.BUF;
+      int hr = ntile >= 0 ? 0 : NR;
+      if (ntile >= 0 && nslc == nslice - 1) dma_mask(ntile, par ^ 1);
+      int guard = 0;
+      while (true) {
+        const int lim = min(credit(), qmax + 1);
+        int issued = 0;
+        for (int b = 0; b < 4 && qi < lim; ++b) {
+          issue_w();
+          ++issued;
+          if (hr < NR) {
+            dma_job_rows(ntile, nslc, bo, hr, hr + 1);
+            ++hr;
+          }
+        }
+        if (!issued) {
+          for (int b = 0; b < 2 && hr < NR; ++b) {
+            dma_job_rows(ntile, nslc, bo, hr, hr + 1);
+            ++hr;
+            ++issued;
+          }
+        }
+        if (issued) {
+          publish();
+          guard = 0;
+          continue;
+        }
+        if (qi > qmax && hr >= NR) break;        // everything this period can issue, landed
+        // (no credit: the compute waves are behind by the whole ring.  The loop is bounded: after
+        // 2^20 empty polls -- tens of ms, far past any k-step -- it gives up and sets the abort flag
+        // that ends every wait of the workgroup, rather than hang the GPU)
+        if (++guard > (1 << 20) || ld_cnt(s_wabort)) {
+          if (lane == 0) st_cnt(s_wabort, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (nslc == 0 && ntile >= 0) {
+        if (!stat_chunk) t_next = next_tile(kjob);
+        ++kjob;
+      }
+      tile = ntile;
+      slice = nslc;
+      par ^= 1;
+      ++jcur;
+    }
+    tile_lds_barrier();                          // R
+  } else if (loader) {
     // ======================= loader wave =======================
     int tile = __builtin_amdgcn_readfirstlane(s_job[0]), slice = 0, t_next = -1, kjob = 1;
     // (the chunk walk hands out the next tile only once the current one is published: t_next is
@@ -393,7 +541,9 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
     unsigned fs[SR];
     int scl_job = 0;                             // BS: the lane's scale byte of the job's scale plane
                                                  // (less the lane's halo plane offset, see read_s)
-    Frag fb[PD][NT];
+    // B operand: the PD-deep register ring of weight fragments streamed from global memory, or (WL)
+    // two k-steps of fragments read from the LDS weight ring one k-step ahead
+    Frag fb[WL ? 2 : PD][NT];
     // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
     // ct0*16 + 4*NT*lg + 4nt + r: a lane ends with NV = 4*NT consecutive columns of one position
     const int gc8 = ct0 * 16 + NV * lg;
@@ -476,8 +626,28 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       for (int q = 0; q < 4; ++q) rsum[h][q] = rsq[h][q] = (ct_f32x2){0.f, 0.f};
     // ring prologue: the first job's k-steps 0..PD-1 (slice 0); every later job's come from
     // the previous job's last turn, so no job starts on an exposed L2 latency
+    if constexpr (!WL) {
 #pragma unroll
-    for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * FTILE, u);
+      for (int u = 0; u < PD; ++u) load_b(reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * FTILE, u);
+    }
+    // WL: the workgroup's k-step counter (uniform), the ring slot of the NEXT step, the published
+    // count as read during the previous step (one LDS read per step, used a step later)
+    int wq = 0, wslot1 = wring > 1 ? 1 : 0, wr_v = 0;
+    const unsigned char* rbase = dsm + ring_off + lane * 16;
+    // (bounded wait for the loader: no hang, whatever happens to it)
+    auto ring_wait = [&](int need) -> int {
+      int c = __builtin_amdgcn_readfirstlane(wr_v);
+      for (int guard = 0; c <= need; ++guard) {
+        if (guard > (1 << 20) || ld_cnt(s_wabort)) {   // (bounded: give up, and make every other
+          st_cnt(s_wabort, 1);                         //  wait of the workgroup give up at once)
+          return need + 1;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        c = __builtin_amdgcn_readfirstlane(ld_cnt(s_wrdy));
+      }
+      return c;
+    };
+    bool wfirst = true;
     int par = 0;
     while (true) {
       st_1 = stamp();
@@ -509,6 +679,14 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
         }
       }
       int ko_n = kofs(1);                        // offsets of the next k-step
+      if constexpr (WL) {
+        if (wfirst) {                            // (every later job's first step: read ahead by the
+          wfirst = false;                        //  previous job's last one)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) fb[0][nt] = *(const Frag*)(rbase + nt * 1024);
+          wr_v = ld_cnt(s_wrdy);
+        }
+      }
       for (int ks = 0; ks < nks; ks += PD) {
         const unsigned char* wl = ks + PD >= nks ? wnext : wbase;   // last turn: next job's steps
 #pragma unroll
@@ -536,7 +714,8 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
                 acc[mt][nt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[u][nt], fa[mt], acc[mt][nt], 0, 0,
                                                                                  0, 127, 0, 127);
               else
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u][nt], fa[mt], acc[mt][nt], 0, 0, 0);
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[WL ? (u & 1) : u][nt], fa[mt], acc[mt][nt],
+                                                                      0, 0, 0);
             }
             if constexpr (!(DBG & 2)) {
               fa[mt] = read_a(mt, ko);
@@ -545,10 +724,33 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
                 fs[r % SR] = read_s(r < MT ? r : r - MT, r < MT ? kos_c : kos_x);
               }
             }
+            if constexpr (WL) {
+              if (mt == 0) {
+                // the next k-step's fragments from the ring (published? the count read a step ago;
+                // rarely short -- then wait), then tell the loader this wave is done with the slot
+                // before it (volatile: the reads, the count store and the next count read stay in
+                // this order -- LDS runs one wave's accesses in order)
+                int c = __builtin_amdgcn_readfirstlane(wr_v);
+                if (c <= wq + 1) c = ring_wait(wq + 1);
+                // (the slot offset through an opaque copy that takes the checked count as an input:
+                // the reads cannot be hoisted above the check)
+                int so;
+                asm volatile("s_mov_b32 %0, %1" : "=s"(so) : "s"(wslot1 * (int)WSLOT), "s"(c));
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) fb[(u + 1) & 1][nt] = *(const Frag*)(rbase + so + nt * 1024);
+                st_cnt(s_wdone + wave, wq + 2);
+                wr_v = ld_cnt(s_wrdy);
+              }
+            }
             if constexpr (!(DBG & 128)) __builtin_amdgcn_sched_barrier(0);   // (DBG 128: free scheduling
           }                                                                  //  within a k-step)
           // k-step ks+u+PD, or the next job's step u
-          if constexpr (!(DBG & 1)) load_b(wl, u);
+          if constexpr (WL) {
+            ++wq;
+            wslot1 = wslot1 + 1 == wring ? 0 : wslot1 + 1;
+          } else if constexpr (!(DBG & 1)) {
+            load_b(wl, u);
+          }
           if constexpr (F8 && BS) kos_c = kos_x;
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -988,6 +1190,7 @@ static int tile_chunk(const TileGeom& g) {
 
 // rows of the BN-statistics slab [rows][2][Ncol] a statistics launch writes: one per chunk (or, with
 // the static schedule, one per workgroup)
+extern "C" int fn_conv_tile_wring(const int* geom, int Ncol, int MT, int NT, int mask);
 extern "C" int fn_conv_tile_slab_rows(const int* geom, int Ncol, int NT) {
   const TileGeom g = parse_tile(geom);
   const int c = tile_chunk(g);
@@ -998,24 +1201,38 @@ extern "C" int fn_conv_tile_slab_rows(const int* geom, int Ncol, int NT) {
 }
 
 template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false,
-          int NCW = CT_NCW>
+          int NCW = CT_NCW, bool WL = false>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
                        float oscale = 0.f, const void* gmask = nullptr, const void* xsc = nullptr,
-                       void* osc = nullptr, int chunk = 0) {
+                       void* osc = nullptr, int chunk = 0, int wring = 0) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW, WL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW>), grid, dim3(64 * (NCW + 1)), lds, st,
-                     (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act, sched,
-                     stamps, scale, oscale, (const unsigned char*)gmask, (const unsigned*)xsc,
-                     (unsigned char*)osc, chunk);
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW, WL>), grid, dim3(64 * (NCW + 1)), lds,
+                     st, (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act,
+                     sched, stamps, scale, oscale, (const unsigned char*)gmask, (const unsigned*)xsc,
+                     (unsigned char*)osc, chunk, wring);
   return 0;
+}
+
+// The LDS weight ring (conv_tile_kernel WL): on unless FN_TILE_WLDS=0, for the bf16 instances whose
+// plan leaves room for at least CT_WRING_MIN k-step slots (up to CT_WRING_MAX) in the 160 KiB
+#define CT_WRING_MIN 4
+#define CT_WRING_MAX 8
+static int g_tile_wlds = -1;      // -1: FN_TILE_WLDS (default on); 0 / 1 set by fn_conv_tile_set_wlds (tests)
+extern "C" void fn_conv_tile_set_wlds(int mode) { g_tile_wlds = mode < 0 ? -1 : (mode ? 1 : 0); }
+static int tile_wring(size_t lds, int NT) {
+  static const bool env_on = [] { const char* e = getenv("FN_TILE_WLDS"); return !(e && atoi(e) == 0); }();
+  const bool on = g_tile_wlds < 0 ? env_on : g_tile_wlds == 1;
+  if (!on || lds >= 160 * 1024) return 0;
+  const int r = (int)std::min<size_t>(CT_WRING_MAX, (160 * 1024 - lds) / ((size_t)NT * 1024));
+  return r >= CT_WRING_MIN ? r : 0;
 }
 
 // instantiations (MT, NT, CPP) -- the Python planner only emits these
@@ -1089,6 +1306,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   // (tests: a smaller grid must give the same bits -- only the dynamic schedules take it)
   if (g_tile_grid_cap > 0 && (!stats || tile_chunk(g) > 0)) grid.x = std::min<unsigned>(grid.x, g_tile_grid_cap);
+  const int wring = (oscale > 0.f || osc) ? 0 : tile_wring(lds, NT);
   int rc = -2;
 #ifdef FN_EXPERIMENTS
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();
@@ -1132,9 +1350,15 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
                              : launch_tile<M, N, C, 0, false, C == 1 && N == 2>(                                  \
                                    grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp,  \
                                    bias, out, stats, g, Ncol, act, sched, nullptr, nullptr, oscale))              \
-                      : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,                 \
-                                             (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, nullptr,     \
-                                             nullptr, 0.f, bny, nullptr, nullptr, stats ? tile_chunk(g) : 0);
+                      : (wring ? launch_tile<M, N, C, 0, false, false, false, false, CT_NCW, true>(                \
+                                     grid, lds + (size_t)wring * N * 1024, st, src, (const uint4*)wp,                 \
+                                     (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act,       \
+                                     sched, nullptr, nullptr, 0.f, bny, nullptr, nullptr, stats ? tile_chunk(g) : 0,   \
+                                     wring)                                                                            \
+                               : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,       \
+                                                      (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched,    \
+                                                      nullptr, nullptr, 0.f, bny, nullptr, nullptr,                    \
+                                                      stats ? tile_chunk(g) : 0));
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;
@@ -1269,4 +1493,11 @@ extern "C" int fn_conv_tile_f8(const void* src, const void* wp, const void* rowt
   if (rc) return rc;
   FN_CHECK_LAUNCH();
   return 0;
+}
+
+// k-step slots of the LDS weight ring a bf16 launch of this plan gets (0: the register path) --
+// the test / profile hook for which path a layer takes
+extern "C" int fn_conv_tile_wring(const int* geom, int Ncol, int MT, int NT, int mask) {
+  const TileGeom g = parse_tile(geom);
+  return tile_wring(tile_lds_total(g, MT, NT, false, Ncol, mask != 0), NT);
 }

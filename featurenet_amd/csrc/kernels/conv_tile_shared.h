@@ -84,11 +84,13 @@ __host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : 4; }
 // loader): interior halos (the common case for unpadded convs) use SGPR base + the
 // per-position byte offsets of s_pos, no address math per DMA row; halos crossing the input
 // boundary check every position and read the zero page outside.
+// (r_lo, r_hi: only DMA rows [r_lo, r_hi) of the job's HPpad / 64 -- the LDS-weight-ring loader
+// interleaves a job's halo with the weight stream; -1: to the last row)
 template <int CPP, int ESZ>
 __device__ __forceinline__ void ct_dma_job(const TileGeom& g, const unsigned char* __restrict__ src,
                                            const unsigned char* __restrict__ zp, unsigned char* dsm,
                                            const int2* s_pos, int tile, int slice, int bufoff, int lane, int tdn,
-                                           int thn, int twn) {
+                                           int thn, int twn, int r_lo = 0, int r_hi = -1) {
   const int HH = g.TH + g.KH - 1, HW = g.TW + g.KW - 1;
   const int PLANE = g.HPpad * 16;
   tile = __builtin_amdgcn_readfirstlane(tile);   // (wave-uniform: the SGPR operands need proof)
@@ -106,10 +108,10 @@ __device__ __forceinline__ void ct_dma_job(const TileGeom& g, const unsigned cha
   const unsigned dst0 = ct_lds_addr(dsm) + bufoff;
   // position rows in batches of 8: the s_pos reads of a batch are in flight together
   // (one LDS latency per batch, not per DMA row)
-  const int NR = g.HPpad >> 6;
+  const int NR = r_hi < 0 ? (g.HPpad >> 6) : r_hi;
   if (interior) {
     const unsigned char* obase = base + (((long long)dlo * g.IH + hlo) * g.IW + wlo) * g.C * ESZ;
-    for (int r0 = 0; r0 < NR; r0 += 8) {
+    for (int r0 = r_lo; r0 < NR; r0 += 8) {
       int po[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) po[i] = s_pos[((r0 + i < NR ? r0 + i : NR - 1) << 6) + lane].x;
@@ -123,7 +125,7 @@ __device__ __forceinline__ void ct_dma_job(const TileGeom& g, const unsigned cha
       }
     }
   } else {
-    for (int r0 = 0; r0 < NR; r0 += 8) {
+    for (int r0 = r_lo; r0 < NR; r0 += 8) {
       int e[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) e[i] = s_pos[((r0 + i < NR ? r0 + i : NR - 1) << 6) + lane].y;

@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round 6, first box: conv_tile tests after the chunked statistics schedule, the RCCL GPU tests,
-# the 1-GPU bench (chunked vs the round-5 static schedule, alternating), and the CU-interference
-# sweep (scripts/dp_interference.py) of both schedules.  Each GPU step has its own time limit; a
-# crash, abort or timeout ends the script.
+# Round 6: conv_tile after the chunked statistics schedule and the LDS weight ring -- the ring's
+# bitwise test first (short limit), then the conv / determinism / RCCL / BN-fusion GPU tests, the
+# 1-GPU bench (ring on / off, static schedule; alternating) and the CU-interference sweep
+# (scripts/dp_interference.py) of the chunked and the static schedules.  Each GPU step has its own
+# time limit; a crash, abort or timeout ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -16,12 +17,12 @@ step() {
   tail -n 12 "gpurun_out/$name.log"
   return $rc
 }
-step tests 900 python -u -m pytest tests/test_determinism_gpu.py tests/test_conv_tile_gpu.py tests/test_rccl_gpu.py tests/test_bnfuse_gpu.py tests/test_subpixel_gpu.py -x -v -s -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider || exit $?
+step ring 240 python -u -m pytest "tests/test_determinism_gpu.py::test_weight_ring_gives_the_register_path_bits" -x -v -s -m gpu --timeout 200 --timeout-method thread -p no:cacheprovider || exit $?
 for i in 1 2; do
-  step bench_chunk_$i 200 python bench.py --steps 30 --warmup 5 || exit $?
-  FN_TILE_STATIC=1 step bench_static_$i 200 python bench.py --steps 30 --warmup 5 || exit $?
+  step bench_wl_$i 150 python bench.py --steps 30 --warmup 5 || exit $?
+  FN_TILE_WLDS=0 step bench_reg_$i 150 python bench.py --steps 30 --warmup 5 || exit $?
 done
-step interf_chunk 400 python -u scripts/dp_interference.py --cus 0 8 16 32 --lds 98304 0 --steps 15 || exit $?
-FN_TILE_STATIC=1 step interf_static 400 python -u scripts/dp_interference.py --cus 0 8 16 32 --lds 98304 0 --steps 15 || exit $?
-step interf_bwd_chunk 300 python -u scripts/dp_interference.py --cus 0 16 --lds 98304 --steps 15 --phase backward || exit $?
-FN_TILE_STATIC=1 step interf_bwd_static 300 python -u scripts/dp_interference.py --cus 0 16 --lds 98304 --steps 15 --phase backward || exit $?
+FN_TILE_STATIC=1 FN_TILE_WLDS=0 step bench_r5sched 150 python bench.py --steps 30 --warmup 5 || exit $?
+step tests 900 python -u -m pytest tests/test_determinism_gpu.py tests/test_conv_tile_gpu.py tests/test_rccl_gpu.py tests/test_bnfuse_gpu.py tests/test_subpixel_gpu.py -x -v -s -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider || exit $?
+step interf_chunk 300 python -u scripts/dp_interference.py --cus 0 8 16 32 --lds 98304 0 --steps 15 || exit $?
+FN_TILE_STATIC=1 step interf_static 300 python -u scripts/dp_interference.py --cus 0 8 16 32 --lds 98304 0 --steps 15 || exit $?
