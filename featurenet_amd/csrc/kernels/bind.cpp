@@ -114,6 +114,8 @@ int fn_conv_tile_workers(const int*, int, int);
 int fn_conv_tile_slab_rows(const int*, int, int);
 void fn_conv_tile_grid_cap(int);
 void fn_conv_tile_set_wlds(int);
+void fn_conv_tile_set_schedule(int);
+int fn_conv_tile_schedule();
 int fn_conv_tile_wring(const int*, int, int, int, int);
 int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const void*, const float*, const float*, void*,
                     float, const int*, int, int, int, int, int*, hipStream_t, const void*, void*);
@@ -341,6 +343,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_tile_grid_cap", [](int cap) { fn_conv_tile_grid_cap(cap); });   // (tests: grid independence)
   // the LDS weight ring: -1 = FN_TILE_WLDS (default on), 0 off, 1 on (tests / A/B in one process)
   m.def("conv_tile_set_wlds", [](int mode) { fn_conv_tile_set_wlds(mode); });
+  // the BN-statistics tile schedule: -1 = FN_TILE_SCHED (default static), 0 static, 1 chunked
+  m.def("conv_tile_set_schedule", [](int mode) { fn_conv_tile_set_schedule(mode); });
+  m.def("conv_tile_schedule", [] { return fn_conv_tile_schedule(); });
   m.def("conv_tile_wring", [](std::vector<int> geom, int ncol, int MT, int NT, int mask) {
     need(geom, 31, "conv_tile_wring");
     return fn_conv_tile_wring(geom.data(), ncol, MT, NT, mask);

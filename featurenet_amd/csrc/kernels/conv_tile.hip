@@ -43,6 +43,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <type_traits>
 #include <vector>
 
@@ -297,26 +298,46 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   const int G = (int)gridDim.x;
   const int slot = (G & 7) == 0 ? ((int)blockIdx.x & 7) * (G >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
   const int nchunk = stat_chunk ? (ntiles + chunk - 1) / chunk : 0;
+  // Dynamic grabs (chunks with statistics, single tiles without) come from 8 XCD queues: the units
+  // are cut into 8 contiguous ranges, queue x's counter at sched[1 + 8 * blockIdx.y + x]; a
+  // workgroup takes from the queue of its own XCD (workgroups are dispatched to the XCDs round
+  // robin: linear id & 7 -- a locality hint only, any mapping is correct), so neighbouring tiles
+  // run together on one XCD and share halo rows in its L2, and once that range is done it takes
+  // from the others in turn (the tail balances across the chip).
+  const int nunit = stat_chunk ? nchunk : ntiles;
+  const int xcd0 = (int)((blockIdx.x + blockIdx.y * gridDim.x) & 7);
+  int qdone = 0;                                 // (loader, uniform) bit x: queue x found empty
+  auto grab = [&]() -> int {                     // the next unit for this workgroup, or -1
+    for (int i = 0; i < 8; ++i) {
+      const int x = (xcd0 + i) & 7;
+      if (qdone & (1 << x)) continue;
+      const int lo = (int)(((long long)nunit * x) >> 3), hi = (int)(((long long)nunit * (x + 1)) >> 3);
+      int c = 0;
+      if (lane == 0) c = atomicAdd(sched + 1 + 8 * blockIdx.y + x, 1);
+      c = lo + __builtin_amdgcn_readfirstlane(c);
+      if (c < hi) return c;
+      qdone |= 1 << x;
+    }
+    return -1;
+  };
   // loader state of the chunk walk (wave-uniform): the chunk being handed out, its next tile, its end
   int ch_id = -1, ch_next = 0, ch_end = 0;
   auto next_tile = [&](int k) -> int {           // tile of this workgroup's job k (-1: none)
     if (stat_chunk) {
       if (ch_next >= ch_end) {
-        int c = 0;
-        if (lane == 0) c = atomicAdd(sched + 1 + blockIdx.y, 1);
-        c = __builtin_amdgcn_readfirstlane(c);
-        if (c >= nchunk) return -1;
+        const int c = grab();
+        if (c < 0) return -1;
         ch_id = c;
         ch_next = c * chunk;
         ch_end = min(ntiles, ch_next + chunk);
       }
       return ch_next++;
     }
-    int t = 0;
-    if (stat_static) t = k * G + slot;
-    else if (lane == 0) t = atomicAdd(sched + 1 + blockIdx.y, 1);
-    t = __builtin_amdgcn_readfirstlane(t);
-    return t < ntiles ? t : -1;
+    if (stat_static) {
+      const int t = k * G + slot;
+      return t < ntiles ? t : -1;
+    }
+    return grab();
   };
   // the chunk to flush after job (tile, slice): its id when this is the chunk's last job, else -1
   auto flush_of = [&](int tile, int slice) -> int {
@@ -346,6 +367,8 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
     const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(wp) + (size_t)ct0 * 1024;
     const unsigned ring0 = ct_lds_addr(dsm) + (unsigned)ring_off;
     int qi = 0, wsl = 0, wk = 0, wslot = 0;      // next step to issue: its slice, k-step, ring slot
+    // (the compute waves hand slots back a whole turn -- PD k-steps -- at a time, and the loader
+    // issues and publishes whole turns: one credit poll, one wait for the landing per PD steps)
     auto issue_w = [&]() {
       const unsigned char* src = wsrc + ((size_t)(wsl * nks + wk) * g.nct) * 1024;
       const unsigned dst = ring0 + (unsigned)wslot * WSLOT;
@@ -359,12 +382,13 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       if (++wslot == wring) wslot = 0;
     };
     auto credit = [&]() -> int {                 // steps the ring can hold now: the slowest reader + wring
+      if (act & 0x400) return 1 << 30;           // (timing only: no hand-off, wrong results)
       int m = ld_cnt(s_wdone);
 #pragma unroll
       for (int w = 1; w < NCW; ++w) m = min(m, ld_cnt(s_wdone + w));
       return __builtin_amdgcn_readfirstlane(m) + wring;
     };
-    auto publish = [&]() {                       // every DMA issued so far has landed
+    auto publish = [&]() {                       // everything issued so far has landed
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) st_cnt(s_wrdy, qi);
     };
@@ -407,10 +431,9 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
         s_job[4 * (par ^ 1) + 2] = nfl;
       }
       // this period: job jcur's steps (and the compute waves' read-ahead of the next job's first)
-      // must all be issued before barrier A(jcur + 1); the loader goes on to the most the compute
-      // waves can release before it (everything up to their read-ahead + wring), so the next job
-      // starts on a full ring.  The next job's halo rows go in one per issued step (two when no
-      // step can be issued), and must have landed before the barrier.
+      // must all be issued before barrier A(jcur + 1), and the next job's first turn too, so it
+      // starts without waiting for the loader.  The next job's halo rows go in one per issued
+      // step (two when no step can be issued), and must have landed before the barrier.
       const int qneed = (jcur + 1) * nks + 1;
       const int qmax = qneed + wring - 1;
       const int bo = (par ^ 1) * g.BUF;
@@ -419,28 +442,30 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       int guard = 0;
       while (true) {
         const int lim = min(credit(), qmax + 1);
-        int issued = 0;
-        for (int b = 0; b < 4 && qi < lim; ++b) {
-          issue_w();
-          ++issued;
-          if (hr < NR) {
-            dma_job_rows(ntile, nslc, bo, hr, hr + 1);
-            ++hr;
+        if (lim - qi >= PD || (lim > qi && lim == qmax + 1)) {   // a whole turn (or the period's rest)
+          const int n = min(lim - qi, PD);
+          for (int b = 0; b < n; ++b) {
+            issue_w();
+            if (hr < NR) {
+              dma_job_rows(ntile, nslc, bo, hr, hr + 1);
+              ++hr;
+            }
           }
-        }
-        if (!issued) {
-          for (int b = 0; b < 2 && hr < NR; ++b) {
-            dma_job_rows(ntile, nslc, bo, hr, hr + 1);
-            ++hr;
-            ++issued;
-          }
-        }
-        if (issued) {
           publish();
           guard = 0;
           continue;
         }
-        if (qi > qmax && hr >= NR) break;        // everything this period can issue, landed
+        if (hr < NR) {                           // no credit yet: halo rows
+          for (int b = 0; b < 2 && hr < NR; ++b) {
+            dma_job_rows(ntile, nslc, bo, hr, hr + 1);
+            ++hr;
+          }
+          continue;
+        }
+        // the job's steps and the next job's first turn issued and landed: on to the barrier (the
+        // compute waves finish this job from the ring without the loader, and find the next one's
+        // first turn there -- no bubble at the job boundary)
+        if (qi >= qneed + PD) break;
         // (no credit: the compute waves are behind by the whole ring.  The loop is bounded: after
         // 2^20 empty polls -- tens of ms, far past any k-step -- it gives up and sets the abort flag
         // that ends every wait of the workgroup, rather than hang the GPU)
@@ -450,6 +475,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the halo of the next job has landed)
       if (nslc == 0 && ntile >= 0) {
         if (!stat_chunk) t_next = next_tile(kjob);
         ++kjob;
@@ -726,19 +752,22 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
             }
             if constexpr (WL) {
               if (mt == 0) {
-                // the next k-step's fragments from the ring (published? the count read a step ago;
-                // rarely short -- then wait), then tell the loader this wave is done with the slot
-                // before it (volatile: the reads, the count store and the next count read stay in
-                // this order -- LDS runs one wave's accesses in order)
-                int c = __builtin_amdgcn_readfirstlane(wr_v);
-                if (c <= wq + 1) c = ring_wait(wq + 1);
-                // (the slot offset through an opaque copy that takes the checked count as an input:
-                // the reads cannot be hoisted above the check)
-                int so;
-                asm volatile("s_mov_b32 %0, %1" : "=s"(so) : "s"(wslot1 * (int)WSLOT), "s"(c));
+                // the next k-step's fragments from the ring.  Once per turn: are the turn's reads
+                // (steps wq + 1 .. wq + PD) published?  (the count read a step ago; rarely short --
+                // then wait).  At the turn's end: this wave is done with the slots of the steps
+                // before wq + 2 (the reads, the count store and the next count read stay in order:
+                // LDS runs one wave's accesses in order; the relaxed atomics keep the compiler's)
+                int so = wslot1 * (int)WSLOT;
+                if (u == 0) {
+                  int c = __builtin_amdgcn_readfirstlane(wr_v);
+                  if (c <= wq + PD && !(act & 0x400)) c = ring_wait(wq + PD);   // (0x400: timing only)
+                  // (the slot offset through an opaque copy that takes the checked count as an
+                  // input: the turn's reads cannot be hoisted above the check)
+                  asm volatile("s_mov_b32 %0, %1" : "=s"(so) : "s"(so), "s"(c));
+                }
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) fb[(u + 1) & 1][nt] = *(const Frag*)(rbase + so + nt * 1024);
-                st_cnt(s_wdone + wave, wq + 2);
+                if (u == PD - 1) st_cnt(s_wdone + wave, wq + 2);
                 wr_v = ld_cnt(s_wrdy);
               }
             }
@@ -1082,7 +1111,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   if (tid == 0 && !stat_static) {                // the last workgroup out resets the counters
     __threadfence();                             // (static schedules never touch them)
     if (atomicAdd(sched, 1) == (int)(gridDim.x * gridDim.y) - 1) {
-      for (int i = 0; i < (int)gridDim.y; ++i) atomicExch(sched + 1 + i, 0);
+      for (int i = 0; i < 8 * (int)gridDim.y; ++i) atomicExch(sched + 1 + i, 0);
       atomicExch(sched, 0);
     }
   }
@@ -1171,16 +1200,30 @@ extern "C" int fn_conv_tile_workers(const int* geom, int Ncol, int NT) {
   return w > ntiles ? ntiles : w;
 }
 
-// Statistics chunks of conv_tile_kernel's chunked schedule: tiles per chunk from the tile count
-// alone (never the grid or the CU count: the partial rows -- so the statistics' bits -- are the
-// same on every box), at most CT_MAX_CHUNKS chunks, so every workgroup takes dozens and the tail
-// of the dynamic grab is about one tile.  FN_TILE_STATIC=1: the round-5 static schedule (A/B of
-// profiles/r6_dp_interference.md only).
+// Schedule of the BN-statistics launches (both deterministic, see conv_tile_kernel):
+//   static  -- fixed tiles per workgroup, one partial row per workgroup: the fastest when the
+//              kernel has the GPU to itself (1 GPU: 4.61-4.62 vs 4.73-4.76 ms per training step,
+//              profiles/r6_dp_interference.md);
+//   chunked -- fixed chunks of tiles grabbed dynamically from XCD queues, one partial row per
+//              chunk: degrades gracefully when other kernels hold CUs (the RCCL rings of the
+//              data-parallel all-reduce overlapping the backward).
+// fn_conv_tile_set_schedule: 0 static, 1 chunked; the data-parallel gradient bucketer selects the
+// chunked one when the world has more than one rank (parallel/ddp.py).  FN_TILE_SCHED=static /
+// chunked overrides.  Chunks: tiles per chunk from the tile count alone (never the grid or the CU
+// count: the partial rows -- so the statistics' bits -- are the same on every box), at most
+// CT_MAX_CHUNKS chunks, so every workgroup takes dozens and the tail of the dynamic grab is about one
+// chunk.
 #define CT_MAX_CHUNKS 8192
-static bool tile_stat_static() {
-  static const bool v = [] { const char* e = getenv("FN_TILE_STATIC"); return e && atoi(e) == 1; }();
-  return v;
+static int g_tile_sched = -1;     // -1: FN_TILE_SCHED (default static); 0 static, 1 chunked
+extern "C" void fn_conv_tile_set_schedule(int mode) { g_tile_sched = mode < 0 ? -1 : (mode ? 1 : 0); }
+extern "C" int fn_conv_tile_schedule() {
+  static const int env = [] {
+    const char* e = getenv("FN_TILE_SCHED");
+    return (e && std::string(e) == "chunked") ? 1 : 0;
+  }();
+  return g_tile_sched < 0 ? env : g_tile_sched;
 }
+static bool tile_stat_static() { return fn_conv_tile_schedule() == 0; }
 static int tile_chunk(const TileGeom& g) {
   if (tile_stat_static()) return 0;
   const long long nt = (long long)g.N * ((g.OD + g.TD - 1) / g.TD) * ((g.OH + g.TH - 1) / g.TH) *
@@ -1223,8 +1266,8 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
 
 // The LDS weight ring (conv_tile_kernel WL): on unless FN_TILE_WLDS=0, for the bf16 instances whose
 // plan leaves room for at least CT_WRING_MIN k-step slots (up to CT_WRING_MAX) in the 160 KiB
-#define CT_WRING_MIN 4
-#define CT_WRING_MAX 8
+#define CT_WRING_MIN 8
+#define CT_WRING_MAX 12
 static int g_tile_wlds = -1;      // -1: FN_TILE_WLDS (default on); 0 / 1 set by fn_conv_tile_set_wlds (tests)
 extern "C" void fn_conv_tile_set_wlds(int mode) { g_tile_wlds = mode < 0 ? -1 : (mode ? 1 : 0); }
 static int tile_wring(size_t lds, int NT) {
@@ -1258,7 +1301,7 @@ static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false,
 // wp: packed weights (fn_tile_pack_w) with PD zero k-steps past the last slice; rowtab:
 // int2[4 * MT * 16] (halo position of the row, natural tile row or -1); ktab: int4[nks + PD
 // + 2] byte offsets of the tap each lane group reads per k-step (zero past nks);
-// zp: >= 16 zero bytes; sched: int[64] zeroed counters (left zero); stats: fp32
+// zp: >= 16 zero bytes; sched: int[1 + 8 * column blocks] zeroed counters (left zero); stats: fp32
 // [fn_conv_tile_slab_rows][2][Ncol], or null.  bny (bnp null): the relu-mask bytes [output
 // positions][Ncol / 8] of the BN whose output this dgrad's conv consumed -- the epilogue's column
 // sums are of g = dx * mask (dx stored as is); stats required, act none.
@@ -1297,7 +1340,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   const size_t lds = tile_lds_total(g, MT, NT, false, Ncol, bny != nullptr);
   if (lds > 160 * 1024) return -4;
   const int ncb = (Ncol + NT * 16 - 1) / (NT * 16);
-  if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;
+  if (!sched || !zp || !ktab || ncb > 63 || ncb * NT > g.nct) return -6;   // (sched: int[1 + 8 * 63] and more)
   if (Ncol % 8 || ((act & 0xff) != ACT_NONE && (act & 0xff) != ACT_RELU)) return -2;   // 16-B column groups
   // oscale > 0: e4m3 output of y * oscale (no statistics; the 8-channel-slice instances: the
   // space-to-depth stem of the fp8 inference path)
@@ -1307,6 +1350,8 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   // (tests: a smaller grid must give the same bits -- only the dynamic schedules take it)
   if (g_tile_grid_cap > 0 && (!stats || tile_chunk(g) > 0)) grid.x = std::min<unsigned>(grid.x, g_tile_grid_cap);
   const int wring = (oscale > 0.f || osc) ? 0 : tile_wring(lds, NT);
+  static const bool wl_nowait = [] { const char* e = getenv("FN_TILE_WLDBG"); return e && atoi(e) == 1; }();
+  if (wring && wl_nowait) act |= 0x400;           // (timing only: the ring without its hand-off)
   int rc = -2;
 #ifdef FN_EXPERIMENTS
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();

@@ -469,7 +469,8 @@ def sched(device, stream: int) -> torch.Tensor:
     key = (str(device), stream)
     t = _SCHED.get(key)
     if t is None:
-        t = torch.zeros(64, dtype=torch.int32, device=device)
+        # (conv_tile's dynamic schedules: a done counter + 8 XCD queue counters per column block)
+        t = torch.zeros(1024, dtype=torch.int32, device=device)
         with _LOCK:
             _SCHED[key] = t
     return t

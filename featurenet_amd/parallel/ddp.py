@@ -128,6 +128,24 @@ def plan_buckets(sizes: list[int], cap: int, tail_cap: int | None = None) -> lis
     return out
 
 
+def use_chunked_tile_schedule(device) -> bool:
+    """Data parallelism: the conv kernels' BN-statistics launches take the chunked schedule
+    (``conv_tile.hip``: fixed chunks of tiles from XCD queues, one partial row per chunk -- the same
+    bits whatever workgroup ran what), which degrades gracefully while the RCCL rings of the
+    bucketed all-reduce hold CUs during backward; one GPU keeps the static schedule, the faster
+    one when a kernel has the GPU to itself (``profiles/r6_dp_interference.md``).  ``FN_TILE_SCHED``
+    set in the environment wins."""
+    if os.environ.get("FN_TILE_SCHED") or getattr(device, "type", "cpu") != "cuda":
+        return False
+    try:
+        from .. import _native
+
+        _native.kernels().conv_tile_set_schedule(1)
+        return True
+    except Exception:  # noqa: BLE001 - no kernel library (CPU): nothing to select
+        return False
+
+
 class GradBucketer:
     def __init__(self, flat: FlatParams, group=None, bucket_mb: float = 32.0, overlap: bool = True,
                  force: bool = False, tail_mb: float | None = 0.25):
@@ -162,6 +180,8 @@ class GradBucketer:
         self.works: list = []
         self.hooks = []
         self.n_collectives = 0
+        if self.active and self.world > 1:
+            use_chunked_tile_schedule(flat.data.device)
         if self.active and overlap:
             for p, _, _ in flat.slices:
                 self.hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))

@@ -224,6 +224,7 @@ def test_tile_statistics_do_not_depend_on_the_grid():
     x = (torch.rand(16, 64, 64, 64, 1, device=dev) < 0.3).to(torch.bfloat16)
     y = torch.randint(0, 24, (16,), device=dev)
     runs = []
+    K.conv_tile_set_schedule(1)                 # the chunked schedule (data parallelism's)
     try:
         for cap in (0, 37, 100):
             K.conv_tile_grid_cap(cap)
@@ -234,7 +235,35 @@ def test_tile_statistics_do_not_depend_on_the_grid():
             runs.append((loss.detach().clone(), _grads(model)))
     finally:
         K.conv_tile_grid_cap(0)
+        K.conv_tile_set_schedule(-1)
     _assert_same(runs)
+
+
+@pytest.mark.parametrize("sched", [0, 1])
+def test_both_tile_schedules_match_the_reference_statistics(sched):
+    """The static (1 GPU) and the chunked (data-parallel) schedules of conv_tile's BN-statistics
+    launches: forward BN statistics and the masked-dgrad column sums against fp32 sums of the
+    stored outputs (the two schedules add the same values in different orders)."""
+    from featurenet_amd.ops import conv_tile as ct
+    from featurenet_amd.ops.spec import ConvSpec
+
+    K = _native.kernels()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(18)
+    x = torch.randn(8, 25, 25, 25, 32, device=dev).to(torch.bfloat16)
+    spec = ConvSpec.make(x.shape, 64, 4, 1, "valid")
+    w = (torch.randn(64, 4, 4, 4, 32, device=dev) * 0.05).float()
+    K.conv_tile_set_schedule(sched)
+    try:
+        p = ct.fwd_plan(spec)
+        y, stats = ct.conv_fwd(x, w, None, spec, 0, True, p)
+        torch.cuda.synchronize()
+    finally:
+        K.conv_tile_set_schedule(-1)
+    yf = y.float().reshape(-1, 64)
+    s1, s2 = stats[:, 0].double().sum(0), stats[:, 1].double().sum(0)
+    assert torch.allclose(s1, yf.double().sum(0), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(s2, (yf.double() ** 2).sum(0), rtol=1e-4, atol=1e-2)
 
 
 def test_weight_ring_gives_the_register_path_bits():
