@@ -107,6 +107,7 @@ int fn_cast_f32_bf16(const float*, void*, long long, hipStream_t);
 int fn_scale_unless_one(void*, int, const float*, long long, hipStream_t);
 int fn_copy2(void*, const void*, long long, void*, const void*, long long, hipStream_t);
 int fn_cu_occupy(int, int, int, void*, hipStream_t);
+int fn_softmax_rows(const float*, float*, long long, int, int, const float*, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
                  const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float, void*);
@@ -802,6 +803,14 @@ PYBIND11_MODULE(_C, m) {
     chk(fn_softmax_xent_rows(P<const void*>(logits), in_bf16, P<const long long*>(labels), P<float*>(block_loss),
                              P<void*>(dlogits), P<int*>(correct), B, NC, gscale, smoothing, S(st)),
         "softmax_xent_rows");
+  });
+  m.def("softmax_rows", [](uintptr_t x, uintptr_t y, long long M, int N, int backward, uintptr_t g, uintptr_t st,
+                           std::vector<long long> ext) {
+    // forward: y = softmax(x) over rows of N fp32; backward (x = y, y = dx): dx = y * (g - sum g y)
+    fits(ext, 0, M * N, "softmax_rows", "x");
+    fits(ext, 1, M * N, "softmax_rows", "y");
+    if (backward) fits(ext, 2, M * N, "softmax_rows", "g");
+    chk(fn_softmax_rows(P<const float*>(x), P<float*>(y), M, N, backward, P<const float*>(g), S(st)), "softmax_rows");
   });
   m.def("cu_occupy", [](int nwg, int usec, int lds, uintptr_t sink, uintptr_t st) {
     // (measurement only: pins nwg CUs on the given stream for usec microseconds; sink >= 1 KB)

@@ -372,8 +372,10 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
     auto issue_w = [&]() {
       const unsigned char* src = wsrc + ((size_t)(wsl * nks + wk) * g.nct) * 1024;
       const unsigned dst = ring0 + (unsigned)wslot * WSLOT;
+      if (!(act & 0x800)) {                      // (0x800, timing only: no weight DMAs at all)
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) ct_glds16_s(src + nt * 1024, (unsigned)lane * 16u, dst + (unsigned)nt * 1024u);
+        for (int nt = 0; nt < NT; ++nt) ct_glds16_s(src + nt * 1024, (unsigned)lane * 16u, dst + (unsigned)nt * 1024u);
+      }
       ++qi;
       if (++wk == nks) {
         wk = 0;
@@ -767,8 +769,12 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
                 }
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt) fb[(u + 1) & 1][nt] = *(const Frag*)(rbase + so + nt * 1024);
-                if (u == PD - 1) st_cnt(s_wdone + wave, wq + 2);
-                wr_v = ld_cnt(s_wrdy);
+                if (u == PD - 1) {
+                  st_cnt(s_wdone + wave, wq + 2);
+                  // (once per turn, for the next turn's check: a count read every step would be dead
+                  // until overwritten, and the overwrite waits for it -- lgkmcnt(0) every step)
+                  wr_v = ld_cnt(s_wrdy);
+                }
               }
             }
             if constexpr (!(DBG & 128)) __builtin_amdgcn_sched_barrier(0);   // (DBG 128: free scheduling
@@ -1350,8 +1356,10 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   // (tests: a smaller grid must give the same bits -- only the dynamic schedules take it)
   if (g_tile_grid_cap > 0 && (!stats || tile_chunk(g) > 0)) grid.x = std::min<unsigned>(grid.x, g_tile_grid_cap);
   const int wring = (oscale > 0.f || osc) ? 0 : tile_wring(lds, NT);
-  static const bool wl_nowait = [] { const char* e = getenv("FN_TILE_WLDBG"); return e && atoi(e) == 1; }();
-  if (wring && wl_nowait) act |= 0x400;           // (timing only: the ring without its hand-off)
+  // (timing only: FN_TILE_WLDBG=1 the ring without its hand-off, 3 also without the weight DMAs)
+  static const int wl_dbg = [] { const char* e = getenv("FN_TILE_WLDBG"); return e ? atoi(e) : 0; }();
+  if (wring && (wl_dbg & 1)) act |= 0x400;
+  if (wring && (wl_dbg & 2)) act |= 0x800;
   int rc = -2;
 #ifdef FN_EXPERIMENTS
   static const int dbg = [] { const char* e = getenv("FN_TILE_DBG"); return e ? atoi(e) : 0; }();

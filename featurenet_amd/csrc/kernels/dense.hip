@@ -295,7 +295,7 @@ __global__ __launch_bounds__(DN_THREADS) void dense_dgrad_kernel(const bf16* __r
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (n >= N) {
       // zero rows of the padded k dimension
-    } else if (kk + 4 <= K) {
+    } else if (kk + 4 <= K && (K & 3) == 0) {   // (16-B aligned rows only)
       v = *(const float4*)(w + (long long)n * K + kk);
     } else {
       float t[4] = {0.f, 0.f, 0.f, 0.f};
@@ -554,7 +554,7 @@ static int dn_lds_attr(const void* fn, size_t lds) {
 // ya / act: see dense_dgrad_kernel (null: g is the gradient itself)
 extern "C" int fn_dense_dgrad(const void* g, const float* w, void* dx, int M, int N, int K, hipStream_t st,
                               const void* ya, int act) {
-  if (M <= 0 || K <= 0 || N <= 0 || K % 4) return -2;
+  if (M <= 0 || K <= 0 || N <= 0) return -2;   // (any K: rows of W and dx not 4-aligned go scalar)
   const size_t lds = (size_t)64 * (((N + 31) & ~31) + 8) * 2;
   if (lds > 160 * 1024) return -4;
   if (int e = dn_lds_attr((const void*)dense_dgrad_kernel, lds)) return e;

@@ -678,3 +678,61 @@ extern "C" int fn_cu_occupy(int nwg, int usec, int lds, void* sink, hipStream_t 
   FN_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Row softmax of fp32 rows (a Dense layer with a softmax activation inside a NAS candidate; the
+// classifier head's softmax lives in softmax_xent): one wave per row, 8 rows per 512-thread
+// block, any N (lanes stride the row); the backward dx = y * (g - sum(g * y)) the same way.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sm_wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float sm_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(512) void softmax_rows_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               long long M, int N) {
+  const long long m = (long long)blockIdx.x * 8 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (m >= M) return;
+  const float* xr = x + m * N;
+  float mx = -INFINITY;
+  for (int i = lane; i < N; i += 64) mx = fmaxf(mx, xr[i]);
+  mx = sm_wave_max(mx);
+  float s = 0.f;
+  for (int i = lane; i < N; i += 64) s += __expf(xr[i] - mx);
+  const float inv = 1.f / sm_wave_sum(s);
+  float* yr = y + m * N;
+  for (int i = lane; i < N; i += 64) yr[i] = __expf(xr[i] - mx) * inv;
+}
+
+__global__ __launch_bounds__(512) void softmax_rows_bwd_kernel(const float* __restrict__ y, const float* __restrict__ g,
+                                                               float* __restrict__ dx, long long M, int N) {
+  const long long m = (long long)blockIdx.x * 8 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (m >= M) return;
+  const float* yr = y + m * N;
+  const float* gr = g + m * N;
+  float s = 0.f;
+  for (int i = lane; i < N; i += 64) s += gr[i] * yr[i];
+  s = sm_wave_sum(s);
+  float* dr = dx + m * N;
+  for (int i = lane; i < N; i += 64) dr[i] = yr[i] * (gr[i] - s);
+}
+
+extern "C" int fn_softmax_rows(const float* x, float* y, long long M, int N, int backward, const float* g,
+                               hipStream_t st) {
+  if (M <= 0 || N <= 0 || (backward && !g)) return -2;
+  const dim3 grid((unsigned)((M + 7) / 8));
+  if (backward)
+    hipLaunchKernelGGL(softmax_rows_bwd_kernel, grid, dim3(512), 0, st, x, g, y, M, N);
+  else
+    hipLaunchKernelGGL(softmax_rows_fwd_kernel, grid, dim3(512), 0, st, x, y, M, N);
+  FN_CHECK_LAUNCH();
+  return 0;
+}

@@ -9,8 +9,9 @@ bias + activation in the split reduction, a dgrad and a weight-gradient kernel
 that writes the fp32 ``dW`` (and ``db``) straight into the parameters' flat
 gradients.  Any K / N / M: the kernels pad the MFMA dims with zeros and load unaligned rows
 element-wise; the weight gradient splits the batch into slices (own dW slabs, summed in a
-fixed order) so small dW matrices still fill the GPU.  Only dgrad with K % 4 != 0 falls back
-to hipBLASLt through torch.
+fixed order) so small dW matrices still fill the GPU.  A softmax activation (a Dense inside a
+NAS candidate) is a native row-softmax kernel with its own backward (``misc.hip``).  torch /
+hipBLASLt only with ``FN_DENSE_NATIVE=0`` (the A/B switch).
 """
 from __future__ import annotations
 
@@ -77,7 +78,8 @@ class LinearFn(torch.autograd.Function):
         g = dy.reshape(M, N).to(torch.bfloat16).contiguous()
         wf = w.detach()
         NP = -(-N // 32) * 32                          # (any N: the dgrad kernel pads its k dim to 32)
-        dgrad_native = _NATIVE and K % 4 == 0 and wf.dtype == torch.float32 and 64 * (NP + 8) * 2 <= 160 * 1024
+        # (any K: the kernel stages W rows and stores dx rows that are not 16-B aligned element by element)
+        dgrad_native = _NATIVE and wf.dtype == torch.float32 and 64 * (NP + 8) * 2 <= 160 * 1024
         # the activation backward inside the dgrad / wgrad kernels (g = dy * act'(y) as they load
         # it) when both run natively and the wgrad kernel produces db: no separate pass.  Small
         # layers only (K <= 4096): every dgrad / wgrad workgroup re-applies it to the g rows it
@@ -150,11 +152,35 @@ def linear_infer(x: torch.Tensor, w_bf16: torch.Tensor, b: torch.Tensor | None =
     return y.reshape(*x.shape[:-1], N)
 
 
+class SoftmaxRowsFn(torch.autograd.Function):
+    """softmax over the last axis of an fp32 tensor on the native row kernels (forward and backward)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N = x.shape[-1]
+        x2 = x.reshape(-1, N).contiguous()
+        y = torch.empty_like(x2)
+        _native.kernels().softmax_rows(x2.data_ptr(), y.data_ptr(), x2.shape[0], N, 0, 0, _native.stream(x2),
+                                       [x2.numel(), y.numel()])
+        ctx.save_for_backward(y)
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        N = y.shape[-1]
+        g2 = g.reshape(-1, N).float().contiguous()
+        dx = torch.empty_like(y)
+        _native.kernels().softmax_rows(y.data_ptr(), dx.data_ptr(), y.shape[0], N, 1, g2.data_ptr(),
+                                       _native.stream(y), [y.numel(), dx.numel(), g2.numel()])
+        return dx.reshape(g.shape)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act=None, out_fp32: bool = False):
     if _native.use_native(x):
         if act == "softmax":
             y = LinearFn.apply(x, w, b, 0, True)
-            return torch.softmax(y, dim=-1)
+            return SoftmaxRowsFn.apply(y)
         return LinearFn.apply(x, w, b, act_code(act), out_fp32)
     y = torch.nn.functional.linear(x, w.to(x.dtype), None if b is None else b.to(x.dtype))
     return ref.activation(y, act)
