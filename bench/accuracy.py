@@ -151,6 +151,8 @@ class OracleFeatureNet3D(torch.nn.Module):
     def forward(self, x):                              # x: [N, S, S, S, 1]
         F = torch.nn.functional
         h = x.permute(0, 4, 1, 2, 3)
+        if h.is_cuda:
+            h = h.contiguous(memory_format=torch.channels_last_3d)
         for i in range(len(self.w)):
             h = F.conv3d(h, self.w[i].to(h.dtype) if h.dtype != torch.float32 else self.w[i], stride=self.strides[i])
             mom, eps = self.bn[i]
@@ -174,6 +176,10 @@ def torch_oracle(a) -> None:
     from featurenet_amd.training.data import DeviceLoader, voxel_dataset
 
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    # MIOpen find mode (time the solvers once per shape, keep the fastest) and channels-last 3-D
+    # tensors: without them stock PyTorch runs MIOpen's fallback 3-D kernels (~100 samples/s,
+    # bench.py --impl torch); the math is the same
+    torch.backends.cudnn.benchmark = True
     t0 = time.time()
     ds = voxel_dataset(a.train_per_class * a.classes, a.test_per_class * a.classes, size=a.size,
                        num_classes=a.classes, seed=a.seed)
@@ -181,6 +187,9 @@ def torch_oracle(a) -> None:
     torch.manual_seed(a.seed)                           # the native api.train's initial weights
     native = FeatureNet3D(FeatureNet3DConfig(input_size=a.size, num_classes=a.classes))
     model = OracleFeatureNet3D(native).to(dev)
+    if dev.type == "cuda":
+        for w in model.w:
+            w.data = w.data.contiguous(memory_format=torch.channels_last_3d)
     params = [p for p in model.parameters()]
     m = [torch.zeros_like(p) for p in params]
     v = [torch.zeros_like(p) for p in params]
@@ -226,10 +235,12 @@ def torch_oracle(a) -> None:
         loader.set_epoch(epoch)
         te = time.time()
         lsum, hits, seen = 0.0, 0, 0
-        for xb, yb in loader:
+        for bi, (xb, yb) in enumerate(loader):
             with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=amp):
                 lg = model(prep(xb)).float()
             loss = torch.nn.functional.cross_entropy(lg, yb)
+            if bi % 40 == 0:                             # (progress: a long epoch stays visibly alive)
+                print(f"  epoch {epoch + 1} batch {bi}", flush=True)
             for p in params:
                 p.grad = None
             loss.backward()

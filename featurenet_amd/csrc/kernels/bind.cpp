@@ -110,7 +110,8 @@ int fn_cu_occupy(int, int, int, void*, hipStream_t);
 int fn_softmax_rows(const float*, float*, long long, int, int, const float*, hipStream_t);
 int fn_unpack_bits(const void*, void*, long long, hipStream_t);
 int fn_conv_tile(const void*, const void*, const void*, const void*, const void*, const float*, void*, float*,
-                 const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float, void*);
+                 const int*, int, int, int, int, int*, hipStream_t, const void*, const float*, float, void*,
+                 const float*, void*, void*, int);
 int fn_conv_tile_workers(const int*, int, int);
 int fn_conv_tile_slab_rows(const int*, int, int);
 void fn_conv_tile_grid_cap(int);
@@ -122,7 +123,7 @@ int fn_conv_tile_f8(const void*, const void*, const void*, const void*, const vo
                     float, const int*, int, int, int, int, int*, hipStream_t, const void*, void*);
 int fn_conv_tile_f8_supported(int, int, int);
 int fn_conv_wtile(const void*, const void*, float*, float*, const void*, const void*, const void*, const int*, int, int,
-                  int*, hipStream_t, const float*, float*);
+                  int*, hipStream_t, const float*, float*, const float*, int);
 int fn_conv_wtile_supported(int, int);
 int fn_tile_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int fn_tile_pack_w2(const float*, void*, void*, int, int, int, const int*, const int*, hipStream_t);
@@ -262,7 +263,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_tile", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp, uintptr_t bias,
                         uintptr_t out, uintptr_t stats, std::vector<int> geom, int ncol, int act, int MT, int NT,
                         uintptr_t sched, uintptr_t st, std::vector<long long> ext, uintptr_t bny, uintptr_t bnp,
-                        float oscale, uintptr_t osc, long long osc_n) {
+                        float oscale, uintptr_t osc, long long osc_n, uintptr_t pst, uintptr_t pz, uintptr_t pmask,
+                        int pact, std::vector<long long> pext) {
     need(geom, 31, "conv_tile");
     check_tile(geom, ext, ncol, MT, "conv_tile", NT);
     // osc: block scales of an e4m3 output, one dword per output position
@@ -273,15 +275,25 @@ PYBIND11_MODULE(_C, m) {
     } else if (bny) {   // the relu-mask bytes: ext[5] = their count (one per 8 output columns)
       fits(ext, 5, view_extent(geom, ncol) / 8, "conv_tile", "mask");
     }
+    // the BN prologue: pext = {pst, pz, pmask} element counts -- [scale C][shift C] of the source's
+    // channels, z of the source's shape, one mask byte per 8 source elements
+    if (pst) {
+      if (pext.size() < 3) throw std::runtime_error("conv_tile: the BN prologue needs pext = {pst, pz, pmask}");
+      const long long nsrc = prod({geom[0], geom[1], geom[2], geom[3], geom[4]});
+      fits(pext, 0, 2LL * geom[4], "conv_tile", "pst");
+      if (pz) fits(pext, 1, nsrc, "conv_tile", "pz");
+      if (pmask) fits(pext, 2, nsrc / 8, "conv_tile", "pmask");
+    }
     chk(fn_conv_tile(P<const void*>(src), P<const void*>(wpk), P<const void*>(rowtab), P<const void*>(ktab),
                      P<const void*>(zp), P<const float*>(bias), P<void*>(out), P<float*>(stats), geom.data(), ncol,
                      act, MT, NT, P<int*>(sched), S(st), P<const void*>(bny), P<const float*>(bnp), oscale,
-                     P<void*>(osc)),
+                     P<void*>(osc), P<const float*>(pst), P<void*>(pz), P<void*>(pmask), pact),
         "conv_tile");
   }, py::arg("src"), py::arg("wpk"), py::arg("rowtab"), py::arg("ktab"), py::arg("zp"), py::arg("bias"), py::arg("out"),
      py::arg("stats"), py::arg("geom"), py::arg("ncol"), py::arg("act"), py::arg("MT"), py::arg("NT"),
      py::arg("sched"), py::arg("st"), py::arg("ext") = std::vector<long long>(), py::arg("bny") = 0,
-     py::arg("bnp") = 0, py::arg("oscale") = 0.f, py::arg("osc") = 0, py::arg("osc_n") = 0);
+     py::arg("bnp") = 0, py::arg("oscale") = 0.f, py::arg("osc") = 0, py::arg("osc_n") = 0, py::arg("pst") = 0,
+     py::arg("pz") = 0, py::arg("pmask") = 0, py::arg("pact") = 0, py::arg("pext") = std::vector<long long>());
   m.def("conv_tile_f8", [](uintptr_t src, uintptr_t wpk, uintptr_t rowtab, uintptr_t ktab, uintptr_t zp,
                            uintptr_t scale, uintptr_t bias, uintptr_t out, float oscale, std::vector<int> geom, int ncol,
                            int relu, int MT, int NT, uintptr_t st, uintptr_t sched, std::vector<long long> ext,
@@ -309,8 +321,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_tile_f8_supported", &fn_conv_tile_f8_supported);
   m.def("conv_wtile", [](uintptr_t x, uintptr_t dy, uintptr_t dw, uintptr_t part, uintptr_t rowtab, uintptr_t postab,
                          uintptr_t zp, std::vector<int> geom, int nacc, int workers, uintptr_t sched, uintptr_t st,
-                         std::vector<long long> ext, uintptr_t wsrc, uintptr_t wdp) {
+                         std::vector<long long> ext, uintptr_t wsrc, uintptr_t wdp, uintptr_t pst, int pact) {
     need(geom, 24, "conv_wtile");
+    // the BN prologue: pst = [scale C][shift C] of x's channels (ext[8] = its element count)
+    if (pst) fits(ext, 8, 2LL * geom[4], "conv_wtile", "pst");
     const long long T = (long long)geom[9] * geom[10] * geom[11];
     fits(ext, 0, prod({geom[0], geom[1], geom[2], geom[3], geom[4]}), "conv_wtile", "x");
     const bool sp = (nacc >> 14) & 1;             // sub-pixel form: dy = [N, OD+1, OH+1, OW+1, 8 K]
@@ -331,11 +345,12 @@ PYBIND11_MODULE(_C, m) {
       throw std::runtime_error("conv_wtile: output larger than the padded input");
     chk(fn_conv_wtile(P<const void*>(x), P<const void*>(dy), P<float*>(dw), P<float*>(part), P<const void*>(rowtab),
                       P<const void*>(postab), P<const void*>(zp), geom.data(), nacc, workers, P<int*>(sched), S(st),
-                      P<const float*>(wsrc), P<float*>(wdp)),
+                      P<const float*>(wsrc), P<float*>(wdp), P<const float*>(pst), pact),
         "conv_wtile");
   }, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("part"), py::arg("rowtab"), py::arg("postab"), py::arg("zp"),
      py::arg("geom"), py::arg("nacc"), py::arg("workers"), py::arg("sched"), py::arg("st"),
-     py::arg("ext") = std::vector<long long>(), py::arg("wsrc") = 0, py::arg("wdp") = 0);
+     py::arg("ext") = std::vector<long long>(), py::arg("wsrc") = 0, py::arg("wdp") = 0, py::arg("pst") = 0,
+     py::arg("pact") = 0);
   m.def("conv_wtile_supported", &fn_conv_wtile_supported);
   m.def("conv_tile_workers", [](std::vector<int> geom, int ncol, int NT) {
     need(geom, 31, "conv_tile_workers");

@@ -91,7 +91,9 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
                                                                const unsigned char* __restrict__ gmask,
                                                                const unsigned* __restrict__ xsc,
                                                                unsigned char* __restrict__ osc, int chunk,
-                                                               int wring) {
+                                                               int wring, const float* __restrict__ pst,
+                                                               bf16* __restrict__ pz,
+                                                               unsigned char* __restrict__ pmask, int pact) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   static_assert(!BS || F8 || Q8O, "block scales: fp8 operands or an e4m3 output");
   constexpr int NTHR = 64 * (NCW + 1);
@@ -260,6 +262,73 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
     }
   };
 
+  // BN prologue (pst != null; bf16 forward only, host-checked): the source is the PREVIOUS layer's
+  // pre-BN output y, and the layer's input is z = act(y * scale + shift) per input channel
+  // (pst = [scale C][shift C]).  Once a job's halo has landed the loader rewrites it in LDS as z --
+  // the same fma, activation and bf16 rounding as bn_apply_kernel, so the conv sees the same bits --
+  // leaving the zero page's padding positions alone (the conv pads z, not y), and for the positions
+  // the tile OWNS (per dimension the input rows [t*T - pad, (t+1)*T - pad) of output tile t, the
+  // last tile also everything past them: every input position has exactly one owner) the first
+  // column block also writes z (pz, for the weight gradient) and the relu-mask byte of each 8
+  // channels (pmask, bit j = z_j > 0: the statistics identity of the backward, ops/bnfuse.py).
+  // bn_apply's separate pass over y -- and its re-read of y here -- disappears.
+  auto xform_job = [&](int tile, int slice, int bufoff) {
+    if constexpr (!F8) {
+      if (!pst) return;
+      int t = __builtin_amdgcn_readfirstlane(tile);
+      const int tw_ = t % twn; t /= twn;
+      const int th_ = t % thn; t /= thn;
+      const int td_ = t % tdn;
+      const int n = t / tdn;
+      const int dlo = td_ * g.TD - g.pd, hlo = th_ * g.TH - g.ph, wlo = tw_ * g.TW - g.pw;
+      const int HD = g.TD + g.KD - 1;
+      const bool interior = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + HD <= g.ID && hlo + HH <= g.IH &&
+                            wlo + HW <= g.IW;
+      // owned halo rows per dimension: [0, T) (all of them for the last tile)
+      const int od = td_ == tdn - 1 ? 255 : g.TD, oh = th_ == thn - 1 ? 255 : g.TH, ow = tw_ == twn - 1 ? 255 : g.TW;
+      const bool writer = blockIdx.y == 0 && (pz || pmask);
+      const long long nbase = (long long)n * g.ID * g.IH * g.IW;
+      unsigned char* buf = dsm + bufoff + lane * 16;
+#pragma unroll 1
+      for (int c = 0; c < CPP; ++c) {
+        const int ch0 = __builtin_amdgcn_readfirstlane(slice * g.CS + c * 8);
+        float sc[8], sh[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sc[j] = pst[ch0 + j];
+          sh[j] = pst[g.C + ch0 + j];
+        }
+#pragma unroll 2
+        for (int r = 0; r < (g.HPpad >> 6); ++r) {
+          const int p = (r << 6) + lane;
+          const int e = s_pos[p].y;
+          const int hd = e >> 16, hh = (e >> 8) & 255, hw = e & 255;
+          const int gd = dlo + hd, gh = hlo + hh, gw = wlo + hw;
+          const bool ok = interior || ((unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                                       (unsigned)gw < (unsigned)g.IW);
+          unsigned char* a = buf + c * PLANE + (r << 10);
+          const uint4 v = *(const uint4*)a;
+          const unsigned vi[4] = {v.x, v.y, v.z, v.w};
+          unsigned o[4], bits = 0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = act_fwd(__builtin_fmaf(bf16_lo(vi[q]), sc[2 * q], sh[2 * q]), pact);
+            const float hi = act_fwd(__builtin_fmaf(bf16_hi(vi[q]), sc[2 * q + 1], sh[2 * q + 1]), pact);
+            bits |= (lo > 0.f ? 1u : 0u) << (2 * q);
+            bits |= (hi > 0.f ? 1u : 0u) << (2 * q + 1);
+            o[q] = bf16x2_pack(lo, hi);
+          }
+          if (ok) *(uint4*)a = make_uint4(o[0], o[1], o[2], o[3]);
+          if (writer && ok && p < HP && hd < od && hh < oh && hw < ow) {
+            const long long pos = nbase + ((long long)gd * g.IH + gh) * g.IW + gw;
+            if (pz) *(uint4*)(pz + pos * g.C + ch0) = make_uint4(o[0], o[1], o[2], o[3]);
+            if (pmask) pmask[pos * (g.C >> 3) + (ch0 >> 3)] = (unsigned char)bits;
+          }
+        }
+      }
+    }
+  };
+
   // DBG & 16: cycle stamps of wave 0 and the loader (barrier-A wait, job work, tile end)
   long long st_a = 0, st_k = 0, st_e = 0, st_0 = 0, st_1 = 0;
   auto stamp = [&]() -> long long { return (DBG & 16) ? (long long)__builtin_amdgcn_s_memtime() : 0; };
@@ -394,6 +463,33 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) st_cnt(s_wrdy, qi);
     };
+    // Turns stay in flight while the next one is issued: DMA instructions issued so far (nis:
+    // weights and halo rows; anything uncounted only lengthens a wait below), and for the last
+    // three issued batches the step count and nis right after them (uniform shift registers).
+    // Publishing batch b waits vmcnt(DMAs issued after it) -- the newer batches stay in flight.
+    int nis = 0, nfl = 0;                        // (nfl: batches in flight, <= 3)
+    int bq0 = 0, bq1 = 0, bq2 = 0, bn0 = 0, bn1 = 0, bn2 = 0;   // [0] = the oldest in flight
+    auto wait_vm = [&](int n) {                  // s_waitcnt vmcnt(n), n rounded down to a multiple of 4
+      switch (min(n, 60) >> 2) {
+#define CT_VMW(k) case k: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * k) : "memory"); break;
+        CT_VMW(0) CT_VMW(1) CT_VMW(2) CT_VMW(3) CT_VMW(4) CT_VMW(5) CT_VMW(6) CT_VMW(7)
+        CT_VMW(8) CT_VMW(9) CT_VMW(10) CT_VMW(11) CT_VMW(12) CT_VMW(13) CT_VMW(14)
+        default: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+#undef CT_VMW
+      }
+    };
+    auto push_batch = [&]() {                    // a batch just issued (qi, nis after it)
+      if (nfl == 0) { bq0 = qi; bn0 = nis; }
+      else if (nfl == 1) { bq1 = qi; bn1 = nis; }
+      else { bq2 = qi; bn2 = nis; }
+      ++nfl;
+    };
+    auto publish_oldest = [&]() {                // the oldest batch in flight has landed
+      wait_vm(nis - bn0);
+      if (lane == 0) st_cnt(s_wrdy, bq0);
+      bq0 = bq1; bn0 = bn1; bq1 = bq2; bn1 = bn2;
+      --nfl;
+    };
     if (tile >= 0) {
       dma_job(tile, 0, 0);
       if (nslice == 1) dma_mask(tile, 0);
@@ -425,12 +521,11 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
         nslc = 0;
         ntile = stat_chunk ? next_tile(kjob) : t_next;
       }
-      const int nfl = flush_of(ntile, nslc);
-      fl_cur = nfl;
+      fl_cur = flush_of(ntile, nslc);
       if (lane == 0) {
         s_job[4 * (par ^ 1)] = ntile;
         s_job[4 * (par ^ 1) + 1] = nslc;
-        s_job[4 * (par ^ 1) + 2] = nfl;
+        s_job[4 * (par ^ 1) + 2] = fl_cur;
       }
       // this period: job jcur's steps (and the compute waves' read-ahead of the next job's first)
       // must all be issued before barrier A(jcur + 1), and the next job's first turn too, so it
@@ -448,20 +543,28 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
           const int n = min(lim - qi, PD);
           for (int b = 0; b < n; ++b) {
             issue_w();
+            nis += NT;
             if (hr < NR) {
               dma_job_rows(ntile, nslc, bo, hr, hr + 1);
+              nis += CPP;
               ++hr;
             }
           }
-          publish();
+          push_batch();
+          if (nfl > 2) publish_oldest();         // (two batches stay in flight)
           guard = 0;
           continue;
         }
         if (hr < NR) {                           // no credit yet: halo rows
           for (int b = 0; b < 2 && hr < NR; ++b) {
             dma_job_rows(ntile, nslc, bo, hr, hr + 1);
+            nis += CPP;
             ++hr;
           }
+          continue;
+        }
+        if (nfl > 0) {                           // nothing to issue: the oldest batch lands
+          publish_oldest();
           continue;
         }
         // the job's steps and the next job's first turn issued and landed: on to the barrier (the
@@ -501,6 +604,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       ++kjob;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tile >= 0) xform_job(tile, 0, 0);
     int par = 0;
     int fl_prev = -1;                            // flush (chunk id) of the job before the current one
     int fl_cur = __builtin_amdgcn_readfirstlane(s_job[2]);
@@ -543,6 +647,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
         ++kjob;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (ntile >= 0) xform_job(ntile, nslc, (par ^ 1) * g.BUF);
       lap(st_k);
       tile = ntile;
       slice = nslc;
@@ -1255,7 +1360,8 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
                        float oscale = 0.f, const void* gmask = nullptr, const void* xsc = nullptr,
-                       void* osc = nullptr, int chunk = 0, int wring = 0) {
+                       void* osc = nullptr, int chunk = 0, int wring = 0, const float* pst = nullptr,
+                       void* pz = nullptr, void* pmask = nullptr, int pact = 0) {
   static size_t configured = 0;
   if (lds > configured) {
     hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW, WL>,
@@ -1266,18 +1372,19 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
   hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW, WL>), grid, dim3(64 * (NCW + 1)), lds,
                      st, (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act,
                      sched, stamps, scale, oscale, (const unsigned char*)gmask, (const unsigned*)xsc,
-                     (unsigned char*)osc, chunk, wring);
+                     (unsigned char*)osc, chunk, wring, pst, (bf16*)pz, (unsigned char*)pmask, pact);
   return 0;
 }
 
-// The LDS weight ring (conv_tile_kernel WL): on unless FN_TILE_WLDS=0, for the bf16 instances whose
+// The LDS weight ring (conv_tile_kernel WL): off unless FN_TILE_WLDS=1 (measured slower than the
+// register path, profiles/r6_weight_ring.md), for the bf16 instances whose
 // plan leaves room for at least CT_WRING_MIN k-step slots (up to CT_WRING_MAX) in the 160 KiB
 #define CT_WRING_MIN 8
 #define CT_WRING_MAX 12
-static int g_tile_wlds = -1;      // -1: FN_TILE_WLDS (default on); 0 / 1 set by fn_conv_tile_set_wlds (tests)
+static int g_tile_wlds = -1;      // -1: FN_TILE_WLDS (default off); 0 / 1 set by fn_conv_tile_set_wlds (tests)
 extern "C" void fn_conv_tile_set_wlds(int mode) { g_tile_wlds = mode < 0 ? -1 : (mode ? 1 : 0); }
 static int tile_wring(size_t lds, int NT) {
-  static const bool env_on = [] { const char* e = getenv("FN_TILE_WLDS"); return !(e && atoi(e) == 0); }();
+  static const bool env_on = [] { const char* e = getenv("FN_TILE_WLDS"); return e && atoi(e) == 1; }();
   const bool on = g_tile_wlds < 0 ? env_on : g_tile_wlds == 1;
   if (!on || lds >= 160 * 1024) return 0;
   const int r = (int)std::min<size_t>(CT_WRING_MAX, (160 * 1024 - lds) / ((size_t)NT * 1024));
@@ -1316,7 +1423,7 @@ static size_t tile_lds_total(const TileGeom& g, int MT, int NT, bool f8 = false,
 extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab, const void* ktab, const void* zp,
                             const float* bias, void* out, float* stats, const int* geom, int Ncol, int act, int MT,
                             int NT, int* sched, hipStream_t st, const void* bny, const float* bnp, float oscale,
-                            void* osc) {
+                            void* osc, const float* pst, void* pz, void* pmask, int pact) {
   const TileGeom g = parse_tile(geom);
   if (g.CS != 8 && g.CS != 16 && g.CS != 32 && g.CS != 64) return -2;
   const int CPP = g.CS / 8;
@@ -1352,10 +1459,13 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   // space-to-depth stem of the fp8 inference path)
   if (!(oscale >= 0.f) || (oscale > 0.f && (stats || NT != 2 || CPP != 1))) return -2;
   if (osc && (oscale <= 0.f || Ncol > 128)) return -2;
+  // the BN prologue: a bf16 forward (no relu-mask dgrad, no fp8 output), z none / relu
+  if (pst && (bny || oscale != 0.f || osc || (pact != ACT_NONE && pact != ACT_RELU))) return -2;
+  if (!pst && (pz || pmask)) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   // (tests: a smaller grid must give the same bits -- only the dynamic schedules take it)
   if (g_tile_grid_cap > 0 && (!stats || tile_chunk(g) > 0)) grid.x = std::min<unsigned>(grid.x, g_tile_grid_cap);
-  const int wring = (oscale > 0.f || osc) ? 0 : tile_wring(lds, NT);
+  const int wring = (oscale > 0.f || osc || pst) ? 0 : tile_wring(lds, NT);   // (the ring's loader: no prologue)
   // (timing only: FN_TILE_WLDBG=1 the ring without its hand-off, 3 also without the weight DMAs)
   static const int wl_dbg = [] { const char* e = getenv("FN_TILE_WLDBG"); return e ? atoi(e) : 0; }();
   if (wring && (wl_dbg & 1)) act |= 0x400;
@@ -1411,7 +1521,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
                                : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,       \
                                                       (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched,    \
                                                       nullptr, nullptr, 0.f, bny, nullptr, nullptr,                    \
-                                                      stats ? tile_chunk(g) : 0));
+                                                      stats ? tile_chunk(g) : 0, 0, pst, pz, pmask, pact));
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;

@@ -72,7 +72,8 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
                                                                 const int2* __restrict__ rowtab,
                                                                 const int* __restrict__ postab,
                                                                 const bf16* __restrict__ zp, WGeom g,
-                                                                int* __restrict__ sched, int dbg) {
+                                                                int* __restrict__ sched, int dbg,
+                                                                const float* __restrict__ pst, int pact) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   constexpr int CO = MT * 16;
   // SP: the sub-pixel (upsample x2 + 3^3 conv) weight gradient.  Rows are low-resolution
@@ -292,6 +293,54 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
     }
   };
 
+  // BN prologue (pst != null; 16-channel slices of a plain conv, host-checked): x is the previous
+  // layer's pre-BN output y and the conv's input is z = act(y * scale + shift) (pst = [scale C]
+  // [shift C]) -- the forward's conv_tile loader normalised its halos the same way and never wrote
+  // z.  Whoever DMA'd a job's x slots rewrites them in LDS once they have landed (the loader, or
+  // in the loaderless form each wave its own 1/NW), with bn_apply_kernel's fma, activation and
+  // rounding; zero-page slots (padding) stay zero.
+  auto xform_x = [&](int tile, int bufoff, int first, int step) {
+    if constexpr (!SP && !C8) {
+      if (!pst) return;
+      tile = __builtin_amdgcn_readfirstlane(tile);
+      int n, d0, h0, w0;
+      decode(tile, n, d0, h0, w0);
+      const int dlo = d0 - g.pd, hlo = h0 - g.ph, wlo = w0 - g.pw;
+      const bool x_in = dlo >= 0 && hlo >= 0 && wlo >= 0 && dlo + g.TD + g.KD - 1 <= g.ID && hlo + HH <= g.IH &&
+                        wlo + HW <= g.IW;
+      const int nx = (g.HPpad * XR) >> 10;
+      const int ch0 = slice * 16 + (lane & 1) * 8;   // (a lane's slots: one 8-channel half)
+      float sc[8], sh[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[j] = pst[ch0 + j];
+        sh[j] = pst[g.C + ch0 + j];
+      }
+      unsigned char* buf = dsm + bufoff + lane * 16;
+#pragma unroll 2
+      for (int j = first; j < nx; j += step) {
+        const int e = s_pos[(64 * j + lane) >> 1];
+        const int gd = dlo + (e >> 16), gh = hlo + ((e >> 8) & 255), gw = wlo + (e & 255);
+        const bool ok = e >= 0 && (x_in || ((unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                                            (unsigned)gw < (unsigned)g.IW));
+        unsigned char* a = buf + (j << 10);
+        const uint4 v = *(const uint4*)a;
+        const unsigned vi[4] = {v.x, v.y, v.z, v.w};
+        unsigned o[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const float lo = act_fwd(__builtin_fmaf(__uint_as_float(vi[qq] << 16), sc[2 * qq], sh[2 * qq]), pact);
+          const float hi = act_fwd(__builtin_fmaf(__uint_as_float(vi[qq] & 0xffff0000u), sc[2 * qq + 1], sh[2 * qq + 1]),
+                                   pact);
+          typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+          const bf2_t pk = {f2bf(lo), f2bf(hi)};
+          o[qq] = __builtin_bit_cast(unsigned, pk);
+        }
+        if (ok) *(uint4*)a = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  };
+
   if constexpr (!HAS_LOADER) {                  // job 0, 1/NW of it by each wave
     const int t0 = tile_of(0);
     if (t0 >= 0) {
@@ -308,6 +357,7 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
       dma_dy(cur, 0, 0, 1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (cur >= 0) xform_x(cur, 0, 0, 1);
     int par = 0, j = 0;
     while (true) {
       tile_lds_barrier();                        // A(j): job j's buffer landed, the other is free
@@ -318,6 +368,7 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
         if (!(dbg & 1)) dma_x(nxt, (par ^ 1) * g.BUF, 0, 1);   // (dbg 1: timing only, stale data)
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (nxt >= 0 && !(dbg & 1)) xform_x(nxt, (par ^ 1) * g.BUF, 0, 1);
       if (lane == 0) s_job[(j + 2) % 3] = t2;
       cur = nxt;
       nxt = t2;
@@ -392,6 +443,10 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   };
   auto start_job = [&]() -> bool {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of the job about to start
+    if constexpr (!HAS_LOADER) {                 // (this wave's x slots of it: the BN prologue)
+      const int tj = tile_of(jc);
+      if (tj >= 0 && !(dbg & 1)) xform_x(tj, par * g.BUF, wave, NW);
+    }
     tile_lds_barrier();                          // A
     const int tile = HAS_LOADER ? __builtin_amdgcn_readfirstlane(s_job[jc % 3]) : tile_of(jc);
     if (tile < 0) return false;
@@ -699,7 +754,7 @@ extern "C" int fn_conv_wtile_supported(int K, int nacc) {
 // (fn_part_reduce_wdot)
 extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* part, const void* rowtab,
                              const void* postab, const void* zp, const int* geom, int nacc, int workers, int* sched,
-                             hipStream_t st, const float* wsrc, float* wdp) {
+                             hipStream_t st, const float* wsrc, float* wdp, const float* pst, int pact) {
   const WGeom g = parse_wgeom(geom);
   // nacc | (8 << 8): the loaderless 8-wave variant; | (1 << 12): its 8-input-channel form;
   // | (1 << 13): k-steps split between the wave halves; | (1 << 14): the sub-pixel form
@@ -708,6 +763,8 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
   const bool c8 = ((nacc >> 12) & 1) != 0, ks2 = ((nacc >> 13) & 1) != 0, sp = ((nacc >> 14) & 1) != 0;
   const int nw = ((nacc >> 8) & 15) == 8 ? 8 : 4;
   if (!fn_conv_wtile_supported(g.K, nacc)) return -2;
+  // the BN prologue (x = pre-BN y; pst = [scale C][shift C]): 16-channel slices only, act none / relu
+  if (pst && (c8 || sp || (pact != ACT_NONE && pact != ACT_RELU))) return -2;
   nacc &= 255;
   const int xr = c8 ? 16 : 32, tpf = c8 ? 2 : 1;
   if ((c8 ? g.C != 8 : g.C % (sp ? 32 : 16)) || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;
@@ -742,7 +799,7 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
     }                                                                                                          \
     hipLaunchKernelGGL((conv_wtile_kernel<M, A, W, C, S, P>), dim3(grid), dim3(wt_nthr(W)), lds, st,           \
                        (const bf16*)x, (const bf16*)dy, part, (const int2*)rowtab, (const int*)postab,         \
-                       (const bf16*)zp, g, sched, dbg);                                                        \
+                       (const bf16*)zp, g, sched, dbg, pst, pact);                                             \
   }
   WT_CASE(1, 16, 4, false, false, false)
   WT_CASE(2, 8, 4, false, false, false)

@@ -95,8 +95,11 @@ class FeatureNet3D(nn.Module):
     def features(self, x: torch.Tensor) -> torch.Tensor:
         if x.dim() == 4:  # [N, D, H, W] occupancy -> add channel axis
             x = x.unsqueeze(-1)
-        for c in self.convs:
-            x = c(x)
+        n = len(self.convs)
+        for i, c in enumerate(self.convs):
+            # (each BN + ReLU output but the last feeds only the next conv: that conv's forward
+            # kernel normalises its input halo itself and writes it, ops/bnfuse.py defer)
+            x = c(x, conv_next=i < n - 1)
         return x
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -150,8 +153,8 @@ class FeatureNet3DSeg(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.dim() == 4:
             x = x.unsqueeze(-1)
-        for c in self.enc:
-            x = c(x)
+        for i, c in enumerate(self.enc):
+            x = c(x, conv_next=i < len(self.enc) - 1)
         return self._decode(x)
 
     def _decode(self, x: torch.Tensor) -> torch.Tensor:
@@ -185,8 +188,8 @@ class FeatureNet3DSeg(nn.Module):
         d, h = self.dec, self.head
         if self.training:
             z = x
-            for c in self.enc:
-                z = c(z)
+            for i, c in enumerate(self.enc):
+                z = c(z, conv_next=i < len(self.enc) - 1)
             if subpixel.gpu_ok(z, d.cout, z.shape[-1]) and bn_ops.fused_pointwise_ok(z, d.cout, h.cout, d.act) \
                     and subpixel.xent_ok(d.cout, h.cout):
                 loss, hits = subpixel.decoder_head_xent(z, d.weight, d.gamma, d.beta, d.running_mean, d.running_var,

@@ -76,7 +76,9 @@ class Conv(nn.Module):
             self._spec_cache[shape5] = s
         return s
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, conv_next: bool = False) -> torch.Tensor:
+        """``conv_next``: the output goes to one following Conv and nowhere else, so a BN + act
+        output may be left to that conv's forward kernel to write (ops/bn.py ``batchnorm_act``)."""
         in_shape = x.shape
         x5 = x.reshape(to5d_shape(in_shape))
         cs, ps = self.specs(tuple(x5.shape))
@@ -97,7 +99,8 @@ class Conv(nn.Module):
                                              self.act, stats_slab=slab)
             else:
                 out = ops.batchnorm_act(y, self.gamma, self.beta, self.running_mean, self.running_var,
-                                        self.training, self.bn_momentum, self.bn_eps, self.act, stats_slab=slab)
+                                        self.training, self.bn_momentum, self.bn_eps, self.act, stats_slab=slab,
+                                        conv_next=conv_next)
         else:
             out = ops.conv(x5, self.weight, self.bias, cs, self.act)
             if ps is not None:

@@ -123,7 +123,7 @@ def _bwd_input(dz2, y2, prm, dbeta, dgamma, act, training):
 
 class BatchNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, gamma, beta, slab, rmean, rvar, training, momentum, eps, act, tag=False):
+    def forward(ctx, y, gamma, beta, slab, rmean, rvar, training, momentum, eps, act, tag=False, lazy=False):
         C = y.shape[-1]
         y2 = y.reshape(-1, C)
         if training:
@@ -137,8 +137,17 @@ class BatchNormActFn(torch.autograd.Function):
         # dgrad applies them, so the backward needs no colstats pass
         mask = (torch.empty(y2.numel() // 8, dtype=torch.uint8, device=y.device)
                 if tag and bnfuse.identity_ok(C, act) else None)
-        _native.kernels().bn_apply(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), z.data_ptr(), y2.numel(), C,
-                                   act, _native.stream(y), _native.ptr(mask), 0 if mask is None else mask.numel())
+
+        def fill():
+            _native.kernels().bn_apply(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), z.data_ptr(), y2.numel(),
+                                       C, act, _native.stream(y), _native.ptr(mask), 0 if mask is None else mask.numel())
+
+        if lazy and act in (0, 1) and C % 8 == 0 and bnfuse.prologue_enabled():
+            # the caller's next op is a conv: its conv_tile loader applies BN + act to y's halo and
+            # writes z and the mask (ops/bnfuse.py defer / settle), else ``fill`` runs there
+            bnfuse.defer(z, y, prm, act, mask, fill)
+        else:
+            fill()
         if tag and act in (0, 1):                # none / relu: the dgrad epilogue's forms
             bnfuse.tag_output(z, y, prm, act, mask)
         ctx.mask = mask                          # (alive until the backward: the conv's dgrad reads it)
@@ -159,7 +168,7 @@ class BatchNormActFn(torch.autograd.Function):
         if isinstance(part, tuple) and ctx.needs_input_grad[0]:
             dy, dbeta, dgamma = _bwd_identity(dz2, y2, prm, *ctx.params, gslab=part[1], wpart=part[2])
             return (dy.reshape(y.shape), dgamma if ctx.has_gamma else None, dbeta if ctx.has_beta else None,
-                    None, None, None, None, None, None, None, None)
+                    None, None, None, None, None, None, None, None, None)
         dbeta = dgamma = None
         if ctx.training or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             # (no identity slab, or no input gradient wanted: the colstats pass.  Eval mode with
@@ -167,7 +176,7 @@ class BatchNormActFn(torch.autograd.Function):
             dbeta, dgamma = _bwd_param_grads(dz2, y2, prm, ctx.act, *ctx.params)
         dy = _bwd_input(dz2, y2, prm, dbeta, dgamma, ctx.act, ctx.training) if ctx.needs_input_grad[0] else None
         return (None if dy is None else dy.reshape(y.shape), dgamma if ctx.has_gamma else None,
-                dbeta if ctx.has_beta else None, None, None, None, None, None, None, None, None)
+                dbeta if ctx.has_beta else None, None, None, None, None, None, None, None, None, None)
 
 
 class BatchNormActPoolFn(torch.autograd.Function):
@@ -236,13 +245,15 @@ class BatchNormActPoolFn(torch.autograd.Function):
 
 
 def batchnorm_act(y5, gamma, beta, running_mean, running_var, training: bool, momentum: float = 0.1,
-                  eps: float = 1e-5, act=None, stats_slab=None):
+                  eps: float = 1e-5, act=None, stats_slab=None, conv_next: bool = False):
+    """z = act(bn(y)).  ``conv_next``: the caller promises that z goes to one ``ops.conv`` and
+    nowhere else -- z may then be written by that conv's forward kernel (ops/bnfuse.py defer)."""
     if _native.use_native(y5):
         # (grad mode is off inside Function.forward: decide here whether a backward will run)
         tag = training and torch.is_grad_enabled() and (y5.requires_grad or any(
             p is not None and p.requires_grad for p in (gamma, beta)))
         return BatchNormActFn.apply(y5.to(torch.bfloat16).contiguous(), gamma, beta, stats_slab, running_mean,
-                                    running_var, training, momentum, eps, act_code(act), tag)
+                                    running_var, training, momentum, eps, act_code(act), tag, bool(conv_next))
     return ref.batchnorm_act(y5, gamma, beta, running_mean, running_var, training, momentum, eps, act)
 
 

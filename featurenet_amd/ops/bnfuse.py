@@ -93,6 +93,48 @@ def source_of(x: torch.Tensor):
     return y, prm, e[3], mask
 
 
+_LAZY: dict = {}     # z.data_ptr() -> (ref z, y, prm, act, mask, fill)
+
+
+def prologue_enabled() -> bool:
+    """BN + act of a conv's input inside the consuming conv_tile forward (``FN_BN_PROLOGUE``,
+    default on): the BN forward leaves ``z`` unwritten, the conv's loader normalises the landed
+    halo of ``y`` in LDS and writes ``z`` (and the relu mask) once, for the positions its tile owns
+    (conv_tile.hip ``xform_job``) -- no ``bn_apply`` pass."""
+    return os.environ.get("FN_BN_PROLOGUE", "1") != "0"
+
+
+def defer(z: torch.Tensor, y: torch.Tensor, prm: torch.Tensor, act: int, mask, fill) -> None:
+    """BN forward with a promised conv consumer: ``z`` is allocated but not written; ``fill()``
+    writes it (and ``mask``) with the separate pass if the consumer cannot take the prologue."""
+    with _LOCK:
+        _purge(_LAZY)
+        _LAZY[z.data_ptr()] = (weakref.ref(z), y, prm, act, mask, fill)
+
+
+def pending(x: torch.Tensor):
+    """(y, prm, act, mask) when ``x`` is a deferred BN output not yet written, else None."""
+    e = _LAZY.get(x.data_ptr())
+    if e is None or e[0]() is None or e[0]().numel() != x.numel():
+        return None
+    return e[1], e[2], e[3], e[4]
+
+
+def filler(x: torch.Tensor):
+    """The separate pass that writes the deferred ``x`` (and its mask), for a later reader."""
+    e = _LAZY.get(x.data_ptr())
+    return e[5] if e is not None else (lambda: None)
+
+
+def settle(x: torch.Tensor, written: bool) -> None:
+    """The deferred ``x`` is dealt with: ``written`` -- the consumer's prologue wrote z and the mask;
+    otherwise the separate pass writes them now (before anything reads ``x``)."""
+    with _LOCK:
+        e = _LAZY.pop(x.data_ptr(), None)
+    if e is not None and not written:
+        e[5]()
+
+
 def offer(dz: torch.Tensor, slab, y: torch.Tensor) -> None:
     """``slab``: ``("identity", gslab, wpart)`` -- the tile dgrad's sum-g slab and the S partials of
     the conv's W . dW."""

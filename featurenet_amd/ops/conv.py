@@ -459,7 +459,9 @@ def halo_conv_dgrad(dy5, w, spec: ConvSpec, plan):
 # raw native calls
 # ---------------------------------------------------------------------------
 def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: ConvSpec, act: int,
-                    want_stats: bool, w: torch.Tensor | None = None, dstash: dict | None = None):
+                    want_stats: bool, w: torch.Tensor | None = None, dstash: dict | None = None, pro=None):
+    """``pro`` = ``bnfuse.pending(x5)``: x5 is a deferred BN output -- the tile kernel's prologue
+    writes it from (y, prm) while it convolves, any other kernel has it written first."""
     # the tile kernel's epilogue has the identity and relu only
     tplan = conv_tile.fwd_plan(spec) if w is not None and act in (0, act_code("relu")) else None
     plan = halo_fwd_plan(spec) if w is not None else None
@@ -468,7 +470,15 @@ def native_conv_fwd(x5: torch.Tensor, wmat: torch.Tensor, ldw: int, bias, spec: 
     if tplan is not None and (plan is None or conv_tile.choose(
             "fwd", spec, lambda: conv_tile.conv_fwd(x5, pad_to_spec(w, spec), bias, spec, act, want_stats, tplan),
             lambda: halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan))):
-        return conv_tile.conv_fwd(x5, pad_to_spec(w, spec), bias, spec, act, want_stats, tplan, dstash=dstash)
+        # (z itself is written only when something will read it: ``pro[4]`` -- the weight gradient
+        # normalises y itself where it can, ConvFn decides)
+        r = conv_tile.conv_fwd(x5, pad_to_spec(w, spec), bias, spec, act, want_stats, tplan, dstash=dstash,
+                               pro=pro and (pro[0], pro[1], pro[2], x5 if pro[4] else None, pro[3]))
+        if pro is not None:
+            bnfuse.settle(x5, True)
+        return r
+    if pro is not None:
+        bnfuse.settle(x5, False)
     if plan is not None:
         return halo_conv_fwd(x5, w, bias, spec, act, want_stats, plan)
     K = _native.kernels()
@@ -550,19 +560,41 @@ def wgrad_splits(spec: ConvSpec, target_blocks: int = 1024) -> int:
     return int(min(s, max(1, spec.M // 256)))
 
 
-def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=None, wdot=None):
+def wgrad_takes_prologue(spec: ConvSpec) -> bool:
+    """:func:`native_conv_wgrad` of ``spec`` will run conv_wtile in a form that applies a BN prologue
+    to x itself (decided without timing; False when only an autotune run could tell)."""
+    wplan = conv_wtile.plan(spec)
+    if wplan is None or not conv_wtile.prologue_ok(wplan):
+        return False
+    if halo_wgrad_plan(spec) is None or conv_wtile.mode() == "2":
+        return True
+    from . import tuning
+
+    return tuning.predict("wgrad", spec) is True
+
+
+def native_conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec: ConvSpec, out=None, wdot=None, pro=None):
     """fp32 dW [K, KD, KH, KW, C]; ``out`` (zeroed, contiguous, that shape) receives it in place
     where the kernel allows.  ``wdot`` (the fp32 weights): returns ``(dW, S partials or None)``
     -- the big-tile kernel's reduce also sums S = W . dW per input channel (see
-    :func:`conv_wtile.conv_wgrad`); None where another kernel ran."""
+    :func:`conv_wtile.conv_wgrad`); None where another kernel ran.  ``pro`` = (y, prm, act, fill):
+    x5 is a BN output the forward never wrote -- conv_wtile normalises y's halos itself, any other
+    kernel has ``fill()`` write x5 first."""
     plan = halo_wgrad_plan(spec)
     wplan = conv_wtile.plan(spec)
     if wplan is not None:
         dy5, x5 = dy5.contiguous(), x5.contiguous()
         use = plan is None or conv_wtile.choose(
             spec, lambda: conv_wtile.conv_wgrad(dy5, x5, spec, wplan), lambda: halo_conv_wgrad(dy5, x5, spec, plan))
+        if use and pro is not None and conv_wtile.prologue_ok(wplan):
+            return conv_wtile.conv_wgrad(dy5, pro[0], spec, wplan, out=out, wdot=wdot, pro=(pro[1], pro[2]))
+        if pro is not None:
+            pro[3]()
+            pro = None
         if use:
             return conv_wtile.conv_wgrad(dy5, x5, spec, wplan, out=out, wdot=wdot)
+    if pro is not None:
+        pro[3]()
     if wdot is not None:
         return native_conv_wgrad(dy5, x5, spec, out=out), None
     if plan is not None:
@@ -936,6 +968,22 @@ class ConvFn(torch.autograd.Function):
         x_saved = x5
         ctx.pw = pointwise_ok(spec, want_stats)
         ctx.cpad = 0
+        # x = a deferred BN output (ops/bnfuse.py): the tile forward writes it; every other branch
+        # has it written before reading it
+        pro = bnfuse.pending(x5)
+        tile_branch = (not ctx.pw and s2d is None and not chan_pad_needed(spec) and
+                       (halo_fwd_plan(spec) is not None or
+                        (conv_tile.fwd_plan(spec) is not None and act in (0, act_code("relu")))))
+        if pro is not None and not tile_branch:
+            bnfuse.settle(x5, False)
+            pro = None
+        ctx.pro_w = None                 # (y, prm, act, fill): the backward's wgrad normalises y itself
+        if pro is not None:
+            # z is read by nothing but this conv's weight gradient
+            zw = bool(ctx.needs_input_grad[1]) and not wgrad_takes_prologue(spec)
+            if ctx.needs_input_grad[1] and not zw:
+                ctx.pro_w = (pro[0], pro[1], pro[2], bnfuse.filler(x5))
+            pro = pro + (zw,)
         if not ctx.pw and s2d is None and chan_pad_needed(spec):
             # C % 8 != 0 (NAS convs: 12, 18, 120 ... channels): gather 16-B channel vectors of a
             # zero-padded copy instead of single elements; the padded copy is what wgrad reads
@@ -970,7 +1018,7 @@ class ConvFn(torch.autograd.Function):
             # (the tile forward also packs the backward's dgrad weights, in the same launch)
             ctx.dstash = {} if ctx.needs_input_grad[0] else None
             y, stats = native_conv_fwd(x5.contiguous(), None, 0, bias, spec, act, want_stats,
-                                       w=w.detach(), dstash=ctx.dstash)
+                                       w=w.detach(), dstash=ctx.dstash, pro=pro)
         else:
             wmat, ldw = pack_weight_rows(w.detach(), spec)
             y, stats = native_conv_fwd(x5.contiguous(), wmat, ldw, bias, spec, act, want_stats)
@@ -1005,6 +1053,12 @@ class ConvFn(torch.autograd.Function):
         # layer): it applies the activation backward and sums the bias gradient as it loads dy
         wg_igemm = (not ctx.pw and ctx.s2d is None and ctx.needs_input_grad[1] and igemm_wgrad_takes(spec)
                     and (not padded or ctx.cpad or spec.C == w.shape[-1]))
+        # x5 unwritten (the forward's BN prologue): native_conv_wgrad's conv_wtile normalises y
+        # itself; any other weight-gradient path has x5 written first
+        prow, ctx.pro_w = getattr(ctx, "pro_w", None), None
+        if prow is not None and (padded or ctx.pw or ctx.s2d is not None or wg_igemm):
+            prow[3]()
+            prow = None
         fuse_act = bool(act) and wg_igemm and not ctx.x_needs
         if act and not fuse_act:
             dy = native_act_bwd(dy, y, act)
@@ -1047,10 +1101,11 @@ class ConvFn(torch.autograd.Function):
                     dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=tgt)
             elif ident is not None and w.dtype == torch.float32:
                 # (+ S = sum W . dW for the statistics identity from the reduce pass, when it can)
-                dw, wpart = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w), wdot=w.detach())
+                dw, wpart = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w), wdot=w.detach(),
+                                              pro=prow)
             else:
                 # straight into the parameter's zeroed flat gradient when FlatParams offers it
-                dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w))
+                dw = native_conv_wgrad(dy, x5.contiguous(), spec, out=grad_target(w), pro=prow)
         if want_db and db is None:
             db = native_colsum(dy.reshape(-1, spec.K), out=grad_target(ctx.bparam))
         if ident is not None:

@@ -617,8 +617,18 @@ def workers(p: TilePlan, geom: list, ncol: int) -> int:
 
 
 def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p: TilePlan, geom: list, kdims: tuple,
-        ncol: int, act: int, bny=None, bnp=None, oscale: float = 0.0, osc=None) -> None:
+        ncol: int, act: int, bny=None, bnp=None, oscale: float = 0.0, osc=None, pro=None) -> None:
+    """``pro`` = (prm [4, C], act, z, mask or None): ``src5`` is a BN's pre-normalisation y and the
+    kernel's loader applies z = act(y * prm[2] + prm[3]) to every landed halo, writing z (and the
+    relu-mask bytes) for the positions its tiles own (conv_tile.hip ``xform_job``)."""
     st = _native.stream(src5)
+    pk = {}
+    if pro is not None:
+        prm, pact, z, mask = pro
+        assert prm.is_contiguous() and prm.shape == (4, src5.shape[-1]) and prm.dtype == torch.float32
+        assert z is None or (z.is_contiguous() and z.numel() == src5.numel() and z.dtype == torch.bfloat16)
+        pk = dict(pst=prm[2].data_ptr(), pz=_native.ptr(z), pmask=_native.ptr(mask), pact=int(pact),
+                  pext=[2 * prm.shape[1], z.numel() if z is not None else 0, mask.numel() if mask is not None else 0])
     rt = rowtab_tensor(p, kdims, src5.device)
     kt = ktab_tensor(p, kdims, src5.device)
     ext = [src5.numel(), wpk.numel(), out.numel(), rt.numel() // 2, kt.numel() // 4]
@@ -628,15 +638,18 @@ def run(src5: torch.Tensor, wpk: torch.Tensor, bias, out: torch.Tensor, stats, p
                                 zero_page(src5.device).data_ptr(), _native.ptr(bias), out.data_ptr(),
                                 _native.ptr(stats), geom, ncol, act, p.MT, p.NT, sched(src5.device, st).data_ptr(),
                                 st, ext, _native.ptr(bny), _native.ptr(bnp), float(oscale), _native.ptr(osc),
-                                osc.numel() if osc is not None else 0)
+                                osc.numel() if osc is not None else 0, **pk)
 
 
 def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats: bool, p: TilePlan,
-             out_scale: float | None = None, dstash: dict | None = None):
+             out_scale: float | None = None, dstash: dict | None = None, pro=None):
     """y = act(conv(x, w) + b) (+ BN statistics slab) for a stride-1 conv on the tile kernel;
     ``out_scale``: e4m3 bytes of y / out_scale instead (fp8 inference input, no statistics).
     ``dstash`` (a dict kept by the caller until its backward): the dgrad's packed weights are made
-    in the same launch and left there as ``(plan, packed)`` for :func:`conv_dgrad`."""
+    in the same launch and left there as ``(plan, packed)`` for :func:`conv_dgrad`.
+    ``pro`` = (yb, prm, act, z, mask): x5 = z = act(bn(yb)) is not written yet -- the kernel reads
+    yb, normalises in its loader and writes z (unless z is None: nothing will read it) and the mask
+    (see :func:`run`)."""
     kd = (spec.KD, spec.KH, spec.KW)
     geom = geometry(p, (spec.N, spec.D, spec.H, spec.W, spec.C), (spec.OD, spec.OH, spec.OW), kd,
                     (spec.pd, spec.ph, spec.pw))
@@ -651,6 +664,12 @@ def conv_fwd(x5: torch.Tensor, w: torch.Tensor, bias, spec, act: int, want_stats
     if want_stats:
         assert not out_scale, "statistics with an fp8 output"
         stats = torch.empty(workers(p, geom, spec.K), 2, spec.K, dtype=torch.float32, device=x5.device)
+    if pro is not None:
+        assert not out_scale
+        yb, prm, pact, z, mask = pro
+        assert (z is None or z.data_ptr() == x5.data_ptr()) and yb.shape == x5.shape
+        run(yb, wpk, bias, y, stats, p, geom, kd, spec.K, act, pro=(prm, pact, z, mask))
+        return y, stats
     run(x5, wpk, bias, y, stats, p, geom, kd, spec.K, act, oscale=1.0 / out_scale if out_scale else 0.0)
     return y, stats
 

@@ -336,12 +336,20 @@ def flags(p: WPlan) -> int:
             | (1 << 14 if p.sp else 0))
 
 
-def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None, wdot=None):
+def prologue_ok(p: WPlan) -> bool:
+    """The plan's kernel form can normalise its x halos itself (BN prologue: 16-channel slices --
+    not the 8-channel space-to-depth stem form nor the sub-pixel form)."""
+    return not p.c8 and not p.sp
+
+
+def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None, wdot=None, pro=None):
     """dW fp32 [K, KD, KH, KW, C] on the big-tile wgrad kernel (accumulated into ``out``
     when given: a zeroed contiguous fp32 tensor of that size, e.g. the flat gradient).
     ``wdot`` (the layer's fp32 weights, that layout): returns ``(dW, S partials)`` where the
     partial slab [blocks, C] of S = sum W . dW comes from the kernel's reduce pass (the BN
-    statistics identity, ``bn_pool.hip``; no separate bn_wdot launch)."""
+    statistics identity, ``bn_pool.hip``; no separate bn_wdot launch).
+    ``pro`` = (prm [4, C], act): ``x5`` is a BN's pre-normalisation y and the conv's input is
+    act(y * prm[2] + prm[3]), applied by the kernel to every landed x halo (:func:`prologue_ok`)."""
     kd = (spec.KD, spec.KH, spec.KW)
     dev = x5.device
     rt_np, pt_np = tables(p, kd)
@@ -357,11 +365,16 @@ def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None, wd
         wsrc = wdot.detach().float().contiguous()
         wdp = torch.empty(-(-dw.numel() // 256), spec.C, dtype=torch.float32, device=dev)
     ext = [x5.numel(), dy5.numel(), dw.numel(), rt.numel() // 2, pt.numel(), part.numel()]
-    if wsrc is not None:
-        ext += [wsrc.numel(), wdp.numel()]
+    ext += [wsrc.numel(), wdp.numel()] if wsrc is not None else [0, 0]
+    pk = {}
+    if pro is not None:
+        prm, pact = pro
+        assert prologue_ok(p) and prm.is_contiguous() and prm.shape == (4, spec.C) and prm.dtype == torch.float32
+        ext.append(2 * spec.C)
+        pk = dict(pst=prm[2].data_ptr(), pact=int(pact))
     _native.kernels().conv_wtile(x5.data_ptr(), dy5.data_ptr(), dw.data_ptr(), part.data_ptr(), rt.data_ptr(),
                                  pt.data_ptr(), zp.data_ptr(), geometry(p, spec), flags(p), p.workers, sched.data_ptr(),
-                                 st, ext, _native.ptr(wsrc), _native.ptr(wdp))
+                                 st, ext, _native.ptr(wsrc), _native.ptr(wdp), **pk)
     dw = dw.reshape(spec.K, spec.KD, spec.KH, spec.KW, spec.C)
     return dw if wdot is None else (dw, wdp)
 

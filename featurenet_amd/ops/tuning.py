@@ -97,6 +97,19 @@ def select(kind: str, spec, run_tile=None, run_other=None) -> bool:
     return c
 
 
+def predict(kind: str, spec):
+    """What :func:`select` will return for ``kind`` of ``spec`` without timing anything: True /
+    False, or None when only an autotune measurement can tell."""
+    key = (kind, shape_key(spec))
+    c = _DECIDED.get(key)
+    if c is not None:
+        return c
+    tk = (kind,) + key[1]
+    if tk in EXCEPTIONS:
+        return bool(EXCEPTIONS[tk])
+    return None if mode() == "autotune" else True
+
+
 def decisions() -> dict:
     return dict(_DECIDED)
 

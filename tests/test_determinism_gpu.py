@@ -270,7 +270,9 @@ def test_weight_ring_gives_the_register_path_bits():
     """conv_tile's LDS weight ring (the loader DMAs each k-step's weight fragments once per
     workgroup; per-k-step counters hand the slots over) runs the same MFMAs in the same order as
     the register path (every compute wave streaming the fragments itself): the FeatureNet-3D step
-    with the ring on and off gives the same bits -- and the ring is on for most layers."""
+    with the ring on and off gives the same bits -- and the ring, when switched on, is on for most
+    layers.  (It is opt-in -- FN_TILE_WLDS=1 -- being slower than the register path,
+    profiles/r6_weight_ring.md.)"""
     from featurenet_amd.models.featurenet3d import FeatureNet3D
     from featurenet_amd.ops import conv_tile as ct
     from featurenet_amd.ops import softmax_xent
@@ -280,7 +282,11 @@ def test_weight_ring_gives_the_register_path_bits():
     # which layers take the ring (the plan must leave room for >= 4 slots)
     sp = ct.plan(16, (22, 22, 22), (4, 4, 4), 32, 64)
     geom = ct.geometry(sp, (16, 25, 25, 25, 32), (22, 22, 22), (4, 4, 4), (0, 0, 0))
-    assert K.conv_tile_wring(geom, 64, sp.MT, sp.NT, 0) >= 4
+    K.conv_tile_set_wlds(1)
+    try:
+        assert K.conv_tile_wring(geom, 64, sp.MT, sp.NT, 0) >= 4
+    finally:
+        K.conv_tile_set_wlds(-1)
     torch.manual_seed(17)
     model = FeatureNet3D().to(dev)
     x = (torch.rand(16, 64, 64, 64, 1, device=dev) < 0.3).to(torch.bfloat16)
