@@ -181,6 +181,16 @@ def torch_oracle(a) -> None:
     # bench.py --impl torch); the math is the same
     torch.backends.cudnn.benchmark = True
     t0 = time.time()
+    # (MIOpen's first find of each 3-D fp32 shape compiles and times its solvers for minutes without
+    # printing anything: a heartbeat keeps a supervised run visibly alive)
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(30)
+            print(f"  [{time.time() - t0:.0f} s]", flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     ds = voxel_dataset(a.train_per_class * a.classes, a.test_per_class * a.classes, size=a.size,
                        num_classes=a.classes, seed=a.seed)
     t_gen = time.time() - t0

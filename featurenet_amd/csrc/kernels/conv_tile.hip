@@ -263,7 +263,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   };
 
   // BN prologue (pst != null; bf16 forward only, host-checked): the source is the PREVIOUS layer's
-  // pre-BN output y, and the layer's input is z = act(y * scale + shift) per input channel
+  // pre-BN output y, and the layer's input is z = relu(y * scale + shift) per input channel
   // (pst = [scale C][shift C]).  Once a job's halo has landed the loader rewrites it in LDS as z --
   // the same fma, activation and bf16 rounding as bn_apply_kernel, so the conv sees the same bits --
   // leaving the zero page's padding positions alone (the conv pads z, not y), and for the positions
@@ -288,44 +288,67 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       const int od = td_ == tdn - 1 ? 255 : g.TD, oh = th_ == thn - 1 ? 255 : g.TH, ow = tw_ == twn - 1 ? 255 : g.TW;
       const bool writer = blockIdx.y == 0 && (pz || pmask);
       const long long nbase = (long long)n * g.ID * g.IH * g.IW;
+      // (the loader shares SIMD 0 with compute wave 0, whose MFMA stream wins the issue arbitration
+      // at equal priority: the transform -- on the loader's critical path -- runs at a raised one)
+      __builtin_amdgcn_s_setprio(2);
       unsigned char* buf = dsm + bufoff + lane * 16;
-#pragma unroll 1
-      for (int c = 0; c < CPP; ++c) {
-        const int ch0 = __builtin_amdgcn_readfirstlane(slice * g.CS + c * 8);
-        float sc[8], sh[8];
+      // the slice's scale / shift pairs in VGPRs (an opaque zero in the index: uniform loads would
+      // take 16 SGPRs per chunk, and the kernel already spills SGPRs)
+      int z0;
+      asm("v_mov_b32 %0, 0" : "=v"(z0));
+      const float* ps = pst + slice * g.CS + z0;
+      ct_f32x2 sc[CPP][4], sh[CPP][4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          sc[j] = pst[ch0 + j];
-          sh[j] = pst[g.C + ch0 + j];
-        }
-#pragma unroll 2
-        for (int r = 0; r < (g.HPpad >> 6); ++r) {
-          const int p = (r << 6) + lane;
-          const int e = s_pos[p].y;
-          const int hd = e >> 16, hh = (e >> 8) & 255, hw = e & 255;
-          const int gd = dlo + hd, gh = hlo + hh, gw = wlo + hw;
-          const bool ok = interior || ((unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
-                                       (unsigned)gw < (unsigned)g.IW);
-          unsigned char* a = buf + c * PLANE + (r << 10);
-          const uint4 v = *(const uint4*)a;
-          const unsigned vi[4] = {v.x, v.y, v.z, v.w};
-          unsigned o[4], bits = 0;
+      for (int c = 0; c < CPP; ++c)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float lo = act_fwd(__builtin_fmaf(bf16_lo(vi[q]), sc[2 * q], sh[2 * q]), pact);
-            const float hi = act_fwd(__builtin_fmaf(bf16_hi(vi[q]), sc[2 * q + 1], sh[2 * q + 1]), pact);
-            bits |= (lo > 0.f ? 1u : 0u) << (2 * q);
-            bits |= (hi > 0.f ? 1u : 0u) << (2 * q + 1);
-            o[q] = bf16x2_pack(lo, hi);
+        for (int q = 0; q < 4; ++q) {
+          sc[c][q] = *(const ct_f32x2*)(ps + c * 8 + 2 * q);
+          sh[c][q] = *(const ct_f32x2*)(ps + g.C + c * 8 + 2 * q);
+        }
+      // a position's CPP chunks together (one s_pos read, one bounds test); every LDS read of a row
+      // -- its chunks and the next row's s_pos entry -- is issued before the row's writes (the
+      // compiler cannot tell the planes apart and would otherwise wait out each read alone)
+      const int NR = g.HPpad >> 6;
+      int e = s_pos[lane].y;
+      for (int r = 0; r < NR; ++r) {
+        const int p = (r << 6) + lane;
+        uint4 v[CPP];
+#pragma unroll
+        for (int c = 0; c < CPP; ++c) v[c] = *(const uint4*)(buf + c * PLANE + (r << 10));
+        const int e_next = s_pos[(r + 1 < NR ? p + 64 : p)].y;
+        const int hd = e >> 16, hh = (e >> 8) & 255, hw = e & 255;
+        const int gd = dlo + hd, gh = hlo + hh, gw = wlo + hw;
+        const bool ok = interior || ((unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
+                                     (unsigned)gw < (unsigned)g.IW);
+        uint4 o[CPP];
+        unsigned bits[CPP];
+#pragma unroll
+        for (int c = 0; c < CPP; ++c) {
+          o[c] = ct_bn_chunk(v[c], sc[c], sh[c], true, bits[c]);
+          if (ok) *(uint4*)(buf + c * PLANE + (r << 10)) = o[c];
+        }
+        if (writer && ok && p < HP && hd < od && hh < oh && hw < ow) {
+          const long long pos = nbase + ((long long)gd * g.IH + gh) * g.IW + gw;
+          if (pz) {
+#pragma unroll
+            for (int c = 0; c < CPP; ++c) *(uint4*)(pz + pos * g.C + slice * g.CS + c * 8) = o[c];
           }
-          if (ok) *(uint4*)a = make_uint4(o[0], o[1], o[2], o[3]);
-          if (writer && ok && p < HP && hd < od && hh < oh && hw < ow) {
-            const long long pos = nbase + ((long long)gd * g.IH + gh) * g.IW + gw;
-            if (pz) *(uint4*)(pz + pos * g.C + ch0) = make_uint4(o[0], o[1], o[2], o[3]);
-            if (pmask) pmask[pos * (g.C >> 3) + (ch0 >> 3)] = (unsigned char)bits;
+          if (pmask) {                             // (CPP consecutive mask bytes, CPP-aligned)
+            unsigned char* mp = pmask + pos * (g.C >> 3) + slice * (g.CS >> 3);
+            if constexpr (CPP == 1) {
+              *mp = (unsigned char)bits[0];
+            } else if constexpr (CPP == 2) {
+              *(unsigned short*)mp = (unsigned short)(bits[0] | (bits[1] << 8));
+            } else {
+#pragma unroll
+              for (int c = 0; c < CPP; c += 4)
+                *(unsigned*)(mp + c) = bits[c] | (bits[c + 1] << 8) | (bits[c + 2] << 16) | (bits[c + 3] << 24);
+            }
           }
         }
+        e = e_next;
       }
+      __builtin_amdgcn_s_setprio(0);
     }
   };
 
@@ -647,8 +670,9 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
         ++kjob;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (ntile >= 0) xform_job(ntile, nslc, (par ^ 1) * g.BUF);
       lap(st_k);
+      if (ntile >= 0) xform_job(ntile, nslc, (par ^ 1) * g.BUF);
+      lap(st_e);                                 // (the loader's "epilogue" stamp: the BN prologue)
       tile = ntile;
       slice = nslc;
       par ^= 1;
@@ -1377,7 +1401,7 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
 }
 
 // The LDS weight ring (conv_tile_kernel WL): off unless FN_TILE_WLDS=1 (measured slower than the
-// register path, profiles/r6_weight_ring.md), for the bf16 instances whose
+// register path, profiles/r6_bn_prologue.md), for the bf16 instances whose
 // plan leaves room for at least CT_WRING_MIN k-step slots (up to CT_WRING_MAX) in the 160 KiB
 #define CT_WRING_MIN 8
 #define CT_WRING_MAX 12
@@ -1460,7 +1484,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
   if (!(oscale >= 0.f) || (oscale > 0.f && (stats || NT != 2 || CPP != 1))) return -2;
   if (osc && (oscale <= 0.f || Ncol > 128)) return -2;
   // the BN prologue: a bf16 forward (no relu-mask dgrad, no fp8 output), z none / relu
-  if (pst && (bny || oscale != 0.f || osc || (pact != ACT_NONE && pact != ACT_RELU))) return -2;
+  if (pst && (bny || oscale != 0.f || osc || pact != ACT_RELU)) return -2;   // (relu only)
   if (!pst && (pz || pmask)) return -2;
   dim3 grid((unsigned)fn_conv_tile_workers(geom, Ncol, NT), (unsigned)ncb);
   // (tests: a smaller grid must give the same bits -- only the dynamic schedules take it)
@@ -1480,7 +1504,8 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     if ((dbg & 16) && !stamps && hipMalloc(&stamps, 256 * 64 * 16 * sizeof(long long)) != hipSuccess) return -5;
     if ((dbg & 16) && hipMemsetAsync(stamps, 0, nst * sizeof(long long), st) != hipSuccess) return -5;
 #define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, src, \
-      (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, stamps);
+      (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, stamps, \
+      nullptr, 0.f, bny, nullptr, nullptr, stats ? tile_chunk(g) : 0, 0, pst, pz, pmask, pact);
     CT_DBG(1, 1) CT_DBG(1, 2) CT_DBG(1, 4) CT_DBG(1, 16)   // (the space-to-depth stem)
     CT_DBG(1, 8) CT_DBG(1, 24) CT_DBG(2, 8) CT_DBG(2, 24)
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)

@@ -76,6 +76,30 @@ __device__ __forceinline__ unsigned ct_relu_bf16x2(unsigned w) {
   return __builtin_bit_cast(unsigned, s);
 }
 
+// BN (+ relu) of 8 bf16 values (one 16-B chunk, packed pairs) with per-channel scale / shift pairs:
+// z = act(y * scale + shift) as bn_apply_kernel computes it -- one fma, bf16 rounding, then relu on
+// the bf16 bits (the same bits as relu before the rounding, NaN aside).  Packed: per pair two
+// unpacks, one v_pk_fma_f32, one v_cvt_pk_bf16_f32, one v_pk_max_i16.  bits (relu): bit j = z_j > 0.
+typedef unsigned short ct_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ct_bn_chunk(uint4 v, const ct_f32x2* sc, const ct_f32x2* sh, bool relu,
+                                             unsigned& bits) {
+  const unsigned vi[4] = {v.x, v.y, v.z, v.w};
+  unsigned o[4];
+  bits = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const ct_f32x2 x = {bf16_lo(vi[q]), bf16_hi(vi[q])};
+    const ct_f32x2 r = __builtin_elementwise_fma(x, sc[q], sh[q]);
+    unsigned w = bf16x2_pack(r.x, r.y);
+    if (relu) w = ct_relu_bf16x2(w);
+    o[q] = w;
+    const unsigned m = __builtin_bit_cast(unsigned, __builtin_elementwise_min(__builtin_bit_cast(ct_u16x2, w),
+                                                                               (ct_u16x2){1, 1}));
+    bits |= ((m | (m >> 15)) & 3u) << (2 * q);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // B-ring depth (k-steps in flight): a bf16 k-step is MT*NT 16-cycle MFMAs, an fp8 one
 // MT*NT 32-cycle block-scaled MFMAs, so 2 fp8 steps cover the latency 4 bf16 steps do
 __host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : 4; }

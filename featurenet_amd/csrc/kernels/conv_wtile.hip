@@ -31,6 +31,7 @@
 // Reference semantics: the weight gradient of Keras Conv3D (reference model/input.py:294
 // via TF autodiff); the layout / schedule here is MI355X-specific.
 #include "common.h"
+#include "conv_tile_shared.h"
 #include "tile_dma.h"
 
 #include <cstdlib>
@@ -310,33 +311,30 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
                         wlo + HW <= g.IW;
       const int nx = (g.HPpad * XR) >> 10;
       const int ch0 = slice * 16 + (lane & 1) * 8;   // (a lane's slots: one 8-channel half)
-      float sc[8], sh[8];
+      ct_f32x2 sc[4], sh[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sc[j] = pst[ch0 + j];
-        sh[j] = pst[g.C + ch0 + j];
+      for (int qq = 0; qq < 4; ++qq) {
+        sc[qq] = *(const ct_f32x2*)(pst + ch0 + 2 * qq);
+        sh[qq] = *(const ct_f32x2*)(pst + g.C + ch0 + 2 * qq);
       }
       unsigned char* buf = dsm + bufoff + lane * 16;
-#pragma unroll 2
+      if (first >= nx) return;
+      // the next slot's LDS reads go out before this slot's write (the compiler would otherwise
+      // wait out every read alone)
+      uint4 v = *(const uint4*)(buf + (first << 10));
+      int e = s_pos[(64 * first + lane) >> 1];
       for (int j = first; j < nx; j += step) {
-        const int e = s_pos[(64 * j + lane) >> 1];
+        const int jn = j + step < nx ? j + step : j;
+        const uint4 vn = *(const uint4*)(buf + (jn << 10));
+        const int en = s_pos[(64 * jn + lane) >> 1];
         const int gd = dlo + (e >> 16), gh = hlo + ((e >> 8) & 255), gw = wlo + (e & 255);
         const bool ok = e >= 0 && (x_in || ((unsigned)gd < (unsigned)g.ID && (unsigned)gh < (unsigned)g.IH &&
                                             (unsigned)gw < (unsigned)g.IW));
-        unsigned char* a = buf + (j << 10);
-        const uint4 v = *(const uint4*)a;
-        const unsigned vi[4] = {v.x, v.y, v.z, v.w};
-        unsigned o[4];
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-          const float lo = act_fwd(__builtin_fmaf(__uint_as_float(vi[qq] << 16), sc[2 * qq], sh[2 * qq]), pact);
-          const float hi = act_fwd(__builtin_fmaf(__uint_as_float(vi[qq] & 0xffff0000u), sc[2 * qq + 1], sh[2 * qq + 1]),
-                                   pact);
-          typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
-          const bf2_t pk = {f2bf(lo), f2bf(hi)};
-          o[qq] = __builtin_bit_cast(unsigned, pk);
-        }
-        if (ok) *(uint4*)a = make_uint4(o[0], o[1], o[2], o[3]);
+        unsigned bits;
+        const uint4 o = ct_bn_chunk(v, sc, sh, true, bits);
+        if (ok) *(uint4*)(buf + (j << 10)) = o;
+        v = vn;
+        e = en;
       }
     }
   };
@@ -764,7 +762,7 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
   const int nw = ((nacc >> 8) & 15) == 8 ? 8 : 4;
   if (!fn_conv_wtile_supported(g.K, nacc)) return -2;
   // the BN prologue (x = pre-BN y; pst = [scale C][shift C]): 16-channel slices only, act none / relu
-  if (pst && (c8 || sp || (pact != ACT_NONE && pact != ACT_RELU))) return -2;
+  if (pst && (c8 || sp || pact != ACT_RELU)) return -2;   // (relu only)
   nacc &= 255;
   const int xr = c8 ? 16 : 32, tpf = c8 ? 2 : 1;
   if ((c8 ? g.C != 8 : g.C % (sp ? 32 : 16)) || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;

@@ -142,7 +142,7 @@ class BatchNormActFn(torch.autograd.Function):
             _native.kernels().bn_apply(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), z.data_ptr(), y2.numel(),
                                        C, act, _native.stream(y), _native.ptr(mask), 0 if mask is None else mask.numel())
 
-        if lazy and act in (0, 1) and C % 8 == 0 and bnfuse.prologue_enabled():
+        if lazy and act == 1 and C % 8 == 0 and bnfuse.prologue_enabled():
             # the caller's next op is a conv: its conv_tile loader applies BN + act to y's halo and
             # writes z and the mask (ops/bnfuse.py defer / settle), else ``fill`` runs there
             bnfuse.defer(z, y, prm, act, mask, fill)

@@ -97,11 +97,22 @@ _LAZY: dict = {}     # z.data_ptr() -> (ref z, y, prm, act, mask, fill)
 
 
 def prologue_enabled() -> bool:
-    """BN + act of a conv's input inside the consuming conv_tile forward (``FN_BN_PROLOGUE``,
-    default on): the BN forward leaves ``z`` unwritten, the conv's loader normalises the landed
+    """BN + relu of a conv's input inside the consuming conv_tile forward (``FN_BN_PROLOGUE=1``;
+    off by default): the BN forward leaves ``z`` unwritten, the conv's loader normalises the landed
     halo of ``y`` in LDS and writes ``z`` (and the relu mask) once, for the positions its tile owns
-    (conv_tile.hip ``xform_job``) -- no ``bn_apply`` pass."""
-    return os.environ.get("FN_BN_PROLOGUE", "1") != "0"
+    (conv_tile.hip ``xform_job``) -- no ``bn_apply`` pass.  Bit-identical, but measured slower:
+    the loader shares SIMD 0 with compute wave 0, and its ~20 VALU instructions per 16-B chunk
+    take MFMA issue cycles from that wave -- the forward convs ran 1.6-2.3x longer, far more than
+    the 170 us of bn_apply passes they replace (profiles/r6_bn_prologue.md)."""
+    return os.environ.get("FN_BN_PROLOGUE", "0") == "1"
+
+
+def prologue_wgrad_enabled() -> bool:
+    """The weight gradient of the conv that took a BN prologue normalises its x halos itself
+    (``FN_BN_PROLOGUE_WGRAD=1``) instead of reading the z that the forward's loader writes
+    (default): the loader has idle cycles for the write, the weight-gradient waves have none for
+    the normalisation."""
+    return os.environ.get("FN_BN_PROLOGUE_WGRAD", "0") == "1"
 
 
 def defer(z: torch.Tensor, y: torch.Tensor, prm: torch.Tensor, act: int, mask, fill) -> None:

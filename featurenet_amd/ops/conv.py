@@ -980,7 +980,8 @@ class ConvFn(torch.autograd.Function):
         ctx.pro_w = None                 # (y, prm, act, fill): the backward's wgrad normalises y itself
         if pro is not None:
             # z is read by nothing but this conv's weight gradient
-            zw = bool(ctx.needs_input_grad[1]) and not wgrad_takes_prologue(spec)
+            zw = bool(ctx.needs_input_grad[1]) and not (bnfuse.prologue_wgrad_enabled() and
+                                                        wgrad_takes_prologue(spec))
             if ctx.needs_input_grad[1] and not zw:
                 ctx.pro_w = (pro[0], pro[1], pro[2], bnfuse.filler(x5))
             pro = pro + (zw,)

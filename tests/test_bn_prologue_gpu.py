@@ -24,7 +24,7 @@ CASES = [
     (2, 25, 25, 25, 32, 64, (4, 4, 4), "valid", 1),   # conv3
     (3, 22, 22, 22, 64, 64, (3, 3, 3), "valid", 1),   # conv4: 2 slices per tile, 2 column blocks
     (3, 11, 12, 13, 16, 48, (3, 3, 3), "same", 1),    # border tiles: zero-page padding positions
-    (2, 9, 10, 11, 64, 64, (3, 3, 3), "same", 0),     # identity activation (no relu), CS 32/64
+    (2, 9, 10, 11, 64, 64, (3, 3, 3), "same", 1),     # 64 input channels: CS 32/64
     (3, 10, 11, 12, 8, 16, (3, 3, 3), "same", 1),     # 8-channel slices
 ]
 
@@ -116,12 +116,13 @@ def test_prologue_without_mask_or_z_writeback():
     assert rel < 1e-2, rel
 
 
-def _step(monkeypatch, prologue: str):
+def _step(monkeypatch, prologue: str, wgrad: str = "0"):
     from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
     from featurenet_amd.ops import softmax_xent
     from featurenet_amd.training.flat import FlatParams
 
     monkeypatch.setenv("FN_BN_PROLOGUE", prologue)
+    monkeypatch.setenv("FN_BN_PROLOGUE_WGRAD", wgrad)
     torch.manual_seed(5)
     dev = torch.device("cuda", 0)
     model = FeatureNet3D(FeatureNet3DConfig()).to(dev)
@@ -136,9 +137,12 @@ def _step(monkeypatch, prologue: str):
     return loss.detach().clone(), flat.grad.clone(), [b.clone() for b in model.buffers()]
 
 
-def test_model_step_prologue_bitwise(monkeypatch):
+@pytest.mark.parametrize("wgrad", ["0", "1"])
+def test_model_step_prologue_bitwise(monkeypatch, wgrad):
+    """The FeatureNet-3D step with the prologue (z written by the forward's loader, or -- wgrad
+    "1" -- never written, the weight gradients normalising y themselves) against bn_apply."""
     l0, g0, b0 = _step(monkeypatch, "0")
-    l1, g1, b1 = _step(monkeypatch, "1")
+    l1, g1, b1 = _step(monkeypatch, "1", wgrad)
     assert torch.equal(l0, l1)
     assert torch.equal(g0, g1), float((g0 - g1).norm() / g0.norm())
     assert all(torch.equal(a, b) for a, b in zip(b0, b1))   # running statistics

@@ -272,7 +272,7 @@ def test_weight_ring_gives_the_register_path_bits():
     the register path (every compute wave streaming the fragments itself): the FeatureNet-3D step
     with the ring on and off gives the same bits -- and the ring, when switched on, is on for most
     layers.  (It is opt-in -- FN_TILE_WLDS=1 -- being slower than the register path,
-    profiles/r6_weight_ring.md.)"""
+    profiles/r6_bn_prologue.md.)"""
     from featurenet_amd.models.featurenet3d import FeatureNet3D
     from featurenet_amd.ops import conv_tile as ct
     from featurenet_amd.ops import softmax_xent
