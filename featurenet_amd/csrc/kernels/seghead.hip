@@ -24,6 +24,7 @@
 // model/keras_model.py:124, tensorflow_generator.py:232-235), Keras Conv (1,1) head
 // (model/input.py:294).
 #include "common.h"
+#include "conv_tile_shared.h"
 
 #define SH_BM 256
 #define SH_NTHR 256
@@ -59,7 +60,9 @@ __device__ __forceinline__ float bf16_round(float x) { return bf2f(f2bf(x)); }
 // y [M][32] bf16; sc / sh [32]; w [NC][32] bf16; bias [NC] fp32 or null; labels LT [M];
 // dz [M][32] bf16 out; part: per workgroup [loss, hits | db[32] | dWt[32][32] | msum[32] | msq[32]]
 // (fp32; dWt[ch][cls] = sum z[r][ch] d[r][cls]).
-template <int ACT, typename LT>
+// NCT: the class count when it is 25 (the FeatureNet3DSeg head: loops of exactly 25 classes, 25
+// live logits per row), 32 for any NC <= 32 (runtime bound)
+template <int ACT, typename LT, int NCT = 32>
 __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __restrict__ y,
                                                                  const float* __restrict__ sc,
                                                                  const float* __restrict__ shf,
@@ -104,21 +107,22 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
       const int cls = 16 * nb + 4 * lg + i;
       bl[nb][i] = (bias && cls < NC) ? bias[cls] : 0.f;
     }
-  // this thread's input chunks always start at channel 8 (tid mod 4): 8 (scale, shift) pairs
-  float psc[8], psh[8];
+  // this thread's input chunks always start at channel 8 (tid mod 4): 8 (scale, shift) pairs,
+  // packed for v_pk_fma_f32 (conv_tile_shared.h ct_bn_chunk)
+  ct_f32x2 psc[4], psh[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    psc[j] = sc[8 * (tid & 3) + j];
-    psh[j] = shf[8 * (tid & 3) + j];
+  for (int j = 0; j < 4; ++j) {
+    psc[j] = (ct_f32x2){sc[8 * (tid & 3) + 2 * j], sc[8 * (tid & 3) + 2 * j + 1]};
+    psh[j] = (ct_f32x2){shf[8 * (tid & 3) + 2 * j], shf[8 * (tid & 3) + 2 * j + 1]};
   }
-  // the moments' columns: 16 nb + 4 lg + i
-  float msc[2][4], msh[2][4];
+  // the moments' columns: 16 nb + 4 lg + i, as pairs (i = 0, 1) and (2, 3)
+  ct_f32x2 msc[2][2], msh[2][2];
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      msc[nb][i] = sc[16 * nb + 4 * lg + i];
-      msh[nb][i] = shf[16 * nb + 4 * lg + i];
+    for (int h = 0; h < 2; ++h) {
+      msc[nb][h] = (ct_f32x2){sc[16 * nb + 4 * lg + 2 * h], sc[16 * nb + 4 * lg + 2 * h + 1]};
+      msh[nb][h] = (ct_f32x2){shf[16 * nb + 4 * lg + 2 * h], shf[16 * nb + 4 * lg + 2 * h + 1]};
     }
   Pack8 ones;
 #pragma unroll
@@ -132,11 +136,11 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
 #pragma unroll
     for (int j = 0; j < 2; ++j) adw[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   }
-  float ms[2][4], mq[2][4];                      // BN moments of columns 16 nb + 4 lg + i
+  ct_f32x2 ms[2][2], mq[2][2];                   // BN moments of columns 16 nb + 4 lg + 2 h + (0, 1)
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ms[nb][i] = mq[nb][i] = 0.f;
+    for (int h = 0; h < 2; ++h) ms[nb][h] = mq[nb][h] = (ct_f32x2){0.f, 0.f};
   float xl = 0.f, xc = 0.f;                       // loss, hits (row threads)
 
   uint4 rb[4];
@@ -160,8 +164,8 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
       Pack8 raw, zz;
       raw.u = rb[i];
       if (r >= rows) raw.u = make_uint4(0u, 0u, 0u, 0u);   // (partial tile: zero rows)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) zz.e[j] = f2bf(act_fwd(bf2f(raw.e[j]) * psc[j] + psh[j], ACT));
+      unsigned bits;
+      zz.u = ct_bn_chunk(raw.u, psc, psh, ACT == ACT_RELU, bits);
       if (r >= rows) zz.u = make_uint4(0u, 0u, 0u, 0u);
       *(uint4*)(Ys + r * SH_LD + k) = raw.u;
       *(uint4*)(Zs + r * SH_LD + k) = zz.u;
@@ -198,20 +202,22 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
         Pack8 lv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) lv[j].u = *(const uint4*)(orow + 8 * j);
-        float v[32];
+        // (NCT = 25: the loops end at the real class count, no padded-class selects)
+        auto live = [&](int c) { return NCT != 32 || c < NC; };
+        float v[NCT];
         float mx = -INFINITY;
         int am = 0;
 #pragma unroll
-        for (int c = 0; c < 32; ++c) {
-          v[c] = c < NC ? bf2f(lv[c >> 3].e[c & 7]) : -INFINITY;
+        for (int c = 0; c < NCT; ++c) {
+          v[c] = live(c) ? bf2f(lv[c >> 3].e[c & 7]) : -INFINITY;
           if (v[c] > mx) { mx = v[c]; am = c; }
         }
         // one exp per class: e_c = exp(v_c - max) serves the sum and the softmax (e_c / sum); the
         // loss -sum_c tgt_c (v_c - lse) = lse - sum_c tgt_c v_c (the targets sum to 1)
         float se = 0.f, sv = 0.f;
 #pragma unroll
-        for (int c = 0; c < 32; ++c) {
-          if (c < NC) {
+        for (int c = 0; c < NCT; ++c) {
+          if (live(c)) {
             sv += ((c == yl) ? on : off) * v[c];
             v[c] = __expf(v[c] - mx);
             se += v[c];
@@ -221,7 +227,7 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
         const float lrow = lse - sv;
 #pragma unroll
         for (int c = 0; c < 32; ++c) {
-          const float d = c < NC ? (v[c] * inv - ((c == yl) ? on : off)) * xscale : 0.f;
+          const float d = (c < NCT && live(c)) ? (v[c < NCT ? c : 0] * inv - ((c == yl) ? on : off)) * xscale : 0.f;
           lv[c >> 3].e[c & 7] = f2bf(d);         // (padded classes: 0)
         }
 #pragma unroll
@@ -269,12 +275,17 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
         const uint2 y4 = *(const uint2*)(Ys + row * SH_LD + 16 * nb + 4 * lg);
         const unsigned yw[2] = {y4.x, y4.y};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float g0 = bf16_round(dzc[mt][nb][i]);   // the stored dz
-          const float yy = (i & 1) ? __uint_as_float(yw[i >> 1] & 0xffff0000u) : __uint_as_float(yw[i >> 1] << 16);
-          const float g = act_bwd_from_out(act_fwd(yy * msc[nb][i] + msh[nb][i], ACT), ACT) * g0;
-          ms[nb][i] += g;
-          mq[nb][i] += g * yy;
+        for (int h = 0; h < 2; ++h) {               // channel pairs: v_pk_fma_f32 / v_pk_add_f32
+          const unsigned dp = bf16x2_pack(dzc[mt][nb][2 * h], dzc[mt][nb][2 * h + 1]);   // the stored dz
+          ct_f32x2 g = {bf16_lo(dp), bf16_hi(dp)};
+          const ct_f32x2 yy = {bf16_lo(yw[h]), bf16_hi(yw[h])};
+          if constexpr (ACT == ACT_RELU) {          // g = dz * relu'(z), z > 0 <=> y * sc + sh > 0
+            const ct_f32x2 tz = __builtin_elementwise_fma(yy, msc[nb][h], msh[nb][h]);
+            g.x = tz.x > 0.f ? g.x : 0.f;
+            g.y = tz.y > 0.f ? g.y : 0.f;
+          }
+          ms[nb][h] += g;
+          mq[nb][h] = __builtin_elementwise_fma(g, yy, mq[nb][h]);
         }
       }
     }
@@ -298,15 +309,19 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
   }
   // ---- workgroup partials (fixed order) ----
   // moments: the 16 lanes lr of lane group lg hold columns 16 nb + 4 lg + i
+  float msf[2][4], mqf[2][4];
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      msf[nb][i] = ms[nb][i >> 1][i & 1];
+      mqf[nb][i] = mq[nb][i >> 1][i & 1];
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
-        ms[nb][i] += __shfl_xor(ms[nb][i], o, 64);
-        mq[nb][i] += __shfl_xor(mq[nb][i], o, 64);
+        msf[nb][i] += __shfl_xor(msf[nb][i], o, 64);
+        mqf[nb][i] += __shfl_xor(mqf[nb][i], o, 64);
       }
+    }
   xl = wave_sum(xl);
   xc = wave_sum(xc);
   __syncthreads();                               // (Ys / Zs are free: the per-wave partials go there)
@@ -333,8 +348,8 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
     for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        rw[34 + 1024 + 16 * nb + 4 * lg + i] = ms[nb][i];
-        rw[34 + 1024 + 32 + 16 * nb + 4 * lg + i] = mq[nb][i];
+        rw[34 + 1024 + 16 * nb + 4 * lg + i] = msf[nb][i];
+        rw[34 + 1024 + 32 + 16 * nb + 4 * lg + i] = mqf[nb][i];
       }
   }
   __syncthreads();
@@ -367,8 +382,12 @@ extern "C" int fn_seghead_loss(const void* y, const float* sc, const float* sh, 
   if (act != ACT_RELU && act != ACT_NONE) return -2;
   const dim3 grid((unsigned)fn_seghead_blocks(M));
 #define SH_LAUNCH(A, T)                                                                                       \
-  hipLaunchKernelGGL((seghead_loss_kernel<A, T>), grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,           \
-                     (const bf16*)w, bias, (const T*)labels, (bf16*)dz, part, M, NC, xscale, smoothing)
+  if (NC == 25)                                                                                               \
+    hipLaunchKernelGGL((seghead_loss_kernel<A, T, 25>), grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,     \
+                       (const bf16*)w, bias, (const T*)labels, (bf16*)dz, part, M, NC, xscale, smoothing);       \
+  else                                                                                                        \
+    hipLaunchKernelGGL((seghead_loss_kernel<A, T>), grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,         \
+                       (const bf16*)w, bias, (const T*)labels, (bf16*)dz, part, M, NC, xscale, smoothing)
   if (act == ACT_RELU) {
     if (lab8) SH_LAUNCH(ACT_RELU, unsigned char); else SH_LAUNCH(ACT_RELU, long long);
   } else {

@@ -54,12 +54,14 @@ def main():
         extra = f", weights sha256 {r['weights_sha256']}" if "weights_sha256" in r else ""
         rate = f", {sum(sps) / len(sps):,.0f} samples/s" if sps else ""
         print(f"* `{name}`{extra}{rate}: " + " ".join(f"{x:.3f}" for x in v))
-    a, b = runs.get("native_s3"), runs.get("native_s3_repeat")
-    if a and b and "weights_sha256" in a:
-        same = a["weights_sha256"] == b["weights_sha256"] and a["val_acc_per_epoch"] == b["val_acc_per_epoch"]
-        print()
-        print(f"Seed 3, two processes: weights {a['weights_sha256']} / {b['weights_sha256']} -- "
-              f"{'identical bits' if same else 'DIFFERENT'}.")
+    a = runs.get("native_s3")
+    for other, what in (("native_s3_repeat", "two processes, one box"), ("native_s3_box2", "another box")):
+        b = runs.get(other)
+        if a and b and "weights_sha256" in a:
+            same = a["weights_sha256"] == b["weights_sha256"] and a["val_acc_per_epoch"] == b["val_acc_per_epoch"]
+            print()
+            print(f"Seed 3, {what}: weights {a['weights_sha256']} / {b['weights_sha256']} -- "
+                  f"{'identical bits' if same else 'DIFFERENT'}.")
 
 
 if __name__ == "__main__":
