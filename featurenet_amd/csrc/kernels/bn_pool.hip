@@ -13,6 +13,9 @@
 // (FeatureNet-3D conv4 -> BN -> ReLU -> MaxPool3d is one read of y4).
 #include "common.h"
 
+#include <algorithm>
+#include <type_traits>
+
 // ---------------------------------------------------------------------------
 // Column statistics: per-block partial sums over rows of a [M][C] tensor.
 //   MODE 0: (sum x, sum x^2)                       -- forward stats
@@ -520,6 +523,65 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_s2d_kernel(const bf16* __res
   }
 }
 
+// The same pass, one (n, cell-d, cell-h) row of the shifted grid at a time (grid-stride over the
+// rows): a row is W2 cells x 8 sub-positions x C / 8 chunks, so every per-chunk index is a shift of
+// the thread's offset in the row -- the flat form above spent six 64-bit divisions per 16-B chunk
+// (1.28-1.44 ms per seg step, VALU-bound).  Same arithmetic, same bits.
+template <int ACT, int LCPR>
+__global__ __launch_bounds__(256) void bn_bwd_apply_s2d_rows_kernel(const bf16* __restrict__ dz,
+                                                                    const bf16* __restrict__ y,
+                                                                    const float* __restrict__ scale,
+                                                                    const float* __restrict__ shift,
+                                                                    const float* __restrict__ mean,
+                                                                    const float* __restrict__ invstd,
+                                                                    const float* __restrict__ dbeta,
+                                                                    const float* __restrict__ dgamma,
+                                                                    bf16* __restrict__ dsh, int N, int FD, int FH,
+                                                                    int FW, int C, float inv_count) {
+  constexpr int act = ACT;
+  constexpr int cpr = 1 << LCPR;
+  const int D2 = FD / 2 + 1, H2 = FH / 2 + 1, W2 = FW / 2 + 1;
+  const int k = (int)(threadIdx.x & (cpr - 1));   // (256 is a multiple of cpr: the chunk is fixed)
+  float sc[8], sh[8], k2[8], k3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = k * 8 + j;
+    sc[j] = scale[c];
+    sh[j] = shift[c];
+    const float is = invstd[c];
+    k2[j] = -sc[j] * is * dgamma[c] * inv_count;
+    k3[j] = -sc[j] * (dbeta[c] * inv_count - mean[c] * is * dgamma[c] * inv_count);
+  }
+  const int rowlen = W2 * 8 * cpr;
+  const int nrows = N * D2 * H2;
+  for (int row = blockIdx.x; row < nrows; row += gridDim.x) {
+    const int chh = row % H2, r2 = row / H2;
+    const int cd = r2 % D2, n = r2 / D2;
+    bf16* orow = dsh + (long long)row * rowlen * 8;
+    for (int t = threadIdx.x; t < rowlen; t += 256) {
+      const int jp = (t >> LCPR) & 7, cw = t >> (LCPR + 3);
+      const int qd = 2 * cd - 1 + (jp >> 2), qh = 2 * chh - 1 + ((jp >> 1) & 1), qw = 2 * cw - 1 + (jp & 1);
+      Pack8 po;
+      if ((unsigned)qd < (unsigned)FD && (unsigned)qh < (unsigned)FH && (unsigned)qw < (unsigned)FW) {
+        const long long off = ((((long long)n * FD + qd) * FH + qh) * FW + qw) * C + k * 8;
+        Pack8 py, pd;
+        py.u = *(const uint4*)(y + off);
+        pd.u = *(const uint4*)(dz + off);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float yv = bf2f(py.e[j]);
+          const float zv = act_fwd(yv * sc[j] + sh[j], act);
+          const float g = bf2f(pd.e[j]) * act_bwd_from_out(zv, act);
+          po.e[j] = f2bf(sc[j] * g + k2[j] * yv + k3[j]);
+        }
+      } else {
+        po.u = make_uint4(0u, 0u, 0u, 0u);
+      }
+      *(uint4*)(orow + t * 8) = po.u;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Pooling (max / avg), 1-D/2-D/3-D channels-last with optional BN+act prologue.
 // geom: N, D, H, W, C, OD, OH, OW, KD, KH, KW, SD, SH, SW, PD, PH, PW
@@ -595,10 +657,12 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(const bf16* __restrict__ 
 // Non-overlapping 2x2x2 (or 1x2x2) windows with 8-channel vectors: the common
 // FeatureNet / CNN pooling.  Per-channel BN params live in registers, all window
 // loads are issued before the reduction, 32-bit index math.
-template <int KD>
+template <int KD, int ACT = -1>
 __global__ __launch_bounds__(256) void pool2_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
                                                         const float* __restrict__ scale, const float* __restrict__ shift,
                                                         PoolGeom g, int is_max, int act, int total) {
+  const int actc = ACT >= 0 ? ACT : act;         // (compile-time relu / none: a runtime switch kept
+                                                 //  tanh / sigmoid code in every element's path)
   const int cpr = g.C >> 3;
   // grid-stride over a resident-sized grid (the stride is a multiple of 256, so with
   // 256 % cpr == 0 -- host-checked -- a thread keeps its 8-channel chunk and the BN parameters
@@ -642,7 +706,7 @@ __global__ __launch_bounds__(256) void pool2_fwd_kernel(const bf16* __restrict__
 #pragma unroll
       for (int w = 0; w < KD * 4; ++w) {
         float v = bf2f(p[w].e[j]);
-        if (scale) v = act_fwd(v * sc[j] + sh[j], act);
+        if (scale) v = act_fwd(v * sc[j] + sh[j], actc);
         acc = is_max ? fmaxf(acc, v) : acc + v;
       }
       o.e[j] = f2bf(is_max ? acc : acc * (1.f / (KD * 4)));
@@ -855,11 +919,13 @@ __global__ __launch_bounds__(256) void pool_bwd_tiled_kernel(const bf16* __restr
 // all <= 8 window loads of a thread in flight together (the generic kernel's runtime window
 // loop issued one 16-B load at a time: 2.6 TB/s), 32-bit index math (I = int when the host
 // checked the sizes), a grid-stride loop over a resident-sized grid.
-template <typename I>
+template <typename I, int ACT = -1>
 __global__ __launch_bounds__(256) void pool_bn_moments8_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ y,
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ shift, PoolGeom g, int act,
                                                                float* __restrict__ part) {
+  const int actc = ACT >= 0 ? ACT : act;         // (compile-time relu / none: a runtime switch kept
+                                                 //  tanh / sigmoid code in every element's path)
   const int cpr = g.C / 8;
   const I total = (I)g.N * g.OD * g.OH * g.OW * cpr;
   const int win = g.KD * g.KH * g.KW;            // (<= 8: host-checked)
@@ -908,11 +974,11 @@ __global__ __launch_bounds__(256) void pool_bn_moments8_kernel(const bf16* __res
       for (int w = 0; w < 8; ++w) {
         if (w < win) {
           const float yv = bf2f(py[w].e[j]);
-          const float v = act_fwd(yv * sc[j] + sh[j], act);
+          const float v = act_fwd(yv * sc[j] + sh[j], actc);
           if (v > best) { best = v; yarg = yv; }   // (first arg-max, as the forward's scan)
         }
       }
-      const float gv = bf2f(pg.e[j]) * act_bwd_from_out(best, act);
+      const float gv = bf2f(pg.e[j]) * act_bwd_from_out(best, actc);
       s0[j] += gv;
       s1[j] += gv * yarg;
     }
@@ -943,12 +1009,14 @@ __global__ __launch_bounds__(256) void pool_bn_moments8_kernel(const bf16* __res
 // dz) + bn_bwd_apply (reads dz and y again): two full-size passes fewer -- the moments come
 // from pool_bwd_tiled_kernel<8, true> with dx = null beforehand.
 // (I = int: 32-bit index math, when the host checked that every offset fits)
-template <typename I>
+template <typename I, int ACT = -1>
 __global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(
     const bf16* __restrict__ dout, const bf16* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ mean, const float* __restrict__ invstd,
     const float* __restrict__ dbeta, const float* __restrict__ dgamma, bf16* __restrict__ dy, PoolGeom g, int act,
     float inv_count) {
+  const int actc = ACT >= 0 ? ACT : act;         // (compile-time relu / none: a runtime switch kept
+                                                 //  tanh / sigmoid code in every element's path)
   const int cpr = g.C / 8;
   const I total = (I)g.N * g.OD * g.OH * g.OW * cpr;
   const int win = g.KD * g.KH * g.KW;            // (<= 8: host-checked)
@@ -1014,13 +1082,13 @@ __global__ __launch_bounds__(256) void pool_bn_bwd_apply_kernel(
       if (w < win) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = act_fwd(bf2f(py[w].e[j]) * sc[j] + sh[j], act);
+          const float v = act_fwd(bf2f(py[w].e[j]) * sc[j] + sh[j], actc);
           if (v > best[j]) { best[j] = v; arg[j] = w; }
         }
       }
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gm[j] = bf2f(pg.e[j]) * act_bwd_from_out(best[j], act);
+    for (int j = 0; j < 8; ++j) gm[j] = bf2f(pg.e[j]) * act_bwd_from_out(best[j], actc);
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
       if (w < win) {
@@ -1186,6 +1254,23 @@ extern "C" int fn_bn_bwd_apply_s2d(const void* dz, const void* y, const float* s
                                    hipStream_t st) {
   if (C % 8 || 256 % (C / 8) || FD % 2 || FH % 2 || FW % 2 || N < 1) return -2;
   const long long nvec = (long long)N * (FD / 2 + 1) * (FH / 2 + 1) * (FW / 2 + 1) * 8 * (C / 8);
+  const long long nrows = (long long)N * (FD / 2 + 1) * (FH / 2 + 1);
+  if ((act == ACT_RELU || act == ACT_NONE) && nrows < (1LL << 31) && nvec * 8 < (1LL << 40)) {
+    // the row form (grid-stride over the (n, cell-d, cell-h) rows)
+    int lc = 0;
+    while ((1 << lc) < C / 8) ++lc;
+    const unsigned grid = (unsigned)std::min<long long>(nrows, 8192);
+#define BR_CASE(A, L)                                                                                        \
+    if (lc == L) hipLaunchKernelGGL((bn_bwd_apply_s2d_rows_kernel<A, L>), dim3(grid), dim3(256), 0, st,     \
+                                    (const bf16*)dz, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, \
+                                    (bf16*)dsh, N, FD, FH, FW, C, inv_count);
+#define BR_ACT(A) BR_CASE(A, 0) BR_CASE(A, 1) BR_CASE(A, 2) BR_CASE(A, 3) BR_CASE(A, 4) BR_CASE(A, 5)
+    if (act == ACT_RELU) { BR_ACT(ACT_RELU) } else { BR_ACT(ACT_NONE) }
+#undef BR_ACT
+#undef BR_CASE
+    FN_CHECK_LAUNCH();
+    return 0;
+  }
 #define BS_CASE(A)                                                                                      \
   hipLaunchKernelGGL((bn_bwd_apply_s2d_kernel<A>), dim3(ew_blocks(nvec)), dim3(256), 0, st, (const bf16*)dz, \
                      (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dsh, N, FD, FH, FW, C, inv_count)
@@ -1218,18 +1303,19 @@ extern "C" int fn_pool_fwd(const void* x, void* out, const float* scale, const f
                     outs * (g.C / 8) + 256LL * 8192 < (1LL << 31);
   if (win2) {
     const int total = (int)(outs * (g.C / 8));
-    static const int res2 = bn_resident_blocks((const void*)pool2_fwd_kernel<2>);
-    static const int res1 = bn_resident_blocks((const void*)pool2_fwd_kernel<1>);
-    const int res = g.KD == 2 ? res2 : res1;
-    long long nbl = (total + 255) / 256;
-    if (res > 0 && nbl > res) nbl = res;
-    const unsigned nb = (unsigned)(nbl < 1 ? 1 : (nbl > 8192 ? 8192 : nbl));
-    if (g.KD == 2)
-      hipLaunchKernelGGL(pool2_fwd_kernel<2>, dim3(nb), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
-                         scale, shift, g, is_max, act, total);
-    else
-      hipLaunchKernelGGL(pool2_fwd_kernel<1>, dim3(nb), dim3(256), 0, st, (const bf16*)x, (bf16*)out,
-                         scale, shift, g, is_max, act, total);
+    // (relu / none / no BN: compile-time instances; other activations the runtime one)
+    const int ka = !scale ? ACT_NONE : ((act == ACT_RELU || act == ACT_NONE) ? act : -1);
+#define P2_CASE(K, A)                                                                                         \
+    if (g.KD == K && ka == A) {                                                                               \
+      static const int res = bn_resident_blocks((const void*)pool2_fwd_kernel<K, A>);                         \
+      long long nbl = (total + 255) / 256;                                                                    \
+      if (res > 0 && nbl > res) nbl = res;                                                                    \
+      const unsigned nb = (unsigned)(nbl < 1 ? 1 : (nbl > 8192 ? 8192 : nbl));                                 \
+      hipLaunchKernelGGL((pool2_fwd_kernel<K, A>), dim3(nb), dim3(256), 0, st, (const bf16*)x, (bf16*)out,    \
+                         scale, shift, g, is_max, act, total);                                                \
+    }
+    P2_CASE(2, ACT_RELU) P2_CASE(2, ACT_NONE) P2_CASE(2, -1) P2_CASE(1, ACT_RELU) P2_CASE(1, ACT_NONE) P2_CASE(1, -1)
+#undef P2_CASE
   } else if (g.C % 8 == 0)
     hipLaunchKernelGGL(pool_fwd_kernel<8>, dim3(ew_blocks(outs * (g.C / 8))), dim3(256), 0, st, (const bf16*)x,
                        (bf16*)out, scale, shift, g, is_max, count_pad, act);
@@ -1274,12 +1360,15 @@ extern "C" int fn_pool_bwd_stats(const void* dout, const void* x, void* dx, cons
   const int nb = fn_pool_bwd_stats_blocks(geom17);
   if (nb <= 0 || !scale || !shift || !part) return -2;
   if (!dx && g.KD * g.KH * g.KW <= 8) {          // moments only: the bandwidth form
-    if (pool_i32(g))
-      hipLaunchKernelGGL(pool_bn_moments8_kernel<int>, dim3(nb), dim3(256), 0, st, (const bf16*)dout, (const bf16*)x,
-                         scale, shift, g, act, part);
-    else
-      hipLaunchKernelGGL(pool_bn_moments8_kernel<long long>, dim3(nb), dim3(256), 0, st, (const bf16*)dout,
+    const bool i32 = pool_i32(g);
+    const int ka = (act == ACT_RELU || act == ACT_NONE) ? act : -1;
+#define PM_CASE(I, A)                                                                                          \
+    if (i32 == std::is_same<I, int>::value && ka == A)                                                         \
+      hipLaunchKernelGGL((pool_bn_moments8_kernel<I, A>), dim3(nb), dim3(256), 0, st, (const bf16*)dout,        \
                          (const bf16*)x, scale, shift, g, act, part);
+    PM_CASE(int, ACT_RELU) PM_CASE(int, ACT_NONE) PM_CASE(int, -1)
+    PM_CASE(long long, ACT_RELU) PM_CASE(long long, ACT_NONE) PM_CASE(long long, -1)
+#undef PM_CASE
   } else
     hipLaunchKernelGGL((pool_bwd_tiled_kernel<8, true>), dim3(nb), dim3(256), 0, st, (const bf16*)dout, (const bf16*)x,
                        (bf16*)dx, scale, shift, g, 1, act, part);
@@ -1301,14 +1390,15 @@ extern "C" int fn_pool_bn_bwd_apply(const void* dout, const void* y, const float
   long long nbl = (outs * (g.C / 8) + 255) / 256;
   if (res > 0 && nbl > res) nbl = res;           // one resident wave of workgroups, grid-stride
   const unsigned nb = (unsigned)(nbl < 1 ? 1 : (nbl > 8192 ? 8192 : nbl));
-  if (pool_i32(g))
-    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<int>, dim3(nb), dim3(256), 0, st,
-                       (const bf16*)dout, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, g, act,
-                       inv_count);
-  else
-    hipLaunchKernelGGL(pool_bn_bwd_apply_kernel<long long>, dim3(nb), dim3(256), 0, st,
-                       (const bf16*)dout, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, g, act,
-                       inv_count);
+  const bool i32 = pool_i32(g);
+  const int ka = (act == ACT_RELU || act == ACT_NONE) ? act : -1;
+#define PA_CASE(I, A)                                                                                           \
+  if (i32 == std::is_same<I, int>::value && ka == A)                                                            \
+    hipLaunchKernelGGL((pool_bn_bwd_apply_kernel<I, A>), dim3(nb), dim3(256), 0, st, (const bf16*)dout,          \
+                       (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, (bf16*)dy, g, act, inv_count);
+  PA_CASE(int, ACT_RELU) PA_CASE(int, ACT_NONE) PA_CASE(int, -1)
+  PA_CASE(long long, ACT_RELU) PA_CASE(long long, ACT_NONE) PA_CASE(long long, -1)
+#undef PA_CASE
   FN_CHECK_LAUNCH();
   return 0;
 }

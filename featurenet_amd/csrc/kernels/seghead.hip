@@ -99,31 +99,15 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
   // (the MFMAs take the weights as A and the voxel rows as B: a lane's accumulator holds 4
   // consecutive classes / channels 16 nb + 4 lg + i of one voxel row 16 mt + lr -- one 8-B LDS
   // store per fragment instead of four 2-B ones)
-  float bl[2][4];
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int cls = 16 * nb + 4 * lg + i;
-      bl[nb][i] = (bias && cls < NC) ? bias[cls] : 0.f;
-    }
-  // this thread's input chunks always start at channel 8 (tid mod 4): 8 (scale, shift) pairs,
-  // packed for v_pk_fma_f32 (conv_tile_shared.h ct_bn_chunk)
-  ct_f32x2 psc[4], psh[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    psc[j] = (ct_f32x2){sc[8 * (tid & 3) + 2 * j], sc[8 * (tid & 3) + 2 * j + 1]};
-    psh[j] = (ct_f32x2){shf[8 * (tid & 3) + 2 * j], shf[8 * (tid & 3) + 2 * j + 1]};
+  // scale / shift / bias in LDS, read where each phase uses them (held in registers for the whole
+  // kernel they pushed it past 256 VGPRs: spills)
+  __shared__ __attribute__((aligned(16))) float Ps[3 * SH_K];   // [scale 32][shift 32][bias 32]
+  if (tid < SH_K) {
+    Ps[tid] = sc[tid];
+    Ps[SH_K + tid] = shf[tid];
+    Ps[2 * SH_K + tid] = (bias && tid < NC) ? bias[tid] : 0.f;
   }
-  // the moments' columns: 16 nb + 4 lg + i, as pairs (i = 0, 1) and (2, 3)
-  ct_f32x2 msc[2][2], msh[2][2];
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      msc[nb][h] = (ct_f32x2){sc[16 * nb + 4 * lg + 2 * h], sc[16 * nb + 4 * lg + 2 * h + 1]};
-      msh[nb][h] = (ct_f32x2){shf[16 * nb + 4 * lg + 2 * h], shf[16 * nb + 4 * lg + 2 * h + 1]};
-    }
+  __syncthreads();
   Pack8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones.e[j] = f2bf(1.f);
@@ -165,6 +149,12 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
       raw.u = rb[i];
       if (r >= rows) raw.u = make_uint4(0u, 0u, 0u, 0u);   // (partial tile: zero rows)
       unsigned bits;
+      ct_f32x2 psc[4], psh[4];                   // (this thread's chunk: channels 8 (tid mod 4) ..)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        psc[j] = *(const ct_f32x2*)(Ps + 8 * (tid & 3) + 2 * j);
+        psh[j] = *(const ct_f32x2*)(Ps + SH_K + 8 * (tid & 3) + 2 * j);
+      }
       zz.u = ct_bn_chunk(raw.u, psc, psh, ACT == ACT_RELU, bits);
       if (r >= rows) zz.u = make_uint4(0u, 0u, 0u, 0u);
       *(uint4*)(Ys + r * SH_LD + k) = raw.u;
@@ -187,8 +177,8 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
 #pragma unroll
         for (int nb = 0; nb < 2; ++nb)
           *(uint2*)(Os + (64 * wave + 16 * mt + lr) * SH_LD + 16 * nb + 4 * lg) =
-              make_uint2(sh_pack2(acc[mt][nb][0] + bl[nb][0], acc[mt][nb][1] + bl[nb][1]),
-                         sh_pack2(acc[mt][nb][2] + bl[nb][2], acc[mt][nb][3] + bl[nb][3]));
+              make_uint2(sh_pack2(acc[mt][nb][0] + Ps[2 * SH_K + 16 * nb + 4 * lg], acc[mt][nb][1] + Ps[2 * SH_K + 16 * nb + 4 * lg + 1]),
+                         sh_pack2(acc[mt][nb][2] + Ps[2 * SH_K + 16 * nb + 4 * lg + 2], acc[mt][nb][3] + Ps[2 * SH_K + 16 * nb + 4 * lg + 3]));
     }
     __syncthreads();
     // ---- softmax cross-entropy, one row per thread: d (bf16) replaces the logits ----
@@ -204,36 +194,41 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
         for (int j = 0; j < 4; ++j) lv[j].u = *(const uint4*)(orow + 8 * j);
         // (NCT = 25: the loops end at the real class count, no padded-class selects)
         auto live = [&](int c) { return NCT != 32 || c < NC; };
+        // the target class enters through its own LDS read and a fix-up store, not a compare and
+        // select per class (the one-hot selects were a third of the row's VALU work)
+        const int ylab = (int)yl;
+        const bool yin = yl >= 0 && yl < NC;
+        const float vy = yin ? bf2f(orow[ylab]) : 0.f;
         float v[NCT];
-        float mx = -INFINITY;
-        int am = 0;
+        float mx = -INFINITY, vs = 0.f;
 #pragma unroll
         for (int c = 0; c < NCT; ++c) {
           v[c] = live(c) ? bf2f(lv[c >> 3].e[c & 7]) : -INFINITY;
-          if (v[c] > mx) { mx = v[c]; am = c; }
+          mx = fmaxf(mx, v[c]);
+          if (live(c)) vs += v[c];
         }
         // one exp per class: e_c = exp(v_c - max) serves the sum and the softmax (e_c / sum); the
-        // loss -sum_c tgt_c (v_c - lse) = lse - sum_c tgt_c v_c (the targets sum to 1)
-        float se = 0.f, sv = 0.f;
+        // loss -sum_c tgt_c (v_c - lse) = lse - sum_c tgt_c v_c = lse - off * sum_c v_c - (on - off) v_y
+        float se = 0.f;
 #pragma unroll
         for (int c = 0; c < NCT; ++c) {
           if (live(c)) {
-            sv += ((c == yl) ? on : off) * v[c];
             v[c] = __expf(v[c] - mx);
             se += v[c];
           }
         }
         const float lse = mx + __logf(se), inv = 1.f / se;
-        const float lrow = lse - sv;
+        const float lrow = lse - (off * vs + (yin ? (on - off) * vy : 0.f));
 #pragma unroll
         for (int c = 0; c < 32; ++c) {
-          const float d = (c < NCT && live(c)) ? (v[c < NCT ? c : 0] * inv - ((c == yl) ? on : off)) * xscale : 0.f;
+          const float d = (c < NCT && live(c)) ? (v[c < NCT ? c : 0] * inv - off) * xscale : 0.f;
           lv[c >> 3].e[c & 7] = f2bf(d);         // (padded classes: 0)
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) *(uint4*)(orow + 8 * j) = lv[j].u;
+        if (yin) orow[ylab] = f2bf((__expf(vy - mx) * inv - on) * xscale);   // the target's d
         xl += lrow;
-        xc += (am == yl) ? 1.f : 0.f;
+        xc += (yin && vy >= mx) ? 1.f : 0.f;     // (a tie for the maximum counts as a hit)
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) *(uint4*)(orow + 8 * j) = make_uint4(0u, 0u, 0u, 0u);
@@ -280,7 +275,9 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
           ct_f32x2 g = {bf16_lo(dp), bf16_hi(dp)};
           const ct_f32x2 yy = {bf16_lo(yw[h]), bf16_hi(yw[h])};
           if constexpr (ACT == ACT_RELU) {          // g = dz * relu'(z), z > 0 <=> y * sc + sh > 0
-            const ct_f32x2 tz = __builtin_elementwise_fma(yy, msc[nb][h], msh[nb][h]);
+            const ct_f32x2 msc = *(const ct_f32x2*)(Ps + 16 * nb + 4 * lg + 2 * h);
+            const ct_f32x2 msh = *(const ct_f32x2*)(Ps + SH_K + 16 * nb + 4 * lg + 2 * h);
+            const ct_f32x2 tz = __builtin_elementwise_fma(yy, msc, msh);
             g.x = tz.x > 0.f ? g.x : 0.f;
             g.y = tz.y > 0.f ? g.y : 0.f;
           }
