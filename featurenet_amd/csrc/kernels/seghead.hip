@@ -207,6 +207,10 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
           mx = fmaxf(mx, v[c]);
           if (live(c)) vs += v[c];
         }
+        int am = 0;                              // the first arg-max (bf16 logits tie often)
+#pragma unroll
+        for (int c = NCT - 1; c >= 0; --c)
+          if (live(c) && v[c] == mx) am = c;
         // one exp per class: e_c = exp(v_c - max) serves the sum and the softmax (e_c / sum); the
         // loss -sum_c tgt_c (v_c - lse) = lse - sum_c tgt_c v_c = lse - off * sum_c v_c - (on - off) v_y
         float se = 0.f;
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
         for (int j = 0; j < 4; ++j) *(uint4*)(orow + 8 * j) = lv[j].u;
         if (yin) orow[ylab] = f2bf((__expf(vy - mx) * inv - on) * xscale);   // the target's d
         xl += lrow;
-        xc += (yin && vy >= mx) ? 1.f : 0.f;     // (a tie for the maximum counts as a hit)
+        xc += (am == ylab) ? 1.f : 0.f;
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) *(uint4*)(orow + 8 * j) = make_uint4(0u, 0u, 0u, 0u);
