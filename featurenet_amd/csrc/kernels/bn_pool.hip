@@ -558,26 +558,37 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_s2d_rows_kernel(const bf16* 
     const int chh = row % H2, r2 = row / H2;
     const int cd = r2 % D2, n = r2 / D2;
     bf16* orow = dsh + (long long)row * rowlen * 8;
-    for (int t = threadIdx.x; t < rowlen; t += 256) {
-      const int jp = (t >> LCPR) & 7, cw = t >> (LCPR + 3);
-      const int qd = 2 * cd - 1 + (jp >> 2), qh = 2 * chh - 1 + ((jp >> 1) & 1), qw = 2 * cw - 1 + (jp & 1);
-      Pack8 po;
-      if ((unsigned)qd < (unsigned)FD && (unsigned)qh < (unsigned)FH && (unsigned)qw < (unsigned)FW) {
-        const long long off = ((((long long)n * FD + qd) * FH + qh) * FW + qw) * C + k * 8;
-        Pack8 py, pd;
-        py.u = *(const uint4*)(y + off);
-        pd.u = *(const uint4*)(dz + off);
+    // four chunks per thread per pass, their eight loads issued before any is used
+    for (int t0 = threadIdx.x; t0 < rowlen; t0 += 4 * 256) {
+      Pack8 py[4], pd[4];
+      bool in[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float yv = bf2f(py.e[j]);
-          const float zv = act_fwd(yv * sc[j] + sh[j], act);
-          const float g = bf2f(pd.e[j]) * act_bwd_from_out(zv, act);
-          po.e[j] = f2bf(sc[j] * g + k2[j] * yv + k3[j]);
-        }
-      } else {
-        po.u = make_uint4(0u, 0u, 0u, 0u);
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * 256;
+        const int jp = (t >> LCPR) & 7, cw = t >> (LCPR + 3);
+        const int qd = 2 * cd - 1 + (jp >> 2), qh = 2 * chh - 1 + ((jp >> 1) & 1), qw = 2 * cw - 1 + (jp & 1);
+        in[u] = t < rowlen && (unsigned)qd < (unsigned)FD && (unsigned)qh < (unsigned)FH && (unsigned)qw < (unsigned)FW;
+        const long long off = in[u] ? ((((long long)n * FD + qd) * FH + qh) * FW + qw) * C + k * 8 : 0;
+        py[u].u = *(const uint4*)(y + off);
+        pd[u].u = *(const uint4*)(dz + off);
       }
-      *(uint4*)(orow + t * 8) = po.u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * 256;
+        Pack8 po;
+        if (in[u]) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float yv = bf2f(py[u].e[j]);
+            const float zv = act_fwd(yv * sc[j] + sh[j], act);
+            const float g = bf2f(pd[u].e[j]) * act_bwd_from_out(zv, act);
+            po.e[j] = f2bf(sc[j] * g + k2[j] * yv + k3[j]);
+          }
+        } else {
+          po.u = make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (t < rowlen) *(uint4*)(orow + t * 8) = po.u;
+      }
     }
   }
 }

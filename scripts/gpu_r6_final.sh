@@ -16,6 +16,9 @@ if [ "$1" = suite ]; then
   tail -n 1 gpurun_out/final_smoke.log
   exit 0
 fi
+timeout -k 10 300 python -u -m pytest tests/test_subpixel_gpu.py -q -m gpu --timeout 200 --timeout-method thread \
+  -p no:cacheprovider > gpurun_out/final_subpixel.log 2>&1 || { tail -5 gpurun_out/final_subpixel.log; exit 1; }
+tail -n 1 gpurun_out/final_subpixel.log
 for i in 1 2 3; do
   timeout -k 10 150 python bench.py --steps 30 --warmup 5 > gpurun_out/final_bench_$i.log 2>&1 || exit $?
   tail -n 1 gpurun_out/final_bench_$i.log | cut -c1-160
