@@ -391,13 +391,7 @@ def part_scratch(n: int, device) -> torch.Tensor:
 def halo_sched(device, stream: int) -> torch.Tensor:
     """int32[64] tile-schedule counters of the halo kernel (one buffer per device and stream:
     kernels on one stream run in order, and every launch leaves the counters zero)."""
-    key = (str(device), stream)
-    t = _SCHED.get(key)
-    if t is None:
-        t = torch.zeros(64, dtype=torch.int32, device=device)
-        with _TAB_LOCK:
-            _SCHED[key] = t
-    return t
+    return conv_tile.counters(_SCHED, _TAB_LOCK, device, stream, 64)
 
 
 def halo_conv_wgrad(dy5, x5, spec: ConvSpec, plan, target_wgs: int = 512, out=None) -> torch.Tensor:

@@ -465,15 +465,28 @@ def zero_page(device) -> torch.Tensor:
     return _dev_cached(_ZERO, device, lambda: torch.zeros(64, dtype=torch.bfloat16, device=device))
 
 
-def sched(device, stream: int) -> torch.Tensor:
+def counters(cache: dict, lock, device, stream: int, n: int) -> torch.Tensor:
+    """Zeroed int32 schedule counters, one buffer per (device, stream) -- kernels on one stream run
+    in order and every launch leaves its counters zero.  Under hipGraph capture a stream's first
+    use would record the zero fill into the graph (a fill kernel in every replay): the capture
+    takes the device's eagerly made buffer instead (a captured step and eager launches on the same
+    device do not run concurrently)."""
     key = (str(device), stream)
-    t = _SCHED.get(key)
+    t = cache.get(key)
     if t is None:
-        # (conv_tile's dynamic schedules: a done counter + 8 XCD queue counters per column block)
-        t = torch.zeros(1024, dtype=torch.int32, device=device)
-        with _LOCK:
-            _SCHED[key] = t
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            for (dev, _), u in list(cache.items()):
+                if dev == str(device) and u.numel() == n:
+                    return u
+        t = torch.zeros(n, dtype=torch.int32, device=device)
+        with lock:
+            cache[key] = t
     return t
+
+
+def sched(device, stream: int) -> torch.Tensor:
+    # (conv_tile's dynamic schedules: a done counter + 8 XCD queue counters per column block)
+    return counters(_SCHED, _LOCK, device, stream, 1024)
 
 
 def rowtab_tensor(p: TilePlan, kdims: tuple, device) -> torch.Tensor:

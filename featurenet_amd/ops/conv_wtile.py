@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from . import conv_tile
 
 LDS_MAX = 160 * 1024
 N_CUS = 256
@@ -312,7 +313,7 @@ def conv_wgrad_subpixel(dsh: torch.Tensor, x5: torch.Tensor, p: WPlan) -> torch.
     pt = _dev(_TABS, ("pt", p, kd, str(dev)), lambda: torch.from_numpy(pt_np).to(dev))
     zp = _dev(_ZERO, str(dev), lambda: torch.zeros(64, dtype=torch.bfloat16, device=dev))
     st = _native.stream(x5)
-    sched = _dev(_SCHED, (str(dev), st), lambda: torch.zeros(64, dtype=torch.int32, device=dev))
+    sched = conv_tile.counters(_SCHED, _LOCK, dev, st, 64)
     dw = torch.zeros(8 * K, 8, C, dtype=torch.float32, device=dev)
     part = _partials(dev, st, 8 * p.workers * dw.numel())
     geom = [N, D, H, W, C, D, H, W, K, 3, 3, 3, 1, 1, 1, p.TD, p.TH, p.TW, p.HPpad, p.kst, 2 * p.HPpad * 32, p.BUF,
@@ -357,7 +358,7 @@ def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None, wd
     pt = _dev(_TABS, ("pt", p, kd, str(dev)), lambda: torch.from_numpy(pt_np).to(dev))
     zp = _dev(_ZERO, str(dev), lambda: torch.zeros(64, dtype=torch.bfloat16, device=dev))
     st = _native.stream(x5)
-    sched = _dev(_SCHED, (str(dev), st), lambda: torch.zeros(64, dtype=torch.int32, device=dev))
+    sched = conv_tile.counters(_SCHED, _LOCK, dev, st, 64)
     dw = out if out is not None else torch.zeros(spec.K, spec.taps, spec.C, dtype=torch.float32, device=dev)
     part = _partials(dev, st, 8 * p.workers * (2 if p.ks2 else 1) * dw.numel())
     wsrc = wdp = None
