@@ -1242,6 +1242,13 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
       d[2] = st_e;
       d[6] = stamp() - st_0;
     }
+    if (lane == 0 && wave == 1) {                // (compute wave 1, alone on SIMD 1: slots 3, 4, 5, 7)
+      long long* d = stamps + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 16;
+      d[3] = st_a;
+      d[4] = st_k;
+      d[5] = st_e;
+      d[7] = stamp() - st_0;
+    }
   }
   if (tid == 0 && !stat_static) {                // the last workgroup out resets the counters
     __threadfence();                             // (static schedules never touch them)
@@ -1525,6 +1532,8 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
         fprintf(stderr,
                 "[conv_tile stamps MT8 CPP%d dbg%d %s] barrierA %.0f job %.0f epilogue %.0f | total %.0f\n", CPP, dbg,
                 w ? "loader" : "wave0 ", m[8 * w], m[8 * w + 1], m[8 * w + 2], m[8 * w + 6]);
+      fprintf(stderr, "[conv_tile stamps MT8 CPP%d dbg%d wave1 ] barrierA %.0f job %.0f epilogue %.0f | total %.0f\n",
+              CPP, dbg, m[3], m[4], m[5], m[7]);
     }
     return 0;
   }
