@@ -125,6 +125,7 @@ int fn_conv_tile_f8_supported(int, int, int);
 int fn_conv_wtile(const void*, const void*, float*, float*, const void*, const void*, const void*, const int*, int, int,
                   int*, hipStream_t, const float*, float*, const float*, int);
 int fn_conv_wtile_supported(int, int);
+int fn_conv_wtile_prologue_built();
 int fn_tile_pack_w(const float*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 int fn_tile_pack_w2(const float*, void*, void*, int, int, int, const int*, const int*, hipStream_t);
 }
@@ -352,6 +353,7 @@ PYBIND11_MODULE(_C, m) {
      py::arg("ext") = std::vector<long long>(), py::arg("wsrc") = 0, py::arg("wdp") = 0, py::arg("pst") = 0,
      py::arg("pact") = 0);
   m.def("conv_wtile_supported", &fn_conv_wtile_supported);
+  m.def("conv_wtile_prologue_built", &fn_conv_wtile_prologue_built);
   m.def("conv_tile_workers", [](std::vector<int> geom, int ncol, int NT) {
     need(geom, 31, "conv_tile_workers");
     return fn_conv_tile_workers(geom.data(), ncol, NT);

@@ -76,8 +76,13 @@
 // LDS-DMAs (one copy per workgroup instead of one per compute wave through L1), with per-k-step
 // counters in LDS for the hand-off (see the loader); wring = 0 / WL false: every compute wave
 // streams the fragments global -> VGPRs itself (the PD-deep register ring).
+// PRO: the BN prologue instances (xform_job below; opt-in, measured slower) -- a template flag so the
+// default instances carry none of its code (it doubled their SGPR spills)
+// CHK: the instances with the chunked BN-statistics schedule (data parallelism); the others run the
+// static one only (the chunk walk's state cost the one-GPU instances ~25 SGPR spills and 1-4 % of
+// their time)
 template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false,
-          int NCW = CT_NCW, bool WL = false>
+          int NCW = CT_NCW, bool WL = false, bool PRO = false, bool CHK = true>
 __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsigned char* __restrict__ src,
                                                                const uint4* __restrict__ wp,
                                                                const int2* __restrict__ rowtab,
@@ -273,7 +278,7 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   // channels (pmask, bit j = z_j > 0: the statistics identity of the backward, ops/bnfuse.py).
   // bn_apply's separate pass over y -- and its re-read of y here -- disappears.
   auto xform_job = [&](int tile, int slice, int bufoff) {
-    if constexpr (!F8) {
+    if constexpr (!F8 && PRO) {
       if (!pst) return;
       int t = __builtin_amdgcn_readfirstlane(tile);
       const int tw_ = t % twn; t /= twn;
@@ -385,8 +390,8 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   //   * chunk == 0: the round-5 STATIC schedule (job k = tile k * G + slot, slots XCD-major;
   //     per-workgroup partial rows), kept for the A/B of that measurement: a CU held by another
   //     kernel there delays its workgroup's whole fixed share.
-  const bool stat_static = stats != nullptr && chunk <= 0;
-  const bool stat_chunk = stats != nullptr && chunk > 0;
+  const bool stat_static = stats != nullptr && (!CHK || chunk <= 0);
+  const bool stat_chunk = CHK && stats != nullptr && chunk > 0;
   const int G = (int)gridDim.x;
   const int slot = (G & 7) == 0 ? ((int)blockIdx.x & 7) * (G >> 3) + ((int)blockIdx.x >> 3) : (int)blockIdx.x;
   const int nchunk = stat_chunk ? (ntiles + chunk - 1) / chunk : 0;
@@ -1386,7 +1391,7 @@ extern "C" int fn_conv_tile_slab_rows(const int* geom, int Ncol, int NT) {
 }
 
 template <int MT, int NT, int CPP, int DBG = 0, bool F8 = false, bool Q8O = false, bool I8 = false, bool BS = false,
-          int NCW = CT_NCW, bool WL = false>
+          int NCW = CT_NCW, bool WL = false, bool PRO = false, bool CHK = true>
 static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, const uint4* w, const int2* rt,
                        const int4* kt, const void* zp, const float* b, void* o, float* stats, const TileGeom& g,
                        int Ncol, int act, int* sched, long long* stamps = nullptr, const float* scale = nullptr,
@@ -1395,12 +1400,12 @@ static int launch_tile(dim3 grid, size_t lds, hipStream_t st, const void* s, con
                        void* pz = nullptr, void* pmask = nullptr, int pact = 0) {
   static size_t configured = 0;
   if (lds > configured) {
-    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW, WL>,
+    hipError_t e = hipFuncSetAttribute((const void*)conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW, WL, PRO, CHK>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
     configured = lds;
   }
-  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW, WL>), grid, dim3(64 * (NCW + 1)), lds,
+  hipLaunchKernelGGL((conv_tile_kernel<MT, NT, CPP, DBG, F8, Q8O, I8, BS, NCW, WL, PRO, CHK>), grid, dim3(64 * (NCW + 1)), lds,
                      st, (const unsigned char*)s, w, rt, kt, (const unsigned char*)zp, b, o, stats, g, Ncol, act,
                      sched, stamps, scale, oscale, (const unsigned char*)gmask, (const unsigned*)xsc,
                      (unsigned char*)osc, chunk, wring, pst, (bf16*)pz, (unsigned char*)pmask, pact);
@@ -1512,7 +1517,7 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
     if ((dbg & 16) && hipMemsetAsync(stamps, 0, nst * sizeof(long long), st) != hipSuccess) return -5;
 #define CT_DBG(C, D) if (CPP == C && dbg == D) rc = launch_tile<8, 2, C, D>(grid, lds, st, src, \
       (const uint4*)wp, (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, stamps, \
-      nullptr, 0.f, bny, nullptr, nullptr, stats ? tile_chunk(g) : 0, 0, pst, pz, pmask, pact);
+      nullptr, 0.f, bny, nullptr, nullptr, stats ? tile_chunk(g) : 0);
     CT_DBG(1, 1) CT_DBG(1, 2) CT_DBG(1, 4) CT_DBG(1, 16)   // (the space-to-depth stem)
     CT_DBG(1, 8) CT_DBG(1, 24) CT_DBG(2, 8) CT_DBG(2, 24)
     CT_DBG(2, 1) CT_DBG(2, 2) CT_DBG(2, 4) CT_DBG(2, 3) CT_DBG(2, 7) CT_DBG(2, 16) CT_DBG(4, 16) CT_DBG(2, 23)
@@ -1552,10 +1557,22 @@ extern "C" int fn_conv_tile(const void* src, const void* wp, const void* rowtab,
                                      (const int2*)rowtab, (const int4*)ktab, zp, bias, out, stats, g, Ncol, act,       \
                                      sched, nullptr, nullptr, 0.f, bny, nullptr, nullptr, stats ? tile_chunk(g) : 0,   \
                                      wring)                                                                            \
-                               : launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,       \
-                                                      (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched,    \
-                                                      nullptr, nullptr, 0.f, bny, nullptr, nullptr,                    \
-                                                      stats ? tile_chunk(g) : 0, 0, pst, pz, pmask, pact));
+                               : (pst ? launch_tile<M, N, C, 0, false, false, false, false, CT_NCW, false, true>(      \
+                                            grid, lds, st, src, (const uint4*)wp, (const int2*)rowtab,                 \
+                                            (const int4*)ktab, zp, bias, out, stats, g, Ncol, act, sched, nullptr,     \
+                                            nullptr, 0.f, bny, nullptr, nullptr, stats ? tile_chunk(g) : 0, 0, pst, pz, \
+                                            pmask, pact)                                                              \
+                                      : ((stats && tile_chunk(g) > 0)                                          \
+                                             ? launch_tile<M, N, C>(grid, lds, st, src, (const uint4*)wp,              \
+                                                                    (const int2*)rowtab, (const int4*)ktab, zp, bias,  \
+                                                                    out, stats, g, Ncol, act, sched, nullptr, nullptr, \
+                                                                    0.f, bny, nullptr, nullptr, tile_chunk(g))         \
+                                             : launch_tile<M, N, C, 0, false, false, false, false, CT_NCW, false,      \
+                                                           false, false>(grid, lds, st, src, (const uint4*)wp,         \
+                                                                         (const int2*)rowtab, (const int4*)ktab, zp,   \
+                                                                         bias, out, stats, g, Ncol, act, sched,        \
+                                                                         nullptr, nullptr, 0.f, bny, nullptr,          \
+                                                                         nullptr, 0))));
   CT_INSTANCES(CT_CASE)
 #undef CT_CASE
   if (rc) return rc;

@@ -300,7 +300,10 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
   // z.  Whoever DMA'd a job's x slots rewrites them in LDS once they have landed (the loader, or
   // in the loaderless form each wave its own 1/NW), with bn_apply_kernel's fma, activation and
   // rounding; zero-page slots (padding) stay zero.
+  // (experiment builds only: in the default instances this code raised the VGPR count and doubled
+  // the SGPR spills of the weight-gradient kernels the FeatureNet-3D step runs)
   auto xform_x = [&](int tile, int bufoff, int first, int step) {
+#ifdef FN_EXPERIMENTS
     if constexpr (!SP && !C8) {
       if (!pst) return;
       tile = __builtin_amdgcn_readfirstlane(tile);
@@ -337,6 +340,9 @@ __global__ __launch_bounds__(wt_nthr(NW), 1) void conv_wtile_kernel(const bf16* 
         e = en;
       }
     }
+#else
+    (void)tile; (void)bufoff; (void)first; (void)step;
+#endif
   };
 
   if constexpr (!HAS_LOADER) {                  // job 0, 1/NW of it by each wave
@@ -732,6 +738,15 @@ static size_t wtile_lds(const WGeom& g) {
   return 2 * (size_t)g.BUF + 64 + (size_t)g.kst * 32 * 12 + (size_t)g.HPpad * 8;
 }
 
+// the BN prologue of the x halos is compiled into experiment builds only (FN_BUILD_EXPERIMENTS=1)
+extern "C" int fn_conv_wtile_prologue_built() {
+#ifdef FN_EXPERIMENTS
+  return 1;
+#else
+  return 0;
+#endif
+}
+
 extern "C" int fn_conv_wtile_supported(int K, int nacc) {
   const int c8 = (nacc >> 12) & 1, ks2 = (nacc >> 13) & 1, sp = (nacc >> 14) & 1;
   const int nw = (nacc >> 8) & 15;
@@ -762,7 +777,7 @@ extern "C" int fn_conv_wtile(const void* x, const void* dy, float* dw, float* pa
   const int nw = ((nacc >> 8) & 15) == 8 ? 8 : 4;
   if (!fn_conv_wtile_supported(g.K, nacc)) return -2;
   // the BN prologue (x = pre-BN y; pst = [scale C][shift C]): 16-channel slices only, act none / relu
-  if (pst && (c8 || sp || pact != ACT_RELU)) return -2;   // (relu only)
+  if (pst && (c8 || sp || pact != ACT_RELU || !fn_conv_wtile_prologue_built())) return -2;   // (relu only)
   nacc &= 255;
   const int xr = c8 ? 16 : 32, tpf = c8 ? 2 : 1;
   if ((c8 ? g.C != 8 : g.C % (sp ? 32 : 16)) || g.TD < 1 || g.TH < 1 || g.TW < 1) return -2;

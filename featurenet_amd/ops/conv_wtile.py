@@ -339,8 +339,8 @@ def flags(p: WPlan) -> int:
 
 def prologue_ok(p: WPlan) -> bool:
     """The plan's kernel form can normalise its x halos itself (BN prologue: 16-channel slices --
-    not the 8-channel space-to-depth stem form nor the sub-pixel form)."""
-    return not p.c8 and not p.sp
+    not the 8-channel space-to-depth stem form nor the sub-pixel form; experiment builds only)."""
+    return not p.c8 and not p.sp and bool(_native.kernels().conv_wtile_prologue_built())
 
 
 def conv_wgrad(dy5: torch.Tensor, x5: torch.Tensor, spec, p: WPlan, out=None, wdot=None, pro=None):
