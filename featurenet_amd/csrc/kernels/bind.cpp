@@ -29,7 +29,7 @@ int fn_seghead_part_len();
 int fn_part_reduce(const float*, float*, long long, int, int, hipStream_t);
 int fn_seghead_blocks(long long);
 int fn_seghead_loss(const void*, const float*, const float*, const void*, const float*, const void*, void*, float*,
-                    long long, int, int, int, float, float, hipStream_t, int);
+                    long long, int, int, int, float, float, hipStream_t, int, int);
 int fn_pw_xent_blocks(long long);
 int fn_pw_fwd_xent(const void*, const void*, const float*, void*, long long, int, int, const float*, const float*, int,
                    const long long*, float*, float, float, hipStream_t);
@@ -609,7 +609,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("seghead_blocks", &fn_seghead_blocks);
   m.def("seghead_loss", [](uintptr_t y, uintptr_t sc, uintptr_t sh, uintptr_t w, uintptr_t bias, uintptr_t labels,
                            uintptr_t dz, uintptr_t part, long long M, int K, int NC, int act, float xscale,
-                           float smoothing, uintptr_t st, std::vector<long long> ext, int lab8) {
+                           float smoothing, uintptr_t st, std::vector<long long> ext, int lab8, int hits) {
     fits(ext, 0, M * K, "seghead_loss", "y");
     fits(ext, 1, (long long)NC * K, "seghead_loss", "w");
     fits(ext, 2, M, "seghead_loss", "labels");
@@ -617,11 +617,11 @@ PYBIND11_MODULE(_C, m) {
     fits(ext, 4, (long long)fn_seghead_blocks(M) * fn_seghead_part_len(), "seghead_loss", "part");
     chk(fn_seghead_loss(P<const void*>(y), P<const float*>(sc), P<const float*>(sh), P<const void*>(w),
                         P<const float*>(bias), P<const void*>(labels), P<void*>(dz), P<float*>(part), M, K, NC,
-                        act, xscale, smoothing, S(st), lab8),
+                        act, xscale, smoothing, S(st), lab8, hits),
         "seghead_loss");
   }, py::arg("y"), py::arg("sc"), py::arg("sh"), py::arg("w"), py::arg("bias"), py::arg("labels"), py::arg("dz"),
      py::arg("part"), py::arg("M"), py::arg("K"), py::arg("NC"), py::arg("act"), py::arg("xscale"),
-     py::arg("smoothing"), py::arg("st"), py::arg("ext"), py::arg("lab8") = 0);
+     py::arg("smoothing"), py::arg("st"), py::arg("ext"), py::arg("lab8") = 0, py::arg("hits") = 1);
   m.def("pw_fwd_xent", [](uintptr_t x, uintptr_t w, uintptr_t bias, uintptr_t dlog, long long M, int K, int N,
                           uintptr_t psc, uintptr_t psh, int pact, uintptr_t labels, uintptr_t xpart, float xscale,
                           float smoothing, uintptr_t st, std::vector<long long> ext) {

@@ -37,10 +37,12 @@ __host__ __device__ constexpr int ct_red_bytes(int NT, int ncw = CT_NCW, bool f8
 // packed bf16 pairs (low half = element 0)
 __device__ __forceinline__ float bf16_lo(unsigned w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(unsigned w) { return __uint_as_float(w & 0xffff0000u); }
+// (one vector conversion: a pair of scalar f2bf's feeding bit operations is emitted as two
+// half-empty v_cvt_pk_bf16_f32 and a v_perm_b32; the vector form is one v_cvt_pk_bf16_f32, same RNE bits)
 __device__ __forceinline__ unsigned bf16x2_pack(float lo, float hi) {
   typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-  const bf16x2_t p = {f2bf(lo), f2bf(hi)};
-  return __builtin_bit_cast(unsigned, p);
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
 }
 
 // sum over the 16 lanes of a DPP row (every lane of the row gets it): quad swaps, then

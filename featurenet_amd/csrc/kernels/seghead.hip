@@ -26,6 +26,8 @@
 #include "common.h"
 #include "conv_tile_shared.h"
 
+#include <type_traits>
+
 #define SH_BM 256
 #define SH_NTHR 256
 #define SH_K 32                                  // decoder channels (the head's input)
@@ -48,11 +50,7 @@ __device__ __forceinline__ sh_s4 sh_tr4(const bf16* p) {
 }
 
 __device__ __forceinline__ float sh_bf(short s) { return __uint_as_float(((unsigned)(unsigned short)s) << 16); }
-__device__ __forceinline__ unsigned sh_pack2(float lo, float hi) {
-  typedef __bf16 sh_b2 __attribute__((ext_vector_type(2)));
-  const sh_b2 p = {f2bf(lo), f2bf(hi)};
-  return __builtin_bit_cast(unsigned, p);
-}
+__device__ __forceinline__ unsigned sh_pack2(float lo, float hi) { return bf16x2_pack(lo, hi); }
 __device__ __forceinline__ float bf16_round(float x) { return bf2f(f2bf(x)); }
 
 // ACT: the decoder BN's activation (ACT_NONE / ACT_RELU); LT: the label type (int64, or uint8 --
@@ -61,8 +59,10 @@ __device__ __forceinline__ float bf16_round(float x) { return bf2f(f2bf(x)); }
 // dz [M][32] bf16 out; part: per workgroup [loss, hits | db[32] | dWt[32][32] | msum[32] | msq[32]]
 // (fp32; dWt[ch][cls] = sum z[r][ch] d[r][cls]).
 // NCT: the class count when it is 25 (the FeatureNet3DSeg head: loops of exactly 25 classes, 25
-// live logits per row), 32 for any NC <= 32 (runtime bound)
-template <int ACT, typename LT, int NCT = 32>
+// live logits per row), 32 for any NC <= 32 (runtime bound).  XF: the extras -- top-1 hits and label
+// smoothing; the lean instance (a training step that asks for neither, smoothing == 0) skips the
+// arg-max and the logit sum, a third of the row's VALU work.
+template <int ACT, typename LT, int NCT = 32, bool XF = true>
 __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __restrict__ y,
                                                                  const float* __restrict__ sc,
                                                                  const float* __restrict__ shf,
@@ -142,24 +142,32 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
   for (; t < ntiles; t += gridDim.x) {
     const int rows = (int)(M - (long long)t * SH_BM < SH_BM ? M - (long long)t * SH_BM : SH_BM);
     __syncthreads();                             // the previous tile's LDS readers are done
+    // y and z = act(y*sc + sh) into LDS; the zero rows of a partial tile in their own (uniform)
+    // branch, so full tiles carry no per-dword selects
+    auto stage = [&](auto partial) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = i * SH_NTHR + tid, r = c >> 2, k = (c & 3) * 8;
-      Pack8 raw, zz;
-      raw.u = rb[i];
-      if (r >= rows) raw.u = make_uint4(0u, 0u, 0u, 0u);   // (partial tile: zero rows)
-      unsigned bits;
-      ct_f32x2 psc[4], psh[4];                   // (this thread's chunk: channels 8 (tid mod 4) ..)
+      for (int i = 0; i < 4; ++i) {
+        const int c = i * SH_NTHR + tid, r = c >> 2, k = (c & 3) * 8;
+        Pack8 raw, zz;
+        raw.u = rb[i];
+        if constexpr (decltype(partial)::value)
+          if (r >= rows) raw.u = make_uint4(0u, 0u, 0u, 0u);
+        unsigned bits;
+        ct_f32x2 psc[4], psh[4];                 // (this thread's chunk: channels 8 (tid mod 4) ..)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        psc[j] = *(const ct_f32x2*)(Ps + 8 * (tid & 3) + 2 * j);
-        psh[j] = *(const ct_f32x2*)(Ps + SH_K + 8 * (tid & 3) + 2 * j);
+        for (int j = 0; j < 4; ++j) {
+          psc[j] = *(const ct_f32x2*)(Ps + 8 * (tid & 3) + 2 * j);
+          psh[j] = *(const ct_f32x2*)(Ps + SH_K + 8 * (tid & 3) + 2 * j);
+        }
+        zz.u = ct_bn_chunk(raw.u, psc, psh, ACT == ACT_RELU, bits);
+        if constexpr (decltype(partial)::value)
+          if (r >= rows) zz.u = make_uint4(0u, 0u, 0u, 0u);
+        *(uint4*)(Ys + r * SH_LD + k) = raw.u;
+        *(uint4*)(Zs + r * SH_LD + k) = zz.u;
       }
-      zz.u = ct_bn_chunk(raw.u, psc, psh, ACT == ACT_RELU, bits);
-      if (r >= rows) zz.u = make_uint4(0u, 0u, 0u, 0u);
-      *(uint4*)(Ys + r * SH_LD + k) = raw.u;
-      *(uint4*)(Zs + r * SH_LD + k) = zz.u;
-    }
+    };
+    if (rows == SH_BM) stage(std::false_type{});
+    else stage(std::true_type{});
     __syncthreads();
     if (t + gridDim.x < ntiles) load(t + gridDim.x);   // next tile in flight
     // ---- logits = z W^T + b: wave rows 64 wave + 16 mt ----
@@ -188,7 +196,7 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
       bf16* orow = Os + tid * SH_LD;
       if (tid < rows) {
         const long long yl = (long long)labels[(long long)t * SH_BM + tid];
-        const float off = smoothing / (float)NC, on = 1.f - smoothing + off;
+        const float off = XF ? smoothing / (float)NC : 0.f, on = XF ? 1.f - smoothing + off : 1.f;
         Pack8 lv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) lv[j].u = *(const uint4*)(orow + 8 * j);
@@ -205,34 +213,54 @@ __global__ __launch_bounds__(SH_NTHR, 2) void seghead_loss_kernel(const bf16* __
         for (int c = 0; c < NCT; ++c) {
           v[c] = live(c) ? bf2f(lv[c >> 3].e[c & 7]) : -INFINITY;
           mx = fmaxf(mx, v[c]);
-          if (live(c)) vs += v[c];
+          if constexpr (XF)
+            if (live(c)) vs += v[c];
         }
         int am = 0;                              // the first arg-max (bf16 logits tie often)
+        if constexpr (XF) {
 #pragma unroll
-        for (int c = NCT - 1; c >= 0; --c)
-          if (live(c) && v[c] == mx) am = c;
-        // one exp per class: e_c = exp(v_c - max) serves the sum and the softmax (e_c / sum); the
-        // loss -sum_c tgt_c (v_c - lse) = lse - sum_c tgt_c v_c = lse - off * sum_c v_c - (on - off) v_y
-        float se = 0.f;
-#pragma unroll
-        for (int c = 0; c < NCT; ++c) {
-          if (live(c)) {
-            v[c] = __expf(v[c] - mx);
-            se += v[c];
-          }
+          for (int c = NCT - 1; c >= 0; --c)
+            if (live(c) && v[c] == mx) am = c;
         }
-        const float lse = mx + __logf(se), inv = 1.f / se;
-        const float lrow = lse - (off * vs + (yin ? (on - off) * vy : 0.f));
+        // one exp per class: e_c = exp(v_c - max) = exp2(v_c log2e - max log2e) (one fma, one
+        // v_exp_f32, pairs on v_pk_fma_f32) serves the sum and the softmax (e_c / sum); padded
+        // classes are -inf -> 0.  The loss -sum_c tgt_c (v_c - lse) = lse - off * sum_c v_c - (on - off) v_y
+        constexpr float L2E = 1.4426950408889634f;
+        const ct_f32x2 l2e = {L2E, L2E}, nml = {-mx * L2E, -mx * L2E};
+        ct_f32x2 sp = {0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 32; ++c) {
-          const float d = (c < NCT && live(c)) ? (v[c < NCT ? c : 0] * inv - off) * xscale : 0.f;
-          lv[c >> 3].e[c & 7] = f2bf(d);         // (padded classes: 0)
+        for (int c = 0; c + 1 < NCT; c += 2) {
+          const ct_f32x2 a = __builtin_elementwise_fma((ct_f32x2){v[c], v[c + 1]}, l2e, nml);
+          v[c] = __builtin_amdgcn_exp2f(a.x);
+          v[c + 1] = __builtin_amdgcn_exp2f(a.y);
+          sp += (ct_f32x2){v[c], v[c + 1]};
+        }
+        if constexpr (NCT % 2) {
+          v[NCT - 1] = __builtin_amdgcn_exp2f(__builtin_fmaf(v[NCT - 1], L2E, nml.x));
+          sp.x += v[NCT - 1];
+        }
+        const float se = sp.x + sp.y;
+        const float lse = mx + __logf(se), inv = 1.f / se;
+        const float lrow = XF ? lse - (off * vs + (yin ? (on - off) * vy : 0.f)) : lse - (yin ? vy : 0.f);
+        // d = (softmax - off) * xscale = e * (inv xscale) - off xscale, pairs on v_pk_fma_f32
+        const ct_f32x2 ix = {inv * xscale, inv * xscale}, ox = {-off * xscale, -off * xscale};
+#pragma unroll
+        for (int c = 0; c < 32; c += 2) {
+          ct_f32x2 d = {0.f, 0.f};
+          if (c < NCT) {
+            d = __builtin_elementwise_fma((ct_f32x2){v[c], v[c + 1 < NCT ? c + 1 : c]}, ix, ox);
+            if (!live(c)) d.x = 0.f;
+            if (!(c + 1 < NCT && live(c + 1))) d.y = 0.f;   // (padded classes: 0)
+          }
+          lv[c >> 3].e[c & 7] = f2bf(d.x);
+          lv[(c + 1) >> 3].e[(c + 1) & 7] = f2bf(d.y);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) *(uint4*)(orow + 8 * j) = lv[j].u;
-        if (yin) orow[ylab] = f2bf((__expf(vy - mx) * inv - on) * xscale);   // the target's d
+        if (yin)                                 // the target's d
+          orow[ylab] = f2bf(__builtin_amdgcn_exp2f(__builtin_fmaf(vy, L2E, nml.x)) * ix.x - on * xscale);
         xl += lrow;
-        xc += (am == ylab) ? 1.f : 0.f;
+        if constexpr (XF) xc += (am == ylab) ? 1.f : 0.f;
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) *(uint4*)(orow + 8 * j) = make_uint4(0u, 0u, 0u, 0u);
@@ -375,15 +403,21 @@ extern "C" int fn_seghead_blocks(long long M) {
 
 // y [M][32] bf16 (M % 8 == 0), sc / sh [32], w [NC][32] bf16 (NC <= 32), bias [NC] or null,
 // labels int64 [M] (lab8 = 0) or uint8 [M] (lab8 = 1), dz [M][32] bf16, part fp32
-// [fn_seghead_blocks(M)][fn_seghead_part_len()]
+// [fn_seghead_blocks(M)][fn_seghead_part_len()]; hits = 0: the caller does not read part's hits
+// column (0 there with smoothing == 0 and 25 classes)
 extern "C" int fn_seghead_loss(const void* y, const float* sc, const float* sh, const void* w, const float* bias,
                                const void* labels, void* dz, float* part, long long M, int K, int NC, int act,
-                               float xscale, float smoothing, hipStream_t st, int lab8) {
+                               float xscale, float smoothing, hipStream_t st, int lab8, int hits) {
   if (K != SH_K || NC < 2 || NC > 32 || M < 8 || M % 8 || !sc || !sh || !labels || !part) return -2;
   if (act != ACT_RELU && act != ACT_NONE) return -2;
   const dim3 grid((unsigned)fn_seghead_blocks(M));
+  // the lean instances (no hits, no smoothing: a training step) for the 25-class head
+  const bool lean = !hits && smoothing == 0.f;
 #define SH_LAUNCH(A, T)                                                                                       \
-  if (NC == 25)                                                                                               \
+  if (NC == 25 && lean)                                                                                       \
+    hipLaunchKernelGGL((seghead_loss_kernel<A, T, 25, false>), grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc,  \
+                       sh, (const bf16*)w, bias, (const T*)labels, (bf16*)dz, part, M, NC, xscale, smoothing);   \
+  else if (NC == 25)                                                                                          \
     hipLaunchKernelGGL((seghead_loss_kernel<A, T, 25>), grid, dim3(SH_NTHR), 0, st, (const bf16*)y, sc, sh,     \
                        (const bf16*)w, bias, (const T*)labels, (bf16*)dz, part, M, NC, xscale, smoothing);       \
   else                                                                                                        \

@@ -470,7 +470,7 @@ class SubpixelDecoderHeadLossFn(torch.autograd.Function):
         Kn.seghead_loss(y2.data_ptr(), prm[2].data_ptr(), prm[3].data_ptr(), wb.data_ptr(), _native.ptr(bias),
                         lab.data_ptr(), dz.data_ptr(), part.data_ptr(), M, K, NC, act, 1.0 / M, float(smoothing),
                         _native.stream(y2), [y2.numel(), wb.numel(), lab.numel(), dz.numel(), part.numel()],
-                        int(lab.dtype == torch.uint8))
+                        int(lab.dtype == torch.uint8), int(bool(want_hits)))
         # the workgroups' partials summed once, in row order (one launch), for the loss here and the
         # head / BN-moment gradients in the backward
         tot = torch.empty(part.shape[1], dtype=torch.float32, device=y.device)

@@ -211,3 +211,40 @@ def test_fused_head_loss_uint8_labels_match_int64():
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
     for k in res[0][2]:
         assert torch.equal(res[0][2][k], res[1][2][k]), k
+
+
+@pytest.mark.parametrize("S", [24, 20])
+def test_fused_head_lean_instance_matches_full(monkeypatch, S):
+    """A training step asks for neither top-1 hits nor label smoothing: seghead.hip's lean
+    instance (no arg-max, no logit sum) must give the loss and every gradient bit for bit as the
+    full instance (hits requested), and both must match the unfused head + softmax_xent.
+    S = 20: 2 x 20^3 voxels, a partial last 256-row tile (the zero-row branch)."""
+    from featurenet_amd.models.featurenet3d import FeatureNet3DSeg
+    from featurenet_amd.ops import subpixel as sp
+
+    torch.manual_seed(11)
+    N = 2
+    m = FeatureNet3DSeg(input_size=S, num_classes=25).cuda().train()
+    x = (torch.rand(N, S, S, S, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    lab = torch.randint(0, 25, (N, S, S, S), device="cuda").to(torch.uint8)
+    calls = []
+    orig = sp.decoder_head_xent
+    monkeypatch.setattr(sp, "decoder_head_xent", lambda *a, **k: (calls.append(k.get("want_hits")), orig(*a, **k))[1])
+    res = []
+    for flag, with_correct in (("1", True), ("1", False), ("0", False)):
+        monkeypatch.setenv("FN_SEG_XENT", flag)
+        m.zero_grad(set_to_none=True)
+        out = m.loss(x, lab, 0.0, with_correct=with_correct)
+        loss = out[0] if with_correct else out
+        loss.backward()
+        res.append((loss.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()
+                                            if p.grad is not None}))
+    assert calls[:2] == [True, False], calls          # both fused passes took the seghead path
+    (lf, gf), (ll, gl), (lu, gu) = res
+    assert torch.equal(lf, ll)
+    for k in gf:
+        assert torch.equal(gf[k], gl[k]), k
+    assert float(ll) == pytest.approx(float(lu), rel=1e-4)
+    for k in gu:
+        r = _rel(gl[k].float(), gu[k].float())
+        assert r < 2e-2, (k, r)
