@@ -439,7 +439,10 @@ def test_featurenet3d_matches_reference_step(bn):
     like sqrt(flip fraction) (~5-12 % here, largest at the first layer) while
     the gradient direction stays aligned.  Train-mode BN at batch 8 adds the
     cancellation of its mean terms.  Per-op numerics are asserted tightly in
-    the tests above; this test guards the composition (cosine + loose L2).
+    the tests above; this test guards the composition (cosine + L2 drift), and
+    ``test_featurenet3d_per_layer_oracle_64cube`` bounds every layer at 2e-2.
+    Measured (round 6; the step is bitwise repeatable, so these are the values on any box):
+    without BN rel <= 0.122, cos >= 0.9926; with BN rel <= 0.237, cos >= 0.9731 (conv1's beta).
     """
     _native_loaded()
     from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
@@ -467,9 +470,9 @@ def test_featurenet3d_matches_reference_step(bn):
     print("\n".join(f"{n:24s} rel={r:.4f} cos={c:.5f}" for n, r, c in report))
     for n, r, c in report:
         if bn:
-            assert c > 0.96 and r < 0.35, f"{n}: rel={r:.3g} cos={c:.4f}"
+            assert c > 0.97 and r < 0.28, f"{n}: rel={r:.3g} cos={c:.4f}"
         else:
-            assert c > 0.985 and r < 0.2, f"{n}: rel={r:.3g} cos={c:.4f}"
+            assert c > 0.99 and r < 0.15, f"{n}: rel={r:.3g} cos={c:.4f}"
 
 
 HALO_CASES = [
