@@ -319,8 +319,10 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
 
     # int8 stem (v_mfma_i32_16x16x64_i8): an experiment build only (FN_BUILD_EXPERIMENTS=1)
     qi = quantize_model(model, cx, fp8_stem="i8") if experiments_built() else None
+    # the calibration check deciding the numerics (block scales -> per-tensor -> bf16)
+    qa = quantize_model(model, cx, fallback=True)
     y = np.asarray(ds.y_test)
-    pb, pq, ps, pi, pt = [], [], [], [], []
+    pb, pq, ps, pi, pt, pa = [], [], [], [], [], []
     for i in range(0, len(y), chunk):
         xb = batch(ds.x_test, i, chunk)
         pb.append(model(xb).float().argmax(-1).cpu())
@@ -328,13 +330,14 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
         ps.append(qs(xb).float().argmax(-1).cpu())
         if qi is not None:
             pi.append(qi(xb).float().argmax(-1).cpu())
+        pa.append(qa(xb).float().argmax(-1).cpu())
         os.environ["FN_F8_BLOCK"] = "0"                 # the per-tensor activation scales, same model
         try:
             pt.append(qs(xb).float().argmax(-1).cpu())
         finally:
             os.environ.pop("FN_F8_BLOCK")
-    pb, pq, ps, pt = (torch.cat(t).numpy() for t in (pb, pq, ps, pt))
-    acc_b, acc_q, acc_s, acc_t = (float((t == y).mean()) for t in (pb, pq, ps, pt))
+    pb, pq, ps, pt, pa = (torch.cat(t).numpy() for t in (pb, pq, ps, pt, pa))
+    acc_b, acc_q, acc_s, acc_t, acc_a = (float((t == y).mean()) for t in (pb, pq, ps, pt, pa))
     i8 = None
     if qi is not None:
         pi = torch.cat(pi).numpy()
@@ -351,6 +354,9 @@ def fp8_parity(model, ds, size: int, calib: int = 256, chunk: int = 128) -> dict
             "per_tensor": {"top1_fp8": round(acc_t, 4), "drop_pt": round(100 * (acc_b - acc_t), 2),
                            "agreement": round(float((pb == pt).mean()), 4)},
             "calib_agreement": q.calib_agreement,
+            "auto_fallback": {"mode": qa.calib_history[-1][0], "calib_history": qa.calib_history,
+                              "top1_fp8": round(acc_a, 4), "drop_pt": round(100 * (acc_b - acc_a), 2),
+                              "agreement": round(float((pb == pa).mean()), 4)},
             "i8_stem": i8,
             "kernel": ("conv_halo_f8" if os.environ.get("FN_F8_TILE", "1") == "0" else "conv_tile F8 variant")
                       + " (v_mfma_scale_f32_16x16x128_f8f6f4, e4m3)"}

@@ -40,6 +40,7 @@ from ..ops.spec import ConvSpec, PoolSpec
 FP8_MAX = 448.0
 I8_MAX = 127.0
 AGREEMENT_WARN = 0.97      # calibration-set top-1 agreement below which quantize_model warns
+FALLBACK_AT = 0.99         # quantize_model(fallback=True): the agreement each fallback step must reach
 
 
 def _fold_bn(conv) -> tuple[torch.Tensor, torch.Tensor]:
@@ -239,6 +240,10 @@ class Fp8FeatureNet3D:
         self._stem_w2 = {}
         self._block_ok = {}
         self.calib_agreement = None
+        # quantize_model(fallback=True): None (as built), "per_tensor" (block scales off for this
+        # model) or "bf16" (the model itself); calib_history: (mode, agreement) per step tried
+        self.fallback = None
+        self.calib_history = []
         self.stem = None
         self.stem_int8 = bool(stem_int8)
         if in_scale is not None:
@@ -265,7 +270,7 @@ class Fp8FeatureNet3D:
     def block_mode(self, in_shape5: tuple) -> bool:
         """Block-scaled activations for this input: ``FN_F8_BLOCK`` on (default), the bf16 stem, and a
         block-scaled tile plan for every fp8 layer (else the per-tensor path)."""
-        if os.environ.get("FN_F8_BLOCK", "1") == "0" or self.stem is not None:
+        if os.environ.get("FN_F8_BLOCK", "1") == "0" or self.stem is not None or self.fallback is not None:
             return False
         key = (tuple(in_shape5), os.environ.get("FN_F8_TILE", "1"), os.environ.get("FN_F8_POOL", "1"))
         ok = self._block_ok.get(key)
@@ -290,6 +295,8 @@ class Fp8FeatureNet3D:
         m = self.model
         if x.dim() == 4:
             x = x.unsqueeze(-1)
+        if self.fallback == "bf16":
+            return m(x.to(torch.bfloat16)).float()
         c1 = m.convs[0]
         if self.block_mode(tuple(x.shape)):
             return self._forward_block(x)
@@ -400,7 +407,23 @@ def stem_mode() -> str:
 CHECK_CHUNK = 64          # samples per forward of quantize_model's agreement check
 
 
-def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem=None) -> Fp8FeatureNet3D:
+def _agreement(model: FeatureNet3D, q: Fp8FeatureNet3D, x: torch.Tensor) -> float:
+    """Top-1 agreement of the fp8 and bf16 models on ``x`` (in chunks of CHECK_CHUNK samples: two
+    full-batch forwards over a 128^3 calibration set would double calibrate()'s peak activation
+    memory)."""
+    hits = 0
+    with torch.no_grad():
+        for i in range(0, x.shape[0], CHECK_CHUNK):
+            xc = x[i:i + CHECK_CHUNK]
+            a = model(xc.to(torch.bfloat16)).float().argmax(-1)
+            b = q(xc).float().argmax(-1)
+            hits += int((a == b).sum())
+            del a, b
+    return round(hits / max(1, x.shape[0]), 4)
+
+
+def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem=None, fallback: bool = False,
+                   fallback_at: float = FALLBACK_AT) -> Fp8FeatureNet3D:
     """fp8 model with activation scales from a bf16 pass over ``calib_x``.
 
     ``fp8_stem`` (default :func:`stem_mode`): 'bf16' keeps the stem on the bf16 tile kernel,
@@ -409,7 +432,15 @@ def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem=None) ->
     per-channel e4m3 stem weights cost a trained model ~16 points of top-1 on the held-out set
     (the stem output error 6 % vs 3 %); 'i8' runs it on the int8 MFMA (v_mfma_i32_16x16x64_i8,
     2x the bf16 rate): binary inputs are exact in int8 and per-channel int8 weights keep ~8
-    bits of each weight, the precision the e4m3 stem lacked."""
+    bits of each weight, the precision the e4m3 stem lacked.
+
+    ``fallback``: the calibration check decides the numerics instead of only warning -- while the
+    top-1 agreement with the bf16 model on ``calib_x`` is below ``fallback_at``, step down from
+    block-scaled activations to per-tensor scales (the form that held the parity bar on the model
+    where block scales did not, profiles/r5_fp8_block_parity.md), then to the bf16 model itself.
+    ``q.fallback`` names the step taken, ``q.calib_history`` the agreement of each one tried.
+    (Off by default: the kernel tests and the speed bench quantise random-init models, whose
+    agreement says nothing about deployment.)"""
     if fp8_stem is None:
         fp8_stem = stem_mode()
     mode = {True: "e4m3", False: "bf16"}.get(fp8_stem, fp8_stem)
@@ -424,18 +455,18 @@ def quantize_model(model: FeatureNet3D, calib_x: torch.Tensor, fp8_stem=None) ->
     q = Fp8FeatureNet3D(model, calibrate(model, calib_x), in_scale, stem_int8=mode == "i8")
     # post-quantisation check on the calibration set: top-1 agreement of the fp8 and bf16 models
     # (a model whose activations the chosen scales do not fit shows up here, not in deployment)
-    # (in chunks of CHECK_CHUNK samples: two full-batch forwards over a 128^3 calibration set would
-    # double calibrate()'s peak activation memory)
-    with torch.no_grad():
-        x = calib_x if calib_x.dim() == 5 else calib_x.unsqueeze(-1)
-        hits = 0
-        for i in range(0, x.shape[0], CHECK_CHUNK):
-            xc = x[i:i + CHECK_CHUNK]
-            a = model(xc.to(torch.bfloat16)).float().argmax(-1)
-            b = q(xc).float().argmax(-1)
-            hits += int((a == b).sum())
-            del a, b
-        q.calib_agreement = round(hits / max(1, x.shape[0]), 4)
+    x = calib_x if calib_x.dim() == 5 else calib_x.unsqueeze(-1)
+    block = q.block_mode(tuple(x[:CHECK_CHUNK].shape))
+    q.calib_agreement = _agreement(model, q, x)
+    q.calib_history.append(("block" if block else "per_tensor", q.calib_agreement))
+    if fallback and q.calib_agreement < fallback_at and block:
+        q.fallback = "per_tensor"
+        q.calib_agreement = _agreement(model, q, x)
+        q.calib_history.append(("per_tensor", q.calib_agreement))
+    if fallback and q.calib_agreement < fallback_at:
+        q.fallback = "bf16"
+        q.calib_agreement = 1.0
+        q.calib_history.append(("bf16", 1.0))
     if q.calib_agreement < AGREEMENT_WARN:
         warnings.warn(f"fp8 model agrees with bf16 on {q.calib_agreement:.1%} of the calibration set "
                       f"(< {AGREEMENT_WARN:.0%}): keep this model in bf16", RuntimeWarning)

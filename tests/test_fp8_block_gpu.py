@@ -146,6 +146,37 @@ def test_fp8_featurenet3d_block_matches_bf16():
     assert cos > 0.98, cos
 
 
+def test_quantize_fallback_reaches_the_agreement_bar():
+    """quantize_model(fallback=True): the calibration check steps down (block scales -> per-tensor
+    -> the bf16 model) until the fp8 model agrees with bf16 on >= FALLBACK_AT of the calibration
+    set, and the model it returns agrees as much as it reports.  A random-init model (logits close
+    together: a few % of fp8 noise flips the arg-max) exercises the steps; without fallback the
+    same model keeps its block-scaled numerics and its (lower) agreement."""
+    from featurenet_amd.inference import fp8 as F8
+    from featurenet_amd.models.featurenet3d import FeatureNet3D, FeatureNet3DConfig
+
+    torch.manual_seed(3)
+    m = FeatureNet3D(FeatureNet3DConfig(input_size=64, num_classes=24)).cuda().eval()
+    x = (torch.rand(16, 64, 64, 64, 1, device="cuda") < 0.3).to(torch.bfloat16)
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        q0 = F8.quantize_model(m, x, fp8_stem=False)
+        q = F8.quantize_model(m, x, fp8_stem=False, fallback=True)
+    assert q0.fallback is None and q0.calib_history[0][0] == "block"
+    assert q.calib_history[0] == q0.calib_history[0]          # (same first step, same bits)
+    assert q.calib_agreement >= F8.FALLBACK_AT or q.fallback == "bf16"
+    if q0.calib_agreement >= F8.FALLBACK_AT:
+        assert q.fallback is None
+    else:
+        assert q.fallback in ("per_tensor", "bf16") and len(q.calib_history) >= 2
+    with torch.no_grad():
+        a = m(x).float().argmax(-1)
+        b = q(x).float().argmax(-1)
+    assert round(float((a == b).float().mean()), 4) == q.calib_agreement
+
+
 def _e4m3(v: torch.Tensor) -> torch.Tensor:
     return v.to(torch.float8_e4m3fn).view(torch.uint8)
 
