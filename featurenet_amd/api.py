@@ -149,12 +149,18 @@ def load(path: str | Path, device=None) -> tuple[torch.nn.Module, dict]:
 
 
 @torch.no_grad()
-def classify(model, x, batch_size: int = 256, device=None, packed_size: int | None = None):
+def classify(model, x, batch_size: int = 256, device=None, packed_size: int | None = None, fp8_calib=None):
     """Predict classes for ``x`` -> (labels int64 [N], probabilities [N, C]).
 
     ``model`` may be a module or a checkpoint path.  For voxel models ``x`` is
     ``[N, S, S, S]`` / ``[N, S, S, S, 1]`` occupancy (any dtype) or bit-packed
     ``uint8 [N, S^3/8]`` with ``packed_size=S``.
+
+    ``fp8_calib`` (FeatureNet-3D on the GPU): calibration voxels in the same format as ``x``; the
+    model then runs in fp8 (OCP e4m3) with the numerics its calibration check chooses --
+    block-scaled activations, per-tensor scales, or bf16 when neither agrees with the bf16 model
+    on >= 99 % of the calibration set (``inference.fp8.quantize_model(fallback=True)``,
+    profiles/r6_fp8_fallback.md).
     """
     if isinstance(model, (str, Path)):
         model, _ = load(model, device)
@@ -162,17 +168,26 @@ def classify(model, x, batch_size: int = 256, device=None, packed_size: int | No
     model.eval()
     from .training.data import unpack_voxels
 
+    def prep(xb):
+        xb = xb.to(dev)
+        if packed_size is not None:
+            xb = unpack_voxels(xb, packed_size)
+        return xb.to(torch.bfloat16) if dev.type == "cuda" else xb.float()
+
+    fwd = model
+    if fp8_calib is not None:
+        from .models.featurenet3d import FeatureNet3D
+
+        if dev.type != "cuda" or not isinstance(model, FeatureNet3D):
+            raise ValueError("fp8 inference (fp8_calib) takes a FeatureNet-3D model on the GPU")
+        from .inference.fp8 import quantize_model
+
+        ct = torch.as_tensor(np.asarray(fp8_calib)) if not isinstance(fp8_calib, torch.Tensor) else fp8_calib
+        fwd = quantize_model(model, prep(ct), fallback=True)
     xt = torch.as_tensor(np.asarray(x)) if not isinstance(x, torch.Tensor) else x
     probs = []
     for i in range(0, len(xt), batch_size):
-        xb = xt[i:i + batch_size].to(dev)
-        if packed_size is not None:
-            xb = unpack_voxels(xb, packed_size)
-        if dev.type == "cuda":
-            xb = xb.to(torch.bfloat16)
-        else:
-            xb = xb.float()
-        probs.append(torch.softmax(model(xb).float(), -1).cpu())
+        probs.append(torch.softmax(fwd(prep(xt[i:i + batch_size])).float(), -1).cpu())
     p = torch.cat(probs).numpy() if probs else np.zeros((0, 0), np.float32)
     return p.argmax(-1), p
 

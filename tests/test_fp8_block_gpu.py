@@ -214,6 +214,10 @@ def test_trained_model_fp8_argmax_agreement():
     assert q.fallback != "bf16", q.calib_history
     assert agree >= 0.99, (agree, q.calib_history)
     assert drop <= 0.005, (drop, q.calib_history)
+    # the public API's fp8 path: the same quantisation from bit-packed calibration voxels
+    labels, probs = fn.classify(model, ds.x_test, packed_size=64, fp8_calib=ds.x_train[:256])
+    assert probs.shape == (len(y), 24)
+    assert float((labels == pq).mean()) >= 0.995          # (batch 256 vs 128: the Dense split may differ)
 
 
 def _e4m3(v: torch.Tensor) -> torch.Tensor:

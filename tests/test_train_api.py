@@ -44,6 +44,16 @@ def test_api_train_save_load_classify(tmp_path):
     assert fn.evaluate(model, xte, yte) == pytest.approx(res.accuracy, abs=1e-6)
 
 
+def test_classify_fp8_needs_featurenet3d_on_gpu():
+    """classify(fp8_calib=...) is the GPU fp8 path of FeatureNet-3D: refused on the CPU."""
+    m = FeatureNet3D(FeatureNet3DConfig.tiny())
+    x, _ = _voxels(4, 16, 0)
+    labels, probs = fn.classify(m, x, device="cpu")
+    assert probs.shape[0] == 4
+    with pytest.raises(ValueError, match="fp8"):
+        fn.classify(m, x, device="cpu", fp8_calib=x)
+
+
 def test_featurenet3d_tiny_learns_on_cpu():
     """BASELINE config 1: 16^3-voxel 2-class tiny 3D-CNN on the CPU reference path."""
     xtr, ytr = _voxels(128, 16, 0)
