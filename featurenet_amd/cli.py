@@ -184,7 +184,10 @@ def cmd_classify(a) -> int:
         x = np.asarray(x, np.float32)[..., None]
     else:
         x = np.load(a.input, allow_pickle=False)
-    labels, probs = api.classify(a.model, x, packed_size=a.packed_size)
+    calib = None
+    if a.fp8_calib is not None:          # (the first N inputs calibrate the fp8 activation scales)
+        calib = x[:a.fp8_calib]
+    labels, probs = api.classify(a.model, x, packed_size=a.packed_size, fp8_calib=calib)
     print(json.dumps({"labels": labels.tolist(), "confidence": probs.max(-1).round(4).tolist()}))
     return 0
 
@@ -318,6 +321,9 @@ def build_parser() -> argparse.ArgumentParser:
     cl.add_argument("model")
     cl.add_argument("input", help=".npy array or a folder of .binvox files")
     cl.add_argument("--packed-size", type=int, default=None)
+    cl.add_argument("--fp8-calib", type=int, default=None, metavar="N",
+                    help="FeatureNet-3D on the GPU: run in fp8, activation scales calibrated on the first N inputs "
+                         "(block / per-tensor scales or bf16, as the calibration check decides)")
     cl.set_defaults(fn=cmd_classify)
 
     e = sub.add_parser("extend", help="expand the 1-block template to B x C")
