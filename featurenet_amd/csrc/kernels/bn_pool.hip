@@ -527,7 +527,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_s2d_kernel(const bf16* __res
 // rows): a row is W2 cells x 8 sub-positions x C / 8 chunks, so every per-chunk index is a shift of
 // the thread's offset in the row -- the flat form above spent six 64-bit divisions per 16-B chunk
 // (1.28-1.44 ms per seg step, VALU-bound).  Same arithmetic, same bits.
-template <int ACT, int LCPR>
+// U: chunks per thread per pass -- ceil(row length / 256) where that is small, so a row is one
+// pass (the seg decoder's rows are 1056 chunks: 4 per thread left a 32-chunk second pass per row)
+template <int ACT, int LCPR, int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_s2d_rows_kernel(const bf16* __restrict__ dz,
                                                                     const bf16* __restrict__ y,
                                                                     const float* __restrict__ scale,
@@ -558,12 +560,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_s2d_rows_kernel(const bf16* 
     const int chh = row % H2, r2 = row / H2;
     const int cd = r2 % D2, n = r2 / D2;
     bf16* orow = dsh + (long long)row * rowlen * 8;
-    // four chunks per thread per pass, their eight loads issued before any is used
-    for (int t0 = threadIdx.x; t0 < rowlen; t0 += 4 * 256) {
-      Pack8 py[4], pd[4];
-      bool in[4];
+    // U chunks per thread per pass, their 2U loads issued before any is used
+    for (int t0 = threadIdx.x; t0 < rowlen; t0 += U * 256) {
+      Pack8 py[U], pd[U];
+      bool in[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int t = t0 + u * 256;
         const int jp = (t >> LCPR) & 7, cw = t >> (LCPR + 3);
         const int qd = 2 * cd - 1 + (jp >> 2), qh = 2 * chh - 1 + ((jp >> 1) & 1), qw = 2 * cw - 1 + (jp & 1);
@@ -573,7 +575,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_s2d_rows_kernel(const bf16* 
         pd[u].u = *(const uint4*)(dz + off);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int t = t0 + u * 256;
         Pack8 po;
         if (in[u]) {
@@ -1271,10 +1273,20 @@ extern "C" int fn_bn_bwd_apply_s2d(const void* dz, const void* y, const float* s
     int lc = 0;
     while ((1 << lc) < C / 8) ++lc;
     const unsigned grid = (unsigned)std::min<long long>(nrows, 8192);
+    const long long rowlen = (long long)(FW / 2 + 1) * 8 * (C / 8);
+    const int u = rowlen > 4 * 256 && rowlen <= 5 * 256 ? 5 : (rowlen > 5 * 256 && rowlen <= 8 * 256 ? 8 : 4);
 #define BR_CASE(A, L)                                                                                        \
-    if (lc == L) hipLaunchKernelGGL((bn_bwd_apply_s2d_rows_kernel<A, L>), dim3(grid), dim3(256), 0, st,     \
-                                    (const bf16*)dz, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, \
-                                    (bf16*)dsh, N, FD, FH, FW, C, inv_count);
+    if (lc == L) {                                                                                           \
+      if (u == 5) hipLaunchKernelGGL((bn_bwd_apply_s2d_rows_kernel<A, L, 5>), dim3(grid), dim3(256), 0, st,  \
+                                     (const bf16*)dz, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma, \
+                                     (bf16*)dsh, N, FD, FH, FW, C, inv_count);                              \
+      else if (u == 8) hipLaunchKernelGGL((bn_bwd_apply_s2d_rows_kernel<A, L, 8>), dim3(grid), dim3(256), 0, \
+                                          st, (const bf16*)dz, (const bf16*)y, scale, shift, mean, invstd,  \
+                                          dbeta, dgamma, (bf16*)dsh, N, FD, FH, FW, C, inv_count);          \
+      else hipLaunchKernelGGL((bn_bwd_apply_s2d_rows_kernel<A, L, 4>), dim3(grid), dim3(256), 0, st,         \
+                              (const bf16*)dz, (const bf16*)y, scale, shift, mean, invstd, dbeta, dgamma,   \
+                              (bf16*)dsh, N, FD, FH, FW, C, inv_count);                                     \
+    }
 #define BR_ACT(A) BR_CASE(A, 0) BR_CASE(A, 1) BR_CASE(A, 2) BR_CASE(A, 3) BR_CASE(A, 4) BR_CASE(A, 5)
     if (act == ACT_RELU) { BR_ACT(ACT_RELU) } else { BR_ACT(ACT_NONE) }
 #undef BR_ACT

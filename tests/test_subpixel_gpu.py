@@ -38,9 +38,10 @@ def test_upconv_forward_and_stats(N, S):
     torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=2e-3, atol=2e-1)
 
 
-@pytest.mark.parametrize("shape", [(2, 12, 12, 12, 32), (3, 10, 14, 8, 64), (4, 64, 64, 64, 32)])
+@pytest.mark.parametrize("shape", [(2, 12, 12, 12, 32), (3, 10, 14, 8, 64), (4, 64, 64, 64, 32), (2, 8, 8, 48, 64)])
 def test_bn_backward_shifted_layout_matches_natural(shape):
-    """bn_bwd_apply_s2d == the natural BN backward, shifted (incl. non-cubic grids, 64 channels)."""
+    """bn_bwd_apply_s2d == the natural BN backward, shifted (incl. non-cubic grids, 64 channels;
+    rows of 1056 and 1600 16-B chunks: the 5- and 8-chunk-per-thread instances)."""
     torch.manual_seed(1)
     K = shape[-1]
     y = _bf(torch.randn(*shape, device="cuda"))
