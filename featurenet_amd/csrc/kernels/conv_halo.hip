@@ -788,10 +788,6 @@ static int launch_halo(dim3 grid, size_t lds, int region, hipStream_t st, const 
 }
 
 static int g_num_cus = 0;
-static const bool g_halo_static = [] {
-  const char* e = getenv("FN_HALO_STATIC");
-  return e && e[0] == '1';
-}();
 extern "C" int fn_conv_halo_workers(const int* geom17, int Ncol);
 
 // wt: [Ncol][C/CS][Tp][CS] bf16 (taps padded to a multiple of 128/CS), CS = 16 when
@@ -819,7 +815,7 @@ extern "C" int fn_conv_halo(const void* src, const void* wt, const float* bias, 
   int chunk = ntiles_all / (4 * workers) > 1 ? ntiles_all / (4 * workers) : 1;
   // BN statistics: one partial row per workgroup, so its tiles must not depend on the dynamic
   // schedule (bitwise-repeatable statistics): the static partition
-  if (g_halo_static || stats) chunk = -((ntiles_all + workers - 1) / workers);
+  if (stats) chunk = -((ntiles_all + workers - 1) / workers);
   dim3 grid((unsigned)workers, ncb);
   const bf16* s = (const bf16*)src;
   const bf16* w = (const bf16*)wt;

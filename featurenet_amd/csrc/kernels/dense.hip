@@ -469,12 +469,10 @@ __global__ __launch_bounds__(DN_THREADS) void dense_wgrad_kernel(const bf16* __r
 // column waves per forward workgroup: 2 (128 columns, x rows read once) when N > 64 and the
 // batch spans row blocks (inference chunks); one 128-row block (FC1 at training batch 128) takes
 // 64-column workgroups -- 250 of them over K, one per CU: 30.6 us against 37.8 us for 128-column
-// workgroups over 250 K slices (scripts/bench_fc_native.py, FN_DENSE_NCW A/B)
+// workgroups over 250 K slices (scripts/bench_fc_native.py, round-4 A/B)
 // -- and so does a layer too shallow to split over K whose 128-column tiles would leave CUs idle
 // (LeNet's 120 -> 84 Dense on 16,384 rows: 128 workgroups of 128 columns)
 static int dn_ncw(int M, int N, int K) {
-  static const int forced = [] { const char* e = getenv("FN_DENSE_NCW"); return e ? atoi(e) : 0; }();   // (A/B)
-  if (forced == 1 || forced == 2) return forced;
   if (N <= 64 || M <= 128) return 1;
   if (K < 512 && ((N + 127) / 128) * ((M + 127) / 128) < 256) return 1;
   return 2;

@@ -254,10 +254,8 @@ class Fp8FeatureNet3D:
             last = i == len(convs) - 1
             self.layers.append(Fp8Conv(conv, act_scales[i - 1], None if last else act_scales[i], relu=True))
         self.pool = convs[-1].pool
-        # the dense layers read bf16 weight copies (FN_F8_FC_BF16=0: the fp32 master weights)
-        self.fc_w = None
-        if os.environ.get("FN_F8_FC_BF16", "1") != "0":
-            self.fc_w = [fc.weight.detach().to(torch.bfloat16).contiguous() for fc in (model.fc1, model.fc2)]
+        # the dense layers read bf16 weight copies
+        self.fc_w = [fc.weight.detach().to(torch.bfloat16).contiguous() for fc in (model.fc1, model.fc2)]
 
     def _dense(self, f: torch.Tensor) -> torch.Tensor:
         m = self.model

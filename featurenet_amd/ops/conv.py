@@ -40,7 +40,7 @@ from .spec import ConvSpec, act_code
 _TAB_LOCK = threading.Lock()
 # the space-to-depth forward pads K (FeatureNet-3D stem: 512 vs 343); it is taken when
 # the padded K is at most this multiple of the real one (else the packed-W gather runs)
-S2D_FWD_RATIO = float(os.environ.get("FN_S2D_FWD_RATIO", "1.5"))
+S2D_FWD_RATIO = 1.5
 _TAB_CACHE: dict = {}
 
 
