@@ -796,7 +796,7 @@ extern "C" int fn_pack_w_multi(const long long* jobs, int n, hipStream_t st) {
     } else if (jb.kind == 5) {                   // (fn_tile_pack_w's checks)
       const int CS = a[3], nks = a[4], nct = a[5], nslice = a[6], nt = a[8];
       if (CS != 8 && CS != 16 && CS % 32 != 0) return -2;
-      if ((nt != 2 && nt != 32) || nct % 2 || nks <= 0 || nslice <= 0) return -2;
+      if ((nt != 2 && nt != 4 && nt != 32) || nct % (nt == 4 ? 4 : 2) || nks <= 0 || nslice <= 0) return -2;
       cnt = ((long long)nslice * nks + 4) * nct * 64;
     } else {
       return -2;

@@ -105,11 +105,12 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
   constexpr int PD = ct_pd(NT, F8);
   constexpr int ESZ = F8 ? 1 : 2;                // bytes per element of the source / weights
   constexpr int FRAG = F8 ? 32 : 16;             // bytes per lane of one MFMA operand fragment
-  // NT = 2: 32-column blocks (a lane stores 8 consecutive columns).  (Round 3 measured 64-column
-  // NT = 4 workgroups 3-4 % slower -- 256 VGPRs for 5 waves per CU -- and round 4 removed them;
-  // a 32x32x16-MFMA form of this kernel measured 2-8 % slower per layer in round 4,
-  // profiles/r4_m32_ab.md, and was removed in round 6.)
-  static_assert(NT == 2, "32-column blocks");
+  // NT = 2: 32-column blocks (a lane stores 8 consecutive columns).  NT = 4 (bf16, MT = 4: the
+  // same 64 accumulator registers): 64-column workgroups over 256 rows, for loader-bound convs whose
+  // 32-column blocks would each DMA the whole halo (the sub-pixel decoder's dgrad: 8 taps over 256
+  // channels into 64 columns).  (Round 3 measured MT 8 x NT 4 3-4 % slower on the classifier --
+  // 256 VGPRs -- and a 32x32x16-MFMA form measured 2-8 % slower per layer in round 4.)
+  static_assert(NT == 2 || (NT == 4 && !F8), "32-column blocks, or 64 for the bf16 kernel");
   constexpr int RC = NT * 16;                    // columns of the workgroup (BN partial row length)
   constexpr int NV = 4 * NT;                     // consecutive columns per lane in the epilogue
   static_assert(!F8 || CPP == 2 || CPP == 4, "fp8: 32- or 64-channel slices");
@@ -709,11 +710,16 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
     // the packed weight columns are ordered so that fragment nt row 4lg+r is output column
     // ct0*16 + 4*NT*lg + 4nt + r: a lane ends with NV = 4*NT consecutive columns of one position
     const int gc8 = ct0 * 16 + NV * lg;
-    ct_f32x2 bias2[4];                           // (fp8: read in the epilogue from LDS, no live
+    ct_f32x2 bias2[NT / 2][4];                   // (fp8: read in the epilogue from LDS, no live
 #pragma unroll                                   // registers across the k-loop)
-    for (int q = 0; q < 4; ++q)
+    for (int h = 0; h < NT / 2; ++h)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) bias2[q][e] = (!F8 && bias && gc8 + 2 * q + e < Ncol) ? bias[gc8 + 2 * q + e] : 0.f;
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int c = gc8 + 8 * h + 2 * q + e;
+          bias2[h][q][e] = (!F8 && bias && c < Ncol) ? bias[c] : 0.f;
+        }
     constexpr unsigned FTILE = 64u * FRAG;       // bytes of one 16-column fragment of a k-step
     const unsigned wstep = (unsigned)g.nct * FTILE;   // bytes per k-step of the packed weights
     unsigned voffb[PD];                          // per-lane B offsets of the PD ring slots
@@ -956,10 +962,12 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
           // parity, [fragment slot][Ncol / 8])
           const unsigned char* mb = dsm + 2 * g.BUF + mask_off + par * mask_bytes +
                                     ((wave * MT * 16 + lr) * (Ncol >> 3) + (gc8 >> 3));
-          unsigned mrows[MSK ? MT : 1];          // (all MT byte reads in flight together)
-          if constexpr (MSK) {
+          unsigned mrows[MSK ? MT : 1][NT / 2];  // (all the byte reads in flight together; byte h:
+          if constexpr (MSK) {                   //  the lane's columns 8h .. 8h + 7)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt) mrows[mt] = mb[mt * 16 * (Ncol >> 3)];
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+              for (int h = 0; h < NT / 2; ++h) mrows[mt][h] = mb[mt * 16 * (Ncol >> 3) + h];
           }
           bool okm[MT];
 #pragma unroll
@@ -983,12 +991,12 @@ __global__ __launch_bounds__(64 * (NCW + 1), 1) void conv_tile_kernel(const unsi
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) {
               const bool ok = okm[mt];
-              const unsigned mrow = MSK ? mrows[mt] : 0u;
+              const unsigned mrow = MSK ? mrows[mt][h] : 0u;
               unsigned pw[4];                    // the stored bf16 pairs (columns 2q, 2q+1)
 #pragma unroll
               for (int q = 0; q < 4; ++q) {
                 const f32x4 a4 = acc[mt][2 * h + (q >> 1)];
-                const ct_f32x2 v = (ct_f32x2){a4[(2 * q) & 3], a4[(2 * q + 1) & 3]} + bias2[q];
+                const ct_f32x2 v = (ct_f32x2){a4[(2 * q) & 3], a4[(2 * q + 1) & 3]} + bias2[h][q];
                 unsigned w = bf16x2_pack(v[0], v[1]);
                 if constexpr (RELU_OUT) w = ct_relu_bf16x2(w);
                 pw[q] = w;
@@ -1303,7 +1311,7 @@ extern "C" int fn_tile_pack_w2(const float* w, void* out0, void* out1, int K, in
   for (int q = 0; q < 2; ++q) {
     const int* p = ps[q];
     if (p[0] != 8 && p[0] != 16 && p[0] % 32 != 0) return -2;
-    if (p[5] != 2 || p[2] % 2) return -2;
+    if ((p[5] != 2 && p[5] != 4) || p[2] % p[5]) return -2;   // (nt: the workgroup's 16-column tiles)
     j[q] = TilePackJob{(uint4*)(q ? out1 : out0), p[0], p[1], p[2], p[3], p[4], p[5]};
     total += ((long long)p[3] * p[1] + 4) * p[2] * 64;
   }
@@ -1316,7 +1324,7 @@ extern "C" int fn_tile_pack_w2(const float* w, void* out0, void* out1, int K, in
 extern "C" int fn_tile_pack_w(const float* w, void* out, int K, int T, int C, int CS, int nks, int nct, int nslice,
                               int dgrad, int nt, hipStream_t st) {
   if (CS != 8 && CS != 16 && CS % 32 != 0) return -2;
-  if (nt != 2 || nct % 2) return -2;
+  if ((nt != 2 && nt != 4) || nct % nt) return -2;
   const long long total = ((long long)nslice * nks + 4) * nct * 64;
   hipLaunchKernelGGL(tile_pack_w_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, w, (uint4*)out, K, T,
                      C, CS, nks, nct, nslice, dgrad, nt);
@@ -1428,7 +1436,7 @@ static int tile_wring(size_t lds, int NT) {
 }
 
 // instantiations (MT, NT, CPP) -- the Python planner only emits these
-#define CT_INSTANCES(X) X(8, 2, 1) X(9, 2, 1) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4)
+#define CT_INSTANCES(X) X(8, 2, 1) X(9, 2, 1) X(8, 2, 2) X(9, 2, 2) X(8, 2, 4) X(9, 2, 4) X(4, 4, 4)
 
 extern "C" int fn_conv_tile_supported(int MT, int NT, int CPP) {
 #define CT_SUP(M, N, C) if (MT == M && NT == N && CPP == C) return 1;

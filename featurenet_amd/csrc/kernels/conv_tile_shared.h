@@ -103,8 +103,9 @@ __device__ __forceinline__ uint4 ct_bn_chunk(uint4 v, const ct_f32x2* sc, const 
 }
 
 // B-ring depth (k-steps in flight): a bf16 k-step is MT*NT 16-cycle MFMAs, an fp8 one
-// MT*NT 32-cycle block-scaled MFMAs, so 2 fp8 steps cover the latency 4 bf16 steps do
-__host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : 4; }
+// MT*NT 32-cycle block-scaled MFMAs, so 2 fp8 steps cover the latency 4 bf16 steps do; NT = 4
+// (MT = 4) holds 2: four 4-fragment slots are 64 registers, past the budget (spills)
+__host__ __device__ constexpr int ct_pd(int NT, bool F8) { return F8 ? 2 : (NT == 4 ? 2 : 4); }
 
 // Halo of job (tile, slice) into the LDS buffer at bufoff, issued by one wave (the
 // loader): interior halos (the common case for unpadded convs) use SGPR base + the

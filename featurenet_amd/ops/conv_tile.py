@@ -106,40 +106,43 @@ def _ksteps(T: int, CS: int, PD: int) -> int:
 
 
 def plan(N: int, out_dims: tuple, kdims: tuple, Csrc: int, Ncol: int, n_cus: int = 256, f8: bool = False,
-         pool: bool = False, bs: bool = False):
+         pool: bool = False, bs: bool = False, nt4: bool = False):
     """Best TilePlan for an (N, OD, OH, OW) output of a (KD, KH, KW) stride-1 conv over
     ``Csrc`` input channels into ``Ncol`` columns, or None when the kernel does not apply
     (``f8``: the e4m3 inference variant, 32- or 64-channel slices; ``pool``: with the fused
     2^3 max-pool epilogue -- even output and tile dims; ``bs``: block-scaled fp8 operands, the
-    LDS also holds two planes of the halo positions' scale dwords)."""
+    LDS also holds two planes of the halo positions' scale dwords; ``nt4``: 64-column workgroups
+    over 256 rows (MT 4 x NT 4, bf16, Ncol % 64 == 0) -- one halo DMA for 64 columns instead of
+    one per 32-column block, for loader-bound convs)."""
     bs = bool(bs and f8)
-    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, pool, bs,
+    nt4 = bool(nt4 and not f8 and Ncol % 64 == 0)
+    key = (N, tuple(out_dims), tuple(kdims), Csrc, Ncol, n_cus, f8, pool, bs, nt4,
            os.environ.get("FN_TILE_PLAN_RANK", "0"))
     if key in _PLANS:
         return _PLANS[key]
     if pool and (not f8 or any(d % 2 for d in out_dims)):
         return None
-    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, pool, bs)
+    best = _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8, pool, bs, nt4)
     with _LOCK:
         _PLANS[key] = best
     return best
 
 
-def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, bs=False):
+def _plan(N, out_dims, kdims, Csrc, Ncol, n_cus, f8=False, pool=False, bs=False, nt4=False):
     OD, OH, OW = out_dims
     KD, KH, KW = kdims
     T = KD * KH * KW
     if Ncol < 16 or Ncol % 8 or Csrc % 8 or T < 2:
         return None
-    NT = 2                                       # 32-column workgroups
+    NT = 4 if nt4 else 2                         # 32-column workgroups (nt4: 64, MT = 4)
     ncb = -(-Ncol // (NT * 16))
     nct = ncb * NT
     PD = PD_F8 if f8 else 4
     workers = max(1, n_cus // ncb)
     cands = []
     cs_only = int(os.environ.get("FN_TILE_CS", "0"))
-    mt_choices = (8,) if f8 else MT_CHOICES
-    for CS in ((64, 32) if f8 else (32, 16, 8)):
+    mt_choices = (8,) if f8 else ((4,) if nt4 else MT_CHOICES)
+    for CS in ((64, 32) if f8 else ((32,) if nt4 else (32, 16, 8))):
         if Csrc % CS or (cs_only and CS != cs_only) or (CS == 8 and Csrc % 16 == 0):
             continue
         CPP = CS // 16 if f8 else CS // 8
@@ -726,16 +729,20 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None, w
     return dx if bn is None else (dx, None)
 
 
+def _nt4() -> bool:
+    return os.environ.get("FN_TILE_NT4", "0") == "1"
+
+
 def fwd_plan(spec):
     if not enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
         return None
-    return plan(spec.N, (spec.OD, spec.OH, spec.OW), (spec.KD, spec.KH, spec.KW), spec.C, spec.K)
+    return plan(spec.N, (spec.OD, spec.OH, spec.OW), (spec.KD, spec.KH, spec.KW), spec.C, spec.K, nt4=_nt4())
 
 
 def dgrad_plan(spec):
     if not enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
         return None
-    return plan(spec.N, (spec.D, spec.H, spec.W), (spec.KD, spec.KH, spec.KW), spec.K, spec.C)
+    return plan(spec.N, (spec.D, spec.H, spec.W), (spec.KD, spec.KH, spec.KW), spec.K, spec.C, nt4=_nt4())
 
 
 # ---------------------------------------------------------------------------

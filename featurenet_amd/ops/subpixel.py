@@ -205,7 +205,7 @@ def gpu_ok(x5: torch.Tensor, K: int, C: int) -> bool:
         return False
     N, D, H, W, Cx = x5.shape
     return (Cx == C and K == 32 and C % 32 == 0 and conv_tile.plan(N, (D, H, W), (2, 2, 2), C, K) is not None
-            and conv_tile.plan(N, (D, H, W), (2, 2, 2), 8 * K, C) is not None
+            and _dgrad_plan(x5.shape, K) is not None
             and conv_wtile.plan_subpixel(N, (D, H, W), C, K) is not None)
 
 
@@ -240,14 +240,19 @@ def upconv_forward(x5: torch.Tensor, w: torch.Tensor):
     return y, slab
 
 
-def _dgrad_plan(x_shape, K: int):
+def _dgrad_plan(x_shape, K: int, nt4: bool = True):
+    """The dgrad's tile plan: 8 taps over the 8K shifted-layout channels into C columns -- DMA-bound
+    (each job's halo feeds only 8 taps), so C = 64 takes 64-column workgroups (one halo DMA for
+    all the columns instead of one per 32-column block: 1.70 -> 1.50 ms at batch 128, seg step
+    -1.4 %, profiles/r6_subpixel_nt4.md)."""
     from . import conv_tile
 
     N, D, H, W, C = x_shape
-    return conv_tile.plan(N, (D, H, W), (2, 2, 2), 8 * K, C)
+    return (nt4 and conv_tile.plan(N, (D, H, W), (2, 2, 2), 8 * K, C, nt4=True)) or \
+        conv_tile.plan(N, (D, H, W), (2, 2, 2), 8 * K, C)
 
 
-def upconv_dgrad(dsh: torch.Tensor, w: torch.Tensor, x_shape, mask=None):
+def upconv_dgrad(dsh: torch.Tensor, w: torch.Tensor, x_shape, mask=None, nt4: bool = True):
     """dx [N, D, H, W, C] = the 2^3 'valid' conv over the shifted view with :func:`dgrad_weights`.
     ``mask`` (x = relu(bn(y)) with its relu-mask bytes, the BN statistics identity of
     ops/bnfuse.py): returns ``(dx, slab)``, the slab's row 0 the column sums of dx * relu'(x)."""
@@ -255,7 +260,7 @@ def upconv_dgrad(dsh: torch.Tensor, w: torch.Tensor, x_shape, mask=None):
 
     N, D, H, W, C = x_shape
     K = w.shape[0]
-    p = _dgrad_plan(x_shape, K)
+    p = _dgrad_plan(x_shape, K, nt4)
     kd = dgrad_weights(w.detach().float()).reshape(C, 8, 8 * K)
     wpk = conv_tile.pack_weights(kd, C, 8, 8 * K, p, dgrad=False)
     geom = conv_tile.geometry(p, (N, D + 1, H + 1, W + 1, 8 * K), (D, H, W), (2, 2, 2), (0, 0, 0))

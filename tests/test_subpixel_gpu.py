@@ -249,3 +249,33 @@ def test_fused_head_lean_instance_matches_full(monkeypatch, S):
     for k in gu:
         r = _rel(gl[k].float(), gu[k].float())
         assert r < 2e-2, (k, r)
+
+
+@pytest.mark.parametrize("N,S", [(2, 12), (3, 16)])
+def test_upconv_dgrad_64_column_workgroups_match_32(N, S):
+    """The sub-pixel dgrad on 64-column workgroups (conv_tile MT 4 x NT 4: one halo DMA for all
+    64 columns) against the 32-column-block plan, with and without the relu-mask BN-statistics
+    epilogue.  At these small grids the 32-column plan takes 16-channel slices (two taps per
+    k-step) where the 64-column one takes 32, so the MFMA sums group differently: measured 0.02 %
+    of dx elements 1 bf16 ulp apart (rel 3e-5); the partial rows of the statistics differ in
+    number, their column sums agree to rounding."""
+    torch.manual_seed(9)
+    C, K = 64, 32
+    w = torch.randn(K, 3, 3, 3, C, device="cuda") * 0.05
+    dsh = _bf(torch.randn(N, S + 1, S + 1, S + 1, 8 * K, device="cuda"))
+    mask = torch.randint(0, 256, (N * S * S * S * C // 8,), dtype=torch.uint8, device="cuda")
+    res = {}
+    for flag in ("0", "1"):
+        nt4 = flag == "1"
+        p = sp._dgrad_plan((N, S, S, S, C), K, nt4)
+        assert p.NT == (4 if nt4 else 2), p
+        dx = sp.upconv_dgrad(dsh, w, (N, S, S, S, C), nt4=nt4)
+        dxm, slab = sp.upconv_dgrad(dsh, w, (N, S, S, S, C), mask=mask, nt4=nt4)
+        torch.cuda.synchronize()
+        res[flag] = (dx, dxm, slab.sum(0))
+    for i in (0, 1):
+        a, b = res["0"][i].float(), res["1"][i].float()
+        assert ((a - b).norm() / a.norm()).item() < 1e-4
+        assert ((a - b) != 0).float().mean().item() < 2e-3
+    assert torch.equal(res["1"][0], res["1"][1])           # (dx is stored unmasked)
+    torch.testing.assert_close(res["1"][2], res["0"][2], rtol=1e-3, atol=1e-2)
