@@ -729,20 +729,21 @@ def conv_dgrad(dy5: torch.Tensor, w: torch.Tensor, spec, p: TilePlan, bn=None, w
     return dx if bn is None else (dx, None)
 
 
-def _nt4() -> bool:
-    return os.environ.get("FN_TILE_NT4", "0") == "1"
-
-
 def fwd_plan(spec):
     if not enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
         return None
-    return plan(spec.N, (spec.OD, spec.OH, spec.OW), (spec.KD, spec.KH, spec.KW), spec.C, spec.K, nt4=_nt4())
+    return plan(spec.N, (spec.OD, spec.OH, spec.OW), (spec.KD, spec.KH, spec.KW), spec.C, spec.K)
 
 
 def dgrad_plan(spec):
+    """dgrad into 64 columns (conv4's): 64-column workgroups -- one DMA of the 64-channel dy halo
+    instead of one per 32-column block; that dgrad waited on its loader (profiles/r6_bn_prologue.md,
+    waves addendum): 341.5 -> 312.5 us, where the 64-column forwards measured 1-2 % slower
+    (profiles/r6_subpixel_nt4.md)."""
     if not enabled() or (spec.sd, spec.sh, spec.sw, spec.dd, spec.dh, spec.dw) != (1,) * 6:
         return None
-    return plan(spec.N, (spec.D, spec.H, spec.W), (spec.KD, spec.KH, spec.KW), spec.K, spec.C, nt4=_nt4())
+    dims, kd = (spec.D, spec.H, spec.W), (spec.KD, spec.KH, spec.KW)
+    return plan(spec.N, dims, kd, spec.K, spec.C, nt4=True) or plan(spec.N, dims, kd, spec.K, spec.C)
 
 
 # ---------------------------------------------------------------------------
