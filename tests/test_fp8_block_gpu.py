@@ -181,9 +181,11 @@ def test_trained_model_fp8_argmax_agreement():
     """FeatureNet-3D trained with the accuracy bench's recipe (procedural machining-feature voxels,
     64^3, 24 classes, 1,000 per class, 16 epochs, seed 0: ~20 s), then fp8 with the
     calibration-driven fallback: held-out top-1 agreement with the bf16 model >= 0.99 and top-1
-    within 0.5 points, on an fp8 path (not the bf16 fallback).  The step is bitwise repeatable, so
-    this is the seed-0 row of profiles/r6_fp8_fallback.md: block scales lose 3.17 pt on this model,
-    the check moves it to per-tensor scales (0.17 pt, 0.9983)."""
+    within 0.5 points (6 of 1,200 samples), on an fp8 path (not the bf16 fallback).  The step is
+    bitwise repeatable, so the trained model is fixed by the tree's kernels: with the round-6
+    32-column conv4 dgrad it was the seed-0 row of profiles/r6_fp8_fallback.md (block scales lose
+    3.17 pt, the check moves it to per-tensor: 0.17 pt, 0.9983); with the 64-column dgrad's
+    rounding the model differs and stays on block scales (calibration 0.9922; 0.50 pt, 0.9950)."""
     import numpy as np
 
     import featurenet_amd as fn
@@ -213,7 +215,7 @@ def test_trained_model_fp8_argmax_agreement():
     assert float((pb == y).mean()) > 0.9                     # (a trained model)
     assert q.fallback != "bf16", q.calib_history
     assert agree >= 0.99, (agree, q.calib_history)
-    assert drop <= 0.005, (drop, q.calib_history)
+    assert drop <= 0.005 + 1e-9, (drop, q.calib_history)
     # the public API's fp8 path: the same quantisation from bit-packed calibration voxels
     labels, probs = fn.classify(model, ds.x_test, packed_size=64, fp8_calib=ds.x_train[:256])
     assert probs.shape == (len(y), 24)
